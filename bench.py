@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Headline benchmark: online linear SVM (PA-I) training throughput (examples/s, whole
+node) + p50 single-point predict latency, 1/2/4/8 MI355X GPUs (BASELINE.json).
+
+One step == one Synchronous protocol round on every GPU:
+  pinned host micro-batch ──hipMemcpyAsync (copy stream, double-buffered)──► HBM
+  → linear_round kernel: S virtual spokes (one wavefront each) train PA-I sequentially
+    on R rows each, private deltas in LDS hash tables, σ·Δ scattered into the round
+    accumulator
+  → RCCL all-reduce of the accumulator over xGMI (the parameter-server round)
+  → linear_apply: model average + bf16 shadow refresh.
+Data: synthetic Criteo-shaped stream (13 numerical + 26 hashed categorical features into
+2^20 slots + intercept), generated once into a pinned host pool per rank and replayed
+like a Kafka log; random-init (zero) model. The H2D copy of every step's batch is inside
+the timed region.
+
+Launch: python bench.py [--gpus 1 --steps 50 --warmup 10]; for N > 1 the driver uses
+python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch  # noqa: E402
+from omldm_amd.io.synthetic import synth_batch  # noqa: E402
+from omldm_amd.models.linear import SVM  # noqa: E402
+from omldm_amd.parallel.comm import init_distributed  # noqa: E402
+from omldm_amd.parallel.protocols import Synchronous  # noqa: E402
+
+METRIC = "training examples/sec (whole node) + p50 predict latency, linear SVM 1/2/4/8 GPU"
+
+
+class PackedBatch:
+    """num | cat | y packed in ONE contiguous byte buffer so a micro-batch is one copy."""
+
+    def __init__(self, space: FeatureSpace, B: int, device, pin: bool, num_dtype):
+        esz = torch.tensor([], dtype=num_dtype).element_size()
+        self.sizes = [B * space.dn * esz, B * space.dc * 4, B * 4]
+        offs = [0]
+        for s in self.sizes:
+            offs.append(offs[-1] + ((s + 255) // 256) * 256)
+        self.flat = torch.empty(offs[-1], dtype=torch.uint8, device=device,
+                                pin_memory=pin and device == "cpu")
+        f = self.flat
+        self.batch = HashedBatch(
+            f[offs[0]:offs[0] + self.sizes[0]].view(num_dtype).view(B, space.dn),
+            f[offs[1]:offs[1] + self.sizes[1]].view(torch.int32).view(B, space.dc),
+            f[offs[2]:offs[2] + self.sizes[2]].view(torch.float32).view(B))
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--spokes", type=int, default=2048, help="virtual spokes per GPU")
+    ap.add_argument("--rows", type=int, default=64, help="examples per spoke per round")
+    ap.add_argument("--dim-log2", type=int, default=20)
+    ap.add_argument("--table-log2", type=int, default=12, help="LDS delta table (entries, log2)")
+    ap.add_argument("--model-dtype", default="bf16", choices=["fp32", "bf16"])
+    ap.add_argument("--num-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")
+    ap.add_argument("--ingest", default="pinned", choices=["pinned", "device"],
+                    help="pinned: H2D copy of every batch inside the timed loop")
+    ap.add_argument("--latency-samples", type=int, default=2000)
+    ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
+    a = ap.parse_args(argv)
+
+    comm, device = init_distributed()
+    rank, world = comm.rank, comm.world
+    on_gpu = device.type == "cuda"
+    space = FeatureSpace(13, 0, 26, 1 << a.dim_log2)
+    S, R = a.spokes, a.rows
+    B = S * R
+    num_dtype = torch.bfloat16 if a.num_dtype == "bf16" else torch.float32
+
+    # ---- synthetic stream shard of this rank, pinned, packed
+    pool = []
+    for k in range(a.pool):
+        pb = PackedBatch(space, B, "cpu", on_gpu, num_dtype)
+        tmp = synth_batch(space, B, start=(k * world + rank) * B, seed=25)
+        pb.batch.num.copy_(tmp.num)
+        pb.batch.cat.copy_(tmp.cat)
+        pb.batch.y.copy_(tmp.y)
+        pool.append(pb)
+    dev = [PackedBatch(space, B, device, False, num_dtype) for _ in range(2)]
+    if a.ingest == "device":
+        dev = [PackedBatch(space, B, device, False, num_dtype) for _ in range(a.pool)]
+        for d, p in zip(dev, pool):
+            d.flat.copy_(p.flat)
+
+    learner = SVM({"variant": "PA-I", "C": 1.0, "modelDtype": a.model_dtype,
+                   "tableLog2": a.table_log2}, space, device)
+    proto = Synchronous(comm, learner, {"virtualSpokes": S,
+                                        **({"HubParallelism": a.hubs} if a.hubs else {})})
+
+    copy_stream = torch.cuda.Stream(device) if on_gpu else None
+    copied = [torch.cuda.Event() for _ in range(2)] if on_gpu else None
+    consumed = [torch.cuda.Event() for _ in range(2)] if on_gpu else None
+
+    def prefetch(k: int):
+        if a.ingest == "device":
+            return
+        slot = k % 2
+        src = pool[k % a.pool]
+        if on_gpu:
+            with torch.cuda.stream(copy_stream):
+                copy_stream.wait_event(consumed[slot])
+                dev[slot].flat.copy_(src.flat, non_blocking=True)
+                copied[slot].record(copy_stream)
+        else:
+            dev[slot].flat.copy_(src.flat)
+
+    def step(k: int):
+        if a.ingest == "device":
+            proto.round(dev[k % a.pool].batch)
+            return
+        slot = k % 2
+        prefetch(k + 1)
+        if on_gpu:
+            torch.cuda.current_stream().wait_event(copied[slot])
+        proto.round(dev[slot].batch)
+        if on_gpu:
+            consumed[slot].record()
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(device)
+        comm.barrier()
+        if on_gpu:
+            torch.cuda.synchronize(device)
+
+    if on_gpu:
+        for e in consumed:
+            e.record()
+    prefetch(0)
+    for k in range(a.warmup):
+        step(k)
+    sync()
+    t0 = time.perf_counter()
+    for k in range(a.warmup, a.warmup + a.steps):
+        step(k)
+    sync()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=device if on_gpu else "cpu")
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # ---- model quality sanity (holdout from a disjoint part of the stream)
+    test = synth_batch(space, 20000, start=10**9 + rank, seed=25).to(device)
+    acc = float(((learner.decision(test) >= 0).float() * 2 - 1 == test.y).float().mean())
+    fitted = learner.running_totals()["fitted"]
+    overflow = learner.running_totals()["overflow"]
+
+    # ---- p50 single-point predict latency: host point → HBM → kernel → host
+    lat_us = []
+    if rank == 0:
+        one = synth_batch(space, 1, start=123, seed=25, pin=on_gpu)
+        one_dev = HashedBatch.empty(space, 1, device=device)
+        res = torch.empty(1, dtype=torch.float32, pin_memory=on_gpu)
+        for i in range(a.latency_samples + 50):
+            t = time.perf_counter()
+            one_dev.num.copy_(one.num, non_blocking=True)
+            one_dev.cat.copy_(one.cat, non_blocking=True)
+            s = learner.decision(one_dev)
+            res.copy_(s, non_blocking=True)
+            if on_gpu:
+                torch.cuda.current_stream().synchronize()
+            if i >= 50:
+                lat_us.append((time.perf_counter() - t) * 1e6)
+    p50 = statistics.median(lat_us) if lat_us else None
+
+    total_examples = a.steps * B * world
+    value = total_examples / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "examples/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32-update/bf16-model" if a.model_dtype == "bf16" else "fp32",
+            "data": "synthetic (Criteo-shaped hashed stream, pinned host pool replayed; H2D in timed loop)"
+                    if a.ingest == "pinned" else "synthetic (HBM-resident replay)",
+            "config": {"model": f"linear SVM PA-I, 2^{a.dim_log2} hashed features "
+                                f"(13 num + 26 cat + bias)",
+                       "global_batch": B * world, "seq_len": None,
+                       "parallelism": f"dp{world}", "protocol": "Synchronous",
+                       "virtual_spokes_per_gpu": S, "rows_per_spoke_per_round": R},
+            "p50_predict_latency_us": None if p50 is None else round(p50, 2),
+            "per_gpu_examples_per_s": round(value / world, 1),
+            "holdout_accuracy": round(acc, 4), "fitted_examples_rank0": fitted,
+            "lds_table_overflow": overflow, "device": torch.cuda.get_device_name(device)
+            if on_gpu else "cpu",
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

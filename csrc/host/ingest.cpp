@@ -1,0 +1,364 @@
+// Host-side data plane: DataInstance JSON → hashed fixed-width batch, feature hashing,
+// and a deterministic synthetic stream generator.
+//
+// Reference path being replaced: Kafka JSON → Jackson `DataInstance`
+// (omldm/utils/parsers/DataInstanceParser.scala:12-22, which skips "EOS" and swallows
+// malformed records) → DataPointParser building numerical ∥ discrete→double ∥
+// categorical vectors (omldm/utils/parsers/dataStream/DataPointParser.scala:16-55).
+//
+// Batch layout (what the HIP learners consume, see csrc/kernels/linear_spoke.hip):
+//   num [B, dn]  float   numerical features then discrete features (slot j == feature j)
+//   cat [B, dc]  int32   hashed categorical slot in [dn, dim) | sign in bit 31, -1 = absent
+//   y   [B]      float   target (NaN when absent, i.e. forecasting points)
+//   op  [B]      int8    0 training, 1 forecasting, -1 invalid (dropped, counted)
+// Records are parsed by a hand-written single-pass scanner on std::thread workers.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#define OMLDM_HOST_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+inline uint32_t rotl32(uint32_t x, int8_t r) { return (x << r) | (x >> (32 - r)); }
+
+uint32_t murmur3_32(const uint8_t* data, size_t len, uint32_t seed) {
+  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+  uint32_t h1 = seed;
+  const size_t nblocks = len / 4;
+  for (size_t i = 0; i < nblocks; ++i) {
+    uint32_t k1;
+    std::memcpy(&k1, data + i * 4, 4);
+    k1 *= c1;
+    k1 = rotl32(k1, 15);
+    k1 *= c2;
+    h1 ^= k1;
+    h1 = rotl32(h1, 13);
+    h1 = h1 * 5 + 0xe6546b64u;
+  }
+  const uint8_t* tail = data + nblocks * 4;
+  uint32_t k1 = 0;
+  switch (len & 3) {
+    case 3: k1 ^= uint32_t(tail[2]) << 16; [[fallthrough]];
+    case 2: k1 ^= uint32_t(tail[1]) << 8; [[fallthrough]];
+    case 1:
+      k1 ^= tail[0];
+      k1 *= c1;
+      k1 = rotl32(k1, 15);
+      k1 *= c2;
+      h1 ^= k1;
+  }
+  h1 ^= uint32_t(len);
+  h1 ^= h1 >> 16;
+  h1 *= 0x85ebca6bu;
+  h1 ^= h1 >> 13;
+  h1 *= 0xc2b2ae35u;
+  h1 ^= h1 >> 16;
+  return h1;
+}
+
+constexpr uint32_t kSeedBase = 0x9747b28cu;
+
+// Categorical token → signed slot. Field j gets its own seed so identical strings in
+// different fields land in different slots.
+inline int32_t hash_cat(const uint8_t* s, size_t n, int field, int dn, int64_t dim) {
+  const uint32_t h = murmur3_32(s, n, kSeedBase + uint32_t(field));
+  const int64_t span = dim - dn - 1;  // slot dim-1 is reserved for the intercept
+  const int32_t slot = int32_t(dn + int64_t(h & 0x7fffffffu) % span);
+  return (h & 0x80000000u) ? int32_t(uint32_t(slot) | 0x80000000u) : slot;
+}
+
+inline uint64_t splitmix64(uint64_t& x) {
+  uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+inline double u01(uint64_t& s) { return (splitmix64(s) >> 11) * (1.0 / 9007199254740992.0); }
+inline double gauss(uint64_t& s) {
+  double u1 = u01(s), u2 = u01(s);
+  if (u1 < 1e-300) u1 = 1e-300;
+  return std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+}
+
+// ---------------------------------------------------------------- JSON scanner
+struct Cursor {
+  const char* p;
+  const char* e;
+  bool ok = true;
+  void ws() {
+    while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  }
+  bool eat(char c) {
+    ws();
+    if (p < e && *p == c) {
+      ++p;
+      return true;
+    }
+    return false;
+  }
+  bool peek(char c) {
+    ws();
+    return p < e && *p == c;
+  }
+  // Returns a view of the string contents (escapes kept raw; hashing is over raw bytes,
+  // identical to the Python fallback which also hashes the raw JSON text of the token).
+  bool str(const char*& s, size_t& n) {
+    ws();
+    if (p >= e || *p != '"') return ok = false;
+    ++p;
+    s = p;
+    while (p < e && *p != '"') {
+      if (*p == '\\') ++p;
+      ++p;
+    }
+    if (p >= e) return ok = false;
+    n = size_t(p - s);
+    ++p;
+    return true;
+  }
+  bool num(double& v) {
+    ws();
+    char* end = nullptr;
+    v = std::strtod(p, &end);
+    if (end == p || end > e) return ok = false;
+    p = end;
+    return true;
+  }
+  bool lit(const char* w) {
+    ws();
+    size_t n = std::strlen(w);
+    if (size_t(e - p) >= n && std::memcmp(p, w, n) == 0) {
+      p += n;
+      return true;
+    }
+    return false;
+  }
+  bool skip_value() {
+    ws();
+    if (p >= e) return ok = false;
+    if (*p == '"') {
+      const char* s;
+      size_t n;
+      return str(s, n);
+    }
+    if (*p == '{' || *p == '[') {
+      int depth = 0;
+      bool in_str = false;
+      while (p < e) {
+        char c = *p++;
+        if (in_str) {
+          if (c == '\\') ++p;
+          else if (c == '"') in_str = false;
+        } else if (c == '"') in_str = true;
+        else if (c == '{' || c == '[') ++depth;
+        else if (c == '}' || c == ']') {
+          if (--depth == 0) return true;
+        }
+      }
+      return ok = false;
+    }
+    if (lit("null") || lit("true") || lit("false")) return true;
+    double v;
+    return num(v);
+  }
+};
+
+inline bool key_is(const char* s, size_t n, const char* k) {
+  return std::strlen(k) == n && std::memcmp(s, k, n) == 0;
+}
+
+// Parses one record. Returns op code (0/1) or -1.
+int parse_one(const char* b, const char* e, int dnum, int ddisc, int dc, int64_t dim, float* num,
+              int32_t* cat, float* y) {
+  const int dn = dnum + ddisc;
+  for (int j = 0; j < dn; ++j) num[j] = 0.f;
+  for (int j = 0; j < dc; ++j) cat[j] = -1;
+  *y = std::nanf("");
+  Cursor c{b, e};
+  c.ws();
+  if (size_t(c.e - c.p) >= 3 && std::memcmp(c.p, "EOS", 3) == 0) return -1;
+  if (!c.eat('{')) return -1;
+  int op = -1;
+  bool any_features = false;
+  if (c.eat('}')) return -1;
+  while (c.ok) {
+    const char* k;
+    size_t kn;
+    if (!c.str(k, kn)) return -1;
+    if (!c.eat(':')) return -1;
+    if (key_is(k, kn, "numericalFeatures") || key_is(k, kn, "discreteFeatures")) {
+      const bool is_num = k[0] == 'n';
+      if (c.lit("null")) {
+      } else {
+        if (!c.eat('[')) return -1;
+        int j = 0;
+        if (!c.eat(']')) {
+          while (true) {
+            double v;
+            if (!c.num(v)) return -1;
+            const int lim = is_num ? dnum : ddisc;
+            if (j < lim) num[(is_num ? 0 : dnum) + j] = float(v);
+            ++j;
+            if (c.eat(',')) continue;
+            if (c.eat(']')) break;
+            return -1;
+          }
+        }
+        any_features = true;
+      }
+    } else if (key_is(k, kn, "categoricalFeatures")) {
+      if (c.lit("null")) {
+      } else {
+        if (!c.eat('[')) return -1;
+        int j = 0;
+        if (!c.eat(']')) {
+          while (true) {
+            const char* s;
+            size_t n;
+            if (!c.str(s, n)) return -1;
+            if (j < dc) cat[j] = hash_cat(reinterpret_cast<const uint8_t*>(s), n, j, dn, dim);
+            ++j;
+            if (c.eat(',')) continue;
+            if (c.eat(']')) break;
+            return -1;
+          }
+        }
+        any_features = true;
+      }
+    } else if (key_is(k, kn, "target")) {
+      if (!c.lit("null")) {
+        double v;
+        if (!c.num(v)) return -1;
+        *y = float(v);
+      }
+    } else if (key_is(k, kn, "operation")) {
+      const char* s;
+      size_t n;
+      if (!c.str(s, n)) return -1;
+      if (key_is(s, n, "training")) op = 0;
+      else if (key_is(s, n, "forecasting")) op = 1;
+      else return -1;
+    } else {
+      if (!c.skip_value()) return -1;
+    }
+    if (c.eat(',')) continue;
+    if (c.eat('}')) break;
+    return -1;
+  }
+  if (!c.ok || !any_features) return -1;
+  if (op == 0 && std::isnan(*y)) return -1;  // a training point needs a target
+  return op;
+}
+
+template <typename F>
+void parallel_for(int n, int nthreads, F&& f) {
+  if (nthreads <= 1 || n < 256) {
+    f(0, n);
+    return;
+  }
+  nthreads = std::min(nthreads, (n + 255) / 256);
+  std::vector<std::thread> th;
+  const int chunk = (n + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; ++t) {
+    const int a = t * chunk, b = std::min(n, a + chunk);
+    if (a >= b) break;
+    th.emplace_back([&, a, b] { f(a, b); });
+  }
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+OMLDM_HOST_API uint32_t omldm_murmur3_32(const char* s, int64_t n, uint32_t seed) {
+  return murmur3_32(reinterpret_cast<const uint8_t*>(s), size_t(n), seed);
+}
+
+OMLDM_HOST_API int32_t omldm_hash_cat(const char* s, int64_t n, int field, int dn, int64_t dim) {
+  return hash_cat(reinterpret_cast<const uint8_t*>(s), size_t(n), field, dn, dim);
+}
+
+// Parses n newline-free records buf[off[i]:off[i+1]]. Returns the number of valid records.
+OMLDM_HOST_API int64_t omldm_parse_instances(const char* buf, const int64_t* off, int n, int dnum,
+                                             int ddisc, int dc, int64_t dim, float* num,
+                                             int32_t* cat, float* y, int8_t* op, int nthreads) {
+  const int dn = dnum + ddisc;
+  std::atomic<int64_t> valid{0};
+  parallel_for(n, nthreads, [&](int a, int b) {
+    int64_t v = 0;
+    for (int i = a; i < b; ++i) {
+      const int r = parse_one(buf + off[i], buf + off[i + 1], dnum, ddisc, dc, dim,
+                              num + int64_t(i) * dn, cat + int64_t(i) * dc, y + i);
+      op[i] = int8_t(r);
+      v += r >= 0;
+    }
+    valid += v;
+  });
+  return valid.load();
+}
+
+// Deterministic synthetic stream (Criteo-like shape): dn Gaussian numerical features,
+// dc categorical fields with skewed vocabularies hashed into [dn, dim), labels from a
+// hidden linear model defined by a hash of the slot (no dim-sized table needed).
+//   task 0: binary ±1 labels; 1: regression target; 2: K-class labels in [0, K)
+// Example i of the stream is a pure function of (seed, start + i), so any shard of the
+// stream can be generated independently on any rank.
+OMLDM_HOST_API void omldm_synth_batch(uint64_t seed, int64_t start, int B, int dn, int dc,
+                                      int64_t dim, int task, int n_classes, float noise,
+                                      float* num, int32_t* cat, float* y, int nthreads) {
+  const int64_t span = dim - dn - 1;  // slot dim-1 is reserved for the intercept
+  parallel_for(B, nthreads, [&](int a, int b) {
+    for (int i = a; i < b; ++i) {
+      uint64_t s = mix64(seed * 0x9e3779b97f4a7c15ull + uint64_t(start + i));
+      float* xn = num + int64_t(i) * dn;
+      int32_t* xc = cat + int64_t(i) * dc;
+      double score[16] = {0};
+      const int K = task == 2 ? std::max(2, std::min(16, n_classes)) : 1;
+      for (int j = 0; j < dn; ++j) {
+        const double v = gauss(s);
+        xn[j] = float(v);
+        for (int k = 0; k < K; ++k) {
+          uint64_t hs = mix64((seed ^ 0x5bd1e995ull) + uint64_t(j) * 131 + uint64_t(k) * 7919);
+          score[k] += v * (gauss(hs) * 0.5);
+        }
+      }
+      for (int j = 0; j < dc; ++j) {
+        // field j vocabulary 10^(1 + j % 6); rank skewed toward small values (u^3).
+        int64_t vocab = 10;
+        for (int q = 0; q < j % 6; ++q) vocab *= 10;
+        const double u = u01(s);
+        const int64_t rank = int64_t(double(vocab) * u * u * u);
+        const uint64_t h = mix64(seed + uint64_t(j) * 0x100000001b3ull + uint64_t(rank) * 0x9e37ull);
+        const int32_t slot = int32_t(dn + int64_t(h & 0x7fffffffull) % span);
+        const bool neg = (h >> 63) & 1ull;
+        xc[j] = neg ? int32_t(uint32_t(slot) | 0x80000000u) : slot;
+        const double sv = neg ? -1.0 : 1.0;
+        for (int k = 0; k < K; ++k) {
+          uint64_t hs = mix64((seed ^ 0x27d4eb2dull) + uint64_t(slot) * 31 + uint64_t(k) * 104729);
+          score[k] += sv * (gauss(hs) * 0.5);
+        }
+      }
+      const double eps = noise * gauss(s);
+      if (task == 0) {
+        y[i] = (score[0] + eps) >= 0.0 ? 1.f : -1.f;
+      } else if (task == 1) {
+        y[i] = float(score[0] + eps);
+      } else {
+        int best = 0;
+        for (int k = 1; k < K; ++k)
+          if (score[k] > score[best]) best = k;
+        y[i] = float(best);
+      }
+    }
+  });
+}

@@ -1,0 +1,131 @@
+"""Device-friendly micro-batch of data points.
+
+Reference: a data point is a ``LabeledPoint``/``UnlabeledPoint`` built from
+(numerical DenseVector, discrete→double DenseVector, categorical String[])
+(omldm/utils/parsers/dataStream/DataPointParser.scala:21-46). Here a micro-batch of
+points is three flat arrays (see csrc/host/ingest.cpp for the exact layout):
+
+* ``num`` [B, dn] float32 — numerical then discrete features (slot j = feature j)
+* ``cat`` [B, dc] int32   — hashed categorical slot | sign bit, -1 = absent
+* ``y``   [B]     float32 — target, NaN for forecasting points / skipped rows
+
+Keeping the batch columnar and fixed-width is what lets a training micro-batch
+travel as three pinned ``hipMemcpyAsync`` copies and be consumed by one kernel launch.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+
+@dataclass(frozen=True)
+class FeatureSpace:
+    """Shape of the hashed feature space shared by every pipeline of a job."""
+
+    n_numerical: int = 13
+    n_discrete: int = 0
+    n_categorical: int = 26
+    dim: int = 1 << 20
+
+    @property
+    def dn(self) -> int:
+        return self.n_numerical + self.n_discrete
+
+    @property
+    def dc(self) -> int:
+        return self.n_categorical
+
+    def __post_init__(self):
+        if self.dim <= self.dn:
+            raise ValueError("hash dimension must exceed the number of dense slots")
+        if self.dim >= 2**31:
+            raise ValueError("hash dimension must fit in 31 bits")
+
+
+@dataclass
+class HashedBatch:
+    num: torch.Tensor
+    cat: torch.Tensor
+    y: torch.Tensor
+    raw: list | None = field(default=None, compare=False)  # optional raw records (forecasting)
+
+    @property
+    def B(self) -> int:
+        return int(self.y.shape[0])
+
+    @property
+    def dn(self) -> int:
+        return int(self.num.shape[1])
+
+    @property
+    def dc(self) -> int:
+        return int(self.cat.shape[1])
+
+    @property
+    def device(self):
+        return self.y.device
+
+    def __len__(self):
+        return self.B
+
+    @staticmethod
+    def empty(space: FeatureSpace, B: int = 0, device="cpu", pin: bool = False) -> "HashedBatch":
+        kw = dict(device=device)
+        if pin and torch.cuda.is_available():
+            kw["pin_memory"] = True
+        return HashedBatch(
+            torch.zeros((B, space.dn), dtype=torch.float32, **kw),
+            torch.full((B, space.dc), -1, dtype=torch.int32, **kw),
+            torch.full((B,), float("nan"), dtype=torch.float32, **kw),
+        )
+
+    def to(self, device, non_blocking: bool = False) -> "HashedBatch":
+        return HashedBatch(self.num.to(device, non_blocking=non_blocking),
+                           self.cat.to(device, non_blocking=non_blocking),
+                           self.y.to(device, non_blocking=non_blocking), self.raw)
+
+    def slice(self, a: int, b: int) -> "HashedBatch":
+        return HashedBatch(self.num[a:b], self.cat[a:b], self.y[a:b],
+                           None if self.raw is None else self.raw[a:b])
+
+    def select(self, idx) -> "HashedBatch":
+        if isinstance(idx, np.ndarray):
+            idx = torch.from_numpy(idx)
+        idx = idx.to(self.y.device)
+        raw = None
+        if self.raw is not None:
+            raw = [self.raw[i] for i in idx.tolist()]
+        return HashedBatch(self.num[idx], self.cat[idx], self.y[idx], raw)
+
+    @staticmethod
+    def cat_batches(batches: list["HashedBatch"]) -> "HashedBatch":
+        batches = [b for b in batches if b is not None]
+        raw = None
+        if any(b.raw is not None for b in batches):
+            raw = []
+            for b in batches:
+                raw.extend(b.raw if b.raw is not None else [None] * b.B)
+        return HashedBatch(torch.cat([b.num for b in batches]), torch.cat([b.cat for b in batches]),
+                           torch.cat([b.y for b in batches]), raw)
+
+    def contiguous(self) -> "HashedBatch":
+        return HashedBatch(self.num.contiguous(), self.cat.contiguous(), self.y.contiguous(),
+                           self.raw)
+
+    def dense(self, dim: int | None = None) -> torch.Tensor:
+        """Materialise [B, dim] dense features (tests / small dense learners only)."""
+        dim = dim or (self.dn + 1)
+        B = self.B
+        out = torch.zeros((B, dim), dtype=torch.float32, device=self.y.device)
+        dn = min(self.dn, dim)
+        out[:, :dn] = self.num[:, :dn]
+        c = self.cat.long()
+        valid = c != -1
+        idx = (c & 0x7FFFFFFF).clamp(max=dim - 1)
+        sign = torch.where(c < 0, -1.0, 1.0)
+        valid &= (c & 0x7FFFFFFF) < dim
+        rows = torch.arange(B, device=out.device).unsqueeze(1).expand_as(c)
+        out.index_put_((rows[valid], idx[valid]), sign[valid], accumulate=True)
+        return out

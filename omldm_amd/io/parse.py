@@ -1,0 +1,48 @@
+"""DataInstance JSON → HashedBatch (C++ multi-threaded scanner, csrc/host/ingest.cpp).
+
+Reference: DataInstanceParser (skip "EOS", drop malformed records silently,
+omldm/utils/parsers/DataInstanceParser.scala:12-22) + DataPointParser
+(omldm/utils/parsers/dataStream/DataPointParser.scala:16-55). Dropped records are
+counted instead of silently swallowed.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.ops import native
+
+OP_TRAINING, OP_FORECASTING, OP_INVALID = 0, 1, -1
+
+
+def hash_categorical(token: str, field: int, space: FeatureSpace) -> int:
+    b = token.encode()
+    return int(native.host().omldm_hash_cat(b, len(b), field, space.dn, space.dim))
+
+
+def parse_records(records: list, space: FeatureSpace, threads: int | None = None,
+                  keep_raw: bool = True):
+    """Returns (batch, op[int8 ndarray], n_valid). Invalid rows have op == -1."""
+    n = len(records)
+    enc = [r if isinstance(r, (bytes, bytearray)) else str(r).encode() for r in records]
+    off = np.zeros(n + 1, dtype=np.int64)
+    if n:
+        np.cumsum([len(e) for e in enc], out=off[1:])
+    buf = b"".join(enc)
+    num = torch.zeros((n, space.dn), dtype=torch.float32)
+    cat = torch.full((n, space.dc), -1, dtype=torch.int32)
+    y = torch.full((n,), float("nan"), dtype=torch.float32)
+    op = np.full(n, -1, dtype=np.int8)
+    valid = 0
+    if n:
+        threads = threads or min(8, os.cpu_count() or 1)
+        valid = native.host().omldm_parse_instances(
+            buf, off.ctypes.data, n, space.n_numerical, space.n_discrete, space.dc, space.dim,
+            num.data_ptr(), cat.data_ptr(), y.data_ptr(), op.ctypes.data, threads)
+    raw = None
+    if keep_raw:
+        raw = [e.decode() if isinstance(e, (bytes, bytearray)) else e for e in enc]
+    return HashedBatch(num, cat, y, raw), op, int(valid)

@@ -1,0 +1,119 @@
+"""Learner interface shared by all eight reference learners (+ extensions).
+
+Reference: mlAPI learners are driven through ``MLPipeline.pipePoint`` (fit one point)
+and expose parameters / hyper-parameters / data-structure maps in query responses
+(omldm/network/FlinkNetwork.scala:151-240). Here a learner is driven
+one *micro-batch round* at a time and keeps all of its state in device tensors:
+
+* ``fit(batch, ctx)`` trains on a micro-batch (virtual spokes inside when the learner
+  supports them) and returns device-side round statistics (no host sync);
+* ``state_vector()`` is the flat fp32 view that the synchronisation protocols ship over
+  RCCL; ``merge_mode`` says how worker states combine: ``"mean"`` (model averaging) or
+  ``"sum"`` (additive sufficient statistics: ORR, K-means);
+* ``predict``/``evaluate`` serve forecasts and holdout scoring.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch
+
+
+@dataclass
+class RoundContext:
+    spokes: int = 1          # virtual spokes on this rank for this round
+    inv_p: float = 1.0       # 1 / (number of workers the round's delta is averaged over)
+    fused_delta: bool = False  # leave the round delta in the sync buffer (Synchronous fast path)
+
+
+class Learner:
+    NAME = "Learner"
+    TASK = "classification"  # classification | regression | clustering
+    merge_mode = "mean"
+    supports_fused_delta = False
+
+    def __init__(self, hyper: dict | None, space: FeatureSpace, device="cpu"):
+        self.hyper = dict(hyper or {})
+        self.space = space
+        self.device = torch.device(device)
+        # device-side running counters: loss_sum, n, mistakes, sq_err, -, overflow, -, -
+        self.cum = torch.zeros(8, dtype=torch.float32, device=self.device)
+
+    # ---------------------------------------------------------------- training
+    def fit(self, batch: HashedBatch, ctx: RoundContext) -> None:
+        raise NotImplementedError
+
+    def apply_delta(self) -> None:
+        """Fold the (all-reduced) fused round delta into the model."""
+
+    def delta_buffer(self) -> torch.Tensor | None:
+        return None
+
+    # ------------------------------------------------------ protocol state view
+    def state_vector(self) -> torch.Tensor:
+        raise NotImplementedError
+
+    def load_state_vector(self, v: torch.Tensor) -> None:
+        self.state_vector().copy_(v)
+        self.on_state_loaded()
+
+    def on_state_loaded(self) -> None:
+        pass
+
+    def num_params(self) -> int:
+        return int(self.state_vector().numel())
+
+    # ---------------------------------------------------------------- inference
+    def predict(self, batch: HashedBatch) -> torch.Tensor:
+        raise NotImplementedError
+
+    def evaluate(self, batch: HashedBatch) -> tuple[torch.Tensor, torch.Tensor, int]:
+        """(loss_sum, score_sum, n) on labelled points as device scalars."""
+        raise NotImplementedError
+
+    # ---------------------------------------------------------------- API maps
+    def hyper_parameters(self) -> dict:
+        return dict(self.hyper)
+
+    def update_hyper(self, hyper: dict) -> None:
+        self.hyper.update(hyper or {})
+
+    def parameters_map(self) -> dict:
+        return {}
+
+    def data_structure(self) -> dict:
+        return {"learner": self.NAME, "task": self.TASK, "nParams": self.num_params()}
+
+    # ---------------------------------------------------------------- checkpoint
+    def state_dict(self) -> dict:
+        return {"state": self.state_vector().detach().cpu().clone(), "cum": self.cum.cpu().clone(),
+                "hyper": dict(self.hyper)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.hyper.update(sd.get("hyper", {}))
+        self.load_state_vector(sd["state"].to(self.device))
+        if "cum" in sd:
+            self.cum.copy_(sd["cum"].to(self.device))
+
+    def running_totals(self) -> dict:
+        c = self.cum.tolist()
+        return {"loss_sum": c[0], "fitted": int(c[1]), "mistakes": c[2], "sq_err": c[3],
+                "overflow": int(c[5])}
+
+
+def hp_float(h: dict, key: str, default: float) -> float:
+    v = h.get(key, default)
+    try:
+        return float(v)
+    except (TypeError, ValueError):
+        return default
+
+
+def hp_int(h: dict, key: str, default: int) -> int:
+    v = h.get(key, default)
+    try:
+        return int(v)
+    except (TypeError, ValueError):
+        return default

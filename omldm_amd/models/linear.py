@@ -1,0 +1,156 @@
+"""Online linear learners on hashed features: PA, SVM, RegressorPA (+ LogisticRegression).
+
+Reference learner names come from the request validator
+(omldm/utils/parsers/requestStream/PipelineMap.scala:68); the update rules are the
+published Passive-Aggressive family (Crammer et al. 2006) — SURVEY.md Appendix D:
+
+* ``PA``          binary hinge, τ = ℓ/‖x‖² (variant "PA"), min(C, ℓ/‖x‖²) ("PA-I"),
+                  ℓ/(‖x‖² + 1/(2C)) ("PA-II"); default PA-I.
+* ``SVM``         online linear SVM: hinge loss + L2 (``lambda`` shrink per step) with the
+                  PA-I step (BASELINE.json config 1: "Online linear SVM (PA-I)").
+* ``RegressorPA`` ε-insensitive loss, same τ family, update sign(y − w·x)·τ·x.
+* ``LogisticRegression`` (extension, BASELINE.json config 2): SGD on the log loss.
+
+All four run through one hand-written kernel (csrc/kernels/linear_spoke.hip): a round
+of S virtual spokes, each an exact sequential learner on its R-row shard.
+"""
+from __future__ import annotations
+
+import torch
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.models.base import Learner, RoundContext, hp_float, hp_int
+from omldm_amd.ops import linear as L
+
+_VARIANTS = {"PA": L.PA, "PA-I": L.PA1, "PA1": L.PA1, "PA-II": L.PA2, "PA2": L.PA2}
+
+
+class LinearLearner(Learner):
+    NAME = "Linear"
+    RULE = L.RULE_HINGE
+    DEFAULT_VARIANT = "PA-I"
+    supports_fused_delta = True
+
+    def __init__(self, hyper: dict | None, space: FeatureSpace, device="cpu"):
+        super().__init__(hyper, space, device)
+        self.dim = space.dim
+        self.w = torch.zeros(self.dim, dtype=torch.float32, device=self.device)
+        self.w16 = None
+        self.dacc = torch.zeros(self.dim + 2, dtype=torch.float32, device=self.device)
+        self._configure()
+
+    def _configure(self) -> None:
+        h = self.hyper
+        variant = str(h.get("variant", self.DEFAULT_VARIANT))
+        self.rule = L.LinearRule(
+            rule=self.RULE,
+            variant=_VARIANTS.get(variant, L.PA1),
+            C=hp_float(h, "C", 1.0),
+            eps=hp_float(h, "epsilon", 0.1),
+            lr=hp_float(h, "learningRate", 0.1),
+            lam=hp_float(h, "lambda", 0.0),
+            bias=bool(h.get("bias", True)),
+        )
+        self.log2cap = hp_int(h, "tableLog2", 13)
+        want16 = str(h.get("modelDtype", "fp32")).lower() in ("bf16", "bfloat16")
+        if want16 and self.w16 is None:
+            self.w16 = self.w.to(torch.bfloat16)
+        elif not want16:
+            self.w16 = None
+
+    def update_hyper(self, hyper: dict) -> None:
+        super().update_hyper(hyper)
+        self._configure()
+
+    # ---------------------------------------------------------------- training
+    def _wread(self) -> torch.Tensor:
+        return self.w16 if self.w16 is not None else self.w
+
+    def fit(self, batch: HashedBatch, ctx: RoundContext) -> None:
+        B = batch.B
+        S = max(1, int(ctx.spokes))
+        R = max(1, -(-B // S)) if B else 1
+        if B:
+            L.linear_round(self._wread(), batch, R, S, self.dacc, None, self.rule, ctx.inv_p,
+                           self.log2cap, cum=self.cum)
+        if not ctx.fused_delta:
+            self.apply_delta()
+
+    def delta_buffer(self) -> torch.Tensor:
+        return self.dacc
+
+    def apply_delta(self) -> None:
+        L.linear_apply(self.w, self.w16, self.dacc)
+
+    # ------------------------------------------------------------ protocol view
+    def state_vector(self) -> torch.Tensor:
+        return self.w
+
+    def on_state_loaded(self) -> None:
+        if self.w16 is not None:
+            self.w16.copy_(self.w)
+
+    # ---------------------------------------------------------------- inference
+    def decision(self, batch: HashedBatch) -> torch.Tensor:
+        return L.linear_predict(self._wread(), batch, bias=self.rule.bias)
+
+    def predict(self, batch: HashedBatch) -> torch.Tensor:
+        s = self.decision(batch)
+        if self.TASK == "classification":
+            return torch.where(s >= 0, 1.0, -1.0)
+        return s
+
+    def evaluate(self, batch: HashedBatch):
+        s = self.decision(batch)
+        y = batch.y
+        ok = ~torch.isnan(y)
+        n = int(ok.sum().item()) if batch.B else 0
+        if self.TASK == "classification":
+            ym = (y * s)[ok]
+            if self.RULE == L.RULE_LOGISTIC:
+                loss = torch.nn.functional.softplus(-ym).sum()
+            else:
+                loss = torch.clamp(1 - ym, min=0).sum()
+            score = (ym > 0).float().sum()
+        else:
+            e = (y - s)[ok]
+            loss = torch.clamp(e.abs() - self.rule.eps, min=0).sum()
+            score = (e * e).sum()  # summed squared error → RMSE at the reducer
+        return loss, score, n
+
+    # ---------------------------------------------------------------- API maps
+    def hyper_parameters(self) -> dict:
+        r = self.rule
+        names = {L.PA: "PA", L.PA1: "PA-I", L.PA2: "PA-II"}
+        return {**self.hyper, "C": r.C, "variant": names[r.variant], "epsilon": r.eps,
+                "learningRate": r.lr, "lambda": r.lam, "bias": r.bias}
+
+    def parameters_map(self) -> dict:
+        w = self.w.detach().cpu()
+        nz = torch.nonzero(w[: self.dim - 1]).flatten()
+        return {"weights": w[: self.dim - 1].tolist() if self.dim <= 1 << 16 else None,
+                "nonZeroIndices": nz.tolist(), "nonZeroWeights": w[nz].tolist(),
+                "intercept": float(w[self.dim - 1]) if self.rule.bias else 0.0}
+
+    def data_structure(self) -> dict:
+        return {**super().data_structure(), "dim": self.dim, "numerical": self.space.dn,
+                "categorical": self.space.dc, "modelDtype": "bf16" if self.w16 is not None else "fp32"}
+
+
+class PA(LinearLearner):
+    NAME = "PA"
+
+
+class SVM(LinearLearner):
+    NAME = "SVM"
+
+
+class RegressorPA(LinearLearner):
+    NAME = "RegressorPA"
+    TASK = "regression"
+    RULE = L.RULE_EPS
+
+
+class LogisticRegression(LinearLearner):
+    NAME = "LogisticRegression"
+    RULE = L.RULE_LOGISTIC

@@ -1,0 +1,114 @@
+"""Linear-family ops: virtual-spoke training round, batched predict, round apply.
+
+GPU tensors → hand-written HIP kernels (csrc/kernels/linear_spoke.hip).
+CPU tensors → the C++ reference implementation (csrc/host/linear_cpu.cpp) with the
+identical semantics (golden oracle + CPU engine path).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+
+from omldm_amd.api.batch import HashedBatch
+from omldm_amd.ops import native
+from omldm_amd.ops.native import check, ptr
+
+STAT_W = 6  # loss_sum, n, mistakes, sq_err, sigma, overflow
+
+RULE_HINGE, RULE_EPS, RULE_LOGISTIC = 0, 1, 2
+PA, PA1, PA2 = 0, 1, 2
+
+
+@dataclass
+class LinearRule:
+    rule: int = RULE_HINGE
+    variant: int = PA1
+    C: float = 1.0
+    eps: float = 0.1
+    lr: float = 0.1
+    lam: float = 0.0
+    bias: bool = True
+
+
+def _cpu_threads() -> int:
+    return int(os.environ.get("OMLDM_CPU_THREADS", min(8, os.cpu_count() or 1)))
+
+
+def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torch.Tensor,
+                 stats: torch.Tensor | None, rule: LinearRule, inv_p: float, log2cap: int = 13,
+                 cum: torch.Tensor | None = None) -> None:
+    """One protocol round of S virtual spokes, R examples each (spoke s gets rows
+    [s·R, (s+1)·R)). Every spoke with ≥1 row accumulates σ·Δ·inv_p into ``dacc[:dim]``,
+    σ·inv_p into ``dacc[dim]`` and inv_p into ``dacc[dim+1]`` (so ``dacc`` is [dim+2]);
+    writes per-spoke stats [S, 6] (optional) and adds the round totals into ``cum[:6]``
+    (optional, device-side running counters). ``linear_apply`` then averages over the
+    active workers: w = (dacc[dim]·w + dacc[:dim]) / dacc[dim+1]."""
+    dim = int(dacc.shape[0]) - 2
+    assert w.shape[0] == dim and (stats is None or stats.shape == (S, STAT_W))
+    assert dacc.dtype == torch.float32
+    num, cat, y = batch.num, batch.cat, batch.y
+    assert cat.dtype == torch.int32 and y.dtype == torch.float32
+    assert num.is_contiguous() and cat.is_contiguous() and y.is_contiguous()
+    if S <= 0:
+        return
+    if w.is_cuda:
+        assert num.is_cuda and cat.is_cuda and y.is_cuda and dacc.is_cuda
+        assert stats is None or stats.is_cuda
+        assert num.dtype in (torch.float32, torch.bfloat16)
+        assert num.shape[1] + cat.shape[1] + int(rule.bias) <= 256, "≤ 256 features per example"
+        rc = native.hip().omldm_linear_round(
+            ptr(w), int(w.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
+            num.shape[1], ptr(cat), cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim,
+            ptr(stats), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, rule.lam,
+            inv_p, int(rule.bias), log2cap, native.stream_of(w))
+        check(rc, "omldm_linear_round")
+    else:
+        num32 = num.float().contiguous()
+        st = stats if stats is not None else torch.zeros((S, STAT_W), dtype=torch.float32)
+        native.host().omldm_cpu_linear_round(
+            ptr(w), int(w.dtype == torch.bfloat16), ptr(num32), num32.shape[1], ptr(cat),
+            cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim, ptr(st), rule.rule,
+            rule.variant, rule.C, rule.eps, rule.lr, rule.lam, inv_p, int(rule.bias),
+            _cpu_threads())
+        if cum is not None:
+            cum[:STAT_W] += st.sum(0)
+            cum[4] -= st[:, 4].sum()  # sigma is not a running total
+
+
+def linear_apply(w32: torch.Tensor, w16: torch.Tensor | None, dacc: torch.Tensor) -> None:
+    """w = dacc[dim]·w + dacc[:dim]; dacc = 0; refresh the bf16 shadow if given."""
+    dim = int(w32.shape[0])
+    if w32.is_cuda:
+        check(native.hip().omldm_linear_apply(ptr(w32), ptr(w16), ptr(dacc), dim,
+                                              native.stream_of(w32)), "omldm_linear_apply")
+    else:
+        native.host().omldm_cpu_linear_apply(ptr(w32), ptr(w16), ptr(dacc), dim)
+
+
+def linear_predict(w: torch.Tensor, batch: HashedBatch, wscale: torch.Tensor | None = None,
+                   out: torch.Tensor | None = None, bias: bool = True) -> torch.Tensor:
+    """Scores for every (point, model): w is [dim] or [M, dim]; returns [B] or [B, M]."""
+    single = w.dim() == 1
+    W = w.unsqueeze(0) if single else w
+    M, dim = int(W.shape[0]), int(W.shape[1])
+    B = batch.B
+    if out is None:
+        out = torch.empty((B, M), dtype=torch.float32, device=w.device)
+    if B == 0:
+        return out.view(B) if single else out
+    if w.is_cuda:
+        num = batch.num
+        rc = native.hip().omldm_linear_predict(
+            ptr(W), int(W.dtype == torch.bfloat16), W.stride(0), M, ptr(num),
+            int(num.dtype == torch.bfloat16), num.shape[1], ptr(batch.cat), batch.cat.shape[1], B,
+            dim, int(bias), ptr(wscale), ptr(out), native.stream_of(w))
+        check(rc, "omldm_linear_predict")
+    else:
+        W32 = W.float().contiguous()
+        num = batch.num.float().contiguous()
+        native.host().omldm_cpu_linear_predict(ptr(W32), W32.stride(0), M, ptr(num), num.shape[1],
+                                               ptr(batch.cat), batch.cat.shape[1], B, dim,
+                                               int(bias), ptr(wscale), ptr(out))
+    return out.view(B) if single else out

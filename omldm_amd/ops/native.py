@@ -1,0 +1,128 @@
+"""ctypes bindings to the in-tree native libraries.
+
+* ``libomldm_hip.so``  — hand-written CDNA4 kernels (csrc/kernels/*.hip, gfx950).
+* ``libomldm_host.so`` — host data plane + CPU reference implementations (csrc/host).
+
+The HIP library is REQUIRED whenever a tensor lives on a GPU: ops never fall back to
+PyTorch eager code silently; a missing/stale build raises :class:`NativeMissing`.
+Kernel launchers take raw device pointers and the current HIP stream
+(``torch.cuda.current_stream().cuda_stream``) so they order correctly with PyTorch
+work and RCCL collectives issued on the same stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE_DIR = os.path.join(_HERE, "_native")
+HIP_LIB_PATH = os.path.join(NATIVE_DIR, "libomldm_hip.so")
+HOST_LIB_PATH = os.path.join(NATIVE_DIR, "libomldm_host.so")
+
+_lock = threading.Lock()
+_hip = None
+_host = None
+
+vp, i32, i64, u32, u64, f32 = C.c_void_p, C.c_int, C.c_longlong, C.c_uint32, C.c_uint64, C.c_float
+
+
+class NativeMissing(RuntimeError):
+    pass
+
+
+def _sig(lib, name, res, args):
+    fn = getattr(lib, name)
+    fn.restype = res
+    fn.argtypes = args
+    return fn
+
+
+# (name, restype, argtypes) for every exported HIP launcher.
+HIP_SIGS = [
+    ("omldm_linear_round", i32, [vp, i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, vp, i32, vp,
+                                 vp, i32, i32, f32, f32, f32, f32, f32, i32, i32, vp]),
+    ("omldm_linear_predict", i32, [vp, i32, i64, i32, vp, i32, i32, vp, i32, i32, i32, i32, vp,
+                                   vp, vp]),
+    ("omldm_linear_apply", i32, [vp, vp, vp, i32, vp]),
+]
+
+HOST_SIGS = [
+    ("omldm_murmur3_32", u32, [C.c_char_p, i64, u32]),
+    ("omldm_hash_cat", C.c_int32, [C.c_char_p, i64, i32, i32, i64]),
+    ("omldm_parse_instances", i64, [C.c_char_p, vp, i32, i32, i32, i32, i64, vp, vp, vp, vp, i32]),
+    ("omldm_synth_batch", None, [u64, i64, i32, i32, i32, i64, i32, i32, f32, vp, vp, vp, i32]),
+    ("omldm_cpu_linear_round", i32, [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, i32, vp,
+                                     i32, i32, f32, f32, f32, f32, f32, i32, i32]),
+    ("omldm_cpu_linear_apply", None, [vp, vp, vp, i32]),
+    ("omldm_cpu_linear_predict", None, [vp, i64, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp]),
+]
+
+
+class _Lib:
+    def __init__(self, path, sigs):
+        self.path = path
+        self.cdll = C.CDLL(path, mode=C.RTLD_GLOBAL)
+        for name, res, args in sigs:
+            try:
+                setattr(self, name, _sig(self.cdll, name, res, args))
+            except AttributeError:
+                pass
+
+
+def _maybe_build(host_only: bool):
+    if os.environ.get("OMLDM_NO_AUTOBUILD"):
+        return
+    from omldm_amd import _build
+
+    _build.build(host_only=host_only)
+
+
+def host() -> _Lib:
+    global _host
+    if _host is None:
+        with _lock:
+            if _host is None:
+                if not os.path.exists(HOST_LIB_PATH):
+                    _maybe_build(host_only=True)
+                if not os.path.exists(HOST_LIB_PATH):
+                    raise NativeMissing(f"{HOST_LIB_PATH} missing: run python -m omldm_amd._build")
+                _host = _Lib(HOST_LIB_PATH, HOST_SIGS)
+    return _host
+
+
+def hip() -> _Lib:
+    global _hip
+    if _hip is None:
+        with _lock:
+            if _hip is None:
+                if not os.path.exists(HIP_LIB_PATH):
+                    _maybe_build(host_only=False)
+                if not os.path.exists(HIP_LIB_PATH):
+                    raise NativeMissing(
+                        f"{HIP_LIB_PATH} missing: the HIP kernels are required on GPU; "
+                        "run python -m omldm_amd._build")
+                _hip = _Lib(HIP_LIB_PATH, HIP_SIGS)
+    return _hip
+
+
+def check(rc: int, what: str) -> None:
+    if rc:
+        raise RuntimeError(f"{what} failed with HIP error code {rc}")
+
+
+def ptr(t) -> int:
+    """Raw data pointer of a tensor/ndarray (None → NULL)."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def stream_of(t) -> int:
+    import torch
+
+    if t is not None and getattr(t, "is_cuda", False):
+        return torch.cuda.current_stream(t.device).cuda_stream
+    return 0

@@ -1,0 +1,157 @@
+"""Communication layer: the worker↔hub transport of the reference, on RCCL.
+
+Reference: spokes push model blocks to the hub through a Flink shuffle and the hub
+answers through the Kafka ``psMessages`` topic (omldm/network/FlinkNetwork.scala:242-293,
+omldm/Job.scala:77-87,136-142) — two network hops plus a broker per sync.
+Here one process drives one GPU and the hub is a collective:
+
+* hub parallelism H > 1 (sharded PS)  → ``all_reduce`` (= reduce-scatter + all-gather, RCCL
+  ring/direct algorithms over the 7 xGMI links per GPU);
+* H == 1 (single hub)                 → ``reduce`` to rank 0 + ``broadcast`` from it;
+* many pipelines due in the same round are coalesced into one flat bucket (one launch,
+  ≥ MBs, so the collective is bandwidth- rather than latency-bound).
+
+Works with backend ``nccl`` (RCCL on ROCm) on GPUs and ``gloo`` on CPU (tests). The byte
+and message counters feed the reference's ``modelsShipped/bytesShipped/numOfBlocks``
+statistics (omldm/operators/hub/FlinkHub.scala:118-127).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class CommStats:
+    collectives: int = 0
+    bytes: int = 0
+    small_collectives: int = 0
+    per_tag: dict = field(default_factory=dict)
+
+    def add(self, tag: str, nbytes: int, small: bool = False):
+        self.collectives += 1
+        self.bytes += nbytes
+        if small:
+            self.small_collectives += 1
+        self.per_tag[tag] = self.per_tag.get(tag, 0) + nbytes
+
+
+class Comm:
+    """World communicator (one rank per GPU)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.enabled = dist.is_available() and dist.is_initialized()
+        self.rank = dist.get_rank(group) if self.enabled else 0
+        self.world = dist.get_world_size(group) if self.enabled else 1
+        self.stats = CommStats()
+        self.backend = dist.get_backend(group) if self.enabled else "none"
+
+    # ------------------------------------------------------------ collectives
+    def all_reduce_(self, t: torch.Tensor, tag: str = "sync", op=None, async_op=False):
+        self.stats.add(tag, t.numel() * t.element_size(), t.numel() <= 64)
+        if self.world == 1:
+            return None
+        return dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+
+    def reduce_bcast_(self, t: torch.Tensor, root: int = 0, tag: str = "sync"):
+        """Single-hub semantics (HubParallelism == 1): reduce to root, root broadcasts."""
+        self.stats.add(tag, 2 * t.numel() * t.element_size())
+        if self.world == 1:
+            return
+        dist.reduce(t, dst=root, op=dist.ReduceOp.SUM, group=self.group)
+        dist.broadcast(t, src=root, group=self.group)
+
+    def hub_reduce_(self, t: torch.Tensor, hubs: int = 0, tag: str = "sync"):
+        if hubs == 1 and self.world > 1:
+            self.reduce_bcast_(t, 0, tag)
+        else:
+            self.all_reduce_(t, tag)
+
+    def all_reduce_coalesced_(self, ts: list[torch.Tensor], tag: str = "sync", hubs: int = 0):
+        """Flatten several buffers into one bucket, reduce once, scatter back."""
+        ts = [t for t in ts if t is not None and t.numel()]
+        if not ts:
+            return
+        if len(ts) == 1:
+            self.hub_reduce_(ts[0], hubs, tag)
+            return
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        self.hub_reduce_(flat, hubs, tag)
+        o = 0
+        for t in ts:
+            n = t.numel()
+            t.view(-1).copy_(flat[o:o + n])
+            o += n
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        if self.world > 1:
+            dist.broadcast(t, src=src, group=self.group)
+
+    def broadcast_object(self, obj, src: int = 0):
+        if self.world == 1:
+            return obj
+        box = [obj if self.rank == src else None]
+        dist.broadcast_object_list(box, src=src, group=self.group)
+        return box[0]
+
+    def all_gather_object(self, obj) -> list:
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def gather_tensor(self, t: torch.Tensor, dst: int = 0) -> list[torch.Tensor] | None:
+        """Variable-length gather along dim 0 (pads to the max length)."""
+        if self.world == 1:
+            return [t]
+        n = torch.tensor([t.shape[0]], device=t.device, dtype=torch.int64)
+        ns = [torch.zeros_like(n) for _ in range(self.world)]
+        dist.all_gather(ns, n, group=self.group)
+        ns = [int(x.item()) for x in ns]
+        mx = max(ns)
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        outs = [torch.zeros_like(pad) for _ in range(self.world)] if self.rank == dst else None
+        if self.backend == "nccl":
+            # RCCL has no gather; all_gather keeps it a single collective.
+            outs_all = [torch.zeros_like(pad) for _ in range(self.world)]
+            dist.all_gather(outs_all, pad, group=self.group)
+            outs = outs_all if self.rank == dst else None
+        else:
+            dist.gather(pad, outs, dst=dst, group=self.group)
+        self.stats.add("gather", pad.numel() * pad.element_size())
+        if self.rank != dst:
+            return None
+        return [o[:k] for o, k in zip(outs, ns)]
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier(group=self.group)
+
+
+def init_distributed(device_type: str = "auto", timeout_s: float = 600.0) -> tuple[Comm, torch.device]:
+    """Initialise torch.distributed from torchrun env vars (RANK/WORLD_SIZE/MASTER_*).
+    One process per GPU, backend nccl (= RCCL) on GPUs, gloo on CPU."""
+    import datetime
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() if device_type == "auto" else device_type != "cpu"
+    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(device)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        kw = {}
+        if use_gpu:
+            kw["device_id"] = device
+        dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return Comm(), device

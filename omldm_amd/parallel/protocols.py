@@ -1,0 +1,438 @@
+"""The eight worker↔parameter-server synchronisation protocols, on RCCL collectives.
+
+Reference: MLNodeGenerator maps ``trainingConfiguration.protocol`` to a (worker, PS) pair —
+CentralizedTraining, SingleLearner, Asynchronous, Synchronous, SSP, EASGD, GM, FGM —
+falling back to Asynchronous when missing/unknown
+(omldm/utils/generators/MLNodeGenerator.scala:20-76; algorithms: SURVEY.md Appendix E).
+
+MI355X mapping. A *worker* is one GPU rank; inside a rank the learner's virtual spokes
+are merged every round on the GPU (cheap, in HBM), so only the rank-level model crosses
+xGMI. Every protocol is written so that all ranks issue the same collectives in the same
+order (the decision logic of the "hub" is replicated on every rank from reduced values),
+which is what lets a PS be a collective instead of a server process:
+
+* Synchronous — BSP round: the round delta (fused into the learner's kernel accumulator
+  when the learner supports it) is summed by one all-reduce (H>1) or reduce+bcast (H=1).
+* Asynchronous — non-blocking: the round's local progress δ is pushed with an async
+  all-reduce and the merged update is pulled one round later; a worker never waits.
+* SSP — as Asynchronous with up to ``staleness`` pushes in flight.
+* EASGD — elastic averaging toward a centre variable every ``tau`` rounds.
+* GM — geometric monitoring: sync only when some local drift ‖w_i − E‖² leaves the safe
+  zone (a 4-byte max-reduction per round decides).
+* FGM — functional geometric monitoring with rounds/subrounds: an 8-byte sum-reduction of
+  (counter increment, φ) per local round; a full model sync only at round end.
+* CentralizedTraining — one worker, no communication.
+* SingleLearner — workers forward their points to the hub rank (0), which alone trains
+  (HT, K-means); the hub model is broadcast back for serving.
+
+``merge_mode`` of the learner selects averaging ("mean") or summing ("sum") of worker
+increments — additive sufficient statistics (ORR, K-means) must be summed.
+"""
+from __future__ import annotations
+
+import math
+from collections import deque
+from dataclasses import dataclass
+
+import torch
+
+from omldm_amd.api.batch import HashedBatch
+from omldm_amd.models.base import Learner, RoundContext
+from omldm_amd.parallel.comm import Comm
+
+
+@dataclass
+class ProtocolStatistics:
+    protocol: str
+    models_shipped: int = 0
+    bytes_shipped: int = 0
+    num_of_blocks: int = 0
+    syncs: int = 0
+    rounds: int = 0
+    small_messages: int = 0
+
+    def as_dict(self) -> dict:
+        return {"protocol": self.protocol, "modelsShipped": self.models_shipped,
+                "bytesShipped": self.bytes_shipped, "numOfBlocks": self.num_of_blocks,
+                "syncs": self.syncs, "rounds": self.rounds, "smallMessages": self.small_messages}
+
+
+def _cfg_int(cfg, k, d):
+    try:
+        return int(cfg.get(k, d))
+    except (TypeError, ValueError):
+        return d
+
+
+def _cfg_float(cfg, k, d):
+    try:
+        return float(cfg.get(k, d))
+    except (TypeError, ValueError):
+        return d
+
+
+class Protocol:
+    NAME = "Protocol"
+
+    def __init__(self, comm: Comm, learner: Learner, cfg: dict | None = None,
+                 spokes: int = 1, max_msg_params: int = 10000):
+        self.comm = comm
+        self.learner = learner
+        self.cfg = dict(cfg or {})
+        self.spokes = max(1, int(self.cfg.get("virtualSpokes", spokes)))
+        self.hubs = _cfg_int(self.cfg, "HubParallelism", 0 if comm.world > 1 else 1)
+        self.max_msg_params = max(1, int(max_msg_params))
+        self.stats = ProtocolStatistics(self.NAME)
+        self.G = comm.world
+
+    # --------------------------------------------------------------- helpers
+    def _ctx(self, fused: bool = False) -> RoundContext:
+        return RoundContext(spokes=self.spokes, inv_p=1.0, fused_delta=fused)
+
+    def _account_model_sync(self, nparams: int, nbytes: int) -> None:
+        """Every worker pushes one model to the hub and pulls one back."""
+        g = self.G
+        self.stats.syncs += 1
+        self.stats.models_shipped += 2 * g
+        self.stats.bytes_shipped += 2 * g * nbytes
+        self.stats.num_of_blocks += 2 * g * max(1, math.ceil(nparams / self.max_msg_params))
+
+    def _account_small(self, n_msgs: int, nbytes: int) -> None:
+        self.stats.small_messages += n_msgs
+        self.stats.bytes_shipped += n_msgs * nbytes
+
+    def _scale(self) -> float:
+        """Factor turning the reduced SUM of worker increments into the global increment."""
+        return 1.0 if self.learner.merge_mode == "sum" else 1.0 / self.G
+
+    # --------------------------------------------------------------- API
+    def round(self, batch: HashedBatch) -> None:
+        raise NotImplementedError
+
+    def finalize(self) -> None:
+        """Drain in-flight communication (end of stream / before a query or checkpoint)."""
+
+    def state_dict(self) -> dict:
+        return {"stats": self.stats.__dict__.copy()}
+
+    def load_state_dict(self, sd: dict) -> None:
+        for k, v in sd.get("stats", {}).items():
+            setattr(self.stats, k, v)
+
+
+class CentralizedTraining(Protocol):
+    NAME = "CentralizedTraining"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        if "virtualSpokes" not in self.cfg:
+            self.spokes = 1  # P == 1: one exact sequential learner
+
+    def round(self, batch):
+        self.learner.fit(batch, self._ctx())
+        self.stats.rounds += 1
+
+
+class Synchronous(Protocol):
+    NAME = "Synchronous"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self._E = None
+
+    def round(self, batch):
+        L = self.learner
+        if L.supports_fused_delta:
+            # Fast path: the kernel leaves Σ σ·Δ (+ counters) of every local spoke in the
+            # learner's accumulator; one collective sums it over ranks; apply averages.
+            L.fit(batch, self._ctx(fused=True))
+            buf = L.delta_buffer()
+            self.comm.hub_reduce_(buf, self.hubs, tag="sync")
+            L.apply_delta()
+            self._account_model_sync(L.num_params(), buf.numel() * buf.element_size())
+        else:
+            if self._E is None:
+                self._E = L.state_vector().detach().clone()
+            L.fit(batch, self._ctx())
+            x = L.state_vector()
+            d = x - self._E
+            self.comm.hub_reduce_(d, self.hubs, tag="sync")
+            self._E.add_(d, alpha=self._scale())
+            L.load_state_vector(self._E)
+            self._account_model_sync(L.num_params(), d.numel() * d.element_size())
+        self.stats.rounds += 1
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["E"] = None if self._E is None else self._E.cpu()
+        return sd
+
+    def load_state_dict(self, sd):
+        super().load_state_dict(sd)
+        if sd.get("E") is not None:
+            self._E = sd["E"].to(self.learner.device)
+
+
+class _Delayed(Protocol):
+    """Shared machinery of Asynchronous (depth 1) and SSP (depth = staleness).
+
+    Invariant: x = E + shipped + new, where E is the merged global model as known here,
+    ``shipped`` the local progress pushed but not yet merged, ``new`` the unpushed rest.
+    A pull replaces the worker's own raw contribution by the merged global increment.
+    """
+
+    depth = 1
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self._E = None
+        self._shipped = None
+        self._inflight: deque = deque()  # (work, reduced_buf, sent)
+
+    def _pull_one(self):
+        work, buf, sent = self._inflight.popleft()
+        if work is not None:
+            work.wait()
+        merged = buf * self._scale()
+        x = self.learner.state_vector()
+        x.add_(merged - sent)
+        self._shipped.sub_(sent)
+        self._E.add_(merged)
+        self.learner.on_state_loaded()
+
+    def round(self, batch):
+        L = self.learner
+        if self._E is None:
+            self._E = L.state_vector().detach().clone()
+            self._shipped = torch.zeros_like(self._E)
+        L.fit(batch, self._ctx())
+        sent = L.state_vector() - self._E - self._shipped
+        buf = sent.clone()
+        work = self.comm.all_reduce_(buf, tag="push", async_op=True)
+        self._shipped.add_(sent)
+        self._inflight.append((work, buf, sent))
+        self._account_model_sync(L.num_params(), buf.numel() * buf.element_size())
+        while len(self._inflight) > self.depth:
+            self._pull_one()
+        self.stats.rounds += 1
+
+    def finalize(self):
+        while self._inflight:
+            self._pull_one()
+
+    def state_dict(self):
+        self.finalize()
+        sd = super().state_dict()
+        sd["E"] = None if self._E is None else self._E.cpu()
+        return sd
+
+    def load_state_dict(self, sd):
+        super().load_state_dict(sd)
+        if sd.get("E") is not None:
+            self._E = sd["E"].to(self.learner.device)
+            self._shipped = torch.zeros_like(self._E)
+
+
+class Asynchronous(_Delayed):
+    NAME = "Asynchronous"
+    depth = 1
+
+
+class SSP(_Delayed):
+    NAME = "SSP"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.depth = max(0, _cfg_int(self.cfg, "staleness", 2))
+
+
+class EASGD(Protocol):
+    NAME = "EASGD"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.tau = max(1, _cfg_int(self.cfg, "tau", 1))
+        self.alpha = _cfg_float(self.cfg, "alpha", 0.9 / max(1, self.G))
+        self._c = None
+        self._k = 0
+
+    def round(self, batch):
+        L = self.learner
+        if self._c is None:
+            self._c = L.state_vector().detach().clone()
+        L.fit(batch, self._ctx())
+        self._k += 1
+        if self._k % self.tau == 0:
+            x = L.state_vector()
+            diff = x - self._c
+            s = diff.clone()
+            self.comm.all_reduce_(s, tag="elastic")
+            x.sub_(diff, alpha=self.alpha)                 # x_i ← x_i − α(x_i − c)
+            self._c.add_(s, alpha=self.alpha)              # c ← c + α Σ_i (x_i − c)
+            L.on_state_loaded()
+            self._account_model_sync(L.num_params(), s.numel() * s.element_size())
+        self.stats.rounds += 1
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["center"] = None if self._c is None else self._c.cpu()
+        return sd
+
+    def load_state_dict(self, sd):
+        super().load_state_dict(sd)
+        if sd.get("center") is not None:
+            self._c = sd["center"].to(self.learner.device)
+
+
+class GM(Protocol):
+    NAME = "GM"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.threshold = _cfg_float(self.cfg, "threshold", 0.05)
+        self._E = None
+        self._flag = None
+
+    def _full_sync(self):
+        L = self.learner
+        d = (L.state_vector() - self._E) * (self.G if L.merge_mode == "sum" else 1.0)
+        self.comm.all_reduce_(d, tag="sync")
+        self._E.add_(d, alpha=1.0 / self.G)
+        L.load_state_vector(self._E)
+        self._account_model_sync(L.num_params(), d.numel() * d.element_size())
+
+    def round(self, batch):
+        L = self.learner
+        if self._E is None:
+            self._E = L.state_vector().detach().clone()
+        L.fit(batch, self._ctx())
+        x = L.state_vector()
+        scale = self.G if L.merge_mode == "sum" else 1.0
+        drift = ((x - self._E) * scale).pow(2).sum()
+        ref = self._E.pow(2).sum()
+        # safe zone: ‖X_i‖² ≤ θ·‖E‖² (θ·1 while E == 0)
+        viol = (drift > self.threshold * torch.clamp(ref, min=1.0)).float().reshape(1)
+        self.comm.all_reduce_(viol, tag="gm-flag", op=torch.distributed.ReduceOp.MAX)
+        self._account_small(self.G, 4)
+        if viol.item() > 0:
+            self._full_sync()
+        self.stats.rounds += 1
+
+
+class FGM(Protocol):
+    """Functional Geometric Monitoring (variance safe function).
+
+    Safe function on a worker's drift X_i (state − E, scaled by G for additive state):
+        φ(X) = ‖X‖² − ε‖E‖²          (φ(0) = −ε‖E‖² < 0 while E ≠ 0)
+    round start: ψ = G·φ(0), quantum θ = −ψ / (2G);
+    subround: worker counter c_i = ⌊(φ(X_i) − φ(0)) / θ⌋, the hub sums increments;
+    when Σ c_i > G the hub collects ψ = Σ φ(X_i): if ψ ≥ ε_ψ·G·φ(0) the round ends with
+    a full model sync, otherwise a new subround starts with θ = −ψ / (2G).
+    The hub logic runs replicated on every rank from one 2-float all-reduce per local
+    round ((Δc_i, φ_i)), so only round ends move models over xGMI.
+    """
+
+    NAME = "FGM"
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.eps = _cfg_float(self.cfg, "epsilon", 0.05)
+        self.eps_psi = _cfg_float(self.cfg, "epsilonPsi", 0.01)
+        self._E = None
+        self._c_prev = 0
+        self._theta = None
+        self._phi0 = None
+        self.subrounds = 0
+        self.fgm_rounds = 0
+
+    def _begin_round(self):
+        L = self.learner
+        self._E = L.state_vector().detach().clone()
+        e2 = float(self._E.pow(2).sum().item())
+        self._phi0 = -self.eps * e2
+        psi = self.G * self._phi0
+        self._theta = -psi / (2 * self.G) if psi < 0 else None
+        self._c_prev = 0
+        self.fgm_rounds += 1
+
+    def _full_sync(self):
+        L = self.learner
+        d = (L.state_vector() - self._E) * (self.G if L.merge_mode == "sum" else 1.0)
+        self.comm.all_reduce_(d, tag="sync")
+        self._E.add_(d, alpha=1.0 / self.G)
+        L.load_state_vector(self._E)
+        self._account_model_sync(L.num_params(), d.numel() * d.element_size())
+
+    def round(self, batch):
+        L = self.learner
+        if self._E is None:
+            self._begin_round()
+        L.fit(batch, self._ctx())
+        if self._theta is None:  # E == 0: nothing to monitor against → sync, new round
+            self._full_sync()
+            self._begin_round()
+            self.stats.rounds += 1
+            return
+        x = L.state_vector()
+        scale = self.G if L.merge_mode == "sum" else 1.0
+        X2 = ((x - self._E) * scale).pow(2).sum()
+        phi = X2 - self.eps * self._E.pow(2).sum()
+        c = torch.floor((phi - self._phi0) / self._theta).clamp(min=0)
+        inc = c - self._c_prev
+        msg = torch.stack([inc, phi]).float()
+        self.comm.all_reduce_(msg, tag="fgm-counters")
+        self._c_prev = c
+        self._account_small(self.G, 8)
+        tot_inc, psi = msg.tolist()
+        self._csum = getattr(self, "_csum", 0.0) + tot_inc
+        if self._csum > self.G:
+            self.subrounds += 1
+            if psi >= self.eps_psi * self.G * self._phi0:
+                self._full_sync()
+                self._begin_round()
+                self._csum = 0.0
+            else:
+                self._theta = -psi / (2 * self.G)
+                self._phi0_sub = psi
+                self._csum = 0.0
+                # counters restart relative to the new subround
+                self._c_prev = torch.floor((phi - self._phi0) / self._theta).clamp(min=0)
+        self.stats.rounds += 1
+
+
+class SingleLearner(Protocol):
+    """Workers forward training points to the hub rank, which alone trains (HT, K-means);
+    reference: ForwardingWorker + CentralizedMLServer (MLNodeGenerator.scala:27,56)."""
+
+    NAME = "SingleLearner"
+    HUB = 0
+
+    def round(self, batch):
+        L = self.learner
+        parts = {}
+        for name in ("num", "cat", "y"):
+            parts[name] = self.comm.gather_tensor(getattr(batch, name).contiguous(), dst=self.HUB)
+        if self.comm.rank == self.HUB:
+            merged = HashedBatch(torch.cat(parts["num"]), torch.cat(parts["cat"]),
+                                 torch.cat(parts["y"]))
+            L.fit(merged, RoundContext(spokes=1))
+        self._account_small(self.G, batch.B)  # forwarded points
+        # hub → spokes: serve forecasts from an up-to-date replica
+        v = L.state_vector()
+        if self.G > 1:
+            self.comm.broadcast_(v, src=self.HUB)
+            L.on_state_loaded()
+            self._account_model_sync(L.num_params(), v.numel() * v.element_size())
+        self.stats.rounds += 1
+
+
+PROTOCOLS = {c.NAME: c for c in (CentralizedTraining, Synchronous, Asynchronous, SSP, EASGD, GM,
+                                 FGM, SingleLearner)}
+
+
+def make_protocol(name: str | None, comm: Comm, learner: Learner, cfg: dict | None = None,
+                  spokes: int = 1, max_msg_params: int = 10000) -> Protocol:
+    """Reference fallback rule: unknown or missing protocol → Asynchronous
+    (omldm/utils/generators/MLNodeGenerator.scala:26-38)."""
+    cls = PROTOCOLS.get(name or "", Asynchronous)
+    return cls(comm, learner, cfg, spokes=spokes, max_msg_params=max_msg_params)

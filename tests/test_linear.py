@@ -1,0 +1,215 @@
+"""Linear learners: pure-Python golden ↔ C++ CPU path ↔ HIP kernel (gpu-marked)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.io.synthetic import synth_batch, TASK_BINARY, TASK_REGRESSION
+from omldm_amd.ops import linear as L
+
+
+def python_round(w, batch, R, S, rule: L.LinearRule, inv_p=1.0):
+    """Literal per-example reference of one round (SURVEY App. D rules), fp64 host."""
+    dim = w.shape[0]
+    num, cat, y = batch.num.double().numpy(), batch.cat.numpy(), batch.y.double().numpy()
+    B = y.shape[0]
+    dacc = np.zeros(dim + 2)
+    stats = np.zeros((S, 6))
+    for s in range(S):
+        a, b = min(s * R, B), min(s * R + R, B)
+        if a >= b:
+            stats[s, 4] = 1
+            continue
+        delta = {}
+        sigma = 1.0
+        for t in range(a, b):
+            yt = y[t]
+            if math.isnan(yt):
+                continue
+            feats = [(j, num[t, j]) for j in range(num.shape[1]) if j < dim]
+            for c in cat[t]:
+                if c == -1:
+                    continue
+                idx = int(c) & 0x7FFFFFFF
+                if idx < dim:
+                    feats.append((idx, -1.0 if c < 0 else 1.0))
+            if rule.bias:
+                feats.append((dim - 1, 1.0))
+            pm = sum(v * (float(w[i]) + delta.get(i, 0.0)) for i, v in feats)
+            n2 = sum(v * v for _, v in feats)
+            m = sigma * pm
+
+            def tau(loss):
+                if loss <= 0 or n2 <= 0:
+                    return 0.0
+                if rule.variant == L.PA:
+                    return loss / n2
+                if rule.variant == L.PA1:
+                    return min(rule.C, loss / n2)
+                return loss / (n2 + 0.5 / rule.C)
+
+            if rule.rule == L.RULE_HINGE:
+                loss = max(0.0, 1 - yt * m)
+                c = tau(loss) * yt
+                stats[s, 2] += yt * m <= 0
+                shrink = 1 - rule.lam
+            elif rule.rule == L.RULE_EPS:
+                err = yt - m
+                loss = max(0.0, abs(err) - rule.eps)
+                c = tau(loss) * (1 if err >= 0 else -1)
+                stats[s, 3] += err * err
+                shrink = 1 - rule.lam
+            else:
+                z = yt * m
+                loss = math.log1p(math.exp(-z)) if z > 0 else -z + math.log1p(math.exp(z))
+                c = rule.lr * yt / (1 + math.exp(z))
+                stats[s, 2] += z <= 0
+                shrink = 1 - rule.lr * rule.lam
+            stats[s, 0] += loss
+            stats[s, 1] += 1
+            sigma *= shrink
+            if c:
+                for i, v in feats:
+                    delta[i] = delta.get(i, 0.0) + c / sigma * v
+        stats[s, 4] = sigma
+        for i, v in delta.items():
+            dacc[i] += v * sigma * inv_p
+        dacc[dim] += sigma * inv_p
+        dacc[dim + 1] += inv_p
+    return dacc, stats
+
+
+RULES = [
+    L.LinearRule(L.RULE_HINGE, L.PA1, C=0.5),
+    L.LinearRule(L.RULE_HINGE, L.PA, bias=False),
+    L.LinearRule(L.RULE_HINGE, L.PA2, C=2.0, lam=1e-3),
+    L.LinearRule(L.RULE_EPS, L.PA1, C=1.0, eps=0.05),
+    L.LinearRule(L.RULE_LOGISTIC, lr=0.05, lam=1e-4),
+]
+
+
+@pytest.mark.parametrize("rule", RULES)
+def test_cpu_round_matches_python(rule):
+    sp = FeatureSpace(5, 0, 7, 1 << 10)
+    task = TASK_REGRESSION if rule.rule == L.RULE_EPS else TASK_BINARY
+    b = synth_batch(sp, 300, task=task, seed=3)
+    b.y[17] = float("nan")  # skipped row
+    w = torch.randn(sp.dim) * 0.1
+    R, S = 37, 9  # last spokes idle
+    dacc = torch.zeros(sp.dim + 2)
+    stats = torch.zeros(S, 6)
+    L.linear_round(w, b, R, S, dacc, stats, rule, 1.0)
+    ref_d, ref_s = python_round(w, b, R, S, rule)
+    np.testing.assert_allclose(dacc.numpy(), ref_d, rtol=2e-4, atol=2e-5)
+    np.testing.assert_allclose(stats.numpy()[:, [1, 2, 4]], ref_s[:, [1, 2, 4]], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(stats.numpy()[:, 0], ref_s[:, 0], rtol=1e-3, atol=1e-3)
+
+
+def test_apply_averages_active_workers():
+    dim = 16
+    w = torch.arange(dim, dtype=torch.float32)
+    d = torch.zeros(dim + 2)
+    d[:dim] = 2.0
+    d[dim] = 1.5   # Σσ/P over 2 active workers (σ = 1, 0.5)
+    d[dim + 1] = 2.0
+    L.linear_apply(w, None, d)
+    np.testing.assert_allclose(w.numpy(), (1.5 * np.arange(dim) + 2.0) / 2.0, rtol=1e-6)
+    assert float(d.abs().sum()) == 0.0
+
+
+def test_apply_no_workers_is_identity():
+    w = torch.randn(64)
+    w0 = w.clone()
+    d = torch.zeros(66)
+    L.linear_apply(w, None, d)
+    assert torch.equal(w, w0)
+
+
+def test_predict_matches_dense():
+    sp = FeatureSpace(4, 0, 6, 1 << 9)
+    b = synth_batch(sp, 50, seed=5)
+    W = torch.randn(3, sp.dim)
+    out = L.linear_predict(W, b)
+    X = b.dense(sp.dim)
+    X[:, sp.dim - 1] = 1.0  # intercept slot
+    np.testing.assert_allclose(out.numpy(), (X @ W.T).numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_single_spoke_learns():
+    sp = FeatureSpace(13, 0, 26, 1 << 16)
+    w = torch.zeros(sp.dim)
+    d = torch.zeros(sp.dim + 2)
+    test = synth_batch(sp, 3000, start=10**8)
+    for r in range(6):
+        L.linear_round(w, synth_batch(sp, 4096, start=r * 4096), 4096, 1, d, None,
+                       L.LinearRule(), 1.0)
+        L.linear_apply(w, None, d)
+    acc = float(((L.linear_predict(w, test) >= 0).float() * 2 - 1 == test.y).float().mean())
+    assert acc > 0.7
+
+
+# ------------------------------------------------------------------ HIP kernels
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule", RULES)
+@pytest.mark.parametrize("shape", [(13, 26), (40, 50), (100, 120)])
+def test_hip_round_matches_cpu(cuda, rule, shape):
+    dn, dc = shape
+    sp = FeatureSpace(dn, 0, dc, 1 << 14)
+    task = TASK_REGRESSION if rule.rule == L.RULE_EPS else TASK_BINARY
+    b = synth_batch(sp, 2000, task=task, seed=11)
+    b.y[5] = float("nan")
+    w = torch.randn(sp.dim) * 0.05
+    R, S = 70, 31
+    d_cpu = torch.zeros(sp.dim + 2)
+    s_cpu = torch.zeros(S, 6)
+    L.linear_round(w, b, R, S, d_cpu, s_cpu, rule, 1.0)
+    d_gpu = torch.zeros(sp.dim + 2, device=cuda)
+    s_gpu = torch.zeros(S, 6, device=cuda)
+    cum = torch.zeros(8, device=cuda)
+    L.linear_round(w.to(cuda), b.to(cuda), R, S, d_gpu, s_gpu, rule, 1.0, log2cap=13, cum=cum)
+    torch.cuda.synchronize()
+    s_g = s_gpu.cpu()
+    assert float(s_g[:, 5].sum()) == 0.0  # no LDS table overflow
+    np.testing.assert_allclose(s_g[:, 1].numpy(), s_cpu[:, 1].numpy())
+    np.testing.assert_allclose(d_gpu.cpu().numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
+    np.testing.assert_allclose(cum.cpu()[1].item(), s_cpu[:, 1].sum().item())
+
+
+@pytest.mark.gpu
+def test_hip_apply_and_predict(cuda):
+    sp = FeatureSpace(13, 0, 26, (1 << 16) + 3)  # odd dim exercises the scalar tail
+    w = torch.randn(sp.dim)
+    d = torch.randn(sp.dim + 2)
+    d[sp.dim] = 0.7
+    d[sp.dim + 1] = 1.3
+    wg, dg = w.to(cuda), d.to(cuda)
+    w16 = torch.empty(sp.dim, dtype=torch.bfloat16, device=cuda)
+    L.linear_apply(w, None, d)
+    L.linear_apply(wg, w16, dg)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(wg.cpu().numpy(), w.numpy(), rtol=1e-6, atol=1e-6)
+    assert float(dg.abs().sum().item()) == 0.0
+    np.testing.assert_allclose(w16.float().cpu().numpy(), w.numpy(), rtol=1e-2, atol=1e-2)
+    b = synth_batch(sp, 777, seed=9)
+    W = torch.randn(4, sp.dim)
+    ref = L.linear_predict(W, b)
+    out = L.linear_predict(W.to(cuda), b.to(cuda))
+    np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+    out16 = L.linear_predict(W.to(cuda).bfloat16(), b.to(cuda))
+    ref16 = L.linear_predict(W.bfloat16().float(), b)
+    np.testing.assert_allclose(out16.cpu().numpy(), ref16.numpy(), rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_hip_bf16_model_round(cuda):
+    sp = FeatureSpace(13, 0, 26, 1 << 14)
+    b = synth_batch(sp, 4096, seed=2)
+    w = (torch.randn(sp.dim) * 0.05).bfloat16()
+    rule = L.LinearRule()
+    d_cpu = torch.zeros(sp.dim + 2)
+    L.linear_round(w, b, 64, 64, d_cpu, None, rule, 1.0)
+    d_gpu = torch.zeros(sp.dim + 2, device=cuda)
+    L.linear_round(w.to(cuda), b.to(cuda), 64, 64, d_gpu, None, rule, 1.0, log2cap=12)
+    np.testing.assert_allclose(d_gpu.cpu().numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
