@@ -74,6 +74,7 @@ def main(argv=None) -> int:
                     help="pinned: H2D copy of every batch inside the timed loop")
     ap.add_argument("--latency-samples", type=int, default=2000)
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
+    ap.add_argument("--ablate", type=int, default=0, help="kernel phase ablation (diagnostics)")
     a = ap.parse_args(argv)
 
     comm, device = init_distributed()
@@ -100,7 +101,7 @@ def main(argv=None) -> int:
             d.flat.copy_(p.flat)
 
     learner = SVM({"variant": "PA-I", "C": 1.0, "modelDtype": a.model_dtype,
-                   "tableLog2": a.table_log2}, space, device)
+                   "tableLog2": a.table_log2, "_ablate": a.ablate}, space, device)
     proto = Synchronous(comm, learner, {"virtualSpokes": S,
                                         **({"HubParallelism": a.hubs} if a.hubs else {})})
 

@@ -41,7 +41,6 @@ struct LinParams {
   int bias;
 };
 
-constexpr int kStatW = 6;  // loss_sum, n, mistakes, sq_err, sigma, overflow
 
 __device__ __forceinline__ float pa_tau(float loss, float n2, const LinParams& p) {
   if (loss <= 0.f || n2 <= 0.f) return 0.f;
@@ -80,23 +79,40 @@ __device__ __forceinline__ void load_feature(const NumT* __restrict__ num, int d
   }
 }
 
+// Per-spoke workspace row: [loss, n, mistakes, sq_err, sigma, overflow, σ/P, 1/P,
+//                           Δ(dense slot 0..dn-1)·σ/P, Δ(intercept)·σ/P]
+constexpr int kWsStat = 8;
+
+// Dense column of feature j: numerical slot j → j, intercept → dn; hashed features → -1.
+// Dense features live in a register per lane for the whole round (every example has
+// them), so they never touch the LDS table and never hit the same global address from
+// every spoke: they are reduced by linear_round_finish instead of by atomics.
+__device__ __forceinline__ int dense_col(int j, int dn, int dc, int bias) {
+  if (j < dn) return j;
+  if (bias && j == dn + dc) return dn;
+  return -1;
+}
+
+// ablate (timing diagnostics only, never set in production): bit0 skip the categorical
+// flush atomics, bit1 skip the sequential phase, bit2 skip the LDS slot resolution.
 template <int FPL, int CH, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void linear_round_kernel(
     const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const int* __restrict__ cat,
     int dc, const float* __restrict__ yv, int B, int R, float* __restrict__ dacc, int dim,
-    float* __restrict__ stats, float* __restrict__ cum, LinParams p, int log2cap) {
+    float* __restrict__ ws, LinParams p, int log2cap, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int cap = 1 << log2cap;
   int* keys = reinterpret_cast<int*>(smem);
   float* vals = reinterpret_cast<float*>(smem + (size_t)cap * sizeof(int));
   const int lane = threadIdx.x;
   const int s = blockIdx.x;
+  const int wsw = kWsStat + dn + 1;
+  float* wrow = ws + (size_t)s * wsw;
   const long long t0ll = (long long)s * R;
   const int t0 = t0ll > B ? B : (int)t0ll;
   const int t1 = (t0ll + R) > B ? B : (int)(t0ll + R);
   if (t0 >= t1) {  // idle spoke: not a worker of this round (does not dilute the average)
-    if (stats && lane == 0)
-      for (int k = 0; k < kStatW; ++k) stats[(size_t)s * kStatW + k] = k == 4 ? 1.f : 0.f;
+    for (int k = lane; k < wsw; k += kWave) wrow[k] = k == 4 ? 1.f : 0.f;
     return;
   }
   for (int i = lane; i < cap; i += kWave) {
@@ -105,6 +121,13 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
   }
   __syncthreads();
 
+  int dcol[FPL];
+  float dreg[FPL];
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) {
+    dcol[f] = dense_col(lane + kWave * f, dn, dc, p.bias);
+    dreg[f] = 0.f;
+  }
   float sigma = 1.f, loss_sum = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f, ovf = 0.f;
 
   for (int tc = t0; tc < t1; tc += CH) {
@@ -132,16 +155,31 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     for (int e = 0; e < CH; ++e)
 #pragma unroll
       for (int f = 0; f < FPL; ++f) wv[e][f] = slot[e][f] >= 0 ? to_f(w[slot[e][f]]) : 0.f;
-    // Phase 1c: resolve LDS slots of the private delta (insert-or-find).
+    // Phase 1c: resolve LDS slots of the private delta for hashed features.
+    if (!(ablate & 4)) {
 #pragma unroll
-    for (int e = 0; e < CH; ++e)
+      for (int e = 0; e < CH; ++e)
 #pragma unroll
-      for (int f = 0; f < FPL; ++f)
-        if (slot[e][f] >= 0) {
-          const int sl = lds_find_or_insert(keys, slot[e][f], log2cap);
-          if (sl < 0) ovf += 1.f;
-          slot[e][f] = sl;
-        }
+        for (int f = 0; f < FPL; ++f)
+          if (dcol[f] < 0 && slot[e][f] >= 0) {
+            const int sl = lds_find_or_insert(keys, slot[e][f], log2cap);
+            if (sl < 0) ovf += 1.f;
+            slot[e][f] = sl;
+          }
+    } else {
+#pragma unroll
+      for (int e = 0; e < CH; ++e)
+#pragma unroll
+        for (int f = 0; f < FPL; ++f)
+          if (slot[e][f] >= 0) slot[e][f] = (int)hslot((uint32_t)slot[e][f], log2cap);
+    }
+    if (ablate & 2) {
+#pragma unroll
+      for (int e = 0; e < CH; ++e)
+#pragma unroll
+        for (int f = 0; f < FPL; ++f) loss_sum += wv[e][f] + xv[e][f] + (float)slot[e][f];
+      continue;
+    }
     // Phase 2: exact sequential online updates.
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
@@ -150,7 +188,7 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
       float pm = 0.f, pn = 0.f;
 #pragma unroll
       for (int f = 0; f < FPL; ++f) {
-        const float d = slot[e][f] >= 0 ? vals[slot[e][f]] : 0.f;
+        const float d = dcol[f] >= 0 ? dreg[f] : (slot[e][f] >= 0 ? vals[slot[e][f]] : 0.f);
         pm = fmaf(xv[e][f], wv[e][f] + d, pm);
         pn = fmaf(xv[e][f], xv[e][f], pn);
       }
@@ -185,41 +223,67 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
       if (c != 0.f) {
         const float cv = c / sigma;
 #pragma unroll
-        for (int f = 0; f < FPL; ++f)
-          if (slot[e][f] >= 0) atomicAdd(&vals[slot[e][f]], cv * xv[e][f]);
+        for (int f = 0; f < FPL; ++f) {
+          if (dcol[f] >= 0) dreg[f] = fmaf(cv, xv[e][f], dreg[f]);
+          else if (slot[e][f] >= 0) atomicAdd(&vals[slot[e][f]], cv * xv[e][f]);
+        }
       }
     }
   }
   __syncthreads();
-  // Round end: ship σ·Δ/P into the round accumulator (sparse scatter, f32 atomics).
+  // Round end: ship σ·Δ/P. Hashed features: sparse scatter with no-return f32 atomics
+  // (distinct spokes rarely share a hashed slot); dense features: workspace row.
   const float scale = sigma * p.inv_p;
-  for (int i = lane; i < cap; i += kWave) {
-    const int k = keys[i];
-    if (k >= 0) {
-      const float v = vals[i];
-      if (v != 0.f) atomicAdd(&dacc[k], v * scale);
+  if (!(ablate & 1)) {
+    for (int i = lane; i < cap; i += kWave) {
+      const int k = keys[i];
+      if (k >= 0) {
+        const float v = vals[i];
+        if (v != 0.f) atomicAdd(&dacc[k], v * scale);
+      }
     }
   }
-  // overflow is per-lane; reduce it.
+#pragma unroll
+  for (int f = 0; f < FPL; ++f)
+    if (dcol[f] >= 0) wrow[kWsStat + dcol[f]] = dreg[f] * scale;
   const float ovf_total = wave_sum(ovf);
   if (lane == 0) {
-    atomicAdd(&dacc[dim], scale);         // Σ σ_s / P   (weight of w0)
-    atomicAdd(&dacc[dim + 1], p.inv_p);   // Σ 1 / P     (active workers)
-    if (stats) {
-      float* st = stats + (size_t)s * kStatW;
-      st[0] = loss_sum;
-      st[1] = nex;
-      st[2] = mist;
-      st[3] = sqe;
-      st[4] = sigma;
-      st[5] = ovf_total;
-    }
-    if (cum) {  // running totals, read lazily by the host (no per-round sync)
-      atomicAdd(cum + 0, loss_sum);
-      atomicAdd(cum + 1, nex);
-      atomicAdd(cum + 2, mist);
-      atomicAdd(cum + 3, sqe);
-      atomicAdd(cum + 5, ovf_total);
+    wrow[0] = loss_sum;
+    wrow[1] = nex;
+    wrow[2] = mist;
+    wrow[3] = sqe;
+    wrow[4] = sigma;
+    wrow[5] = ovf_total;
+    wrow[6] = scale;
+    wrow[7] = p.inv_p;
+  }
+}
+
+// Column sums of the per-spoke workspace (one block per column) → accumulator slots
+// that every spoke would otherwise hit with same-address atomics:
+//   dense columns → dacc[0:dn], intercept → dacc[dim-1], Σσ/P → dacc[dim],
+//   Σ1/P → dacc[dim+1], loss/n/mistakes/sq_err/overflow → cum (device running totals).
+__global__ __launch_bounds__(256) void linear_round_finish_kernel(const float* __restrict__ ws,
+                                                                  int S, int dn, int dim,
+                                                                  float* __restrict__ dacc,
+                                                                  float* __restrict__ cum) {
+  __shared__ float part[4];
+  const int c = blockIdx.x;
+  const int wsw = kWsStat + dn + 1;
+  float acc = 0.f;
+  for (int s = threadIdx.x; s < S; s += 256) acc += ws[(size_t)s * wsw + c];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = (part[0] + part[1]) + (part[2] + part[3]);
+    if (c < kWsStat) {
+      if (c == 6) dacc[dim] += t;
+      else if (c == 7) dacc[dim + 1] += t;
+      else if (c != 4 && cum) cum[c] += t;
+    } else {
+      const int j = c - kWsStat;
+      dacc[j < dn ? j : dim - 1] += t;
     }
   }
 }
@@ -290,34 +354,36 @@ __global__ __launch_bounds__(256) void linear_apply_kernel(float* __restrict__ w
 
 template <int FPL, int CH, typename NumT, typename WT>
 static int launch_round(const void* w, const void* num, int dn, const int* cat, int dc,
-                        const float* y, int B, int R, int S, float* dacc, int dim, float* stats,
-                        float* cum, const LinParams& p, int log2cap, hipStream_t st) {
+                        const float* y, int B, int R, int S, float* dacc, int dim, float* ws,
+                        float* cum, const LinParams& p, int log2cap, int ablate, hipStream_t st) {
   auto fn = linear_round_kernel<FPL, CH, NumT, WT>;
   const size_t lds = (size_t(1) << log2cap) * 8;
   int e = check_dyn_lds((const void*)fn, lds);
   if (e) return e;
   hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)w, (const NumT*)num, dn, cat, dc,
-                     y, B, R, dacc, dim, stats, cum, p, log2cap);
+                     y, B, R, dacc, dim, ws, p, log2cap, ablate);
+  hipLaunchKernelGGL(linear_round_finish_kernel, dim3(kWsStat + dn + 1), dim3(256), 0, st, ws, S,
+                     dn, dim, dacc, cum);
   return (int)hipGetLastError();
 }
 
 template <int FPL, int CH>
 static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                           const int* cat, int dc, const float* y, int B, int R, int S, float* dacc,
-                          int dim, float* stats, float* cum, const LinParams& p, int log2cap,
-                          hipStream_t st) {
+                          int dim, float* ws, float* cum, const LinParams& p, int log2cap,
+                          int ablate, hipStream_t st) {
   if (num_bf16) {
     if (w_bf16)
       return launch_round<FPL, CH, __hip_bfloat16, __hip_bfloat16>(w, num, dn, cat, dc, y, B, R, S,
-                                                                   dacc, dim, stats, cum, p, log2cap, st);
+                                                                   dacc, dim, ws, cum, p, log2cap, ablate, st);
     return launch_round<FPL, CH, __hip_bfloat16, float>(w, num, dn, cat, dc, y, B, R, S, dacc, dim,
-                                                        stats, cum, p, log2cap, st);
+                                                        ws, cum, p, log2cap, ablate, st);
   }
   if (w_bf16)
     return launch_round<FPL, CH, float, __hip_bfloat16>(w, num, dn, cat, dc, y, B, R, S, dacc, dim,
-                                                        stats, cum, p, log2cap, st);
-  return launch_round<FPL, CH, float, float>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, stats,
-                                             cum, p, log2cap, st);
+                                                        ws, cum, p, log2cap, ablate, st);
+  return launch_round<FPL, CH, float, float>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, ws,
+                                             cum, p, log2cap, ablate, st);
 }
 
 template <int FPL, typename NumT, typename WT>
@@ -356,18 +422,18 @@ using namespace omldm;
 
 OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                                  const int* cat, int dc, const float* y, int B, int R, int S,
-                                 float* dacc, int dim, float* stats, float* cum, int rule,
+                                 float* dacc, int dim, float* ws, float* cum, int rule,
                                  int variant,
                                  float C, float eps, float lr, float lam, float inv_p, int bias,
-                                 int log2cap, void* stream) {
+                                 int log2cap, int ablate, void* stream) {
   if (S <= 0) return 0;
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
   const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias};
   const int F = dn + dc + (bias ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
-  if (F <= 64) return dispatch_round<1, 16>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, stats, cum, p, log2cap, st);
-  if (F <= 128) return dispatch_round<2, 8>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, stats, cum, p, log2cap, st);
-  if (F <= 256) return dispatch_round<4, 4>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, stats, cum, p, log2cap, st);
+  if (F <= 64) return dispatch_round<1, 16>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, cum, p, log2cap, ablate, st);
+  if (F <= 128) return dispatch_round<2, 8>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, cum, p, log2cap, ablate, st);
+  if (F <= 256) return dispatch_round<4, 4>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, cum, p, log2cap, ablate, st);
   return -2;
 }
 

@@ -52,6 +52,7 @@ class LinearLearner(Learner):
             bias=bool(h.get("bias", True)),
         )
         self.log2cap = hp_int(h, "tableLog2", 13)
+        self.ablate = hp_int(h, "_ablate", 0)  # timing diagnostics only
         want16 = str(h.get("modelDtype", "fp32")).lower() in ("bf16", "bfloat16")
         if want16 and self.w16 is None:
             self.w16 = self.w.to(torch.bfloat16)
@@ -72,7 +73,7 @@ class LinearLearner(Learner):
         R = max(1, -(-B // S)) if B else 1
         if B:
             L.linear_round(self._wread(), batch, R, S, self.dacc, None, self.rule, ctx.inv_p,
-                           self.log2cap, cum=self.cum)
+                           self.log2cap, cum=self.cum, ablate=self.ablate)
         if not ctx.fused_delta:
             self.apply_delta()
 

@@ -32,13 +32,27 @@ class LinearRule:
     bias: bool = True
 
 
+WS_STAT = 8  # per-spoke workspace stat columns (see linear_spoke.hip kWsStat)
+_WS: dict = {}
+
+
+def _workspace(device, n: int) -> torch.Tensor:
+    """Per-device scratch for the per-spoke rows (stream-ordered reuse is safe: every
+    round kernel fully rewrites the rows its finish kernel reads)."""
+    t = _WS.get(device)
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=device)
+        _WS[device] = t
+    return t
+
+
 def _cpu_threads() -> int:
     return int(os.environ.get("OMLDM_CPU_THREADS", min(8, os.cpu_count() or 1)))
 
 
 def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torch.Tensor,
                  stats: torch.Tensor | None, rule: LinearRule, inv_p: float, log2cap: int = 13,
-                 cum: torch.Tensor | None = None) -> None:
+                 cum: torch.Tensor | None = None, ablate: int = 0) -> None:
     """One protocol round of S virtual spokes, R examples each (spoke s gets rows
     [s·R, (s+1)·R)). Every spoke with ≥1 row accumulates σ·Δ·inv_p into ``dacc[:dim]``,
     σ·inv_p into ``dacc[dim]`` and inv_p into ``dacc[dim+1]`` (so ``dacc`` is [dim+2]);
@@ -58,12 +72,17 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         assert stats is None or stats.is_cuda
         assert num.dtype in (torch.float32, torch.bfloat16)
         assert num.shape[1] + cat.shape[1] + int(rule.bias) <= 256, "≤ 256 features per example"
+        assert 4 <= log2cap <= 14
+        wsw = WS_STAT + num.shape[1] + 1
+        ws = _workspace(w.device, S * wsw)
         rc = native.hip().omldm_linear_round(
             ptr(w), int(w.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
             num.shape[1], ptr(cat), cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim,
-            ptr(stats), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, rule.lam,
-            inv_p, int(rule.bias), log2cap, native.stream_of(w))
+            ptr(ws), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, rule.lam,
+            inv_p, int(rule.bias), log2cap, int(ablate), native.stream_of(w))
         check(rc, "omldm_linear_round")
+        if stats is not None:
+            stats.copy_(ws[: S * wsw].view(S, wsw)[:, :STAT_W])
     else:
         num32 = num.float().contiguous()
         st = stats if stats is not None else torch.zeros((S, STAT_W), dtype=torch.float32)
