@@ -256,6 +256,7 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     wrow[5] = ovf_total;
     wrow[6] = scale;
     wrow[7] = p.inv_p;
+    if (!p.bias) wrow[kWsStat + dn] = 0.f;  // intercept column unused
   }
 }
 
