@@ -45,6 +45,9 @@ HIP_SIGS = [
     ("omldm_linear_predict", i32, [vp, i32, i64, i32, vp, i32, i32, vp, i32, i32, i32, i32, vp,
                                    vp, vp]),
     ("omldm_linear_apply", i32, [vp, vp, vp, i32, vp]),
+    ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
+    ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
+    ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
 ]
 
 HOST_SIGS = [
