@@ -48,6 +48,7 @@ HIP_SIGS = [
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
     ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
+    ("omldm_pull_copy", i32, [vp, vp, i64, i32, vp]),
 ]
 
 HOST_SIGS = [
