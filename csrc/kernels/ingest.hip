@@ -10,18 +10,20 @@
 
 namespace omldm {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 // Plain 16-byte-per-lane streaming copy (host-mapped src → device dst), 4 loads in
 // flight per lane before the stores.
-__global__ __launch_bounds__(256) void pull_copy_kernel(const uint4* __restrict__ src,
-                                                        uint4* __restrict__ dst, long long n16) {
+__global__ __launch_bounds__(256) void pull_copy_kernel(const u32x4* __restrict__ src,
+                                                        u32x4* __restrict__ dst, long long n16) {
   const long long tid = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long stride = (long long)gridDim.x * 256;
   long long i = tid;
   for (; i + 3 * stride < n16; i += 4 * stride) {
-    const uint4 a = __builtin_nontemporal_load(src + i);
-    const uint4 b = __builtin_nontemporal_load(src + i + stride);
-    const uint4 c = __builtin_nontemporal_load(src + i + 2 * stride);
-    const uint4 d = __builtin_nontemporal_load(src + i + 3 * stride);
+    const u32x4 a = __builtin_nontemporal_load(src + i);
+    const u32x4 b = __builtin_nontemporal_load(src + i + stride);
+    const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+    const u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
     dst[i] = a;
     dst[i + stride] = b;
     dst[i + 2 * stride] = c;
@@ -53,8 +55,8 @@ OMLDM_API int omldm_pull_copy(const void* host_src, void* dst, long long nbytes,
   if (((uintptr_t)src & 15) || ((uintptr_t)dst & 15)) return -1;
   if (n16) {
     if (blocks <= 0) blocks = 1024;
-    hipLaunchKernelGGL(pull_copy_kernel, dim3(blocks), dim3(256), 0, st, (const uint4*)src,
-                       (uint4*)dst, n16);
+    hipLaunchKernelGGL(pull_copy_kernel, dim3(blocks), dim3(256), 0, st, (const u32x4*)src,
+                       (u32x4*)dst, n16);
   }
   const long long tail = nbytes - n16 * 16;
   if (tail)
