@@ -63,10 +63,10 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--spokes", type=int, default=2048, help="virtual spokes per GPU")
-    ap.add_argument("--rows", type=int, default=64, help="examples per spoke per round")
+    ap.add_argument("--spokes", type=int, default=4096, help="virtual spokes per GPU")
+    ap.add_argument("--rows", type=int, default=32, help="examples per spoke per round")
     ap.add_argument("--dim-log2", type=int, default=20)
-    ap.add_argument("--table-log2", type=int, default=12, help="LDS delta table (entries, log2)")
+    ap.add_argument("--table-log2", type=int, default=11, help="LDS delta table (entries, log2)")
     ap.add_argument("--model-dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--num-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")

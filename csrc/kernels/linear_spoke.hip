@@ -39,15 +39,21 @@ struct LinParams {
   float lam;
   float inv_p;
   int bias;
+  float cclip;    // τ clip: C for PA-I, +inf otherwise
+  float kadd;     // τ denominator offset: 1/(2C) for PA-II, 0 otherwise
+  float shrink;   // per-step multiplicative L2 shrink of w (1 when λ = 0)
+  float rshrink;  // 1 / shrink
 };
 
-
-__device__ __forceinline__ float pa_tau(float loss, float n2, const LinParams& p) {
-  if (loss <= 0.f || n2 <= 0.f) return 0.f;
-  if (p.variant == kPA) return loss / n2;
-  if (p.variant == kPA1) return fminf(p.C, loss / n2);
-  return loss / (n2 + 0.5f / p.C);
-}
+// Bucketed LDS delta table geometry (host-computed, see omldm_linear_round):
+//   keys/vals [cap + kOvf]; bucket(key) = key >> kshift owns slots
+//   [bucket·BS, (bucket+1)·BS), BS = cap >> log2nb; the kOvf tail is a shared overflow area.
+struct TableGeom {
+  int log2cap;
+  int log2nb;
+  int kshift;
+};
+constexpr int kOvf = 64;
 
 // Loads feature f of example t for this lane. Numeric features occupy slots [0, dn);
 // categorical features carry their hashed slot in the low 31 bits and the hash sign in
@@ -93,17 +99,79 @@ __device__ __forceinline__ int dense_col(int j, int dn, int dc, int bias) {
   return -1;
 }
 
-// ablate (timing diagnostics only, never set in production): bit0 skip the categorical
-// flush atomics, bit1 skip the sequential phase, bit2 skip the LDS slot resolution.
-template <int FPL, int CH, typename NumT, typename WT>
+__device__ __forceinline__ uint32_t hmix(uint32_t k) { return k * 0x9E3779B1u; }
+
+// Slow path of the bucketed table: probe the whole bucket, then the overflow area.
+__device__ __noinline__ int table_find_or_insert(int* keys, int key, TableGeom g) {
+  const int bs_log2 = g.log2cap - g.log2nb;
+  const uint32_t bmask = (1u << bs_log2) - 1u;
+  const int base = (key >> g.kshift) << bs_log2;
+  const uint32_t h = hmix((uint32_t)key);
+  for (uint32_t q = 0; q <= bmask; ++q) {
+    const int i = base + (int)((h + q) & bmask);
+    const int k = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (k == key) return i;
+    if (k == kEmptyKey) {
+      const int prev = atomicCAS(&keys[i], kEmptyKey, key);
+      if (prev == kEmptyKey || prev == key) return i;
+    }
+  }
+  const int ob = 1 << g.log2cap;
+  for (int q = 0; q < kOvf; ++q) {
+    const int i = ob + (int)((h + q) & (kOvf - 1));
+    const int k = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (k == key) return i;
+    if (k == kEmptyKey) {
+      const int prev = atomicCAS(&keys[i], kEmptyKey, key);
+      if (prev == kEmptyKey || prev == key) return i;
+    }
+  }
+  return -1;  // table full: the update is dropped and counted as overflow
+}
+
+template <int RULE>
+struct Step {
+  // returns (loss, c) for margin m, label y, ‖x‖² n2; updates counters
+  __device__ __forceinline__ static void run(float m, float y, float n2, const LinParams& p,
+                                             float& loss_sum, float& mist, float& sqe, float& c) {
+    if constexpr (RULE == kHinge) {
+      const float ym = y * m;
+      const float loss = fmaxf(0.f, 1.f - ym);
+      loss_sum += loss;
+      mist += ym <= 0.f ? 1.f : 0.f;
+      const float tau = n2 > 0.f ? fminf(p.cclip, loss * __builtin_amdgcn_rcpf(n2 + p.kadd)) : 0.f;
+      c = tau * y;
+    } else if constexpr (RULE == kEpsInsensitive) {
+      const float err = y - m;
+      const float loss = fmaxf(0.f, fabsf(err) - p.eps);
+      loss_sum += loss;
+      sqe = fmaf(err, err, sqe);
+      const float tau = n2 > 0.f ? fminf(p.cclip, loss * __builtin_amdgcn_rcpf(n2 + p.kadd)) : 0.f;
+      c = err >= 0.f ? tau : -tau;
+    } else {
+      const float z = y * m;
+      const float ez = __expf(-fabsf(z));
+      loss_sum += fmaxf(-z, 0.f) + __logf(1.f + ez);
+      mist += z <= 0.f ? 1.f : 0.f;
+      // σ(−z) = 1/(1+e^z), computed from e^{−|z|} without overflow
+      const float sg = z >= 0.f ? ez * __builtin_amdgcn_rcpf(1.f + ez) : __builtin_amdgcn_rcpf(1.f + ez);
+      c = p.lr * y * sg;
+    }
+  }
+};
+
+// ablate (timing diagnostics only): bit0 skip the table flush, bit1 skip the sequential
+// phase.
+template <int FPL, int CH, int RULE, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void linear_round_kernel(
     const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const int* __restrict__ cat,
-    int dc, const float* __restrict__ yv, int B, int R, float* __restrict__ dacc, int dim,
-    float* __restrict__ ws, LinParams p, int log2cap, int ablate) {
+    int dc, const float* __restrict__ yv, int B, int R, int dim, float* __restrict__ ws,
+    int2* __restrict__ tables, LinParams p, TableGeom g, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int cap = 1 << log2cap;
+  const int cap = 1 << g.log2cap;
+  const int tsz = cap + kOvf;
   int* keys = reinterpret_cast<int*>(smem);
-  float* vals = reinterpret_cast<float*>(smem + (size_t)cap * sizeof(int));
+  float* vals = reinterpret_cast<float*>(smem + (size_t)tsz * sizeof(int));
   const int lane = threadIdx.x;
   const int s = blockIdx.x;
   const int wsw = kWsStat + dn + 1;
@@ -115,12 +183,14 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     for (int k = lane; k < wsw; k += kWave) wrow[k] = k == 4 ? 1.f : 0.f;
     return;
   }
-  for (int i = lane; i < cap; i += kWave) {
+  for (int i = lane; i < tsz; i += kWave) {
     keys[i] = kEmptyKey;
     vals[i] = 0.f;
   }
   __syncthreads();
 
+  const int bs_log2 = g.log2cap - g.log2nb;
+  const uint32_t bmask = (1u << bs_log2) - 1u;
   int dcol[FPL];
   float dreg[FPL];
 #pragma unroll
@@ -128,51 +198,85 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     dcol[f] = dense_col(lane + kWave * f, dn, dc, p.bias);
     dreg[f] = 0.f;
   }
-  float sigma = 1.f, loss_sum = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f, ovf = 0.f;
+  float sigma = 1.f, rsig = 1.f, loss_sum = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f, ovf = 0.f;
+
+  // Software pipeline: the features of chunk c+1 are in flight while chunk c computes.
+  int nidx[CH][FPL];
+  float nxv[CH][FPL];
+  float nyy[CH];
+  auto load_chunk = [&](int tc) {
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const int t = tc + e;
+      const bool ok = t < t1;
+      nyy[e] = ok ? yv[t] : __builtin_nanf("");
+#pragma unroll
+      for (int f = 0; f < FPL; ++f) {
+        int idx = -1;
+        float v = 0.f;
+        if (ok) load_feature(num, dn, cat, dc, t, lane + kWave * f, dim, p.bias, idx, v);
+        nidx[e][f] = idx;
+        nxv[e][f] = v;
+      }
+    }
+  };
+  load_chunk(t0);
 
   for (int tc = t0; tc < t1; tc += CH) {
     int slot[CH][FPL];
     float xv[CH][FPL];
     float wv[CH][FPL];
     float yy[CH];
-    // Phase 1a: stream the chunk's features in (all loads independent).
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
-      const int t = tc + e;
-      const bool ok = t < t1;
-      yy[e] = ok ? yv[t] : __builtin_nanf("");
+      yy[e] = nyy[e];
 #pragma unroll
       for (int f = 0; f < FPL; ++f) {
-        int idx = -1;
-        float v = 0.f;
-        if (ok) load_feature(num, dn, cat, dc, t, lane + kWave * f, dim, p.bias, idx, v);
-        slot[e][f] = idx;
-        xv[e][f] = v;
+        slot[e][f] = nidx[e][f];
+        xv[e][f] = nxv[e][f];
       }
     }
-    // Phase 1b: gather w0 for the whole chunk (read-only during the round).
+    // Gather w0 for the whole chunk (read-only during the round).
 #pragma unroll
     for (int e = 0; e < CH; ++e)
 #pragma unroll
       for (int f = 0; f < FPL; ++f) wv[e][f] = slot[e][f] >= 0 ? to_f(w[slot[e][f]]) : 0.f;
-    // Phase 1c: resolve LDS slots of the private delta for hashed features.
-    if (!(ablate & 4)) {
+    if (tc + CH < t1) load_chunk(tc + CH);
+    // Resolve the LDS slots of hashed features: one batched first probe for the
+    // whole chunk (independent ds_reads, then independent CAS), slow path rarely.
+    int h0[CH][FPL];
+    int k0[CH][FPL];
 #pragma unroll
-      for (int e = 0; e < CH; ++e)
+    for (int e = 0; e < CH; ++e)
 #pragma unroll
-        for (int f = 0; f < FPL; ++f)
-          if (dcol[f] < 0 && slot[e][f] >= 0) {
-            const int sl = lds_find_or_insert(keys, slot[e][f], log2cap);
-            if (sl < 0) ovf += 1.f;
-            slot[e][f] = sl;
+      for (int f = 0; f < FPL; ++f) {
+        const int key = slot[e][f];
+        h0[e][f] = ((key >> g.kshift) << bs_log2) + (int)(hmix((uint32_t)key) & bmask);
+        k0[e][f] = (dcol[f] < 0 && key >= 0)
+                       ? __hip_atomic_load(&keys[h0[e][f]], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP)
+                       : 0;
+      }
+#pragma unroll
+    for (int e = 0; e < CH; ++e)
+#pragma unroll
+      for (int f = 0; f < FPL; ++f) {
+        const int key = slot[e][f];
+        if (dcol[f] < 0 && key >= 0) {
+          int sl = -2;
+          if (k0[e][f] == key) {
+            sl = h0[e][f];
+          } else if (k0[e][f] == kEmptyKey) {
+            const int prev = atomicCAS(&keys[h0[e][f]], kEmptyKey, key);
+            if (prev == kEmptyKey || prev == key) sl = h0[e][f];
           }
-    } else {
-#pragma unroll
-      for (int e = 0; e < CH; ++e)
-#pragma unroll
-        for (int f = 0; f < FPL; ++f)
-          if (slot[e][f] >= 0) slot[e][f] = (int)hslot((uint32_t)slot[e][f], log2cap);
-    }
+          if (sl == -2) {
+            sl = table_find_or_insert(keys, key, g);
+            if (sl < 0) ovf += 1.f;
+          }
+          slot[e][f] = sl;
+        }
+      }
     if (ablate & 2) {
 #pragma unroll
       for (int e = 0; e < CH; ++e)
@@ -180,7 +284,7 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
         for (int f = 0; f < FPL; ++f) loss_sum += wv[e][f] + xv[e][f] + (float)slot[e][f];
       continue;
     }
-    // Phase 2: exact sequential online updates.
+    // Exact sequential online updates.
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
       const float y = yy[e];
@@ -193,35 +297,13 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
         pn = fmaf(xv[e][f], xv[e][f], pn);
       }
       wave_sum2(pm, pn);
-      const float m = sigma * pm;
-      float c = 0.f;      // coefficient of x in w-space
-      float shrink = 1.f;  // multiplicative L2 shrink of w this step
-      if (p.rule == kHinge) {
-        const float ym = y * m;
-        const float loss = fmaxf(0.f, 1.f - ym);
-        loss_sum += loss;
-        mist += ym <= 0.f ? 1.f : 0.f;
-        c = pa_tau(loss, pn, p) * y;
-        shrink = 1.f - p.lam;
-      } else if (p.rule == kEpsInsensitive) {
-        const float err = y - m;
-        const float loss = fmaxf(0.f, fabsf(err) - p.eps);
-        loss_sum += loss;
-        sqe += err * err;
-        c = pa_tau(loss, pn, p) * (err >= 0.f ? 1.f : -1.f);
-        shrink = 1.f - p.lam;
-      } else {
-        const float z = y * m;
-        const float loss = z > 0.f ? log1pf(__expf(-z)) : (-z + log1pf(__expf(z)));
-        loss_sum += loss;
-        mist += z <= 0.f ? 1.f : 0.f;
-        c = p.lr * y / (1.f + __expf(z));
-        shrink = 1.f - p.lr * p.lam;
-      }
+      float c;
+      Step<RULE>::run(sigma * pm, y, pn, p, loss_sum, mist, sqe, c);
       nex += 1.f;
-      sigma *= shrink;
-      if (c != 0.f) {
-        const float cv = c / sigma;
+      sigma *= p.shrink;
+      rsig *= p.rshrink;
+      if (c != 0.f) {  // wave-uniform
+        const float cv = c * rsig;
 #pragma unroll
         for (int f = 0; f < FPL; ++f) {
           if (dcol[f] >= 0) dreg[f] = fmaf(cv, xv[e][f], dreg[f]);
@@ -231,16 +313,14 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     }
   }
   __syncthreads();
-  // Round end: ship σ·Δ/P. Hashed features: sparse scatter with no-return f32 atomics
-  // (distinct spokes rarely share a hashed slot); dense features: workspace row.
+  // Round end: the whole table (σ·Δ/P per slot) goes out with plain coalesced stores;
+  // linear_bucket_reduce sums it per key range, no global atomics on the hot path.
   const float scale = sigma * p.inv_p;
   if (!(ablate & 1)) {
-    for (int i = lane; i < cap; i += kWave) {
+    int2* trow = tables + (size_t)s * tsz;
+    for (int i = lane; i < tsz; i += kWave) {
       const int k = keys[i];
-      if (k >= 0) {
-        const float v = vals[i];
-        if (v != 0.f) atomicAdd(&dacc[k], v * scale);
-      }
+      trow[i] = make_int2(k, __float_as_int(vals[i] * scale));
     }
   }
 #pragma unroll
@@ -257,6 +337,53 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     wrow[6] = scale;
     wrow[7] = p.inv_p;
     if (!p.bias) wrow[kWsStat + dn] = 0.f;  // intercept column unused
+  }
+}
+
+// Bucket b owns keys [b·2^kshift, (b+1)·2^kshift): it streams bucket b of every active
+// spoke's table (BS consecutive int2 per spoke), accumulates into a 16 KiB LDS image
+// with ds_add_f32 and writes its slice of the round accumulator with plain stores.
+__global__ __launch_bounds__(256) void linear_bucket_reduce_kernel(
+    const int2* __restrict__ tables, int S_act, TableGeom g, int dim, float* __restrict__ dacc) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* acc = reinterpret_cast<float*>(smem);
+  const int span = 1 << g.kshift;
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < span; i += 256) acc[i] = 0.f;
+  __syncthreads();
+  const int bs_log2 = g.log2cap - g.log2nb;
+  const int BS = 1 << bs_log2;
+  const int tsz = (1 << g.log2cap) + kOvf;
+  const int lo = b << g.kshift;
+  const long long items = (long long)S_act * BS;
+  for (long long it = threadIdx.x; it < items; it += 256) {
+    const int sp = (int)(it >> bs_log2);
+    const int j = (int)(it & (BS - 1));
+    const int2 e = tables[(size_t)sp * tsz + ((size_t)b << bs_log2) + j];
+    if (e.x >= 0) atomicAdd(&acc[e.x - lo], __int_as_float(e.y));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < span; i += 256) {
+    const int k = lo + i;
+    if (k < dim) dacc[k] = acc[i];
+  }
+}
+
+// Overflow-area entries (rare) are added with global atomics after the bucket reduce.
+__global__ __launch_bounds__(256) void linear_overflow_kernel(const int2* __restrict__ tables,
+                                                              int S_act, int log2cap,
+                                                              float* __restrict__ dacc) {
+  const int tsz = (1 << log2cap) + kOvf;
+  const long long n = (long long)S_act * kOvf;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const int sp = (int)(i / kOvf);
+    const int j = (int)(i % kOvf);
+    const int2 e = tables[(size_t)sp * tsz + (1 << log2cap) + j];
+    if (e.x >= 0) {
+      const float v = __int_as_float(e.y);
+      if (v != 0.f) atomicAdd(&dacc[e.x], v);
+    }
   }
 }
 
@@ -353,38 +480,63 @@ __global__ __launch_bounds__(256) void linear_apply_kernel(float* __restrict__ w
   }
 }
 
-template <int FPL, int CH, typename NumT, typename WT>
+template <int FPL, int CH, int RULE, typename NumT, typename WT>
 static int launch_round(const void* w, const void* num, int dn, const int* cat, int dc,
                         const float* y, int B, int R, int S, float* dacc, int dim, float* ws,
-                        float* cum, const LinParams& p, int log2cap, int ablate, hipStream_t st) {
-  auto fn = linear_round_kernel<FPL, CH, NumT, WT>;
-  const size_t lds = (size_t(1) << log2cap) * 8;
+                        int2* tables, float* cum, const LinParams& p, TableGeom g, int ablate,
+                        hipStream_t st) {
+  auto fn = linear_round_kernel<FPL, CH, RULE, NumT, WT>;
+  const size_t lds = ((size_t(1) << g.log2cap) + kOvf) * 8;
   int e = check_dyn_lds((const void*)fn, lds);
   if (e) return e;
   hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)w, (const NumT*)num, dn, cat, dc,
-                     y, B, R, dacc, dim, ws, p, log2cap, ablate);
+                     y, B, R, dim, ws, tables, p, g, ablate);
+  const long long sact_ll = R > 0 ? ((long long)B + R - 1) / R : 0;
+  const int S_act = sact_ll < S ? (int)sact_ll : S;
+  if (!(ablate & 1) && S_act > 0) {
+    const int nb = (dim + (1 << g.kshift) - 1) >> g.kshift;
+    hipLaunchKernelGGL(linear_bucket_reduce_kernel, dim3(nb), dim3(256),
+                       (size_t(1) << g.kshift) * 4, st, tables, S_act, g, dim, dacc);
+    int ob = (int)(((long long)S_act * kOvf + 255) / 256);
+    if (ob > 1024) ob = 1024;
+    hipLaunchKernelGGL(linear_overflow_kernel, dim3(ob), dim3(256), 0, st, tables, S_act,
+                       g.log2cap, dacc);
+  }
   hipLaunchKernelGGL(linear_round_finish_kernel, dim3(kWsStat + dn + 1), dim3(256), 0, st, ws, S,
                      dn, dim, dacc, cum);
   return (int)hipGetLastError();
 }
 
-template <int FPL, int CH>
+template <int FPL, int CH, int RULE>
 static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                           const int* cat, int dc, const float* y, int B, int R, int S, float* dacc,
-                          int dim, float* ws, float* cum, const LinParams& p, int log2cap,
-                          int ablate, hipStream_t st) {
+                          int dim, float* ws, int2* tables, float* cum, const LinParams& p,
+                          TableGeom g, int ablate, hipStream_t st) {
+#define OMLDM_LR(NT, WTT)                                                                      \
+  return launch_round<FPL, CH, RULE, NT, WTT>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, ws, \
+                                              tables, cum, p, g, ablate, st)
   if (num_bf16) {
-    if (w_bf16)
-      return launch_round<FPL, CH, __hip_bfloat16, __hip_bfloat16>(w, num, dn, cat, dc, y, B, R, S,
-                                                                   dacc, dim, ws, cum, p, log2cap, ablate, st);
-    return launch_round<FPL, CH, __hip_bfloat16, float>(w, num, dn, cat, dc, y, B, R, S, dacc, dim,
-                                                        ws, cum, p, log2cap, ablate, st);
+    if (w_bf16) OMLDM_LR(__hip_bfloat16, __hip_bfloat16);
+    OMLDM_LR(__hip_bfloat16, float);
   }
-  if (w_bf16)
-    return launch_round<FPL, CH, float, __hip_bfloat16>(w, num, dn, cat, dc, y, B, R, S, dacc, dim,
-                                                        ws, cum, p, log2cap, ablate, st);
-  return launch_round<FPL, CH, float, float>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, ws,
-                                             cum, p, log2cap, ablate, st);
+  if (w_bf16) OMLDM_LR(float, __hip_bfloat16);
+  OMLDM_LR(float, float);
+#undef OMLDM_LR
+}
+
+template <int FPL, int CH>
+static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, int num_bf16,
+                         int dn, const int* cat, int dc, const float* y, int B, int R, int S,
+                         float* dacc, int dim, float* ws, int2* tables, float* cum,
+                         const LinParams& p, TableGeom g, int ablate, hipStream_t st) {
+  if (rule == kHinge)
+    return dispatch_round<FPL, CH, kHinge>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
+                                           dim, ws, tables, cum, p, g, ablate, st);
+  if (rule == kEpsInsensitive)
+    return dispatch_round<FPL, CH, kEpsInsensitive>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R,
+                                                    S, dacc, dim, ws, tables, cum, p, g, ablate, st);
+  return dispatch_round<FPL, CH, kLogistic>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
+                                            dacc, dim, ws, tables, cum, p, g, ablate, st);
 }
 
 template <int FPL, typename NumT, typename WT>
@@ -421,20 +573,46 @@ static int dispatch_predict(const void* w, int w_bf16, long long wstride, int M,
 
 using namespace omldm;
 
+static int ceil_log2(long long x) {
+  int k = 0;
+  while ((1LL << k) < x) ++k;
+  return k;
+}
+
+// Table geometry for a hash dimension: bucket span ≤ 4096 keys (16 KiB LDS in the
+// reducer), ≥ 4 slots per bucket. Returns false when log2cap is too small.
+OMLDM_API int omldm_linear_table_geom(int dim, int log2cap, int* out3) {
+  const int ld = ceil_log2(dim);
+  const int kshift = ld < 12 ? ld : 12;
+  const int log2nb = ld - kshift;
+  if (log2cap - log2nb < 2) return -1;
+  out3[0] = log2cap;
+  out3[1] = log2nb;
+  out3[2] = kshift;
+  return 0;
+}
+
+// tables: device scratch of S * ((1 << log2cap) + 64) int2.
 OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                                  const int* cat, int dc, const float* y, int B, int R, int S,
-                                 float* dacc, int dim, float* ws, float* cum, int rule,
-                                 int variant,
-                                 float C, float eps, float lr, float lam, float inv_p, int bias,
-                                 int log2cap, int ablate, void* stream) {
+                                 float* dacc, int dim, float* ws, void* tables, float* cum,
+                                 int rule, int variant, float C, float eps, float lr, float lam,
+                                 float inv_p, int bias, int log2cap, int ablate, void* stream) {
   if (S <= 0) return 0;
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
-  const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias};
+  int geo[3];
+  if (omldm_linear_table_geom(dim, log2cap, geo)) return -3;
+  const TableGeom g{geo[0], geo[1], geo[2]};
+  const float shrink = rule == kLogistic ? 1.f - lr * lam : 1.f - lam;
+  const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias,
+                    variant == kPA1 ? C : INFINITY, variant == kPA2 ? 0.5f / C : 0.f, shrink,
+                    1.f / shrink};
   const int F = dn + dc + (bias ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
-  if (F <= 64) return dispatch_round<1, 16>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, cum, p, log2cap, ablate, st);
-  if (F <= 128) return dispatch_round<2, 8>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, cum, p, log2cap, ablate, st);
-  if (F <= 256) return dispatch_round<4, 4>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, cum, p, log2cap, ablate, st);
+  int2* tb = (int2*)tables;
+  if (F <= 64) return dispatch_rule<1, 16>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
+  if (F <= 128) return dispatch_rule<2, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
+  if (F <= 256) return dispatch_rule<4, 4>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
   return -2;
 }
 

@@ -36,14 +36,20 @@ WS_STAT = 8  # per-spoke workspace stat columns (see linear_spoke.hip kWsStat)
 _WS: dict = {}
 
 
-def _workspace(device, n: int) -> torch.Tensor:
-    """Per-device scratch for the per-spoke rows (stream-ordered reuse is safe: every
-    round kernel fully rewrites the rows its finish kernel reads)."""
-    t = _WS.get(device)
+def _workspace(device, n: int, key: str = "ws") -> torch.Tensor:
+    """Per-device scratch (per-spoke rows, spoke delta tables). Stream-ordered reuse is
+    safe: every round kernel fully rewrites what its reduce/finish kernels read."""
+    t = _WS.get((device, key))
     if t is None or t.numel() < n:
         t = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=device)
-        _WS[device] = t
+        _WS[(device, key)] = t
     return t
+
+
+def min_log2cap(dim: int) -> int:
+    """Smallest LDS table (log2 entries) with ≥ 4 slots per key bucket for this dim."""
+    ld = max(0, (dim - 1).bit_length())
+    return max(4, ld - min(ld, 12) + 2)
 
 
 def _cpu_threads() -> int:
@@ -72,14 +78,16 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         assert stats is None or stats.is_cuda
         assert num.dtype in (torch.float32, torch.bfloat16)
         assert num.shape[1] + cat.shape[1] + int(rule.bias) <= 256, "≤ 256 features per example"
+        log2cap = max(log2cap, min_log2cap(dim))
         assert 4 <= log2cap <= 14
         wsw = WS_STAT + num.shape[1] + 1
         ws = _workspace(w.device, S * wsw)
+        tables = _workspace(w.device, S * ((1 << log2cap) + 64) * 2, key="tables")
         rc = native.hip().omldm_linear_round(
             ptr(w), int(w.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
             num.shape[1], ptr(cat), cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim,
-            ptr(ws), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, rule.lam,
-            inv_p, int(rule.bias), log2cap, int(ablate), native.stream_of(w))
+            ptr(ws), ptr(tables), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr,
+            rule.lam, inv_p, int(rule.bias), log2cap, int(ablate), native.stream_of(w))
         check(rc, "omldm_linear_round")
         if stats is not None:
             stats.copy_(ws[: S * wsw].view(S, wsw)[:, :STAT_W])

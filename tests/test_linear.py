@@ -213,3 +213,36 @@ def test_hip_bf16_model_round(cuda):
     d_gpu = torch.zeros(sp.dim + 2, device=cuda)
     L.linear_round(w.to(cuda), b.to(cuda), 64, 64, d_gpu, None, rule, 1.0, log2cap=12)
     np.testing.assert_allclose(d_gpu.cpu().numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log2cap,R", [(11, 32), (12, 64)])
+def test_hip_round_bucketed_table_large_dim(cuda, log2cap, R):
+    """2^20-dim hashing: 256 key buckets, 8-16 slots each, overflow area; exact vs CPU."""
+    sp = FeatureSpace(13, 0, 26, 1 << 20)
+    S = 96
+    b = synth_batch(sp, S * R, seed=7)
+    w = (torch.randn(sp.dim) * 0.01)
+    rule = L.LinearRule()
+    d_cpu = torch.zeros(sp.dim + 2)
+    s_cpu = torch.zeros(S, 6)
+    L.linear_round(w, b, R, S, d_cpu, s_cpu, rule, 1.0)
+    d_gpu = torch.zeros(sp.dim + 2, device=cuda)
+    s_gpu = torch.zeros(S, 6, device=cuda)
+    L.linear_round(w.to(cuda), b.to(cuda), R, S, d_gpu, s_gpu, rule, 1.0, log2cap=log2cap)
+    assert float(s_gpu[:, 5].sum()) == 0.0
+    np.testing.assert_allclose(d_gpu.cpu().numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+def test_hip_round_table_overflow_is_counted(cuda):
+    sp = FeatureSpace(13, 0, 26, 1 << 20)
+    S, R = 8, 128  # ~3000 distinct keys into 1024 + 64 slots
+    b = synth_batch(sp, S * R, seed=8)
+    d = torch.zeros(sp.dim + 2, device=cuda)
+    st = torch.zeros(S, 6, device=cuda)
+    L.linear_round(torch.zeros(sp.dim, device=cuda), b.to(cuda), R, S, d, st, L.LinearRule(), 1.0,
+                   log2cap=10)
+    torch.cuda.synchronize()
+    assert float(st[:, 5].sum()) > 0
+    assert torch.isfinite(d).all()
