@@ -355,12 +355,30 @@ __global__ __launch_bounds__(256) void linear_bucket_reduce_kernel(
   const int BS = 1 << bs_log2;
   const int tsz = (1 << g.log2cap) + kOvf;
   const int lo = b << g.kshift;
-  const long long items = (long long)S_act * BS;
-  for (long long it = threadIdx.x; it < items; it += 256) {
-    const int sp = (int)(it >> bs_log2);
-    const int j = (int)(it & (BS - 1));
-    const int2 e = tables[(size_t)sp * tsz + ((size_t)b << bs_log2) + j];
-    if (e.x >= 0) atomicAdd(&acc[e.x - lo], __int_as_float(e.y));
+  // 16-byte loads (two slots), four in flight per thread.
+  const int pr_log2 = bs_log2 - 1;  // BS ≥ 4 → ≥ 2 slot pairs per bucket
+  const long long items = (long long)S_act << pr_log2;
+  const int4* t4 = reinterpret_cast<const int4*>(tables);
+  const size_t row4 = (size_t)tsz >> 1;
+  const size_t boff4 = ((size_t)b << bs_log2) >> 1;
+  auto addr = [&](long long ii) {
+    return (size_t)(ii >> pr_log2) * row4 + boff4 + (size_t)(ii & ((1 << pr_log2) - 1));
+  };
+  long long it = threadIdx.x;
+  for (; it + 3 * 256 < items; it += 4 * 256) {
+    int4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = t4[addr(it + u * 256)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v[u].x >= 0) atomicAdd(&acc[v[u].x - lo], __int_as_float(v[u].y));
+      if (v[u].z >= 0) atomicAdd(&acc[v[u].z - lo], __int_as_float(v[u].w));
+    }
+  }
+  for (; it < items; it += 256) {
+    const int4 v = t4[addr(it)];
+    if (v.x >= 0) atomicAdd(&acc[v.x - lo], __int_as_float(v.y));
+    if (v.z >= 0) atomicAdd(&acc[v.z - lo], __int_as_float(v.w));
   }
   __syncthreads();
   for (int i = threadIdx.x; i < span; i += 256) {
@@ -406,8 +424,8 @@ __global__ __launch_bounds__(256) void linear_round_finish_kernel(const float* _
   if (threadIdx.x == 0) {
     const float t = (part[0] + part[1]) + (part[2] + part[3]);
     if (c < kWsStat) {
-      if (c == 6) dacc[dim] += t;
-      else if (c == 7) dacc[dim + 1] += t;
+      if (c == 6) dacc[dim] = t;       // the round's counters (apply does not clear them)
+      else if (c == 7) dacc[dim + 1] = t;
       else if (c != 4 && cum) cum[c] += t;
     } else {
       const int j = c - kWsStat;
@@ -444,7 +462,7 @@ __global__ __launch_bounds__(256) void linear_predict_kernel(
 
 // Model average over the round's active workers:
 //   w = (a·w + D) / n,  a = D[dim] = Σσ/P, n = D[dim+1] = Σ1/P  (n == 0: no change);
-// D[0:dim] = 0 (D[dim:dim+2] cleared by a memset node after the kernel);
+// D[0:dim] = 0 (D[dim:dim+2] are overwritten by the next round's finish kernel);
 // optional bf16 shadow of w for the gathers of the next round.
 __global__ __launch_bounds__(256) void linear_apply_kernel(float* __restrict__ w32,
                                                            __hip_bfloat16* __restrict__ w16,
@@ -597,7 +615,8 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
                                  const int* cat, int dc, const float* y, int B, int R, int S,
                                  float* dacc, int dim, float* ws, void* tables, float* cum,
                                  int rule, int variant, float C, float eps, float lr, float lam,
-                                 float inv_p, int bias, int log2cap, int ablate, void* stream) {
+                                 float inv_p, int bias, int log2cap, int chunk, int ablate,
+                                 void* stream) {
   if (S <= 0) return 0;
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
   int geo[3];
@@ -610,6 +629,7 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
   const int F = dn + dc + (bias ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
   int2* tb = (int2*)tables;
+  if (F <= 64 && chunk <= 8) return dispatch_rule<1, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
   if (F <= 64) return dispatch_rule<1, 16>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
   if (F <= 128) return dispatch_rule<2, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
   if (F <= 256) return dispatch_rule<4, 4>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
@@ -636,7 +656,5 @@ OMLDM_API int omldm_linear_apply(float* w32, void* w16, float* dacc, int dim, vo
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(linear_apply_kernel, dim3(blocks), dim3(256), 0, st, w32,
                      (__hip_bfloat16*)w16, dacc, dim);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  return (int)hipMemsetAsync(dacc + dim, 0, 2 * sizeof(float), st);
+  return (int)hipGetLastError();
 }

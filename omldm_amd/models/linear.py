@@ -53,6 +53,7 @@ class LinearLearner(Learner):
         )
         self.log2cap = hp_int(h, "tableLog2", 13)
         self.ablate = hp_int(h, "_ablate", 0)  # timing diagnostics only
+        self.chunk = hp_int(h, "chunk", 8)      # rows staged per software-pipeline step
         want16 = str(h.get("modelDtype", "fp32")).lower() in ("bf16", "bfloat16")
         if want16 and self.w16 is None:
             self.w16 = self.w.to(torch.bfloat16)
@@ -73,7 +74,9 @@ class LinearLearner(Learner):
         R = max(1, -(-B // S)) if B else 1
         if B:
             L.linear_round(self._wread(), batch, R, S, self.dacc, None, self.rule, ctx.inv_p,
-                           self.log2cap, cum=self.cum, ablate=self.ablate)
+                           self.log2cap, cum=self.cum, ablate=self.ablate, chunk=self.chunk)
+        else:
+            self.dacc[self.dim:].zero_()  # no workers this round on this rank
         if not ctx.fused_delta:
             self.apply_delta()
 

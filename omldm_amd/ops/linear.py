@@ -58,7 +58,7 @@ def _cpu_threads() -> int:
 
 def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torch.Tensor,
                  stats: torch.Tensor | None, rule: LinearRule, inv_p: float, log2cap: int = 13,
-                 cum: torch.Tensor | None = None, ablate: int = 0) -> None:
+                 cum: torch.Tensor | None = None, ablate: int = 0, chunk: int = 8) -> None:
     """One protocol round of S virtual spokes, R examples each (spoke s gets rows
     [s·R, (s+1)·R)). Every spoke with ≥1 row accumulates σ·Δ·inv_p into ``dacc[:dim]``,
     σ·inv_p into ``dacc[dim]`` and inv_p into ``dacc[dim+1]`` (so ``dacc`` is [dim+2]);
@@ -87,7 +87,8 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
             ptr(w), int(w.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
             num.shape[1], ptr(cat), cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim,
             ptr(ws), ptr(tables), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr,
-            rule.lam, inv_p, int(rule.bias), log2cap, int(ablate), native.stream_of(w))
+            rule.lam, inv_p, int(rule.bias), log2cap, int(chunk), int(ablate),
+            native.stream_of(w))
         check(rc, "omldm_linear_round")
         if stats is not None:
             stats.copy_(ws[: S * wsw].view(S, wsw)[:, :STAT_W])
