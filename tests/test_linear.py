@@ -190,7 +190,7 @@ def test_hip_apply_and_predict(cuda):
     L.linear_apply(wg, w16, dg)
     torch.cuda.synchronize()
     np.testing.assert_allclose(wg.cpu().numpy(), w.numpy(), rtol=1e-6, atol=1e-6)
-    assert float(dg.abs().sum().item()) == 0.0
+    assert float(dg[: sp.dim].abs().sum().item()) == 0.0  # counters are overwritten per round
     np.testing.assert_allclose(w16.float().cpu().numpy(), w.numpy(), rtol=1e-2, atol=1e-2)
     b = synth_batch(sp, 777, seed=9)
     W = torch.randn(4, sp.dim)
