@@ -75,6 +75,7 @@ def main(argv=None) -> int:
     ap.add_argument("--latency-samples", type=int, default=2000)
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
     ap.add_argument("--ablate", type=int, default=0, help="kernel phase ablation (diagnostics)")
+    ap.add_argument("--chunk", type=int, default=8, help="rows per kernel pipeline step")
     a = ap.parse_args(argv)
 
     comm, device = init_distributed()
@@ -101,7 +102,8 @@ def main(argv=None) -> int:
             d.flat.copy_(p.flat)
 
     learner = SVM({"variant": "PA-I", "C": 1.0, "modelDtype": a.model_dtype,
-                   "tableLog2": a.table_log2, "_ablate": a.ablate}, space, device)
+                   "tableLog2": a.table_log2, "_ablate": a.ablate, "chunk": a.chunk}, space,
+                  device)
     proto = Synchronous(comm, learner, {"virtualSpokes": S,
                                         **({"HubParallelism": a.hubs} if a.hubs else {})})
 
