@@ -36,6 +36,7 @@ from omldm_amd.io.synthetic import synth_batch  # noqa: E402
 from omldm_amd.models.linear import SVM  # noqa: E402
 from omldm_amd.parallel.comm import init_distributed  # noqa: E402
 from omldm_amd.parallel.protocols import Synchronous  # noqa: E402
+from omldm_amd.ops import native  # noqa: E402
 
 METRIC = "training examples/sec (whole node) + p50 predict latency, linear SVM 1/2/4/8 GPU"
 
@@ -76,6 +77,7 @@ def main(argv=None) -> int:
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
     ap.add_argument("--ablate", type=int, default=0, help="kernel phase ablation (diagnostics)")
     ap.add_argument("--chunk", type=int, default=8, help="rows per kernel pipeline step")
+    ap.add_argument("--h2d", default="sdma", choices=["sdma", "pull"], help="H2D engine")
     a = ap.parse_args(argv)
 
     comm, device = init_distributed()
@@ -111,18 +113,30 @@ def main(argv=None) -> int:
     copied = [torch.cuda.Event() for _ in range(2)] if on_gpu else None
     consumed = [torch.cuda.Event() for _ in range(2)] if on_gpu else None
 
+    host_t = {"prefetch": 0.0, "round": 0.0}
+
+    def h2d(dst: torch.Tensor, src: torch.Tensor):
+        if a.h2d == "pull":  # GPU pulls the pinned batch over PCIe (csrc/kernels/ingest.hip)
+            native.check(native.hip().omldm_pull_copy(src.data_ptr(), dst.data_ptr(),
+                                                      src.numel(), 512,
+                                                      copy_stream.cuda_stream), "pull_copy")
+        else:  # SDMA engine (hipMemcpyAsync)
+            dst.copy_(src, non_blocking=True)
+
     def prefetch(k: int):
         if a.ingest == "device":
             return
+        t = time.perf_counter()
         slot = k % 2
         src = pool[k % a.pool]
         if on_gpu:
             with torch.cuda.stream(copy_stream):
                 copy_stream.wait_event(consumed[slot])
-                dev[slot].flat.copy_(src.flat, non_blocking=True)
+                h2d(dev[slot].flat, src.flat)
                 copied[slot].record(copy_stream)
         else:
             dev[slot].flat.copy_(src.flat)
+        host_t["prefetch"] += time.perf_counter() - t
 
     def step(k: int):
         if a.ingest == "device":
@@ -130,11 +144,13 @@ def main(argv=None) -> int:
             return
         slot = k % 2
         prefetch(k + 1)
+        t = time.perf_counter()
         if on_gpu:
             torch.cuda.current_stream().wait_event(copied[slot])
         proto.round(dev[slot].batch)
         if on_gpu:
             consumed[slot].record()
+        host_t["round"] += time.perf_counter() - t
 
     def sync():
         if on_gpu:
@@ -150,6 +166,7 @@ def main(argv=None) -> int:
     for k in range(a.warmup):
         step(k)
     sync()
+    host_t["prefetch"] = host_t["round"] = 0.0
     t0 = time.perf_counter()
     for k in range(a.warmup, a.warmup + a.steps):
         step(k)
@@ -202,6 +219,7 @@ def main(argv=None) -> int:
             "p50_predict_latency_us": None if p50 is None else round(p50, 2),
             "per_gpu_examples_per_s": round(value / world, 1),
             "holdout_accuracy": round(acc, 4), "fitted_examples_rank0": fitted,
+            "host_us_per_step": {k: round(v / a.steps * 1e6, 1) for k, v in host_t.items()},
             "lds_table_overflow": overflow, "device": torch.cuda.get_device_name(device)
             if on_gpu else "cpu",
         }
