@@ -77,7 +77,7 @@ def main(argv=None) -> int:
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
     ap.add_argument("--ablate", type=int, default=0, help="kernel phase ablation (diagnostics)")
     ap.add_argument("--chunk", type=int, default=8, help="rows per kernel pipeline step")
-    ap.add_argument("--h2d", default="sdma", choices=["sdma", "pull"], help="H2D engine")
+    ap.add_argument("--h2d", default="sdma", choices=["sdma", "pull", "raw"], help="H2D engine")
     a = ap.parse_args(argv)
 
     comm, device = init_distributed()
@@ -120,6 +120,10 @@ def main(argv=None) -> int:
             native.check(native.hip().omldm_pull_copy(src.data_ptr(), dst.data_ptr(),
                                                       src.numel(), 512,
                                                       copy_stream.cuda_stream), "pull_copy")
+        elif a.h2d == "raw":  # hipMemcpyAsync issued directly
+            native.check(native.hip().omldm_h2d_async(dst.data_ptr(), src.data_ptr(),
+                                                      src.numel(), copy_stream.cuda_stream),
+                         "h2d_async")
         else:  # SDMA engine (hipMemcpyAsync)
             dst.copy_(src, non_blocking=True)
 

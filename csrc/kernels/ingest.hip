@@ -42,6 +42,16 @@ __global__ void pull_tail_kernel(const unsigned char* __restrict__ src,
 
 using namespace omldm;
 
+// Plain async SDMA copy, issued straight to the runtime (no framework bookkeeping).
+OMLDM_API int omldm_h2d_async(void* dst, const void* src, long long nbytes, void* stream) {
+  return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+}
+
+// Registers an existing host allocation as pinned+mapped (for buffers not allocated pinned).
+OMLDM_API int omldm_host_register(void* p, long long nbytes) {
+  return (int)hipHostRegister(p, (size_t)nbytes, hipHostRegisterMapped);
+}
+
 // Copies nbytes from a pinned (device-mapped) host buffer to device memory by kernel.
 OMLDM_API int omldm_pull_copy(const void* host_src, void* dst, long long nbytes, int blocks,
                               void* stream) {

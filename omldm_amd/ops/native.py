@@ -51,6 +51,8 @@ HIP_SIGS = [
     ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
     ("omldm_pull_copy", i32, [vp, vp, i64, i32, vp]),
+    ("omldm_h2d_async", i32, [vp, vp, i64, vp]),
+    ("omldm_host_register", i32, [vp, i64]),
 ]
 
 HOST_SIGS = [
