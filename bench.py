@@ -78,6 +78,9 @@ def main(argv=None) -> int:
     ap.add_argument("--ablate", type=int, default=0, help="kernel phase ablation (diagnostics)")
     ap.add_argument("--chunk", type=int, default=8, help="rows per kernel pipeline step")
     ap.add_argument("--h2d", default="sdma", choices=["sdma", "pull", "raw"], help="H2D engine")
+    ap.add_argument("--pull-blocks", type=int, default=512)
+    ap.add_argument("--ingest-cus", type=int, default=0,
+                    help=">0: run the ingest stream on a CU-masked slice of this many CUs")
     a = ap.parse_args(argv)
 
     comm, device = init_distributed()
@@ -110,6 +113,10 @@ def main(argv=None) -> int:
                                         **({"HubParallelism": a.hubs} if a.hubs else {})})
 
     copy_stream = torch.cuda.Stream(device) if on_gpu else None
+    if on_gpu and a.ingest_cus > 0:
+        raw = native.hip().omldm_stream_create_cumask(a.ingest_cus)
+        assert raw, "hipExtStreamCreateWithCUMask failed"
+        copy_stream = torch.cuda.ExternalStream(raw, device=device)
     copied = [torch.cuda.Event() for _ in range(2)] if on_gpu else None
     consumed = [torch.cuda.Event() for _ in range(2)] if on_gpu else None
 
@@ -118,7 +125,7 @@ def main(argv=None) -> int:
     def h2d(dst: torch.Tensor, src: torch.Tensor):
         if a.h2d == "pull":  # GPU pulls the pinned batch over PCIe (csrc/kernels/ingest.hip)
             native.check(native.hip().omldm_pull_copy(src.data_ptr(), dst.data_ptr(),
-                                                      src.numel(), 512,
+                                                      src.numel(), a.pull_blocks,
                                                       copy_stream.cuda_stream), "pull_copy")
         elif a.h2d == "raw":  # hipMemcpyAsync issued directly
             native.check(native.hip().omldm_h2d_async(dst.data_ptr(), src.data_ptr(),

@@ -42,6 +42,27 @@ __global__ void pull_tail_kernel(const unsigned char* __restrict__ src,
 
 using namespace omldm;
 
+// A stream whose kernels may only run on `ncu` CUs spread over all XCDs (every
+// (256/ncu)-th CU), so the ingest pull kernel never competes with the training kernels
+// for more than that slice of the chip. Returns the hipStream_t (0 on failure).
+OMLDM_API void* omldm_stream_create_cumask(int ncu) {
+  hipDeviceProp_t prop;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+    return nullptr;
+  const int total = prop.multiProcessorCount;
+  if (ncu <= 0 || ncu >= total) ncu = total;
+  uint32_t mask[16] = {0};
+  const int step = total / ncu;
+  for (int i = 0, c = total - 1; i < ncu && c >= 0; ++i, c -= step) mask[c >> 5] |= 1u << (c & 31);
+  hipStream_t s = nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)((total + 31) / 32), mask) != hipSuccess)
+    return nullptr;
+  return (void*)s;
+}
+
+OMLDM_API int omldm_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }
+
 // Plain async SDMA copy, issued straight to the runtime (no framework bookkeeping).
 OMLDM_API int omldm_h2d_async(void* dst, const void* src, long long nbytes, void* stream) {
   return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyHostToDevice, (hipStream_t)stream);

@@ -52,6 +52,8 @@ HIP_SIGS = [
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
     ("omldm_pull_copy", i32, [vp, vp, i64, i32, vp]),
     ("omldm_h2d_async", i32, [vp, vp, i64, vp]),
+    ("omldm_stream_create_cumask", vp, [i32]),
+    ("omldm_stream_destroy", i32, [vp]),
     ("omldm_host_register", i32, [vp, i64]),
 ]
 
