@@ -46,7 +46,8 @@ class PackedBatch:
 
     def __init__(self, space: FeatureSpace, B: int, device, pin: bool, num_dtype):
         esz = torch.tensor([], dtype=num_dtype).element_size()
-        self.sizes = [B * space.dn * esz, B * space.dc * 4, B * 4]
+        csz = torch.tensor([], dtype=space.cat_dtype).element_size()
+        self.sizes = [B * space.dn * esz, B * space.dc * csz, B * 4]
         offs = [0]
         for s in self.sizes:
             offs.append(offs[-1] + ((s + 255) // 256) * 256)
@@ -55,8 +56,9 @@ class PackedBatch:
         f = self.flat
         self.batch = HashedBatch(
             f[offs[0]:offs[0] + self.sizes[0]].view(num_dtype).view(B, space.dn),
-            f[offs[1]:offs[1] + self.sizes[1]].view(torch.int32).view(B, space.dc),
-            f[offs[2]:offs[2] + self.sizes[2]].view(torch.float32).view(B))
+            f[offs[1]:offs[1] + self.sizes[1]].view(space.cat_dtype).view(B, space.dc),
+            f[offs[2]:offs[2] + self.sizes[2]].view(torch.float32).view(B),
+            cat_span=space.cat_span)
 
 
 def main(argv=None) -> int:
@@ -70,6 +72,8 @@ def main(argv=None) -> int:
     ap.add_argument("--table-log2", type=int, default=11, help="LDS delta table (entries, log2)")
     ap.add_argument("--model-dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--num-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--wire", default="wide", choices=["wide", "compact"],
+                    help="compact: field-aware uint16 categorical slots (half the PCIe bytes)")
     ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")
     ap.add_argument("--ingest", default="pinned", choices=["pinned", "device"],
                     help="pinned: H2D copy of every batch inside the timed loop")
@@ -86,7 +90,7 @@ def main(argv=None) -> int:
     comm, device = init_distributed()
     rank, world = comm.rank, comm.world
     on_gpu = device.type == "cuda"
-    space = FeatureSpace(13, 0, 26, 1 << a.dim_log2)
+    space = FeatureSpace(13, 0, 26, 1 << a.dim_log2, field_aware=a.wire == "compact")
     S, R = a.spokes, a.rows
     B = S * R
     num_dtype = torch.bfloat16 if a.num_dtype == "bf16" else torch.float32

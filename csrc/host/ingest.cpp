@@ -73,6 +73,14 @@ inline int32_t hash_cat(const uint8_t* s, size_t n, int field, int dn, int64_t d
   return (h & 0x80000000u) ? int32_t(uint32_t(slot) | 0x80000000u) : slot;
 }
 
+// Field-aware compact form: field f owns slots [dn + f·cspan, dn + (f+1)·cspan), the wire
+// value is uint16 {sign:1, local:15} (0xFFFF = absent), cspan ≤ 32767.
+inline uint16_t hash_cat16(const uint8_t* s, size_t n, int field, int cspan) {
+  const uint32_t h = murmur3_32(s, n, kSeedBase + uint32_t(field));
+  const uint32_t local = (h & 0x7fffffffu) % uint32_t(cspan);
+  return uint16_t(((h >> 31) << 15) | local);
+}
+
 inline uint64_t splitmix64(uint64_t& x) {
   uint64_t z = (x += 0x9e3779b97f4a7c15ull);
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -180,10 +188,17 @@ inline bool key_is(const char* s, size_t n, const char* k) {
 
 // Parses one record. Returns op code (0/1) or -1.
 int parse_one(const char* b, const char* e, int dnum, int ddisc, int dc, int64_t dim, float* num,
-              int32_t* cat, float* y) {
+              void* catv, int cspan, float* y) {
+  int32_t* cat = static_cast<int32_t*>(catv);
+  uint16_t* cat16 = static_cast<uint16_t*>(catv);
+  if (cspan > 0) {
+    for (int j = 0; j < dc; ++j) cat16[j] = 0xFFFF;
+    cat = nullptr;
+  }
   const int dn = dnum + ddisc;
   for (int j = 0; j < dn; ++j) num[j] = 0.f;
-  for (int j = 0; j < dc; ++j) cat[j] = -1;
+  if (cat)
+    for (int j = 0; j < dc; ++j) cat[j] = -1;
   *y = std::nanf("");
   Cursor c{b, e};
   c.ws();
@@ -227,7 +242,11 @@ int parse_one(const char* b, const char* e, int dnum, int ddisc, int dc, int64_t
             const char* s;
             size_t n;
             if (!c.str(s, n)) return -1;
-            if (j < dc) cat[j] = hash_cat(reinterpret_cast<const uint8_t*>(s), n, j, dn, dim);
+            if (j < dc) {
+              const uint8_t* us = reinterpret_cast<const uint8_t*>(s);
+              if (cat) cat[j] = hash_cat(us, n, j, dn, dim);
+              else cat16[j] = hash_cat16(us, n, j, cspan);
+            }
             ++j;
             if (c.eat(',')) continue;
             if (c.eat(']')) break;
@@ -288,17 +307,24 @@ OMLDM_HOST_API int32_t omldm_hash_cat(const char* s, int64_t n, int field, int d
   return hash_cat(reinterpret_cast<const uint8_t*>(s), size_t(n), field, dn, dim);
 }
 
+OMLDM_HOST_API int32_t omldm_hash_cat16(const char* s, int64_t n, int field, int cspan) {
+  return hash_cat16(reinterpret_cast<const uint8_t*>(s), size_t(n), field, cspan);
+}
+
 // Parses n newline-free records buf[off[i]:off[i+1]]. Returns the number of valid records.
 OMLDM_HOST_API int64_t omldm_parse_instances(const char* buf, const int64_t* off, int n, int dnum,
-                                             int ddisc, int dc, int64_t dim, float* num,
-                                             int32_t* cat, float* y, int8_t* op, int nthreads) {
+                                             int ddisc, int dc, int64_t dim, int cspan,
+                                             float* num, void* cat, float* y, int8_t* op,
+                                             int nthreads) {
+  const int esz = cspan > 0 ? 2 : 4;
   const int dn = dnum + ddisc;
   std::atomic<int64_t> valid{0};
   parallel_for(n, nthreads, [&](int a, int b) {
     int64_t v = 0;
     for (int i = a; i < b; ++i) {
       const int r = parse_one(buf + off[i], buf + off[i + 1], dnum, ddisc, dc, dim,
-                              num + int64_t(i) * dn, cat + int64_t(i) * dc, y + i);
+                              num + int64_t(i) * dn,
+                              static_cast<char*>(cat) + int64_t(i) * dc * esz, cspan, y + i);
       op[i] = int8_t(r);
       v += r >= 0;
     }
@@ -315,13 +341,14 @@ OMLDM_HOST_API int64_t omldm_parse_instances(const char* buf, const int64_t* off
 // stream can be generated independently on any rank.
 OMLDM_HOST_API void omldm_synth_batch(uint64_t seed, int64_t start, int B, int dn, int dc,
                                       int64_t dim, int task, int n_classes, float noise,
-                                      float* num, int32_t* cat, float* y, int nthreads) {
+                                      int cspan, float* num, void* cat, float* y, int nthreads) {
   const int64_t span = dim - dn - 1;  // slot dim-1 is reserved for the intercept
   parallel_for(B, nthreads, [&](int a, int b) {
     for (int i = a; i < b; ++i) {
       uint64_t s = mix64(seed * 0x9e3779b97f4a7c15ull + uint64_t(start + i));
       float* xn = num + int64_t(i) * dn;
-      int32_t* xc = cat + int64_t(i) * dc;
+      int32_t* xc = cspan > 0 ? nullptr : static_cast<int32_t*>(cat) + int64_t(i) * dc;
+      uint16_t* xc16 = cspan > 0 ? static_cast<uint16_t*>(cat) + int64_t(i) * dc : nullptr;
       double score[16] = {0};
       const int K = task == 2 ? std::max(2, std::min(16, n_classes)) : 1;
       for (int j = 0; j < dn; ++j) {
@@ -339,9 +366,16 @@ OMLDM_HOST_API void omldm_synth_batch(uint64_t seed, int64_t start, int B, int d
         const double u = u01(s);
         const int64_t rank = int64_t(double(vocab) * u * u * u);
         const uint64_t h = mix64(seed + uint64_t(j) * 0x100000001b3ull + uint64_t(rank) * 0x9e37ull);
-        const int32_t slot = int32_t(dn + int64_t(h & 0x7fffffffull) % span);
         const bool neg = (h >> 63) & 1ull;
-        xc[j] = neg ? int32_t(uint32_t(slot) | 0x80000000u) : slot;
+        int32_t slot;
+        if (xc16) {
+          const uint32_t local = uint32_t((h & 0x7fffffffull) % uint64_t(cspan));
+          slot = int32_t(dn + int64_t(j) * cspan + local);
+          xc16[j] = uint16_t((neg ? 0x8000u : 0u) | local);
+        } else {
+          slot = int32_t(dn + int64_t(h & 0x7fffffffull) % span);
+          xc[j] = neg ? int32_t(uint32_t(slot) | 0x80000000u) : slot;
+        }
         const double sv = neg ? -1.0 : 1.0;
         for (int k = 0; k < K; ++k) {
           uint64_t hs = mix64((seed ^ 0x27d4eb2dull) + uint64_t(slot) * 31 + uint64_t(k) * 104729);

@@ -37,15 +37,34 @@ inline float bf16_to_f(uint16_t b) {
   return f;
 }
 
+// Decodes categorical field j of row t (int32 signed-slot form, or the compact uint16
+// field-aware form when cspan > 0). Returns false when absent / out of range.
+inline bool cat_at(const void* cat, int dc, long long t, int j, int dn, int dim, int cspan,
+                   int& idx, float& v) {
+  if (cspan > 0) {
+    const unsigned c = static_cast<const uint16_t*>(cat)[t * dc + j];
+    if (c == 0xFFFFu) return false;
+    idx = dn + j * cspan + int(c & 0x7fffu);
+    v = (c & 0x8000u) ? -1.f : 1.f;
+  } else {
+    const int c = static_cast<const int32_t*>(cat)[t * dc + j];
+    if (c == -1) return false;
+    idx = c & 0x7fffffff;
+    v = c < 0 ? -1.f : 1.f;
+  }
+  return idx < dim;
+}
+
 }  // namespace
 
 // w: fp32 [dim] or bf16 [dim] (w_bf16); num: fp32 [B, dn]. stats: [S, 6].
 // dacc: [dim + 1] accumulates σ·Δ/P (+ σ/P at [dim]), exactly like the kernel.
 OMLDM_HOST_API int omldm_cpu_linear_round(const void* w, int w_bf16, const float* num, int dn,
-                                          const int32_t* cat, int dc, const float* y, int B,
+                                          const void* cat, int dc, const float* y, int B,
                                           int R, int S, float* dacc, int dim, float* stats,
                                           int rule, int variant, float C, float eps, float lr,
-                                          float lam, float inv_p, int bias, int nthreads) {
+                                          float lam, float inv_p, int bias, int cspan,
+                                          int nthreads) {
   const P p{rule, variant, C, eps, lr, lam, inv_p};
   const float* w32 = static_cast<const float*>(w);
   const uint16_t* w16 = static_cast<const uint16_t*>(w);
@@ -71,12 +90,11 @@ OMLDM_HOST_API int omldm_cpu_linear_round(const void* w, int w_bf16, const float
           }
         }
         for (int j = 0; j < dc; ++j) {
-          const int c = cat[t * dc + j];
-          if (c == -1) continue;
-          const int id = c & 0x7fffffff;
-          if (id >= dim) continue;
+          int id;
+          float v;
+          if (!cat_at(cat, dc, t, j, dn, dim, cspan, id, v)) continue;
           idx[F] = id;
-          xv[F++] = c < 0 ? -1.f : 1.f;
+          xv[F++] = v;
         }
         if (bias) {
           idx[F] = dim - 1;
@@ -175,20 +193,18 @@ OMLDM_HOST_API void omldm_cpu_linear_apply(float* w32, uint16_t* w16, float* dac
 }
 
 OMLDM_HOST_API void omldm_cpu_linear_predict(const float* w, long long wstride, int M,
-                                             const float* num, int dn, const int32_t* cat, int dc,
-                                             int B, int dim, int bias, const float* wscale,
-                                             float* out) {
+                                             const float* num, int dn, const void* cat, int dc,
+                                             int B, int dim, int bias, int cspan,
+                                             const float* wscale, float* out) {
   for (int t = 0; t < B; ++t)
     for (int m = 0; m < M; ++m) {
       const float* wm = w + (size_t)m * wstride;
       float acc = 0.f;
       for (int j = 0; j < dn && j < dim; ++j) acc += num[(size_t)t * dn + j] * wm[j];
       for (int j = 0; j < dc; ++j) {
-        const int c = cat[(size_t)t * dc + j];
-        if (c == -1) continue;
-        const int id = c & 0x7fffffff;
-        if (id >= dim) continue;
-        acc += (c < 0 ? -1.f : 1.f) * wm[id];
+        int id;
+        float v;
+        if (cat_at(cat, dc, t, j, dn, dim, cspan, id, v)) acc += v * wm[id];
       }
       if (bias) acc += wm[dim - 1];
       out[(size_t)t * M + m] = acc * (wscale ? wscale[m] : 1.f);

@@ -39,7 +39,8 @@ struct LinParams {
   float lam;
   float inv_p;
   int bias;
-  float cclip;    // τ clip: C for PA-I, +inf otherwise
+  int cspan;      // > 0: compact uint16 categorical wire format (see load_feature)
+  float cclip;   // τ clip: C for PA-I, +inf otherwise
   float kadd;     // τ denominator offset: 1/(2C) for PA-II, 0 otherwise
   float shrink;   // per-step multiplicative L2 shrink of w (1 when λ = 0)
   float rshrink;  // 1 / shrink
@@ -60,10 +61,13 @@ constexpr int kOvf = 64;
 // bit 31; -1 marks an absent categorical feature.
 // With bias != 0 the feature right after the categorical ones is the intercept: slot
 // dim-1 (reserved by the hasher) with constant value 1 (reference VectorBias, U23).
+// Compact wire format (cspan > 0): categorical field f is a uint16 {sign:1, local:15}
+// with slot = dn + f·cspan + local (field-aware hashing), 0xFFFF = absent — half the
+// PCIe bytes of the int32 form for Criteo-shaped streams.
 template <typename NumT>
 __device__ __forceinline__ void load_feature(const NumT* __restrict__ num, int dn,
-                                             const int* __restrict__ cat, int dc, int t, int j,
-                                             int dim, int bias, int& idx, float& v) {
+                                             const void* __restrict__ cat, int dc, int t, int j,
+                                             int dim, int bias, int cspan, int& idx, float& v) {
   idx = -1;
   v = 0.f;
   if (j == dn + dc && bias) {
@@ -73,10 +77,18 @@ __device__ __forceinline__ void load_feature(const NumT* __restrict__ num, int d
     idx = j;
     v = to_f(num[(size_t)t * dn + j]);
   } else if (j < dn + dc) {
-    const int c = cat[(size_t)t * dc + (j - dn)];
-    if (c != -1) {
-      idx = c & 0x7fffffff;
-      v = c < 0 ? -1.f : 1.f;
+    if (cspan > 0) {
+      const unsigned c = static_cast<const unsigned short*>(cat)[(size_t)t * dc + (j - dn)];
+      if (c != 0xFFFFu) {
+        idx = dn + (j - dn) * cspan + (int)(c & 0x7fffu);
+        v = (c & 0x8000u) ? -1.f : 1.f;
+      }
+    } else {
+      const int c = static_cast<const int*>(cat)[(size_t)t * dc + (j - dn)];
+      if (c != -1) {
+        idx = c & 0x7fffffff;
+        v = c < 0 ? -1.f : 1.f;
+      }
     }
   }
   if ((unsigned)idx >= (unsigned)dim) {  // never gather out of bounds
@@ -164,7 +176,7 @@ struct Step {
 // phase.
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void linear_round_kernel(
-    const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const int* __restrict__ cat,
+    const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
     int dc, const float* __restrict__ yv, int B, int R, int dim, float* __restrict__ ws,
     int2* __restrict__ tables, LinParams p, TableGeom g, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -214,7 +226,7 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
       for (int f = 0; f < FPL; ++f) {
         int idx = -1;
         float v = 0.f;
-        if (ok) load_feature(num, dn, cat, dc, t, lane + kWave * f, dim, p.bias, idx, v);
+        if (ok) load_feature(num, dn, cat, dc, t, lane + kWave * f, dim, p.bias, p.cspan, idx, v);
         nidx[e][f] = idx;
         nxv[e][f] = v;
       }
@@ -438,7 +450,7 @@ __global__ __launch_bounds__(256) void linear_round_finish_kernel(const float* _
 template <int FPL, typename NumT, typename WT>
 __global__ __launch_bounds__(256) void linear_predict_kernel(
     const WT* __restrict__ w, long long wstride, int M, const NumT* __restrict__ num, int dn,
-    const int* __restrict__ cat, int dc, int B, int dim, int bias,
+    const void* __restrict__ cat, int dc, int B, int dim, int bias, int cspan,
     const float* __restrict__ wscale, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -452,7 +464,7 @@ __global__ __launch_bounds__(256) void linear_predict_kernel(
     for (int f = 0; f < FPL; ++f) {
       int idx;
       float v;
-      load_feature(num, dn, cat, dc, t, lane + kWave * f, dim, bias, idx, v);
+      load_feature(num, dn, cat, dc, t, lane + kWave * f, dim, bias, cspan, idx, v);
       if (idx >= 0) acc = fmaf(v, to_f(wm[idx]), acc);
     }
     acc = wave_sum(acc);
@@ -499,7 +511,7 @@ __global__ __launch_bounds__(256) void linear_apply_kernel(float* __restrict__ w
 }
 
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
-static int launch_round(const void* w, const void* num, int dn, const int* cat, int dc,
+static int launch_round(const void* w, const void* num, int dn, const void* cat, int dc,
                         const float* y, int B, int R, int S, float* dacc, int dim, float* ws,
                         int2* tables, float* cum, const LinParams& p, TableGeom g, int ablate,
                         hipStream_t st) {
@@ -527,7 +539,7 @@ static int launch_round(const void* w, const void* num, int dn, const int* cat, 
 
 template <int FPL, int CH, int RULE>
 static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
-                          const int* cat, int dc, const float* y, int B, int R, int S, float* dacc,
+                          const void* cat, int dc, const float* y, int B, int R, int S, float* dacc,
                           int dim, float* ws, int2* tables, float* cum, const LinParams& p,
                           TableGeom g, int ablate, hipStream_t st) {
 #define OMLDM_LR(NT, WTT)                                                                      \
@@ -544,7 +556,7 @@ static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf
 
 template <int FPL, int CH>
 static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, int num_bf16,
-                         int dn, const int* cat, int dc, const float* y, int B, int R, int S,
+                         int dn, const void* cat, int dc, const float* y, int B, int R, int S,
                          float* dacc, int dim, float* ws, int2* tables, float* cum,
                          const LinParams& p, TableGeom g, int ablate, hipStream_t st) {
   if (rule == kHinge)
@@ -559,31 +571,33 @@ static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, i
 
 template <int FPL, typename NumT, typename WT>
 static int launch_predict(const void* w, long long wstride, int M, const void* num, int dn,
-                          const int* cat, int dc, int B, int dim, int bias, const float* wscale,
+                          const void* cat, int dc, int B, int dim, int bias, int cspan,
+                          const float* wscale,
                           float* out, hipStream_t st) {
   const int waves = B < 1 ? 1 : B;
   int blocks = (waves + 3) / 4;
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL((linear_predict_kernel<FPL, NumT, WT>), dim3(blocks, M), dim3(256), 0, st,
-                     (const WT*)w, wstride, M, (const NumT*)num, dn, cat, dc, B, dim, bias, wscale, out);
+                     (const WT*)w, wstride, M, (const NumT*)num, dn, cat, dc, B, dim, bias, cspan, wscale, out);
   return (int)hipGetLastError();
 }
 
 template <int FPL>
 static int dispatch_predict(const void* w, int w_bf16, long long wstride, int M, const void* num,
-                            int num_bf16, int dn, const int* cat, int dc, int B, int dim, int bias,
-                            const float* wscale, float* out, hipStream_t st) {
+                            int num_bf16, int dn, const void* cat, int dc, int B, int dim, int bias,
+                            int cspan, const float* wscale, float* out, hipStream_t st) {
   if (num_bf16) {
     if (w_bf16)
       return launch_predict<FPL, __hip_bfloat16, __hip_bfloat16>(w, wstride, M, num, dn, cat, dc,
-                                                                 B, dim, bias, wscale, out, st);
-    return launch_predict<FPL, __hip_bfloat16, float>(w, wstride, M, num, dn, cat, dc, B, dim, bias,
+                                                                 B, dim, bias, cspan, wscale, out,
+                                                                 st);
+    return launch_predict<FPL, __hip_bfloat16, float>(w, wstride, M, num, dn, cat, dc, B, dim, bias, cspan,
                                                       wscale, out, st);
   }
   if (w_bf16)
-    return launch_predict<FPL, float, __hip_bfloat16>(w, wstride, M, num, dn, cat, dc, B, dim, bias,
+    return launch_predict<FPL, float, __hip_bfloat16>(w, wstride, M, num, dn, cat, dc, B, dim, bias, cspan,
                                                       wscale, out, st);
-  return launch_predict<FPL, float, float>(w, wstride, M, num, dn, cat, dc, B, dim, bias, wscale,
+  return launch_predict<FPL, float, float>(w, wstride, M, num, dn, cat, dc, B, dim, bias, cspan, wscale,
                                            out, st);
 }
 
@@ -612,18 +626,18 @@ OMLDM_API int omldm_linear_table_geom(int dim, int log2cap, int* out3) {
 
 // tables: device scratch of S * ((1 << log2cap) + 64) int2.
 OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
-                                 const int* cat, int dc, const float* y, int B, int R, int S,
+                                 const void* cat, int dc, const float* y, int B, int R, int S,
                                  float* dacc, int dim, float* ws, void* tables, float* cum,
                                  int rule, int variant, float C, float eps, float lr, float lam,
-                                 float inv_p, int bias, int log2cap, int chunk, int ablate,
-                                 void* stream) {
+                                 float inv_p, int bias, int cspan, int log2cap, int chunk,
+                                 int ablate, void* stream) {
   if (S <= 0) return 0;
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
   int geo[3];
   if (omldm_linear_table_geom(dim, log2cap, geo)) return -3;
   const TableGeom g{geo[0], geo[1], geo[2]};
   const float shrink = rule == kLogistic ? 1.f - lr * lam : 1.f - lam;
-  const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias,
+  const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias, cspan,
                     variant == kPA1 ? C : INFINITY, variant == kPA2 ? 0.5f / C : 0.f, shrink,
                     1.f / shrink};
   const int F = dn + dc + (bias ? 1 : 0);
@@ -637,15 +651,15 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
 }
 
 OMLDM_API int omldm_linear_predict(const void* w, int w_bf16, long long wstride, int M,
-                                   const void* num, int num_bf16, int dn, const int* cat, int dc,
-                                   int B, int dim, int bias, const float* wscale, float* out,
-                                   void* stream) {
+                                   const void* num, int num_bf16, int dn, const void* cat, int dc,
+                                   int B, int dim, int bias, int cspan, const float* wscale,
+                                   float* out, void* stream) {
   if (B <= 0 || M <= 0) return 0;
   const int F = dn + dc + (bias ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
-  if (F <= 64) return dispatch_predict<1>(w, w_bf16, wstride, M, num, num_bf16, dn, cat, dc, B, dim, bias, wscale, out, st);
-  if (F <= 128) return dispatch_predict<2>(w, w_bf16, wstride, M, num, num_bf16, dn, cat, dc, B, dim, bias, wscale, out, st);
-  if (F <= 256) return dispatch_predict<4>(w, w_bf16, wstride, M, num, num_bf16, dn, cat, dc, B, dim, bias, wscale, out, st);
+  if (F <= 64) return dispatch_predict<1>(w, w_bf16, wstride, M, num, num_bf16, dn, cat, dc, B, dim, bias, cspan, wscale, out, st);
+  if (F <= 128) return dispatch_predict<2>(w, w_bf16, wstride, M, num, num_bf16, dn, cat, dc, B, dim, bias, cspan, wscale, out, st);
+  if (F <= 256) return dispatch_predict<4>(w, w_bf16, wstride, M, num, num_bf16, dn, cat, dc, B, dim, bias, cspan, wscale, out, st);
   return -2;
 }
 

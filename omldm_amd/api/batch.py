@@ -28,6 +28,9 @@ class FeatureSpace:
     n_discrete: int = 0
     n_categorical: int = 26
     dim: int = 1 << 20
+    # Compact wire format: field-aware hashing, categorical slot carried as uint16
+    # {sign, local} with slot = dn + field·cat_span + local (half the PCIe bytes).
+    field_aware: bool = False
 
     @property
     def dn(self) -> int:
@@ -37,11 +40,23 @@ class FeatureSpace:
     def dc(self) -> int:
         return self.n_categorical
 
+    @property
+    def cat_span(self) -> int:
+        if not self.field_aware or self.dc == 0:
+            return 0
+        return min(32767, (self.dim - self.dn - 1) // self.dc)
+
+    @property
+    def cat_dtype(self):
+        return torch.int16 if self.field_aware else torch.int32
+
     def __post_init__(self):
         if self.dim <= self.dn:
             raise ValueError("hash dimension must exceed the number of dense slots")
         if self.dim >= 2**31:
             raise ValueError("hash dimension must fit in 31 bits")
+        if self.field_aware and self.dc and (self.dim - self.dn - 1) // self.dc < 1:
+            raise ValueError("hash dimension too small for field-aware hashing")
 
 
 @dataclass
@@ -50,6 +65,7 @@ class HashedBatch:
     cat: torch.Tensor
     y: torch.Tensor
     raw: list | None = field(default=None, compare=False)  # optional raw records (forecasting)
+    cat_span: int = 0  # > 0: compact uint16 field-aware categorical format (int16 storage)
 
     @property
     def B(self) -> int:
@@ -71,24 +87,29 @@ class HashedBatch:
         return self.B
 
     @staticmethod
-    def empty(space: FeatureSpace, B: int = 0, device="cpu", pin: bool = False) -> "HashedBatch":
+    def empty(space: FeatureSpace, B: int = 0, device="cpu", pin: bool = False,
+              num_dtype=torch.float32) -> "HashedBatch":
         kw = dict(device=device)
         if pin and torch.cuda.is_available():
             kw["pin_memory"] = True
         return HashedBatch(
-            torch.zeros((B, space.dn), dtype=torch.float32, **kw),
-            torch.full((B, space.dc), -1, dtype=torch.int32, **kw),
+            torch.zeros((B, space.dn), dtype=num_dtype, **kw),
+            torch.full((B, space.dc), -1, dtype=space.cat_dtype, **kw),
             torch.full((B,), float("nan"), dtype=torch.float32, **kw),
+            cat_span=space.cat_span,
         )
 
+    def _like(self, num, cat, y, raw) -> "HashedBatch":
+        return HashedBatch(num, cat, y, raw, self.cat_span)
+
     def to(self, device, non_blocking: bool = False) -> "HashedBatch":
-        return HashedBatch(self.num.to(device, non_blocking=non_blocking),
-                           self.cat.to(device, non_blocking=non_blocking),
-                           self.y.to(device, non_blocking=non_blocking), self.raw)
+        return self._like(self.num.to(device, non_blocking=non_blocking),
+                          self.cat.to(device, non_blocking=non_blocking),
+                          self.y.to(device, non_blocking=non_blocking), self.raw)
 
     def slice(self, a: int, b: int) -> "HashedBatch":
-        return HashedBatch(self.num[a:b], self.cat[a:b], self.y[a:b],
-                           None if self.raw is None else self.raw[a:b])
+        return self._like(self.num[a:b], self.cat[a:b], self.y[a:b],
+                          None if self.raw is None else self.raw[a:b])
 
     def select(self, idx) -> "HashedBatch":
         if isinstance(idx, np.ndarray):
@@ -97,7 +118,7 @@ class HashedBatch:
         raw = None
         if self.raw is not None:
             raw = [self.raw[i] for i in idx.tolist()]
-        return HashedBatch(self.num[idx], self.cat[idx], self.y[idx], raw)
+        return self._like(self.num[idx], self.cat[idx], self.y[idx], raw)
 
     @staticmethod
     def cat_batches(batches: list["HashedBatch"]) -> "HashedBatch":
@@ -108,11 +129,23 @@ class HashedBatch:
             for b in batches:
                 raw.extend(b.raw if b.raw is not None else [None] * b.B)
         return HashedBatch(torch.cat([b.num for b in batches]), torch.cat([b.cat for b in batches]),
-                           torch.cat([b.y for b in batches]), raw)
+                           torch.cat([b.y for b in batches]), raw, batches[0].cat_span)
 
     def contiguous(self) -> "HashedBatch":
-        return HashedBatch(self.num.contiguous(), self.cat.contiguous(), self.y.contiguous(),
-                           self.raw)
+        return self._like(self.num.contiguous(), self.cat.contiguous(), self.y.contiguous(),
+                          self.raw)
+
+    def cat_slots(self) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """(slot [B, dc] int64, sign [B, dc] float, valid [B, dc] bool) for either format."""
+        if self.cat_span > 0:
+            c = self.cat.long() & 0xFFFF
+            valid = c != 0xFFFF
+            f = torch.arange(self.dc, device=c.device).unsqueeze(0)
+            slot = self.dn + f * self.cat_span + (c & 0x7FFF)
+            sign = torch.where((c & 0x8000) != 0, -1.0, 1.0)
+            return slot, sign, valid
+        c = self.cat.long()
+        return c & 0x7FFFFFFF, torch.where(c < 0, -1.0, 1.0), c != -1
 
     def dense(self, dim: int | None = None) -> torch.Tensor:
         """Materialise [B, dim] dense features (tests / small dense learners only)."""
@@ -120,12 +153,9 @@ class HashedBatch:
         B = self.B
         out = torch.zeros((B, dim), dtype=torch.float32, device=self.y.device)
         dn = min(self.dn, dim)
-        out[:, :dn] = self.num[:, :dn]
-        c = self.cat.long()
-        valid = c != -1
-        idx = (c & 0x7FFFFFFF).clamp(max=dim - 1)
-        sign = torch.where(c < 0, -1.0, 1.0)
-        valid &= (c & 0x7FFFFFFF) < dim
-        rows = torch.arange(B, device=out.device).unsqueeze(1).expand_as(c)
-        out.index_put_((rows[valid], idx[valid]), sign[valid], accumulate=True)
+        out[:, :dn] = self.num[:, :dn].float()
+        slot, sign, valid = self.cat_slots()
+        valid = valid & (slot < dim)
+        rows = torch.arange(B, device=out.device).unsqueeze(1).expand_as(slot)
+        out.index_put_((rows[valid], slot[valid]), sign[valid], accumulate=True)
         return out

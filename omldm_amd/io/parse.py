@@ -20,6 +20,8 @@ OP_TRAINING, OP_FORECASTING, OP_INVALID = 0, 1, -1
 
 def hash_categorical(token: str, field: int, space: FeatureSpace) -> int:
     b = token.encode()
+    if space.cat_span:
+        return int(native.host().omldm_hash_cat16(b, len(b), field, space.cat_span))
     return int(native.host().omldm_hash_cat(b, len(b), field, space.dn, space.dim))
 
 
@@ -33,7 +35,7 @@ def parse_records(records: list, space: FeatureSpace, threads: int | None = None
         np.cumsum([len(e) for e in enc], out=off[1:])
     buf = b"".join(enc)
     num = torch.zeros((n, space.dn), dtype=torch.float32)
-    cat = torch.full((n, space.dc), -1, dtype=torch.int32)
+    cat = torch.full((n, space.dc), -1, dtype=space.cat_dtype)
     y = torch.full((n,), float("nan"), dtype=torch.float32)
     op = np.full(n, -1, dtype=np.int8)
     valid = 0
@@ -41,8 +43,9 @@ def parse_records(records: list, space: FeatureSpace, threads: int | None = None
         threads = threads or min(8, os.cpu_count() or 1)
         valid = native.host().omldm_parse_instances(
             buf, off.ctypes.data, n, space.n_numerical, space.n_discrete, space.dc, space.dim,
-            num.data_ptr(), cat.data_ptr(), y.data_ptr(), op.ctypes.data, threads)
+            space.cat_span, num.data_ptr(), cat.data_ptr(), y.data_ptr(), op.ctypes.data,
+            threads)
     raw = None
     if keep_raw:
         raw = [e.decode() if isinstance(e, (bytes, bytearray)) else e for e in enc]
-    return HashedBatch(num, cat, y, raw), op, int(valid)
+    return HashedBatch(num, cat, y, raw, space.cat_span), op, int(valid)

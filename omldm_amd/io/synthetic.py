@@ -26,11 +26,12 @@ def synth_batch(space: FeatureSpace, B: int, start: int = 0, seed: int = 25, tas
                 out: HashedBatch | None = None, threads: int | None = None) -> HashedBatch:
     if out is None:
         out = HashedBatch.empty(space, B, pin=pin)
-    assert out.B == B and not out.y.is_cuda
+    assert out.B == B and not out.y.is_cuda and out.num.dtype == torch.float32
+    assert out.cat.dtype == space.cat_dtype
     threads = threads or min(16, os.cpu_count() or 1)
     native.host().omldm_synth_batch(seed, start, B, space.dn, space.dc, space.dim, task,
-                                    n_classes, noise, ptr(out.num), ptr(out.cat), ptr(out.y),
-                                    threads)
+                                    n_classes, noise, space.cat_span, ptr(out.num), ptr(out.cat),
+                                    ptr(out.y), threads)
     return out
 
 

@@ -69,7 +69,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
     assert w.shape[0] == dim and (stats is None or stats.shape == (S, STAT_W))
     assert dacc.dtype == torch.float32
     num, cat, y = batch.num, batch.cat, batch.y
-    assert cat.dtype == torch.int32 and y.dtype == torch.float32
+    assert cat.dtype == (torch.int16 if batch.cat_span else torch.int32) and y.dtype == torch.float32
     assert num.is_contiguous() and cat.is_contiguous() and y.is_contiguous()
     if S <= 0:
         return
@@ -87,7 +87,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
             ptr(w), int(w.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
             num.shape[1], ptr(cat), cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim,
             ptr(ws), ptr(tables), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr,
-            rule.lam, inv_p, int(rule.bias), log2cap, int(chunk), int(ablate),
+            rule.lam, inv_p, int(rule.bias), batch.cat_span, log2cap, int(chunk), int(ablate),
             native.stream_of(w))
         check(rc, "omldm_linear_round")
         if stats is not None:
@@ -98,7 +98,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         native.host().omldm_cpu_linear_round(
             ptr(w), int(w.dtype == torch.bfloat16), ptr(num32), num32.shape[1], ptr(cat),
             cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim, ptr(st), rule.rule,
-            rule.variant, rule.C, rule.eps, rule.lr, rule.lam, inv_p, int(rule.bias),
+            rule.variant, rule.C, rule.eps, rule.lr, rule.lam, inv_p, int(rule.bias), batch.cat_span,
             _cpu_threads())
         if cum is not None:
             cum[:STAT_W] += st.sum(0)
@@ -131,12 +131,12 @@ def linear_predict(w: torch.Tensor, batch: HashedBatch, wscale: torch.Tensor | N
         rc = native.hip().omldm_linear_predict(
             ptr(W), int(W.dtype == torch.bfloat16), W.stride(0), M, ptr(num),
             int(num.dtype == torch.bfloat16), num.shape[1], ptr(batch.cat), batch.cat.shape[1], B,
-            dim, int(bias), ptr(wscale), ptr(out), native.stream_of(w))
+            dim, int(bias), batch.cat_span, ptr(wscale), ptr(out), native.stream_of(w))
         check(rc, "omldm_linear_predict")
     else:
         W32 = W.float().contiguous()
         num = batch.num.float().contiguous()
         native.host().omldm_cpu_linear_predict(ptr(W32), W32.stride(0), M, ptr(num), num.shape[1],
                                                ptr(batch.cat), batch.cat.shape[1], B, dim,
-                                               int(bias), ptr(wscale), ptr(out))
+                                               int(bias), batch.cat_span, ptr(wscale), ptr(out))
     return out.view(B) if single else out

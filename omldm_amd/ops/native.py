@@ -42,10 +42,10 @@ def _sig(lib, name, res, args):
 HIP_SIGS = [
     ("omldm_linear_round", i32, [vp, i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, vp, i32, vp,
                                  vp, vp, i32, i32, f32, f32, f32, f32, f32, i32, i32, i32, i32,
-                                 vp]),
+                                 i32, vp]),
     ("omldm_linear_table_geom", i32, [i32, i32, vp]),
-    ("omldm_linear_predict", i32, [vp, i32, i64, i32, vp, i32, i32, vp, i32, i32, i32, i32, vp,
-                                   vp, vp]),
+    ("omldm_linear_predict", i32, [vp, i32, i64, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32,
+                                   vp, vp, vp]),
     ("omldm_linear_apply", i32, [vp, vp, vp, i32, vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
     ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
@@ -60,12 +60,16 @@ HIP_SIGS = [
 HOST_SIGS = [
     ("omldm_murmur3_32", u32, [C.c_char_p, i64, u32]),
     ("omldm_hash_cat", C.c_int32, [C.c_char_p, i64, i32, i32, i64]),
-    ("omldm_parse_instances", i64, [C.c_char_p, vp, i32, i32, i32, i32, i64, vp, vp, vp, vp, i32]),
-    ("omldm_synth_batch", None, [u64, i64, i32, i32, i32, i64, i32, i32, f32, vp, vp, vp, i32]),
+    ("omldm_hash_cat16", C.c_int32, [C.c_char_p, i64, i32, i32]),
+    ("omldm_parse_instances", i64, [C.c_char_p, vp, i32, i32, i32, i32, i64, i32, vp, vp, vp, vp,
+                                    i32]),
+    ("omldm_synth_batch", None, [u64, i64, i32, i32, i32, i64, i32, i32, f32, i32, vp, vp, vp,
+                                 i32]),
     ("omldm_cpu_linear_round", i32, [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, i32, vp,
-                                     i32, i32, f32, f32, f32, f32, f32, i32, i32]),
+                                     i32, i32, f32, f32, f32, f32, f32, i32, i32, i32]),
     ("omldm_cpu_linear_apply", None, [vp, vp, vp, i32]),
-    ("omldm_cpu_linear_predict", None, [vp, i64, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp]),
+    ("omldm_cpu_linear_predict", None, [vp, i64, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp,
+                                        vp]),
 ]
 
 
