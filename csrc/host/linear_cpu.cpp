@@ -173,6 +173,79 @@ OMLDM_HOST_API int omldm_cpu_linear_round(const void* w, int w_bf16, const float
 }
 
 // w = (a·w + D)/n with a = D[dim], n = D[dim+1] (n == 0: unchanged) — see linear_apply_kernel.
+// MultiClassPA round (CPU mirror of csrc/kernels/multiclass_spoke.hip, int32 cat format).
+// dacc [K][dim] accumulates Σ_s Δ_s; stats[0..5] += loss, n, mistakes, active, -, -.
+OMLDM_HOST_API int omldm_cpu_multiclass_round(const float* W, const float* num, int dn,
+                                              const int32_t* cat, int dc, const float* y, int B,
+                                              int R, int S, int dim, int nclass, int variant,
+                                              float C, int bias, float* dacc, float* stats) {
+  std::vector<int> idx(dn + dc + 1);
+  std::vector<float> xv(dn + dc + 1), sc(nclass);
+  for (int s = 0; s < S; ++s) {
+    const long long a = std::min<long long>((long long)s * R, B);
+    const long long b = std::min<long long>(a + R, B);
+    if (a >= b) continue;
+    std::unordered_map<long long, float> delta;  // key = k*dim + idx
+    for (long long t = a; t < b; ++t) {
+      if (std::isnan(y[t])) continue;
+      const int yc = int(y[t]);
+      int F = 0;
+      for (int j = 0; j < dn && j < dim; ++j) {
+        idx[F] = j;
+        xv[F++] = num[t * dn + j];
+      }
+      for (int j = 0; j < dc; ++j) {
+        int id;
+        float v;
+        if (!cat_at(cat, dc, t, j, dn, dim, 0, id, v)) continue;
+        idx[F] = id;
+        xv[F++] = v;
+      }
+      if (bias) {
+        idx[F] = dim - 1;
+        xv[F++] = 1.f;
+      }
+      float n2 = 0.f;
+      for (int k = 0; k < nclass; ++k) sc[k] = 0.f;
+      for (int f = 0; f < F; ++f) {
+        n2 += xv[f] * xv[f];
+        for (int k = 0; k < nclass; ++k) {
+          auto it = delta.find((long long)k * dim + idx[f]);
+          const float d = it == delta.end() ? 0.f : it->second;
+          sc[k] += xv[f] * (W[(size_t)k * dim + idx[f]] + d);
+        }
+      }
+      int r = -1;
+      float best = -INFINITY;
+      for (int k = 0; k < nclass; ++k)
+        if (k != yc && sc[k] > best) {
+          best = sc[k];
+          r = k;
+        }
+      const float sy = (yc >= 0 && yc < nclass) ? sc[yc] : 0.f;
+      const float margin = sy - best;
+      const float loss = std::fmax(0.f, 1.f - margin);
+      stats[0] += loss;
+      stats[1] += 1.f;
+      stats[2] += margin <= 0.f ? 1.f : 0.f;
+      float tau = 0.f;
+      if (loss > 0.f && n2 > 0.f && r >= 0) {
+        const float den = 2.f * n2;
+        tau = variant == 0 ? loss / den
+                           : (variant == 1 ? std::fmin(C, loss / den) : loss / (den + 0.5f / C));
+      }
+      if (tau != 0.f)
+        for (int f = 0; f < F; ++f) {
+          if (yc >= 0 && yc < nclass) delta[(long long)yc * dim + idx[f]] += tau * xv[f];
+          delta[(long long)r * dim + idx[f]] -= tau * xv[f];
+        }
+    }
+    stats[3] += 1.f;
+    for (auto& kv : delta) dacc[kv.first] += kv.second;
+  }
+  return 0;
+}
+
 OMLDM_HOST_API void omldm_cpu_linear_apply(float* w32, uint16_t* w16, float* dacc, int dim) {
   const float n = dacc[dim + 1];
   const float a = n > 0.f ? dacc[dim] : 1.f;

@@ -1,0 +1,221 @@
+"""Topic transports: the engine's user-facing I/O (Kafka-style topics of JSON records).
+
+Reference: every input/output of the job is a Kafka topic (README.md:20-26; SURVEY.md
+Appendix B): requests (1 partition), trainingData / forecastingData (36), responses (1),
+predictions (36), performance; psMessages is gone (RCCL replaces it).
+
+Brokers (selected by the ``*Addr`` flag):
+* ``memory://name``        in-process broker (tests, single-process jobs)
+* ``file:///dir``          one append-only JSONL log per (topic, partition); consumers keep
+                           their own offsets — shared by all ranks of a node-local job
+* ``host:port``            Kafka wire protocol (omldm_amd.io.kafka)
+Partition assignment mirrors Flink's source subtasks: rank r of G consumes partitions
+p with p % G == r (omldm/Job.scala:42-57).
+"""
+from __future__ import annotations
+
+import os
+import threading
+from collections import defaultdict
+
+
+class Broker:
+    def partitions(self, topic: str) -> int:
+        raise NotImplementedError
+
+    def produce(self, topic: str, value: str | bytes, partition: int | None = None,
+                key: str | None = None) -> None:
+        raise NotImplementedError
+
+    def consume(self, topic: str, partition: int, offset: int, max_records: int
+                ) -> tuple[list[bytes], int]:
+        """Returns (records, next_offset)."""
+        raise NotImplementedError
+
+    def end_offset(self, topic: str, partition: int) -> int:
+        raise NotImplementedError
+
+    def create_topic(self, topic: str, partitions: int) -> None:
+        pass
+
+    def flush(self) -> None:
+        pass
+
+
+class MemoryBroker(Broker):
+    _registry: dict = {}
+    _reg_lock = threading.Lock()
+
+    def __init__(self):
+        self._logs = defaultdict(list)     # (topic, p) -> list[bytes]
+        self._nparts = {}
+        self._lock = threading.Lock()
+        self._rr = defaultdict(int)
+
+    @classmethod
+    def named(cls, name: str) -> "MemoryBroker":
+        with cls._reg_lock:
+            if name not in cls._registry:
+                cls._registry[name] = MemoryBroker()
+            return cls._registry[name]
+
+    def create_topic(self, topic, partitions):
+        with self._lock:
+            self._nparts[topic] = max(self._nparts.get(topic, 0), int(partitions))
+
+    def partitions(self, topic):
+        return self._nparts.get(topic, 1)
+
+    def produce(self, topic, value, partition=None, key=None):
+        if isinstance(value, str):
+            value = value.encode()
+        with self._lock:
+            n = self._nparts.setdefault(topic, 1)
+            if partition is None:
+                partition = self._rr[topic] % n
+                self._rr[topic] += 1
+            self._logs[(topic, partition % n)].append(value)
+
+    def consume(self, topic, partition, offset, max_records):
+        with self._lock:
+            log = self._logs.get((topic, partition), [])
+            recs = log[offset:offset + max_records]
+        return recs, offset + len(recs)
+
+    def end_offset(self, topic, partition):
+        with self._lock:
+            return len(self._logs.get((topic, partition), []))
+
+    def records(self, topic) -> list[bytes]:
+        """All records of a topic (partition order) — test helper."""
+        with self._lock:
+            out = []
+            for p in range(self.partitions(topic)):
+                out.extend(self._logs.get((topic, p), []))
+            return out
+
+
+class FileBroker(Broker):
+    """Append-only JSONL logs: <root>/<topic>/<partition>.jsonl (one record per line).
+    Consumer offsets are byte offsets, so every rank can tail its partitions."""
+
+    def __init__(self, root: str):
+        self.root = root
+        os.makedirs(root, exist_ok=True)
+        self._rr = defaultdict(int)
+        self._lock = threading.Lock()
+
+    def _dir(self, topic):
+        d = os.path.join(self.root, topic)
+        os.makedirs(d, exist_ok=True)
+        return d
+
+    def create_topic(self, topic, partitions):
+        d = self._dir(topic)
+        for p in range(int(partitions)):
+            open(os.path.join(d, f"{p}.jsonl"), "ab").close()
+
+    def partitions(self, topic):
+        d = self._dir(topic)
+        n = len([f for f in os.listdir(d) if f.endswith(".jsonl")])
+        return max(1, n)
+
+    def produce(self, topic, value, partition=None, key=None):
+        if isinstance(value, str):
+            value = value.encode()
+        value = value.replace(b"\n", b" ")
+        n = self.partitions(topic)
+        with self._lock:
+            if partition is None:
+                partition = self._rr[topic] % n
+                self._rr[topic] += 1
+            with open(os.path.join(self._dir(topic), f"{partition % n}.jsonl"), "ab") as f:
+                f.write(value + b"\n")
+
+    def consume(self, topic, partition, offset, max_records):
+        path = os.path.join(self._dir(topic), f"{partition}.jsonl")
+        if not os.path.exists(path):
+            return [], offset
+        with open(path, "rb") as f:
+            f.seek(offset)
+            data = f.read(max(1, max_records) * 4096)
+        if not data:
+            return [], offset
+        cut = data.rfind(b"\n")
+        if cut < 0:
+            return [], offset  # partial line still being written
+        lines = data[:cut].split(b"\n")
+        if len(lines) > max_records:
+            lines = lines[:max_records]
+            used = sum(len(x) + 1 for x in lines)
+        else:
+            used = cut + 1
+        return [x for x in lines if x.strip()], offset + used
+
+    def end_offset(self, topic, partition):
+        path = os.path.join(self._dir(topic), f"{partition}.jsonl")
+        return os.path.getsize(path) if os.path.exists(path) else 0
+
+
+def broker_for(addr: str) -> Broker:
+    if addr.startswith("memory://"):
+        return MemoryBroker.named(addr[len("memory://"):] or "default")
+    if addr.startswith("file://"):
+        return FileBroker(addr[len("file://"):])
+    from omldm_amd.io.kafka import KafkaBroker
+
+    return KafkaBroker(addr)
+
+
+class Consumer:
+    """Consumer of the partitions of one topic owned by this rank (p % world == rank).
+    ``start`` = "earliest" | "latest" (reference: requests/data earliest, performance
+    latest; omldm/Job.scala:42-57,127-142)."""
+
+    def __init__(self, broker: Broker, topic: str, rank: int = 0, world: int = 1,
+                 start: str = "earliest", all_partitions: bool = False):
+        self.broker = broker
+        self.topic = topic
+        n = broker.partitions(topic)
+        self.parts = list(range(n)) if all_partitions else [p for p in range(n)
+                                                            if p % world == rank]
+        self.offsets = {p: (broker.end_offset(topic, p) if start == "latest" else 0)
+                        for p in self.parts}
+
+    def poll(self, max_records: int) -> list[bytes]:
+        out = []
+        if not self.parts:
+            return out
+        share = max(1, max_records // len(self.parts))
+        for p in self.parts:
+            recs, nxt = self.broker.consume(self.topic, p, self.offsets[p], share)
+            self.offsets[p] = nxt
+            out.extend(recs)
+        return out
+
+    def state_dict(self) -> dict:
+        return {"offsets": dict(self.offsets)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        for p, o in sd.get("offsets", {}).items():
+            if int(p) in self.offsets:
+                self.offsets[int(p)] = int(o)
+
+
+def hub_message_partition(network_id: int, destination: int | None, n_partitions: int,
+                          terminate: bool = False) -> int:
+    """Reference FlinkHubMessagePartitioner (omldm/utils/kafkaPartitioners/
+    FlinkHubMessagePartitioner.scala:7-20): terminate → 0; unicast → dest % n;
+    broadcast → networkId % n. Kept for topic-compatible producers."""
+    if terminate:
+        return 0
+    if destination is not None:
+        return destination % n_partitions
+    return network_id % n_partitions
+
+
+def identity_partition(key: int, n: int) -> int:
+    """Reference random_partitioner — actually the identity (random_partitioner.scala:7-15)."""
+    if not 0 <= key < n:
+        raise ValueError(f"partition key {key} out of range [0, {n})")
+    return key

@@ -52,6 +52,11 @@ HIP_SIGS = [
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
     ("omldm_pull_copy", i32, [vp, vp, i64, i32, vp]),
     ("omldm_h2d_async", i32, [vp, vp, i64, vp]),
+    ("omldm_gram_update", i32, [vp, vp, i32, i32, vp, i32, vp]),
+    ("omldm_kmeans_assign", i32, [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+    ("omldm_multiclass_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, f32,
+                                     i32, vp, vp, i32, vp]),
+    ("omldm_multiclass_apply", i32, [vp, vp, i64, vp, vp]),
     ("omldm_stream_create_cumask", vp, [i32]),
     ("omldm_stream_destroy", i32, [vp]),
     ("omldm_host_register", i32, [vp, i64]),
@@ -68,6 +73,8 @@ HOST_SIGS = [
     ("omldm_cpu_linear_round", i32, [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, i32, vp,
                                      i32, i32, f32, f32, f32, f32, f32, i32, i32, i32]),
     ("omldm_cpu_linear_apply", None, [vp, vp, vp, i32]),
+    ("omldm_cpu_multiclass_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32,
+                                         f32, i32, vp, vp]),
     ("omldm_cpu_linear_predict", None, [vp, i64, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp,
                                         vp]),
 ]

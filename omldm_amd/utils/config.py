@@ -1,0 +1,112 @@
+"""Job configuration: the reference's CLI flags (same names, same defaults) + the
+MI355X-native engine's own flags.
+
+Reference flags: omldm/Job.scala:110-168 (ParameterTool.fromArgs), defaults in
+omldm/utils/DefaultJobParameters.scala:4-11, omldm/utils/Checkpointing.scala:11-23,
+omldm/job/FlinkLearning.scala:43-48. ``psMessages*`` flags are
+accepted and ignored: the parameter-server feedback loop is RCCL, not a Kafka topic.
+"""
+from __future__ import annotations
+
+import argparse
+from dataclasses import asdict, dataclass, field, fields
+
+
+def _bool(v) -> bool:
+    if isinstance(v, bool):
+        return v
+    return str(v).strip().lower() in ("1", "true", "yes", "y", "on")
+
+
+@dataclass
+class JobConfig:
+    # ---- reference flags (names and defaults kept)
+    parallelism: int = 16
+    jobName: str = "OML_job_1"
+    checkpointing: bool = False
+    local: bool = True
+    checkInterval: int = 5000
+    stateBackend: str = "file:///tmp/omldm_checkpoints"
+    trainingDataTopic: str = "trainingData"
+    trainingDataAddr: str = "localhost:9092"
+    forecastingDataTopic: str = "forecastingData"
+    forecastingDataAddr: str = "localhost:9092"
+    requestsTopic: str = "requests"
+    requestsAddr: str = "localhost:9092"
+    psMessagesTopic: str = "psMessages"
+    psMessagesAddr: str = "localhost:9092"
+    responsesTopic: str = "responses"
+    responsesAddr: str = "localhost:9092"
+    predictionsTopic: str = "predictions"
+    predictionsAddr: str = "localhost:9092"
+    performanceTopic: str = "performance"
+    performanceAddr: str = "localhost:9092"
+    test: bool = True
+    maxMsgParams: int = 2000
+    timeout: int = 30000
+    testSetSize: int = 256
+    # ---- reference constants made configurable
+    recordBufferSize: int = 100000        # SpokeLogic.scala:32
+    requestBufferSize: int = 10000        # SpokeLogic.scala:35
+    hubCacheSize: int = 20000             # StateAccumulators.scala:38
+    queryBucketSize: int = 10000          # FlinkNetwork.scala:50
+    heartbeatEvery: int = 100             # FlinkSpoke.scala:85
+    seed: int = 25                        # FlinkSpoke.scala:52
+    # ---- MI355X-native engine
+    numFeatures: int = 13                 # numerical features per point (dense slots)
+    discreteFeatures: int = 0             # discrete features per point (dense slots)
+    catFeatures: int = 26                 # categorical features per point (hashed)
+    hashDim: int = 1 << 20                # hashed feature space (incl. dense slots, intercept)
+    fieldAware: bool = False              # compact uint16 field-aware categorical slots
+    batchSize: int = 65536                # records per engine tick and rank
+    spokesPerDevice: int = 0              # virtual spokes per rank (0: parallelism / world)
+    device: str = "auto"                  # auto | cuda | cpu
+    maxTicks: int = 0                     # 0: until terminated (tests use a bound)
+    restore: bool = False                 # restore from the latest checkpoint in stateBackend
+    parseThreads: int = 8
+    extra: dict = field(default_factory=dict)
+
+    @staticmethod
+    def from_args(argv=None) -> "JobConfig":
+        """Flink ParameterTool style: ``--key value`` pairs; unknown keys land in ``extra``."""
+        argv = list(argv or [])
+        cfg = JobConfig()
+        names = {f.name: f for f in fields(JobConfig) if f.name != "extra"}
+        i = 0
+        while i < len(argv):
+            a = argv[i]
+            if not a.startswith("-"):
+                i += 1
+                continue
+            key = a.lstrip("-")
+            val = "true"
+            if "=" in key:
+                key, val = key.split("=", 1)
+            elif i + 1 < len(argv) and not argv[i + 1].startswith("--"):
+                val = argv[i + 1]
+                i += 1
+            i += 1
+            if key in names:
+                typ = names[key].type
+                if typ in ("bool", bool):
+                    setattr(cfg, key, _bool(val))
+                elif typ in ("int", int):
+                    setattr(cfg, key, int(float(val)))
+                else:
+                    setattr(cfg, key, val)
+            else:
+                cfg.extra[key] = val
+        return cfg
+
+    def as_dict(self) -> dict:
+        return asdict(self)
+
+
+def argparser() -> argparse.ArgumentParser:
+    """argparse mirror (for --help); parsing itself uses JobConfig.from_args."""
+    ap = argparse.ArgumentParser(prog="omldm", description="MI355X-native online ML engine")
+    for f in fields(JobConfig):
+        if f.name == "extra":
+            continue
+        ap.add_argument(f"--{f.name}", default=getattr(JobConfig, f.name, None))
+    return ap
