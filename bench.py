@@ -71,8 +71,8 @@ def main(argv=None) -> int:
     ap.add_argument("--dim-log2", type=int, default=20)
     ap.add_argument("--table-log2", type=int, default=11, help="LDS delta table (entries, log2)")
     ap.add_argument("--model-dtype", default="bf16", choices=["fp32", "bf16"])
-    ap.add_argument("--num-dtype", default="fp32", choices=["fp32", "bf16"])
-    ap.add_argument("--wire", default="wide", choices=["wide", "compact"],
+    ap.add_argument("--num-dtype", default="bf16", choices=["fp32", "bf16"])
+    ap.add_argument("--wire", default="compact", choices=["wide", "compact"],
                     help="compact: field-aware uint16 categorical slots (half the PCIe bytes)")
     ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")
     ap.add_argument("--ingest", default="pinned", choices=["pinned", "device"],
@@ -81,8 +81,9 @@ def main(argv=None) -> int:
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
     ap.add_argument("--ablate", type=int, default=0, help="kernel phase ablation (diagnostics)")
     ap.add_argument("--chunk", type=int, default=8, help="rows per kernel pipeline step")
-    ap.add_argument("--h2d", default="sdma", choices=["sdma", "pull", "raw"], help="H2D engine")
-    ap.add_argument("--pull-blocks", type=int, default=512)
+    ap.add_argument("--h2d", default="pull", choices=["sdma", "pull", "raw"],
+                    help="H2D engine: pull = GPU kernel reads the pinned batch over PCIe")
+    ap.add_argument("--pull-blocks", type=int, default=64)
     ap.add_argument("--ingest-cus", type=int, default=0,
                     help=">0: run the ingest stream on a CU-masked slice of this many CUs")
     a = ap.parse_args(argv)

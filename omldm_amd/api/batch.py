@@ -147,6 +147,16 @@ class HashedBatch:
         c = self.cat.long()
         return c & 0x7FFFFFFF, torch.where(c < 0, -1.0, 1.0), c != -1
 
+    def to_wide(self) -> "HashedBatch":
+        """Compact uint16 categorical form → int32 signed-slot form (no-op if wide)."""
+        if self.cat_span == 0:
+            return self
+        slot, sign, valid = self.cat_slots()
+        c = torch.where(sign < 0, slot | 0x80000000, slot)
+        c = torch.where(valid, c, torch.full_like(c, -1)).to(torch.int64)
+        c32 = ((c + 2**31) % 2**32 - 2**31).to(torch.int32)
+        return HashedBatch(self.num, c32.contiguous(), self.y, self.raw, 0)
+
     def dense(self, dim: int | None = None) -> torch.Tensor:
         """Materialise [B, dim] dense features (tests / small dense learners only)."""
         dim = dim or (self.dn + 1)

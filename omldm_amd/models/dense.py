@@ -1,0 +1,483 @@
+"""Dense-feature learners: ORR, K-means, NN (MLP) and HT (Hoeffding tree), plus the
+hashed MultiClassPA.
+
+Reference learner names: omldm/utils/parsers/requestStream/PipelineMap.scala:68; rules
+[lit] in SURVEY.md Appendix D. Dense learners consume the dense block of the micro-batch
+(numerical ∥ discrete features after the pipeline's preprocessors); hashed categorical
+slots feed the linear family and MultiClassPA.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.models.base import Learner, RoundContext, hp_float, hp_int
+from omldm_amd.ops import dense as D
+from omldm_amd.ops import linear as L
+
+
+def _in_dim(h: dict, space: FeatureSpace) -> int:
+    return int(h.get("_inDim", space.dn))
+
+
+# ---------------------------------------------------------------------------- ORR
+class ORR(Learner):
+    """Online ridge regression: A = λI + Σxxᵀ, b = Σyx, w = A⁻¹b (intercept included).
+    State = the augmented Gram matrix of [x, 1, y] — additive sufficient statistics, so
+    worker merges are sums (merge_mode "sum") and exact. The per-round update is one
+    MFMA pass (csrc/kernels/dense_learners.hip: gram_mfma_kernel); the solve is a
+    Cholesky factorisation of the (d+1)×(d+1) system, refreshed lazily."""
+
+    NAME = "ORR"
+    TASK = "regression"
+    merge_mode = "sum"
+
+    def __init__(self, hyper, space, device="cpu"):
+        super().__init__(hyper, space, device)
+        self.d = _in_dim(self.hyper, space)
+        self.ld = ((self.d + 2 + 31) // 32) * 32
+        self.G = torch.zeros((self.ld, self.ld), dtype=torch.float32, device=self.device)
+        self._w = None
+        self.lam = hp_float(self.hyper, "lambda", 1.0)
+
+    def fit(self, batch, ctx):
+        x = batch.num.float()
+        if batch.B:
+            D.gram_update(x, batch.y, self.G)
+            n = (~torch.isnan(batch.y)).sum()
+            self.cum[1] += n
+        self._w = None
+
+    def state_vector(self):
+        return self.G.view(-1)
+
+    def on_state_loaded(self):
+        self._w = None
+
+    def weights(self) -> torch.Tensor:
+        if self._w is None:
+            d = self.d
+            A = self.G[: d + 1, : d + 1].double()
+            A = A + self.lam * torch.eye(d + 1, dtype=A.dtype, device=A.device)
+            b = self.G[: d + 1, d + 1].double()
+            Lc, info = torch.linalg.cholesky_ex(A)
+            if int(info.item()) == 0:
+                self._w = torch.cholesky_solve(b.unsqueeze(1), Lc).squeeze(1).float()
+            else:
+                self._w = torch.linalg.lstsq(A, b.unsqueeze(1)).solution.squeeze(1).float()
+        return self._w
+
+    def predict(self, batch):
+        w = self.weights()
+        return batch.num.float() @ w[: self.d] + w[self.d]
+
+    def evaluate(self, batch):
+        ok = ~torch.isnan(batch.y)
+        e = (batch.y - self.predict(batch))[ok]
+        se = (e * e).sum()
+        return se, se, int(ok.sum())
+
+    def update_hyper(self, hyper):
+        super().update_hyper(hyper)
+        self.lam = hp_float(self.hyper, "lambda", self.lam)
+        self._w = None
+
+    def parameters_map(self):
+        w = self.weights().cpu()
+        return {"weights": w[: self.d].tolist(), "intercept": float(w[self.d]),
+                "fitted": float(self.G[self.d, self.d])}
+
+    def hyper_parameters(self):
+        return {**self.hyper, "lambda": self.lam}
+
+
+# ------------------------------------------------------------------------- K-means
+class KMeans(Learner):
+    """Online (sequential) k-means; a micro-batch moves each centroid by
+    c ← (n·c + Σx)/(n + m) — the sequential update c ← c + (x − c)/n with assignments
+    taken against the batch-start centroids. Runs in SingleLearner mode (the reference
+    forces it for K-means: omldm/operators/spoke/FlinkSpoke.scala:203-209)."""
+
+    NAME = "K-means"
+    TASK = "clustering"
+    merge_mode = "mean"
+
+    def __init__(self, hyper, space, device="cpu"):
+        super().__init__(hyper, space, device)
+        self.k = hp_int(self.hyper, "k", 8)
+        self.d = _in_dim(self.hyper, space)
+        self.state = torch.zeros(self.k * self.d + self.k, dtype=torch.float32, device=self.device)
+        self.C = self.state[: self.k * self.d].view(self.k, self.d)
+        self.n = self.state[self.k * self.d:]
+        self._sums = torch.zeros_like(self.C)
+        self._cnt = torch.zeros_like(self.n)
+        self._inert = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._seeded = 0
+
+    def fit(self, batch, ctx):
+        if batch.B == 0:
+            return
+        x = batch.num.float()
+        train = ~torch.isnan(batch.y)
+        if self._seeded < self.k:  # seed centroids with the first k training points
+            rows = x[train][: self.k - self._seeded]
+            m = rows.shape[0]
+            self.C[self._seeded:self._seeded + m] = rows
+            self.n[self._seeded:self._seeded + m] = 1.0
+            self._seeded += m
+        self._sums.zero_()
+        self._cnt.zero_()
+        D.kmeans_assign(x, batch.y, self.C, self._sums, self._cnt, self._inert)
+        tot = self.n + self._cnt
+        upd = tot > 0
+        newc = (self.C * self.n.unsqueeze(1) + self._sums) / torch.clamp(tot, min=1).unsqueeze(1)
+        self.C.copy_(torch.where(upd.unsqueeze(1), newc, self.C))
+        self.n.copy_(tot)
+        self.cum[1] += train.sum()
+        self.cum[0] += self._inert[0]
+        self._inert.zero_()
+
+    def state_vector(self):
+        return self.state
+
+    def predict(self, batch):
+        a = D.kmeans_assign(batch.num.float(), None, self.C, None, None, want_assign=True)
+        return a.float()
+
+    def evaluate(self, batch):
+        x = batch.num.float()
+        dist = torch.cdist(x, self.C) ** 2
+        inert = dist.min(1).values.sum()
+        return inert, inert, batch.B
+
+    def parameters_map(self):
+        return {"centroids": self.C.cpu().tolist(), "counts": self.n.cpu().tolist()}
+
+
+# ---------------------------------------------------------------------- MultiClassPA
+class MultiClassPA(Learner):
+    """K-prototype Passive-Aggressive classifier on hashed features (labels 0..K-1);
+    virtual spokes per round (csrc/kernels/multiclass_spoke.hip)."""
+
+    NAME = "MultiClassPA"
+    TASK = "classification"
+    merge_mode = "mean"
+
+    def __init__(self, hyper, space, device="cpu"):
+        super().__init__(hyper, space, device)
+        self.K = max(2, hp_int(self.hyper, "nClasses", 2))
+        self.dim = space.dim
+        self.W = torch.zeros((self.K, self.dim), dtype=torch.float32, device=self.device)
+        self.dacc = torch.zeros_like(self.W)
+        self.st = torch.zeros(8, dtype=torch.float32, device=self.device)
+        v = str(self.hyper.get("variant", "PA-I"))
+        self.variant = {"PA": 0, "PA-I": 1, "PA-II": 2}.get(v, 1)
+        self.C = hp_float(self.hyper, "C", 1.0)
+        self.bias = bool(self.hyper.get("bias", True))
+
+    def fit(self, batch, ctx):
+        if batch.B == 0:
+            return
+        batch = batch.to_wide()
+        S = max(1, ctx.spokes)
+        R = max(1, -(-batch.B // S))
+        self.st[3] = 0.0
+        D.multiclass_round(self.W, batch, R, S, self.K, self.variant, self.C, self.bias,
+                           self.dacc, self.st, log2cap=hp_int(self.hyper, "tableLog2", 11))
+        D.multiclass_apply(self.W, self.dacc, self.st[3:4])
+        self.cum[:3] += self.st[:3]
+        self.st[:3] = 0.0
+
+    def state_vector(self):
+        return self.W.view(-1)
+
+    def scores(self, batch):
+        return L.linear_predict(self.W, batch.to_wide(), bias=self.bias)
+
+    def predict(self, batch):
+        return self.scores(batch).argmax(1).float()
+
+    def evaluate(self, batch):
+        ok = ~torch.isnan(batch.y)
+        if batch.B == 0 or not bool(ok.any()):
+            z = torch.zeros((), device=self.device)
+            return z, z, 0
+        s = self.scores(batch)[ok]
+        y = batch.y[ok].long().clamp(0, self.K - 1)
+        sy = s.gather(1, y.unsqueeze(1)).squeeze(1)
+        s2 = s.clone()
+        s2.scatter_(1, y.unsqueeze(1), float("-inf"))
+        loss = torch.clamp(1 - (sy - s2.max(1).values), min=0).sum()
+        return loss, (s.argmax(1) == y).float().sum(), int(ok.sum())
+
+    def parameters_map(self):
+        return {"nClasses": self.K, "nonZero": int((self.W != 0).sum())}
+
+
+# ------------------------------------------------------------------------------ NN
+class NN(Learner):
+    """Multi-layer perceptron trained by mini-batch SGD (the reference's DL4J
+    MultiLayerNetwork path, hs_err_pid77107.log:97-110). Parameters live in ONE flat
+    fp32 buffer (layer weights are views), which is the protocols' state vector."""
+
+    NAME = "NN"
+    merge_mode = "mean"
+
+    def __init__(self, hyper, space, device="cpu"):
+        super().__init__(hyper, space, device)
+        h = self.hyper
+        self.d = _in_dim(h, space)
+        hidden = h.get("hiddenLayers", [32, 32])
+        if isinstance(hidden, str):
+            hidden = [int(v) for v in hidden.strip("[]").split(",") if v.strip()]
+        self.K = hp_int(h, "nClasses", 1)   # 1: binary (±1 or {0,1}) / regression output
+        self.TASK = "regression" if str(h.get("task", "classification")) == "regression" \
+            else "classification"
+        self.lr = hp_float(h, "learningRate", 0.05)
+        self.mb = hp_int(h, "miniBatchSize", 256)
+        sizes = [self.d] + [int(v) for v in hidden] + [max(1, self.K)]
+        shapes = []
+        for a, b in zip(sizes[:-1], sizes[1:]):
+            shapes += [(b, a), (b,)]
+        total = sum(math.prod(s) for s in shapes)
+        g = torch.Generator().manual_seed(hp_int(h, "seed", 25))
+        flat = torch.zeros(total, dtype=torch.float32)
+        o = 0
+        for s in shapes:
+            n = math.prod(s)
+            if len(s) == 2:
+                flat[o:o + n] = torch.randn(n, generator=g) * math.sqrt(2.0 / s[1])
+            o += n
+        self.flat = flat.to(self.device).requires_grad_(True)
+        self.shapes = shapes
+
+    def _layers(self):
+        o = 0
+        out = []
+        for s in self.shapes:
+            n = math.prod(s)
+            out.append(self.flat[o:o + n].view(s))
+            o += n
+        return out
+
+    def forward(self, x):
+        ps = self._layers()
+        h = x
+        for i in range(0, len(ps), 2):
+            h = torch.nn.functional.linear(h, ps[i], ps[i + 1])
+            if i + 2 < len(ps):
+                h = torch.relu(h)
+        return h
+
+    def _loss(self, out, y):
+        if self.TASK == "regression":
+            return torch.nn.functional.mse_loss(out.squeeze(1), y, reduction="sum")
+        if self.K <= 1:
+            t = (y > 0).float()
+            return torch.nn.functional.binary_cross_entropy_with_logits(out.squeeze(1), t,
+                                                                        reduction="sum")
+        return torch.nn.functional.cross_entropy(out, y.long(), reduction="sum")
+
+    def fit(self, batch, ctx):
+        ok = ~torch.isnan(batch.y)
+        x = batch.num.float()[ok]
+        y = batch.y[ok]
+        n = x.shape[0]
+        tot = torch.zeros((), device=self.device)
+        for a in range(0, n, self.mb):
+            xb, yb = x[a:a + self.mb], y[a:a + self.mb]
+            loss = self._loss(self.forward(xb), yb)
+            g, = torch.autograd.grad(loss, self.flat)
+            with torch.no_grad():
+                self.flat.sub_(g, alpha=self.lr / xb.shape[0])
+            tot = tot + loss.detach()
+        self.cum[0] += tot
+        self.cum[1] += n
+
+    def state_vector(self):
+        return self.flat.data
+
+    def predict(self, batch):
+        with torch.no_grad():
+            out = self.forward(batch.num.float())
+        if self.TASK == "regression":
+            return out.squeeze(1)
+        if self.K <= 1:
+            return torch.where(out.squeeze(1) >= 0, 1.0, -1.0)
+        return out.argmax(1).float()
+
+    def evaluate(self, batch):
+        ok = ~torch.isnan(batch.y)
+        if not bool(ok.any()):
+            z = torch.zeros((), device=self.device)
+            return z, z, 0
+        with torch.no_grad():
+            out = self.forward(batch.num.float()[ok])
+            y = batch.y[ok]
+            loss = self._loss(out, y)
+            if self.TASK == "regression":
+                score = ((out.squeeze(1) - y) ** 2).sum()
+            elif self.K <= 1:
+                score = ((out.squeeze(1) >= 0) == (y > 0)).float().sum()
+            else:
+                score = (out.argmax(1) == y.long()).float().sum()
+        return loss, score, int(ok.sum())
+
+    def parameters_map(self):
+        return {"layers": [list(s) for s in self.shapes], "nParams": int(self.flat.numel())}
+
+
+# ------------------------------------------------------------------------------ HT
+class HT(Learner):
+    """Hoeffding tree (VFDT) for classification on dense features.
+
+    Leaves keep class counts and per-(feature, class) Gaussian sufficient statistics
+    (n, Σx, Σx²); every ``gracePeriod`` points a leaf evaluates ``nBins`` candidate
+    thresholds per feature (class mass split by the Gaussian CDFs), and splits when the
+    information-gain lead of the best attribute beats the Hoeffding bound
+    ε = sqrt(R² ln(1/δ) / (2n)) or ε < τ (tie). Routing, statistics and split search
+    are batched tensor ops on the device; the tree is flat arrays (state vector)."""
+
+    NAME = "HT"
+    merge_mode = "mean"
+
+    def __init__(self, hyper, space, device="cpu"):
+        super().__init__(hyper, space, device)
+        h = self.hyper
+        self.d = _in_dim(h, space)
+        self.Cn = max(2, hp_int(h, "nClasses", 2))
+        self.N = hp_int(h, "maxNodes", 255)
+        self.depth = hp_int(h, "maxDepth", 12)
+        self.grace = hp_int(h, "gracePeriod", 200)
+        self.delta = hp_float(h, "delta", 1e-7)
+        self.tau = hp_float(h, "tau", 0.05)
+        self.nb = hp_int(h, "nBins", 16)
+        dev = self.device
+        N, d, C = self.N, self.d, self.Cn
+        # flat state: feature, threshold, left, right, class counts, S0, S1, S2, lo, hi, since
+        self.sizes = [N, N, N, N, N * C, N * d * C, N * d * C, N * d * C, N * d, N * d, N, 1]
+        self.state = torch.zeros(sum(self.sizes), dtype=torch.float32, device=dev)
+        v = torch.split(self.state, self.sizes)
+        self.feat, self.thr, self.left, self.right = v[0], v[1], v[2], v[3]
+        self.cc = v[4].view(N, C)
+        self.S0, self.S1, self.S2 = (t.view(N, d, C) for t in v[5:8])
+        self.lo, self.hi = v[8].view(N, d), v[9].view(N, d)
+        self.since = v[10]
+        self.nnodes = v[11]
+        self.feat.fill_(-1)
+        self.lo.fill_(float("inf"))
+        self.hi.fill_(float("-inf"))
+        self.nnodes.fill_(1)
+
+    def _route(self, x):
+        node = torch.zeros(x.shape[0], dtype=torch.long, device=x.device)
+        for _ in range(self.depth + 1):
+            f = self.feat[node].long()
+            inner = f >= 0
+            if not bool(inner.any()):
+                break
+            xv = x.gather(1, f.clamp(min=0).unsqueeze(1)).squeeze(1)
+            go_left = xv <= self.thr[node]
+            nxt = torch.where(go_left, self.left[node], self.right[node]).long()
+            node = torch.where(inner, nxt, node)
+        return node
+
+    def fit(self, batch, ctx):
+        ok = ~torch.isnan(batch.y)
+        if not bool(ok.any()):
+            return
+        x = batch.num.float()[ok]
+        y = batch.y[ok].long().clamp(0, self.Cn - 1)
+        y = torch.where(y < 0, 0, y)
+        leaf = self._route(x)
+        N, d, C = self.N, self.d, self.Cn
+        self.cc.view(-1).index_add_(0, leaf * C + y, torch.ones_like(y, dtype=torch.float32))
+        idx = ((leaf * d).unsqueeze(1) + torch.arange(d, device=x.device)) * C + y.unsqueeze(1)
+        self.S0.view(-1).index_add_(0, idx.reshape(-1), torch.ones(idx.numel(), device=x.device))
+        self.S1.view(-1).index_add_(0, idx.reshape(-1), x.reshape(-1))
+        self.S2.view(-1).index_add_(0, idx.reshape(-1), (x * x).reshape(-1))
+        li = (leaf * d).unsqueeze(1) + torch.arange(d, device=x.device)
+        self.lo.view(-1).scatter_reduce_(0, li.reshape(-1), x.reshape(-1), "amin")
+        self.hi.view(-1).scatter_reduce_(0, li.reshape(-1), x.reshape(-1), "amax")
+        self.since.index_add_(0, leaf, torch.ones(leaf.shape[0], device=x.device))
+        self.cum[1] += x.shape[0]
+        self._try_split()
+
+    @staticmethod
+    def _entropy(counts):
+        tot = counts.sum(-1, keepdim=True).clamp(min=1e-12)
+        p = counts / tot
+        return -(p * torch.log2(p.clamp(min=1e-12))).sum(-1)
+
+    def _try_split(self):
+        cand = torch.nonzero((self.since >= self.grace) & (self.feat < 0)).flatten()
+        if cand.numel() == 0:
+            return
+        for node in cand.tolist():
+            n_total = float(self.cc[node].sum())
+            self.since[node] = 0
+            if n_total < 2 or int(self.nnodes.item()) + 2 > self.N:
+                continue
+            cc = self.cc[node]
+            if int((cc > 0).sum()) < 2:
+                continue
+            S0, S1, S2 = self.S0[node], self.S1[node], self.S2[node]  # [d, C]
+            mu = S1 / S0.clamp(min=1)
+            var = (S2 / S0.clamp(min=1) - mu * mu).clamp(min=1e-6)
+            sd = var.sqrt()
+            lo, hi = self.lo[node], self.hi[node]
+            span = (hi - lo).clamp(min=0)
+            q = torch.linspace(0, 1, self.nb + 2, device=S0.device)[1:-1]
+            t = lo.unsqueeze(1) + span.unsqueeze(1) * q.unsqueeze(0)      # [d, nb]
+            z = (t.unsqueeze(2) - mu.unsqueeze(1)) / sd.unsqueeze(1)      # [d, nb, C]
+            cdf = 0.5 * (1 + torch.erf(z / math.sqrt(2)))
+            left = S0.unsqueeze(1) * cdf                                  # [d, nb, C]
+            right = S0.unsqueeze(1) - left
+            nl, nr = left.sum(-1), right.sum(-1)
+            h0 = self._entropy(cc)
+            gain = h0 - (nl * self._entropy(left) + nr * self._entropy(right)) / \
+                (nl + nr).clamp(min=1e-12)
+            gain = torch.where(span.unsqueeze(1) > 0, gain, torch.full_like(gain, -1))
+            per_feat, arg = gain.max(1)
+            order = torch.argsort(per_feat, descending=True)
+            g1 = float(per_feat[order[0]])
+            g2 = float(per_feat[order[1]]) if self.d > 1 else 0.0
+            R = math.log2(self.Cn)
+            eps = math.sqrt(R * R * math.log(1.0 / self.delta) / (2.0 * n_total))
+            if g1 > 0 and (g1 - g2 > eps or eps < self.tau):
+                f = int(order[0])
+                thr = float(t[f, arg[f]])
+                nn = int(self.nnodes.item())
+                lch, rch = nn, nn + 1
+                self.nnodes += 2
+                self.feat[node] = f
+                self.thr[node] = thr
+                self.left[node], self.right[node] = lch, rch
+                # children start with the class mass estimated on each side
+                self.cc[lch] = left[f, arg[f]]
+                self.cc[rch] = right[f, arg[f]]
+
+    def state_vector(self):
+        return self.state
+
+    def predict(self, batch):
+        leaf = self._route(batch.num.float())
+        return self.cc[leaf].argmax(1).float()
+
+    def evaluate(self, batch):
+        ok = ~torch.isnan(batch.y)
+        if not bool(ok.any()):
+            z = torch.zeros((), device=self.device)
+            return z, z, 0
+        p = self.predict(batch)[ok]
+        y = batch.y[ok]
+        err = (p != y).float().sum()
+        return err, (p == y).float().sum(), int(ok.sum())
+
+    def parameters_map(self):
+        n = int(self.nnodes.item())
+        return {"nodes": n, "feature": self.feat[:n].int().tolist(),
+                "threshold": self.thr[:n].tolist(), "left": self.left[:n].int().tolist(),
+                "right": self.right[:n].int().tolist(), "classCounts": self.cc[:n].tolist()}
