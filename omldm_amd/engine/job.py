@@ -1,0 +1,262 @@
+"""The per-rank streaming job: control plane, data plane, queries, statistics, termination.
+
+Reference dataflow (omldm/Job.scala:35-168, omldm/job/FlinkLearning.scala:33-152):
+requests → PipelineMap (p=1) → broadcast to every spoke; training ∪ forecasting data →
+FlinkSpoke (holdout routing, per-pipeline learning, predictions, query answers) ↔ FlinkHub
+(parameter server, statistics) with the hub→spoke leg through the Kafka psMessages
+topic; ResponseConstructor reduces query answers; StatisticsOperator detects idleness
+and emits JobStatistics to the performance topic, which kills the job.
+
+MI355X-native redesign. One process per GPU; every process runs this loop in lockstep
+("tick" = one micro-batch per rank):
+  1. rank 0 drains the requests topic through PipelineMap; the resulting control
+     messages are broadcast to all ranks (one small object broadcast per tick);
+  2. each rank polls its partitions of trainingData/forecastingData, parses them with
+     the C++ scanner into one HashedBatch, and moves it to HBM;
+  3. forecasting rows → every pipeline's predict kernel → predictions topic;
+  4. training rows → holdout routing → every pipeline's protocol round (the parameter
+     server is an RCCL collective inside the round, not a Kafka loop);
+  5. Query requests are answered from the holdout set with one all-reduce
+     (ResponseConstructor semantics) and written by rank 0 to the responses topic;
+  6. a 2-float all-reduce per tick carries global activity and the termination flag
+     (idle timeout → final statistics → performance topic → graceful stop);
+  7. optional asynchronous checkpoint every ``checkInterval`` ms.
+"""
+from __future__ import annotations
+
+import json
+import time
+
+import numpy as np
+import torch
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.api.schemas import Prediction, Request
+from omldm_amd.engine.holdout import HoldoutSet
+from omldm_amd.engine.pipeline import Pipeline
+from omldm_amd.engine.pipeline_map import ALL, PipelineMap
+from omldm_amd.engine import statistics as ST
+from omldm_amd.io.parse import OP_FORECASTING, OP_TRAINING, parse_records
+from omldm_amd.io.transport import Consumer, broker_for
+from omldm_amd.parallel.comm import Comm
+from omldm_amd.utils.config import JobConfig
+from omldm_amd.utils import tracing
+
+
+class Job:
+    def __init__(self, cfg: JobConfig, comm: Comm, device):
+        self.cfg = cfg
+        self.comm = comm
+        self.device = torch.device(device)
+        self.rank, self.world = comm.rank, comm.world
+        self.space = FeatureSpace(cfg.numFeatures, cfg.discreteFeatures, cfg.catFeatures,
+                                  cfg.hashDim, field_aware=cfg.fieldAware)
+        self.spokes = cfg.spokesPerDevice or max(1, cfg.parallelism // self.world)
+        b = {k: broker_for(getattr(cfg, k + "Addr")) for k in
+             ("trainingData", "forecastingData", "requests", "responses", "predictions",
+              "performance")}
+        self.brokers = b
+        self.train_in = Consumer(b["trainingData"], cfg.trainingDataTopic, self.rank, self.world)
+        self.fcst_in = Consumer(b["forecastingData"], cfg.forecastingDataTopic, self.rank,
+                                self.world)
+        self.req_in = Consumer(b["requests"], cfg.requestsTopic, all_partitions=True) \
+            if self.rank == 0 else None
+        self.pmap = PipelineMap() if self.rank == 0 else None
+        self.pipes: dict[int, Pipeline] = {}
+        self.holdout = HoldoutSet(self.space, cfg.testSetSize, self.device)
+        self.record_buffer: list[bytes] = []
+        self.idle = ST.IdleDetector(cfg.timeout)
+        self.ticks = 0
+        self.terminated = False
+        self.final_stats = None
+        self.counters = {"records": 0, "invalid": 0, "predictions": 0, "responses": 0,
+                         "dropped_buffer": 0}
+        self._flags = torch.zeros(3, dtype=torch.float32, device=self._coll_device())
+        self.checkpointer = None
+        if cfg.checkpointing or cfg.restore:
+            from omldm_amd.utils.checkpoint import Checkpointer
+
+            self.checkpointer = Checkpointer(cfg, self.rank, self.world)
+            if cfg.restore:
+                self.checkpointer.restore(self)
+
+    def _coll_device(self):
+        return self.device if self.comm.backend == "nccl" else torch.device("cpu")
+
+    # ------------------------------------------------------------------ control
+    def _control(self):
+        msgs = []
+        if self.rank == 0:
+            for rec in self.req_in.poll(self.cfg.requestBufferSize):
+                for m in self.pmap.process(rec):
+                    msgs.append((m.network_id, m.destination, m.request.to_obj()))
+        if self.world > 1:
+            msgs = self.comm.broadcast_object(msgs, src=0)
+        queries = []
+        for net, dest, robj in msgs:
+            req = Request.from_json(robj)
+            if dest not in (ALL, self.rank) and req.request != "Query":
+                continue
+            if req.request == "Create":
+                if net not in self.pipes:
+                    self.pipes[net] = Pipeline(req, self.space, self.comm, self.device,
+                                               self.spokes, self.cfg.parallelism,
+                                               self.cfg.maxMsgParams)
+            elif req.request == "Update" and net in self.pipes:
+                self.pipes[net].update(req)
+            elif req.request == "Delete":
+                self.pipes.pop(net, None)
+            elif req.request == "Query" and net in self.pipes:
+                queries.append(req)
+        return len(msgs), queries
+
+    # --------------------------------------------------------------------- data
+    def _poll(self) -> list[bytes]:
+        n = self.cfg.batchSize
+        recs = self.train_in.poll(n) + self.fcst_in.poll(n)
+        if not self.pipes:
+            # reference: points wait in a bounded record buffer until a pipeline exists
+            room = self.cfg.recordBufferSize - len(self.record_buffer)
+            if len(recs) > room:
+                self.counters["dropped_buffer"] += len(recs) - max(room, 0)
+                recs = recs[:max(room, 0)]
+            self.record_buffer.extend(recs)
+            return []
+        if self.record_buffer:
+            recs = self.record_buffer + recs
+            self.record_buffer = []
+        return recs
+
+    def _forecast(self, batch: HashedBatch):
+        prod = self.brokers["predictions"]
+        for pid in sorted(self.pipes):
+            with tracing.range(f"predict:{pid}"):
+                preds = self.pipes[pid].predict(batch).float().cpu().tolist()
+            for raw, p in zip(batch.raw or [None] * batch.B, preds):
+                prod.produce(self.cfg.predictionsTopic, Prediction(pid, raw, p).to_json())
+            self.counters["predictions"] += len(preds)
+
+    def _train(self, batch: HashedBatch):
+        routed = self.holdout.route(batch)
+        for pid in sorted(self.pipes):
+            with tracing.range(f"round:{pid}"):
+                self.pipes[pid].train(routed)
+
+    # ------------------------------------------------------------------- queries
+    def _answer(self, req: Request, response_id=None, write=True) -> dict:
+        pipe = self.pipes[req.id]
+        pipe.protocol.finalize()
+        test = self.holdout.test_set()
+        loss, score, n = pipe.evaluate(test) if test.B else (0.0, 0.0, 0)
+        tot = pipe.learner.running_totals()
+        m = ST.reduce_query_metrics(self.comm, float(loss), float(score), int(n), tot["fitted"],
+                                    tot["loss_sum"])
+        if pipe.learner.TASK == "regression":
+            m["score"] = float(np.sqrt(max(m["score"], 0.0)))  # mean squared error → RMSE
+        if self.rank == 0 and write:
+            learner = {"name": pipe.learner.NAME,
+                       "hyperParameters": pipe.learner.hyper_parameters(),
+                       "parameters": pipe.learner.parameters_map(),
+                       "dataStructure": pipe.learner.data_structure()}
+            pre = [p.to_obj() for p in pipe.preprocessors]
+            rid = req.requestId if response_id is None else response_id
+            for qr in ST.build_query_responses(int(rid if rid is not None else -1), pipe.id, pre,
+                                               learner, pipe.protocol_name, m,
+                                               self.cfg.queryBucketSize):
+                self.brokers["responses"].produce(self.cfg.responsesTopic, qr.to_json())
+                self.counters["responses"] += 1
+        return m
+
+    # --------------------------------------------------------------------- tick
+    def tick(self) -> None:
+        t0 = time.time()
+        n_ctrl, queries = self._control()
+        recs = self._poll()
+        n_local = len(recs)
+        if recs:
+            with tracing.range("parse"):
+                batch, op, nvalid = parse_records(recs, self.space, self.cfg.parseThreads)
+            self.counters["records"] += nvalid
+            self.counters["invalid"] += len(recs) - nvalid
+            opt = torch.from_numpy(op)
+            fidx = torch.nonzero(opt == OP_FORECASTING).flatten()
+            tidx = torch.nonzero(opt == OP_TRAINING).flatten()
+            if fidx.numel():
+                self._forecast(batch.select(fidx).to(self.device))
+            tb = batch.select(tidx).to(self.device, non_blocking=True)
+        else:
+            tb = HashedBatch.empty(self.space, 0, device=self.device)
+        # global activity + termination flag (one tiny all-reduce per tick); every rank
+        # then takes the same decisions, so the pipelines' collectives stay aligned
+        self._flags[0] = float(n_local + n_ctrl)
+        self._flags[1] = 0.0
+        if self.rank == 0 and self.cfg.test and self.idle.expired(t0) and self.pipes:
+            self._flags[1] = 1.0
+        self._flags[2] = float(tb.B)
+        self.comm.all_reduce_(self._flags, tag="heartbeat")
+        active, term, n_train = (float(v) for v in self._flags.tolist())
+        if self.pipes and n_train > 0:
+            self._train(tb)
+        for q in queries:
+            self._answer(q)
+        for pipe in self.pipes.values():
+            pipe.record_learning_curve()
+        if active > 0:
+            self.idle.activity(t0)
+        if term > 0:
+            self._terminate()
+        if self.checkpointer is not None and self.checkpointer.due():
+            self.checkpointer.save(self)
+        self.ticks += 1
+        if active == 0 and not self.terminated:
+            time.sleep(0.001)
+
+    def _terminate(self):
+        """Final −1 query of every pipeline + JobStatistics (reference §3.7), graceful."""
+        stats = []
+        for pid in sorted(self.pipes):
+            pipe = self.pipes[pid]
+            m = self._answer(Request(id=pid, request="Query", requestId=-1), write=False)
+            stats.append(ST.pipeline_statistics(pipe, m))
+        js = ST.job_statistics(self.cfg.jobName, self.world, self.idle.duration_ms(), stats)
+        self.final_stats = js
+        if self.rank == 0:
+            self.brokers["performance"].produce(self.cfg.performanceTopic, js.to_json())
+        self.terminated = True
+
+    def run(self) -> "Job":
+        while not self.terminated and (self.cfg.maxTicks <= 0 or self.ticks < self.cfg.maxTicks):
+            self.tick()
+        for p in self.pipes.values():
+            p.protocol.finalize()
+        return self
+
+    # --------------------------------------------------------------- checkpoint
+    def state_dict(self) -> dict:
+        sd = {"pipelines": {pid: p.state_dict() for pid, p in self.pipes.items()},
+              "holdout": self.holdout.state_dict(),
+              "consumers": {"train": self.train_in.state_dict(),
+                            "forecast": self.fcst_in.state_dict()},
+              "record_buffer": list(self.record_buffer), "ticks": self.ticks,
+              "counters": dict(self.counters), "world": self.world}
+        if self.rank == 0:
+            sd["pipeline_map"] = self.pmap.state_dict()
+            sd["requests"] = self.req_in.state_dict()
+        return sd
+
+    def load_state_dict(self, sd: dict, same_world: bool = True) -> None:
+        for pid, psd in sd.get("pipelines", {}).items():
+            req = Request.from_json(psd["request"])
+            pipe = Pipeline(req, self.space, self.comm, self.device, self.spokes,
+                            self.cfg.parallelism, self.cfg.maxMsgParams)
+            pipe.load_state_dict(psd)
+            self.pipes[int(pid)] = pipe
+        self.holdout.load_state_dict(sd["holdout"])
+        if same_world:  # partition ownership only matches at the same world size
+            self.train_in.load_state_dict(sd["consumers"]["train"])
+            self.fcst_in.load_state_dict(sd["consumers"]["forecast"])
+        self.record_buffer = list(sd.get("record_buffer", []))
+        self.ticks = int(sd.get("ticks", 0))
+        if self.rank == 0 and "pipeline_map" in sd:
+            self.pmap.load_state_dict(sd["pipeline_map"])
+            self.req_in.load_state_dict(sd.get("requests", {}))

@@ -1,0 +1,103 @@
+"""One ML pipeline (= one reference ``networkId``): preprocessors → learner, driven by a
+synchronisation protocol, plus its statistics.
+
+Reference: a pipeline is created by a Create request (FlinkSpoke.createWrapper,
+omldm/operators/spoke/FlinkSpoke.scala:177-224): parallel jobs force SingleLearner for
+HT / K-means (:203-209), a single-worker job forces CentralizedTraining (:213-215), and
+the protocol/hub parallelism come from ``trainingConfiguration`` (:181-190; factory
+omldm/utils/generators/MLNodeGenerator.scala:20-76). Points are piped through the
+preprocessors into the learner (MLPipeline.pipePoint, hs_err_pid77107.log:111).
+"""
+from __future__ import annotations
+
+import torch
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.api.schemas import SINGLE_LEARNER_MODELS, Request
+from omldm_amd.models import make_learner, make_preprocessor
+from omldm_amd.parallel.comm import Comm
+from omldm_amd.parallel.protocols import make_protocol
+
+
+class Pipeline:
+    def __init__(self, request: Request, space: FeatureSpace, comm: Comm, device,
+                 spokes: int, parallelism: int, max_msg_params: int = 10000):
+        self.id = int(request.id)
+        self.request = request
+        self.space = space
+        self.device = device
+        cfg = dict(request.trainingConfiguration or {})
+        name = request.learner.name
+        # Preprocessors first: they fix the learner's dense input width.
+        self.preprocessors = [make_preprocessor(p.name, p.hyperParameters, device)
+                              for p in (request.preProcessors or [])]
+        d = space.dn
+        for p in self.preprocessors:
+            d = p.out_dim(d)
+        hyper = dict(request.learner.hyperParameters or {})
+        hyper["_inDim"] = d
+        # A widened dense block (PolynomialFeatures) keeps slots [0, d) for the hashed
+        # learners; its top overlaps the lowest hashed slots like any hash collision.
+        if d + 1 >= space.dim:
+            raise ValueError("dense block wider than the hashed feature space")
+        self.learner = make_learner(name, hyper, space, device)
+        # Protocol selection rules of the reference.
+        if parallelism <= 1 and comm.world == 1:
+            proto = "CentralizedTraining"
+        elif name in SINGLE_LEARNER_MODELS and comm.world > 1:
+            proto = "SingleLearner"
+        else:
+            proto = cfg.get("protocol")
+        if name in SINGLE_LEARNER_MODELS and comm.world == 1 and proto != "CentralizedTraining":
+            cfg.setdefault("virtualSpokes", 1)
+        self.protocol = make_protocol(proto, comm, self.learner, cfg, spokes=spokes,
+                                      max_msg_params=max_msg_params)
+        self.protocol_name = self.protocol.NAME
+        # running statistics (reference Statistics / learning curve, FlinkHub.scala:95-156)
+        self.learning_curve: list[tuple[float, int]] = []
+        self._lc_last = (0.0, 0)
+
+    # --------------------------------------------------------------- data path
+    def _pre(self, batch: HashedBatch, train: bool) -> HashedBatch:
+        for p in self.preprocessors:
+            batch = p(batch, train=train)
+        return batch
+
+    def train(self, batch: HashedBatch) -> None:
+        """One protocol round on this rank's training rows (possibly empty)."""
+        self.protocol.round(self._pre(batch, True))
+
+    def predict(self, batch: HashedBatch) -> torch.Tensor:
+        return self.learner.predict(self._pre(batch, False))
+
+    def evaluate(self, batch: HashedBatch):
+        return self.learner.evaluate(self._pre(batch, False))
+
+    def record_learning_curve(self) -> None:
+        tot = self.learner.running_totals()
+        loss, n = tot["loss_sum"], tot["fitted"]
+        dl, dn = loss - self._lc_last[0], n - self._lc_last[1]
+        if dn > 0:
+            self.learning_curve.append((dl / dn, n))
+            self._lc_last = (loss, n)
+
+    def update(self, request: Request) -> None:
+        """Reference Update is a no-op (FlinkSpoke.scala:158); here it updates the
+        learner's hyper-parameters (documented extension)."""
+        if request.learner is not None and request.learner.hyperParameters:
+            self.learner.update_hyper(request.learner.hyperParameters)
+
+    # --------------------------------------------------------------- checkpoint
+    def state_dict(self) -> dict:
+        self.protocol.finalize()
+        return {"request": self.request.to_obj(), "learner": self.learner.state_dict(),
+                "preprocessors": [p.state_dict() for p in self.preprocessors],
+                "protocol": self.protocol.state_dict(),
+                "learning_curve": list(self.learning_curve)}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.learner.load_state_dict(sd["learner"])
+        for p, s in zip(self.preprocessors, sd.get("preprocessors", [])):
+            p.load_state_dict(s)
+        self.protocol.load_state_dict(sd.get("protocol", {}))
+        self.learning_curve = [tuple(x) for x in sd.get("learning_curve", [])]

@@ -1,0 +1,110 @@
+"""Contract layer: schemas, PipelineMap routing rules, response bucketing, transports,
+config flags (reference behaviours cited in each module)."""
+import json
+
+import pytest
+
+from omldm_amd.api.schemas import JobStatistics, QueryResponse, Request, Statistics
+from omldm_amd.engine.pipeline_map import ALL, PipelineMap
+from omldm_amd.engine.statistics import build_query_responses, split_params
+from omldm_amd.io.transport import (Consumer, FileBroker, MemoryBroker, hub_message_partition,
+                                    identity_partition)
+from omldm_amd.utils.config import JobConfig
+
+
+def req(**kw):
+    base = {"id": 1, "request": "Create", "learner": {"name": "PA"}}
+    base.update(kw)
+    return json.dumps(base)
+
+
+def test_request_parse_and_validate():
+    r = Request.from_json(req(requestId=5, preProcessors=[{"name": "StandardScaler"}],
+                              trainingConfiguration={"protocol": "FGM", "HubParallelism": 2}))
+    assert r.is_valid() and r.requestId == 5 and r.preProcessors[0].name == "StandardScaler"
+    assert Request.from_json(r.to_json()).to_obj() == r.to_obj()
+    assert not Request.from_json(json.dumps({"id": 1, "request": "Create"})).is_valid()
+    assert not Request.from_json(json.dumps({"id": -1, "request": "Query"})).is_valid()
+    assert not Request.from_json(json.dumps({"id": 1, "request": "Bogus"})).is_valid()
+
+
+def test_pipeline_map_rules():
+    pm = PipelineMap()
+    assert [m.destination for m in pm.process(req())] == [ALL]
+    assert pm.process(req()) == []                       # duplicate Create dropped
+    assert pm.process(req(id=2, learner={"name": "Nope"})) == []  # invalid learner
+    assert pm.process(req(id=3, preProcessors=[{"name": "PCA"}])) == []
+    assert pm.process("{not json") == [] and pm.dropped == 4
+    assert pm.process(json.dumps({"id": 9, "request": "Query"})) == []  # unknown id
+    pm.process(req(id=4, learner={"name": "HT"}))
+    assert [m.destination for m in pm.process(json.dumps({"id": 4, "request": "Query",
+                                                          "requestId": 1}))] == [0]
+    assert [m.destination for m in pm.process(json.dumps({"id": 1, "request": "Query",
+                                                          "requestId": 1}))] == [ALL]
+    assert len(pm.process(json.dumps({"id": 1, "request": "Update"}))) == 1
+    assert len(pm.process(json.dumps({"id": 1, "request": "Delete"}))) == 1
+    assert 1 not in pm.node_map
+    sd = pm.state_dict()
+    pm2 = PipelineMap()
+    pm2.load_state_dict(sd)
+    assert set(pm2.node_map) == set(pm.node_map)
+
+
+def test_split_params_reference_buckets():
+    b = split_params({"w": list(range(25000)), "b": 3.0}, 10000)
+    assert len(b) == 3
+    assert list(b[0]) == ["w[0-9999]", "b"] and list(b[2]) == ["w[20000-24999]"]
+    assert b[2]["w[20000-24999]"][-1] == 24999
+
+
+def test_query_responses_bucketed_last_carries_stats():
+    m = {"dataFitted": 10, "loss": 0.5, "cumulativeLoss": 0.4, "score": 0.9}
+    learner = {"name": "PA", "parameters": {"weights": [0.0] * 25000}}
+    qs = build_query_responses(7, 1, [], learner, "Synchronous", m, 10000)
+    assert [q.id for q in qs] == [0, 1, 2]
+    assert qs[0].score is None and qs[-1].score == 0.9 and qs[-1].protocol == "Synchronous"
+    one = build_query_responses(7, 1, [], {"name": "PA", "parameters": {"w": [1, 2]}},
+                                "Sync", m, 10000)
+    assert len(one) == 1 and one[0].dataFitted == 10
+    assert QueryResponse.from_json(one[0].to_json()).score == 0.9
+
+
+def test_job_statistics_json():
+    js = JobStatistics("j", 2, 100, [Statistics(2, "FGM"), Statistics(1, "Synchronous")])
+    o = json.loads(js.to_json())
+    assert o["parallelism"] == 2 and o["statistics"][0]["protocol"] == "FGM"
+
+
+def test_memory_and_file_brokers(tmp_path):
+    for br in (MemoryBroker(), FileBroker(str(tmp_path))):
+        br.create_topic("t", 4)
+        for i in range(40):
+            br.produce("t", json.dumps({"i": i}))
+        c0 = Consumer(br, "t", rank=0, world=2)
+        c1 = Consumer(br, "t", rank=1, world=2)
+        assert c0.parts == [0, 2] and c1.parts == [1, 3]
+        got = c0.poll(100) + c1.poll(100)
+        assert sorted(json.loads(x)["i"] for x in got) == list(range(40))
+        assert c0.poll(100) == []
+        late = Consumer(br, "t", start="latest", all_partitions=True)
+        br.produce("t", "x", partition=1)
+        assert late.poll(10) == [b"x"]
+
+
+def test_partitioners():
+    assert hub_message_partition(5, None, 4, terminate=True) == 0
+    assert hub_message_partition(5, 6, 4) == 2
+    assert hub_message_partition(5, None, 4) == 1
+    assert identity_partition(3, 4) == 3
+    with pytest.raises(ValueError):
+        identity_partition(4, 4)
+
+
+def test_config_reference_defaults_and_flags():
+    c = JobConfig.from_args([])
+    assert (c.parallelism, c.jobName, c.maxMsgParams, c.timeout, c.testSetSize, c.test) == \
+        (16, "OML_job_1", 2000, 30000, 256, True)
+    c = JobConfig.from_args(["--parallelism", "8", "--test", "false", "--jobName=x",
+                             "--psMessagesTopic", "ignored", "--fooBar", "1"])
+    assert c.parallelism == 8 and c.test is False and c.jobName == "x"
+    assert c.psMessagesTopic == "ignored" and c.extra == {"fooBar": "1"}

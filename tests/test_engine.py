@@ -1,0 +1,141 @@
+"""End-to-end engine tests on the in-process broker (CPU): the reference's request →
+train → forecast → query → termination flow, record buffering, holdout semantics,
+checkpoint/restore (with the spoke pipelines restored, SURVEY §2.8 Q1 fixed)."""
+import json
+import uuid
+
+import torch
+
+from omldm_amd.api.batch import FeatureSpace
+from omldm_amd.engine.holdout import HoldoutSet
+from omldm_amd.engine.job import Job
+from omldm_amd.io.synthetic import synth_batch, synth_json_records
+from omldm_amd.io.transport import MemoryBroker
+from omldm_amd.parallel.comm import Comm
+from omldm_amd.utils.config import JobConfig
+
+SP = FeatureSpace(13, 0, 26, 1 << 16)
+
+
+def make_job(extra=(), name=None):
+    name = name or uuid.uuid4().hex
+    addr = f"memory://{name}"
+    args = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        args += [f"--{k}", addr]
+    args += ["--hashDim", str(SP.dim), "--batchSize", "500", "--timeout", "200",
+             "--parallelism", "4", *extra]
+    cfg = JobConfig.from_args(args)
+    br = MemoryBroker.named(name)
+    br.create_topic(cfg.trainingDataTopic, 4)
+    return Job(cfg, Comm(), "cpu"), br, cfg
+
+
+def create(br, pid, learner, protocol="Synchronous", pre=None, hyper=None):
+    br.produce("requests", json.dumps({
+        "id": pid, "request": "Create",
+        "learner": {"name": learner, "hyperParameters": hyper or {}},
+        "preProcessors": [{"name": p} for p in (pre or [])],
+        "trainingConfiguration": {"protocol": protocol}}))
+
+
+def test_e2e_create_train_forecast_query_terminate():
+    job, br, cfg = make_job()
+    for r in synth_json_records(1500, SP):
+        br.produce("trainingData", r)
+    create(br, 1, "SVM", pre=["StandardScaler"])
+    create(br, 2, "ORR", "FGM", pre=["PolynomialFeatures"])
+    create(br, 3, "K-means", hyper={"k": 3})
+    for _ in range(5):
+        job.tick()
+    assert set(job.pipes) == {1, 2, 3}
+    for r in synth_json_records(7, SP, start=50, operation="forecasting"):
+        br.produce("forecastingData", r)
+    br.produce("requests", json.dumps({"id": 1, "request": "Query", "requestId": 42}))
+    for _ in range(3):
+        job.tick()
+    preds = [json.loads(x) for x in br.records("predictions")]
+    assert len(preds) == 21 and {p["mlpId"] for p in preds} == {1, 2, 3}
+    resp = [json.loads(x) for x in br.records("responses")]
+    assert resp[-1]["responseId"] == 42 and resp[-1]["dataFitted"] > 0
+    assert 0.0 <= resp[-1]["score"] <= 1.0
+    job.run()  # idle timeout → final statistics → performance topic
+    assert job.terminated
+    perf = json.loads(br.records("performance")[-1])
+    assert perf["jobName"] == cfg.jobName
+    assert [s["pipeline"] for s in perf["statistics"]] == [1, 2, 3]
+    syn = perf["statistics"][0]
+    assert syn["protocol"] == "Synchronous" and syn["fitted"] > 0 and syn["modelsShipped"] > 0
+
+
+def test_records_buffered_until_create_and_delete():
+    job, br, _ = make_job()
+    for r in synth_json_records(300, SP):
+        br.produce("trainingData", r)
+    job.tick()
+    assert len(job.record_buffer) == 300 and not job.pipes
+    create(br, 5, "PA")
+    job.tick()
+    job.tick()
+    assert job.record_buffer == [] and job.pipes[5].learner.running_totals()["fitted"] > 0
+    br.produce("requests", json.dumps({"id": 5, "request": "Delete"}))
+    job.tick()
+    assert 5 not in job.pipes
+
+
+def test_update_changes_hyper_parameters():
+    job, br, _ = make_job()
+    create(br, 1, "PA", hyper={"C": 0.5})
+    job.tick()
+    br.produce("requests", json.dumps({"id": 1, "request": "Update",
+                                       "learner": {"name": "PA", "hyperParameters": {"C": 0.01}}}))
+    job.tick()
+    assert abs(job.pipes[1].learner.rule.C - 0.01) < 1e-9
+
+
+def test_invalid_records_counted_not_fatal():
+    job, br, _ = make_job()
+    create(br, 1, "PA")
+    job.tick()
+    br.produce("trainingData", "EOS")
+    br.produce("trainingData", "{broken")
+    br.produce("trainingData", json.dumps({"numericalFeatures": [1.0], "operation": "training"}))
+    for r in synth_json_records(10, SP):
+        br.produce("trainingData", r)
+    job.tick()
+    assert job.counters["invalid"] == 3 and job.counters["records"] == 10
+
+
+def test_holdout_reference_semantics():
+    h = HoldoutSet(SP, 4, "cpu")
+    b = synth_batch(SP, 10)
+    out = h.route(b)
+    assert out.B == 8 and h.filled == 2           # positions 8, 9 held out
+    out = h.route(synth_batch(SP, 20, start=10))
+    assert h.filled == 4 and out.B == 16 + 2      # 4 more held: 2 evictions trained
+    big = h.route(synth_batch(SP, 100, start=30))
+    assert h.filled == 4 and big.B == 80 + 4 + 16  # 20 held: ring + 16 spill trained
+    assert h.test_set().B == 4
+
+
+def test_checkpoint_restore_roundtrip(tmp_path):
+    name = uuid.uuid4().hex
+    extra = ["--checkpointing", "true", "--checkInterval", "0", "--stateBackend",
+             f"file://{tmp_path}"]
+    job, br, _ = make_job(extra, name=name)
+    for r in synth_json_records(800, SP):
+        br.produce("trainingData", r)
+    create(br, 1, "SVM")
+    create(br, 2, "HT", hyper={"nClasses": 2})
+    for _ in range(4):
+        job.tick()
+    w = job.pipes[1].learner.state_vector().clone()
+    fitted = job.pipes[1].learner.running_totals()["fitted"]
+    job.checkpointer.save(job)
+    job2, _, _ = make_job(["--restore", "true", "--stateBackend", f"file://{tmp_path}"], name=name)
+    assert set(job2.pipes) == {1, 2}
+    assert torch.equal(job2.pipes[1].learner.state_vector(), w)
+    assert job2.pipes[1].learner.running_totals()["fitted"] == fitted
+    assert job2.holdout.filled == job.holdout.filled
+    assert job2.train_in.offsets == job.train_in.offsets

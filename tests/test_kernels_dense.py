@@ -1,0 +1,176 @@
+"""HIP kernels of the preprocessors and dense/multi-class learners vs fp32/fp64 PyTorch
+references (gpu-marked), plus CPU-path math checks."""
+import json
+import uuid
+
+import numpy as np
+import pytest
+import torch
+
+from omldm_amd.api.batch import FeatureSpace
+from omldm_amd.io.synthetic import synth_batch, synth_json_records
+from omldm_amd.models import make_learner
+from omldm_amd.models.base import RoundContext
+from omldm_amd.models.preprocess import MinMaxScaler, PolynomialFeatures, StandardScaler
+from omldm_amd.ops import dense as D
+from omldm_amd.ops import preprocess as P
+
+SP = FeatureSpace(13, 0, 26, 1 << 14)
+
+
+def test_cpu_scalers_match_numpy():
+    rng = np.random.default_rng(0)
+    xs = [rng.normal(3.0, 2.0, size=(n, 5)).astype(np.float32) for n in (100, 7, 300)]
+    sc, mm = StandardScaler(), MinMaxScaler()
+    for x in xs:
+        t = torch.from_numpy(x)
+        sc.fit_transform(t, True)
+        mm.fit_transform(t, True)
+    allx = np.concatenate(xs)
+    np.testing.assert_allclose(sc.mean.numpy(), allx.mean(0), rtol=1e-5)
+    np.testing.assert_allclose((sc.m2 / sc.count).numpy(), allx.var(0), rtol=1e-4)
+    np.testing.assert_allclose(mm.lo.numpy(), allx.min(0))
+    np.testing.assert_allclose(mm.hi.numpy(), allx.max(0))
+
+
+def test_poly_expansion():
+    x = torch.tensor([[1.0, 2.0, 3.0]])
+    pf = PolynomialFeatures({"degree": 2})
+    out = pf.fit_transform(x, True)
+    assert pf.out_dim(3) == 9
+    np.testing.assert_allclose(out.numpy()[0], [1, 2, 3, 1, 2, 3, 4, 6, 9])
+
+
+def test_gram_cpu_and_orr_solution():
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(500, 4)).astype(np.float32)
+    wtrue = np.array([1.0, -2.0, 0.5, 3.0], np.float32)
+    y = X @ wtrue + 0.7
+    L = make_learner("ORR", {"lambda": 1e-6, "_inDim": 4}, SP, "cpu")
+    from omldm_amd.api.batch import HashedBatch
+    b = HashedBatch(torch.from_numpy(X), torch.full((500, 26), -1, dtype=torch.int32),
+                    torch.from_numpy(y))
+    L.fit(b, RoundContext())
+    w = L.weights().numpy()
+    np.testing.assert_allclose(w[:4], wtrue, atol=1e-3)
+    assert abs(w[4] - 0.7) < 1e-3
+
+
+@pytest.mark.gpu
+def test_hip_colstats_scale_poly(cuda):
+    torch.manual_seed(0)
+    x = torch.randn(5000, 37) * 3 + 5
+    for shift_rows in (1234, 3766):
+        pass
+    mean = torch.zeros(37, dtype=torch.float64)
+    m2 = torch.zeros_like(mean)
+    c = 0.0
+    mg, m2g = mean.to(cuda), m2.to(cuda)
+    cg = 0.0
+    lo = torch.full((37,), float("inf"), device=cuda)
+    hi = torch.full((37,), float("-inf"), device=cuda)
+    for part in (x[:1234], x[1234:]):
+        c = P.welford_update(part, c, mean, m2)
+        cg = P.welford_update(part.to(cuda), cg, mg, m2g)
+        P.minmax_update(part.to(cuda), lo, hi)
+    np.testing.assert_allclose(mg.cpu().numpy(), mean.numpy(), rtol=1e-5)
+    np.testing.assert_allclose(m2g.cpu().numpy(), m2.numpy(), rtol=1e-4)
+    np.testing.assert_allclose(lo.cpu().numpy(), x.min(0).values.numpy())
+    np.testing.assert_allclose(hi.cpu().numpy(), x.max(0).values.numpy())
+    xs = x[:100]
+    np.testing.assert_allclose(P.standardize(xs.to(cuda), mg, m2g, cg).cpu().numpy(),
+                               P.standardize(xs, mean, m2, c).numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(P.minmax_scale(xs.to(cuda), lo, hi).cpu().numpy(),
+                               P.minmax_scale(xs, lo.cpu(), hi.cpu()).numpy(), atol=1e-6)
+    pf = PolynomialFeatures({"degree": 3})
+    idx = pf._index(6, "cpu")
+    np.testing.assert_allclose(P.poly_expand(xs[:, :6].to(cuda), idx.to(cuda)).cpu().numpy(),
+                               P.poly_expand(xs[:, :6], idx).numpy(), rtol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,d", [(1000, 13), (4097, 104), (333, 30)])
+def test_hip_gram_mfma_vs_fp64(cuda, B, d):
+    torch.manual_seed(B)
+    x = torch.randn(B, d)
+    y = torch.randn(B)
+    y[::7] = float("nan")
+    ld = ((d + 2 + 31) // 32) * 32
+    G = torch.zeros(ld, ld, device=cuda)
+    D.gram_update(x.to(cuda), y.to(cuda), G)
+    ok = ~torch.isnan(y)
+    z = torch.cat([x[ok], torch.ones(int(ok.sum()), 1), y[ok].unsqueeze(1)], 1).double()
+    ref = (z.T @ z).numpy()
+    got = G.cpu().double().numpy()[: d + 2, : d + 2]
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-2)
+    assert float(G[d + 2:, :].abs().sum()) == 0.0
+
+
+@pytest.mark.gpu
+def test_hip_kmeans_assign(cuda):
+    torch.manual_seed(3)
+    x = torch.randn(3000, 13)
+    cent = torch.randn(5, 13)
+    y = torch.zeros(3000)
+    s, n, inert = torch.zeros(5, 13), torch.zeros(5), torch.zeros(1)
+    a_ref = D.kmeans_assign(x, y, cent, s, n, inert, want_assign=True)
+    sg, ng, ig = torch.zeros(5, 13, device=cuda), torch.zeros(5, device=cuda), \
+        torch.zeros(1, device=cuda)
+    a = D.kmeans_assign(x.to(cuda), y.to(cuda), cent.to(cuda), sg, ng, ig, want_assign=True)
+    assert torch.equal(a.cpu().long(), a_ref.long())
+    np.testing.assert_allclose(sg.cpu().numpy(), s.numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(ng.cpu().numpy(), n.numpy())
+
+
+@pytest.mark.gpu
+def test_hip_multiclass_round_vs_cpu(cuda):
+    b = synth_batch(SP, 2000, task=2, n_classes=4, seed=5)
+    W = torch.randn(4, SP.dim) * 0.01
+    st, dacc = torch.zeros(8), torch.zeros(4, SP.dim)
+    D.multiclass_round(W, b, 50, 40, 4, 1, 1.0, True, dacc, st)
+    stg, daccg = torch.zeros(8, device=cuda), torch.zeros(4, SP.dim, device=cuda)
+    D.multiclass_round(W.to(cuda), b.to(cuda), 50, 40, 4, 1, 1.0, True, daccg, stg, log2cap=11)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(stg.cpu()[[1, 3]].numpy(), st[[1, 3]].numpy())
+    np.testing.assert_allclose(daccg.cpu().numpy(), dacc.numpy(), rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,task,hyper", [
+    ("PA", 0, {}), ("RegressorPA", 1, {}), ("SVM", 0, {"modelDtype": "bf16"}),
+    ("LogisticRegression", 0, {}), ("MultiClassPA", 2, {"nClasses": 3}),
+    ("ORR", 1, {}), ("K-means", 0, {"k": 3}), ("NN", 0, {}), ("HT", 2, {"nClasses": 3})])
+def test_learners_on_gpu(cuda, name, task, hyper):
+    L = make_learner(name, hyper, SP, cuda)
+    for r in range(3):
+        L.fit(synth_batch(SP, 2048, start=r * 2048, task=task, n_classes=3).to(cuda),
+              RoundContext(spokes=16))
+    t = synth_batch(SP, 512, start=10**6, task=task, n_classes=3).to(cuda)
+    loss, score, n = L.evaluate(t)
+    assert n == 512 and np.isfinite(float(loss))
+    assert L.running_totals()["fitted"] == 3 * 2048
+
+
+@pytest.mark.gpu
+def test_engine_on_gpu(cuda):
+    from omldm_amd.engine.job import Job
+    from omldm_amd.io.transport import MemoryBroker
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.utils.config import JobConfig
+
+    name = uuid.uuid4().hex
+    args = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        args += [f"--{k}", f"memory://{name}"]
+    cfg = JobConfig.from_args(args + ["--hashDim", str(SP.dim), "--timeout", "200",
+                                      "--batchSize", "1000"])
+    br = MemoryBroker.named(name)
+    for r in synth_json_records(2000, SP):
+        br.produce("trainingData", r)
+    br.produce("requests", json.dumps({"id": 1, "request": "Create", "learner": {"name": "SVM"},
+                                       "preProcessors": [{"name": "StandardScaler"}],
+                                       "trainingConfiguration": {"protocol": "Synchronous"}}))
+    job = Job(cfg, Comm(), cuda).run()
+    assert job.terminated and job.pipes[1].learner.running_totals()["fitted"] > 0
+    assert json.loads(br.records("performance")[-1])["statistics"][0]["fitted"] > 0

@@ -1,0 +1,125 @@
+"""Synchronisation protocols on real multi-process collectives (gloo, CPU, world 2 and 4).
+
+Invariants checked per protocol:
+* Synchronous (H>1 all-reduce and H=1 reduce+broadcast): replicas identical after every
+  round and equal to one process running all workers' spokes;
+* Asynchronous / SSP: after draining, every rank holds the same merged model;
+* EASGD: centre variables identical; GM / FGM: estimates identical, syncs counted;
+* SingleLearner: only the hub trains, replicas equal to the hub model.
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from omldm_amd.api.batch import FeatureSpace
+from omldm_amd.io.synthetic import synth_batch
+from omldm_amd.models import make_learner
+from omldm_amd.parallel.comm import Comm
+from omldm_amd.parallel.protocols import make_protocol
+
+SP = FeatureSpace(13, 0, 26, 1 << 14)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out, learner, proto, cfg, rounds, B, task):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ["OMLDM_CPU_THREADS"] = "1"
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm()
+    L = make_learner(learner, {"nClasses": 3, "k": 3}, SP, "cpu")
+    P = make_protocol(proto, comm, L, cfg, spokes=2, max_msg_params=1000)
+    states = []
+    for r in range(rounds):
+        b = synth_batch(SP, B, start=(r * world + rank) * B, task=task, n_classes=3)
+        P.round(b)
+        states.append(L.state_vector().clone())
+    P.finalize()
+    res = {"final": L.state_vector().clone(), "states": states, "stats": P.stats.as_dict(),
+           "fitted": L.running_totals()["fitted"]}
+    for attr in ("_E", "_c"):
+        if getattr(P, attr, None) is not None:
+            res[attr] = getattr(P, attr).clone()
+    torch.save(res, os.path.join(out, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run(world, learner, proto, cfg=None, rounds=4, B=256, task=0):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, _free_port(), d, learner, proto, cfg or {},
+                                          rounds, B, task), nprocs=world, start_method="fork")
+        return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+
+
+def same(a, b, tol=1e-5):
+    return torch.allclose(a, b, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("hubs", [0, 1])
+def test_synchronous_replicas_and_equivalence(hubs):
+    cfg = {"HubParallelism": hubs} if hubs else {}
+    res = run(2, "SVM", "Synchronous", cfg)
+    for s0, s1 in zip(res[0]["states"], res[1]["states"]):
+        assert same(s0, s1)
+    # one process running both ranks' spokes over the concatenated shards
+    L = make_learner("SVM", {}, SP, "cpu")
+    P = make_protocol("Synchronous", Comm(), L, {}, spokes=4)
+    for r in range(4):
+        b0 = synth_batch(SP, 256, start=(r * 2) * 256)
+        b1 = synth_batch(SP, 256, start=(r * 2 + 1) * 256)
+        from omldm_amd.api.batch import HashedBatch
+        P.round(HashedBatch.cat_batches([b0, b1]))
+    assert same(L.state_vector(), res[0]["final"], 1e-4)
+    assert res[0]["stats"]["modelsShipped"] == 4 * 2 * 2
+
+
+@pytest.mark.parametrize("proto,cfg", [("Asynchronous", {}), ("SSP", {"staleness": 2})])
+def test_delayed_protocols_converge_to_same_model(proto, cfg):
+    res = run(2, "PA", proto, cfg, rounds=5)
+    assert same(res[0]["final"], res[1]["final"])
+    assert same(res[0]["_E"], res[1]["_E"])
+    assert res[0]["fitted"] > 0 and float(res[0]["final"].abs().sum()) > 0
+
+
+def test_easgd_centre_consistent():
+    res = run(2, "PA", "EASGD", {"tau": 2, "alpha": 0.3}, rounds=4)
+    assert same(res[0]["_c"], res[1]["_c"])
+
+
+@pytest.mark.parametrize("proto", ["GM", "FGM"])
+def test_monitoring_protocols(proto):
+    res = run(2, "ORR", proto, {"threshold": 0.01, "epsilon": 0.01}, rounds=6, task=1)
+    assert same(res[0]["_E"], res[1]["_E"])
+    assert res[0]["stats"]["syncs"] >= 1
+    assert res[0]["stats"]["smallMessages"] > 0
+
+
+def test_fgm_linear_world4():
+    res = run(4, "SVM", "FGM", {"epsilon": 0.05}, rounds=5)
+    for r in res[1:]:
+        assert same(r["_E"], res[0]["_E"])
+
+
+def test_single_learner_hub_only():
+    res = run(2, "K-means", "SingleLearner", rounds=3)
+    assert same(res[0]["final"], res[1]["final"])
+    assert res[0]["fitted"] > 0 and res[1]["fitted"] == 0
+
+
+def test_unknown_protocol_falls_back_to_asynchronous():
+    L = make_learner("PA", {}, SP, "cpu")
+    assert make_protocol("Bogus", Comm(), L).NAME == "Asynchronous"
+    assert make_protocol(None, Comm(), L).NAME == "Asynchronous"
