@@ -37,7 +37,7 @@ __global__ __launch_bounds__(kPPThreads) void colmoments_kernel(
   for (long long e = threadIdx.x; e < n; e += kPPThreads) {
     const int c = (int)(e % d);
     const float v = base[e];
-    const float z = v - (float)shift[c];
+    const float z = shift ? v - (float)shift[c] : v;  // extrema-only mode passes no shift
     atomicAdd(&s1[c], z);
     atomicAdd(&s2[c], z * z);
     const int iv = __float_as_int(v);
@@ -168,6 +168,7 @@ OMLDM_API int omldm_colstats_update(const float* x, int B, int d, double count, 
                                     double* m2, float* lo, float* hi, int mode, float* partial,
                                     int rows_per_block, void* stream) {
   if (B <= 0) return 0;
+  if (((mode & 1) && (!mean || !m2)) || ((mode & 2) && (!lo || !hi)) || !partial) return -4;
   hipStream_t st = (hipStream_t)stream;
   const int nblk = (B + rows_per_block - 1) / rows_per_block;
   const size_t lds = (size_t)d * 16;
