@@ -75,7 +75,10 @@ def main(argv=None) -> int:
     ap.add_argument("--wire", default="compact", choices=["wide", "compact"],
                     help="compact: field-aware uint16 categorical slots (half the PCIe bytes)")
     ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")
-    ap.add_argument("--ingest", default="pinned", choices=["pinned", "device"],
+    ap.add_argument("--latency-mode", default="zerocopy", choices=["copy", "zerocopy"],
+                    help="zerocopy: the predict kernel reads the point from and writes the "
+                         "score to pinned host memory (one launch per request)")
+    ap.add_argument("--ingest", default="pinned", choices=["pinned", "device", "zerocopy"],
                     help="pinned: H2D copy of every batch inside the timed loop")
     ap.add_argument("--latency-samples", type=int, default=2000)
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
@@ -140,7 +143,7 @@ def main(argv=None) -> int:
             dst.copy_(src, non_blocking=True)
 
     def prefetch(k: int):
-        if a.ingest == "device":
+        if a.ingest in ("device", "zerocopy"):
             return
         t = time.perf_counter()
         slot = k % 2
@@ -157,6 +160,11 @@ def main(argv=None) -> int:
     def step(k: int):
         if a.ingest == "device":
             proto.round(dev[k % a.pool].batch)
+            return
+        if a.ingest == "zerocopy":  # the round kernel reads the pinned batch over PCIe
+            t = time.perf_counter()
+            proto.round(pool[k % a.pool].batch if on_gpu else pool[k % a.pool].batch)
+            host_t["round"] += time.perf_counter() - t
             return
         slot = k % 2
         prefetch(k + 1)
@@ -203,14 +211,22 @@ def main(argv=None) -> int:
     lat_us = []
     if rank == 0:
         one = synth_batch(space, 1, start=123, seed=25, pin=on_gpu)
-        one_dev = HashedBatch.empty(space, 1, device=device)
+        one_dev = HashedBatch.empty(space, 1, device=device, num_dtype=num_dtype)
+        one_pin = HashedBatch.empty(space, 1, pin=on_gpu, num_dtype=num_dtype)
+        one_pin.num.copy_(one.num)
+        one_pin.cat.copy_(one.cat)
         res = torch.empty(1, dtype=torch.float32, pin_memory=on_gpu)
+        res2 = torch.empty((1, 1), dtype=torch.float32, pin_memory=on_gpu)
+        from omldm_amd.ops import linear as LO
         for i in range(a.latency_samples + 50):
             t = time.perf_counter()
-            one_dev.num.copy_(one.num, non_blocking=True)
-            one_dev.cat.copy_(one.cat, non_blocking=True)
-            s = learner.decision(one_dev)
-            res.copy_(s, non_blocking=True)
+            if a.latency_mode == "zerocopy" and on_gpu:
+                LO.linear_predict(learner._wread(), one_pin, out=res2)
+            else:
+                one_dev.num.copy_(one_pin.num, non_blocking=True)
+                one_dev.cat.copy_(one_pin.cat, non_blocking=True)
+                s = learner.decision(one_dev)
+                res.copy_(s, non_blocking=True)
             if on_gpu:
                 torch.cuda.current_stream().synchronize()
             if i >= 50:

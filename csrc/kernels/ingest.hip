@@ -68,6 +68,14 @@ OMLDM_API int omldm_h2d_async(void* dst, const void* src, long long nbytes, void
   return (int)hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyHostToDevice, (hipStream_t)stream);
 }
 
+// Device-side alias of a pinned host pointer (kernels may then read/write host memory
+// directly over PCIe: zero-copy ingest of single-use rows, zero-copy predict results).
+OMLDM_API void* omldm_host_device_ptr(void* host) {
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess) return nullptr;
+  return dev;
+}
+
 // Registers an existing host allocation as pinned+mapped (for buffers not allocated pinned).
 OMLDM_API int omldm_host_register(void* p, long long nbytes) {
   return (int)hipHostRegister(p, (size_t)nbytes, hipHostRegisterMapped);

@@ -74,7 +74,8 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
     if S <= 0:
         return
     if w.is_cuda:
-        assert num.is_cuda and cat.is_cuda and y.is_cuda and dacc.is_cuda
+        # batch rows may be device tensors or pinned host memory (zero-copy ingest)
+        assert all(t.is_cuda or t.is_pinned() for t in (num, cat, y)) and dacc.is_cuda
         assert stats is None or stats.is_cuda
         assert num.dtype in (torch.float32, torch.bfloat16)
         assert num.shape[1] + cat.shape[1] + int(rule.bias) <= 256, "≤ 256 features per example"
@@ -83,9 +84,10 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         wsw = WS_STAT + num.shape[1] + 1
         ws = _workspace(w.device, S * wsw)
         tables = _workspace(w.device, S * ((1 << log2cap) + 64) * 2, key="tables")
+        dp = native.dptr
         rc = native.hip().omldm_linear_round(
-            ptr(w), int(w.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
-            num.shape[1], ptr(cat), cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim,
+            ptr(w), int(w.dtype == torch.bfloat16), dp(num), int(num.dtype == torch.bfloat16),
+            num.shape[1], dp(cat), cat.shape[1], dp(y), batch.B, R, S, ptr(dacc), dim,
             ptr(ws), ptr(tables), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr,
             rule.lam, inv_p, int(rule.bias), batch.cat_span, log2cap, int(chunk), int(ablate),
             native.stream_of(w))
@@ -128,10 +130,11 @@ def linear_predict(w: torch.Tensor, batch: HashedBatch, wscale: torch.Tensor | N
         return out.view(B) if single else out
     if w.is_cuda:
         num = batch.num
+        dp = native.dptr  # inputs/outputs may be pinned host memory (zero-copy predict)
         rc = native.hip().omldm_linear_predict(
-            ptr(W), int(W.dtype == torch.bfloat16), W.stride(0), M, ptr(num),
-            int(num.dtype == torch.bfloat16), num.shape[1], ptr(batch.cat), batch.cat.shape[1], B,
-            dim, int(bias), batch.cat_span, ptr(wscale), ptr(out), native.stream_of(w))
+            ptr(W), int(W.dtype == torch.bfloat16), W.stride(0), M, dp(num),
+            int(num.dtype == torch.bfloat16), num.shape[1], dp(batch.cat), batch.cat.shape[1], B,
+            dim, int(bias), batch.cat_span, ptr(wscale), dp(out), native.stream_of(w))
         check(rc, "omldm_linear_predict")
     else:
         W32 = W.float().contiguous()

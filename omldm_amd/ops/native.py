@@ -58,6 +58,7 @@ HIP_SIGS = [
                                      i32, vp, vp, i32, vp]),
     ("omldm_multiclass_apply", i32, [vp, vp, i64, vp, vp]),
     ("omldm_stream_create_cumask", vp, [i32]),
+    ("omldm_host_device_ptr", vp, [vp]),
     ("omldm_stream_destroy", i32, [vp]),
     ("omldm_host_register", i32, [vp, i64]),
 ]
@@ -139,6 +140,21 @@ def ptr(t) -> int:
     if hasattr(t, "data_ptr"):
         return t.data_ptr()
     return t.ctypes.data
+
+
+def dptr(t) -> int:
+    """Pointer usable by a kernel: device tensors as-is, pinned host tensors through
+    their device alias (zero-copy access over PCIe)."""
+    if t is None:
+        return None
+    if getattr(t, "is_cuda", False):
+        return t.data_ptr()
+    if t.is_pinned():
+        p = hip().omldm_host_device_ptr(t.data_ptr())
+        if not p:
+            raise RuntimeError("pinned host tensor has no device mapping")
+        return p
+    raise ValueError("kernel argument must be a device tensor or pinned host memory")
 
 
 def stream_of(t) -> int:
