@@ -75,7 +75,8 @@ def main(argv=None) -> int:
     ap.add_argument("--wire", default="compact", choices=["wide", "compact"],
                     help="compact: field-aware uint16 categorical slots (half the PCIe bytes)")
     ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")
-    ap.add_argument("--latency-mode", default="zerocopy", choices=["copy", "zerocopy"],
+    ap.add_argument("--latency-mode", default="persistent",
+                    choices=["copy", "zerocopy", "persistent"],
                     help="zerocopy: the predict kernel reads the point from and writes the "
                          "score to pinned host memory (one launch per request)")
     ap.add_argument("--ingest", default="pinned", choices=["pinned", "device", "zerocopy"],
@@ -218,7 +219,25 @@ def main(argv=None) -> int:
         res = torch.empty(1, dtype=torch.float32, pin_memory=on_gpu)
         res2 = torch.empty((1, 1), dtype=torch.float32, pin_memory=on_gpu)
         from omldm_amd.ops import linear as LO
-        for i in range(a.latency_samples + 50):
+        server = None
+        if a.latency_mode == "persistent" and on_gpu:
+            from omldm_amd.ops.serving import PredictServer
+
+            torch.cuda.synchronize(device)
+            server = PredictServer(learner._wread(), space.dn, space.dc, True, space.cat_span)
+            server.start(lifetime_us=20_000_000)
+            num_h = one_pin.num[0].float().contiguous()
+            cat_h = (one_pin.cat[0].to(torch.int64) & (0xFFFF if space.cat_span else -1))
+            cat_h = cat_h.to(torch.int32).contiguous()
+            ref = float(LO.linear_predict(learner._wread(), one_pin.to(device))[0])
+            for i in range(a.latency_samples + 50):
+                t = time.perf_counter()
+                got = server.request_raw(num_h.data_ptr(), cat_h.data_ptr())
+                if i >= 50:
+                    lat_us.append((time.perf_counter() - t) * 1e6)
+            server.close()
+            assert abs(got[0] - ref) <= 1e-3 * max(1.0, abs(ref)), (got, ref)
+        for i in range(a.latency_samples + 50 if server is None else 0):
             t = time.perf_counter()
             if a.latency_mode == "zerocopy" and on_gpu:
                 LO.linear_predict(learner._wread(), one_pin, out=res2)

@@ -1,0 +1,177 @@
+// Low-latency forecasting: a persistent predict wavefront fed through a host mailbox.
+//
+// Reference path: forecasting record → FlinkSpoke → learner predict → Prediction side
+// output → predictions topic (omldm/operators/spoke/FlinkSpoke.scala:105,
+// omldm/network/FlinkNetwork.scala:250); its latency is a Flink task hop + JVM call.
+// Here one resident wavefront polls a sequence word in fine-grained (coherent), pinned
+// host memory; the host writes one point + bumps the sequence; the wave reads the point
+// over PCIe with system-scope loads, scores it against M models (the same feature
+// decoding as the training kernel) and publishes the scores + the completion sequence
+// with system-scope stores. No kernel launch and no stream synchronisation per request.
+//
+// Safety: the wave exits on the stop word or after `lifetime_us` of wall time
+// (s_memrealtime, 100 MHz), whichever comes first; every spin is bounded by it.
+#include "common.h"
+
+#include <chrono>
+#include <cstring>
+
+namespace omldm {
+
+struct Mailbox {
+  unsigned int seq_req;   // host → device: request sequence number
+  unsigned int seq_done;  // device → host: last completed sequence number
+  unsigned int stop;      // host → device: exit request
+  unsigned int alive;     // device → host: 1 while the wave is polling
+  float result[60];       // scores of up to 60 models
+  // payload: num [dn] floats, then cat [dc] ints
+  float num[256];
+  int cat[256];
+};
+
+template <typename T>
+__device__ __forceinline__ T sys_load(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ void sys_store(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ unsigned long long rt_now() {
+  return __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
+}
+
+template <typename WT>
+__global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, long long wstride,
+                                                   int M, int dn, int dc, int dim, int bias,
+                                                   int cspan, Mailbox* mb,
+                                                   unsigned long long lifetime_ticks) {
+  const int lane = threadIdx.x;
+  const unsigned long long t_end = rt_now() + lifetime_ticks;
+  unsigned int last = sys_load(&mb->seq_req);
+  if (lane == 0) sys_store(&mb->alive, 1u);
+  while (true) {
+    unsigned int seq = 0;
+    bool go = false, quit = false;
+    if (lane == 0) {
+      // bounded poll: re-check the clock every 64 polls
+      for (int i = 0; i < 64; ++i) {
+        seq = sys_load(&mb->seq_req);
+        if (seq != last) {
+          go = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!go) quit = sys_load(&mb->stop) != 0u || rt_now() > t_end;
+    }
+    go = __builtin_amdgcn_readfirstlane(go ? 1 : 0) != 0;
+    quit = __builtin_amdgcn_readfirstlane(quit ? 1 : 0) != 0;
+    if (quit) break;
+    if (!go) continue;
+    seq = __builtin_amdgcn_readfirstlane(seq);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // order payload reads after the sequence
+    // lane = feature (≤ 64 features: dn + dc + bias)
+    int idx = -1;
+    float v = 0.f;
+    const int j = lane;
+    if (j == dn + dc && bias) {
+      idx = dim - 1;
+      v = 1.f;
+    } else if (j < dn) {
+      idx = j;
+      v = sys_load(&mb->num[j]);
+    } else if (j < dn + dc) {
+      const int c = sys_load(&mb->cat[j - dn]);
+      if (cspan > 0) {
+        const unsigned u = (unsigned)c & 0xFFFFu;
+        if (u != 0xFFFFu) {
+          idx = dn + (j - dn) * cspan + (int)(u & 0x7fffu);
+          v = (u & 0x8000u) ? -1.f : 1.f;
+        }
+      } else if (c != -1) {
+        idx = c & 0x7fffffff;
+        v = c < 0 ? -1.f : 1.f;
+      }
+    }
+    if ((unsigned)idx >= (unsigned)dim) {
+      idx = -1;
+      v = 0.f;
+    }
+    for (int m = 0; m < M; ++m) {
+      float acc = idx >= 0 ? v * to_f(w[(size_t)m * wstride + idx]) : 0.f;
+      acc = wave_sum(acc);
+      if (lane == 0) sys_store(&mb->result[m], acc);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (lane == 0) sys_store(&mb->seq_done, seq);
+    last = seq;
+  }
+  if (lane == 0) sys_store(&mb->alive, 0u);
+}
+
+}  // namespace omldm
+
+using namespace omldm;
+
+OMLDM_API void* omldm_mailbox_alloc() {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, sizeof(Mailbox), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return nullptr;
+  memset(p, 0, sizeof(Mailbox));
+  return p;
+}
+
+OMLDM_API void omldm_mailbox_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+// Launches the persistent wave on `stream` (use a stream of its own).
+OMLDM_API int omldm_serve_start(const void* w, int w_bf16, long long wstride, int M, int dn,
+                                int dc, int dim, int bias, int cspan, void* mailbox,
+                                long long lifetime_us, void* stream) {
+  if (M < 1 || M > 60 || dn + dc + (bias ? 1 : 0) > 64 || dn > 256 || dc > 256) return -2;
+  Mailbox* hmb = (Mailbox*)mailbox;
+  void* dmb = nullptr;
+  if (hipHostGetDevicePointer(&dmb, mailbox, 0) != hipSuccess || !dmb) return -3;
+  __atomic_store_n(&hmb->stop, 0u, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&hmb->alive, 0u, __ATOMIC_SEQ_CST);
+  const unsigned long long ticks = (unsigned long long)lifetime_us * 100ull;  // 100 MHz
+  if (w_bf16)
+    hipLaunchKernelGGL(serve_kernel<__hip_bfloat16>, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       (const __hip_bfloat16*)w, wstride, M, dn, dc, dim, bias, cspan,
+                       (Mailbox*)dmb, ticks);
+  else
+    hipLaunchKernelGGL(serve_kernel<float>, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       (const float*)w, wstride, M, dn, dc, dim, bias, cspan, (Mailbox*)dmb,
+                       ticks);
+  return (int)hipGetLastError();
+}
+
+// Host side of one request: writes the point, bumps the sequence, spins (bounded) for
+// completion, copies the M scores out. Returns 0, or -1 on timeout.
+OMLDM_API int omldm_serve_request(void* mailbox, const float* num, int dn, const int* cat, int dc,
+                                  int M, float* out, long long timeout_us) {
+  Mailbox* mb = (Mailbox*)mailbox;
+  for (int j = 0; j < dn; ++j) mb->num[j] = num[j];
+  for (int j = 0; j < dc; ++j) mb->cat[j] = cat[j];
+  const unsigned int seq = __atomic_load_n(&mb->seq_req, __ATOMIC_RELAXED) + 1u;
+  __atomic_store_n(&mb->seq_req, seq, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(&mb->seq_done, __ATOMIC_ACQUIRE) != seq) {
+    if (std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() -
+                                                              t0).count() > timeout_us)
+      return -1;
+  }
+  for (int m = 0; m < M; ++m) out[m] = mb->result[m];
+  return 0;
+}
+
+OMLDM_API void omldm_serve_stop(void* mailbox) {
+  __atomic_store_n(&((Mailbox*)mailbox)->stop, 1u, __ATOMIC_SEQ_CST);
+}
+
+OMLDM_API int omldm_serve_alive(void* mailbox) {
+  return (int)__atomic_load_n(&((Mailbox*)mailbox)->alive, __ATOMIC_ACQUIRE);
+}
