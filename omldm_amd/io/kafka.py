@@ -1,0 +1,355 @@
+"""Minimal Kafka wire-protocol client (no client library is installed or fetchable).
+
+Reference: every OMLDM input/output is a Kafka topic (FlinkKafkaConsumer/Producer,
+omldm/Job.scala:42-105; omldm/utils/KafkaUtils.scala:13-18 sets bootstrap.servers — and
+the misspelled ``group.flink_worker_id``; we track offsets ourselves and
+need no consumer group). Implemented subset, enough for produce/consume of JSON records:
+
+* Metadata v1 (api 3)   — topic → partitions + leader brokers
+* ListOffsets v1 (api 2) — earliest (-2) / latest (-1) offsets
+* Produce v3 (api 0)    — RecordBatch v2, acks=1, no compression
+* Fetch v4 (api 1)      — RecordBatch v2 decoding (magic 2; older message sets skipped)
+* CreateTopics v0 (api 19) — best effort, for ``create_topic``
+CRC-32C of record batches is computed by the host library (csrc/host/crc32c.cpp).
+Compatibility is at the level of the public protocol spec; tests exercise it against a
+protocol-level fake broker (tests/fake_kafka.py) — there is no real broker here.
+"""
+from __future__ import annotations
+
+import socket
+import struct
+import threading
+import time
+
+# ------------------------------------------------------------------ primitives
+
+
+def crc32c(data: bytes) -> int:
+    from omldm_amd.ops import native
+
+    return int(native.host().omldm_crc32c(data, len(data), 0))
+
+
+def _zz(n: int) -> int:
+    return (n << 1) ^ (n >> 63)
+
+
+def _unzz(n: int) -> int:
+    return (n >> 1) ^ -(n & 1)
+
+
+def varint(n: int) -> bytes:
+    n = _zz(n) & 0xFFFFFFFFFFFFFFFF
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        if n:
+            out.append(b | 0x80)
+        else:
+            out.append(b)
+            return bytes(out)
+
+
+def read_varint(buf: bytes, pos: int) -> tuple[int, int]:
+    shift = 0
+    res = 0
+    while True:
+        b = buf[pos]
+        pos += 1
+        res |= (b & 0x7F) << shift
+        if not b & 0x80:
+            return _unzz(res), pos
+        shift += 7
+
+
+class W:
+    def __init__(self):
+        self.b = bytearray()
+
+    def i8(self, v):
+        self.b += struct.pack(">b", v)
+        return self
+
+    def i16(self, v):
+        self.b += struct.pack(">h", v)
+        return self
+
+    def i32(self, v):
+        self.b += struct.pack(">i", v)
+        return self
+
+    def i64(self, v):
+        self.b += struct.pack(">q", v)
+        return self
+
+    def s(self, v: str | None):
+        if v is None:
+            return self.i16(-1)
+        e = v.encode()
+        self.i16(len(e))
+        self.b += e
+        return self
+
+    def by(self, v: bytes | None):
+        if v is None:
+            return self.i32(-1)
+        self.i32(len(v))
+        self.b += v
+        return self
+
+    def arr(self, items, fn):
+        self.i32(len(items))
+        for it in items:
+            fn(self, it)
+        return self
+
+
+class R:
+    def __init__(self, b: bytes):
+        self.b = b
+        self.p = 0
+
+    def _u(self, fmt, n):
+        v = struct.unpack_from(fmt, self.b, self.p)[0]
+        self.p += n
+        return v
+
+    def i8(self):
+        return self._u(">b", 1)
+
+    def i16(self):
+        return self._u(">h", 2)
+
+    def i32(self):
+        return self._u(">i", 4)
+
+    def i64(self):
+        return self._u(">q", 8)
+
+    def s(self):
+        n = self.i16()
+        if n < 0:
+            return None
+        v = self.b[self.p:self.p + n].decode()
+        self.p += n
+        return v
+
+    def by(self):
+        n = self.i32()
+        if n < 0:
+            return None
+        v = self.b[self.p:self.p + n]
+        self.p += n
+        return v
+
+    def arr(self, fn):
+        return [fn(self) for _ in range(self.i32())]
+
+
+# ----------------------------------------------------------------- record batch
+
+
+def encode_batch(values: list[bytes], base_offset: int = 0, ts_ms: int | None = None,
+                 keys: list | None = None) -> bytes:
+    ts = int(time.time() * 1000) if ts_ms is None else ts_ms
+    recs = bytearray()
+    for i, v in enumerate(values):
+        k = keys[i] if keys else None
+        body = bytearray()
+        body += struct.pack(">b", 0)       # attributes
+        body += varint(0)                  # timestamp delta
+        body += varint(i)                  # offset delta
+        if k is None:
+            body += varint(-1)
+        else:
+            body += varint(len(k)) + k
+        body += varint(len(v)) + v
+        body += varint(0)                  # headers
+        recs += varint(len(body)) + body
+    tail = W()
+    tail.i16(0).i32(len(values) - 1).i64(ts).i64(ts).i64(-1).i16(-1).i32(-1).i32(len(values))
+    payload = bytes(tail.b) + bytes(recs)
+    crc = crc32c(payload)
+    head = W()
+    head.i64(base_offset).i32(4 + 1 + 4 + len(payload)).i32(0).i8(2)
+    head.b += struct.pack(">I", crc)
+    return bytes(head.b) + payload
+
+
+def decode_batches(data: bytes, verify: bool = True) -> list[tuple[int, bytes]]:
+    """[(offset, value)] of every record in a (possibly truncated) record set."""
+    out = []
+    p = 0
+    while p + 17 <= len(data):
+        base, blen = struct.unpack_from(">qi", data, p)
+        end = p + 12 + blen
+        if end > len(data):
+            break  # partial batch at the end of a fetch
+        magic = data[p + 16]
+        if magic != 2:
+            p = end
+            continue
+        crc = struct.unpack_from(">I", data, p + 17)[0]
+        body = data[p + 21:end]
+        if verify and crc32c(body) != crc:
+            raise ValueError("record batch CRC mismatch")
+        attrs = struct.unpack_from(">h", body, 0)[0]
+        if attrs & 0x7:
+            raise ValueError("compressed record batches are not supported")
+        count = struct.unpack_from(">i", body, 36)[0]
+        q = 40
+        for _ in range(count):
+            ln, q = read_varint(body, q)
+            rend = q + ln
+            q += 1
+            _, q = read_varint(body, q)       # timestamp delta
+            od, q = read_varint(body, q)      # offset delta
+            kl, q = read_varint(body, q)
+            if kl > 0:
+                q += kl
+            vl, q = read_varint(body, q)
+            val = body[q:q + vl] if vl >= 0 else b""
+            out.append((base + od, bytes(val)))
+            q = rend
+        p = end
+    return out
+
+
+# ---------------------------------------------------------------------- client
+
+
+class _Conn:
+    def __init__(self, host: str, port: int, timeout: float = 10.0):
+        self.sock = socket.create_connection((host, port), timeout=timeout)
+        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        self.cid = 0
+        self.lock = threading.Lock()
+
+    def call(self, api: int, ver: int, body: bytes, client: str = "omldm-amd") -> R:
+        with self.lock:
+            self.cid += 1
+            h = W().i16(api).i16(ver).i32(self.cid).s(client)
+            msg = bytes(h.b) + body
+            self.sock.sendall(struct.pack(">i", len(msg)) + msg)
+            n = struct.unpack(">i", self._recv(4))[0]
+            r = R(self._recv(n))
+            if r.i32() != self.cid:
+                raise IOError("kafka correlation id mismatch")
+            return r
+
+    def _recv(self, n: int) -> bytes:
+        buf = bytearray()
+        while len(buf) < n:
+            chunk = self.sock.recv(n - len(buf))
+            if not chunk:
+                raise IOError("kafka connection closed")
+            buf += chunk
+        return bytes(buf)
+
+    def close(self):
+        self.sock.close()
+
+
+class KafkaBroker:
+    """transport.Broker over the Kafka protocol (bootstrap ``host:port[,host:port]``)."""
+
+    def __init__(self, bootstrap: str, timeout: float = 10.0):
+        self.bootstrap = [(h, int(p)) for h, p in (x.rsplit(":", 1) for x in bootstrap.split(","))]
+        self.timeout = timeout
+        self._conns: dict = {}
+        self._meta: dict = {}     # topic -> {partition: leader}
+        self._brokers: dict = {}  # node -> (host, port)
+        self._rr: dict = {}
+
+    def _conn(self, node=None) -> _Conn:
+        addr = self._brokers.get(node, self.bootstrap[0]) if node is not None else self.bootstrap[0]
+        if addr not in self._conns:
+            self._conns[addr] = _Conn(addr[0], addr[1], self.timeout)
+        return self._conns[addr]
+
+    def _metadata(self, topic: str, refresh: bool = False) -> dict:
+        if topic in self._meta and not refresh:
+            return self._meta[topic]
+        r = self._conn().call(3, 1, bytes(W().arr([topic], lambda w, t: w.s(t)).b))
+        for node, host, port, _ in r.arr(lambda r: (r.i32(), r.s(), r.i32(), r.s())):
+            self._brokers[node] = (host, port)
+        r.i32()  # controller
+        for err, name, _internal, parts in r.arr(lambda r: (
+                r.i16(), r.s(), r.i8(),
+                r.arr(lambda r: (r.i16(), r.i32(), r.i32(), r.arr(lambda r: r.i32()),
+                                 r.arr(lambda r: r.i32()))))):
+            if name == topic and err == 0:
+                self._meta[topic] = {p[1]: p[2] for p in parts}
+        return self._meta.get(topic, {})
+
+    def create_topic(self, topic: str, partitions: int) -> None:
+        body = W().arr([topic], lambda w, t: w.s(t).i32(partitions).i16(1).i32(0).i32(0)).i32(
+            int(self.timeout * 1000))
+        try:
+            self._conn().call(19, 0, bytes(body.b))
+        except (IOError, OSError):
+            pass
+        self._meta.pop(topic, None)
+
+    def partitions(self, topic: str) -> int:
+        return max(1, len(self._metadata(topic)))
+
+    def produce(self, topic, value, partition=None, key=None):
+        if isinstance(value, str):
+            value = value.encode()
+        n = self.partitions(topic)
+        if partition is None:
+            partition = self._rr.get(topic, 0) % n
+            self._rr[topic] = partition + 1
+        self.produce_batch(topic, partition, [value])
+
+    def produce_batch(self, topic: str, partition: int, values: list[bytes]) -> int:
+        rs = encode_batch(values)
+        body = W().s(None).i16(1).i32(int(self.timeout * 1000)).arr(
+            [topic], lambda w, t: w.s(t).arr([partition], lambda w, p: w.i32(p).by(rs)))
+        leader = self._metadata(topic).get(partition)
+        r = self._conn(leader).call(0, 3, bytes(body.b))
+        res = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.i16(), r.i64(), r.i64()))))
+        err = res[0][1][0][1]
+        if err:
+            raise IOError(f"kafka produce error {err}")
+        return res[0][1][0][2]
+
+    def _list_offset(self, topic: str, partition: int, ts: int) -> int:
+        body = W().i32(-1).arr([topic], lambda w, t: w.s(t).arr(
+            [partition], lambda w, p: w.i32(p).i64(ts)))
+        r = self._conn(self._metadata(topic).get(partition)).call(2, 1, bytes(body.b))
+        res = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.i16(), r.i64(), r.i64()))))
+        return int(res[0][1][0][3])
+
+    def end_offset(self, topic, partition):
+        return self._list_offset(topic, partition, -1)
+
+    def consume(self, topic, partition, offset, max_records):
+        body = W().i32(-1).i32(100).i32(1).i32(8 << 20).i8(0).arr(
+            [topic], lambda w, t: w.s(t).arr(
+                [partition], lambda w, p: w.i32(p).i64(offset).i32(4 << 20)))
+        r = self._conn(self._metadata(topic).get(partition)).call(1, 4, bytes(body.b))
+        r.i32()  # throttle
+        res = r.arr(lambda r: (r.s(), r.arr(lambda r: (
+            r.i32(), r.i16(), r.i64(), r.i64(),
+            r.arr(lambda r: (r.i64(), r.i64())), r.by()))))
+        recs = []
+        for _t, parts in res:
+            for _p, err, _hw, _ls, _ab, rs in parts:
+                if err:
+                    raise IOError(f"kafka fetch error {err}")
+                recs.extend(decode_batches(rs or b""))
+        recs = [(o, v) for o, v in recs if o >= offset][:max_records]
+        if not recs:
+            return [], offset
+        return [v for _, v in recs], recs[-1][0] + 1
+
+    def flush(self):
+        pass
+
+    def close(self):
+        for c in self._conns.values():
+            c.close()
+        self._conns.clear()

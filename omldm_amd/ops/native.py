@@ -65,6 +65,7 @@ HIP_SIGS = [
 
 HOST_SIGS = [
     ("omldm_murmur3_32", u32, [C.c_char_p, i64, u32]),
+    ("omldm_crc32c", u32, [C.c_char_p, i64, u32]),
     ("omldm_hash_cat", C.c_int32, [C.c_char_p, i64, i32, i32, i64]),
     ("omldm_hash_cat16", C.c_int32, [C.c_char_p, i64, i32, i32]),
     ("omldm_parse_instances", i64, [C.c_char_p, vp, i32, i32, i32, i32, i64, i32, vp, vp, vp, vp,

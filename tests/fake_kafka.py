@@ -1,0 +1,125 @@
+"""Protocol-level fake Kafka broker for tests (no real broker exists in this sandbox).
+
+Speaks the same request subset as omldm_amd.io.kafka (Metadata v1, ListOffsets v1,
+Produce v3, Fetch v4, CreateTopics v0) on 127.0.0.1, stores records in memory and
+re-encodes RecordBatch v2 on fetch — so the client's framing, varints and CRC-32C are
+exercised in both directions. Compatibility with a real broker is "parity unpinned".
+"""
+from __future__ import annotations
+
+import socketserver
+import struct
+import threading
+from collections import defaultdict
+
+from omldm_amd.io.kafka import R, W, decode_batches, encode_batch
+
+
+class FakeKafka:
+    def __init__(self, default_partitions: int = 4):
+        self.logs = defaultdict(list)      # (topic, p) -> [bytes]
+        self.nparts = {}
+        self.default_partitions = default_partitions
+        self.lock = threading.Lock()
+        outer = self
+
+        class H(socketserver.BaseRequestHandler):
+            def handle(self):
+                s = self.request
+                while True:
+                    hdr = self._recv(4)
+                    if not hdr:
+                        return
+                    n = struct.unpack(">i", hdr)[0]
+                    req = R(self._recv(n))
+                    api, ver, cid = req.i16(), req.i16(), req.i32()
+                    req.s()
+                    body = outer.dispatch(api, ver, req)
+                    msg = struct.pack(">i", cid) + body
+                    s.sendall(struct.pack(">i", len(msg)) + msg)
+
+            def _recv(self, n):
+                buf = bytearray()
+                while len(buf) < n:
+                    c = self.request.recv(n - len(buf))
+                    if not c:
+                        return None
+                    buf += c
+                return bytes(buf)
+
+        class S(socketserver.ThreadingTCPServer):
+            allow_reuse_address = True
+            daemon_threads = True
+
+        self.server = S(("127.0.0.1", 0), H)
+        self.port = self.server.server_address[1]
+        self.thread = threading.Thread(target=self.server.serve_forever, daemon=True)
+        self.thread.start()
+
+    @property
+    def addr(self) -> str:
+        return f"127.0.0.1:{self.port}"
+
+    def close(self):
+        self.server.shutdown()
+        self.server.server_close()
+
+    def _parts(self, topic):
+        return self.nparts.setdefault(topic, self.default_partitions)
+
+    def dispatch(self, api, ver, r: R) -> bytes:
+        with self.lock:
+            if api == 3:  # Metadata v1
+                topics = r.arr(lambda r: r.s())
+                w = W().arr([(0, "127.0.0.1", self.port)],
+                            lambda w, b: w.i32(b[0]).s(b[1]).i32(b[2]).s(None)).i32(0)
+                w.arr(topics, lambda w, t: w.i16(0).s(t).i8(0).arr(
+                    list(range(self._parts(t))),
+                    lambda w, p: w.i16(0).i32(p).i32(0).arr([0], lambda w, x: w.i32(x)).arr(
+                        [0], lambda w, x: w.i32(x))))
+                return bytes(w.b)
+            if api == 19:  # CreateTopics v0
+                reqs = r.arr(lambda r: (r.s(), r.i32(), r.i16(),
+                                        r.arr(lambda r: (r.i32(), r.arr(lambda r: r.i32()))),
+                                        r.arr(lambda r: (r.s(), r.s()))))
+                for name, n, *_ in reqs:
+                    self.nparts[name] = max(1, n)
+                return bytes(W().arr(reqs, lambda w, q: w.s(q[0]).i16(0)).b)
+            if api == 0:  # Produce v3
+                r.s(), r.i16(), r.i32()
+                topics = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.by()))))
+                out = []
+                for t, parts in topics:
+                    po = []
+                    for p, rs in parts:
+                        log = self.logs[(t, p)]
+                        base = len(log)
+                        log.extend(v for _, v in decode_batches(rs))
+                        po.append((p, base))
+                    out.append((t, po))
+                w = W().arr(out, lambda w, tp: w.s(tp[0]).arr(
+                    tp[1], lambda w, pb: w.i32(pb[0]).i16(0).i64(pb[1]).i64(-1))).i32(0)
+                return bytes(w.b)
+            if api == 2:  # ListOffsets v1
+                r.i32()
+                topics = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.i64()))))
+                w = W().arr(topics, lambda w, tp: w.s(tp[0]).arr(
+                    tp[1], lambda w, pt: w.i32(pt[0]).i16(0).i64(-1).i64(
+                        len(self.logs[(tp[0], pt[0])]) if pt[1] == -1 else 0)))
+                return bytes(w.b)
+            if api == 1:  # Fetch v4
+                r.i32(), r.i32(), r.i32(), r.i32(), r.i8()
+                topics = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.i64(), r.i32()))))
+                w = W().i32(0)
+
+                def part(w, pt, t):
+                    p, off, _mx = pt
+                    log = self.logs[(t, p)]
+                    vals = log[off:off + 500]
+                    rs = encode_batch(vals, base_offset=off) if vals else b""
+                    w.i32(p).i16(0).i64(len(log)).i64(len(log)).i32(0).by(rs)
+
+                w.arr(topics, lambda w, tp: w.s(tp[0]).arr(tp[1], lambda w, pt: part(w, pt,
+                                                                                     tp[0])))
+                return bytes(w.b)
+        raise ValueError(f"unsupported api {api}")
