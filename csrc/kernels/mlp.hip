@@ -1,0 +1,348 @@
+// NN learner: fused MLP training and inference on the fp32 matrix cores.
+//
+// Reference: the NN learner runs DL4J MultiLayerNetwork.fit on ND4J/OpenBLAS — GEMM,
+// the row-wise bias broadcast that crashed (BaseLayer.preOutputWithPreNorm → doRowWise →
+// execBroadcast, hs_err_pid77107.log:97-110), activations and an SGD step, each a
+// separate native call per layer per mini-batch.
+//
+// Design (one kernel per protocol round):
+// * one workgroup (4 waves) = one virtual spoke. It copies the round-start model into
+//   LDS and runs plain mini-batch SGD over its row range: forward, loss gradient,
+//   backward and the weight update never leave LDS/registers;
+// * every GEMM-shaped step is v_mfma_f32_32x32x2_f32 on 32-row mini-batches:
+//     forward   H_{l+1} = act(H_l · W_lᵀ + b_l)     (bias + ReLU fused in the epilogue)
+//     backward  dH_l    = (dZ_{l+1} · W_l) ⊙ [H_l > 0]
+//               W_l    -= η · dZ_{l+1}ᵀ · H_l       (applied straight from the MFMA
+//                                                     accumulators — each element has
+//                                                     exactly one owner lane)
+//   widths are zero-padded to 32; padding stays exactly zero through every step;
+// * LDS row strides are padded to an odd number of floats so the 32 lanes of an MFMA
+//   operand column hit distinct banks;
+// * round end: each spoke adds its model delta to a device accumulator and an apply
+//   pass averages the deltas of the active spokes (omldm_multiclass_apply) — the
+//   intra-GPU hub; across GPUs the protocol ships the flat parameter vector over RCCL.
+#include "common.h"
+
+namespace omldm {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kMB = 32;
+constexpr int kMaxLayers = 4;
+
+struct MlpDesc {
+  int L, task, K;
+  int n[kMaxLayers + 1], np[kMaxLayers + 1];
+  int woff[kMaxLayers], boff[kMaxLayers];
+  int lw[kMaxLayers], lb[kMaxLayers], ldw[kMaxLayers];
+  int lh[kMaxLayers + 1], ldh[kMaxLayers + 1];
+  int lg0, lg1, ldg, ly, total;
+};
+
+// C[32×32] = A[32×K]·B[K×32] with A(i,k) = a[i·ars + k·acs], B(k,j) = b[k·brs + j·bcs].
+// Operand map (v_mfma_f32_32x32x2_f32): lane supplies A(lane&31, k + lane>>5) and
+// B(k + lane>>5, lane&31); result reg q of lane is C(row(q, lane), lane&31).
+__device__ __forceinline__ f32x16 wave_gemm32(const float* a, int ars, int acs, const float* b,
+                                              int brs, int bcs, int K) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, kh = lane >> 5;
+  f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float* ap = a + r * ars + kh * acs;
+  const float* bp = b + kh * brs + r * bcs;
+  for (int k = 0; k < K; k += 2) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[k * acs], bp[k * brs], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ int crow(int q, int lane) {
+  return (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+}
+
+__device__ void load_model(const float* __restrict__ w, float* sm, const MlpDesc& g) {
+  for (int l = 0; l < g.L; ++l) {
+    const int rows = g.np[l + 1], ld = g.ldw[l], nin = g.n[l], nout = g.n[l + 1];
+    float* W = sm + g.lw[l];
+    for (int i = threadIdx.x; i < rows * ld; i += blockDim.x) {
+      const int o = i / ld, c = i - o * ld;
+      W[i] = (o < nout && c < nin) ? w[g.woff[l] + o * nin + c] : 0.f;
+    }
+    for (int o = threadIdx.x; o < rows; o += blockDim.x)
+      sm[g.lb[l] + o] = o < nout ? w[g.boff[l] + o] : 0.f;
+  }
+}
+
+// Forward of one 32-row tile already staged in H_0; H_L holds the logits.
+__device__ void forward(float* sm, const MlpDesc& g) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int l = 0; l < g.L; ++l) {
+    const float* H = sm + g.lh[l];
+    float* Ho = sm + g.lh[l + 1];
+    const float* W = sm + g.lw[l];
+    const float* bs = sm + g.lb[l];
+    const int nt = g.np[l + 1] >> 5, ldo = g.ldh[l + 1];
+    const bool relu = l + 1 < g.L;
+    for (int t = wave; t < nt; t += 4) {
+      const f32x16 acc = wave_gemm32(H, g.ldh[l], 1, W + t * 32 * g.ldw[l], 1, g.ldw[l], g.np[l]);
+      const int col = t * 32 + (lane & 31);
+      const float bias = bs[col];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        float v = acc[q] + bias;
+        if (relu) v = fmaxf(v, 0.f);
+        Ho[crow(q, lane) * ldo + col] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__device__ void stage_rows(const float* __restrict__ x, long long r0, long long r1, float* sm,
+                           const MlpDesc& g) {
+  const int np0 = g.np[0], n0 = g.n[0], ld = g.ldh[0];
+  float* H = sm + g.lh[0];
+  for (int i = threadIdx.x; i < kMB * np0; i += blockDim.x) {
+    const int r = i / np0, c = i - r * np0;
+    const long long row = r0 + r;
+    H[r * ld + c] = (row < r1 && c < n0) ? x[row * n0 + c] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict__ w,
+                                                        const float* __restrict__ x,
+                                                        const float* __restrict__ yv, long long B,
+                                                        int R, float lr, float* __restrict__ dacc,
+                                                        float* __restrict__ stats, MlpDesc g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const long long r0 = (long long)blockIdx.x * R;
+  const long long r1 = min(B, r0 + R);
+  if (r0 >= B) return;
+  load_model(w, sm, g);
+  float loss = 0.f, corr = 0.f, nv = 0.f;
+  const int L = g.L, npL = g.np[L];
+  for (long long m0 = r0; m0 < r1; m0 += kMB) {
+    stage_rows(x, m0, r1, sm, g);
+    if (tid < kMB) {
+      const long long row = m0 + tid;
+      sm[g.ly + tid] = row < r1 ? yv[row] : __builtin_nanf("");
+    }
+    __syncthreads();
+    forward(sm, g);
+    // ---- loss gradient dZ_L (one thread per row)
+    bool valid = false;
+    if (tid < kMB) {
+      const float y = sm[g.ly + tid];
+      valid = !__builtin_isnan(y);
+      const float* o = sm + g.lh[L] + tid * g.ldh[L];
+      float* G = sm + g.lg0 + tid * g.ldg;
+      for (int k = 0; k < npL; ++k) G[k] = 0.f;
+      if (valid) {
+        if (g.task == 0) {  // regression, squared error (sum)
+          const float e = o[0] - y;
+          G[0] = 2.f * e;
+          loss += e * e;
+        } else if (g.task == 1) {  // binary logistic on ±1 / {0,1} labels
+          const float t = y > 0.f ? 1.f : 0.f, z = o[0];
+          G[0] = 1.f / (1.f + __expf(-z)) - t;
+          loss += fmaxf(z, 0.f) - z * t + log1pf(__expf(-fabsf(z)));
+          corr += ((z >= 0.f) == (t > 0.f)) ? 1.f : 0.f;
+        } else {  // multiclass softmax cross-entropy
+          int yi = (int)y;
+          yi = yi < 0 ? 0 : (yi >= g.K ? g.K - 1 : yi);
+          float m = o[0];
+          int am = 0;
+          for (int k = 1; k < g.K; ++k)
+            if (o[k] > m) {
+              m = o[k];
+              am = k;
+            }
+          float se = 0.f;
+          for (int k = 0; k < g.K; ++k) se += __expf(o[k] - m);
+          const float inv = 1.f / se;
+          for (int k = 0; k < g.K; ++k) G[k] = __expf(o[k] - m) * inv - (k == yi ? 1.f : 0.f);
+          loss += -(o[yi] - m - __logf(se));
+          corr += am == yi ? 1.f : 0.f;
+        }
+        nv += 1.f;
+      }
+    }
+    const int cnt = __syncthreads_count(valid ? 1 : 0);
+    if (cnt == 0) continue;
+    const float eta = lr / (float)cnt;
+    int gcur = g.lg0, gnext = g.lg1;
+    for (int l = L - 1; l >= 0; --l) {
+      const float* Gc = sm + gcur;
+      float* W = sm + g.lw[l];
+      const float* H = sm + g.lh[l];
+      const int ldw = g.ldw[l], ldh = g.ldh[l], nin = g.np[l], nout = g.np[l + 1];
+      if (l > 0) {  // dH_l = (dZ · W_l) ⊙ relu'(H_l)
+        float* Gn = sm + gnext;
+        for (int t = wave; t < (nin >> 5); t += 4) {
+          const f32x16 acc = wave_gemm32(Gc, g.ldg, 1, W + t * 32, ldw, 1, nout);
+          const int col = t * 32 + (lane & 31);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int row = crow(q, lane);
+            Gn[row * g.ldg + col] = H[row * ldh + col] > 0.f ? acc[q] : 0.f;
+          }
+        }
+      }
+      __syncthreads();  // W_l fully read before it is updated
+      const int ntc = nin >> 5, nto = nout >> 5;
+      for (int t = wave; t < nto * ntc; t += 4) {
+        const int to = t / ntc, tc = t - to * ntc;
+        const f32x16 acc = wave_gemm32(Gc + to * 32, 1, g.ldg, H + tc * 32, ldh, 1, kMB);
+        const int c = tc * 32 + (lane & 31);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int o = to * 32 + crow(q, lane);
+          W[o * ldw + c] -= eta * acc[q];
+        }
+      }
+      for (int o = tid; o < nout; o += blockDim.x) {
+        float s = 0.f;
+        for (int i = 0; i < kMB; ++i) s += Gc[i * g.ldg + o];
+        sm[g.lb[l] + o] -= eta * s;
+      }
+      __syncthreads();
+      const int tmp = gcur;
+      gcur = gnext;
+      gnext = tmp;
+    }
+  }
+  // ---- round end: Δ = W_spoke − W_0 into the accumulator
+  for (int l = 0; l < L; ++l) {
+    const int nin = g.n[l], nout = g.n[l + 1], ld = g.ldw[l];
+    const float* W = sm + g.lw[l];
+    for (int i = tid; i < nout * nin; i += blockDim.x) {
+      const int o = i / nin, c = i - o * nin;
+      const float d = W[o * ld + c] - w[g.woff[l] + i];
+      if (d != 0.f) atomicAdd(&dacc[g.woff[l] + i], d);
+    }
+    for (int o = tid; o < nout; o += blockDim.x) {
+      const float d = sm[g.lb[l] + o] - w[g.boff[l] + o];
+      if (d != 0.f) atomicAdd(&dacc[g.boff[l] + o], d);
+    }
+  }
+  if (wave == 0) {
+    loss = wave_sum(loss);
+    corr = wave_sum(corr);
+    nv = wave_sum(nv);
+    if (lane == 0 && nv > 0.f) {
+      atomicAdd(&stats[0], loss);
+      atomicAdd(&stats[1], nv);
+      atomicAdd(&stats[2], corr);
+      atomicAdd(&stats[3], 1.f);
+    }
+  }
+}
+
+// Inference: every block stages the model once and walks 32-row tiles (grid-stride).
+__global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restrict__ w,
+                                                          const float* __restrict__ x,
+                                                          long long B, float* __restrict__ out,
+                                                          MlpDesc g) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  load_model(w, sm, g);
+  const int L = g.L;
+  for (long long m0 = (long long)blockIdx.x * kMB; m0 < B; m0 += (long long)gridDim.x * kMB) {
+    __syncthreads();  // previous tile's H_L consumed
+    stage_rows(x, m0, B, sm, g);
+    __syncthreads();
+    forward(sm, g);
+    const float* o = sm + g.lh[L];
+    for (int i = threadIdx.x; i < kMB * g.K; i += blockDim.x) {
+      const int r = i / g.K, k = i - r * g.K;
+      if (m0 + r < B) out[(m0 + r) * g.K + k] = o[r * g.ldh[L] + k];
+    }
+  }
+}
+
+static int make_desc(int L, const int* widths, int task, MlpDesc* g) {
+  if (L < 1 || L > kMaxLayers) return -1;
+  *g = MlpDesc{};
+  g->L = L;
+  g->task = task;
+  g->K = widths[L];
+  int off = 0;
+  for (int l = 0; l <= L; ++l) {
+    if (widths[l] < 1) return -1;
+    g->n[l] = widths[l];
+    g->np[l] = (widths[l] + 31) & ~31;
+  }
+  for (int l = 0; l < L; ++l) {  // flat parameter layout: W_l [n_{l+1} × n_l], b_l
+    g->woff[l] = off;
+    off += g->n[l + 1] * g->n[l];
+    g->boff[l] = off;
+    off += g->n[l + 1];
+  }
+  int p = 0, maxnp = 0;
+  for (int l = 0; l < L; ++l) {
+    g->ldw[l] = g->np[l] + 1;
+    g->lw[l] = p;
+    p += g->np[l + 1] * g->ldw[l];
+    g->lb[l] = p;
+    p += g->np[l + 1];
+  }
+  for (int l = 0; l <= L; ++l) {
+    g->ldh[l] = g->np[l] + 1;
+    g->lh[l] = p;
+    p += kMB * g->ldh[l];
+    if (g->np[l] > maxnp) maxnp = g->np[l];
+  }
+  g->ldg = maxnp + 1;
+  g->lg0 = p;
+  p += kMB * g->ldg;
+  g->lg1 = p;
+  p += kMB * g->ldg;
+  g->ly = p;
+  p += kMB;
+  g->total = p;
+  return 0;
+}
+
+}  // namespace omldm
+
+using namespace omldm;
+
+// LDS bytes the fused kernels need for this layer stack (host-side feasibility check).
+OMLDM_API long long omldm_mlp_lds_bytes(int L, const int* widths) {
+  MlpDesc g;
+  if (make_desc(L, widths, 0, &g)) return -1;
+  return (long long)g.total * 4;
+}
+
+// One protocol round: S spokes × R rows (spoke s owns rows [sR, sR+R)); task 0 regression,
+// 1 binary logistic, 2 softmax. dacc[nparams] += Σ_s Δ_s; stats[0..3] += loss, n, correct,
+// active spokes. Follow with omldm_multiclass_apply(w, dacc, nparams, stats+3).
+OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, long long B, int R,
+                              int S, int L, const int* widths, int task, float lr, float* dacc,
+                              float* stats, void* stream) {
+  if (B <= 0 || S <= 0) return 0;
+  if (R <= 0 || (long long)R * S < B) return -3;
+  MlpDesc g;
+  if (make_desc(L, widths, task, &g)) return -1;
+  const size_t lds = (size_t)g.total * 4;
+  if (lds > 160 * 1024) return -2;
+  int e = check_dyn_lds((const void*)mlp_round_kernel, lds);
+  if (e) return e;
+  hipLaunchKernelGGL(mlp_round_kernel, dim3(S), dim3(256), lds, (hipStream_t)stream, w, x, y, B,
+                     R, lr, dacc, stats, g);
+  return (int)hipGetLastError();
+}
+
+OMLDM_API int omldm_mlp_forward(const float* w, const float* x, long long B, int L,
+                                const int* widths, float* out, void* stream) {
+  if (B <= 0) return 0;
+  MlpDesc g;
+  if (make_desc(L, widths, 0, &g)) return -1;
+  const size_t lds = (size_t)g.total * 4;
+  if (lds > 160 * 1024) return -2;
+  int e = check_dyn_lds((const void*)mlp_forward_kernel, lds);
+  if (e) return e;
+  long long tiles = (B + kMB - 1) / kMB;
+  int blocks = (int)(tiles < 1024 ? tiles : 1024);
+  hipLaunchKernelGGL(mlp_forward_kernel, dim3(blocks), dim3(256), lds, (hipStream_t)stream, w, x,
+                     B, out, g);
+  return (int)hipGetLastError();
+}

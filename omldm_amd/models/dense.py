@@ -218,12 +218,20 @@ class MultiClassPA(Learner):
 
 # ------------------------------------------------------------------------------ NN
 class NN(Learner):
-    """Multi-layer perceptron trained by mini-batch SGD (the reference's DL4J
-    MultiLayerNetwork path, hs_err_pid77107.log:97-110). Parameters live in ONE flat
-    fp32 buffer (layer weights are views), which is the protocols' state vector."""
+    """Multi-layer perceptron (ReLU hidden layers) trained by mini-batch SGD — the
+    reference's DL4J MultiLayerNetwork path (hs_err_pid77107.log:97-110).
+
+    A round runs S virtual spokes (one workgroup each, csrc/kernels/mlp.hip): spoke s does
+    32-row mini-batch SGD over its rows from the round-start model entirely in LDS on the
+    fp32 matrix cores; the spokes' models are then averaged (intra-GPU hub). Parameters
+    live in ONE flat fp32 buffer (W_0, b_0, W_1, b_1, … row-major) — the protocols' state
+    vector. Loss: squared error (task=regression), logistic (nClasses ≤ 1, labels ±1 or
+    {0,1}) or softmax cross-entropy (nClasses = K ≥ 2). At most 4 layers whose padded
+    widths fit the 160 KB LDS of a CU (e.g. 128-wide hidden layers)."""
 
     NAME = "NN"
     merge_mode = "mean"
+    MB = D.MLP_MB
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -235,77 +243,57 @@ class NN(Learner):
         self.K = hp_int(h, "nClasses", 1)   # 1: binary (±1 or {0,1}) / regression output
         self.TASK = "regression" if str(h.get("task", "classification")) == "regression" \
             else "classification"
+        self.task_id = 0 if self.TASK == "regression" else (1 if self.K <= 1 else 2)
         self.lr = hp_float(h, "learningRate", 0.05)
-        self.mb = hp_int(h, "miniBatchSize", 256)
-        sizes = [self.d] + [int(v) for v in hidden] + [max(1, self.K)]
-        shapes = []
-        for a, b in zip(sizes[:-1], sizes[1:]):
-            shapes += [(b, a), (b,)]
-        total = sum(math.prod(s) for s in shapes)
+        self.widths = [self.d] + [int(v) for v in hidden] + [max(1, self.K)]
+        if len(self.widths) - 1 > D.MLP_MAX_LAYERS:
+            raise ValueError(f"NN supports at most {D.MLP_MAX_LAYERS} layers")
+        self.shapes = []
+        for a, b in zip(self.widths[:-1], self.widths[1:]):
+            self.shapes += [(b, a), (b,)]
+        total = sum(math.prod(s) for s in self.shapes)
         g = torch.Generator().manual_seed(hp_int(h, "seed", 25))
         flat = torch.zeros(total, dtype=torch.float32)
         o = 0
-        for s in shapes:
+        for s in self.shapes:
             n = math.prod(s)
             if len(s) == 2:
                 flat[o:o + n] = torch.randn(n, generator=g) * math.sqrt(2.0 / s[1])
             o += n
-        self.flat = flat.to(self.device).requires_grad_(True)
-        self.shapes = shapes
-
-    def _layers(self):
-        o = 0
-        out = []
-        for s in self.shapes:
-            n = math.prod(s)
-            out.append(self.flat[o:o + n].view(s))
-            o += n
-        return out
-
-    def forward(self, x):
-        ps = self._layers()
-        h = x
-        for i in range(0, len(ps), 2):
-            h = torch.nn.functional.linear(h, ps[i], ps[i + 1])
-            if i + 2 < len(ps):
-                h = torch.relu(h)
-        return h
-
-    def _loss(self, out, y):
-        if self.TASK == "regression":
-            return torch.nn.functional.mse_loss(out.squeeze(1), y, reduction="sum")
-        if self.K <= 1:
-            t = (y > 0).float()
-            return torch.nn.functional.binary_cross_entropy_with_logits(out.squeeze(1), t,
-                                                                        reduction="sum")
-        return torch.nn.functional.cross_entropy(out, y.long(), reduction="sum")
+        self.flat = flat.to(self.device)
+        self.dacc = torch.zeros_like(self.flat)
+        self.st = torch.zeros(8, dtype=torch.float32, device=self.device)
+        if self.device.type == "cuda" and D.mlp_lds_bytes(self.widths) > 160 * 1024:
+            raise ValueError("NN layer widths exceed the LDS budget of the fused kernel")
 
     def fit(self, batch, ctx):
-        ok = ~torch.isnan(batch.y)
-        x = batch.num.float()[ok]
-        y = batch.y[ok]
-        n = x.shape[0]
-        tot = torch.zeros((), device=self.device)
-        for a in range(0, n, self.mb):
-            xb, yb = x[a:a + self.mb], y[a:a + self.mb]
-            loss = self._loss(self.forward(xb), yb)
-            g, = torch.autograd.grad(loss, self.flat)
-            with torch.no_grad():
-                self.flat.sub_(g, alpha=self.lr / xb.shape[0])
-            tot = tot + loss.detach()
-        self.cum[0] += tot
-        self.cum[1] += n
+        B = batch.B
+        if B == 0:
+            return
+        S = max(1, ctx.spokes)
+        per = -(-B // S)
+        R = -(-per // self.MB) * self.MB
+        S = -(-B // R)
+        D.mlp_round(self.flat, batch.num, batch.y, R, S, self.widths, self.task_id, self.lr,
+                    self.dacc, self.st)
+        D.multiclass_apply(self.flat, self.dacc, self.st[3:4])
+        self.cum[0] += self.st[0]
+        self.cum[1] += self.st[1]
+        self.cum[2] += self.st[1] - self.st[2] if self.task_id else 0.0
+        self.st.zero_()
 
     def state_vector(self):
-        return self.flat.data
+        return self.flat
+
+    def forward(self, x):
+        return D.mlp_forward(self.flat, x.float(), self.widths)
 
     def predict(self, batch):
-        with torch.no_grad():
-            out = self.forward(batch.num.float())
-        if self.TASK == "regression":
-            return out.squeeze(1)
-        if self.K <= 1:
-            return torch.where(out.squeeze(1) >= 0, 1.0, -1.0)
+        out = self.forward(batch.num)
+        if self.task_id == 0:
+            return out[:, 0]
+        if self.task_id == 1:
+            return torch.where(out[:, 0] >= 0, 1.0, -1.0)
         return out.argmax(1).float()
 
     def evaluate(self, batch):
@@ -313,17 +301,14 @@ class NN(Learner):
         if not bool(ok.any()):
             z = torch.zeros((), device=self.device)
             return z, z, 0
-        with torch.no_grad():
-            out = self.forward(batch.num.float()[ok])
-            y = batch.y[ok]
-            loss = self._loss(out, y)
-            if self.TASK == "regression":
-                score = ((out.squeeze(1) - y) ** 2).sum()
-            elif self.K <= 1:
-                score = ((out.squeeze(1) >= 0) == (y > 0)).float().sum()
-            else:
-                score = (out.argmax(1) == y.long()).float().sum()
+        out = self.forward(batch.num)[ok]
+        y = batch.y[ok]
+        _, loss, correct = D._mlp_grad_out(out, y, self.task_id, max(1, self.K))
+        score = loss if self.task_id == 0 else correct
         return loss, score, int(ok.sum())
+
+    def hyper_parameters(self):
+        return {**self.hyper, "learningRate": self.lr, "miniBatchSize": self.MB}
 
     def parameters_map(self):
         return {"layers": [list(s) for s in self.shapes], "nParams": int(self.flat.numel())}
@@ -384,7 +369,19 @@ class HT(Learner):
             node = torch.where(inner, nxt, node)
         return node
 
+    def _tree(self):
+        return [self.feat, self.thr, self.left, self.right, self.cc, self.S0, self.S1, self.S2,
+                self.lo, self.hi, self.since, self.nnodes]
+
     def fit(self, batch, ctx):
+        if self.device.type == "cuda":
+            # device path (csrc/kernels/hoeffding.hip): no host synchronisation per round
+            if batch.B:
+                D.ht_update(batch.num, batch.y, self.Cn, self.depth, self._tree(),
+                            self.cum[1:2])
+                D.ht_split(self.N, self.d, self.Cn, self.nb, float(self.grace), self.delta,
+                           self.tau, self._tree())
+            return
         ok = ~torch.isnan(batch.y)
         if not bool(ok.any()):
             return
@@ -463,6 +460,8 @@ class HT(Learner):
         return self.state
 
     def predict(self, batch):
+        if self.device.type == "cuda":
+            return D.ht_predict(batch.num, self.Cn, self.depth, self._tree())
         leaf = self._route(batch.num.float())
         return self.cc[leaf].argmax(1).float()
 

@@ -78,6 +78,125 @@ def multiclass_round(W: torch.Tensor, batch: HashedBatch, R: int, S: int, nclass
             batch.B, R, S, dim, nclass, variant, C, int(bias), ptr(dacc), ptr(stats))
 
 
+MLP_MB = 32          # mini-batch rows of the fused MLP kernel
+MLP_MAX_LAYERS = 4
+
+
+def _widths_arr(widths):
+    import ctypes
+
+    return (ctypes.c_int * len(widths))(*[int(v) for v in widths])
+
+
+def mlp_lds_bytes(widths: list[int]) -> int:
+    return int(native.hip().omldm_mlp_lds_bytes(len(widths) - 1, _widths_arr(widths)))
+
+
+def _mlp_unflatten(w: torch.Tensor, widths):
+    out, o = [], 0
+    for a, b in zip(widths[:-1], widths[1:]):
+        out.append((w[o:o + a * b].view(b, a), w[o + a * b:o + a * b + b]))
+        o += a * b + b
+    return out
+
+
+def mlp_forward_reference(w: torch.Tensor, x: torch.Tensor, widths) -> torch.Tensor:
+    h = x
+    layers = _mlp_unflatten(w, widths)
+    for i, (W, b) in enumerate(layers):
+        h = torch.nn.functional.linear(h, W, b)
+        if i + 1 < len(layers):
+            h = torch.relu(h)
+    return h
+
+
+def _mlp_grad_out(o: torch.Tensor, y: torch.Tensor, task: int, K: int):
+    """dLoss/dlogits (sum over rows) + (loss, correct) — same rules as the kernel."""
+    if task == 0:
+        e = o[:, 0] - y
+        g = torch.zeros_like(o)
+        g[:, 0] = 2 * e
+        return g, (e * e).sum(), torch.zeros((), device=o.device)
+    if task == 1:
+        t = (y > 0).float()
+        z = o[:, 0]
+        g = torch.zeros_like(o)
+        g[:, 0] = torch.sigmoid(z) - t
+        loss = (torch.clamp(z, min=0) - z * t + torch.log1p(torch.exp(-z.abs()))).sum()
+        return g, loss, ((z >= 0).float() == t).float().sum()
+    yi = y.long().clamp(0, K - 1)
+    p = torch.softmax(o, 1)
+    g = p - torch.nn.functional.one_hot(yi, K).float()
+    loss = -torch.log_softmax(o, 1).gather(1, yi.unsqueeze(1)).sum()
+    return g, loss, (o.argmax(1) == yi).float().sum()
+
+
+def mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats) -> None:
+    """CPU mirror of mlp_round_kernel: spoke s runs 32-row mini-batch SGD over rows
+    [sR, sR+R) from the round-start model; dacc += Σ Δ_s; stats += (loss, n, correct,
+    active spokes)."""
+    B = x.shape[0]
+    K = widths[-1]
+    for s in range(S):
+        r0, r1 = s * R, min(B, s * R + R)
+        if r0 >= B:
+            break
+        ws = w.detach().clone()
+        loss_s, n_s, c_s = 0.0, 0, 0.0
+        for m0 in range(r0, r1, MLP_MB):
+            xb, yb = x[m0:min(r1, m0 + MLP_MB)], y[m0:min(r1, m0 + MLP_MB)]
+            ok = ~torch.isnan(yb)
+            cnt = int(ok.sum())
+            if cnt == 0:
+                continue
+            wv = ws.clone().requires_grad_(True)
+            o = mlp_forward_reference(wv, xb[ok], widths)
+            g, ls, cs = _mlp_grad_out(o.detach(), yb[ok], task, K)
+            gw, = torch.autograd.grad(o, wv, grad_outputs=g)
+            ws -= (lr / cnt) * gw
+            loss_s += float(ls)
+            c_s += float(cs)
+            n_s += cnt
+        dacc += ws - w
+        if n_s:
+            stats[0] += loss_s
+            stats[1] += n_s
+            stats[2] += c_s
+            stats[3] += 1
+
+
+def mlp_round(w: torch.Tensor, x: torch.Tensor, y: torch.Tensor, R: int, S: int,
+              widths: list[int], task: int, lr: float, dacc: torch.Tensor,
+              stats: torch.Tensor) -> None:
+    B = x.shape[0]
+    if B == 0:
+        return
+    x = x.float().contiguous()
+    y = y.float().contiguous()
+    if len(widths) - 1 > MLP_MAX_LAYERS:
+        raise ValueError(f"NN: at most {MLP_MAX_LAYERS} layers on the fused kernel")
+    if x.is_cuda:
+        check(native.hip().omldm_mlp_round(ptr(w), ptr(x), ptr(y), B, R, S, len(widths) - 1,
+                                           _widths_arr(widths), task, lr, ptr(dacc), ptr(stats),
+                                           native.stream_of(x)), "omldm_mlp_round")
+    else:
+        mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats)
+
+
+def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int]) -> torch.Tensor:
+    B = x.shape[0]
+    out = torch.empty((B, widths[-1]), dtype=torch.float32, device=x.device)
+    if B == 0:
+        return out
+    x = x.float().contiguous()
+    if x.is_cuda:
+        check(native.hip().omldm_mlp_forward(ptr(w), ptr(x), B, len(widths) - 1,
+                                             _widths_arr(widths), ptr(out),
+                                             native.stream_of(x)), "omldm_mlp_forward")
+        return out
+    return mlp_forward_reference(w, x, widths)
+
+
 def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor) -> None:
     if W.is_cuda:
         check(native.hip().omldm_multiclass_apply(ptr(W), ptr(dacc), W.numel(), ptr(nact),
@@ -87,3 +206,35 @@ def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor) ->
         if n > 0:
             W.add_(dacc / n)
         dacc.zero_()
+
+
+def _tree_ptrs(tree: list[torch.Tensor]):
+    import ctypes
+
+    return (ctypes.c_void_p * len(tree))(*[t.data_ptr() for t in tree])
+
+
+def ht_update(x: torch.Tensor, y: torch.Tensor, C: int, depth: int, tree: list[torch.Tensor],
+              nfit: torch.Tensor) -> None:
+    """Route rows to leaves and scatter their Gaussian statistics (device only)."""
+    B, d = x.shape
+    x = x.float().contiguous()
+    y = y.float().contiguous()
+    check(native.hip().omldm_ht_update(ptr(x), ptr(y), B, d, C, depth, _tree_ptrs(tree),
+                                       ptr(nfit), native.stream_of(x)), "omldm_ht_update")
+
+
+def ht_split(N: int, d: int, C: int, nb: int, grace: float, delta: float, tau: float,
+             tree: list[torch.Tensor]) -> None:
+    check(native.hip().omldm_ht_split(N, d, C, nb, grace, delta, tau, _tree_ptrs(tree),
+                                      native.stream_of(tree[0])), "omldm_ht_split")
+
+
+def ht_predict(x: torch.Tensor, C: int, depth: int, tree: list[torch.Tensor]) -> torch.Tensor:
+    B, d = x.shape
+    out = torch.empty(B, dtype=torch.float32, device=x.device)
+    if B:
+        x = x.float().contiguous()
+        check(native.hip().omldm_ht_predict(ptr(x), B, d, C, depth, _tree_ptrs(tree), ptr(out),
+                                            native.stream_of(x)), "omldm_ht_predict")
+    return out

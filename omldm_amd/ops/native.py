@@ -57,6 +57,18 @@ HIP_SIGS = [
     ("omldm_multiclass_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32, f32,
                                      i32, vp, vp, i32, vp]),
     ("omldm_multiclass_apply", i32, [vp, vp, i64, vp, vp]),
+    ("omldm_mlp_lds_bytes", i64, [i32, vp]),
+    ("omldm_mlp_round", i32, [vp, vp, vp, i64, i32, i32, i32, vp, i32, f32, vp, vp, vp]),
+    ("omldm_mlp_forward", i32, [vp, vp, i64, i32, vp, vp, vp]),
+    ("omldm_ht_update", i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp]),
+    ("omldm_ht_split", i32, [i32, i32, i32, i32, f32, f32, f32, vp, vp]),
+    ("omldm_ht_predict", i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
+    ("omldm_drift_norms", i32, [vp, vp, i64, f32, vp, vp]),
+    ("omldm_fold_reload", i32, [vp, vp, f32, vp, i64, vp]),
+    ("omldm_elastic_pre", i32, [vp, vp, vp, vp, i64, vp]),
+    ("omldm_elastic_post", i32, [vp, vp, vp, vp, f32, i64, vp]),
+    ("omldm_async_push", i32, [vp, vp, vp, vp, vp, i64, vp]),
+    ("omldm_async_pull", i32, [vp, vp, vp, vp, vp, f32, i64, vp]),
     ("omldm_stream_create_cumask", vp, [i32]),
     ("omldm_host_device_ptr", vp, [vp]),
     ("omldm_stream_destroy", i32, [vp]),

@@ -174,3 +174,86 @@ def test_engine_on_gpu(cuda):
     job = Job(cfg, Comm(), cuda).run()
     assert job.terminated and job.pipes[1].learner.running_totals()["fitted"] > 0
     assert json.loads(br.records("performance")[-1])["statistics"][0]["fitted"] > 0
+
+
+def _mlp_case(widths, task, B, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    n = sum(a * b + b for a, b in zip(widths[:-1], widths[1:]))
+    w = torch.randn(n, generator=g) * 0.3
+    x = torch.randn(B, widths[0], generator=g)
+    if task == 0:
+        y = x[:, 0] * 0.5 - x[:, 1]
+    elif task == 1:
+        y = torch.where(x[:, 0] + x[:, 2] > 0, 1.0, -1.0)
+    else:
+        y = (x[:, :widths[-1]].argmax(1)).float()
+    y[5] = float("nan")  # excluded row inside a mini-batch
+    return w, x, y
+
+
+def test_mlp_reference_learns():
+    widths = [6, 16, 1]
+    w, x, y = _mlp_case(widths, 1, 2048)
+    dacc, st = torch.zeros_like(w), torch.zeros(8)
+    for _ in range(3):
+        D.mlp_round_reference(w, x, y, 256, 8, widths, 1, 0.2, dacc, st)
+        w += dacc / st[3]
+        dacc.zero_()
+        st.zero_()
+    out = D.mlp_forward_reference(w, x, widths)[:, 0]
+    ok = ~torch.isnan(y)
+    assert ((out[ok] >= 0) == (y[ok] > 0)).float().mean() > 0.9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("widths,task", [([13, 32, 32, 1], 1), ([13, 32, 1], 0),
+                                         ([40, 64, 48, 5], 2), ([7, 100, 3], 2)])
+def test_hip_mlp_round_vs_reference(cuda, widths, task):
+    B, R, S = 1000, 96, 11
+    w, x, y = _mlp_case(widths, task, B, seed=len(widths) + task)
+    lr = 0.05
+    d_ref, s_ref = torch.zeros_like(w), torch.zeros(8)
+    D.mlp_round_reference(w, x, y, R, S, widths, task, lr, d_ref, s_ref)
+    wd, d_gpu, s_gpu = w.to(cuda), torch.zeros_like(w, device=cuda), torch.zeros(8, device=cuda)
+    D.mlp_round(wd, x.to(cuda), y.to(cuda), R, S, widths, task, lr, d_gpu, s_gpu)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(d_gpu.cpu(), d_ref, rtol=2e-3, atol=2e-4)
+    torch.testing.assert_close(s_gpu.cpu()[:4], s_ref[:4], rtol=2e-3, atol=1e-2)
+    out = D.mlp_forward(wd, x.to(cuda), widths)
+    torch.testing.assert_close(out.cpu(), D.mlp_forward_reference(w, x, widths), rtol=1e-4,
+                               atol=1e-4)
+
+
+def _ht_data(n, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, 13, generator=g)
+    y = ((x[:, 3] > 0.3).long() + (x[:, 7] > 0).long()).float()  # 3 classes, axis-aligned
+    return x, y
+
+
+@pytest.mark.gpu
+def test_hip_hoeffding_tree(cuda):
+    from omldm_amd.api.batch import HashedBatch
+
+    hyper = {"nClasses": 3, "gracePeriod": 200}
+    cpu = make_learner("HT", hyper, SP, "cpu")
+    gpu = make_learner("HT", hyper, SP, cuda)
+    x, y = _ht_data(150)  # below the grace period: statistics only, no split yet
+    b = HashedBatch(x, torch.zeros((150, 0), dtype=torch.int32), y)
+    cpu.fit(b, RoundContext())
+    gpu.fit(b.to(cuda), RoundContext())
+    torch.cuda.synchronize()
+    for name in ("cc", "S0", "S1", "S2", "lo", "hi", "since"):
+        torch.testing.assert_close(getattr(gpu, name).cpu(), getattr(cpu, name), rtol=1e-5,
+                                   atol=1e-4)
+    for s in range(1, 30):
+        x, y = _ht_data(400, seed=s)
+        b = HashedBatch(x, torch.zeros((400, 0), dtype=torch.int32), y)
+        cpu.fit(b, RoundContext())
+        gpu.fit(b.to(cuda), RoundContext())
+    x, y = _ht_data(2000, seed=99)
+    b = HashedBatch(x, torch.zeros((2000, 0), dtype=torch.int32), y)
+    acc_g = (gpu.predict(b.to(cuda)).cpu() == y).float().mean()
+    acc_c = (cpu.predict(b) == y).float().mean()
+    assert int(gpu.nnodes.item()) > 1
+    assert acc_g > 0.85 and acc_c > 0.85, (acc_g, acc_c)
