@@ -57,8 +57,9 @@ inline bool cat_at(const void* cat, int dc, long long t, int j, int dn, int dim,
 
 }  // namespace
 
-// w: fp32 [dim] or bf16 [dim] (w_bf16); num: fp32 [B, dn]. stats: [S, 6].
-// dacc: [dim + 1] accumulates σ·Δ/P (+ σ/P at [dim]), exactly like the kernel.
+// w: fp32 [dim] or bf16 [dim] (w_bf16); num: fp32 [B, dn]. stats: per-spoke [S, 6]
+// (loss, n, mistakes, sq_err, σ, -). dacc: [dim + 2] accumulates σ·Δ/P, plus Σσ/P at
+// [dim] and Σ1/P at [dim + 1], exactly like the kernel.
 OMLDM_HOST_API int omldm_cpu_linear_round(const void* w, int w_bf16, const float* num, int dn,
                                           const void* cat, int dc, const float* y, int B,
                                           int R, int S, float* dacc, int dim, float* stats,

@@ -72,6 +72,13 @@ class Job:
         self.counters = {"records": 0, "invalid": 0, "predictions": 0, "responses": 0,
                          "dropped_buffer": 0}
         self._flags = torch.zeros(3, dtype=torch.float32, device=self._coll_device())
+        from omldm_amd.utils.fault import FaultPlan, Watchdog
+
+        self.faults = FaultPlan.from_config(cfg, self.rank)
+        if self.faults:
+            comm.fault = self.faults
+        self.watchdog = Watchdog(cfg.watchdogTimeout / 1000.0, self.rank) \
+            if cfg.watchdogTimeout > 0 else None
         self.checkpointer = None
         if cfg.checkpointing or cfg.restore:
             from omldm_amd.utils.checkpoint import Checkpointer
@@ -170,6 +177,10 @@ class Job:
     # --------------------------------------------------------------------- tick
     def tick(self) -> None:
         t0 = time.time()
+        if self.faults:
+            self.faults.on_tick(self.ticks)
+        if self.watchdog is not None:
+            self.watchdog.beat()
         n_ctrl, queries = self._control()
         recs = self._poll()
         n_local = len(recs)
@@ -229,6 +240,8 @@ class Job:
             self.tick()
         for p in self.pipes.values():
             p.protocol.finalize()
+        if self.watchdog is not None:
+            self.watchdog.stop()
         return self
 
     # --------------------------------------------------------------- checkpoint
@@ -244,7 +257,8 @@ class Job:
             sd["requests"] = self.req_in.state_dict()
         return sd
 
-    def load_state_dict(self, sd: dict, same_world: bool = True) -> None:
+    def load_state_dict(self, sd: dict, same_world: bool = True,
+                        consumer_offsets: dict | None = None) -> None:
         for pid, psd in sd.get("pipelines", {}).items():
             req = Request.from_json(psd["request"])
             pipe = Pipeline(req, self.space, self.comm, self.device, self.spokes,
@@ -255,6 +269,9 @@ class Job:
         if same_world:  # partition ownership only matches at the same world size
             self.train_in.load_state_dict(sd["consumers"]["train"])
             self.fcst_in.load_state_dict(sd["consumers"]["forecast"])
+        elif consumer_offsets is not None:  # Consumer keeps only the partitions it owns
+            self.train_in.load_state_dict({"offsets": consumer_offsets["train"]})
+            self.fcst_in.load_state_dict({"offsets": consumer_offsets["forecast"]})
         self.record_buffer = list(sd.get("record_buffer", []))
         self.ticks = int(sd.get("ticks", 0))
         if self.rank == 0 and "pipeline_map" in sd:

@@ -49,10 +49,13 @@ class Comm:
         self.world = dist.get_world_size(group) if self.enabled else 1
         self.stats = CommStats()
         self.backend = dist.get_backend(group) if self.enabled else "none"
+        self.fault = None  # utils.fault.FaultPlan (tests): may drop this rank's messages
 
     # ------------------------------------------------------------ collectives
     def all_reduce_(self, t: torch.Tensor, tag: str = "sync", op=None, async_op=False):
         self.stats.add(tag, t.numel() * t.element_size(), t.numel() <= 64)
+        if self.fault is not None and self.fault.drop(tag):
+            t.zero_()  # lost message: the rank still joins, its contribution is gone
         if self.world == 1:
             return None
         return dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group, async_op=async_op)

@@ -82,8 +82,21 @@ class Checkpointer:
         d = os.path.join(self.root, f"ckpt-{idx:06d}")
         with open(os.path.join(d, "manifest.json")) as f:
             man = json.load(f)
-        src = self.rank % int(man["world"])
+        old_world = int(man["world"])
+        src = self.rank % old_world
         sd = torch.load(os.path.join(d, f"rank-{src}.pt"), map_location="cpu", weights_only=True)
-        job.load_state_dict(sd, same_world=int(man["world"]) == self.world)
+        if old_world == self.world:
+            job.load_state_dict(sd, same_world=True)
+        else:
+            # Re-scaled restore: partition ownership changes, so gather every old rank's
+            # consumer offsets (each partition had exactly one owner) and let the new
+            # owners resume from them — no record is trained twice or skipped.
+            offsets = {"train": {}, "forecast": {}}
+            for r in range(old_world):
+                o = sd if r == src else torch.load(os.path.join(d, f"rank-{r}.pt"),
+                                                   map_location="cpu", weights_only=True)
+                for k in offsets:
+                    offsets[k].update(o["consumers"][k].get("offsets", {}))
+            job.load_state_dict(sd, same_world=False, consumer_offsets=offsets)
         self.n = idx + 1
         return True

@@ -63,6 +63,7 @@ class JobConfig:
     device: str = "auto"                  # auto | cuda | cpu
     maxTicks: int = 0                     # 0: until terminated (tests use a bound)
     restore: bool = False                 # restore from the latest checkpoint in stateBackend
+    watchdogTimeout: int = 0              # ms without a finished tick → abort + exit (0: off)
     parseThreads: int = 8
     extra: dict = field(default_factory=dict)
 
