@@ -33,12 +33,14 @@ import torch
 from omldm_amd.api.batch import FeatureSpace, HashedBatch
 from omldm_amd.api.schemas import Prediction, Request
 from omldm_amd.engine.holdout import HoldoutSet
+from omldm_amd.engine.model_store import ModelStore
 from omldm_amd.engine.pipeline import Pipeline
 from omldm_amd.engine.pipeline_map import ALL, PipelineMap
 from omldm_amd.engine import statistics as ST
 from omldm_amd.io.parse import OP_FORECASTING, OP_TRAINING, parse_records
 from omldm_amd.io.transport import Consumer, broker_for
 from omldm_amd.parallel.comm import Comm
+from omldm_amd.parallel.protocols import Synchronous
 from omldm_amd.utils.config import JobConfig
 from omldm_amd.utils import tracing
 
@@ -64,6 +66,7 @@ class Job:
         self.pmap = PipelineMap() if self.rank == 0 else None
         self.pipes: dict[int, Pipeline] = {}
         self.holdout = HoldoutSet(self.space, cfg.testSetSize, self.device)
+        self.store = ModelStore(self.space.dim, self.device)
         self.record_buffer: list[bytes] = []
         self.idle = ST.IdleDetector(cfg.timeout)
         self.ticks = 0
@@ -108,11 +111,13 @@ class Job:
                 if net not in self.pipes:
                     self.pipes[net] = Pipeline(req, self.space, self.comm, self.device,
                                                self.spokes, self.cfg.parallelism,
-                                               self.cfg.maxMsgParams)
+                                               self.cfg.maxMsgParams, store=self.store)
             elif req.request == "Update" and net in self.pipes:
                 self.pipes[net].update(req)
             elif req.request == "Delete":
-                self.pipes.pop(net, None)
+                old = self.pipes.pop(net, None)
+                if old is not None:
+                    old.close()
             elif req.request == "Query" and net in self.pipes:
                 queries.append(req)
         return len(msgs), queries
@@ -136,18 +141,47 @@ class Job:
 
     def _forecast(self, batch: HashedBatch):
         prod = self.brokers["predictions"]
+        out: dict[int, list] = {}
+        # pipelines whose weights live in the HBM model store: ONE multi-model launch
+        groups: dict[bool, list] = {}
         for pid in sorted(self.pipes):
-            with tracing.range(f"predict:{pid}"):
-                preds = self.pipes[pid].predict(batch).float().cpu().tolist()
-            for raw, p in zip(batch.raw or [None] * batch.B, preds):
+            p = self.pipes[pid]
+            if p.store is not None:
+                groups.setdefault(bool(p.learner.rule.bias), []).append(p)
+        for bias, pipes in groups.items():
+            with tracing.range("predict:store"):
+                s = self.store.scores(batch, [p.store_row for p in pipes], bias=bias)
+                for j, p in enumerate(pipes):
+                    out[p.id] = p.scores_to_predictions(s[:, j]).float().cpu().tolist()
+        for pid in sorted(self.pipes):
+            if pid not in out:
+                with tracing.range(f"predict:{pid}"):
+                    out[pid] = self.pipes[pid].predict(batch).float().cpu().tolist()
+        for pid in sorted(out):
+            for raw, p in zip(batch.raw or [None] * batch.B, out[pid]):
                 prod.produce(self.cfg.predictionsTopic, Prediction(pid, raw, p).to_json())
-            self.counters["predictions"] += len(preds)
+            self.counters["predictions"] += len(out[pid])
 
     def _train(self, batch: HashedBatch):
+        """One round of every pipeline. Synchronous pipelines train first and their
+        round buffers are summed over ranks in ONE coalesced collective per hub layout
+        (one flat bucket instead of one launch per pipeline); the other
+        protocols run their own rounds."""
         routed = self.holdout.route(batch)
+        groups: dict[int, list] = {}
         for pid in sorted(self.pipes):
+            pipe = self.pipes[pid]
             with tracing.range(f"round:{pid}"):
-                self.pipes[pid].train(routed)
+                if self.world > 1 and isinstance(pipe.protocol, Synchronous):
+                    groups.setdefault(pipe.protocol.hubs, []).append(
+                        (pipe, pipe.train_local(routed)))
+                else:
+                    pipe.train(routed)
+        for hubs, items in groups.items():
+            with tracing.range("sync:coalesced"):
+                self.comm.all_reduce_coalesced_([b for _, b in items], tag="sync", hubs=hubs)
+            for pipe, _ in items:
+                pipe.protocol.finish()
 
     # ------------------------------------------------------------------- queries
     def _answer(self, req: Request, response_id=None, write=True) -> dict:
@@ -262,7 +296,7 @@ class Job:
         for pid, psd in sd.get("pipelines", {}).items():
             req = Request.from_json(psd["request"])
             pipe = Pipeline(req, self.space, self.comm, self.device, self.spokes,
-                            self.cfg.parallelism, self.cfg.maxMsgParams)
+                            self.cfg.parallelism, self.cfg.maxMsgParams, store=self.store)
             pipe.load_state_dict(psd)
             self.pipes[int(pid)] = pipe
         self.holdout.load_state_dict(sd["holdout"])

@@ -21,7 +21,7 @@ from omldm_amd.parallel.protocols import make_protocol
 
 class Pipeline:
     def __init__(self, request: Request, space: FeatureSpace, comm: Comm, device,
-                 spokes: int, parallelism: int, max_msg_params: int = 10000):
+                 spokes: int, parallelism: int, max_msg_params: int = 10000, store=None):
         self.id = int(request.id)
         self.request = request
         self.space = space
@@ -41,6 +41,12 @@ class Pipeline:
         if d + 1 >= space.dim:
             raise ValueError("dense block wider than the hashed feature space")
         self.learner = make_learner(name, hyper, space, device)
+        # hashed-linear pipelines without preprocessors keep their weights in the shared
+        # HBM model store so forecasts are scored for all of them in one launch
+        self.store, self.store_row = None, None
+        if store is not None and not self.preprocessors and hasattr(self.learner, "attach"):
+            self.store = store
+            self.store_row = store.add(self.learner)
         # Protocol selection rules of the reference.
         if parallelism <= 1 and comm.world == 1:
             proto = "CentralizedTraining"
@@ -67,11 +73,26 @@ class Pipeline:
         """One protocol round on this rank's training rows (possibly empty)."""
         self.protocol.round(self._pre(batch, True))
 
+    def train_local(self, batch: HashedBatch) -> torch.Tensor:
+        """Phase 1 of a split Synchronous round: train, return the buffer to reduce."""
+        return self.protocol.local(self._pre(batch, True))
+
     def predict(self, batch: HashedBatch) -> torch.Tensor:
         return self.learner.predict(self._pre(batch, False))
 
     def evaluate(self, batch: HashedBatch):
         return self.learner.evaluate(self._pre(batch, False))
+
+    def close(self) -> None:
+        if self.store is not None:
+            self.store.remove(self.store_row)
+            self.store = None
+
+    def scores_to_predictions(self, s: torch.Tensor) -> torch.Tensor:
+        """Decision values from the model store → this learner's prediction values."""
+        if self.learner.TASK == "classification":
+            return torch.where(s >= 0, 1.0, -1.0)
+        return s
 
     def record_learning_curve(self) -> None:
         tot = self.learner.running_totals()

@@ -64,6 +64,15 @@ class LinearLearner(Learner):
         super().update_hyper(hyper)
         self._configure()
 
+    # ---------------------------------------------------------- model store rows
+    def attach(self, row: torch.Tensor) -> None:
+        """Re-point the fp32 weights at a row of the HBM model store (engine/model_store.py);
+        ``row`` already holds the current weights."""
+        self.w = row
+
+    def detach(self) -> None:
+        self.w = self.w.clone()
+
     # ---------------------------------------------------------------- training
     def _wread(self) -> torch.Tensor:
         return self.w16 if self.w16 is not None else self.w

@@ -141,28 +141,39 @@ class Synchronous(Protocol):
         super().__init__(*a, **k)
         self._E = None
 
-    def round(self, batch):
+    # The round is split in two so the engine can coalesce the collectives of several
+    # pipelines into one bucket: local() trains and returns the buffer to
+    # sum over ranks, finish() consumes the reduced buffer.
+    def local(self, batch) -> torch.Tensor:
         L = self.learner
         if L.supports_fused_delta:
             # Fast path: the kernel leaves Σ σ·Δ (+ counters) of every local spoke in the
             # learner's accumulator; one collective sums it over ranks; apply averages.
             L.fit(batch, self._ctx(fused=True))
-            buf = L.delta_buffer()
-            self.comm.hub_reduce_(buf, self.hubs, tag="sync")
-            L.apply_delta()
-            self._account_model_sync(L.num_params(), buf.numel() * buf.element_size())
+            self._buf = L.delta_buffer()
         else:
             if self._E is None:
                 self._E = L.state_vector().detach().clone()
                 self._d = torch.empty_like(self._E)
             L.fit(batch, self._ctx())
-            x = L.state_vector()
-            d = torch.sub(x, self._E, out=self._d)
-            self.comm.hub_reduce_(d, self.hubs, tag="sync")
-            M.fold_reload(self._E, d, self._scale(), x)      # E += scale·Σd ; x = E
+            self._buf = torch.sub(L.state_vector(), self._E, out=self._d)
+        return self._buf
+
+    def finish(self) -> None:
+        L, buf = self.learner, self._buf
+        if L.supports_fused_delta:
+            L.apply_delta()
+        else:
+            M.fold_reload(self._E, buf, self._scale(), L.state_vector())  # E += s·Σd ; x = E
             L.on_state_loaded()
-            self._account_model_sync(L.num_params(), d.numel() * d.element_size())
+        self._account_model_sync(L.num_params(), buf.numel() * buf.element_size())
+        self._buf = None
         self.stats.rounds += 1
+
+    def round(self, batch):
+        buf = self.local(batch)
+        self.comm.hub_reduce_(buf, self.hubs, tag="sync")
+        self.finish()
 
     def state_dict(self):
         sd = super().state_dict()
