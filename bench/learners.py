@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Per-learner training throughput on one GPU (every reference learner + extension):
+one round = the learner's fit on a micro-batch with S virtual spokes (where the learner
+has them), HBM-resident synthetic data, model update included. One JSON line per run
+with examples/s per learner — the regression guard for the non-headline kernels.
+
+    python bench/learners.py [--batch 131072 --steps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from omldm_amd.api.batch import FeatureSpace, HashedBatch  # noqa: E402
+from omldm_amd.io.synthetic import synth_batch  # noqa: E402
+from omldm_amd.models import make_learner  # noqa: E402
+from omldm_amd.models.base import RoundContext  # noqa: E402
+
+CASES = [
+    ("PA", 0, {}, 4096),
+    ("SVM", 0, {"modelDtype": "bf16", "tableLog2": 11}, 4096),
+    ("RegressorPA", 1, {}, 4096),
+    ("LogisticRegression", 0, {}, 4096),
+    ("MultiClassPA", 2, {"nClasses": 4}, 4096),
+    ("ORR", 1, {}, 1),
+    ("K-means", 0, {"k": 16}, 1),
+    ("NN", 0, {"hiddenLayers": [64, 64]}, 2048),
+    ("HT", 2, {"nClasses": 4}, 1),
+]
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=131072)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args(argv)
+    dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    space = FeatureSpace(13, 0, 26, 1 << 20)
+    res = {}
+    for name, task, hyper, spokes in CASES:
+        if a.only and name not in a.only.split(","):
+            continue
+        ring = []
+        for k in range(3):
+            b = synth_batch(space, a.batch, start=k * a.batch, seed=25, task=task, n_classes=4)
+            if name in ("NN",):
+                b = HashedBatch(b.num, b.cat, torch.where(b.y > 0, 1.0, -1.0))
+            ring.append(b.to(dev))
+        L = make_learner(name, hyper, space, dev)
+        ctx = RoundContext(spokes=spokes)
+        for k in range(2):
+            L.fit(ring[k % 3], ctx)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        t = time.perf_counter()
+        for k in range(a.steps):
+            L.fit(ring[k % 3], ctx)
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        el = time.perf_counter() - t
+        res[name] = {"examples_per_s": round(a.steps * a.batch / el, 1),
+                     "ms_per_round": round(el / a.steps * 1e3, 3), "spokes": spokes}
+    print(json.dumps({"metric": "per-learner training examples/s (1 GPU, 1 pipeline)",
+                      "batch": a.batch, "steps": a.steps, "device": str(dev),
+                      "learners": res}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
