@@ -206,8 +206,11 @@ class JobStatistics:
     parallelism: int
     duration: int                      # ms between the first and last statistic
     statistics: list[Statistics] = field(default_factory=list)
+    metrics: dict | None = None        # engine metrics (extension)
 
     def to_json(self) -> str:
-        return json.dumps({"jobName": self.jobName, "parallelism": self.parallelism,
-                           "duration": self.duration,
-                           "statistics": [s.to_obj() for s in self.statistics]})
+        o = {"jobName": self.jobName, "parallelism": self.parallelism,
+             "duration": self.duration, "statistics": [s.to_obj() for s in self.statistics]}
+        if self.metrics is not None:
+            o["metrics"] = self.metrics
+        return json.dumps(o)

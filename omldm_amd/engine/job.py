@@ -24,6 +24,7 @@ MI355X-native redesign. One process per GPU; every process runs this loop in loc
 """
 from __future__ import annotations
 
+import collections
 import json
 import time
 
@@ -74,6 +75,8 @@ class Job:
         self.final_stats = None
         self.counters = {"records": 0, "invalid": 0, "predictions": 0, "responses": 0,
                          "dropped_buffer": 0}
+        self._fc_lat: collections.deque = collections.deque(maxlen=4096)  # ms per forecast batch
+        self._trained_global = 0
         self._flags = torch.zeros(3, dtype=torch.float32, device=self._coll_device())
         from omldm_amd.utils.fault import FaultPlan, Watchdog
 
@@ -227,7 +230,9 @@ class Job:
             fidx = torch.nonzero(opt == OP_FORECASTING).flatten()
             tidx = torch.nonzero(opt == OP_TRAINING).flatten()
             if fidx.numel():
+                tf = time.perf_counter()
                 self._forecast(batch.select(fidx).to(self.device))
+                self._fc_lat.append((time.perf_counter() - tf) * 1e3)
             tb = batch.select(tidx).to(self.device, non_blocking=True)
         else:
             tb = HashedBatch.empty(self.space, 0, device=self.device)
@@ -240,6 +245,7 @@ class Job:
         self._flags[2] = float(tb.B)
         self.comm.all_reduce_(self._flags, tag="heartbeat")
         active, term, n_train = (float(v) for v in self._flags.tolist())
+        self._trained_global += int(n_train)
         if self.pipes and n_train > 0:
             self._train(tb)
         for q in queries:
@@ -264,10 +270,25 @@ class Job:
             m = self._answer(Request(id=pid, request="Query", requestId=-1), write=False)
             stats.append(ST.pipeline_statistics(pipe, m))
         js = ST.job_statistics(self.cfg.jobName, self.world, self.idle.duration_ms(), stats)
+        js.metrics = self._metrics(js.duration)
         self.final_stats = js
         if self.rank == 0:
             self.brokers["performance"].produce(self.cfg.performanceTopic, js.to_json())
         self.terminated = True
+
+    def _metrics(self, duration_ms: int) -> dict:
+        """Engine metrics attached to JobStatistics: node-wide training
+        throughput, forecast latency percentiles (rank 0), collective traffic, stages."""
+        lat = sorted(self._fc_lat)
+        pct = (lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))], 3)) if lat else \
+            (lambda q: None)
+        cs = self.comm.stats
+        return {"trainedExamples": self._trained_global,
+                "examplesPerSec": round(self._trained_global / max(duration_ms, 1) * 1e3, 1),
+                "forecastBatchLatencyMs": {"p50": pct(0.5), "p99": pct(0.99)},
+                "collectives": cs.collectives, "collectiveBytes": cs.bytes,
+                "collectiveBytesPerTag": dict(cs.per_tag), "counters": dict(self.counters),
+                "stages": tracing.report(), "modelStoreMB": round(self.store.bytes() / 2**20, 2)}
 
     def run(self) -> "Job":
         while not self.terminated and (self.cfg.maxTicks <= 0 or self.ticks < self.cfg.maxTicks):

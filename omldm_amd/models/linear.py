@@ -73,6 +73,11 @@ class LinearLearner(Learner):
     def detach(self) -> None:
         self.w = self.w.clone()
 
+    def vector_bias(self) -> tuple[torch.Tensor, float]:
+        """The reference's ``VectorBias(weights, bias)`` view: the
+        intercept lives in the reserved last slot of the flat weight vector."""
+        return self.w[: self.dim - 1], float(self.w[self.dim - 1]) if self.rule.bias else 0.0
+
     # ---------------------------------------------------------------- training
     def _wread(self) -> torch.Tensor:
         return self.w16 if self.w16 is not None else self.w

@@ -1,0 +1,76 @@
+"""Operator tools (the reference's deployment recipe, README.md:20-41: create the Kafka
+topics, then ``flink run``):
+
+    python -m omldm_amd.tools topics  --bootstrap host:9092 [--data-partitions 36]
+    python -m omldm_amd.tools produce --bootstrap host:9092 --topic requests --file reqs.jsonl
+    python -m omldm_amd.tools tail    --bootstrap host:9092 --topic responses [-n 20]
+    python -m omldm_amd.tools synth   --bootstrap host:9092 --topic trainingData --n 100000
+
+``--bootstrap`` also accepts ``file:///dir`` (FileBroker) for single-node runs.
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+
+from omldm_amd.io.transport import Consumer, broker_for
+
+# Partition counts of the reference deployment (README.md:21-26); psMessages is not
+# needed (RCCL replaces the feedback topic).
+TOPICS = {"requests": 1, "responses": 1, "trainingData": 36, "forecastingData": 36,
+          "predictions": 36, "performance": 1}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m omldm_amd.tools")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    t = sub.add_parser("topics")
+    t.add_argument("--bootstrap", required=True)
+    t.add_argument("--data-partitions", type=int, default=36)
+    p = sub.add_parser("produce")
+    p.add_argument("--bootstrap", required=True)
+    p.add_argument("--topic", required=True)
+    p.add_argument("--file", required=True)
+    tl = sub.add_parser("tail")
+    tl.add_argument("--bootstrap", required=True)
+    tl.add_argument("--topic", required=True)
+    tl.add_argument("-n", type=int, default=20)
+    s = sub.add_parser("synth")
+    s.add_argument("--bootstrap", required=True)
+    s.add_argument("--topic", default="trainingData")
+    s.add_argument("--n", type=int, default=10000)
+    s.add_argument("--operation", default="training")
+    s.add_argument("--hash-dim", type=int, default=1 << 20)
+    a = ap.parse_args(argv)
+    br = broker_for(a.bootstrap)
+    if a.cmd == "topics":
+        for name, n in TOPICS.items():
+            n = a.data_partitions if n == 36 else n
+            br.create_topic(name, n)
+            print(f"{name}: {n} partition(s)")
+    elif a.cmd == "produce":
+        k = 0
+        with open(a.file, "rb") as f:
+            for line in f:
+                if line.strip():
+                    br.produce(a.topic, line.rstrip(b"\n"))
+                    k += 1
+        br.flush()
+        print(f"produced {k} record(s) to {a.topic}")
+    elif a.cmd == "tail":
+        for rec in Consumer(br, a.topic, all_partitions=True).poll(10**9)[-a.n:]:
+            sys.stdout.write(rec.decode(errors="replace") + "\n")
+    elif a.cmd == "synth":
+        from omldm_amd.api.batch import FeatureSpace
+        from omldm_amd.io.synthetic import synth_json_records
+
+        for r in synth_json_records(a.n, FeatureSpace(13, 0, 26, a.hash_dim),
+                                    operation=a.operation):
+            br.produce(a.topic, r)
+        br.flush()
+        print(f"produced {a.n} synthetic record(s) to {a.topic}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -108,3 +108,57 @@ def test_config_reference_defaults_and_flags():
                              "--psMessagesTopic", "ignored", "--fooBar", "1"])
     assert c.parallelism == 8 and c.test is False and c.jobName == "x"
     assert c.psMessagesTopic == "ignored" and c.extra == {"fooBar": "1"}
+
+
+def test_serde_helpers():
+    from omldm_amd.io.serde import (RecordMetadata, deserialize_data_instance,
+                                    deserialize_request, serialize, string_to_doubles)
+
+    md = RecordMetadata("trainingData", 3, None, 17, 1234)
+    di = deserialize_data_instance(b'{"numericalFeatures":[1,2],"target":1}', md)
+    assert di is not None and di.metadata["offset"] == 17
+    assert deserialize_data_instance(b"EOS") is None
+    assert deserialize_data_instance(b'{"operation":"training"}') is None
+    rq = deserialize_request(b'{"id":1,"request":"Create","learner":{"name":"PA"}}', md)
+    assert rq.learner.name == "PA" and rq.metadata["partition"] == 3
+    assert deserialize_request(b'{"id":-1,"request":"Create"}') is None
+    assert json.loads(serialize(rq))["request"] == "Create"
+    assert json.loads(serialize({"a": 1})) == {"a": 1}
+    assert string_to_doubles("1, 2.5,,-3") == [1.0, 2.5, -3.0]
+
+
+def test_points_roundtrip_matches_parser():
+    from omldm_amd.api.batch import FeatureSpace
+    from omldm_amd.api.points import LabeledPoint, UnlabeledPoint, sparse_vector, to_batch
+    from omldm_amd.io.parse import parse_records
+
+    for fa in (False, True):
+        sp = FeatureSpace(3, 1, 2, 1 << 12, field_aware=fa)
+        pts = [LabeledPoint([1.0, 2.0, 3.0], [4], ["a", "b"], target=1.0),
+               UnlabeledPoint([0.5, 0.0, -1.0], [0], ["zz"])]
+        b = to_batch(pts, sp)
+        recs = [json.dumps({"numericalFeatures": [1.0, 2.0, 3.0], "discreteFeatures": [4],
+                            "categoricalFeatures": ["a", "b"], "target": 1.0}),
+                json.dumps({"numericalFeatures": [0.5, 0.0, -1.0], "discreteFeatures": [0],
+                            "categoricalFeatures": ["zz"], "operation": "forecasting"})]
+        ref, _, _ = parse_records([r.encode() for r in recs], sp, 1)
+        assert (b.num == ref.num).all() and (b.cat == ref.cat).all()
+        assert float(b.y[0]) == 1.0 and b.y[1].isnan()
+        idx, val = sparse_vector(b, 0)
+        assert len(idx) == 4 + 2 and val[:4] == [1.0, 2.0, 3.0, 4.0]
+
+
+def test_tools_topics_and_produce(tmp_path):
+    from omldm_amd import tools
+    from omldm_amd.io.transport import FileBroker
+
+    root = f"file://{tmp_path}"
+    assert tools.main(["topics", "--bootstrap", root, "--data-partitions", "4"]) == 0
+    fb = FileBroker(str(tmp_path))
+    assert fb.partitions("trainingData") == 4 and fb.partitions("requests") == 1
+    f = tmp_path / "reqs.jsonl"
+    f.write_text('{"id":1,"request":"Create","learner":{"name":"PA"}}\n')
+    assert tools.main(["produce", "--bootstrap", root, "--topic", "requests",
+                       "--file", str(f)]) == 0
+    assert fb.end_offset("requests", 0) > 0
+    assert tools.main(["synth", "--bootstrap", root, "--n", "10"]) == 0
