@@ -66,10 +66,10 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--spokes", type=int, default=4096, help="virtual spokes per GPU")
-    ap.add_argument("--rows", type=int, default=32, help="examples per spoke per round")
+    ap.add_argument("--spokes", type=int, default=8192, help="virtual spokes per GPU")
+    ap.add_argument("--rows", type=int, default=16, help="examples per spoke per round")
     ap.add_argument("--dim-log2", type=int, default=20)
-    ap.add_argument("--table-log2", type=int, default=11, help="LDS delta table (entries, log2)")
+    ap.add_argument("--table-log2", type=int, default=10, help="LDS delta table (entries, log2)")
     ap.add_argument("--model-dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--num-dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--wire", default="compact", choices=["wide", "compact"],
@@ -85,9 +85,14 @@ def main(argv=None) -> int:
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
     ap.add_argument("--ablate", type=int, default=0, help="kernel phase ablation (diagnostics)")
     ap.add_argument("--chunk", type=int, default=8, help="rows per kernel pipeline step")
-    ap.add_argument("--h2d", default="pull", choices=["sdma", "pull", "raw"],
-                    help="H2D engine: pull = GPU kernel reads the pinned batch over PCIe")
-    ap.add_argument("--pull-blocks", type=int, default=64)
+    ap.add_argument("--h2d", default="pull", choices=["sdma", "pull", "raw", "engine"],
+                    help="H2D engine: pull = GPU kernel reads the pinned batch over PCIe; "
+                         "engine = native copy thread issuing SDMA copies")
+    ap.add_argument("--copy-streams", type=int, default=2, help="SDMA streams (engine)")
+    ap.add_argument("--slots", type=int, default=3, help="HBM staging buffers (2 = double)")
+    ap.add_argument("--copy-priority", type=int, default=0,
+                    help="1: ingest stream at high priority (its blocks dispatch first)")
+    ap.add_argument("--pull-blocks", type=int, default=16)
     ap.add_argument("--ingest-cus", type=int, default=0,
                     help=">0: run the ingest stream on a CU-masked slice of this many CUs")
     a = ap.parse_args(argv)
@@ -109,7 +114,7 @@ def main(argv=None) -> int:
         pb.batch.cat.copy_(tmp.cat)
         pb.batch.y.copy_(tmp.y)
         pool.append(pb)
-    dev = [PackedBatch(space, B, device, False, num_dtype) for _ in range(2)]
+    dev = [PackedBatch(space, B, device, False, num_dtype) for _ in range(a.slots)]
     if a.ingest == "device":
         dev = [PackedBatch(space, B, device, False, num_dtype) for _ in range(a.pool)]
         for d, p in zip(dev, pool):
@@ -121,13 +126,24 @@ def main(argv=None) -> int:
     proto = Synchronous(comm, learner, {"virtualSpokes": S,
                                         **({"HubParallelism": a.hubs} if a.hubs else {})})
 
-    copy_stream = torch.cuda.Stream(device) if on_gpu else None
+    copy_stream = torch.cuda.Stream(device, priority=-1 if a.copy_priority else 0) \
+        if on_gpu else None
     if on_gpu and a.ingest_cus > 0:
         raw = native.hip().omldm_stream_create_cumask(a.ingest_cus)
         assert raw, "hipExtStreamCreateWithCUMask failed"
         copy_stream = torch.cuda.ExternalStream(raw, device=device)
-    copied = [torch.cuda.Event() for _ in range(2)] if on_gpu else None
-    consumed = [torch.cuda.Event() for _ in range(2)] if on_gpu else None
+    copied = [torch.cuda.Event() for _ in range(a.slots)] if on_gpu else None
+    consumed = [torch.cuda.Event() for _ in range(a.slots)] if on_gpu else None
+    engine = None
+    if on_gpu and a.h2d == "engine" and a.ingest == "pinned":
+        from omldm_amd.ops.ingest import CopyEngine
+
+        engine = CopyEngine(a.copy_streams)
+        ev_done = [engine.event() for _ in range(a.slots)]
+        ev_free = [engine.event() for _ in range(a.slots)]
+        tickets = [0] * a.slots
+        for ev in ev_free:
+            engine.record(ev)
 
     host_t = {"prefetch": 0.0, "round": 0.0}
 
@@ -147,9 +163,11 @@ def main(argv=None) -> int:
         if a.ingest in ("device", "zerocopy"):
             return
         t = time.perf_counter()
-        slot = k % 2
+        slot = k % a.slots
         src = pool[k % a.pool]
-        if on_gpu:
+        if engine is not None:
+            tickets[slot] = engine.submit(dev[slot].flat, src.flat, ev_free[slot], ev_done[slot])
+        elif on_gpu:
             with torch.cuda.stream(copy_stream):
                 copy_stream.wait_event(consumed[slot])
                 h2d(dev[slot].flat, src.flat)
@@ -167,13 +185,17 @@ def main(argv=None) -> int:
             proto.round(pool[k % a.pool].batch if on_gpu else pool[k % a.pool].batch)
             host_t["round"] += time.perf_counter() - t
             return
-        slot = k % 2
+        slot = k % a.slots
         prefetch(k + 1)
         t = time.perf_counter()
-        if on_gpu:
+        if engine is not None:
+            engine.stream_wait(tickets[slot], ev_done[slot])
+        elif on_gpu:
             torch.cuda.current_stream().wait_event(copied[slot])
         proto.round(dev[slot].batch)
-        if on_gpu:
+        if engine is not None:
+            engine.record(ev_free[slot])
+        elif on_gpu:
             consumed[slot].record()
         host_t["round"] += time.perf_counter() - t
 

@@ -69,6 +69,13 @@ HIP_SIGS = [
     ("omldm_elastic_post", i32, [vp, vp, vp, vp, f32, i64, vp]),
     ("omldm_async_push", i32, [vp, vp, vp, vp, vp, i64, vp]),
     ("omldm_async_pull", i32, [vp, vp, vp, vp, vp, f32, i64, vp]),
+    ("omldm_copy_engine_create", vp, [i32]),
+    ("omldm_copy_engine_destroy", None, [vp]),
+    ("omldm_copy_engine_submit", u64, [vp, vp, vp, i64, vp, vp]),
+    ("omldm_copy_engine_stream_wait", i32, [vp, u64, vp, vp]),
+    ("omldm_event_create", vp, []),
+    ("omldm_event_destroy", i32, [vp]),
+    ("omldm_event_record", i32, [vp, vp]),
     ("omldm_stream_create_cumask", vp, [i32]),
     ("omldm_host_device_ptr", vp, [vp]),
     ("omldm_stream_destroy", i32, [vp]),
