@@ -19,10 +19,12 @@
 //    sequential part per example is: ds_read Δ → fma → DPP wave reduction →
 //    closed-form τ → ds_add_f32. Slot lookups/inserts for the whole chunk happen
 //    before the sequential part (they do not depend on the updates).
-//  * At round end each spoke scatters σ·Δ/P into the dense round accumulator with
-//    no-return global f32 atomics, plus σ/P into accumulator[dim] (the w0 weight);
-//    the accumulator is then all-reduced over xGMI by RCCL and folded into w by
-//    linear_apply (below) — that is the Synchronous PS round.
+//  * At round end each spoke stores its bucketed table (σ·Δ/P per slot) with plain
+//    coalesced stores; linear_reduce_kernel sums the tables per key range in LDS and
+//    adds them to the dense round accumulator, while its finish blocks sum the per-spoke
+//    dense columns and σ/P (the w0 weight, accumulator[dim]). The accumulator is then
+//    all-reduced over xGMI by RCCL and folded into w by linear_apply (below) — that is
+//    the Synchronous PS round.
 #include "common.h"
 
 namespace omldm {
@@ -104,7 +106,7 @@ constexpr int kWsStat = 8;
 // Dense column of feature j: numerical slot j → j, intercept → dn; hashed features → -1.
 // Dense features live in a register per lane for the whole round (every example has
 // them), so they never touch the LDS table and never hit the same global address from
-// every spoke: they are reduced by linear_round_finish instead of by atomics.
+// every spoke: they are reduced by the finish blocks of linear_reduce_kernel instead of by atomics.
 __device__ __forceinline__ int dense_col(int j, int dn, int dc, int bias) {
   if (j < dn) return j;
   if (bias && j == dn + dc) return dn;
@@ -178,7 +180,7 @@ template <int FPL, int CH, int RULE, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void linear_round_kernel(
     const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
     int dc, const float* __restrict__ yv, int B, int R, int dim, float* __restrict__ ws,
-    int2* __restrict__ tables, LinParams p, TableGeom g, int ablate) {
+    int2* __restrict__ tables, float* __restrict__ dacc, LinParams p, TableGeom g, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int cap = 1 << g.log2cap;
   const int tsz = cap + kOvf;
@@ -325,14 +327,18 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     }
   }
   __syncthreads();
-  // Round end: the whole table (σ·Δ/P per slot) goes out with plain coalesced stores;
-  // linear_bucket_reduce sums it per key range, no global atomics on the hot path.
+  // Round end: the bucketed table (σ·Δ/P per slot) goes out with plain coalesced stores
+  // and linear_reduce_kernel sums it per key range — no global atomics on the hot path;
+  // the (rare) overflow-area entries are added to the accumulator directly.
   const float scale = sigma * p.inv_p;
   if (!(ablate & 1)) {
     int2* trow = tables + (size_t)s * tsz;
-    for (int i = lane; i < tsz; i += kWave) {
+    for (int i = lane; i < cap; i += kWave)
+      trow[i] = make_int2(keys[i], __float_as_int(vals[i] * scale));
+    for (int i = cap + lane; i < tsz; i += kWave) {
       const int k = keys[i];
-      trow[i] = make_int2(k, __float_as_int(vals[i] * scale));
+      const float v = vals[i] * scale;
+      if (k >= 0 && v != 0.f) atomicAdd(&dacc[k], v);
     }
   }
 #pragma unroll
@@ -352,12 +358,47 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
   }
 }
 
-// Bucket b owns keys [b·2^kshift, (b+1)·2^kshift): it streams bucket b of every active
-// spoke's table (BS consecutive int2 per spoke), accumulates into a 16 KiB LDS image
-// with ds_add_f32 and writes its slice of the round accumulator with plain stores.
-__global__ __launch_bounds__(256) void linear_bucket_reduce_kernel(
-    const int2* __restrict__ tables, int S_act, TableGeom g, int dim, float* __restrict__ dacc) {
+// Column sums of the per-spoke workspace (one block per column) → accumulator slots
+// that every spoke would otherwise hit with same-address atomics:
+//   dense columns → dacc[0:dn], intercept → dacc[dim-1], Σσ/P → dacc[dim],
+//   Σ1/P → dacc[dim+1], loss/n/mistakes/sq_err/overflow → cum (device running totals).
+__device__ __forceinline__ void finish_column(int c, const float* __restrict__ ws, int S, int dn,
+                                              int dim, float* __restrict__ dacc,
+                                              float* __restrict__ cum) {
+  __shared__ float part[4];
+  const int wsw = kWsStat + dn + 1;
+  float acc = 0.f;
+  for (int s = threadIdx.x; s < S; s += 256) acc += ws[(size_t)s * wsw + c];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = (part[0] + part[1]) + (part[2] + part[3]);
+    if (c < kWsStat) {
+      if (c == 6) dacc[dim] = t;       // the round's counters (apply does not clear them)
+      else if (c == 7) dacc[dim + 1] = t;
+      else if (c != 4 && cum) cum[c] += t;
+    } else {
+      const int j = c - kWsStat;
+      dacc[j < dn ? j : dim - 1] += t;
+    }
+  }
+}
+
+// One launch after the round kernel. Blocks [0, nb): bucket b owns keys
+// [b·2^kshift, (b+1)·2^kshift); it streams bucket b of every active spoke's table (BS
+// consecutive int2 per spoke), accumulates into an LDS image with ds_add_f32 and adds its
+// non-zero slots to the accumulator (which the apply pass left at zero; overflow entries
+// were added by the round kernel). Blocks [nb, nb + wsw): workspace column sums. Hashed
+// keys never map to dense / intercept slots, so the two block kinds touch disjoint slots.
+__global__ __launch_bounds__(256) void linear_reduce_kernel(
+    const int2* __restrict__ tables, int S_act, TableGeom g, int dim, float* __restrict__ dacc,
+    int nb, const float* __restrict__ ws, int S, int dn, float* __restrict__ cum) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if ((int)blockIdx.x >= nb) {
+    finish_column(blockIdx.x - nb, ws, S, dn, dim, dacc, cum);
+    return;
+  }
   float* acc = reinterpret_cast<float*>(smem);
   const int span = 1 << g.kshift;
   const int b = blockIdx.x;
@@ -395,54 +436,8 @@ __global__ __launch_bounds__(256) void linear_bucket_reduce_kernel(
   __syncthreads();
   for (int i = threadIdx.x; i < span; i += 256) {
     const int k = lo + i;
-    if (k < dim) dacc[k] = acc[i];
-  }
-}
-
-// Overflow-area entries (rare) are added with global atomics after the bucket reduce.
-__global__ __launch_bounds__(256) void linear_overflow_kernel(const int2* __restrict__ tables,
-                                                              int S_act, int log2cap,
-                                                              float* __restrict__ dacc) {
-  const int tsz = (1 << log2cap) + kOvf;
-  const long long n = (long long)S_act * kOvf;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (long long)gridDim.x * 256) {
-    const int sp = (int)(i / kOvf);
-    const int j = (int)(i % kOvf);
-    const int2 e = tables[(size_t)sp * tsz + (1 << log2cap) + j];
-    if (e.x >= 0) {
-      const float v = __int_as_float(e.y);
-      if (v != 0.f) atomicAdd(&dacc[e.x], v);
-    }
-  }
-}
-
-// Column sums of the per-spoke workspace (one block per column) → accumulator slots
-// that every spoke would otherwise hit with same-address atomics:
-//   dense columns → dacc[0:dn], intercept → dacc[dim-1], Σσ/P → dacc[dim],
-//   Σ1/P → dacc[dim+1], loss/n/mistakes/sq_err/overflow → cum (device running totals).
-__global__ __launch_bounds__(256) void linear_round_finish_kernel(const float* __restrict__ ws,
-                                                                  int S, int dn, int dim,
-                                                                  float* __restrict__ dacc,
-                                                                  float* __restrict__ cum) {
-  __shared__ float part[4];
-  const int c = blockIdx.x;
-  const int wsw = kWsStat + dn + 1;
-  float acc = 0.f;
-  for (int s = threadIdx.x; s < S; s += 256) acc += ws[(size_t)s * wsw + c];
-  acc = wave_sum(acc);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float t = (part[0] + part[1]) + (part[2] + part[3]);
-    if (c < kWsStat) {
-      if (c == 6) dacc[dim] = t;       // the round's counters (apply does not clear them)
-      else if (c == 7) dacc[dim + 1] = t;
-      else if (c != 4 && cum) cum[c] += t;
-    } else {
-      const int j = c - kWsStat;
-      dacc[j < dn ? j : dim - 1] += t;
-    }
+    const float v = acc[i];
+    if (k < dim && v != 0.f) dacc[k] += v;
   }
 }
 
@@ -520,20 +515,15 @@ static int launch_round(const void* w, const void* num, int dn, const void* cat,
   int e = check_dyn_lds((const void*)fn, lds);
   if (e) return e;
   hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)w, (const NumT*)num, dn, cat, dc,
-                     y, B, R, dim, ws, tables, p, g, ablate);
+                     y, B, R, dim, ws, tables, dacc, p, g, ablate);
   const long long sact_ll = R > 0 ? ((long long)B + R - 1) / R : 0;
   const int S_act = sact_ll < S ? (int)sact_ll : S;
-  if (!(ablate & 1) && S_act > 0) {
-    const int nb = (dim + (1 << g.kshift) - 1) >> g.kshift;
-    hipLaunchKernelGGL(linear_bucket_reduce_kernel, dim3(nb), dim3(256),
-                       (size_t(1) << g.kshift) * 4, st, tables, S_act, g, dim, dacc);
-    int ob = (int)(((long long)S_act * kOvf + 255) / 256);
-    if (ob > 1024) ob = 1024;
-    hipLaunchKernelGGL(linear_overflow_kernel, dim3(ob), dim3(256), 0, st, tables, S_act,
-                       g.log2cap, dacc);
-  }
-  hipLaunchKernelGGL(linear_round_finish_kernel, dim3(kWsStat + dn + 1), dim3(256), 0, st, ws, S,
-                     dn, dim, dacc, cum);
+  const int nb = (!(ablate & 1) && S_act > 0) ? (dim + (1 << g.kshift) - 1) >> g.kshift : 0;
+  const size_t rlds = nb ? (size_t(1) << g.kshift) * 4 : 0;
+  e = check_dyn_lds((const void*)linear_reduce_kernel, rlds);
+  if (e) return e;
+  hipLaunchKernelGGL(linear_reduce_kernel, dim3(nb + kWsStat + dn + 1), dim3(256), rlds, st,
+                     tables, S_act, g, dim, dacc, nb, ws, S, dn, cum);
   return (int)hipGetLastError();
 }
 
