@@ -85,14 +85,16 @@ def main(argv=None) -> int:
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
     ap.add_argument("--ablate", type=int, default=0, help="kernel phase ablation (diagnostics)")
     ap.add_argument("--chunk", type=int, default=8, help="rows per kernel pipeline step")
-    ap.add_argument("--h2d", default="pull", choices=["sdma", "pull", "raw", "engine"],
+    ap.add_argument("--h2d", default="pull", choices=["sdma", "pull", "raw", "engine", "pull-hbm"],
                     help="H2D engine: pull = GPU kernel reads the pinned batch over PCIe; "
                          "engine = native copy thread issuing SDMA copies")
     ap.add_argument("--copy-streams", type=int, default=2, help="SDMA streams (engine)")
     ap.add_argument("--slots", type=int, default=3, help="HBM staging buffers (2 = double)")
     ap.add_argument("--copy-priority", type=int, default=0,
                     help="1: ingest stream at high priority (its blocks dispatch first)")
-    ap.add_argument("--pull-blocks", type=int, default=16)
+    ap.add_argument("--pull-blocks", type=int, default=8)
+    ap.add_argument("--pull-unroll", type=int, default=4, choices=[4, 8, 16],
+                    help="16-B loads in flight per lane in the pull kernel")
     ap.add_argument("--ingest-cus", type=int, default=0,
                     help=">0: run the ingest stream on a CU-masked slice of this many CUs")
     a = ap.parse_args(argv)
@@ -147,10 +149,19 @@ def main(argv=None) -> int:
 
     host_t = {"prefetch": 0.0, "round": 0.0}
 
-    def h2d(dst: torch.Tensor, src: torch.Tensor):
-        if a.h2d == "pull":  # GPU pulls the pinned batch over PCIe (csrc/kernels/ingest.hip)
-            native.check(native.hip().omldm_pull_copy(src.data_ptr(), dst.data_ptr(),
+    dsrc = None
+    if a.h2d == "pull-hbm" and on_gpu:  # diagnostics: same copy kernel, HBM source
+        dsrc = [p.flat.to(device) for p in pool]
+
+    def h2d(dst: torch.Tensor, src: torch.Tensor, k: int = 0):
+        if a.h2d == "pull-hbm":
+            native.check(native.hip().omldm_pull_copy(dsrc[k % a.pool].data_ptr(), dst.data_ptr(),
                                                       src.numel(), a.pull_blocks,
+                                                      copy_stream.cuda_stream), "pull_copy")
+        elif a.h2d == "pull":  # GPU pulls the pinned batch over PCIe (csrc/kernels/ingest.hip)
+            blk = a.pull_blocks | ((a.pull_unroll if a.pull_unroll != 4 else 0) << 16)
+            native.check(native.hip().omldm_pull_copy(src.data_ptr(), dst.data_ptr(),
+                                                      src.numel(), blk,
                                                       copy_stream.cuda_stream), "pull_copy")
         elif a.h2d == "raw":  # hipMemcpyAsync issued directly
             native.check(native.hip().omldm_h2d_async(dst.data_ptr(), src.data_ptr(),
@@ -170,7 +181,7 @@ def main(argv=None) -> int:
         elif on_gpu:
             with torch.cuda.stream(copy_stream):
                 copy_stream.wait_event(consumed[slot])
-                h2d(dev[slot].flat, src.flat)
+                h2d(dev[slot].flat, src.flat, k)
                 copied[slot].record(copy_stream)
         else:
             dev[slot].flat.copy_(src.flat)

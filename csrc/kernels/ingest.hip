@@ -32,6 +32,24 @@ __global__ __launch_bounds__(256) void pull_copy_kernel(const u32x4* __restrict_
   for (; i < n16; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
 }
 
+// U loads in flight per lane before the stores (few waves, deep queues: long-latency PCIe
+// reads from many waves clog the memory pipeline shared with the training kernels).
+template <int U>
+__global__ __launch_bounds__(256) void pull_copy_u_kernel(const u32x4* __restrict__ src,
+                                                          u32x4* __restrict__ dst, long long n16) {
+  const long long tid = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long stride = (long long)gridDim.x * 256;
+  long long i = tid;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) dst[i + u * stride] = v[u];
+  }
+  for (; i < n16; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
+}
+
 __global__ void pull_tail_kernel(const unsigned char* __restrict__ src,
                                  unsigned char* __restrict__ dst, long long n) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -94,8 +112,19 @@ OMLDM_API int omldm_pull_copy(const void* host_src, void* dst, long long nbytes,
   if (((uintptr_t)src & 15) || ((uintptr_t)dst & 15)) return -1;
   if (n16) {
     if (blocks <= 0) blocks = 1024;
-    hipLaunchKernelGGL(pull_copy_kernel, dim3(blocks), dim3(256), 0, st, (const u32x4*)src,
-                       (u32x4*)dst, n16);
+    // blocks < 0 is not used; the high bits of `blocks` select the unroll depth:
+    // blocks = nblk | (U << 16), U ∈ {8, 16} (default 4).
+    const int U = blocks >> 16;
+    const int nblk = blocks & 0xFFFF;
+    if (U == 8)
+      hipLaunchKernelGGL(pull_copy_u_kernel<8>, dim3(nblk), dim3(256), 0, st, (const u32x4*)src,
+                         (u32x4*)dst, n16);
+    else if (U == 16)
+      hipLaunchKernelGGL(pull_copy_u_kernel<16>, dim3(nblk), dim3(256), 0, st,
+                         (const u32x4*)src, (u32x4*)dst, n16);
+    else
+      hipLaunchKernelGGL(pull_copy_kernel, dim3(nblk), dim3(256), 0, st, (const u32x4*)src,
+                         (u32x4*)dst, n16);
   }
   const long long tail = nbytes - n16 * 16;
   if (tail)
