@@ -146,15 +146,19 @@ def init_distributed(device_type: str = "auto", timeout_s: float = 600.0) -> tup
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() if device_type == "auto" else device_type != "cpu"
-    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    # OMLDM_DIST_BACKEND=gloo rehearses several ranks on fewer GPUs (ranks share a device
+    # round-robin); production is one rank per GPU over RCCL.
+    backend = os.environ.get("OMLDM_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+    ndev = torch.cuda.device_count() if use_gpu else 0
+    device = torch.device("cuda", local_rank % max(1, ndev)) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(device)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         kw = {}
-        if use_gpu:
+        if use_gpu and backend == "nccl":
             kw["device_id"] = device
-        dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
+        dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return Comm(), device

@@ -1,0 +1,74 @@
+"""Multi-rank rehearsal on ONE GPU: two ranks share cuda:0 and talk over gloo (the
+8-GPU RCCL run is the driver's). It exercises the exact multi-GPU code path of bench.py —
+device-resident fused round accumulators summed by a collective, then applied — and
+checks the Synchronous invariant: two ranks × S spokes == one rank × 2S spokes on the
+concatenated batch."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from omldm_amd.api.batch import FeatureSpace
+
+SP = FeatureSpace(13, 0, 26, 1 << 16, field_aware=True)
+S, R, ROUNDS = 64, 16, 3
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batch(rank, world, r):
+    from omldm_amd.io.synthetic import synth_batch
+
+    return synth_batch(SP, S * R, start=(r * world + rank) * S * R, seed=7)
+
+
+def _rank(rank, world, port, out):
+    import torch.distributed as dist
+
+    from omldm_amd.models.linear import SVM
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.parallel.protocols import Synchronous
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    L = SVM({"variant": "PA-I", "modelDtype": "bf16", "tableLog2": 10}, SP, dev)
+    P = Synchronous(Comm(), L, {"virtualSpokes": S})
+    for r in range(ROUNDS):
+        P.round(_batch(rank, world, r).to(dev))
+    torch.cuda.synchronize()
+    torch.save({"w": L.w.cpu()}, os.path.join(out, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_one_gpu_equal_one_rank_double_spokes(cuda):
+    from omldm_amd.api.batch import HashedBatch
+    from omldm_amd.models.linear import SVM
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.parallel.protocols import Synchronous
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rank, args=(2, _port(), d), nprocs=2, start_method="spawn")
+        w0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)["w"]
+        w1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)["w"]
+    torch.testing.assert_close(w0, w1)
+    assert float(w0.abs().sum()) > 0
+    # single rank, 2S spokes, rank-0 rows then rank-1 rows (spoke s ↔ rows [sR, sR+R))
+    L = SVM({"variant": "PA-I", "modelDtype": "bf16", "tableLog2": 10}, SP, cuda)
+    P = Synchronous(Comm(), L, {"virtualSpokes": 2 * S})
+    for r in range(ROUNDS):
+        b = HashedBatch.cat_batches([_batch(0, 2, r), _batch(1, 2, r)])
+        P.round(b.to(cuda))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(L.w.cpu(), w0, rtol=1e-3, atol=1e-4)
