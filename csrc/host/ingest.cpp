@@ -126,18 +126,80 @@ struct Cursor {
     if (p >= e || *p != '"') return ok = false;
     ++p;
     s = p;
-    while (p < e && *p != '"') {
-      if (*p == '\\') ++p;
-      ++p;
+    for (;;) {  // memchr (vectorised) to the next quote; re-scan only across escapes
+      const char* q = static_cast<const char*>(std::memchr(p, '"', size_t(e - p)));
+      if (!q) return ok = false;
+      const char* bs = static_cast<const char*>(std::memchr(p, '\\', size_t(q - p)));
+      if (!bs) {
+        p = q;
+        break;
+      }
+      p = bs + 2;  // skip the escaped character
+      if (p > e) return ok = false;
     }
-    if (p >= e) return ok = false;
     n = size_t(p - s);
     ++p;
     return true;
   }
+  // JSON number. Fast path (Clinger): ≤ 19 significant digits and a decimal exponent
+  // within ±22 convert exactly from one integer and one power-of-ten table entry
+  // (both exactly representable in double); anything else falls back to strtod.
   bool num(double& v) {
     ws();
-    char* end = nullptr;
+    const char* q = p;
+    bool neg = false;
+    if (q < e && (*q == '-' || *q == '+')) neg = *q++ == '-';
+    uint64_t m = 0;
+    int nd = 0, exp10 = 0;
+    const char* d0 = q;
+    while (q < e && unsigned(*q - '0') < 10u) {
+      if (nd < 19) {
+        m = m * 10 + unsigned(*q - '0');
+        if (m) ++nd;
+      } else {
+        ++exp10;
+      }
+      ++q;
+    }
+    bool any = q > d0;
+    if (q < e && *q == '.') {
+      ++q;
+      const char* f0 = q;
+      while (q < e && unsigned(*q - '0') < 10u) {
+        if (nd < 19) {
+          m = m * 10 + unsigned(*q - '0');
+          if (m) ++nd;
+          --exp10;
+        }
+        ++q;
+      }
+      any = any || q > f0;
+    }
+    if (!any) return ok = false;
+    if (q < e && (*q == 'e' || *q == 'E')) {
+      ++q;
+      bool eneg = false;
+      if (q < e && (*q == '-' || *q == '+')) eneg = *q++ == '-';
+      int ev = 0;
+      const char* e0 = q;
+      while (q < e && unsigned(*q - '0') < 10u) {
+        if (ev < 100000) ev = ev * 10 + int(*q - '0');
+        ++q;
+      }
+      if (q == e0) return ok = false;
+      exp10 += eneg ? -ev : ev;
+    }
+    static const double kPow10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                    1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                    1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    if (m < (1ull << 53) && exp10 >= -22 && exp10 <= 22) {
+      const double dm = double(m);
+      v = exp10 >= 0 ? dm * kPow10[exp10] : dm / kPow10[-exp10];
+      if (neg) v = -v;
+      p = q;
+      return true;
+    }
+    char* end = nullptr;  // rare: long mantissas, huge exponents
     v = std::strtod(p, &end);
     if (end == p || end > e) return ok = false;
     p = end;

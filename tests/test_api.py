@@ -3,6 +3,7 @@ config flags (reference behaviours cited in each module)."""
 import json
 
 import pytest
+import torch
 
 from omldm_amd.api.schemas import JobStatistics, QueryResponse, Request, Statistics
 from omldm_amd.engine.pipeline_map import ALL, PipelineMap
@@ -162,3 +163,31 @@ def test_tools_topics_and_produce(tmp_path):
                        "--file", str(f)]) == 0
     assert fb.end_offset("requests", 0) > 0
     assert tools.main(["synth", "--bootstrap", root, "--n", "10"]) == 0
+
+
+def test_fast_number_parser_matches_python_float():
+    import random
+
+    from omldm_amd.api.batch import FeatureSpace
+    from omldm_amd.io.parse import parse_records
+
+    sp = FeatureSpace(6, 0, 0, 1 << 10)
+    rng = random.Random(3)
+    texts = ["0", "-0", "1e-5", "-0.000123", "123456789012345678901234", "3.14159265358979323846",
+             "1E+10", "2.5e-300", "1.7976931348623157e308", "4.9e-324", "0.1", "-12345.678e3"]
+    for _ in range(300):
+        m = rng.choice(["%d" % rng.randint(-10**9, 10**9), "%.17g" % rng.uniform(-1e6, 1e6),
+                        "%.6e" % rng.uniform(-1, 1), "%.3f" % rng.uniform(-100, 100)])
+        texts.append(m)
+    while len(texts) % 6:
+        texts.append("7")
+    recs, expect = [], []
+    for i in range(0, len(texts), 6):
+        row = texts[i:i + 6]
+        recs.append(('{"numericalFeatures":[%s],"target":1,"operation":"training"}'
+                     % ",".join(row)).encode())
+        expect.append([float(t) for t in row])
+    b, op, n = parse_records(recs, sp, 2)
+    assert n == len(recs)
+    want = torch.tensor(expect, dtype=torch.float64).float()
+    assert torch.equal(b.num, want)
