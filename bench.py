@@ -93,6 +93,8 @@ def main(argv=None) -> int:
     ap.add_argument("--copy-priority", type=int, default=0,
                     help="1: ingest stream at high priority (its blocks dispatch first)")
     ap.add_argument("--pull-blocks", type=int, default=8)
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: capture each pipelined step (copy ‖ round) as a hipGraph (1 GPU)")
     ap.add_argument("--pull-unroll", type=int, default=4, choices=[4, 8, 16],
                     help="16-B loads in flight per lane in the pull kernel")
     ap.add_argument("--ingest-cus", type=int, default=0,
@@ -217,10 +219,56 @@ def main(argv=None) -> int:
         if on_gpu:
             torch.cuda.synchronize(device)
 
-    if on_gpu:
-        for e in consumed:
-            e.record()
-    prefetch(0)
+    # ---- hipGraph mode: step k = {pull copy of batch k+1 into its slot ‖ protocol round on
+    # slot k} captured as ONE graph with a fork/join; the cycle repeats every
+    # lcm(pool, slots) steps, so that many graphs are captured once and replayed.
+    use_graph = bool(a.graph) and on_gpu and world == 1 and a.ingest == "pinned" \
+        and a.h2d in ("pull", "raw") and engine is None
+    graphs = []
+    if use_graph:
+        import math
+
+        period = a.pool * a.slots // math.gcd(a.pool, a.slots)
+        fork, join = torch.cuda.Event(), torch.cuda.Event()
+
+        def graph_step(k: int):
+            nxt = (k + 1) % a.slots
+            fork.record()
+            copy_stream.wait_event(fork)
+            with torch.cuda.stream(copy_stream):
+                h2d(dev[nxt].flat, pool[(k + 1) % a.pool].flat, k + 1)
+            join.record(copy_stream)
+            proto.round(dev[k % a.slots].batch)
+            torch.cuda.current_stream().wait_event(join)
+
+        # eager warm-up of every code path (allocations, LDS attributes) before capture
+        h2d(dev[0].flat, pool[0].flat, 0)
+        torch.cuda.synchronize(device)
+        graph_step(0)
+        torch.cuda.synchronize(device)
+        for k in range(period):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                graph_step(k)
+            graphs.append(g)
+        torch.cuda.synchronize(device)
+        # the replays re-train from here: reset to a fresh stream position and model
+        learner.w.zero_()
+        if learner.w16 is not None:
+            learner.w16.zero_()
+        learner.cum.zero_()
+        h2d(dev[0].flat, pool[0].flat, 0)
+        torch.cuda.synchronize(device)
+
+        def step(k: int):  # noqa: F811 - graph replay replaces the eager step
+            t = time.perf_counter()
+            graphs[k % period].replay()
+            host_t["round"] += time.perf_counter() - t
+    else:
+        if on_gpu:
+            for e in consumed:
+                e.record()
+        prefetch(0)
     for k in range(a.warmup):
         step(k)
     sync()
@@ -262,10 +310,23 @@ def main(argv=None) -> int:
             num_h = one_pin.num[0].float().contiguous()
             cat_h = (one_pin.cat[0].to(torch.int64) & (0xFFFF if space.cat_span else -1))
             cat_h = cat_h.to(torch.int32).contiguous()
+            alive0 = server.lib.omldm_serve_alive(server.mb)
             ref = float(LO.linear_predict(learner._wread(), one_pin.to(device))[0])
+            alive1 = server.lib.omldm_serve_alive(server.mb)
+            if not alive1:
+                import ctypes as _C
+                tt = (_C.c_ulonglong * 3)()
+                server.lib.cdll.omldm_serve_times(_C.c_void_p(server.mb), tt)
+                print(f"[bench] serving wave exited early (alive after start={alive0}, "
+                      f"reason={server.lib.omldm_serve_exit_reason(server.mb)}, "
+                      f"t_start={tt[0]} t_exit={tt[1]} t_end={tt[2]})", file=sys.stderr)
             for i in range(a.latency_samples + 50):
                 t = time.perf_counter()
-                got = server.request_raw(num_h.data_ptr(), cat_h.data_ptr())
+                try:
+                    got = server.request_raw(num_h.data_ptr(), cat_h.data_ptr())
+                except TimeoutError:
+                    raise TimeoutError(f"serving wave stopped answering at request {i} "
+                                       f"(alive={server.lib.omldm_serve_alive(server.mb)})")
                 if i >= 50:
                     lat_us.append((time.perf_counter() - t) * 1e6)
             server.close()

@@ -27,6 +27,9 @@ struct Mailbox {
   // payload: num [dn] floats, then cat [dc] ints
   float num[256];
   int cat[256];
+  unsigned int exit_reason;  // device → host: 1 stop word, 2 lifetime expired
+  unsigned int pad;
+  unsigned long long t_start, t_exit, t_end;  // diagnostics (100 MHz clock)
 };
 
 template <typename T>
@@ -50,7 +53,11 @@ __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, lon
   const int lane = threadIdx.x;
   const unsigned long long t_end = rt_now() + lifetime_ticks;
   unsigned int last = sys_load(&mb->seq_req);
-  if (lane == 0) sys_store(&mb->alive, 1u);
+  if (lane == 0) {
+    sys_store(&mb->t_start, t_end - lifetime_ticks);
+    sys_store(&mb->t_end, t_end);
+    sys_store(&mb->alive, 1u);
+  }
   while (true) {
     unsigned int seq = 0;
     bool go = false, quit = false;
@@ -64,7 +71,15 @@ __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, lon
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (!go) quit = sys_load(&mb->stop) != 0u || rt_now() > t_end;
+      if (!go) {
+        const bool st = sys_load(&mb->stop) != 0u;
+        const bool late = rt_now() > t_end;
+        quit = st || late;
+        if (quit) {
+          sys_store(&mb->exit_reason, st ? 1u : 2u);
+          sys_store(&mb->t_exit, rt_now());
+        }
+      }
     }
     go = __builtin_amdgcn_readfirstlane(go ? 1 : 0) != 0;
     quit = __builtin_amdgcn_readfirstlane(quit ? 1 : 0) != 0;
@@ -136,6 +151,7 @@ OMLDM_API int omldm_serve_start(const void* w, int w_bf16, long long wstride, in
   void* dmb = nullptr;
   if (hipHostGetDevicePointer(&dmb, mailbox, 0) != hipSuccess || !dmb) return -3;
   __atomic_store_n(&hmb->stop, 0u, __ATOMIC_SEQ_CST);
+  __atomic_store_n(&hmb->exit_reason, 0u, __ATOMIC_SEQ_CST);
   __atomic_store_n(&hmb->alive, 0u, __ATOMIC_SEQ_CST);
   const unsigned long long ticks = (unsigned long long)lifetime_us * 100ull;  // 100 MHz
   if (w_bf16)
@@ -170,6 +186,17 @@ OMLDM_API int omldm_serve_request(void* mailbox, const float* num, int dn, const
 
 OMLDM_API void omldm_serve_stop(void* mailbox) {
   __atomic_store_n(&((Mailbox*)mailbox)->stop, 1u, __ATOMIC_SEQ_CST);
+}
+
+OMLDM_API void omldm_serve_times(void* mailbox, unsigned long long* out3) {
+  const Mailbox* m = (const Mailbox*)mailbox;
+  out3[0] = m->t_start;
+  out3[1] = m->t_exit;
+  out3[2] = m->t_end;
+}
+
+OMLDM_API int omldm_serve_exit_reason(void* mailbox) {
+  return (int)__atomic_load_n(&((Mailbox*)mailbox)->exit_reason, __ATOMIC_ACQUIRE);
 }
 
 OMLDM_API int omldm_serve_alive(void* mailbox) {

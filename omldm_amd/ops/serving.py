@@ -26,6 +26,7 @@ SIGS = [
                                       C.c_int, C.c_void_p, C.c_longlong]),
     ("omldm_serve_stop", None, [C.c_void_p]),
     ("omldm_serve_alive", C.c_int, [C.c_void_p]),
+    ("omldm_serve_exit_reason", C.c_int, [C.c_void_p]),
 ]
 
 
@@ -49,7 +50,13 @@ class PredictServer:
         self.mb = self.lib.omldm_mailbox_alloc()
         if not self.mb:
             raise RuntimeError("hipHostMalloc(coherent) failed for the serving mailbox")
-        self.stream = torch.cuda.Stream(w.device)
+        # The resident wave must not block other work queued on the device: a blocking
+        # stream (e.g. hipExtStreamCreateWithCUMask's) serialises with the legacy default
+        # stream, and a normal-priority pool stream can share a hardware queue with the
+        # training streams. Measured (scripts/diag_serve_queue.py): a high-priority,
+        # non-blocking stream never delays work on other streams.
+        self._raw_stream = None
+        self.stream = torch.cuda.Stream(w.device, priority=-1)
         self.out = (C.c_float * self.M)()
 
     def start(self, lifetime_us: int = 10_000_000) -> None:
@@ -90,3 +97,6 @@ class PredictServer:
             self.stop()
             self.lib.omldm_mailbox_free(self.mb)
             self.mb = None
+        if getattr(self, "_raw_stream", None):
+            native.hip().omldm_stream_destroy(self._raw_stream)
+            self._raw_stream = None
