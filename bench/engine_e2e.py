@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""End-to-end engine throughput: JSON DataInstance records in a topic → parse + hash (C++)
+→ HBM → holdout routing → protocol round → statistics, through the real Job loop
+(the path a reference user exercises; the headline bench replays pre-hashed batches).
+
+    python bench/engine_e2e.py [--records 2000000 --batch 65536 --pipelines 1]
+Prints one JSON line: records/s of the training stream through the whole engine.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from omldm_amd.api.batch import FeatureSpace  # noqa: E402
+from omldm_amd.engine.job import Job  # noqa: E402
+from omldm_amd.io.synthetic import synth_json_records  # noqa: E402
+from omldm_amd.io.transport import FileBroker  # noqa: E402
+from omldm_amd.parallel.comm import init_distributed  # noqa: E402
+from omldm_amd.utils.config import JobConfig  # noqa: E402
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--pipelines", type=int, default=1)
+    ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--threads", type=int, default=16)
+    a = ap.parse_args(argv)
+    comm, device = init_distributed()
+    sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
+    with tempfile.TemporaryDirectory() as root:
+        br = FileBroker(root)
+        br.create_topic("trainingData", a.partitions)
+        t = time.time()
+        chunk = 100_000
+        for s in range(0, a.records, chunk):
+            recs = synth_json_records(min(chunk, a.records - s), sp, start=s, seed=3)
+            for i, r in enumerate(recs):
+                br.produce("trainingData", r, partition=(s + i) % a.partitions)
+        gen_s = time.time() - t
+        for i in range(a.pipelines):
+            br.produce("requests", json.dumps({
+                "id": i + 1, "request": "Create",
+                "learner": {"name": "SVM", "hyperParameters": {"modelDtype": "bf16",
+                                                               "tableLog2": 11}},
+                "trainingConfiguration": {"protocol": "Synchronous"}}))
+        addr = f"file://{root}"
+        args = []
+        for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+                  "predictionsAddr", "performanceAddr"):
+            args += [f"--{k}", addr]
+        cfg = JobConfig.from_args(args + ["--hashDim", str(sp.dim), "--fieldAware", "true",
+                                          "--batchSize", str(a.batch), "--timeout", "1000",
+                                          "--spokesPerDevice", "4096",
+                                          "--parseThreads", str(a.threads), "--jobName", "e2e"])
+        job = Job(cfg, comm, device)
+        t0 = time.time()
+        job.run()
+        wall = time.time() - t0 - cfg.timeout / 1000.0  # minus the idle wait at the end
+        m = job.final_stats.metrics if job.final_stats else {}
+        if comm.rank == 0:
+            print(json.dumps({
+                "metric": "end-to-end engine training records/s (JSON topic → model)",
+                "value": round(job.counters["records"] * comm.world / max(wall, 1e-9), 1),
+                "unit": "records/s", "n_gpus": comm.world, "records": job.counters["records"],
+                "pipelines": a.pipelines, "batch": a.batch, "wall_s": round(wall, 3),
+                "generate_s": round(gen_s, 1), "stages_ms": m.get("stages"),
+                "device": str(device)}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -131,6 +131,9 @@ class HashedBatch:
         return HashedBatch(torch.cat([b.num for b in batches]), torch.cat([b.cat for b in batches]),
                            torch.cat([b.y for b in batches]), raw, batches[0].cat_span)
 
+    def without_raw(self) -> "HashedBatch":
+        return self._like(self.num, self.cat, self.y, None)
+
     def contiguous(self) -> "HashedBatch":
         return self._like(self.num.contiguous(), self.cat.contiguous(), self.y.contiguous(),
                           self.raw)

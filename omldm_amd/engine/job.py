@@ -38,12 +38,29 @@ from omldm_amd.engine.model_store import ModelStore
 from omldm_amd.engine.pipeline import Pipeline
 from omldm_amd.engine.pipeline_map import ALL, PipelineMap
 from omldm_amd.engine import statistics as ST
-from omldm_amd.io.parse import OP_FORECASTING, OP_TRAINING, parse_records
+from omldm_amd.io.parse import OP_FORECASTING, OP_TRAINING, RawView, parse_block
+from omldm_amd.io.transport import join_block
 from omldm_amd.io.transport import Consumer, broker_for
 from omldm_amd.parallel.comm import Comm
 from omldm_amd.parallel.protocols import Synchronous
 from omldm_amd.utils.config import JobConfig
 from omldm_amd.utils import tracing
+
+
+EMPTY_BLOCK = (b"", np.zeros(1, dtype=np.int64))
+
+
+def concat_blocks(blocks: list) -> tuple[bytes, np.ndarray]:
+    blocks = [b for b in blocks if len(b[1]) > 1]
+    if not blocks:
+        return EMPTY_BLOCK
+    if len(blocks) == 1:
+        return blocks[0]
+    offs, base = [np.zeros(1, dtype=np.int64)], 0
+    for buf, o in blocks:
+        offs.append(o[1:] + base)
+        base += len(buf)
+    return b"".join(b for b, _ in blocks), np.concatenate(offs)
 
 
 class Job:
@@ -68,7 +85,8 @@ class Job:
         self.pipes: dict[int, Pipeline] = {}
         self.holdout = HoldoutSet(self.space, cfg.testSetSize, self.device)
         self.store = ModelStore(self.space.dim, self.device)
-        self.record_buffer: list[bytes] = []
+        self.record_buffer: list = []          # blocks (buf, offsets) waiting for a Create
+        self._buffered = 0
         self.idle = ST.IdleDetector(cfg.timeout)
         self.ticks = 0
         self.terminated = False
@@ -126,21 +144,26 @@ class Job:
         return len(msgs), queries
 
     # --------------------------------------------------------------------- data
-    def _poll(self) -> list[bytes]:
+    def _poll(self) -> tuple[bytes, np.ndarray]:
+        """This tick's records as one buffer + offsets (no per-record Python objects)."""
         n = self.cfg.batchSize
-        recs = self.train_in.poll(n) + self.fcst_in.poll(n)
+        block = concat_blocks([self.train_in.poll_block(n), self.fcst_in.poll_block(n)])
+        nrec = len(block[1]) - 1
         if not self.pipes:
             # reference: points wait in a bounded record buffer until a pipeline exists
-            room = self.cfg.recordBufferSize - len(self.record_buffer)
-            if len(recs) > room:
-                self.counters["dropped_buffer"] += len(recs) - max(room, 0)
-                recs = recs[:max(room, 0)]
-            self.record_buffer.extend(recs)
-            return []
+            room = max(0, self.cfg.recordBufferSize - self._buffered)
+            if nrec > room:
+                self.counters["dropped_buffer"] += nrec - room
+                block = (block[0][:int(block[1][room])], block[1][:room + 1])
+                nrec = room
+            if nrec:
+                self.record_buffer.append(block)
+                self._buffered += nrec
+            return EMPTY_BLOCK
         if self.record_buffer:
-            recs = self.record_buffer + recs
-            self.record_buffer = []
-        return recs
+            block = concat_blocks(self.record_buffer + [block])
+            self.record_buffer, self._buffered = [], 0
+        return block
 
     def _forecast(self, batch: HashedBatch):
         prod = self.brokers["predictions"]
@@ -219,13 +242,13 @@ class Job:
         if self.watchdog is not None:
             self.watchdog.beat()
         n_ctrl, queries = self._control()
-        recs = self._poll()
-        n_local = len(recs)
-        if recs:
+        buf, offs = self._poll()
+        n_local = len(offs) - 1
+        if n_local:
             with tracing.range("parse"):
-                batch, op, nvalid = parse_records(recs, self.space, self.cfg.parseThreads)
+                batch, op, nvalid = parse_block(buf, offs, self.space, self.cfg.parseThreads)
             self.counters["records"] += nvalid
-            self.counters["invalid"] += len(recs) - nvalid
+            self.counters["invalid"] += n_local - nvalid
             opt = torch.from_numpy(op)
             fidx = torch.nonzero(opt == OP_FORECASTING).flatten()
             tidx = torch.nonzero(opt == OP_TRAINING).flatten()
@@ -233,7 +256,7 @@ class Job:
                 tf = time.perf_counter()
                 self._forecast(batch.select(fidx).to(self.device))
                 self._fc_lat.append((time.perf_counter() - tf) * 1e3)
-            tb = batch.select(tidx).to(self.device, non_blocking=True)
+            tb = batch.without_raw().select(tidx).to(self.device, non_blocking=True)
         else:
             tb = HashedBatch.empty(self.space, 0, device=self.device)
         # global activity + termination flag (one tiny all-reduce per tick); every rank
@@ -305,7 +328,8 @@ class Job:
               "holdout": self.holdout.state_dict(),
               "consumers": {"train": self.train_in.state_dict(),
                             "forecast": self.fcst_in.state_dict()},
-              "record_buffer": list(self.record_buffer), "ticks": self.ticks,
+              "record_buffer": [r for b in self.record_buffer for r in RawView(*b)],
+              "ticks": self.ticks,
               "counters": dict(self.counters), "world": self.world}
         if self.rank == 0:
             sd["pipeline_map"] = self.pmap.state_dict()
@@ -327,7 +351,9 @@ class Job:
         elif consumer_offsets is not None:  # Consumer keeps only the partitions it owns
             self.train_in.load_state_dict({"offsets": consumer_offsets["train"]})
             self.fcst_in.load_state_dict({"offsets": consumer_offsets["forecast"]})
-        self.record_buffer = list(sd.get("record_buffer", []))
+        recs = list(sd.get("record_buffer", []))
+        self.record_buffer = [join_block(recs)] if recs else []
+        self._buffered = len(recs)
         self.ticks = int(sd.get("ticks", 0))
         if self.rank == 0 and "pipeline_map" in sd:
             self.pmap.load_state_dict(sd["pipeline_map"])

@@ -21,6 +21,8 @@ import struct
 import threading
 import time
 
+from omldm_amd.io.transport import Broker
+
 # ------------------------------------------------------------------ primitives
 
 
@@ -251,7 +253,7 @@ class _Conn:
         self.sock.close()
 
 
-class KafkaBroker:
+class KafkaBroker(Broker):
     """transport.Broker over the Kafka protocol (bootstrap ``host:port[,host:port]``)."""
 
     def __init__(self, bootstrap: str, timeout: float = 10.0):

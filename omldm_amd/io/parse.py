@@ -25,6 +25,46 @@ def hash_categorical(token: str, field: int, space: FeatureSpace) -> int:
     return int(native.host().omldm_hash_cat(b, len(b), field, space.dn, space.dim))
 
 
+class RawView:
+    """Lazy per-record view of a parsed block (the raw text is only materialised for
+    the records that need it: forecasts echo their point in the Prediction)."""
+
+    __slots__ = ("buf", "offs")
+
+    def __init__(self, buf: bytes, offs: np.ndarray):
+        self.buf, self.offs = buf, offs
+
+    def __len__(self):
+        return len(self.offs) - 1
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        i = int(i)
+        return self.buf[int(self.offs[i]):int(self.offs[i + 1])].rstrip(b"\n")
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
+def parse_block(buf: bytes, offs: np.ndarray, space: FeatureSpace, threads: int | None = None):
+    """Parses buf[offs[i]:offs[i+1]] for every i. Returns (batch, op, n_valid)."""
+    n = len(offs) - 1
+    num = torch.zeros((n, space.dn), dtype=torch.float32)
+    cat = torch.full((n, space.dc), -1, dtype=space.cat_dtype)
+    y = torch.full((n,), float("nan"), dtype=torch.float32)
+    op = np.full(n, -1, dtype=np.int8)
+    valid = 0
+    if n > 0:
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        threads = threads or min(8, os.cpu_count() or 1)
+        valid = native.host().omldm_parse_instances(
+            buf, offs.ctypes.data, n, space.n_numerical, space.n_discrete, space.dc, space.dim,
+            space.cat_span, num.data_ptr(), cat.data_ptr(), y.data_ptr(), op.ctypes.data,
+            threads)
+    return HashedBatch(num, cat, y, RawView(buf, offs), space.cat_span), op, int(valid)
+
+
 def parse_records(records: list, space: FeatureSpace, threads: int | None = None,
                   keep_raw: bool = True):
     """Returns (batch, op[int8 ndarray], n_valid). Invalid rows have op == -1."""

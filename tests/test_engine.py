@@ -74,7 +74,7 @@ def test_records_buffered_until_create_and_delete():
     for r in synth_json_records(300, SP):
         br.produce("trainingData", r)
     job.tick()
-    assert len(job.record_buffer) == 300 and not job.pipes
+    assert job._buffered == 300 and not job.pipes
     create(br, 5, "PA")
     job.tick()
     job.tick()
