@@ -94,6 +94,11 @@ class Job:
         self.counters = {"records": 0, "invalid": 0, "predictions": 0, "responses": 0,
                          "dropped_buffer": 0}
         self._fc_lat: collections.deque = collections.deque(maxlen=4096)  # ms per forecast batch
+        self._gpu_parser = None
+        if self.device.type == "cuda" and cfg.gpuParse:
+            from omldm_amd.ops.ingest import GpuJsonParser
+
+            self._gpu_parser = GpuJsonParser(self.device)
         self._trained_global = 0
         self._flags = torch.zeros(3, dtype=torch.float32, device=self._coll_device())
         from omldm_amd.utils.fault import FaultPlan, Watchdog
@@ -246,7 +251,12 @@ class Job:
         n_local = len(offs) - 1
         if n_local:
             with tracing.range("parse"):
-                batch, op, nvalid = parse_block(buf, offs, self.space, self.cfg.parseThreads)
+                if self._gpu_parser is not None:  # raw JSON → HBM → one thread per record
+                    batch, op_d, _ = self._gpu_parser.parse(buf, offs, self.space)
+                    op = op_d.cpu().numpy()
+                else:
+                    batch, op, _ = parse_block(buf, offs, self.space, self.cfg.parseThreads)
+                nvalid = int((op >= 0).sum())
             self.counters["records"] += nvalid
             self.counters["invalid"] += n_local - nvalid
             opt = torch.from_numpy(op)

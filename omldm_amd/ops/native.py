@@ -69,6 +69,7 @@ HIP_SIGS = [
     ("omldm_elastic_post", i32, [vp, vp, vp, vp, f32, i64, vp]),
     ("omldm_async_push", i32, [vp, vp, vp, vp, vp, i64, vp]),
     ("omldm_async_pull", i32, [vp, vp, vp, vp, vp, f32, i64, vp]),
+    ("omldm_json_parse", i32, [vp, vp, i32, i32, i32, i32, i64, i32, vp, vp, vp, vp, vp, vp]),
     ("omldm_copy_engine_create", vp, [i32]),
     ("omldm_copy_engine_destroy", None, [vp]),
     ("omldm_copy_engine_submit", u64, [vp, vp, vp, i64, vp, vp]),

@@ -65,6 +65,7 @@ class JobConfig:
     restore: bool = False                 # restore from the latest checkpoint in stateBackend
     watchdogTimeout: int = 0              # ms without a finished tick → abort + exit (0: off)
     parseThreads: int = 8
+    gpuParse: bool = True                 # parse + hash JSON records on the GPU (cuda only)
     extra: dict = field(default_factory=dict)
 
     @staticmethod
