@@ -10,8 +10,9 @@
 //   LDS and runs plain mini-batch SGD over its row range: forward, loss gradient,
 //   backward and the weight update never leave LDS/registers;
 // * every GEMM-shaped step is v_mfma_f32_32x32x2_f32 on 32-row mini-batches:
-//     forward   H_{l+1} = act(H_l · W_lᵀ + b_l)     (bias + ReLU fused in the epilogue)
-//     backward  dH_l    = (dZ_{l+1} · W_l) ⊙ [H_l > 0]
+//     forward   H_{l+1} = act(H_l · W_lᵀ + b_l)     (bias + activation fused in the
+//                                                     epilogue: ReLU / tanh / sigmoid / identity)
+//     backward  dH_l    = (dZ_{l+1} · W_l) ⊙ act'(H_l)  (derivative from the stored output)
 //               W_l    -= η · dZ_{l+1}ᵀ · H_l       (applied straight from the MFMA
 //                                                     accumulators — each element has
 //                                                     exactly one owner lane)
@@ -29,8 +30,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kMB = 32;
 constexpr int kMaxLayers = 4;
 
+enum MlpAct : int { kRelu = 0, kTanh = 1, kSigmoid = 2, kIdentity = 3 };
+
 struct MlpDesc {
-  int L, task, K;
+  int L, task, K, act;  // act: hidden-layer activation (MlpAct)
   int n[kMaxLayers + 1], np[kMaxLayers + 1];
   int woff[kMaxLayers], boff[kMaxLayers];
   int lw[kMaxLayers], lb[kMaxLayers], ldw[kMaxLayers];
@@ -52,6 +55,26 @@ __device__ __forceinline__ f32x16 wave_gemm32(const float* a, int ars, int acs, 
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[k * acs], bp[k * brs], acc, 0, 0, 0);
   }
   return acc;
+}
+
+// Activation and its derivative expressed through the activation's OUTPUT h (what the
+// forward pass keeps in LDS): relu' = [h > 0], tanh' = 1 − h², σ' = h(1 − h).
+__device__ __forceinline__ float act_fwd(float v, int act) {
+  switch (act) {
+    case kTanh: return tanhf(v);
+    case kSigmoid: return 1.f / (1.f + __expf(-v));
+    case kIdentity: return v;
+    default: return fmaxf(v, 0.f);
+  }
+}
+
+__device__ __forceinline__ float act_grad(float h, int act) {
+  switch (act) {
+    case kTanh: return 1.f - h * h;
+    case kSigmoid: return h * (1.f - h);
+    case kIdentity: return 1.f;
+    default: return h > 0.f ? 1.f : 0.f;
+  }
 }
 
 __device__ __forceinline__ int crow(int q, int lane) {
@@ -80,15 +103,16 @@ __device__ void forward(float* sm, const MlpDesc& g) {
     const float* W = sm + g.lw[l];
     const float* bs = sm + g.lb[l];
     const int nt = g.np[l + 1] >> 5, ldo = g.ldh[l + 1];
-    const bool relu = l + 1 < g.L;
+    const bool hidden = l + 1 < g.L;
     for (int t = wave; t < nt; t += 4) {
       const f32x16 acc = wave_gemm32(H, g.ldh[l], 1, W + t * 32 * g.ldw[l], 1, g.ldw[l], g.np[l]);
       const int col = t * 32 + (lane & 31);
       const float bias = bs[col];
+      const bool pad = col >= g.n[l + 1];  // padding columns stay exactly zero
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         float v = acc[q] + bias;
-        if (relu) v = fmaxf(v, 0.f);
+        if (hidden) v = pad ? 0.f : act_fwd(v, g.act);
         Ho[crow(q, lane) * ldo + col] = v;
       }
     }
@@ -175,7 +199,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       float* W = sm + g.lw[l];
       const float* H = sm + g.lh[l];
       const int ldw = g.ldw[l], ldh = g.ldh[l], nin = g.np[l], nout = g.np[l + 1];
-      if (l > 0) {  // dH_l = (dZ · W_l) ⊙ relu'(H_l)
+      if (l > 0) {  // dH_l = (dZ · W_l) ⊙ act'(H_l)
         float* Gn = sm + gnext;
         for (int t = wave; t < (nin >> 5); t += 4) {
           const f32x16 acc = wave_gemm32(Gc, g.ldg, 1, W + t * 32, ldw, 1, nout);
@@ -183,7 +207,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int row = crow(q, lane);
-            Gn[row * g.ldg + col] = H[row * ldh + col] > 0.f ? acc[q] : 0.f;
+            Gn[row * g.ldg + col] = acc[q] * act_grad(H[row * ldh + col], g.act);
           }
         }
       }
@@ -258,11 +282,12 @@ __global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restric
   }
 }
 
-static int make_desc(int L, const int* widths, int task, MlpDesc* g) {
-  if (L < 1 || L > kMaxLayers) return -1;
+static int make_desc(int L, const int* widths, int task, int act, MlpDesc* g) {
+  if (L < 1 || L > kMaxLayers || act < 0 || act > kIdentity) return -1;
   *g = MlpDesc{};
   g->L = L;
   g->task = task;
+  g->act = act;
   g->K = widths[L];
   int off = 0;
   for (int l = 0; l <= L; ++l) {
@@ -308,7 +333,7 @@ using namespace omldm;
 // LDS bytes the fused kernels need for this layer stack (host-side feasibility check).
 OMLDM_API long long omldm_mlp_lds_bytes(int L, const int* widths) {
   MlpDesc g;
-  if (make_desc(L, widths, 0, &g)) return -1;
+  if (make_desc(L, widths, 0, 0, &g)) return -1;
   return (long long)g.total * 4;
 }
 
@@ -316,12 +341,12 @@ OMLDM_API long long omldm_mlp_lds_bytes(int L, const int* widths) {
 // 1 binary logistic, 2 softmax. dacc[nparams] += Σ_s Δ_s; stats[0..3] += loss, n, correct,
 // active spokes. Follow with omldm_multiclass_apply(w, dacc, nparams, stats+3).
 OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, long long B, int R,
-                              int S, int L, const int* widths, int task, float lr, float* dacc,
-                              float* stats, void* stream) {
+                              int S, int L, const int* widths, int task, int act, float lr,
+                              float* dacc, float* stats, void* stream) {
   if (B <= 0 || S <= 0) return 0;
   if (R <= 0 || (long long)R * S < B) return -3;
   MlpDesc g;
-  if (make_desc(L, widths, task, &g)) return -1;
+  if (make_desc(L, widths, task, act, &g)) return -1;
   const size_t lds = (size_t)g.total * 4;
   if (lds > 160 * 1024) return -2;
   int e = check_dyn_lds((const void*)mlp_round_kernel, lds);
@@ -332,10 +357,10 @@ OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, lo
 }
 
 OMLDM_API int omldm_mlp_forward(const float* w, const float* x, long long B, int L,
-                                const int* widths, float* out, void* stream) {
+                                const int* widths, int act, float* out, void* stream) {
   if (B <= 0) return 0;
   MlpDesc g;
-  if (make_desc(L, widths, 0, &g)) return -1;
+  if (make_desc(L, widths, 0, act, &g)) return -1;
   const size_t lds = (size_t)g.total * 4;
   if (lds > 160 * 1024) return -2;
   int e = check_dyn_lds((const void*)mlp_forward_kernel, lds);

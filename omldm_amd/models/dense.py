@@ -218,7 +218,8 @@ class MultiClassPA(Learner):
 
 # ------------------------------------------------------------------------------ NN
 class NN(Learner):
-    """Multi-layer perceptron (ReLU hidden layers) trained by mini-batch SGD — the
+    """Multi-layer perceptron (ReLU / tanh / sigmoid / identity hidden layers,
+    ``activation`` hyper-parameter) trained by mini-batch SGD — the
     reference's DL4J MultiLayerNetwork path (hs_err_pid77107.log:97-110).
 
     A round runs S virtual spokes (one workgroup each, csrc/kernels/mlp.hip): spoke s does
@@ -245,6 +246,10 @@ class NN(Learner):
             else "classification"
         self.task_id = 0 if self.TASK == "regression" else (1 if self.K <= 1 else 2)
         self.lr = hp_float(h, "learningRate", 0.05)
+        act = str(h.get("activation", "relu")).lower()
+        if act not in D.MLP_ACTS:
+            raise ValueError(f"NN activation must be one of {sorted(D.MLP_ACTS)}")
+        self.act_name, self.act = act, D.MLP_ACTS[act]
         self.widths = [self.d] + [int(v) for v in hidden] + [max(1, self.K)]
         if len(self.widths) - 1 > D.MLP_MAX_LAYERS:
             raise ValueError(f"NN supports at most {D.MLP_MAX_LAYERS} layers")
@@ -275,7 +280,7 @@ class NN(Learner):
         R = -(-per // self.MB) * self.MB
         S = -(-B // R)
         D.mlp_round(self.flat, batch.num, batch.y, R, S, self.widths, self.task_id, self.lr,
-                    self.dacc, self.st)
+                    self.dacc, self.st, self.act)
         D.multiclass_apply(self.flat, self.dacc, self.st[3:4])
         self.cum[0] += self.st[0]
         self.cum[1] += self.st[1]
@@ -286,7 +291,7 @@ class NN(Learner):
         return self.flat
 
     def forward(self, x):
-        return D.mlp_forward(self.flat, x.float(), self.widths)
+        return D.mlp_forward(self.flat, x.float(), self.widths, self.act)
 
     def predict(self, batch):
         out = self.forward(batch.num)
@@ -308,7 +313,8 @@ class NN(Learner):
         return loss, score, int(ok.sum())
 
     def hyper_parameters(self):
-        return {**self.hyper, "learningRate": self.lr, "miniBatchSize": self.MB}
+        return {**self.hyper, "learningRate": self.lr, "miniBatchSize": self.MB,
+                "activation": self.act_name}
 
     def parameters_map(self):
         return {"layers": [list(s) for s in self.shapes], "nParams": int(self.flat.numel())}

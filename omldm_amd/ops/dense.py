@@ -100,13 +100,18 @@ def _mlp_unflatten(w: torch.Tensor, widths):
     return out
 
 
-def mlp_forward_reference(w: torch.Tensor, x: torch.Tensor, widths) -> torch.Tensor:
+MLP_ACTS = {"relu": 0, "tanh": 1, "sigmoid": 2, "identity": 3}
+_ACT_FN = {0: torch.relu, 1: torch.tanh, 2: torch.sigmoid, 3: lambda t: t}
+
+
+def mlp_forward_reference(w: torch.Tensor, x: torch.Tensor, widths, act: int = 0
+                          ) -> torch.Tensor:
     h = x
     layers = _mlp_unflatten(w, widths)
     for i, (W, b) in enumerate(layers):
         h = torch.nn.functional.linear(h, W, b)
         if i + 1 < len(layers):
-            h = torch.relu(h)
+            h = _ACT_FN[act](h)
     return h
 
 
@@ -131,7 +136,7 @@ def _mlp_grad_out(o: torch.Tensor, y: torch.Tensor, task: int, K: int):
     return g, loss, (o.argmax(1) == yi).float().sum()
 
 
-def mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats) -> None:
+def mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats, act: int = 0) -> None:
     """CPU mirror of mlp_round_kernel: spoke s runs 32-row mini-batch SGD over rows
     [sR, sR+R) from the round-start model; dacc += Σ Δ_s; stats += (loss, n, correct,
     active spokes)."""
@@ -150,7 +155,7 @@ def mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats) -> None:
             if cnt == 0:
                 continue
             wv = ws.clone().requires_grad_(True)
-            o = mlp_forward_reference(wv, xb[ok], widths)
+            o = mlp_forward_reference(wv, xb[ok], widths, act)
             g, ls, cs = _mlp_grad_out(o.detach(), yb[ok], task, K)
             gw, = torch.autograd.grad(o, wv, grad_outputs=g)
             ws -= (lr / cnt) * gw
@@ -167,7 +172,7 @@ def mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats) -> None:
 
 def mlp_round(w: torch.Tensor, x: torch.Tensor, y: torch.Tensor, R: int, S: int,
               widths: list[int], task: int, lr: float, dacc: torch.Tensor,
-              stats: torch.Tensor) -> None:
+              stats: torch.Tensor, act: int = 0) -> None:
     B = x.shape[0]
     if B == 0:
         return
@@ -177,13 +182,14 @@ def mlp_round(w: torch.Tensor, x: torch.Tensor, y: torch.Tensor, R: int, S: int,
         raise ValueError(f"NN: at most {MLP_MAX_LAYERS} layers on the fused kernel")
     if x.is_cuda:
         check(native.hip().omldm_mlp_round(ptr(w), ptr(x), ptr(y), B, R, S, len(widths) - 1,
-                                           _widths_arr(widths), task, lr, ptr(dacc), ptr(stats),
-                                           native.stream_of(x)), "omldm_mlp_round")
+                                           _widths_arr(widths), task, act, lr, ptr(dacc),
+                                           ptr(stats), native.stream_of(x)), "omldm_mlp_round")
     else:
-        mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats)
+        mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats, act)
 
 
-def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int]) -> torch.Tensor:
+def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int], act: int = 0
+                ) -> torch.Tensor:
     B = x.shape[0]
     out = torch.empty((B, widths[-1]), dtype=torch.float32, device=x.device)
     if B == 0:
@@ -191,10 +197,10 @@ def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int]) -> torch.Te
     x = x.float().contiguous()
     if x.is_cuda:
         check(native.hip().omldm_mlp_forward(ptr(w), ptr(x), B, len(widths) - 1,
-                                             _widths_arr(widths), ptr(out),
+                                             _widths_arr(widths), act, ptr(out),
                                              native.stream_of(x)), "omldm_mlp_forward")
         return out
-    return mlp_forward_reference(w, x, widths)
+    return mlp_forward_reference(w, x, widths, act)
 
 
 def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor) -> None:

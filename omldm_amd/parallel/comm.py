@@ -69,8 +69,27 @@ class Comm:
         dist.broadcast(t, src=root, group=self.group)
 
     def hub_reduce_(self, t: torch.Tensor, hubs: int = 0, tag: str = "sync"):
-        if hubs == 1 and self.world > 1:
+        """Sum ``t`` over workers through ``hubs`` parameter-server shards.
+        hubs == 1: one hub (rank 0) — reduce + broadcast;
+        1 < hubs < world: hub h (rank h) owns the h-th contiguous slice — one reduce to and
+        one broadcast from each hub (the reference's sharded PS, FlinkHub keyed
+        ``net_hubIdx``);
+        hubs == 0 or ≥ world: every rank is a hub — all-reduce (reduce-scatter +
+        all-gather inside RCCL)."""
+        if self.world == 1:
+            self.all_reduce_(t, tag)
+        elif hubs == 1:
             self.reduce_bcast_(t, 0, tag)
+        elif 1 < hubs < self.world:
+            flat = t.view(-1)
+            n = flat.numel()
+            step = -(-n // hubs)
+            self.stats.add(tag, 2 * n * t.element_size())
+            for h in range(hubs):
+                sl = flat[h * step:min(n, (h + 1) * step)]
+                if sl.numel():
+                    dist.reduce(sl, dst=h, op=dist.ReduceOp.SUM, group=self.group)
+                    dist.broadcast(sl, src=h, group=self.group)
         else:
             self.all_reduce_(t, tag)
 

@@ -206,22 +206,24 @@ def test_mlp_reference_learns():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("widths,task", [([13, 32, 32, 1], 1), ([13, 32, 1], 0),
-                                         ([40, 64, 48, 5], 2), ([7, 100, 3], 2)])
-def test_hip_mlp_round_vs_reference(cuda, widths, task):
+@pytest.mark.parametrize("widths,task,act", [([13, 32, 32, 1], 1, 0), ([13, 32, 1], 0, 0),
+                                             ([40, 64, 48, 5], 2, 0), ([7, 100, 3], 2, 0),
+                                             ([13, 40, 24, 1], 1, 1), ([13, 33, 4], 2, 2),
+                                             ([9, 16, 1], 0, 3)])
+def test_hip_mlp_round_vs_reference(cuda, widths, task, act):
     B, R, S = 1000, 96, 11
     w, x, y = _mlp_case(widths, task, B, seed=len(widths) + task)
     lr = 0.05
     d_ref, s_ref = torch.zeros_like(w), torch.zeros(8)
-    D.mlp_round_reference(w, x, y, R, S, widths, task, lr, d_ref, s_ref)
+    D.mlp_round_reference(w, x, y, R, S, widths, task, lr, d_ref, s_ref, act)
     wd, d_gpu, s_gpu = w.to(cuda), torch.zeros_like(w, device=cuda), torch.zeros(8, device=cuda)
-    D.mlp_round(wd, x.to(cuda), y.to(cuda), R, S, widths, task, lr, d_gpu, s_gpu)
+    D.mlp_round(wd, x.to(cuda), y.to(cuda), R, S, widths, task, lr, d_gpu, s_gpu, act)
     torch.cuda.synchronize()
     torch.testing.assert_close(d_gpu.cpu(), d_ref, rtol=2e-3, atol=2e-4)
     torch.testing.assert_close(s_gpu.cpu()[:4], s_ref[:4], rtol=2e-3, atol=1e-2)
-    out = D.mlp_forward(wd, x.to(cuda), widths)
-    torch.testing.assert_close(out.cpu(), D.mlp_forward_reference(w, x, widths), rtol=1e-4,
-                               atol=1e-4)
+    out = D.mlp_forward(wd, x.to(cuda), widths, act)
+    torch.testing.assert_close(out.cpu(), D.mlp_forward_reference(w, x, widths, act),
+                               rtol=1e-4, atol=1e-4)
 
 
 def _ht_data(n, seed=0):

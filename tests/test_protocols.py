@@ -123,3 +123,13 @@ def test_unknown_protocol_falls_back_to_asynchronous():
     L = make_learner("PA", {}, SP, "cpu")
     assert make_protocol("Bogus", Comm(), L).NAME == "Asynchronous"
     assert make_protocol(None, Comm(), L).NAME == "Asynchronous"
+
+
+def test_sharded_hubs_world4():
+    """HubParallelism 2 of 4 workers: each hub owns half of the model; replicas equal to
+    the all-reduce (every-rank-a-hub) result."""
+    res_h2 = run(4, "SVM", "Synchronous", {"HubParallelism": 2}, rounds=3)
+    res_all = run(4, "SVM", "Synchronous", {}, rounds=3)
+    for r in res_h2[1:]:
+        assert same(r["final"], res_h2[0]["final"])
+    assert same(res_h2[0]["final"], res_all[0]["final"], 1e-5)
