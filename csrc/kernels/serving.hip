@@ -3,11 +3,15 @@
 // Reference path: forecasting record → FlinkSpoke → learner predict → Prediction side
 // output → predictions topic (omldm/operators/spoke/FlinkSpoke.scala:105,
 // omldm/network/FlinkNetwork.scala:250); its latency is a Flink task hop + JVM call.
-// Here one resident wavefront polls a sequence word in fine-grained (coherent), pinned
-// host memory; the host writes one point + bumps the sequence; the wave reads the point
-// over PCIe with system-scope loads, scores it against M models (the same feature
-// decoding as the training kernel) and publishes the scores + the completion sequence
-// with system-scope stores. No kernel launch and no stream synchronisation per request.
+// Here one resident wavefront polls a 256-byte request line in fine-grained (coherent),
+// pinned host memory. Every poll is ONE wave-wide PCIe read of the whole line (lane l
+// loads dword l): sequence number, checksum and the point itself — so a new request is
+// picked up together with its payload in a single round trip instead of "read sequence,
+// then read payload". The host writes the payload, then a position-mixed checksum keyed
+// by the sequence, then the sequence (release); a torn read (new sequence, stale payload)
+// fails the checksum and is simply re-polled. The wave scores the point against M models
+// (same feature decoding as the training kernel) and publishes scores + the completion
+// sequence with system-scope stores. No kernel launch or stream sync per request.
 //
 // Safety: the wave exits on the stop word or after `lifetime_us` of wall time
 // (s_memrealtime, 100 MHz), whichever comes first; every spin is bounded by it.
@@ -18,17 +22,15 @@
 
 namespace omldm {
 
-struct Mailbox {
-  unsigned int seq_req;   // host → device: request sequence number
-  unsigned int seq_done;  // device → host: last completed sequence number
-  unsigned int stop;      // host → device: exit request
-  unsigned int alive;     // device → host: 1 while the wave is polling
-  float result[60];       // scores of up to 60 models
-  // payload: num [dn] floats, then cat [dc] ints
-  float num[256];
-  int cat[256];
-  unsigned int exit_reason;  // device → host: 1 stop word, 2 lifetime expired
-  unsigned int pad;
+constexpr int kReqWords = 64;  // request line: [seq, csum, payload (dn + dc dwords)]
+
+struct alignas(256) Mailbox {
+  unsigned int req[kReqWords];  // host → device (one 256-B line)
+  unsigned int seq_done;        // device → host: last completed sequence number
+  unsigned int stop;            // host → device: exit request
+  unsigned int alive;           // device → host: 1 while the wave is polling
+  unsigned int exit_reason;     // device → host: 1 stop word, 2 lifetime expired
+  float result[60];             // scores of up to 60 models
   unsigned long long t_start, t_exit, t_end;  // diagnostics (100 MHz clock)
 };
 
@@ -45,60 +47,76 @@ __device__ __forceinline__ unsigned long long rt_now() {
   return __builtin_amdgcn_s_memrealtime();  // 100 MHz constant clock
 }
 
+__host__ __device__ __forceinline__ uint32_t line_mix(uint32_t d, uint32_t pos) {
+  uint32_t h = d + pos * 0x9E3779B9u;
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
+  return v;
+}
+
 template <typename WT>
 __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, long long wstride,
                                                    int M, int dn, int dc, int dim, int bias,
                                                    int cspan, Mailbox* mb,
                                                    unsigned long long lifetime_ticks) {
   const int lane = threadIdx.x;
+  const int nf = dn + dc;
   const unsigned long long t_end = rt_now() + lifetime_ticks;
-  unsigned int last = sys_load(&mb->seq_req);
+  unsigned int last = sys_load(&mb->req[0]);
   if (lane == 0) {
     sys_store(&mb->t_start, t_end - lifetime_ticks);
     sys_store(&mb->t_end, t_end);
     sys_store(&mb->alive, 1u);
   }
+  int polls = 0;
   while (true) {
-    unsigned int seq = 0;
-    bool go = false, quit = false;
-    if (lane == 0) {
-      // bounded poll: re-check the clock every 64 polls
-      for (int i = 0; i < 64; ++i) {
-        seq = sys_load(&mb->seq_req);
-        if (seq != last) {
-          go = true;
-          break;
+    const unsigned int d = sys_load(&mb->req[lane]);  // the whole line in one read
+    const unsigned int seq = __builtin_amdgcn_readfirstlane(d);
+    if (seq == last) {
+      if (++polls >= 64) {  // re-check the clock / stop word every 64 polls
+        polls = 0;
+        bool quit = false;
+        if (lane == 0) {
+          const bool st = sys_load(&mb->stop) != 0u;
+          const bool late = rt_now() > t_end;
+          quit = st || late;
+          if (quit) {
+            sys_store(&mb->exit_reason, st ? 1u : 2u);
+            sys_store(&mb->t_exit, rt_now());
+          }
         }
-        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_readfirstlane(quit ? 1 : 0)) break;
       }
-      if (!go) {
-        const bool st = sys_load(&mb->stop) != 0u;
-        const bool late = rt_now() > t_end;
-        quit = st || late;
-        if (quit) {
-          sys_store(&mb->exit_reason, st ? 1u : 2u);
-          sys_store(&mb->t_exit, rt_now());
-        }
-      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
     }
-    go = __builtin_amdgcn_readfirstlane(go ? 1 : 0) != 0;
-    quit = __builtin_amdgcn_readfirstlane(quit ? 1 : 0) != 0;
-    if (quit) break;
-    if (!go) continue;
-    seq = __builtin_amdgcn_readfirstlane(seq);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // order payload reads after the sequence
-    // lane = feature (≤ 64 features: dn + dc + bias)
+    // checksum over the payload lanes (position-mixed), keyed by the sequence
+    const bool pl = lane >= 2 && lane < 2 + nf;
+    const uint32_t x = wave_xor(pl ? line_mix(d, (uint32_t)lane) : 0u) ^ line_mix(seq, 0u);
+    const uint32_t csum = (uint32_t)__shfl((int)d, 1, 64);
+    if (__builtin_amdgcn_readfirstlane(x == csum ? 1 : 0) == 0) continue;  // torn: re-poll
+    // lane j ← payload dword j (feature j)
+    const unsigned int fj = (unsigned int)__shfl((int)d, (lane + 2) & 63, 64);
     int idx = -1;
     float v = 0.f;
     const int j = lane;
-    if (j == dn + dc && bias) {
+    if (j == nf && bias) {
       idx = dim - 1;
       v = 1.f;
     } else if (j < dn) {
       idx = j;
-      v = sys_load(&mb->num[j]);
-    } else if (j < dn + dc) {
-      const int c = sys_load(&mb->cat[j - dn]);
+      v = __uint_as_float(fj);
+    } else if (j < nf) {
+      const int c = (int)fj;
       if (cspan > 0) {
         const unsigned u = (unsigned)c & 0xFFFFu;
         if (u != 0xFFFFu) {
@@ -122,6 +140,7 @@ __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, lon
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     if (lane == 0) sys_store(&mb->seq_done, seq);
     last = seq;
+    polls = 0;
   }
   if (lane == 0) sys_store(&mb->alive, 0u);
 }
@@ -139,14 +158,13 @@ OMLDM_API void* omldm_mailbox_alloc() {
 }
 
 OMLDM_API void omldm_mailbox_free(void* p) {
-  if (p) (void)hipHostFree(p);
+  if (p) hipHostFree(p);
 }
 
-// Launches the persistent wave on `stream` (use a stream of its own).
 OMLDM_API int omldm_serve_start(const void* w, int w_bf16, long long wstride, int M, int dn,
                                 int dc, int dim, int bias, int cspan, void* mailbox,
                                 long long lifetime_us, void* stream) {
-  if (M < 1 || M > 60 || dn + dc + (bias ? 1 : 0) > 64 || dn > 256 || dc > 256) return -2;
+  if (M < 1 || M > 60 || dn + dc > kReqWords - 2 || dn + dc + (bias ? 1 : 0) > 64) return -2;
   Mailbox* hmb = (Mailbox*)mailbox;
   void* dmb = nullptr;
   if (hipHostGetDevicePointer(&dmb, mailbox, 0) != hipSuccess || !dmb) return -3;
@@ -165,15 +183,26 @@ OMLDM_API int omldm_serve_start(const void* w, int w_bf16, long long wstride, in
   return (int)hipGetLastError();
 }
 
-// Host side of one request: writes the point, bumps the sequence, spins (bounded) for
-// completion, copies the M scores out. Returns 0, or -1 on timeout.
+// Host side of one request: payload → checksum → sequence (release), then a bounded spin
+// on the completion sequence; copies the M scores out. Returns 0, or -1 on timeout.
 OMLDM_API int omldm_serve_request(void* mailbox, const float* num, int dn, const int* cat, int dc,
                                   int M, float* out, long long timeout_us) {
   Mailbox* mb = (Mailbox*)mailbox;
-  for (int j = 0; j < dn; ++j) mb->num[j] = num[j];
-  for (int j = 0; j < dc; ++j) mb->cat[j] = cat[j];
-  const unsigned int seq = __atomic_load_n(&mb->seq_req, __ATOMIC_RELAXED) + 1u;
-  __atomic_store_n(&mb->seq_req, seq, __ATOMIC_RELEASE);
+  const unsigned int seq = __atomic_load_n(&mb->req[0], __ATOMIC_RELAXED) + 1u;
+  uint32_t x = line_mix(seq, 0u);
+  for (int j = 0; j < dn; ++j) {
+    uint32_t u;
+    std::memcpy(&u, &num[j], 4);
+    __atomic_store_n(&mb->req[2 + j], u, __ATOMIC_RELAXED);
+    x ^= line_mix(u, (uint32_t)(2 + j));
+  }
+  for (int j = 0; j < dc; ++j) {
+    const uint32_t u = (uint32_t)cat[j];
+    __atomic_store_n(&mb->req[2 + dn + j], u, __ATOMIC_RELAXED);
+    x ^= line_mix(u, (uint32_t)(2 + dn + j));
+  }
+  __atomic_store_n(&mb->req[1], x, __ATOMIC_RELAXED);
+  __atomic_store_n(&mb->req[0], seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();
   while (__atomic_load_n(&mb->seq_done, __ATOMIC_ACQUIRE) != seq) {
     if (std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() -
