@@ -55,6 +55,7 @@ struct TableGeom {
   int log2cap;
   int log2nb;
   int kshift;
+  int lgg;  // log2 buckets per reduce group (flush layout: [group][spoke][2^lgg · BS])
 };
 constexpr int kOvf = 64;
 
@@ -332,9 +333,15 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
   // the (rare) overflow-area entries are added to the accumulator directly.
   const float scale = sigma * p.inv_p;
   if (!(ablate & 1)) {
-    int2* trow = tables + (size_t)s * tsz;
-    for (int i = lane; i < cap; i += kWave)
-      trow[i] = make_int2(keys[i], __float_as_int(vals[i] * scale));
+    // group-major layout: the reducer of group q then streams one contiguous region
+    // (slot i of spoke s → [q = i >> seg][s][i & (2^seg − 1)], full-line segments)
+    const int seg_log2 = (g.log2cap - g.log2nb) + g.lgg;
+    const size_t S_tot = gridDim.x;
+    for (int i = lane; i < cap; i += kWave) {
+      const size_t q = (size_t)(i >> seg_log2);
+      tables[((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1))] =
+          make_int2(keys[i], __float_as_int(vals[i] * scale));
+    }
     for (int i = cap + lane; i < tsz; i += kWave) {
       const int k = keys[i];
       const float v = vals[i] * scale;
@@ -400,23 +407,17 @@ __global__ __launch_bounds__(256) void linear_reduce_kernel(
     return;
   }
   float* acc = reinterpret_cast<float*>(smem);
-  const int span = 1 << g.kshift;
-  const int b = blockIdx.x;
+  const int span = 1 << (g.kshift + g.lgg);  // keys of the 2^lgg buckets of this group
+  const int q = blockIdx.x;
   for (int i = threadIdx.x; i < span; i += 256) acc[i] = 0.f;
   __syncthreads();
-  const int bs_log2 = g.log2cap - g.log2nb;
-  const int BS = 1 << bs_log2;
-  const int tsz = (1 << g.log2cap) + kOvf;
-  const int lo = b << g.kshift;
-  // 16-byte loads (two slots), four in flight per thread.
-  const int pr_log2 = bs_log2 - 1;  // BS ≥ 4 → ≥ 2 slot pairs per bucket
-  const long long items = (long long)S_act << pr_log2;
-  const int4* t4 = reinterpret_cast<const int4*>(tables);
-  const size_t row4 = (size_t)tsz >> 1;
-  const size_t boff4 = ((size_t)b << bs_log2) >> 1;
-  auto addr = [&](long long ii) {
-    return (size_t)(ii >> pr_log2) * row4 + boff4 + (size_t)(ii & ((1 << pr_log2) - 1));
-  };
+  const int seg_log2 = (g.log2cap - g.log2nb) + g.lgg;
+  const int lo = q << (g.kshift + g.lgg);
+  // the group's region is contiguous: S_act segments of 2^seg int2 → 16-byte loads (two
+  // slots), four in flight per thread
+  const long long items = (long long)S_act << (seg_log2 - 1);
+  const int4* t4 = reinterpret_cast<const int4*>(tables) + (((size_t)q * S) << (seg_log2 - 1));
+  auto addr = [](long long ii) { return (size_t)ii; };
   long long it = threadIdx.x;
   for (; it + 3 * 256 < items; it += 4 * 256) {
     int4 v[4];
@@ -439,6 +440,13 @@ __global__ __launch_bounds__(256) void linear_reduce_kernel(
     const float v = acc[i];
     if (k < dim && v != 0.f) dacc[k] += v;
   }
+}
+
+// Buckets per reduce group: the group's LDS image (2^(kshift+lgg) floats) ≤ 64 KiB.
+static inline int reduce_lgg(int kshift, int log2nb) {
+  int lgg = 14 - kshift;
+  if (lgg < 0) lgg = 0;
+  return lgg < log2nb ? lgg : log2nb;
 }
 
 // One wavefront per example; M stacked models (w + m*wstride) → out[t*M + m].
@@ -518,8 +526,9 @@ static int launch_round(const void* w, const void* num, int dn, const void* cat,
                      y, B, R, dim, ws, tables, dacc, p, g, ablate);
   const long long sact_ll = R > 0 ? ((long long)B + R - 1) / R : 0;
   const int S_act = sact_ll < S ? (int)sact_ll : S;
-  const int nb = (!(ablate & 1) && S_act > 0) ? (dim + (1 << g.kshift) - 1) >> g.kshift : 0;
-  const size_t rlds = nb ? (size_t(1) << g.kshift) * 4 : 0;
+  const int gspan_log2 = g.kshift + g.lgg;
+  const int nb = (!(ablate & 1) && S_act > 0) ? (dim + (1 << gspan_log2) - 1) >> gspan_log2 : 0;
+  const size_t rlds = nb ? (size_t(1) << gspan_log2) * 4 : 0;
   e = check_dyn_lds((const void*)linear_reduce_kernel, rlds);
   if (e) return e;
   hipLaunchKernelGGL(linear_reduce_kernel, dim3(nb + kWsStat + dn + 1), dim3(256), rlds, st,
@@ -625,7 +634,8 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
   int geo[3];
   if (omldm_linear_table_geom(dim, log2cap, geo)) return -3;
-  const TableGeom g{geo[0], geo[1], geo[2]};
+  const TableGeom g{geo[0], geo[1], geo[2], reduce_lgg(geo[2], geo[1])};
+  if ((g.log2cap - g.log2nb) + g.lgg < 1) return -3;  // ≥ 2 slots per segment (int4 loads)
   const float shrink = rule == kLogistic ? 1.f - lr * lam : 1.f - lam;
   const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias, cspan,
                     variant == kPA1 ? C : INFINITY, variant == kPA2 ? 0.5f / C : 0.f, shrink,
