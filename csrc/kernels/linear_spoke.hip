@@ -442,9 +442,13 @@ __global__ __launch_bounds__(256) void linear_reduce_kernel(
   }
 }
 
-// Buckets per reduce group: the group's LDS image (2^(kshift+lgg) floats) ≤ 64 KiB.
+// Buckets per reduce group (2^lgg). Measured at 8192 spokes × 1K tables, dim 2^20:
+// lgg 0 → 0.135 ms/step (256 reduce blocks, each streaming its 256 KiB region), lgg 1 →
+// 0.149, lgg 2 → 0.195 (64 blocks: too few to pull HBM bandwidth), so one bucket per group.
 static inline int reduce_lgg(int kshift, int log2nb) {
-  int lgg = 14 - kshift;
+  (void)kshift;
+  int lgg = 0;
+  if (const char* e = getenv("OMLDM_REDUCE_LGG")) lgg = atoi(e);  // diagnostics sweep
   if (lgg < 0) lgg = 0;
   return lgg < log2nb ? lgg : log2nb;
 }
