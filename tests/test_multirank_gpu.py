@@ -72,3 +72,52 @@ def test_two_ranks_one_gpu_equal_one_rank_double_spokes(cuda):
         P.round(b.to(cuda))
     torch.cuda.synchronize()
     torch.testing.assert_close(L.w.cpu(), w0, rtol=1e-3, atol=1e-4)
+
+
+def _proto_rank(rank, world, port, out, proto, learner, cfg):
+    import torch.distributed as dist
+
+    from omldm_amd.io.synthetic import synth_batch
+    from omldm_amd.models import make_learner
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.parallel.protocols import make_protocol
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    task = 1 if learner == "ORR" else 0
+    L = make_learner(learner, {}, SP, dev)
+    P = make_protocol(proto, Comm(), L, cfg, spokes=16)
+    for r in range(4):
+        b = synth_batch(SP, 1024, start=(r * world + rank) * 1024, seed=11, task=task)
+        P.round(b.to(dev))
+    P.finalize()
+    torch.cuda.synchronize()
+    res = {"w": L.state_vector().detach().cpu()}
+    for attr in ("_E", "_c"):
+        if getattr(P, attr, None) is not None:
+            res[attr] = getattr(P, attr).detach().cpu()
+    torch.save(res, os.path.join(out, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto,learner,cfg", [
+    ("Asynchronous", "PA", {}), ("SSP", "SVM", {"staleness": 2}),
+    ("EASGD", "PA", {"tau": 2, "alpha": 0.3}), ("GM", "ORR", {"threshold": 0.01}),
+    ("FGM", "SVM", {"epsilon": 0.05})])
+def test_protocols_on_gpu_two_ranks(cuda, proto, learner, cfg):
+    """Every distributed protocol with device tensors (fused merge kernels on the GPU):
+    replicas / estimates / centres agree across ranks after the run."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_proto_rank, args=(2, _port(), d, proto, learner, cfg), nprocs=2,
+                           start_method="spawn")
+        r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+    for k in ("_E", "_c"):
+        if k in r0:
+            torch.testing.assert_close(r0[k], r1[k], rtol=1e-5, atol=1e-6)
+    if proto in ("Asynchronous", "SSP"):
+        torch.testing.assert_close(r0["w"], r1["w"], rtol=1e-5, atol=1e-6)
+    assert float(r0["w"].abs().sum()) > 0
