@@ -122,8 +122,12 @@ __device__ __noinline__ int table_find_or_insert(int* keys, int key, TableGeom g
   const uint32_t bmask = (1u << bs_log2) - 1u;
   const int base = (key >> g.kshift) << bs_log2;
   const uint32_t h = hmix((uint32_t)key);
+  // linear probing from the 4-aligned hashed start — the same order as the vector first
+  // probe in the round kernel (which covers start..start+3), so a key is never inserted
+  // twice: it sits after its start only if every slot in between was taken at insertion
+  const uint32_t s0 = (h & bmask) & ~3u;
   for (uint32_t q = 0; q <= bmask; ++q) {
-    const int i = base + (int)((h + q) & bmask);
+    const int i = base + (int)((s0 + q) & bmask);
     const int k = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (k == key) return i;
     if (k == kEmptyKey) {
@@ -176,7 +180,7 @@ struct Step {
 };
 
 // ablate (timing diagnostics only): bit0 skip the table flush, bit1 skip the sequential
-// phase.
+// phase, bit2 skip the w0 gathers, bit3 skip the LDS table probes.
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void linear_round_kernel(
     const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
@@ -255,35 +259,58 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
 #pragma unroll
     for (int e = 0; e < CH; ++e)
 #pragma unroll
-      for (int f = 0; f < FPL; ++f) wv[e][f] = slot[e][f] >= 0 ? to_f(w[slot[e][f]]) : 0.f;
+      for (int f = 0; f < FPL; ++f)
+        wv[e][f] = (slot[e][f] >= 0 && !(ablate & 4)) ? to_f(w[slot[e][f]]) : 0.f;
     if (tc + CH < t1) load_chunk(tc + CH);
-    // Resolve the LDS slots of hashed features: one batched first probe for the
-    // whole chunk (independent ds_reads, then independent CAS), slow path rarely.
-    int h0[CH][FPL];
-    int k0[CH][FPL];
+    // Resolve the LDS slots of hashed features. First probe: ONE 16-byte ds_read of the
+    // four slots at the key's 4-aligned hashed start in its bucket per (row, feature), all
+    // issued for the whole
+    // chunk before any is consumed; a hit or a first-empty CAS settles almost every key,
+    // the full-bucket / lost-race case takes the slow path (which scans the whole bucket,
+    // so keys are found wherever either path inserted them).
+    int b0[CH][FPL];
+    int4 kq[CH][FPL];
 #pragma unroll
     for (int e = 0; e < CH; ++e)
 #pragma unroll
       for (int f = 0; f < FPL; ++f) {
         const int key = slot[e][f];
-        h0[e][f] = ((key >> g.kshift) << bs_log2) + (int)(hmix((uint32_t)key) & bmask);
-        k0[e][f] = (dcol[f] < 0 && key >= 0)
-                       ? __hip_atomic_load(&keys[h0[e][f]], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP)
-                       : 0;
+        b0[e][f] = ((key >> g.kshift) << bs_log2) + (int)((hmix((uint32_t)key) & bmask) & ~3u);
+        kq[e][f] = (dcol[f] < 0 && key >= 0 && !(ablate & 8))
+                       ? *reinterpret_cast<const int4*>(&keys[b0[e][f]])
+                       : make_int4(0, 0, 0, 0);
       }
 #pragma unroll
     for (int e = 0; e < CH; ++e)
 #pragma unroll
       for (int f = 0; f < FPL; ++f) {
         const int key = slot[e][f];
-        if (dcol[f] < 0 && key >= 0) {
-          int sl = -2;
-          if (k0[e][f] == key) {
-            sl = h0[e][f];
-          } else if (k0[e][f] == kEmptyKey) {
-            const int prev = atomicCAS(&keys[h0[e][f]], kEmptyKey, key);
-            if (prev == kEmptyKey || prev == key) sl = h0[e][f];
+        if (dcol[f] < 0 && key >= 0 && (ablate & 8)) {
+          slot[e][f] = -1;  // diagnostics: no table slot
+        } else if (dcol[f] < 0 && key >= 0) {
+          const int4 q = kq[e][f];
+          const int b = b0[e][f];
+          int sl = q.x == key ? b : q.y == key ? b + 1 : q.z == key ? b + 2 : q.w == key ? b + 3 : -2;
+          if (sl == -2) {
+            const int j = q.x == kEmptyKey ? 0 : q.y == kEmptyKey ? 1 : q.z == kEmptyKey ? 2
+                        : q.w == kEmptyKey ? 3 : -1;
+            if (j >= 0) {
+              const int prev = atomicCAS(&keys[b + j], kEmptyKey, key);
+              if (prev == kEmptyKey || prev == key) sl = b + j;
+            }
+          }
+          // lost a race to an earlier row of the chunk (stale view): re-read the four
+          // slots and retry inline — rows of one chunk often share a bucket
+          for (int r = 0; r < 3 && sl == -2; ++r) {
+            const int4 q2 = *reinterpret_cast<const int4*>(&keys[b]);
+            sl = q2.x == key ? b : q2.y == key ? b + 1 : q2.z == key ? b + 2
+               : q2.w == key ? b + 3 : -2;
+            if (sl != -2) break;
+            const int j = q2.x == kEmptyKey ? 0 : q2.y == kEmptyKey ? 1 : q2.z == kEmptyKey ? 2
+                        : q2.w == kEmptyKey ? 3 : -1;
+            if (j < 0) break;  // the four slots are full: slow path
+            const int prev = atomicCAS(&keys[b + j], kEmptyKey, key);
+            if (prev == kEmptyKey || prev == key) sl = b + j;
           }
           if (sl == -2) {
             sl = table_find_or_insert(keys, key, g);
@@ -618,7 +645,9 @@ static int ceil_log2(long long x) {
 // reducer), ≥ 4 slots per bucket. Returns false when log2cap is too small.
 OMLDM_API int omldm_linear_table_geom(int dim, int log2cap, int* out3) {
   const int ld = ceil_log2(dim);
-  const int kshift = ld < 12 ? ld : 12;
+  int kbase = 12;
+  if (const char* e = getenv("OMLDM_KSHIFT")) kbase = atoi(e);  // diagnostics sweep
+  const int kshift = ld < kbase ? ld : kbase;
   const int log2nb = ld - kshift;
   if (log2cap - log2nb < 2) return -1;
   out3[0] = log2cap;
