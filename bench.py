@@ -365,7 +365,7 @@ def main(argv=None) -> int:
             "per_gpu_examples_per_s": round(value / world, 1),
             "holdout_accuracy": round(acc, 4), "fitted_examples_rank0": fitted,
             "host_us_per_step": {k: round(v / a.steps * 1e6, 1) for k, v in host_t.items()},
-            "lds_table_overflow": overflow, "device": torch.cuda.get_device_name(device)
+            "lds_table_overflow": overflow, "numa": comm.placement, "device": torch.cuda.get_device_name(device)
             if on_gpu else "cpu",
         }
         print(json.dumps(out), flush=True)

@@ -50,6 +50,7 @@ class Comm:
         self.stats = CommStats()
         self.backend = dist.get_backend(group) if self.enabled else "none"
         self.fault = None  # utils.fault.FaultPlan (tests): may drop this rank's messages
+        self.placement: dict = {}  # NUMA binding of this rank (utils/topology.py)
 
     # ------------------------------------------------------------ collectives
     def all_reduce_(self, t: torch.Tensor, tag: str = "sync", op=None, async_op=False):
@@ -170,8 +171,13 @@ def init_distributed(device_type: str = "auto", timeout_s: float = 600.0) -> tup
     backend = os.environ.get("OMLDM_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     ndev = torch.cuda.device_count() if use_gpu else 0
     device = torch.device("cuda", local_rank % max(1, ndev)) if use_gpu else torch.device("cpu")
+    placement = {}
     if use_gpu:
         torch.cuda.set_device(device)
+        # host thread + pinned pages on the GPU's socket (utils/topology.py)
+        from omldm_amd.utils.topology import bind_to_device
+
+        placement = bind_to_device(device)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
@@ -180,4 +186,6 @@ def init_distributed(device_type: str = "auto", timeout_s: float = 600.0) -> tup
             kw["device_id"] = device
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    return Comm(), device
+    comm = Comm()
+    comm.placement = placement
+    return comm, device
