@@ -24,6 +24,7 @@ from omldm_amd.engine.job import Job  # noqa: E402
 from omldm_amd.io.synthetic import synth_json_records  # noqa: E402
 from omldm_amd.io.transport import FileBroker  # noqa: E402
 from omldm_amd.parallel.comm import init_distributed  # noqa: E402
+from omldm_amd.utils import tracing  # noqa: E402
 from omldm_amd.utils.config import JobConfig  # noqa: E402
 
 
@@ -34,6 +35,9 @@ def main(argv=None) -> int:
     ap.add_argument("--pipelines", type=int, default=1)
     ap.add_argument("--partitions", type=int, default=8)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--warmup-ticks", type=int, default=4)
+    ap.add_argument("--unique", type=int, default=100_000,
+                    help="distinct JSON records generated; the topic replays them")
     a = ap.parse_args(argv)
     comm, device = init_distributed()
     sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
@@ -41,11 +45,13 @@ def main(argv=None) -> int:
         br = FileBroker(root)
         br.create_topic("trainingData", a.partitions)
         t = time.time()
-        chunk = 100_000
-        for s in range(0, a.records, chunk):
-            recs = synth_json_records(min(chunk, a.records - s), sp, start=s, seed=3)
-            for i, r in enumerate(recs):
-                br.produce("trainingData", r, partition=(s + i) % a.partitions)
+        uniq = synth_json_records(min(a.unique, a.records), sp, start=0, seed=3)
+        per_part = [[] for _ in range(a.partitions)]
+        for i in range(a.records):
+            per_part[i % a.partitions].append(uniq[i % len(uniq)])
+        for p, recs in enumerate(per_part):
+            br.produce_block("trainingData", p, ("\n".join(recs) + "\n").encode())
+        del per_part
         gen_s = time.time() - t
         for i in range(a.pipelines):
             br.produce("requests", json.dumps({
@@ -65,24 +71,28 @@ def main(argv=None) -> int:
         job = Job(cfg, comm, device)
         while not job.pipes:  # pipeline creation (and first-touch setup) is not timed
             job.tick()
+        for _ in range(a.warmup_ticks):  # staging slots grow to the record size
+            job.tick()
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         r0 = job.counters["records"]
+        tracing.reset()
         t0 = time.time()
         while job.counters["records"] + job.counters["invalid"] < a.records // comm.world:
             job.tick()
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         wall = time.time() - t0
+        stages = tracing.report()
         job.run()  # idle timeout → final statistics
-        m = job.final_stats.metrics if job.final_stats else {}
         if comm.rank == 0:
             print(json.dumps({
                 "metric": "end-to-end engine training records/s (JSON topic → model)",
                 "value": round((job.counters["records"] - r0) * comm.world / max(wall, 1e-9), 1),
                 "unit": "records/s", "n_gpus": comm.world, "records": job.counters["records"],
                 "pipelines": a.pipelines, "batch": a.batch, "wall_s": round(wall, 3),
-                "generate_s": round(gen_s, 1), "stages_ms": m.get("stages"),
+                "generate_s": round(gen_s, 1), "stages_ms": stages,
+                "ticks_timed": stages.get("poll", {}).get("calls"),
                 "device": str(device)}), flush=True)
     return 0
 

@@ -299,18 +299,27 @@ __device__ int parse_record(const unsigned char* b, const unsigned char* e, int 
 __global__ __launch_bounds__(256) void json_parse_kernel(
     const unsigned char* __restrict__ buf, const long long* __restrict__ offs, int n, int dnum,
     int ddisc, int dc, long long dim, int cspan, float* __restrict__ num, void* __restrict__ cat,
-    float* __restrict__ y, signed char* __restrict__ op, int* __restrict__ nvalid) {
+    float* __restrict__ y, signed char* __restrict__ op, int* __restrict__ counts) {
   const int dn = dnum + ddisc;
-  int mine = 0;
+  int ntrain = 0, nfcst = 0, nbad = 0;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int r = parse_record(buf + offs[i], buf + offs[i + 1], dnum, ddisc, dc, dim, cspan,
                                num + (size_t)i * dn, static_cast<int*>(cat) + (size_t)i * dc,
                                static_cast<unsigned short*>(cat) + (size_t)i * dc, y + i);
     op[i] = (signed char)r;
-    mine += r >= 0;
+    ntrain += r == 0;
+    nfcst += r == 1;
+    nbad += r < 0;
   }
-  const float tot = wave_sum((float)mine);
-  if ((threadIdx.x & 63) == 0 && tot > 0.f && nvalid) atomicAdd(nvalid, (int)tot);
+  // counts[0..2] += (training, forecasting, invalid): one atomic per wave and kind
+  float a = (float)ntrain, b = (float)nfcst;
+  wave_sum2(a, b);
+  const float c = wave_sum((float)nbad);
+  if ((threadIdx.x & 63) == 0 && counts) {
+    if (a > 0.f) atomicAdd(counts, (int)a);
+    if (b > 0.f) atomicAdd(counts + 1, (int)b);
+    if (c > 0.f) atomicAdd(counts + 2, (int)c);
+  }
 }
 
 }  // namespace omldm
@@ -318,16 +327,17 @@ __global__ __launch_bounds__(256) void json_parse_kernel(
 using namespace omldm;
 
 // buf/offs/outputs are device pointers; offs has n+1 entries (record i = buf[offs[i],
-// offs[i+1])). Layout of the outputs as omldm_parse_instances (host).
+// offs[i+1])). Layout of the outputs as omldm_parse_instances (host). counts (optional,
+// 3 ints, accumulated): training, forecasting and invalid records.
 OMLDM_API int omldm_json_parse(const void* buf, const long long* offs, int n, int dnum,
                                int ddisc, int dc, long long dim, int cspan, float* num,
-                               void* cat, float* y, signed char* op, int* nvalid,
+                               void* cat, float* y, signed char* op, int* counts,
                                void* stream) {
   if (n <= 0) return 0;
   int blocks = (n + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
                      (const unsigned char*)buf, offs, n, dnum, ddisc, dc, dim, cspan, num, cat, y,
-                     op, nvalid);
+                     op, counts);
   return (int)hipGetLastError();
 }

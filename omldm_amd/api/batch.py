@@ -59,6 +59,21 @@ class FeatureSpace:
             raise ValueError("hash dimension too small for field-aware hashing")
 
 
+def index_tensor(idx, device) -> torch.Tensor:
+    """Host index array (ndarray / CPU tensor) → int64 tensor on ``device``. On GPUs the
+    copy goes through a pinned block of the caching host allocator and is
+    non-blocking: a pageable ``.to(device)`` would wait for the whole stream (the
+    previous round's kernels) before returning."""
+    if isinstance(idx, np.ndarray):
+        idx = torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64))
+    device = torch.device(device)
+    if idx.device == device:
+        return idx
+    if device.type == "cuda" and idx.device.type == "cpu":
+        return idx.to(torch.int64).pin_memory().to(device, non_blocking=True)
+    return idx.to(device)
+
+
 @dataclass
 class HashedBatch:
     num: torch.Tensor
@@ -112,12 +127,11 @@ class HashedBatch:
                           None if self.raw is None else self.raw[a:b])
 
     def select(self, idx) -> "HashedBatch":
-        if isinstance(idx, np.ndarray):
-            idx = torch.from_numpy(idx)
-        idx = idx.to(self.y.device)
         raw = None
         if self.raw is not None:
-            raw = [self.raw[i] for i in idx.tolist()]
+            host = idx if isinstance(idx, np.ndarray) else idx.cpu().numpy()
+            raw = [self.raw[int(i)] for i in host]
+        idx = index_tensor(idx, self.y.device)
         return self._like(self.num[idx], self.cat[idx], self.y[idx], raw)
 
     @staticmethod

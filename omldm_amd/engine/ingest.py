@@ -1,0 +1,263 @@
+"""Tick ingest: this rank's training ∪ forecasting records, read one tick ahead.
+
+Reference: one Flink Kafka source subtask per partition deserialises records one at a
+time and forwards them to the spokes (omldm/Job.scala:42-57,
+omldm/job/FlinkLearning.scala:70,83). Here a tick's records are ONE byte block:
+
+    topic log ──pread (no GIL, csrc/host/logio.cpp)──► pinned staging slot
+              ──H2D──► HBM ──GPU JSON parser (csrc/kernels/json_ingest.hip)──► batch
+
+Two background stages run behind the tick: a reader thread fills slot k+2 from the logs
+while a staging thread moves slot k+1 to HBM and parses it on the GPU (its own copy
+stream), while the tick trains on slot k. Slots are reused round-robin; a slot's host
+bytes are rewritten only after its H2D copy event, its HBM buffers only after the
+``consumed`` event the tick records behind its last use.
+
+Latency: a prefetched block that came back empty is re-polled synchronously at the start
+of the tick, so an idle stream's new records are picked up by the next tick, as with
+synchronous polling (records that arrive while a read is in flight may land one tick
+later; CPU jobs poll synchronously by default, which keeps tests tick-exact). Offsets for checkpoints are the consumers' offsets
+*after* the block the job has actually processed (``TickBlock.offsets``), never the
+prefetcher's read-ahead position.
+"""
+from __future__ import annotations
+
+import collections
+import concurrent.futures as cf
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+
+@dataclass
+class TickBlock:
+    slot: int
+    data: torch.Tensor            # uint8 staging slot (pinned on GPU ranks)
+    offs_t: torch.Tensor          # int64 record offsets (pinned), [n + 1] valid
+    n: int = 0
+    nbytes: int = 0
+    offsets: dict = field(default_factory=dict)  # consumer offsets after this block
+    event: object = None          # GPU event behind the H2D copy of this slot
+    ends: np.ndarray | None = None  # true record ends where a region gap follows
+    d_raw: torch.Tensor | None = None   # HBM copy of the slot (staged by the ingest thread)
+    d_offs: torch.Tensor | None = None
+    staged: object = None         # copy-stream event: d_raw/d_offs hold this block
+    consumed: object = None       # compute-stream event: the tick is done with the slot
+    parsed: tuple | None = None   # (num, cat, y, op) device views, parsed by the thread
+    counts: np.ndarray | None = None  # host (training, forecasting, invalid) of `parsed`
+    out: tuple | None = None      # slot-persistent parse outputs + counts buffers
+
+    @property
+    def offs(self) -> np.ndarray:
+        return self.offs_t.numpy()[: self.n + 1]
+
+    @property
+    def buf(self) -> np.ndarray:
+        return self.data.numpy()[: self.nbytes]
+
+    def raw(self):
+        from omldm_amd.io.parse import RawView
+
+        return RawView(self.buf, self.offs, self.ends)
+
+    def to_bytes(self) -> tuple[bytes, np.ndarray]:
+        """Detached, gap-free copy (records kept past this tick, e.g. the pre-Create
+        buffer)."""
+        if self.ends is None:
+            return self.buf.tobytes(), self.offs.copy()
+        from omldm_amd.io.transport import join_block
+
+        return join_block(list(self.raw()))
+
+
+class TickIngest:
+    def __init__(self, consumers: list, batch_size: int, pinned: bool, prefetch: bool = True,
+                 depth: int = 2, bytes_per_record: int = 1024, device=None,
+                 copy_blocks: int = 128, space=None):
+        self.consumers = consumers
+        self.space = space  # set: the ingest thread also parses each block on the GPU
+        # GPU ranks: the ingest thread also moves each block to HBM on its own copy
+        # stream (pull-copy kernel), so the tick only waits for an event
+        self.device = torch.device(device) if device is not None else None
+        self.stage = self.device is not None and self.device.type == "cuda" and pinned
+        self.copy_blocks = copy_blocks
+        self._copy_stream = torch.cuda.Stream(self.device) if self.stage else None
+        self.batch = max(1, int(batch_size))
+        self.pinned = bool(pinned)
+        self.slots: list[TickBlock] = []
+        cap = self.batch * bytes_per_record
+        # the tick's slot + `depth` read-ahead slots + one being recycled
+        self.depth = max(1, int(depth)) if prefetch else 0
+        for i in range(self.depth + 2):
+            self.slots.append(TickBlock(i, self._alloc(cap, torch.uint8),
+                                        self._alloc(len(consumers) * self.batch + 1, torch.int64)))
+        self._k = 0
+        # two pipeline stages on their own threads: host read of block k+2 ‖ H2D + GPU
+        # parse of block k+1 ‖ the tick trains on block k
+        self._pool = cf.ThreadPoolExecutor(1, thread_name_prefix="omldm-read-ahead") \
+            if prefetch else None
+        self._dev_pool = cf.ThreadPoolExecutor(1, thread_name_prefix="omldm-stage") \
+            if prefetch and self.stage else None
+        self._pending: collections.deque = collections.deque()
+        nreg = sum(len(c.parts) for c in consumers)
+        self._readers = cf.ThreadPoolExecutor(min(8, nreg), thread_name_prefix="omldm-read") \
+            if nreg > 1 else None
+
+    def _alloc(self, n: int, dtype) -> torch.Tensor:
+        return torch.empty(max(1, n), dtype=dtype, pin_memory=self.pinned)
+
+    def _fill(self, blk: TickBlock) -> TickBlock:
+        if blk.event is not None:
+            blk.event.synchronize()  # the GPU has finished copying this slot's last use
+            blk.event = None
+        # one region of the slot per (consumer, partition), sized from the observed
+        # bytes per record; regions are read concurrently when the broker allows it
+        jobs, pos = [], 0
+        for c in self.consumers:
+            for p, share, cap in c.read_plan(self.batch):
+                jobs.append((c, p, share, pos, cap))
+                pos += cap
+        if pos > blk.data.numel():
+            blk.data = self._alloc(int(pos * 1.25), torch.uint8)
+        dst = blk.data.numpy()
+
+        def read(j):
+            c, p, share, start, cap = j
+            return c.read_region(p, share, dst[start:start + cap])
+
+        if self._readers is not None and len(jobs) > 1 and \
+                all(c.broker.parallel_reads for c in self.consumers):
+            results = list(self._readers.map(read, jobs))
+        else:
+            results = [read(j) for j in jobs]
+        # Offsets: records of a region are contiguous; the first record of a region
+        # starts at the region start, so the record before it also spans the unused tail
+        # of its own region. Parsers stop at the record's closing brace; ``ends`` keeps
+        # the true end of such records for the raw echo of forecasts.
+        offs = blk.offs_t.numpy()
+        offs[0] = 0
+        n, end, gaps = 0, 0, []
+        for (c, p, share, start, cap), (k, o) in zip(jobs, results):
+            if not k:
+                continue
+            if n and start != end:
+                gaps.append((n - 1, end))
+            offs[n] = start
+            offs[n + 1:n + k + 1] = o[1:k + 1] + start
+            n += k
+            end = start + int(o[k])
+        blk.ends = None
+        if gaps:
+            ends = offs[1:n + 1].copy()
+            for i, e in gaps:
+                ends[i] = e
+            blk.ends = ends
+        blk.n, blk.nbytes = n, end
+        blk.offsets = [dict(c.offsets) for c in self.consumers]
+        return blk
+
+    def _finish(self, blk: TickBlock) -> TickBlock:
+        if self.stage and blk.n:
+            self._to_device(blk)
+        return blk
+
+    def _to_device(self, blk: TickBlock) -> None:
+        from omldm_amd.ops.ingest import pull_copy
+
+        n, nbytes = blk.n, blk.nbytes
+        with torch.cuda.device(self.device):
+            grow = (blk.d_raw is None or blk.d_raw.numel() < nbytes + 16 or
+                    blk.d_offs is None or blk.d_offs.numel() < n + 1)
+            if grow and blk.consumed is not None:
+                blk.consumed.synchronize()  # old buffers are freed: nothing may read them
+            if blk.d_raw is None or blk.d_raw.numel() < nbytes + 16:
+                blk.d_raw = torch.empty(int((nbytes + 16) * 1.25), dtype=torch.uint8,
+                                        device=self.device)
+            if blk.d_offs is None or blk.d_offs.numel() < n + 1:
+                blk.d_offs = torch.empty(blk.offs_t.numel(), dtype=torch.int64,
+                                         device=self.device)
+            cs = self._copy_stream
+            if blk.consumed is not None:
+                cs.wait_event(blk.consumed)  # the parser of this slot's last use is done
+                blk.consumed = None
+            pull_copy(blk.d_raw, blk.data[:nbytes], self.copy_blocks, cs.cuda_stream)
+            pull_copy(blk.d_offs, blk.offs_t[:n + 1], self.copy_blocks, cs.cuda_stream)
+            blk.parsed = None
+            if self.space is not None:
+                self._parse(blk, cs)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+            blk.staged = ev
+            blk.event = ev  # the host slot may be rewritten once this copy is done
+            if blk.parsed is not None:
+                ev.synchronize()  # (ingest thread) the tick gets host-side counts
+                blk.counts = blk.out[5].numpy().copy()
+
+    def _parse(self, blk: TickBlock, cs) -> None:
+        """JSON parse of the staged block into slot-persistent device outputs, plus the
+        (training, forecasting, invalid) counts read back to pinned memory."""
+        from omldm_amd.ops.ingest import json_parse
+
+        sp, dev = self.space, self.device
+        cap = self.batch * len(self.consumers)
+        if blk.out is None:
+            blk.out = (torch.empty((cap, sp.dn), dtype=torch.float32, device=dev),
+                       torch.empty((cap, sp.dc), dtype=sp.cat_dtype, device=dev),
+                       torch.empty(cap, dtype=torch.float32, device=dev),
+                       torch.empty(cap, dtype=torch.int8, device=dev),
+                       torch.zeros(3, dtype=torch.int32, device=dev),
+                       torch.zeros(3, dtype=torch.int32, pin_memory=True))
+        num, cat, y, op, cnt_d, cnt_h = blk.out
+        with torch.cuda.stream(cs):
+            cnt_d.zero_()
+            json_parse(blk.d_raw, blk.d_offs, blk.n, sp, num, cat, y, op, cnt_d, cs.cuda_stream)
+            cnt_h.copy_(cnt_d, non_blocking=True)
+        blk.parsed = (num, cat, y, op)
+
+    def _next_slot(self) -> TickBlock:
+        blk = self.slots[self._k % len(self.slots)]
+        self._k += 1
+        return blk
+
+    def _submit(self) -> None:
+        blk = self._next_slot()
+        f = self._pool.submit(self._fill, blk)
+        if self._dev_pool is not None:
+            f = self._dev_pool.submit(lambda fut=f: self._finish(fut.result()))
+        self._pending.append(f)
+
+    def next(self) -> TickBlock:
+        """This tick's block; keeps ``depth`` blocks reading / staging behind it."""
+        if self._pool is None:
+            return self._finish(self._fill(self._next_slot()))
+        if not self._pending:
+            self._submit()
+        blk = self._pending.popleft().result()
+        if blk.n == 0:
+            # idle stream: skip empty read-aheads, then poll once more now so that new
+            # records are picked up by this tick (empty reads moved no offsets)
+            while self._pending and blk.n == 0:
+                blk = self._pending.popleft().result()
+            if blk.n == 0:
+                blk = self._finish(self._fill(blk))
+        while len(self._pending) < self.depth:
+            self._submit()
+        return blk
+
+    def drain(self) -> None:
+        """Waits for the in-flight read-aheads (before reading/restoring offsets)."""
+        for f in self._pending:
+            f.result()
+
+    def close(self) -> None:
+        self.drain()
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
+        if self._dev_pool is not None:
+            self._dev_pool.shutdown(wait=True)
+            self._dev_pool = None
+        if self._readers is not None:
+            self._readers.shutdown(wait=True)
+            self._readers = None

@@ -34,6 +34,7 @@ import torch
 from omldm_amd.api.batch import FeatureSpace, HashedBatch
 from omldm_amd.api.schemas import Prediction, Request
 from omldm_amd.engine.holdout import HoldoutSet
+from omldm_amd.engine.ingest import TickBlock, TickIngest
 from omldm_amd.engine.model_store import ModelStore
 from omldm_amd.engine.pipeline import Pipeline
 from omldm_amd.engine.pipeline_map import ALL, PipelineMap
@@ -82,6 +83,16 @@ class Job:
         self.req_in = Consumer(b["requests"], cfg.requestsTopic, all_partitions=True) \
             if self.rank == 0 else None
         self.pmap = PipelineMap() if self.rank == 0 else None
+        # this rank's training ∪ forecasting records, one pinned block per tick, read one
+        # tick ahead on a background thread (engine/ingest.py)
+        self.ingest = TickIngest([self.train_in, self.fcst_in], cfg.batchSize,
+                                 pinned=self.device.type == "cuda",
+                                 prefetch=str(cfg.prefetch).lower() in ("true", "1") or (
+                                     str(cfg.prefetch).lower() == "auto" and
+                                     self.device.type == "cuda"),
+                                 device=self.device if cfg.gpuParse else None,
+                                 space=self.space if cfg.gpuParse else None)
+        self._committed = None  # consumer offsets after the last processed block
         self.pipes: dict[int, Pipeline] = {}
         self.holdout = HoldoutSet(self.space, cfg.testSetSize, self.device)
         self.store = ModelStore(self.space.dim, self.device)
@@ -149,26 +160,38 @@ class Job:
         return len(msgs), queries
 
     # --------------------------------------------------------------------- data
-    def _poll(self) -> tuple[bytes, np.ndarray]:
-        """This tick's records as one buffer + offsets (no per-record Python objects)."""
-        n = self.cfg.batchSize
-        block = concat_blocks([self.train_in.poll_block(n), self.fcst_in.poll_block(n)])
-        nrec = len(block[1]) - 1
+    def _poll(self):
+        """This tick's records: a pinned ``TickBlock`` (no per-record Python objects), a
+        (bytes, offsets) block when records buffered before the first Create are
+        replayed, or ``EMPTY_BLOCK``."""
+        blk = self.ingest.next()
+        self._committed = blk.offsets
+        nrec = blk.n
         if not self.pipes:
             # reference: points wait in a bounded record buffer until a pipeline exists
             room = max(0, self.cfg.recordBufferSize - self._buffered)
-            if nrec > room:
-                self.counters["dropped_buffer"] += nrec - room
-                block = (block[0][:int(block[1][room])], block[1][:room + 1])
-                nrec = room
             if nrec:
-                self.record_buffer.append(block)
-                self._buffered += nrec
+                buf, offs = blk.to_bytes()
+                if nrec > room:
+                    self.counters["dropped_buffer"] += nrec - room
+                    buf, offs = buf[:int(offs[room])], offs[:room + 1]
+                    nrec = room
+                if nrec:
+                    self.record_buffer.append((buf, offs))
+                    self._buffered += nrec
             return EMPTY_BLOCK
         if self.record_buffer:
-            block = concat_blocks(self.record_buffer + [block])
+            block = concat_blocks(self.record_buffer + [blk.to_bytes()])
             self.record_buffer, self._buffered = [], 0
-        return block
+            return block
+        return blk
+
+    def consumer_offsets(self) -> dict:
+        """Offsets after the last block this job processed (the prefetcher may have read
+        further; those records are re-read after a restore)."""
+        if self._committed is not None:
+            return {"train": dict(self._committed[0]), "forecast": dict(self._committed[1])}
+        return {"train": dict(self.train_in.offsets), "forecast": dict(self.fcst_in.offsets)}
 
     def _forecast(self, batch: HashedBatch):
         prod = self.brokers["predictions"]
@@ -198,7 +221,8 @@ class Job:
         round buffers are summed over ranks in ONE coalesced collective per hub layout
         (one flat bucket instead of one launch per pipeline); the other
         protocols run their own rounds."""
-        routed = self.holdout.route(batch)
+        with tracing.range("route"):
+            routed = self.holdout.route(batch)
         groups: dict[int, list] = {}
         for pid in sorted(self.pipes):
             pipe = self.pipes[pid]
@@ -246,27 +270,48 @@ class Job:
             self.faults.on_tick(self.ticks)
         if self.watchdog is not None:
             self.watchdog.beat()
-        n_ctrl, queries = self._control()
-        buf, offs = self._poll()
-        n_local = len(offs) - 1
+        with tracing.range("control"):
+            n_ctrl, queries = self._control()
+        with tracing.range("poll"):
+            block = self._poll()
+        if isinstance(block, TickBlock):
+            n_local = block.n
+        else:
+            buf, offs = block
+            n_local = len(offs) - 1
         if n_local:
             with tracing.range("parse"):
                 if self._gpu_parser is not None:  # raw JSON → HBM → one thread per record
-                    batch, op_d, _ = self._gpu_parser.parse(buf, offs, self.space)
-                    op = op_d.cpu().numpy()
+                    if isinstance(block, TickBlock):
+                        batch, op_d, cnt = self._gpu_parser.parse_block(block, self.space)
+                    else:
+                        batch, op_d, cnt = self._gpu_parser.parse(buf, offs, self.space)
+                    cnt = cnt if isinstance(cnt, np.ndarray) else cnt.cpu().numpy()
+                    n_tr, n_fc, n_bad = (int(v) for v in cnt)
+                    # the op array is only needed on the host to pick rows out
+                    op = None if n_tr == n_local else op_d.cpu().numpy()
+                elif isinstance(block, TickBlock):
+                    batch, op, _ = parse_block(block.buf, block.offs, self.space,
+                                               self.cfg.parseThreads)
+                    batch.raw = block.raw()
                 else:
                     batch, op, _ = parse_block(buf, offs, self.space, self.cfg.parseThreads)
-                nvalid = int((op >= 0).sum())
-            self.counters["records"] += nvalid
-            self.counters["invalid"] += n_local - nvalid
-            opt = torch.from_numpy(op)
-            fidx = torch.nonzero(opt == OP_FORECASTING).flatten()
-            tidx = torch.nonzero(opt == OP_TRAINING).flatten()
-            if fidx.numel():
-                tf = time.perf_counter()
-                self._forecast(batch.select(fidx).to(self.device))
-                self._fc_lat.append((time.perf_counter() - tf) * 1e3)
-            tb = batch.without_raw().select(tidx).to(self.device, non_blocking=True)
+                if op is not None:
+                    n_tr, n_fc = int((op == OP_TRAINING).sum()), int((op == OP_FORECASTING).sum())
+                    n_bad = n_local - n_tr - n_fc
+            self.counters["records"] += n_tr + n_fc
+            self.counters["invalid"] += n_bad
+            if op is None:  # a pure, valid training block: train on it as it is
+                tb = batch.without_raw()
+            else:
+                opt = torch.from_numpy(op)
+                fidx = torch.nonzero(opt == OP_FORECASTING).flatten()
+                tidx = torch.nonzero(opt == OP_TRAINING).flatten()
+                if fidx.numel():
+                    tf = time.perf_counter()
+                    self._forecast(batch.select(fidx).to(self.device))
+                    self._fc_lat.append((time.perf_counter() - tf) * 1e3)
+                tb = batch.without_raw().select(tidx).to(self.device, non_blocking=True)
         else:
             tb = HashedBatch.empty(self.space, 0, device=self.device)
         # global activity + termination flag (one tiny all-reduce per tick); every rank
@@ -276,8 +321,9 @@ class Job:
         if self.rank == 0 and self.cfg.test and self.idle.expired(t0) and self.pipes:
             self._flags[1] = 1.0
         self._flags[2] = float(tb.B)
-        self.comm.all_reduce_(self._flags, tag="heartbeat")
-        active, term, n_train = (float(v) for v in self._flags.tolist())
+        with tracing.range("flags"):
+            self.comm.all_reduce_(self._flags, tag="heartbeat")
+            active, term, n_train = (float(v) for v in self._flags.tolist())
         self._trained_global += int(n_train)
         if self.pipes and n_train > 0:
             self._train(tb)
@@ -285,8 +331,12 @@ class Job:
             self._answer(q)
         for pipe in self.pipes.values():
             pipe.record_learning_curve()
+        if isinstance(block, TickBlock) and block.n and self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            block.consumed = ev  # the ingest thread reuses this slot's HBM after this
         if active > 0:
-            self.idle.activity(t0)
+            self.idle.activity(time.time())  # idle = time since the last active tick ended
         if term > 0:
             self._terminate()
         if self.checkpointer is not None and self.checkpointer.due():
@@ -328,6 +378,7 @@ class Job:
             self.tick()
         for p in self.pipes.values():
             p.protocol.finalize()
+        self.ingest.close()
         if self.watchdog is not None:
             self.watchdog.stop()
         return self
@@ -336,8 +387,7 @@ class Job:
     def state_dict(self) -> dict:
         sd = {"pipelines": {pid: p.state_dict() for pid, p in self.pipes.items()},
               "holdout": self.holdout.state_dict(),
-              "consumers": {"train": self.train_in.state_dict(),
-                            "forecast": self.fcst_in.state_dict()},
+              "consumers": {k: {"offsets": v} for k, v in self.consumer_offsets().items()},
               "record_buffer": [r for b in self.record_buffer for r in RawView(*b)],
               "ticks": self.ticks,
               "counters": dict(self.counters), "world": self.world}

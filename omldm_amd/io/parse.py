@@ -7,6 +7,7 @@ counted instead of silently swallowed.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import numpy as np
@@ -29,10 +30,10 @@ class RawView:
     """Lazy per-record view of a parsed block (the raw text is only materialised for
     the records that need it: forecasts echo their point in the Prediction)."""
 
-    __slots__ = ("buf", "offs")
+    __slots__ = ("buf", "offs", "ends")
 
-    def __init__(self, buf: bytes, offs: np.ndarray):
-        self.buf, self.offs = buf, offs
+    def __init__(self, buf, offs: np.ndarray, ends: np.ndarray | None = None):
+        self.buf, self.offs, self.ends = buf, offs, ends
 
     def __len__(self):
         return len(self.offs) - 1
@@ -41,14 +42,19 @@ class RawView:
         if isinstance(i, slice):
             return [self[j] for j in range(*i.indices(len(self)))]
         i = int(i)
-        return self.buf[int(self.offs[i]):int(self.offs[i + 1])].rstrip(b"\n")
+        e = self.offs[i + 1] if self.ends is None else self.ends[i]
+        r = self.buf[int(self.offs[i]):int(e)]
+        if not isinstance(r, bytes):  # a view of a pinned staging slot
+            r = r.tobytes()
+        return r.rstrip(b"\n")
 
     def __iter__(self):
         return (self[i] for i in range(len(self)))
 
 
-def parse_block(buf: bytes, offs: np.ndarray, space: FeatureSpace, threads: int | None = None):
-    """Parses buf[offs[i]:offs[i+1]] for every i. Returns (batch, op, n_valid)."""
+def parse_block(buf, offs: np.ndarray, space: FeatureSpace, threads: int | None = None):
+    """Parses buf[offs[i]:offs[i+1]] for every i (``buf``: bytes or a uint8 ndarray,
+    e.g. a staging slot). Returns (batch, op, n_valid)."""
     n = len(offs) - 1
     num = torch.zeros((n, space.dn), dtype=torch.float32)
     cat = torch.full((n, space.dc), -1, dtype=space.cat_dtype)
@@ -58,8 +64,10 @@ def parse_block(buf: bytes, offs: np.ndarray, space: FeatureSpace, threads: int 
     if n > 0:
         offs = np.ascontiguousarray(offs, dtype=np.int64)
         threads = threads or min(8, os.cpu_count() or 1)
+        src = buf if isinstance(buf, bytes) else \
+            C.cast(C.c_void_p(np.ascontiguousarray(buf).ctypes.data), C.c_char_p)
         valid = native.host().omldm_parse_instances(
-            buf, offs.ctypes.data, n, space.n_numerical, space.n_discrete, space.dc, space.dim,
+            src, offs.ctypes.data, n, space.n_numerical, space.n_discrete, space.dc, space.dim,
             space.cat_span, num.data_ptr(), cat.data_ptr(), y.data_ptr(), op.ctypes.data,
             threads)
     return HashedBatch(num, cat, y, RawView(buf, offs), space.cat_span), op, int(valid)

@@ -30,6 +30,8 @@ def join_block(recs: list) -> tuple[bytes, np.ndarray]:
 
 
 class Broker:
+    parallel_reads = False  # may consume_into run concurrently for different partitions?
+
     def partitions(self, topic: str) -> int:
         raise NotImplementedError
 
@@ -52,6 +54,22 @@ class Broker:
         recs, nxt = self.consume(topic, partition, offset, max_records)
         buf, offs = join_block(recs)
         return buf, offs, nxt
+
+    def consume_into(self, topic: str, partition: int, offset: int, max_records: int,
+                     dst: np.ndarray, cap: int) -> tuple[int, np.ndarray, int]:
+        """Reads up to ``max_records`` whole records (≤ ``cap`` bytes) straight into
+        ``dst[:cap]`` (a pinned staging slot). Returns (n, offs[n+1] relative to dst,
+        next_offset). Generic form: consume_block + one copy; FileBroker reads the log
+        into ``dst`` directly (csrc/host/logio.cpp)."""
+        while max_records > 0:
+            buf, offs, nxt = self.consume_block(topic, partition, offset, max_records)
+            n = len(offs) - 1
+            if n == 0 or offs[-1] <= cap:
+                if n:
+                    dst[:int(offs[-1])] = np.frombuffer(buf, dtype=np.uint8, count=int(offs[-1]))
+                return n, offs, nxt
+            max_records = int(np.searchsorted(offs, cap, side="right")) - 1  # what fits
+        return 0, np.zeros(1, dtype=np.int64), offset
 
     def create_topic(self, topic: str, partitions: int) -> None:
         pass
@@ -117,11 +135,52 @@ class FileBroker(Broker):
     """Append-only JSONL logs: <root>/<topic>/<partition>.jsonl (one record per line).
     Consumer offsets are byte offsets, so every rank can tail its partitions."""
 
+    parallel_reads = True  # consume_into is a GIL-free pread: partitions read concurrently
+
     def __init__(self, root: str):
         self.root = root
         os.makedirs(root, exist_ok=True)
         self._rr = defaultdict(int)
         self._lock = threading.Lock()
+        self._fds: dict[str, int] = {}
+
+    def _fd(self, path: str) -> int:
+        fd = self._fds.get(path)
+        if fd is None:
+            fd = os.open(path, os.O_RDONLY)
+            self._fds[path] = fd
+        return fd
+
+    def close(self) -> None:
+        for fd in self._fds.values():
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+        self._fds.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+    def consume_into(self, topic, partition, offset, max_records, dst, cap):
+        """pread of the log straight into ``dst`` + memchr record index, without the GIL
+        (csrc/host/logio.cpp: omldm_read_log)."""
+        from omldm_amd.ops import native
+
+        path = os.path.join(self.root, topic, f"{partition}.jsonl")
+        offs = np.empty(max(1, max_records) + 1, dtype=np.int64)
+        if max_records <= 0 or cap <= 0 or not os.path.exists(path):
+            offs[0] = 0
+            return 0, offs[:1], offset
+        used = np.zeros(1, dtype=np.int64)
+        n = native.host().omldm_read_log(self._fd(path), offset, dst.ctypes.data, int(cap),
+                                         int(max_records), offs.ctypes.data, used.ctypes.data)
+        if n < 0:
+            raise OSError(-n, f"reading {path}")
+        return int(n), offs[:n + 1], offset + int(used[0])
 
     def _dir(self, topic):
         d = os.path.join(self.root, topic)
@@ -149,6 +208,16 @@ class FileBroker(Broker):
                 self._rr[topic] += 1
             with open(os.path.join(self._dir(topic), f"{partition % n}.jsonl"), "ab") as f:
                 f.write(value + b"\n")
+
+    def produce_block(self, topic: str, partition: int, block: bytes) -> None:
+        """Bulk append of newline-terminated records (producers that batch, e.g. a
+        Kafka producer's linger buffer)."""
+        if block and not block.endswith(b"\n"):
+            block += b"\n"
+        n = self.partitions(topic)
+        with self._lock:
+            with open(os.path.join(self._dir(topic), f"{partition % n}.jsonl"), "ab") as f:
+                f.write(block)
 
     def consume(self, topic, partition, offset, max_records):
         path = os.path.join(self._dir(topic), f"{partition}.jsonl")
@@ -226,6 +295,7 @@ class Consumer:
                                                             if p % world == rank]
         self.offsets = {p: (broker.end_offset(topic, p) if start == "latest" else 0)
                         for p in self.parts}
+        self._avg_len = 1024.0  # running bytes-per-record estimate (sizes poll_into reads)
 
     def poll(self, max_records: int) -> list[bytes]:
         out = []
@@ -252,6 +322,28 @@ class Consumer:
                 offs.append(o[1:] + base)
                 base += len(buf)
         return b"".join(bufs), np.concatenate(offs)
+
+    def read_plan(self, max_records: int) -> list[tuple[int, int, int]]:
+        """(partition, max records, byte budget) of every owned partition for one block
+        of ≤ ``max_records`` records — the regions of a staging slot that
+        ``engine.ingest.TickIngest`` fills (in parallel when the broker allows)."""
+        if not self.parts or max_records <= 0:
+            return []
+        share = max(1, max_records // len(self.parts))
+        cap = int(share * self._avg_len * 1.5) + (64 << 10)
+        return [(p, share, cap) for p in self.parts]
+
+    def read_region(self, p: int, share: int, dst: np.ndarray) -> tuple[int, np.ndarray]:
+        """Reads partition ``p`` into ``dst`` (its region); advances the offset and the
+        bytes-per-record estimate. Returns (records, offsets relative to dst)."""
+        k, o, nxt = self.broker.consume_into(self.topic, p, self.offsets[p], share, dst,
+                                             len(dst))
+        self.offsets[p] = nxt
+        if k:
+            self._avg_len = 0.8 * self._avg_len + 0.2 * (int(o[k]) / k)
+        elif self.broker.end_offset(self.topic, p) > nxt:
+            self._avg_len *= 2  # a record longer than the region: bigger regions next time
+        return k, o
 
     def state_dict(self) -> dict:
         return {"offsets": dict(self.offsets)}

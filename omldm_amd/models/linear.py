@@ -51,7 +51,7 @@ class LinearLearner(Learner):
             lam=hp_float(h, "lambda", 0.0),
             bias=bool(h.get("bias", True)),
         )
-        self.log2cap = hp_int(h, "tableLog2", 13)
+        self.log2cap = hp_int(h, "tableLog2", 0)  # 0: auto (ops/linear.py:auto_log2cap)
         self.ablate = hp_int(h, "_ablate", 0)  # timing diagnostics only
         self.chunk = hp_int(h, "chunk", 8)      # rows staged per software-pipeline step
         want16 = str(h.get("modelDtype", "fp32")).lower() in ("bf16", "bfloat16")

@@ -59,6 +59,17 @@ def pull_copy(dst: torch.Tensor, src: torch.Tensor, blocks: int = 16, stream=Non
                  "omldm_pull_copy")
 
 
+def json_parse(dbuf, doffs, n: int, space, num, cat, y, op, counts, stream) -> None:
+    """Launches csrc/kernels/json_ingest.hip on HBM-resident records (one thread each);
+    ``counts`` (3 × int32, accumulated) receives training / forecasting / invalid."""
+    assert num.shape[0] >= n and cat.shape[0] >= n and y.shape[0] >= n and op.shape[0] >= n
+    assert doffs.numel() >= n + 1 and counts.numel() >= 3
+    native.check(native.hip().omldm_json_parse(
+        dbuf.data_ptr(), doffs.data_ptr(), n, space.n_numerical, space.n_discrete, space.dc,
+        space.dim, space.cat_span, num.data_ptr(), cat.data_ptr(), y.data_ptr(), op.data_ptr(),
+        counts.data_ptr(), stream), "omldm_json_parse")
+
+
 class GpuJsonParser:
     """Parses a block of DataInstance JSON records on the GPU
     (csrc/kernels/json_ingest.hip): the raw bytes go to HBM through a pinned staging ring
@@ -90,9 +101,55 @@ class GpuJsonParser:
         self.events[i] = ev
         return d
 
+    def _dev(self, key: str, n: int, dtype) -> torch.Tensor:
+        t = getattr(self, key, None)
+        if t is None or t.numel() < n:
+            t = torch.empty(max(n, 1 << 16), dtype=dtype, device=self.device)
+            setattr(self, key, t)
+        return t
+
+    def parse_block(self, blk, space, copy_blocks: int = 32):
+        """Parses a pinned ``engine.ingest.TickBlock``. Returns (device batch with a lazy
+        raw view, device int8 op, counts) where counts = (training, forecasting,
+        invalid) — a host ndarray when the ingest thread already parsed the block
+        (``blk.parsed``: this stream only waits for its event), else a device tensor.
+        Otherwise the bytes and offsets move to HBM with the pull-copy kernel
+        (non-blocking for the host) and the parse kernel follows on this stream."""
+        from omldm_amd.api.batch import HashedBatch
+
+        n, nbytes = blk.n, blk.nbytes
+        dev = self.device
+        cur = torch.cuda.current_stream(dev)
+        if blk.parsed is not None:
+            cur.wait_event(blk.staged)
+            num, cat, y, op = (t[:n] for t in blk.parsed)
+            return HashedBatch(num, cat, y, blk.raw(), space.cat_span), op, blk.counts.copy()
+        num = torch.empty((n, space.dn), dtype=torch.float32, device=dev)
+        cat = torch.empty((n, space.dc), dtype=space.cat_dtype, device=dev)
+        y = torch.empty(n, dtype=torch.float32, device=dev)
+        op = torch.empty(n, dtype=torch.int8, device=dev)
+        counts = torch.zeros(3, dtype=torch.int32, device=dev)
+        if n > 0:
+            s = cur.cuda_stream
+            if blk.staged is not None:  # moved to HBM by the ingest thread
+                cur.wait_event(blk.staged)
+                dbuf, doffs = blk.d_raw, blk.d_offs
+            else:
+                assert blk.data.is_pinned() and blk.offs_t.is_pinned()
+                dbuf = self._dev("_raw", nbytes + 16, torch.uint8)
+                doffs = self._dev("_offs", n + 1, torch.int64)
+                pull_copy(dbuf, blk.data[:nbytes], copy_blocks, s)
+                pull_copy(doffs, blk.offs_t[: n + 1], copy_blocks, s)
+                ev = torch.cuda.Event()
+                ev.record()
+                blk.event = ev
+            assert dbuf.numel() >= nbytes and doffs.numel() >= n + 1
+            json_parse(dbuf, doffs, n, space, num, cat, y, op, counts, s)
+        return HashedBatch(num, cat, y, blk.raw(), space.cat_span), op, counts
+
     def parse(self, buf: bytes, offs, space):
         """Returns (device HashedBatch with a lazy raw view, device int8 op, device int32
-        valid count)."""
+        counts: training, forecasting, invalid)."""
         import numpy as np
 
         from omldm_amd.api.batch import HashedBatch
@@ -104,14 +161,11 @@ class GpuJsonParser:
         cat = torch.empty((n, space.dc), dtype=space.cat_dtype, device=dev)
         y = torch.empty(n, dtype=torch.float32, device=dev)
         op = torch.empty(n, dtype=torch.int8, device=dev)
-        nvalid = torch.zeros(1, dtype=torch.int32, device=dev)
+        counts = torch.zeros(3, dtype=torch.int32, device=dev)
         if n > 0:
             dbuf = self._stage(buf)
             offs64 = np.ascontiguousarray(offs, dtype=np.int64)
             doffs = torch.from_numpy(offs64).to(dev, non_blocking=False)
-            native.check(native.hip().omldm_json_parse(
-                dbuf.data_ptr(), doffs.data_ptr(), n, space.n_numerical, space.n_discrete,
-                space.dc, space.dim, space.cat_span, num.data_ptr(), cat.data_ptr(),
-                y.data_ptr(), op.data_ptr(), nvalid.data_ptr(),
-                torch.cuda.current_stream(dev).cuda_stream), "omldm_json_parse")
-        return HashedBatch(num, cat, y, RawView(buf, offs), space.cat_span), op, nvalid
+            json_parse(dbuf, doffs, n, space, num, cat, y, op, counts,
+                       torch.cuda.current_stream(dev).cuda_stream)
+        return HashedBatch(num, cat, y, RawView(buf, offs), space.cat_span), op, counts

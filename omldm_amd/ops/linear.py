@@ -52,12 +52,22 @@ def min_log2cap(dim: int) -> int:
     return max(4, ld - min(ld, 12) + 2)
 
 
+def auto_log2cap(dim: int, rows: int, keys_per_row: int) -> int:
+    """LDS delta-table size (log2 entries) for a spoke that sees ``rows`` examples with
+    ``keys_per_row`` hashed keys each: load factor ≤ 1/2 for distinct keys, clamped so
+    a wave's table stays ≤ 64 KiB (occupancy: 8 KiB tables allow 20 waves per CU,
+    64 KiB only 2 — profiles/round1_ablation.md "Occupancy"). Keys beyond the table
+    spill to the overflow path, so the size only affects speed, never the result."""
+    want = max(1, 2 * rows * max(1, keys_per_row) - 1).bit_length()
+    return min(13, max(min_log2cap(dim), want))
+
+
 def _cpu_threads() -> int:
     return int(os.environ.get("OMLDM_CPU_THREADS", min(8, os.cpu_count() or 1)))
 
 
 def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torch.Tensor,
-                 stats: torch.Tensor | None, rule: LinearRule, inv_p: float, log2cap: int = 13,
+                 stats: torch.Tensor | None, rule: LinearRule, inv_p: float, log2cap: int = 0,
                  cum: torch.Tensor | None = None, ablate: int = 0, chunk: int = 8) -> None:
     """One protocol round of S virtual spokes, R examples each (spoke s gets rows
     [s·R, (s+1)·R)). Every spoke with ≥1 row accumulates σ·Δ·inv_p into ``dacc[:dim]``,
@@ -79,6 +89,8 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         assert stats is None or stats.is_cuda
         assert num.dtype in (torch.float32, torch.bfloat16)
         assert num.shape[1] + cat.shape[1] + int(rule.bias) <= 256, "≤ 256 features per example"
+        if log2cap <= 0:  # auto: sized from rows per spoke × keys per row
+            log2cap = auto_log2cap(dim, R, cat.shape[1])
         log2cap = max(log2cap, min_log2cap(dim))
         assert 4 <= log2cap <= 14
         wsw = WS_STAT + num.shape[1] + 1

@@ -69,6 +69,8 @@ HIP_SIGS = [
     ("omldm_elastic_post", i32, [vp, vp, vp, vp, f32, i64, vp]),
     ("omldm_async_push", i32, [vp, vp, vp, vp, vp, i64, vp]),
     ("omldm_async_pull", i32, [vp, vp, vp, vp, vp, f32, i64, vp]),
+    ("omldm_holdout_route", i32, [vp, vp, vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, i64, i64,
+                                  i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp]),
     ("omldm_json_parse", i32, [vp, vp, i32, i32, i32, i32, i64, i32, vp, vp, vp, vp, vp, vp]),
     ("omldm_copy_engine_create", vp, [i32]),
     ("omldm_copy_engine_destroy", None, [vp]),
@@ -95,6 +97,8 @@ HOST_SIGS = [
     ("omldm_cpu_linear_round", i32, [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, i32, vp,
                                      i32, i32, f32, f32, f32, f32, f32, i32, i32, i32]),
     ("omldm_cpu_linear_apply", None, [vp, vp, vp, i32]),
+    ("omldm_index_lines", i64, [vp, i64, i64, vp]),
+    ("omldm_read_log", i64, [i32, i64, vp, i64, i64, vp, vp]),
     ("omldm_cpu_multiclass_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32,
                                          f32, i32, vp, vp]),
     ("omldm_cpu_linear_predict", None, [vp, i64, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp,

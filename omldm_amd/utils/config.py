@@ -66,6 +66,7 @@ class JobConfig:
     watchdogTimeout: int = 0              # ms without a finished tick → abort + exit (0: off)
     parseThreads: int = 8
     gpuParse: bool = True                 # parse + hash JSON records on the GPU (cuda only)
+    prefetch: str = "auto"                # read tick k+1 while tick k trains (auto: on GPU)
     extra: dict = field(default_factory=dict)
 
     @staticmethod

@@ -138,4 +138,4 @@ def test_checkpoint_restore_roundtrip(tmp_path):
     assert torch.equal(job2.pipes[1].learner.state_vector(), w)
     assert job2.pipes[1].learner.running_totals()["fitted"] == fitted
     assert job2.holdout.filled == job.holdout.filled
-    assert job2.train_in.offsets == job.train_in.offsets
+    assert job2.train_in.offsets == job.consumer_offsets()["train"]

@@ -1,0 +1,114 @@
+"""Tick ingest (engine/ingest.py + csrc/host/logio.cpp): regions of a staging slot read
+per partition (in parallel for file logs), one tick ahead on a background thread."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from omldm_amd.api.batch import FeatureSpace
+from omldm_amd.engine.ingest import TickIngest
+from omldm_amd.io.parse import parse_block, parse_records
+from omldm_amd.io.synthetic import synth_json_records
+from omldm_amd.io.transport import Consumer, FileBroker, MemoryBroker
+from omldm_amd.ops import native
+
+SP = FeatureSpace(4, 0, 3, 1 << 12)
+
+
+def _records(n, seed=0):
+    recs = synth_json_records(n, SP, seed=seed)
+    out = []
+    for i, r in enumerate(recs):
+        if i % 7 == 3:  # forecasting points (no target) and some long padding fields
+            d = json.loads(r)
+            d.pop("target", None)
+            d["operation"] = "forecasting"
+            d["pad"] = "x" * (i % 50)
+            r = json.dumps(d)
+        out.append(r)
+    return out
+
+
+def test_index_lines_native():
+    buf = np.frombuffer(b'{"a":1}\n{"b":22}\n{"partial"', dtype=np.uint8)
+    offs = np.zeros(8, dtype=np.int64)
+    n = native.host().omldm_index_lines(buf.ctypes.data, len(buf), 10, offs.ctypes.data)
+    assert n == 2 and list(offs[:3]) == [0, 8, 17]
+    n = native.host().omldm_index_lines(buf.ctypes.data, len(buf), 1, offs.ctypes.data)
+    assert n == 1 and offs[1] == 8
+
+
+@pytest.mark.parametrize("broker_kind", ["file", "memory"])
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_tick_ingest_reads_every_record_once(tmp_path, broker_kind, prefetch):
+    br = FileBroker(str(tmp_path)) if broker_kind == "file" else MemoryBroker()
+    br.create_topic("t", 4)
+    br.create_topic("f", 2)
+    recs = _records(700)
+    for i, r in enumerate(recs):
+        br.produce("t" if i % 3 else "f", r, partition=i % 4)
+    cons = [Consumer(br, "t"), Consumer(br, "f")]
+    ing = TickIngest(cons, batch_size=64, pinned=False, prefetch=prefetch)
+    got = []
+    for _ in range(200):
+        blk = ing.next()
+        if blk.n == 0:
+            break
+        raw = list(blk.raw())
+        assert len(raw) == blk.n
+        got.extend(r.decode() for r in raw)
+        # the parser over the slot (with region gaps) == the parser over clean records
+        b1, op1, v1 = parse_block(blk.buf, blk.offs, SP, 2)
+        b2, op2, v2 = parse_records(raw, SP, 2)
+        assert v1 == v2 and np.array_equal(op1, op2)
+        assert torch.equal(b1.cat, b2.cat) and torch.allclose(b1.num, b2.num)
+        assert torch.equal(torch.isnan(b1.y), torch.isnan(b2.y))
+    ing.close()
+    assert sorted(got) == sorted(recs)
+    if broker_kind == "file":
+        assert all(c.offsets[p] == br.end_offset(c.topic, p) for c in cons for p in c.parts)
+
+
+def test_empty_prefetch_is_repolled(tmp_path):
+    br = FileBroker(str(tmp_path))
+    br.create_topic("t", 2)
+    c = Consumer(br, "t")
+    ing = TickIngest([c], batch_size=16, pinned=False, prefetch=True)
+    assert ing.next().n == 0          # starts an (empty) background read
+    ing.drain()                       # ... which completes before the records arrive
+    for r in _records(10):
+        br.produce("t", r)
+    assert ing.next().n == 10         # produced between ticks: seen by the next tick
+    ing.close()
+
+
+def test_bulk_produce_block(tmp_path):
+    br = FileBroker(str(tmp_path))
+    br.create_topic("t", 1)
+    br.produce_block("t", 0, b'{"a":1}\n{"a":2}')
+    recs, _ = br.consume("t", 0, 0, 10)
+    assert recs == [b'{"a":1}', b'{"a":2}']
+
+
+def test_holdout_closed_forms():
+    """The index arithmetic of csrc/kernels/holdout.hip (mirrored here) enumerates the
+    non-held / held rows of a batch exactly like the counter rule (pos % 10 >= 8)."""
+    from omldm_amd.engine.holdout import HoldoutSet
+
+    def nonheld_row(r, c):
+        q = min(c, 8) + r
+        return (q // 8) * 10 + q % 8 - c
+
+    def held_row(r, c):
+        q = max(c - 8, 0) + r
+        return (q // 2) * 10 + 8 + q % 2 - c
+
+    for c in range(10):
+        for B in (1, 2, 9, 10, 11, 57, 300):
+            pos = (np.arange(B) + c) % 10
+            hold = np.flatnonzero(pos >= 8)
+            keep = np.flatnonzero(pos < 8)
+            assert [nonheld_row(r, c) for r in range(len(keep))] == keep.tolist()
+            assert [held_row(r, c) for r in range(len(hold))] == hold.tolist()
+            assert HoldoutSet._held_before(c + B) - HoldoutSet._held_before(c) == len(hold)

@@ -47,7 +47,9 @@ def test_gpu_parser_matches_host(cuda, field_aware):
     gb, gop, gval = GpuJsonParser(cuda).parse(buf, offs, sp)
     torch.cuda.synchronize()
     assert np.array_equal(gop.cpu().numpy(), hop)
-    assert int(gval.item()) == hval
+    c = gval.cpu().tolist()
+    assert c[0] + c[1] == hval and c[2] == len(recs) - hval
+    assert c[0] == int((hop == 0).sum()) and c[1] == int((hop == 1).sum())
     ok = torch.from_numpy(hop >= 0)
     assert torch.equal(gb.num.cpu()[ok], hb.num[ok])
     assert torch.equal(gb.cat.cpu()[ok], hb.cat[ok])
