@@ -36,6 +36,8 @@ def main(argv=None) -> int:
     ap.add_argument("--partitions", type=int, default=8)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--warmup-ticks", type=int, default=4)
+    ap.add_argument("--forecast-frac", type=float, default=0.0,
+                    help="share of the records sent to forecastingData (→ predictions)")
     ap.add_argument("--unique", type=int, default=100_000,
                     help="distinct JSON records generated; the topic replays them")
     a = ap.parse_args(argv)
@@ -46,11 +48,18 @@ def main(argv=None) -> int:
         br.create_topic("trainingData", a.partitions)
         t = time.time()
         uniq = synth_json_records(min(a.unique, a.records), sp, start=0, seed=3)
-        per_part = [[] for _ in range(a.partitions)]
-        for i in range(a.records):
-            per_part[i % a.partitions].append(uniq[i % len(uniq)])
-        for p, recs in enumerate(per_part):
-            br.produce_block("trainingData", p, ("\n".join(recs) + "\n").encode())
+        n_fc = int(a.records * a.forecast_frac)
+        fc = synth_json_records(min(a.unique, max(n_fc, 1)), sp, start=10**7, seed=3,
+                                operation="forecasting") if n_fc else []
+        br.create_topic("forecastingData", a.partitions)
+        for topic, n, src in (("trainingData", a.records - n_fc, uniq),
+                              ("forecastingData", n_fc, fc)):
+            per_part = [[] for _ in range(a.partitions)]
+            for i in range(n):
+                per_part[i % a.partitions].append(src[i % len(src)])
+            for p, recs in enumerate(per_part):
+                if recs:
+                    br.produce_block(topic, p, ("\n".join(recs) + "\n").encode())
         del per_part
         gen_s = time.time() - t
         for i in range(a.pipelines):
@@ -80,6 +89,7 @@ def main(argv=None) -> int:
         t0 = time.time()
         while job.counters["records"] + job.counters["invalid"] < a.records // comm.world:
             job.tick()
+        job.egress.flush()  # predictions are in their topic
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         wall = time.time() - t0
@@ -87,10 +97,11 @@ def main(argv=None) -> int:
         job.run()  # idle timeout → final statistics
         if comm.rank == 0:
             print(json.dumps({
-                "metric": "end-to-end engine training records/s (JSON topic → model)",
+                "metric": "end-to-end engine records/s (JSON topics → training + predictions)",
                 "value": round((job.counters["records"] - r0) * comm.world / max(wall, 1e-9), 1),
                 "unit": "records/s", "n_gpus": comm.world, "records": job.counters["records"],
                 "pipelines": a.pipelines, "batch": a.batch, "wall_s": round(wall, 3),
+                "forecast_frac": a.forecast_frac, "predictions": job.counters["predictions"],
                 "generate_s": round(gen_s, 1), "stages_ms": stages,
                 "ticks_timed": stages.get("poll", {}).get("calls"),
                 "device": str(device)}), flush=True)

@@ -39,6 +39,7 @@ from omldm_amd.engine.model_store import ModelStore
 from omldm_amd.engine.pipeline import Pipeline
 from omldm_amd.engine.pipeline_map import ALL, PipelineMap
 from omldm_amd.engine import statistics as ST
+from omldm_amd.io.egress import EgressWriter, RawRecords, format_predictions_chunks
 from omldm_amd.io.parse import OP_FORECASTING, OP_TRAINING, RawView, parse_block
 from omldm_amd.io.transport import join_block
 from omldm_amd.io.transport import Consumer, broker_for
@@ -93,6 +94,8 @@ class Job:
                                  device=self.device if cfg.gpuParse else None,
                                  space=self.space if cfg.gpuParse else None)
         self._committed = None  # consumer offsets after the last processed block
+        # predictions leave through a producer thread (formatted natively, io/egress.py)
+        self.egress = EgressWriter(b["predictions"], enabled=self.device.type == "cuda")
         self.pipes: dict[int, Pipeline] = {}
         self.holdout = HoldoutSet(self.space, cfg.testSetSize, self.device)
         self.store = ModelStore(self.space.dim, self.device)
@@ -193,9 +196,12 @@ class Job:
             return {"train": dict(self._committed[0]), "forecast": dict(self._committed[1])}
         return {"train": dict(self.train_in.offsets), "forecast": dict(self.fcst_in.offsets)}
 
-    def _forecast(self, batch: HashedBatch):
+    def _forecast(self, batch: HashedBatch, raw: RawRecords | None):
+        """Predictions of every pipeline for the forecasting rows; ``raw`` holds their
+        JSON records, echoed in each Prediction (one native-formatted block per
+        pipeline, io/egress.py)."""
         prod = self.brokers["predictions"]
-        out: dict[int, list] = {}
+        out: dict[int, np.ndarray] = {}
         # pipelines whose weights live in the HBM model store: ONE multi-model launch
         groups: dict[bool, list] = {}
         for pid in sorted(self.pipes):
@@ -206,15 +212,21 @@ class Job:
             with tracing.range("predict:store"):
                 s = self.store.scores(batch, [p.store_row for p in pipes], bias=bias)
                 for j, p in enumerate(pipes):
-                    out[p.id] = p.scores_to_predictions(s[:, j]).float().cpu().tolist()
+                    out[p.id] = p.scores_to_predictions(s[:, j]).float().cpu().numpy()
         for pid in sorted(self.pipes):
             if pid not in out:
                 with tracing.range(f"predict:{pid}"):
-                    out[pid] = self.pipes[pid].predict(batch).float().cpu().tolist()
-        for pid in sorted(out):
-            for raw, p in zip(batch.raw or [None] * batch.B, out[pid]):
-                prod.produce(self.cfg.predictionsTopic, Prediction(pid, raw, p).to_json())
-            self.counters["predictions"] += len(out[pid])
+                    out[pid] = self.pipes[pid].predict(batch).float().cpu().numpy()
+        with tracing.range("egress"):
+            for pid in sorted(out):
+                preds = out[pid]
+                if raw is not None:
+                    for block, offs in format_predictions_chunks(raw, pid, preds):
+                        self.egress.submit(self.cfg.predictionsTopic, block, offs)
+                else:
+                    for p in preds.tolist():
+                        prod.produce(self.cfg.predictionsTopic, Prediction(pid, None, p).to_json())
+                self.counters["predictions"] += len(preds)
 
     def _train(self, batch: HashedBatch):
         """One round of every pipeline. Synchronous pipelines train first and their
@@ -309,7 +321,9 @@ class Job:
                 tidx = torch.nonzero(opt == OP_TRAINING).flatten()
                 if fidx.numel():
                     tf = time.perf_counter()
-                    self._forecast(batch.select(fidx).to(self.device))
+                    raw = RawRecords.from_view(batch.raw, fidx.numpy()) \
+                        if batch.raw is not None else None
+                    self._forecast(batch.without_raw().select(fidx).to(self.device), raw)
                     self._fc_lat.append((time.perf_counter() - tf) * 1e3)
                 tb = batch.without_raw().select(tidx).to(self.device, non_blocking=True)
         else:
@@ -340,6 +354,7 @@ class Job:
         if term > 0:
             self._terminate()
         if self.checkpointer is not None and self.checkpointer.due():
+            self.egress.flush()  # outputs of the checkpointed ticks are in their topic
             self.checkpointer.save(self)
         self.ticks += 1
         if active == 0 and not self.terminated:
@@ -352,6 +367,7 @@ class Job:
             pipe = self.pipes[pid]
             m = self._answer(Request(id=pid, request="Query", requestId=-1), write=False)
             stats.append(ST.pipeline_statistics(pipe, m))
+        self.egress.flush()
         js = ST.job_statistics(self.cfg.jobName, self.world, self.idle.duration_ms(), stats)
         js.metrics = self._metrics(js.duration)
         self.final_stats = js
@@ -379,6 +395,7 @@ class Job:
         for p in self.pipes.values():
             p.protocol.finalize()
         self.ingest.close()
+        self.egress.close()
         if self.watchdog is not None:
             self.watchdog.stop()
         return self

@@ -71,6 +71,14 @@ class Broker:
             max_records = int(np.searchsorted(offs, cap, side="right")) - 1  # what fits
         return 0, np.zeros(1, dtype=np.int64), offset
 
+    def produce_lines(self, topic: str, block: bytes, offs: np.ndarray,
+                      partition: int | None = None) -> None:
+        """Appends the newline-terminated records block[offs[i]:offs[i+1]] (egress of a
+        whole forecast batch). Generic form: one produce per record."""
+        for i in range(len(offs) - 1):
+            rec = block[int(offs[i]):int(offs[i + 1]) - 1]
+            self.produce(topic, rec if isinstance(rec, bytes) else bytes(rec), partition=partition)
+
     def create_topic(self, topic: str, partitions: int) -> None:
         pass
 
@@ -209,15 +217,26 @@ class FileBroker(Broker):
             with open(os.path.join(self._dir(topic), f"{partition % n}.jsonl"), "ab") as f:
                 f.write(value + b"\n")
 
-    def produce_block(self, topic: str, partition: int, block: bytes) -> None:
+    def produce_block(self, topic: str, partition: int, block) -> None:
         """Bulk append of newline-terminated records (producers that batch, e.g. a
-        Kafka producer's linger buffer)."""
-        if block and not block.endswith(b"\n"):
+        Kafka producer's linger buffer); ``block``: bytes or a uint8 ndarray."""
+        if isinstance(block, np.ndarray):
+            block = memoryview(np.ascontiguousarray(block))
+        elif block and not block.endswith(b"\n"):
             block += b"\n"
         n = self.partitions(topic)
         with self._lock:
             with open(os.path.join(self._dir(topic), f"{partition % n}.jsonl"), "ab") as f:
                 f.write(block)
+
+    def produce_lines(self, topic, block, offs, partition=None):
+        if len(block) == 0:
+            return
+        if partition is None:
+            with self._lock:
+                partition = self._rr[topic] % self.partitions(topic)
+                self._rr[topic] += 1
+        self.produce_block(topic, partition, block)
 
     def consume(self, topic, partition, offset, max_records):
         path = os.path.join(self._dir(topic), f"{partition}.jsonl")

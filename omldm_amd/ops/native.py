@@ -98,6 +98,7 @@ HOST_SIGS = [
                                      i32, i32, f32, f32, f32, f32, f32, i32, i32, i32]),
     ("omldm_cpu_linear_apply", None, [vp, vp, vp, i32]),
     ("omldm_index_lines", i64, [vp, i64, i64, vp]),
+    ("omldm_format_predictions", i64, [vp, vp, vp, i64, i32, vp, vp, i64, vp]),
     ("omldm_read_log", i64, [i32, i64, vp, i64, i64, vp, vp]),
     ("omldm_cpu_multiclass_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32,
                                          f32, i32, vp, vp]),

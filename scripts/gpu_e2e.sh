@@ -8,3 +8,7 @@ if [ -n "${LEARNERS:-}" ]; then
   timeout -k 10 300 python bench/learners.py > gpurun_out/learners.json 2> gpurun_out/learners.err || { tail -20 gpurun_out/learners.err; exit 2; }
   cat gpurun_out/learners.json
 fi
+if [ -n "${FORECAST:-}" ]; then
+  timeout -k 10 300 python bench/engine_e2e.py --records 4000000 --batch 65536 --forecast-frac $FORECAST > gpurun_out/e2e_fc.json 2> gpurun_out/e2e_fc.err || { tail -20 gpurun_out/e2e_fc.err; exit 3; }
+  cat gpurun_out/e2e_fc.json
+fi
