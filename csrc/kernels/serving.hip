@@ -18,6 +18,7 @@
 #include "common.h"
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 namespace omldm {
@@ -63,7 +64,7 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
   return v;
 }
 
-template <typename WT>
+template <typename WT, bool GROUPED>
 __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, long long wstride,
                                                    int M, int dn, int dc, int dim, int bias,
                                                    int cspan, Mailbox* mb,
@@ -132,10 +133,31 @@ __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, lon
       idx = -1;
       v = 0.f;
     }
-    for (int m = 0; m < M; ++m) {
-      float acc = idx >= 0 ? v * to_f(w[(size_t)m * wstride + idx]) : 0.f;
-      acc = wave_sum(acc);
-      if (lane == 0) sys_store(&mb->result[m], acc);
+    if constexpr (GROUPED) {
+      // Models in groups of 16: the group's 16 gathers are issued back to back (one HBM
+      // round trip per group, not per model), then reduced; lane m keeps model m's
+      // score and the wave publishes all M scores with ONE wave-wide store.
+      float mine = 0.f;
+      for (int m0 = 0; m0 < M; m0 += 16) {
+        float g[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          g[k] = (idx >= 0 && m0 + k < M) ? to_f(w[(size_t)(m0 + k) * wstride + idx]) : 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          if (m0 + k < M) {  // wave-uniform: no reductions for absent models
+            const float sk = wave_sum(v * g[k]);
+            if (lane == m0 + k) mine = sk;
+          }
+        }
+      }
+      if (lane < M) sys_store(&mb->result[lane], mine);
+    } else {  // one model: gather, reduce, lane 0 publishes
+      for (int m = 0; m < M; ++m) {
+        float acc = idx >= 0 ? v * to_f(w[(size_t)m * wstride + idx]) : 0.f;
+        acc = wave_sum(acc);
+        if (lane == 0) sys_store(&mb->result[m], acc);
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     if (lane == 0) sys_store(&mb->seq_done, seq);
@@ -172,14 +194,21 @@ OMLDM_API int omldm_serve_start(const void* w, int w_bf16, long long wstride, in
   __atomic_store_n(&hmb->exit_reason, 0u, __ATOMIC_SEQ_CST);
   __atomic_store_n(&hmb->alive, 0u, __ATOMIC_SEQ_CST);
   const unsigned long long ticks = (unsigned long long)lifetime_us * 100ull;  // 100 MHz
-  if (w_bf16)
-    hipLaunchKernelGGL(serve_kernel<__hip_bfloat16>, dim3(1), dim3(64), 0, (hipStream_t)stream,
-                       (const __hip_bfloat16*)w, wstride, M, dn, dc, dim, bias, cspan,
-                       (Mailbox*)dmb, ticks);
-  else
-    hipLaunchKernelGGL(serve_kernel<float>, dim3(1), dim3(64), 0, (hipStream_t)stream,
-                       (const float*)w, wstride, M, dn, dc, dim, bias, cspan, (Mailbox*)dmb,
-                       ticks);
+  // grouped gathers for several models; OMLDM_SERVE_GROUPED=0/1 forces a variant (A/B)
+  bool grouped = M > 1;
+  if (const char* e = getenv("OMLDM_SERVE_GROUPED")) grouped = e[0] == '1';
+  hipStream_t st = (hipStream_t)stream;
+#define OMLDM_SERVE(WT, G)                                                                   \
+  hipLaunchKernelGGL((serve_kernel<WT, G>), dim3(1), dim3(64), 0, st, (const WT*)w, wstride, M, \
+                     dn, dc, dim, bias, cspan, (Mailbox*)dmb, ticks)
+  if (w_bf16) {
+    if (grouped) OMLDM_SERVE(__hip_bfloat16, true);
+    else OMLDM_SERVE(__hip_bfloat16, false);
+  } else {
+    if (grouped) OMLDM_SERVE(float, true);
+    else OMLDM_SERVE(float, false);
+  }
+#undef OMLDM_SERVE
   return (int)hipGetLastError();
 }
 
