@@ -114,7 +114,12 @@ class Job:
 
             self._gpu_parser = GpuJsonParser(self.device)
         self._trained_global = 0
-        self._flags = torch.zeros(3, dtype=torch.float32, device=self._coll_device())
+        self._flags = torch.zeros(4, dtype=torch.float32, device=self._coll_device())
+        # multi-rank control plane: rank 0 polls requests at the end of a tick and the
+        # tick's flag all-reduce says whether the next tick must broadcast them — ticks
+        # without requests (nearly all) cost no object broadcast
+        self._ctrl_pending: list = []
+        self._ctrl_due = True
         from omldm_amd.utils.fault import FaultPlan, Watchdog
 
         self.faults = FaultPlan.from_config(cfg, self.rank)
@@ -134,14 +139,23 @@ class Job:
         return self.device if self.comm.backend == "nccl" else torch.device("cpu")
 
     # ------------------------------------------------------------------ control
-    def _control(self):
+    def _poll_requests(self) -> list:
         msgs = []
-        if self.rank == 0:
-            for rec in self.req_in.poll(self.cfg.requestBufferSize):
-                for m in self.pmap.process(rec):
-                    msgs.append((m.network_id, m.destination, m.request.to_obj()))
-        if self.world > 1:
-            msgs = self.comm.broadcast_object(msgs, src=0)
+        for rec in self.req_in.poll(self.cfg.requestBufferSize):
+            for m in self.pmap.process(rec):
+                msgs.append((m.network_id, m.destination, m.request.to_obj()))
+        return msgs
+
+    def _control(self):
+        if self.world == 1:
+            msgs = getattr(self, "_restored_ctrl", []) + self._poll_requests()
+            self._restored_ctrl = []
+        elif self._ctrl_due:
+            msgs = self.comm.broadcast_object(self._ctrl_pending if self.rank == 0 else None,
+                                              src=0)
+            self._ctrl_pending = []
+        else:
+            msgs = []
         queries = []
         for net, dest, robj in msgs:
             req = Request.from_json(robj)
@@ -335,9 +349,15 @@ class Job:
         if self.rank == 0 and self.cfg.test and self.idle.expired(t0) and self.pipes:
             self._flags[1] = 1.0
         self._flags[2] = float(tb.B)
+        self._flags[3] = 0.0
+        if self.world > 1 and self.rank == 0:
+            self._ctrl_pending += self._poll_requests()
+            self._flags[3] = float(len(self._ctrl_pending))
         with tracing.range("flags"):
             self.comm.all_reduce_(self._flags, tag="heartbeat")
-            active, term, n_train = (float(v) for v in self._flags.tolist())
+            active, term, n_train, n_req = (float(v) for v in self._flags.tolist())
+        self._ctrl_due = n_req > 0
+        active += n_req
         self._trained_global += int(n_train)
         if self.pipes and n_train > 0:
             self._train(tb)
@@ -411,6 +431,7 @@ class Job:
         if self.rank == 0:
             sd["pipeline_map"] = self.pmap.state_dict()
             sd["requests"] = self.req_in.state_dict()
+            sd["control_pending"] = list(self._ctrl_pending)  # polled, not yet applied
         return sd
 
     def load_state_dict(self, sd: dict, same_world: bool = True,
@@ -435,3 +456,8 @@ class Job:
         if self.rank == 0 and "pipeline_map" in sd:
             self.pmap.load_state_dict(sd["pipeline_map"])
             self.req_in.load_state_dict(sd.get("requests", {}))
+            pending = [tuple(m) for m in sd.get("control_pending", [])]
+            if self.world == 1:  # single rank: applied at the next tick's _control
+                self._restored_ctrl = pending
+            else:
+                self._ctrl_pending = pending
