@@ -260,7 +260,8 @@ class Job:
                     pipe.train(routed)
         for hubs, items in groups.items():
             with tracing.range("sync:coalesced"):
-                self.comm.all_reduce_coalesced_([b for _, b in items], tag="sync", hubs=hubs)
+                self.comm.all_reduce_coalesced_([b for _, b in items], tag="sync", hubs=hubs,
+                                                bucket_bytes=self.cfg.bucketBytes)
             for pipe, _ in items:
                 pipe.protocol.finish()
 

@@ -50,6 +50,7 @@ class JobConfig:
     requestBufferSize: int = 10000        # SpokeLogic.scala:35
     hubCacheSize: int = 20000             # StateAccumulators.scala:38
     queryBucketSize: int = 10000          # FlinkNetwork.scala:50
+    bucketBytes: int = 64 << 20           # cap of one coalesced collective bucket
     heartbeatEvery: int = 100             # FlinkSpoke.scala:85
     seed: int = 25                        # FlinkSpoke.scala:52
     # ---- MI355X-native engine

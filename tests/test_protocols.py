@@ -133,3 +133,33 @@ def test_sharded_hubs_world4():
     for r in res_h2[1:]:
         assert same(r["final"], res_h2[0]["final"])
     assert same(res_h2[0]["final"], res_all[0]["final"], 1e-5)
+
+
+def _bucket_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm()
+    g = torch.Generator().manual_seed(rank)
+    ts = [torch.randn(n, generator=g) for n in (5, 300, 17, 1000, 3)]
+    ref = [t.clone() for t in ts]
+    for t in ref:
+        dist.all_reduce(t)
+    for cap, hubs in ((64, 0), (1 << 20, 0), (256, 1)):
+        xs = [t.clone() for t in ts]
+        comm.all_reduce_coalesced_(xs, hubs=hubs, bucket_bytes=cap)
+        for x, r in zip(xs, ref):
+            assert torch.allclose(x, r, atol=1e-5), (cap, hubs)
+    torch.save({"ok": True, "collectives": comm.stats.collectives}, os.path.join(out, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_coalesced_buckets_world2():
+    """bucketBytes caps a coalesced collective; small caps split (and slice) buffers,
+    results equal plain per-tensor all-reduces."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_bucket_worker, args=(2, _free_port(), d), nprocs=2,
+                           start_method="fork")
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(2)]
+    assert all(r["ok"] for r in res)
+    assert res[0]["collectives"] > 3  # the 64-byte cap produced many buckets
