@@ -3,7 +3,8 @@
 node) + p50 single-point predict latency, 1/2/4/8 MI355X GPUs (BASELINE.json).
 
 One step == one Synchronous protocol round on every GPU:
-  pinned host micro-batch ──hipMemcpyAsync (copy stream, double-buffered)──► HBM
+  pinned host micro-batch ──pull-copy kernel on a 16-CU slice inside one XCD (copy
+    stream, triple-buffered; training runs on the other CUs)──► HBM
   → linear_round kernel: S virtual spokes (one wavefront each) train PA-I sequentially
     on R rows each, private deltas in LDS hash tables, σ·Δ scattered into the round
     accumulator
@@ -44,15 +45,25 @@ METRIC = "training examples/sec (whole node) + p50 predict latency, linear SVM 1
 class PackedBatch:
     """num | cat | y packed in ONE contiguous byte buffer so a micro-batch is one copy."""
 
-    def __init__(self, space: FeatureSpace, B: int, device, pin: bool, num_dtype):
+    def __init__(self, space: FeatureSpace, B: int, device, pin: bool, num_dtype,
+                 thp: bool = False):
         esz = torch.tensor([], dtype=num_dtype).element_size()
         csz = torch.tensor([], dtype=space.cat_dtype).element_size()
         self.sizes = [B * space.dn * esz, B * space.dc * csz, B * 4]
         offs = [0]
         for s in self.sizes:
             offs.append(offs[-1] + ((s + 255) // 256) * 256)
-        self.flat = torch.empty(offs[-1], dtype=torch.uint8, device=device,
-                                pin_memory=pin and device == "cpu")
+        if thp and device == "cpu" and pin:
+            # pinned pages backed by transparent huge pages (2 MiB GPU translations)
+            import ctypes
+
+            p = native.hip().omldm_host_alloc_thp(offs[-1])
+            assert p, "omldm_host_alloc_thp failed"
+            self.flat = torch.frombuffer((ctypes.c_uint8 * offs[-1]).from_address(p),
+                                         dtype=torch.uint8)
+        else:
+            self.flat = torch.empty(offs[-1], dtype=torch.uint8, device=device,
+                                    pin_memory=pin and device == "cpu")
         f = self.flat
         self.batch = HashedBatch(
             f[offs[0]:offs[0] + self.sizes[0]].view(num_dtype).view(B, space.dn),
@@ -75,6 +86,8 @@ def main(argv=None) -> int:
     ap.add_argument("--wire", default="compact", choices=["wide", "compact"],
                     help="compact: field-aware uint16 categorical slots (half the PCIe bytes)")
     ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")
+    ap.add_argument("--pool-alloc", default="torch", choices=["torch", "thp"],
+                    help="thp: pinned pool on transparent huge pages (2 MiB GPU translations)")
     ap.add_argument("--latency-mode", default="persistent",
                     choices=["copy", "zerocopy", "persistent"],
                     help="zerocopy: the predict kernel reads the point from and writes the "
@@ -92,13 +105,23 @@ def main(argv=None) -> int:
     ap.add_argument("--slots", type=int, default=3, help="HBM staging buffers (2 = double)")
     ap.add_argument("--copy-priority", type=int, default=0,
                     help="1: ingest stream at high priority (its blocks dispatch first)")
-    ap.add_argument("--pull-blocks", type=int, default=8)
+    ap.add_argument("--pull-blocks", type=int, default=16)
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture each pipelined step (copy ‖ round) as a hipGraph (1 GPU)")
     ap.add_argument("--pull-unroll", type=int, default=4, choices=[4, 8, 16],
                     help="16-B loads in flight per lane in the pull kernel")
-    ap.add_argument("--ingest-cus", type=int, default=0,
+    ap.add_argument("--ingest-cus", type=int, default=16,
                     help=">0: run the ingest stream on a CU-masked slice of this many CUs")
+    ap.add_argument("--cu-layout", type=int, default=1,
+                    help="ingest CU slice: 0 every (256/N)-th CU, 1 the block [0, N) (inside "
+                         "one XCD: its PCIe reads then only occupy that XCD's L2)")
+    ap.add_argument("--lane", default="auto", choices=["auto", "split", "plain"],
+                    help="ingest lane (see the lanes block); auto: time both, keep the faster")
+    ap.add_argument("--tune-steps", type=int, default=16,
+                    help="steps per lane and pass of the untimed lane selection")
+    ap.add_argument("--split-cus", type=int, default=1,
+                    help="1 (with --ingest-cus N): training runs on the complementary CUs, "
+                         "so ingest and training never share a CU")
     a = ap.parse_args(argv)
 
     comm, device = init_distributed()
@@ -112,7 +135,7 @@ def main(argv=None) -> int:
     # ---- synthetic stream shard of this rank, pinned, packed
     pool = []
     for k in range(a.pool):
-        pb = PackedBatch(space, B, "cpu", on_gpu, num_dtype)
+        pb = PackedBatch(space, B, "cpu", on_gpu, num_dtype, thp=a.pool_alloc == "thp")
         tmp = synth_batch(space, B, start=(k * world + rank) * B, seed=25)
         pb.batch.num.copy_(tmp.num)
         pb.batch.cat.copy_(tmp.cat)
@@ -130,12 +153,33 @@ def main(argv=None) -> int:
     proto = Synchronous(comm, learner, {"virtualSpokes": S,
                                         **({"HubParallelism": a.hubs} if a.hubs else {})})
 
-    copy_stream = torch.cuda.Stream(device, priority=-1 if a.copy_priority else 0) \
-        if on_gpu else None
-    if on_gpu and a.ingest_cus > 0:
-        raw = native.hip().omldm_stream_create_cumask(a.ingest_cus)
-        assert raw, "hipExtStreamCreateWithCUMask failed"
-        copy_stream = torch.cuda.ExternalStream(raw, device=device)
+    # ---- ingest lanes: which stream (and CUs) the H2D pull copy and the training use.
+    # "split": the copy runs on a block of --ingest-cus CUs inside one XCD and training on
+    #          the complementary CUs, so the copy's long-latency PCIe reads only occupy
+    #          one XCD's L2 (profiles/round1_ablation.md: 0.2405 -> 0.2005 ms/step);
+    # "plain": ordinary streams, copy with 8 blocks anywhere on the chip.
+    # --lane auto times both on this node before the warmup and keeps the faster (ranks
+    # agree on the slowest rank's times), so a runtime where CU-masked queues behave
+    # worse next to the collectives falls back to the plain lane.
+    lanes = {}
+    raw_streams = []  # natively created (CU-masked) streams, destroyed before exit
+    if on_gpu:
+        lanes["plain"] = {"copy": torch.cuda.Stream(device, priority=-1 if a.copy_priority else 0),
+                          "compute": torch.cuda.current_stream(device), "blocks": 8}
+        if a.ingest_cus > 0:
+            raw = native.hip().omldm_stream_create_cumask_ex(a.ingest_cus, 0, a.cu_layout)
+            assert raw, "hipExtStreamCreateWithCUMask failed"
+            raw_streams.append(raw)
+            comp = torch.cuda.current_stream(device)
+            if a.split_cus:
+                rawc = native.hip().omldm_stream_create_cumask_ex(a.ingest_cus, 1, a.cu_layout)
+                assert rawc, "hipExtStreamCreateWithCUMask (complement) failed"
+                raw_streams.append(rawc)
+                comp = torch.cuda.ExternalStream(rawc, device=device)
+            lanes["split"] = {"copy": torch.cuda.ExternalStream(raw, device=device),
+                              "compute": comp, "blocks": a.pull_blocks}
+    lane_name = ("split" if "split" in lanes else "plain") if a.lane == "auto" else a.lane
+    lane = lanes.get(lane_name, {"copy": None, "compute": None, "blocks": a.pull_blocks})
     copied = [torch.cuda.Event() for _ in range(a.slots)] if on_gpu else None
     consumed = [torch.cuda.Event() for _ in range(a.slots)] if on_gpu else None
     engine = None
@@ -158,16 +202,16 @@ def main(argv=None) -> int:
     def h2d(dst: torch.Tensor, src: torch.Tensor, k: int = 0):
         if a.h2d == "pull-hbm":
             native.check(native.hip().omldm_pull_copy(dsrc[k % a.pool].data_ptr(), dst.data_ptr(),
-                                                      src.numel(), a.pull_blocks,
-                                                      copy_stream.cuda_stream), "pull_copy")
+                                                      src.numel(), lane["blocks"],
+                                                      lane["copy"].cuda_stream), "pull_copy")
         elif a.h2d == "pull":  # GPU pulls the pinned batch over PCIe (csrc/kernels/ingest.hip)
-            blk = a.pull_blocks | ((a.pull_unroll if a.pull_unroll != 4 else 0) << 16)
+            blk = lane["blocks"] | ((a.pull_unroll if a.pull_unroll != 4 else 0) << 16)
             native.check(native.hip().omldm_pull_copy(src.data_ptr(), dst.data_ptr(),
                                                       src.numel(), blk,
-                                                      copy_stream.cuda_stream), "pull_copy")
+                                                      lane["copy"].cuda_stream), "pull_copy")
         elif a.h2d == "raw":  # hipMemcpyAsync issued directly
             native.check(native.hip().omldm_h2d_async(dst.data_ptr(), src.data_ptr(),
-                                                      src.numel(), copy_stream.cuda_stream),
+                                                      src.numel(), lane["copy"].cuda_stream),
                          "h2d_async")
         else:  # SDMA engine (hipMemcpyAsync)
             dst.copy_(src, non_blocking=True)
@@ -181,15 +225,23 @@ def main(argv=None) -> int:
         if engine is not None:
             tickets[slot] = engine.submit(dev[slot].flat, src.flat, ev_free[slot], ev_done[slot])
         elif on_gpu:
-            with torch.cuda.stream(copy_stream):
-                copy_stream.wait_event(consumed[slot])
+            cs = lane["copy"]
+            with torch.cuda.stream(cs):
+                cs.wait_event(consumed[slot])
                 h2d(dev[slot].flat, src.flat, k)
-                copied[slot].record(copy_stream)
+                copied[slot].record(cs)
         else:
             dev[slot].flat.copy_(src.flat)
         host_t["prefetch"] += time.perf_counter() - t
 
     def step(k: int):
+        if on_gpu:
+            with torch.cuda.stream(lane["compute"]):
+                _step(k)
+        else:
+            _step(k)
+
+    def _step(k: int):
         if a.ingest == "device":
             proto.round(dev[k % a.pool].batch)
             return
@@ -234,10 +286,10 @@ def main(argv=None) -> int:
         def graph_step(k: int):
             nxt = (k + 1) % a.slots
             fork.record()
-            copy_stream.wait_event(fork)
-            with torch.cuda.stream(copy_stream):
+            lane["copy"].wait_event(fork)
+            with torch.cuda.stream(lane["copy"]):
                 h2d(dev[nxt].flat, pool[(k + 1) % a.pool].flat, k + 1)
-            join.record(copy_stream)
+            join.record(lane["copy"])
             proto.round(dev[k % a.slots].batch)
             torch.cuda.current_stream().wait_event(join)
 
@@ -269,12 +321,38 @@ def main(argv=None) -> int:
             for e in consumed:
                 e.record()
         prefetch(0)
-    for k in range(a.warmup):
+    k0 = 0
+    if a.lane == "auto" and len(lanes) > 1 and not use_graph and a.ingest == "pinned" \
+            and engine is None and a.tune_steps > 0:
+        # lane selection (untimed setup): two passes over both lanes, best pass per lane,
+        # max over ranks, then the faster lane for warmup + timed steps
+        best = {n: float("inf") for n in lanes}
+        for _ in range(2):
+            for n in lanes:
+                lane = lanes[n]
+                sync()
+                t = time.perf_counter()
+                for k in range(k0, k0 + a.tune_steps):
+                    step(k)
+                sync()
+                best[n] = min(best[n], time.perf_counter() - t)
+                k0 += a.tune_steps
+        names = sorted(lanes)
+        tt = torch.tensor([best[n] for n in names], dtype=torch.float64,
+                          device=device if comm.backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        lane_name = names[int(torch.argmin(tt).item())]
+        lane = lanes[lane_name]
+        lane_ms = {n: round(float(v) / a.tune_steps * 1e3, 4) for n, v in zip(names, tt.tolist())}
+    else:
+        lane_ms = None
+    for k in range(k0, k0 + a.warmup):
         step(k)
     sync()
     host_t["prefetch"] = host_t["round"] = 0.0
     t0 = time.perf_counter()
-    for k in range(a.warmup, a.warmup + a.steps):
+    for k in range(k0 + a.warmup, k0 + a.warmup + a.steps):
         step(k)
     sync()
     elapsed = time.perf_counter() - t0
@@ -365,10 +443,15 @@ def main(argv=None) -> int:
             "per_gpu_examples_per_s": round(value / world, 1),
             "holdout_accuracy": round(acc, 4), "fitted_examples_rank0": fitted,
             "host_us_per_step": {k: round(v / a.steps * 1e6, 1) for k, v in host_t.items()},
-            "lds_table_overflow": overflow, "numa": comm.placement, "device": torch.cuda.get_device_name(device)
+            "lds_table_overflow": overflow, "numa": comm.placement,
+            "ingest_lane": lane_name if on_gpu else None, "lane_tune_ms_per_step": lane_ms, "device": torch.cuda.get_device_name(device)
             if on_gpu else "cpu",
         }
         print(json.dumps(out), flush=True)
+    if on_gpu:
+        torch.cuda.synchronize(device)
+        for rs in raw_streams:
+            native.hip().omldm_stream_destroy(rs)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

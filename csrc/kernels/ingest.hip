@@ -8,6 +8,10 @@
 // unpack the compact wire format into the kernel layout (no second HBM pass).
 #include "common.h"
 
+#include <cstdlib>
+#include <cstring>
+#include <sys/mman.h>
+
 namespace omldm {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -63,7 +67,8 @@ using namespace omldm;
 // A stream whose kernels may only run on `ncu` CUs spread over all XCDs (every
 // (256/ncu)-th CU), so the ingest pull kernel never competes with the training kernels
 // for more than that slice of the chip. Returns the hipStream_t (0 on failure).
-OMLDM_API void* omldm_stream_create_cumask(int ncu) {
+// layout 0: every (total/ncu)-th CU; layout 1: CUs [0, ncu) (a contiguous block).
+OMLDM_API void* omldm_stream_create_cumask_ex(int ncu, int invert, int layout) {
   hipDeviceProp_t prop;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
@@ -72,12 +77,22 @@ OMLDM_API void* omldm_stream_create_cumask(int ncu) {
   if (ncu <= 0 || ncu >= total) ncu = total;
   uint32_t mask[16] = {0};
   const int step = total / ncu;
-  for (int i = 0, c = total - 1; i < ncu && c >= 0; ++i, c -= step) mask[c >> 5] |= 1u << (c & 31);
+  if (layout == 1) {
+    for (int c = 0; c < ncu; ++c) mask[c >> 5] |= 1u << (c & 31);
+  } else {
+    for (int i = 0, c = total - 1; i < ncu && c >= 0; ++i, c -= step) mask[c >> 5] |= 1u << (c & 31);
+  }
+  const int words = (total + 31) / 32;
+  if (invert) {  // the complement: every CU the slice above does not own
+    for (int w = 0; w < words; ++w) mask[w] = ~mask[w];
+    if (total & 31) mask[words - 1] &= (1u << (total & 31)) - 1u;
+  }
   hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)((total + 31) / 32), mask) != hipSuccess)
-    return nullptr;
+  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess) return nullptr;
   return (void*)s;
 }
+
+OMLDM_API void* omldm_stream_create_cumask(int ncu) { return omldm_stream_create_cumask_ex(ncu, 0, 0); }
 
 OMLDM_API int omldm_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }
 
@@ -92,6 +107,31 @@ OMLDM_API void* omldm_host_device_ptr(void* host) {
   void* dev = nullptr;
   if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess) return nullptr;
   return dev;
+}
+
+// Pinned host buffer backed by transparent huge pages: 2 MiB-aligned anonymous memory
+// with MADV_HUGEPAGE, faulted in, then registered (pinned + device-mapped). The GPU then
+// reaches it through 2 MiB translations instead of 4 KiB ones, which matters for a copy
+// kernel streaming host memory next to training kernels that share the GPU's address
+// translation caches. Returns nullptr on failure; free with omldm_host_free_thp.
+OMLDM_API void* omldm_host_alloc_thp(long long nbytes) {
+  const size_t huge = size_t(2) << 20;
+  const size_t n = ((size_t)nbytes + huge - 1) / huge * huge;
+  void* p = nullptr;
+  if (posix_memalign(&p, huge, n) != 0) return nullptr;
+  madvise(p, n, MADV_HUGEPAGE);
+  memset(p, 0, n);
+  if (hipHostRegister(p, n, hipHostRegisterMapped) != hipSuccess) {
+    free(p);
+    return nullptr;
+  }
+  return p;
+}
+
+OMLDM_API void omldm_host_free_thp(void* p) {
+  if (!p) return;
+  hipHostUnregister(p);
+  free(p);
 }
 
 // Registers an existing host allocation as pinned+mapped (for buffers not allocated pinned).

@@ -80,9 +80,12 @@ HIP_SIGS = [
     ("omldm_event_destroy", i32, [vp]),
     ("omldm_event_record", i32, [vp, vp]),
     ("omldm_stream_create_cumask", vp, [i32]),
+    ("omldm_stream_create_cumask_ex", vp, [i32, i32, i32]),
     ("omldm_host_device_ptr", vp, [vp]),
     ("omldm_stream_destroy", i32, [vp]),
     ("omldm_host_register", i32, [vp, i64]),
+    ("omldm_host_alloc_thp", vp, [i64]),
+    ("omldm_host_free_thp", None, [vp]),
 ]
 
 HOST_SIGS = [
