@@ -162,7 +162,7 @@ def main(argv=None) -> int:
     # agree on the slowest rank's times), so a runtime where CU-masked queues behave
     # worse next to the collectives falls back to the plain lane.
     lanes = {}
-    raw_streams = []  # natively created (CU-masked) streams, destroyed before exit
+    raw_streams = []  # natively created (CU-masked) streams, destroyed at the end
     if on_gpu:
         lanes["plain"] = {"copy": torch.cuda.Stream(device, priority=-1 if a.copy_priority else 0),
                           "compute": torch.cuda.current_stream(device), "blocks": 8}
@@ -449,7 +449,16 @@ def main(argv=None) -> int:
         }
         print(json.dumps(out), flush=True)
     if on_gpu:
+        # teardown order: events recorded on the CU-masked streams first, then the
+        # streams (leaving them to the runtime's exit-time teardown crashed under
+        # rocprofv3 in __cxa_finalize)
         torch.cuda.synchronize(device)
+        for evs in (copied, consumed):
+            if evs:
+                evs.clear()
+        import gc
+
+        gc.collect()
         for rs in raw_streams:
             native.hip().omldm_stream_destroy(rs)
     if world > 1:

@@ -74,7 +74,7 @@ class TickBlock:
 class TickIngest:
     def __init__(self, consumers: list, batch_size: int, pinned: bool, prefetch: bool = True,
                  depth: int = 2, bytes_per_record: int = 1024, device=None,
-                 copy_blocks: int = 128, space=None):
+                 copy_blocks: int = 128, space=None, copy_stream=None, parse_stream=None):
         self.consumers = consumers
         self.space = space  # set: the ingest thread also parses each block on the GPU
         # GPU ranks: the ingest thread also moves each block to HBM on its own copy
@@ -82,7 +82,8 @@ class TickIngest:
         self.device = torch.device(device) if device is not None else None
         self.stage = self.device is not None and self.device.type == "cuda" and pinned
         self.copy_blocks = copy_blocks
-        self._copy_stream = torch.cuda.Stream(self.device) if self.stage else None
+        self._copy_stream = (copy_stream or torch.cuda.Stream(self.device)) if self.stage else None
+        self._parse_stream = parse_stream  # None: the parse follows the copy on its stream
         self.batch = max(1, int(batch_size))
         self.pinned = bool(pinned)
         self.slots: list[TickBlock] = []
@@ -185,7 +186,14 @@ class TickIngest:
             pull_copy(blk.d_offs, blk.offs_t[:n + 1], self.copy_blocks, cs.cuda_stream)
             blk.parsed = None
             if self.space is not None:
-                self._parse(blk, cs)
+                ps = cs
+                if self._parse_stream is not None:
+                    copied = torch.cuda.Event()
+                    copied.record(cs)
+                    ps = self._parse_stream
+                    ps.wait_event(copied)
+                self._parse(blk, ps)
+                cs = ps
             ev = torch.cuda.Event()
             ev.record(cs)
             blk.staged = ev

@@ -86,13 +86,22 @@ class Job:
         self.pmap = PipelineMap() if self.rank == 0 else None
         # this rank's training ∪ forecasting records, one pinned block per tick, read one
         # tick ahead on a background thread (engine/ingest.py)
+        # GPU ranks: the ingest copies run on one XCD's CUs, everything else on the rest
+        self.lanes = None
+        if self.device.type == "cuda" and cfg.gpuParse and cfg.ingestCUs > 0:
+            from omldm_amd.ops.ingest import XcdLanes
+
+            self.lanes = XcdLanes.get(self.device, cfg.ingestCUs)
         self.ingest = TickIngest([self.train_in, self.fcst_in], cfg.batchSize,
                                  pinned=self.device.type == "cuda",
                                  prefetch=str(cfg.prefetch).lower() in ("true", "1") or (
                                      str(cfg.prefetch).lower() == "auto" and
                                      self.device.type == "cuda"),
                                  device=self.device if cfg.gpuParse else None,
-                                 space=self.space if cfg.gpuParse else None)
+                                 space=self.space if cfg.gpuParse else None,
+                                 copy_blocks=16 if self.lanes else 128,
+                                 copy_stream=self.lanes.copy if self.lanes else None,
+                                 parse_stream=self.lanes.aux if self.lanes else None)
         self._committed = None  # consumer offsets after the last processed block
         # predictions leave through a producer thread (formatted natively, io/egress.py)
         self.egress = EgressWriter(b["predictions"], enabled=self.device.type == "cuda")
@@ -292,6 +301,13 @@ class Job:
 
     # --------------------------------------------------------------------- tick
     def tick(self) -> None:
+        if self.lanes is not None:
+            with torch.cuda.stream(self.lanes.compute):
+                self._tick()
+        else:
+            self._tick()
+
+    def _tick(self) -> None:
         t0 = time.time()
         if self.faults:
             self.faults.on_tick(self.ticks)

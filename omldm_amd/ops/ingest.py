@@ -52,6 +52,46 @@ class CopyEngine:
             pass
 
 
+class XcdLanes:
+    """CU-masked streams: ``copy`` on a contiguous block of ``ingest_cus`` CUs (inside
+    one XCD) for host→HBM pull copies; ``compute`` and ``aux`` on every other CU. A pull
+    copy spread over the chip lets its long-latency PCIe reads occupy every XCD's L2 and
+    slows training; confined to one XCD it runs at the PCIe peak next to training
+    (profiles/round1_ablation.md, "XCD-local ingest"). The streams are blocking
+    (hipExtStreamCreateWithCUMask): nothing may run on the legacy default stream
+    meanwhile, so the user switches all its GPU work to ``compute``.
+
+    One set per (device, ingest_cus) for the whole process (``XcdLanes.get``): events and
+    pinned-memory bookkeeping recorded on a stream must never outlive it, so the streams
+    are never destroyed while the process runs."""
+
+    _cache: dict = {}
+
+    def __init__(self, device, ingest_cus: int = 16):
+        lib = native.hip()
+        self.device = torch.device(device)
+        with torch.cuda.device(self.device):
+            raw = [lib.omldm_stream_create_cumask_ex(int(ingest_cus), 0, 1),
+                   lib.omldm_stream_create_cumask_ex(int(ingest_cus), 1, 1),
+                   lib.omldm_stream_create_cumask_ex(int(ingest_cus), 1, 1)]
+        if not all(raw):
+            raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+        self.copy = torch.cuda.ExternalStream(raw[0], device=self.device)
+        self.compute = torch.cuda.ExternalStream(raw[1], device=self.device)
+        # a second stream on the compute CUs for work the ingest thread issues after a
+        # copy (the JSON parse), so it neither queues behind training nor runs on the
+        # ingest CUs
+        self.aux = torch.cuda.ExternalStream(raw[2], device=self.device)
+
+    @classmethod
+    def get(cls, device, ingest_cus: int = 16) -> "XcdLanes":
+        dev = torch.device(device)
+        key = (dev.index if dev.index is not None else torch.cuda.current_device(), ingest_cus)
+        if key not in cls._cache:
+            cls._cache[key] = cls(dev, ingest_cus)
+        return cls._cache[key]
+
+
 def pull_copy(dst: torch.Tensor, src: torch.Tensor, blocks: int = 16, stream=None) -> None:
     s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
     native.check(native.hip().omldm_pull_copy(src.data_ptr(), dst.data_ptr(),

@@ -68,6 +68,7 @@ class JobConfig:
     parseThreads: int = 8
     gpuParse: bool = True                 # parse + hash JSON records on the GPU (cuda only)
     prefetch: str = "auto"                # read tick k+1 while tick k trains (auto: on GPU)
+    ingestCUs: int = 0                    # GPU: CUs (one XCD block) for ingest copies; 0 off (e2e A/B: no gain, host-bound)
     extra: dict = field(default_factory=dict)
 
     @staticmethod
