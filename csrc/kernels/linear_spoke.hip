@@ -427,7 +427,7 @@ __device__ __forceinline__ void finish_column(int c, const float* __restrict__ w
 // keys never map to dense / intercept slots, so the two block kinds touch disjoint slots.
 __global__ __launch_bounds__(256) void linear_reduce_kernel(
     const int2* __restrict__ tables, int S_act, TableGeom g, int dim, float* __restrict__ dacc,
-    int nb, const float* __restrict__ ws, int S, int dn, float* __restrict__ cum) {
+    int nb, int split, const float* __restrict__ ws, int S, int dn, float* __restrict__ cum) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if ((int)blockIdx.x >= nb) {
     finish_column(blockIdx.x - nb, ws, S, dn, dim, dacc, cum);
@@ -435,15 +435,20 @@ __global__ __launch_bounds__(256) void linear_reduce_kernel(
   }
   float* acc = reinterpret_cast<float*>(smem);
   const int span = 1 << (g.kshift + g.lgg);  // keys of the 2^lgg buckets of this group
-  const int q = blockIdx.x;
+  const int q = blockIdx.x / split;            // key group
+  const int part = blockIdx.x - q * split;     // this block's share of the spokes
+  const int s_lo = (int)(((long long)S_act * part) / split);
+  const int s_hi = (int)(((long long)S_act * (part + 1)) / split);
   for (int i = threadIdx.x; i < span; i += 256) acc[i] = 0.f;
   __syncthreads();
   const int seg_log2 = (g.log2cap - g.log2nb) + g.lgg;
   const int lo = q << (g.kshift + g.lgg);
-  // the group's region is contiguous: S_act segments of 2^seg int2 → 16-byte loads (two
-  // slots), four in flight per thread
-  const long long items = (long long)S_act << (seg_log2 - 1);
-  const int4* t4 = reinterpret_cast<const int4*>(tables) + (((size_t)q * S) << (seg_log2 - 1));
+  // the group's region is contiguous ([group][spoke][segment]), so is every part of it:
+  // (s_hi − s_lo) segments of 2^seg int2 → 16-byte loads (two slots), four in flight per
+  // thread
+  const long long items = (long long)(s_hi - s_lo) << (seg_log2 - 1);
+  const int4* t4 = reinterpret_cast<const int4*>(tables) +
+                   (((size_t)q * S + s_lo) << (seg_log2 - 1));
   auto addr = [](long long ii) { return (size_t)ii; };
   long long it = threadIdx.x;
   for (; it + 3 * 256 < items; it += 4 * 256) {
@@ -462,16 +467,37 @@ __global__ __launch_bounds__(256) void linear_reduce_kernel(
     if (v.z >= 0) atomicAdd(&acc[v.z - lo], __int_as_float(v.w));
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < span; i += 256) {
-    const int k = lo + i;
-    const float v = acc[i];
-    if (k < dim && v != 0.f) dacc[k] += v;
+  if (split == 1) {  // sole owner of the key range
+    for (int i = threadIdx.x; i < span; i += 256) {
+      const int k = lo + i;
+      const float v = acc[i];
+      if (k < dim && v != 0.f) dacc[k] += v;
+    }
+  } else {  // the group's parts meet in L2 (hardware fp32 atomics, no return value)
+    for (int i = threadIdx.x; i < span; i += 256) {
+      const int k = lo + i;
+      const float v = acc[i];
+      if (k < dim && v != 0.f) unsafeAtomicAdd(&dacc[k], v);
+    }
   }
 }
 
 // Buckets per reduce group (2^lgg). Measured at 8192 spokes × 1K tables, dim 2^20:
 // lgg 0 → 0.135 ms/step (256 reduce blocks, each streaming its 256 KiB region), lgg 1 →
 // 0.149, lgg 2 → 0.195 (64 blocks: too few to pull HBM bandwidth), so one bucket per group.
+// Reduce blocks per key group. One block per group gives 256 blocks at dim 2^20: one per
+// CU, four waves each, too few loads in flight to stream the 64 MiB of tables at HBM rate.
+// Splitting the spokes of a group over several blocks (partial LDS images, combined with
+// L2 atomics) raises the memory-level parallelism; see profiles/round1_ablation.md.
+static inline int reduce_split(int ngroups, int S_act) {
+  int sp = ngroups >= 1024 ? 1 : 4;
+  if (const char* e = getenv("OMLDM_REDUCE_SPLIT")) sp = atoi(e);  // diagnostics sweep
+  if (sp < 1) sp = 1;
+  if (sp > 16) sp = 16;
+  while (sp > 1 && sp > S_act) sp >>= 1;
+  return sp;
+}
+
 static inline int reduce_lgg(int kshift, int log2nb) {
   (void)kshift;
   int lgg = 0;
@@ -558,12 +584,14 @@ static int launch_round(const void* w, const void* num, int dn, const void* cat,
   const long long sact_ll = R > 0 ? ((long long)B + R - 1) / R : 0;
   const int S_act = sact_ll < S ? (int)sact_ll : S;
   const int gspan_log2 = g.kshift + g.lgg;
-  const int nb = (!(ablate & 1) && S_act > 0) ? (dim + (1 << gspan_log2) - 1) >> gspan_log2 : 0;
+  const int ng = (!(ablate & 1) && S_act > 0) ? (dim + (1 << gspan_log2) - 1) >> gspan_log2 : 0;
+  const int split = ng ? reduce_split(ng, S_act) : 1;
+  const int nb = ng * split;
   const size_t rlds = nb ? (size_t(1) << gspan_log2) * 4 : 0;
   e = check_dyn_lds((const void*)linear_reduce_kernel, rlds);
   if (e) return e;
   hipLaunchKernelGGL(linear_reduce_kernel, dim3(nb + kWsStat + dn + 1), dim3(256), rlds, st,
-                     tables, S_act, g, dim, dacc, nb, ws, S, dn, cum);
+                     tables, S_act, g, dim, dacc, nb, split, ws, S, dn, cum);
   return (int)hipGetLastError();
 }
 
