@@ -119,6 +119,10 @@ def main(argv=None) -> int:
                     help="ingest lane (see the lanes block); auto: time both, keep the faster")
     ap.add_argument("--tune-steps", type=int, default=16,
                     help="steps per lane and pass of the untimed lane selection")
+    ap.add_argument("--reduce-parts", default="auto", choices=["auto", "1", "2", "4", "8"],
+                    help="N > 1: all-reduce the round accumulator in this many key-range "
+                         "slices, each started as soon as its reduce launch is enqueued "
+                         "(auto: timed with the lanes before the warmup)")
     ap.add_argument("--split-cus", type=int, default=1,
                     help="1 (with --ingest-cus N): training runs on the complementary CUs, "
                          "so ingest and training never share a CU")
@@ -322,31 +326,43 @@ def main(argv=None) -> int:
                 e.record()
         prefetch(0)
     k0 = 0
-    if a.lane == "auto" and len(lanes) > 1 and not use_graph and a.ingest == "pinned" \
-            and engine is None and a.tune_steps > 0:
-        # lane selection (untimed setup): two passes over both lanes, best pass per lane,
-        # max over ranks, then the faster lane for warmup + timed steps
-        best = {n: float("inf") for n in lanes}
+    # (lane, reduce parts) candidates. Reduce parts only matter with a collective (N > 1):
+    # the accumulator's all-reduce is split into key-range slices started as soon as each
+    # slice's reduce launch is enqueued (protocols.Synchronous.reduce_parts) — the same
+    # sums, so the choice is purely a timing one, made on this node.
+    lane_cands = sorted(lanes) if (a.lane == "auto" and len(lanes) > 1) else [lane_name]
+    if a.reduce_parts != "auto":
+        part_cands = [int(a.reduce_parts)]
+    else:
+        part_cands = [1, 2, 4] if world > 1 else [1]
+    proto.reduce_parts = part_cands[0]
+    cands = [(n, pp) for n in lane_cands for pp in part_cands]
+    if len(cands) > 1 and not use_graph and a.ingest == "pinned" and engine is None \
+            and a.tune_steps > 0:
+        # selection (untimed setup): two passes over every candidate, best pass each, max
+        # over ranks, then the fastest for warmup + timed steps
+        best = {c: float("inf") for c in cands}
         for _ in range(2):
-            for n in lanes:
-                lane = lanes[n]
+            for c in cands:
+                lane, proto.reduce_parts = lanes.get(c[0], lane), c[1]
                 sync()
                 t = time.perf_counter()
                 for k in range(k0, k0 + a.tune_steps):
                     step(k)
                 sync()
-                best[n] = min(best[n], time.perf_counter() - t)
+                best[c] = min(best[c], time.perf_counter() - t)
                 k0 += a.tune_steps
-        names = sorted(lanes)
-        tt = torch.tensor([best[n] for n in names], dtype=torch.float64,
+        tt = torch.tensor([best[c] for c in cands], dtype=torch.float64,
                           device=device if comm.backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        lane_name = names[int(torch.argmin(tt).item())]
-        lane = lanes[lane_name]
-        lane_ms = {n: round(float(v) / a.tune_steps * 1e3, 4) for n, v in zip(names, tt.tolist())}
+        lane_name, proto.reduce_parts = cands[int(torch.argmin(tt).item())]
+        lane_ms = {(n if len(part_cands) == 1 else f"{n}/parts{pp}"):
+                   round(float(v) / a.tune_steps * 1e3, 4) for (n, pp), v in zip(cands, tt.tolist())}
     else:
         lane_ms = None
+    if on_gpu:
+        lane = lanes.get(lane_name, lane)
     for k in range(k0, k0 + a.warmup):
         step(k)
     sync()
@@ -444,8 +460,9 @@ def main(argv=None) -> int:
             "holdout_accuracy": round(acc, 4), "fitted_examples_rank0": fitted,
             "host_us_per_step": {k: round(v / a.steps * 1e6, 1) for k, v in host_t.items()},
             "lds_table_overflow": overflow, "numa": comm.placement,
-            "ingest_lane": lane_name if on_gpu else None, "lane_tune_ms_per_step": lane_ms, "device": torch.cuda.get_device_name(device)
-            if on_gpu else "cpu",
+            "ingest_lane": lane_name if on_gpu else None, "lane_tune_ms_per_step": lane_ms,
+            "reduce_parts": proto.reduce_parts,
+            "device": torch.cuda.get_device_name(device) if on_gpu else "cpu",
         }
         print(json.dumps(out), flush=True)
     if on_gpu:

@@ -419,7 +419,8 @@ __device__ __forceinline__ void finish_column(int c, const float* __restrict__ w
   }
 }
 
-// One launch after the round kernel. Blocks [0, nb): bucket b owns keys
+// One launch after the round kernel (or `parts` launches, see launch_reduce). Blocks
+// [0, nb): `split` blocks per key group, group q0 + b / split; bucket b owns keys
 // [b·2^kshift, (b+1)·2^kshift); it streams bucket b of every active spoke's table (BS
 // consecutive int2 per spoke), accumulates into an LDS image with ds_add_f32 and adds its
 // non-zero slots to the accumulator (which the apply pass left at zero; overflow entries
@@ -427,7 +428,8 @@ __device__ __forceinline__ void finish_column(int c, const float* __restrict__ w
 // keys never map to dense / intercept slots, so the two block kinds touch disjoint slots.
 __global__ __launch_bounds__(256) void linear_reduce_kernel(
     const int2* __restrict__ tables, int S_act, TableGeom g, int dim, float* __restrict__ dacc,
-    int nb, int split, const float* __restrict__ ws, int S, int dn, float* __restrict__ cum) {
+    int nb, int split, int q0, const float* __restrict__ ws, int S, int dn,
+    float* __restrict__ cum) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if ((int)blockIdx.x >= nb) {
     finish_column(blockIdx.x - nb, ws, S, dn, dim, dacc, cum);
@@ -435,8 +437,8 @@ __global__ __launch_bounds__(256) void linear_reduce_kernel(
   }
   float* acc = reinterpret_cast<float*>(smem);
   const int span = 1 << (g.kshift + g.lgg);  // keys of the 2^lgg buckets of this group
-  const int q = blockIdx.x / split;            // key group
-  const int part = blockIdx.x - q * split;     // this block's share of the spokes
+  const int q = q0 + (int)blockIdx.x / split;  // key group
+  const int part = (int)blockIdx.x % split;    // this block's share of the spokes
   const int s_lo = (int)(((long long)S_act * part) / split);
   const int s_hi = (int)(((long long)S_act * (part + 1)) / split);
   for (int i = threadIdx.x; i < span; i += 256) acc[i] = 0.f;
@@ -570,39 +572,70 @@ __global__ __launch_bounds__(256) void linear_apply_kernel(float* __restrict__ w
   }
 }
 
+// Key range [lo, hi) of the accumulator that reduce part `part` of `parts` completes:
+// part k owns key groups [ng·k/parts, ng·(k+1)/parts). Part 0 also runs the workspace
+// column sums, so it completes dacc[0:dn], and the last part extends to dim + 2 (the
+// intercept slot dim − 1 and the round counters dacc[dim:dim+2], written by part 0's
+// finish blocks earlier in stream order). Independent of the table size: every rank
+// derives the same slices from dim alone.
+static void part_bounds(int dim, TableGeom g, int part, int parts, long long* lo, long long* hi) {
+  const int gspan_log2 = g.kshift + g.lgg;
+  const long long ng = ((long long)dim + (1LL << gspan_log2) - 1) >> gspan_log2;
+  const long long q0 = ng * part / parts, q1 = ng * (part + 1) / parts;
+  *lo = part == 0 ? 0 : q0 << gspan_log2;
+  *hi = part == parts - 1 ? (long long)dim + 2 : q1 << gspan_log2;
+  if (*hi > (long long)dim + 2) *hi = (long long)dim + 2;
+}
+
+// Reduce part `part` of `parts` (parts == 1: the whole reduce in one launch). With
+// parts > 1 the caller issues the collective of each part's key range right after that
+// part's launch, so the all-reduce of part k runs on the RCCL stream while part k+1
+// reduces (protocols.Synchronous, reduce_parts).
+static int launch_reduce(const int2* tables, int B, int R, int S, TableGeom g, int dim,
+                         float* dacc, const float* ws, int dn, float* cum, int part, int parts,
+                         int ablate, hipStream_t st) {
+  const long long sact_ll = R > 0 ? ((long long)B + R - 1) / R : 0;
+  const int S_act = sact_ll < S ? (int)sact_ll : S;
+  const int gspan_log2 = g.kshift + g.lgg;
+  const int ng = (!(ablate & 1) && S_act > 0) ? (dim + (1 << gspan_log2) - 1) >> gspan_log2 : 0;
+  const int q0 = (int)((long long)ng * part / parts);
+  const int q1 = (int)((long long)ng * (part + 1) / parts);
+  const int split = ng ? reduce_split(ng, S_act) : 1;
+  const int nb = (q1 - q0) * split;
+  const int nfin = part == 0 ? kWsStat + dn + 1 : 0;
+  if (nb + nfin == 0) return 0;
+  const size_t rlds = nb ? (size_t(1) << gspan_log2) * 4 : 0;
+  int e = check_dyn_lds((const void*)linear_reduce_kernel, rlds);
+  if (e) return e;
+  hipLaunchKernelGGL(linear_reduce_kernel, dim3(nb + nfin), dim3(256), rlds, st, tables, S_act,
+                     g, dim, dacc, nb, split, q0, ws, S, dn, cum);
+  return (int)hipGetLastError();
+}
+
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
 static int launch_round(const void* w, const void* num, int dn, const void* cat, int dc,
                         const float* y, int B, int R, int S, float* dacc, int dim, float* ws,
                         int2* tables, float* cum, const LinParams& p, TableGeom g, int ablate,
-                        hipStream_t st) {
+                        int parts, hipStream_t st) {
   auto fn = linear_round_kernel<FPL, CH, RULE, NumT, WT>;
   const size_t lds = ((size_t(1) << g.log2cap) + kOvf) * 8;
   int e = check_dyn_lds((const void*)fn, lds);
   if (e) return e;
   hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)w, (const NumT*)num, dn, cat, dc,
                      y, B, R, dim, ws, tables, dacc, p, g, ablate);
-  const long long sact_ll = R > 0 ? ((long long)B + R - 1) / R : 0;
-  const int S_act = sact_ll < S ? (int)sact_ll : S;
-  const int gspan_log2 = g.kshift + g.lgg;
-  const int ng = (!(ablate & 1) && S_act > 0) ? (dim + (1 << gspan_log2) - 1) >> gspan_log2 : 0;
-  const int split = ng ? reduce_split(ng, S_act) : 1;
-  const int nb = ng * split;
-  const size_t rlds = nb ? (size_t(1) << gspan_log2) * 4 : 0;
-  e = check_dyn_lds((const void*)linear_reduce_kernel, rlds);
+  e = (int)hipGetLastError();
   if (e) return e;
-  hipLaunchKernelGGL(linear_reduce_kernel, dim3(nb + kWsStat + dn + 1), dim3(256), rlds, st,
-                     tables, S_act, g, dim, dacc, nb, split, ws, S, dn, cum);
-  return (int)hipGetLastError();
+  return launch_reduce(tables, B, R, S, g, dim, dacc, ws, dn, cum, 0, parts, ablate, st);
 }
 
 template <int FPL, int CH, int RULE>
 static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                           const void* cat, int dc, const float* y, int B, int R, int S, float* dacc,
                           int dim, float* ws, int2* tables, float* cum, const LinParams& p,
-                          TableGeom g, int ablate, hipStream_t st) {
+                          TableGeom g, int ablate, int parts, hipStream_t st) {
 #define OMLDM_LR(NT, WTT)                                                                      \
   return launch_round<FPL, CH, RULE, NT, WTT>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, ws, \
-                                              tables, cum, p, g, ablate, st)
+                                              tables, cum, p, g, ablate, parts, st)
   if (num_bf16) {
     if (w_bf16) OMLDM_LR(__hip_bfloat16, __hip_bfloat16);
     OMLDM_LR(__hip_bfloat16, float);
@@ -616,15 +649,17 @@ template <int FPL, int CH>
 static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, int num_bf16,
                          int dn, const void* cat, int dc, const float* y, int B, int R, int S,
                          float* dacc, int dim, float* ws, int2* tables, float* cum,
-                         const LinParams& p, TableGeom g, int ablate, hipStream_t st) {
+                         const LinParams& p, TableGeom g, int ablate, int parts,
+                         hipStream_t st) {
   if (rule == kHinge)
     return dispatch_round<FPL, CH, kHinge>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
-                                           dim, ws, tables, cum, p, g, ablate, st);
+                                           dim, ws, tables, cum, p, g, ablate, parts, st);
   if (rule == kEpsInsensitive)
     return dispatch_round<FPL, CH, kEpsInsensitive>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R,
-                                                    S, dacc, dim, ws, tables, cum, p, g, ablate, st);
+                                                    S, dacc, dim, ws, tables, cum, p, g, ablate,
+                                                    parts, st);
   return dispatch_round<FPL, CH, kLogistic>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
-                                            dacc, dim, ws, tables, cum, p, g, ablate, st);
+                                            dacc, dim, ws, tables, cum, p, g, ablate, parts, st);
 }
 
 template <int FPL, typename NumT, typename WT>
@@ -690,9 +725,10 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
                                  float* dacc, int dim, float* ws, void* tables, float* cum,
                                  int rule, int variant, float C, float eps, float lr, float lam,
                                  float inv_p, int bias, int cspan, int log2cap, int chunk,
-                                 int ablate, void* stream) {
+                                 int ablate, int parts, void* stream) {
   if (S <= 0) return 0;
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
+  if (parts < 1 || parts > 64) return -4;
   int geo[3];
   if (omldm_linear_table_geom(dim, log2cap, geo)) return -3;
   const TableGeom g{geo[0], geo[1], geo[2], reduce_lgg(geo[2], geo[1])};
@@ -704,11 +740,36 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
   const int F = dn + dc + (bias ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
   int2* tb = (int2*)tables;
-  if (F <= 64 && chunk <= 8) return dispatch_rule<1, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
-  if (F <= 64) return dispatch_rule<1, 16>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
-  if (F <= 128) return dispatch_rule<2, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
-  if (F <= 256) return dispatch_rule<4, 4>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, st);
+  if (F <= 64 && chunk <= 8) return dispatch_rule<1, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, st);
+  if (F <= 64) return dispatch_rule<1, 16>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, st);
+  if (F <= 128) return dispatch_rule<2, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, st);
+  if (F <= 256) return dispatch_rule<4, 4>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, st);
   return -2;
+}
+
+// Reduce part `part` (1 ≤ part < parts) of the round launched by omldm_linear_round with
+// the same arguments; part 0 was launched by the round call itself.
+OMLDM_API int omldm_linear_reduce_part(void* tables, float* ws, float* cum, float* dacc, int dim,
+                                       int dn, int B, int R, int S, int log2cap, int part,
+                                       int parts, int ablate, void* stream) {
+  if (S <= 0) return 0;
+  if (parts < 1 || parts > 64 || part < 1 || part >= parts) return -4;
+  int geo[3];
+  if (omldm_linear_table_geom(dim, log2cap, geo)) return -3;
+  const TableGeom g{geo[0], geo[1], geo[2], reduce_lgg(geo[2], geo[1])};
+  return launch_reduce((const int2*)tables, B, R, S, g, dim, dacc, ws, dn, cum, part, parts,
+                       ablate, (hipStream_t)stream);
+}
+
+// Accumulator slice [lo, hi) completed by reduce part `part` of `parts` (see part_bounds).
+OMLDM_API int omldm_linear_part_bounds(int dim, int part, int parts, long long* lo_hi) {
+  if (parts < 1 || part < 0 || part >= parts) return -4;
+  int geo[3];
+  const int ld = ceil_log2(dim);
+  if (omldm_linear_table_geom(dim, ld + 2, geo)) return -3;  // kshift/log2nb depend on dim only
+  const TableGeom g{geo[0], geo[1], geo[2], reduce_lgg(geo[2], geo[1])};
+  part_bounds(dim, g, part, parts, &lo_hi[0], &lo_hi[1]);
+  return 0;
 }
 
 OMLDM_API int omldm_linear_predict(const void* w, int w_bf16, long long wstride, int M,

@@ -15,6 +15,7 @@ one *micro-batch round* at a time and keeps all of its state in device tensors:
 from __future__ import annotations
 
 from dataclasses import dataclass
+from typing import Callable
 
 import torch
 
@@ -26,6 +27,12 @@ class RoundContext:
     spokes: int = 1          # virtual spokes on this rank for this round
     inv_p: float = 1.0       # 1 / (number of workers the round's delta is averaged over)
     fused_delta: bool = False  # leave the round delta in the sync buffer (Synchronous fast path)
+    # pipelined sync (learners with supports_reduce_parts): the delta reduce runs in
+    # ``reduce_parts`` launches and ``on_reduce_part(k, lo, hi)`` is called right after
+    # part k is enqueued, with the slice [lo, hi) of the sync buffer it completes — the
+    # protocol starts that slice's collective while the next part reduces
+    reduce_parts: int = 1
+    on_reduce_part: Callable[[int, int, int], None] | None = None
 
 
 class Learner:
@@ -33,6 +40,7 @@ class Learner:
     TASK = "classification"  # classification | regression | clustering
     merge_mode = "mean"
     supports_fused_delta = False
+    supports_reduce_parts = False
 
     def __init__(self, hyper: dict | None, space: FeatureSpace, device="cpu"):
         self.hyper = dict(hyper or {})

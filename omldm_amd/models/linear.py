@@ -30,6 +30,7 @@ class LinearLearner(Learner):
     RULE = L.RULE_HINGE
     DEFAULT_VARIANT = "PA-I"
     supports_fused_delta = True
+    supports_reduce_parts = True
 
     def __init__(self, hyper: dict | None, space: FeatureSpace, device="cpu"):
         super().__init__(hyper, space, device)
@@ -86,11 +87,16 @@ class LinearLearner(Learner):
         B = batch.B
         S = max(1, int(ctx.spokes))
         R = max(1, -(-B // S)) if B else 1
+        parts = max(1, int(ctx.reduce_parts)) if ctx.on_reduce_part is not None else 1
         if B:
             L.linear_round(self._wread(), batch, R, S, self.dacc, None, self.rule, ctx.inv_p,
-                           self.log2cap, cum=self.cum, ablate=self.ablate, chunk=self.chunk)
+                           self.log2cap, cum=self.cum, ablate=self.ablate, chunk=self.chunk,
+                           parts=parts, on_part=ctx.on_reduce_part)
         else:
             self.dacc[self.dim:].zero_()  # no workers this round on this rank
+            if ctx.on_reduce_part is not None:  # still join every collective of the round
+                for k in range(parts):
+                    ctx.on_reduce_part(k, *L.part_bounds(self.dim, k, parts, self.dacc.is_cuda))
         if not ctx.fused_delta:
             self.apply_delta()
 

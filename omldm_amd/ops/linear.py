@@ -68,13 +68,20 @@ def _cpu_threads() -> int:
 
 def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torch.Tensor,
                  stats: torch.Tensor | None, rule: LinearRule, inv_p: float, log2cap: int = 0,
-                 cum: torch.Tensor | None = None, ablate: int = 0, chunk: int = 8) -> None:
+                 cum: torch.Tensor | None = None, ablate: int = 0, chunk: int = 8,
+                 parts: int = 1, on_part=None) -> None:
     """One protocol round of S virtual spokes, R examples each (spoke s gets rows
     [s·R, (s+1)·R)). Every spoke with ≥1 row accumulates σ·Δ·inv_p into ``dacc[:dim]``,
     σ·inv_p into ``dacc[dim]`` and inv_p into ``dacc[dim+1]`` (so ``dacc`` is [dim+2]);
     writes per-spoke stats [S, 6] (optional) and adds the round totals into ``cum[:6]``
     (optional, device-side running counters). ``linear_apply`` then averages over the
-    active workers: w = (dacc[dim]·w + dacc[:dim]) / dacc[dim+1]."""
+    active workers: w = (dacc[dim]·w + dacc[:dim]) / dacc[dim+1].
+
+    ``parts`` > 1 (GPU): the reduce of the spoke tables into ``dacc`` is issued as that
+    many launches over disjoint key ranges, and ``on_part(k, lo, hi)`` runs after part k
+    is enqueued with the slice ``dacc[lo:hi]`` it completes (``part_bounds``), so the
+    caller can start that slice's collective while the next part reduces. The CPU path
+    computes everything first and reports the same slices."""
     dim = int(dacc.shape[0]) - 2
     assert w.shape[0] == dim and (stats is None or stats.shape == (S, STAT_W))
     assert dacc.dtype == torch.float32
@@ -102,8 +109,17 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
             num.shape[1], dp(cat), cat.shape[1], dp(y), batch.B, R, S, ptr(dacc), dim,
             ptr(ws), ptr(tables), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr,
             rule.lam, inv_p, int(rule.bias), batch.cat_span, log2cap, int(chunk), int(ablate),
-            native.stream_of(w))
+            int(parts), native.stream_of(w))
         check(rc, "omldm_linear_round")
+        if on_part is not None:
+            on_part(0, *part_bounds(dim, 0, parts, cuda=True))
+        for k in range(1, parts):
+            rc = native.hip().omldm_linear_reduce_part(
+                ptr(tables), ptr(ws), ptr(cum), ptr(dacc), dim, num.shape[1], batch.B, R, S,
+                log2cap, k, parts, int(ablate), native.stream_of(w))
+            check(rc, "omldm_linear_reduce_part")
+            if on_part is not None:
+                on_part(k, *part_bounds(dim, k, parts, cuda=True))
         if stats is not None:
             stats.copy_(ws[: S * wsw].view(S, wsw)[:, :STAT_W])
     else:
@@ -117,6 +133,29 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         if cum is not None:
             cum[:STAT_W] += st.sum(0)
             cum[4] -= st[:, 4].sum()  # sigma is not a running total
+        if on_part is not None:
+            for k in range(parts):
+                on_part(k, *part_bounds(dim, k, parts, cuda=False))
+
+
+def part_bounds(dim: int, part: int, parts: int, cuda: bool = True) -> tuple[int, int]:
+    """Slice [lo, hi) of a [dim + 2] round accumulator completed by reduce part ``part``
+    of ``parts`` — a function of dim only, so every rank issues identical collectives
+    (GPU: the kernel library's own key-group split; CPU: the same formula with the
+    default geometry, 4096-key groups)."""
+    if cuda:
+        import ctypes
+
+        lh = (ctypes.c_longlong * 2)()
+        check(native.hip().omldm_linear_part_bounds(dim, part, parts, lh),
+              "omldm_linear_part_bounds")
+        return int(lh[0]), int(lh[1])
+    ld = max(0, (dim - 1).bit_length())
+    g = min(ld, 12)
+    ng = (dim + (1 << g) - 1) >> g
+    lo = 0 if part == 0 else (ng * part // parts) << g
+    hi = dim + 2 if part == parts - 1 else min(dim + 2, (ng * (part + 1) // parts) << g)
+    return lo, hi
 
 
 def linear_apply(w32: torch.Tensor, w16: torch.Tensor | None, dacc: torch.Tensor) -> None:

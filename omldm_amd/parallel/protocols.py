@@ -140,6 +140,11 @@ class Synchronous(Protocol):
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
         self._E = None
+        # > 1: pipelined sync — the learner's delta reduce runs in that many key-range
+        # launches and each range's all-reduce starts as soon as its launch is enqueued
+        # (RCCL works on range k while the GPU reduces range k+1). Same sums, same
+        # collectives on every rank; only with every rank a hub (all-reduce).
+        self.reduce_parts = max(1, _cfg_int(self.cfg, "reduceParts", 1))
 
     # The round is split in two so the engine can coalesce the collectives of several
     # pipelines into one bucket: local() trains and returns the buffer to
@@ -170,7 +175,29 @@ class Synchronous(Protocol):
         self._buf = None
         self.stats.rounds += 1
 
+    def _pipelined(self) -> bool:
+        L = self.learner
+        return (self.reduce_parts > 1 and self.G > 1 and L.supports_fused_delta
+                and L.supports_reduce_parts and (self.hubs == 0 or self.hubs >= self.G))
+
     def round(self, batch):
+        if self._pipelined():
+            L, works = self.learner, []
+            buf = L.delta_buffer()
+
+            def on_part(k: int, lo: int, hi: int) -> None:
+                if hi > lo:
+                    works.append(self.comm.all_reduce_(buf[lo:hi], "sync", async_op=True))
+
+            ctx = self._ctx(fused=True)
+            ctx.reduce_parts, ctx.on_reduce_part = self.reduce_parts, on_part
+            L.fit(batch, ctx)
+            for w in works:
+                if w is not None:
+                    w.wait()  # the compute stream waits for RCCL; the host does not block
+            self._buf = buf
+            self.finish()
+            return
         buf = self.local(batch)
         self.comm.hub_reduce_(buf, self.hubs, tag="sync")
         self.finish()

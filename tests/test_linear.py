@@ -246,3 +246,36 @@ def test_hip_round_table_overflow_is_counted(cuda):
     torch.cuda.synchronize()
     assert float(st[:, 5].sum()) > 0
     assert torch.isfinite(d).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [2, 4, 7])
+def test_hip_round_reduce_parts(cuda, parts):
+    """Reduce issued as `parts` key-range launches (pipelined sync): the slices reported
+    after each launch tile [0, dim + 2), match the kernel library's bounds, and the
+    accumulator equals the CPU round; a slice is final when it is reported."""
+    sp = FeatureSpace(13, 0, 26, 1 << 20)
+    S, R = 96, 32
+    b = synth_batch(sp, S * R, seed=9)
+    w = torch.randn(sp.dim) * 0.01
+    rule = L.LinearRule()
+    d_cpu = torch.zeros(sp.dim + 2)
+    L.linear_round(w, b, R, S, d_cpu, None, rule, 1.0)
+    d_gpu = torch.zeros(sp.dim + 2, device=cuda)
+    seen, snaps = [], []
+
+    def on_part(k, lo, hi):
+        seen.append((k, lo, hi))
+        snaps.append(d_gpu[lo:hi].clone())  # stream-ordered: taken right after part k
+
+    L.linear_round(w.to(cuda), b.to(cuda), R, S, d_gpu, None, rule, 1.0, log2cap=11,
+                   parts=parts, on_part=on_part)
+    torch.cuda.synchronize()
+    assert [k for k, _, _ in seen] == list(range(parts))
+    assert seen[0][1] == 0 and seen[-1][2] == sp.dim + 2
+    assert all(seen[k][2] == seen[k + 1][1] for k in range(parts - 1))
+    assert [(lo, hi) for _, lo, hi in seen] == [L.part_bounds(sp.dim, k, parts, cuda=False)
+                                                for k in range(parts)]
+    np.testing.assert_allclose(d_gpu.cpu().numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
+    final = torch.cat(snaps).cpu()
+    np.testing.assert_allclose(final.numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)

@@ -31,7 +31,7 @@ def _batch(rank, world, r):
     return synth_batch(SP, S * R, start=(r * world + rank) * S * R, seed=7)
 
 
-def _rank(rank, world, port, out):
+def _rank(rank, world, port, out, parts=1):
     import torch.distributed as dist
 
     from omldm_amd.models.linear import SVM
@@ -42,7 +42,7 @@ def _rank(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     L = SVM({"variant": "PA-I", "modelDtype": "bf16", "tableLog2": 10}, SP, dev)
-    P = Synchronous(Comm(), L, {"virtualSpokes": S})
+    P = Synchronous(Comm(), L, {"virtualSpokes": S, "reduceParts": parts})
     for r in range(ROUNDS):
         P.round(_batch(rank, world, r).to(dev))
     torch.cuda.synchronize()
@@ -52,14 +52,15 @@ def _rank(rank, world, port, out):
 
 
 @pytest.mark.gpu
-def test_two_ranks_one_gpu_equal_one_rank_double_spokes(cuda):
+@pytest.mark.parametrize("parts", [1, 3])
+def test_two_ranks_one_gpu_equal_one_rank_double_spokes(cuda, parts):
     from omldm_amd.api.batch import HashedBatch
     from omldm_amd.models.linear import SVM
     from omldm_amd.parallel.comm import Comm
     from omldm_amd.parallel.protocols import Synchronous
 
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_rank, args=(2, _port(), d), nprocs=2, start_method="spawn")
+        mp.start_processes(_rank, args=(2, _port(), d, parts), nprocs=2, start_method="spawn")
         w0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)["w"]
         w1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)["w"]
     torch.testing.assert_close(w0, w1)

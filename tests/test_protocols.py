@@ -86,6 +86,28 @@ def test_synchronous_replicas_and_equivalence(hubs):
     assert res[0]["stats"]["modelsShipped"] == 4 * 2 * 2
 
 
+def test_synchronous_pipelined_reduce_matches_one_shot():
+    """reduceParts > 1: the delta is all-reduced in key-range slices as they complete —
+    the same sums as one all-reduce of the whole buffer, same accounting."""
+    base = run(2, "SVM", "Synchronous", {})
+    piped = run(2, "SVM", "Synchronous", {"reduceParts": 3})
+    for r in range(2):
+        for a, b in zip(base[r]["states"], piped[r]["states"]):
+            assert same(a, b, 1e-6)
+    assert piped[0]["stats"]["modelsShipped"] == base[0]["stats"]["modelsShipped"]
+    assert piped[0]["stats"]["bytesShipped"] == base[0]["stats"]["bytesShipped"]
+
+
+def test_part_bounds_cover_accumulator():
+    from omldm_amd.ops.linear import part_bounds
+
+    for dim in (1 << 14, (1 << 20) + 7, 100):
+        for parts in (1, 2, 3, 4, 8):
+            sl = [part_bounds(dim, k, parts, cuda=False) for k in range(parts)]
+            assert sl[0][0] == 0 and sl[-1][1] == dim + 2
+            assert all(sl[k][1] == sl[k + 1][0] for k in range(parts - 1))
+
+
 @pytest.mark.parametrize("proto,cfg", [("Asynchronous", {}), ("SSP", {"staleness": 2})])
 def test_delayed_protocols_converge_to_same_model(proto, cfg):
     res = run(2, "PA", proto, cfg, rounds=5)
