@@ -46,10 +46,11 @@ class PackedBatch:
     """num | cat | y packed in ONE contiguous byte buffer so a micro-batch is one copy."""
 
     def __init__(self, space: FeatureSpace, B: int, device, pin: bool, num_dtype,
-                 thp: bool = False):
+                 thp: bool = False, y_dtype=torch.float32):
         esz = torch.tensor([], dtype=num_dtype).element_size()
         csz = torch.tensor([], dtype=space.cat_dtype).element_size()
-        self.sizes = [B * space.dn * esz, B * space.dc * csz, B * 4]
+        ysz = torch.tensor([], dtype=y_dtype).element_size()
+        self.sizes = [B * space.dn * esz, B * space.dc * csz, B * ysz]
         offs = [0]
         for s in self.sizes:
             offs.append(offs[-1] + ((s + 255) // 256) * 256)
@@ -68,7 +69,7 @@ class PackedBatch:
         self.batch = HashedBatch(
             f[offs[0]:offs[0] + self.sizes[0]].view(num_dtype).view(B, space.dn),
             f[offs[1]:offs[1] + self.sizes[1]].view(space.cat_dtype).view(B, space.dc),
-            f[offs[2]:offs[2] + self.sizes[2]].view(torch.float32).view(B),
+            f[offs[2]:offs[2] + self.sizes[2]].view(y_dtype).view(B),
             cat_span=space.cat_span)
 
 
@@ -85,6 +86,8 @@ def main(argv=None) -> int:
     ap.add_argument("--num-dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--wire", default="compact", choices=["wide", "compact"],
                     help="compact: field-aware uint16 categorical slots (half the PCIe bytes)")
+    ap.add_argument("--label-dtype", default="int8", choices=["int8", "fp32"],
+                    help="wire type of the ±1 labels (int8: 79 instead of 82 B per example)")
     ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")
     ap.add_argument("--pool-alloc", default="torch", choices=["torch", "thp"],
                     help="thp: pinned pool on transparent huge pages (2 MiB GPU translations)")
@@ -135,19 +138,24 @@ def main(argv=None) -> int:
     S, R = a.spokes, a.rows
     B = S * R
     num_dtype = torch.bfloat16 if a.num_dtype == "bf16" else torch.float32
+    y_dtype = torch.int8 if a.label_dtype == "int8" else torch.float32
 
     # ---- synthetic stream shard of this rank, pinned, packed
     pool = []
     for k in range(a.pool):
-        pb = PackedBatch(space, B, "cpu", on_gpu, num_dtype, thp=a.pool_alloc == "thp")
+        pb = PackedBatch(space, B, "cpu", on_gpu, num_dtype, thp=a.pool_alloc == "thp",
+                         y_dtype=y_dtype)
         tmp = synth_batch(space, B, start=(k * world + rank) * B, seed=25)
         pb.batch.num.copy_(tmp.num)
         pb.batch.cat.copy_(tmp.cat)
-        pb.batch.y.copy_(tmp.y)
+        pb.batch.y.copy_(tmp.y)  # ±1 → int8 exactly
+        assert torch.equal(pb.batch.y.float(), tmp.y)
         pool.append(pb)
-    dev = [PackedBatch(space, B, device, False, num_dtype) for _ in range(a.slots)]
+    dev = [PackedBatch(space, B, device, False, num_dtype, y_dtype=y_dtype)
+           for _ in range(a.slots)]
     if a.ingest == "device":
-        dev = [PackedBatch(space, B, device, False, num_dtype) for _ in range(a.pool)]
+        dev = [PackedBatch(space, B, device, False, num_dtype, y_dtype=y_dtype)
+               for _ in range(a.pool)]
         for d, p in zip(dev, pool):
             d.flat.copy_(p.flat)
 
@@ -448,7 +456,9 @@ def main(argv=None) -> int:
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32-update/bf16-model" if a.model_dtype == "bf16" else "fp32",
-            "data": "synthetic (Criteo-shaped hashed stream, pinned host pool replayed; H2D in timed loop)"
+            "data": "synthetic (Criteo-shaped hashed stream, pinned host pool replayed; H2D in timed loop; "
+                    f"{sum(pool[0].sizes) // B} B/example on the wire: bf16 numerical, uint16 field-aware "
+                    f"categorical slots, {a.label_dtype} labels)"
                     if a.ingest == "pinned" else "synthetic (HBM-resident replay)",
             "config": {"model": f"linear SVM PA-I, 2^{a.dim_log2} hashed features "
                                 f"(13 num + 26 cat + bias)",

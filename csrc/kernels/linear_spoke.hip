@@ -46,7 +46,14 @@ struct LinParams {
   float kadd;     // τ denominator offset: 1/(2C) for PA-II, 0 otherwise
   float shrink;   // per-step multiplicative L2 shrink of w (1 when λ = 0)
   float rshrink;  // 1 / shrink
+  int y_i8;       // labels on the wire as int8 (classification streams: ±1 exactly)
 };
+
+// Label of example t: fp32, or int8 on the compact classification wire (1 B instead of 4
+// per example over PCIe; ±1 and class ids are exact).
+__device__ __forceinline__ float load_label(const void* __restrict__ yv, int t, int y_i8) {
+  return y_i8 ? (float)static_cast<const signed char*>(yv)[t] : static_cast<const float*>(yv)[t];
+}
 
 // Bucketed LDS delta table geometry (host-computed, see omldm_linear_round):
 //   keys/vals [cap + kOvf]; bucket(key) = key >> kshift owns slots
@@ -184,7 +191,7 @@ struct Step {
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void linear_round_kernel(
     const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
-    int dc, const float* __restrict__ yv, int B, int R, int dim, float* __restrict__ ws,
+    int dc, const void* __restrict__ yv, int B, int R, int dim, float* __restrict__ ws,
     int2* __restrict__ tables, float* __restrict__ dacc, LinParams p, TableGeom g, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int cap = 1 << g.log2cap;
@@ -228,7 +235,7 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     for (int e = 0; e < CH; ++e) {
       const int t = tc + e;
       const bool ok = t < t1;
-      nyy[e] = ok ? yv[t] : __builtin_nanf("");
+      nyy[e] = ok ? load_label(yv, t, p.y_i8) : __builtin_nanf("");
 #pragma unroll
       for (int f = 0; f < FPL; ++f) {
         int idx = -1;
@@ -614,7 +621,7 @@ static int launch_reduce(const int2* tables, int B, int R, int S, TableGeom g, i
 
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
 static int launch_round(const void* w, const void* num, int dn, const void* cat, int dc,
-                        const float* y, int B, int R, int S, float* dacc, int dim, float* ws,
+                        const void* y, int B, int R, int S, float* dacc, int dim, float* ws,
                         int2* tables, float* cum, const LinParams& p, TableGeom g, int ablate,
                         int parts, hipStream_t st) {
   auto fn = linear_round_kernel<FPL, CH, RULE, NumT, WT>;
@@ -630,7 +637,7 @@ static int launch_round(const void* w, const void* num, int dn, const void* cat,
 
 template <int FPL, int CH, int RULE>
 static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
-                          const void* cat, int dc, const float* y, int B, int R, int S, float* dacc,
+                          const void* cat, int dc, const void* y, int B, int R, int S, float* dacc,
                           int dim, float* ws, int2* tables, float* cum, const LinParams& p,
                           TableGeom g, int ablate, int parts, hipStream_t st) {
 #define OMLDM_LR(NT, WTT)                                                                      \
@@ -647,7 +654,7 @@ static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf
 
 template <int FPL, int CH>
 static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, int num_bf16,
-                         int dn, const void* cat, int dc, const float* y, int B, int R, int S,
+                         int dn, const void* cat, int dc, const void* y, int B, int R, int S,
                          float* dacc, int dim, float* ws, int2* tables, float* cum,
                          const LinParams& p, TableGeom g, int ablate, int parts,
                          hipStream_t st) {
@@ -721,11 +728,11 @@ OMLDM_API int omldm_linear_table_geom(int dim, int log2cap, int* out3) {
 
 // tables: device scratch of S * ((1 << log2cap) + 64) int2.
 OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
-                                 const void* cat, int dc, const float* y, int B, int R, int S,
-                                 float* dacc, int dim, float* ws, void* tables, float* cum,
-                                 int rule, int variant, float C, float eps, float lr, float lam,
-                                 float inv_p, int bias, int cspan, int log2cap, int chunk,
-                                 int ablate, int parts, void* stream) {
+                                 const void* cat, int dc, const void* y, int y_i8, int B,
+                                 int R, int S, float* dacc, int dim, float* ws, void* tables,
+                                 float* cum, int rule, int variant, float C, float eps, float lr,
+                                 float lam, float inv_p, int bias, int cspan, int log2cap,
+                                 int chunk, int ablate, int parts, void* stream) {
   if (S <= 0) return 0;
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
   if (parts < 1 || parts > 64) return -4;
@@ -736,7 +743,7 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
   const float shrink = rule == kLogistic ? 1.f - lr * lam : 1.f - lam;
   const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias, cspan,
                     variant == kPA1 ? C : INFINITY, variant == kPA2 ? 0.5f / C : 0.f, shrink,
-                    1.f / shrink};
+                    1.f / shrink, y_i8 ? 1 : 0};
   const int F = dn + dc + (bias ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
   int2* tb = (int2*)tables;

@@ -86,7 +86,9 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
     assert w.shape[0] == dim and (stats is None or stats.shape == (S, STAT_W))
     assert dacc.dtype == torch.float32
     num, cat, y = batch.num, batch.cat, batch.y
-    assert cat.dtype == (torch.int16 if batch.cat_span else torch.int32) and y.dtype == torch.float32
+    assert cat.dtype == (torch.int16 if batch.cat_span else torch.int32)
+    # labels: fp32, or int8 on the compact classification wire (GPU kernel reads either)
+    assert y.dtype == torch.float32 or (y.dtype == torch.int8 and rule.rule != RULE_EPS)
     assert num.is_contiguous() and cat.is_contiguous() and y.is_contiguous()
     if S <= 0:
         return
@@ -106,7 +108,8 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         dp = native.dptr
         rc = native.hip().omldm_linear_round(
             ptr(w), int(w.dtype == torch.bfloat16), dp(num), int(num.dtype == torch.bfloat16),
-            num.shape[1], dp(cat), cat.shape[1], dp(y), batch.B, R, S, ptr(dacc), dim,
+            num.shape[1], dp(cat), cat.shape[1], dp(y), int(y.dtype == torch.int8), batch.B, R, S,
+            ptr(dacc), dim,
             ptr(ws), ptr(tables), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr,
             rule.lam, inv_p, int(rule.bias), batch.cat_span, log2cap, int(chunk), int(ablate),
             int(parts), native.stream_of(w))
@@ -124,6 +127,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
             stats.copy_(ws[: S * wsw].view(S, wsw)[:, :STAT_W])
     else:
         num32 = num.float().contiguous()
+        y = y.float().contiguous()
         st = stats if stats is not None else torch.zeros((S, STAT_W), dtype=torch.float32)
         native.host().omldm_cpu_linear_round(
             ptr(w), int(w.dtype == torch.bfloat16), ptr(num32), num32.shape[1], ptr(cat),

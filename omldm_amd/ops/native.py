@@ -40,7 +40,8 @@ def _sig(lib, name, res, args):
 
 # (name, restype, argtypes) for every exported HIP launcher.
 HIP_SIGS = [
-    ("omldm_linear_round", i32, [vp, i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, vp, i32, vp,
+    ("omldm_linear_round", i32, [vp, i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, i32, vp, i32,
+                                 vp,
                                  vp, vp, i32, i32, f32, f32, f32, f32, f32, i32, i32, i32, i32,
                                  i32, i32, vp]),
     ("omldm_linear_reduce_part", i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,

@@ -279,3 +279,25 @@ def test_hip_round_reduce_parts(cuda, parts):
     np.testing.assert_allclose(d_gpu.cpu().numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
     final = torch.cat(snaps).cpu()
     np.testing.assert_allclose(final.numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule", [L.LinearRule(), L.LinearRule(rule=L.RULE_LOGISTIC, variant=0)])
+def test_hip_round_int8_labels(cuda, rule):
+    """Compact classification wire: ±1 labels as int8 give the same round as fp32 labels
+    (and as the CPU round, which widens them)."""
+    sp = FeatureSpace(13, 0, 26, 1 << 16, field_aware=True)
+    S, R = 64, 16
+    b = synth_batch(sp, S * R, seed=11)
+    b8 = HashedBatch(b.num, b.cat, b.y.to(torch.int8), cat_span=b.cat_span)
+    assert torch.equal(b8.y.float(), b.y)
+    w = torch.randn(sp.dim) * 0.01
+    d32 = torch.zeros(sp.dim + 2, device=cuda)
+    d8 = torch.zeros(sp.dim + 2, device=cuda)
+    L.linear_round(w.to(cuda), b.to(cuda), R, S, d32, None, rule, 1.0)
+    L.linear_round(w.to(cuda), b8.to(cuda), R, S, d8, None, rule, 1.0)
+    dc = torch.zeros(sp.dim + 2)
+    L.linear_round(w, b8, R, S, dc, None, rule, 1.0)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(d8.cpu().numpy(), d32.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(d8.cpu().numpy(), dc.numpy(), rtol=2e-3, atol=2e-4)
