@@ -29,6 +29,7 @@ CASES = [
     ("RegressorPA", 1, {}, 4096),
     ("LogisticRegression", 0, {}, 4096),
     ("MultiClassPA", 2, {"nClasses": 4}, 4096),
+    ("MultiClassPA@8192", 2, {"nClasses": 4}, 8192),
     ("ORR", 1, {}, 1),
     ("K-means", 0, {"k": 16}, 1),
     ("NN", 0, {"hiddenLayers": [64, 64]}, 2048),
@@ -46,7 +47,7 @@ def main(argv=None) -> int:
     space = FeatureSpace(13, 0, 26, 1 << 20)
     res = {}
     for name, task, hyper, spokes in CASES:
-        if a.only and name not in a.only.split(","):
+        if a.only and name.split("@")[0] not in a.only.split(","):
             continue
         ring = []
         for k in range(3):
@@ -54,7 +55,7 @@ def main(argv=None) -> int:
             if name in ("NN",):
                 b = HashedBatch(b.num, b.cat, torch.where(b.y > 0, 1.0, -1.0))
             ring.append(b.to(dev))
-        L = make_learner(name, hyper, space, dev)
+        L = make_learner(name.split("@")[0], hyper, space, dev)
         ctx = RoundContext(spokes=spokes)
         for k in range(2):
             L.fit(ring[k % 3], ctx)

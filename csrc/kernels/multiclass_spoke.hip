@@ -5,123 +5,264 @@
 //   r = argmax_{k≠y} w_k·x,  ℓ = max(0, 1 − (w_y − w_r)·x),
 //   τ = ℓ/(2‖x‖²) (PA), min(C, ℓ/(2‖x‖²)) (PA-I), ℓ/(2‖x‖² + 1/(2C)) (PA-II),
 //   w_y += τx,  w_r −= τx.
-// Same structure as linear_spoke.hip: one wavefront per virtual spoke, lane = feature,
-// K scores per example by K interleaved DPP wave reductions; the spoke's private deltas
-// live in an LDS table keyed by feature with K floats per key; dense features keep
-// their K deltas in registers; round end ships Δ/P with row-contiguous atomics.
-#include "common.h"
+//
+// Same machinery as the binary learners (linear_spoke.hip, spoke_table.h): one wavefront
+// per virtual spoke, lane = feature, exact sequential updates over the spoke's rows.
+//  * The spoke's private deltas live in a bucketed LDS table keyed by feature with K
+//    floats per slot, so the K deltas of a feature come back in one vector LDS read on
+//    the sequential chain.
+//  * Rows, the K round-start prototype gathers and the slot probes (16-byte first probe
+//    of four slots, inline retry, slow path) of a chunk of CH rows are issued before the
+//    chunk's sequential part, rows one chunk ahead.
+//  * Dense features (numerical + intercept) keep their K deltas in registers and leave
+//    through a per-spoke workspace row whose columns one small kernel sums — no
+//    same-address atomics from thousands of spokes.
+//  * Round end: class k of the table is flushed group-major into its own region and
+//    summed by the shared bucket reducer into dacc[k]; multiclass_apply then averages
+//    over the active spokes.
+#include "spoke_table.h"
 
 namespace omldm {
 
+constexpr int kMcStat = 8;  // ws row: loss, n, mistakes, active, -, overflow, -, -, K×(dn+1) dense
+
+// Slot of hashed key `key` (find or insert): one 16-byte read of the four slots at the
+// key's 4-aligned hashed start in its bucket, CAS into the first empty one, inline
+// re-reads when another lane won it, then the slow path (same probe order, so a key is
+// never inserted twice). -1: table full (counted as overflow, the update is dropped).
+__device__ __forceinline__ int mc_slot(int* keys, int key, int b, int4 q, TableGeom g,
+                                       float& ovf) {
+  int sl = q.x == key ? b : q.y == key ? b + 1 : q.z == key ? b + 2 : q.w == key ? b + 3 : -2;
+  if (sl == -2) {
+    const int j = q.x == kEmptyKey ? 0 : q.y == kEmptyKey ? 1 : q.z == kEmptyKey ? 2
+                : q.w == kEmptyKey ? 3 : -1;
+    if (j >= 0) {
+      const int prev = atomicCAS(&keys[b + j], kEmptyKey, key);
+      if (prev == kEmptyKey || prev == key) sl = b + j;
+    }
+  }
+  for (int r = 0; r < 3 && sl == -2; ++r) {
+    const int4 q2 = *reinterpret_cast<const int4*>(&keys[b]);
+    sl = q2.x == key ? b : q2.y == key ? b + 1 : q2.z == key ? b + 2 : q2.w == key ? b + 3 : -2;
+    if (sl != -2) break;
+    const int j = q2.x == kEmptyKey ? 0 : q2.y == kEmptyKey ? 1 : q2.z == kEmptyKey ? 2
+                : q2.w == kEmptyKey ? 3 : -1;
+    if (j < 0) break;
+    const int prev = atomicCAS(&keys[b + j], kEmptyKey, key);
+    if (prev == kEmptyKey || prev == key) sl = b + j;
+  }
+  if (sl == -2) {
+    sl = table_find_or_insert(keys, key, g);
+    if (sl < 0) ovf += 1.f;
+  }
+  return sl;
+}
+
+// The K round-start prototype weights of one key from the key-major shadow Wt[dim][K]
+// (fp32 or bf16): one or a few vector loads, one cache line, instead of K gathers 4 MiB
+// apart in W[K][dim].
 template <int K>
+__device__ __forceinline__ void load_protos(const float* __restrict__ Wt, int idx, float (&o)[K]) {
+  if constexpr (K == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(Wt + (size_t)idx * 2);
+    o[0] = v.x;
+    o[1] = v.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; k += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(Wt + (size_t)idx * K + k);
+      o[k] = v.x; o[k + 1] = v.y; o[k + 2] = v.z; o[k + 3] = v.w;
+    }
+  }
+}
+template <int K>
+__device__ __forceinline__ void load_protos(const __hip_bfloat16* __restrict__ Wt, int idx,
+                                            float (&o)[K]) {
+  auto lo = [](uint32_t u) { return __uint_as_float(u << 16); };
+  auto hi = [](uint32_t u) { return __uint_as_float(u & 0xffff0000u); };
+  if constexpr (K == 2) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(Wt + (size_t)idx * 2);
+    o[0] = lo(v);
+    o[1] = hi(v);
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; k += 4) {
+      const uint2 v = *reinterpret_cast<const uint2*>(Wt + (size_t)idx * K + k);
+      o[k] = lo(v.x); o[k + 1] = hi(v.x); o[k + 2] = lo(v.y); o[k + 3] = hi(v.y);
+    }
+  }
+}
+
+template <int K, int CH, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void multiclass_round_kernel(
-    const float* __restrict__ W, const float* __restrict__ num, int dn,
-    const int* __restrict__ cat, int dc, const float* __restrict__ yv, int B, int R, int dim,
-    int nclass, int variant, float C, int bias, float* __restrict__ dacc,
-    float* __restrict__ stats, int log2cap) {
+    const WT* __restrict__ Wt, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
+    int dc, int cspan, const void* __restrict__ yv, int y_i8, int B, int R, int dim, int nclass,
+    int variant, float C, int bias, float* __restrict__ ws, int2* __restrict__ tables,
+    float* __restrict__ dacc, TableGeom g, int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int cap = 1 << log2cap;
+  const int cap = 1 << g.log2cap;
+  const int tsz = cap + kOvf;
   int* keys = reinterpret_cast<int*>(smem);
-  float* vals = reinterpret_cast<float*>(smem + (size_t)cap * sizeof(int));  // [cap][K]
+  float* vals = reinterpret_cast<float*>(smem + (size_t)tsz * sizeof(int));  // [tsz][K]
   const int lane = threadIdx.x;
   const int s = blockIdx.x;
+  const int wsw = kMcStat + nclass * (dn + 1);
+  float* wrow = ws + (size_t)s * wsw;
   const long long t0ll = (long long)s * R;
   const int t0 = t0ll > B ? B : (int)t0ll;
   const int t1 = (t0ll + R) > B ? B : (int)(t0ll + R);
-  if (t0 >= t1) return;
-  for (int i = lane; i < cap; i += kWave) {
+  if (t0 >= t1) {  // idle spoke: not a worker this round
+    for (int k = lane; k < wsw; k += kWave) wrow[k] = 0.f;
+    return;
+  }
+  for (int i = lane; i < tsz; i += kWave) {
     keys[i] = kEmptyKey;
 #pragma unroll
     for (int k = 0; k < K; ++k) vals[(size_t)i * K + k] = 0.f;
   }
   __syncthreads();
-  const int F = dn + dc + (bias ? 1 : 0);
-  float loss_sum = 0.f, nex = 0.f, mist = 0.f, ovf = 0.f;
+  const int bs_log2 = g.log2cap - g.log2nb;
+  const uint32_t bmask = (1u << bs_log2) - 1u;
+  const int dcol = lane < dn ? lane : ((bias && lane == dn + dc) ? dn : -1);
   float dreg[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) dreg[k] = 0.f;
-  const bool dense = lane < dn || (bias && lane == dn + dc);
-  for (int t = t0; t < t1; ++t) {
-    const float yf = yv[t];
-    if (__builtin_isnan(yf)) continue;
-    const int yc = (int)yf;
-    int idx = -1;
-    float xv = 0.f;
-    if (lane < F) {
-      if (bias && lane == dn + dc) {
-        idx = dim - 1;
-        xv = 1.f;
-      } else if (lane < dn) {
-        idx = lane;
-        xv = num[(size_t)t * dn + lane];
+  float loss_sum = 0.f, nex = 0.f, mist = 0.f, ovf = 0.f;
+
+  int nidx[CH];
+  float nxv[CH], nyy[CH];
+  auto load_chunk = [&](int tc) {
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const int t = tc + e;
+      const bool ok = t < t1;
+      nyy[e] = ok ? load_label(yv, t, y_i8) : __builtin_nanf("");
+      int idx = -1;
+      float v = 0.f;
+      if (ok) load_feature(num, dn, cat, dc, t, lane, dim, bias, cspan, idx, v);
+      nidx[e] = idx;
+      nxv[e] = v;
+    }
+  };
+  load_chunk(t0);
+  for (int tc = t0; tc < t1; tc += CH) {
+    int idx[CH], slot[CH];
+    float xv[CH], yy[CH], wv[CH][K];
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      idx[e] = nidx[e];
+      xv[e] = nxv[e];
+      yy[e] = nyy[e];
+    }
+    // round-start prototypes of the whole chunk (read-only during the round)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      if (idx[e] >= 0) {
+        load_protos<K>(Wt, idx[e], wv[e]);
       } else {
-        const int c = cat[(size_t)t * dc + (lane - dn)];
-        if (c != -1) {
-          idx = c & 0x7fffffff;
-          xv = c < 0 ? -1.f : 1.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) wv[e][k] = 0.f;
+      }
+    }
+    if (tc + CH < t1) load_chunk(tc + CH);
+    // slots of the chunk's hashed features: all first probes issued, then resolved
+    int b0[CH];
+    int4 kq[CH];
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const int key = idx[e];
+      b0[e] = ((key >> g.kshift) << bs_log2) + (int)((hmix((uint32_t)key) & bmask) & ~3u);
+      kq[e] = (dcol < 0 && key >= 0) ? *reinterpret_cast<const int4*>(&keys[b0[e]])
+                                     : make_int4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < CH; ++e)
+      slot[e] = (dcol < 0 && idx[e] >= 0) ? mc_slot(keys, idx[e], b0[e], kq[e], g, ovf) : -1;
+    // exact sequential updates
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const float y = yy[e];
+      if (__builtin_isnan(y) || (ablate & 2)) continue;  // wave-uniform
+      const int yc = (int)y;
+      float d[K];
+      if (dcol >= 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) d[k] = dreg[k];
+      } else if (slot[e] >= 0) {
+        if constexpr (K % 4 == 0) {
+#pragma unroll
+          for (int k = 0; k < K; k += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(&vals[(size_t)slot[e] * K + k]);
+            d[k] = v.x; d[k + 1] = v.y; d[k + 2] = v.z; d[k + 3] = v.w;
+          }
+        } else {
+          const float2 v = *reinterpret_cast<const float2*>(&vals[(size_t)slot[e] * K]);
+          d[0] = v.x;
+          d[1] = v.y;
         }
-      }
-      if ((unsigned)idx >= (unsigned)dim) {
-        idx = -1;
-        xv = 0.f;
-      }
-    }
-    int slot = -1;
-    if (!dense && idx >= 0) {
-      slot = lds_find_or_insert(keys, idx, log2cap);
-      if (slot < 0) ovf += 1.f;
-    }
-    float sc[K];
+      } else {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      float wv = 0.f, d = 0.f;
-      if (idx >= 0 && k < nclass) {
-        wv = W[(size_t)k * dim + idx];
-        d = dense ? dreg[k] : (slot >= 0 ? vals[(size_t)slot * K + k] : 0.f);
+        for (int k = 0; k < K; ++k) d[k] = 0.f;
       }
-      sc[k] = xv * (wv + d);
-    }
-    float n2 = xv * xv;
-    // K + 1 interleaved wave reductions
+      float sc[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) sc[k] = wave_sum(sc[k]);
-    n2 = wave_sum(n2);
-    int r = -1;
-    float best = -INFINITY;
+      for (int k = 0; k < K; ++k) sc[k] = (k < nclass) ? xv[e] * (wv[e][k] + d[k]) : 0.f;
+      float n2 = xv[e] * xv[e];
 #pragma unroll
-    for (int k = 0; k < K; ++k)
-      if (k < nclass && k != yc && sc[k] > best) {
-        best = sc[k];
-        r = k;
-      }
-    float sy = 0.f;
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-      if (k == yc) sy = sc[k];
-    const float margin = sy - best;
-    const float loss = fmaxf(0.f, 1.f - margin);
-    loss_sum += loss;
-    nex += 1.f;
-    mist += margin <= 0.f ? 1.f : 0.f;
-    float tau = 0.f;
-    if (loss > 0.f && n2 > 0.f && r >= 0) {
-      const float den = 2.f * n2;
-      tau = variant == 0 ? loss / den : (variant == 1 ? fminf(C, loss / den) : loss / (den + 0.5f / C));
-    }
-    if (tau != 0.f && idx >= 0) {
+      for (int k = 0; k < K; k += 2) wave_sum2(sc[k], sc[k + 1]);
+      n2 = wave_sum(n2);
+      int r = -1;
+      float best = -INFINITY, sy = 0.f;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const float g = k == yc ? tau * xv : (k == r ? -tau * xv : 0.f);
-        if (g != 0.f) {
-          if (dense) dreg[k] += g;
-          else if (slot >= 0) atomicAdd(&vals[(size_t)slot * K + k], g);
+        if (k < nclass && k != yc && sc[k] > best) {
+          best = sc[k];
+          r = k;
+        }
+        if (k == yc) sy = sc[k];
+      }
+      const float margin = sy - best;
+      const float loss = fmaxf(0.f, 1.f - margin);
+      loss_sum += loss;
+      nex += 1.f;
+      mist += margin <= 0.f ? 1.f : 0.f;
+      float tau = 0.f;
+      if (loss > 0.f && n2 > 0.f && r >= 0) {
+        const float den = 2.f * n2;
+        tau = variant == 0 ? loss * __builtin_amdgcn_rcpf(den)
+            : variant == 1 ? fminf(C, loss * __builtin_amdgcn_rcpf(den))
+                           : loss * __builtin_amdgcn_rcpf(den + 0.5f / C);
+      }
+      if (tau != 0.f && idx[e] >= 0) {  // wave-uniform τ
+        const float gy = tau * xv[e];
+        if (dcol >= 0) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            if (k == yc) dreg[k] += gy;
+            if (k == r) dreg[k] -= gy;
+          }
+        } else if (slot[e] >= 0) {
+          if (yc >= 0 && yc < nclass) atomicAdd(&vals[(size_t)slot[e] * K + yc], gy);
+          atomicAdd(&vals[(size_t)slot[e] * K + r], -gy);
         }
       }
     }
   }
   __syncthreads();
-  // Round end: Δ/P (inv count is applied by the caller's averaging) into dacc[K][dim].
-  for (int i = lane; i < cap; i += kWave) {
+  // Round end: class k of slot i of spoke s → region k, [i >> seg][s][i & seg mask]
+  // (group-major, the shared bucket reducer's layout); overflow-area entries go straight
+  // to dacc.
+  const int seg_log2 = bs_log2 + g.lgg;
+  const size_t S_tot = gridDim.x;
+  const size_t region = S_tot << g.log2cap;
+  for (int i = lane; i < cap && !(ablate & 1); i += kWave) {
+    const size_t q = (size_t)(i >> seg_log2);
+    const size_t o = ((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1));
+    const int key = keys[i];
+    for (int k = 0; k < nclass; ++k)
+      tables[(size_t)k * region + o] = make_int2(key, __float_as_int(vals[(size_t)i * K + k]));
+  }
+  for (int i = cap + lane; i < tsz; i += kWave) {
     const int key = keys[i];
     if (key >= 0)
       for (int k = 0; k < nclass; ++k) {
@@ -129,69 +270,153 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
         if (v != 0.f) atomicAdd(&dacc[(size_t)k * dim + key], v);
       }
   }
-  if (dense && lane < F) {
-    const int key = lane < dn ? lane : dim - 1;
-    for (int k = 0; k < nclass; ++k)
-      if (dreg[k] != 0.f) atomicAdd(&dacc[(size_t)k * dim + key], dreg[k]);
-  }
+  if (dcol >= 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k < nclass) wrow[kMcStat + k * (dn + 1) + dcol] = dreg[k];
   const float ovf_total = wave_sum(ovf);
   if (lane == 0) {
-    atomicAdd(stats + 0, loss_sum);
-    atomicAdd(stats + 1, nex);
-    atomicAdd(stats + 2, mist);
-    atomicAdd(stats + 3, 1.f);  // active workers this round
-    atomicAdd(stats + 5, ovf_total);
+    wrow[0] = loss_sum;
+    wrow[1] = nex;
+    wrow[2] = mist;
+    wrow[3] = 1.f;  // active worker
+    wrow[4] = 0.f;
+    wrow[5] = ovf_total;
+    wrow[6] = 0.f;
+    wrow[7] = 0.f;
+    if (!bias)
+      for (int k = 0; k < nclass; ++k) wrow[kMcStat + k * (dn + 1) + dn] = 0.f;
   }
 }
 
-// W[k] += dacc[k] / n_active ; dacc = 0.
+// Workspace column sums (one block per column): stats[c] += Σ_s ws[s][c] for c < 8;
+// dense column (k, j) → dacc[k][j] (j < dn) or dacc[k][dim-1] (intercept).
+__global__ __launch_bounds__(256) void multiclass_finish_kernel(const float* __restrict__ ws,
+                                                                int S, int dn, int nclass, int dim,
+                                                                float* __restrict__ dacc,
+                                                                float* __restrict__ stats) {
+  __shared__ float part[4];
+  const int wsw = kMcStat + nclass * (dn + 1);
+  const int c = blockIdx.x;
+  float acc = 0.f;
+  for (int s = threadIdx.x; s < S; s += 256) acc += ws[(size_t)s * wsw + c];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = (part[0] + part[1]) + (part[2] + part[3]);
+    if (c < kMcStat) {
+      if (c != 4 && c < 6) stats[c] += t;
+    } else {
+      const int j = c - kMcStat, k = j / (dn + 1), jj = j % (dn + 1);
+      dacc[(size_t)k * dim + (jj < dn ? jj : dim - 1)] += t;
+    }
+  }
+}
+
+// W[k][i] += dacc[k][i] / n_active ; dacc = 0 ; key-major shadow Wt[i][k] = W[k][i]
+// (fp32 or bf16, row stride kp) for the next round's gathers.
 __global__ __launch_bounds__(256) void multiclass_apply_kernel(float* __restrict__ W,
-                                                               float* __restrict__ dacc,
-                                                               long long n,
+                                                               float* __restrict__ dacc, int dim,
+                                                               int nclass, void* __restrict__ Wt,
+                                                               int wt_bf16, int kp,
                                                                const float* __restrict__ nact) {
   const float na = *nact;
   const float r = na > 0.f ? 1.f / na : 0.f;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (long long)gridDim.x * 256) {
-    W[i] = fmaf(dacc[i], r, W[i]);
-    dacc[i] = 0.f;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < dim; i += gridDim.x * 256) {
+    for (int k = 0; k < nclass; ++k) {
+      const size_t o = (size_t)k * dim + i;
+      const float v = fmaf(dacc[o], r, W[o]);
+      W[o] = v;
+      dacc[o] = 0.f;
+      if (Wt) {
+        if (wt_bf16) static_cast<__hip_bfloat16*>(Wt)[(size_t)i * kp + k] = __float2bfloat16(v);
+        else static_cast<float*>(Wt)[(size_t)i * kp + k] = v;
+      }
+    }
   }
+}
+
+template <int K, typename NumT, typename WT>
+static void launch_mc(const void* Wt, const void* num, int dn, const void* cat, int dc, int cspan,
+                      const void* y, int y_i8, int B, int R, int S, int dim, int nclass,
+                      int variant, float C, int bias, float* ws, int2* tables, float* dacc,
+                      TableGeom g, size_t lds, hipStream_t st, int* err) {
+  auto fn = multiclass_round_kernel<K, 4, NumT, WT>;
+  int ablate = 0;  // timing diagnostics only: bit0 no flush, bit1 no sequential part
+  if (const char* e = getenv("OMLDM_MC_ABLATE")) ablate = atoi(e);
+  *err = check_dyn_lds((const void*)fn, lds);
+  if (*err) return;
+  hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)Wt, (const NumT*)num, dn, cat, dc,
+                     cspan, y, y_i8, B, R, dim, nclass, variant, C, bias, ws, tables, dacc, g,
+                     ablate);
 }
 
 }  // namespace omldm
 
 using namespace omldm;
 
-// stats: [8] device accumulators (loss, n, mistakes, active, -, overflow)
-OMLDM_API int omldm_multiclass_round(const float* W, const float* num, int dn, const int* cat,
-                                     int dc, const float* y, int B, int R, int S, int dim,
-                                     int nclass, int variant, float C, int bias, float* dacc,
-                                     float* stats, int log2cap, void* stream) {
+// One round of S spokes: dacc[nclass][dim] += Σ_s Δ_s, stats[0..5] += (loss, n, mistakes,
+// active spokes, -, overflow). ws: S·(8 + nclass·(dn+1)) floats; tables: nclass·S·2^log2cap
+// int2.
+OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* num, int num_bf16,
+                                     int dn, const void* cat, int dc, int cspan, const void* y, int y_i8,
+                                     int B, int R, int S, int dim, int nclass, int variant,
+                                     float C, int bias, float* dacc, float* stats, int log2cap,
+                                     float* ws, void* tables, void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (dn + dc + (bias ? 1 : 0) > 64) return -2;
   if (nclass < 2 || nclass > 16) return -3;
+  if (log2cap < 6 || log2cap > 13) return -1;
+  TableGeom g;
+  if (bucket_geom(dim, log2cap, &g)) return -4;  // per-class key space: the linear geometry
   const int K = nclass <= 2 ? 2 : nclass <= 4 ? 4 : nclass <= 8 ? 8 : 16;
-  const size_t lds = (size_t(1) << log2cap) * (4 + 4 * (size_t)K);
+  const size_t lds = ((size_t(1) << log2cap) + kOvf) * (4 + 4 * (size_t)K);
   if (lds > 160 * 1024) return -1;
   hipStream_t st = (hipStream_t)stream;
-#define OMLDM_MC(KK)                                                                           \
-  {                                                                                            \
-    int e = check_dyn_lds((const void*)multiclass_round_kernel<KK>, lds);                      \
-    if (e) return e;                                                                           \
-    hipLaunchKernelGGL(multiclass_round_kernel<KK>, dim3(S), dim3(64), lds, st, W, num, dn, cat, \
-                       dc, y, B, R, dim, nclass, variant, C, bias, dacc, stats, log2cap);      \
+  int e = 0;
+#define OMLDM_MC(KK)                                                                         \
+  {                                                                                          \
+    if (num_bf16 && wt_bf16)                                                                 \
+      launch_mc<KK, __hip_bfloat16, __hip_bfloat16>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, \
+          S, dim, nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, st, &e);           \
+    else if (num_bf16)                                                                       \
+      launch_mc<KK, __hip_bfloat16, float>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim,  \
+          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, st, &e);                   \
+    else if (wt_bf16)                                                                        \
+      launch_mc<KK, float, __hip_bfloat16>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim,  \
+          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, st, &e);                   \
+    else                                                                                     \
+      launch_mc<KK, float, float>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim, nclass,   \
+          variant, C, bias, ws, (int2*)tables, dacc, g, lds, st, &e);                           \
   }
   if (K == 2) OMLDM_MC(2) else if (K == 4) OMLDM_MC(4) else if (K == 8) OMLDM_MC(8) else OMLDM_MC(16)
 #undef OMLDM_MC
+  if (e) return e;
+  e = (int)hipGetLastError();
+  if (e) return e;
+  const long long sact_ll = ((long long)B + R - 1) / R;
+  const int S_act = sact_ll < S ? (int)sact_ll : S;
+  const int gspan = g.kshift + g.lgg;
+  const int ng = (dim + (1 << gspan) - 1) >> gspan;
+  const size_t region = (size_t)S << log2cap;
+  for (int k = 0; k < nclass; ++k) {
+    e = bucket_reduce_launch((const int2*)tables + k * region, S_act, S, g, dim,
+                             dacc + (size_t)k * dim, 0, ng, st);
+    if (e) return e;
+  }
+  hipLaunchKernelGGL(multiclass_finish_kernel, dim3(kMcStat + nclass * (dn + 1)), dim3(256), 0, st,
+                     ws, S, dn, nclass, dim, dacc, stats);
   return (int)hipGetLastError();
 }
 
-OMLDM_API int omldm_multiclass_apply(float* W, float* dacc, long long n, const float* nact,
-                                     void* stream) {
-  int blocks = (int)((n + 255) / 256);
-  if (blocks > 2048) blocks = 2048;
+// Wt: key-major shadow [dim][kp] (nullptr: none).
+OMLDM_API int omldm_multiclass_apply(float* W, float* dacc, int dim, int nclass, void* Wt,
+                                     int wt_bf16, int kp, const float* nact, void* stream) {
+  int blocks = (dim + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(multiclass_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, W,
-                     dacc, n, nact);
+                     dacc, dim, nclass, Wt, wt_bf16, kp, nact);
   return (int)hipGetLastError();
 }

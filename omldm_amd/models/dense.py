@@ -176,17 +176,27 @@ class MultiClassPA(Learner):
         self.variant = {"PA": 0, "PA-I": 1, "PA-II": 2}.get(v, 1)
         self.C = hp_float(self.hyper, "C", 1.0)
         self.bias = bool(self.hyper.get("bias", True))
+        # GPU: key-major prototype shadow for the round's gathers (fp32, or bf16 with
+        # modelDtype=bf16), refreshed by the apply pass and on every state load
+        self.Wt = None
+        if self.device.type == "cuda":
+            bf16 = str(self.hyper.get("modelDtype", "fp32")).lower() in ("bf16", "bfloat16")
+            self.Wt = D.proto_shadow(self.W, torch.bfloat16 if bf16 else torch.float32)
+
+    def on_state_loaded(self):
+        if self.Wt is not None:
+            self.Wt[:, : self.K].copy_(self.W.t())
 
     def fit(self, batch, ctx):
         if batch.B == 0:
             return
-        batch = batch.to_wide()
         S = max(1, ctx.spokes)
         R = max(1, -(-batch.B // S))
         self.st[3] = 0.0
         D.multiclass_round(self.W, batch, R, S, self.K, self.variant, self.C, self.bias,
-                           self.dacc, self.st, log2cap=hp_int(self.hyper, "tableLog2", 11))
-        D.multiclass_apply(self.W, self.dacc, self.st[3:4])
+                           self.dacc, self.st, log2cap=hp_int(self.hyper, "tableLog2", 0),
+                           Wt=self.Wt)
+        D.multiclass_apply(self.W, self.dacc, self.st[3:4], self.Wt)
         self.cum[:3] += self.st[:3]
         self.st[:3] = 0.0
 

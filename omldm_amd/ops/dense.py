@@ -57,25 +57,68 @@ def kmeans_assign(x: torch.Tensor, y: torch.Tensor | None, cent: torch.Tensor,
     return assign
 
 
+def class_pad(nclass: int) -> int:
+    """Row stride of the key-major prototype shadow (a power of two ≥ nclass)."""
+    return 2 if nclass <= 2 else 4 if nclass <= 4 else 8 if nclass <= 8 else 16
+
+
+def proto_shadow(W: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    """Key-major copy Wt[dim][kp] of the prototypes W[K][dim] (zero-padded classes) —
+    what the GPU round gathers: one cache line per key instead of K."""
+    K, dim = W.shape
+    Wt = torch.zeros((dim, class_pad(K)), dtype=dtype, device=W.device)
+    Wt[:, :K].copy_(W.t())
+    return Wt
+
+
 def multiclass_round(W: torch.Tensor, batch: HashedBatch, R: int, S: int, nclass: int,
                      variant: int, C: float, bias: bool, dacc: torch.Tensor,
-                     stats: torch.Tensor, log2cap: int = 11) -> None:
+                     stats: torch.Tensor, log2cap: int = 0,
+                     Wt: torch.Tensor | None = None) -> None:
     """S virtual spokes of MultiClassPA; dacc[K, dim] += Σ_s Δ_s; stats += (loss, n,
-    mistakes, active spokes, -, overflow)."""
+    mistakes, active spokes, -, overflow).
+
+    GPU: the compact or wide categorical wire, bf16 or fp32 numerical features and fp32
+    or int8 labels are read as they are; ``log2cap`` 0 sizes the LDS delta table (one
+    slot of K floats per hashed key) from the spoke's rows. CPU: the C++ mirror on the
+    wide int32 format."""
+    from omldm_amd.ops.linear import _workspace
+
     K, dim = W.shape
-    assert batch.cat_span == 0, "MultiClassPA consumes the int32 categorical format"
     if batch.B == 0:
         return
-    num = batch.num.float().contiguous()
     if W.is_cuda:
+        num, cat, y = batch.num, batch.cat, batch.y
+        assert num.dtype in (torch.float32, torch.bfloat16) and y.dtype in (torch.float32, torch.int8)
+        assert all(t.is_contiguous() for t in (num, cat, y))
+        dn, dc = int(num.shape[1]), int(cat.shape[1])
+        if log2cap <= 0:  # ≤ 1/2 load for the spoke's hashed keys (K floats per slot)
+            from omldm_amd.ops.linear import min_log2cap
+
+            want = max(1, 2 * R * max(1, dc) - 1).bit_length()
+            kp = 2 if nclass <= 2 else 4 if nclass <= 4 else 8 if nclass <= 8 else 16
+            log2cap = max(min_log2cap(dim), min(12, want))
+            while log2cap > min_log2cap(dim) and ((1 << log2cap) + 64) * (4 + 4 * kp) > 64 << 10:
+                log2cap -= 1  # ≤ 64 KiB of LDS per spoke wave
+        wsw = 8 + nclass * (dn + 1)
+        ws = _workspace(W.device, S * wsw, key="mc_ws")
+        tables = _workspace(W.device, nclass * S * (1 << log2cap) * 2, key="mc_tables")
+        if Wt is None:
+            Wt = proto_shadow(W)
+        assert Wt.shape == (dim, class_pad(nclass)) and Wt.is_contiguous()
         check(native.hip().omldm_multiclass_round(
-            ptr(W), ptr(num), num.shape[1], ptr(batch.cat), batch.cat.shape[1], ptr(batch.y),
-            batch.B, R, S, dim, nclass, variant, C, int(bias), ptr(dacc), ptr(stats), log2cap,
-            native.stream_of(W)), "omldm_multiclass_round")
+            ptr(Wt), int(Wt.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
+            dn, ptr(cat), dc, batch.cat_span,
+            ptr(y), int(y.dtype == torch.int8), batch.B, R, S, dim, nclass, variant, C, int(bias),
+            ptr(dacc), ptr(stats), log2cap, ptr(ws), ptr(tables), native.stream_of(W)),
+            "omldm_multiclass_round")
     else:
+        batch = batch.to_wide()
+        num = batch.num.float().contiguous()
         native.host().omldm_cpu_multiclass_round(
-            ptr(W), ptr(num), num.shape[1], ptr(batch.cat), batch.cat.shape[1], ptr(batch.y),
-            batch.B, R, S, dim, nclass, variant, C, int(bias), ptr(dacc), ptr(stats))
+            ptr(W), ptr(num), num.shape[1], ptr(batch.cat), batch.cat.shape[1],
+            ptr(batch.y.float().contiguous()), batch.B, R, S, dim, nclass, variant, C, int(bias),
+            ptr(dacc), ptr(stats))
 
 
 MLP_MB = 32          # mini-batch rows of the fused MLP kernel
@@ -203,10 +246,15 @@ def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int], act: int = 
     return mlp_forward_reference(w, x, widths, act)
 
 
-def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor) -> None:
+def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor,
+                     Wt: torch.Tensor | None = None) -> None:
+    """W += dacc / n_active; dacc = 0; refresh the key-major shadow ``Wt`` if given."""
     if W.is_cuda:
-        check(native.hip().omldm_multiclass_apply(ptr(W), ptr(dacc), W.numel(), ptr(nact),
-                                                  native.stream_of(W)), "omldm_multiclass_apply")
+        K, dim = (1, W.numel()) if W.dim() == 1 else W.shape  # 1-D: a flat parameter vector
+        assert Wt is None or W.dim() == 2
+        check(native.hip().omldm_multiclass_apply(
+            ptr(W), ptr(dacc), dim, K, ptr(Wt), int(Wt is not None and Wt.dtype == torch.bfloat16),
+            class_pad(K), ptr(nact), native.stream_of(W)), "omldm_multiclass_apply")
     else:
         n = float(nact.item())
         if n > 0:

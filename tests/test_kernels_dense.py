@@ -123,16 +123,41 @@ def test_hip_kmeans_assign(cuda):
 
 
 @pytest.mark.gpu
-def test_hip_multiclass_round_vs_cpu(cuda):
-    b = synth_batch(SP, 2000, task=2, n_classes=4, seed=5)
-    W = torch.randn(4, SP.dim) * 0.01
-    st, dacc = torch.zeros(8), torch.zeros(4, SP.dim)
-    D.multiclass_round(W, b, 50, 40, 4, 1, 1.0, True, dacc, st)
-    stg, daccg = torch.zeros(8, device=cuda), torch.zeros(4, SP.dim, device=cuda)
-    D.multiclass_round(W.to(cuda), b.to(cuda), 50, 40, 4, 1, 1.0, True, daccg, stg, log2cap=11)
+@pytest.mark.parametrize("nclass,R,S", [(4, 50, 40), (3, 16, 96), (2, 8, 64), (7, 16, 32)])
+def test_hip_multiclass_round_vs_cpu(cuda, nclass, R, S):
+    b = synth_batch(SP, R * S, task=2, n_classes=nclass, seed=5)
+    W = torch.randn(nclass, SP.dim) * 0.01
+    st, dacc = torch.zeros(8), torch.zeros(nclass, SP.dim)
+    D.multiclass_round(W, b, R, S, nclass, 1, 1.0, True, dacc, st)
+    stg, daccg = torch.zeros(8, device=cuda), torch.zeros(nclass, SP.dim, device=cuda)
+    D.multiclass_round(W.to(cuda), b.to(cuda), R, S, nclass, 1, 1.0, True, daccg, stg)
     torch.cuda.synchronize()
+    assert float(stg[5]) == 0.0  # no LDS table overflow
     np.testing.assert_allclose(stg.cpu()[[1, 3]].numpy(), st[[1, 3]].numpy())
+    np.testing.assert_allclose(stg.cpu()[[0, 2]].numpy(), st[[0, 2]].numpy(), rtol=1e-3)
     np.testing.assert_allclose(daccg.cpu().numpy(), dacc.numpy(), rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+def test_hip_multiclass_round_compact_wire(cuda):
+    """Field-aware uint16 categoricals, bf16 numericals and int8 class labels read
+    directly by the kernel == the CPU mirror on the widened batch."""
+    from omldm_amd.api.batch import FeatureSpace, HashedBatch
+
+    sp = FeatureSpace(13, 0, 26, 1 << 18, field_aware=True)
+    b = synth_batch(sp, 16 * 64, task=2, n_classes=3, seed=6)
+    W = torch.randn(3, sp.dim) * 0.01
+    st, dacc = torch.zeros(8), torch.zeros(3, sp.dim)
+    D.multiclass_round(W, b, 16, 64, 3, 1, 1.0, True, dacc, st)
+    bc = HashedBatch(b.num.to(torch.bfloat16).float(), b.cat, b.y, cat_span=b.cat_span)
+    stc, daccc = torch.zeros(8), torch.zeros(3, sp.dim)
+    D.multiclass_round(W, bc, 16, 64, 3, 1, 1.0, True, daccc, stc)
+    g = HashedBatch(b.num.to(torch.bfloat16), b.cat, b.y.to(torch.int8), cat_span=b.cat_span)
+    stg, daccg = torch.zeros(8, device=cuda), torch.zeros(3, sp.dim, device=cuda)
+    D.multiclass_round(W.to(cuda), g.to(cuda), 16, 64, 3, 1, 1.0, True, daccg, stg)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(stg.cpu()[[1, 3]].numpy(), stc[[1, 3]].numpy())
+    np.testing.assert_allclose(daccg.cpu().numpy(), daccc.numpy(), rtol=2e-3, atol=2e-4)
 
 
 @pytest.mark.gpu
@@ -259,3 +284,19 @@ def test_hip_hoeffding_tree(cuda):
     acc_c = (cpu.predict(b) == y).float().mean()
     assert int(gpu.nnodes.item()) > 1
     assert acc_g > 0.85 and acc_c > 0.85, (acc_g, acc_c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_multiclass_learner_shadow_tracks_prototypes(cuda, dtype):
+    """The key-major gather shadow follows W through apply and state loads."""
+    L = make_learner("MultiClassPA", {"nClasses": 3, "modelDtype": dtype}, SP, cuda)
+    for r in range(3):
+        L.fit(synth_batch(SP, 4096, start=r * 4096, task=2, n_classes=3).to(cuda),
+              RoundContext(spokes=64))
+    tol = 0 if dtype == "fp32" else 1e-2
+    torch.testing.assert_close(L.Wt[:, :3].float(), L.W.t(), rtol=tol, atol=tol * 1e-2)
+    assert float(L.Wt[:, 3:].abs().sum()) == 0.0
+    v = torch.randn_like(L.state_vector())
+    L.load_state_vector(v)
+    torch.testing.assert_close(L.Wt[:, :3].float(), L.W.t(), rtol=tol, atol=tol * 1e-2)
