@@ -8,8 +8,9 @@
 // Tree = flat arrays (feature, threshold, left, right per node; class counts per node;
 // per (node, feature, class) Gaussian moments n, Σx, Σx²; per (node, feature) range).
 // * ht_update_kernel — one thread per row: route to the leaf through the (L2-resident)
-//   node arrays, then scatter-add the row into that leaf's statistics with float atomics
-//   (range via the sign-split integer atomic min/max trick);
+//   node arrays; the wave aggregates its rows per (leaf, class) with ballots and DPP
+//   reductions, then one lane per pair adds them to the leaf's statistics (float
+//   atomics; range via the sign-split integer atomic min/max trick);
 // * ht_split_kernel  — one workgroup per node; leaves that saw ≥ gracePeriod points
 //   score nBins candidate thresholds per feature (class mass split by the Gaussian
 //   CDFs, information gain) in parallel, reduce best / second-best attribute, apply the
@@ -20,6 +21,7 @@
 namespace omldm {
 
 constexpr int kHtMaxC = 32;
+constexpr int kHtRegF = 8;  // features reduced per unrolled step of the wave aggregation
 
 __device__ __forceinline__ void atomic_min_f(float* a, float v) {
   if (v >= 0.f)
@@ -48,6 +50,15 @@ __device__ __forceinline__ int ht_route(const float* __restrict__ xr, const floa
   return node;
 }
 
+__device__ __forceinline__ float wave_min(float v) { return -wave_max(-v); }
+
+// One thread per row routes it to its leaf; the rows of a wavefront are then aggregated
+// per distinct (leaf, class) pair before touching global memory: the wave repeatedly
+// takes the first pending pair, ballots the lanes that share it, reduces their
+// per-feature Σ1 (popcount), Σx, Σx², min and max with DPP wave reductions, and one
+// lane issues the pair's atomics. Early in the stream every row of a wave lands in the
+// same one or few leaves, so this turns ~64·(5d+2) same-address atomics per wave into
+// (5d+2) per distinct pair (the previous per-row version serialised on them).
 __global__ __launch_bounds__(256) void ht_update_kernel(
     const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int C, int depth,
     const float* __restrict__ feat, const float* __restrict__ thr, const float* __restrict__ left,
@@ -55,27 +66,64 @@ __global__ __launch_bounds__(256) void ht_update_kernel(
     float* __restrict__ S1, float* __restrict__ S2, float* __restrict__ lo, float* __restrict__ hi,
     float* __restrict__ since, float* __restrict__ nfit) {
   const int row = blockIdx.x * 256 + threadIdx.x;
-  float one = 0.f;
+  const int lane = threadIdx.x & 63;
+  int key = -1, node = 0, yi = 0;
+  const float* xr = x;
   if (row < B && !__builtin_isnan(yv[row])) {
-    int yi = (int)yv[row];
+    yi = (int)yv[row];
     yi = yi < 0 ? 0 : (yi >= C ? C - 1 : yi);
-    const float* xr = x + (size_t)row * d;
-    const int node = ht_route(xr, feat, thr, left, right, depth);
-    atomicAdd(&cc[node * C + yi], 1.f);
-    for (int f = 0; f < d; ++f) {
-      const float v = xr[f];
-      const size_t b = ((size_t)node * d + f) * C + yi;
-      atomicAdd(&S0[b], 1.f);
-      atomicAdd(&S1[b], v);
-      atomicAdd(&S2[b], v * v);
-      atomic_min_f(&lo[node * d + f], v);
-      atomic_max_f(&hi[node * d + f], v);
-    }
-    atomicAdd(&since[node], 1.f);
-    one = 1.f;
+    xr = x + (size_t)row * d;
+    node = ht_route(xr, feat, thr, left, right, depth);
+    key = node * C + yi;
   }
-  const float n = wave_sum(one);
-  if ((threadIdx.x & 63) == 0 && n > 0.f && nfit) atomicAdd(nfit, n);
+  unsigned long long pending = __ballot(key >= 0);
+  const float n = (float)__popcll(pending);
+  if (lane == 0 && n > 0.f && nfit) atomicAdd(nfit, n);
+  while (pending) {  // wave-uniform
+    const int leader = __ffsll((long long)pending) - 1;
+    const int k = __shfl(key, leader);
+    const bool mine = key == k;
+    const unsigned long long grp = __ballot(mine);
+    pending &= ~grp;
+    const float cnt = (float)__popcll(grp);
+    const int nd = k / C, yc = k - nd * C;
+    if (lane == leader) {
+      atomicAdd(&cc[nd * C + yc], cnt);
+      atomicAdd(&since[nd], cnt);
+    }
+    for (int f0 = 0; f0 < d; f0 += kHtRegF) {
+      // features [f0, f0 + kHtRegF) of this lane's row, loaded once per chunk and pair
+#pragma unroll
+      for (int u = 0; u < kHtRegF; u += 2) {
+        const int fa = f0 + u, fb = f0 + u + 1;
+        const float va = (mine && fa < d) ? xr[fa] : 0.f;
+        const float vb = (mine && fb < d) ? xr[fb] : 0.f;
+        float s1a = va, s2a = va * va, s1b = vb, s2b = vb * vb;
+        wave_sum2(s1a, s1b);
+        wave_sum2(s2a, s2b);
+        const float mna = wave_min(mine ? va : INFINITY), mxa = wave_max(mine ? va : -INFINITY);
+        const float mnb = wave_min(mine ? vb : INFINITY), mxb = wave_max(mine ? vb : -INFINITY);
+        if (lane == leader) {
+          if (fa < d) {
+            const size_t b = ((size_t)nd * d + fa) * C + yc;
+            atomicAdd(&S0[b], cnt);
+            atomicAdd(&S1[b], s1a);
+            atomicAdd(&S2[b], s2a);
+            atomic_min_f(&lo[nd * d + fa], mna);
+            atomic_max_f(&hi[nd * d + fa], mxa);
+          }
+          if (fb < d) {
+            const size_t b = ((size_t)nd * d + fb) * C + yc;
+            atomicAdd(&S0[b], cnt);
+            atomicAdd(&S1[b], s1b);
+            atomicAdd(&S2[b], s2b);
+            atomic_min_f(&lo[nd * d + fb], mnb);
+            atomic_max_f(&hi[nd * d + fb], mxb);
+          }
+        }
+      }
+    }
+  }
 }
 
 __device__ __forceinline__ float entropy(const float* m, int C, float tot) {
