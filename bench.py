@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from omldm_amd.api.batch import FeatureSpace, HashedBatch  # noqa: E402
 from omldm_amd.io.synthetic import synth_batch  # noqa: E402
-from omldm_amd.models.linear import SVM  # noqa: E402
+from omldm_amd.models.linear import SVM, LogisticRegression  # noqa: E402
 from omldm_amd.parallel.comm import init_distributed  # noqa: E402
 from omldm_amd.parallel.protocols import Synchronous  # noqa: E402
 from omldm_amd.ops import native  # noqa: E402
@@ -86,6 +86,9 @@ def main(argv=None) -> int:
     ap.add_argument("--num-dtype", default="bf16", choices=["fp32", "bf16"])
     ap.add_argument("--wire", default="compact", choices=["wide", "compact"],
                     help="compact: field-aware uint16 categorical slots (half the PCIe bytes)")
+    ap.add_argument("--learner", default="SVM", choices=["SVM", "LogisticRegression"],
+                    help="SVM: the headline (PA-I); LogisticRegression: BASELINE config 2 "
+                         "(bf16 model, same stream and pipeline)")
     ap.add_argument("--label-dtype", default="int8", choices=["int8", "fp32"],
                     help="wire type of the ±1 labels (int8: 79 instead of 82 B per example)")
     ap.add_argument("--pool", type=int, default=12, help="pinned host batches per rank")
@@ -159,9 +162,12 @@ def main(argv=None) -> int:
         for d, p in zip(dev, pool):
             d.flat.copy_(p.flat)
 
-    learner = SVM({"variant": "PA-I", "C": 1.0, "modelDtype": a.model_dtype,
-                   "tableLog2": a.table_log2, "_ablate": a.ablate, "chunk": a.chunk}, space,
-                  device)
+    common = {"modelDtype": a.model_dtype, "tableLog2": a.table_log2, "_ablate": a.ablate,
+              "chunk": a.chunk}
+    if a.learner == "SVM":
+        learner = SVM({"variant": "PA-I", "C": 1.0, **common}, space, device)
+    else:
+        learner = LogisticRegression({"learningRate": 0.1, **common}, space, device)
     proto = Synchronous(comm, learner, {"virtualSpokes": S,
                                         **({"HubParallelism": a.hubs} if a.hubs else {})})
 
@@ -452,7 +458,9 @@ def main(argv=None) -> int:
     value = total_examples / elapsed
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "examples/s", "n_gpus": world,
+            "metric": METRIC if a.learner == "SVM" else
+                      "training examples/sec (whole node), online logistic regression bf16, "
+                      "1M-dim hashed features (BASELINE config 2)", "value": round(value, 1), "unit": "examples/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32-update/bf16-model" if a.model_dtype == "bf16" else "fp32",
@@ -460,7 +468,8 @@ def main(argv=None) -> int:
                     f"{sum(pool[0].sizes) // B} B/example on the wire: bf16 numerical, uint16 field-aware "
                     f"categorical slots, {a.label_dtype} labels)"
                     if a.ingest == "pinned" else "synthetic (HBM-resident replay)",
-            "config": {"model": f"linear SVM PA-I, 2^{a.dim_log2} hashed features "
+            "config": {"model": ("linear SVM PA-I" if a.learner == "SVM" else "logistic regression (SGD)")
+                                + f", 2^{a.dim_log2} hashed features "
                                 f"(13 num + 26 cat + bias)",
                        "global_batch": B * world, "seq_len": None,
                        "parallelism": f"dp{world}", "protocol": "Synchronous",
