@@ -126,6 +126,179 @@ __global__ __launch_bounds__(256) void ht_update_kernel(
   }
 }
 
+// ---- sort-based update (default): no atomics on the leaf statistics --------------------
+// Rows are counting-sorted by key = leaf·C + class, then blocks reduce contiguous chunks
+// of one key's rows and add each chunk's totals with one atomic per statistic. Four short
+// launches:
+//   1. route + per-block key histogram (LDS), keys[row] kept;
+//   2. scan: per-(block, key) bases in key-major order, segment starts/lengths;
+//   3. scatter row ids to their sorted positions (LDS cursors, no global atomics);
+//   4. per-chunk segment reduce (Σ1, Σx, Σx², min, max per feature).
+constexpr int kHtRowsPerBlock = 4096;  // rows per route/scatter block (1024 threads)
+constexpr int kHtSegChunk = 1024;      // rows per segment-reduce block (a key may span many)
+
+__global__ __launch_bounds__(1024) void ht_route_hist_kernel(
+    const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int C, int depth,
+    const float* __restrict__ feat, const float* __restrict__ thr, const float* __restrict__ left,
+    const float* __restrict__ right, int nbins, int* __restrict__ keys, int* __restrict__ hist,
+    float* __restrict__ nfit) {
+  extern __shared__ int h[];  // [nbins]
+  for (int b = threadIdx.x; b < nbins; b += 1024) h[b] = 0;
+  __syncthreads();
+  const int r0 = blockIdx.x * kHtRowsPerBlock;
+  float cnt = 0.f;
+  for (int r = r0 + threadIdx.x; r < r0 + kHtRowsPerBlock && r < B; r += 1024) {
+    int key = -1;
+    if (!__builtin_isnan(yv[r])) {
+      int yi = (int)yv[r];
+      yi = yi < 0 ? 0 : (yi >= C ? C - 1 : yi);
+      key = ht_route(x + (size_t)r * d, feat, thr, left, right, depth) * C + yi;
+      if (key >= nbins) key = -1;
+    }
+    keys[r] = key;
+    if (key >= 0) {
+      atomicAdd(&h[key], 1);
+      cnt += 1.f;
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += 1024) hist[(size_t)blockIdx.x * nbins + b] = h[b];
+  const float n = wave_sum(cnt);
+  if ((threadIdx.x & 63) == 0 && n > 0.f && nfit) atomicAdd(nfit, n);
+}
+
+// Inclusive block scan of one int per thread (1024 threads).
+__device__ __forceinline__ int block_scan_1024(int v, int* part) {
+  part[threadIdx.x] = v;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele
+    const int u = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += u;
+    __syncthreads();
+  }
+  const int r = part[threadIdx.x];
+  __syncthreads();
+  return r;
+}
+
+// One block of 1024 threads. hist[blk][bin] (counts) → bases; seg[bin] = (start, length);
+// cstart[bin] = first segment-reduce chunk of the bin, cstart[nbins] = chunk count.
+__global__ __launch_bounds__(1024) void ht_scan_kernel(int nblk, int nbins, int* __restrict__ hist,
+                                                       int2* __restrict__ seg,
+                                                       int* __restrict__ cstart) {
+  __shared__ int part[1024];
+  // per thread: a contiguous range of bins; bin totals, then a block scan of the ranges
+  const int per = (nbins + 1023) / 1024;
+  const int b0 = threadIdx.x * per, b1 = min(nbins, b0 + per);
+  int tot = 0, ch = 0;
+  for (int b = b0; b < b1; ++b) {
+    int run = 0;
+#pragma unroll 8
+    for (int k = 0; k < nblk; ++k) run += hist[(size_t)k * nbins + b];
+    seg[b] = make_int2(0, run);
+    tot += run;
+    ch += (run + kHtSegChunk - 1) / kHtSegChunk;
+  }
+  int start = block_scan_1024(tot, part) - tot;
+  int cs = block_scan_1024(ch, part) - ch;
+  for (int b = b0; b < b1; ++b) {
+    const int len = seg[b].y;
+    seg[b] = make_int2(start, len);
+    cstart[b] = cs;
+    cs += (len + kHtSegChunk - 1) / kHtSegChunk;
+    int run = start;
+    for (int k = 0; k < nblk; ++k) {
+      const size_t o = (size_t)k * nbins + b;
+      const int c = hist[o];
+      hist[o] = run;
+      run += c;
+    }
+    start += len;
+  }
+  if (threadIdx.x == 1023) cstart[nbins] = cs;
+}
+
+__global__ __launch_bounds__(1024) void ht_scatter_kernel(int B, int nbins,
+                                                          const int* __restrict__ keys,
+                                                          const int* __restrict__ hist,
+                                                          int* __restrict__ sorted) {
+  extern __shared__ int cur[];  // [nbins]
+  for (int b = threadIdx.x; b < nbins; b += 1024) cur[b] = hist[(size_t)blockIdx.x * nbins + b];
+  __syncthreads();
+  const int r0 = blockIdx.x * kHtRowsPerBlock;
+  for (int r = r0 + threadIdx.x; r < r0 + kHtRowsPerBlock && r < B; r += 1024) {
+    const int key = keys[r];
+    if (key >= 0) sorted[atomicAdd(&cur[key], 1)] = r;
+  }
+}
+
+// One block per chunk of ≤ kHtSegChunk rows of one key (leaf·C + class), found by a
+// binary search over the chunk starts; the chunk's per-feature totals are added to the
+// leaf statistics with one atomic each (a key with a single chunk — the common case once
+// the tree has grown — is the only writer of its statistics).
+__global__ __launch_bounds__(256) void ht_segment_kernel(
+    const float* __restrict__ x, int d, int C, int nbins, const int2* __restrict__ seg,
+    const int* __restrict__ cstart, const int* __restrict__ sorted, float* __restrict__ cc,
+    float* __restrict__ S0, float* __restrict__ S1, float* __restrict__ S2,
+    float* __restrict__ lo, float* __restrict__ hi, float* __restrict__ since) {
+  const int chunk = blockIdx.x;
+  if (chunk >= cstart[nbins]) return;
+  int a = 0, b = nbins - 1;  // last bin with cstart[bin] <= chunk (and a non-empty segment)
+  while (a < b) {
+    const int m = (a + b + 1) >> 1;
+    if (cstart[m] <= chunk) a = m;
+    else b = m - 1;
+  }
+  const int key = a;
+  const int2 sg = seg[key];
+  const int off = (chunk - cstart[key]) * kHtSegChunk;
+  const int len = min(kHtSegChunk, sg.y - off);
+  if (len <= 0) return;
+  __shared__ float red[4][4];
+  const int node = key / C, yc = key - node * C;
+  const float cnt = (float)len;
+  const int* rows = sorted + sg.x + off;
+  for (int f = 0; f < d; ++f) {
+    float s1 = 0.f, s2 = 0.f, mn = INFINITY, mx = -INFINITY;
+    for (int i = threadIdx.x; i < len; i += 256) {
+      const float v = x[(size_t)rows[i] * d + f];
+      s1 += v;
+      s2 = fmaf(v, v, s2);
+      mn = fminf(mn, v);
+      mx = fmaxf(mx, v);
+    }
+    wave_sum2(s1, s2);
+    mn = -wave_max(-mn);
+    mx = wave_max(mx);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      red[w][0] = s1;
+      red[w][1] = s2;
+      red[w][2] = mn;
+      red[w][3] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float t1 = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+      const float t2 = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+      const float tmn = fminf(fminf(red[0][2], red[1][2]), fminf(red[2][2], red[3][2]));
+      const float tmx = fmaxf(fmaxf(red[0][3], red[1][3]), fmaxf(red[2][3], red[3][3]));
+      const size_t o = ((size_t)node * d + f) * C + yc;
+      atomicAdd(&S0[o], cnt);
+      atomicAdd(&S1[o], t1);
+      atomicAdd(&S2[o], t2);
+      atomic_min_f(&lo[node * d + f], tmn);
+      atomic_max_f(&hi[node * d + f], tmx);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(&cc[key], cnt);
+    atomicAdd(&since[node], cnt);
+  }
+}
+
 __device__ __forceinline__ float entropy(const float* m, int C, float tot) {
   if (tot <= 1e-12f) return 0.f;
   float h = 0.f;
@@ -253,13 +426,46 @@ __global__ __launch_bounds__(256) void ht_predict_kernel(
 using namespace omldm;
 
 // tree: pointers in the order feat, thr, left, right, cc, S0, S1, S2, lo, hi, since, nnodes.
+// N: node capacity. ws: int scratch of omldm_ht_update_ws_ints(B, N, C) (0 → the wave-
+// aggregated atomic kernel, kept as the fallback / A-B reference).
+OMLDM_API long long omldm_ht_update_ws_ints(int B, int N, int C) {
+  const long long nblk = (B + kHtRowsPerBlock - 1) / kHtRowsPerBlock;
+  return 2LL * B + ((nblk * N * C + 1) & ~1LL) + 2LL * N * C + (N * C + 2);
+}
+
 OMLDM_API int omldm_ht_update(const float* x, const float* y, int B, int d, int C, int depth,
-                              float* const* tree, float* nfit, void* stream) {
+                              int N, float* const* tree, float* nfit, int* ws, void* stream) {
   if (B <= 0) return 0;
   if (C < 1 || C > kHtMaxC) return -1;
-  hipLaunchKernelGGL(ht_update_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     x, y, B, d, C, depth, tree[0], tree[1], tree[2], tree[3], tree[4], tree[5],
-                     tree[6], tree[7], tree[8], tree[9], tree[10], nfit);
+  hipStream_t st = (hipStream_t)stream;
+  if (!ws) {
+    hipLaunchKernelGGL(ht_update_kernel, dim3((B + 255) / 256), dim3(256), 0, st, x, y, B, d, C,
+                       depth, tree[0], tree[1], tree[2], tree[3], tree[4], tree[5], tree[6],
+                       tree[7], tree[8], tree[9], tree[10], nfit);
+    return (int)hipGetLastError();
+  }
+  const int nbins = N * C;
+  if ((size_t)nbins * 4 > 64 * 1024) return -2;
+  const int nblk = (B + kHtRowsPerBlock - 1) / kHtRowsPerBlock;
+  int* keys = ws;
+  int* sorted = ws + B;
+  int* hist = ws + 2 * (size_t)B;
+  int2* seg = reinterpret_cast<int2*>(hist + (((size_t)nblk * nbins + 1) & ~(size_t)1));
+  int* cstart = reinterpret_cast<int*>(seg + nbins);  // [nbins + 1]
+  const size_t lds = (size_t)nbins * 4;
+  int e = check_dyn_lds((const void*)ht_route_hist_kernel, lds);
+  if (!e) e = check_dyn_lds((const void*)ht_scatter_kernel, lds);
+  if (e) return e;
+  hipLaunchKernelGGL(ht_route_hist_kernel, dim3(nblk), dim3(1024), lds, st, x, y, B, d, C, depth,
+                     tree[0], tree[1], tree[2], tree[3], nbins, keys, hist, nfit);
+  hipLaunchKernelGGL(ht_scan_kernel, dim3(1), dim3(1024), 0, st, nblk, nbins, hist, seg, cstart);
+  hipLaunchKernelGGL(ht_scatter_kernel, dim3(nblk), dim3(1024), lds, st, B, nbins, keys, hist,
+                     sorted);
+  // chunk count ≤ nbins + B / kHtSegChunk; surplus blocks exit on cstart[nbins]
+  const int nchunk = nbins + (B + kHtSegChunk - 1) / kHtSegChunk;
+  hipLaunchKernelGGL(ht_segment_kernel, dim3(nchunk), dim3(256), 0, st, x, d, C, nbins, seg,
+                     cstart, sorted, tree[4], tree[5], tree[6], tree[7], tree[8], tree[9],
+                     tree[10]);
   return (int)hipGetLastError();
 }
 

@@ -394,7 +394,7 @@ class HT(Learner):
             # device path (csrc/kernels/hoeffding.hip): no host synchronisation per round
             if batch.B:
                 D.ht_update(batch.num, batch.y, self.Cn, self.depth, self._tree(),
-                            self.cum[1:2])
+                            self.cum[1:2], N=self.N)
                 D.ht_split(self.N, self.d, self.Cn, self.nb, float(self.grace), self.delta,
                            self.tau, self._tree())
             return

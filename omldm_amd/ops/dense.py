@@ -268,14 +268,28 @@ def _tree_ptrs(tree: list[torch.Tensor]):
     return (ctypes.c_void_p * len(tree))(*[t.data_ptr() for t in tree])
 
 
+_HT_WS: dict = {}
+
+
 def ht_update(x: torch.Tensor, y: torch.Tensor, C: int, depth: int, tree: list[torch.Tensor],
-              nfit: torch.Tensor) -> None:
-    """Route rows to leaves and scatter their Gaussian statistics (device only)."""
+              nfit: torch.Tensor, N: int = 0, sort: bool = True) -> None:
+    """Route rows to leaves and add their Gaussian statistics (device only).
+    sort (default, needs the node capacity N): rows counting-sorted by (leaf, class) and
+    one reducer block per pair — no atomics on the statistics; otherwise the
+    wave-aggregated atomic kernel."""
     B, d = x.shape
     x = x.float().contiguous()
     y = y.float().contiguous()
-    check(native.hip().omldm_ht_update(ptr(x), ptr(y), B, d, C, depth, _tree_ptrs(tree),
-                                       ptr(nfit), native.stream_of(x)), "omldm_ht_update")
+    ws = None
+    if sort and N > 0 and N * C * 4 <= 64 << 10:
+        n = int(native.hip().omldm_ht_update_ws_ints(B, N, C))
+        ws = _HT_WS.get(x.device)
+        if ws is None or ws.numel() < n:
+            ws = torch.empty(max(n, 1 << 16), dtype=torch.int32, device=x.device)
+            _HT_WS[x.device] = ws
+    check(native.hip().omldm_ht_update(ptr(x), ptr(y), B, d, C, depth, int(N), _tree_ptrs(tree),
+                                       ptr(nfit), ptr(ws), native.stream_of(x)),
+          "omldm_ht_update")
 
 
 def ht_split(N: int, d: int, C: int, nb: int, grace: float, delta: float, tau: float,

@@ -64,7 +64,8 @@ HIP_SIGS = [
     ("omldm_mlp_lds_bytes", i64, [i32, vp]),
     ("omldm_mlp_round", i32, [vp, vp, vp, i64, i32, i32, i32, vp, i32, i32, f32, vp, vp, vp]),
     ("omldm_mlp_forward", i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
-    ("omldm_ht_update", i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp]),
+    ("omldm_ht_update", i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+    ("omldm_ht_update_ws_ints", i64, [i32, i32, i32]),
     ("omldm_ht_split", i32, [i32, i32, i32, i32, f32, f32, f32, vp, vp]),
     ("omldm_ht_predict", i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
     ("omldm_drift_norms", i32, [vp, vp, i64, f32, vp, vp]),

@@ -287,6 +287,38 @@ def test_hip_hoeffding_tree(cuda):
 
 
 @pytest.mark.gpu
+def test_hip_hoeffding_sorted_update_matches_atomic(cuda):
+    """The counting-sort update (one reducer block per (leaf, class)) and the
+    wave-aggregated atomic update add the same statistics to a grown tree, with NaN
+    labels (forecast rows) skipped."""
+    from omldm_amd.api.batch import HashedBatch
+    from omldm_amd.ops import dense as D
+
+    hyper = {"nClasses": 3, "gracePeriod": 200}
+    L = make_learner("HT", hyper, SP, cuda)
+    for s in range(1, 30):
+        x, y = _ht_data(400, seed=s)
+        L.fit(HashedBatch(x, torch.zeros((400, 0), dtype=torch.int32), y).to(cuda),
+              RoundContext())
+    assert int(L.nnodes.item()) > 1
+    x, y = _ht_data(5000, seed=77)
+    y[::7] = float("nan")
+    xs, ys = x.to(cuda), y.to(cuda)
+    base = [t.clone() for t in L._tree()]
+    outs = []
+    for sort in (True, False):
+        tree = [t.clone() for t in base]
+        nfit = torch.zeros(1, device=cuda)
+        D.ht_update(xs, ys, 3, L.depth, tree, nfit, N=L.N, sort=sort)
+        torch.cuda.synchronize()
+        outs.append((tree, float(nfit)))
+    (ts, ns), (ta, na) = outs
+    assert ns == na == float((~torch.isnan(y)).sum())
+    for a, b in zip(ts, ta):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_multiclass_learner_shadow_tracks_prototypes(cuda, dtype):
     """The key-major gather shadow follows W through apply and state loads."""
