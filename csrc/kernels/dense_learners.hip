@@ -118,9 +118,52 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
   }
 }
 
+// Count-weighted centroid move of one micro-batch, fused with the bookkeeping the learner
+// used to do in ~12 small elementwise launches:
+//   tot = n + cnt; c ← (n·c + Σx)/tot where tot > 0; n ← tot; Σx, cnt ← 0;
+//   cum[0] += inertia, cum[1] += Σ cnt (training rows); inertia ← 0.
+__global__ __launch_bounds__(256) void kmeans_apply_kernel(float* __restrict__ cent,
+                                                           float* __restrict__ n, int k, int d,
+                                                           float* __restrict__ sums,
+                                                           float* __restrict__ counts,
+                                                           float* __restrict__ inertia,
+                                                           float* __restrict__ cum) {
+  for (int i = threadIdx.x; i < k * d; i += 256) {
+    const int j = i / d;
+    const float nj = n[j], tot = nj + counts[j];
+    if (tot > 0.f) cent[i] = (cent[i] * nj + sums[i]) / tot;
+    sums[i] = 0.f;
+  }
+  __syncthreads();  // every centroid read n and counts before they change
+  float fitted = 0.f;
+  for (int j = threadIdx.x; j < k; j += 256) {
+    fitted += counts[j];
+    n[j] += counts[j];
+    counts[j] = 0.f;
+  }
+  fitted = wave_sum(fitted);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = fitted;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (cum) {
+      cum[0] += *inertia;
+      cum[1] += (part[0] + part[1]) + (part[2] + part[3]);
+    }
+    *inertia = 0.f;
+  }
+}
+
 }  // namespace omldm
 
 using namespace omldm;
+
+OMLDM_API int omldm_kmeans_apply(float* cent, float* n, int k, int d, float* sums, float* counts,
+                                 float* inertia, float* cum, void* stream) {
+  hipLaunchKernelGGL(kmeans_apply_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, cent, n, k,
+                     d, sums, counts, inertia, cum);
+  return (int)hipGetLastError();
+}
 
 // G[ld×ld] += [X 1 y]ᵀ[X 1 y] over rows with finite y (ld ≥ d + 2).
 OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, float* G, int ld,

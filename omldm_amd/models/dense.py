@@ -120,13 +120,17 @@ class KMeans(Learner):
         if batch.B == 0:
             return
         x = batch.num.float()
-        train = ~torch.isnan(batch.y)
         if self._seeded < self.k:  # seed centroids with the first k training points
+            train = ~torch.isnan(batch.y)
             rows = x[train][: self.k - self._seeded]
             m = rows.shape[0]
             self.C[self._seeded:self._seeded + m] = rows
             self.n[self._seeded:self._seeded + m] = 1.0
             self._seeded += m
+        if self.device.type == "cuda":  # Σx/cnt are left at zero by the previous apply
+            D.kmeans_assign(x, batch.y, self.C, self._sums, self._cnt, self._inert)
+            D.kmeans_apply(self.C, self.n, self._sums, self._cnt, self._inert, self.cum)
+            return
         self._sums.zero_()
         self._cnt.zero_()
         D.kmeans_assign(x, batch.y, self.C, self._sums, self._cnt, self._inert)
@@ -135,7 +139,7 @@ class KMeans(Learner):
         newc = (self.C * self.n.unsqueeze(1) + self._sums) / torch.clamp(tot, min=1).unsqueeze(1)
         self.C.copy_(torch.where(upd.unsqueeze(1), newc, self.C))
         self.n.copy_(tot)
-        self.cum[1] += train.sum()
+        self.cum[1] += (~torch.isnan(batch.y)).sum()
         self.cum[0] += self._inert[0]
         self._inert.zero_()
 

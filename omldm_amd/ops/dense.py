@@ -121,6 +121,16 @@ def multiclass_round(W: torch.Tensor, batch: HashedBatch, R: int, S: int, nclass
             ptr(dacc), ptr(stats))
 
 
+def kmeans_apply(cent: torch.Tensor, n: torch.Tensor, sums: torch.Tensor, counts: torch.Tensor,
+                 inertia: torch.Tensor, cum: torch.Tensor | None) -> None:
+    """GPU: one launch — c ← (n·c + Σx)/(n + cnt) where n + cnt > 0, n += cnt, Σx = cnt = 0,
+    cum[0] += inertia, cum[1] += Σcnt, inertia = 0."""
+    k, d = cent.shape
+    check(native.hip().omldm_kmeans_apply(ptr(cent), ptr(n), k, d, ptr(sums), ptr(counts),
+                                          ptr(inertia), ptr(cum), native.stream_of(cent)),
+          "omldm_kmeans_apply")
+
+
 MLP_MB = 32          # mini-batch rows of the fused MLP kernel
 MLP_MAX_LAYERS = 4
 

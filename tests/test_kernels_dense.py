@@ -332,3 +332,23 @@ def test_multiclass_learner_shadow_tracks_prototypes(cuda, dtype):
     v = torch.randn_like(L.state_vector())
     L.load_state_vector(v)
     torch.testing.assert_close(L.Wt[:, :3].float(), L.W.t(), rtol=tol, atol=tol * 1e-2)
+
+
+@pytest.mark.gpu
+def test_kmeans_learner_gpu_matches_cpu(cuda):
+    """Fused GPU centroid apply == the CPU learner's torch update (same seeding)."""
+    from omldm_amd.api.batch import HashedBatch
+
+    cpu = make_learner("K-means", {"k": 5}, SP, "cpu")
+    gpu = make_learner("K-means", {"k": 5}, SP, cuda)
+    for r in range(4):
+        torch.manual_seed(r)
+        x = torch.randn(3000, 13) + (r % 2)
+        y = torch.zeros(3000)
+        y[::9] = float("nan")  # forecast rows are not trained on
+        b = HashedBatch(x, torch.zeros((3000, 0), dtype=torch.int32), y)
+        cpu.fit(b, RoundContext())
+        gpu.fit(b.to(cuda), RoundContext())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(gpu.state.cpu(), cpu.state, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gpu.cum.cpu()[:2], cpu.cum[:2], rtol=1e-4, atol=1e-2)
