@@ -135,7 +135,8 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
                                                         const float* __restrict__ x,
                                                         const float* __restrict__ yv, long long B,
                                                         int R, float lr, float* __restrict__ dacc,
-                                                        float* __restrict__ stats, MlpDesc g) {
+                                                        float* __restrict__ stats, MlpDesc g,
+                                                        float* __restrict__ ws, int nparams) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const long long r0 = (long long)blockIdx.x * R;
@@ -234,18 +235,23 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       gnext = tmp;
     }
   }
-  // ---- round end: Δ = W_spoke − W_0 into the accumulator
+  // ---- round end: Δ = W_spoke − W_0. With a workspace: the spoke's own row, plain
+  // coalesced stores (mlp_colsum_kernel sums the rows); without: atomics into the
+  // accumulator (every spoke hits the same nparams addresses — the slow fallback).
+  float* wrow = ws ? ws + (size_t)blockIdx.x * nparams : nullptr;
   for (int l = 0; l < L; ++l) {
     const int nin = g.n[l], nout = g.n[l + 1], ld = g.ldw[l];
     const float* W = sm + g.lw[l];
     for (int i = tid; i < nout * nin; i += blockDim.x) {
       const int o = i / nin, c = i - o * nin;
       const float d = W[o * ld + c] - w[g.woff[l] + i];
-      if (d != 0.f) atomicAdd(&dacc[g.woff[l] + i], d);
+      if (wrow) wrow[g.woff[l] + i] = d;
+      else if (d != 0.f) atomicAdd(&dacc[g.woff[l] + i], d);
     }
     for (int o = tid; o < nout; o += blockDim.x) {
       const float d = sm[g.lb[l] + o] - w[g.boff[l] + o];
-      if (d != 0.f) atomicAdd(&dacc[g.boff[l] + o], d);
+      if (wrow) wrow[g.boff[l] + o] = d;
+      else if (d != 0.f) atomicAdd(&dacc[g.boff[l] + o], d);
     }
   }
   if (wave == 0) {
@@ -326,6 +332,27 @@ static int make_desc(int L, const int* widths, int task, int act, MlpDesc* g) {
   return 0;
 }
 
+// dacc[c] += Σ_{s in this block's 64-spoke slab} ws[s][c]: one atomic per (column, slab)
+// instead of one per (column, spoke).
+constexpr int kMlpSlab = 64;
+__global__ __launch_bounds__(256) void mlp_colsum_kernel(const float* __restrict__ ws, int S,
+                                                         int n, float* __restrict__ dacc) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n) return;
+  const int s0 = blockIdx.y * kMlpSlab, s1 = min(S, s0 + kMlpSlab);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = s0;
+  for (; s + 3 < s1; s += 4) {
+    a0 += ws[(size_t)s * n + c];
+    a1 += ws[(size_t)(s + 1) * n + c];
+    a2 += ws[(size_t)(s + 2) * n + c];
+    a3 += ws[(size_t)(s + 3) * n + c];
+  }
+  for (; s < s1; ++s) a0 += ws[(size_t)s * n + c];
+  const float t = (a0 + a1) + (a2 + a3);
+  if (t != 0.f) atomicAdd(&dacc[c], t);
+}
+
 }  // namespace omldm
 
 using namespace omldm;
@@ -340,9 +367,10 @@ OMLDM_API long long omldm_mlp_lds_bytes(int L, const int* widths) {
 // One protocol round: S spokes × R rows (spoke s owns rows [sR, sR+R)); task 0 regression,
 // 1 binary logistic, 2 softmax. dacc[nparams] += Σ_s Δ_s; stats[0..3] += loss, n, correct,
 // active spokes. Follow with omldm_multiclass_apply(w, dacc, nparams, stats+3).
+// ws: optional S × nparams scratch (spoke deltas by plain stores + slab column sums).
 OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, long long B, int R,
                               int S, int L, const int* widths, int task, int act, float lr,
-                              float* dacc, float* stats, void* stream) {
+                              float* dacc, float* stats, float* ws, void* stream) {
   if (B <= 0 || S <= 0) return 0;
   if (R <= 0 || (long long)R * S < B) return -3;
   MlpDesc g;
@@ -351,8 +379,12 @@ OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, lo
   if (lds > 160 * 1024) return -2;
   int e = check_dyn_lds((const void*)mlp_round_kernel, lds);
   if (e) return e;
+  const int nparams = g.boff[g.L - 1] + g.n[g.L];
   hipLaunchKernelGGL(mlp_round_kernel, dim3(S), dim3(256), lds, (hipStream_t)stream, w, x, y, B,
-                     R, lr, dacc, stats, g);
+                     R, lr, dacc, stats, g, ws, nparams);
+  if (ws)
+    hipLaunchKernelGGL(mlp_colsum_kernel, dim3((nparams + 255) / 256, (S + kMlpSlab - 1) / kMlpSlab),
+                       dim3(256), 0, (hipStream_t)stream, ws, S, nparams, dacc);
   return (int)hipGetLastError();
 }
 

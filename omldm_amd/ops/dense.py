@@ -234,9 +234,14 @@ def mlp_round(w: torch.Tensor, x: torch.Tensor, y: torch.Tensor, R: int, S: int,
     if len(widths) - 1 > MLP_MAX_LAYERS:
         raise ValueError(f"NN: at most {MLP_MAX_LAYERS} layers on the fused kernel")
     if x.is_cuda:
+        from omldm_amd.ops.linear import _workspace
+
+        # spoke deltas as plain rows + slab column sums (no per-spoke same-address atomics)
+        ws = _workspace(x.device, S * w.numel(), key="mlp_ws")
         check(native.hip().omldm_mlp_round(ptr(w), ptr(x), ptr(y), B, R, S, len(widths) - 1,
                                            _widths_arr(widths), task, act, lr, ptr(dacc),
-                                           ptr(stats), native.stream_of(x)), "omldm_mlp_round")
+                                           ptr(stats), ptr(ws), native.stream_of(x)),
+              "omldm_mlp_round")
     else:
         mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats, act)
 
