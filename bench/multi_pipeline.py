@@ -40,8 +40,10 @@ def main(argv=None) -> int:
     ap.add_argument("--pipelines", type=int, default=16)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--spokes", type=int, default=4096)
-    ap.add_argument("--rows", type=int, default=32)
+    # same spoke geometry as the headline bench (profiles/round1_ablation.md "Multi-pipeline")
+    ap.add_argument("--spokes", type=int, default=8192)
+    ap.add_argument("--rows", type=int, default=16)
+    ap.add_argument("--table-log2", type=int, default=10)
     ap.add_argument("--dim-log2", type=int, default=20)
     ap.add_argument("--ring", type=int, default=4)
     ap.add_argument("--latency-samples", type=int, default=1000)
@@ -65,7 +67,7 @@ def main(argv=None) -> int:
     protos = []
     for i in range(M):
         L = SVM({"variant": "PA-I", "C": 0.25 * (1 + i % 8), "modelDtype": "bf16",
-                 "tableLog2": 11}, space, device)
+                 "tableLog2": a.table_log2}, space, device)
         store.add(L)
         protos.append(Synchronous(comm, L, {"virtualSpokes": S}))
 
