@@ -38,6 +38,8 @@ def main(argv=None) -> int:
     ap.add_argument("--warmup-ticks", type=int, default=4)
     ap.add_argument("--ingest-cus", type=int, default=None,
                     help="engine ingestCUs (XCD-local ingest copies; 0 = plain streams)")
+    ap.add_argument("--ingest-copy", default=None, choices=["pull", "sdma"],
+                    help="engine ingestCopy (staging copy: pull kernel or SDMA)")
     ap.add_argument("--forecast-frac", type=float, default=0.0,
                     help="share of the records sent to forecastingData (→ predictions)")
     ap.add_argument("--unique", type=int, default=100_000,
@@ -80,7 +82,9 @@ def main(argv=None) -> int:
                                           "--spokesPerDevice", "4096",
                                           "--parseThreads", str(a.threads), "--jobName", "e2e"]
                                   + (["--ingestCUs", str(a.ingest_cus)]
-                                     if a.ingest_cus is not None else []))
+                                     if a.ingest_cus is not None else [])
+                                  + (["--ingestCopy", a.ingest_copy]
+                                     if a.ingest_copy is not None else []))
         job = Job(cfg, comm, device)
         while not job.pipes:  # pipeline creation (and first-touch setup) is not timed
             job.tick()

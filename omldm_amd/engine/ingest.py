@@ -74,7 +74,8 @@ class TickBlock:
 class TickIngest:
     def __init__(self, consumers: list, batch_size: int, pinned: bool, prefetch: bool = True,
                  depth: int = 2, bytes_per_record: int = 1024, device=None,
-                 copy_blocks: int = 128, space=None, copy_stream=None, parse_stream=None):
+                 copy_blocks: int = 128, space=None, copy_stream=None, parse_stream=None,
+                 copy_method: str = "pull"):
         self.consumers = consumers
         self.space = space  # set: the ingest thread also parses each block on the GPU
         # GPU ranks: the ingest thread also moves each block to HBM on its own copy
@@ -82,6 +83,10 @@ class TickIngest:
         self.device = torch.device(device) if device is not None else None
         self.stage = self.device is not None and self.device.type == "cuda" and pinned
         self.copy_blocks = copy_blocks
+        # pull: the GPU reads the pinned slot (csrc/kernels/ingest.hip); sdma: a
+        # hipMemcpyAsync on the copy stream (copy engine; enqueue stalls only hit this thread)
+        assert copy_method in ("pull", "sdma"), copy_method
+        self.copy_method = copy_method
         self._copy_stream = (copy_stream or torch.cuda.Stream(self.device)) if self.stage else None
         self._parse_stream = parse_stream  # None: the parse follows the copy on its stream
         self.batch = max(1, int(batch_size))
@@ -182,8 +187,13 @@ class TickIngest:
             if blk.consumed is not None:
                 cs.wait_event(blk.consumed)  # the parser of this slot's last use is done
                 blk.consumed = None
-            pull_copy(blk.d_raw, blk.data[:nbytes], self.copy_blocks, cs.cuda_stream)
-            pull_copy(blk.d_offs, blk.offs_t[:n + 1], self.copy_blocks, cs.cuda_stream)
+            if self.copy_method == "sdma":
+                with torch.cuda.stream(cs):
+                    blk.d_raw[:nbytes].copy_(blk.data[:nbytes], non_blocking=True)
+                    blk.d_offs[:n + 1].copy_(blk.offs_t[:n + 1], non_blocking=True)
+            else:
+                pull_copy(blk.d_raw, blk.data[:nbytes], self.copy_blocks, cs.cuda_stream)
+                pull_copy(blk.d_offs, blk.offs_t[:n + 1], self.copy_blocks, cs.cuda_stream)
             blk.parsed = None
             if self.space is not None:
                 ps = cs

@@ -100,6 +100,7 @@ class Job:
                                  device=self.device if cfg.gpuParse else None,
                                  space=self.space if cfg.gpuParse else None,
                                  copy_blocks=16 if self.lanes else 128,
+                                 copy_method=str(cfg.ingestCopy).lower(),
                                  copy_stream=self.lanes.copy if self.lanes else None,
                                  parse_stream=self.lanes.aux if self.lanes else None)
         self._committed = None  # consumer offsets after the last processed block

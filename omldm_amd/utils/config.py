@@ -69,6 +69,7 @@ class JobConfig:
     gpuParse: bool = True                 # parse + hash JSON records on the GPU (cuda only)
     prefetch: str = "auto"                # read tick k+1 while tick k trains (auto: on GPU)
     ingestCUs: int = 0                    # GPU: CUs (one XCD block) for ingest copies; 0 off (e2e A/B: no gain, host-bound)
+    ingestCopy: str = "pull"              # GPU staging copy: pull (kernel) | sdma (hipMemcpyAsync)
     extra: dict = field(default_factory=dict)
 
     @staticmethod
