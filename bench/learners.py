@@ -33,6 +33,7 @@ CASES = [
     ("ORR", 1, {}, 1),
     ("K-means", 0, {"k": 16}, 1),
     ("NN", 0, {"hiddenLayers": [64, 64]}, 2048),
+    ("NN@bf16", 0, {"hiddenLayers": [64, 64], "matmulDtype": "bf16"}, 2048),
     ("HT", 2, {"nClasses": 4}, 1),
 ]
 
@@ -52,7 +53,7 @@ def main(argv=None) -> int:
         ring = []
         for k in range(3):
             b = synth_batch(space, a.batch, start=k * a.batch, seed=25, task=task, n_classes=4)
-            if name in ("NN",):
+            if name.split("@")[0] in ("NN",):
                 b = HashedBatch(b.num, b.cat, torch.where(b.y > 0, 1.0, -1.0))
             ring.append(b.to(dev))
         L = make_learner(name.split("@")[0], hyper, space, dev)

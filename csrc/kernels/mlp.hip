@@ -34,6 +34,7 @@ enum MlpAct : int { kRelu = 0, kTanh = 1, kSigmoid = 2, kIdentity = 3 };
 
 struct MlpDesc {
   int L, task, K, act;  // act: hidden-layer activation (MlpAct)
+  int bf16;             // 1: GEMM operands rounded to bf16 (v_mfma_f32_32x32x16_bf16)
   int n[kMaxLayers + 1], np[kMaxLayers + 1];
   int woff[kMaxLayers], boff[kMaxLayers];
   int lw[kMaxLayers], lb[kMaxLayers], ldw[kMaxLayers];
@@ -44,8 +45,8 @@ struct MlpDesc {
 // C[32×32] = A[32×K]·B[K×32] with A(i,k) = a[i·ars + k·acs], B(k,j) = b[k·brs + j·bcs].
 // Operand map (v_mfma_f32_32x32x2_f32): lane supplies A(lane&31, k + lane>>5) and
 // B(k + lane>>5, lane&31); result reg q of lane is C(row(q, lane), lane&31).
-__device__ __forceinline__ f32x16 wave_gemm32(const float* a, int ars, int acs, const float* b,
-                                              int brs, int bcs, int K) {
+__device__ __forceinline__ f32x16 wave_gemm32_f32(const float* a, int ars, int acs,
+                                                  const float* b, int brs, int bcs, int K) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, kh = lane >> 5;
   f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -55,6 +56,40 @@ __device__ __forceinline__ f32x16 wave_gemm32(const float* a, int ars, int acs, 
     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[k * acs], bp[k * brs], acc, 0, 0, 0);
   }
   return acc;
+}
+
+// Mixed precision: the same product with operands rounded to bf16 (RNE) as they leave
+// LDS and fp32 accumulation, on v_mfma_f32_32x32x16_bf16 — K/16 instructions instead
+// of K/2. Operand map: lane l (r = l&31, h = l>>5) supplies A(r, k + 8h + j) and
+// B(k + 8h + j, r), j = 0..7; the C layout is the fp32 form's. K % 16 == 0 (widths are
+// padded to 32, mini-batches are 32 rows).
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ short bf16_bits(float v) {
+  return __builtin_bit_cast(short, __float2bfloat16(v));
+}
+__device__ __forceinline__ f32x16 wave_gemm32_bf16(const float* a, int ars, int acs,
+                                                   const float* b, int brs, int bcs, int K) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, kh = lane >> 5;
+  f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float* ap = a + r * ars + 8 * kh * acs;
+  const float* bp = b + 8 * kh * brs + r * bcs;
+  for (int k = 0; k < K; k += 16) {
+    bf16x8 af, bfr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      af[j] = bf16_bits(ap[(k + j) * acs]);
+      bfr[j] = bf16_bits(bp[(k + j) * brs]);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ f32x16 wave_gemm32(const float* a, int ars, int acs, const float* b,
+                                              int brs, int bcs, int K, int bf16) {
+  return bf16 ? wave_gemm32_bf16(a, ars, acs, b, brs, bcs, K)
+              : wave_gemm32_f32(a, ars, acs, b, brs, bcs, K);
 }
 
 // Activation and its derivative expressed through the activation's OUTPUT h (what the
@@ -105,7 +140,8 @@ __device__ void forward(float* sm, const MlpDesc& g) {
     const int nt = g.np[l + 1] >> 5, ldo = g.ldh[l + 1];
     const bool hidden = l + 1 < g.L;
     for (int t = wave; t < nt; t += 4) {
-      const f32x16 acc = wave_gemm32(H, g.ldh[l], 1, W + t * 32 * g.ldw[l], 1, g.ldw[l], g.np[l]);
+      const f32x16 acc =
+          wave_gemm32(H, g.ldh[l], 1, W + t * 32 * g.ldw[l], 1, g.ldw[l], g.np[l], g.bf16);
       const int col = t * 32 + (lane & 31);
       const float bias = bs[col];
       const bool pad = col >= g.n[l + 1];  // padding columns stay exactly zero
@@ -203,7 +239,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       if (l > 0) {  // dH_l = (dZ · W_l) ⊙ act'(H_l)
         float* Gn = sm + gnext;
         for (int t = wave; t < (nin >> 5); t += 4) {
-          const f32x16 acc = wave_gemm32(Gc, g.ldg, 1, W + t * 32, ldw, 1, nout);
+          const f32x16 acc = wave_gemm32(Gc, g.ldg, 1, W + t * 32, ldw, 1, nout, g.bf16);
           const int col = t * 32 + (lane & 31);
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
@@ -216,7 +252,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       const int ntc = nin >> 5, nto = nout >> 5;
       for (int t = wave; t < nto * ntc; t += 4) {
         const int to = t / ntc, tc = t - to * ntc;
-        const f32x16 acc = wave_gemm32(Gc + to * 32, 1, g.ldg, H + tc * 32, ldh, 1, kMB);
+        const f32x16 acc = wave_gemm32(Gc + to * 32, 1, g.ldg, H + tc * 32, ldh, 1, kMB, g.bf16);
         const int c = tc * 32 + (lane & 31);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -289,11 +325,12 @@ __global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restric
 }
 
 static int make_desc(int L, const int* widths, int task, int act, MlpDesc* g) {
-  if (L < 1 || L > kMaxLayers || act < 0 || act > kIdentity) return -1;
+  if (L < 1 || L > kMaxLayers || (act & 0xff) > kIdentity || (act & ~0x1ff)) return -1;
   *g = MlpDesc{};
   g->L = L;
   g->task = task;
-  g->act = act;
+  g->act = act & 0xff;        // low byte: hidden activation
+  g->bf16 = (act >> 8) & 1;   // bit 8: bf16 GEMM operands
   g->K = widths[L];
   int off = 0;
   for (int l = 0; l <= L; ++l) {

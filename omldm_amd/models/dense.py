@@ -264,6 +264,11 @@ class NN(Learner):
         if act not in D.MLP_ACTS:
             raise ValueError(f"NN activation must be one of {sorted(D.MLP_ACTS)}")
         self.act_name, self.act = act, D.MLP_ACTS[act]
+        # matmulDtype bf16: GEMM operands rounded to bf16 on the matrix cores (fp32
+        # accumulation, fp32 master weights and activations in LDS) — K/16 MFMAs per tile
+        # instead of K/2; default fp32 keeps DL4J's fp32 arithmetic
+        if str(h.get("matmulDtype", "fp32")).lower() in ("bf16", "bfloat16"):
+            self.act |= D.MLP_BF16
         self.widths = [self.d] + [int(v) for v in hidden] + [max(1, self.K)]
         if len(self.widths) - 1 > D.MLP_MAX_LAYERS:
             raise ValueError(f"NN supports at most {D.MLP_MAX_LAYERS} layers")

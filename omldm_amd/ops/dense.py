@@ -154,7 +154,18 @@ def _mlp_unflatten(w: torch.Tensor, widths):
 
 
 MLP_ACTS = {"relu": 0, "tanh": 1, "sigmoid": 2, "identity": 3}
-_ACT_FN = {0: torch.relu, 1: torch.tanh, 2: torch.sigmoid, 3: lambda t: t}
+MLP_BF16 = 0x100  # flag OR-ed into `act`: bf16 GEMM operands (v_mfma_f32_32x32x16_bf16)
+_ACT_FN_BASE = {0: torch.relu, 1: torch.tanh, 2: torch.sigmoid, 3: lambda t: t}
+
+
+class _ActFns(dict):
+    """Activation lookup that ignores the precision flag (the CPU mirror is fp32)."""
+
+    def __getitem__(self, k):
+        return super().__getitem__(k & 0xFF)
+
+
+_ACT_FN = _ActFns(_ACT_FN_BASE)
 
 
 def mlp_forward_reference(w: torch.Tensor, x: torch.Tensor, widths, act: int = 0

@@ -251,6 +251,35 @@ def test_hip_mlp_round_vs_reference(cuda, widths, task, act):
                                rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("widths,task,act", [([13, 32, 32, 1], 1, 0), ([40, 64, 48, 5], 2, 1),
+                                             ([13, 64, 64, 1], 0, 0)])
+def test_hip_mlp_bf16_matmul_vs_fp32_reference(cuda, widths, task, act):
+    """matmulDtype bf16 (v_mfma_f32_32x32x16_bf16 operands, fp32 accumulate) tracks the
+    fp32 reference to bf16 rounding; forward output likewise; an exact-integer product
+    checks the operand map."""
+    B, R, S = 1000, 96, 11
+    w, x, y = _mlp_case(widths, task, B, seed=len(widths) + task)
+    lr = 0.05
+    d_ref, s_ref = torch.zeros_like(w), torch.zeros(8)
+    D.mlp_round_reference(w, x, y, R, S, widths, task, lr, d_ref, s_ref, act)
+    wd, d_gpu, s_gpu = w.to(cuda), torch.zeros_like(w, device=cuda), torch.zeros(8, device=cuda)
+    D.mlp_round(wd, x.to(cuda), y.to(cuda), R, S, widths, task, lr, d_gpu, s_gpu,
+                act | D.MLP_BF16)
+    torch.cuda.synchronize()
+    scale = float(d_ref.abs().max())
+    torch.testing.assert_close(d_gpu.cpu(), d_ref, rtol=5e-2, atol=2e-2 * scale)
+    out = D.mlp_forward(wd, x.to(cuda), widths, act | D.MLP_BF16).cpu()
+    ref = D.mlp_forward_reference(w, x, widths, act)
+    torch.testing.assert_close(out, ref, rtol=3e-2, atol=3e-2 * float(ref.abs().max()))
+    # integer-valued operands are exact in bf16: identity activation, one layer
+    wi = torch.randint(-3, 4, (13 * 32 + 32 + 32 * 1 + 1,)).float()
+    xi = torch.randint(-3, 4, (64, 13)).float()
+    o32 = D.mlp_forward(wi.to(cuda), xi.to(cuda), [13, 32, 1], 3).cpu()
+    o16 = D.mlp_forward(wi.to(cuda), xi.to(cuda), [13, 32, 1], 3 | D.MLP_BF16).cpu()
+    assert torch.equal(o32, o16)
+
+
 def _ht_data(n, seed=0):
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, 13, generator=g)
