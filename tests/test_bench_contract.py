@@ -62,3 +62,17 @@ def test_bench_two_ranks_contract():
     assert r["config"]["global_batch"] == 2 * 32 * 8
     assert r["reduce_parts"] in (1, 2, 4)
     assert set(r["lane_tune_ms_per_step"]) == {"plain/parts1", "plain/parts2", "plain/parts4"}
+
+
+def test_bench_eight_ranks_rehearsal():
+    """The driver's N=8 scaling run, rehearsed on gloo: 8 ranks under torch.distributed.run
+    agree on one tuned reduce-slice choice (MAX over ranks) and rank 0 alone prints the
+    whole-job line."""
+    recs = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                 "--nproc-per-node", "8", "--master-addr", "127.0.0.1", "--master-port",
+                 str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "8", *SMALL])
+    assert len(recs) == 1
+    r = recs[0]
+    assert r["n_gpus"] == 8 and r["config"]["parallelism"] == "dp8"
+    assert r["config"]["global_batch"] == 8 * 32 * 8
+    assert r["value"] > 0 and r["reduce_parts"] in (1, 2, 4)

@@ -185,3 +185,23 @@ def test_coalesced_buckets_world2():
         res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(2)]
     assert all(r["ok"] for r in res)
     assert res[0]["collectives"] > 3  # the 64-byte cap produced many buckets
+
+
+def test_synchronous_world8_pipelined_and_sharded():
+    """8 ranks (the size of one MI355X node): all-reduce, pipelined key-range slices and
+    4 sharded hubs give the same replicas."""
+    base = run(8, "SVM", "Synchronous", {}, rounds=2, B=128)
+    piped = run(8, "SVM", "Synchronous", {"reduceParts": 4}, rounds=2, B=128)
+    sharded = run(8, "SVM", "Synchronous", {"HubParallelism": 4}, rounds=2, B=128)
+    for res in (base, piped, sharded):
+        for r in res[1:]:
+            assert same(r["final"], res[0]["final"])
+    assert same(piped[0]["final"], base[0]["final"], 1e-6)
+    assert same(sharded[0]["final"], base[0]["final"], 1e-5)
+
+
+def test_ssp_world8_replicas_agree():
+    res = run(8, "PA", "SSP", {"staleness": 2}, rounds=4, B=128)
+    for r in res[1:]:
+        assert same(r["final"], res[0]["final"])
+        assert same(r["_E"], res[0]["_E"])
