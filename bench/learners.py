@@ -43,11 +43,15 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=131072)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--cases", default="",
+                    help='JSON list of [name, task, hyper, spokes] replacing the default cases '
+                         '(geometry sweeps)')
     a = ap.parse_args(argv)
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     space = FeatureSpace(13, 0, 26, 1 << 20)
     res = {}
-    for name, task, hyper, spokes in CASES:
+    cases = [tuple(c) for c in json.loads(a.cases)] if a.cases else CASES
+    for name, task, hyper, spokes in cases:
         if a.only and name.split("@")[0] not in a.only.split(","):
             continue
         ring = []
@@ -58,8 +62,12 @@ def main(argv=None) -> int:
             ring.append(b.to(dev))
         L = make_learner(name.split("@")[0], hyper, space, dev)
         ctx = RoundContext(spokes=spokes)
-        for k in range(2):
-            L.fit(ring[k % 3], ctx)
+        try:
+            for k in range(2):
+                L.fit(ring[k % 3], ctx)
+        except RuntimeError as e:  # a geometry the host guards refuse (sweeps)
+            res[name] = {"error": str(e), "spokes": spokes}
+            continue
         if dev.type == "cuda":
             torch.cuda.synchronize()
         t = time.perf_counter()

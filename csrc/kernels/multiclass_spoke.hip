@@ -98,7 +98,7 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
     const WT* __restrict__ Wt, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
     int dc, int cspan, const void* __restrict__ yv, int y_i8, int B, int R, int dim, int nclass,
     int variant, float C, int bias, float* __restrict__ ws, int2* __restrict__ tables,
-    float* __restrict__ dacc, TableGeom g, int ablate) {
+    float* __restrict__ dacc, TableGeom g, int ablate, int compact) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int cap = 1 << g.log2cap;
   const int tsz = cap + kOvf;
@@ -255,12 +255,34 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
   const int seg_log2 = bs_log2 + g.lgg;
   const size_t S_tot = gridDim.x;
   const size_t region = S_tot << g.log2cap;
-  for (int i = lane; i < cap && !(ablate & 1); i += kWave) {
-    const size_t q = (size_t)(i >> seg_log2);
-    const size_t o = ((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1));
-    const int key = keys[i];
-    for (int k = 0; k < nclass; ++k)
-      tables[(size_t)k * region + o] = make_int2(key, __float_as_int(vals[(size_t)i * K + k]));
+  if (compact) {
+    // One record per slot: the key once ([group][spoke][segment] int32 region) and its
+    // K deltas as one vector ([group][spoke][segment][K] floats after it) — 4 + 4K bytes
+    // instead of 8 per class, one reduce launch for all classes (multiclass_reduce_kernel).
+    int* kout = reinterpret_cast<int*>(tables);
+    float* vout = reinterpret_cast<float*>(kout + region);
+    for (int i = lane; i < cap && !(ablate & 1); i += kWave) {
+      const size_t q = (size_t)(i >> seg_log2);
+      const size_t o = ((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1));
+      kout[o] = keys[i];
+      if constexpr (K % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < K; k += 4)
+          *reinterpret_cast<float4*>(vout + o * K + k) =
+              *reinterpret_cast<const float4*>(&vals[(size_t)i * K + k]);
+      } else {
+        *reinterpret_cast<float2*>(vout + o * K) =
+            *reinterpret_cast<const float2*>(&vals[(size_t)i * K]);
+      }
+    }
+  } else {
+    for (int i = lane; i < cap && !(ablate & 1); i += kWave) {
+      const size_t q = (size_t)(i >> seg_log2);
+      const size_t o = ((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1));
+      const int key = keys[i];
+      for (int k = 0; k < nclass; ++k)
+        tables[(size_t)k * region + o] = make_int2(key, __float_as_int(vals[(size_t)i * K + k]));
+    }
   }
   for (int i = cap + lane; i < tsz; i += kWave) {
     const int key = keys[i];
@@ -287,6 +309,102 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
     if (!bias)
       for (int k = 0; k < nclass; ++k) wrow[kMcStat + k * (dn + 1) + dn] = 0.f;
   }
+}
+
+// Compact-flush reducer: `split` blocks per key group (group = blockIdx / split) sum the
+// (key, K-vector) records of their share of the active spokes into an LDS image
+// acc[span][K] (ds_add_f32), then add its non-zero entries to dacc[k][key] — plainly when
+// a block owns the group, with L2 fp32 atomics when the group is split. Same invariants as
+// linear_reduce_kernel: slot i of a table lies in group i >> seg, and its key in that
+// group's key range (overflow-area keys never reach the flushed region).
+template <int K>
+__global__ __launch_bounds__(256) void multiclass_reduce_kernel(
+    const int* __restrict__ keys, const float* __restrict__ vals, int S_act, int S, TableGeom g,
+    int dim, int nclass, float* __restrict__ dacc, int split) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* acc = reinterpret_cast<float*>(smem);
+  const int gl = g.kshift + g.lgg;
+  const int span = 1 << gl;
+  const int q = (int)blockIdx.x / split;
+  const int part = (int)blockIdx.x % split;
+  const int s_lo = (int)(((long long)S_act * part) / split);
+  const int s_hi = (int)(((long long)S_act * (part + 1)) / split);
+  for (int i = threadIdx.x; i < span * K; i += 256) acc[i] = 0.f;
+  __syncthreads();
+  const int seg_log2 = (g.log2cap - g.log2nb) + g.lgg;
+  const int lo = q << gl;
+  const size_t base = ((size_t)q * S + s_lo) << seg_log2;
+  const long long items = (long long)(s_hi - s_lo) << seg_log2;
+  auto add = [&](int key, const float (&v)[K]) {
+    const unsigned off = (unsigned)(key - lo);
+    if (key < 0 || off >= (unsigned)span) return;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k < nclass && v[k] != 0.f) atomicAdd(&acc[off * K + k], v[k]);
+  };
+  auto load = [&](long long it, int& key, float (&v)[K]) {
+    const size_t o = base + (size_t)it;
+    key = keys[o];
+    if constexpr (K % 4 == 0) {
+#pragma unroll
+      for (int k = 0; k < K; k += 4) {
+        const float4 f = *reinterpret_cast<const float4*>(vals + o * K + k);
+        v[k] = f.x; v[k + 1] = f.y; v[k + 2] = f.z; v[k + 3] = f.w;
+      }
+    } else {
+      const float2 f = *reinterpret_cast<const float2*>(vals + o * K);
+      v[0] = f.x;
+      v[1] = f.y;
+    }
+  };
+  long long it = threadIdx.x;
+  for (; it + 3 * 256 < items; it += 4 * 256) {
+    int key[4];
+    float v[4][K];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load(it + u * 256, key[u], v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) add(key[u], v[u]);
+  }
+  for (; it < items; it += 256) {
+    int key;
+    float v[K];
+    load(it, key, v);
+    add(key, v);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < span * K; i += 256) {
+    const int k = i % K;
+    const int key = lo + i / K;
+    const float v = acc[i];
+    if (k < nclass && key < dim && v != 0.f) {
+      if (split == 1) dacc[(size_t)k * dim + key] += v;
+      else unsafeAtomicAdd(&dacc[(size_t)k * dim + key], v);
+    }
+  }
+}
+
+template <int K>
+static int launch_mc_reduce(const void* tables, int S_act, int S, TableGeom g, int dim,
+                            int nclass, float* dacc, hipStream_t st) {
+  if (S_act <= 0) return 0;
+  const int gl = g.kshift + g.lgg;
+  const int ng = (dim + (1 << gl) - 1) >> gl;
+  int split = ng >= 1024 ? 1 : 4;  // memory-level parallelism, as linear_reduce_kernel
+  if (const char* e = getenv("OMLDM_REDUCE_SPLIT")) split = atoi(e);
+  if (split < 1) split = 1;
+  if (split > 16) split = 16;
+  while (split > 1 && split > S_act) split >>= 1;
+  const size_t lds = (size_t(1) << gl) * K * sizeof(float);
+  auto fn = multiclass_reduce_kernel<K>;
+  int e = check_dyn_lds((const void*)fn, lds);
+  if (e) return e;
+  const size_t region = (size_t)S << g.log2cap;
+  const int* keys = static_cast<const int*>(tables);
+  hipLaunchKernelGGL(fn, dim3(ng * split), dim3(256), lds, st, keys,
+                     reinterpret_cast<const float*>(keys + region), S_act, S, g, dim, nclass,
+                     dacc, split);
+  return (int)hipGetLastError();
 }
 
 // Workspace column sums (one block per column): stats[c] += Σ_s ws[s][c] for c < 8;
@@ -341,7 +459,7 @@ template <int K, typename NumT, typename WT>
 static void launch_mc(const void* Wt, const void* num, int dn, const void* cat, int dc, int cspan,
                       const void* y, int y_i8, int B, int R, int S, int dim, int nclass,
                       int variant, float C, int bias, float* ws, int2* tables, float* dacc,
-                      TableGeom g, size_t lds, hipStream_t st, int* err) {
+                      TableGeom g, size_t lds, int compact, hipStream_t st, int* err) {
   auto fn = multiclass_round_kernel<K, 4, NumT, WT>;
   int ablate = 0;  // timing diagnostics only: bit0 no flush, bit1 no sequential part
   if (const char* e = getenv("OMLDM_MC_ABLATE")) ablate = atoi(e);
@@ -349,7 +467,7 @@ static void launch_mc(const void* Wt, const void* num, int dn, const void* cat, 
   if (*err) return;
   hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)Wt, (const NumT*)num, dn, cat, dc,
                      cspan, y, y_i8, B, R, dim, nclass, variant, C, bias, ws, tables, dacc, g,
-                     ablate);
+                     ablate, compact);
 }
 
 }  // namespace omldm
@@ -374,21 +492,26 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
   const size_t lds = ((size_t(1) << log2cap) + kOvf) * (4 + 4 * (size_t)K);
   if (lds > 160 * 1024) return -1;
   hipStream_t st = (hipStream_t)stream;
+  // Compact flush + one reduce launch when the reducer's LDS image acc[span][K] fits
+  // (K ≤ 8 at the default 4096-key groups); per-class int2 regions otherwise. Both fit
+  // the caller's nclass·S·2^log2cap int2 scratch, since 1 + K ≤ 2·nclass.
+  int compact = ((size_t(1) << (g.kshift + g.lgg)) * K * sizeof(float)) <= 160 * 1024;
+  if (const char* ev = getenv("OMLDM_MC_COMPACT")) compact = compact && atoi(ev) != 0;  // A/B
   int e = 0;
 #define OMLDM_MC(KK)                                                                         \
   {                                                                                          \
     if (num_bf16 && wt_bf16)                                                                 \
       launch_mc<KK, __hip_bfloat16, __hip_bfloat16>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, \
-          S, dim, nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, st, &e);           \
+          S, dim, nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, st, &e);           \
     else if (num_bf16)                                                                       \
       launch_mc<KK, __hip_bfloat16, float>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim,  \
-          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, st, &e);                   \
+          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, st, &e);                   \
     else if (wt_bf16)                                                                        \
       launch_mc<KK, float, __hip_bfloat16>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim,  \
-          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, st, &e);                   \
+          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, st, &e);                   \
     else                                                                                     \
       launch_mc<KK, float, float>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim, nclass,   \
-          variant, C, bias, ws, (int2*)tables, dacc, g, lds, st, &e);                           \
+          variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, st, &e);                           \
   }
   if (K == 2) OMLDM_MC(2) else if (K == 4) OMLDM_MC(4) else if (K == 8) OMLDM_MC(8) else OMLDM_MC(16)
 #undef OMLDM_MC
@@ -400,10 +523,18 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
   const int gspan = g.kshift + g.lgg;
   const int ng = (dim + (1 << gspan) - 1) >> gspan;
   const size_t region = (size_t)S << log2cap;
-  for (int k = 0; k < nclass; ++k) {
-    e = bucket_reduce_launch((const int2*)tables + k * region, S_act, S, g, dim,
-                             dacc + (size_t)k * dim, 0, ng, st);
+  if (compact) {
+    e = K == 2 ? launch_mc_reduce<2>(tables, S_act, S, g, dim, nclass, dacc, st)
+      : K == 4 ? launch_mc_reduce<4>(tables, S_act, S, g, dim, nclass, dacc, st)
+      : K == 8 ? launch_mc_reduce<8>(tables, S_act, S, g, dim, nclass, dacc, st)
+               : launch_mc_reduce<16>(tables, S_act, S, g, dim, nclass, dacc, st);
     if (e) return e;
+  } else {
+    for (int k = 0; k < nclass; ++k) {
+      e = bucket_reduce_launch((const int2*)tables + k * region, S_act, S, g, dim,
+                               dacc + (size_t)k * dim, 0, ng, st);
+      if (e) return e;
+    }
   }
   hipLaunchKernelGGL(multiclass_finish_kernel, dim3(kMcStat + nclass * (dn + 1)), dim3(256), 0, st,
                      ws, S, dn, nclass, dim, dacc, stats);

@@ -123,7 +123,8 @@ def test_hip_kmeans_assign(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nclass,R,S", [(4, 50, 40), (3, 16, 96), (2, 8, 64), (7, 16, 32)])
+@pytest.mark.parametrize("nclass,R,S", [(4, 50, 40), (3, 16, 96), (2, 8, 64), (7, 16, 32),
+                                         (12, 8, 32)])
 def test_hip_multiclass_round_vs_cpu(cuda, nclass, R, S):
     b = synth_batch(SP, R * S, task=2, n_classes=nclass, seed=5)
     W = torch.randn(nclass, SP.dim) * 0.01
@@ -136,6 +137,30 @@ def test_hip_multiclass_round_vs_cpu(cuda, nclass, R, S):
     np.testing.assert_allclose(stg.cpu()[[1, 3]].numpy(), st[[1, 3]].numpy())
     np.testing.assert_allclose(stg.cpu()[[0, 2]].numpy(), st[[0, 2]].numpy(), rtol=1e-3)
     np.testing.assert_allclose(daccg.cpu().numpy(), dacc.numpy(), rtol=2e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nclass", [2, 4, 6])
+def test_hip_multiclass_compact_flush_matches_per_class(cuda, nclass, monkeypatch):
+    """The compact (key, K-vector) flush + one-launch reducer == the per-class int2 regions
+    reduced one class at a time, at the learners-bench geometry (2^20 dims, 16 rows per
+    spoke, split reduce blocks)."""
+    from omldm_amd.api.batch import FeatureSpace
+
+    sp = FeatureSpace(13, 0, 26, 1 << 20)
+    S, R = 2048, 16
+    b = synth_batch(sp, S * R, task=2, n_classes=nclass, seed=8).to(cuda)
+    W = (torch.randn(nclass, sp.dim) * 0.01).to(cuda)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("OMLDM_MC_COMPACT", flag)
+        st, dacc = torch.zeros(8, device=cuda), torch.zeros(nclass, sp.dim, device=cuda)
+        D.multiclass_round(W, b, R, S, nclass, 1, 1.0, True, dacc, st)
+        torch.cuda.synchronize()
+        out.append((st.cpu(), dacc.cpu()))
+    assert torch.equal(out[0][0][[1, 3, 5]], out[1][0][[1, 3, 5]])
+    np.testing.assert_allclose(out[0][1].numpy(), out[1][1].numpy(), rtol=1e-5, atol=1e-6)
+    assert float(out[0][1].abs().sum()) > 0
 
 
 @pytest.mark.gpu
