@@ -28,12 +28,13 @@ CASES = [
     ("SVM", 0, {"modelDtype": "bf16", "tableLog2": 11}, 4096),
     ("RegressorPA", 1, {}, 4096),
     ("LogisticRegression", 0, {}, 4096),
-    ("MultiClassPA", 2, {"nClasses": 4}, 4096),
-    ("MultiClassPA@8192", 2, {"nClasses": 4}, 8192),
+    ("MultiClassPA", 2, {"nClasses": 4}, 8192),
+    ("MultiClassPA@4096", 2, {"nClasses": 4}, 4096),
     ("ORR", 1, {}, 1),
     ("K-means", 0, {"k": 16}, 1),
-    ("NN", 0, {"hiddenLayers": [64, 64]}, 2048),
-    ("NN@bf16", 0, {"hiddenLayers": [64, 64], "matmulDtype": "bf16"}, 2048),
+    # 512 spokes × 256 rows: fastest of 256..2048 (bench/sweep_cases_nn.json)
+    ("NN", 0, {"hiddenLayers": [64, 64]}, 512),
+    ("NN@bf16", 0, {"hiddenLayers": [64, 64], "matmulDtype": "bf16"}, 512),
     ("HT", 2, {"nClasses": 4}, 1),
 ]
 
