@@ -437,11 +437,26 @@ __global__ __launch_bounds__(256) void multiclass_finish_kernel(const float* __r
 
 // W[k][i] += dacc[k][i] / n_active ; dacc = 0 ; key-major shadow Wt[i][k] = W[k][i]
 // (fp32 or bf16, row stride kp) for the next round's gathers.
+// fold != 0 also folds the round's statistics into the running totals (block 0, one
+// lane; `st` is not read by any other block — nact is its own buffer):
+//   fold 1: cum[k] += st[k], k < 3;  fold 2 (NN regression): cum[0..1] += st[0..1];
+//   fold 3 (NN classification): as 2 plus cum[2] += st[1] − st[2];  then st[0..3] = 0.
+// This replaces four small elementwise launches per round.
 __global__ __launch_bounds__(256) void multiclass_apply_kernel(float* __restrict__ W,
                                                                float* __restrict__ dacc, int dim,
                                                                int nclass, void* __restrict__ Wt,
                                                                int wt_bf16, int kp,
-                                                               const float* __restrict__ nact) {
+                                                               const float* __restrict__ nact,
+                                                               float* __restrict__ st,
+                                                               float* __restrict__ cum, int fold) {
+  if (fold && blockIdx.x == 0 && threadIdx.x == 0) {
+    const float a = st[0], b = st[1], c = st[2];
+    cum[0] += a;
+    cum[1] += b;
+    if (fold == 1) cum[2] += c;
+    if (fold == 3) cum[2] += b - c;
+    st[0] = st[1] = st[2] = st[3] = 0.f;
+  }
   const float na = *nact;
   const float r = na > 0.f ? 1.f / na : 0.f;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < dim; i += gridDim.x * 256) {
@@ -546,11 +561,13 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
 
 // Wt: key-major shadow [dim][kp] (nullptr: none).
 OMLDM_API int omldm_multiclass_apply(float* W, float* dacc, int dim, int nclass, void* Wt,
-                                     int wt_bf16, int kp, const float* nact, void* stream) {
+                                     int wt_bf16, int kp, const float* nact, float* st,
+                                     float* cum, int fold, void* stream) {
+  if (fold && (!st || !cum || st == nact)) return -1;
   int blocks = (dim + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(multiclass_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, W,
-                     dacc, dim, nclass, Wt, wt_bf16, kp, nact);
+                     dacc, dim, nclass, Wt, wt_bf16, kp, nact, st, cum, fold);
   return (int)hipGetLastError();
 }

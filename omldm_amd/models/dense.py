@@ -23,6 +23,16 @@ def _in_dim(h: dict, space: FeatureSpace) -> int:
 
 
 # ---------------------------------------------------------------------------- ORR
+
+def _host_scalar(owner, v: float) -> torch.Tensor:
+    """Device scalar holding ``v``, cached per value on ``owner`` (one H2D per distinct
+    value, none per round): the active-spoke count the apply kernel divides by."""
+    cache = owner.__dict__.setdefault("_scalar_cache", {})
+    t = cache.get(v)
+    if t is None:
+        t = cache[v] = torch.full((1,), float(v), dtype=torch.float32, device=owner.device)
+    return t
+
 class ORR(Learner):
     """Online ridge regression: A = λI + Σxxᵀ, b = Σyx, w = A⁻¹b (intercept included).
     State = the augmented Gram matrix of [x, 1, y] — additive sufficient statistics, so
@@ -196,13 +206,12 @@ class MultiClassPA(Learner):
             return
         S = max(1, ctx.spokes)
         R = max(1, -(-batch.B // S))
-        self.st[3] = 0.0
         D.multiclass_round(self.W, batch, R, S, self.K, self.variant, self.C, self.bias,
                            self.dacc, self.st, log2cap=hp_int(self.hyper, "tableLog2", 0),
                            Wt=self.Wt)
-        D.multiclass_apply(self.W, self.dacc, self.st[3:4], self.Wt)
-        self.cum[:3] += self.st[:3]
-        self.st[:3] = 0.0
+        # every spoke with rows is active: ceil(B / R) of them, known on the host
+        D.multiclass_apply(self.W, self.dacc, _host_scalar(self, -(-batch.B // R)), self.Wt,
+                           st=self.st, cum=self.cum, fold=1)
 
     def state_vector(self):
         return self.W.view(-1)
@@ -300,11 +309,9 @@ class NN(Learner):
         S = -(-B // R)
         D.mlp_round(self.flat, batch.num, batch.y, R, S, self.widths, self.task_id, self.lr,
                     self.dacc, self.st, self.act)
-        D.multiclass_apply(self.flat, self.dacc, self.st[3:4])
-        self.cum[0] += self.st[0]
-        self.cum[1] += self.st[1]
-        self.cum[2] += self.st[1] - self.st[2] if self.task_id else 0.0
-        self.st.zero_()
+        # S = ceil(B / R): every spoke has rows
+        D.multiclass_apply(self.flat, self.dacc, _host_scalar(self, S), st=self.st,
+                           cum=self.cum, fold=3 if self.task_id else 2)
 
     def state_vector(self):
         return self.flat

@@ -273,19 +273,33 @@ def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int], act: int = 
 
 
 def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor,
-                     Wt: torch.Tensor | None = None) -> None:
-    """W += dacc / n_active; dacc = 0; refresh the key-major shadow ``Wt`` if given."""
+                     Wt: torch.Tensor | None = None, st: torch.Tensor | None = None,
+                     cum: torch.Tensor | None = None, fold: int = 0) -> None:
+    """W += dacc / n_active; dacc = 0; refresh the key-major shadow ``Wt`` if given.
+    ``fold`` > 0 also folds the round statistics ``st`` into the running totals ``cum``
+    and clears st[0..3] in the same launch (1: cum[:3] += st[:3]; 2: cum[:2] += st[:2];
+    3: as 2 plus cum[2] += st[1] − st[2]). ``nact`` must then be its own buffer."""
+    if fold:
+        assert st is not None and cum is not None and nact.data_ptr() != st.data_ptr()
     if W.is_cuda:
         K, dim = (1, W.numel()) if W.dim() == 1 else W.shape  # 1-D: a flat parameter vector
         assert Wt is None or W.dim() == 2
         check(native.hip().omldm_multiclass_apply(
             ptr(W), ptr(dacc), dim, K, ptr(Wt), int(Wt is not None and Wt.dtype == torch.bfloat16),
-            class_pad(K), ptr(nact), native.stream_of(W)), "omldm_multiclass_apply")
+            class_pad(K), ptr(nact), ptr(st), ptr(cum), int(fold), native.stream_of(W)),
+            "omldm_multiclass_apply")
     else:
         n = float(nact.item())
         if n > 0:
             W.add_(dacc / n)
         dacc.zero_()
+        if fold:
+            cum[:2] += st[:2]
+            if fold == 1:
+                cum[2] += st[2]
+            elif fold == 3:
+                cum[2] += st[1] - st[2]
+            st[:4] = 0.0
 
 
 def _tree_ptrs(tree: list[torch.Tensor]):
