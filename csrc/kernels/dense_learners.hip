@@ -37,7 +37,8 @@ __device__ __forceinline__ float zval(const float* __restrict__ x, const float* 
 __global__ __launch_bounds__(64) void gram_mfma_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ y, int B, int d,
                                                        int rows_per_split,
-                                                       float* __restrict__ G, int ld) {
+                                                       float* __restrict__ G, int ld,
+                                                       float* __restrict__ cnt) {
   const int lane = threadIdx.x;
   const int i0 = blockIdx.x * 32, j0 = blockIdx.y * 32;
   const long long r0 = (long long)blockIdx.z * rows_per_split;
@@ -58,7 +59,12 @@ __global__ __launch_bounds__(64) void gram_mfma_kernel(const float* __restrict__
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int row = i0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-    if (row < dz && col < dz && acc[r] != 0.f) atomicAdd(&G[(size_t)row * ld + col], acc[r]);
+    if (row < dz && col < dz && acc[r] != 0.f) {
+      atomicAdd(&G[(size_t)row * ld + col], acc[r]);
+      // entry (d, d) = Σ 1·1 over the split's valid rows: the fitted-row count, exact
+      // (integers < 2^24), handed to the learner's running total without extra launches
+      if (cnt && row == d && col == d) atomicAdd(cnt, acc[r]);
+    }
   }
 }
 
@@ -166,8 +172,9 @@ OMLDM_API int omldm_kmeans_apply(float* cent, float* n, int k, int d, float* sum
 }
 
 // G[ld×ld] += [X 1 y]ᵀ[X 1 y] over rows with finite y (ld ≥ d + 2).
+// cnt (may be null): += number of rows with finite y.
 OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, float* G, int ld,
-                                void* stream) {
+                                float* cnt, void* stream) {
   if (B <= 0) return 0;
   const int dz = d + 2;
   if (ld < dz) return -1;
@@ -180,7 +187,7 @@ OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, fl
   rows = (rows + 1) & ~1;
   ksplit = (B + rows - 1) / rows;
   hipLaunchKernelGGL(gram_mfma_kernel, dim3(t, t, ksplit), dim3(64), 0, (hipStream_t)stream, x,
-                     y, B, d, rows, G, ld);
+                     y, B, d, rows, G, ld, cnt);
   return (int)hipGetLastError();
 }
 

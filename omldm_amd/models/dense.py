@@ -55,9 +55,7 @@ class ORR(Learner):
     def fit(self, batch, ctx):
         x = batch.num.float()
         if batch.B:
-            D.gram_update(x, batch.y, self.G)
-            n = (~torch.isnan(batch.y)).sum()
-            self.cum[1] += n
+            D.gram_update(x, batch.y, self.G, cnt=self.cum[1:2])
         self._w = None
 
     def state_vector(self):

@@ -12,18 +12,24 @@ from omldm_amd.ops import native
 from omldm_amd.ops.native import check, ptr
 
 
-def gram_update(x: torch.Tensor, y: torch.Tensor, G: torch.Tensor) -> None:
-    """G[:d+2, :d+2] += Σ_rows z zᵀ with z = [x, 1, y] over rows whose y is finite."""
+def gram_update(x: torch.Tensor, y: torch.Tensor, G: torch.Tensor,
+                cnt: torch.Tensor | None = None) -> None:
+    """G[:d+2, :d+2] += Σ_rows z zᵀ with z = [x, 1, y] over rows whose y is finite;
+    ``cnt`` (one fp32 element) += the number of those rows, read off the Gram's (d, d)
+    entry inside the same kernel."""
     B, d = x.shape
     if B == 0:
         return
     x = x.float().contiguous()
     y = y.float().contiguous()
+    assert cnt is None or (cnt.dtype == torch.float32 and cnt.numel() == 1)
     if x.is_cuda:
-        check(native.hip().omldm_gram_update(ptr(x), ptr(y), B, d, ptr(G), G.shape[1],
+        check(native.hip().omldm_gram_update(ptr(x), ptr(y), B, d, ptr(G), G.shape[1], ptr(cnt),
                                              native.stream_of(x)), "omldm_gram_update")
         return
     ok = ~torch.isnan(y)
+    if cnt is not None:
+        cnt += ok.sum()
     z = torch.cat([x[ok], torch.ones((int(ok.sum()), 1)), y[ok].unsqueeze(1)], 1).double()
     G[: d + 2, : d + 2] += (z.T @ z).float()
 

@@ -97,8 +97,10 @@ def test_hip_gram_mfma_vs_fp64(cuda, B, d):
     y[::7] = float("nan")
     ld = ((d + 2 + 31) // 32) * 32
     G = torch.zeros(ld, ld, device=cuda)
-    D.gram_update(x.to(cuda), y.to(cuda), G)
+    cnt = torch.zeros(1, device=cuda)
+    D.gram_update(x.to(cuda), y.to(cuda), G, cnt=cnt)
     ok = ~torch.isnan(y)
+    assert float(cnt) == float(ok.sum())  # fitted-row count from the (d, d) entry
     z = torch.cat([x[ok], torch.ones(int(ok.sum()), 1), y[ok].unsqueeze(1)], 1).double()
     ref = (z.T @ z).numpy()
     got = G.cpu().double().numpy()[: d + 2, : d + 2]
