@@ -38,7 +38,7 @@ __global__ __launch_bounds__(64) void gram_mfma_kernel(const float* __restrict__
                                                        const float* __restrict__ y, int B, int d,
                                                        int rows_per_split,
                                                        float* __restrict__ G, int ld,
-                                                       float* __restrict__ cnt) {
+                                                       double* __restrict__ cnt) {
   const int lane = threadIdx.x;
   const int i0 = blockIdx.x * 32, j0 = blockIdx.y * 32;
   const long long r0 = (long long)blockIdx.z * rows_per_split;
@@ -61,9 +61,10 @@ __global__ __launch_bounds__(64) void gram_mfma_kernel(const float* __restrict__
     const int row = i0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (row < dz && col < dz && acc[r] != 0.f) {
       atomicAdd(&G[(size_t)row * ld + col], acc[r]);
-      // entry (d, d) = Σ 1·1 over the split's valid rows: the fitted-row count, exact
-      // (integers < 2^24), handed to the learner's running total without extra launches
-      if (cnt && row == d && col == d) atomicAdd(cnt, acc[r]);
+      // entry (d, d) = Σ 1·1 over the split's valid rows: the split's fitted-row count
+      // (exact: < 2^24 per split), added to the learner's fp64 running total without extra
+      // launches (an fp32 total would stop counting past ~2^30 rows)
+      if (cnt && row == d && col == d) atomicAdd(cnt, (double)acc[r]);
     }
   }
 }
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(256) void kmeans_apply_kernel(float* __restrict__ c
                                                            float* __restrict__ sums,
                                                            float* __restrict__ counts,
                                                            float* __restrict__ inertia,
-                                                           float* __restrict__ cum) {
+                                                           double* __restrict__ cum) {
   for (int i = threadIdx.x; i < k * d; i += 256) {
     const int j = i / d;
     const float nj = n[j], tot = nj + counts[j];
@@ -153,8 +154,8 @@ __global__ __launch_bounds__(256) void kmeans_apply_kernel(float* __restrict__ c
   __syncthreads();
   if (threadIdx.x == 0) {
     if (cum) {
-      cum[0] += *inertia;
-      cum[1] += (part[0] + part[1]) + (part[2] + part[3]);
+      cum[0] += (double)*inertia;
+      cum[1] += (double)((part[0] + part[1]) + (part[2] + part[3]));
     }
     *inertia = 0.f;
   }
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256) void kmeans_apply_kernel(float* __restrict__ c
 using namespace omldm;
 
 OMLDM_API int omldm_kmeans_apply(float* cent, float* n, int k, int d, float* sums, float* counts,
-                                 float* inertia, float* cum, void* stream) {
+                                 float* inertia, double* cum, void* stream) {
   hipLaunchKernelGGL(kmeans_apply_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, cent, n, k,
                      d, sums, counts, inertia, cum);
   return (int)hipGetLastError();
@@ -174,7 +175,7 @@ OMLDM_API int omldm_kmeans_apply(float* cent, float* n, int k, int d, float* sum
 // G[ld×ld] += [X 1 y]ᵀ[X 1 y] over rows with finite y (ld ≥ d + 2).
 // cnt (may be null): += number of rows with finite y.
 OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, float* G, int ld,
-                                float* cnt, void* stream) {
+                                double* cnt, void* stream) {
   if (B <= 0) return 0;
   const int dz = d + 2;
   if (ld < dz) return -1;

@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void ht_update_kernel(
     const float* __restrict__ feat, const float* __restrict__ thr, const float* __restrict__ left,
     const float* __restrict__ right, float* __restrict__ cc, float* __restrict__ S0,
     float* __restrict__ S1, float* __restrict__ S2, float* __restrict__ lo, float* __restrict__ hi,
-    float* __restrict__ since, float* __restrict__ nfit) {
+    float* __restrict__ since, double* __restrict__ nfit) {
   const int row = blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   int key = -1, node = 0, yi = 0;
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void ht_update_kernel(
   }
   unsigned long long pending = __ballot(key >= 0);
   const float n = (float)__popcll(pending);
-  if (lane == 0 && n > 0.f && nfit) atomicAdd(nfit, n);
+  if (lane == 0 && n > 0.f && nfit) atomicAdd(nfit, (double)n);
   while (pending) {  // wave-uniform
     const int leader = __ffsll((long long)pending) - 1;
     const int k = __shfl(key, leader);
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(1024) void ht_route_hist_kernel(
     const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int C, int depth,
     const float* __restrict__ feat, const float* __restrict__ thr, const float* __restrict__ left,
     const float* __restrict__ right, int nbins, int* __restrict__ keys, int* __restrict__ hist,
-    float* __restrict__ nfit) {
+    double* __restrict__ nfit) {
   extern __shared__ int h[];  // [nbins]
   for (int b = threadIdx.x; b < nbins; b += 1024) h[b] = 0;
   __syncthreads();
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(1024) void ht_route_hist_kernel(
   __syncthreads();
   for (int b = threadIdx.x; b < nbins; b += 1024) hist[(size_t)blockIdx.x * nbins + b] = h[b];
   const float n = wave_sum(cnt);
-  if ((threadIdx.x & 63) == 0 && n > 0.f && nfit) atomicAdd(nfit, n);
+  if ((threadIdx.x & 63) == 0 && n > 0.f && nfit) atomicAdd(nfit, (double)n);
 }
 
 // Inclusive block scan of one int per thread (1024 threads).
@@ -434,7 +434,7 @@ OMLDM_API long long omldm_ht_update_ws_ints(int B, int N, int C) {
 }
 
 OMLDM_API int omldm_ht_update(const float* x, const float* y, int B, int d, int C, int depth,
-                              int N, float* const* tree, float* nfit, int* ws, void* stream) {
+                              int N, float* const* tree, double* nfit, int* ws, void* stream) {
   if (B <= 0) return 0;
   if (C < 1 || C > kHtMaxC) return -1;
   hipStream_t st = (hipStream_t)stream;

@@ -313,7 +313,7 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
 //   Σ1/P → dacc[dim+1], loss/n/mistakes/sq_err/overflow → cum (device running totals).
 __device__ __forceinline__ void finish_column(int c, const float* __restrict__ ws, int S, int dn,
                                               int dim, float* __restrict__ dacc,
-                                              float* __restrict__ cum) {
+                                              double* __restrict__ cum) {
   __shared__ float part[4];
   const int wsw = kWsStat + dn + 1;
   float acc = 0.f;
@@ -326,7 +326,7 @@ __device__ __forceinline__ void finish_column(int c, const float* __restrict__ w
     if (c < kWsStat) {
       if (c == 6) dacc[dim] = t;       // the round's counters (apply does not clear them)
       else if (c == 7) dacc[dim + 1] = t;
-      else if (c != 4 && cum) cum[c] += t;
+      else if (c != 4 && cum) cum[c] += (double)t;
     } else {
       const int j = c - kWsStat;
       dacc[j < dn ? j : dim - 1] += t;
@@ -344,7 +344,7 @@ __device__ __forceinline__ void finish_column(int c, const float* __restrict__ w
 __global__ __launch_bounds__(256) void linear_reduce_kernel(
     const int2* __restrict__ tables, int S_act, TableGeom g, int dim, float* __restrict__ dacc,
     int nb, int split, int q0, const float* __restrict__ ws, int S, int dn,
-    float* __restrict__ cum) {
+    double* __restrict__ cum) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if ((int)blockIdx.x >= nb) {
     finish_column(blockIdx.x - nb, ws, S, dn, dim, dacc, cum);
@@ -507,7 +507,7 @@ static void part_bounds(int dim, TableGeom g, int part, int parts, long long* lo
 // part's launch, so the all-reduce of part k runs on the RCCL stream while part k+1
 // reduces (protocols.Synchronous, reduce_parts).
 static int launch_reduce(const int2* tables, int B, int R, int S, TableGeom g, int dim,
-                         float* dacc, const float* ws, int dn, float* cum, int part, int parts,
+                         float* dacc, const float* ws, int dn, double* cum, int part, int parts,
                          int ablate, hipStream_t st) {
   const long long sact_ll = R > 0 ? ((long long)B + R - 1) / R : 0;
   const int S_act = sact_ll < S ? (int)sact_ll : S;
@@ -538,14 +538,14 @@ int bucket_reduce_launch(const int2* tables, int S_act, int S, TableGeom g, int 
   int e = check_dyn_lds((const void*)linear_reduce_kernel, rlds);
   if (e) return e;
   hipLaunchKernelGGL(linear_reduce_kernel, dim3(nb), dim3(256), rlds, st, tables, S_act, g, dim,
-                     dacc, nb, split, q0, (const float*)nullptr, S, 0, (float*)nullptr);
+                     dacc, nb, split, q0, (const float*)nullptr, S, 0, (double*)nullptr);
   return (int)hipGetLastError();
 }
 
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
 static int launch_round(const void* w, const void* num, int dn, const void* cat, int dc,
                         const void* y, int B, int R, int S, float* dacc, int dim, float* ws,
-                        int2* tables, float* cum, const LinParams& p, TableGeom g, int ablate,
+                        int2* tables, double* cum, const LinParams& p, TableGeom g, int ablate,
                         int parts, hipStream_t st) {
   auto fn = linear_round_kernel<FPL, CH, RULE, NumT, WT>;
   const size_t lds = ((size_t(1) << g.log2cap) + kOvf) * 8;
@@ -561,7 +561,7 @@ static int launch_round(const void* w, const void* num, int dn, const void* cat,
 template <int FPL, int CH, int RULE>
 static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                           const void* cat, int dc, const void* y, int B, int R, int S, float* dacc,
-                          int dim, float* ws, int2* tables, float* cum, const LinParams& p,
+                          int dim, float* ws, int2* tables, double* cum, const LinParams& p,
                           TableGeom g, int ablate, int parts, hipStream_t st) {
 #define OMLDM_LR(NT, WTT)                                                                      \
   return launch_round<FPL, CH, RULE, NT, WTT>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, ws, \
@@ -578,7 +578,7 @@ static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf
 template <int FPL, int CH>
 static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, int num_bf16,
                          int dn, const void* cat, int dc, const void* y, int B, int R, int S,
-                         float* dacc, int dim, float* ws, int2* tables, float* cum,
+                         float* dacc, int dim, float* ws, int2* tables, double* cum,
                          const LinParams& p, TableGeom g, int ablate, int parts,
                          hipStream_t st) {
   if (rule == kHinge)
@@ -663,7 +663,7 @@ int bucket_geom(int dim, int log2cap, TableGeom* g) {
 OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                                  const void* cat, int dc, const void* y, int y_i8, int B,
                                  int R, int S, float* dacc, int dim, float* ws, void* tables,
-                                 float* cum, int rule, int variant, float C, float eps, float lr,
+                                 double* cum, int rule, int variant, float C, float eps, float lr,
                                  float lam, float inv_p, int bias, int cspan, int log2cap,
                                  int chunk, int ablate, int parts, void* stream) {
   if (S <= 0) return 0;
@@ -689,7 +689,7 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
 
 // Reduce part `part` (1 ≤ part < parts) of the round launched by omldm_linear_round with
 // the same arguments; part 0 was launched by the round call itself.
-OMLDM_API int omldm_linear_reduce_part(void* tables, float* ws, float* cum, float* dacc, int dim,
+OMLDM_API int omldm_linear_reduce_part(void* tables, float* ws, double* cum, float* dacc, int dim,
                                        int dn, int B, int R, int S, int log2cap, int part,
                                        int parts, int ablate, void* stream) {
   if (S <= 0) return 0;

@@ -171,7 +171,8 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
                                                         const float* __restrict__ x,
                                                         const float* __restrict__ yv, long long B,
                                                         int R, float lr, float* __restrict__ dacc,
-                                                        float* __restrict__ stats, MlpDesc g,
+                                                        float* __restrict__ stats,
+                                                        float* __restrict__ nact, MlpDesc g,
                                                         float* __restrict__ ws, int nparams) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -299,6 +300,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       atomicAdd(&stats[1], nv);
       atomicAdd(&stats[2], corr);
       atomicAdd(&stats[3], 1.f);
+      if (nact) atomicAdd(nact, 1.f);  // the apply kernel's divisor (its own buffer)
     }
   }
 }
@@ -403,11 +405,13 @@ OMLDM_API long long omldm_mlp_lds_bytes(int L, const int* widths) {
 
 // One protocol round: S spokes × R rows (spoke s owns rows [sR, sR+R)); task 0 regression,
 // 1 binary logistic, 2 softmax. dacc[nparams] += Σ_s Δ_s; stats[0..3] += loss, n, correct,
-// active spokes. Follow with omldm_multiclass_apply(w, dacc, nparams, stats+3).
+// active spokes (spokes with ≥ 1 labelled row); nact (optional, zeroed beforehand) += active
+// spokes too. Follow with omldm_multiclass_apply(w, dacc, nparams, ..., nact, ...): the
+// apply kernel clears stats, so its divisor must live in a separate buffer.
 // ws: optional S × nparams scratch (spoke deltas by plain stores + slab column sums).
 OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, long long B, int R,
                               int S, int L, const int* widths, int task, int act, float lr,
-                              float* dacc, float* stats, float* ws, void* stream) {
+                              float* dacc, float* stats, float* nact, float* ws, void* stream) {
   if (B <= 0 || S <= 0) return 0;
   if (R <= 0 || (long long)R * S < B) return -3;
   MlpDesc g;
@@ -418,7 +422,7 @@ OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, lo
   if (e) return e;
   const int nparams = g.boff[g.L - 1] + g.n[g.L];
   hipLaunchKernelGGL(mlp_round_kernel, dim3(S), dim3(256), lds, (hipStream_t)stream, w, x, y, B,
-                     R, lr, dacc, stats, g, ws, nparams);
+                     R, lr, dacc, stats, nact, g, ws, nparams);
   if (ws)
     hipLaunchKernelGGL(mlp_colsum_kernel, dim3((nparams + 255) / 256, (S + kMlpSlab - 1) / kMlpSlab),
                        dim3(256), 0, (hipStream_t)stream, ws, S, nparams, dacc);

@@ -448,13 +448,17 @@ __global__ __launch_bounds__(256) void multiclass_apply_kernel(float* __restrict
                                                                int wt_bf16, int kp,
                                                                const float* __restrict__ nact,
                                                                float* __restrict__ st,
-                                                               float* __restrict__ cum, int fold) {
+                                                               double* __restrict__ cum, int fold,
+                                                               float* __restrict__ nact_next) {
+  // nact_next (optional, ≠ nact): the divisor buffer of the NEXT round, zeroed here so the
+  // next round kernel can count into it (callers alternate two buffers)
+  if (nact_next && blockIdx.x == 0 && threadIdx.x == 0) *nact_next = 0.f;
   if (fold && blockIdx.x == 0 && threadIdx.x == 0) {
     const float a = st[0], b = st[1], c = st[2];
-    cum[0] += a;
-    cum[1] += b;
-    if (fold == 1) cum[2] += c;
-    if (fold == 3) cum[2] += b - c;
+    cum[0] += (double)a;
+    cum[1] += (double)b;
+    if (fold == 1) cum[2] += (double)c;
+    if (fold == 3) cum[2] += (double)(b - c);
     st[0] = st[1] = st[2] = st[3] = 0.f;
   }
   const float na = *nact;
@@ -562,12 +566,13 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
 // Wt: key-major shadow [dim][kp] (nullptr: none).
 OMLDM_API int omldm_multiclass_apply(float* W, float* dacc, int dim, int nclass, void* Wt,
                                      int wt_bf16, int kp, const float* nact, float* st,
-                                     float* cum, int fold, void* stream) {
+                                     double* cum, int fold, float* nact_next, void* stream) {
   if (fold && (!st || !cum || st == nact)) return -1;
+  if (nact_next && nact_next == nact) return -1;
   int blocks = (dim + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(multiclass_apply_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, W,
-                     dacc, dim, nclass, Wt, wt_bf16, kp, nact, st, cum, fold);
+                     dacc, dim, nclass, Wt, wt_bf16, kp, nact, st, cum, fold, nact_next);
   return (int)hipGetLastError();
 }

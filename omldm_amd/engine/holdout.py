@@ -136,6 +136,38 @@ class HoldoutSet:
         return {"num": self.ring.num.cpu(), "cat": self.ring.cat.cpu(), "y": self.ring.y.cpu(),
                 "count": self.count, "head": self.head, "filled": self.filled}
 
+    @staticmethod
+    def _rows_in_order(sd: dict) -> tuple[torch.Tensor, ...]:
+        size, filled = sd["num"].shape[0], int(sd["filled"])
+        idx = (torch.arange(filled) + (int(sd["head"]) - filled)) % max(1, size)
+        return sd["num"][idx], sd["cat"][idx], sd["y"][idx]
+
+    def load_merged(self, sds: list[dict]) -> HashedBatch | None:
+        """Re-scaled restore: the rings of several old ranks merged into this one, oldest
+        rows first (old-rank order). Rows beyond ``size`` are returned to be trained on
+        (reference restore: the merged test set is popped down to its maximum size and
+        the popped points are fed to every pipeline, FlinkSpoke.scala:307-317)."""
+        self.count, self.head, self.filled = 0, 0, 0
+        if not sds:
+            return None
+        parts = [self._rows_in_order(sd) for sd in sds]
+        num = torch.cat([p[0] for p in parts])
+        cat = torch.cat([p[1] for p in parts])
+        y = torch.cat([p[2] for p in parts])
+        n = num.shape[0]
+        keep = min(n, self.size)
+        spill = n - keep
+        if keep:
+            self.ring.num[:keep] = num[spill:].to(self.device, self.ring.num.dtype)
+            self.ring.cat[:keep] = cat[spill:].to(self.device)
+            self.ring.y[:keep] = y[spill:].to(self.device)
+        self.filled, self.head = keep, keep % max(1, self.size)
+        self.count = int(sds[0]["count"])
+        if spill == 0:
+            return None
+        return HashedBatch(num[:spill].to(self.ring.num.dtype), cat[:spill], y[:spill],
+                           cat_span=self.ring.cat_span)
+
     def load_state_dict(self, sd: dict) -> None:
         n = min(self.size, sd["num"].shape[0])
         self.ring.num[:n] = sd["num"][:n].to(self.device)

@@ -252,13 +252,15 @@ class Job:
                         prod.produce(self.cfg.predictionsTopic, Prediction(pid, None, p).to_json())
                 self.counters["predictions"] += len(preds)
 
-    def _train(self, batch: HashedBatch):
+    def _train(self, batch: HashedBatch, direct: HashedBatch | None = None):
         """One round of every pipeline. Synchronous pipelines train first and their
         round buffers are summed over ranks in ONE coalesced collective per hub layout
         (one flat bucket instead of one launch per pipeline); the other
         protocols run their own rounds."""
         with tracing.range("route"):
             routed = self.holdout.route(batch)
+        if direct is not None and direct.B:  # rows that bypass the holdout
+            routed = HashedBatch.cat_batches([direct, routed]) if routed.B else direct
         groups: dict[int, list] = {}
         for pid in sorted(self.pipes):
             pipe = self.pipes[pid]
@@ -360,13 +362,21 @@ class Job:
                 tb = batch.without_raw().select(tidx).to(self.device, non_blocking=True)
         else:
             tb = HashedBatch.empty(self.space, 0, device=self.device)
+        spill = getattr(self, "_restored_train", None)
+        if spill is not None and self.pipes:
+            # holdout rows that no longer fit the merged ring after a re-scaled restore:
+            # trained on directly (not routed through the holdout again)
+            self._restored_train = None
+            spill = spill.to(self.device)
+        else:
+            spill = None
         # global activity + termination flag (one tiny all-reduce per tick); every rank
         # then takes the same decisions, so the pipelines' collectives stay aligned
         self._flags[0] = float(n_local + n_ctrl)
         self._flags[1] = 0.0
         if self.rank == 0 and self.cfg.test and self.idle.expired(t0) and self.pipes:
             self._flags[1] = 1.0
-        self._flags[2] = float(tb.B)
+        self._flags[2] = float(tb.B + (spill.B if spill is not None else 0))
         self._flags[3] = 0.0
         if self.world > 1 and self.rank == 0:
             self._ctrl_pending += self._poll_requests()
@@ -378,7 +388,7 @@ class Job:
         active += n_req
         self._trained_global += int(n_train)
         if self.pipes and n_train > 0:
-            self._train(tb)
+            self._train(tb, spill)
         for q in queries:
             self._answer(q)
         for pipe in self.pipes.values():
@@ -453,21 +463,42 @@ class Job:
         return sd
 
     def load_state_dict(self, sd: dict, same_world: bool = True,
-                        consumer_offsets: dict | None = None) -> None:
+                        consumer_offsets: dict | None = None, owned: list | None = None) -> None:
+        """``owned`` (re-scaled restore only): the state dicts of the old ranks whose
+        per-rank data this rank takes over (utils/checkpoint.py:rescale_owners); models
+        and protocol state come from ``sd``."""
         for pid, psd in sd.get("pipelines", {}).items():
             req = Request.from_json(psd["request"])
             pipe = Pipeline(req, self.space, self.comm, self.device, self.spokes,
                             self.cfg.parallelism, self.cfg.maxMsgParams, store=self.store)
             pipe.load_state_dict(psd)
             self.pipes[int(pid)] = pipe
-        self.holdout.load_state_dict(sd["holdout"])
         if same_world:  # partition ownership only matches at the same world size
+            self.holdout.load_state_dict(sd["holdout"])
             self.train_in.load_state_dict(sd["consumers"]["train"])
             self.fcst_in.load_state_dict(sd["consumers"]["forecast"])
-        elif consumer_offsets is not None:  # Consumer keeps only the partitions it owns
-            self.train_in.load_state_dict({"offsets": consumer_offsets["train"]})
-            self.fcst_in.load_state_dict({"offsets": consumer_offsets["forecast"]})
-        recs = list(sd.get("record_buffer", []))
+            recs = list(sd.get("record_buffer", []))
+            self.counters.update(sd.get("counters", {}))
+        else:
+            if consumer_offsets is not None:  # Consumer keeps only the partitions it owns
+                self.train_in.load_state_dict({"offsets": consumer_offsets["train"]})
+                self.fcst_in.load_state_dict({"offsets": consumer_offsets["forecast"]})
+            owned = list(owned or [])
+            # holdout rings merged oldest-first; rows beyond the ring are trained on
+            spill = self.holdout.load_merged([o["holdout"] for o in owned])
+            if spill is not None and spill.B:
+                self._restored_train = spill
+            recs = [r for o in owned for r in o.get("record_buffer", [])]
+            # running totals are per rank and summed by queries: sum the owned ranks'
+            for pid, pipe in self.pipes.items():
+                cums = [o["pipelines"][pid]["learner"]["cum"] for o in owned
+                        if pid in o.get("pipelines", {})]
+                tot = torch.stack([c.to(torch.float64) for c in cums]).sum(0) if cums else \
+                    torch.zeros_like(pipe.learner.cum, device="cpu")
+                pipe.learner.cum.copy_(tot.to(pipe.learner.cum.device))
+            for o in owned:
+                for k, v in o.get("counters", {}).items():
+                    self.counters[k] = self.counters.get(k, 0) + v
         self.record_buffer = [join_block(recs)] if recs else []
         self._buffered = len(recs)
         self.ticks = int(sd.get("ticks", 0))

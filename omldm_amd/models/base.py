@@ -47,7 +47,9 @@ class Learner:
         self.space = space
         self.device = torch.device(device)
         # device-side running counters: loss_sum, n, mistakes, sq_err, -, overflow, -, -
-        self.cum = torch.zeros(8, dtype=torch.float32, device=self.device)
+        # fp64: kernels add per-round fp32 partials into them, and an fp32 total stops
+        # counting once it passes 2^24..2^31 (integer increments round away)
+        self.cum = torch.zeros(8, dtype=torch.float64, device=self.device)
 
     # ---------------------------------------------------------------- training
     def fit(self, batch: HashedBatch, ctx: RoundContext) -> None:
@@ -103,7 +105,7 @@ class Learner:
         self.hyper.update(sd.get("hyper", {}))
         self.load_state_vector(sd["state"].to(self.device))
         if "cum" in sd:
-            self.cum.copy_(sd["cum"].to(self.device))
+            self.cum.copy_(sd["cum"].to(self.device, torch.float64))
 
     def running_totals(self) -> dict:
         c = self.cum.tolist()

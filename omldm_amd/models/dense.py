@@ -294,6 +294,8 @@ class NN(Learner):
         self.flat = flat.to(self.device)
         self.dacc = torch.zeros_like(self.flat)
         self.st = torch.zeros(8, dtype=torch.float32, device=self.device)
+        self._nact = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self._parity = 0
         if self.device.type == "cuda" and D.mlp_lds_bytes(self.widths) > 160 * 1024:
             raise ValueError("NN layer widths exceed the LDS budget of the fused kernel")
 
@@ -305,11 +307,16 @@ class NN(Learner):
         per = -(-B // S)
         R = -(-per // self.MB) * self.MB
         S = -(-B // R)
+        # divisor = spokes with ≥ 1 labelled row, counted by the round kernel on the device
+        # (rows with NaN targets make no update); two buffers alternate so the apply can
+        # zero the next round's while it reads this round's
+        k = self._parity
+        self._parity ^= 1
         D.mlp_round(self.flat, batch.num, batch.y, R, S, self.widths, self.task_id, self.lr,
-                    self.dacc, self.st, self.act)
-        # S = ceil(B / R): every spoke has rows
-        D.multiclass_apply(self.flat, self.dacc, _host_scalar(self, S), st=self.st,
-                           cum=self.cum, fold=3 if self.task_id else 2)
+                    self.dacc, self.st, self.act, nact=self._nact[k:k + 1])
+        D.multiclass_apply(self.flat, self.dacc, self._nact[k:k + 1], st=self.st,
+                           cum=self.cum, fold=3 if self.task_id else 2,
+                           nact_next=self._nact[k ^ 1:(k ^ 1) + 1])
 
     def state_vector(self):
         return self.flat

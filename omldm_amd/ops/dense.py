@@ -15,14 +15,14 @@ from omldm_amd.ops.native import check, ptr
 def gram_update(x: torch.Tensor, y: torch.Tensor, G: torch.Tensor,
                 cnt: torch.Tensor | None = None) -> None:
     """G[:d+2, :d+2] += Σ_rows z zᵀ with z = [x, 1, y] over rows whose y is finite;
-    ``cnt`` (one fp32 element) += the number of those rows, read off the Gram's (d, d)
-    entry inside the same kernel."""
+    ``cnt`` (one fp64 element: a running total) += the number of those rows, read off
+    the Gram's (d, d) entry inside the same kernel."""
     B, d = x.shape
     if B == 0:
         return
     x = x.float().contiguous()
     y = y.float().contiguous()
-    assert cnt is None or (cnt.dtype == torch.float32 and cnt.numel() == 1)
+    assert cnt is None or (cnt.dtype == torch.float64 and cnt.numel() == 1)
     if x.is_cuda:
         check(native.hip().omldm_gram_update(ptr(x), ptr(y), B, d, ptr(G), G.shape[1], ptr(cnt),
                                              native.stream_of(x)), "omldm_gram_update")
@@ -132,6 +132,7 @@ def kmeans_apply(cent: torch.Tensor, n: torch.Tensor, sums: torch.Tensor, counts
     """GPU: one launch — c ← (n·c + Σx)/(n + cnt) where n + cnt > 0, n += cnt, Σx = cnt = 0,
     cum[0] += inertia, cum[1] += Σcnt, inertia = 0."""
     k, d = cent.shape
+    assert cum is None or cum.dtype == torch.float64
     check(native.hip().omldm_kmeans_apply(ptr(cent), ptr(n), k, d, ptr(sums), ptr(counts),
                                           ptr(inertia), ptr(cum), native.stream_of(cent)),
           "omldm_kmeans_apply")
@@ -206,7 +207,8 @@ def _mlp_grad_out(o: torch.Tensor, y: torch.Tensor, task: int, K: int):
     return g, loss, (o.argmax(1) == yi).float().sum()
 
 
-def mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats, act: int = 0) -> None:
+def mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats, act: int = 0,
+                        nact=None) -> None:
     """CPU mirror of mlp_round_kernel: spoke s runs 32-row mini-batch SGD over rows
     [sR, sR+R) from the round-start model; dacc += Σ Δ_s; stats += (loss, n, correct,
     active spokes)."""
@@ -238,11 +240,15 @@ def mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats, act: int =
             stats[1] += n_s
             stats[2] += c_s
             stats[3] += 1
+            if nact is not None:
+                nact += 1
 
 
 def mlp_round(w: torch.Tensor, x: torch.Tensor, y: torch.Tensor, R: int, S: int,
               widths: list[int], task: int, lr: float, dacc: torch.Tensor,
-              stats: torch.Tensor, act: int = 0) -> None:
+              stats: torch.Tensor, act: int = 0, nact: torch.Tensor | None = None) -> None:
+    """``nact`` (optional, one fp32 element, zero on entry): += the number of spokes with at
+    least one labelled row — the divisor of the following apply."""
     B = x.shape[0]
     if B == 0:
         return
@@ -257,10 +263,10 @@ def mlp_round(w: torch.Tensor, x: torch.Tensor, y: torch.Tensor, R: int, S: int,
         ws = _workspace(x.device, S * w.numel(), key="mlp_ws")
         check(native.hip().omldm_mlp_round(ptr(w), ptr(x), ptr(y), B, R, S, len(widths) - 1,
                                            _widths_arr(widths), task, act, lr, ptr(dacc),
-                                           ptr(stats), ptr(ws), native.stream_of(x)),
+                                           ptr(stats), ptr(nact), ptr(ws), native.stream_of(x)),
               "omldm_mlp_round")
     else:
-        mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats, act)
+        mlp_round_reference(w, x, y, R, S, widths, task, lr, dacc, stats, act, nact)
 
 
 def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int], act: int = 0
@@ -280,19 +286,25 @@ def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int], act: int = 
 
 def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor,
                      Wt: torch.Tensor | None = None, st: torch.Tensor | None = None,
-                     cum: torch.Tensor | None = None, fold: int = 0) -> None:
+                     cum: torch.Tensor | None = None, fold: int = 0,
+                     nact_next: torch.Tensor | None = None) -> None:
     """W += dacc / n_active; dacc = 0; refresh the key-major shadow ``Wt`` if given.
     ``fold`` > 0 also folds the round statistics ``st`` into the running totals ``cum``
     and clears st[0..3] in the same launch (1: cum[:3] += st[:3]; 2: cum[:2] += st[:2];
-    3: as 2 plus cum[2] += st[1] − st[2]). ``nact`` must then be its own buffer."""
+    3: as 2 plus cum[2] += st[1] − st[2]). ``nact`` must then be its own buffer.
+    ``nact_next`` (optional, another buffer) is zeroed in the same launch: the divisor the
+    next round counts into."""
+    assert nact_next is None or nact_next.data_ptr() != nact.data_ptr()
     if fold:
         assert st is not None and cum is not None and nact.data_ptr() != st.data_ptr()
+        assert cum.dtype == torch.float64  # running totals (kernel adds in fp64)
     if W.is_cuda:
         K, dim = (1, W.numel()) if W.dim() == 1 else W.shape  # 1-D: a flat parameter vector
         assert Wt is None or W.dim() == 2
         check(native.hip().omldm_multiclass_apply(
             ptr(W), ptr(dacc), dim, K, ptr(Wt), int(Wt is not None and Wt.dtype == torch.bfloat16),
-            class_pad(K), ptr(nact), ptr(st), ptr(cum), int(fold), native.stream_of(W)),
+            class_pad(K), ptr(nact), ptr(st), ptr(cum), int(fold), ptr(nact_next),
+            native.stream_of(W)),
             "omldm_multiclass_apply")
     else:
         n = float(nact.item())
@@ -306,6 +318,8 @@ def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor,
             elif fold == 3:
                 cum[2] += st[1] - st[2]
             st[:4] = 0.0
+        if nact_next is not None:
+            nact_next.zero_()
 
 
 def _tree_ptrs(tree: list[torch.Tensor]):
@@ -326,6 +340,7 @@ def ht_update(x: torch.Tensor, y: torch.Tensor, C: int, depth: int, tree: list[t
     B, d = x.shape
     x = x.float().contiguous()
     y = y.float().contiguous()
+    assert nfit is None or nfit.dtype == torch.float64
     ws = None
     if sort and N > 0 and N * C * 4 <= 64 << 10:
         n = int(native.hip().omldm_ht_update_ws_ints(B, N, C))

@@ -85,6 +85,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
     dim = int(dacc.shape[0]) - 2
     assert w.shape[0] == dim and (stats is None or stats.shape == (S, STAT_W))
     assert dacc.dtype == torch.float32
+    assert cum is None or cum.dtype == torch.float64  # running totals, added in fp64
     num, cat, y = batch.num, batch.cat, batch.y
     assert cat.dtype == (torch.int16 if batch.cat_span else torch.int32)
     # labels: fp32, or int8 on the compact classification wire (GPU kernel reads either)

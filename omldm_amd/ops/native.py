@@ -61,9 +61,10 @@ HIP_SIGS = [
     ("omldm_kmeans_apply", i32, [vp, vp, i32, i32, vp, vp, vp, vp, vp]),
     ("omldm_multiclass_round", i32, [vp, i32, vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32,
                                      i32, i32, i32, f32, i32, vp, vp, i32, vp, vp, vp]),
-    ("omldm_multiclass_apply", i32, [vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, i32, vp]),
+    ("omldm_multiclass_apply", i32, [vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, i32, vp, vp]),
     ("omldm_mlp_lds_bytes", i64, [i32, vp]),
-    ("omldm_mlp_round", i32, [vp, vp, vp, i64, i32, i32, i32, vp, i32, i32, f32, vp, vp, vp, vp]),
+    ("omldm_mlp_round", i32, [vp, vp, vp, i64, i32, i32, i32, vp, i32, i32, f32, vp, vp, vp, vp,
+                              vp]),
     ("omldm_mlp_forward", i32, [vp, vp, i64, i32, vp, i32, vp, vp]),
     ("omldm_ht_update", i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
     ("omldm_ht_update_ws_ints", i64, [i32, i32, i32]),

@@ -365,6 +365,19 @@ class GM(Protocol):
             self._full_sync()
         self.stats.rounds += 1
 
+    # E is identical on every rank (it only changes in a full sync) while the local
+    # models differ by their unsynced drifts: E must be checkpointed, or a restored rank
+    # would re-seed it from its own model and the replicas would never agree again.
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["E"] = None if self._E is None else self._E.cpu()
+        return sd
+
+    def load_state_dict(self, sd):
+        super().load_state_dict(sd)
+        if sd.get("E") is not None:
+            self._E = sd["E"].to(self.learner.device)
+
 
 class FGM(Protocol):
     """Functional Geometric Monitoring (variance safe function).
@@ -386,7 +399,8 @@ class FGM(Protocol):
         self.eps = _cfg_float(self.cfg, "epsilon", 0.05)
         self.eps_psi = _cfg_float(self.cfg, "epsilonPsi", 0.01)
         self._E = None
-        self._c_prev = 0
+        self._c_prev = 0.0     # this worker's counter in the current subround
+        self._csum = 0.0       # Σ counter increments of all workers (hub, replicated)
         self._theta = None
         self._phi0 = None
         self.subrounds = 0
@@ -426,7 +440,7 @@ class FGM(Protocol):
         self._c_prev = c
         self._account_small(self.G, 8)
         tot_inc, psi = msg.tolist()
-        self._csum = getattr(self, "_csum", 0.0) + tot_inc
+        self._csum += tot_inc
         if self._csum > self.G:
             self.subrounds += 1
             if psi >= self.eps_psi * self.G * self._phi0:
@@ -435,11 +449,31 @@ class FGM(Protocol):
                 self._csum = 0.0
             else:
                 self._theta = -psi / (2 * self.G)
-                self._phi0_sub = psi
                 self._csum = 0.0
                 # counters restart relative to the new subround
                 self._c_prev = torch.floor((phi - self._phi0) / self._theta).clamp(min=0)
         self.stats.rounds += 1
+
+    def state_dict(self):
+        """The round/subround state is the hub's (identical on every rank) plus this
+        worker's counter; E is the estimate every local drift is measured against."""
+        sd = super().state_dict()
+        sd["E"] = None if self._E is None else self._E.cpu()
+        sd["fgm"] = {"c_prev": float(self._c_prev), "csum": float(self._csum),
+                     "theta": self._theta, "phi0": self._phi0, "subrounds": self.subrounds,
+                     "fgm_rounds": self.fgm_rounds}
+        return sd
+
+    def load_state_dict(self, sd):
+        super().load_state_dict(sd)
+        if sd.get("E") is not None:
+            self._E = sd["E"].to(self.learner.device)
+        f = sd.get("fgm")
+        if f:
+            self._c_prev, self._csum = float(f["c_prev"]), float(f["csum"])
+            self._theta = None if f["theta"] is None else float(f["theta"])
+            self._phi0 = None if f["phi0"] is None else float(f["phi0"])
+            self.subrounds, self.fgm_rounds = int(f["subrounds"]), int(f["fgm_rounds"])
 
 
 class SingleLearner(Protocol):

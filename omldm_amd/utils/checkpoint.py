@@ -9,8 +9,13 @@ pipelines.
 Here every rank writes ``<stateBackend>/ckpt-<n>/rank-<r>.pt`` (tensors moved to host
 first, so the GPU stream is not held), and rank 0 writes ``manifest.json`` after a
 barrier (so a manifest only exists for complete checkpoints). Everything is restored,
-including the pipelines (Q1 fixed); a checkpoint taken with G ranks restores on G' ranks
-(rank r reads rank r mod G — model replicas are identical across ranks after a sync).
+including the pipelines (Q1 fixed). A checkpoint taken with G ranks restores on G' ranks
+(``rescale_owners``): new rank r OWNS old ranks {o : o mod G' = r} and takes over exactly
+their per-rank data — record buffers concatenated, holdout rings merged in FIFO order
+(rows beyond the ring are trained on, as the reference's restore does,
+FlinkSpoke.scala:307-317), running counters summed — so no record is trained twice or
+lost and Σ-over-ranks metrics are preserved. Models and protocol state come from old
+rank r mod G (replicas agree after a sync; GM/FGM estimates are identical everywhere).
 Files are loaded with ``weights_only=True``.
 """
 from __future__ import annotations
@@ -30,6 +35,14 @@ def _root(state_backend: str) -> str:
     if "://" in state_backend:
         raise ValueError(f"unsupported state backend {state_backend!r} (use file://)")
     return state_backend
+
+
+def rescale_owners(old_world: int, new_world: int, rank: int) -> list[int]:
+    """Old ranks whose per-rank data (record buffer, holdout, counters) new rank ``rank``
+    takes over on a restore at a different world size: every old rank has exactly one
+    new owner (o mod new_world), so shrinking merges and growing leaves the extra new
+    ranks empty."""
+    return [o for o in range(old_world) if o % new_world == rank]
 
 
 class Checkpointer:
@@ -84,19 +97,28 @@ class Checkpointer:
             man = json.load(f)
         old_world = int(man["world"])
         src = self.rank % old_world
-        sd = torch.load(os.path.join(d, f"rank-{src}.pt"), map_location="cpu", weights_only=True)
+
+        def load(r):
+            return torch.load(os.path.join(d, f"rank-{r}.pt"), map_location="cpu",
+                              weights_only=True)
+
+        sd = load(src)
         if old_world == self.world:
             job.load_state_dict(sd, same_world=True)
         else:
             # Re-scaled restore: partition ownership changes, so gather every old rank's
             # consumer offsets (each partition had exactly one owner) and let the new
-            # owners resume from them — no record is trained twice or skipped.
+            # owners resume from them; the per-rank data of the old ranks this rank owns
+            # (buffers, holdout, counters) moves here and nowhere else.
             offsets = {"train": {}, "forecast": {}}
+            owned = []
+            mine = set(rescale_owners(old_world, self.world, self.rank))
             for r in range(old_world):
-                o = sd if r == src else torch.load(os.path.join(d, f"rank-{r}.pt"),
-                                                   map_location="cpu", weights_only=True)
+                o = sd if r == src else load(r)
                 for k in offsets:
                     offsets[k].update(o["consumers"][k].get("offsets", {}))
-            job.load_state_dict(sd, same_world=False, consumer_offsets=offsets)
+                if r in mine:
+                    owned.append(o)
+            job.load_state_dict(sd, same_world=False, consumer_offsets=offsets, owned=owned)
         self.n = idx + 1
         return True

@@ -139,3 +139,57 @@ def test_checkpoint_restore_roundtrip(tmp_path):
     assert job2.pipes[1].learner.running_totals()["fitted"] == fitted
     assert job2.holdout.filled == job.holdout.filled
     assert job2.train_in.offsets == job.consumer_offsets()["train"]
+
+
+def test_rescale_owners_partition_old_ranks():
+    from omldm_amd.utils.checkpoint import rescale_owners
+
+    for old in (1, 2, 3, 4, 8):
+        for new in (1, 2, 3, 4, 8):
+            owned = [rescale_owners(old, new, r) for r in range(new)]
+            flat = sorted(o for x in owned for o in x)
+            assert flat == list(range(old))  # every old rank has exactly one new owner
+
+
+def test_shrink_restore_merges_buffers_holdout_and_counters(tmp_path):
+    """2 → 1 restore: both old ranks' buffered records (taken before any Create), their
+    holdout rows and their running counters all land on the single new rank — nothing
+    lost, nothing counted twice."""
+    import os
+
+    name = uuid.uuid4().hex
+    sds = []
+    for r in range(2):
+        job, br, _ = make_job(["--testSetSize", "64"], name=f"{name}-{r}")
+        for rec in synth_json_records(300, SP, seed=r):
+            br.produce("trainingData", rec)
+        job.tick()                               # no pipeline yet → records buffered
+        assert job._buffered == 300
+        create(br, 1, "SVM")
+        for rec in synth_json_records(200, SP, seed=10 + r):
+            br.produce("trainingData", rec)
+        job.tick()                               # Create + train (buffer replayed)
+        for rec in synth_json_records(150, SP, seed=20 + r):
+            br.produce("trainingData", rec)
+        sd = job.state_dict()
+        sd["record_buffer"] = [s.encode() if isinstance(s, str) else s
+                               for s in synth_json_records(40 + r, SP, seed=30 + r)]
+        sds.append(sd)
+    d = tmp_path / "ckpt-000000"
+    d.mkdir()
+    for r, sd in enumerate(sds):
+        torch.save(sd, os.path.join(d, f"rank-{r}.pt"))
+    (d / "manifest.json").write_text(json.dumps({"index": 0, "world": 2, "time": 0,
+                                                 "ticks": 2, "pipelines": [1]}))
+    job2, _, _ = make_job(["--restore", "true", "--stateBackend", f"file://{tmp_path}",
+                           "--testSetSize", "64"], name=f"{name}-new")
+    assert job2._buffered == 40 + 41
+    fit = [sd["pipelines"][1]["learner"]["cum"][1].item() for sd in sds]
+    assert job2.pipes[1].learner.running_totals()["fitted"] == int(sum(fit))
+    held = sum(sd["holdout"]["filled"] for sd in sds)
+    spill = job2._restored_train.B if getattr(job2, "_restored_train", None) is not None else 0
+    assert job2.holdout.filled + spill == held
+    assert job2.holdout.filled == job2.holdout.size == 64 and spill == held - 64 > 0
+    assert job2.counters["records"] == sum(sd["counters"]["records"] for sd in sds)
+    job2.tick()  # the spilled holdout rows are trained on (not held out again)
+    assert job2.pipes[1].learner.running_totals()["fitted"] >= int(sum(fit)) + spill

@@ -97,15 +97,42 @@ def test_hip_gram_mfma_vs_fp64(cuda, B, d):
     y[::7] = float("nan")
     ld = ((d + 2 + 31) // 32) * 32
     G = torch.zeros(ld, ld, device=cuda)
-    cnt = torch.zeros(1, device=cuda)
+    # the running total starts past 2^31: an fp32 total would drop these increments
+    base = float(2 ** 31 + 3)
+    cnt = torch.full((1,), base, dtype=torch.float64, device=cuda)
     D.gram_update(x.to(cuda), y.to(cuda), G, cnt=cnt)
     ok = ~torch.isnan(y)
-    assert float(cnt) == float(ok.sum())  # fitted-row count from the (d, d) entry
+    assert float(cnt) - base == float(ok.sum())  # fitted-row count from the (d, d) entry
     z = torch.cat([x[ok], torch.ones(int(ok.sum()), 1), y[ok].unsqueeze(1)], 1).double()
     ref = (z.T @ z).numpy()
     got = G.cpu().double().numpy()[: d + 2, : d + 2]
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-2)
     assert float(G[d + 2:, :].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("name,task,hyper", [("ORR", 1, {}), ("K-means", 0, {"k": 3}),
+                                              ("NN", 0, {}), ("SVM", 1, {}),
+                                              ("MultiClassPA", 2, {"nClasses": 3})])
+def test_fitted_count_keeps_counting_past_2_31(name, task, hyper, device="cpu"):
+    """Running totals are fp64: a count already past 2^31 still grows by every row
+    (fp32 would round increments of < 2^7 away)."""
+    L = make_learner(name, dict(hyper, _inDim=SP.dn), SP, device)
+    assert L.cum.dtype == torch.float64
+    base = 2 ** 31 + 5
+    L.cum[1] = base
+    b = synth_batch(SP, 96, task=task, n_classes=3).to(device)
+    L.fit(b, RoundContext(spokes=4))
+    assert L.running_totals()["fitted"] == base + 96
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,task,hyper", [("ORR", 1, {}), ("K-means", 0, {"k": 3}),
+                                              ("NN", 0, {}), ("SVM", 1, {}),
+                                              ("MultiClassPA", 2, {"nClasses": 3}),
+                                              ("HT", 2, {"nClasses": 3})])
+def test_hip_fitted_count_keeps_counting_past_2_31(cuda, name, task, hyper):
+    """The kernels add their per-round counts into the fp64 running totals."""
+    test_fitted_count_keeps_counting_past_2_31(name, task, hyper, device=cuda)
 
 
 @pytest.mark.gpu
@@ -364,7 +391,7 @@ def test_hip_hoeffding_sorted_update_matches_atomic(cuda):
     outs = []
     for sort in (True, False):
         tree = [t.clone() for t in base]
-        nfit = torch.zeros(1, device=cuda)
+        nfit = torch.zeros(1, dtype=torch.float64, device=cuda)
         D.ht_update(xs, ys, 3, L.depth, tree, nfit, N=L.N, sort=sort)
         torch.cuda.synchronize()
         outs.append((tree, float(nfit)))

@@ -167,7 +167,7 @@ def test_hip_round_matches_cpu(cuda, rule, shape):
     L.linear_round(w, b, R, S, d_cpu, s_cpu, rule, 1.0)
     d_gpu = torch.zeros(sp.dim + 2, device=cuda)
     s_gpu = torch.zeros(S, 6, device=cuda)
-    cum = torch.zeros(8, device=cuda)
+    cum = torch.zeros(8, dtype=torch.float64, device=cuda)
     L.linear_round(w.to(cuda), b.to(cuda), R, S, d_gpu, s_gpu, rule, 1.0, log2cap=13, cum=cum)
     torch.cuda.synchronize()
     s_g = s_gpu.cpu()

@@ -205,3 +205,53 @@ def test_ssp_world8_replicas_agree():
     for r in res[1:]:
         assert same(r["final"], res[0]["final"])
         assert same(r["_E"], res[0]["_E"])
+
+
+def _ckpt_worker(rank, world, port, out, learner, proto, cfg, rounds, split, B, task):
+    """Run ``rounds`` rounds; when ``split`` ≥ 0 checkpoint after that many rounds, build a
+    fresh learner + protocol from the saved state (a restore) and continue on it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ["OMLDM_CPU_THREADS"] = "1"
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm()
+    L = make_learner(learner, {}, SP, "cpu")
+    P = make_protocol(proto, comm, L, cfg, spokes=2, max_msg_params=1000)
+    for r in range(rounds):
+        if r == split:
+            f = os.path.join(out, f"ck{rank}.pt")
+            torch.save({"learner": L.state_dict(), "protocol": P.state_dict()}, f)
+            sd = torch.load(f, weights_only=True)
+            L = make_learner(learner, {}, SP, "cpu")
+            P = make_protocol(proto, comm, L, cfg, spokes=2, max_msg_params=1000)
+            L.load_state_dict(sd["learner"])
+            P.load_state_dict(sd["protocol"])
+        b = synth_batch(SP, B, start=(r * world + rank) * B, task=task)
+        P.round(b)
+    torch.save({"E": P._E.clone(), "final": L.state_vector().clone(),
+                "stats": P.stats.as_dict()}, os.path.join(out, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_ckpt(proto, cfg, split, learner="ORR", rounds=8, task=1):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ckpt_worker, args=(2, _free_port(), d, learner, proto, cfg, rounds,
+                                               split, 128, task), nprocs=2, start_method="fork")
+        return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(2)]
+
+
+@pytest.mark.parametrize("proto", ["GM", "FGM"])
+def test_monitoring_protocols_checkpoint_mid_run(proto):
+    """A GM/FGM checkpoint taken between syncs (local models differ) restores the shared
+    estimate E and the round state: the estimates stay bitwise equal on all ranks and
+    the run is bitwise the run without the restore."""
+    cfg = {"threshold": 0.02, "epsilon": 0.02}
+    ref = _run_ckpt(proto, cfg, split=-1)
+    res = _run_ckpt(proto, cfg, split=3)
+    assert torch.equal(res[0]["E"], res[1]["E"])
+    for r in range(2):
+        assert torch.equal(res[r]["E"], ref[r]["E"])
+        assert torch.equal(res[r]["final"], ref[r]["final"])
+        assert res[r]["stats"]["syncs"] == ref[r]["stats"]["syncs"]
+    assert ref[0]["stats"]["syncs"] >= 1
