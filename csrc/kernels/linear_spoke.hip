@@ -95,7 +95,8 @@ struct Step {
 };
 
 // ablate (timing diagnostics only): bit0 skip the table flush, bit1 skip the sequential
-// phase, bit2 skip the w0 gathers, bit3 skip the LDS table probes.
+// phase, bit2 skip the w0 gathers, bit3 skip the LDS table probes; bit4 selects this
+// kernel where the register-dedup kernel (below) would run (exact either way).
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void linear_round_kernel(
     const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
@@ -279,7 +280,8 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     // (slot i of spoke s → [q = i >> seg][s][i & (2^seg − 1)], full-line segments)
     const int seg_log2 = (g.log2cap - g.log2nb) + g.lgg;
     const size_t S_tot = gridDim.x;
-    for (int i = lane; i < cap; i += kWave) {
+    const int used = (int)min((long long)g.qused << seg_log2, (long long)cap);
+    for (int i = lane; i < used; i += kWave) {
       const size_t q = (size_t)(i >> seg_log2);
       tables[((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1))] =
           make_int2(keys[i], __float_as_int(vals[i] * scale));
@@ -305,6 +307,215 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
     wrow[7] = p.inv_p;
     if (!p.bias) wrow[kWsStat + dn] = 0.f;  // intercept column unused
   }
+}
+
+// Diagnostics only (csrc/tests/rd_stamp_probe.hip builds with OMLDM_RD_STAMPS): per-spoke
+// phase timestamps of linear_round_rd_kernel, each after a full wait on the wave's
+// memory operations, so a phase's time includes its latency.
+#ifdef OMLDM_RD_STAMPS
+__device__ unsigned long long* g_rd_stamps;
+#define RD_STAMP(k)                                                              \
+  do {                                                                           \
+    __builtin_amdgcn_s_waitcnt(0);                                               \
+    if (lane == 0) g_rd_stamps[(size_t)s * 8 + (k)] = (k) == 0 ? wall_clock64() : clock64(); \
+  } while (0)
+#else
+#define RD_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
+// Register-dedup round (field-aware compact wire, ≤ RMAX rows per spoke, ≤ 64 features).
+//
+// On the field-aware wire lane f only ever sees keys of field f (slot ranges of different
+// fields, the numerical slots and the intercept are disjoint), so a spoke's delta for a
+// key lives with ONE lane, and a spoke's R rows are few: the whole spoke fits in
+// registers. Each lane keeps its R keys, values and round-start weights, and d[e] = the
+// delta of row e's key as row e sees it. After row e's closed-form step u = c·x_e, the
+// lane adds u to d[e'] of every later row e' with the same key (compile-time indices:
+// plain VALU compares/selects, no LDS on the sequential chain, no hash probes, no CAS,
+// no table overflow). This is the same per-key accumulation order as the LDS table, so
+// the deltas are bitwise those of linear_round_kernel.
+// At round end the last occurrence of each key holds its total delta; those go into an
+// LDS staging image with the round kernel's bucketed layout (one LDS atomic counter per
+// bucket; a bucket that is full sends its extra keys to the accumulator with an L2
+// atomic — exact, nothing is dropped) and leave with the same coalesced group-major flush,
+// so linear_reduce_kernel is unchanged.
+template <int RMAX, int RULE, typename NumT, typename WT>
+__global__ __launch_bounds__(64, 5) void linear_round_rd_kernel(
+    const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
+    int dc, const void* __restrict__ yv, int B, int R, int dim, float* __restrict__ ws,
+    int2* __restrict__ tables, float* __restrict__ dacc, LinParams p, TableGeom g, int ablate) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int cap = 1 << g.log2cap;
+  const int nbk = 1 << g.log2nb;
+  const int bs_log2 = g.log2cap - g.log2nb;
+  int2* tab = reinterpret_cast<int2*>(smem);                     // [cap] staging image
+  int* bcnt = reinterpret_cast<int*>(smem + (size_t)cap * 8);     // [nbk / 2] bucket fill
+  int* dummy = bcnt + ((nbk + 1) >> 1);                           // [64] no-op atomics
+  const int lane = threadIdx.x;
+  const int s = blockIdx.x;
+  const int wsw = kWsStat + dn + 1;
+  float* wrow = ws + (size_t)s * wsw;
+  RD_STAMP(0);
+  RD_STAMP(1);
+  const long long t0ll = (long long)s * R;
+  const int t0 = t0ll > B ? B : (int)t0ll;
+  const int t1 = (t0ll + R) > B ? B : (int)(t0ll + R);
+  if (t0 >= t1) {  // idle spoke: not a worker of this round
+    for (int k = lane; k < wsw; k += kWave) wrow[k] = k == 4 ? 1.f : 0.f;
+    return;
+  }
+  // the spoke's rows, every load in flight at once: branch-free loads from clamped (always
+  // valid) addresses, decoded only after the last one is issued — a load inside a
+  // lane-divergent branch is waited for inside it, which serialised the rows.
+  // Row e's label sits in lane e (one VGPR for all labels, v_readlane on the chain).
+  // one unconditional aligned dword per lane: the fp32 label, or the word holding the
+  // int8 label (a wave-uniform branch around the load made the wave wait inside it)
+  const int ty = min(t0 + lane, t1 - 1);
+  const uintptr_t ya = reinterpret_cast<uintptr_t>(yv) + (p.y_i8 ? (uintptr_t)ty : (uintptr_t)ty * 4);
+  const uint32_t yword = *reinterpret_cast<const uint32_t*>(ya & ~uintptr_t(3));
+  const bool is_num = lane < dn;
+  const bool is_cat = lane >= dn && lane < dn + dc;
+  const bool is_bias = p.bias && lane == dn + dc;
+  const int jn = is_num ? lane : 0;
+  const int jc = is_cat ? lane - dn : 0;
+  // one 16-bit load per row and lane when the numericals are bf16 (lane-dependent base and
+  // stride: numerical slot or categorical field), two loads otherwise
+  unsigned short raw[RMAX];
+  NumT nraw[sizeof(NumT) == 2 ? 1 : RMAX];
+  if constexpr (sizeof(NumT) == 2) {
+    const unsigned short* base = is_num ? reinterpret_cast<const unsigned short*>(num) + jn
+                                        : static_cast<const unsigned short*>(cat) + jc;
+    const int stride = is_num ? dn : dc;
+#pragma unroll
+    for (int e = 0; e < RMAX; ++e) raw[e] = base[(size_t)min(t0 + e, t1 - 1) * stride];
+  } else {
+#pragma unroll
+    for (int e = 0; e < RMAX; ++e) {
+      const int t = min(t0 + e, t1 - 1);
+      nraw[e] = num[(size_t)t * dn + jn];
+      raw[e] = static_cast<const unsigned short*>(cat)[(size_t)t * dc + jc];
+    }
+  }
+  int key[RMAX];
+  float xv[RMAX], wv[RMAX], d[RMAX];
+  const int cbase = dn + jc * p.cspan;
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) {
+    const unsigned c = raw[e];
+    float nv;
+    if constexpr (sizeof(NumT) == 2) nv = __uint_as_float(c << 16);  // bf16 bits
+    else nv = to_f(nraw[e]);
+    int idx = is_num ? lane : is_bias ? dim - 1 : (is_cat && c != 0xFFFFu) ? cbase + (int)(c & 0x7fffu) : -1;
+    const float v = is_num ? nv : is_bias ? 1.f : (c & 0x8000u) ? -1.f : 1.f;
+    if ((unsigned)idx >= (unsigned)dim || t0 + e >= t1) idx = -1;
+    key[e] = idx;
+    xv[e] = idx >= 0 ? v : 0.f;
+    d[e] = 0.f;
+  }
+  const float yraw = p.y_i8 ? (float)(signed char)(yword >> (8 * (ya & 3))) : __uint_as_float(yword);
+  const float ylane = lane < t1 - t0 ? yraw : __builtin_nanf("");
+  RD_STAMP(2);
+  // staging image init overlaps the gathers
+  for (int i = lane; i < cap; i += kWave) tab[i] = make_int2(kEmptyKey, 0);
+  for (int i = lane; i < (nbk + 1) >> 1; i += kWave) bcnt[i] = 0;
+  // round-start weights (read-only for the round; the bf16 shadow sits in L2), gathered
+  // unconditionally (absent features read slot 0 and are zeroed after)
+  WT wraw[RMAX];
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) wraw[e] = w[key[e] >= 0 ? key[e] : 0];
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) wv[e] = key[e] >= 0 ? to_f(wraw[e]) : 0.f;
+  RD_STAMP(3);
+  const int dcol = dense_col(lane, dn, dc, p.bias);
+  float sigma = 1.f, rsig = 1.f, loss_sum = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f;
+  // ‖x_e‖² does not depend on the updates: every row's norm first (independent
+  // reductions, off the sequential chain)
+  float pn[RMAX];
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) pn[e] = wave_sum(xv[e] * xv[e]);
+  // exact sequential online updates, all in registers
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) {
+    const float y = readlane_f(ylane, e);
+    if (__builtin_isnan(y)) continue;  // wave-uniform (rows past t1 are NaN too)
+    const float pm = wave_sum(xv[e] * (wv[e] + d[e]));
+    float c;
+    Step<RULE>::run(sigma * pm, y, pn[e], p, loss_sum, mist, sqe, c);
+    nex += 1.f;
+    sigma *= p.shrink;
+    rsig *= p.rshrink;
+    if (c != 0.f) {  // wave-uniform
+      const float u = (c * rsig) * xv[e];
+      d[e] += u;
+#pragma unroll
+      for (int e2 = e + 1; e2 < RMAX; ++e2) d[e2] += key[e2] == key[e] ? u : 0.f;
+    }
+  }
+  RD_STAMP(4);
+  __syncthreads();  // staging image initialised
+  const float scale = sigma * p.inv_p;
+  float dense_total = 0.f, ovf = 0.f;
+  // The last occurrence of a key carries its total delta. Its bucket position comes from
+  // an LDS counter; every lane issues all RMAX counter atomics back to back (lanes with
+  // nothing to place add 0 to a private dummy word: no branch to wait inside, no
+  // same-address serialisation), then places its entries.
+  int pos[RMAX];
+  bool emit[RMAX];
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) {
+    bool last = key[e] >= 0;
+#pragma unroll
+    for (int e2 = e + 1; e2 < RMAX; ++e2) last = last && key[e2] != key[e];
+    last = last && d[e] != 0.f;
+    if (dcol >= 0 && last) dense_total = d[e];
+    emit[e] = last && dcol < 0 && !(ablate & 1);
+    const int b = emit[e] ? key[e] >> g.kshift : 0;
+    const int sh = 16 * (b & 1);
+    // 16-bit counters, two buckets per word: a spoke has at most 64 × RMAX ≤ 1024 keys,
+    // so a half-word never carries into its neighbour
+    int* ctr = emit[e] ? &bcnt[b >> 1] : &dummy[lane];
+    pos[e] = (atomicAdd(ctr, emit[e] ? 1 << sh : 0) >> sh) & 0xffff;
+  }
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) {
+    if (emit[e]) {
+      const int b = key[e] >> g.kshift;
+      const float v = d[e] * scale;
+      if (pos[e] < (1 << bs_log2)) {
+        tab[(b << bs_log2) + pos[e]] = make_int2(key[e], __float_as_int(v));
+      } else {  // bucket full: straight to the accumulator (exact)
+        unsafeAtomicAdd(&dacc[key[e]], v);
+        ovf += 1.f;
+      }
+    }
+  }
+  __syncthreads();
+  RD_STAMP(5);
+  if (!(ablate & 1)) {
+    const int seg_log2 = bs_log2 + g.lgg;
+    const size_t S_tot = gridDim.x;
+    const int used = min(cap, (int)min((long long)g.qused << seg_log2, (long long)cap));
+    for (int i = lane; i < used; i += kWave) {
+      const size_t q = (size_t)(i >> seg_log2);
+      tables[((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1))] = tab[i];
+    }
+  }
+  if (dcol >= 0) wrow[kWsStat + dcol] = dense_total * scale;
+  (void)ovf;  // spilled keys went to the accumulator: nothing was dropped
+  if (lane == 0) {
+    wrow[0] = loss_sum;
+    wrow[1] = nex;
+    wrow[2] = mist;
+    wrow[3] = sqe;
+    wrow[4] = sigma;
+    wrow[5] = 0.f;  // dropped updates (none on this path)
+    wrow[6] = scale;
+    wrow[7] = p.inv_p;
+    if (!p.bias) wrow[kWsStat + dn] = 0.f;
+  }
+  RD_STAMP(6);
 }
 
 // Column sums of the per-spoke workspace (one block per column) → accumulator slots
@@ -514,7 +725,8 @@ static int launch_reduce(const int2* tables, int B, int R, int S, TableGeom g, i
   const int gspan_log2 = g.kshift + g.lgg;
   const int ng = (!(ablate & 1) && S_act > 0) ? (dim + (1 << gspan_log2) - 1) >> gspan_log2 : 0;
   const int q0 = (int)((long long)ng * part / parts);
-  const int q1 = (int)((long long)ng * (part + 1) / parts);
+  // part slices follow dim alone (every rank agrees); groups past qused hold no keys
+  const int q1 = min((int)((long long)ng * (part + 1) / parts), max(q0, g.qused));
   const int split = ng ? reduce_split(ng, S_act) : 1;
   const int nb = (q1 - q0) * split;
   const int nfin = part == 0 ? kWsStat + dn + 1 : 0;
@@ -558,6 +770,54 @@ static int launch_round(const void* w, const void* num, int dn, const void* cat,
   return launch_reduce(tables, B, R, S, g, dim, dacc, ws, dn, cum, 0, parts, ablate, st);
 }
 
+template <int RMAX, int RULE, typename NumT, typename WT>
+static int launch_round_rd(const void* w, const void* num, int dn, const void* cat, int dc,
+                           const void* y, int B, int R, int S, float* dacc, int dim, float* ws,
+                           int2* tables, double* cum, const LinParams& p, TableGeom g, int ablate,
+                           int parts, hipStream_t st) {
+  auto fn = linear_round_rd_kernel<RMAX, RULE, NumT, WT>;
+  const size_t lds =
+      (size_t(1) << g.log2cap) * 8 + (((size_t(1) << g.log2nb) + 1) / 2) * 4 + kWave * 4;
+  int e = check_dyn_lds((const void*)fn, lds);
+  if (e) return e;
+  hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)w, (const NumT*)num, dn, cat, dc,
+                     y, B, R, dim, ws, tables, dacc, p, g, ablate);
+  e = (int)hipGetLastError();
+  if (e) return e;
+  return launch_reduce(tables, B, R, S, g, dim, dacc, ws, dn, cum, 0, parts, ablate, st);
+}
+
+// Register-dedup path (linear_round_rd_kernel): field-aware compact wire, ≤ 64 features,
+// ≤ 16 rows per spoke. ablate bit 4 (or OMLDM_LINEAR_RD=0) forces the LDS-hash-table
+// kernel (A/B and equality tests).
+static bool use_rd_path(int cspan, int F, int R, int ablate) {
+  if (cspan <= 0 || F > 64 || R > 16 || R < 1 || (ablate & 16)) return false;
+  const char* e = getenv("OMLDM_LINEAR_RD");
+  return !(e && atoi(e) == 0);
+}
+
+template <int RULE>
+static int dispatch_round_rd(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
+                             const void* cat, int dc, const void* y, int B, int R, int S,
+                             float* dacc, int dim, float* ws, int2* tables, double* cum,
+                             const LinParams& p, TableGeom g, int ablate, int parts,
+                             hipStream_t st) {
+#define OMLDM_RD(RM, NT, WTT)                                                                  \
+  return launch_round_rd<RM, RULE, NT, WTT>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, ws,  \
+                                            tables, cum, p, g, ablate, parts, st)
+#define OMLDM_RD_R(NT, WTT) \
+  if (R <= 8) OMLDM_RD(8, NT, WTT); \
+  OMLDM_RD(16, NT, WTT)
+  if (num_bf16) {
+    if (w_bf16) { OMLDM_RD_R(__hip_bfloat16, __hip_bfloat16); }
+    OMLDM_RD_R(__hip_bfloat16, float);
+  }
+  if (w_bf16) { OMLDM_RD_R(float, __hip_bfloat16); }
+  OMLDM_RD_R(float, float);
+#undef OMLDM_RD_R
+#undef OMLDM_RD
+}
+
 template <int FPL, int CH, int RULE>
 static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                           const void* cat, int dc, const void* y, int B, int R, int S, float* dacc,
@@ -581,6 +841,17 @@ static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, i
                          float* dacc, int dim, float* ws, int2* tables, double* cum,
                          const LinParams& p, TableGeom g, int ablate, int parts,
                          hipStream_t st) {
+  if (FPL == 1 && use_rd_path(p.cspan, dn + dc + (p.bias ? 1 : 0), R, ablate)) {
+    if (rule == kHinge)
+      return dispatch_round_rd<kHinge>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
+                                       dim, ws, tables, cum, p, g, ablate, parts, st);
+    if (rule == kEpsInsensitive)
+      return dispatch_round_rd<kEpsInsensitive>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
+                                                dacc, dim, ws, tables, cum, p, g, ablate, parts,
+                                                st);
+    return dispatch_round_rd<kLogistic>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
+                                        dim, ws, tables, cum, p, g, ablate, parts, st);
+  }
   if (rule == kHinge)
     return dispatch_round<FPL, CH, kHinge>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
                                            dim, ws, tables, cum, p, g, ablate, parts, st);
@@ -634,6 +905,15 @@ static int ceil_log2(long long x) {
   return k;
 }
 
+// Key groups that can hold hashed keys: all of them, except on the field-aware wire
+// (cspan > 0), whose categorical slots end at dn + dc·cspan.
+static int used_groups(int dim, int dn, int dc, int cspan, const TableGeom& g) {
+  const int gl = g.kshift + g.lgg;
+  const long long hi = cspan > 0 ? (long long)dn + (long long)dc * cspan : (long long)dim;
+  const long long lim = hi < dim ? hi : dim;
+  return (int)((lim + (1LL << gl) - 1) >> gl);
+}
+
 // Table geometry for a hash dimension: bucket span ≤ 4096 keys (16 KiB LDS in the
 // reducer), ≥ 4 slots per bucket. Returns false when log2cap is too small.
 OMLDM_API int omldm_linear_table_geom(int dim, int log2cap, int* out3) {
@@ -671,8 +951,9 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
   if (parts < 1 || parts > 64) return -4;
   int geo[3];
   if (omldm_linear_table_geom(dim, log2cap, geo)) return -3;
-  const TableGeom g{geo[0], geo[1], geo[2], reduce_lgg(geo[2], geo[1])};
+  TableGeom g{geo[0], geo[1], geo[2], reduce_lgg(geo[2], geo[1])};
   if ((g.log2cap - g.log2nb) + g.lgg < 1) return -3;  // ≥ 2 slots per segment (int4 loads)
+  g.qused = used_groups(dim, dn, dc, cspan, g);
   const float shrink = rule == kLogistic ? 1.f - lr * lam : 1.f - lam;
   const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias, cspan,
                     variant == kPA1 ? C : INFINITY, variant == kPA2 ? 0.5f / C : 0.f, shrink,
@@ -690,13 +971,15 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
 // Reduce part `part` (1 ≤ part < parts) of the round launched by omldm_linear_round with
 // the same arguments; part 0 was launched by the round call itself.
 OMLDM_API int omldm_linear_reduce_part(void* tables, float* ws, double* cum, float* dacc, int dim,
-                                       int dn, int B, int R, int S, int log2cap, int part,
-                                       int parts, int ablate, void* stream) {
+                                       int dn, int dc, int cspan, int B, int R, int S,
+                                       int log2cap, int part, int parts, int ablate,
+                                       void* stream) {
   if (S <= 0) return 0;
   if (parts < 1 || parts > 64 || part < 1 || part >= parts) return -4;
   int geo[3];
   if (omldm_linear_table_geom(dim, log2cap, geo)) return -3;
-  const TableGeom g{geo[0], geo[1], geo[2], reduce_lgg(geo[2], geo[1])};
+  TableGeom g{geo[0], geo[1], geo[2], reduce_lgg(geo[2], geo[1])};
+  g.qused = used_groups(dim, dn, dc, cspan, g);
   return launch_reduce((const int2*)tables, B, R, S, g, dim, dacc, ws, dn, cum, part, parts,
                        ablate, (hipStream_t)stream);
 }

@@ -20,6 +20,10 @@ struct TableGeom {
   int log2nb;
   int kshift;
   int lgg;  // log2 buckets per reduce group (flush layout: [group][spoke][2^lgg · BS])
+  // key groups that can hold hashed keys at all: on the field-aware wire the categorical
+  // slots end at dn + dc·cspan, so the groups above are empty in every table — neither
+  // flushed nor reduced
+  int qused = 1 << 30;
 };
 constexpr int kOvf = 64;
 

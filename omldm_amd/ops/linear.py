@@ -119,8 +119,8 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
             on_part(0, *part_bounds(dim, 0, parts, cuda=True))
         for k in range(1, parts):
             rc = native.hip().omldm_linear_reduce_part(
-                ptr(tables), ptr(ws), ptr(cum), ptr(dacc), dim, num.shape[1], batch.B, R, S,
-                log2cap, k, parts, int(ablate), native.stream_of(w))
+                ptr(tables), ptr(ws), ptr(cum), ptr(dacc), dim, num.shape[1], cat.shape[1],
+                batch.cat_span, batch.B, R, S, log2cap, k, parts, int(ablate), native.stream_of(w))
             check(rc, "omldm_linear_reduce_part")
             if on_part is not None:
                 on_part(k, *part_bounds(dim, k, parts, cuda=True))

@@ -45,7 +45,7 @@ HIP_SIGS = [
                                  vp, vp, i32, i32, f32, f32, f32, f32, f32, i32, i32, i32, i32,
                                  i32, i32, vp]),
     ("omldm_linear_reduce_part", i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,
-                                       i32, vp]),
+                                       i32, i32, i32, vp]),
     ("omldm_linear_part_bounds", i32, [i32, i32, i32, vp]),
     ("omldm_linear_table_geom", i32, [i32, i32, vp]),
     ("omldm_linear_predict", i32, [vp, i32, i64, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32,

@@ -301,3 +301,37 @@ def test_hip_round_int8_labels(cuda, rule):
     torch.cuda.synchronize()
     np.testing.assert_allclose(d8.cpu().numpy(), d32.cpu().numpy(), rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(d8.cpu().numpy(), dc.numpy(), rtol=2e-3, atol=2e-4)
+
+
+RD_TABLE = 16  # ablate bit: force the LDS-hash-table round kernel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule", RULES)
+@pytest.mark.parametrize("R,S", [(16, 64), (13, 40), (8, 50), (5, 33), (1, 70)])
+@pytest.mark.parametrize("model_dtype", [torch.float32, torch.bfloat16])
+def test_hip_register_dedup_round_matches_table_kernel_and_cpu(cuda, rule, R, S, model_dtype):
+    """Field-aware compact wire, ≤ 16 rows per spoke: the register-dedup round kernel
+    (deltas in registers, no LDS hash table) gives the LDS-table kernel's round and the
+    CPU round. Stats (loss, n, mistakes, sq_err, σ) agree too; the last spokes are idle."""
+    sp = FeatureSpace(13, 0, 26, 1 << 16, field_aware=True)
+    task = TASK_REGRESSION if rule.rule == L.RULE_EPS else TASK_BINARY
+    B = S * R - R // 2 - 1  # ragged last spoke
+    b = synth_batch(sp, B, seed=R * 131 + S, task=task)
+    w = (torch.randn(sp.dim) * 0.02).to(model_dtype).float()
+    out = {}
+    for name, ablate in (("rd", 0), ("table", RD_TABLE)):
+        d = torch.zeros(sp.dim + 2, device=cuda)
+        st = torch.zeros(S, 6, device=cuda)
+        L.linear_round(w.to(cuda).to(model_dtype), b.to(cuda), R, S, d, st, rule, 1.0,
+                       ablate=ablate)
+        out[name] = (d.cpu(), st.cpu())
+    d_cpu = torch.zeros(sp.dim + 2)
+    s_cpu = torch.zeros(S, 6)
+    L.linear_round(w, b, R, S, d_cpu, s_cpu, rule, 1.0)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out["rd"][0].numpy(), out["table"][0].numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(out["rd"][1][:, :5].numpy(), out["table"][1][:, :5].numpy(),
+                               rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(out["rd"][0].numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
+    np.testing.assert_allclose(out["rd"][1][:, 1].numpy(), s_cpu[:, 1].numpy())
