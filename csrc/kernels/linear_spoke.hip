@@ -522,18 +522,21 @@ __global__ __launch_bounds__(64, 5) void linear_round_rd_kernel(
 // that every spoke would otherwise hit with same-address atomics:
 //   dense columns → dacc[0:dn], intercept → dacc[dim-1], Σσ/P → dacc[dim],
 //   Σ1/P → dacc[dim+1], loss/n/mistakes/sq_err/overflow → cum (device running totals).
+template <int NT>
 __device__ __forceinline__ void finish_column(int c, const float* __restrict__ ws, int S, int dn,
                                               int dim, float* __restrict__ dacc,
                                               double* __restrict__ cum) {
-  __shared__ float part[4];
+  __shared__ float part[NT / 64];
   const int wsw = kWsStat + dn + 1;
   float acc = 0.f;
-  for (int s = threadIdx.x; s < S; s += 256) acc += ws[(size_t)s * wsw + c];
+  for (int s = threadIdx.x; s < S; s += NT) acc += ws[(size_t)s * wsw + c];
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float t = (part[0] + part[1]) + (part[2] + part[3]);
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < NT / 64; ++k) t += part[k];
     if (c < kWsStat) {
       if (c == 6) dacc[dim] = t;       // the round's counters (apply does not clear them)
       else if (c == 7) dacc[dim + 1] = t;
@@ -552,13 +555,14 @@ __device__ __forceinline__ void finish_column(int c, const float* __restrict__ w
 // non-zero slots to the accumulator (which the apply pass left at zero; overflow entries
 // were added by the round kernel). Blocks [nb, nb + wsw): workspace column sums. Hashed
 // keys never map to dense / intercept slots, so the two block kinds touch disjoint slots.
-__global__ __launch_bounds__(256) void linear_reduce_kernel(
+template <int NT>
+__global__ __launch_bounds__(NT) void linear_reduce_kernel(
     const int2* __restrict__ tables, int S_act, TableGeom g, int dim, float* __restrict__ dacc,
     int nb, int split, int q0, const float* __restrict__ ws, int S, int dn,
     double* __restrict__ cum) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if ((int)blockIdx.x >= nb) {
-    finish_column(blockIdx.x - nb, ws, S, dn, dim, dacc, cum);
+    finish_column<NT>(blockIdx.x - nb, ws, S, dn, dim, dacc, cum);
     return;
   }
   float* acc = reinterpret_cast<float*>(smem);
@@ -567,7 +571,7 @@ __global__ __launch_bounds__(256) void linear_reduce_kernel(
   const int part = (int)blockIdx.x % split;    // this block's share of the spokes
   const int s_lo = (int)(((long long)S_act * part) / split);
   const int s_hi = (int)(((long long)S_act * (part + 1)) / split);
-  for (int i = threadIdx.x; i < span; i += 256) acc[i] = 0.f;
+  for (int i = threadIdx.x; i < span; i += NT) acc[i] = 0.f;
   __syncthreads();
   const int seg_log2 = (g.log2cap - g.log2nb) + g.lgg;
   const int lo = q << (g.kshift + g.lgg);
@@ -579,30 +583,30 @@ __global__ __launch_bounds__(256) void linear_reduce_kernel(
                    (((size_t)q * S + s_lo) << (seg_log2 - 1));
   auto addr = [](long long ii) { return (size_t)ii; };
   long long it = threadIdx.x;
-  for (; it + 3 * 256 < items; it += 4 * 256) {
+  for (; it + 3 * NT < items; it += 4 * NT) {
     int4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = t4[addr(it + u * 256)];
+    for (int u = 0; u < 4; ++u) v[u] = t4[addr(it + u * NT)];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (v[u].x >= 0) atomicAdd(&acc[v[u].x - lo], __int_as_float(v[u].y));
       if (v[u].z >= 0) atomicAdd(&acc[v[u].z - lo], __int_as_float(v[u].w));
     }
   }
-  for (; it < items; it += 256) {
+  for (; it < items; it += NT) {
     const int4 v = t4[addr(it)];
     if (v.x >= 0) atomicAdd(&acc[v.x - lo], __int_as_float(v.y));
     if (v.z >= 0) atomicAdd(&acc[v.z - lo], __int_as_float(v.w));
   }
   __syncthreads();
   if (split == 1) {  // sole owner of the key range
-    for (int i = threadIdx.x; i < span; i += 256) {
+    for (int i = threadIdx.x; i < span; i += NT) {
       const int k = lo + i;
       const float v = acc[i];
       if (k < dim && v != 0.f) dacc[k] += v;
     }
   } else {  // the group's parts meet in L2 (hardware fp32 atomics, no return value)
-    for (int i = threadIdx.x; i < span; i += 256) {
+    for (int i = threadIdx.x; i < span; i += NT) {
       const int k = lo + i;
       const float v = acc[i];
       if (k < dim && v != 0.f) unsafeAtomicAdd(&dacc[k], v);
@@ -624,6 +628,37 @@ static inline int reduce_split(int ngroups, int S_act) {
   if (sp > 16) sp = 16;
   while (sp > 1 && sp > S_act) sp >>= 1;
   return sp;
+}
+
+// Threads per reduce block (diagnostics sweep: OMLDM_REDUCE_THREADS = 256 | 512 | 1024).
+static inline int reduce_threads() {
+  int nt = 256;
+  if (const char* e = getenv("OMLDM_REDUCE_THREADS")) nt = atoi(e);
+  return nt == 1024 ? 1024 : nt == 512 ? 512 : 256;
+}
+
+template <int NT>
+static int launch_reduce_t(dim3 grid, size_t lds, hipStream_t st, const int2* tables, int S_act,
+                           TableGeom g, int dim, float* dacc, int nb, int split, int q0,
+                           const float* ws, int S, int dn, double* cum) {
+  int e = check_dyn_lds((const void*)linear_reduce_kernel<NT>, lds);
+  if (e) return e;
+  hipLaunchKernelGGL(linear_reduce_kernel<NT>, grid, dim3(NT), lds, st, tables, S_act, g, dim, dacc,
+                     nb, split, q0, ws, S, dn, cum);
+  return (int)hipGetLastError();
+}
+
+static int launch_reduce_nt(int nt, dim3 grid, size_t lds, hipStream_t st, const int2* tables,
+                            int S_act, TableGeom g, int dim, float* dacc, int nb, int split, int q0,
+                            const float* ws, int S, int dn, double* cum) {
+  if (nt == 1024)
+    return launch_reduce_t<1024>(grid, lds, st, tables, S_act, g, dim, dacc, nb, split, q0, ws, S,
+                                 dn, cum);
+  if (nt == 512)
+    return launch_reduce_t<512>(grid, lds, st, tables, S_act, g, dim, dacc, nb, split, q0, ws, S,
+                                dn, cum);
+  return launch_reduce_t<256>(grid, lds, st, tables, S_act, g, dim, dacc, nb, split, q0, ws, S, dn,
+                              cum);
 }
 
 static inline int reduce_lgg(int kshift, int log2nb) {
@@ -732,11 +767,8 @@ static int launch_reduce(const int2* tables, int B, int R, int S, TableGeom g, i
   const int nfin = part == 0 ? kWsStat + dn + 1 : 0;
   if (nb + nfin == 0) return 0;
   const size_t rlds = nb ? (size_t(1) << gspan_log2) * 4 : 0;
-  int e = check_dyn_lds((const void*)linear_reduce_kernel, rlds);
-  if (e) return e;
-  hipLaunchKernelGGL(linear_reduce_kernel, dim3(nb + nfin), dim3(256), rlds, st, tables, S_act,
-                     g, dim, dacc, nb, split, q0, ws, S, dn, cum);
-  return (int)hipGetLastError();
+  return launch_reduce_nt(reduce_threads(), dim3(nb + nfin), rlds, st, tables, S_act, g, dim, dacc,
+                          nb, split, q0, ws, S, dn, cum);
 }
 
 int bucket_reduce_launch(const int2* tables, int S_act, int S, TableGeom g, int dim,
@@ -747,11 +779,8 @@ int bucket_reduce_launch(const int2* tables, int S_act, int S, TableGeom g, int 
   const int split = reduce_split(ng, S_act);
   const int nb = (q1 - q0) * split;
   const size_t rlds = (size_t(1) << gspan_log2) * 4;
-  int e = check_dyn_lds((const void*)linear_reduce_kernel, rlds);
-  if (e) return e;
-  hipLaunchKernelGGL(linear_reduce_kernel, dim3(nb), dim3(256), rlds, st, tables, S_act, g, dim,
-                     dacc, nb, split, q0, (const float*)nullptr, S, 0, (double*)nullptr);
-  return (int)hipGetLastError();
+  return launch_reduce_nt(256, dim3(nb), rlds, st, tables, S_act, g, dim, dacc, nb, split, q0,
+                          (const float*)nullptr, S, 0, (double*)nullptr);
 }
 
 template <int FPL, int CH, int RULE, typename NumT, typename WT>
