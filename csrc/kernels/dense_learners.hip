@@ -69,6 +69,182 @@ __global__ __launch_bounds__(64) void gram_mfma_kernel(const float* __restrict__
   }
 }
 
+// ---- ORR Gram, v2: LDS-staged rows, every wave on every tile, feature map fused ------
+// gram_mfma_kernel above reads each operand straight from global memory with one scalar
+// load per lane and one 32×32 tile per wave: ≈ 4 % of the fp32 matrix-core peak (917 µs
+// for 262144 rows × 106 columns, profiles/orr_fgm_kernel_summary.txt). Here a workgroup
+// owns a contiguous row range. 64-row chunks of the RAW rows [x (d0 values), valid, y·valid,
+// 0] are staged in LDS (coalesced global reads, the next chunk's loads in flight while the
+// current one computes), and each of the 4 waves takes a quarter of the chunk's row pairs
+// for ALL upper-triangle tiles (I ≤ J) of the (NB·32)² Gram — T = NB(NB+1)/2
+// accumulators, so the waves are balanced whatever T is.
+// Column c of z is a product of two staged entries, z_c = s[pa_c]·s[pb_c], formed in the
+// operand fetch: c < d0 → x_c·valid; then the degree-2 pairs x_a·x_b of a fused
+// PolynomialFeatures(2) (pairs table; zeroed rows stay zero); then valid (the intercept
+// column), then y·valid; beyond → 0. So ORR behind PolynomialFeatures reads the d0 raw
+// features instead of the expanded d0 + d0(d0+1)/2 ones (13 → 104 floats per row) and the
+// expansion never reaches HBM. At the end the four waves' tiles are summed through LDS and
+// the block adds them to G with full-rate atomics (each accumulator register of a wave
+// covers two 128-B row segments); a second tiny launch mirrors the upper triangle into
+// the lower one. Exact fp32 products (v_mfma_f32_32x32x2_f32), like the v1 kernel (a pair
+// feature is rounded once, as the separate expansion rounds it).
+template <int NB, int EPT>
+__global__ __launch_bounds__(256) void gram_map_kernel(const float* __restrict__ x,
+                                                       const float* __restrict__ y, int B, int d0,
+                                                       const int* __restrict__ pairs, int npairs,
+                                                       int rows_per_block, float* __restrict__ G,
+                                                       int ld, double* __restrict__ cnt) {
+  constexpr int T = NB * (NB + 1) / 2;
+  constexpr int RC = 64;  // rows per staged chunk
+  constexpr int MAXW = NB * 32 + 1;
+  const int d = d0 + npairs;     // z = [mapped features (d), 1, y]
+  const int W = d0 + 3;          // staged row: x (d0), valid, y·valid, 0
+  const int LDW = W | 1;         // odd row stride: the half-waves' rows on different banks
+  const int ONE = d0, YC = d0 + 1, ZERO = d0 + 2;
+  constexpr int ZF = 2 * RC * MAXW;
+  constexpr int RF = T * 1024;  // floats of the tile-sum image
+  __shared__ float lds[ZF > RF ? ZF : RF];
+  float* xs = lds;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const long long r_begin = (long long)blockIdx.x * rows_per_block;
+  const long long r_end = min((long long)B, r_begin + rows_per_block);
+  for (int i = tid; i < 2 * RC * LDW; i += 256) xs[i] = 0.f;  // the ZERO column stays 0
+  // operand map of this lane's column in each 32-column block
+  const int half = lane >> 5, col = lane & 31;
+  int fa[NB], fb[NB];
+#pragma unroll
+  for (int I = 0; I < NB; ++I) {
+    const int c = I * 32 + col;
+    if (c < d0) {
+      fa[I] = c;
+      fb[I] = ONE;
+    } else if (c < d) {
+      fa[I] = pairs[2 * (c - d0)];
+      fb[I] = pairs[2 * (c - d0) + 1];
+    } else if (c == d) {
+      fa[I] = ONE;  // valid · valid · valid = valid
+      fb[I] = ONE;
+    } else if (c == d + 1) {
+      fa[I] = YC;
+      fb[I] = ONE;
+    } else {
+      fa[I] = ZERO;
+      fb[I] = ZERO;
+    }
+  }
+  // staging: the chunk's x values are RC·d0 contiguous floats; element slot k of this
+  // thread is e = tid + 256k, the same (row, col) in every chunk (EPT ≥ RC·d0 / 256)
+  const int nel = RC * d0;
+  int eoff[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = tid + 256 * k;
+    const int r = e < nel ? e / d0 : 0;
+    eoff[k] = e < nel ? r * LDW + (e - r * d0) : -1;
+  }
+  float xr[EPT];
+  float yr = 0.f;
+  auto load = [&](long long rc) {
+    const long long rows = min((long long)RC, r_end - rc);
+    const float* xp = x + rc * d0;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int e = tid + 256 * k;
+      xr[k] = xp[e < rows * d0 ? e : 0];  // unconditional (a load in a branch waits inside it)
+    }
+    if (tid < RC) {
+      yr = y[rc + (tid < rows ? tid : 0)];
+      if (tid >= rows) yr = __builtin_nanf("");  // past the range: excluded
+    }
+  };
+  // raw x values as they are; a row's `valid` entry (0 for a NaN target or past the
+  // range) multiplies every operand of that row (z_c = s[pa]·s[pb]·valid)
+  auto store = [&](int buf) {
+    float* b = xs + (size_t)buf * RC * LDW;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+      if (eoff[k] >= 0) b[eoff[k]] = xr[k];
+    if (tid < RC) {
+      const bool valid = !__builtin_isnan(yr);
+      b[(size_t)tid * LDW + ONE] = valid ? 1.f : 0.f;
+      b[(size_t)tid * LDW + YC] = valid ? yr : 0.f;
+    }
+  };
+  f32x16 acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  int buf = 0;
+  __syncthreads();
+  if (r_begin < r_end) {
+    load(r_begin);
+    store(0);
+  }
+  __syncthreads();
+  for (long long rc = r_begin; rc < r_end; rc += RC) {
+    const bool more = rc + RC < r_end;
+    if (more) load(rc + RC);  // in flight while this chunk computes
+    const float* xb = xs + (size_t)buf * RC * LDW;
+#pragma unroll
+    for (int kp = wave; kp < RC / 2; kp += 4) {
+      const float* xrow = xb + (size_t)(2 * kp + half) * LDW;
+      float a[NB];
+#pragma unroll
+      for (int I = 0; I < NB; ++I) a[I] = (xrow[fa[I]] * xrow[fb[I]]) * xrow[ONE];
+      int t = 0;
+#pragma unroll
+      for (int I = 0; I < NB; ++I)
+#pragma unroll
+        for (int J = I; J < NB; ++J, ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[I], a[J], acc[t], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);  // buffer buf^1 was last read two chunks ago
+    __syncthreads();
+    buf ^= 1;
+  }
+  // sum the four waves' tiles through LDS (the staging buffers are free now)
+  float* red = lds;
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float* p = red + t * 1024 + r * 64 + lane;
+          *p = (w == 0 ? 0.f : *p) + acc[t][r];
+        }
+    }
+    __syncthreads();
+  }
+  // element e of the image: tile t, register r, lane l → (row, col) of that tile
+  for (int e = tid; e < RF; e += 256) {
+    const int t = e >> 10, r = (e >> 6) & 15, l = e & 63;
+    int I = 0, J = 0, k = t;
+    while (k >= NB - I) {  // t-th upper-triangle tile in row-major order
+      k -= NB - I;
+      ++I;
+    }
+    J = I + k;
+    const int row = I * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+    const int cl = J * 32 + (l & 31);
+    const float v = red[e];
+    if (v != 0.f && row < ld && cl < ld) {
+      atomicAdd(&G[(size_t)row * ld + cl], v);
+      // entry (d, d) = Σ 1·1 over the block's valid rows (exact: < 2^24 per block)
+      if (cnt && row == d && cl == d) atomicAdd(cnt, (double)v);
+    }
+  }
+}
+
+// G[i][j] = G[j][i] for j < i < n (gram_map_kernel accumulates the upper triangle).
+__global__ __launch_bounds__(256) void gram_mirror_kernel(float* __restrict__ G, int ld, int n) {
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < n * n; e += gridDim.x * 256) {
+    const int i = e / n, j = e % n;
+    if (i > j) G[(size_t)i * ld + j] = G[(size_t)j * ld + i];
+  }
+}
+
 // ---- K-means -------------------------------------------------------------------------
 // One thread per row: nearest centroid (centroids staged in LDS), per-block LDS sums of
 // rows and counts per cluster, one atomic per (cluster, feature) per block.
@@ -172,6 +348,39 @@ OMLDM_API int omldm_kmeans_apply(float* cent, float* n, int k, int d, float* sum
   return (int)hipGetLastError();
 }
 
+template <int NB, int EPT>
+static int launch_gram_map(const float* x, const float* y, int B, int d0, const int* pairs,
+                           int npairs, float* G, int ld, double* cnt, hipStream_t st) {
+  // ≤ one block per CU, each ≥ one chunk: every block's image costs T·4 KiB of atomics
+  long long rpb = ((long long)B + 255) / 256;
+  rpb = ((rpb + 63) / 64) * 64;
+  const int blocks = (int)(((long long)B + rpb - 1) / rpb);
+  hipLaunchKernelGGL((gram_map_kernel<NB, EPT>), dim3(blocks), dim3(256), 0, st, x, y, B, d0, pairs,
+                     npairs, (int)rpb, G, ld, cnt);
+  const int n = NB * 32 < ld ? NB * 32 : ld;
+  hipLaunchKernelGGL(gram_mirror_kernel, dim3((n * n + 255) / 256), dim3(256), 0, st, G, ld, n);
+  return (int)hipGetLastError();
+}
+
+template <int NB>
+static int gram_map_e(const float* x, const float* y, int B, int d0, const int* pairs, int npairs,
+                      float* G, int ld, double* cnt, hipStream_t st) {
+  // element slots per thread: 64 staged rows × d0 raw values over 256 threads
+  if (d0 <= 16) return launch_gram_map<NB, 4>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+  if (d0 <= 32) return launch_gram_map<NB, 8>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+  if (d0 <= 64) return launch_gram_map<NB, 16>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+  return launch_gram_map<NB, 32>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+}
+
+static int gram_map(const float* x, const float* y, int B, int d0, const int* pairs, int npairs,
+                    float* G, int ld, double* cnt, hipStream_t st) {
+  const int dz = d0 + npairs + 2;
+  if (dz <= 32) return gram_map_e<1>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+  if (dz <= 64) return gram_map_e<2>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+  if (dz <= 96) return gram_map_e<3>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+  return gram_map_e<4>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+}
+
 // G[ld×ld] += [X 1 y]ᵀ[X 1 y] over rows with finite y (ld ≥ d + 2).
 // cnt (may be null): += number of rows with finite y.
 OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, float* G, int ld,
@@ -179,6 +388,11 @@ OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, fl
   if (B <= 0) return 0;
   const int dz = d + 2;
   if (ld < dz) return -1;
+  static const int v1 = [] {
+    const char* e = getenv("OMLDM_GRAM_V1");  // A/B: the one-tile-per-wave v1 kernel
+    return e ? atoi(e) : 0;
+  }();
+  if (!v1 && dz <= 128) return gram_map(x, y, B, d, nullptr, 0, G, ld, cnt, (hipStream_t)stream);
   const int t = (dz + 31) / 32;
   int ksplit = (2048 + t * t - 1) / (t * t);  // ≥ ~2048 waves in flight
   const long long maxsplit = (B + 63) / 64;
@@ -205,4 +419,17 @@ OMLDM_API int omldm_kmeans_assign(const float* x, const float* y, int B, int d, 
   hipLaunchKernelGGL(kmeans_assign_kernel, dim3(blocks), dim3(256), lds, (hipStream_t)stream, x,
                      y, B, d, k, cent, sums, counts, assign, inertia);
   return (int)hipGetLastError();
+}
+
+// G += Σ zzᵀ with z = [x, x_a·x_b for (a, b) in pairs, 1, y] over rows with finite y: the
+// Gram of PolynomialFeatures(2)(x) without materialising the expansion (pairs: int32
+// [npairs][2]; d0 + npairs + 2 ≤ 128, else -2: expand and call omldm_gram_update).
+OMLDM_API int omldm_gram_update_poly2(const float* x, const float* y, int B, int d0,
+                                      const int* pairs, int npairs, float* G, int ld, double* cnt,
+                                      void* stream) {
+  if (B <= 0) return 0;
+  const int dz = d0 + npairs + 2;
+  if (ld < dz) return -1;
+  if (dz > 128) return -2;
+  return gram_map(x, y, B, d0, pairs, npairs, G, ld, cnt, (hipStream_t)stream);
 }

@@ -41,7 +41,7 @@ struct LinParams {
   float lam;
   float inv_p;
   int bias;
-  int cspan;      // > 0: compact uint16 categorical wire format (see load_feature)
+  int cspan;      // > 0: compact uint16 categorical wire format (spoke_table.h)
   float cclip;   // τ clip: C for PA-I, +inf otherwise
   float kadd;     // τ denominator offset: 1/(2C) for PA-II, 0 otherwise
   float shrink;   // per-step multiplicative L2 shrink of w (1 when λ = 0)
@@ -139,20 +139,26 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
   int nidx[CH][FPL];
   float nxv[CH][FPL];
   float nyy[CH];
+  // every load of a chunk is issued before any is decoded (branch-free, clamped rows)
   auto load_chunk = [&](int tc) {
+    FeatRaw raw[CH][FPL];
+    float yr[CH];
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
-      const int t = tc + e;
-      const bool ok = t < t1;
-      nyy[e] = ok ? load_label(yv, t, p.y_i8) : __builtin_nanf("");
+      const int t = min(tc + e, t1 - 1);
+      yr[e] = load_label(yv, t, p.y_i8);
 #pragma unroll
-      for (int f = 0; f < FPL; ++f) {
-        int idx = -1;
-        float v = 0.f;
-        if (ok) load_feature(num, dn, cat, dc, t, lane + kWave * f, dim, p.bias, p.cspan, idx, v);
-        nidx[e][f] = idx;
-        nxv[e][f] = v;
-      }
+      for (int f = 0; f < FPL; ++f)
+        raw[e][f] = load_feature_raw(num, dn, cat, dc, t, lane + kWave * f, p.cspan);
+    }
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const bool ok = tc + e < t1;
+      nyy[e] = ok ? yr[e] : __builtin_nanf("");
+#pragma unroll
+      for (int f = 0; f < FPL; ++f)
+        decode_feature(raw[e][f], dn, dc, lane + kWave * f, dim, p.bias, p.cspan, ok, nidx[e][f],
+                       nxv[e][f]);
     }
   };
   load_chunk(t0);
@@ -370,11 +376,7 @@ __global__ __launch_bounds__(64, 5) void linear_round_rd_kernel(
   // valid) addresses, decoded only after the last one is issued — a load inside a
   // lane-divergent branch is waited for inside it, which serialised the rows.
   // Row e's label sits in lane e (one VGPR for all labels, v_readlane on the chain).
-  // one unconditional aligned dword per lane: the fp32 label, or the word holding the
-  // int8 label (a wave-uniform branch around the load made the wave wait inside it)
-  const int ty = min(t0 + lane, t1 - 1);
-  const uintptr_t ya = reinterpret_cast<uintptr_t>(yv) + (p.y_i8 ? (uintptr_t)ty : (uintptr_t)ty * 4);
-  const uint32_t yword = *reinterpret_cast<const uint32_t*>(ya & ~uintptr_t(3));
+  const float yraw = load_label(yv, min(t0 + lane, t1 - 1), p.y_i8);  // unconditional
   const bool is_num = lane < dn;
   const bool is_cat = lane >= dn && lane < dn + dc;
   const bool is_bias = p.bias && lane == dn + dc;
@@ -414,7 +416,6 @@ __global__ __launch_bounds__(64, 5) void linear_round_rd_kernel(
     xv[e] = idx >= 0 ? v : 0.f;
     d[e] = 0.f;
   }
-  const float yraw = p.y_i8 ? (float)(signed char)(yword >> (8 * (ya & 3))) : __uint_as_float(yword);
   const float ylane = lane < t1 - t0 ? yraw : __builtin_nanf("");
   RD_STAMP(2);
   // staging image init overlaps the gathers
@@ -683,12 +684,15 @@ __global__ __launch_bounds__(256) void linear_predict_kernel(
   const float sc = wscale ? wscale[m] : 1.f;
   for (int t = wv; t < B; t += nwaves) {
     float acc = 0.f;
+    FeatRaw raw[FPL];
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) raw[f] = load_feature_raw(num, dn, cat, dc, t, lane + kWave * f, cspan);
 #pragma unroll
     for (int f = 0; f < FPL; ++f) {
       int idx;
       float v;
-      load_feature(num, dn, cat, dc, t, lane + kWave * f, dim, bias, cspan, idx, v);
-      if (idx >= 0) acc = fmaf(v, to_f(wm[idx]), acc);
+      decode_feature(raw[f], dn, dc, lane + kWave * f, dim, bias, cspan, true, idx, v);
+      acc = fmaf(v, to_f(wm[idx >= 0 ? idx : 0]), acc);  // v = 0 when absent
     }
     acc = wave_sum(acc);
     if (lane == 0) out[(size_t)t * M + m] = acc * sc;

@@ -131,17 +131,21 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
 
   int nidx[CH];
   float nxv[CH], nyy[CH];
+  // every load of a chunk is issued before any is decoded (branch-free, clamped rows)
   auto load_chunk = [&](int tc) {
+    FeatRaw raw[CH];
+    float yr[CH];
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
-      const int t = tc + e;
-      const bool ok = t < t1;
-      nyy[e] = ok ? load_label(yv, t, y_i8) : __builtin_nanf("");
-      int idx = -1;
-      float v = 0.f;
-      if (ok) load_feature(num, dn, cat, dc, t, lane, dim, bias, cspan, idx, v);
-      nidx[e] = idx;
-      nxv[e] = v;
+      const int t = min(tc + e, t1 - 1);
+      yr[e] = load_label(yv, t, y_i8);
+      raw[e] = load_feature_raw(num, dn, cat, dc, t, lane, cspan);
+    }
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const bool ok = tc + e < t1;
+      nyy[e] = ok ? yr[e] : __builtin_nanf("");
+      decode_feature(raw[e], dn, dc, lane, dim, bias, cspan, ok, nidx[e], nxv[e]);
     }
   };
   load_chunk(t0);

@@ -7,9 +7,13 @@
 namespace omldm {
 
 // Label of example t: fp32, or int8 on the compact classification wire (1 B instead of 4
-// per example over PCIe; ±1 and class ids are exact).
+// per example over PCIe; ±1 and class ids are exact). One unconditional aligned dword load
+// (the word holding the int8 label, tensor allocations being ≥ 4-byte granular): a
+// y_i8 branch around two loads made the wave wait inside the branch.
 __device__ __forceinline__ float load_label(const void* __restrict__ yv, int t, int y_i8) {
-  return y_i8 ? (float)static_cast<const signed char*>(yv)[t] : static_cast<const float*>(yv)[t];
+  const uintptr_t a = reinterpret_cast<uintptr_t>(yv) + (y_i8 ? (uintptr_t)t : (uintptr_t)t * 4);
+  const uint32_t w = *reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  return y_i8 ? (float)(signed char)(w >> (8 * (a & 3))) : __uint_as_float(w);
 }
 
 // Bucketed LDS delta table geometry (host-computed, see omldm_linear_round):
@@ -27,7 +31,7 @@ struct TableGeom {
 };
 constexpr int kOvf = 64;
 
-// Loads feature f of example t for this lane. Numeric features occupy slots [0, dn);
+// Feature f of example t for this lane (wire format). Numeric features occupy slots [0, dn);
 // categorical features carry their hashed slot in the low 31 bits and the hash sign in
 // bit 31; -1 marks an absent categorical feature.
 // With bias != 0 the feature right after the categorical ones is the intercept: slot
@@ -35,37 +39,59 @@ constexpr int kOvf = 64;
 // Compact wire format (cspan > 0): categorical field f is a uint16 {sign:1, local:15}
 // with slot = dn + f·cspan + local (field-aware hashing), 0xFFFF = absent — half the
 // PCIe bytes of the int32 form for Criteo-shaped streams.
+// Loading is split in two so a caller can issue the loads of many rows before decoding
+// any (a load inside a lane-divergent or per-row branch is waited for
+// inside that branch, which serialised the rows of the spoke kernels):
+//   load_feature_raw — unconditional loads from always-valid addresses (t must be a valid
+//     row; absent numerical/categorical blocks read a zero word): the numerical value and
+//     the categorical word (the aligned dword holding a 16-bit compact slot — tensor
+//     allocations are at least 4-byte granular — or the int32 slot of the wide format);
+//   decode_feature — (idx, v) of the format above, or (-1, 0) when !ok or out of range.
+__device__ const uint32_t kZeroWords[4] = {0u, 0u, 0u, 0u};
+
+struct FeatRaw {
+  float nv;
+  uint32_t c;
+};
+
 template <typename NumT>
-__device__ __forceinline__ void load_feature(const NumT* __restrict__ num, int dn,
-                                             const void* __restrict__ cat, int dc, int t, int j,
-                                             int dim, int bias, int cspan, int& idx, float& v) {
-  idx = -1;
-  v = 0.f;
-  if (j == dn + dc && bias) {
-    idx = dim - 1;
-    v = 1.f;
-  } else if (j < dn) {
-    idx = j;
-    v = to_f(num[(size_t)t * dn + j]);
-  } else if (j < dn + dc) {
-    if (cspan > 0) {
-      const unsigned c = static_cast<const unsigned short*>(cat)[(size_t)t * dc + (j - dn)];
-      if (c != 0xFFFFu) {
-        idx = dn + (j - dn) * cspan + (int)(c & 0x7fffu);
-        v = (c & 0x8000u) ? -1.f : 1.f;
-      }
-    } else {
-      const int c = static_cast<const int*>(cat)[(size_t)t * dc + (j - dn)];
-      if (c != -1) {
-        idx = c & 0x7fffffff;
-        v = c < 0 ? -1.f : 1.f;
-      }
-    }
+__device__ __forceinline__ FeatRaw load_feature_raw(const NumT* __restrict__ num, int dn,
+                                                    const void* __restrict__ cat, int dc, int t,
+                                                    int j, int cspan) {
+  const bool is_num = j < dn;
+  const bool is_cat = j >= dn && j < dn + dc;
+  const NumT* np = dn > 0 ? num + ((size_t)t * dn + (is_num ? j : 0))
+                          : reinterpret_cast<const NumT*>(kZeroWords);
+  const uintptr_t ca =
+      dc > 0 ? reinterpret_cast<uintptr_t>(cat) +
+                   ((size_t)t * dc + (is_cat ? j - dn : 0)) * (cspan > 0 ? 2u : 4u)
+             : reinterpret_cast<uintptr_t>(kZeroWords);
+  const uint32_t cw = *reinterpret_cast<const uint32_t*>(ca & ~uintptr_t(3));
+  FeatRaw r;
+  r.nv = to_f(*np);
+  r.c = cspan > 0 ? (cw >> (8 * (ca & 3))) & 0xffffu : cw;
+  return r;
+}
+
+__device__ __forceinline__ void decode_feature(FeatRaw r, int dn, int dc, int j, int dim,
+                                               int bias, int cspan, bool ok, int& idx,
+                                               float& v) {
+  const bool is_num = j < dn;
+  const bool is_cat = j >= dn && j < dn + dc;
+  const bool is_bias = bias && j == dn + dc;
+  int ci;
+  float cv;
+  if (cspan > 0) {  // wave-uniform; no loads inside
+    ci = r.c != 0xFFFFu ? dn + (j - dn) * cspan + (int)(r.c & 0x7fffu) : -1;
+    cv = (r.c & 0x8000u) ? -1.f : 1.f;
+  } else {
+    ci = r.c != 0xFFFFFFFFu ? (int)(r.c & 0x7fffffffu) : -1;
+    cv = (r.c & 0x80000000u) ? -1.f : 1.f;
   }
-  if ((unsigned)idx >= (unsigned)dim) {  // never gather out of bounds
-    idx = -1;
-    v = 0.f;
-  }
+  idx = is_num ? j : is_cat ? ci : is_bias ? dim - 1 : -1;
+  v = is_num ? r.nv : is_cat ? cv : 1.f;
+  if (!ok || (unsigned)idx >= (unsigned)dim) idx = -1;
+  if (idx < 0) v = 0.f;
 }
 
 __device__ __forceinline__ uint32_t hmix(uint32_t k) { return k * 0x9E3779B1u; }

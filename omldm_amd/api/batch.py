@@ -186,3 +186,25 @@ class HashedBatch:
         rows = torch.arange(B, device=out.device).unsqueeze(1).expand_as(slot)
         out.index_put_((rows[valid], slot[valid]), sign[valid], accumulate=True)
         return out
+
+
+@dataclass
+class PolyBatch(HashedBatch):
+    """A training batch whose dense learner input is PolynomialFeatures(2) of ``num`` —
+    ``[num, num[:, a]·num[:, b] for (a, b) in pairs]`` — left unexpanded. The pipeline hands
+    it to learners that fuse the expansion into their update (ORR's Gram kernel reads the
+    d raw values per row instead of the d + d(d+1)/2 expanded ones); ``expanded()`` is the
+    materialised batch for everything else."""
+
+    pairs: torch.Tensor | None = field(default=None, compare=False)  # int32 [np, 2]
+
+    def _like(self, num, cat, y, raw) -> "PolyBatch":
+        return PolyBatch(num, cat, y, raw, self.cat_span, self.pairs)
+
+    def expanded(self) -> HashedBatch:
+        from omldm_amd.ops.preprocess import poly_expand
+
+        x = self.num.float().contiguous()
+        num = poly_expand(x, self.pairs) if self.B else torch.zeros(
+            (0, x.shape[1] + self.pairs.shape[0]), dtype=torch.float32, device=x.device)
+        return HashedBatch(num, self.cat, self.y, self.raw, self.cat_span)

@@ -10,9 +10,11 @@ preprocessors into the learner (MLPipeline.pipePoint, hs_err_pid77107.log:111).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
-from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.api.batch import FeatureSpace, HashedBatch, PolyBatch
 from omldm_amd.api.schemas import SINGLE_LEARNER_MODELS, Request
 from omldm_amd.models import make_learner, make_preprocessor
 from omldm_amd.parallel.comm import Comm
@@ -59,12 +61,25 @@ class Pipeline:
         self.protocol = make_protocol(proto, comm, self.learner, cfg, spokes=spokes,
                                       max_msg_params=max_msg_params)
         self.protocol_name = self.protocol.NAME
+        # PolynomialFeatures(2) in front of a learner that fuses the map into its update
+        # (ORR): training batches reach the learner unexpanded (api/batch.py: PolyBatch)
+        last = self.preprocessors[-1] if self.preprocessors else None
+        self._fuse_poly2 = (os.environ.get("OMLDM_FUSE_POLY", "1") != "0"  # A/B knob
+                            and getattr(self.learner, "supports_poly2_map", False)
+                            and last is not None and last.NAME == "PolynomialFeatures"
+                            and last.degree == 2)
         # running statistics (reference Statistics / learning curve, FlinkHub.scala:95-156)
         self.learning_curve: list[tuple[float, int]] = []
         self._lc_last = (0.0, 0)
 
     # --------------------------------------------------------------- data path
     def _pre(self, batch: HashedBatch, train: bool) -> HashedBatch:
+        if train and self._fuse_poly2:
+            for p in self.preprocessors[:-1]:
+                batch = p(batch, train=True)
+            pairs = self.preprocessors[-1].pair_index(batch.dn, batch.num.device)
+            return PolyBatch(batch.num.float().contiguous(), batch.cat, batch.y, batch.raw,
+                             batch.cat_span, pairs)
         for p in self.preprocessors:
             batch = p(batch, train=train)
         return batch

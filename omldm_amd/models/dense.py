@@ -43,6 +43,7 @@ class ORR(Learner):
     NAME = "ORR"
     TASK = "regression"
     merge_mode = "sum"
+    supports_poly2_map = True  # fit() accepts an unexpanded PolyBatch (fused Gram kernel)
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -53,9 +54,9 @@ class ORR(Learner):
         self.lam = hp_float(self.hyper, "lambda", 1.0)
 
     def fit(self, batch, ctx):
-        x = batch.num.float()
         if batch.B:
-            D.gram_update(x, batch.y, self.G, cnt=self.cum[1:2])
+            D.gram_update(batch.num.float(), batch.y, self.G, cnt=self.cum[1:2],
+                          pairs=getattr(batch, "pairs", None))
         self._w = None
 
     def state_vector(self):

@@ -131,6 +131,12 @@ class PolynomialFeatures(Preprocessor):
     def fit_transform(self, x, train):
         return P.poly_expand(x, self._index(x.shape[1], x.device))
 
+    def pair_index(self, d: int, device) -> torch.Tensor:
+        """int32 [np, 2] (a, b) of the degree-2 products appended after the d inputs (the
+        fused learners' form of this map; degree 2 only)."""
+        assert self.degree == 2
+        return self._index(d, device)
+
 
 PREPROCESSORS = {c.NAME: c for c in (StandardScaler, MinMaxScaler, PolynomialFeatures)}
 

@@ -13,16 +13,31 @@ from omldm_amd.ops.native import check, ptr
 
 
 def gram_update(x: torch.Tensor, y: torch.Tensor, G: torch.Tensor,
-                cnt: torch.Tensor | None = None) -> None:
+                cnt: torch.Tensor | None = None, pairs: torch.Tensor | None = None) -> None:
     """G[:d+2, :d+2] += Σ_rows z zᵀ with z = [x, 1, y] over rows whose y is finite;
     ``cnt`` (one fp64 element: a running total) += the number of those rows, read off
-    the Gram's (d, d) entry inside the same kernel."""
-    B, d = x.shape
+    the Gram's (d, d) entry inside the same kernel. ``pairs`` (int32 [np, 2]): x holds the
+    raw features of a PolynomialFeatures(2) map and z = [x, x_a·x_b per pair, 1, y] — the
+    GPU kernel forms the products in its operand fetch (csrc/kernels/dense_learners.hip
+    gram_map_kernel), so the expansion never reaches HBM."""
+    B, d0 = x.shape
     if B == 0:
         return
     x = x.float().contiguous()
     y = y.float().contiguous()
     assert cnt is None or (cnt.dtype == torch.float64 and cnt.numel() == 1)
+    if pairs is not None:
+        pairs = pairs.to(device=x.device, dtype=torch.int32).contiguous()
+        assert pairs.dim() == 2 and pairs.shape[1] == 2
+        if x.is_cuda and d0 + pairs.shape[0] + 2 <= 128:
+            check(native.hip().omldm_gram_update_poly2(
+                ptr(x), ptr(y), B, d0, ptr(pairs), pairs.shape[0], ptr(G), G.shape[1], ptr(cnt),
+                native.stream_of(x)), "omldm_gram_update_poly2")
+            return
+        from omldm_amd.ops.preprocess import poly_expand
+
+        x = poly_expand(x, pairs)
+    B, d = x.shape
     if x.is_cuda:
         check(native.hip().omldm_gram_update(ptr(x), ptr(y), B, d, ptr(G), G.shape[1], ptr(cnt),
                                              native.stream_of(x)), "omldm_gram_update")

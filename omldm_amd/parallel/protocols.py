@@ -98,6 +98,12 @@ class Protocol:
         self.stats.bytes_shipped += 2 * g * nbytes
         self.stats.num_of_blocks += 2 * g * max(1, math.ceil(nparams / self.max_msg_params))
 
+    def _small(self, vals: list) -> torch.Tensor:
+        """A few fp32 scalars for a small collective, on the device the backend reduces
+        (RCCL: the learner's GPU; gloo: host)."""
+        dev = self.learner.device if self.comm.backend == "nccl" else "cpu"
+        return torch.tensor(vals, dtype=torch.float32, device=dev)
+
     def _account_small(self, n_msgs: int, nbytes: int) -> None:
         self.stats.small_messages += n_msgs
         self.stats.bytes_shipped += n_msgs * nbytes
@@ -356,12 +362,15 @@ class GM(Protocol):
         L.fit(batch, self._ctx())
         x = L.state_vector()
         scale = self.G if L.merge_mode == "sum" else 1.0
-        nrm = M.drift_norms(x, self._E, scale)             # [‖X_i‖², ‖E‖²], one pass
-        # safe zone: ‖X_i‖² ≤ θ·‖E‖² (θ·1 while E == 0)
-        viol = (nrm[0:1] > self.threshold * torch.clamp(nrm[1:2], min=1.0)).float()
-        self.comm.all_reduce_(viol, tag="gm-flag", op=torch.distributed.ReduceOp.MAX)
+        x2, e2 = M.drift_norms(x, self._E, scale).tolist()  # [‖X_i‖², ‖E‖²], one pass
+        # safe zone: ‖X_i‖² ≤ θ·‖E‖² (θ·1 while E == 0); the decision is host arithmetic
+        viol = 1.0 if x2 > self.threshold * max(e2, 1.0) else 0.0
+        if self.G > 1:
+            v = self._small([viol])
+            self.comm.all_reduce_(v, tag="gm-flag", op=torch.distributed.ReduceOp.MAX)
+            viol = float(v.item())
         self._account_small(self.G, 4)
-        if viol.item() > 0:
+        if viol > 0:
             self._full_sync()
         self.stats.rounds += 1
 
@@ -413,7 +422,7 @@ class FGM(Protocol):
         self._phi0 = -self.eps * e2
         psi = self.G * self._phi0
         self._theta = -psi / (2 * self.G) if psi < 0 else None
-        self._c_prev = 0
+        self._c_prev = 0.0
         self.fgm_rounds += 1
 
     def _full_sync(self):
@@ -431,15 +440,20 @@ class FGM(Protocol):
             return
         x = L.state_vector()
         scale = self.G if L.merge_mode == "sum" else 1.0
-        nrm = M.drift_norms(x, self._E, scale)             # [‖X_i‖², ‖E‖²], one pass
-        phi = nrm[0] - self.eps * nrm[1]
-        c = torch.floor((phi - self._phi0) / self._theta).clamp(min=0)
+        # [‖X_i‖², ‖E‖²] in one device pass, then host arithmetic on two scalars (one
+        # read-back instead of a string of tiny launches per round)
+        x2, e2 = M.drift_norms(x, self._E, scale).tolist()
+        phi = x2 - self.eps * e2
+        c = max(0.0, math.floor((phi - self._phi0) / self._theta))
         inc = c - self._c_prev
-        msg = torch.stack([inc, phi]).float()
-        self.comm.all_reduce_(msg, tag="fgm-counters")
         self._c_prev = c
+        if self.G > 1:
+            msg = self._small([inc, phi])
+            self.comm.all_reduce_(msg, tag="fgm-counters")
+            tot_inc, psi = msg.tolist()
+        else:
+            tot_inc, psi = inc, phi
         self._account_small(self.G, 8)
-        tot_inc, psi = msg.tolist()
         self._csum += tot_inc
         if self._csum > self.G:
             self.subrounds += 1
@@ -451,7 +465,7 @@ class FGM(Protocol):
                 self._theta = -psi / (2 * self.G)
                 self._csum = 0.0
                 # counters restart relative to the new subround
-                self._c_prev = torch.floor((phi - self._phi0) / self._theta).clamp(min=0)
+                self._c_prev = max(0.0, math.floor((phi - self._phi0) / self._theta))
         self.stats.rounds += 1
 
     def state_dict(self):

@@ -89,7 +89,7 @@ def test_hip_colstats_scale_poly(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,d", [(1000, 13), (4097, 104), (333, 30)])
+@pytest.mark.parametrize("B,d", [(1000, 13), (4097, 104), (333, 30), (70001, 104), (9000, 61)])
 def test_hip_gram_mfma_vs_fp64(cuda, B, d):
     torch.manual_seed(B)
     x = torch.randn(B, d)
@@ -435,3 +435,63 @@ def test_kmeans_learner_gpu_matches_cpu(cuda):
     torch.cuda.synchronize()
     torch.testing.assert_close(gpu.state.cpu(), cpu.state, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(gpu.cum.cpu()[:2], cpu.cum[:2], rtol=1e-4, atol=1e-2)
+
+
+def _poly_pairs(d):
+    from omldm_amd.models.preprocess import PolynomialFeatures
+
+    return PolynomialFeatures({"degree": 2}).pair_index(d, "cpu")
+
+
+def test_orr_pipeline_fuses_polynomial_map_on_cpu():
+    """Request → PolynomialFeatures(2) → ORR: training batches reach ORR unexpanded
+    (PolyBatch) and its Gram equals the Gram of the expanded batch."""
+    from omldm_amd.api.batch import PolyBatch
+    from omldm_amd.api.schemas import Request
+    from omldm_amd.engine.pipeline import Pipeline
+    from omldm_amd.parallel.comm import Comm
+
+    req = Request.from_json({"id": 1, "request": "Create", "learner": {"name": "ORR"},
+                             "preProcessors": [{"name": "PolynomialFeatures",
+                                                "hyperParameters": {"degree": 2}}],
+                             "trainingConfiguration": {"protocol": "Synchronous"}})
+    pipe = Pipeline(req, SP, Comm(), "cpu", 1, 1)
+    b = synth_batch(SP, 300, task=1)
+    assert isinstance(pipe._pre(b, True), PolyBatch)
+    pipe.train(b)
+    ref = make_learner("ORR", {"_inDim": pipe.learner.d}, SP, "cpu")
+    ref.fit(pipe.preprocessors[0](b, train=True), RoundContext())
+    torch.testing.assert_close(pipe.learner.G, ref.G)
+    assert pipe.learner.running_totals()["fitted"] == 300
+    assert pipe.predict(b).shape == (300,)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,d0", [(5000, 13), (70001, 13), (999, 5), (4096, 10)])
+def test_hip_gram_fused_poly2_vs_expanded_and_fp64(cuda, B, d0):
+    """The fused PolynomialFeatures(2) Gram (products formed in the MFMA operand fetch)
+    equals the Gram of the expanded batch and the fp64 reference."""
+    from omldm_amd.ops.preprocess import poly_expand
+
+    torch.manual_seed(B + d0)
+    x = torch.randn(B, d0)
+    y = torch.randn(B)
+    y[::5] = float("nan")
+    pairs = _poly_pairs(d0)
+    d = d0 + pairs.shape[0]
+    ld = ((d + 2 + 31) // 32) * 32
+    Gf = torch.zeros(ld, ld, device=cuda)
+    Ge = torch.zeros(ld, ld, device=cuda)
+    cf = torch.zeros(1, dtype=torch.float64, device=cuda)
+    D.gram_update(x.to(cuda), y.to(cuda), Gf, cnt=cf, pairs=pairs)
+    D.gram_update(poly_expand(x, pairs).to(cuda), y.to(cuda), Ge)
+    torch.cuda.synchronize()
+    ok = ~torch.isnan(y)
+    assert float(cf) == float(ok.sum())
+    xe = poly_expand(x, pairs)[ok]
+    z = torch.cat([xe, torch.ones(int(ok.sum()), 1), y[ok].unsqueeze(1)], 1).double()
+    ref = (z.T @ z).numpy()
+    np.testing.assert_allclose(Gf.cpu().double().numpy()[: d + 2, : d + 2], ref, rtol=1e-4,
+                               atol=2e-2)
+    np.testing.assert_allclose(Gf.cpu().numpy(), Ge.cpu().numpy(), rtol=1e-5, atol=1e-2)
+    assert torch.equal(Gf.cpu(), Gf.cpu().T)  # mirrored
