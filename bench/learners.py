@@ -23,13 +23,20 @@ from omldm_amd.io.synthetic import synth_batch  # noqa: E402
 from omldm_amd.models import make_learner  # noqa: E402
 from omldm_amd.models.base import RoundContext  # noqa: E402
 
+# (name, task, hyper, spokes[, wire]); wire "compact" = the field-aware uint16 wire of the
+# headline bench (the register-dedup kernels run there with ≤ 16 rows per spoke)
 CASES = [
     ("PA", 0, {}, 4096),
     ("SVM", 0, {"modelDtype": "bf16", "tableLog2": 11}, 4096),
     ("RegressorPA", 1, {}, 4096),
     ("LogisticRegression", 0, {}, 4096),
+    ("PA@compact", 0, {}, 8192, "compact"),
+    ("SVM@compact", 0, {"modelDtype": "bf16"}, 8192, "compact"),
+    ("RegressorPA@compact", 1, {}, 8192, "compact"),
+    ("LogisticRegression@compact", 0, {}, 8192, "compact"),
     ("MultiClassPA", 2, {"nClasses": 4}, 8192),
     ("MultiClassPA@4096", 2, {"nClasses": 4}, 4096),
+    ("MultiClassPA@compact", 2, {"nClasses": 4}, 8192, "compact"),
     ("ORR", 1, {}, 1),
     ("K-means", 0, {"k": 16}, 1),
     # 512 spokes × 256 rows: fastest of 256..2048 (bench/sweep_cases_nn.json)
@@ -49,10 +56,13 @@ def main(argv=None) -> int:
                          '(geometry sweeps)')
     a = ap.parse_args(argv)
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
-    space = FeatureSpace(13, 0, 26, 1 << 20)
+    spaces = {"wide": FeatureSpace(13, 0, 26, 1 << 20),
+              "compact": FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)}
     res = {}
     cases = [tuple(c) for c in json.loads(a.cases)] if a.cases else CASES
-    for name, task, hyper, spokes in cases:
+    for case in cases:
+        name, task, hyper, spokes = case[:4]
+        space = spaces[case[4] if len(case) > 4 else "wide"]
         if a.only and name.split("@")[0] not in a.only.split(","):
             continue
         ring = []

@@ -372,50 +372,16 @@ __global__ __launch_bounds__(64, 5) void linear_round_rd_kernel(
     for (int k = lane; k < wsw; k += kWave) wrow[k] = k == 4 ? 1.f : 0.f;
     return;
   }
-  // the spoke's rows, every load in flight at once: branch-free loads from clamped (always
-  // valid) addresses, decoded only after the last one is issued — a load inside a
-  // lane-divergent branch is waited for inside it, which serialised the rows.
-  // Row e's label sits in lane e (one VGPR for all labels, v_readlane on the chain).
+  // the spoke's rows, every load in flight at once (spoke_table.h: load_spoke_rows) — a
+  // load inside a lane-divergent branch is waited for inside it, which serialised the
+  // rows of the first version. Row e's label sits in lane e (one VGPR for all labels,
+  // v_readlane on the chain).
   const float yraw = load_label(yv, min(t0 + lane, t1 - 1), p.y_i8);  // unconditional
-  const bool is_num = lane < dn;
-  const bool is_cat = lane >= dn && lane < dn + dc;
-  const bool is_bias = p.bias && lane == dn + dc;
-  const int jn = is_num ? lane : 0;
-  const int jc = is_cat ? lane - dn : 0;
-  // one 16-bit load per row and lane when the numericals are bf16 (lane-dependent base and
-  // stride: numerical slot or categorical field), two loads otherwise
-  unsigned short raw[RMAX];
-  NumT nraw[sizeof(NumT) == 2 ? 1 : RMAX];
-  if constexpr (sizeof(NumT) == 2) {
-    const unsigned short* base = is_num ? reinterpret_cast<const unsigned short*>(num) + jn
-                                        : static_cast<const unsigned short*>(cat) + jc;
-    const int stride = is_num ? dn : dc;
-#pragma unroll
-    for (int e = 0; e < RMAX; ++e) raw[e] = base[(size_t)min(t0 + e, t1 - 1) * stride];
-  } else {
-#pragma unroll
-    for (int e = 0; e < RMAX; ++e) {
-      const int t = min(t0 + e, t1 - 1);
-      nraw[e] = num[(size_t)t * dn + jn];
-      raw[e] = static_cast<const unsigned short*>(cat)[(size_t)t * dc + jc];
-    }
-  }
   int key[RMAX];
   float xv[RMAX], wv[RMAX], d[RMAX];
-  const int cbase = dn + jc * p.cspan;
+  load_spoke_rows<RMAX>(num, dn, cat, dc, t0, t1, lane, dim, p.bias, p.cspan, key, xv);
 #pragma unroll
-  for (int e = 0; e < RMAX; ++e) {
-    const unsigned c = raw[e];
-    float nv;
-    if constexpr (sizeof(NumT) == 2) nv = __uint_as_float(c << 16);  // bf16 bits
-    else nv = to_f(nraw[e]);
-    int idx = is_num ? lane : is_bias ? dim - 1 : (is_cat && c != 0xFFFFu) ? cbase + (int)(c & 0x7fffu) : -1;
-    const float v = is_num ? nv : is_bias ? 1.f : (c & 0x8000u) ? -1.f : 1.f;
-    if ((unsigned)idx >= (unsigned)dim || t0 + e >= t1) idx = -1;
-    key[e] = idx;
-    xv[e] = idx >= 0 ? v : 0.f;
-    d[e] = 0.f;
-  }
+  for (int e = 0; e < RMAX; ++e) d[e] = 0.f;
   const float ylane = lane < t1 - t0 ? yraw : __builtin_nanf("");
   RD_STAMP(2);
   // staging image init overlaps the gathers

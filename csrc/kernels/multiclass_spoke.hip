@@ -259,13 +259,14 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
   const int seg_log2 = bs_log2 + g.lgg;
   const size_t S_tot = gridDim.x;
   const size_t region = S_tot << g.log2cap;
+  const int used = (int)min((long long)g.qused << seg_log2, (long long)cap);  // see TableGeom
   if (compact) {
     // One record per slot: the key once ([group][spoke][segment] int32 region) and its
     // K deltas as one vector ([group][spoke][segment][K] floats after it) — 4 + 4K bytes
     // instead of 8 per class, one reduce launch for all classes (multiclass_reduce_kernel).
     int* kout = reinterpret_cast<int*>(tables);
     float* vout = reinterpret_cast<float*>(kout + region);
-    for (int i = lane; i < cap && !(ablate & 1); i += kWave) {
+    for (int i = lane; i < used && !(ablate & 1); i += kWave) {
       const size_t q = (size_t)(i >> seg_log2);
       const size_t o = ((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1));
       kout[o] = keys[i];
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
       }
     }
   } else {
-    for (int i = lane; i < cap && !(ablate & 1); i += kWave) {
+    for (int i = lane; i < used && !(ablate & 1); i += kWave) {
       const size_t q = (size_t)(i >> seg_log2);
       const size_t o = ((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1));
       const int key = keys[i];
@@ -308,6 +309,195 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
     wrow[3] = 1.f;  // active worker
     wrow[4] = 0.f;
     wrow[5] = ovf_total;
+    wrow[6] = 0.f;
+    wrow[7] = 0.f;
+    if (!bias)
+      for (int k = 0; k < nclass; ++k) wrow[kMcStat + k * (dn + 1) + dn] = 0.f;
+  }
+}
+
+// Register-dedup MultiClassPA round (field-aware compact wire, ≤ RMAX rows per spoke, ≤ 64
+// features, compact flush): the binary register-dedup idea (linear_spoke.hip,
+// linear_round_rd_kernel) with K deltas per row. On the field-aware wire lane f only sees
+// keys of field f, so a spoke's K deltas for a key belong to one lane: per lane its
+// rows' keys, values, K round-start prototype weights and d[e][k] (the delta of row e's
+// key for class k as row e sees it). Row e's step touches classes y and r (wave-uniform):
+// u = τ·x_e is added to d[e'][y] and subtracted from d[e'][r] of row e and every later row
+// with the same key (compile-time row and class indices: selects, no LDS, no probes, no
+// overflow on the chain). The per-key accumulation order is the LDS table's, so the round
+// equals multiclass_round_kernel's. The last occurrence of each key carries its K totals
+// into the compact staging image (bucket positions from LDS counters; a full bucket adds
+// straight to the accumulator) and the unchanged compact flush / reducer.
+template <int K, int RMAX, typename NumT, typename WT>
+__global__ __launch_bounds__(64) void multiclass_round_rd_kernel(
+    const WT* __restrict__ Wt, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
+    int dc, int cspan, const void* __restrict__ yv, int y_i8, int B, int R, int dim, int nclass,
+    int variant, float C, int bias, float* __restrict__ ws, int* __restrict__ tables,
+    float* __restrict__ dacc, TableGeom g, int ablate) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int cap = 1 << g.log2cap;
+  const int nbk = 1 << g.log2nb;
+  const int bs_log2 = g.log2cap - g.log2nb;
+  int* keys = reinterpret_cast<int*>(smem);                               // [cap]
+  float* vals = reinterpret_cast<float*>(smem + (size_t)cap * 4);         // [cap][K]
+  int* bcnt = reinterpret_cast<int*>(vals + (size_t)cap * K);             // [nbk / 2]
+  int* dummy = bcnt + ((nbk + 1) >> 1);                                   // [64]
+  const int lane = threadIdx.x;
+  const int s = blockIdx.x;
+  const int wsw = kMcStat + nclass * (dn + 1);
+  float* wrow = ws + (size_t)s * wsw;
+  const long long t0ll = (long long)s * R;
+  const int t0 = t0ll > B ? B : (int)t0ll;
+  const int t1 = (t0ll + R) > B ? B : (int)(t0ll + R);
+  if (t0 >= t1) {  // idle spoke: not a worker this round
+    for (int k = lane; k < wsw; k += kWave) wrow[k] = 0.f;
+    return;
+  }
+  const float yraw = load_label(yv, min(t0 + lane, t1 - 1), y_i8);  // row e's class in lane e
+  int key[RMAX];
+  float xv[RMAX];
+  load_spoke_rows<RMAX>(num, dn, cat, dc, t0, t1, lane, dim, bias, cspan, key, xv);
+  const float ylane = lane < t1 - t0 ? yraw : __builtin_nanf("");
+  for (int i = lane; i < cap; i += kWave) {
+    keys[i] = kEmptyKey;
+#pragma unroll
+    for (int k = 0; k < K; ++k) vals[(size_t)i * K + k] = 0.f;
+  }
+  for (int i = lane; i < (nbk + 1) >> 1; i += kWave) bcnt[i] = 0;
+  // round-start prototypes (key-major shadow, one vector load per row), unconditional
+  float wv[RMAX][K], d[RMAX][K];
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) load_protos<K>(Wt, key[e] >= 0 ? key[e] : 0, wv[e]);
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (key[e] < 0) wv[e][k] = 0.f;
+      d[e][k] = 0.f;
+    }
+  float pn[RMAX];  // ‖x_e‖²: off the sequential chain
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) pn[e] = wave_sum(xv[e] * xv[e]);
+  const int dcol = lane < dn ? lane : ((bias && lane == dn + dc) ? dn : -1);
+  float loss_sum = 0.f, nex = 0.f, mist = 0.f;
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) {
+    const float y = readlane_f(ylane, e);
+    if (__builtin_isnan(y) || (ablate & 2)) continue;  // wave-uniform
+    const int yc = (int)y;
+    float sc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) sc[k] = (k < nclass) ? xv[e] * (wv[e][k] + d[e][k]) : 0.f;
+#pragma unroll
+    for (int k = 0; k < K; k += 2) wave_sum2(sc[k], sc[k + 1]);
+    int r = -1;
+    float best = -INFINITY, sy = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (k < nclass && k != yc && sc[k] > best) {
+        best = sc[k];
+        r = k;
+      }
+      if (k == yc) sy = sc[k];
+    }
+    const float margin = sy - best;
+    const float loss = fmaxf(0.f, 1.f - margin);
+    loss_sum += loss;
+    nex += 1.f;
+    mist += margin <= 0.f ? 1.f : 0.f;
+    float tau = 0.f;
+    if (loss > 0.f && pn[e] > 0.f && r >= 0) {
+      const float den = 2.f * pn[e];
+      tau = variant == 0 ? loss * __builtin_amdgcn_rcpf(den)
+          : variant == 1 ? fminf(C, loss * __builtin_amdgcn_rcpf(den))
+                         : loss * __builtin_amdgcn_rcpf(den + 0.5f / C);
+    }
+    if (tau != 0.f) {  // wave-uniform
+      const float u = tau * xv[e];
+      float du[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        du[k] = (k == yc && yc < nclass ? u : 0.f) - (k == r ? u : 0.f);
+#pragma unroll
+      for (int k = 0; k < K; ++k) d[e][k] += du[k];
+#pragma unroll
+      for (int e2 = e + 1; e2 < RMAX; ++e2) {
+        const bool m = key[e2] == key[e];
+#pragma unroll
+        for (int k = 0; k < K; ++k) d[e2][k] += m ? du[k] : 0.f;
+      }
+    }
+  }
+  __syncthreads();  // staging image initialised
+  float dreg[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) dreg[k] = 0.f;
+  int pos[RMAX];
+  bool emit[RMAX];
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) {
+    bool last = key[e] >= 0;
+#pragma unroll
+    for (int e2 = e + 1; e2 < RMAX; ++e2) last = last && key[e2] != key[e];
+    bool nz = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) nz = nz || d[e][k] != 0.f;
+    last = last && nz;
+    if (dcol >= 0 && last)
+#pragma unroll
+      for (int k = 0; k < K; ++k) dreg[k] = d[e][k];
+    emit[e] = last && dcol < 0 && !(ablate & 1);
+    const int b = emit[e] ? key[e] >> g.kshift : 0;
+    const int sh = 16 * (b & 1);
+    int* ctr = emit[e] ? &bcnt[b >> 1] : &dummy[lane];  // 16-bit counters, see linear_spoke
+    pos[e] = (atomicAdd(ctr, emit[e] ? 1 << sh : 0) >> sh) & 0xffff;
+  }
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) {
+    if (emit[e]) {
+      if (pos[e] < (1 << bs_log2)) {
+        const int sl = ((key[e] >> g.kshift) << bs_log2) + pos[e];
+        keys[sl] = key[e];
+#pragma unroll
+        for (int k = 0; k < K; ++k) vals[(size_t)sl * K + k] = d[e][k];
+      } else {  // bucket full: straight to the accumulator (exact)
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (k < nclass && d[e][k] != 0.f) unsafeAtomicAdd(&dacc[(size_t)k * dim + key[e]], d[e][k]);
+      }
+    }
+  }
+  __syncthreads();
+  // compact flush (multiclass_round_kernel's layout): key once, K deltas as one vector
+  const int seg_log2 = bs_log2 + g.lgg;
+  const size_t S_tot = gridDim.x;
+  const size_t region = S_tot << g.log2cap;
+  float* vout = reinterpret_cast<float*>(tables + region);
+  const int used = (int)min((long long)g.qused << seg_log2, (long long)cap);
+  for (int i = lane; i < used && !(ablate & 1); i += kWave) {
+    const size_t q = (size_t)(i >> seg_log2);
+    const size_t o = ((q * S_tot + s) << seg_log2) + (i & ((1 << seg_log2) - 1));
+    tables[o] = keys[i];
+    if constexpr (K % 4 == 0) {
+#pragma unroll
+      for (int k = 0; k < K; k += 4)
+        *reinterpret_cast<float4*>(vout + o * K + k) =
+            *reinterpret_cast<const float4*>(&vals[(size_t)i * K + k]);
+    } else {
+      *reinterpret_cast<float2*>(vout + o * K) = *reinterpret_cast<const float2*>(&vals[(size_t)i * K]);
+    }
+  }
+  if (dcol >= 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k < nclass) wrow[kMcStat + k * (dn + 1) + dcol] = dreg[k];
+  if (lane == 0) {
+    wrow[0] = loss_sum;
+    wrow[1] = nex;
+    wrow[2] = mist;
+    wrow[3] = 1.f;  // active worker
+    wrow[4] = 0.f;
+    wrow[5] = 0.f;  // dropped updates (none on this path)
     wrow[6] = 0.f;
     wrow[7] = 0.f;
     if (!bias)
@@ -393,7 +583,7 @@ static int launch_mc_reduce(const void* tables, int S_act, int S, TableGeom g, i
                             int nclass, float* dacc, hipStream_t st) {
   if (S_act <= 0) return 0;
   const int gl = g.kshift + g.lgg;
-  const int ng = (dim + (1 << gl) - 1) >> gl;
+  const int ng = min((dim + (1 << gl) - 1) >> gl, g.qused);
   // Spokes of a key group split over 2 blocks: measured at 4 classes, 8192 spokes, 2^20
   // dims (256 groups): split 1 / 2 / 4 / 8 → 0.370 / 0.348 / 0.361 / 0.385 ms per round
   // (the 64 KiB image allows 2 blocks per CU; wider splits pay in L2 atomics).
@@ -486,9 +676,29 @@ static void launch_mc(const void* Wt, const void* num, int dn, const void* cat, 
                       const void* y, int y_i8, int B, int R, int S, int dim, int nclass,
                       int variant, float C, int bias, float* ws, int2* tables, float* dacc,
                       TableGeom g, size_t lds, int compact, hipStream_t st, int* err) {
-  auto fn = multiclass_round_kernel<K, 4, NumT, WT>;
   int ablate = 0;  // timing diagnostics only: bit0 no flush, bit1 no sequential part
   if (const char* e = getenv("OMLDM_MC_ABLATE")) ablate = atoi(e);
+  // register-dedup path: field-aware wire, ≤ 16 rows per spoke, K ≤ 4, compact flush
+  // (OMLDM_MC_RD=0: the LDS-table kernel, A/B)
+  const char* rd_env = getenv("OMLDM_MC_RD");
+  if constexpr (K <= 4) {
+  if (compact && cspan > 0 && R <= 16 && !(rd_env && atoi(rd_env) == 0)) {
+    const int nbk = 1 << g.log2nb;
+    const size_t lds_rd =
+        (size_t(1) << g.log2cap) * (4 + 4 * (size_t)K) + (size_t)((nbk + 1) / 2) * 4 + kWave * 4;
+    auto run = [&](auto fn) {
+      *err = check_dyn_lds((const void*)fn, lds_rd);
+      if (*err) return;
+      hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds_rd, st, (const WT*)Wt, (const NumT*)num, dn,
+                         cat, dc, cspan, y, y_i8, B, R, dim, nclass, variant, C, bias, ws,
+                         (int*)tables, dacc, g, ablate);
+    };
+    if (R <= 8) run(multiclass_round_rd_kernel<K, 8, NumT, WT>);
+    else run(multiclass_round_rd_kernel<K, 16, NumT, WT>);
+    return;
+  }
+  }
+  auto fn = multiclass_round_kernel<K, 4, NumT, WT>;
   *err = check_dyn_lds((const void*)fn, lds);
   if (*err) return;
   hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)Wt, (const NumT*)num, dn, cat, dc,
@@ -514,6 +724,11 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
   if (log2cap < 6 || log2cap > 13) return -1;
   TableGeom g;
   if (bucket_geom(dim, log2cap, &g)) return -4;  // per-class key space: the linear geometry
+  if (cspan > 0) {  // field-aware wire: no hashed key at or above dn + dc·cspan
+    const int gl = g.kshift + g.lgg;
+    const long long hi = (long long)dn + (long long)dc * cspan;
+    g.qused = (int)(((hi < dim ? hi : dim) + (1LL << gl) - 1) >> gl);
+  }
   const int K = nclass <= 2 ? 2 : nclass <= 4 ? 4 : nclass <= 8 ? 8 : 16;
   const size_t lds = ((size_t(1) << log2cap) + kOvf) * (4 + 4 * (size_t)K);
   if (lds > 160 * 1024) return -1;
@@ -547,7 +762,7 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
   const long long sact_ll = ((long long)B + R - 1) / R;
   const int S_act = sact_ll < S ? (int)sact_ll : S;
   const int gspan = g.kshift + g.lgg;
-  const int ng = (dim + (1 << gspan) - 1) >> gspan;
+  const int ng = min((dim + (1 << gspan) - 1) >> gspan, g.qused);  // unflushed groups are empty
   const size_t region = (size_t)S << log2cap;
   if (compact) {
     e = K == 2 ? launch_mc_reduce<2>(tables, S_act, S, g, dim, nclass, dacc, st)

@@ -94,6 +94,52 @@ __device__ __forceinline__ void decode_feature(FeatRaw r, int dn, int dc, int j,
   if (idx < 0) v = 0.f;
 }
 
+// The ≤ RMAX rows [t0, t1) of a register-dedup spoke on the field-aware compact wire
+// (cspan > 0; ≤ 64 features, lane = feature): key[e] / xv[e] of row e for this lane, -1 / 0
+// for absent features and rows past t1. Every load is in flight before any is decoded:
+// one 16-bit load per row and lane when the numericals are bf16 (lane-dependent base and
+// stride: numerical slot or categorical field), two loads otherwise.
+template <int RMAX, typename NumT>
+__device__ __forceinline__ void load_spoke_rows(const NumT* __restrict__ num, int dn,
+                                                const void* __restrict__ cat, int dc, int t0,
+                                                int t1, int lane, int dim, int bias, int cspan,
+                                                int (&key)[RMAX], float (&xv)[RMAX]) {
+  const bool is_num = lane < dn;
+  const bool is_cat = lane >= dn && lane < dn + dc;
+  const bool is_bias = bias && lane == dn + dc;
+  const int jn = is_num ? lane : 0;
+  const int jc = is_cat ? lane - dn : 0;
+  unsigned short raw[RMAX];
+  NumT nraw[sizeof(NumT) == 2 ? 1 : RMAX];
+  if constexpr (sizeof(NumT) == 2) {
+    const unsigned short* base = is_num ? reinterpret_cast<const unsigned short*>(num) + jn
+                                        : static_cast<const unsigned short*>(cat) + jc;
+    const int stride = is_num ? dn : dc;
+#pragma unroll
+    for (int e = 0; e < RMAX; ++e) raw[e] = base[(size_t)min(t0 + e, t1 - 1) * stride];
+  } else {
+#pragma unroll
+    for (int e = 0; e < RMAX; ++e) {
+      const int t = min(t0 + e, t1 - 1);
+      nraw[e] = num[(size_t)t * dn + jn];
+      raw[e] = static_cast<const unsigned short*>(cat)[(size_t)t * dc + jc];
+    }
+  }
+  const int cbase = dn + jc * cspan;
+#pragma unroll
+  for (int e = 0; e < RMAX; ++e) {
+    const unsigned c = raw[e];
+    float nv;
+    if constexpr (sizeof(NumT) == 2) nv = __uint_as_float(c << 16);  // bf16 bits
+    else nv = to_f(nraw[e]);
+    int idx = is_num ? lane : is_bias ? dim - 1 : (is_cat && c != 0xFFFFu) ? cbase + (int)(c & 0x7fffu) : -1;
+    const float v = is_num ? nv : is_bias ? 1.f : (c & 0x8000u) ? -1.f : 1.f;
+    if ((unsigned)idx >= (unsigned)dim || t0 + e >= t1) idx = -1;
+    key[e] = idx;
+    xv[e] = idx >= 0 ? v : 0.f;
+  }
+}
+
 __device__ __forceinline__ uint32_t hmix(uint32_t k) { return k * 0x9E3779B1u; }
 
 // Slow path of the bucketed table: probe the whole bucket, then the overflow area.

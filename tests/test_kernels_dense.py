@@ -495,3 +495,34 @@ def test_hip_gram_fused_poly2_vs_expanded_and_fp64(cuda, B, d0):
                                atol=2e-2)
     np.testing.assert_allclose(Gf.cpu().numpy(), Ge.cpu().numpy(), rtol=1e-5, atol=1e-2)
     assert torch.equal(Gf.cpu(), Gf.cpu().T)  # mirrored
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nclass,R,S", [(3, 16, 64), (4, 16, 80), (2, 8, 100), (4, 5, 70)])
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_hip_multiclass_register_dedup_matches_table_kernel(cuda, monkeypatch, nclass, R, S,
+                                                            variant):
+    """Field-aware wire, ≤ 16 rows per spoke, K ≤ 4: the register-dedup MultiClassPA round
+    (K deltas per row in registers) equals the LDS-table round (OMLDM_MC_RD=0) and the CPU
+    mirror; the stats agree."""
+    from omldm_amd.api.batch import FeatureSpace, HashedBatch
+
+    sp = FeatureSpace(13, 0, 26, 1 << 18, field_aware=True)
+    B = S * R - R // 3
+    b = synth_batch(sp, B, task=2, n_classes=nclass, seed=R * 7 + S)
+    W = torch.randn(nclass, sp.dim) * 0.01
+    g = HashedBatch(b.num.to(torch.bfloat16), b.cat, b.y.to(torch.int8), cat_span=b.cat_span)
+    out = {}
+    for rd in ("1", "0"):
+        monkeypatch.setenv("OMLDM_MC_RD", rd)
+        st = torch.zeros(8, device=cuda)
+        dacc = torch.zeros(nclass, sp.dim, device=cuda)
+        D.multiclass_round(W.to(cuda), g.to(cuda), R, S, nclass, variant, 0.7, True, dacc, st)
+        torch.cuda.synchronize()
+        out[rd] = (dacc.cpu(), st.cpu())
+    bc = HashedBatch(b.num.to(torch.bfloat16).float(), b.cat, b.y, cat_span=b.cat_span)
+    stc, daccc = torch.zeros(8), torch.zeros(nclass, sp.dim)
+    D.multiclass_round(W, bc, R, S, nclass, variant, 0.7, True, daccc, stc)
+    np.testing.assert_allclose(out["1"][0].numpy(), out["0"][0].numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(out["1"][1][:4].numpy(), out["0"][1][:4].numpy(), rtol=1e-5)
+    np.testing.assert_allclose(out["1"][0].numpy(), daccc.numpy(), rtol=2e-3, atol=2e-4)
