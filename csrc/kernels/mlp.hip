@@ -52,8 +52,17 @@ __device__ __forceinline__ f32x16 wave_gemm32_f32(const float* a, int ars, int a
   f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const float* ap = a + r * ars + kh * acs;
   const float* bp = b + kh * brs + r * bcs;
-  for (int k = 0; k < K; k += 2) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[k * acs], bp[k * brs], acc, 0, 0, 0);
+  // K is a multiple of 32 (padded widths / 32-row mini-batches): 8 operand pairs read
+  // ahead of their MFMAs, so the LDS latency is not paid once per instruction
+  for (int k = 0; k < K; k += 16) {
+    float av[8], bv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      av[u] = ap[(k + 2 * u) * acs];
+      bv[u] = bp[(k + 2 * u) * brs];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
   }
   return acc;
 }
@@ -74,6 +83,7 @@ __device__ __forceinline__ f32x16 wave_gemm32_bf16(const float* a, int ars, int 
   f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const float* ap = a + r * ars + 8 * kh * acs;
   const float* bp = b + 8 * kh * brs + r * bcs;
+#pragma unroll 2
   for (int k = 0; k < K; k += 16) {
     bf16x8 af, bfr;
 #pragma unroll
@@ -167,6 +177,22 @@ __device__ void stage_rows(const float* __restrict__ x, long long r0, long long 
   }
 }
 
+// Diagnostics only (csrc/tests/mlp_stamp_probe.hip builds with OMLDM_MLP_STAMPS): per
+// spoke, clock64 sums of the mini-batch phases (staging+barrier, forward, loss, backward).
+#ifdef OMLDM_MLP_STAMPS
+__device__ unsigned long long* g_mlp_stamps;
+#define MLP_STAMP(k)                                                                  \
+  do {                                                                                \
+    const unsigned long long now_ = clock64();                                        \
+    if (tid == 0 && (k) > 0) g_mlp_stamps[(size_t)blockIdx.x * 8 + (k)] += now_ - mlp_t_; \
+    mlp_t_ = now_;                                                                    \
+  } while (0)
+#else
+#define MLP_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict__ w,
                                                         const float* __restrict__ x,
                                                         const float* __restrict__ yv, long long B,
@@ -182,14 +208,55 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
   load_model(w, sm, g);
   float loss = 0.f, corr = 0.f, nv = 0.f;
   const int L = g.L, npL = g.np[L];
+  // Row staging with the NEXT mini-batch's loads in flight while the current one trains
+  // (np0 ≤ 64: ≤ 8 slots of the 32 × np0 tile per thread, fixed (row, col) per slot);
+  // wider inputs stage synchronously.
+  constexpr int kSlots = 8;
+  const int np0 = g.np[0], n0 = g.n[0], ld0 = g.ldh[0];
+  const bool pf = np0 <= 64;
+  int soff[kSlots], srow[kSlots], scol[kSlots];
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) {
+    const int i = tid + 256 * j;
+    const bool in = pf && i < kMB * np0;
+    srow[j] = in ? i / np0 : -1;
+    scol[j] = in ? i - srow[j] * np0 : 0;
+    soff[j] = in ? srow[j] * ld0 + scol[j] : 0;
+  }
+  float xr[kSlots];
+  float yr = 0.f;
+  auto fetch = [&](long long m) {  // unconditional loads from clamped rows
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) {
+      const long long row = min(m + (srow[j] < 0 ? 0 : srow[j]), r1 - 1);
+      xr[j] = x[row * n0 + (scol[j] < n0 ? scol[j] : 0)];
+    }
+    yr = yv[min(m + (tid < kMB ? tid : 0), r1 - 1)];
+  };
+  if (pf) fetch(r0);
+#ifdef OMLDM_MLP_STAMPS
+  unsigned long long mlp_t_ = clock64();
+#endif
   for (long long m0 = r0; m0 < r1; m0 += kMB) {
-    stage_rows(x, m0, r1, sm, g);
-    if (tid < kMB) {
-      const long long row = m0 + tid;
-      sm[g.ly + tid] = row < r1 ? yv[row] : __builtin_nanf("");
+    MLP_STAMP(0);
+    if (pf) {
+      float* H = sm + g.lh[0];
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j)
+        if (srow[j] >= 0) H[soff[j]] = (m0 + srow[j] < r1 && scol[j] < n0) ? xr[j] : 0.f;
+      if (tid < kMB) sm[g.ly + tid] = m0 + tid < r1 ? yr : __builtin_nanf("");
+      if (m0 + kMB < r1) fetch(m0 + kMB);
+    } else {
+      stage_rows(x, m0, r1, sm, g);
+      if (tid < kMB) {
+        const long long row = m0 + tid;
+        sm[g.ly + tid] = row < r1 ? yv[row] : __builtin_nanf("");
+      }
     }
     __syncthreads();
+    MLP_STAMP(1);
     forward(sm, g);
+    MLP_STAMP(2);
     // ---- loss gradient dZ_L (one thread per row)
     bool valid = false;
     if (tid < kMB) {
@@ -229,6 +296,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       }
     }
     const int cnt = __syncthreads_count(valid ? 1 : 0);
+    MLP_STAMP(3);
     if (cnt == 0) continue;
     const float eta = lr / (float)cnt;
     int gcur = g.lg0, gnext = g.lg1;
@@ -271,6 +339,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       gcur = gnext;
       gnext = tmp;
     }
+    MLP_STAMP(4);
   }
   // ---- round end: Δ = W_spoke − W_0. With a workspace: the spoke's own row, plain
   // coalesced stores (mlp_colsum_kernel sums the rows); without: atomics into the
