@@ -548,22 +548,40 @@ __global__ __launch_bounds__(NT) void linear_reduce_kernel(
   const long long items = (long long)(s_hi - s_lo) << (seg_log2 - 1);
   const int4* t4 = reinterpret_cast<const int4*>(tables) +
                    (((size_t)q * S + s_lo) << (seg_log2 - 1));
-  auto addr = [](long long ii) { return (size_t)ii; };
+  // Software-pipelined: the next batch of 4 loads is in flight while this batch's entries
+  // are added. Empty slots (key −1, most of a table) are skipped: LDS atomics are this
+  // kernel's bound, and adding 0 to a dummy word for them instead (branch-free) measured
+  // 26 → 46 µs.
+  auto add = [&](int key, int val) {
+    if (key >= 0) atomicAdd(&acc[key - lo], __int_as_float(val));
+  };
   long long it = threadIdx.x;
-  for (; it + 3 * NT < items; it += 4 * NT) {
-    int4 v[4];
+  // this thread's full batches: it + 4·NT·b + 3·NT < items (the old loop's condition)
+  const long long full = items - it - 3 * NT > 0 ? (items - it - 3 * NT - 1) / (4 * NT) + 1 : 0;
+  int4 v[4];
+  if (full > 0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = t4[addr(it + u * NT)];
+    for (int u = 0; u < 4; ++u) v[u] = t4[it + u * NT];
+  }
+  for (long long b = 0; b < full; ++b) {
+    int4 cur[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = v[u];
+    it += 4 * NT;
+    if (b + 1 < full) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = t4[it + u * NT];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (v[u].x >= 0) atomicAdd(&acc[v[u].x - lo], __int_as_float(v[u].y));
-      if (v[u].z >= 0) atomicAdd(&acc[v[u].z - lo], __int_as_float(v[u].w));
+      add(cur[u].x, cur[u].y);
+      add(cur[u].z, cur[u].w);
     }
   }
   for (; it < items; it += NT) {
-    const int4 v = t4[addr(it)];
-    if (v.x >= 0) atomicAdd(&acc[v.x - lo], __int_as_float(v.y));
-    if (v.z >= 0) atomicAdd(&acc[v.z - lo], __int_as_float(v.w));
+    const int4 w4 = t4[it];
+    add(w4.x, w4.y);
+    add(w4.z, w4.w);
   }
   __syncthreads();
   if (split == 1) {  // sole owner of the key range
