@@ -39,6 +39,7 @@ CASES = [
     ("MultiClassPA@compact", 2, {"nClasses": 4}, 8192, "compact"),
     ("ORR", 1, {}, 1),
     ("K-means", 0, {"k": 16}, 1),
+    ("K-means@k256", 0, {"k": 256}, 1),  # matrix-core distances (k >= 32)
     # 512 spokes × 256 rows: fastest of 256..2048 (bench/sweep_cases_nn.json)
     ("NN", 0, {"hiddenLayers": [64, 64]}, 512),
     ("NN@bf16", 0, {"hiddenLayers": [64, 64], "matmulDtype": "bf16"}, 512),

@@ -301,6 +301,107 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
   }
 }
 
+// Nearest-centroid assignment on the matrix cores (k ≥ 32 centroids): distances as
+// ‖c‖² − 2·c·x (the row's own ‖x‖² does not change its argmin) with C·Xᵀ tiles on
+// v_mfma_f32_32x32x2_f32 (exact fp32 products). A wave takes 32-row tiles; A = a 32-centroid
+// tile staged in LDS (odd row stride: the 32 lanes of an operand column on distinct banks),
+// B = the tile's rows, each lane keeping its row's features in registers across all
+// centroid tiles. Lane (j, h) ends a tile holding c_i·x_j for 16 centroids i of its half,
+// so the argmin is an in-lane minimum plus one exchange with lane j ^ 32. Training rows then
+// add x into the block's LDS cluster sums as the scalar kernel does.
+template <int DMAX>
+__global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
+    const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int k,
+    const float* __restrict__ cent, float* __restrict__ sums, float* __restrict__ counts,
+    int* __restrict__ assign, float* __restrict__ inertia) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int kp = (k + 31) & ~31;
+  const int dp = (d + 1) & ~1;
+  const int ldc = dp | 1;
+  float* cs = reinterpret_cast<float*>(smem);  // [kp][ldc]
+  float* cn = cs + (size_t)kp * ldc;           // [kp]  ‖c‖² (+inf for padding)
+  float* s = cn + kp;                          // [k][d] cluster sums of this block
+  float* n = s + (size_t)k * d;                // [k]
+  __shared__ float part[4];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (int i = tid; i < kp * ldc; i += 256) {
+    const int r = i / ldc, c = i - r * ldc;
+    cs[i] = (r < k && c < d) ? cent[(size_t)r * d + c] : 0.f;
+  }
+  for (int i = tid; i < k * d; i += 256) s[i] = 0.f;
+  for (int i = tid; i < k; i += 256) n[i] = 0.f;
+  __syncthreads();
+  for (int r = tid; r < kp; r += 256) {
+    float a = 0.f;
+    for (int c = 0; c < d; ++c) a = fmaf(cs[r * ldc + c], cs[r * ldc + c], a);
+    cn[r] = r < k ? a : INFINITY;
+  }
+  __syncthreads();
+  const int j = lane & 31, h = lane >> 5;
+  float my_in = 0.f;
+  for (long long t = (long long)blockIdx.x * 4 + wave; t * 32 < B; t += (long long)gridDim.x * 4) {
+    const long long row = t * 32 + j;
+    const bool vrow = row < B;
+    const float* xr = x + (vrow ? row : B - 1) * (long long)d;
+    float xv[DMAX / 2];  // features h, h+2, h+4, ... of this lane's row (the B operand)
+#pragma unroll
+    for (int u = 0; u < DMAX / 2; ++u) {
+      const int f = 2 * u + h;
+      xv[u] = f < d ? xr[f < d ? f : 0] : 0.f;
+    }
+    float best = INFINITY;
+    int bi = 0;
+    for (int ct = 0; ct < kp; ct += 32) {
+      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const float* ca = cs + (size_t)(ct + j) * ldc + h;
+#pragma unroll
+      for (int u = 0; u < DMAX / 2; ++u)
+        if (2 * u < dp) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[2 * u], xv[u], acc, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = ct + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const float dist = cn[i] - 2.f * acc[q];
+        if (dist < best) {
+          best = dist;
+          bi = i;
+        }
+      }
+    }
+    // the other half-wave holds the same row's other 16 centroids of every tile
+    const float ob = __shfl_xor(best, 32);
+    const int oi = __shfl_xor(bi, 32);
+    if (ob < best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+    if (h == 0 && vrow) {
+      if (assign) assign[row] = bi;
+      const bool train = yv == nullptr || !__builtin_isnan(yv[row]);
+      if (train && sums) {
+        float xx = 0.f;
+        for (int f = 0; f < d; ++f) {
+          const float v = xr[f];
+          xx = fmaf(v, v, xx);
+          atomicAdd(&s[bi * d + f], v);
+        }
+        atomicAdd(&n[bi], 1.f);
+        my_in += fmaxf(0.f, xx + best);  // ‖x − c‖² ≥ 0 (rounding)
+      }
+    }
+  }
+  __syncthreads();
+  if (sums) {
+    for (int i = tid; i < k * d; i += 256)
+      if (s[i] != 0.f) atomicAdd(&sums[i], s[i]);
+    for (int i = tid; i < k; i += 256)
+      if (n[i] != 0.f) atomicAdd(&counts[i], n[i]);
+    const float w = wave_sum(my_in);
+    if (lane == 0) part[wave] = w;
+    __syncthreads();
+    if (tid == 0 && inertia) atomicAdd(inertia, (part[0] + part[1]) + (part[2] + part[3]));
+  }
+}
+
 // Count-weighted centroid move of one micro-batch, fused with the bookkeeping the learner
 // used to do in ~12 small elementwise launches:
 //   tot = n + cnt; c ← (n·c + Σx)/tot where tot > 0; n ← tot; Σx, cnt ← 0;
@@ -406,10 +507,38 @@ OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, fl
   return (int)hipGetLastError();
 }
 
+template <int DMAX>
+static int launch_kmeans_mfma(const float* x, const float* y, int B, int d, int k,
+                              const float* cent, float* sums, float* counts, int* assign,
+                              float* inertia, size_t lds, hipStream_t st) {
+  auto fn = kmeans_assign_mfma_kernel<DMAX>;
+  int e = check_dyn_lds((const void*)fn, lds);
+  if (e) return e;
+  const long long tiles = ((long long)B + 31) / 32;
+  int blocks = (int)((tiles + 3) / 4);
+  if (blocks > 512) blocks = 512;  // each block flushes k·d sums: keep the flush small
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), lds, st, x, y, B, d, k, cent, sums, counts,
+                     assign, inertia);
+  return (int)hipGetLastError();
+}
+
 OMLDM_API int omldm_kmeans_assign(const float* x, const float* y, int B, int d, int k,
                                   const float* cent, float* sums, float* counts, int* assign,
                                   float* inertia, void* stream) {
   if (B <= 0) return 0;
+  // matrix-core distances once there is a full 32-centroid tile and a few features
+  // (OMLDM_KMEANS_MFMA=0: the scalar kernel, A/B)
+  const char* mf = getenv("OMLDM_KMEANS_MFMA");
+  if (k >= 32 && d >= 4 && d <= 128 && !(mf && atoi(mf) == 0)) {
+    const int kp = (k + 31) & ~31, ldc = ((d + 1) & ~1) | 1;
+    const size_t lds = ((size_t)kp * ldc + kp + (size_t)k * d + k) * 4;
+    if (lds <= 150 * 1024) {
+      hipStream_t st = (hipStream_t)stream;
+      if (d <= 32) return launch_kmeans_mfma<32>(x, y, B, d, k, cent, sums, counts, assign, inertia, lds, st);
+      if (d <= 64) return launch_kmeans_mfma<64>(x, y, B, d, k, cent, sums, counts, assign, inertia, lds, st);
+      return launch_kmeans_mfma<128>(x, y, B, d, k, cent, sums, counts, assign, inertia, lds, st);
+    }
+  }
   const size_t lds = (size_t)(2 * k * d + k) * 4;
   if (lds > 150 * 1024) return -1;
   int e = check_dyn_lds((const void*)kmeans_assign_kernel, lds);

@@ -152,6 +152,33 @@ def test_hip_kmeans_assign(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B,d,k", [(3000, 13, 32), (5001, 8, 50), (20000, 64, 256),
+                                   (4097, 100, 40), (777, 31, 97)])
+def test_hip_kmeans_assign_mfma(cuda, B, d, k):
+    """k ≥ 32: matrix-core distances. The chosen centroid is a nearest one (fp64 distances,
+    up to rounding ties), and sums / counts / inertia follow the kernel's own assignment."""
+    torch.manual_seed(B)
+    x = torch.randn(B, d)
+    cent = torch.randn(k, d)
+    y = torch.zeros(B)
+    y[::7] = float("nan")  # forecast rows: assigned, not summed
+    sg, ng, ig = torch.zeros(k, d, device=cuda), torch.zeros(k, device=cuda), \
+        torch.zeros(1, device=cuda)
+    a = D.kmeans_assign(x.to(cuda), y.to(cuda), cent.to(cuda), sg, ng, ig,
+                        want_assign=True).cpu().long()
+    dist = torch.cdist(x.double(), cent.double()) ** 2
+    dmin = dist.min(1).values
+    chosen = dist.gather(1, a[:, None])[:, 0]
+    assert torch.all(chosen - dmin <= 1e-4 * (1 + dmin)), (chosen - dmin).max()
+    tr = ~torch.isnan(y)
+    s = torch.zeros(k, d, dtype=torch.float64).index_add_(0, a[tr], x[tr].double())
+    n = torch.bincount(a[tr], minlength=k).double()
+    np.testing.assert_allclose(sg.cpu().double().numpy(), s.numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(ng.cpu().double().numpy(), n.numpy())
+    np.testing.assert_allclose(ig.cpu().item(), chosen[tr].sum().item(), rtol=1e-4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("nclass,R,S", [(4, 50, 40), (3, 16, 96), (2, 8, 64), (7, 16, 32),
                                          (12, 8, 32)])
 def test_hip_multiclass_round_vs_cpu(cuda, nclass, R, S):
