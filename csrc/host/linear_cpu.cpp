@@ -20,7 +20,7 @@ namespace {
 
 struct P {
   int rule, variant;
-  float C, eps, lr, lam, inv_p;
+  float C, eps, lr, lam, inv_p, tbase;
 };
 
 inline float pa_tau(float loss, float n2, const P& p) {
@@ -65,8 +65,8 @@ OMLDM_HOST_API int omldm_cpu_linear_round(const void* w, int w_bf16, const float
                                           int R, int S, float* dacc, int dim, float* stats,
                                           int rule, int variant, float C, float eps, float lr,
                                           float lam, float inv_p, int bias, int cspan,
-                                          int nthreads) {
-  const P p{rule, variant, C, eps, lr, lam, inv_p};
+                                          float tbase, int nthreads) {
+  const P p{rule, variant, C, eps, lr, lam, inv_p, tbase};
   const float* w32 = static_cast<const float*>(w);
   const uint16_t* w16 = static_cast<const uint16_t*>(w);
   auto wget = [&](int i) { return w_bf16 ? bf16_to_f(w16[i]) : w32[i]; };
@@ -110,7 +110,14 @@ OMLDM_HOST_API int omldm_cpu_linear_round(const void* w, int w_bf16, const float
         }
         const float m = sigma * pm;
         float c = 0.f, shrink = 1.f;
-        if (p.rule == 0) {
+        if (p.rule == 3) {  // Pegasos: η = 1/(λT), w ← (1 − 1/T)·w + η·y·x·[y·w·x < 1]
+          const float T = p.tbase + (float)(t - a);
+          const float ym = yt * m;
+          loss_sum += std::fmax(0.f, 1.f - ym);
+          mist += ym <= 0.f ? 1.f : 0.f;
+          c = ym < 1.f ? (1.f / (p.lam * T)) * yt : 0.f;
+          shrink = (T - 1.f) / T;
+        } else if (p.rule == 0) {
           const float ym = yt * m;
           const float loss = std::fmax(0.f, 1.f - ym);
           loss_sum += loss;

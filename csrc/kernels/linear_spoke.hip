@@ -29,7 +29,7 @@
 
 namespace omldm {
 
-enum LinRule : int { kHinge = 0, kEpsInsensitive = 1, kLogistic = 2 };
+enum LinRule : int { kHinge = 0, kEpsInsensitive = 1, kLogistic = 2, kPegasos = 3 };
 enum PAVariant : int { kPA = 0, kPA1 = 1, kPA2 = 2 };
 
 struct LinParams {
@@ -47,6 +47,7 @@ struct LinParams {
   float shrink;   // per-step multiplicative L2 shrink of w (1 when λ = 0)
   float rshrink;  // 1 / shrink
   int y_i8;       // labels on the wire as int8 (classification streams: ±1 exactly)
+  float tbase;    // Pegasos: step index T of the spoke's first row this round (≥ 2)
 };
 
 // Per-spoke workspace row: [loss, n, mistakes, sq_err, sigma, overflow, σ/P, 1/P,
@@ -63,12 +64,37 @@ __device__ __forceinline__ int dense_col(int j, int dn, int dc, int bias) {
   return -1;
 }
 
+// Per-row L2 shrink of w (σ ← σ·sh, 1/σ ← 1/σ·rsh) and step size. Pegasos (Shalev-Shwartz
+// et al. 2007, the SVM option of SURVEY Appendix D): at step T, η = 1/(λT) and
+// w ← (1 − ηλ)·w + η·y·x·[y·w·x < 1], so sh = (T − 1)/T; T counts the spoke's rows
+// (p.tbase ≥ 2 keeps σ > 0). Every other rule: the constant shrink of λ.
+template <int RULE>
+__device__ __forceinline__ void row_rate(const LinParams& p, int row, float& sh, float& rsh,
+                                         float& eta) {
+  if constexpr (RULE == kPegasos) {
+    const float T = p.tbase + (float)row;
+    sh = (T - 1.f) / T;
+    rsh = T / (T - 1.f);
+    eta = 1.f / (p.lam * T);
+  } else {
+    sh = p.shrink;
+    rsh = p.rshrink;
+    eta = 0.f;
+  }
+}
+
 template <int RULE>
 struct Step {
   // returns (loss, c) for margin m, label y, ‖x‖² n2; updates counters
-  __device__ __forceinline__ static void run(float m, float y, float n2, const LinParams& p,
-                                             float& loss_sum, float& mist, float& sqe, float& c) {
-    if constexpr (RULE == kHinge) {
+  __device__ __forceinline__ static void run(float m, float y, float n2, float eta,
+                                             const LinParams& p, float& loss_sum, float& mist,
+                                             float& sqe, float& c) {
+    if constexpr (RULE == kPegasos) {  // hinge sub-gradient step
+      const float ym = y * m;
+      loss_sum += fmaxf(0.f, 1.f - ym);
+      mist += ym <= 0.f ? 1.f : 0.f;
+      c = ym < 1.f ? eta * y : 0.f;
+    } else if constexpr (RULE == kHinge) {
       const float ym = y * m;
       const float loss = fmaxf(0.f, 1.f - ym);
       loss_sum += loss;
@@ -261,11 +287,12 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
         pn = fmaf(xv[e][f], xv[e][f], pn);
       }
       wave_sum2(pm, pn);
-      float c;
-      Step<RULE>::run(sigma * pm, y, pn, p, loss_sum, mist, sqe, c);
+      float c, sh, rsh, eta;
+      row_rate<RULE>(p, tc - t0 + e, sh, rsh, eta);
+      Step<RULE>::run(sigma * pm, y, pn, eta, p, loss_sum, mist, sqe, c);
       nex += 1.f;
-      sigma *= p.shrink;
-      rsig *= p.rshrink;
+      sigma *= sh;
+      rsig *= rsh;
       if (c != 0.f) {  // wave-uniform
         const float cv = c * rsig;
 #pragma unroll
@@ -408,11 +435,12 @@ __global__ __launch_bounds__(64, 5) void linear_round_rd_kernel(
     const float y = readlane_f(ylane, e);
     if (__builtin_isnan(y)) continue;  // wave-uniform (rows past t1 are NaN too)
     const float pm = wave_sum(xv[e] * (wv[e] + d[e]));
-    float c;
-    Step<RULE>::run(sigma * pm, y, pn[e], p, loss_sum, mist, sqe, c);
+    float c, sh, rsh, eta;
+    row_rate<RULE>(p, e, sh, rsh, eta);
+    Step<RULE>::run(sigma * pm, y, pn[e], eta, p, loss_sum, mist, sqe, c);
     nex += 1.f;
-    sigma *= p.shrink;
-    rsig *= p.rshrink;
+    sigma *= sh;
+    rsig *= rsh;
     if (c != 0.f) {  // wave-uniform
       const float u = (c * rsig) * xv[e];
       d[e] += u;
@@ -866,6 +894,9 @@ static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, i
       return dispatch_round_rd<kEpsInsensitive>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
                                                 dacc, dim, ws, tables, cum, p, g, ablate, parts,
                                                 st);
+    if (rule == kPegasos)
+      return dispatch_round_rd<kPegasos>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
+                                         dim, ws, tables, cum, p, g, ablate, parts, st);
     return dispatch_round_rd<kLogistic>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
                                         dim, ws, tables, cum, p, g, ablate, parts, st);
   }
@@ -876,6 +907,9 @@ static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, i
     return dispatch_round<FPL, CH, kEpsInsensitive>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R,
                                                     S, dacc, dim, ws, tables, cum, p, g, ablate,
                                                     parts, st);
+  if (rule == kPegasos)
+    return dispatch_round<FPL, CH, kPegasos>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
+                                             dacc, dim, ws, tables, cum, p, g, ablate, parts, st);
   return dispatch_round<FPL, CH, kLogistic>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
                                             dacc, dim, ws, tables, cum, p, g, ablate, parts, st);
 }
@@ -962,9 +996,10 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
                                  int R, int S, float* dacc, int dim, float* ws, void* tables,
                                  double* cum, int rule, int variant, float C, float eps, float lr,
                                  float lam, float inv_p, int bias, int cspan, int log2cap,
-                                 int chunk, int ablate, int parts, void* stream) {
+                                 int chunk, int ablate, int parts, float tbase, void* stream) {
   if (S <= 0) return 0;
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
+  if (rule == kPegasos && !(lam > 0.f && tbase >= 2.f)) return -5;
   if (parts < 1 || parts > 64) return -4;
   int geo[3];
   if (omldm_linear_table_geom(dim, log2cap, geo)) return -3;
@@ -974,7 +1009,7 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
   const float shrink = rule == kLogistic ? 1.f - lr * lam : 1.f - lam;
   const LinParams p{rule, variant, C, eps, lr, lam, inv_p, bias, cspan,
                     variant == kPA1 ? C : INFINITY, variant == kPA2 ? 0.5f / C : 0.f, shrink,
-                    1.f / shrink, y_i8 ? 1 : 0};
+                    1.f / shrink, y_i8 ? 1 : 0, tbase};
   const int F = dn + dc + (bias ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
   int2* tb = (int2*)tables;

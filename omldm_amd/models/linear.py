@@ -7,7 +7,11 @@ published Passive-Aggressive family (Crammer et al. 2006) — SURVEY.md Appendix
 * ``PA``          binary hinge, τ = ℓ/‖x‖² (variant "PA"), min(C, ℓ/‖x‖²) ("PA-I"),
                   ℓ/(‖x‖² + 1/(2C)) ("PA-II"); default PA-I.
 * ``SVM``         online linear SVM: hinge loss + L2 (``lambda`` shrink per step) with the
-                  PA-I step (BASELINE.json config 1: "Online linear SVM (PA-I)").
+                  PA-I step (BASELINE.json config 1: "Online linear SVM (PA-I)");
+                  ``variant: "Pegasos"`` (PA and SVM) selects Pegasos SGD instead (SURVEY
+                  Appendix D): at the spoke's step T, η = 1/(λT) and
+                  w ← (1 − 1/T)·w + η·y·x·[y·w·x < 1]; T counts each spoke's rows from
+                  ``t0`` + 1 (default t0 = 1, so σ never reaches 0; λ defaults to 1e-4).
 * ``RegressorPA`` ε-insensitive loss, same τ family, update sign(y − w·x)·τ·x.
 * ``LogisticRegression`` (extension, BASELINE.json config 2): SGD on the log loss.
 
@@ -43,15 +47,21 @@ class LinearLearner(Learner):
     def _configure(self) -> None:
         h = self.hyper
         variant = str(h.get("variant", self.DEFAULT_VARIANT))
+        pegasos = variant.lower() == "pegasos" and self.RULE == L.RULE_HINGE
         self.rule = L.LinearRule(
-            rule=self.RULE,
+            rule=L.RULE_PEGASOS if pegasos else self.RULE,
             variant=_VARIANTS.get(variant, L.PA1),
             C=hp_float(h, "C", 1.0),
             eps=hp_float(h, "epsilon", 0.1),
             lr=hp_float(h, "learningRate", 0.1),
-            lam=hp_float(h, "lambda", 0.0),
+            lam=hp_float(h, "lambda", 1e-4 if pegasos else 0.0),
             bias=bool(h.get("bias", True)),
         )
+        if pegasos and not self.rule.lam > 0:
+            raise ValueError("Pegasos needs lambda > 0")
+        self.t0 = max(1, hp_int(h, "t0", 1))
+        if not hasattr(self, "steps"):
+            self.steps = 0  # rows per spoke trained in earlier rounds (the Pegasos clock)
         self.log2cap = hp_int(h, "tableLog2", 0)  # 0: auto (ops/linear.py:auto_log2cap)
         self.ablate = hp_int(h, "_ablate", 0)  # timing diagnostics only
         self.chunk = hp_int(h, "chunk", 8)      # rows staged per software-pipeline step
@@ -89,9 +99,11 @@ class LinearLearner(Learner):
         R = max(1, -(-B // S)) if B else 1
         parts = max(1, int(ctx.reduce_parts)) if ctx.on_reduce_part is not None else 1
         if B:
+            self.rule.tbase = float(self.t0 + 1 + self.steps)
             L.linear_round(self._wread(), batch, R, S, self.dacc, None, self.rule, ctx.inv_p,
                            self.log2cap, cum=self.cum, ablate=self.ablate, chunk=self.chunk,
                            parts=parts, on_part=ctx.on_reduce_part)
+            self.steps += R
         else:
             self.dacc[self.dim:].zero_()  # no workers this round on this rank
             if ctx.on_reduce_part is not None:  # still join every collective of the round
@@ -105,6 +117,14 @@ class LinearLearner(Learner):
 
     def apply_delta(self) -> None:
         L.linear_apply(self.w, self.w16, self.dacc)
+
+    def state_dict(self) -> dict:
+        return {**super().state_dict(), "steps": self.steps}
+
+    def load_state_dict(self, sd: dict) -> None:
+        super().load_state_dict(sd)
+        self._configure()
+        self.steps = int(sd.get("steps", self.steps))
 
     # ------------------------------------------------------------ protocol view
     def state_vector(self) -> torch.Tensor:
@@ -146,7 +166,8 @@ class LinearLearner(Learner):
     def hyper_parameters(self) -> dict:
         r = self.rule
         names = {L.PA: "PA", L.PA1: "PA-I", L.PA2: "PA-II"}
-        return {**self.hyper, "C": r.C, "variant": names[r.variant], "epsilon": r.eps,
+        variant = "Pegasos" if r.rule == L.RULE_PEGASOS else names[r.variant]
+        return {**self.hyper, "C": r.C, "variant": variant, "epsilon": r.eps,
                 "learningRate": r.lr, "lambda": r.lam, "bias": r.bias}
 
     def parameters_map(self) -> dict:

@@ -17,7 +17,7 @@ from omldm_amd.ops.native import check, ptr
 
 STAT_W = 6  # loss_sum, n, mistakes, sq_err, sigma, overflow
 
-RULE_HINGE, RULE_EPS, RULE_LOGISTIC = 0, 1, 2
+RULE_HINGE, RULE_EPS, RULE_LOGISTIC, RULE_PEGASOS = 0, 1, 2, 3
 PA, PA1, PA2 = 0, 1, 2
 
 
@@ -30,6 +30,8 @@ class LinearRule:
     lr: float = 0.1
     lam: float = 0.0
     bias: bool = True
+    # RULE_PEGASOS: step index T of each spoke's first row this round (row e: T + e; ≥ 2)
+    tbase: float = 2.0
 
 
 WS_STAT = 8  # per-spoke workspace stat columns (see linear_spoke.hip kWsStat)
@@ -90,6 +92,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
     assert cat.dtype == (torch.int16 if batch.cat_span else torch.int32)
     # labels: fp32, or int8 on the compact classification wire (GPU kernel reads either)
     assert y.dtype == torch.float32 or (y.dtype == torch.int8 and rule.rule != RULE_EPS)
+    assert rule.rule != RULE_PEGASOS or (rule.lam > 0 and rule.tbase >= 2), "Pegasos: λ > 0, T ≥ 2"
     assert num.is_contiguous() and cat.is_contiguous() and y.is_contiguous()
     if S <= 0:
         return
@@ -113,7 +116,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
             ptr(dacc), dim,
             ptr(ws), ptr(tables), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr,
             rule.lam, inv_p, int(rule.bias), batch.cat_span, log2cap, int(chunk), int(ablate),
-            int(parts), native.stream_of(w))
+            int(parts), float(rule.tbase), native.stream_of(w))
         check(rc, "omldm_linear_round")
         if on_part is not None:
             on_part(0, *part_bounds(dim, 0, parts, cuda=True))
@@ -134,7 +137,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
             ptr(w), int(w.dtype == torch.bfloat16), ptr(num32), num32.shape[1], ptr(cat),
             cat.shape[1], ptr(y), batch.B, R, S, ptr(dacc), dim, ptr(st), rule.rule,
             rule.variant, rule.C, rule.eps, rule.lr, rule.lam, inv_p, int(rule.bias), batch.cat_span,
-            _cpu_threads())
+            float(rule.tbase), _cpu_threads())
         if cum is not None:
             cum[:STAT_W] += st.sum(0)
             cum[4] -= st[:, 4].sum()  # sigma is not a running total

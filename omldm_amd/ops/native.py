@@ -43,7 +43,7 @@ HIP_SIGS = [
     ("omldm_linear_round", i32, [vp, i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, i32, vp, i32,
                                  vp,
                                  vp, vp, i32, i32, f32, f32, f32, f32, f32, i32, i32, i32, i32,
-                                 i32, i32, vp]),
+                                 i32, i32, f32, vp]),
     ("omldm_linear_reduce_part", i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,
                                        i32, i32, i32, vp]),
     ("omldm_linear_part_bounds", i32, [i32, i32, i32, vp]),
@@ -106,7 +106,7 @@ HOST_SIGS = [
     ("omldm_synth_batch", None, [u64, i64, i32, i32, i32, i64, i32, i32, f32, i32, vp, vp, vp,
                                  i32]),
     ("omldm_cpu_linear_round", i32, [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, i32, vp,
-                                     i32, i32, f32, f32, f32, f32, f32, i32, i32, i32]),
+                                     i32, i32, f32, f32, f32, f32, f32, i32, i32, f32, i32]),
     ("omldm_cpu_linear_apply", None, [vp, vp, vp, i32]),
     ("omldm_index_lines", i64, [vp, i64, i64, vp]),
     ("omldm_format_predictions", i64, [vp, vp, vp, i64, i32, vp, vp, i64, vp]),

@@ -50,7 +50,13 @@ def python_round(w, batch, R, S, rule: L.LinearRule, inv_p=1.0):
                     return min(rule.C, loss / n2)
                 return loss / (n2 + 0.5 / rule.C)
 
-            if rule.rule == L.RULE_HINGE:
+            if rule.rule == L.RULE_PEGASOS:  # η = 1/(λT), w ← (1 − 1/T)w + η·y·x·[ym < 1]
+                T = rule.tbase + (t - a)
+                loss = max(0.0, 1 - yt * m)
+                c = yt / (rule.lam * T) if yt * m < 1 else 0.0
+                stats[s, 2] += yt * m <= 0
+                shrink = (T - 1) / T
+            elif rule.rule == L.RULE_HINGE:
                 loss = max(0.0, 1 - yt * m)
                 c = tau(loss) * yt
                 stats[s, 2] += yt * m <= 0
@@ -87,6 +93,7 @@ RULES = [
     L.LinearRule(L.RULE_HINGE, L.PA2, C=2.0, lam=1e-3),
     L.LinearRule(L.RULE_EPS, L.PA1, C=1.0, eps=0.05),
     L.LinearRule(L.RULE_LOGISTIC, lr=0.05, lam=1e-4),
+    L.LinearRule(L.RULE_PEGASOS, lam=0.05, tbase=40.0),
 ]
 
 
@@ -335,3 +342,27 @@ def test_hip_register_dedup_round_matches_table_kernel_and_cpu(cuda, rule, R, S,
                                rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(out["rd"][0].numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-4)
     np.testing.assert_allclose(out["rd"][1][:, 1].numpy(), s_cpu[:, 1].numpy())
+
+
+def test_pegasos_variant_learner():
+    """SVM with variant Pegasos: the per-spoke step clock advances by R per round, is
+    checkpointed, and the model separates the synthetic stream."""
+    from omldm_amd.models import make_learner
+    from omldm_amd.models.base import RoundContext
+
+    sp = FeatureSpace(13, 0, 26, 1 << 14)
+    lr = make_learner("SVM", {"variant": "Pegasos", "lambda": 1e-3}, sp, "cpu")
+    assert lr.rule.rule == L.RULE_PEGASOS and lr.hyper_parameters()["variant"] == "Pegasos"
+    for r in range(6):
+        b = synth_batch(sp, 2048, start=r * 2048, seed=4)
+        lr.fit(b, RoundContext(spokes=16))
+    assert lr.steps == 6 * 128
+    sd = lr.state_dict()
+    lr2 = make_learner("SVM", {"variant": "Pegasos", "lambda": 1e-3}, sp, "cpu")
+    lr2.load_state_dict(sd)
+    assert lr2.steps == lr.steps and torch.equal(lr2.w, lr.w)
+    test = synth_batch(sp, 4096, start=10**6, seed=4)
+    acc = float((lr.predict(test) == test.y).float().mean())
+    assert acc > 0.7
+    with pytest.raises(ValueError):
+        make_learner("SVM", {"variant": "Pegasos", "lambda": 0}, sp, "cpu")
