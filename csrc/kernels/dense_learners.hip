@@ -16,6 +16,7 @@
 namespace omldm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kKmeansMaxBlocks = 512;  // rows of the K-means partials image
 
 // Element (k, c) of the augmented row-major batch: c < d → x[k][c]; c == d → 1;
 // c == d+1 → y[k]; beyond → 0 (tile padding). Rows ≥ B → 0.
@@ -245,22 +246,77 @@ __global__ __launch_bounds__(256) void gram_mirror_kernel(float* __restrict__ G,
   }
 }
 
+// Block flush of the K-means partials. With `bpart`: the block's k·d sums, k counts and
+// inertia go to its own row of the partials image with plain coalesced stores
+// (kmeans_colsum_kernel adds the rows per column: a handful of atomics per address instead
+// of one per block, which serialised at the memory side); without: atomics per block.
+__device__ __forceinline__ void kmeans_flush(const float* s, const float* n, float my_in, int k,
+                                             int d, float* __restrict__ sums,
+                                             float* __restrict__ counts,
+                                             float* __restrict__ inertia,
+                                             float* __restrict__ bpart, float* red4) {
+  const int tid = threadIdx.x;
+  const float w = wave_sum(my_in);
+  if ((tid & 63) == 0) red4[tid >> 6] = w;
+  __syncthreads();
+  const float tot = (red4[0] + red4[1]) + (red4[2] + red4[3]);
+  const int kd = k * d;
+  if (bpart) {
+    float* row = bpart + (size_t)blockIdx.x * (kd + k + 1);
+    for (int i = tid; i < kd; i += 256) row[i] = s[i];
+    for (int i = tid; i < k; i += 256) row[kd + i] = n[i];
+    if (tid == 0) row[kd + k] = tot;
+    return;
+  }
+  for (int i = tid; i < kd; i += 256)
+    if (s[i] != 0.f) atomicAdd(&sums[i], s[i]);
+  for (int i = tid; i < k; i += 256)
+    if (n[i] != 0.f) atomicAdd(&counts[i], n[i]);
+  if (tid == 0 && inertia) atomicAdd(inertia, tot);
+}
+
+// Column sums of the partials image [nb][k·d + k + 1] into sums / counts / inertia: thread
+// = column, blockIdx.y = a slab of 64 block rows (one atomic per column per slab).
+__global__ __launch_bounds__(256) void kmeans_colsum_kernel(const float* __restrict__ part, int nb,
+                                                            int k, int d, float* __restrict__ sums,
+                                                            float* __restrict__ counts,
+                                                            float* __restrict__ inertia) {
+  const int kd = k * d, pw = kd + k + 1;
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= pw) return;
+  const int b0 = blockIdx.y * 64, b1 = min(nb, b0 + 64);
+  float a = 0.f;
+#pragma unroll 16
+  for (int b = b0; b < b1; ++b) a += part[(size_t)b * pw + col];
+  if (a == 0.f) return;
+  float* dst = col < kd ? &sums[col] : col < kd + k ? &counts[col - kd] : inertia;
+  if (dst) atomicAdd(dst, a);
+}
+
 // ---- K-means -------------------------------------------------------------------------
 // One thread per row: nearest centroid (centroids staged in LDS), per-block LDS sums of
 // rows and counts per cluster, one atomic per (cluster, feature) per block.
+// DMAX > 0 (d ≤ DMAX): the row is loaded into registers once (all loads in flight
+// together, zero past d) and every distance and the sums read it from there; the
+// centroids are staged zero-padded to DMAX columns, so the distance loop needs no masks.
+// DMAX == 0: any d, the row is re-read through L1 per centroid.
+template <int DMAX>
 __global__ __launch_bounds__(256) void kmeans_assign_kernel(
     const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int k,
     const float* __restrict__ cent, float* __restrict__ sums, float* __restrict__ counts,
-    int* __restrict__ assign, float* __restrict__ inertia) {
+    int* __restrict__ assign, float* __restrict__ inertia, float* __restrict__ bpart) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* c = reinterpret_cast<float*>(smem);  // [k][d]
-  float* s = c + k * d;                       // [k][d]
+  constexpr int kDm = DMAX > 0 ? DMAX : 1;
+  const int cw = DMAX > 0 ? DMAX : d;          // centroid row width in LDS
+  float* c = reinterpret_cast<float*>(smem);  // [k][cw]
+  float* s = c + k * cw;                      // [k][d]
   float* n = s + k * d;                       // [k]
   __shared__ float part[4];
-  for (int i = threadIdx.x; i < k * d; i += 256) {
-    c[i] = cent[i];
-    s[i] = 0.f;
+  for (int i = threadIdx.x; i < k * cw; i += 256) {
+    const int r = i / cw, f = i - r * cw;
+    c[i] = f < d ? cent[r * d + f] : 0.f;
   }
+  for (int i = threadIdx.x; i < k * d; i += 256) s[i] = 0.f;
   for (int i = threadIdx.x; i < k; i += 256) n[i] = 0.f;
   __syncthreads();
   float my_in = 0.f;
@@ -269,36 +325,56 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
     const float* xr = x + r * d;
     int best = 0;
     float bd = INFINITY;
-    for (int j = 0; j < k; ++j) {
-      float dd = 0.f;
-      for (int f = 0; f < d; ++f) {
-        const float t = xr[f] - c[j * d + f];
-        dd = fmaf(t, t, dd);
+    if constexpr (DMAX > 0) {
+      float xv[kDm];
+#pragma unroll
+      for (int f = 0; f < kDm; ++f) xv[f] = xr[f < d ? f : 0];
+#pragma unroll
+      for (int f = 0; f < kDm; ++f) xv[f] = f < d ? xv[f] : 0.f;
+      for (int j = 0; j < k; ++j) {
+        float dd = 0.f;
+#pragma unroll
+        for (int f = 0; f < kDm; ++f) {  // zero-padded on both sides: no masks, no branches
+          const float t = xv[f] - c[j * kDm + f];
+          dd = fmaf(t, t, dd);
+        }
+        if (dd < bd) {
+          bd = dd;
+          best = j;
+        }
       }
-      if (dd < bd) {
-        bd = dd;
-        best = j;
+      if (assign) assign[r] = best;
+      const bool train = yv == nullptr || !__builtin_isnan(yv[r]);
+      if (train && sums) {
+#pragma unroll
+        for (int f = 0; f < kDm; ++f)
+          if (f < d) atomicAdd(&s[best * d + f], xv[f]);
+        atomicAdd(&n[best], 1.f);
+        my_in += bd;
       }
-    }
-    if (assign) assign[r] = best;
-    const bool train = yv == nullptr || !__builtin_isnan(yv[r]);
-    if (train && sums) {
-      for (int f = 0; f < d; ++f) atomicAdd(&s[best * d + f], xr[f]);
-      atomicAdd(&n[best], 1.f);
-      my_in += bd;
+    } else {
+      for (int j = 0; j < k; ++j) {
+        float dd = 0.f;
+        for (int f = 0; f < d; ++f) {
+          const float t = xr[f] - c[j * d + f];
+          dd = fmaf(t, t, dd);
+        }
+        if (dd < bd) {
+          bd = dd;
+          best = j;
+        }
+      }
+      if (assign) assign[r] = best;
+      const bool train = yv == nullptr || !__builtin_isnan(yv[r]);
+      if (train && sums) {
+        for (int f = 0; f < d; ++f) atomicAdd(&s[best * d + f], xr[f]);
+        atomicAdd(&n[best], 1.f);
+        my_in += bd;
+      }
     }
   }
   __syncthreads();
-  if (sums) {
-    for (int i = threadIdx.x; i < k * d; i += 256)
-      if (s[i] != 0.f) atomicAdd(&sums[i], s[i]);
-    for (int i = threadIdx.x; i < k; i += 256)
-      if (n[i] != 0.f) atomicAdd(&counts[i], n[i]);
-    const float w = wave_sum(my_in);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = w;
-    __syncthreads();
-    if (threadIdx.x == 0 && inertia) atomicAdd(inertia, (part[0] + part[1]) + (part[2] + part[3]));
-  }
+  if (sums) kmeans_flush(s, n, my_in, k, d, sums, counts, inertia, bpart, part);
 }
 
 // Nearest-centroid assignment on the matrix cores (k ≥ 32 centroids): distances as
@@ -313,20 +389,39 @@ template <int DMAX>
 __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
     const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int k,
     const float* __restrict__ cent, float* __restrict__ sums, float* __restrict__ counts,
-    int* __restrict__ assign, float* __restrict__ inertia) {
+    int* __restrict__ assign, float* __restrict__ inertia, float* __restrict__ bpart,
+    int ablate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int kp = (k + 31) & ~31;
-  const int dp = (d + 1) & ~1;
-  const int ldc = dp | 1;
+  constexpr int ldc = DMAX | 1;  // ≥ DMAX + 1: every operand read stays inside its row
   float* cs = reinterpret_cast<float*>(smem);  // [kp][ldc]
   float* cn = cs + (size_t)kp * ldc;           // [kp]  ‖c‖² (+inf for padding)
   float* s = cn + kp;                          // [k][d] cluster sums of this block
   float* n = s + (size_t)k * d;                // [k]
   __shared__ float part[4];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // padding (columns d..ldc-1 of every row, rows k..kp-1) is zero; the centroids are read
+  // as one contiguous k·d run, 8 loads per thread in flight at a time (clamped, then masked)
   for (int i = tid; i < kp * ldc; i += 256) {
     const int r = i / ldc, c = i - r * ldc;
-    cs[i] = (r < k && c < d) ? cent[(size_t)r * d + c] : 0.f;
+    if (r >= k || c >= d) cs[i] = 0.f;
+  }
+  const int kd = k * d;
+  for (int base = 0; base < kd; base += 256 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * 256 + tid;
+      v[u] = cent[i < kd ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * 256 + tid;
+      if (i < kd) {
+        const int r = i / d;
+        cs[r * ldc + (i - r * d)] = v[u];
+      }
+    }
   }
   for (int i = tid; i < k * d; i += 256) s[i] = 0.f;
   for (int i = tid; i < k; i += 256) n[i] = 0.f;
@@ -339,24 +434,33 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
   __syncthreads();
   const int j = lane & 31, h = lane >> 5;
   float my_in = 0.f;
-  for (long long t = (long long)blockIdx.x * 4 + wave; t * 32 < B; t += (long long)gridDim.x * 4) {
+  // software pipeline: the next tile's row features and label are in flight while the
+  // current tile computes (unconditional loads from clamped rows, masked afterwards)
+  float nx[DMAX / 2], ny = 0.f;
+  auto fetch = [&](long long t) {
+    const long long row = t * 32 + j;
+    const long long rr = row < B ? row : B - 1;
+    const float* xr = x + rr * (long long)d;
+#pragma unroll
+    for (int u = 0; u < DMAX / 2; ++u) nx[u] = xr[2 * u + h < d ? 2 * u + h : 0];
+    ny = yv ? yv[rr] : 0.f;
+  };
+  constexpr bool kPf = DMAX <= 48;  // wider rows: no room for a second row copy
+  const long long tstride = (long long)gridDim.x * 4;
+  long long t = (long long)blockIdx.x * 4 + wave;
+  if (kPf && t * 32 < B) fetch(t);
+  for (; t * 32 < B; t += tstride) {
     const long long row = t * 32 + j;
     const bool vrow = row < B;
-    const float* xr = x + (vrow ? row : B - 1) * (long long)d;
+    if (!kPf) fetch(t);
     float xv[DMAX / 2];  // features h, h+2, h+4, ... of this lane's row (the B operand)
 #pragma unroll
-    for (int u = 0; u < DMAX / 2; ++u) {
-      const int f = 2 * u + h;
-      xv[u] = f < d ? xr[f < d ? f : 0] : 0.f;
-    }
+    for (int u = 0; u < DMAX / 2; ++u) xv[u] = 2 * u + h < d ? nx[u] : 0.f;
+    const float ycur = ny;
+    if (kPf && (t + tstride) * 32 < B) fetch(t + tstride);
     float best = INFINITY;
     int bi = 0;
-    for (int ct = 0; ct < kp; ct += 32) {
-      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const float* ca = cs + (size_t)(ct + j) * ldc + h;
-#pragma unroll
-      for (int u = 0; u < DMAX / 2; ++u)
-        if (2 * u < dp) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[2 * u], xv[u], acc, 0, 0, 0);
+    auto argmin = [&](const f32x16& acc, int ct) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i = ct + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -366,6 +470,29 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
           bi = i;
         }
       }
+    };
+    // two centroid tiles per step: two independent MFMA chains in flight
+    for (int ct = 0; ct < kp; ct += 64) {
+      const bool two = ct + 32 < kp;
+      f32x16 a0 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      f32x16 a1 = a0;
+      const float* c0 = cs + (size_t)(ct + j) * ldc + h;
+      const float* c1 = two ? c0 + 32 * (size_t)ldc : c0;
+      // all DMAX/2 steps, no branches (a branch per step would wait for each operand
+      // read): columns d..ldc-1 are zero in both operands
+      float o0[DMAX / 2], o1[DMAX / 2];
+#pragma unroll
+      for (int u = 0; u < DMAX / 2; ++u) {
+        o0[u] = c0[2 * u];
+        o1[u] = c1[2 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < DMAX / 2; ++u) {
+        a0 = __builtin_amdgcn_mfma_f32_32x32x2f32(o0[u], xv[u], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x2f32(o1[u], xv[u], a1, 0, 0, 0);
+      }
+      argmin(a0, ct);
+      if (two) argmin(a1, ct + 32);
     }
     // the other half-wave holds the same row's other 16 centroids of every tile
     const float ob = __shfl_xor(best, 32);
@@ -374,32 +501,27 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
       best = ob;
       bi = oi;
     }
-    if (h == 0 && vrow) {
-      if (assign) assign[row] = bi;
-      const bool train = yv == nullptr || !__builtin_isnan(yv[row]);
-      if (train && sums) {
-        float xx = 0.f;
-        for (int f = 0; f < d; ++f) {
-          const float v = xr[f];
-          xx = fmaf(v, v, xx);
-          atomicAdd(&s[bi * d + f], v);
+    // the sums come from the registers: each half adds its own features of the row
+    float xx = 0.f;
+#pragma unroll
+    for (int u = 0; u < DMAX / 2; ++u) xx = fmaf(xv[u], xv[u], xx);
+    xx += __shfl_xor(xx, 32);
+    if (vrow) {
+      if (assign && h == 0) assign[row] = bi;
+      const bool train = !__builtin_isnan(ycur);
+      if (train && sums && !(ablate & 2)) {
+#pragma unroll
+        for (int u = 0; u < DMAX / 2; ++u)
+          if (2 * u + h < d) atomicAdd(&s[bi * d + 2 * u + h], xv[u]);
+        if (h == 0) {
+          atomicAdd(&n[bi], 1.f);
+          my_in += fmaxf(0.f, xx + best);  // ‖x − c‖² ≥ 0 (rounding)
         }
-        atomicAdd(&n[bi], 1.f);
-        my_in += fmaxf(0.f, xx + best);  // ‖x − c‖² ≥ 0 (rounding)
       }
     }
   }
   __syncthreads();
-  if (sums) {
-    for (int i = tid; i < k * d; i += 256)
-      if (s[i] != 0.f) atomicAdd(&sums[i], s[i]);
-    for (int i = tid; i < k; i += 256)
-      if (n[i] != 0.f) atomicAdd(&counts[i], n[i]);
-    const float w = wave_sum(my_in);
-    if (lane == 0) part[wave] = w;
-    __syncthreads();
-    if (tid == 0 && inertia) atomicAdd(inertia, (part[0] + part[1]) + (part[2] + part[3]));
-  }
+  if (sums && !(ablate & 1)) kmeans_flush(s, n, my_in, k, d, sums, counts, inertia, bpart, part);
 }
 
 // Count-weighted centroid move of one micro-batch, fused with the bookkeeping the learner
@@ -510,44 +632,90 @@ OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, fl
 template <int DMAX>
 static int launch_kmeans_mfma(const float* x, const float* y, int B, int d, int k,
                               const float* cent, float* sums, float* counts, int* assign,
-                              float* inertia, size_t lds, hipStream_t st) {
+                              float* inertia, float* bpart, size_t lds, hipStream_t st,
+                              int* nblocks) {
   auto fn = kmeans_assign_mfma_kernel<DMAX>;
   int e = check_dyn_lds((const void*)fn, lds);
   if (e) return e;
   const long long tiles = ((long long)B + 31) / 32;
   int blocks = (int)((tiles + 3) / 4);
-  if (blocks > 512) blocks = 512;  // each block flushes k·d sums: keep the flush small
+  int cap = kKmeansMaxBlocks;
+  if (const char* e = getenv("OMLDM_KMEANS_BLOCKS")) cap = atoi(e) > 0 ? atoi(e) : cap;  // sweep
+  if (blocks > cap) blocks = cap;
+  if (blocks > kKmeansMaxBlocks) blocks = kKmeansMaxBlocks;  // the partials image's rows
+  *nblocks = blocks;
+  // timing diagnostics only: bit 0 skips the global flush, bit 1 the LDS cluster sums
+  const char* ab = getenv("OMLDM_KMEANS_ABLATE");
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), lds, st, x, y, B, d, k, cent, sums, counts,
-                     assign, inertia);
+                     assign, inertia, bpart, ab ? atoi(ab) : 0);
   return (int)hipGetLastError();
 }
 
+static int kmeans_colsum(const float* bpart, int nb, int k, int d, float* sums, float* counts,
+                         float* inertia, hipStream_t st) {
+  const int pw = k * d + k + 1;
+  hipLaunchKernelGGL(kmeans_colsum_kernel, dim3((pw + 255) / 256, (nb + 63) / 64), dim3(256), 0,
+                     st, bpart, nb, k, d, sums, counts, inertia);
+  return (int)hipGetLastError();
+}
+
+// bpart (optional, with sums): a [kKmeansMaxBlocks][k·d + k + 1] float scratch image for
+// the per-block partials (see kmeans_flush); nullptr: per-block atomics.
 OMLDM_API int omldm_kmeans_assign(const float* x, const float* y, int B, int d, int k,
                                   const float* cent, float* sums, float* counts, int* assign,
-                                  float* inertia, void* stream) {
+                                  float* inertia, float* bpart, void* stream) {
   if (B <= 0) return 0;
+  if (!sums) bpart = nullptr;
   // matrix-core distances once there is a full 32-centroid tile and a few features
   // (OMLDM_KMEANS_MFMA=0: the scalar kernel, A/B)
   const char* mf = getenv("OMLDM_KMEANS_MFMA");
   if (k >= 32 && d >= 4 && d <= 128 && !(mf && atoi(mf) == 0)) {
-    const int kp = (k + 31) & ~31, ldc = ((d + 1) & ~1) | 1;
+    // operand width: d rounded up to the next of 16, 24, 32, 48, 64, 96, 128 (the K loop
+    // runs DMAX/2 matrix-core steps unconditionally)
+    const int dm = d <= 16 ? 16 : d <= 24 ? 24 : d <= 32 ? 32 : d <= 48 ? 48 : d <= 64 ? 64
+                 : d <= 96 ? 96 : 128;
+    const int kp = (k + 31) & ~31, ldc = dm | 1;
     const size_t lds = ((size_t)kp * ldc + kp + (size_t)k * d + k) * 4;
     if (lds <= 150 * 1024) {
       hipStream_t st = (hipStream_t)stream;
-      if (d <= 32) return launch_kmeans_mfma<32>(x, y, B, d, k, cent, sums, counts, assign, inertia, lds, st);
-      if (d <= 64) return launch_kmeans_mfma<64>(x, y, B, d, k, cent, sums, counts, assign, inertia, lds, st);
-      return launch_kmeans_mfma<128>(x, y, B, d, k, cent, sums, counts, assign, inertia, lds, st);
+      int nb = 0, rc = -2;
+#define OMLDM_KMM(DM)                                                                           \
+  if (dm == DM)                                                                                 \
+  rc = launch_kmeans_mfma<DM>(x, y, B, d, k, cent, sums, counts, assign, inertia, bpart, lds, st, \
+                              &nb)
+      OMLDM_KMM(16);
+      OMLDM_KMM(24);
+      OMLDM_KMM(32);
+      OMLDM_KMM(48);
+      OMLDM_KMM(64);
+      OMLDM_KMM(96);
+      OMLDM_KMM(128);
+#undef OMLDM_KMM
+      if (rc || !bpart) return rc;
+      return kmeans_colsum(bpart, nb, k, d, sums, counts, inertia, st);
     }
   }
-  const size_t lds = (size_t)(2 * k * d + k) * 4;
+  const int dm = d <= 16 ? 16 : d <= 32 ? 32 : d <= 64 ? 64 : 0;
+  const size_t lds = (size_t)(k * (dm ? dm : d) + k * d + k) * 4;
   if (lds > 150 * 1024) return -1;
-  int e = check_dyn_lds((const void*)kmeans_assign_kernel, lds);
-  if (e) return e;
   int blocks = (B + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(kmeans_assign_kernel, dim3(blocks), dim3(256), lds, (hipStream_t)stream, x,
-                     y, B, d, k, cent, sums, counts, assign, inertia);
-  return (int)hipGetLastError();
+  if (blocks > kKmeansMaxBlocks) blocks = kKmeansMaxBlocks;
+  hipStream_t st = (hipStream_t)stream;
+#define OMLDM_KM(DM)                                                                        \
+  do {                                                                                      \
+    const int e_ = check_dyn_lds((const void*)kmeans_assign_kernel<DM>, lds);               \
+    if (e_) return e_;                                                                      \
+    hipLaunchKernelGGL(kmeans_assign_kernel<DM>, dim3(blocks), dim3(256), lds, st, x, y, B, d, \
+                       k, cent, sums, counts, assign, inertia, bpart);                      \
+  } while (0)
+  if (dm == 16) OMLDM_KM(16);
+  else if (dm == 32) OMLDM_KM(32);
+  else if (dm == 64) OMLDM_KM(64);
+  else OMLDM_KM(0);
+#undef OMLDM_KM
+  const int rc = (int)hipGetLastError();
+  if (rc || !bpart) return rc;
+  return kmeans_colsum(bpart, blocks, k, d, sums, counts, inertia, st);
 }
 
 // G += Σ zzᵀ with z = [x, x_a·x_b for (a, b) in pairs, 1, y] over rows with finite y: the

@@ -49,6 +49,9 @@ def gram_update(x: torch.Tensor, y: torch.Tensor, G: torch.Tensor,
     G[: d + 2, : d + 2] += (z.T @ z).float()
 
 
+KMEANS_MAX_BLOCKS = 512  # csrc/kernels/dense_learners.hip kKmeansMaxBlocks
+
+
 def kmeans_assign(x: torch.Tensor, y: torch.Tensor | None, cent: torch.Tensor,
                   sums: torch.Tensor | None, counts: torch.Tensor | None,
                   inertia: torch.Tensor | None = None, want_assign: bool = False):
@@ -61,8 +64,13 @@ def kmeans_assign(x: torch.Tensor, y: torch.Tensor | None, cent: torch.Tensor,
         return assign
     x = x.float().contiguous()
     if x.is_cuda:
+        from omldm_amd.ops.linear import _workspace
+
+        # per-block partials, summed per column by a second launch (csrc: kmeans_flush)
+        part = _workspace(x.device, KMEANS_MAX_BLOCKS * (k * d + k + 1), key="km_part") \
+            if sums is not None else None
         check(native.hip().omldm_kmeans_assign(ptr(x), ptr(y), B, d, k, ptr(cent), ptr(sums),
-                                               ptr(counts), ptr(assign), ptr(inertia),
+                                               ptr(counts), ptr(assign), ptr(inertia), ptr(part),
                                                native.stream_of(x)), "omldm_kmeans_assign")
         return assign
     dist = torch.cdist(x, cent.float()) ** 2

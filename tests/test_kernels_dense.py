@@ -136,14 +136,16 @@ def test_hip_fitted_count_keeps_counting_past_2_31(cuda, name, task, hyper):
 
 
 @pytest.mark.gpu
-def test_hip_kmeans_assign(cuda):
+@pytest.mark.parametrize("d,k", [(13, 5), (30, 7), (40, 16), (130, 3)])
+def test_hip_kmeans_assign(cuda, d, k):
+    """Scalar kernel (k < 32): row in registers for d ≤ 64, re-read per centroid beyond."""
     torch.manual_seed(3)
-    x = torch.randn(3000, 13)
-    cent = torch.randn(5, 13)
+    x = torch.randn(3000, d)
+    cent = torch.randn(k, d)
     y = torch.zeros(3000)
-    s, n, inert = torch.zeros(5, 13), torch.zeros(5), torch.zeros(1)
+    s, n, inert = torch.zeros(k, d), torch.zeros(k), torch.zeros(1)
     a_ref = D.kmeans_assign(x, y, cent, s, n, inert, want_assign=True)
-    sg, ng, ig = torch.zeros(5, 13, device=cuda), torch.zeros(5, device=cuda), \
+    sg, ng, ig = torch.zeros(k, d, device=cuda), torch.zeros(k, device=cuda), \
         torch.zeros(1, device=cuda)
     a = D.kmeans_assign(x.to(cuda), y.to(cuda), cent.to(cuda), sg, ng, ig, want_assign=True)
     assert torch.equal(a.cpu().long(), a_ref.long())
