@@ -382,8 +382,10 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
 // v_mfma_f32_32x32x2_f32 (exact fp32 products). A wave takes 32-row tiles; A = a 32-centroid
 // tile staged in LDS (odd row stride: the 32 lanes of an operand column on distinct banks),
 // B = the tile's rows, each lane keeping its row's features in registers across all
-// centroid tiles. Lane (j, h) ends a tile holding c_i·x_j for 16 centroids i of its half,
-// so the argmin is an in-lane minimum plus one exchange with lane j ^ 32. Training rows then
+// centroid tiles. The operands are augmented so the product IS the distance: A row i =
+// [c_i, ‖c_i‖²], B column j = [−2·x_j, 1] (−2 is exact), padded centroid rows carry +inf.
+// Lane (j, h) ends a tile holding ‖c_i‖² − 2c_i·x_j for 16 centroids i of its half, so the
+// argmin is an in-lane minimum plus one exchange with lane j ^ 32. Training rows then
 // add x into the block's LDS cluster sums as the scalar kernel does.
 template <int DMAX>
 __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
@@ -394,9 +396,8 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int kp = (k + 31) & ~31;
   constexpr int ldc = DMAX | 1;  // ≥ DMAX + 1: every operand read stays inside its row
-  float* cs = reinterpret_cast<float*>(smem);  // [kp][ldc]
-  float* cn = cs + (size_t)kp * ldc;           // [kp]  ‖c‖² (+inf for padding)
-  float* s = cn + kp;                          // [k][d] cluster sums of this block
+  float* cs = reinterpret_cast<float*>(smem);  // [kp][ldc]: c, ‖c‖² (+inf: padding), 0…
+  float* s = cs + (size_t)kp * ldc;            // [k][d] cluster sums of this block
   float* n = s + (size_t)k * d;                // [k]
   __shared__ float part[4];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
   for (int r = tid; r < kp; r += 256) {
     float a = 0.f;
     for (int c = 0; c < d; ++c) a = fmaf(cs[r * ldc + c], cs[r * ldc + c], a);
-    cn[r] = r < k ? a : INFINITY;
+    cs[r * ldc + d] = r < k ? a : INFINITY;
   }
   __syncthreads();
   const int j = lane & 31, h = lane >> 5;
@@ -453,9 +454,13 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
     const long long row = t * 32 + j;
     const bool vrow = row < B;
     if (!kPf) fetch(t);
-    float xv[DMAX / 2];  // features h, h+2, h+4, ... of this lane's row (the B operand)
+    // B operand: −2·x_f for f = h, h+2, … < d, then 1 at f = d (times ‖c‖²), then 0
+    float xv[DMAX / 2];
 #pragma unroll
-    for (int u = 0; u < DMAX / 2; ++u) xv[u] = 2 * u + h < d ? nx[u] : 0.f;
+    for (int u = 0; u < DMAX / 2; ++u) {
+      const int f = 2 * u + h;
+      xv[u] = f < d ? -2.f * nx[u] : (f == d ? 1.f : 0.f);
+    }
     const float ycur = ny;
     if (kPf && (t + tstride) * 32 < B) fetch(t + tstride);
     float best = INFINITY;
@@ -463,11 +468,9 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
     auto argmin = [&](const f32x16& acc, int ct) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int i = ct + (q & 3) + 8 * (q >> 2) + 4 * h;
-        const float dist = cn[i] - 2.f * acc[q];
-        if (dist < best) {
-          best = dist;
-          bi = i;
+        if (acc[q] < best) {
+          best = acc[q];
+          bi = ct + (q & 3) + 8 * (q >> 2) + 4 * h;
         }
       }
     };
@@ -479,7 +482,7 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
       const float* c0 = cs + (size_t)(ct + j) * ldc + h;
       const float* c1 = two ? c0 + 32 * (size_t)ldc : c0;
       // all DMAX/2 steps, no branches (a branch per step would wait for each operand
-      // read): columns d..ldc-1 are zero in both operands
+      // read): columns d+1..ldc-1 are zero in both operands
       float o0[DMAX / 2], o1[DMAX / 2];
 #pragma unroll
       for (int u = 0; u < DMAX / 2; ++u) {
@@ -502,6 +505,9 @@ __global__ __launch_bounds__(256) void kmeans_assign_mfma_kernel(
       bi = oi;
     }
     // the sums come from the registers: each half adds its own features of the row
+    // (x = −½·xv exactly)
+#pragma unroll
+    for (int u = 0; u < DMAX / 2; ++u) xv[u] = 2 * u + h < d ? -0.5f * xv[u] : 0.f;
     float xx = 0.f;
 #pragma unroll
     for (int u = 0; u < DMAX / 2; ++u) xx = fmaf(xv[u], xv[u], xx);
@@ -669,13 +675,14 @@ OMLDM_API int omldm_kmeans_assign(const float* x, const float* y, int B, int d, 
   // matrix-core distances once there is a full 32-centroid tile and a few features
   // (OMLDM_KMEANS_MFMA=0: the scalar kernel, A/B)
   const char* mf = getenv("OMLDM_KMEANS_MFMA");
-  if (k >= 32 && d >= 4 && d <= 128 && !(mf && atoi(mf) == 0)) {
-    // operand width: d rounded up to the next of 16, 24, 32, 48, 64, 96, 128 (the K loop
-    // runs DMAX/2 matrix-core steps unconditionally)
-    const int dm = d <= 16 ? 16 : d <= 24 ? 24 : d <= 32 ? 32 : d <= 48 ? 48 : d <= 64 ? 64
-                 : d <= 96 ? 96 : 128;
+  if (k >= 32 && d >= 4 && d < 128 && !(mf && atoi(mf) == 0)) {
+    // operand width: d + 1 (the ‖c‖² column) rounded up to the next of 16, 24, 32, 48, 64,
+    // 96, 128 (the K loop runs DMAX/2 matrix-core steps unconditionally)
+    const int da = d + 1;
+    const int dm = da <= 16 ? 16 : da <= 24 ? 24 : da <= 32 ? 32 : da <= 48 ? 48 : da <= 64 ? 64
+                 : da <= 96 ? 96 : 128;
     const int kp = (k + 31) & ~31, ldc = dm | 1;
-    const size_t lds = ((size_t)kp * ldc + kp + (size_t)k * d + k) * 4;
+    const size_t lds = ((size_t)kp * ldc + (size_t)k * d + k) * 4;
     if (lds <= 150 * 1024) {
       hipStream_t st = (hipStream_t)stream;
       int nb = 0, rc = -2;
