@@ -374,8 +374,11 @@ __device__ unsigned long long* g_rd_stamps;
 // bucket; a bucket that is full sends its extra keys to the accumulator with an L2
 // atomic — exact, nothing is dropped) and leave with the same coalesced group-major flush,
 // so linear_reduce_kernel is unchanged.
+#ifndef OMLDM_RD_OCC
+#define OMLDM_RD_OCC 5  // waves per SIMD the register budget is sized for (diagnostics sweep)
+#endif
 template <int RMAX, int RULE, typename NumT, typename WT>
-__global__ __launch_bounds__(64, 5) void linear_round_rd_kernel(
+__global__ __launch_bounds__(64, OMLDM_RD_OCC) void linear_round_rd_kernel(
     const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
     int dc, const void* __restrict__ yv, int B, int R, int dim, float* __restrict__ ws,
     int2* __restrict__ tables, float* __restrict__ dacc, LinParams p, TableGeom g, int ablate) {
