@@ -89,22 +89,41 @@ __global__ __launch_bounds__(64) void gram_mfma_kernel(const float* __restrict__
 // covers two 128-B row segments); a second tiny launch mirrors the upper triangle into
 // the lower one. Exact fp32 products (v_mfma_f32_32x32x2_f32), like the v1 kernel (a pair
 // feature is rounded once, as the separate expansion rounds it).
-template <int NB, int EPT>
+// Element e of a tile-sum image (tile t, register r, lane l) → its (row, col) of G, added
+// with an L2 atomic; entry (d, d) = Σ 1·1 is also the fitted-row count (fp64 total).
+template <int NB>
+__device__ __forceinline__ void gram_add_element(int e, float v, float* __restrict__ G, int ld,
+                                                 int d, double* __restrict__ cnt) {
+  const int t = e >> 10, r = (e >> 6) & 15, l = e & 63;
+  int I = 0, k = t;
+  while (k >= NB - I) {  // t-th upper-triangle tile in row-major order
+    k -= NB - I;
+    ++I;
+  }
+  const int J = I + k;
+  const int row = I * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+  const int cl = J * 32 + (l & 31);
+  if (v != 0.f && row < ld && cl < ld) {
+    atomicAdd(&G[(size_t)row * ld + cl], v);
+    if (cnt && row == d && cl == d) atomicAdd(cnt, (double)v);
+  }
+}
+
+template <int NB, int EPT, int RC>
 __global__ __launch_bounds__(256) void gram_map_kernel(const float* __restrict__ x,
                                                        const float* __restrict__ y, int B, int d0,
                                                        const int* __restrict__ pairs, int npairs,
                                                        int rows_per_block, float* __restrict__ G,
-                                                       int ld, double* __restrict__ cnt) {
-  constexpr int T = NB * (NB + 1) / 2;
-  constexpr int RC = 64;  // rows per staged chunk
-  constexpr int MAXW = NB * 32 + 1;
+                                                       int ld, double* __restrict__ cnt,
+                                                       float* __restrict__ part) {
+  constexpr int T = NB * (NB + 1) / 2;  // RC: rows per staged chunk
   const int d = d0 + npairs;     // z = [mapped features (d), 1, y]
   const int W = d0 + 3;          // staged row: x (d0), valid, y·valid, 0
   const int LDW = W | 1;         // odd row stride: the half-waves' rows on different banks
   const int ONE = d0, YC = d0 + 1, ZERO = d0 + 2;
-  constexpr int ZF = 2 * RC * MAXW;
   constexpr int RF = T * 1024;  // floats of the tile-sum image
-  __shared__ float lds[ZF > RF ? ZF : RF];
+  // dynamic: max(2 staging buffers of RC × LDW, the tile-sum image) floats
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   float* xs = lds;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const long long r_begin = (long long)blockIdx.x * rows_per_block;
@@ -187,12 +206,26 @@ __global__ __launch_bounds__(256) void gram_map_kernel(const float* __restrict__
     const bool more = rc + RC < r_end;
     if (more) load(rc + RC);  // in flight while this chunk computes
     const float* xb = xs + (size_t)buf * RC * LDW;
+    // software pipeline over the wave's row pairs: the LDS reads of pair p+1 are issued
+    // before the MFMAs of pair p and consumed after them (instructions issue in order, so
+    // reads placed after the MFMAs would leave the matrix core idle for their latency)
+    float ra[NB], rb[NB], r1;
+    auto issue = [&](int kp) {
+      const float* xrow = xb + (size_t)(2 * kp + half) * LDW;
+#pragma unroll
+      for (int I = 0; I < NB; ++I) {
+        ra[I] = xrow[fa[I]];
+        rb[I] = xrow[fb[I]];
+      }
+      r1 = xrow[ONE];
+    };
+    issue(wave);
 #pragma unroll
     for (int kp = wave; kp < RC / 2; kp += 4) {
-      const float* xrow = xb + (size_t)(2 * kp + half) * LDW;
       float a[NB];
 #pragma unroll
-      for (int I = 0; I < NB; ++I) a[I] = (xrow[fa[I]] * xrow[fb[I]]) * xrow[ONE];
+      for (int I = 0; I < NB; ++I) a[I] = (ra[I] * rb[I]) * r1;
+      if (kp + 4 < RC / 2) issue(kp + 4);
       int t = 0;
 #pragma unroll
       for (int I = 0; I < NB; ++I)
@@ -218,24 +251,31 @@ __global__ __launch_bounds__(256) void gram_map_kernel(const float* __restrict__
     }
     __syncthreads();
   }
-  // element e of the image: tile t, register r, lane l → (row, col) of that tile
-  for (int e = tid; e < RF; e += 256) {
-    const int t = e >> 10, r = (e >> 6) & 15, l = e & 63;
-    int I = 0, J = 0, k = t;
-    while (k >= NB - I) {  // t-th upper-triangle tile in row-major order
-      k -= NB - I;
-      ++I;
-    }
-    J = I + k;
-    const int row = I * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
-    const int cl = J * 32 + (l & 31);
-    const float v = red[e];
-    if (v != 0.f && row < ld && cl < ld) {
-      atomicAdd(&G[(size_t)row * ld + cl], v);
-      // entry (d, d) = Σ 1·1 over the block's valid rows (exact: < 2^24 per block)
-      if (cnt && row == d && cl == d) atomicAdd(cnt, (double)v);
-    }
+#ifdef OMLDM_GRAM_PROBE_NOFLUSH
+  if (G) return;  // timing diagnostics only (csrc/tests/gram_probe.hip)
+#endif
+  if (part) {  // the block's image to its row of the partials (gram_colsum_kernel adds them)
+    for (int e = tid; e < RF; e += 256) part[(size_t)blockIdx.x * RF + e] = red[e];
+    return;
   }
+  for (int e = tid; e < RF; e += 256) gram_add_element<NB>(e, red[e], G, ld, d, cnt);
+}
+
+// Sum of the blocks' tile images [nb][T·1024] per element into G: thread = element,
+// blockIdx.y = a slab of 32 block rows (one atomic per element per slab instead of one
+// per block: ≈ 2.6 M same-address atomics from 256 blocks serialised at the memory side).
+template <int NB>
+__global__ __launch_bounds__(256) void gram_colsum_kernel(const float* __restrict__ part, int nb,
+                                                          float* __restrict__ G, int ld, int d,
+                                                          double* __restrict__ cnt) {
+  constexpr int RF = NB * (NB + 1) / 2 * 1024;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= RF) return;
+  const int b0 = blockIdx.y * 32, b1 = min(nb, b0 + 32);
+  float a = 0.f;
+#pragma unroll 16
+  for (int b = b0; b < b1; ++b) a += part[(size_t)b * RF + e];
+  gram_add_element<NB>(e, a, G, ld, d, cnt);
 }
 
 // G[i][j] = G[j][i] for j < i < n (gram_map_kernel accumulates the upper triangle).
@@ -577,15 +617,25 @@ OMLDM_API int omldm_kmeans_apply(float* cent, float* n, int k, int d, float* sum
   return (int)hipGetLastError();
 }
 
-template <int NB, int EPT>
+template <int NB, int EPT, int RC>
 static int launch_gram_map(const float* x, const float* y, int B, int d0, const int* pairs,
-                           int npairs, float* G, int ld, double* cnt, hipStream_t st) {
+                           int npairs, float* G, int ld, double* cnt, float* part,
+                           hipStream_t st) {
   // ≤ one block per CU, each ≥ one chunk: every block's image costs T·4 KiB of atomics
   long long rpb = ((long long)B + 255) / 256;
-  rpb = ((rpb + 63) / 64) * 64;
+  rpb = ((rpb + RC - 1) / RC) * RC;
   const int blocks = (int)(((long long)B + rpb - 1) / rpb);
-  hipLaunchKernelGGL((gram_map_kernel<NB, EPT>), dim3(blocks), dim3(256), 0, st, x, y, B, d0, pairs,
-                     npairs, (int)rpb, G, ld, cnt);
+  const int ldw = (d0 + 3) | 1;
+  const int T = NB * (NB + 1) / 2;
+  const size_t lds = (size_t)(2 * RC * ldw > T * 1024 ? 2 * RC * ldw : T * 1024) * 4;
+  auto fn = gram_map_kernel<NB, EPT, RC>;
+  const int e = check_dyn_lds((const void*)fn, lds);
+  if (e) return e;
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), lds, st, x, y, B, d0, pairs, npairs, (int)rpb, G,
+                     ld, cnt, part);
+  if (part)
+    hipLaunchKernelGGL(gram_colsum_kernel<NB>, dim3(T * 4, (blocks + 31) / 32), dim3(256), 0, st,
+                       part, blocks, G, ld, d0 + npairs, cnt);
   const int n = NB * 32 < ld ? NB * 32 : ld;
   hipLaunchKernelGGL(gram_mirror_kernel, dim3((n * n + 255) / 256), dim3(256), 0, st, G, ld, n);
   return (int)hipGetLastError();
@@ -593,27 +643,31 @@ static int launch_gram_map(const float* x, const float* y, int B, int d0, const 
 
 template <int NB>
 static int gram_map_e(const float* x, const float* y, int B, int d0, const int* pairs, int npairs,
-                      float* G, int ld, double* cnt, hipStream_t st) {
-  // element slots per thread: 64 staged rows × d0 raw values over 256 threads
-  if (d0 <= 16) return launch_gram_map<NB, 4>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
-  if (d0 <= 32) return launch_gram_map<NB, 8>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
-  if (d0 <= 64) return launch_gram_map<NB, 16>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
-  return launch_gram_map<NB, 32>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+                      float* G, int ld, double* cnt, float* part, hipStream_t st) {
+  // element slots per thread: RC staged rows × d0 raw values over 256 threads (EPT ≥
+  // RC·d0/256); 128-row chunks halve the per-chunk barriers where the registers allow
+  if (d0 <= 8) return launch_gram_map<NB, 4, 128>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
+  if (d0 <= 16) return launch_gram_map<NB, 8, 128>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
+  if (d0 <= 32) return launch_gram_map<NB, 16, 128>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
+  if (d0 <= 64) return launch_gram_map<NB, 16, 64>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
+  return launch_gram_map<NB, 32, 64>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
 }
 
 static int gram_map(const float* x, const float* y, int B, int d0, const int* pairs, int npairs,
-                    float* G, int ld, double* cnt, hipStream_t st) {
+                    float* G, int ld, double* cnt, float* part, hipStream_t st) {
   const int dz = d0 + npairs + 2;
-  if (dz <= 32) return gram_map_e<1>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
-  if (dz <= 64) return gram_map_e<2>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
-  if (dz <= 96) return gram_map_e<3>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
-  return gram_map_e<4>(x, y, B, d0, pairs, npairs, G, ld, cnt, st);
+  if (dz <= 32) return gram_map_e<1>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
+  if (dz <= 64) return gram_map_e<2>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
+  if (dz <= 96) return gram_map_e<3>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
+  return gram_map_e<4>(x, y, B, d0, pairs, npairs, G, ld, cnt, part, st);
 }
 
 // G[ld×ld] += [X 1 y]ᵀ[X 1 y] over rows with finite y (ld ≥ d + 2).
 // cnt (may be null): += number of rows with finite y.
+// part (optional): a [256][10240]-float scratch image for the per-block tile sums (v2
+// kernel); nullptr: the blocks add into G with atomics.
 OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, float* G, int ld,
-                                double* cnt, void* stream) {
+                                double* cnt, float* part, void* stream) {
   if (B <= 0) return 0;
   const int dz = d + 2;
   if (ld < dz) return -1;
@@ -621,7 +675,7 @@ OMLDM_API int omldm_gram_update(const float* x, const float* y, int B, int d, fl
     const char* e = getenv("OMLDM_GRAM_V1");  // A/B: the one-tile-per-wave v1 kernel
     return e ? atoi(e) : 0;
   }();
-  if (!v1 && dz <= 128) return gram_map(x, y, B, d, nullptr, 0, G, ld, cnt, (hipStream_t)stream);
+  if (!v1 && dz <= 128) return gram_map(x, y, B, d, nullptr, 0, G, ld, cnt, part, (hipStream_t)stream);
   const int t = (dz + 31) / 32;
   int ksplit = (2048 + t * t - 1) / (t * t);  // ≥ ~2048 waves in flight
   const long long maxsplit = (B + 63) / 64;
@@ -730,10 +784,10 @@ OMLDM_API int omldm_kmeans_assign(const float* x, const float* y, int B, int d, 
 // [npairs][2]; d0 + npairs + 2 ≤ 128, else -2: expand and call omldm_gram_update).
 OMLDM_API int omldm_gram_update_poly2(const float* x, const float* y, int B, int d0,
                                       const int* pairs, int npairs, float* G, int ld, double* cnt,
-                                      void* stream) {
+                                      float* part, void* stream) {
   if (B <= 0) return 0;
   const int dz = d0 + npairs + 2;
   if (ld < dz) return -1;
   if (dz > 128) return -2;
-  return gram_map(x, y, B, d0, pairs, npairs, G, ld, cnt, (hipStream_t)stream);
+  return gram_map(x, y, B, d0, pairs, npairs, G, ld, cnt, part, (hipStream_t)stream);
 }

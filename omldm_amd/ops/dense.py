@@ -12,6 +12,14 @@ from omldm_amd.ops import native
 from omldm_amd.ops.native import check, ptr
 
 
+def _gram_part(device) -> torch.Tensor:
+    """Scratch of the Gram kernel's per-block tile sums: ≤ 256 blocks × 10 tiles × 1024
+    (csrc/kernels/dense_learners.hip gram_colsum_kernel adds them into G)."""
+    from omldm_amd.ops.linear import _workspace
+
+    return _workspace(device, 256 * 10 * 1024, key="gram_part")
+
+
 def gram_update(x: torch.Tensor, y: torch.Tensor, G: torch.Tensor,
                 cnt: torch.Tensor | None = None, pairs: torch.Tensor | None = None) -> None:
     """G[:d+2, :d+2] += Σ_rows z zᵀ with z = [x, 1, y] over rows whose y is finite;
@@ -32,7 +40,7 @@ def gram_update(x: torch.Tensor, y: torch.Tensor, G: torch.Tensor,
         if x.is_cuda and d0 + pairs.shape[0] + 2 <= 128:
             check(native.hip().omldm_gram_update_poly2(
                 ptr(x), ptr(y), B, d0, ptr(pairs), pairs.shape[0], ptr(G), G.shape[1], ptr(cnt),
-                native.stream_of(x)), "omldm_gram_update_poly2")
+                ptr(_gram_part(x.device)), native.stream_of(x)), "omldm_gram_update_poly2")
             return
         from omldm_amd.ops.preprocess import poly_expand
 
@@ -40,7 +48,8 @@ def gram_update(x: torch.Tensor, y: torch.Tensor, G: torch.Tensor,
     B, d = x.shape
     if x.is_cuda:
         check(native.hip().omldm_gram_update(ptr(x), ptr(y), B, d, ptr(G), G.shape[1], ptr(cnt),
-                                             native.stream_of(x)), "omldm_gram_update")
+                                             ptr(_gram_part(x.device)), native.stream_of(x)),
+              "omldm_gram_update")
         return
     ok = ~torch.isnan(y)
     if cnt is not None:

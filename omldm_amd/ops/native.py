@@ -56,8 +56,8 @@ HIP_SIGS = [
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
     ("omldm_pull_copy", i32, [vp, vp, i64, i32, vp]),
     ("omldm_h2d_async", i32, [vp, vp, i64, vp]),
-    ("omldm_gram_update", i32, [vp, vp, i32, i32, vp, i32, vp, vp]),
-    ("omldm_gram_update_poly2", i32, [vp, vp, i32, i32, vp, i32, vp, i32, vp, vp]),
+    ("omldm_gram_update", i32, [vp, vp, i32, i32, vp, i32, vp, vp, vp]),
+    ("omldm_gram_update_poly2", i32, [vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp]),
     ("omldm_kmeans_assign", i32, [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
     ("omldm_kmeans_apply", i32, [vp, vp, i32, i32, vp, vp, vp, vp, vp]),
     ("omldm_multiclass_round", i32, [vp, i32, vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32,
