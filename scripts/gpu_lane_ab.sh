@@ -1,12 +1,12 @@
 #!/bin/bash
-# Ingest lanes under the copy: kernel times of the training chain with training on every
-# CU but the copy's 16 ("split") vs off the copy's whole 32-CU block ("xcd").
+# Ingest lanes under the copy: kernel times of the training chain with the copy on a
+# 16-CU block and training on the other CUs ("split") vs plain streams ("plain").
 set -u
 R=${GRAFT_REPO_ROOT:-$PWD}
 mkdir -p $R/gpurun_out
 cd $R
 export TMPDIR=/tmp
-for ln in split xcd; do
+for ln in split plain; do
   rm -rf gpurun_out/lane_$ln
   timeout -k 10 150 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/lane_$ln -o run -- python3 bench.py --lane $ln --steps 200 --warmup 20 --latency-samples 10 > gpurun_out/lane_$ln.json 2> gpurun_out/lane_$ln.err || { tail -5 gpurun_out/lane_$ln.err; exit 3; }
   python3 - $ln <<'PY'
