@@ -557,7 +557,7 @@ template <int NT>
 __global__ __launch_bounds__(NT) void linear_reduce_kernel(
     const int2* __restrict__ tables, int S_act, TableGeom g, int dim, float* __restrict__ dacc,
     int nb, int split, int q0, const float* __restrict__ ws, int S, int dn,
-    double* __restrict__ cum) {
+    double* __restrict__ cum, int hot) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if ((int)blockIdx.x >= nb) {
     finish_column<NT>(blockIdx.x - nb, ws, S, dn, dim, dacc, cum);
@@ -586,9 +586,33 @@ __global__ __launch_bounds__(NT) void linear_reduce_kernel(
   auto add = [&](int key, int val) {
     if (key >= 0) atomicAdd(&acc[key - lo], __int_as_float(val));
   };
+  // Hot keys: a popular category sits in nearly every spoke's table, so the lanes of a
+  // wave (consecutive spokes' segments of one bucket) often carry the same key, and the
+  // LDS atomic serialises them. The wave takes its first valid lane's key; when at least
+  // `hot` lanes share it, their values are summed across the wave (DPP) and added once.
+  // Needs every lane of the wave active (the main loop below runs a wave-uniform count).
+  const int lane = threadIdx.x & 63;
+  auto add_wave = [&](int key, int val) {
+    const unsigned long long vm = __ballot(key >= 0);
+    if (vm == 0) return;
+    const int first = __builtin_ctzll(vm);
+    const int kc = __builtin_amdgcn_readlane(key, first);
+    const unsigned long long hm = __ballot(key == kc);
+    const float fv = __int_as_float(val);
+    if (__builtin_popcountll(hm) >= hot) {
+      const float sum = wave_sum(key == kc ? fv : 0.f);
+      if (lane == first) atomicAdd(&acc[kc - lo], sum);
+      if (key >= 0 && key != kc) atomicAdd(&acc[key - lo], fv);
+    } else if (key >= 0) {
+      atomicAdd(&acc[key - lo], fv);
+    }
+  };
   long long it = threadIdx.x;
-  // this thread's full batches: it + 4·NT·b + 3·NT < items (the old loop's condition)
-  const long long full = items - it - 3 * NT > 0 ? (items - it - 3 * NT - 1) / (4 * NT) + 1 : 0;
+  // full batches: it + 4·NT·b + 3·NT < items (the old loop's condition), evaluated for
+  // the wave's last lane (the smallest count in the wave), so the count is wave-uniform;
+  // the other lanes' remaining items go to the tail loop
+  const long long full_t = items - it - 3 * NT > 0 ? (items - it - 3 * NT - 1) / (4 * NT) + 1 : 0;
+  const long long full = (long long)__builtin_amdgcn_readlane((int)full_t, 63);
   int4 v[4];
   if (full > 0) {
 #pragma unroll
@@ -605,8 +629,8 @@ __global__ __launch_bounds__(NT) void linear_reduce_kernel(
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      add(cur[u].x, cur[u].y);
-      add(cur[u].z, cur[u].w);
+      add_wave(cur[u].x, cur[u].y);
+      add_wave(cur[u].z, cur[u].w);
     }
   }
   for (; it < items; it += NT) {
@@ -646,6 +670,16 @@ static inline int reduce_split(int ngroups, int S_act) {
   return sp;
 }
 
+// Lanes of a wave that must share a key before the reducer sums them across the wave
+// instead of one LDS atomic each (OMLDM_REDUCE_HOT: A/B; 65 = never).
+static inline int reduce_hot() {
+  static const int h = [] {
+    const char* e = getenv("OMLDM_REDUCE_HOT");
+    return e ? atoi(e) : 4;
+  }();
+  return h;
+}
+
 // Threads per reduce block (diagnostics sweep: OMLDM_REDUCE_THREADS = 256 | 512 | 1024).
 static inline int reduce_threads() {
   int nt = 256;
@@ -660,7 +694,7 @@ static int launch_reduce_t(dim3 grid, size_t lds, hipStream_t st, const int2* ta
   int e = check_dyn_lds((const void*)linear_reduce_kernel<NT>, lds);
   if (e) return e;
   hipLaunchKernelGGL(linear_reduce_kernel<NT>, grid, dim3(NT), lds, st, tables, S_act, g, dim, dacc,
-                     nb, split, q0, ws, S, dn, cum);
+                     nb, split, q0, ws, S, dn, cum, reduce_hot());
   return (int)hipGetLastError();
 }
 
