@@ -318,6 +318,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
         }
       }
       __syncthreads();  // W_l fully read before it is updated
+      MLP_STAMP(5);
       const int ntc = nin >> 5, nto = nout >> 5;
       for (int t = wave; t < nto * ntc; t += 4) {
         const int to = t / ntc, tc = t - to * ntc;
@@ -329,12 +330,14 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
           W[o * ldw + c] -= eta * acc[q];
         }
       }
+      MLP_STAMP(6);
       for (int o = tid; o < nout; o += blockDim.x) {
         float s = 0.f;
         for (int i = 0; i < kMB; ++i) s += Gc[i * g.ldg + o];
         sm[g.lb[l] + o] -= eta * s;
       }
       __syncthreads();
+      MLP_STAMP(7);
       const int tmp = gcur;
       gcur = gnext;
       gnext = tmp;

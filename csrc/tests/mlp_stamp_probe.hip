@@ -72,9 +72,10 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> st((size_t)S * 8);
   CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
   printf("S=%d R=%d bf16=%d: round (+colsum) best %.1f us\n", S, R, bf16, best * 1000.f);
-  const char* ph[] = {"", "stage+barrier", "forward", "loss", "backward"};
+  const char* ph[] = {"", "stage+barrier", "forward", "loss", "backward rest", "bwd dH+sync",
+                      "bwd W update", "bwd bias+sync"};
   const int mbs = (R + 31) / 32;
-  for (int k = 1; k <= 4; ++k) {
+  for (int k = 1; k <= 7; ++k) {
     std::vector<double> v;
     for (int s = 0; s < S; ++s) v.push_back((double)st[s * 8 + k] / mbs);
     std::sort(v.begin(), v.end());
