@@ -155,7 +155,8 @@ def test_hip_kmeans_assign(cuda, d, k):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,d,k", [(3000, 13, 32), (5001, 8, 50), (20000, 64, 256),
-                                   (4097, 100, 40), (777, 31, 97)])
+                                   (4097, 100, 40), (777, 31, 97), (2000, 20, 33),
+                                   (2000, 40, 64)])
 def test_hip_kmeans_assign_mfma(cuda, B, d, k):
     """k ≥ 32: matrix-core distances. The chosen centroid is a nearest one (fp64 distances,
     up to rounding ties), and sums / counts / inertia follow the kernel's own assignment."""
