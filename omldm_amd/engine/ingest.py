@@ -114,6 +114,12 @@ class TickIngest:
         return torch.empty(max(1, n), dtype=dtype, pin_memory=self.pinned)
 
     def _fill(self, blk: TickBlock) -> TickBlock:
+        from omldm_amd.utils import tracing
+
+        with tracing.range("ingest_read"):  # (reader thread) per-block cost, diagnostics
+            return self._fill_block(blk)
+
+    def _fill_block(self, blk: TickBlock) -> TickBlock:
         if blk.event is not None:
             blk.event.synchronize()  # the GPU has finished copying this slot's last use
             blk.event = None
@@ -165,7 +171,10 @@ class TickIngest:
 
     def _finish(self, blk: TickBlock) -> TickBlock:
         if self.stage and blk.n:
-            self._to_device(blk)
+            from omldm_amd.utils import tracing
+
+            with tracing.range("ingest_stage"):  # (staging thread) copy + parse + counts
+                self._to_device(blk)
         return blk
 
     def _to_device(self, blk: TickBlock) -> None:
@@ -209,7 +218,10 @@ class TickIngest:
             blk.staged = ev
             blk.event = ev  # the host slot may be rewritten once this copy is done
             if blk.parsed is not None:
-                ev.synchronize()  # (ingest thread) the tick gets host-side counts
+                from omldm_amd.utils import tracing
+
+                with tracing.range("ingest_stage_wait"):
+                    ev.synchronize()  # (ingest thread) the tick gets host-side counts
                 blk.counts = blk.out[5].numpy().copy()
 
     def _parse(self, blk: TickBlock, cs) -> None:
