@@ -43,23 +43,43 @@ struct MlpDesc {
 };
 
 // C[32×32] = A[32×K]·B[K×32] with A(i,k) = a[i·ars + k·acs], B(k,j) = b[k·brs + j·bcs].
-// Operand map (v_mfma_f32_32x32x2_f32): lane supplies A(lane&31, k + lane>>5) and
-// B(k + lane>>5, lane&31); result reg q of lane is C(row(q, lane), lane&31).
+// Result reg q of lane is C(row(q, lane), lane&31). K is a multiple of 16 (widths padded to
+// 32, mini-batches of 32 rows). An operand whose k index is contiguous in LDS (AK: acs ==
+// 1, BK: brs == 1 — forward: H rows and W rows; backward dH: G rows) is read as two 16-byte
+// ds_read_b128 per 8 k values: row strides are ≡ 4 floats mod 64 banks (make_desc), so the
+// 16-lane groups of a b128 read hit disjoint banks, and every row start and k offset is a
+// multiple of 4 floats. Strided operands are read one float per k.
+//
+// fp32 (v_mfma_f32_32x32x2_f32): for its 8 MFMAs of a 16-wide k step, lane half kh supplies
+// the 8 contiguous k = k0 + 8·kh + u (u = MFMA index) of its row / column in both operands
+// — a permutation of the k sum, so one half's values are one contiguous run.
+template <bool AK, bool BK>
 __device__ __forceinline__ f32x16 wave_gemm32_f32(const float* a, int ars, int acs,
                                                   const float* b, int brs, int bcs, int K) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, kh = lane >> 5;
   f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const float* ap = a + r * ars + kh * acs;
-  const float* bp = b + kh * brs + r * bcs;
-  // K is a multiple of 32 (padded widths / 32-row mini-batches): 8 operand pairs read
-  // ahead of their MFMAs, so the LDS latency is not paid once per instruction
+  const float* ap = a + r * ars + 8 * kh * (AK ? 1 : acs);
+  const float* bp = b + 8 * kh * (BK ? 1 : brs) + r * bcs;
   for (int k = 0; k < K; k += 16) {
     float av[8], bv[8];
+    if constexpr (AK) {
+      const float4 x0 = *reinterpret_cast<const float4*>(ap + k);
+      const float4 x1 = *reinterpret_cast<const float4*>(ap + k + 4);
+      av[0] = x0.x; av[1] = x0.y; av[2] = x0.z; av[3] = x0.w;
+      av[4] = x1.x; av[5] = x1.y; av[6] = x1.z; av[7] = x1.w;
+    } else {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      av[u] = ap[(k + 2 * u) * acs];
-      bv[u] = bp[(k + 2 * u) * brs];
+      for (int u = 0; u < 8; ++u) av[u] = ap[(k + u) * acs];
+    }
+    if constexpr (BK) {
+      const float4 y0 = *reinterpret_cast<const float4*>(bp + k);
+      const float4 y1 = *reinterpret_cast<const float4*>(bp + k + 4);
+      bv[0] = y0.x; bv[1] = y0.y; bv[2] = y0.z; bv[3] = y0.w;
+      bv[4] = y1.x; bv[5] = y1.y; bv[6] = y1.z; bv[7] = y1.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) bv[u] = bp[(k + u) * brs];
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
@@ -70,36 +90,52 @@ __device__ __forceinline__ f32x16 wave_gemm32_f32(const float* a, int ars, int a
 // Mixed precision: the same product with operands rounded to bf16 (RNE) as they leave
 // LDS and fp32 accumulation, on v_mfma_f32_32x32x16_bf16 — K/16 instructions instead
 // of K/2. Operand map: lane l (r = l&31, h = l>>5) supplies A(r, k + 8h + j) and
-// B(k + 8h + j, r), j = 0..7; the C layout is the fp32 form's. K % 16 == 0 (widths are
-// padded to 32, mini-batches are 32 rows).
+// B(k + 8h + j, r), j = 0..7 (already one contiguous run per lane); the C layout is the
+// fp32 form's.
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ short bf16_bits(float v) {
   return __builtin_bit_cast(short, __float2bfloat16(v));
 }
+template <bool CONTIG>
+__device__ __forceinline__ void load8_bf16(const float* p, int stride, int k, bf16x8& o) {
+  if constexpr (CONTIG) {
+    const float4 x0 = *reinterpret_cast<const float4*>(p + k);
+    const float4 x1 = *reinterpret_cast<const float4*>(p + k + 4);
+    o[0] = bf16_bits(x0.x); o[1] = bf16_bits(x0.y); o[2] = bf16_bits(x0.z); o[3] = bf16_bits(x0.w);
+    o[4] = bf16_bits(x1.x); o[5] = bf16_bits(x1.y); o[6] = bf16_bits(x1.z); o[7] = bf16_bits(x1.w);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf16_bits(p[(k + j) * stride]);
+  }
+}
+template <bool AK, bool BK>
 __device__ __forceinline__ f32x16 wave_gemm32_bf16(const float* a, int ars, int acs,
                                                    const float* b, int brs, int bcs, int K) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, kh = lane >> 5;
   f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const float* ap = a + r * ars + 8 * kh * acs;
-  const float* bp = b + 8 * kh * brs + r * bcs;
+  const float* ap = a + r * ars + 8 * kh * (AK ? 1 : acs);
+  const float* bp = b + 8 * kh * (BK ? 1 : brs) + r * bcs;
 #pragma unroll 2
   for (int k = 0; k < K; k += 16) {
     bf16x8 af, bfr;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      af[j] = bf16_bits(ap[(k + j) * acs]);
-      bfr[j] = bf16_bits(bp[(k + j) * brs]);
-    }
+    load8_bf16<AK>(ap, acs, k, af);
+    load8_bf16<BK>(bp, brs, k, bfr);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc, 0, 0, 0);
   }
   return acc;
 }
 
+#ifndef OMLDM_MLP_VEC
+#define OMLDM_MLP_VEC 3  // diagnostics: bit 0 vector reads of k-contiguous A, bit 1 of B
+#endif
+constexpr bool kVecA = (OMLDM_MLP_VEC & 1) != 0, kVecB = (OMLDM_MLP_VEC & 2) != 0;
+
+template <bool AK, bool BK>
 __device__ __forceinline__ f32x16 wave_gemm32(const float* a, int ars, int acs, const float* b,
                                               int brs, int bcs, int K, int bf16) {
-  return bf16 ? wave_gemm32_bf16(a, ars, acs, b, brs, bcs, K)
-              : wave_gemm32_f32(a, ars, acs, b, brs, bcs, K);
+  return bf16 ? wave_gemm32_bf16<AK, BK>(a, ars, acs, b, brs, bcs, K)
+              : wave_gemm32_f32<AK, BK>(a, ars, acs, b, brs, bcs, K);
 }
 
 // Activation and its derivative expressed through the activation's OUTPUT h (what the
@@ -151,7 +187,7 @@ __device__ void forward(float* sm, const MlpDesc& g) {
     const bool hidden = l + 1 < g.L;
     for (int t = wave; t < nt; t += 4) {
       const f32x16 acc =
-          wave_gemm32(H, g.ldh[l], 1, W + t * 32 * g.ldw[l], 1, g.ldw[l], g.np[l], g.bf16);
+          wave_gemm32<kVecA, kVecB>(H, g.ldh[l], 1, W + t * 32 * g.ldw[l], 1, g.ldw[l], g.np[l], g.bf16);
       const int col = t * 32 + (lane & 31);
       const float bias = bs[col];
       const bool pad = col >= g.n[l + 1];  // padding columns stay exactly zero
@@ -308,7 +344,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       if (l > 0) {  // dH_l = (dZ · W_l) ⊙ act'(H_l)
         float* Gn = sm + gnext;
         for (int t = wave; t < (nin >> 5); t += 4) {
-          const f32x16 acc = wave_gemm32(Gc, g.ldg, 1, W + t * 32, ldw, 1, nout, g.bf16);
+          const f32x16 acc = wave_gemm32<kVecA, false>(Gc, g.ldg, 1, W + t * 32, ldw, 1, nout, g.bf16);
           const int col = t * 32 + (lane & 31);
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
@@ -322,7 +358,8 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       const int ntc = nin >> 5, nto = nout >> 5;
       for (int t = wave; t < nto * ntc; t += 4) {
         const int to = t / ntc, tc = t - to * ntc;
-        const f32x16 acc = wave_gemm32(Gc + to * 32, 1, g.ldg, H + tc * 32, ldh, 1, kMB, g.bf16);
+        const f32x16 acc =
+            wave_gemm32<false, false>(Gc + to * 32, 1, g.ldg, H + tc * 32, ldh, 1, kMB, g.bf16);
         const int c = tc * 32 + (lane & 31);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -418,21 +455,25 @@ static int make_desc(int L, const int* widths, int task, int act, MlpDesc* g) {
     g->boff[l] = off;
     off += g->n[l + 1];
   }
+  // row strides ≡ 4 floats mod 64 banks (np is a multiple of 32): a 16-lane group reading
+  // 16 bytes each from 16 rows covers all 64 banks once, and a lane reading one float per
+  // row (the strided operands) sees rows 4 banks apart; region starts 16-byte aligned
   int p = 0, maxnp = 0;
+  auto al4 = [](int v) { return (v + 3) & ~3; };
   for (int l = 0; l < L; ++l) {
-    g->ldw[l] = g->np[l] + 1;
+    g->ldw[l] = g->np[l] + 4;
     g->lw[l] = p;
-    p += g->np[l + 1] * g->ldw[l];
+    p = al4(p + g->np[l + 1] * g->ldw[l]);
     g->lb[l] = p;
-    p += g->np[l + 1];
+    p = al4(p + g->np[l + 1]);
   }
   for (int l = 0; l <= L; ++l) {
-    g->ldh[l] = g->np[l] + 1;
+    g->ldh[l] = g->np[l] + 4;
     g->lh[l] = p;
-    p += kMB * g->ldh[l];
+    p = al4(p + kMB * g->ldh[l]);
     if (g->np[l] > maxnp) maxnp = g->np[l];
   }
-  g->ldg = maxnp + 1;
+  g->ldg = maxnp + 4;
   g->lg0 = p;
   p += kMB * g->ldg;
   g->lg1 = p;
