@@ -237,6 +237,10 @@ __global__ __launch_bounds__(1024) void ht_scatter_kernel(int B, int nbins,
 // binary search over the chunk starts; the chunk's per-feature totals are added to the
 // leaf statistics with one atomic each (a key with a single chunk — the common case once
 // the tree has grown — is the only writer of its statistics).
+// DM > 0 (d ≤ DM): one pass over the chunk's rows with every feature's Σx, Σx², min, max in
+// registers (a row's features are one contiguous run of x), then one wave reduction per
+// statistic and a single barrier. DM == 0 (any d): one pass per feature.
+template <int DM>
 __global__ __launch_bounds__(256) void ht_segment_kernel(
     const float* __restrict__ x, int d, int C, int nbins, const int2* __restrict__ seg,
     const int* __restrict__ cstart, const int* __restrict__ sorted, float* __restrict__ cc,
@@ -255,43 +259,92 @@ __global__ __launch_bounds__(256) void ht_segment_kernel(
   const int off = (chunk - cstart[key]) * kHtSegChunk;
   const int len = min(kHtSegChunk, sg.y - off);
   if (len <= 0) return;
-  __shared__ float red[4][4];
   const int node = key / C, yc = key - node * C;
   const float cnt = (float)len;
   const int* rows = sorted + sg.x + off;
-  for (int f = 0; f < d; ++f) {
-    float s1 = 0.f, s2 = 0.f, mn = INFINITY, mx = -INFINITY;
+  const int w = threadIdx.x >> 6;
+  auto publish = [&](int f, float t1, float t2, float tmn, float tmx) {
+    const size_t o = ((size_t)node * d + f) * C + yc;
+    atomicAdd(&S0[o], cnt);
+    atomicAdd(&S1[o], t1);
+    atomicAdd(&S2[o], t2);
+    atomic_min_f(&lo[node * d + f], tmn);
+    atomic_max_f(&hi[node * d + f], tmx);
+  };
+  if constexpr (DM > 0) {
+    __shared__ float red[4][DM][4];
+    float s1[DM], s2[DM], mn[DM], mx[DM];
+#pragma unroll
+    for (int f = 0; f < DM; ++f) {
+      s1[f] = 0.f;
+      s2[f] = 0.f;
+      mn[f] = INFINITY;
+      mx[f] = -INFINITY;
+    }
     for (int i = threadIdx.x; i < len; i += 256) {
-      const float v = x[(size_t)rows[i] * d + f];
-      s1 += v;
-      s2 = fmaf(v, v, s2);
-      mn = fminf(mn, v);
-      mx = fmaxf(mx, v);
+      const float* xr = x + (size_t)rows[i] * d;
+      float v[DM];
+#pragma unroll
+      for (int f = 0; f < DM; ++f) v[f] = xr[f < d ? f : 0];  // all loads in flight
+#pragma unroll
+      for (int f = 0; f < DM; ++f) {
+        if (f < d) {
+          s1[f] += v[f];
+          s2[f] = fmaf(v[f], v[f], s2[f]);
+          mn[f] = fminf(mn[f], v[f]);
+          mx[f] = fmaxf(mx[f], v[f]);
+        }
+      }
     }
-    wave_sum2(s1, s2);
-    mn = -wave_max(-mn);
-    mx = wave_max(mx);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-      red[w][0] = s1;
-      red[w][1] = s2;
-      red[w][2] = mn;
-      red[w][3] = mx;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const float t1 = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
-      const float t2 = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
-      const float tmn = fminf(fminf(red[0][2], red[1][2]), fminf(red[2][2], red[3][2]));
-      const float tmx = fmaxf(fmaxf(red[0][3], red[1][3]), fmaxf(red[2][3], red[3][3]));
-      const size_t o = ((size_t)node * d + f) * C + yc;
-      atomicAdd(&S0[o], cnt);
-      atomicAdd(&S1[o], t1);
-      atomicAdd(&S2[o], t2);
-      atomic_min_f(&lo[node * d + f], tmn);
-      atomic_max_f(&hi[node * d + f], tmx);
+#pragma unroll
+    for (int f = 0; f < DM; ++f) {
+      if (f < d) {
+        wave_sum2(s1[f], s2[f]);
+        const float tmn = -wave_max(-mn[f]), tmx = wave_max(mx[f]);
+        if ((threadIdx.x & 63) == 0) {
+          red[w][f][0] = s1[f];
+          red[w][f][1] = s2[f];
+          red[w][f][2] = tmn;
+          red[w][f][3] = tmx;
+        }
+      }
     }
     __syncthreads();
+    if (threadIdx.x < d) {
+      const int f = threadIdx.x;
+      publish(f, (red[0][f][0] + red[1][f][0]) + (red[2][f][0] + red[3][f][0]),
+              (red[0][f][1] + red[1][f][1]) + (red[2][f][1] + red[3][f][1]),
+              fminf(fminf(red[0][f][2], red[1][f][2]), fminf(red[2][f][2], red[3][f][2])),
+              fmaxf(fmaxf(red[0][f][3], red[1][f][3]), fmaxf(red[2][f][3], red[3][f][3])));
+    }
+  } else {
+    __shared__ float red[4][4];
+    for (int f = 0; f < d; ++f) {
+      float s1 = 0.f, s2 = 0.f, mn = INFINITY, mx = -INFINITY;
+      for (int i = threadIdx.x; i < len; i += 256) {
+        const float v = x[(size_t)rows[i] * d + f];
+        s1 += v;
+        s2 = fmaf(v, v, s2);
+        mn = fminf(mn, v);
+        mx = fmaxf(mx, v);
+      }
+      wave_sum2(s1, s2);
+      mn = -wave_max(-mn);
+      mx = wave_max(mx);
+      if ((threadIdx.x & 63) == 0) {
+        red[w][0] = s1;
+        red[w][1] = s2;
+        red[w][2] = mn;
+        red[w][3] = mx;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0)
+        publish(f, (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]),
+                (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]),
+                fminf(fminf(red[0][2], red[1][2]), fminf(red[2][2], red[3][2])),
+                fmaxf(fmaxf(red[0][3], red[1][3]), fmaxf(red[2][3], red[3][3])));
+      __syncthreads();
+    }
   }
   if (threadIdx.x == 0) {
     atomicAdd(&cc[key], cnt);
@@ -463,9 +516,15 @@ OMLDM_API int omldm_ht_update(const float* x, const float* y, int B, int d, int 
                      sorted);
   // chunk count ≤ nbins + B / kHtSegChunk; surplus blocks exit on cstart[nbins]
   const int nchunk = nbins + (B + kHtSegChunk - 1) / kHtSegChunk;
-  hipLaunchKernelGGL(ht_segment_kernel, dim3(nchunk), dim3(256), 0, st, x, d, C, nbins, seg,
-                     cstart, sorted, tree[4], tree[5], tree[6], tree[7], tree[8], tree[9],
-                     tree[10]);
+#define OMLDM_HT_SEG(DM)                                                                      \
+  hipLaunchKernelGGL(ht_segment_kernel<DM>, dim3(nchunk), dim3(256), 0, st, x, d, C, nbins, seg, \
+                     cstart, sorted, tree[4], tree[5], tree[6], tree[7], tree[8], tree[9],       \
+                     tree[10])
+  if (d <= 8) OMLDM_HT_SEG(8);
+  else if (d <= 16) OMLDM_HT_SEG(16);
+  else if (d <= 32) OMLDM_HT_SEG(32);
+  else OMLDM_HT_SEG(0);
+#undef OMLDM_HT_SEG
   return (int)hipGetLastError();
 }
 
