@@ -137,24 +137,63 @@ __global__ __launch_bounds__(256) void ht_update_kernel(
 constexpr int kHtRowsPerBlock = 4096;  // rows per route/scatter block (1024 threads)
 constexpr int kHtSegChunk = 1024;      // rows per segment-reduce block (a key may span many)
 
+// The tree's (feature, threshold, left, right) are staged in LDS as one int4 per node when
+// they fit (one ds_read_b128 per level instead of four dependent L2 reads), and each thread
+// routes its kHtRowsPerBlock / 1024 rows level-synchronously, so the per-level latency is
+// paid once for all of them rather than once per row.
+constexpr int kHtRowsPerThread = kHtRowsPerBlock / 1024;
+
 __global__ __launch_bounds__(1024) void ht_route_hist_kernel(
     const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int C, int depth,
     const float* __restrict__ feat, const float* __restrict__ thr, const float* __restrict__ left,
-    const float* __restrict__ right, int nbins, int* __restrict__ keys, int* __restrict__ hist,
-    double* __restrict__ nfit) {
-  extern __shared__ int h[];  // [nbins]
+    const float* __restrict__ right, int nbins, int nnodes, int* __restrict__ keys,
+    int* __restrict__ hist, double* __restrict__ nfit) {
+  extern __shared__ int h[];  // [nbins], then int4 tree[nnodes] when nnodes > 0
+  int4* tree = reinterpret_cast<int4*>(h + ((nbins + 3) & ~3));
   for (int b = threadIdx.x; b < nbins; b += 1024) h[b] = 0;
+  for (int n = threadIdx.x; n < nnodes; n += 1024)
+    tree[n] = make_int4((int)feat[n], __float_as_int(thr[n]), (int)left[n], (int)right[n]);
   __syncthreads();
-  const int r0 = blockIdx.x * kHtRowsPerBlock;
-  float cnt = 0.f;
-  for (int r = r0 + threadIdx.x; r < r0 + kHtRowsPerBlock && r < B; r += 1024) {
-    int key = -1;
-    if (!__builtin_isnan(yv[r])) {
-      int yi = (int)yv[r];
-      yi = yi < 0 ? 0 : (yi >= C ? C - 1 : yi);
-      key = ht_route(x + (size_t)r * d, feat, thr, left, right, depth) * C + yi;
-      if (key >= nbins) key = -1;
+  const int r0 = blockIdx.x * kHtRowsPerBlock + threadIdx.x;
+  int node[kHtRowsPerThread], yi[kHtRowsPerThread];
+  bool ok[kHtRowsPerThread];
+#pragma unroll
+  for (int u = 0; u < kHtRowsPerThread; ++u) {
+    const int r = r0 + u * 1024;
+    const float yr = r < B ? yv[r] : __builtin_nanf("");
+    ok[u] = !__builtin_isnan(yr);
+    const int yc = ok[u] ? (int)yr : 0;
+    yi[u] = yc < 0 ? 0 : (yc >= C ? C - 1 : yc);
+    node[u] = 0;
+  }
+  for (int it = 0; it <= depth; ++it) {
+    bool more = false;
+#pragma unroll
+    for (int u = 0; u < kHtRowsPerThread; ++u) {
+      int4 t;
+      if (nnodes > 0) {
+        t = tree[node[u]];
+      } else {
+        t = make_int4((int)feat[node[u]], __float_as_int(thr[node[u]]), (int)left[node[u]],
+                      (int)right[node[u]]);
+      }
+      const bool inner = ok[u] && t.x >= 0;
+      // branch-free gather from a clamped address (row 0 / feature 0 for finished rows)
+      const size_t r = inner ? (size_t)(r0 + u * 1024) : 0;
+      const float v = x[r * d + (inner ? t.x : 0)];
+      const int nx = v <= __int_as_float(t.y) ? t.z : t.w;
+      node[u] = inner ? nx : node[u];
+      more |= inner;
     }
+    if (!more) break;
+  }
+  float cnt = 0.f;
+#pragma unroll
+  for (int u = 0; u < kHtRowsPerThread; ++u) {
+    const int r = r0 + u * 1024;
+    if (r >= B) break;
+    int key = ok[u] ? node[u] * C + yi[u] : -1;
+    if (key >= nbins) key = -1;
     keys[r] = key;
     if (key >= 0) {
       atomicAdd(&h[key], 1);
@@ -167,56 +206,112 @@ __global__ __launch_bounds__(1024) void ht_route_hist_kernel(
   if ((threadIdx.x & 63) == 0 && n > 0.f && nfit) atomicAdd(nfit, (double)n);
 }
 
-// Inclusive block scan of one int per thread (1024 threads).
-__device__ __forceinline__ int block_scan_1024(int v, int* part) {
-  part[threadIdx.x] = v;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele
-    const int u = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-    __syncthreads();
-    part[threadIdx.x] += u;
-    __syncthreads();
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int u = __shfl_up(v, off);
+    v += lane >= off ? u : 0;
   }
-  const int r = part[threadIdx.x];
-  __syncthreads();
-  return r;
+  return v;
 }
 
+// Inclusive scan of two ints per thread over a 1024-thread block: wave scans (no
+// barriers), then each wave adds the totals of the waves before it (one barrier).
+__device__ __forceinline__ void block_scan2_1024(int& a, int& b, int2* wtot) {
+  a = wave_incl_scan(a);
+  b = wave_incl_scan(b);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) wtot[w] = make_int2(a, b);
+  __syncthreads();
+  int pa = 0, pb = 0;
+  for (int i = 0; i < w; ++i) {
+    const int2 t = wtot[i];
+    pa += t.x;
+    pb += t.y;
+  }
+  a += pa;
+  b += pb;
+}
+
+constexpr int kHtScanReg = 32;  // per-bin column of block counts held in registers
+
 // One block of 1024 threads. hist[blk][bin] (counts) → bases; seg[bin] = (start, length);
-// cstart[bin] = first segment-reduce chunk of the bin, cstart[nbins] = chunk count.
+// cstart[bin] = first segment-reduce chunk of the bin, cstart[nbins] = chunk count;
+// ckey[chunk] = the bin (key) the chunk belongs to. With one bin per thread and
+// nblk ≤ kHtScanReg the column is loaded once, all loads in flight together.
 __global__ __launch_bounds__(1024) void ht_scan_kernel(int nblk, int nbins, int* __restrict__ hist,
                                                        int2* __restrict__ seg,
-                                                       int* __restrict__ cstart) {
-  __shared__ int part[1024];
-  // per thread: a contiguous range of bins; bin totals, then a block scan of the ranges
+                                                       int* __restrict__ cstart,
+                                                       int* __restrict__ ckey) {
+  __shared__ int2 wtot[16];
   const int per = (nbins + 1023) / 1024;
   const int b0 = threadIdx.x * per, b1 = min(nbins, b0 + per);
+  const bool reg = per == 1 && nblk <= kHtScanReg;
+  int col[kHtScanReg];
   int tot = 0, ch = 0;
-  for (int b = b0; b < b1; ++b) {
+  if (reg) {
+    const int bb = b0 < nbins ? b0 : 0;
+#pragma unroll
+    for (int k = 0; k < kHtScanReg; ++k)
+      col[k] = hist[(size_t)(k < nblk ? k : 0) * nbins + bb];
     int run = 0;
+#pragma unroll
+    for (int k = 0; k < kHtScanReg; ++k) run += k < nblk ? col[k] : 0;
+    if (b0 < nbins) {
+      tot = run;
+      ch = (run + kHtSegChunk - 1) / kHtSegChunk;
+    }
+  } else {
+    for (int b = b0; b < b1; ++b) {
+      int run = 0;
 #pragma unroll 8
-    for (int k = 0; k < nblk; ++k) run += hist[(size_t)k * nbins + b];
-    seg[b] = make_int2(0, run);
-    tot += run;
-    ch += (run + kHtSegChunk - 1) / kHtSegChunk;
+      for (int k = 0; k < nblk; ++k) run += hist[(size_t)k * nbins + b];
+      seg[b] = make_int2(0, run);
+      tot += run;
+      ch += (run + kHtSegChunk - 1) / kHtSegChunk;
+    }
   }
-  int start = block_scan_1024(tot, part) - tot;
-  int cs = block_scan_1024(ch, part) - ch;
+  int start = tot, cs = ch;
+  block_scan2_1024(start, cs, wtot);
+  start -= tot;
+  cs -= ch;
+  if (threadIdx.x == 1023) cstart[nbins] = cs + ch;
+  if (reg) {
+    if (b0 < nbins) {
+      seg[b0] = make_int2(start, tot);
+      cstart[b0] = cs;
+      for (int c = 0; c < ch; ++c) ckey[cs + c] = b0;
+      int run = start;
+#pragma unroll
+      for (int k = 0; k < kHtScanReg; ++k) {
+        if (k < nblk) hist[(size_t)k * nbins + b0] = run;
+        run += k < nblk ? col[k] : 0;
+      }
+    }
+    return;
+  }
   for (int b = b0; b < b1; ++b) {
     const int len = seg[b].y;
+    const int nch = (len + kHtSegChunk - 1) / kHtSegChunk;
     seg[b] = make_int2(start, len);
     cstart[b] = cs;
-    cs += (len + kHtSegChunk - 1) / kHtSegChunk;
+    for (int c = 0; c < nch; ++c) ckey[cs + c] = b;
+    cs += nch;
     int run = start;
-    for (int k = 0; k < nblk; ++k) {
-      const size_t o = (size_t)k * nbins + b;
-      const int c = hist[o];
-      hist[o] = run;
-      run += c;
+    for (int k0 = 0; k0 < nblk; k0 += 8) {  // 8 loads in flight, then their 8 stores
+      int c[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        c[u] = k0 + u < nblk ? hist[(size_t)(k0 + u) * nbins + b] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (k0 + u < nblk) hist[(size_t)(k0 + u) * nbins + b] = run;
+        run += c[u];
+      }
     }
     start += len;
   }
-  if (threadIdx.x == 1023) cstart[nbins] = cs;
 }
 
 __global__ __launch_bounds__(1024) void ht_scatter_kernel(int B, int nbins,
@@ -243,18 +338,14 @@ __global__ __launch_bounds__(1024) void ht_scatter_kernel(int B, int nbins,
 template <int DM>
 __global__ __launch_bounds__(256) void ht_segment_kernel(
     const float* __restrict__ x, int d, int C, int nbins, const int2* __restrict__ seg,
-    const int* __restrict__ cstart, const int* __restrict__ sorted, float* __restrict__ cc,
-    float* __restrict__ S0, float* __restrict__ S1, float* __restrict__ S2,
-    float* __restrict__ lo, float* __restrict__ hi, float* __restrict__ since) {
+    const int* __restrict__ cstart, const int* __restrict__ ckey, const int* __restrict__ sorted,
+    float* __restrict__ cc, float* __restrict__ S0, float* __restrict__ S1,
+    float* __restrict__ S2, float* __restrict__ lo, float* __restrict__ hi,
+    float* __restrict__ since) {
   const int chunk = blockIdx.x;
-  if (chunk >= cstart[nbins]) return;
-  int a = 0, b = nbins - 1;  // last bin with cstart[bin] <= chunk (and a non-empty segment)
-  while (a < b) {
-    const int m = (a + b + 1) >> 1;
-    if (cstart[m] <= chunk) a = m;
-    else b = m - 1;
-  }
-  const int key = a;
+  const int nch = cstart[nbins];
+  const int key = ckey[chunk];  // ckey has gridDim.x entries; stale beyond nch
+  if (chunk >= nch) return;
   const int2 sg = seg[key];
   const int off = (chunk - cstart[key]) * kHtSegChunk;
   const int len = min(kHtSegChunk, sg.y - off);
@@ -281,18 +372,30 @@ __global__ __launch_bounds__(256) void ht_segment_kernel(
       mn[f] = INFINITY;
       mx[f] = -INFINITY;
     }
-    for (int i = threadIdx.x; i < len; i += 256) {
-      const float* xr = x + (size_t)rows[i] * d;
-      float v[DM];
+    // RPT rows per thread per step: their ids, then all RPT·DM features, in flight together
+    constexpr int RPT = DM <= 16 ? 4 : 2;
+    for (int i0 = threadIdx.x; i0 < len; i0 += 256 * RPT) {
+      int rid[RPT];
 #pragma unroll
-      for (int f = 0; f < DM; ++f) v[f] = xr[f < d ? f : 0];  // all loads in flight
+      for (int u = 0; u < RPT; ++u) rid[u] = rows[i0 + u * 256 < len ? i0 + u * 256 : i0];
+      float v[RPT][DM];
 #pragma unroll
-      for (int f = 0; f < DM; ++f) {
-        if (f < d) {
-          s1[f] += v[f];
-          s2[f] = fmaf(v[f], v[f], s2[f]);
-          mn[f] = fminf(mn[f], v[f]);
-          mx[f] = fmaxf(mx[f], v[f]);
+      for (int u = 0; u < RPT; ++u) {
+        const float* xr = x + (size_t)rid[u] * d;
+#pragma unroll
+        for (int f = 0; f < DM; ++f) v[u][f] = xr[f < d ? f : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        if (i0 + u * 256 >= len) break;
+#pragma unroll
+        for (int f = 0; f < DM; ++f) {
+          if (f < d) {
+            s1[f] += v[u][f];
+            s2[f] = fmaf(v[u][f], v[u][f], s2[f]);
+            mn[f] = fminf(mn[f], v[u][f]);
+            mx[f] = fmaxf(mx[f], v[u][f]);
+          }
         }
       }
     }
@@ -416,17 +519,21 @@ __global__ __launch_bounds__(256) void ht_split_kernel(
     gains[p] = g;
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  // best / second-best attribute: wave 0, one feature per lane (best bin = first maximum),
+  // then a butterfly reduction of (top gain, its feature and bin, runner-up gain) that
+  // keeps the lowest feature index on ties — the order a serial scan would give.
+  if (threadIdx.x >= 64) return;
   float g1 = -2.f, g2 = -2.f;
-  int f1 = 0, b1 = 0;
-  for (int f = 0; f < d; ++f) {
+  int f1 = 0x7fffffff, b1 = 0;
+  for (int f = threadIdx.x; f < d; f += 64) {
     float gm = -2.f;
     int bm = 0;
-    for (int b = 0; b < nb; ++b)
-      if (gains[f * nb + b] > gm) {
-        gm = gains[f * nb + b];
-        bm = b;
-      }
+#pragma unroll 4
+    for (int b = 0; b < nb; ++b) {
+      const float g = gains[f * nb + b];
+      bm = g > gm ? b : bm;
+      gm = g > gm ? g : gm;
+    }
     if (gm > g1) {
       g2 = g1;
       g1 = gm;
@@ -436,6 +543,17 @@ __global__ __launch_bounds__(256) void ht_split_kernel(
       g2 = gm;
     }
   }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const float og1 = __shfl_xor(g1, m), og2 = __shfl_xor(g2, m);
+    const int of1 = __shfl_xor(f1, m), ob1 = __shfl_xor(b1, m);
+    const bool take = og1 > g1 || (og1 == g1 && of1 < f1);
+    g2 = take ? fmaxf(g1, og2) : fmaxf(g2, og1);
+    g1 = take ? og1 : g1;
+    f1 = take ? of1 : f1;
+    b1 = take ? ob1 : b1;
+  }
+  if (threadIdx.x != 0) return;
   if (d == 1) g2 = 0.f;
   since[node] = 0.f;
   const float R = __log2f((float)C);
@@ -483,7 +601,8 @@ using namespace omldm;
 // aggregated atomic kernel, kept as the fallback / A-B reference).
 OMLDM_API long long omldm_ht_update_ws_ints(int B, int N, int C) {
   const long long nblk = (B + kHtRowsPerBlock - 1) / kHtRowsPerBlock;
-  return 2LL * B + ((nblk * N * C + 1) & ~1LL) + 2LL * N * C + (N * C + 2);
+  const long long nchunk = (long long)N * C + (B + kHtSegChunk - 1) / kHtSegChunk;
+  return 2LL * B + ((nblk * N * C + 1) & ~1LL) + 2LL * N * C + (N * C + 2) + nchunk;
 }
 
 OMLDM_API int omldm_ht_update(const float* x, const float* y, int B, int d, int C, int depth,
@@ -505,20 +624,26 @@ OMLDM_API int omldm_ht_update(const float* x, const float* y, int B, int d, int 
   int* hist = ws + 2 * (size_t)B;
   int2* seg = reinterpret_cast<int2*>(hist + (((size_t)nblk * nbins + 1) & ~(size_t)1));
   int* cstart = reinterpret_cast<int*>(seg + nbins);  // [nbins + 1]
-  const size_t lds = (size_t)nbins * 4;
-  int e = check_dyn_lds((const void*)ht_route_hist_kernel, lds);
-  if (!e) e = check_dyn_lds((const void*)ht_scatter_kernel, lds);
-  if (e) return e;
-  hipLaunchKernelGGL(ht_route_hist_kernel, dim3(nblk), dim3(1024), lds, st, x, y, B, d, C, depth,
-                     tree[0], tree[1], tree[2], tree[3], nbins, keys, hist, nfit);
-  hipLaunchKernelGGL(ht_scan_kernel, dim3(1), dim3(1024), 0, st, nblk, nbins, hist, seg, cstart);
-  hipLaunchKernelGGL(ht_scatter_kernel, dim3(nblk), dim3(1024), lds, st, B, nbins, keys, hist,
-                     sorted);
   // chunk count ≤ nbins + B / kHtSegChunk; surplus blocks exit on cstart[nbins]
   const int nchunk = nbins + (B + kHtSegChunk - 1) / kHtSegChunk;
+  int* ckey = cstart + nbins + 2;  // [nchunk]
+  const size_t lds = (size_t)nbins * 4;
+  // tree staged in LDS next to the histogram when both fit in 64 KB
+  const size_t lds_tree = (size_t)((nbins + 3) & ~3) * 4 + (size_t)N * 16;
+  const int nstage = lds_tree <= 64 * 1024 ? N : 0;
+  const size_t lds_route = nstage ? lds_tree : lds;
+  int e = check_dyn_lds((const void*)ht_route_hist_kernel, lds_route);
+  if (!e) e = check_dyn_lds((const void*)ht_scatter_kernel, lds);
+  if (e) return e;
+  hipLaunchKernelGGL(ht_route_hist_kernel, dim3(nblk), dim3(1024), lds_route, st, x, y, B, d, C,
+                     depth, tree[0], tree[1], tree[2], tree[3], nbins, nstage, keys, hist, nfit);
+  hipLaunchKernelGGL(ht_scan_kernel, dim3(1), dim3(1024), 0, st, nblk, nbins, hist, seg, cstart,
+                     ckey);
+  hipLaunchKernelGGL(ht_scatter_kernel, dim3(nblk), dim3(1024), lds, st, B, nbins, keys, hist,
+                     sorted);
 #define OMLDM_HT_SEG(DM)                                                                      \
   hipLaunchKernelGGL(ht_segment_kernel<DM>, dim3(nchunk), dim3(256), 0, st, x, d, C, nbins, seg, \
-                     cstart, sorted, tree[4], tree[5], tree[6], tree[7], tree[8], tree[9],       \
+                     cstart, ckey, sorted, tree[4], tree[5], tree[6], tree[7], tree[8], tree[9],       \
                      tree[10])
   if (d <= 8) OMLDM_HT_SEG(8);
   else if (d <= 16) OMLDM_HT_SEG(16);
