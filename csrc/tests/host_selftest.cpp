@@ -34,6 +34,14 @@ void omldm_cpu_linear_apply(float* w32, uint16_t* w16, float* dacc, int dim);
 void omldm_cpu_linear_predict(const float* w, long long wstride, int M, const float* num, int dn,
                               const void* cat, int dc, int B, int dim, int bias, int cspan,
                               const float* wscale, float* out);
+int omldm_codec_available(int codec);
+int omldm_codec_decompress(int codec, const uint8_t* src, int64_t n, uint8_t** out, int64_t* on);
+int omldm_codec_compress(int codec, const uint8_t* src, int64_t n, int level, uint8_t** out,
+                         int64_t* on);
+void omldm_codec_free(void* p);
+int64_t omldm_kafka_decode_into(const uint8_t* data, int64_t n, int64_t min_offset,
+                                int64_t max_records, uint8_t* dst, int64_t cap, int64_t* offs,
+                                int64_t* next_offset, int verify_crc);
 }
 
 static int failures = 0;
@@ -132,8 +140,73 @@ static void test_concurrent_callers() {
   CHECK(std::memcmp(nums[0].data(), nums[1].data(), nums[0].size() * 4) != 0);
 }
 
+// Kafka codecs: round trips from several threads at once (the libraries are loaded on
+// first use, under TSan here), then mutated streams into every decoder and the record-set
+// decoder — they must fail cleanly, never read or write out of bounds (ASan/UBSan).
+static void test_kafka_wire() {
+  std::vector<uint8_t> src(200000);
+  for (size_t i = 0; i < src.size(); ++i) src[i] = uint8_t((i * 7) % 251 ^ (i / 1000));
+  std::vector<std::thread> ts;
+  std::vector<int> ok(8, 0);
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([&, t] {
+      const int codec = 1 + t % 4;
+      if (!omldm_codec_available(codec)) {
+        ok[t] = 1;
+        return;
+      }
+      uint8_t *z = nullptr, *d = nullptr;
+      int64_t zn = 0, dn = 0;
+      if (omldm_codec_compress(codec, src.data(), (int64_t)src.size(), -1, &z, &zn)) return;
+      if (omldm_codec_decompress(codec, z, zn, &d, &dn) == 0 && dn == (int64_t)src.size() &&
+          std::memcmp(d, src.data(), src.size()) == 0)
+        ok[t] = 1;
+      omldm_codec_free(z);
+      omldm_codec_free(d);
+    });
+  for (auto& t : ts) t.join();
+  for (int v : ok) CHECK(v == 1);
+  uint32_t rng = 12345;
+  for (int codec = 1; codec <= 4; ++codec) {
+    if (!omldm_codec_available(codec)) continue;
+    uint8_t* z = nullptr;
+    int64_t zn = 0;
+    CHECK(omldm_codec_compress(codec, src.data(), 5000, -1, &z, &zn) == 0);
+    std::vector<uint8_t> m(z, z + zn);
+    omldm_codec_free(z);
+    for (int trial = 0; trial < 200; ++trial) {
+      std::vector<uint8_t> b = m;
+      for (int k = 0; k < 3; ++k) {
+        rng = rng * 1664525u + 1013904223u;
+        b[rng % b.size()] ^= uint8_t(rng >> 24);
+      }
+      rng = rng * 1664525u + 1013904223u;
+      const size_t cut = trial % 2 ? b.size() : rng % (b.size() + 1);
+      uint8_t* d = nullptr;
+      int64_t dn = 0;
+      if (omldm_codec_decompress(codec, b.data(), (int64_t)cut, &d, &dn) == 0) omldm_codec_free(d);
+    }
+  }
+  std::vector<uint8_t> junk(4096), dst(1 << 16);
+  std::vector<int64_t> offs(1025);
+  for (int trial = 0; trial < 200; ++trial) {
+    for (auto& c : junk) {
+      rng = rng * 1664525u + 1013904223u;
+      c = uint8_t(rng >> 24);
+    }
+    junk[16] = 2;  // magic 2 so the walk reaches the record parser
+    junk[8] = 0;
+    junk[9] = 0;
+    junk[10] = uint8_t(trial * 13);
+    int64_t nxt = 0;
+    (void)omldm_kafka_decode_into(junk.data(), (int64_t)junk.size(), 0, 1024, dst.data(),
+                                  (int64_t)dst.size(), offs.data(), &nxt, 0);
+  }
+}
+
 int main() {
   test_hashes();
+  test_kafka_wire();
   test_parser();
   test_linear_paths();
   test_concurrent_callers();

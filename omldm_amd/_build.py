@@ -89,7 +89,7 @@ def build_host(force: bool = False) -> str:
         cxx = os.environ.get("CXX", "g++")
         tmp = HOST_LIB + ".tmp"
         _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall",
-              "-I", os.path.join(CSRC, "host"), *srcs, "-o", tmp])
+              "-I", os.path.join(CSRC, "host"), *srcs, "-o", tmp, "-lz", "-ldl"])
         os.replace(tmp, HOST_LIB)
     return HOST_LIB
 

@@ -7,10 +7,16 @@ need no consumer group). Implemented subset, enough for produce/consume of JSON 
 
 * Metadata v1 (api 3)   — topic → partitions + leader brokers
 * ListOffsets v1 (api 2) — earliest (-2) / latest (-1) offsets
-* Produce v3 (api 0)    — RecordBatch v2, acks=1, no compression
-* Fetch v4 (api 1)      — RecordBatch v2 decoding (magic 2; older message sets skipped)
+* Produce v3 (api 0)    — RecordBatch v2, acks=1; v7 when the batch is zstd-compressed
+* Fetch v4 (api 1)      — RecordBatch v2 decoding (magic 2; older message sets and
+                          transactional control batches skipped); v10 once the broker
+                          answers UNSUPPORTED_COMPRESSION_TYPE (zstd topics need ≥ v10)
 * CreateTopics v0 (api 19) — best effort, for ``create_topic``
-CRC-32C of record batches is computed by the host library (csrc/host/crc32c.cpp).
+* compression: gzip / snappy / lz4 / zstd batches are read transparently and any of them
+  can be written (``KafkaBroker(..., compression="lz4")`` or ``host:port?compression=lz4``)
+CRC-32C of record batches is computed by the host library (csrc/host/crc32c.cpp); the
+codecs and the record-set decoder that fills the pinned staging slot without a Python
+object per record are csrc/host/kafka_wire.cpp.
 Compatibility is at the level of the public protocol spec; tests exercise it against a
 protocol-level fake broker (tests/fake_kafka.py) — there is no real broker here.
 """
@@ -152,8 +158,60 @@ class R:
 # ----------------------------------------------------------------- record batch
 
 
+CODECS = {"none": 0, "gzip": 1, "snappy": 2, "lz4": 3, "zstd": 4}
+UNSUPPORTED_COMPRESSION_TYPE = 76
+
+
+def codec_id(c) -> int:
+    if isinstance(c, int):
+        if c not in CODECS.values():
+            raise ValueError(f"unknown Kafka compression codec {c}")
+        return c
+    key = (c or "none").lower()
+    if key not in CODECS:
+        raise ValueError(f"unknown Kafka compression codec {c!r} (one of {sorted(CODECS)})")
+    return CODECS[key]
+
+
+def _codec_call(fn, codec: int, data: bytes, *extra) -> bytes:
+    import ctypes
+
+    from omldm_amd.ops import native
+
+    lib = native.host()
+    out, n = ctypes.c_void_p(), ctypes.c_longlong()
+    rc = getattr(lib, fn)(codec, data, len(data), *extra, ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        what = {-1: "unknown codec", -2: "corrupt data", -3: "codec library not found",
+                -4: "too large", -6: "out of memory"}.get(rc, str(rc))
+        raise ValueError(f"kafka {fn.split('_')[-1]} ({codec}): {what}")
+    try:
+        return ctypes.string_at(out.value, n.value) if n.value else b""
+    finally:
+        lib.omldm_codec_free(out)
+
+
+def compress(codec, data: bytes, level: int = -1) -> bytes:
+    c = codec_id(codec)
+    return data if c == 0 else _codec_call("omldm_codec_compress", c, data, level)
+
+
+def decompress(codec, data: bytes) -> bytes:
+    c = codec_id(codec)
+    return data if c == 0 else _codec_call("omldm_codec_decompress", c, data)
+
+
+def codec_available(codec) -> bool:
+    from omldm_amd.ops import native
+
+    return bool(native.host().omldm_codec_available(codec_id(codec)))
+
+
 def encode_batch(values: list[bytes], base_offset: int = 0, ts_ms: int | None = None,
-                 keys: list | None = None) -> bytes:
+                 keys: list | None = None, compression=0, control: bool = False) -> bytes:
+    """RecordBatch v2 of ``values``; ``compression`` (name or id) compresses the records
+    section and sets attributes bits 0-2; ``control`` marks a transactional control batch."""
+    codec = codec_id(compression)
     ts = int(time.time() * 1000) if ts_ms is None else ts_ms
     recs = bytearray()
     for i, v in enumerate(values):
@@ -170,8 +228,9 @@ def encode_batch(values: list[bytes], base_offset: int = 0, ts_ms: int | None = 
         body += varint(0)                  # headers
         recs += varint(len(body)) + body
     tail = W()
-    tail.i16(0).i32(len(values) - 1).i64(ts).i64(ts).i64(-1).i16(-1).i32(-1).i32(len(values))
-    payload = bytes(tail.b) + bytes(recs)
+    attrs = codec | (0x20 if control else 0)
+    tail.i16(attrs).i32(len(values) - 1).i64(ts).i64(ts).i64(-1).i16(-1).i32(-1).i32(len(values))
+    payload = bytes(tail.b) + (compress(codec, bytes(recs)) if codec else bytes(recs))
     crc = crc32c(payload)
     head = W()
     head.i64(base_offset).i32(4 + 1 + 4 + len(payload)).i32(0).i8(2)
@@ -197,10 +256,14 @@ def decode_batches(data: bytes, verify: bool = True) -> list[tuple[int, bytes]]:
         if verify and crc32c(body) != crc:
             raise ValueError("record batch CRC mismatch")
         attrs = struct.unpack_from(">h", body, 0)[0]
-        if attrs & 0x7:
-            raise ValueError("compressed record batches are not supported")
+        if attrs & 0x20:  # transactional control batch (commit / abort marker)
+            p = end
+            continue
         count = struct.unpack_from(">i", body, 36)[0]
         q = 40
+        if attrs & 0x7:
+            body = decompress(attrs & 0x7, bytes(body[40:]))
+            q = 0
         for _ in range(count):
             ln, q = read_varint(body, q)
             rend = q + ln
@@ -256,9 +319,14 @@ class _Conn:
 class KafkaBroker(Broker):
     """transport.Broker over the Kafka protocol (bootstrap ``host:port[,host:port]``)."""
 
-    def __init__(self, bootstrap: str, timeout: float = 10.0):
+    def __init__(self, bootstrap: str, timeout: float = 10.0, compression=None):
+        bootstrap, _, query = bootstrap.partition("?")
+        opts = dict(kv.split("=", 1) for kv in query.split("&") if "=" in kv)
+        self.codec = codec_id(compression if compression is not None
+                              else opts.get("compression", "none"))
         self.bootstrap = [(h, int(p)) for h, p in (x.rsplit(":", 1) for x in bootstrap.split(","))]
         self.timeout = timeout
+        self._fetch_v10: set = set()  # brokers that asked for Fetch ≥ v10 (zstd topics)
         self._conns: dict = {}
         self._meta: dict = {}     # topic -> {partition: leader}
         self._brokers: dict = {}  # node -> (host, port)
@@ -307,12 +375,14 @@ class KafkaBroker(Broker):
         self.produce_batch(topic, partition, [value])
 
     def produce_batch(self, topic: str, partition: int, values: list[bytes]) -> int:
-        rs = encode_batch(values)
+        rs = encode_batch(values, compression=self.codec)
         body = W().s(None).i16(1).i32(int(self.timeout * 1000)).arr(
             [topic], lambda w, t: w.s(t).arr([partition], lambda w, p: w.i32(p).by(rs)))
         leader = self._metadata(topic).get(partition)
-        r = self._conn(leader).call(0, 3, bytes(body.b))
-        res = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.i16(), r.i64(), r.i64()))))
+        ver = 7 if self.codec == CODECS["zstd"] else 3  # brokers accept zstd from Produce v7
+        r = self._conn(leader).call(0, ver, bytes(body.b))
+        res = r.arr(lambda r: (r.s(), r.arr(lambda r: (
+            r.i32(), r.i16(), r.i64(), r.i64(), *((r.i64(),) if ver >= 5 else ())))))
         err = res[0][1][0][1]
         if err:
             raise IOError(f"kafka produce error {err}")
@@ -328,25 +398,89 @@ class KafkaBroker(Broker):
     def end_offset(self, topic, partition):
         return self._list_offset(topic, partition, -1)
 
+    def _fetch(self, topic: str, partition: int, offset: int, max_bytes: int = 4 << 20) -> bytes:
+        """Raw record set of one partition from ``offset`` (Fetch v4; v10 for brokers that
+        answered UNSUPPORTED_COMPRESSION_TYPE, i.e. zstd data)."""
+        leader = self._metadata(topic).get(partition)
+        conn = self._conn(leader)
+        for _ in range(2):
+            v10 = id(conn) in self._fetch_v10
+            w = W().i32(-1).i32(100).i32(1).i32(max(8 << 20, max_bytes)).i8(0)
+            if v10:
+                w.i32(0).i32(-1)  # no fetch session
+            w.arr([topic], lambda w, t: w.s(t).arr([partition], lambda w, p: (
+                w.i32(p), w.i32(-1) if v10 else None, w.i64(offset),
+                w.i64(-1) if v10 else None, w.i32(max_bytes))))
+            if v10:
+                w.i32(0)  # forgotten topics
+            r = conn.call(1, 10 if v10 else 4, bytes(w.b))
+            r.i32()  # throttle
+            if v10:
+                top_err = r.i16()
+                r.i32()  # session id
+                if top_err:
+                    raise IOError(f"kafka fetch error {top_err}")
+            res = r.arr(lambda r: (r.s(), r.arr(lambda r: (
+                r.i32(), r.i16(), r.i64(), r.i64(), *((r.i64(),) if v10 else ()),
+                r.arr(lambda r: (r.i64(), r.i64())), r.by()))))
+            out, err = b"", 0
+            for _t, parts in res:
+                for part in parts:
+                    err = err or part[1]
+                    out += part[-1] or b""
+            if err == UNSUPPORTED_COMPRESSION_TYPE and not v10:
+                self._fetch_v10.add(id(conn))
+                continue
+            if err:
+                raise IOError(f"kafka fetch error {err}")
+            return out
+        raise IOError("kafka fetch: broker rejected Fetch v10")
+
     def consume(self, topic, partition, offset, max_records):
-        body = W().i32(-1).i32(100).i32(1).i32(8 << 20).i8(0).arr(
-            [topic], lambda w, t: w.s(t).arr(
-                [partition], lambda w, p: w.i32(p).i64(offset).i32(4 << 20)))
-        r = self._conn(self._metadata(topic).get(partition)).call(1, 4, bytes(body.b))
-        r.i32()  # throttle
-        res = r.arr(lambda r: (r.s(), r.arr(lambda r: (
-            r.i32(), r.i16(), r.i64(), r.i64(),
-            r.arr(lambda r: (r.i64(), r.i64())), r.by()))))
-        recs = []
-        for _t, parts in res:
-            for _p, err, _hw, _ls, _ab, rs in parts:
-                if err:
-                    raise IOError(f"kafka fetch error {err}")
-                recs.extend(decode_batches(rs or b""))
+        recs = decode_batches(self._fetch(topic, partition, offset))
         recs = [(o, v) for o, v in recs if o >= offset][:max_records]
         if not recs:
             return [], offset
         return [v for _, v in recs], recs[-1][0] + 1
+
+    @staticmethod
+    def _decode_into(data: bytes, offset: int, max_records: int, dst, cap: int):
+        import ctypes
+
+        import numpy as np
+
+        from omldm_amd.ops import native
+
+        offs = np.zeros(max(0, int(max_records)) + 1, dtype=np.int64)
+        nxt = ctypes.c_longlong(offset)
+        n = native.host().omldm_kafka_decode_into(
+            data, len(data), offset, int(max_records), native.ptr(dst), int(cap),
+            offs.ctypes.data, ctypes.byref(nxt), 1)
+        if n < 0:
+            what = {-2: "corrupt record set", -3: "codec library missing",
+                    -5: "CRC-32C mismatch"}.get(int(n), "error")
+            raise IOError(f"kafka record set decode failed: {what} ({n})")
+        return int(n), offs[:n + 1].copy(), int(nxt.value)
+
+    def consume_into(self, topic, partition, offset, max_records, dst, cap):
+        """Native path: the fetched record set is decoded (and decompressed) by
+        csrc/host/kafka_wire.cpp straight into ``dst[:cap]`` — no per-record objects."""
+        data = self._fetch(topic, partition, offset, max_bytes=max(1 << 20, int(cap)))
+        return self._decode_into(data, offset, max_records, dst, cap)
+
+    def consume_block(self, topic, partition, offset, max_records):
+        import numpy as np
+
+        data = self._fetch(topic, partition, offset)
+        cap = max(len(data) * 4, 1 << 16)  # compressed sets inflate: grow if needed
+        while True:
+            buf = np.empty(cap, dtype=np.uint8)
+            n, offs, nxt = self._decode_into(data, offset, max_records, buf, cap)
+            # done unless the first record alone did not fit (nothing taken, offset not
+            # moved past a control batch); a set that inflates > 256× is not plausible
+            if n or nxt != offset or not data or cap > 256 * len(data) + (1 << 20):
+                return buf[:int(offs[-1])].tobytes(), offs, nxt
+            cap *= 4
 
     def flush(self):
         pass

@@ -1,9 +1,13 @@
 """Protocol-level fake Kafka broker for tests (no real broker exists in this sandbox).
 
 Speaks the same request subset as omldm_amd.io.kafka (Metadata v1, ListOffsets v1,
-Produce v3, Fetch v4, CreateTopics v0) on 127.0.0.1, stores records in memory and
-re-encodes RecordBatch v2 on fetch — so the client's framing, varints and CRC-32C are
-exercised in both directions. Compatibility with a real broker is "parity unpinned".
+Produce v3/v7, Fetch v4/v10, CreateTopics v0) on 127.0.0.1, stores records in memory and
+re-encodes RecordBatch v2 on fetch with the codec the partition was last written with —
+so the client's framing, varints, CRC-32C and codecs are exercised in both directions.
+Like a real broker it refuses to serve zstd batches to Fetch < v10 (error 76,
+UNSUPPORTED_COMPRESSION_TYPE). ``control_every`` > 0 appends a transactional control
+batch after every that many records. Compatibility with a real broker is "parity
+unpinned".
 """
 from __future__ import annotations
 
@@ -16,8 +20,11 @@ from omldm_amd.io.kafka import R, W, decode_batches, encode_batch
 
 
 class FakeKafka:
-    def __init__(self, default_partitions: int = 4):
+    def __init__(self, default_partitions: int = 4, control_every: int = 0):
         self.logs = defaultdict(list)      # (topic, p) -> [bytes]
+        self.codec = defaultdict(int)      # (topic, p) -> codec of the last produce
+        self.control_every = control_every
+        self.fetch_versions = []
         self.nparts = {}
         self.default_partitions = default_partitions
         self.lock = threading.Lock()
@@ -85,7 +92,7 @@ class FakeKafka:
                 for name, n, *_ in reqs:
                     self.nparts[name] = max(1, n)
                 return bytes(W().arr(reqs, lambda w, q: w.s(q[0]).i16(0)).b)
-            if api == 0:  # Produce v3
+            if api == 0:  # Produce v3 / v7 (same request; v5+ answers log_start_offset)
                 r.s(), r.i16(), r.i32()
                 topics = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.by()))))
                 out = []
@@ -94,11 +101,13 @@ class FakeKafka:
                     for p, rs in parts:
                         log = self.logs[(t, p)]
                         base = len(log)
+                        self.codec[(t, p)] = struct.unpack_from(">h", rs, 21)[0] & 7
                         log.extend(v for _, v in decode_batches(rs))
                         po.append((p, base))
                     out.append((t, po))
                 w = W().arr(out, lambda w, tp: w.s(tp[0]).arr(
-                    tp[1], lambda w, pb: w.i32(pb[0]).i16(0).i64(pb[1]).i64(-1))).i32(0)
+                    tp[1], lambda w, pb: (w.i32(pb[0]).i16(0).i64(pb[1]).i64(-1),
+                                          w.i64(0) if ver >= 5 else None))).i32(0)
                 return bytes(w.b)
             if api == 2:  # ListOffsets v1
                 r.i32()
@@ -107,19 +116,46 @@ class FakeKafka:
                     tp[1], lambda w, pt: w.i32(pt[0]).i16(0).i64(-1).i64(
                         len(self.logs[(tp[0], pt[0])]) if pt[1] == -1 else 0)))
                 return bytes(w.b)
-            if api == 1:  # Fetch v4
+            if api == 1:  # Fetch v4 / v10
+                self.fetch_versions.append(ver)
                 r.i32(), r.i32(), r.i32(), r.i32(), r.i8()
-                topics = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.i64(), r.i32()))))
+                if ver >= 7:
+                    r.i32(), r.i32()  # session id / epoch
+                topics = r.arr(lambda r: (r.s(), r.arr(lambda r: (
+                    r.i32(), r.i32() if ver >= 9 else None, r.i64(),
+                    r.i64() if ver >= 5 else None, r.i32()))))
                 w = W().i32(0)
+                if ver >= 7:
+                    w.i16(0).i32(0)
 
                 def part(w, pt, t):
-                    p, off, _mx = pt
+                    p, _epoch, off, _lso, _mx = pt
                     log = self.logs[(t, p)]
-                    vals = log[off:off + 500]
-                    rs = encode_batch(vals, base_offset=off) if vals else b""
-                    w.i32(p).i16(0).i64(len(log)).i64(len(log)).i32(0).by(rs)
+                    codec = self.codec[(t, p)]
+                    err = 76 if codec == 4 and ver < 10 else 0
+                    rs = b"" if err else self._record_set(log, off, codec)
+                    w.i32(p).i16(err).i64(len(log)).i64(len(log))
+                    if ver >= 5:
+                        w.i64(0)
+                    w.i32(0).by(rs)
 
                 w.arr(topics, lambda w, tp: w.s(tp[0]).arr(tp[1], lambda w, pt: part(w, pt,
                                                                                      tp[0])))
                 return bytes(w.b)
         raise ValueError(f"unsupported api {api}")
+
+    def _record_set(self, log, off, codec) -> bytes:
+        """Batches of ≤ 200 records from ``off`` (≤ 500 records). With ``control_every`` a
+        control batch follows each data batch; a real log gives the marker its own offset,
+        this log has none to give, so the marker reuses the batch's last offset."""
+        out, o, end = b"", off, min(len(log), off + 500)
+        while o < end:
+            n = min(200, end - o)
+            if self.control_every:
+                n = min(n, self.control_every)
+            out += encode_batch(log[o:o + n], base_offset=o, compression=codec)
+            if self.control_every:
+                out += encode_batch([b"\x00\x00\x00\x00"], base_offset=o + n - 1,
+                                    control=True)
+            o += n
+        return out

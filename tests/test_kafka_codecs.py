@@ -1,0 +1,178 @@
+"""Kafka compression codecs and the native record-set decoder (csrc/host/kafka_wire.cpp).
+
+Each codec is checked against frames built by hand from its public format description
+(so the decoders are not only tested against their own encoders): a raw and an
+xerial-framed snappy stream, an LZ4 frame with an uncompressed block (header checksum by
+the independent ``xxhash`` package), a zstd frame with a raw block, and gzip against
+Python's ``gzip`` module in both directions. Then RecordBatch v2 with every codec through
+the Python decoder and the native one, and the client against the fake broker (including
+the Fetch v10 fallback that zstd topics need and transactional control batches).
+"""
+import gzip
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from omldm_amd.io import kafka as K
+from omldm_amd.io.transport import Consumer
+from tests.fake_kafka import FakeKafka
+
+CODECS = ["gzip", "snappy", "lz4", "zstd"]
+
+
+def _payloads():
+    rnd = os.urandom(3000)
+    text = b"".join(json.dumps({"numericalFeatures": [i * 0.5, i % 7],
+                                "categoricalFeatures": [f"c{i % 13}"],
+                                "target": 1.0, "operation": "training"}).encode() + b"\n"
+                    for i in range(4000))
+    return [b"", b"a", rnd, text, rnd + text + rnd]
+
+
+@pytest.mark.parametrize("codec", CODECS)
+def test_codec_roundtrip(codec):
+    for d in _payloads():
+        z = K.compress(codec, d)
+        assert K.decompress(codec, z) == d
+    text = _payloads()[3]
+    assert len(K.compress(codec, text)) < len(text) // 4  # it does compress
+
+
+def test_snappy_hand_built_streams():
+    # raw: len 11 | literal "abcd" | copy (1-byte offset form) len 7 offset 4 (overlapping)
+    raw1 = bytes([11, 3 << 2]) + b"abcd" + bytes([(3 << 2) | 1, 4])
+    assert K.decompress("snappy", raw1) == b"abcdabcdabc"
+    # raw: len 8 | literal "xy" | copy (2-byte offset form) len 6 offset 2
+    raw2 = bytes([8, 1 << 2]) + b"xy" + bytes([((6 - 1) << 2) | 2, 2, 0])
+    assert K.decompress("snappy", raw2) == b"xyxyxyxy"
+    # long literal: tag 60 → one length byte follows (len − 1)
+    lit = bytes(range(100))
+    raw3 = bytes([100, 60 << 2, 99]) + lit
+    assert K.decompress("snappy", raw3) == lit
+    # xerial framing (what the Java client writes): magic, version 1, compat 1, blocks
+    xer = b"\x82SNAPPY\x00" + struct.pack(">ii", 1, 1)
+    for blk in (raw1, raw2):
+        xer += struct.pack(">i", len(blk)) + blk
+    assert K.decompress("snappy", xer) == b"abcdabcdabc" + b"xyxyxyxy"
+    # our encoder writes that framing
+    assert K.compress("snappy", b"hello").startswith(b"\x82SNAPPY\x00")
+    with pytest.raises(ValueError):
+        K.decompress("snappy", bytes([20, 3 << 2]) + b"ab")  # truncated literal
+
+
+def test_lz4_hand_built_frame():
+    xxhash = pytest.importorskip("xxhash")
+    data = b"online learning on MI355X " * 20
+    flg, bd = 0x60, 0x40  # version 01, independent blocks; max block 64 KiB
+    hc = (xxhash.xxh32(bytes([flg, bd]), seed=0).intdigest() >> 8) & 0xFF
+    frame = struct.pack("<I", 0x184D2204) + bytes([flg, bd, hc])
+    frame += struct.pack("<I", len(data) | 0x80000000) + data  # uncompressed block
+    frame += struct.pack("<I", 0)  # end mark
+    assert K.decompress("lz4", frame) == data
+    with pytest.raises(ValueError):
+        K.decompress("lz4", frame[:-6])  # truncated
+
+
+def test_zstd_hand_built_frame():
+    data = b"spoke hub round " * 10  # 160 bytes
+    fhd = 0x20  # single segment, 1-byte frame content size, no checksum, no dictionary
+    block = (1 | (0 << 1) | (len(data) << 3)).to_bytes(3, "little")  # last, raw, size
+    frame = struct.pack("<I", 0xFD2FB528) + bytes([fhd, len(data)]) + block + data
+    assert K.decompress("zstd", frame) == data
+    with pytest.raises(ValueError):
+        K.decompress("zstd", frame[:-10])
+
+
+def test_gzip_interop_with_python_gzip():
+    d = _payloads()[4]
+    assert gzip.decompress(K.compress("gzip", d)) == d
+    assert K.decompress("gzip", gzip.compress(d)) == d
+    assert K.decompress("gzip", gzip.compress(d[:100]) + gzip.compress(d[100:])) == d  # members
+
+
+def _native_decode(data, offset, max_records=10**6, cap=1 << 24):
+    dst = np.empty(cap, dtype=np.uint8)
+    n, offs, nxt = K.KafkaBroker._decode_into(data, offset, max_records, dst, cap)
+    return [dst[offs[i]:offs[i + 1]].tobytes() for i in range(n)], nxt
+
+
+@pytest.mark.parametrize("codec", ["none"] + CODECS)
+def test_record_batches_python_and_native_agree(codec):
+    vals = [json.dumps({"i": i, "pad": "x" * (i % 37)}).encode() for i in range(700)]
+    data = (K.encode_batch(vals[:300], base_offset=1000, compression=codec)
+            + K.encode_batch([b"\0\0\0\0"], base_offset=1299, control=True)
+            + K.encode_batch(vals[300:], base_offset=1300, compression=codec))
+    py = K.decode_batches(data)
+    assert [v for _, v in py] == vals and [o for o, _ in py] == list(range(1000, 1700))
+    got, nxt = _native_decode(data, 1000)
+    assert got == vals and nxt == 1700
+    got, nxt = _native_decode(data, 1250)  # mid-batch start: earlier records skipped
+    assert got == vals[250:] and nxt == 1700
+    got, nxt = _native_decode(data, 1000, max_records=10)
+    assert got == vals[:10] and nxt == 1010
+    cap = sum(len(v) for v in vals[:42]) + 5  # the 43rd record does not fit
+    got, nxt = _native_decode(data, 1000, cap=cap)
+    assert got == vals[:42] and nxt == 1042
+    got, nxt = _native_decode(data[:-5], 1000)  # truncated trailing batch ignored
+    assert got == vals[:300] and nxt == 1300  # stepped over the control batch too
+    bad = bytearray(data)
+    bad[60] ^= 0xFF  # inside the first batch's CRC-covered body
+    with pytest.raises(IOError, match="CRC"):
+        _native_decode(bytes(bad), 1000)
+
+
+def test_control_batch_alone_advances_the_offset():
+    data = K.encode_batch([b"\0\0\0\0"], base_offset=7, control=True)
+    assert K.decode_batches(data) == []
+    got, nxt = _native_decode(data, 7)
+    assert got == [] and nxt == 8
+
+
+@pytest.mark.parametrize("codec", CODECS)
+def test_compressed_topics_through_the_fake_broker(codec):
+    fk = FakeKafka(default_partitions=2, control_every=64)
+    try:
+        prod = K.KafkaBroker(f"{fk.addr}?compression={codec}")
+        assert prod.codec == K.CODECS[codec]
+        prod.create_topic("trainingData", 2)
+        recs = [json.dumps({"i": i}).encode() for i in range(600)]
+        prod.produce_batch("trainingData", 0, recs[:400])
+        prod.produce_batch("trainingData", 1, recs[400:])
+        cons = K.KafkaBroker(fk.addr)  # a plain consumer reads any codec
+        got, nxt = cons.consume("trainingData", 0, 0, 10**6)
+        assert got == recs[:400][:len(got)] and nxt == len(got)
+        buf = np.empty(1 << 20, dtype=np.uint8)
+        n, offs, nxt = cons.consume_into("trainingData", 1, 0, 1000, buf, len(buf))
+        assert n == 200 and nxt == 200
+        assert [buf[offs[i]:offs[i + 1]].tobytes() for i in range(n)] == recs[400:]
+        # the engine's consumer (partition share of rank 0 of 1) drains both partitions
+        c = Consumer(cons, "trainingData", rank=0, world=1)
+        seen = []
+        for _ in range(20):
+            block, offs = c.poll_block(128)
+            seen += [block[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+        assert sorted(seen) == sorted(recs)
+        # zstd needs Fetch v10: the client switches after the broker's error 76
+        assert (10 in fk.fetch_versions) == (codec == "zstd")
+    finally:
+        fk.close()
+
+
+def test_consume_block_steps_over_a_lone_control_batch():
+    class OneShot(K.KafkaBroker):
+        def __init__(self, data):
+            self.data = data
+
+        def _fetch(self, topic, partition, offset, max_bytes=4 << 20):
+            return self.data
+
+    br = OneShot(K.encode_batch([b"\0\0\0\0"], base_offset=3, control=True))
+    buf, offs, nxt = br.consume_block("t", 0, 3, 100)
+    assert buf == b"" and list(offs) == [0] and nxt == 4
+    big = b"y" * 300000  # one record larger than the first guess of the capacity
+    br = OneShot(K.encode_batch([big], base_offset=0, compression="zstd"))
+    buf, offs, nxt = br.consume_block("t", 0, 0, 100)
+    assert buf == big and nxt == 1

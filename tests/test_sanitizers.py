@@ -19,7 +19,7 @@ SRCS = sorted(glob.glob(os.path.join(ROOT, "csrc", "host", "*.cpp"))) + [
 def _build_and_run(tmp_path, flags, env_extra):
     exe = str(tmp_path / "selftest")
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-pthread", *flags,
-           "-I", os.path.join(ROOT, "csrc", "host"), *SRCS, "-o", exe]
+           "-I", os.path.join(ROOT, "csrc", "host"), *SRCS, "-o", exe, "-lz", "-ldl"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
     env = dict(os.environ, **env_extra)
