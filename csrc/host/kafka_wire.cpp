@@ -545,3 +545,74 @@ OMLDM_HOST_API int64_t omldm_kafka_decode_into(const uint8_t* data, int64_t n, i
   }
   return cnt;
 }
+
+namespace {
+void put_varint(std::vector<uint8_t>& o, int64_t v) {
+  uint64_t u = (uint64_t(v) << 1) ^ uint64_t(v >> 63);  // zig-zag
+  while (u >= 0x80) {
+    o.push_back(uint8_t(u | 0x80));
+    u >>= 7;
+  }
+  o.push_back(uint8_t(u));
+}
+void put_be(std::vector<uint8_t>& o, uint64_t v, int bytes) {
+  for (int k = bytes - 1; k >= 0; --k) o.push_back(uint8_t(v >> (8 * k)));
+}
+}  // namespace
+
+// One RecordBatch v2 holding records block[offs[i] : offs[i+1]] (i < n; a trailing '\n'
+// dropped when strip_nl) — the egress side: a tick's Prediction / response lines become
+// one batch per Produce request without a Python object per record. Same layout as
+// omldm_amd.io.kafka.encode_batch (null keys, no headers, one timestamp). *out is
+// malloc'ed (omldm_codec_free). Returns 0 or a negative error.
+OMLDM_HOST_API int omldm_kafka_encode_lines(const uint8_t* block, const int64_t* offs, int64_t n,
+                                            int strip_nl, int64_t base_offset, int64_t ts_ms,
+                                            int codec, int level, uint8_t** out,
+                                            int64_t* out_n) {
+  if (n <= 0) return kCorrupt;
+  std::vector<uint8_t> recs, body;
+  recs.reserve(size_t(offs[n] - offs[0]) + size_t(n) * 8);
+  for (int64_t i = 0; i < n; ++i) {
+    int64_t a = offs[i], b = offs[i + 1];
+    if (strip_nl && b > a && block[b - 1] == '\n') --b;
+    const int64_t vl = b - a;
+    std::vector<uint8_t> hdr;  // attributes, ts delta, offset delta, key (null)
+    hdr.push_back(0);
+    put_varint(hdr, 0);
+    put_varint(hdr, i);
+    put_varint(hdr, -1);
+    std::vector<uint8_t> vlen;
+    put_varint(vlen, vl);
+    put_varint(recs, int64_t(hdr.size() + vlen.size()) + vl + 1);  // + 1: header count
+    recs.insert(recs.end(), hdr.begin(), hdr.end());
+    recs.insert(recs.end(), vlen.begin(), vlen.end());
+    recs.insert(recs.end(), block + a, block + b);
+    recs.push_back(0);  // no headers
+  }
+  const int c = codec & 7;
+  put_be(body, uint64_t(c), 2);                          // attributes
+  put_be(body, uint64_t(n - 1), 4);                      // last offset delta
+  put_be(body, uint64_t(ts_ms), 8);                      // first timestamp
+  put_be(body, uint64_t(ts_ms), 8);                      // max timestamp
+  put_be(body, uint64_t(int64_t(-1)), 8);                // producer id
+  put_be(body, uint64_t(uint16_t(int16_t(-1))), 2);      // producer epoch
+  put_be(body, uint64_t(uint32_t(int32_t(-1))), 4);      // base sequence
+  put_be(body, uint64_t(n), 4);                          // record count
+  if (c) {
+    std::vector<uint8_t> z;
+    const int rc = compress(c, recs.data(), recs.size(), level, z);
+    if (rc) return rc;
+    body.insert(body.end(), z.begin(), z.end());
+  } else {
+    body.insert(body.end(), recs.begin(), recs.end());
+  }
+  std::vector<uint8_t> o;
+  o.reserve(body.size() + 21);
+  put_be(o, uint64_t(base_offset), 8);
+  put_be(o, uint64_t(4 + 1 + 4 + body.size()), 4);  // batch length (after this field)
+  put_be(o, 0, 4);                                  // partition leader epoch
+  o.push_back(2);                                   // magic
+  put_be(o, omldm_crc32c(body.data(), int64_t(body.size()), 0), 4);
+  o.insert(o.end(), body.begin(), body.end());
+  return hand_out(o, out, out_n);
+}

@@ -42,6 +42,9 @@ void omldm_codec_free(void* p);
 int64_t omldm_kafka_decode_into(const uint8_t* data, int64_t n, int64_t min_offset,
                                 int64_t max_records, uint8_t* dst, int64_t cap, int64_t* offs,
                                 int64_t* next_offset, int verify_crc);
+int omldm_kafka_encode_lines(const uint8_t* block, const int64_t* offs, int64_t n, int strip_nl,
+                             int64_t base_offset, int64_t ts_ms, int codec, int level,
+                             uint8_t** out, int64_t* out_n);
 }
 
 static int failures = 0;
@@ -185,6 +188,28 @@ static void test_kafka_wire() {
       uint8_t* d = nullptr;
       int64_t dn = 0;
       if (omldm_codec_decompress(codec, b.data(), (int64_t)cut, &d, &dn) == 0) omldm_codec_free(d);
+    }
+  }
+  {  // encode a block of lines with every codec, decode it back into a staging buffer
+    std::string blk;
+    std::vector<int64_t> lo{0};
+    for (int i = 0; i < 300; ++i) {
+      blk += "{\"i\": " + std::to_string(i) + "}\n";
+      lo.push_back((int64_t)blk.size());
+    }
+    for (int codec = 0; codec <= 4; ++codec) {
+      if (!omldm_codec_available(codec)) continue;
+      uint8_t* rs = nullptr;
+      int64_t rn = 0;
+      CHECK(omldm_kafka_encode_lines(reinterpret_cast<const uint8_t*>(blk.data()), lo.data(), 300,
+                                     1, 40, 1, codec, -1, &rs, &rn) == 0);
+      std::vector<uint8_t> dst2(blk.size());
+      std::vector<int64_t> o2(301);
+      int64_t nxt = 0;
+      CHECK(omldm_kafka_decode_into(rs, rn, 40, 300, dst2.data(), (int64_t)dst2.size(), o2.data(),
+                                    &nxt, 1) == 300);
+      CHECK(nxt == 340 && o2[300] == (int64_t)blk.size() - 300);
+      omldm_codec_free(rs);
     }
   }
   std::vector<uint8_t> junk(4096), dst(1 << 16);

@@ -207,6 +207,31 @@ def codec_available(codec) -> bool:
     return bool(native.host().omldm_codec_available(codec_id(codec)))
 
 
+def encode_lines(buf, offs, compression=0, base_offset: int = 0, ts_ms: int | None = None,
+                 strip_nl: bool = True) -> bytes:
+    """Native encode_batch of the records buf[offs[i]:offs[i+1]] (trailing newlines dropped)."""
+    import ctypes
+
+    import numpy as np
+
+    from omldm_amd.ops import native
+
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    ts = int(time.time() * 1000) if ts_ms is None else ts_ms
+    lib = native.host()
+    out, n = ctypes.c_void_p(), ctypes.c_longlong()
+    rc = lib.omldm_kafka_encode_lines(buf.ctypes.data, offs.ctypes.data, len(offs) - 1,
+                                      int(strip_nl), base_offset, ts, codec_id(compression), -1,
+                                      ctypes.byref(out), ctypes.byref(n))
+    if rc:
+        raise ValueError(f"kafka batch encode failed ({rc})")
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        lib.omldm_codec_free(out)
+
+
 def encode_batch(values: list[bytes], base_offset: int = 0, ts_ms: int | None = None,
                  keys: list | None = None, compression=0, control: bool = False) -> bytes:
     """RecordBatch v2 of ``values``; ``compression`` (name or id) compresses the records
@@ -375,7 +400,9 @@ class KafkaBroker(Broker):
         self.produce_batch(topic, partition, [value])
 
     def produce_batch(self, topic: str, partition: int, values: list[bytes]) -> int:
-        rs = encode_batch(values, compression=self.codec)
+        return self._produce_raw(topic, partition, encode_batch(values, compression=self.codec))
+
+    def _produce_raw(self, topic: str, partition: int, rs: bytes) -> int:
         body = W().s(None).i16(1).i32(int(self.timeout * 1000)).arr(
             [topic], lambda w, t: w.s(t).arr([partition], lambda w, p: w.i32(p).by(rs)))
         leader = self._metadata(topic).get(partition)
@@ -387,6 +414,31 @@ class KafkaBroker(Broker):
         if err:
             raise IOError(f"kafka produce error {err}")
         return res[0][1][0][2]
+
+    max_batch_bytes = 900 << 10  # under the brokers' default message.max.bytes (1 MiB)
+
+    def produce_lines(self, topic, block, offs, partition=None):
+        """A tick's newline-terminated output records as RecordBatches built natively
+        (csrc/host/kafka_wire.cpp), ≤ ``max_batch_bytes`` each, one Produce per batch
+        (Produce v3+ takes exactly one batch per partition)."""
+        import numpy as np
+
+        n = len(offs) - 1
+        if n <= 0:
+            return
+        if partition is None:
+            nparts = self.partitions(topic)
+            partition = self._rr.get(topic, 0) % nparts
+            self._rr[topic] = partition + 1
+        buf = np.frombuffer(block, dtype=np.uint8) if isinstance(block, (bytes, bytearray)) \
+            else np.ascontiguousarray(block).view(np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        i = 0
+        while i < n:
+            j = int(np.searchsorted(offs, offs[i] + self.max_batch_bytes, side="right")) - 1
+            j = min(n, max(j, i + 1))
+            self._produce_raw(topic, partition, encode_lines(buf, offs[i:j + 1], self.codec))
+            i = j
 
     def _list_offset(self, topic: str, partition: int, ts: int) -> int:
         body = W().i32(-1).arr([topic], lambda w, t: w.s(t).arr(

@@ -116,6 +116,7 @@ HOST_SIGS = [
     ("omldm_codec_compress", i32, [i32, C.c_char_p, i64, i32, vp, vp]),
     ("omldm_codec_free", None, [vp]),
     ("omldm_kafka_decode_into", i64, [C.c_char_p, i64, i64, i64, vp, i64, vp, vp, i32]),
+    ("omldm_kafka_encode_lines", i32, [vp, vp, i64, i32, i64, i64, i32, i32, vp, vp]),
     ("omldm_cpu_multiclass_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, i32, i32,
                                          f32, i32, vp, vp]),
     ("omldm_cpu_linear_predict", None, [vp, i64, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp,

@@ -176,3 +176,37 @@ def test_consume_block_steps_over_a_lone_control_batch():
     br = OneShot(K.encode_batch([big], base_offset=0, compression="zstd"))
     buf, offs, nxt = br.consume_block("t", 0, 0, 100)
     assert buf == big and nxt == 1
+
+
+@pytest.mark.parametrize("codec", ["none"] + CODECS)
+def test_native_batch_encoder_matches_python(codec):
+    vals = [json.dumps({"mlpId": 1, "prediction": i * 0.25}).encode() for i in range(257)] + [b""]
+    block = b"".join(v + b"\n" for v in vals)
+    offs = np.zeros(len(vals) + 1, dtype=np.int64)
+    np.cumsum([len(v) + 1 for v in vals], out=offs[1:])
+    nat = K.encode_lines(np.frombuffer(block, dtype=np.uint8), offs, codec, base_offset=9,
+                         ts_ms=777)
+    ref = K.encode_batch(vals, base_offset=9, ts_ms=777, compression=codec)
+    if codec == "none":
+        assert nat == ref  # byte-identical framing, varints and CRC
+    assert K.decode_batches(nat) == K.decode_batches(ref)
+    assert [v for _, v in K.decode_batches(nat)] == vals
+
+
+@pytest.mark.parametrize("codec", ["none", "lz4"])
+def test_produce_lines_batches_a_tick_block(codec):
+    fk = FakeKafka(default_partitions=3)
+    try:
+        br = K.KafkaBroker(fk.addr, compression=codec)
+        br.max_batch_bytes = 1000  # force several batches (one Produce each)
+        br.create_topic("predictions", 3)
+        vals = [json.dumps({"mlpId": 2, "prediction": -1.0, "i": i}).encode() for i in range(500)]
+        block = b"".join(v + b"\n" for v in vals)
+        offs = np.zeros(len(vals) + 1, dtype=np.int64)
+        np.cumsum([len(v) + 1 for v in vals], out=offs[1:])
+        br.produce_lines("predictions", block, offs)
+        br.produce_lines("predictions", block, offs, partition=2)
+        assert fk.logs[("predictions", 0)] == vals
+        assert fk.logs[("predictions", 2)] == vals
+    finally:
+        fk.close()
