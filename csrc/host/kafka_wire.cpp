@@ -140,7 +140,11 @@ int snappy_raw_decompress(const uint8_t* p, size_t n, std::vector<uint8_t>& out)
         i += 4;
     }
     if (off == 0 || off > w || w + ln > len) return kCorrupt;
-    for (size_t k = 0; k < ln; ++k) o[w + k] = o[w + k - off];  // copies may overlap
+    if (off >= ln) {
+      std::memcpy(o + w, o + w - off, ln);
+    } else {
+      for (size_t k = 0; k < ln; ++k) o[w + k] = o[w + k - off];  // overlapping: repeats
+    }
     w += ln;
   }
   return w == len ? kOk : kCorrupt;
@@ -572,22 +576,28 @@ OMLDM_HOST_API int omldm_kafka_encode_lines(const uint8_t* block, const int64_t*
   if (n <= 0) return kCorrupt;
   std::vector<uint8_t> recs, body;
   recs.reserve(size_t(offs[n] - offs[0]) + size_t(n) * 8);
+  auto vsize = [](int64_t v) {
+    uint64_t u = (uint64_t(v) << 1) ^ uint64_t(v >> 63);
+    int k = 1;
+    while (u >= 0x80) {
+      u >>= 7;
+      ++k;
+    }
+    return k;
+  };
   for (int64_t i = 0; i < n; ++i) {
     int64_t a = offs[i], b = offs[i + 1];
     if (strip_nl && b > a && block[b - 1] == '\n') --b;
     const int64_t vl = b - a;
-    std::vector<uint8_t> hdr;  // attributes, ts delta, offset delta, key (null)
-    hdr.push_back(0);
-    put_varint(hdr, 0);
-    put_varint(hdr, i);
-    put_varint(hdr, -1);
-    std::vector<uint8_t> vlen;
-    put_varint(vlen, vl);
-    put_varint(recs, int64_t(hdr.size() + vlen.size()) + vl + 1);  // + 1: header count
-    recs.insert(recs.end(), hdr.begin(), hdr.end());
-    recs.insert(recs.end(), vlen.begin(), vlen.end());
+    // attributes, ts delta 0, offset delta i, null key, value length, value, 0 headers
+    put_varint(recs, 1 + 1 + vsize(i) + 1 + vsize(vl) + vl + 1);
+    recs.push_back(0);
+    put_varint(recs, 0);
+    put_varint(recs, i);
+    put_varint(recs, -1);
+    put_varint(recs, vl);
     recs.insert(recs.end(), block + a, block + b);
-    recs.push_back(0);  // no headers
+    recs.push_back(0);
   }
   const int c = codec & 7;
   put_be(body, uint64_t(c), 2);                          // attributes
