@@ -357,11 +357,20 @@ class KafkaBroker(Broker):
         self._brokers: dict = {}  # node -> (host, port)
         self._rr: dict = {}
 
+    # partitions may be fetched concurrently (engine.ingest.TickIngest reads every owned
+    # partition on its own thread): each thread talks over its own connections, and the
+    # native decode runs outside the GIL
+    parallel_reads = True
+
+    def _addr(self, node=None):
+        return self._brokers.get(node, self.bootstrap[0]) if node is not None else self.bootstrap[0]
+
     def _conn(self, node=None) -> _Conn:
-        addr = self._brokers.get(node, self.bootstrap[0]) if node is not None else self.bootstrap[0]
-        if addr not in self._conns:
-            self._conns[addr] = _Conn(addr[0], addr[1], self.timeout)
-        return self._conns[addr]
+        key = (self._addr(node), threading.get_ident())
+        c = self._conns.get(key)
+        if c is None:
+            c = self._conns[key] = _Conn(key[0][0], key[0][1], self.timeout)
+        return c
 
     def _metadata(self, topic: str, refresh: bool = False) -> dict:
         if topic in self._meta and not refresh:
@@ -455,8 +464,9 @@ class KafkaBroker(Broker):
         answered UNSUPPORTED_COMPRESSION_TYPE, i.e. zstd data)."""
         leader = self._metadata(topic).get(partition)
         conn = self._conn(leader)
+        addr = self._addr(leader)
         for _ in range(2):
-            v10 = id(conn) in self._fetch_v10
+            v10 = addr in self._fetch_v10
             w = W().i32(-1).i32(100).i32(1).i32(max(8 << 20, max_bytes)).i8(0)
             if v10:
                 w.i32(0).i32(-1)  # no fetch session
@@ -481,7 +491,7 @@ class KafkaBroker(Broker):
                     err = err or part[1]
                     out += part[-1] or b""
             if err == UNSUPPORTED_COMPRESSION_TYPE and not v10:
-                self._fetch_v10.add(id(conn))
+                self._fetch_v10.add(addr)
                 continue
             if err:
                 raise IOError(f"kafka fetch error {err}")
@@ -538,6 +548,6 @@ class KafkaBroker(Broker):
         pass
 
     def close(self):
-        for c in self._conns.values():
+        for c in list(self._conns.values()):
             c.close()
         self._conns.clear()

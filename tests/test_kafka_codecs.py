@@ -210,3 +210,30 @@ def test_produce_lines_batches_a_tick_block(codec):
         assert fk.logs[("predictions", 2)] == vals
     finally:
         fk.close()
+
+
+def test_partitions_fetched_concurrently_on_own_connections():
+    import concurrent.futures as cf
+
+    fk = FakeKafka(default_partitions=4)
+    try:
+        br = K.KafkaBroker(f"{fk.addr}?compression=zstd")
+        br.create_topic("trainingData", 4)
+        recs = {p: [json.dumps({"p": p, "i": i}).encode() for i in range(300)] for p in range(4)}
+        for p in range(4):
+            br.produce_batch("trainingData", p, recs[p])
+        assert br.parallel_reads
+        bufs = [np.empty(1 << 20, dtype=np.uint8) for _ in range(4)]
+
+        def read(p):
+            n, offs, nxt = br.consume_into("trainingData", p, 0, 1000, bufs[p], 1 << 20)
+            return [bufs[p][offs[i]:offs[i + 1]].tobytes() for i in range(n)], nxt
+
+        with cf.ThreadPoolExecutor(4) as ex:
+            out = list(ex.map(read, range(4)))
+        for p in range(4):
+            assert out[p] == (recs[p], 300)
+        assert len(br._conns) >= 2  # one connection per reading thread
+        br.close()
+    finally:
+        fk.close()
