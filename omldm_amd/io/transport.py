@@ -173,9 +173,10 @@ class FileBroker(Broker):
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 
-    def consume_into(self, topic, partition, offset, max_records, dst, cap):
+    def consume_into(self, topic, partition, offset, max_records, dst, cap, hint=0):
         """pread of the log straight into ``dst`` + memchr record index, without the GIL
-        (csrc/host/logio.cpp: omldm_read_log)."""
+        (csrc/host/logio.cpp: omldm_read_log). ``hint``: bytes the records are expected
+        to take (the first read's size; more is read only if needed, up to ``cap``)."""
         from omldm_amd.ops import native
 
         path = os.path.join(self.root, topic, f"{partition}.jsonl")
@@ -185,7 +186,8 @@ class FileBroker(Broker):
             return 0, offs[:1], offset
         used = np.zeros(1, dtype=np.int64)
         n = native.host().omldm_read_log(self._fd(path), offset, dst.ctypes.data, int(cap),
-                                         int(max_records), offs.ctypes.data, used.ctypes.data)
+                                         int(max_records), offs.ctypes.data, used.ctypes.data,
+                                         int(hint))
         if n < 0:
             raise OSError(-n, f"reading {path}")
         return int(n), offs[:n + 1], offset + int(used[0])
@@ -355,8 +357,13 @@ class Consumer:
     def read_region(self, p: int, share: int, dst: np.ndarray) -> tuple[int, np.ndarray]:
         """Reads partition ``p`` into ``dst`` (its region); advances the offset and the
         bytes-per-record estimate. Returns (records, offsets relative to dst)."""
-        k, o, nxt = self.broker.consume_into(self.topic, p, self.offsets[p], share, dst,
-                                             len(dst))
+        if isinstance(self.broker, FileBroker):  # first read sized to the expected bytes
+            k, o, nxt = self.broker.consume_into(self.topic, p, self.offsets[p], share, dst,
+                                                 len(dst), hint=int(share * self._avg_len * 1.02)
+                                                 + 4096)
+        else:
+            k, o, nxt = self.broker.consume_into(self.topic, p, self.offsets[p], share, dst,
+                                                 len(dst))
         self.offsets[p] = nxt
         if k:
             self._avg_len = 0.8 * self._avg_len + 0.2 * (int(o[k]) / k)

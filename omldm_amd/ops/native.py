@@ -110,7 +110,7 @@ HOST_SIGS = [
     ("omldm_cpu_linear_apply", None, [vp, vp, vp, i32]),
     ("omldm_index_lines", i64, [vp, i64, i64, vp]),
     ("omldm_format_predictions", i64, [vp, vp, vp, i64, i32, vp, vp, i64, vp]),
-    ("omldm_read_log", i64, [i32, i64, vp, i64, i64, vp, vp]),
+    ("omldm_read_log", i64, [i32, i64, vp, i64, i64, vp, vp, i64]),
     ("omldm_codec_available", i32, [i32]),
     ("omldm_codec_decompress", i32, [i32, C.c_char_p, i64, vp, vp]),
     ("omldm_codec_compress", i32, [i32, C.c_char_p, i64, i32, vp, vp]),
