@@ -3,8 +3,8 @@
 // Reference: Jackson parses every record on a JVM thread (DataInstanceParser /
 // DataPointParser, omldm/utils/parsers/DataInstanceParser.scala:12-22,
 // dataStream/DataPointParser.scala:16-55), ~0.5 M records/s per core for our C++ port.
-// Here the raw JSON block (records back to back, int64 offsets) is copied to HBM once
-// and every thread parses one record: numerical ∥ discrete features, categorical tokens
+// Here the raw JSON block (records back to back, int64 offsets) is copied to HBM once,
+// each wave stages its 64 records' bytes in LDS, and every lane parses one record: numerical ∥ discrete features, categorical tokens
 // hashed with murmur3-32 (per-field seeds — bit-identical to csrc/host/ingest.cpp), target,
 // operation. Semantics match the host scanner exactly (same validity rules: "EOS",
 // malformed JSON, missing features / operation, training point without target → -1).
@@ -73,7 +73,7 @@ __device__ __forceinline__ bool jkey(const unsigned char* s, int n, const char* 
   return true;
 }
 
-__device__ bool jnum(JCur& c, double& v) {
+__device__ __forceinline__ bool jnum(JCur& c, double& v) {
   jws(c);
   const unsigned char* q = c.p;
   bool neg = false;
@@ -131,7 +131,7 @@ __device__ bool jnum(JCur& c, double& v) {
   return true;
 }
 
-__device__ bool jskip(JCur& c) {
+__device__ __forceinline__ bool jskip(JCur& c) {
   jws(c);
   if (c.p >= c.e) return c.ok = false;
   if (*c.p == '"') {
@@ -200,7 +200,7 @@ __device__ uint32_t murmur3_dev(const unsigned char* d, int len, uint32_t seed) 
 }
 
 // One record → outputs; returns op (0 training, 1 forecasting) or -1.
-__device__ int parse_record(const unsigned char* b, const unsigned char* e, int dnum, int ddisc,
+__device__ __forceinline__ int parse_record(const unsigned char* b, const unsigned char* e, int dnum, int ddisc,
                             int dc, long long dim, int cspan, float* num, int* cat32,
                             unsigned short* cat16, float* y) {
   const int dn = dnum + ddisc;
@@ -322,6 +322,66 @@ __global__ __launch_bounds__(256) void json_parse_kernel(
   }
 }
 
+// Wave-staged variant (the launch path): one wave = one block = 64 consecutive records.
+// Their bytes are contiguous in the buffer, so the wave first copies the group's byte
+// range into LDS with 16-byte loads (every lane issuing, fully coalesced) and each lane
+// then parses its record out of LDS — the scanner's ~500 dependent byte reads per record
+// become LDS latencies instead of global-memory ones. A group larger than the LDS stage
+// (a record with a huge skipped field) is parsed from global memory as before.
+constexpr int kJsonStage = 36 * 1024;  // bytes per wave: 4 waves per CU fit in LDS
+
+__global__ __launch_bounds__(64) void json_parse_staged_kernel(
+    const unsigned char* __restrict__ buf, const long long* __restrict__ offs, int n, int dnum,
+    int ddisc, int dc, long long dim, int cspan, float* __restrict__ num, void* __restrict__ cat,
+    float* __restrict__ y, signed char* __restrict__ op, int* __restrict__ counts) {
+  __shared__ uint4 stage[kJsonStage / 16];
+  const int lane = threadIdx.x;
+  const int dn = dnum + ddisc;
+  int ntrain = 0, nfcst = 0, nbad = 0;
+  const int groups = (n + 63) >> 6;
+  for (int gi = blockIdx.x; gi < groups; gi += gridDim.x) {
+    const int i0 = gi << 6, iend = min(n, i0 + 64), i = i0 + lane;
+    const long long b0 = offs[i0], b1 = offs[iend];
+    const long long a0 = b0 & ~15ll;  // 16-byte aligned start (hipMalloc bases are aligned)
+    const long long bytes = b1 - a0;
+    const bool staged = bytes <= kJsonStage;
+    if (staged) {
+      const int nfull = (int)(bytes >> 4);  // whole vectors inside [a0, b1): no over-read
+      const uint4* src = reinterpret_cast<const uint4*>(buf + a0);
+      for (int v = lane; v < nfull; v += 64) stage[v] = src[v];
+      const int tail = (int)(bytes & 15);
+      unsigned char* sb = reinterpret_cast<unsigned char*>(stage);
+      if (lane < tail) sb[(nfull << 4) + lane] = buf[a0 + (nfull << 4) + lane];
+    }
+    __syncthreads();
+    if (i < iend) {
+      const unsigned char* sb = reinterpret_cast<const unsigned char*>(stage);
+      const long long o0 = offs[i], o1 = offs[i + 1];
+      float* nr = num + (size_t)i * dn;
+      int* c32 = static_cast<int*>(cat) + (size_t)i * dc;
+      unsigned short* c16 = static_cast<unsigned short*>(cat) + (size_t)i * dc;
+      // two inlined copies: in the staged one every scanner read is provably LDS (ds_read)
+      const int r = staged ? parse_record(sb + (o0 - a0), sb + (o1 - a0), dnum, ddisc, dc, dim,
+                                          cspan, nr, c32, c16, y + i)
+                           : parse_record(buf + o0, buf + o1, dnum, ddisc, dc, dim, cspan, nr,
+                                          c32, c16, y + i);
+      op[i] = (signed char)r;
+      ntrain += r == 0;
+      nfcst += r == 1;
+      nbad += r < 0;
+    }
+    __syncthreads();  // the next group overwrites the stage
+  }
+  float a = (float)ntrain, b = (float)nfcst;
+  wave_sum2(a, b);
+  const float c = wave_sum((float)nbad);
+  if (lane == 0 && counts) {
+    if (a > 0.f) atomicAdd(counts, (int)a);
+    if (b > 0.f) atomicAdd(counts + 1, (int)b);
+    if (c > 0.f) atomicAdd(counts + 2, (int)c);
+  }
+}
+
 }  // namespace omldm
 
 using namespace omldm;
@@ -334,9 +394,17 @@ OMLDM_API int omldm_json_parse(const void* buf, const long long* offs, int n, in
                                void* cat, float* y, signed char* op, int* counts,
                                void* stream) {
   if (n <= 0) return 0;
-  int blocks = (n + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+  if (reinterpret_cast<uintptr_t>(buf) & 15) {  // the staged kernel needs an aligned base
+    int blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(json_parse_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned char*)buf, offs, n, dnum, ddisc, dc, dim, cspan, num, cat,
+                       y, op, counts);
+    return (int)hipGetLastError();
+  }
+  int groups = (n + 63) / 64;
+  if (groups > 8192) groups = 8192;  // grid-stride beyond 32 waves per CU
+  hipLaunchKernelGGL(json_parse_staged_kernel, dim3(groups), dim3(64), 0, (hipStream_t)stream,
                      (const unsigned char*)buf, offs, n, dnum, ddisc, dc, dim, cspan, num, cat, y,
                      op, counts);
   return (int)hipGetLastError();

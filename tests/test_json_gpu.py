@@ -42,6 +42,10 @@ def test_gpu_parser_matches_host(cuda, field_aware):
     sp = FeatureSpace(13, 2, 26, 1 << 20, field_aware=field_aware)
     recs = [r.encode() for r in synth_json_records(3000, sp, seed=9)]
     recs += ADVERSARIAL * 3
+    # a record with a huge skipped field: its 64-record group exceeds the wave's LDS stage
+    # and is parsed from global memory (the other groups from LDS)
+    recs.insert(1000, b'{"numericalFeatures":[7],"blob":"' + b"z" * 50000 + b'","target":1,'
+                b'"operation":"training"}')
     buf, offs = join_block(recs)
     hb, hop, hval = parse_block(buf, offs, sp, 4)
     gb, gop, gval = GpuJsonParser(cuda).parse(buf, offs, sp)
@@ -55,3 +59,28 @@ def test_gpu_parser_matches_host(cuda, field_aware):
     assert torch.equal(gb.cat.cpu()[ok], hb.cat[ok])
     assert torch.equal(torch.nan_to_num(gb.y.cpu()[ok], nan=-7.0),
                        torch.nan_to_num(hb.y[ok], nan=-7.0))
+
+
+@pytest.mark.gpu
+def test_gpu_parser_exact_size_buffer_and_group_edges(cuda):
+    """The staged kernel never reads past the last record (an exact-size device buffer),
+    and record counts that are not multiples of the 64-record group parse identically."""
+    from omldm_amd.ops.ingest import json_parse
+
+    sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
+    for n in (1, 63, 65, 200):
+        recs = [r.encode() for r in synth_json_records(n, sp, seed=n)]
+        buf, offs = join_block(recs)
+        hb, hop, _ = parse_block(buf, offs, sp, 2)
+        d = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(cuda)  # exact size
+        o = torch.from_numpy(offs).to(cuda)
+        num = torch.empty((n, sp.dn), dtype=torch.float32, device=cuda)
+        cat = torch.empty((n, sp.dc), dtype=sp.cat_dtype, device=cuda)
+        y = torch.empty(n, dtype=torch.float32, device=cuda)
+        op = torch.empty(n, dtype=torch.int8, device=cuda)
+        cnt = torch.zeros(3, dtype=torch.int32, device=cuda)
+        json_parse(d, o, n, sp, num, cat, y, op, cnt, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(op.cpu().numpy(), hop)
+        ok = torch.from_numpy(hop >= 0)
+        assert torch.equal(num.cpu()[ok], hb.num[ok]) and torch.equal(cat.cpu()[ok], hb.cat[ok])
