@@ -138,6 +138,75 @@ __device__ __forceinline__ f32x16 wave_gemm32(const float* a, int ars, int acs, 
               : wave_gemm32_f32<AK, BK>(a, ars, acs, b, brs, bcs, K);
 }
 
+// 16×16 tiles (v_mfma_f32_16x16x4_f32 / v_mfma_f32_16x16x16_bf16): a 32-row mini-batch
+// against 64-wide layers then has 8–16 output tiles per GEMM instead of 2–4, so all four
+// waves of the spoke work in every phase rather than one or two. Lane l (i = l&15,
+// g = l>>4) supplies, per 16-wide k step, the 4 consecutive k = k0 + 4g + u of its A row
+// and B column (one b128 read when k is contiguous in LDS); fp32 MFMA u takes value u
+// (a permutation of the k sum), bf16 takes all four at once. acc[j] = C(4g + j, i).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+template <bool AK, bool BK>
+__device__ __forceinline__ f32x4 wave_gemm16(const float* a, int ars, int acs, const float* b,
+                                             int brs, int bcs, int K, int bf16) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float* ap = a + r * ars + 4 * g * (AK ? 1 : acs);
+  const float* bp = b + 4 * g * (BK ? 1 : brs) + r * bcs;
+  for (int k = 0; k < K; k += 16) {
+    float av[4], bv[4];
+    if constexpr (AK) {
+      const float4 x = *reinterpret_cast<const float4*>(ap + k);
+      av[0] = x.x; av[1] = x.y; av[2] = x.z; av[3] = x.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) av[u] = ap[(k + u) * acs];
+    }
+    if constexpr (BK) {
+      const float4 y = *reinterpret_cast<const float4*>(bp + k);
+      bv[0] = y.x; bv[1] = y.y; bv[2] = y.z; bv[3] = y.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bv[u] = bp[(k + u) * brs];
+    }
+    if (bf16) {
+      const bf16x4 af = {bf16_bits(av[0]), bf16_bits(av[1]), bf16_bits(av[2]), bf16_bits(av[3])};
+      const bf16x4 bfv = {bf16_bits(bv[0]), bf16_bits(bv[1]), bf16_bits(bv[2]), bf16_bits(bv[3])};
+      acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, bfv, acc, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+  }
+  return acc;
+}
+
+#ifndef OMLDM_MLP_TILE
+#define OMLDM_MLP_TILE 16  // output tile of the round/forward GEMMs: 16 or 32
+#endif
+#if OMLDM_MLP_TILE == 16
+typedef f32x4 AccT;
+constexpr int kT = 16, kQ = 4;
+__device__ __forceinline__ int trow(int q, int lane) { return 4 * (lane >> 4) + q; }
+template <bool AK, bool BK>
+__device__ __forceinline__ AccT tile_gemm(const float* a, int ars, int acs, const float* b, int brs,
+                                          int bcs, int K, int bf16) {
+  return wave_gemm16<AK, BK>(a, ars, acs, b, brs, bcs, K, bf16);
+}
+#else
+typedef f32x16 AccT;
+constexpr int kT = 32, kQ = 16;
+__device__ __forceinline__ int trow(int q, int lane) {
+  return (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+}
+template <bool AK, bool BK>
+__device__ __forceinline__ AccT tile_gemm(const float* a, int ars, int acs, const float* b, int brs,
+                                          int bcs, int K, int bf16) {
+  return wave_gemm32<AK, BK>(a, ars, acs, b, brs, bcs, K, bf16);
+}
+#endif
+
 // Activation and its derivative expressed through the activation's OUTPUT h (what the
 // forward pass keeps in LDS): relu' = [h > 0], tanh' = 1 − h², σ' = h(1 − h).
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -156,10 +225,6 @@ __device__ __forceinline__ float act_grad(float h, int act) {
     case kIdentity: return 1.f;
     default: return h > 0.f ? 1.f : 0.f;
   }
-}
-
-__device__ __forceinline__ int crow(int q, int lane) {
-  return (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
 }
 
 __device__ void load_model(const float* __restrict__ w, float* sm, const MlpDesc& g) {
@@ -183,19 +248,20 @@ __device__ void forward(float* sm, const MlpDesc& g) {
     float* Ho = sm + g.lh[l + 1];
     const float* W = sm + g.lw[l];
     const float* bs = sm + g.lb[l];
-    const int nt = g.np[l + 1] >> 5, ldo = g.ldh[l + 1];
+    const int ntc = g.np[l + 1] / kT, nt = (kMB / kT) * ntc, ldo = g.ldh[l + 1];
     const bool hidden = l + 1 < g.L;
     for (int t = wave; t < nt; t += 4) {
-      const f32x16 acc =
-          wave_gemm32<kVecA, kVecB>(H, g.ldh[l], 1, W + t * 32 * g.ldw[l], 1, g.ldw[l], g.np[l], g.bf16);
-      const int col = t * 32 + (lane & 31);
+      const int rt = t / ntc, ct = t - rt * ntc;
+      const AccT acc = tile_gemm<kVecA, kVecB>(H + rt * kT * g.ldh[l], g.ldh[l], 1,
+                                               W + ct * kT * g.ldw[l], 1, g.ldw[l], g.np[l], g.bf16);
+      const int col = ct * kT + (lane & (kT - 1));
       const float bias = bs[col];
       const bool pad = col >= g.n[l + 1];  // padding columns stay exactly zero
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
+      for (int q = 0; q < kQ; ++q) {
         float v = acc[q] + bias;
         if (hidden) v = pad ? 0.f : act_fwd(v, g.act);
-        Ho[crow(q, lane) * ldo + col] = v;
+        Ho[(rt * kT + trow(q, lane)) * ldo + col] = v;
       }
     }
     __syncthreads();
@@ -343,27 +409,30 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
       const int ldw = g.ldw[l], ldh = g.ldh[l], nin = g.np[l], nout = g.np[l + 1];
       if (l > 0) {  // dH_l = (dZ · W_l) ⊙ act'(H_l)
         float* Gn = sm + gnext;
-        for (int t = wave; t < (nin >> 5); t += 4) {
-          const f32x16 acc = wave_gemm32<kVecA, false>(Gc, g.ldg, 1, W + t * 32, ldw, 1, nout, g.bf16);
-          const int col = t * 32 + (lane & 31);
+        const int ntc = nin / kT;
+        for (int t = wave; t < (kMB / kT) * ntc; t += 4) {
+          const int rt = t / ntc, ct = t - rt * ntc;
+          const AccT acc = tile_gemm<kVecA, false>(Gc + rt * kT * g.ldg, g.ldg, 1, W + ct * kT, ldw,
+                                                   1, nout, g.bf16);
+          const int col = ct * kT + (lane & (kT - 1));
 #pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int row = crow(q, lane);
+          for (int q = 0; q < kQ; ++q) {
+            const int row = rt * kT + trow(q, lane);
             Gn[row * g.ldg + col] = acc[q] * act_grad(H[row * ldh + col], g.act);
           }
         }
       }
       __syncthreads();  // W_l fully read before it is updated
       MLP_STAMP(5);
-      const int ntc = nin >> 5, nto = nout >> 5;
+      const int ntc = nin / kT, nto = nout / kT;
       for (int t = wave; t < nto * ntc; t += 4) {
         const int to = t / ntc, tc = t - to * ntc;
-        const f32x16 acc =
-            wave_gemm32<false, false>(Gc + to * 32, 1, g.ldg, H + tc * 32, ldh, 1, kMB, g.bf16);
-        const int c = tc * 32 + (lane & 31);
+        const AccT acc =
+            tile_gemm<false, false>(Gc + to * kT, 1, g.ldg, H + tc * kT, ldh, 1, kMB, g.bf16);
+        const int c = tc * kT + (lane & (kT - 1));
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int o = to * 32 + crow(q, lane);
+        for (int q = 0; q < kQ; ++q) {
+          const int o = to * kT + trow(q, lane);
           W[o * ldw + c] -= eta * acc[q];
         }
       }
