@@ -5,13 +5,17 @@ omldm/Job.scala:42-105; omldm/utils/KafkaUtils.scala:13-18 sets bootstrap.server
 the misspelled ``group.flink_worker_id``; we track offsets ourselves and
 need no consumer group). Implemented subset, enough for produce/consume of JSON records:
 
-* Metadata v1 (api 3)   — topic → partitions + leader brokers
+* ApiVersions v0 (api 18) — on every new connection; each request below then uses the
+                          highest version both sides implement (brokers of Kafka 4.0
+                          dropped the oldest versions, KIP-896; pre-0.10 brokers that do
+                          not answer ApiVersions get the lowest versions listed)
+* Metadata v1 / v4 (api 3)   — topic → partitions + leader brokers
 * ListOffsets v1 (api 2) — earliest (-2) / latest (-1) offsets
-* Produce v3 (api 0)    — RecordBatch v2, acks=1; v7 when the batch is zstd-compressed
-* Fetch v4 (api 1)      — RecordBatch v2 decoding (magic 2; older message sets and
-                          transactional control batches skipped); v10 once the broker
+* Produce v3 / v7 (api 0)    — RecordBatch v2, acks=1 (zstd batches need v7)
+* Fetch v4 / v10 (api 1)      — RecordBatch v2 decoding (magic 2; older message sets and
+                          transactional control batches skipped); v10 also once a broker
                           answers UNSUPPORTED_COMPRESSION_TYPE (zstd topics need ≥ v10)
-* CreateTopics v0 (api 19) — best effort, for ``create_topic``
+* CreateTopics v0 / v2 (api 19) — best effort, for ``create_topic``
 * compression: gzip / snappy / lz4 / zstd batches are read transparently and any of them
   can be written (``KafkaBroker(..., compression="lz4")`` or ``host:port?compression=lz4``)
 CRC-32C of record batches is computed by the host library (csrc/host/crc32c.cpp); the
@@ -311,10 +315,39 @@ def decode_batches(data: bytes, verify: bool = True) -> list[tuple[int, bytes]]:
 
 class _Conn:
     def __init__(self, host: str, port: int, timeout: float = 10.0):
-        self.sock = socket.create_connection((host, port), timeout=timeout)
+        self.addr, self.timeout = (host, port), timeout
+        self._open()
+        self.versions = self._api_versions()  # api → (min, max); None: not answered
+
+    def _open(self):
+        self.sock = socket.create_connection(self.addr, timeout=self.timeout)
         self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self.cid = 0
         self.lock = threading.Lock()
+
+    def _api_versions(self):
+        try:
+            r = self.call(18, 0, b"")
+            err = r.i16()
+            vs = r.arr(lambda r: (r.i16(), r.i16(), r.i16()))
+            if err == 0:
+                return {k: (lo, hi) for k, lo, hi in vs}
+        except (IOError, OSError, struct.error):
+            pass
+        self.close()  # a broker without ApiVersions drops the connection: reopen
+        self._open()
+        return None
+
+    def version(self, api: int, ours: tuple) -> int:
+        """Highest of ``ours`` (ascending) the broker accepts for ``api``."""
+        if self.versions is None or api not in self.versions:
+            return ours[0]
+        lo, hi = self.versions[api]
+        ok = [v for v in ours if lo <= v <= hi]
+        if not ok:
+            raise IOError(f"kafka broker {self.addr} supports api {api} v{lo}-v{hi}; "
+                          f"this client implements {ours}")
+        return ok[-1]
 
     def call(self, api: int, ver: int, body: bytes, client: str = "omldm-amd") -> R:
         with self.lock:
@@ -375,9 +408,18 @@ class KafkaBroker(Broker):
     def _metadata(self, topic: str, refresh: bool = False) -> dict:
         if topic in self._meta and not refresh:
             return self._meta[topic]
-        r = self._conn().call(3, 1, bytes(W().arr([topic], lambda w, t: w.s(t)).b))
+        conn = self._conn()
+        ver = conn.version(3, (1, 4))
+        w = W().arr([topic], lambda w, t: w.s(t))
+        if ver >= 4:
+            w.i8(0)  # allow_auto_topic_creation: no (create_topic does that)
+        r = conn.call(3, ver, bytes(w.b))
+        if ver >= 3:
+            r.i32()  # throttle
         for node, host, port, _ in r.arr(lambda r: (r.i32(), r.s(), r.i32(), r.s())):
             self._brokers[node] = (host, port)
+        if ver >= 2:
+            r.s()  # cluster id
         r.i32()  # controller
         for err, name, _internal, parts in r.arr(lambda r: (
                 r.i16(), r.s(), r.i8(),
@@ -388,10 +430,14 @@ class KafkaBroker(Broker):
         return self._meta.get(topic, {})
 
     def create_topic(self, topic: str, partitions: int) -> None:
-        body = W().arr([topic], lambda w, t: w.s(t).i32(partitions).i16(1).i32(0).i32(0)).i32(
-            int(self.timeout * 1000))
         try:
-            self._conn().call(19, 0, bytes(body.b))
+            conn = self._conn()
+            ver = conn.version(19, (0, 2))
+            body = W().arr([topic], lambda w, t: w.s(t).i32(partitions).i16(1).i32(0).i32(0)).i32(
+                int(self.timeout * 1000))
+            if ver >= 1:
+                body.i8(0)  # validate_only
+            conn.call(19, ver, bytes(body.b))
         except (IOError, OSError):
             pass
         self._meta.pop(topic, None)
@@ -414,9 +460,11 @@ class KafkaBroker(Broker):
     def _produce_raw(self, topic: str, partition: int, rs: bytes) -> int:
         body = W().s(None).i16(1).i32(int(self.timeout * 1000)).arr(
             [topic], lambda w, t: w.s(t).arr([partition], lambda w, p: w.i32(p).by(rs)))
-        leader = self._metadata(topic).get(partition)
-        ver = 7 if self.codec == CODECS["zstd"] else 3  # brokers accept zstd from Produce v7
-        r = self._conn(leader).call(0, ver, bytes(body.b))
+        conn = self._conn(self._metadata(topic).get(partition))
+        ver = conn.version(0, (3, 7))
+        if self.codec == CODECS["zstd"] and conn.versions is None:
+            ver = 7  # brokers accept zstd from Produce v7
+        r = conn.call(0, ver, bytes(body.b))
         res = r.arr(lambda r: (r.s(), r.arr(lambda r: (
             r.i32(), r.i16(), r.i64(), r.i64(), *((r.i64(),) if ver >= 5 else ())))))
         err = res[0][1][0][1]
@@ -452,7 +500,8 @@ class KafkaBroker(Broker):
     def _list_offset(self, topic: str, partition: int, ts: int) -> int:
         body = W().i32(-1).arr([topic], lambda w, t: w.s(t).arr(
             [partition], lambda w, p: w.i32(p).i64(ts)))
-        r = self._conn(self._metadata(topic).get(partition)).call(2, 1, bytes(body.b))
+        conn = self._conn(self._metadata(topic).get(partition))
+        r = conn.call(2, conn.version(2, (1,)), bytes(body.b))
         res = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.i16(), r.i64(), r.i64()))))
         return int(res[0][1][0][3])
 
@@ -465,8 +514,9 @@ class KafkaBroker(Broker):
         leader = self._metadata(topic).get(partition)
         conn = self._conn(leader)
         addr = self._addr(leader)
+        best = conn.version(1, (4, 10))
         for _ in range(2):
-            v10 = addr in self._fetch_v10
+            v10 = best >= 10 or addr in self._fetch_v10
             w = W().i32(-1).i32(100).i32(1).i32(max(8 << 20, max_bytes)).i8(0)
             if v10:
                 w.i32(0).i32(-1)  # no fetch session

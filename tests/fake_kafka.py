@@ -1,7 +1,7 @@
 """Protocol-level fake Kafka broker for tests (no real broker exists in this sandbox).
 
-Speaks the same request subset as omldm_amd.io.kafka (Metadata v1, ListOffsets v1,
-Produce v3/v7, Fetch v4/v10, CreateTopics v0) on 127.0.0.1, stores records in memory and
+Speaks the same request subset as omldm_amd.io.kafka (ApiVersions v0, Metadata v1/v4,
+ListOffsets v1, Produce v3/v7, Fetch v4/v10, CreateTopics v0/v2) on 127.0.0.1, stores records in memory and
 re-encodes RecordBatch v2 on fetch with the codec the partition was last written with —
 so the client's framing, varints, CRC-32C and codecs are exercised in both directions.
 Like a real broker it refuses to serve zstd batches to Fetch < v10 (error 76,
@@ -20,7 +20,18 @@ from omldm_amd.io.kafka import R, W, decode_batches, encode_batch
 
 
 class FakeKafka:
-    def __init__(self, default_partitions: int = 4, control_every: int = 0):
+    # ApiVersions answers: "classic" (every version this client implements), "modern"
+    # (Kafka 4.0 ranges after KIP-896 removed the oldest versions) or "legacy" (a
+    # pre-0.10 broker: ApiVersions unknown, the connection is dropped)
+    VERSIONS = {
+        "classic": {18: (0, 2), 3: (0, 8), 0: (0, 8), 1: (0, 11), 2: (0, 5), 19: (0, 4)},
+        "modern": {18: (0, 4), 3: (4, 12), 0: (3, 11), 1: (4, 17), 2: (1, 9), 19: (2, 7)},
+    }
+
+    def __init__(self, default_partitions: int = 4, control_every: int = 0,
+                 versions: str = "classic"):
+        self.versions = versions
+        self.calls = []                    # (api, version) of every request
         self.logs = defaultdict(list)      # (topic, p) -> [bytes]
         self.codec = defaultdict(int)      # (topic, p) -> codec of the last produce
         self.control_every = control_every
@@ -42,6 +53,8 @@ class FakeKafka:
                     api, ver, cid = req.i16(), req.i16(), req.i32()
                     req.s()
                     body = outer.dispatch(api, ver, req)
+                    if body is None:  # unknown request: drop the connection
+                        return
                     msg = struct.pack(">i", cid) + body
                     s.sendall(struct.pack(">i", len(msg)) + msg)
 
@@ -76,22 +89,41 @@ class FakeKafka:
 
     def dispatch(self, api, ver, r: R) -> bytes:
         with self.lock:
-            if api == 3:  # Metadata v1
+            self.calls.append((api, ver))
+            table = self.VERSIONS.get(self.versions)
+            if api == 18:  # ApiVersions v0
+                if table is None:
+                    return None
+                return bytes(W().i16(0).arr(sorted(table.items()), lambda w, kv: w.i16(kv[0]).i16(
+                    kv[1][0]).i16(kv[1][1])).b)
+            if table is not None and api in table and not (table[api][0] <= ver <= table[api][1]):
+                raise ValueError(f"api {api} v{ver} outside the advertised range {table[api]}")
+            if api == 3:  # Metadata v1 / v4
                 topics = r.arr(lambda r: r.s())
-                w = W().arr([(0, "127.0.0.1", self.port)],
-                            lambda w, b: w.i32(b[0]).s(b[1]).i32(b[2]).s(None)).i32(0)
+                w = W()
+                if ver >= 3:
+                    w.i32(0)  # throttle
+                w.arr([(0, "127.0.0.1", self.port)],
+                      lambda w, b: w.i32(b[0]).s(b[1]).i32(b[2]).s(None))
+                if ver >= 2:
+                    w.s("fake-cluster")
+                w.i32(0)
                 w.arr(topics, lambda w, t: w.i16(0).s(t).i8(0).arr(
                     list(range(self._parts(t))),
                     lambda w, p: w.i16(0).i32(p).i32(0).arr([0], lambda w, x: w.i32(x)).arr(
                         [0], lambda w, x: w.i32(x))))
                 return bytes(w.b)
-            if api == 19:  # CreateTopics v0
+            if api == 19:  # CreateTopics v0 / v2
                 reqs = r.arr(lambda r: (r.s(), r.i32(), r.i16(),
                                         r.arr(lambda r: (r.i32(), r.arr(lambda r: r.i32()))),
                                         r.arr(lambda r: (r.s(), r.s()))))
                 for name, n, *_ in reqs:
                     self.nparts[name] = max(1, n)
-                return bytes(W().arr(reqs, lambda w, q: w.s(q[0]).i16(0)).b)
+                w = W()
+                if ver >= 2:
+                    w.i32(0)  # throttle
+                w.arr(reqs, lambda w, q: (w.s(q[0]).i16(0), w.s(None) if ver >= 1 else None))
+                return bytes(w.b)
             if api == 0:  # Produce v3 / v7 (same request; v5+ answers log_start_offset)
                 r.s(), r.i16(), r.i32()
                 topics = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.by()))))

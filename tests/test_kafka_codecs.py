@@ -133,7 +133,9 @@ def test_control_batch_alone_advances_the_offset():
 
 @pytest.mark.parametrize("codec", CODECS)
 def test_compressed_topics_through_the_fake_broker(codec):
-    fk = FakeKafka(default_partitions=2, control_every=64)
+    # a broker without ApiVersions: the client starts at Fetch v4 and must switch to v10
+    # when the broker refuses zstd batches to older fetches
+    fk = FakeKafka(default_partitions=2, control_every=64, versions="legacy")
     try:
         prod = K.KafkaBroker(f"{fk.addr}?compression={codec}")
         assert prod.codec == K.CODECS[codec]
@@ -234,6 +236,31 @@ def test_partitions_fetched_concurrently_on_own_connections():
         for p in range(4):
             assert out[p] == (recs[p], 300)
         assert len(br._conns) >= 2  # one connection per reading thread
+        br.close()
+    finally:
+        fk.close()
+
+
+@pytest.mark.parametrize("versions,expect", [
+    ("classic", {3: 4, 0: 7, 1: 10, 2: 1, 19: 2}),
+    ("modern", {3: 4, 0: 7, 1: 10, 2: 1, 19: 2}),   # Kafka 4.0 ranges (KIP-896)
+    ("legacy", {3: 1, 0: 3, 1: 4, 2: 1, 19: 0}),    # no ApiVersions: lowest versions
+])
+def test_api_versions_negotiation(versions, expect):
+    fk = FakeKafka(default_partitions=2, versions=versions)
+    try:
+        br = K.KafkaBroker(fk.addr)
+        br.create_topic("requests", 2)
+        recs = [json.dumps({"id": i}).encode() for i in range(50)]
+        br.produce_batch("requests", 1, recs)
+        assert br.end_offset("requests", 1) == 50
+        got, nxt = br.consume("requests", 1, 0, 100)
+        assert got == recs and nxt == 50
+        used = {}
+        for api, ver in fk.calls:
+            used.setdefault(api, ver)
+        for api, ver in expect.items():
+            assert used[api] == ver, (api, used)
         br.close()
     finally:
         fk.close()
