@@ -64,9 +64,11 @@ struct Shift {
 };
 
 struct HwCrc {
-  bool ok = __builtin_cpu_supports("sse4.2");
+  bool ok = false;
   Shift s1, s2;
   HwCrc() {
+    __builtin_cpu_init();  // static initialisers may run before libgcc's CPU model is set up
+    ok = __builtin_cpu_supports("sse4.2");
     if (ok) {
       s1.build(kLane);
       s2.build(2 * kLane);
