@@ -39,9 +39,10 @@ class Preprocessor:
         if batch.B == 0:
             num = torch.zeros((0, self.out_dim(batch.dn)), dtype=torch.float32,
                               device=batch.num.device)
-            return HashedBatch(num, batch.cat, batch.y, batch.raw)
+            return HashedBatch(num, batch.cat, batch.y, batch.raw, batch.cat_span)
+        # the categorical slots pass through untouched, in their wire format (cat_span)
         return HashedBatch(self.fit_transform(batch.num.float().contiguous(), train), batch.cat,
-                           batch.y, batch.raw)
+                           batch.y, batch.raw, batch.cat_span)
 
     def state_dict(self) -> dict:
         return {}

@@ -191,3 +191,24 @@ def test_fast_number_parser_matches_python_float():
     assert n == len(recs)
     want = torch.tensor(expect, dtype=torch.float64).float()
     assert torch.equal(b.num, want)
+
+
+def test_preprocessors_keep_the_compact_categorical_wire():
+    """A preprocessor rewrites the numerical block only; the field-aware uint16 slots and
+    their cat_span must pass through (a dropped cat_span made the learner read int16
+    slots as global int32 ones)."""
+    import torch
+
+    from omldm_amd.api.batch import FeatureSpace
+    from omldm_amd.io.synthetic import synth_batch
+    from omldm_amd.models.preprocess import make_preprocessor
+
+    sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
+    b = synth_batch(sp, 64, seed=3)
+    for name in ("StandardScaler", "MinMaxScaler", "PolynomialFeatures"):
+        p = make_preprocessor(name, {}, "cpu")
+        out = p(b, train=True)
+        assert out.cat_span == b.cat_span > 0 and out.cat.dtype == torch.int16
+        assert torch.equal(out.cat, b.cat)
+        empty = p(b.select(torch.arange(0)), train=False)
+        assert empty.cat_span == b.cat_span
