@@ -1,0 +1,74 @@
+"""Configuration matrix through the whole engine (CPU, in-process broker): every reference
+learner × every preprocessor × both categorical wires (global int32 hashing and the
+field-aware uint16 slots). Each job creates the pipeline, trains, forecasts, answers a
+query, applies an Update and a Delete — the flows a reference user drives through the
+requests topic. Catches configuration-only bugs (a dropped wire flag, a learner that
+cannot take a preprocessed batch) that single-path tests miss."""
+import json
+import math
+import uuid
+
+import pytest
+
+from omldm_amd.api.batch import FeatureSpace
+from omldm_amd.api.schemas import VALID_LEARNERS, VALID_PREPROCESSORS
+from omldm_amd.engine.job import Job
+from omldm_amd.io.synthetic import synth_json_records
+from omldm_amd.io.transport import MemoryBroker
+from omldm_amd.parallel.comm import Comm
+from omldm_amd.utils.config import JobConfig
+
+HYPER = {"MultiClassPA": {"nClasses": 3}, "K-means": {"k": 3}, "HT": {"nClasses": 3},
+         "NN": {"hiddenLayers": [16]}}
+TASK = {"RegressorPA": 1, "ORR": 1, "MultiClassPA": 2, "HT": 2}  # synth_json_records task
+
+
+@pytest.mark.parametrize("field_aware", [False, True])
+@pytest.mark.parametrize("pre", [None, *VALID_PREPROCESSORS])
+@pytest.mark.parametrize("learner", VALID_LEARNERS)
+def test_learner_preprocessor_wire_matrix(learner, pre, field_aware):
+    name = uuid.uuid4().hex
+    addr = f"memory://{name}"
+    args = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        args += [f"--{k}", addr]
+    args += ["--hashDim", str(1 << 16), "--batchSize", "400", "--timeout", "200",
+             "--parallelism", "4", "--numFeatures", "5", "--catFeatures", "6",
+             "--fieldAware", str(field_aware).lower()]
+    cfg = JobConfig.from_args(args)
+    sp = FeatureSpace(5, 0, 6, 1 << 16, field_aware=field_aware)
+    br = MemoryBroker.named(name)
+    br.create_topic(cfg.trainingDataTopic, 2)
+    job = Job(cfg, Comm(), "cpu")
+    br.produce("requests", json.dumps({
+        "id": 7, "request": "Create",
+        "learner": {"name": learner, "hyperParameters": HYPER.get(learner, {})},
+        "preProcessors": [{"name": pre}] if pre else [],
+        "trainingConfiguration": {"protocol": "Synchronous"}}))
+    for r in synth_json_records(1200, sp, task=TASK.get(learner, 0)):
+        br.produce("trainingData", r)
+    for _ in range(4):
+        job.tick()
+    assert 7 in job.pipes
+    for r in synth_json_records(5, sp, start=9000, operation="forecasting",
+                                task=TASK.get(learner, 0)):
+        br.produce("forecastingData", r)
+    br.produce("requests", json.dumps({"id": 7, "request": "Query", "requestId": 11}))
+    for _ in range(3):
+        job.tick()
+    preds = [json.loads(x) for x in br.records("predictions")]
+    assert len(preds) == 5 and all(p["mlpId"] == 7 for p in preds)
+    resp = [json.loads(x) for x in br.records("responses")]
+    final = [r for r in resp if r.get("responseId") == 11 and r.get("loss") is not None]
+    assert final and final[-1]["dataFitted"] > 0
+    for k in ("loss", "score"):
+        v = final[-1].get(k)
+        assert v is None or math.isfinite(float(v)), (k, v)
+    br.produce("requests", json.dumps({"id": 7, "request": "Update",
+                                       "learner": {"name": learner,
+                                                   "hyperParameters": HYPER.get(learner, {})}}))
+    job.tick()
+    br.produce("requests", json.dumps({"id": 7, "request": "Delete"}))
+    job.tick()
+    assert 7 not in job.pipes
