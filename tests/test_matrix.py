@@ -27,6 +27,20 @@ TASK = {"RegressorPA": 1, "ORR": 1, "MultiClassPA": 2, "HT": 2}  # synth_json_re
 @pytest.mark.parametrize("pre", [None, *VALID_PREPROCESSORS])
 @pytest.mark.parametrize("learner", VALID_LEARNERS)
 def test_learner_preprocessor_wire_matrix(learner, pre, field_aware):
+    _run(learner, pre, field_aware, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field_aware", [False, True])
+@pytest.mark.parametrize("pre", [None, *VALID_PREPROCESSORS])
+@pytest.mark.parametrize("learner", VALID_LEARNERS)
+def test_learner_preprocessor_wire_matrix_gpu(cuda, learner, pre, field_aware):
+    """The same flows on the HIP kernels (GPU JSON parse, device holdout, every learner's
+    round kernel, preprocessing kernels, both wires)."""
+    _run(learner, pre, field_aware, cuda)
+
+
+def _run(learner, pre, field_aware, device):
     name = uuid.uuid4().hex
     addr = f"memory://{name}"
     args = []
@@ -40,7 +54,7 @@ def test_learner_preprocessor_wire_matrix(learner, pre, field_aware):
     sp = FeatureSpace(5, 0, 6, 1 << 16, field_aware=field_aware)
     br = MemoryBroker.named(name)
     br.create_topic(cfg.trainingDataTopic, 2)
-    job = Job(cfg, Comm(), "cpu")
+    job = Job(cfg, Comm(), device)
     br.produce("requests", json.dumps({
         "id": 7, "request": "Create",
         "learner": {"name": learner, "hyperParameters": HYPER.get(learner, {})},
