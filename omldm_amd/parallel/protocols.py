@@ -503,8 +503,9 @@ class SingleLearner(Protocol):
         for name in ("num", "cat", "y"):
             parts[name] = self.comm.gather_tensor(getattr(batch, name).contiguous(), dst=self.HUB)
         if self.comm.rank == self.HUB:
-            merged = HashedBatch(torch.cat(parts["num"]), torch.cat(parts["cat"]),
-                                 torch.cat(parts["y"]))
+            # same batch kind and wire as the local one (cat_span, a fused PolyBatch's pairs)
+            merged = batch._like(torch.cat(parts["num"]), torch.cat(parts["cat"]),
+                                 torch.cat(parts["y"]), None)
             L.fit(merged, RoundContext(spokes=1))
         self._account_small(self.G, batch.B)  # forwarded points
         # hub → spokes: serve forecasts from an up-to-date replica

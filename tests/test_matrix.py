@@ -40,7 +40,24 @@ def test_learner_preprocessor_wire_matrix_gpu(cuda, learner, pre, field_aware):
     _run(learner, pre, field_aware, cuda)
 
 
-def _run(learner, pre, field_aware, device):
+PROTOCOLS = ("CentralizedTraining", "SingleLearner", "Asynchronous", "Synchronous", "SSP",
+             "EASGD", "GM", "FGM")
+
+
+@pytest.mark.parametrize("protocol", PROTOCOLS)
+@pytest.mark.parametrize("learner", ["SVM", "MultiClassPA", "ORR", "NN"])
+def test_learner_protocol_matrix(learner, protocol):
+    _run(learner, "StandardScaler", True, "cpu", protocol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", PROTOCOLS)
+@pytest.mark.parametrize("learner", ["SVM", "MultiClassPA", "ORR", "NN"])
+def test_learner_protocol_matrix_gpu(cuda, learner, protocol):
+    _run(learner, "StandardScaler", True, cuda, protocol)
+
+
+def _run(learner, pre, field_aware, device, protocol="Synchronous"):
     name = uuid.uuid4().hex
     addr = f"memory://{name}"
     args = []
@@ -59,7 +76,7 @@ def _run(learner, pre, field_aware, device):
         "id": 7, "request": "Create",
         "learner": {"name": learner, "hyperParameters": HYPER.get(learner, {})},
         "preProcessors": [{"name": pre}] if pre else [],
-        "trainingConfiguration": {"protocol": "Synchronous"}}))
+        "trainingConfiguration": {"protocol": protocol}}))
     for r in synth_json_records(1200, sp, task=TASK.get(learner, 0)):
         br.produce("trainingData", r)
     for _ in range(4):
@@ -86,3 +103,10 @@ def _run(learner, pre, field_aware, device):
     br.produce("requests", json.dumps({"id": 7, "request": "Delete"}))
     job.tick()
     assert 7 not in job.pipes
+
+
+@pytest.mark.parametrize("protocol", ["SingleLearner", "Synchronous", "FGM"])
+def test_orr_fused_polynomial_under_every_forwarding_protocol(protocol):
+    """ORR + PolynomialFeatures fuses the degree-2 map into the Gram kernel (a PolyBatch
+    reaches the learner); a protocol that regroups the batch must keep that kind."""
+    _run("ORR", "PolynomialFeatures", True, "cpu", protocol)
