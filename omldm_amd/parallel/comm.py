@@ -24,6 +24,11 @@ import torch
 import torch.distributed as dist
 
 
+# element types RCCL / gloo collectives do not carry (sent as raw bytes instead)
+_BYTE_WIRE = (torch.int16, torch.uint16, torch.bool) if hasattr(torch, "uint16") else \
+    (torch.int16, torch.bool)
+
+
 @dataclass
 class CommStats:
     collectives: int = 0
@@ -175,6 +180,11 @@ class Comm:
         mx = max(ns)
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
+        wire = None
+        if t.dtype in _BYTE_WIRE:
+            # int16 (the compact categorical slots), bool, …: neither RCCL nor gloo has the
+            # type, so the rows travel as their bytes and are viewed back after the gather
+            wire, pad = pad, pad.contiguous().view(torch.uint8)
         outs = [torch.zeros_like(pad) for _ in range(self.world)] if self.rank == dst else None
         if self.backend == "nccl":
             # RCCL has no gather; all_gather keeps it a single collective.
@@ -186,6 +196,8 @@ class Comm:
         self.stats.add("gather", pad.numel() * pad.element_size())
         if self.rank != dst:
             return None
+        if wire is not None:
+            outs = [o.view(wire.dtype) for o in outs]
         return [o[:k] for o, k in zip(outs, ns)]
 
     def barrier(self):

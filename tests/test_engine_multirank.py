@@ -1,0 +1,82 @@
+"""The whole engine on two ranks (gloo, CPU, one process per rank via the supervisor):
+eight pipelines at once — every learner, every distributed protocol, preprocessors, both
+categorical wires — fed from file topics, with forecasts and queries, until the idle
+timeout ends the job. Checks the performance record and the outputs every rank wrote."""
+import json
+import os
+import socket
+
+import pytest
+
+from omldm_amd import launch
+from omldm_amd.api.batch import FeatureSpace
+from omldm_amd.io.synthetic import synth_json_records
+from omldm_amd.io.transport import Consumer, FileBroker
+
+PIPES = [  # id, learner, protocol, preprocessors, hyper
+    (1, "SVM", "Synchronous", [], {}),
+    (2, "MultiClassPA", "Asynchronous", ["StandardScaler"], {"nClasses": 2}),
+    (3, "ORR", "FGM", ["PolynomialFeatures"], {}),
+    (4, "NN", "SSP", ["MinMaxScaler"], {"hiddenLayers": [8]}),
+    (5, "K-means", "Synchronous", [], {"k": 3}),       # forced to SingleLearner
+    (6, "HT", "Asynchronous", [], {"nClasses": 2}),    # forced to SingleLearner
+    (7, "RegressorPA", "EASGD", [], {}),
+    (8, "PA", "GM", ["StandardScaler"], {}),
+]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("field_aware", [False, True])
+def test_two_rank_job_every_learner_and_protocol(tmp_path, field_aware):
+    data = tmp_path / "topics"
+    br = FileBroker(str(data))
+    sp = FeatureSpace(5, 0, 6, 1 << 14, field_aware=field_aware)
+    br.create_topic("trainingData", 4)
+    br.create_topic("forecastingData", 2)
+    for i, r in enumerate(synth_json_records(3000, sp, seed=5)):
+        br.produce("trainingData", r, partition=i % 4)
+    for i, r in enumerate(synth_json_records(10, sp, seed=6, operation="forecasting")):
+        br.produce("forecastingData", r, partition=i % 2)
+    for pid, learner, proto, pre, hyper in PIPES:
+        br.produce("requests", json.dumps({
+            "id": pid, "request": "Create", "learner": {"name": learner, "hyperParameters": hyper},
+            "preProcessors": [{"name": p} for p in pre],
+            "trainingConfiguration": {"protocol": proto}}))
+    addr = f"file://{data}"
+    args = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        args += [f"--{k}", addr]
+    args += ["--hashDim", str(sp.dim), "--numFeatures", "5", "--catFeatures", "6",
+             "--fieldAware", str(field_aware).lower(), "--device", "cpu", "--batchSize", "250",
+             "--timeout", "1500", "--parallelism", "4", "--jobName", "two-rank",
+             "--parseThreads", "2", "--watchdogTimeout", "120000"]
+    env_before = dict(os.environ)
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        logs = []
+        rc = launch.supervise(2, args, max_restarts=0, min_nproc=2, port=_port(), log=logs.append)
+    finally:
+        os.environ.clear()
+        os.environ.update(env_before)
+    assert rc == 0, logs
+    js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
+    assert js["jobName"] == "two-rank" and js["parallelism"] == 2
+    stats = {s["pipeline"]: s for s in js["statistics"]}
+    assert sorted(stats) == [p[0] for p in PIPES]
+    for pid, learner, proto, _, _ in PIPES:
+        st = stats[pid]
+        assert st["fitted"] > 0, (pid, st)
+        want = "SingleLearner" if learner in ("K-means", "HT") else proto
+        assert st["protocol"] == want, (pid, st["protocol"])
+    preds = [json.loads(x) for x in Consumer(br, "predictions", all_partitions=True).poll(1000)]
+    assert len(preds) == 10 * len(PIPES)
+    assert {p["mlpId"] for p in preds} == {p[0] for p in PIPES}
