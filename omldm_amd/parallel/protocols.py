@@ -165,7 +165,8 @@ class Synchronous(Protocol):
         else:
             if self._E is None:
                 self._E = L.state_vector().detach().clone()
-                self._d = torch.empty_like(self._E)
+            if getattr(self, "_d", None) is None or self._d.shape != self._E.shape:
+                self._d = torch.empty_like(self._E)  # also after a restore (E loaded)
             L.fit(batch, self._ctx())
             self._buf = torch.sub(L.state_vector(), self._E, out=self._d)
         return self._buf
@@ -296,12 +297,14 @@ class EASGD(Protocol):
         self.tau = max(1, _cfg_int(self.cfg, "tau", 1))
         self.alpha = _cfg_float(self.cfg, "alpha", 0.9 / max(1, self.G))
         self._c = None
+        self._diff = self._s = None
         self._k = 0
 
     def round(self, batch):
         L = self.learner
         if self._c is None:
             self._c = L.state_vector().detach().clone()
+        if self._s is None or self._s.shape != self._c.shape:  # also after a restore
             self._diff, self._s = torch.empty_like(self._c), torch.empty_like(self._c)
         L.fit(batch, self._ctx())
         self._k += 1
@@ -319,12 +322,14 @@ class EASGD(Protocol):
     def state_dict(self):
         sd = super().state_dict()
         sd["center"] = None if self._c is None else self._c.cpu()
+        sd["k"] = self._k
         return sd
 
     def load_state_dict(self, sd):
         super().load_state_dict(sd)
         if sd.get("center") is not None:
             self._c = sd["center"].to(self.learner.device)
+        self._k = int(sd.get("k", 0))
 
 
 def _model_sync(p: Protocol) -> None:

@@ -25,6 +25,18 @@ PIPES = [  # id, learner, protocol, preprocessors, hyper
 ]
 
 
+PIPES_ALT = [  # the same learners under other protocols (non-fused Synchronous rounds)
+    (1, "SVM", "FGM", [], {}),
+    (2, "MultiClassPA", "Synchronous", [], {"nClasses": 2}),
+    (3, "ORR", "Synchronous", ["StandardScaler"], {}),
+    (4, "NN", "Synchronous", [], {"hiddenLayers": [8]}),
+    (5, "K-means", "FGM", ["MinMaxScaler"], {"k": 2}),
+    (6, "HT", "Synchronous", [], {"nClasses": 2}),
+    (7, "RegressorPA", "SSP", [], {}),
+    (8, "PA", "EASGD", [], {}),
+]
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -80,3 +92,50 @@ def test_two_rank_job_every_learner_and_protocol(tmp_path, field_aware):
     preds = [json.loads(x) for x in Consumer(br, "predictions", all_partitions=True).poll(1000)]
     assert len(preds) == 10 * len(PIPES)
     assert {p["mlpId"] for p in preds} == {p[0] for p in PIPES}
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("pipes", [PIPES, PIPES_ALT], ids=["protocols", "protocols_alt"])
+def test_two_rank_job_killed_and_restored_on_one_rank(tmp_path, pipes):
+    """Checkpoint every tick, rank 1 killed at tick 6, the supervisor restarts the job on
+    one rank from the last checkpoint: every learner's and protocol's state goes through
+    a re-scaled restore (2 → 1 ranks) and the job finishes with all eight pipelines."""
+    data = tmp_path / "topics"
+    br = FileBroker(str(data))
+    sp = FeatureSpace(5, 0, 6, 1 << 14, field_aware=True)
+    br.create_topic("trainingData", 4)
+    for i, r in enumerate(synth_json_records(4000, sp, seed=7)):
+        br.produce("trainingData", r, partition=i % 4)
+    for pid, learner, proto, pre, hyper in pipes:
+        br.produce("requests", json.dumps({
+            "id": pid, "request": "Create", "learner": {"name": learner, "hyperParameters": hyper},
+            "preProcessors": [{"name": p} for p in pre],
+            "trainingConfiguration": {"protocol": proto, "HubParallelism": 1}}))
+    addr = f"file://{data}"
+    args = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        args += [f"--{k}", addr]
+    args += ["--hashDim", str(sp.dim), "--numFeatures", "5", "--catFeatures", "6",
+             "--fieldAware", "true", "--device", "cpu", "--batchSize", "200",
+             "--timeout", "1500", "--parallelism", "4", "--jobName", "restore-all",
+             "--checkpointing", "true", "--checkInterval", "0",
+             "--stateBackend", str(tmp_path / "ckpt"), "--faults", "kill:rank=1:tick=6",
+             "--parseThreads", "2", "--watchdogTimeout", "120000"]
+    env_before = dict(os.environ)
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        logs = []
+        rc = launch.supervise(2, args, max_restarts=2, min_nproc=1, shrink=True, port=_port(),
+                              log=logs.append)
+    finally:
+        os.environ.clear()
+        os.environ.update(env_before)
+    assert rc == 0, logs
+    assert any("on 1 rank(s)" in m for m in logs), logs
+    js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
+    assert js["jobName"] == "restore-all" and js["parallelism"] == 1
+    stats = {s["pipeline"]: s for s in js["statistics"]}
+    assert sorted(stats) == [p[0] for p in pipes]
+    for pid, learner, proto, _, _ in pipes:
+        assert stats[pid]["fitted"] > 0, (pid, stats[pid])
