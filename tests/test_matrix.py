@@ -57,7 +57,29 @@ def test_learner_protocol_matrix_gpu(cuda, learner, protocol):
     _run(learner, "StandardScaler", True, cuda, protocol)
 
 
-def _run(learner, pre, field_aware, device, protocol="Synchronous"):
+VARIANTS = [("SVM", {"variant": "Pegasos", "lambda": 1e-3}), ("SVM", {"modelDtype": "bf16"}),
+            ("PA", {"variant": "PA-II", "C": 0.5}), ("PA", {"variant": "PA"}),
+            ("RegressorPA", {"variant": "PA-I", "epsilon": 0.2, "modelDtype": "bf16"}),
+            ("MultiClassPA", {"nClasses": 4, "variant": "PA-II", "modelDtype": "bf16"}),
+            ("NN", {"hiddenLayers": [24, 12], "activation": "tanh", "matmulDtype": "bf16"}),
+            ("NN", {"hiddenLayers": [8], "activation": "sigmoid", "task": "regression"}),
+            ("NN", {"hiddenLayers": [16], "nClasses": 3}),
+            ("K-means", {"k": 40}), ("HT", {"nClasses": 3, "gracePeriod": 50, "nBins": 8}),
+            ("ORR", {"lambda": 0.1})]
+
+
+@pytest.mark.parametrize("learner,hyper", VARIANTS)
+def test_learner_variants(learner, hyper):
+    _run(learner, None, True, "cpu", hyper=hyper)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("learner,hyper", VARIANTS)
+def test_learner_variants_gpu(cuda, learner, hyper):
+    _run(learner, None, True, cuda, hyper=hyper)
+
+
+def _run(learner, pre, field_aware, device, protocol="Synchronous", hyper=None):
     name = uuid.uuid4().hex
     addr = f"memory://{name}"
     args = []
@@ -74,7 +96,7 @@ def _run(learner, pre, field_aware, device, protocol="Synchronous"):
     job = Job(cfg, Comm(), device)
     br.produce("requests", json.dumps({
         "id": 7, "request": "Create",
-        "learner": {"name": learner, "hyperParameters": HYPER.get(learner, {})},
+        "learner": {"name": learner, "hyperParameters": hyper or HYPER.get(learner, {})},
         "preProcessors": [{"name": pre}] if pre else [],
         "trainingConfiguration": {"protocol": protocol}}))
     for r in synth_json_records(1200, sp, task=TASK.get(learner, 0)):
