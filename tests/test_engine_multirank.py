@@ -139,3 +139,62 @@ def test_two_rank_job_killed_and_restored_on_one_rank(tmp_path, pipes):
     assert sorted(stats) == [p[0] for p in pipes]
     for pid, learner, proto, _, _ in pipes:
         assert stats[pid]["fitted"] > 0, (pid, stats[pid])
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_job_over_kafka_with_compressed_topics(tmp_path):
+    """Two ranks consuming and producing through the Kafka wire client against the
+    protocol-level fake broker: lz4-compressed input batches, zstd-compressed outputs
+    (Produce v7 / Fetch v10 negotiated), every rank reading its share of the partitions."""
+    from omldm_amd.io.kafka import KafkaBroker
+    from tests.fake_kafka import FakeKafka
+
+    fk = FakeKafka(default_partitions=4)
+    try:
+        sp = FeatureSpace(5, 0, 6, 1 << 14, field_aware=True)
+        src = KafkaBroker(f"{fk.addr}?compression=lz4")
+        for t in ("trainingData", "forecastingData", "requests", "responses", "predictions",
+                  "performance"):
+            src.create_topic(t, 1 if t in ("requests", "responses", "performance") else 4)
+        recs = [r.encode() for r in synth_json_records(2000, sp, seed=9)]
+        for p in range(4):
+            src.produce_batch("trainingData", p, recs[p::4])
+        src.produce_batch("forecastingData", 0, [r.encode() for r in synth_json_records(
+            6, sp, seed=10, operation="forecasting")])
+        for pid, learner, proto, pre, hyper in PIPES[:4]:
+            src.produce("requests", json.dumps({
+                "id": pid, "request": "Create",
+                "learner": {"name": learner, "hyperParameters": hyper},
+                "preProcessors": [{"name": p} for p in pre],
+                "trainingConfiguration": {"protocol": proto}}), partition=0)
+        out = f"{fk.addr}?compression=zstd"
+        args = ["--trainingDataAddr", fk.addr, "--forecastingDataAddr", fk.addr,
+                "--requestsAddr", fk.addr, "--responsesAddr", out, "--predictionsAddr", out,
+                "--performanceAddr", out,
+                "--hashDim", str(sp.dim), "--numFeatures", "5", "--catFeatures", "6",
+                "--fieldAware", "true", "--device", "cpu", "--batchSize", "200",
+                "--timeout", "1500", "--parallelism", "4", "--jobName", "kafka-two-rank",
+                "--parseThreads", "2", "--watchdogTimeout", "120000"]
+        env_before = dict(os.environ)
+        os.environ["OMP_NUM_THREADS"] = "1"
+        try:
+            logs = []
+            rc = launch.supervise(2, args, max_restarts=0, min_nproc=2, port=_port(),
+                                  log=logs.append)
+        finally:
+            os.environ.clear()
+            os.environ.update(env_before)
+        assert rc == 0, logs
+        rd = KafkaBroker(fk.addr)
+        perf, _ = rd.consume("performance", 0, 0, 10)
+        js = json.loads(perf[-1])
+        assert js["jobName"] == "kafka-two-rank" and js["parallelism"] == 2
+        assert sorted(s["pipeline"] for s in js["statistics"]) == [1, 2, 3, 4]
+        assert all(s["fitted"] > 0 for s in js["statistics"])
+        preds = []
+        for p in range(rd.partitions("predictions")):
+            v, _ = rd.consume("predictions", p, 0, 1000)
+            preds += v
+        assert len(preds) == 6 * 4
+    finally:
+        fk.close()
