@@ -198,3 +198,49 @@ def test_two_rank_job_over_kafka_with_compressed_topics(tmp_path):
         assert len(preds) == 6 * 4
     finally:
         fk.close()
+
+
+@pytest.mark.timeout(300)
+def test_four_rank_job_mixed_hub_layouts(tmp_path):
+    """Four ranks, Synchronous pipelines with HubParallelism 1 (reduce + broadcast), 2
+    (sharded hubs) and 4 (all-reduce) side by side: the engine coalesces each layout's
+    round buffers into its own collective (collective order must agree on every rank, or
+    the job deadlocks); every pipeline trains and is reported."""
+    data = tmp_path / "topics"
+    br = FileBroker(str(data))
+    sp = FeatureSpace(5, 0, 6, 1 << 14, field_aware=True)
+    br.create_topic("trainingData", 4)
+    for i, r in enumerate(synth_json_records(3200, sp, seed=11)):
+        br.produce("trainingData", r, partition=i % 4)
+    layouts = {1: ("SVM", 1), 2: ("PA", 2), 3: ("RegressorPA", 4), 4: ("ORR", 2), 5: ("NN", 1)}
+    for pid, (learner, hubs) in layouts.items():
+        br.produce("requests", json.dumps({
+            "id": pid, "request": "Create",
+            "learner": {"name": learner,
+                        "hyperParameters": {"hiddenLayers": [8]} if learner == "NN" else {}},
+            "trainingConfiguration": {"protocol": "Synchronous", "HubParallelism": hubs}}))
+    for pid in layouts:
+        br.produce("requests", json.dumps({"id": pid, "request": "Query", "requestId": 100 + pid}))
+    addr = f"file://{data}"
+    args = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        args += [f"--{k}", addr]
+    args += ["--hashDim", str(sp.dim), "--numFeatures", "5", "--catFeatures", "6",
+             "--fieldAware", "true", "--device", "cpu", "--batchSize", "200",
+             "--timeout", "1500", "--parallelism", "8", "--jobName", "hubs",
+             "--parseThreads", "1", "--watchdogTimeout", "120000"]
+    env_before = dict(os.environ)
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        logs = []
+        rc = launch.supervise(4, args, max_restarts=0, min_nproc=4, port=_port(), log=logs.append)
+    finally:
+        os.environ.clear()
+        os.environ.update(env_before)
+    assert rc == 0, logs
+    js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
+    assert js["parallelism"] == 4
+    stats = {s["pipeline"]: s for s in js["statistics"]}
+    assert sorted(stats) == sorted(layouts)
+    assert all(s["fitted"] > 0 and s["protocol"] == "Synchronous" for s in stats.values())
