@@ -244,3 +244,54 @@ def test_four_rank_job_mixed_hub_layouts(tmp_path):
     stats = {s["pipeline"]: s for s in js["statistics"]}
     assert sorted(stats) == sorted(layouts)
     assert all(s["fitted"] > 0 and s["protocol"] == "Synchronous" for s in stats.values())
+
+
+@pytest.mark.timeout(300)
+def test_restore_grows_from_one_rank_to_two(tmp_path):
+    """A one-rank job checkpoints and stops after a few ticks; the job is restarted with
+    --restore on two ranks (the re-scaled restore growing the world): every learner's
+    state, the pipelines and the consumer offsets carry over and the job completes."""
+    data = tmp_path / "topics"
+    br = FileBroker(str(data))
+    sp = FeatureSpace(5, 0, 6, 1 << 14, field_aware=True)
+    br.create_topic("trainingData", 4)
+    for i, r in enumerate(synth_json_records(4000, sp, seed=13)):
+        br.produce("trainingData", r, partition=i % 4)
+    for pid, learner, proto, pre, hyper in PIPES:
+        br.produce("requests", json.dumps({
+            "id": pid, "request": "Create", "learner": {"name": learner, "hyperParameters": hyper},
+            "preProcessors": [{"name": p} for p in pre],
+            "trainingConfiguration": {"protocol": proto}}))
+    addr = f"file://{data}"
+    base = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        base += [f"--{k}", addr]
+    base += ["--hashDim", str(sp.dim), "--numFeatures", "5", "--catFeatures", "6",
+             "--fieldAware", "true", "--device", "cpu", "--batchSize", "200",
+             "--timeout", "1500", "--parallelism", "4", "--jobName", "grow",
+             "--checkpointing", "true", "--checkInterval", "0",
+             "--stateBackend", str(tmp_path / "ckpt"), "--parseThreads", "2",
+             "--watchdogTimeout", "120000"]
+    env_before = dict(os.environ)
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        logs = []
+        rc = launch.supervise(1, base + ["--maxTicks", "6"], max_restarts=0, min_nproc=1,
+                              port=_port(), log=logs.append)
+        assert rc == 0, logs
+        assert not Consumer(br, "performance", all_partitions=True).poll(10)  # not finished
+        rc = launch.supervise(2, base + ["--restore", "true"], max_restarts=0, min_nproc=2,
+                              port=_port(), log=logs.append)
+    finally:
+        os.environ.clear()
+        os.environ.update(env_before)
+    assert rc == 0, logs
+    js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
+    assert js["jobName"] == "grow" and js["parallelism"] == 2
+    # the restored consumer offsets: the second run trained only on what the first did
+    # not consume (a fresh start would re-train on all ≈ 0.8 × 4000 rows)
+    assert js["metrics"]["trainedExamples"] < 2900, js["metrics"]["trainedExamples"]
+    stats = {s["pipeline"]: s for s in js["statistics"]}
+    assert sorted(stats) == [p[0] for p in PIPES]
+    assert all(s["fitted"] > 0 for s in stats.values())
