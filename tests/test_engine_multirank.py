@@ -62,6 +62,8 @@ def test_two_rank_job_every_learner_and_protocol(tmp_path, field_aware):
             "id": pid, "request": "Create", "learner": {"name": learner, "hyperParameters": hyper},
             "preProcessors": [{"name": p} for p in pre],
             "trainingConfiguration": {"protocol": proto}}))
+    for pid, *_ in PIPES:
+        br.produce("requests", json.dumps({"id": pid, "request": "Query", "requestId": 500 + pid}))
     addr = f"file://{data}"
     args = []
     for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
@@ -92,6 +94,10 @@ def test_two_rank_job_every_learner_and_protocol(tmp_path, field_aware):
     preds = [json.loads(x) for x in Consumer(br, "predictions", all_partitions=True).poll(1000)]
     assert len(preds) == 10 * len(PIPES)
     assert {p["mlpId"] for p in preds} == {p[0] for p in PIPES}
+    # one reduced answer per query (the final, non-bucket response carries the metrics)
+    resp = [json.loads(x) for x in Consumer(br, "responses", all_partitions=True).poll(10000)]
+    finals = [r for r in resp if r.get("responseId", -1) >= 500 and r.get("loss") is not None]
+    assert sorted(r["responseId"] for r in finals) == [500 + p[0] for p in PIPES]
 
 
 @pytest.mark.timeout(300)
