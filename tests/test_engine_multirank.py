@@ -48,6 +48,23 @@ def _port():
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("field_aware", [False, True])
 def test_two_rank_job_every_learner_and_protocol(tmp_path, field_aware):
+    _two_rank_job(tmp_path, field_aware, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("field_aware", [False, True])
+def test_two_rank_job_every_learner_and_protocol_gpu(tmp_path, field_aware):
+    """The same job with both ranks on the one GPU of the box (HIP kernels, device-resident
+    state; the two ranks talk over gloo — the 8-GPU RCCL run is the driver's)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _two_rank_job(tmp_path, field_aware, "cuda", {"OMLDM_DIST_BACKEND": "gloo"})
+
+
+def _two_rank_job(tmp_path, field_aware, device, env=None):
     data = tmp_path / "topics"
     br = FileBroker(str(data))
     sp = FeatureSpace(5, 0, 6, 1 << 14, field_aware=field_aware)
@@ -70,11 +87,12 @@ def test_two_rank_job_every_learner_and_protocol(tmp_path, field_aware):
               "predictionsAddr", "performanceAddr"):
         args += [f"--{k}", addr]
     args += ["--hashDim", str(sp.dim), "--numFeatures", "5", "--catFeatures", "6",
-             "--fieldAware", str(field_aware).lower(), "--device", "cpu", "--batchSize", "250",
+             "--fieldAware", str(field_aware).lower(), "--device", device, "--batchSize", "250",
              "--timeout", "1500", "--parallelism", "4", "--jobName", "two-rank",
              "--parseThreads", "2", "--watchdogTimeout", "120000"]
     env_before = dict(os.environ)
     os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ.update(env or {})
     try:
         logs = []
         rc = launch.supervise(2, args, max_restarts=0, min_nproc=2, port=_port(), log=logs.append)
