@@ -124,6 +124,23 @@ def test_two_rank_job_killed_and_restored_on_one_rank(tmp_path, pipes):
     """Checkpoint every tick, rank 1 killed at tick 6, the supervisor restarts the job on
     one rank from the last checkpoint: every learner's and protocol's state goes through
     a re-scaled restore (2 → 1 ranks) and the job finishes with all eight pipelines."""
+    _kill_restore(tmp_path, pipes, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("pipes", [PIPES, PIPES_ALT], ids=["protocols", "protocols_alt"])
+def test_two_rank_job_killed_and_restored_on_one_rank_gpu(tmp_path, pipes):
+    """The same with device-resident learner state (HBM models, shadows, the HT tree)
+    checkpointed from and restored onto the GPU."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _kill_restore(tmp_path, pipes, "cuda", {"OMLDM_DIST_BACKEND": "gloo"})
+
+
+def _kill_restore(tmp_path, pipes, device, env=None):
     data = tmp_path / "topics"
     br = FileBroker(str(data))
     sp = FeatureSpace(5, 0, 6, 1 << 14, field_aware=True)
@@ -141,13 +158,14 @@ def test_two_rank_job_killed_and_restored_on_one_rank(tmp_path, pipes):
               "predictionsAddr", "performanceAddr"):
         args += [f"--{k}", addr]
     args += ["--hashDim", str(sp.dim), "--numFeatures", "5", "--catFeatures", "6",
-             "--fieldAware", "true", "--device", "cpu", "--batchSize", "200",
+             "--fieldAware", "true", "--device", device, "--batchSize", "200",
              "--timeout", "1500", "--parallelism", "4", "--jobName", "restore-all",
              "--checkpointing", "true", "--checkInterval", "0",
              "--stateBackend", str(tmp_path / "ckpt"), "--faults", "kill:rank=1:tick=6",
              "--parseThreads", "2", "--watchdogTimeout", "120000"]
     env_before = dict(os.environ)
     os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ.update(env or {})
     try:
         logs = []
         rc = launch.supervise(2, args, max_restarts=2, min_nproc=1, shrink=True, port=_port(),
