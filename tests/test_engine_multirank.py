@@ -81,6 +81,16 @@ def _two_rank_job(tmp_path, field_aware, device, env=None):
             "trainingConfiguration": {"protocol": proto}}))
     for pid, *_ in PIPES:
         br.produce("requests", json.dumps({"id": pid, "request": "Query", "requestId": 500 + pid}))
+    # lifecycle on every rank: pipeline 9 created, updated, deleted, re-created as another
+    # learner (its final statistics must be the new learner's)
+    for req in ({"id": 9, "request": "Create", "learner": {"name": "SVM"},
+                 "trainingConfiguration": {"protocol": "Synchronous"}},
+                {"id": 9, "request": "Update", "learner": {"name": "SVM",
+                                                            "hyperParameters": {"C": 0.1}}},
+                {"id": 9, "request": "Delete"},
+                {"id": 9, "request": "Create", "learner": {"name": "RegressorPA"},
+                 "trainingConfiguration": {"protocol": "Asynchronous"}}):
+        br.produce("requests", json.dumps(req))
     addr = f"file://{data}"
     args = []
     for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
@@ -103,15 +113,16 @@ def _two_rank_job(tmp_path, field_aware, device, env=None):
     js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
     assert js["jobName"] == "two-rank" and js["parallelism"] == 2
     stats = {s["pipeline"]: s for s in js["statistics"]}
-    assert sorted(stats) == [p[0] for p in PIPES]
+    assert sorted(stats) == [p[0] for p in PIPES] + [9]
+    assert stats[9]["protocol"] == "Asynchronous" and stats[9]["fitted"] > 0
     for pid, learner, proto, _, _ in PIPES:
         st = stats[pid]
         assert st["fitted"] > 0, (pid, st)
         want = "SingleLearner" if learner in ("K-means", "HT") else proto
         assert st["protocol"] == want, (pid, st["protocol"])
     preds = [json.loads(x) for x in Consumer(br, "predictions", all_partitions=True).poll(1000)]
-    assert len(preds) == 10 * len(PIPES)
-    assert {p["mlpId"] for p in preds} == {p[0] for p in PIPES}
+    assert len(preds) == 10 * (len(PIPES) + 1)
+    assert {p["mlpId"] for p in preds} == {p[0] for p in PIPES} | {9}
     # one reduced answer per query (the final, non-bucket response carries the metrics)
     resp = [json.loads(x) for x in Consumer(br, "responses", all_partitions=True).poll(10000)]
     finals = [r for r in resp if r.get("responseId", -1) >= 500 and r.get("loss") is not None]
