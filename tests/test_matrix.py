@@ -79,7 +79,20 @@ def test_learner_variants_gpu(cuda, learner, hyper):
     _run(learner, None, True, cuda, hyper=hyper)
 
 
-def _run(learner, pre, field_aware, device, protocol="Synchronous", hyper=None):
+FLAGS = [["--gpuParse", "false"], ["--prefetch", "false"], ["--ingestCUs", "16"],
+         ["--ingestCopy", "sdma"], ["--gpuParse", "false", "--prefetch", "false"]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", FLAGS, ids=lambda f: "_".join(x.strip("-") for x in f))
+@pytest.mark.parametrize("learner", ["SVM", "MultiClassPA", "HT"])
+def test_engine_ingest_flags_gpu(cuda, learner, flags):
+    """Engine ingest variants on the GPU: host JSON parser instead of the GPU one, no
+    read-ahead, XCD-local ingest CUs, SDMA staging copies."""
+    _run(learner, "StandardScaler", True, cuda, extra=flags)
+
+
+def _run(learner, pre, field_aware, device, protocol="Synchronous", hyper=None, extra=()):
     name = uuid.uuid4().hex
     addr = f"memory://{name}"
     args = []
@@ -88,7 +101,7 @@ def _run(learner, pre, field_aware, device, protocol="Synchronous", hyper=None):
         args += [f"--{k}", addr]
     args += ["--hashDim", str(1 << 16), "--batchSize", "400", "--timeout", "200",
              "--parallelism", "4", "--numFeatures", "5", "--catFeatures", "6",
-             "--fieldAware", str(field_aware).lower()]
+             "--fieldAware", str(field_aware).lower(), *extra]
     cfg = JobConfig.from_args(args)
     sp = FeatureSpace(5, 0, 6, 1 << 16, field_aware=field_aware)
     br = MemoryBroker.named(name)
