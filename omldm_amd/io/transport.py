@@ -245,8 +245,11 @@ class FileBroker(Broker):
         if not os.path.exists(path):
             return [], offset
         with open(path, "rb") as f:
+            left = os.fstat(f.fileno()).st_size - offset  # read() preallocates its size
+            if left <= 0:
+                return [], offset
             f.seek(offset)
-            data = f.read(max(1, max_records) * 4096)
+            data = f.read(min(left, max(1, max_records) * 4096))
         if not data:
             return [], offset
         cut = data.rfind(b"\n")
