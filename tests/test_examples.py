@@ -3,6 +3,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -30,3 +32,11 @@ def test_single_node_recipe_two_ranks(tmp_path):
     assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-3000:])
     perf = [line for line in out.stdout.splitlines() if line.startswith('{"jobName"')]
     assert perf and '"parallelism": 2' in perf[-1]
+
+
+@pytest.mark.gpu
+def test_quickstart_runs_on_gpu(cuda):
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "examples", "quickstart.py"),
+                          "--records", "20000"], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "response 100" in out.stdout and "performance:" in out.stdout
