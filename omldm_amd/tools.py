@@ -21,6 +21,39 @@ TOPICS = {"requests": 1, "responses": 1, "trainingData": 36, "forecastingData": 
           "predictions": 36, "performance": 1}
 
 
+def _produce_all(br, topic: str, recs: list) -> None:
+    """Records spread round-robin over the topic's partitions, one block per partition
+    (a Kafka RecordBatch per ≤ 900 KiB instead of one Produce request per record)."""
+    import numpy as np
+
+    n = br.partitions(topic)
+    for p in range(n):
+        chunk = recs[p::n]
+        if not chunk:
+            continue
+        block = b"".join(r + b"\n" for r in chunk)
+        offs = np.zeros(len(chunk) + 1, dtype=np.int64)
+        np.cumsum([len(r) + 1 for r in chunk], out=offs[1:])
+        br.produce_lines(topic, block, offs, partition=p)
+
+
+def _tail(br, topic: str, n: int) -> list:
+    """The last ``n`` records of every partition (Kafka: read from end − n; file topics,
+    whose offsets are bytes, are read whole)."""
+    c = Consumer(br, topic, all_partitions=True)
+    from omldm_amd.io.kafka import KafkaBroker
+
+    if isinstance(br, KafkaBroker):
+        for p in c.parts:
+            c.offsets[p] = max(0, br.end_offset(topic, p) - n)
+    out = []
+    while True:
+        got = c.poll(10**6)
+        if not got:
+            return out[-n:] if n else out
+        out += got
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m omldm_amd.tools")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -49,24 +82,24 @@ def main(argv=None) -> int:
             br.create_topic(name, n)
             print(f"{name}: {n} partition(s)")
     elif a.cmd == "produce":
-        k = 0
         with open(a.file, "rb") as f:
-            for line in f:
-                if line.strip():
-                    br.produce(a.topic, line.rstrip(b"\n"))
-                    k += 1
+            recs = [line.rstrip(b"\n") for line in f if line.strip()]
+        if br.partitions(a.topic) == 1:
+            for r in recs:  # single-partition control topics keep the file's order
+                br.produce(a.topic, r)
+        else:
+            _produce_all(br, a.topic, recs)
         br.flush()
-        print(f"produced {k} record(s) to {a.topic}")
+        print(f"produced {len(recs)} record(s) to {a.topic}")
     elif a.cmd == "tail":
-        for rec in Consumer(br, a.topic, all_partitions=True).poll(10**9)[-a.n:]:
+        for rec in _tail(br, a.topic, a.n):
             sys.stdout.write(rec.decode(errors="replace") + "\n")
     elif a.cmd == "synth":
         from omldm_amd.api.batch import FeatureSpace
         from omldm_amd.io.synthetic import synth_json_records
 
-        for r in synth_json_records(a.n, FeatureSpace(13, 0, 26, a.hash_dim),
-                                    operation=a.operation):
-            br.produce(a.topic, r)
+        _produce_all(br, a.topic, [r.encode() for r in synth_json_records(
+            a.n, FeatureSpace(13, 0, 26, a.hash_dim), operation=a.operation)])
         br.flush()
         print(f"produced {a.n} synthetic record(s) to {a.topic}")
     return 0
