@@ -79,6 +79,14 @@ def test_learner_variants_gpu(cuda, learner, hyper):
     _run(learner, None, True, cuda, hyper=hyper)
 
 
+@pytest.mark.parametrize("learner", ["SVM", "MultiClassPA", "ORR", "NN", "K-means", "HT"])
+def test_discrete_features_and_serving_mode(learner):
+    """Points with discrete features (dense slots after the numerical ones) and a job in
+    serving mode (--test false: no idle termination, answers still flow)."""
+    _run(learner, "MinMaxScaler", True, "cpu", discrete=2,
+         extra=["--discreteFeatures", "2", "--test", "false"])
+
+
 FLAGS = [["--gpuParse", "false"], ["--prefetch", "false"], ["--ingestCUs", "16"],
          ["--ingestCopy", "sdma"], ["--gpuParse", "false", "--prefetch", "false"]]
 
@@ -92,7 +100,8 @@ def test_engine_ingest_flags_gpu(cuda, learner, flags):
     _run(learner, "StandardScaler", True, cuda, extra=flags)
 
 
-def _run(learner, pre, field_aware, device, protocol="Synchronous", hyper=None, extra=()):
+def _run(learner, pre, field_aware, device, protocol="Synchronous", hyper=None, extra=(),
+         discrete=0):
     name = uuid.uuid4().hex
     addr = f"memory://{name}"
     args = []
@@ -103,7 +112,7 @@ def _run(learner, pre, field_aware, device, protocol="Synchronous", hyper=None, 
              "--parallelism", "4", "--numFeatures", "5", "--catFeatures", "6",
              "--fieldAware", str(field_aware).lower(), *extra]
     cfg = JobConfig.from_args(args)
-    sp = FeatureSpace(5, 0, 6, 1 << 16, field_aware=field_aware)
+    sp = FeatureSpace(5, discrete, 6, 1 << 16, field_aware=field_aware)
     br = MemoryBroker.named(name)
     br.create_topic(cfg.trainingDataTopic, 2)
     job = Job(cfg, Comm(), device)
