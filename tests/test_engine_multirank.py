@@ -259,6 +259,10 @@ def test_four_rank_job_mixed_hub_layouts(tmp_path):
     (sharded hubs) and 4 (all-reduce) side by side: the engine coalesces each layout's
     round buffers into its own collective (collective order must agree on every rank, or
     the job deadlocks); every pipeline trains and is reported."""
+    _four_rank(tmp_path, "cpu")
+
+
+def _four_rank(tmp_path, device, env=None):
     data = tmp_path / "topics"
     br = FileBroker(str(data))
     sp = FeatureSpace(5, 0, 6, 1 << 14, field_aware=True)
@@ -280,11 +284,12 @@ def test_four_rank_job_mixed_hub_layouts(tmp_path):
               "predictionsAddr", "performanceAddr"):
         args += [f"--{k}", addr]
     args += ["--hashDim", str(sp.dim), "--numFeatures", "5", "--catFeatures", "6",
-             "--fieldAware", "true", "--device", "cpu", "--batchSize", "200",
+             "--fieldAware", "true", "--device", device, "--batchSize", "200",
              "--timeout", "1500", "--parallelism", "8", "--jobName", "hubs",
              "--parseThreads", "1", "--watchdogTimeout", "120000"]
     env_before = dict(os.environ)
     os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ.update(env or {})
     try:
         logs = []
         rc = launch.supervise(4, args, max_restarts=0, min_nproc=4, port=_port(), log=logs.append)
