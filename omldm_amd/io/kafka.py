@@ -549,11 +549,10 @@ class KafkaBroker(Broker):
         raise IOError("kafka fetch: broker rejected Fetch v10")
 
     def consume(self, topic, partition, offset, max_records):
-        recs = decode_batches(self._fetch(topic, partition, offset))
-        recs = [(o, v) for o, v in recs if o >= offset][:max_records]
-        if not recs:
-            return [], offset
-        return [v for _, v in recs], recs[-1][0] + 1
+        # the native decoder also steps over transactional control batches (a record-less
+        # fetch still moves the offset), which the per-record form needs as much
+        buf, offs, nxt = self.consume_block(topic, partition, offset, max_records)
+        return [buf[int(offs[i]):int(offs[i + 1])] for i in range(len(offs) - 1)], nxt
 
     @staticmethod
     def _decode_into(data: bytes, offset: int, max_records: int, dst, cap: int):

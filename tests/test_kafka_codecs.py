@@ -279,3 +279,23 @@ def test_api_versions_negotiation(versions, expect):
         br.close()
     finally:
         fk.close()
+
+
+def test_per_record_consume_steps_over_control_batches():
+    """Consumer.poll (requests topic, tools) goes through KafkaBroker.consume: a partition
+    that starts with a transaction marker must not stall it."""
+    class Log(K.KafkaBroker):
+        def __init__(self, data):
+            self.data = data
+
+        def _fetch(self, topic, partition, offset, max_bytes=4 << 20):
+            return self.data
+
+    vals = [b'{"id": 1}', b'{"id": 2}']
+    br = Log(K.encode_batch([b"\0\0\0\0"], base_offset=0, control=True)
+             + K.encode_batch(vals, base_offset=1))
+    got, nxt = br.consume("requests", 0, 0, 10)
+    assert got == vals and nxt == 3
+    br = Log(K.encode_batch([b"\0\0\0\0"], base_offset=0, control=True))
+    got, nxt = br.consume("requests", 0, 0, 10)
+    assert got == [] and nxt == 1
