@@ -164,6 +164,7 @@ class R:
 
 CODECS = {"none": 0, "gzip": 1, "snappy": 2, "lz4": 3, "zstd": 4}
 UNSUPPORTED_COMPRESSION_TYPE = 76
+OFFSET_OUT_OF_RANGE = 1
 
 
 def codec_id(c) -> int:
@@ -509,13 +510,16 @@ class KafkaBroker(Broker):
         return self._list_offset(topic, partition, -1)
 
     def _fetch(self, topic: str, partition: int, offset: int, max_bytes: int = 4 << 20) -> bytes:
-        """Raw record set of one partition from ``offset`` (Fetch v4; v10 for brokers that
-        answered UNSUPPORTED_COMPRESSION_TYPE, i.e. zstd data)."""
+        """Raw record set of one partition from ``offset`` (Fetch v10 when the broker
+        offers it, else v4 — switching to v10 if it answers UNSUPPORTED_COMPRESSION_TYPE,
+        i.e. zstd data). An offset that retention already deleted (OFFSET_OUT_OF_RANGE
+        below the log start) resumes at the log start, as a consumer with
+        auto.offset.reset=earliest would."""
         leader = self._metadata(topic).get(partition)
         conn = self._conn(leader)
         addr = self._addr(leader)
         best = conn.version(1, (4, 10))
-        for _ in range(2):
+        for _ in range(3):
             v10 = best >= 10 or addr in self._fetch_v10
             w = W().i32(-1).i32(100).i32(1).i32(max(8 << 20, max_bytes)).i8(0)
             if v10:
@@ -543,10 +547,15 @@ class KafkaBroker(Broker):
             if err == UNSUPPORTED_COMPRESSION_TYPE and not v10:
                 self._fetch_v10.add(addr)
                 continue
+            if err == OFFSET_OUT_OF_RANGE:
+                start = self._list_offset(topic, partition, -2)
+                if offset < start:
+                    offset = start
+                    continue
             if err:
                 raise IOError(f"kafka fetch error {err}")
             return out
-        raise IOError("kafka fetch: broker rejected Fetch v10")
+        raise IOError(f"kafka fetch of {topic}/{partition} at {offset} failed")
 
     def consume(self, topic, partition, offset, max_records):
         # the native decoder also steps over transactional control batches (a record-less

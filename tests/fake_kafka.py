@@ -34,6 +34,7 @@ class FakeKafka:
         self.calls = []                    # (api, version) of every request
         self.logs = defaultdict(list)      # (topic, p) -> [bytes]
         self.codec = defaultdict(int)      # (topic, p) -> codec of the last produce
+        self.log_start = defaultdict(int)  # (topic, p) -> first offset retention kept
         self.control_every = control_every
         self.fetch_versions = []
         self.nparts = {}
@@ -146,7 +147,8 @@ class FakeKafka:
                 topics = r.arr(lambda r: (r.s(), r.arr(lambda r: (r.i32(), r.i64()))))
                 w = W().arr(topics, lambda w, tp: w.s(tp[0]).arr(
                     tp[1], lambda w, pt: w.i32(pt[0]).i16(0).i64(-1).i64(
-                        len(self.logs[(tp[0], pt[0])]) if pt[1] == -1 else 0)))
+                        len(self.logs[(tp[0], pt[0])]) if pt[1] == -1
+                        else self.log_start[(tp[0], pt[0])])))
                 return bytes(w.b)
             if api == 1:  # Fetch v4 / v10
                 self.fetch_versions.append(ver)
@@ -165,6 +167,8 @@ class FakeKafka:
                     log = self.logs[(t, p)]
                     codec = self.codec[(t, p)]
                     err = 76 if codec == 4 and ver < 10 else 0
+                    if off < self.log_start[(t, p)] or off > len(log):
+                        err = 1  # OFFSET_OUT_OF_RANGE
                     rs = b"" if err else self._record_set(log, off, codec)
                     w.i32(p).i16(err).i64(len(log)).i64(len(log))
                     if ver >= 5:

@@ -299,3 +299,17 @@ def test_per_record_consume_steps_over_control_batches():
     br = Log(K.encode_batch([b"\0\0\0\0"], base_offset=0, control=True))
     got, nxt = br.consume("requests", 0, 0, 10)
     assert got == [] and nxt == 1
+
+
+def test_fetch_below_the_retained_log_resumes_at_log_start():
+    fk = FakeKafka(default_partitions=1)
+    try:
+        br = K.KafkaBroker(fk.addr)
+        br.create_topic("trainingData", 1)
+        recs = [json.dumps({"i": i}).encode() for i in range(30)]
+        br.produce_batch("trainingData", 0, recs)
+        fk.log_start[("trainingData", 0)] = 10  # retention deleted offsets 0..9
+        got, nxt = br.consume("trainingData", 0, 0, 100)
+        assert got == recs[10:] and nxt == 30
+    finally:
+        fk.close()
