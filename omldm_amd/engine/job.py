@@ -173,11 +173,19 @@ class Job:
                 continue
             if req.request == "Create":
                 if net not in self.pipes:
-                    self.pipes[net] = Pipeline(req, self.space, self.comm, self.device,
-                                               self.spokes, self.cfg.parallelism,
-                                               self.cfg.maxMsgParams, store=self.store)
+                    try:
+                        self.pipes[net] = Pipeline(req, self.space, self.comm, self.device,
+                                                   self.spokes, self.cfg.parallelism,
+                                                   self.cfg.maxMsgParams, store=self.store)
+                    except (ValueError, TypeError, KeyError) as e:
+                        # an ill-typed configuration (every rank fails the same way): the
+                        # request is dropped and counted, the job goes on
+                        self._bad_request(req, e)
             elif req.request == "Update" and net in self.pipes:
-                self.pipes[net].update(req)
+                try:
+                    self.pipes[net].update(req)
+                except (ValueError, TypeError, KeyError) as e:
+                    self._bad_request(req, e)
             elif req.request == "Delete":
                 old = self.pipes.pop(net, None)
                 if old is not None:
@@ -185,6 +193,11 @@ class Job:
             elif req.request == "Query" and net in self.pipes:
                 queries.append(req)
         return len(msgs), queries
+
+    def _bad_request(self, req, err) -> None:
+        self.counters["invalid_requests"] = self.counters.get("invalid_requests", 0) + 1
+        if self.rank == 0:
+            print(f"[omldm] request {req.request} id={req.id} dropped: {err}", flush=True)
 
     # --------------------------------------------------------------------- data
     def _poll(self):

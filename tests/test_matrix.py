@@ -154,3 +154,52 @@ def test_orr_fused_polynomial_under_every_forwarding_protocol(protocol):
     """ORR + PolynomialFeatures fuses the degree-2 map into the Gram kernel (a PolyBatch
     reaches the learner); a protocol that regroups the batch must keep that kind."""
     _run("ORR", "PolynomialFeatures", True, "cpu", protocol)
+
+
+def test_hostile_requests_are_dropped_not_fatal():
+    """Malformed or ill-typed requests (reference: a malformed request kills the job,
+    RequestParser.scala:12-16; here it is dropped and counted) next to a valid one."""
+    name = uuid.uuid4().hex
+    addr = f"memory://{name}"
+    args = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        args += [f"--{k}", addr]
+    args += ["--hashDim", str(1 << 16), "--batchSize", "400", "--timeout", "200",
+             "--parallelism", "4", "--numFeatures", "5", "--catFeatures", "6"]
+    cfg = JobConfig.from_args(args)
+    sp = FeatureSpace(5, 0, 6, 1 << 16)
+    br = MemoryBroker.named(name)
+    br.create_topic(cfg.trainingDataTopic, 2)
+    job = Job(cfg, Comm(), "cpu")
+    hostile = [
+        "not json", "[]", "{}", '{"id": 1}', '{"id": "x", "request": "Create"}',
+        json.dumps({"id": 2, "request": "create", "learner": {"name": "SVM"}}),
+        json.dumps({"id": 3, "request": "Create"}),
+        json.dumps({"id": 4, "request": "Create", "learner": {"name": "Nope"}}),
+        json.dumps({"id": 5, "request": "Create", "learner": {"name": "SVM"},
+                    "preProcessors": [{"name": "Whitening"}]}),
+        json.dumps({"id": 6, "request": "Create", "learner": {"name": "SVM",
+                                                              "hyperParameters": [1, 2]}}),
+        json.dumps({"id": 7, "request": "Create", "learner": {"name": "SVM"},
+                    "trainingConfiguration": {"protocol": 42, "HubParallelism": "abc"}}),
+        json.dumps({"id": 8, "request": "Create", "learner": {"name": "NN",
+                                                              "hyperParameters": {"hiddenLayers": "big"}}}),
+        json.dumps({"id": 9, "request": "Query"}),
+        json.dumps({"id": 10, "request": "Delete"}),
+        json.dumps({"id": 11, "request": "Create", "learner": {"name": "PA"},
+                    "trainingConfiguration": {"protocol": "Synchronous"}}),
+    ]
+    for h in hostile:
+        br.produce("requests", h)
+    for r in synth_json_records(800, sp):
+        br.produce("trainingData", r)
+    for _ in range(4):
+        job.tick()
+    assert 11 in job.pipes  # the valid request went through
+    assert not job.terminated
+    br.produce("requests", json.dumps({"id": 11, "request": "Query", "requestId": 5}))
+    for _ in range(2):
+        job.tick()
+    resp = [json.loads(x) for x in br.records("responses")]
+    assert any(r.get("responseId") == 5 for r in resp)
