@@ -262,6 +262,16 @@ def test_four_rank_job_mixed_hub_layouts(tmp_path):
     _four_rank(tmp_path, "cpu")
 
 
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_four_rank_job_mixed_hub_layouts_gpu(tmp_path):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _four_rank(tmp_path, "cuda", {"OMLDM_DIST_BACKEND": "gloo"})
+
+
 def _four_rank(tmp_path, device, env=None):
     data = tmp_path / "topics"
     br = FileBroker(str(data))
