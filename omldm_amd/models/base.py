@@ -87,8 +87,21 @@ class Learner:
     def hyper_parameters(self) -> dict:
         return dict(self.hyper)
 
+    # hyper-parameters that fix the model's shape: an Update may not change them on a
+    # live pipeline (it is dropped and counted, like any invalid request)
+    STRUCTURAL: tuple = ()
+
     def update_hyper(self, hyper: dict) -> None:
-        self.hyper.update(hyper or {})
+        hyper = dict(hyper or {})
+        for k in self.STRUCTURAL:
+            if k in hyper and hyper[k] != self.hyper.get(k, hyper[k]):
+                raise ValueError(f"{self.NAME}: {k} cannot change on a live pipeline")
+        self.hyper.update(hyper)
+        self._retune()
+
+    def _retune(self) -> None:
+        """Re-read the tunable hyper-parameters after an Update (learning rates, margins,
+        split thresholds); the base learner has none."""
 
     def parameters_map(self) -> dict:
         return {}

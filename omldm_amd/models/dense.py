@@ -112,6 +112,7 @@ class KMeans(Learner):
     NAME = "K-means"
     TASK = "clustering"
     merge_mode = "mean"
+    STRUCTURAL = ("k",)
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -177,6 +178,13 @@ class MultiClassPA(Learner):
     NAME = "MultiClassPA"
     TASK = "classification"
     merge_mode = "mean"
+    STRUCTURAL = ("nClasses",)
+
+    def _retune(self) -> None:
+        v = str(self.hyper.get("variant", "PA-I"))
+        self.variant = {"PA": 0, "PA-I": 1, "PA-II": 2}.get(v, 1)
+        self.C = hp_float(self.hyper, "C", 1.0)
+        self.bias = bool(self.hyper.get("bias", True))
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -255,6 +263,17 @@ class NN(Learner):
     NAME = "NN"
     merge_mode = "mean"
     MB = D.MLP_MB
+    STRUCTURAL = ("hiddenLayers", "nClasses", "task", "seed")
+
+    def _retune(self) -> None:  # learning rate, activation and matmul precision
+        h = self.hyper
+        act = str(h.get("activation", "relu")).lower()
+        if act not in D.MLP_ACTS:
+            raise ValueError(f"NN activation must be one of {sorted(D.MLP_ACTS)}")
+        self.lr = hp_float(h, "learningRate", 0.05)
+        self.act_name, self.act = act, D.MLP_ACTS[act]
+        if str(h.get("matmulDtype", "fp32")).lower() in ("bf16", "bfloat16"):
+            self.act |= D.MLP_BF16
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -365,6 +384,12 @@ class HT(Learner):
 
     NAME = "HT"
     merge_mode = "mean"
+    STRUCTURAL = ("nClasses", "maxNodes", "maxDepth", "nBins")
+
+    def _retune(self) -> None:
+        self.grace = hp_int(self.hyper, "gracePeriod", 200)
+        self.delta = hp_float(self.hyper, "delta", 1e-7)
+        self.tau = hp_float(self.hyper, "tau", 0.05)
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)

@@ -203,3 +203,29 @@ def test_hostile_requests_are_dropped_not_fatal():
         job.tick()
     resp = [json.loads(x) for x in br.records("responses")]
     assert any(r.get("responseId") == 5 for r in resp)
+
+
+def test_update_retunes_or_rejects():
+    """Update changes tunable hyper-parameters of a live learner (learning rates, split
+    thresholds, margins) and is refused for shape-fixing ones (layer widths, classes, k),
+    which the engine then drops and counts (the reference's Update is a no-op)."""
+    from omldm_amd.models import make_learner
+
+    sp = FeatureSpace(5, 0, 6, 1 << 12)
+    nn = make_learner("NN", {"hiddenLayers": [8]}, sp, "cpu")
+    nn.update_hyper({"learningRate": 0.2, "activation": "tanh"})
+    assert nn.lr == 0.2 and nn.act_name == "tanh"
+    with pytest.raises(ValueError):
+        nn.update_hyper({"hiddenLayers": [16]})
+    ht = make_learner("HT", {"nClasses": 3}, sp, "cpu")
+    ht.update_hyper({"gracePeriod": 50, "delta": 1e-3})
+    assert ht.grace == 50 and ht.delta == 1e-3
+    with pytest.raises(ValueError):
+        ht.update_hyper({"nClasses": 4})
+    mc = make_learner("MultiClassPA", {"nClasses": 3}, sp, "cpu")
+    mc.update_hyper({"C": 0.25, "variant": "PA-II"})
+    assert mc.C == 0.25 and mc.variant == 2
+    km = make_learner("K-means", {"k": 4}, sp, "cpu")
+    km.update_hyper({"k": 4})  # unchanged value: accepted
+    with pytest.raises(ValueError):
+        km.update_hyper({"k": 5})
