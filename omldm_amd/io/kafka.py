@@ -509,12 +509,14 @@ class KafkaBroker(Broker):
     def end_offset(self, topic, partition):
         return self._list_offset(topic, partition, -1)
 
-    def _fetch(self, topic: str, partition: int, offset: int, max_bytes: int = 4 << 20) -> bytes:
-        """Raw record set of one partition from ``offset`` (Fetch v10 when the broker
-        offers it, else v4 — switching to v10 if it answers UNSUPPORTED_COMPRESSION_TYPE,
-        i.e. zstd data). An offset that retention already deleted (OFFSET_OUT_OF_RANGE
-        below the log start) resumes at the log start, as a consumer with
-        auto.offset.reset=earliest would."""
+    def _fetch(self, topic: str, partition: int, offset: int,
+               max_bytes: int = 4 << 20) -> tuple[bytes, int]:
+        """(raw record set, offset actually fetched from) of one partition (Fetch v10 when
+        the broker offers it, else v4 — switching to v10 if it answers
+        UNSUPPORTED_COMPRESSION_TYPE, i.e. zstd data). An offset that retention already
+        deleted (OFFSET_OUT_OF_RANGE below the log start) resumes at the log start, as a
+        consumer with auto.offset.reset=earliest would; the caller decodes from, and
+        advances past, the returned offset."""
         leader = self._metadata(topic).get(partition)
         conn = self._conn(leader)
         addr = self._addr(leader)
@@ -554,7 +556,7 @@ class KafkaBroker(Broker):
                     continue
             if err:
                 raise IOError(f"kafka fetch error {err}")
-            return out
+            return out, offset
         raise IOError(f"kafka fetch of {topic}/{partition} at {offset} failed")
 
     def consume(self, topic, partition, offset, max_records):
@@ -585,13 +587,20 @@ class KafkaBroker(Broker):
     def consume_into(self, topic, partition, offset, max_records, dst, cap):
         """Native path: the fetched record set is decoded (and decompressed) by
         csrc/host/kafka_wire.cpp straight into ``dst[:cap]`` — no per-record objects."""
-        data = self._fetch(topic, partition, offset, max_bytes=max(1 << 20, int(cap)))
-        return self._decode_into(data, offset, max_records, dst, cap)
+        data, offset = self._fetch(topic, partition, offset, max_bytes=max(1 << 20, int(cap)))
+        n, offs, nxt = self._decode_into(data, offset, max_records, dst, cap)
+        if n == 0 and nxt == offset and data and max_records > 0:
+            # nothing decoded, offset not moved, yet the broker returned records: the
+            # first record alone is larger than the destination — fail loudly instead of
+            # stalling the partition on the same fetch forever
+            raise IOError(f"kafka record at {topic}/{partition}@{offset} does not fit the "
+                          f"{cap}-byte ingest buffer (raise the staging capacity)")
+        return n, offs, nxt
 
     def consume_block(self, topic, partition, offset, max_records):
         import numpy as np
 
-        data = self._fetch(topic, partition, offset)
+        data, offset = self._fetch(topic, partition, offset)
         cap = max(len(data) * 4, 1 << 16)  # compressed sets inflate: grow if needed
         while True:
             buf = np.empty(cap, dtype=np.uint8)

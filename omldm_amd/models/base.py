@@ -91,17 +91,63 @@ class Learner:
     # live pipeline (it is dropped and counted, like any invalid request)
     STRUCTURAL: tuple = ()
 
+    def structural_values(self) -> dict:
+        """The shape-fixing values IN USE (not what Create happened to spell out), keyed
+        like the hyper-parameters, in the normalised form of ``_norm_structural``."""
+        return {}
+
+    @staticmethod
+    def _norm_structural(k: str, v):
+        """One comparable form per structural value: '[8, 8]' / [8, 8] / (8, 8) → (8, 8),
+        '4' / 4 / 4.0 → 4, anything else → its string."""
+        if isinstance(v, str):
+            t = v.strip()
+            if t.startswith("[") and t.endswith("]"):
+                try:
+                    return tuple(int(x) for x in t[1:-1].split(",") if x.strip())
+                except ValueError:
+                    return t
+            try:
+                f = float(t)
+                return int(f) if f == int(f) else f
+            except ValueError:
+                return t
+        if isinstance(v, (list, tuple)):
+            try:
+                return tuple(int(x) for x in v)
+            except (TypeError, ValueError):
+                return tuple(v)
+        if isinstance(v, bool):
+            return v
+        if isinstance(v, (int, float)):
+            return int(v) if float(v) == int(v) else float(v)
+        return str(v)
+
     def update_hyper(self, hyper: dict) -> None:
+        """Apply an Update atomically: the merged hyper-parameters are validated and the
+        derived settings rebuilt first; on any error the learner is left exactly as it
+        was (nothing of a rejected Update is applied), and the error propagates so the
+        engine drops and counts the request."""
         hyper = dict(hyper or {})
+        cur = self.structural_values()
         for k in self.STRUCTURAL:
-            if k in hyper and hyper[k] != self.hyper.get(k, hyper[k]):
+            if k in hyper and k in cur and \
+                    self._norm_structural(k, hyper[k]) != self._norm_structural(k, cur[k]):
                 raise ValueError(f"{self.NAME}: {k} cannot change on a live pipeline")
-        self.hyper.update(hyper)
-        self._retune()
+        saved = dict(self.__dict__)  # shallow: _retune rebinds, never mutates in place
+        self.hyper = {**self.hyper, **hyper}
+        try:
+            self._retune()
+        except Exception:
+            self.__dict__.clear()
+            self.__dict__.update(saved)
+            raise
 
     def _retune(self) -> None:
-        """Re-read the tunable hyper-parameters after an Update (learning rates, margins,
-        split thresholds); the base learner has none."""
+        """Re-read the tunable hyper-parameters after an Update or a restore (learning
+        rates, margins, split thresholds); the base learner has none. Must rebind
+        attributes rather than mutate tensors in place (update_hyper rolls back by
+        restoring the attribute dict)."""
 
     def parameters_map(self) -> dict:
         return {}
@@ -116,6 +162,7 @@ class Learner:
 
     def load_state_dict(self, sd: dict) -> None:
         self.hyper.update(sd.get("hyper", {}))
+        self._retune()  # the restored (possibly Updated) settings, not Create's
         self.load_state_vector(sd["state"].to(self.device))
         if "cum" in sd:
             self.cum.copy_(sd["cum"].to(self.device, torch.float64))

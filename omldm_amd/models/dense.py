@@ -88,9 +88,11 @@ class ORR(Learner):
         se = (e * e).sum()
         return se, se, int(ok.sum())
 
-    def update_hyper(self, hyper):
-        super().update_hyper(hyper)
-        self.lam = hp_float(self.hyper, "lambda", self.lam)
+    def _retune(self):
+        lam = hp_float(self.hyper, "lambda", 1.0)
+        if not lam >= 0:
+            raise ValueError("ORR lambda must be >= 0")
+        self.lam = lam
         self._w = None
 
     def parameters_map(self):
@@ -113,6 +115,9 @@ class KMeans(Learner):
     TASK = "clustering"
     merge_mode = "mean"
     STRUCTURAL = ("k",)
+
+    def structural_values(self):
+        return {"k": self.k}
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -180,10 +185,16 @@ class MultiClassPA(Learner):
     merge_mode = "mean"
     STRUCTURAL = ("nClasses",)
 
+    def structural_values(self):
+        return {"nClasses": self.K}
+
     def _retune(self) -> None:
         v = str(self.hyper.get("variant", "PA-I"))
+        C = hp_float(self.hyper, "C", 1.0)
+        if not C > 0:
+            raise ValueError("MultiClassPA C must be > 0")
         self.variant = {"PA": 0, "PA-I": 1, "PA-II": 2}.get(v, 1)
-        self.C = hp_float(self.hyper, "C", 1.0)
+        self.C = C
         self.bias = bool(self.hyper.get("bias", True))
 
     def __init__(self, hyper, space, device="cpu"):
@@ -193,10 +204,7 @@ class MultiClassPA(Learner):
         self.W = torch.zeros((self.K, self.dim), dtype=torch.float32, device=self.device)
         self.dacc = torch.zeros_like(self.W)
         self.st = torch.zeros(8, dtype=torch.float32, device=self.device)
-        v = str(self.hyper.get("variant", "PA-I"))
-        self.variant = {"PA": 0, "PA-I": 1, "PA-II": 2}.get(v, 1)
-        self.C = hp_float(self.hyper, "C", 1.0)
-        self.bias = bool(self.hyper.get("bias", True))
+        self._retune()
         # GPU: key-major prototype shadow for the round's gathers (fp32, or bf16 with
         # modelDtype=bf16), refreshed by the apply pass and on every state load
         self.Wt = None
@@ -265,6 +273,10 @@ class NN(Learner):
     MB = D.MLP_MB
     STRUCTURAL = ("hiddenLayers", "nClasses", "task", "seed")
 
+    def structural_values(self):
+        return {"hiddenLayers": list(self.widths[1:-1]), "nClasses": self.K,
+                "task": self.TASK, "seed": self.seed}
+
     def _retune(self) -> None:  # learning rate, activation and matmul precision
         h = self.hyper
         act = str(h.get("activation", "relu")).lower()
@@ -296,6 +308,7 @@ class NN(Learner):
         # instead of K/2; default fp32 keeps DL4J's fp32 arithmetic
         if str(h.get("matmulDtype", "fp32")).lower() in ("bf16", "bfloat16"):
             self.act |= D.MLP_BF16
+        self.seed = hp_int(h, "seed", 25)
         self.widths = [self.d] + [int(v) for v in hidden] + [max(1, self.K)]
         if len(self.widths) - 1 > D.MLP_MAX_LAYERS:
             raise ValueError(f"NN supports at most {D.MLP_MAX_LAYERS} layers")
@@ -303,7 +316,7 @@ class NN(Learner):
         for a, b in zip(self.widths[:-1], self.widths[1:]):
             self.shapes += [(b, a), (b,)]
         total = sum(math.prod(s) for s in self.shapes)
-        g = torch.Generator().manual_seed(hp_int(h, "seed", 25))
+        g = torch.Generator().manual_seed(self.seed)
         flat = torch.zeros(total, dtype=torch.float32)
         o = 0
         for s in self.shapes:
@@ -385,6 +398,10 @@ class HT(Learner):
     NAME = "HT"
     merge_mode = "mean"
     STRUCTURAL = ("nClasses", "maxNodes", "maxDepth", "nBins")
+
+    def structural_values(self):
+        return {"nClasses": self.Cn, "maxNodes": self.N, "maxDepth": self.depth,
+                "nBins": self.nb}
 
     def _retune(self) -> None:
         self.grace = hp_int(self.hyper, "gracePeriod", 200)

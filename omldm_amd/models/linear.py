@@ -71,8 +71,7 @@ class LinearLearner(Learner):
         elif not want16:
             self.w16 = None
 
-    def update_hyper(self, hyper: dict) -> None:
-        super().update_hyper(hyper)
+    def _retune(self) -> None:
         self._configure()
 
     # ---------------------------------------------------------- model store rows
@@ -123,7 +122,6 @@ class LinearLearner(Learner):
 
     def load_state_dict(self, sd: dict) -> None:
         super().load_state_dict(sd)
-        self._configure()
         self.steps = int(sd.get("steps", self.steps))
 
     # ------------------------------------------------------------ protocol view

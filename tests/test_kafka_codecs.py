@@ -181,7 +181,7 @@ def test_consume_block_steps_over_a_lone_control_batch():
             self.data = data
 
         def _fetch(self, topic, partition, offset, max_bytes=4 << 20):
-            return self.data
+            return self.data, offset
 
     br = OneShot(K.encode_batch([b"\0\0\0\0"], base_offset=3, control=True))
     buf, offs, nxt = br.consume_block("t", 0, 3, 100)
@@ -289,7 +289,7 @@ def test_per_record_consume_steps_over_control_batches():
             self.data = data
 
         def _fetch(self, topic, partition, offset, max_bytes=4 << 20):
-            return self.data
+            return self.data, offset
 
     vals = [b'{"id": 1}', b'{"id": 2}']
     br = Log(K.encode_batch([b"\0\0\0\0"], base_offset=0, control=True)
@@ -313,3 +313,36 @@ def test_fetch_below_the_retained_log_resumes_at_log_start():
         assert got == recs[10:] and nxt == 30
     finally:
         fk.close()
+
+
+def test_empty_retained_log_advances_to_log_start():
+    """A fetch below a fully-deleted log moves the consumer to the log start for good
+    (the next poll must not repeat the failing Fetch + ListOffsets)."""
+    class Gone(K.KafkaBroker):
+        def __init__(self):
+            self.calls = 0
+
+        def _fetch(self, topic, partition, offset, max_bytes=4 << 20):
+            self.calls += 1
+            return b"", max(offset, 40)  # retention deleted [0, 40): empty log from 40
+
+    br = Gone()
+    buf = np.empty(1 << 16, dtype=np.uint8)
+    n, offs, nxt = br.consume_into("t", 0, 5, 10, buf, 1 << 16)
+    assert n == 0 and nxt == 40
+    n, offs, nxt = br.consume_into("t", 0, nxt, 10, buf, 1 << 16)
+    assert n == 0 and nxt == 40
+
+
+def test_consume_into_oversize_record_raises():
+    class One(K.KafkaBroker):
+        def __init__(self, data):
+            self.data = data
+
+        def _fetch(self, topic, partition, offset, max_bytes=4 << 20):
+            return self.data, offset
+
+    br = One(K.encode_batch([b"z" * 5000], base_offset=0))
+    buf = np.empty(1024, dtype=np.uint8)
+    with pytest.raises(IOError, match="does not fit"):
+        br.consume_into("t", 0, 0, 10, buf, 1024)

@@ -229,3 +229,80 @@ def test_update_retunes_or_rejects():
     km.update_hyper({"k": 4})  # unchanged value: accepted
     with pytest.raises(ValueError):
         km.update_hyper({"k": 5})
+
+
+def test_rejected_update_is_not_partially_applied():
+    """Update {variant: Pegasos, lambda: 0} used to leave the Pegasos rule with
+    λ = 0 behind (the next round failed); NN 'bogus' activation stayed in hyper."""
+    import torch
+
+    from omldm_amd.api.batch import FeatureSpace as FS
+    from omldm_amd.io.synthetic import synth_batch
+    from omldm_amd.models import make_learner
+    from omldm_amd.models.base import RoundContext
+
+    sp = FS(5, 0, 6, 1 << 12)
+    svm = make_learner("SVM", {"variant": "PA-I"}, sp, "cpu")
+    with pytest.raises(ValueError):
+        svm.update_hyper({"variant": "Pegasos", "lambda": 0})
+    assert svm.hyper_parameters()["variant"] == "PA-I"
+    assert "lambda" not in svm.hyper or svm.hyper["lambda"] != 0
+    b = synth_batch(sp, 64, seed=3)
+    svm.fit(b, RoundContext(spokes=2, inv_p=0.5))  # still trains (PA-I)
+    sd = svm.state_dict()
+    svm2 = make_learner("SVM", {"variant": "PA-I"}, sp, "cpu")
+    svm2.load_state_dict(sd)
+    svm2.fit(b, RoundContext(spokes=2, inv_p=0.5))
+    nn = make_learner("NN", {"hiddenLayers": [8]}, sp, "cpu")
+    with pytest.raises(ValueError):
+        nn.update_hyper({"activation": "bogus", "learningRate": 0.5})
+    assert nn.act_name == "relu" and nn.lr == 0.05
+    assert "activation" not in nn.hyper and "learningRate" not in nn.hyper
+    assert torch.isfinite(nn.flat).all()
+
+
+def test_restore_keeps_updated_tunables():
+    """after Update → checkpoint → restore, the restored learner trains with
+    the Updated settings (not Create's) for every learner kind with tunables."""
+    from omldm_amd.models import make_learner
+
+    sp = FeatureSpace(5, 0, 6, 1 << 12)
+    cases = [("NN", {"hiddenLayers": [8]}, {"learningRate": 0.2, "activation": "tanh"},
+              lambda m: (m.lr, m.act_name) == (0.2, "tanh")),
+             ("HT", {"nClasses": 3}, {"gracePeriod": 50, "tau": 0.2},
+              lambda m: (m.grace, m.tau) == (50, 0.2)),
+             ("MultiClassPA", {"nClasses": 3}, {"C": 0.25, "variant": "PA-II"},
+              lambda m: (m.C, m.variant) == (0.25, 2)),
+             ("ORR", {}, {"lambda": 3.0}, lambda m: m.lam == 3.0),
+             ("PA", {}, {"C": 0.5, "variant": "PA-II"},
+              lambda m: (m.rule.C, m.rule.variant) == (0.5, 2))]
+    for name, create, upd, check in cases:
+        a = make_learner(name, dict(create), sp, "cpu")
+        a.update_hyper(upd)
+        assert check(a), name
+        b = make_learner(name, dict(create), sp, "cpu")
+        b.load_state_dict(a.state_dict())
+        assert check(b), name
+
+
+def test_structural_check_uses_values_in_use():
+    """keys Create left at their default must still be refused when changed,
+    and equal values in another spelling ('[8]' vs [8], '4' vs 4) are accepted."""
+    from omldm_amd.models import make_learner
+
+    sp = FeatureSpace(5, 0, 6, 1 << 12)
+    nn = make_learner("NN", {}, sp, "cpu")          # hiddenLayers default [32, 32]
+    with pytest.raises(ValueError):
+        nn.update_hyper({"hiddenLayers": [8]})
+    nn.update_hyper({"hiddenLayers": "[32, 32]"})   # same shape: accepted
+    km = make_learner("K-means", {}, sp, "cpu")     # k default 8
+    with pytest.raises(ValueError):
+        km.update_hyper({"k": 3})
+    km.update_hyper({"k": "8"})
+    ht = make_learner("HT", {}, sp, "cpu")
+    for k, v in (("nClasses", 5), ("maxNodes", 7), ("maxDepth", 3), ("nBins", 4)):
+        with pytest.raises(ValueError):
+            ht.update_hyper({k: v})
+    mc = make_learner("MultiClassPA", {}, sp, "cpu")  # nClasses default 2
+    with pytest.raises(ValueError):
+        mc.update_hyper({"nClasses": 4})
