@@ -21,57 +21,15 @@
 #include <thread>
 #include <vector>
 
+#include "hashing.h"
+
 #define OMLDM_HOST_API extern "C" __attribute__((visibility("default")))
 
 namespace {
 
-inline uint32_t rotl32(uint32_t x, int8_t r) { return (x << r) | (x >> (32 - r)); }
-
-uint32_t murmur3_32(const uint8_t* data, size_t len, uint32_t seed) {
-  const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
-  uint32_t h1 = seed;
-  const size_t nblocks = len / 4;
-  for (size_t i = 0; i < nblocks; ++i) {
-    uint32_t k1;
-    std::memcpy(&k1, data + i * 4, 4);
-    k1 *= c1;
-    k1 = rotl32(k1, 15);
-    k1 *= c2;
-    h1 ^= k1;
-    h1 = rotl32(h1, 13);
-    h1 = h1 * 5 + 0xe6546b64u;
-  }
-  const uint8_t* tail = data + nblocks * 4;
-  uint32_t k1 = 0;
-  switch (len & 3) {
-    case 3: k1 ^= uint32_t(tail[2]) << 16; [[fallthrough]];
-    case 2: k1 ^= uint32_t(tail[1]) << 8; [[fallthrough]];
-    case 1:
-      k1 ^= tail[0];
-      k1 *= c1;
-      k1 = rotl32(k1, 15);
-      k1 *= c2;
-      h1 ^= k1;
-  }
-  h1 ^= uint32_t(len);
-  h1 ^= h1 >> 16;
-  h1 *= 0x85ebca6bu;
-  h1 ^= h1 >> 13;
-  h1 *= 0xc2b2ae35u;
-  h1 ^= h1 >> 16;
-  return h1;
-}
-
-constexpr uint32_t kSeedBase = 0x9747b28cu;
-
-// Categorical token → signed slot. Field j gets its own seed so identical strings in
-// different fields land in different slots.
-inline int32_t hash_cat(const uint8_t* s, size_t n, int field, int dn, int64_t dim) {
-  const uint32_t h = murmur3_32(s, n, kSeedBase + uint32_t(field));
-  const int64_t span = dim - dn - 1;  // slot dim-1 is reserved for the intercept
-  const int32_t slot = int32_t(dn + int64_t(h & 0x7fffffffu) % span);
-  return (h & 0x80000000u) ? int32_t(uint32_t(slot) | 0x80000000u) : slot;
-}
+using omldm_hash::hash_cat;
+using omldm_hash::kSeedBase;
+using omldm_hash::murmur3_32;
 
 // Field-aware compact form: field f owns slots [dn + f·cspan, dn + (f+1)·cspan), the wire
 // value is uint16 {sign:1, local:15} (0xFFFF = absent), cspan ≤ 32767.

@@ -12,10 +12,13 @@
 // fails the checksum and is simply re-polled. The wave scores the point against M models
 // (same feature decoding as the training kernel) and publishes scores + the completion
 // sequence with system-scope stores. No kernel launch or stream sync per request.
+// cspan < 0: the request carries raw 32-bit category tokens (the binary wire), hashed by
+// the wave itself (hash_dev.h) — the same hash as the training round.
 //
 // Safety: the wave exits on the stop word or after `lifetime_us` of wall time
 // (s_memrealtime, 100 MHz), whichever comes first; every spin is bounded by it.
 #include "common.h"
+#include "hash_dev.h"
 
 #include <chrono>
 #include <cstdlib>
@@ -118,7 +121,13 @@ __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, lon
       v = __uint_as_float(fj);
     } else if (j < nf) {
       const int c = (int)fj;
-      if (cspan > 0) {
+      if (cspan < 0) {  // raw binary wire: the 32-bit category token, hashed here
+        const int code = hash_token_dev(fj, j - dn, dn, (uint32_t)(dim - dn - 1));
+        if (code != -1) {
+          idx = code & 0x7fffffff;
+          v = code < 0 ? -1.f : 1.f;
+        }
+      } else if (cspan > 0) {
         const unsigned u = (unsigned)c & 0xFFFFu;
         if (u != 0xFFFFu) {
           idx = dn + (j - dn) * cspan + (int)(u & 0x7fffu);

@@ -208,3 +208,66 @@ class PolyBatch(HashedBatch):
         num = poly_expand(x, self.pairs) if self.B else torch.zeros(
             (0, x.shape[1] + self.pairs.shape[0]), dtype=torch.float32, device=x.device)
         return HashedBatch(num, self.cat, self.y, self.raw, self.cat_span)
+
+
+ABSENT_TOKEN = 0xFFFFFFFF
+
+
+@dataclass
+class RawBatch:
+    """A micro-batch on the raw binary wire: categorical values travel as 32-bit token
+    ids and are hashed on the device inside the training kernel (csrc/kernels/
+    linear_seq.hip), so feature hashing is part of the timed hot path.
+
+    * ``num`` [B, dn] float32 — numerical then discrete features
+    * ``tok`` [B, dc] int32   — raw token id per field (bit pattern of a uint32;
+      0xFFFFFFFF = absent); hashed like ``hash_cat`` of its 4 little-endian bytes
+    * ``y``   [B]     float32 (NaN = no target) or int8 (±1 classification labels)
+    """
+
+    num: torch.Tensor
+    tok: torch.Tensor
+    y: torch.Tensor
+
+    @property
+    def B(self) -> int:
+        return int(self.y.shape[0])
+
+    @property
+    def dn(self) -> int:
+        return int(self.num.shape[1])
+
+    @property
+    def dc(self) -> int:
+        return int(self.tok.shape[1])
+
+    @property
+    def device(self):
+        return self.y.device
+
+    def __len__(self):
+        return self.B
+
+    @staticmethod
+    def empty(space: FeatureSpace, B: int = 0, device="cpu", pin: bool = False,
+              y_dtype=torch.float32) -> "RawBatch":
+        kw = dict(device=device)
+        if pin and torch.cuda.is_available():
+            kw["pin_memory"] = True
+        return RawBatch(torch.zeros((B, space.dn), dtype=torch.float32, **kw),
+                        torch.full((B, space.dc), -1, dtype=torch.int32, **kw),
+                        torch.zeros((B,), dtype=y_dtype, **kw))
+
+    def to(self, device, non_blocking: bool = False) -> "RawBatch":
+        return RawBatch(self.num.to(device, non_blocking=non_blocking),
+                        self.tok.to(device, non_blocking=non_blocking),
+                        self.y.to(device, non_blocking=non_blocking))
+
+    def slice(self, a: int, b: int) -> "RawBatch":
+        return RawBatch(self.num[a:b], self.tok[a:b], self.y[a:b])
+
+    def hashed(self, space: FeatureSpace) -> HashedBatch:
+        """The wide hashed form (int32 signed slots) every learner reads."""
+        from omldm_amd.ops.ingest import hash_raw
+
+        return HashedBatch(self.num, hash_raw(self.tok, space), self.y.float(), None, 0)

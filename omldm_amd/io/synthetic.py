@@ -14,7 +14,7 @@ import os
 import numpy as np
 import torch
 
-from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.api.batch import FeatureSpace, HashedBatch, RawBatch
 from omldm_amd.ops import native
 from omldm_amd.ops.native import ptr
 
@@ -32,6 +32,22 @@ def synth_batch(space: FeatureSpace, B: int, start: int = 0, seed: int = 25, tas
     native.host().omldm_synth_batch(seed, start, B, space.dn, space.dc, space.dim, task,
                                     n_classes, noise, space.cat_span, ptr(out.num), ptr(out.cat),
                                     ptr(out.y), threads)
+    return out
+
+
+def synth_raw(space: FeatureSpace, B: int, start: int = 0, seed: int = 25, task: int = 0,
+              n_classes: int = 4, noise: float = 0.1, missing: float = 0.0, pin: bool = False,
+              out: RawBatch | None = None, threads: int | None = None) -> RawBatch:
+    """Criteo-shaped stream on the raw binary wire (csrc/host/rawwire.cpp:
+    omldm_synth_raw): categorical values are 32-bit token ids, labels come from a hidden
+    model over (field, token). Example i is a pure function of (seed, start + i)."""
+    if out is None:
+        out = RawBatch.empty(space, B, pin=pin)
+    assert out.B == B and out.num.dtype == torch.float32 and out.tok.dtype == torch.int32
+    assert out.y.dtype == torch.float32 and not out.y.is_cuda
+    threads = threads or min(16, os.cpu_count() or 1)
+    native.host().omldm_synth_raw(seed, start, B, space.dn, space.dc, task, n_classes, noise,
+                                  missing, ptr(out.num), ptr(out.tok), ptr(out.y), threads)
     return out
 
 

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import torch
 
-from omldm_amd.api.batch import FeatureSpace, HashedBatch
+from omldm_amd.api.batch import FeatureSpace, HashedBatch, RawBatch
 from omldm_amd.models.base import Learner, RoundContext, hp_float, hp_int
 from omldm_amd.ops import linear as L
 
@@ -42,6 +42,11 @@ class LinearLearner(Learner):
         self.w = torch.zeros(self.dim, dtype=torch.float32, device=self.device)
         self.w16 = None
         self.dacc = torch.zeros(self.dim + 2, dtype=torch.float32, device=self.device)
+        # raw-wire rounds on the GPU: per-spoke fp32 replicas [S, dim] (linear_seq.hip),
+        # equal to w between rounds; invalidated whenever w changes outside a round
+        self.replicas = None
+        self._rep_valid = False
+        self._seq_pending = False
         self._configure()
 
     def _configure(self) -> None:
@@ -79,9 +84,11 @@ class LinearLearner(Learner):
         """Re-point the fp32 weights at a row of the HBM model store (engine/model_store.py);
         ``row`` already holds the current weights."""
         self.w = row
+        self._rep_valid = False
 
     def detach(self) -> None:
         self.w = self.w.clone()
+        self._rep_valid = False
 
     def vector_bias(self) -> tuple[torch.Tensor, float]:
         """The reference's ``VectorBias(weights, bias)`` view: the
@@ -92,7 +99,42 @@ class LinearLearner(Learner):
     def _wread(self) -> torch.Tensor:
         return self.w16 if self.w16 is not None else self.w
 
+    def seq_capable(self) -> bool:
+        """Raw-wire rounds run the exact sequential Gram-scan kernel (PA family, RegressorPA,
+        logistic SGD without L2); other rules hash the batch and take the spoke-table path."""
+        return self.rule.rule in L.SEQ_RULES and self.rule.lam == 0.0 and self.w16 is None
+
+    def _fit_raw(self, batch: RawBatch, ctx: RoundContext) -> None:
+        B = batch.B
+        S = max(1, int(ctx.spokes))
+        R = max(1, -(-B // S)) if B else 1
+        S = max(1, -(-B // R)) if B else S
+        on_gpu = self.w.is_cuda
+        if on_gpu:
+            if self.replicas is None or self.replicas.shape[0] < S:
+                self.replicas = torch.empty((S, self.dim), dtype=torch.float32, device=self.device)
+                self._rep_valid = False
+            if not self._rep_valid:
+                L.linear_seq_broadcast(self.w, self.replicas)
+                self._rep_valid = True
+        if B:
+            L.linear_seq_round(self.w, batch, R, S, self.dacc, self.rule, ctx.inv_p,
+                               cum=self.cum, replicas=self.replicas if on_gpu else None)
+        else:
+            self.dacc[self.dim:].zero_()
+        self._seq_pending = on_gpu
+        if ctx.on_reduce_part is not None:
+            parts = max(1, int(ctx.reduce_parts))
+            for k in range(parts):
+                ctx.on_reduce_part(k, *L.part_bounds(self.dim, k, parts, self.dacc.is_cuda))
+        if not ctx.fused_delta:
+            self.apply_delta()
+
     def fit(self, batch: HashedBatch, ctx: RoundContext) -> None:
+        if isinstance(batch, RawBatch):
+            if self.seq_capable():
+                return self._fit_raw(batch, ctx)
+            batch = batch.hashed(self.space)
         B = batch.B
         S = max(1, int(ctx.spokes))
         R = max(1, -(-B // S)) if B else 1
@@ -115,7 +157,13 @@ class LinearLearner(Learner):
         return self.dacc
 
     def apply_delta(self) -> None:
+        if self._seq_pending and self.replicas is not None:
+            # average + refresh every replica in one pass (they stay equal to w)
+            L.linear_seq_apply(self.w, self.replicas, self.dacc)
+            self._seq_pending = False
+            return
         L.linear_apply(self.w, self.w16, self.dacc)
+        self._rep_valid = False
 
     def state_dict(self) -> dict:
         return {**super().state_dict(), "steps": self.steps}
@@ -129,6 +177,7 @@ class LinearLearner(Learner):
         return self.w
 
     def on_state_loaded(self) -> None:
+        self._rep_valid = False
         if self.w16 is not None:
             self.w16.copy_(self.w)
 

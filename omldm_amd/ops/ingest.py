@@ -7,6 +7,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from omldm_amd.ops import native
@@ -209,3 +211,19 @@ class GpuJsonParser:
             json_parse(dbuf, doffs, n, space, num, cat, y, op, counts,
                        torch.cuda.current_stream(dev).cuda_stream)
         return HashedBatch(num, cat, y, RawView(buf, offs), space.cat_span), op, counts
+
+
+def hash_raw(tok: torch.Tensor, space) -> torch.Tensor:
+    """Raw token ids [B, dc] → wide hashed slots [B, dc] int32 (sign in bit 31, -1 =
+    absent), the csrc/host/hashing.h function on CPU and on the device."""
+    assert tok.dtype == torch.int32 and tok.is_contiguous()
+    out = torch.empty_like(tok)
+    B, dc = tok.shape
+    if tok.is_cuda:
+        native.check(native.hip().omldm_hash_raw(native.ptr(tok), B, dc, space.dn, space.dim,
+                                                 native.ptr(out), native.stream_of(tok)),
+                     "omldm_hash_raw")
+    else:
+        native.host().omldm_cpu_hash_raw(native.ptr(tok), B, dc, space.dn, space.dim,
+                                     native.ptr(out), min(16, os.cpu_count() or 1))
+    return out

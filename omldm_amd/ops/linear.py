@@ -11,7 +11,7 @@ from dataclasses import dataclass
 
 import torch
 
-from omldm_amd.api.batch import HashedBatch
+from omldm_amd.api.batch import HashedBatch, RawBatch
 from omldm_amd.ops import native
 from omldm_amd.ops.native import check, ptr
 
@@ -202,3 +202,68 @@ def linear_predict(w: torch.Tensor, batch: HashedBatch, wscale: torch.Tensor | N
                                                ptr(batch.cat), batch.cat.shape[1], B, dim,
                                                int(bias), batch.cat_span, ptr(wscale), ptr(out))
     return out.view(B) if single else out
+
+
+# ------------------------------------------------------------------ raw-wire sequential round
+SEQ_RULES = (RULE_HINGE, RULE_EPS, RULE_LOGISTIC)
+
+
+def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
+                     rule: LinearRule, inv_p: float, cum: torch.Tensor | None = None,
+                     stats: torch.Tensor | None = None, replicas: torch.Tensor | None = None
+                     ) -> None:
+    """One Synchronous round on the raw binary wire: S spokes, spoke s an exact
+    sequential learner (the reference's per-example fit, FlinkSpoke.scala:92-107) over
+    rows [s·R, (s+1)·R) on its own replica of w; tokens are hashed inside the round.
+
+    Accumulates like ``linear_round`` (dacc[:dim] += Δ_s·inv_p, dacc[dim] and
+    dacc[dim+1] += inv_p per active spoke), so ``linear_apply`` averages the replicas.
+    GPU: csrc/kernels/linear_seq.hip (Gram-scan on the matrix cores, one workgroup per
+    spoke; ``replicas`` is its [S, dim] fp32 scratch, allocated here if None).
+    CPU: csrc/host/rawwire.cpp (the golden oracle)."""
+    dim = int(dacc.shape[0]) - 2
+    assert w.shape[0] == dim and w.dtype == torch.float32 and dacc.dtype == torch.float32
+    assert rule.rule in SEQ_RULES and rule.lam == 0.0, "seq round: PA family / logistic, no L2"
+    num, tok, y = batch.num, batch.tok, batch.y
+    assert num.dtype == torch.float32 and tok.dtype == torch.int32
+    assert y.dtype == torch.float32 or (y.dtype == torch.int8 and rule.rule != RULE_EPS)
+    assert num.is_contiguous() and tok.is_contiguous() and y.is_contiguous()
+    assert cum is None or cum.dtype == torch.float64
+    if S <= 0 or batch.B == 0:
+        return
+    if w.is_cuda:
+        assert all(t.is_cuda for t in (num, tok, y)) and dacc.is_cuda
+        ws = _workspace(w.device, S * WS_STAT, key="seq_ws")
+        if replicas is None:
+            replicas = _workspace(w.device, S * dim, key="seq_replicas")
+        rc = native.hip().omldm_linear_seq_round(
+            ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
+            int(y.dtype == torch.int8), batch.B, R, S, ptr(replicas), ptr(dacc), dim, ptr(ws),
+            ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, inv_p, int(rule.bias),
+            native.stream_of(w))
+        check(rc, "omldm_linear_seq_round")
+        if stats is not None:
+            stats.copy_(ws[: S * WS_STAT].view(S, WS_STAT)[:, :STAT_W])
+    else:
+        st = stats if stats is not None else torch.zeros((S, STAT_W), dtype=torch.float32)
+        native.host().omldm_cpu_linear_seq_round(
+            ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
+            int(y.dtype == torch.int8), batch.B, R, S, ptr(dacc), dim, ptr(st), rule.rule,
+            rule.variant, rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), _cpu_threads())
+        if cum is not None:
+            cum[:STAT_W] += st.sum(0).double()
+            cum[4] -= st[:, 4].sum().double()
+
+
+def linear_seq_apply(w: torch.Tensor, replicas: torch.Tensor, dacc: torch.Tensor) -> None:
+    """GPU: w = model average of the (all-reduced) round accumulator, every replica ← w,
+    dacc ← 0 (one pass over HBM)."""
+    check(native.hip().omldm_linear_seq_apply(ptr(w), ptr(replicas), int(replicas.shape[0]),
+                                              ptr(dacc), int(w.shape[0]), native.stream_of(w)),
+          "omldm_linear_seq_apply")
+
+
+def linear_seq_broadcast(w: torch.Tensor, replicas: torch.Tensor) -> None:
+    check(native.hip().omldm_linear_seq_broadcast(ptr(w), ptr(replicas), int(replicas.shape[0]),
+                                                  int(w.shape[0]), native.stream_of(w)),
+          "omldm_linear_seq_broadcast")

@@ -51,6 +51,11 @@ HIP_SIGS = [
     ("omldm_linear_predict", i32, [vp, i32, i64, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32,
                                    vp, vp, vp]),
     ("omldm_linear_apply", i32, [vp, vp, vp, i32, vp]),
+    ("omldm_linear_seq_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32,
+                                     vp, vp, i32, i32, f32, f32, f32, f32, i32, vp]),
+    ("omldm_linear_seq_apply", i32, [vp, vp, i32, vp, i32, vp]),
+    ("omldm_linear_seq_broadcast", i32, [vp, vp, i32, i32, vp]),
+    ("omldm_hash_raw", i32, [vp, i64, i32, i32, i64, vp, vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
     ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
@@ -121,6 +126,10 @@ HOST_SIGS = [
                                          f32, i32, vp, vp]),
     ("omldm_cpu_linear_predict", None, [vp, i64, i32, vp, i32, vp, i32, i32, i32, i32, i32, vp,
                                         vp]),
+    ("omldm_synth_raw", None, [u64, i64, i32, i32, i32, i32, i32, f32, f32, vp, vp, vp, i32]),
+    ("omldm_cpu_hash_raw", None, [vp, i64, i32, i32, i64, vp, i32]),
+    ("omldm_cpu_linear_seq_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, i32,
+                                         vp, i32, i32, f32, f32, f32, f32, i32, i32]),
 ]
 
 

@@ -151,6 +151,9 @@ class Synchronous(Protocol):
         # (RCCL works on range k while the GPU reduces range k+1). Same sums, same
         # collectives on every rank; only with every rank a hub (all-reduce).
         self.reduce_parts = max(1, _cfg_int(self.cfg, "reduceParts", 1))
+        # benchmarks: CUDA events around every round's collective (collective_time_ms)
+        self.time_collectives = False
+        self._coll_events: list = []
 
     # The round is split in two so the engine can coalesce the collectives of several
     # pipelines into one bucket: local() trains and returns the buffer to
@@ -206,8 +209,24 @@ class Synchronous(Protocol):
             self.finish()
             return
         buf = self.local(batch)
-        self.comm.hub_reduce_(buf, self.hubs, tag="sync")
+        if self.time_collectives and buf.is_cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.comm.hub_reduce_(buf, self.hubs, tag="sync")
+            e1.record()
+            self._coll_events.append((e0, e1))
+        else:
+            self.comm.hub_reduce_(buf, self.hubs, tag="sync")
         self.finish()
+
+    def collective_time_ms(self) -> float:
+        """Device time of the collectives timed since the last call (synchronises)."""
+        if not self._coll_events:
+            return 0.0
+        self._coll_events[-1][1].synchronize()
+        t = sum(a.elapsed_time(b) for a, b in self._coll_events)
+        self._coll_events.clear()
+        return t
 
     def state_dict(self):
         sd = super().state_dict()
