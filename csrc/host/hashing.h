@@ -60,13 +60,24 @@ inline int32_t hash_cat(const uint8_t* s, size_t n, int field, int dn, int64_t d
 }
 
 // Raw binary wire: a categorical value is a 32-bit token id (0xFFFFFFFF = absent),
-// hashed as its 4 little-endian bytes — identical to hash_cat of those 4 bytes.
+// murmur3-hashed as its 4 little-endian bytes with the field's seed, FIELD-AWARE: field f
+// owns the slot range [dn + f·span, dn + (f+1)·span), span = (dim − dn − 1) / dc (at
+// 2^20 dims and 26 fields: 40,329 slots per field, 99.999 % of the model used). Equal
+// slots therefore always come from the same field — what lets the GPU round group a
+// chunk's shared values field by field without atomics (csrc/kernels/linear_seq.hip).
 constexpr uint32_t kAbsentToken = 0xFFFFFFFFu;
 
-inline int32_t hash_token(uint32_t tok, int field, int dn, int64_t dim) {
+inline int64_t field_span(int dn, int dc, int64_t dim) {
+  return dc > 0 ? (dim - dn - 1) / dc : 0;
+}
+
+inline int32_t hash_token(uint32_t tok, int field, int dn, int dc, int64_t dim) {
   uint8_t b[4];
   std::memcpy(b, &tok, 4);
-  return hash_cat(b, 4, field, dn, dim);
+  const uint32_t h = murmur3_32(b, 4, kSeedBase + uint32_t(field));
+  const int64_t span = field_span(dn, dc, dim);
+  const int32_t slot = int32_t(dn + int64_t(field) * span + int64_t(h & 0x7fffffffu) % span);
+  return (h & 0x80000000u) ? int32_t(uint32_t(slot) | 0x80000000u) : slot;
 }
 
 }  // namespace omldm_hash

@@ -4,7 +4,8 @@
 // topic carries):
 //   num [B, dn] float32   numerical then discrete features
 //   tok [B, dc] uint32    raw categorical token id per field (0xFFFFFFFF = absent) —
-//                         hashed on the GPU inside the training kernel (hashing.h)
+//                         hashed field-aware on the GPU inside the training kernel
+//                         (hashing.h: hash_token)
 //   y   [B]     float32 or int8 (±1 classification labels), NaN = no target
 //
 // omldm_cpu_linear_seq_round is the reference semantics of one Synchronous round
@@ -141,7 +142,7 @@ OMLDM_HOST_API void omldm_synth_raw(uint64_t seed, int64_t start, int B, int dn,
         xt[j] = t;
         const uint64_t hv = mix64((seed ^ 0x27d4eb2dull) + uint64_t(j) * 0x1f1f1f1full + uint64_t(t));
         // the value's effect as seen through its hashed feature (x = ±1 by the hash sign)
-        const double sv = (hash_token(t, j, 0, int64_t(1) << 30) < 0) ? -1.0 : 1.0;
+        const double sv = (hash_token(t, j, 0, 1, int64_t(1) << 30) < 0) ? -1.0 : 1.0;
         for (int k = 0; k < K; ++k) {
           uint64_t hs = mix64(hv + uint64_t(k) * 104729);
           score[k] += sv * (gauss(hs) * 0.5);
@@ -169,7 +170,7 @@ OMLDM_HOST_API void omldm_cpu_hash_raw(const uint32_t* tok, int64_t B, int dc, i
     for (int64_t i = a; i < b; ++i)
       for (int j = 0; j < dc; ++j) {
         const uint32_t t = tok[i * dc + j];
-        cat[i * dc + j] = t == kAbsentToken ? -1 : hash_token(t, j, dn, dim);
+        cat[i * dc + j] = t == kAbsentToken ? -1 : hash_token(t, j, dn, dc, dim);
       }
   });
 }
@@ -212,7 +213,7 @@ OMLDM_HOST_API int omldm_cpu_linear_seq_round(const float* w, const float* num, 
         for (int j = 0; j < dc; ++j) {
           const uint32_t tk = tok[t * dc + j];
           if (tk == kAbsentToken) continue;
-          const int32_t h = hash_token(tk, j, dn, dim);
+          const int32_t h = hash_token(tk, j, dn, dc, dim);
           idx[F] = h & 0x7fffffff;
           xv[F++] = h < 0 ? -1.f : 1.f;
         }

@@ -1,5 +1,5 @@
-// Device copy of the feature hash of csrc/host/hashing.h (murmur3_32 of a categorical
-// token's 4 little-endian bytes, one seed per field → signed slot in [dn, dim − 1)).
+// Device copy of the raw-wire feature hash of csrc/host/hashing.h (murmur3_32 of a
+// categorical token's 4 little-endian bytes, one seed per field → field-aware signed slot).
 // tests/test_rawwire.py pins GPU == CPU slot for every field.
 #pragma once
 #include <stdint.h>
@@ -28,11 +28,12 @@ __device__ __forceinline__ uint32_t murmur3_u32(uint32_t k1, uint32_t seed) {
   return h1;
 }
 
-// token of field f → slot | sign << 31 (−1 when absent). span = dim − dn − 1 (> 0).
+// token of field f → slot | sign << 31 (−1 when absent), field-aware (hashing.h:
+// hash_token): slot = dn + f·span + (h & 0x7fffffff) mod span, span = (dim − dn − 1) / dc.
 __device__ __forceinline__ int hash_token_dev(uint32_t tok, int field, int dn, uint32_t span) {
   if (tok == kAbsentToken) return -1;
   const uint32_t h = murmur3_u32(tok, kHashSeedBase + (uint32_t)field);
-  const uint32_t slot = (uint32_t)dn + (h & 0x7fffffffu) % span;
+  const uint32_t slot = (uint32_t)dn + (uint32_t)field * span + (h & 0x7fffffffu) % span;
   return (int)(slot | (h & 0x80000000u));
 }
 

@@ -13,21 +13,26 @@
 // Blocked-exact sequential scan. For additive learners the model after
 // row s of a chunk is w_s = w_0 + Σ_{r<s} c_r x_r, so the margin of row t is
 //     m_t = x_t·w_0 + Σ_{s<t} c_s G_st,   G = X Xᵀ (the chunk's Gram matrix),
-// and only the scalar recurrence c_t = rule(m_t) is sequential. Per chunk of 64 rows:
-//   * producers (waves 1-3) hash the raw 32-bit category tokens (murmur3, hash_dev.h),
-//     group equal slots per field in LDS hash tables, and build G on the matrix cores:
-//     the dense part [numerical | intercept] with fp32-in/fp32-acc MFMA (exact f32
-//     products), the categorical part G_cat[t][s] = Σ_f [slot_tf = slot_sf]·x_tf·x_sf as
-//     U·Uᵀ with bf16 MFMA over a ±1 one-hot "shared group" matrix U in LDS —
-//     all of it for chunk k+1 while
+// and only the scalar recurrence c_t = rule(m_t) is sequential. One workgroup per spoke,
+// 8 waves; chunks of 64 rows are software-pipelined:
 //   * the scanner (wave 0, lane t = row t) runs the recurrence of chunk k: per step one
-//     closed-form candidate per lane, a v_readlane of lane t's, one FMA with row t of G.
-//   * then all 4 waves scatter chunk k's update into the spoke's replica (hardware fp32
-//     atomics in L2) and gather the round-start margins of chunk k+1.
-// One workgroup per spoke, replicas [S][dim] fp32 in HBM (4 MiB each at 2^20 dims).
-// Round end: linear_seq_reduce_kernel averages the replicas into the round accumulator
-// (the RCCL all-reduce runs on it for N > 1) and linear_seq_apply_kernel folds it into w
-// and refreshes every replica.
+//     closed-form candidate per lane, a v_readlane of lane t's, one FMA with row t of G;
+//   * meanwhile the 7 producer waves build chunk k+1: murmur3-hash the raw 32-bit
+//     category tokens (field-aware, hash_dev.h), group each field's equal slots
+//     wave-locally (no atomics), build G on the matrix cores — the dense block
+//     [numerical | intercept] with fp32-in/fp32-acc MFMA (exact f32 products), the
+//     categorical part G_cat[t][s] = Σ_f [slot_tf = slot_sf]·x_tf·x_sf as U·Uᵀ with bf16
+//     MFMA over a ±1 one-hot "shared group" matrix U in LDS — and GATHER chunk k+1's
+//     round-start margins from the spoke's replica BEFORE chunk k's update lands;
+//   * after the scan, chunk k's update is scattered into the replica (L2 fp32 atomics,
+//     not waited for) and chunk k+1's margins get the exact correction for what they
+//     missed: Σ_f x_sf · Σ_{t ∈ k, slot_tf = slot_sf} c_t x_tf + x_s,dense · Δw_dense,k
+//     (the producers link chunk k's entries to chunk k+1's groups while grouping).
+// So no global-memory latency (gather, scatter completion) sits on the scanner's path.
+// Replicas [S][dim] fp32 in HBM (4 MiB each at 2^20 dims). Round end:
+// linear_seq_reduce_kernel averages the replicas into the round accumulator (the RCCL
+// all-reduce runs on it for N > 1) and linear_seq_apply_kernel folds it into w and
+// refreshes every replica.
 #include "common.h"
 #include "hash_dev.h"
 
@@ -35,13 +40,17 @@ namespace omldm {
 
 namespace seq {
 constexpr int CH = 64;     // rows per chunk = scanner lanes
-constexpr int NT = 256;    // threads per workgroup
+constexpr int NP = 7;      // producer waves (wave 0 is the scanner)
+constexpr int NW = NP + 1; // waves per workgroup
+constexpr int NT = 64 * NW;
 constexpr int MAXF = 32;   // categorical fields per row
-constexpr int TB = 128;    // per-field group table entries (≥ 2× the chunk's rows)
-constexpr int KU = 256;    // shared-group columns of U handled on the matrix cores
+constexpr int CPW = 32;    // U columns owned by each producer wave
+constexpr int KU = NP * CPW;  // shared-group columns of U on the matrix cores
 constexpr int UPAD = 8;    // bf16 row padding of U (spreads the 16-B operand reads over banks)
-constexpr int GPAD = 4;    // G row stride 68 floats: 16-B aligned rows, ds_read_b128 spread over banks
-constexpr int WS = 8;      // per-spoke stat row: loss, n, mistakes, sq_err, 1, 0, 0, 0
+constexpr int GPAD = 4;    // G row stride 68 floats: 16-B aligned rows, b128 reads over banks
+constexpr int TB1 = 512;   // per-wave grouping table, first hash
+constexpr int TB2 = 256;   // second hash (keys that lost the first)
+constexpr int WS = 8;      // per-spoke stat row: loss, n, mistakes, sq_err, 1, stuck, 0, 0
 }  // namespace seq
 
 enum SeqRule : int { kSeqHinge = 0, kSeqEps = 1, kSeqLogistic = 2 };
@@ -52,7 +61,7 @@ struct SeqParams {
   float kadd;   // τ denominator offset: 1/(2C) for PA-II
   float eps, lr, inv_p;
   int bias, y8;
-  uint32_t span;  // dim − dn − 1
+  uint32_t span;  // slots per categorical field: (dim − dn − 1) / dc (field-aware hashing)
 };
 
 // v_writelane_b32 (no clang builtin in this toolchain: the LLVM intrinsic by name)
@@ -67,27 +76,32 @@ struct SeqSmem {
   int slots[2][seq::MAXF][seq::CH];               // slot | sign << 31, −1 absent
   alignas(16) float G[2][seq::CH][seq::CH + seq::GPAD];  // Gram of the chunk, lower triangle
   alignas(16) unsigned short U[seq::CH][seq::KU + seq::UPAD];  // bf16 ±1 one-hot of shared groups
-  int tkey[seq::MAXF][seq::TB];                   // group tables: slot (−1 empty)
-  int tcnt[seq::MAXF][seq::TB];                   // members
-  int tcol[seq::MAXF][seq::TB];                   // U column (−1: none yet)
-  float part_p[4][seq::CH];                       // round-start margin partials
-  float part_n[2][3][seq::CH];                    // ‖x‖² partials
+  int tab[seq::NP][seq::TB1 + seq::TB2];          // per producer wave: (local slot << 6) | row
+  int flag[seq::NP][seq::CH];                     // per wave: row is a shared group's rep
+  int gcol[seq::NP][seq::CH];                     // per wave: rep row → its U column
+  int ovl[seq::NP][seq::CH];                      // per wave: third-chance groups (slot)
+  signed char rep[2][seq::MAXF][seq::CH];         // chunk row → its group's representative row
+  signed char xlink[seq::MAXF][seq::CH];          // chunk-k row → chunk-(k+1) group rep (−1)
+  float cgrp[seq::MAXF][seq::CH];                 // Σ c_t x_t of chunk k per chunk-(k+1) group
+  float part_p[seq::NP][seq::CH];                 // round-start margin partials
+  float part_n[2][seq::NP][seq::CH];              // ‖x‖² partials
   float cval[seq::CH];                            // the chunk's c_t
   float wn[KN];                                   // dense weights (numerical, intercept)
-  int ncols[2];
+  float dwn[KN];                                  // the last chunk's dense update
+  int ucnt[2][seq::NP];                           // U columns used per wave
   int ovf[2];
   int pbar;                                       // producer-wave barrier counter
   int stuck;                                      // a producer barrier timed out
 };
 
-// Barrier of the three producer waves only (the scanner wave keeps running): a monotonic
-// LDS counter, one increment per wave, spin until all three arrived. The spin is bounded
-// (≈ 2^22 sleeps, far beyond any legitimate wait): a broken invariant ends the kernel with
-// a wrong result flagged in the spoke's stat row instead of hanging the GPU.
+// Barrier of the producer waves only (the scanner wave keeps running): a monotonic LDS
+// counter, one increment per wave, spin until all arrived. The spin is bounded (≈ 2^22
+// sleeps, far beyond any legitimate wait): a broken invariant ends the kernel with a wrong
+// result flagged in the spoke's stat row instead of hanging the GPU.
 __device__ __forceinline__ bool producer_barrier(int* ctr, int& target) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if ((threadIdx.x & 63) == 0) atomicAdd(ctr, 1);
-  target += 3;
+  target += seq::NP;
   int spins = 0;
   while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
     __builtin_amdgcn_s_sleep(1);
@@ -139,165 +153,255 @@ __device__ __forceinline__ float load_y(const void* yv, int t, int y8) {
 // Producer state carried between chunks: the raw inputs of the next chunk, in registers.
 template <int KN>
 struct ProdRegs {
-  static constexpr int NF = (seq::MAXF + 2) / 3;  // fields per producer thread
-  static constexpr int NJ = (KN + 2) / 3;         // dense columns per producer thread
+  static constexpr int NF = (seq::MAXF + seq::NP - 1) / seq::NP;  // fields per producer thread
+  static constexpr int NJ = (KN + seq::NP - 1) / seq::NP;         // dense columns per thread
   uint32_t tk[NF];
   float xv[NJ];
 };
 
-// Branch-free: every load is issued unconditionally from a clamped address (a load in a
-// lane-divergent branch is waited for inside the branch), invalid lanes are masked after.
+// Issues the loads of one chunk's inputs into registers and returns at once: every load
+// comes from a clamped (always valid) address and NOTHING reads the values here — masking
+// them (rows past the shard, fields ≥ dc) right after the loads made the compiler wait
+// for them, which turned the one-chunk-ahead prefetch into a synchronous HBM round trip
+// per chunk. produce() masks when it consumes the registers, a chunk later.
 template <int KN>
 __device__ __forceinline__ void prod_load(ProdRegs<KN>& R, const float* __restrict__ num, int dn,
                                           const uint32_t* __restrict__ tok, int dc, int row,
-                                          bool valid, int q, int bias, int last_row) {
-  const size_t rc = (size_t)(valid ? row : last_row);
+                                          int q, int last_row) {
+  const size_t rc = (size_t)min(row, last_row);
+  if (dc > 0) {
 #pragma unroll
-  for (int k = 0; k < ProdRegs<KN>::NF; ++k) {
-    const int f = q + 3 * k;
-    R.tk[k] = dc > 0 ? tok[rc * dc + min(f, dc - 1)] : kAbsentToken;
+    for (int k = 0; k < ProdRegs<KN>::NF; ++k)
+      R.tk[k] = tok[rc * dc + min(q + seq::NP * k, dc - 1)];
   }
+  if (dn > 0) {
 #pragma unroll
-  for (int k = 0; k < ProdRegs<KN>::NJ; ++k) {
-    const int j = q + 3 * k;
-    R.xv[k] = dn > 0 ? num[rc * dn + min(j, dn - 1)] : 0.f;
-  }
-#pragma unroll
-  for (int k = 0; k < ProdRegs<KN>::NF; ++k)
-    if (!valid || q + 3 * k >= dc) R.tk[k] = kAbsentToken;
-#pragma unroll
-  for (int k = 0; k < ProdRegs<KN>::NJ; ++k) {
-    const int j = q + 3 * k;
-    R.xv[k] = !valid ? 0.f : (j < dn ? R.xv[k] : ((bias && j == dn) ? 1.f : 0.f));
+    for (int k = 0; k < ProdRegs<KN>::NJ; ++k)
+      R.xv[k] = num[rc * dn + min(q + seq::NP * k, dn - 1)];
   }
 }
 
-// Builds chunk k of the spoke in buffer b: dense block, hashed slots, ‖x‖², group tables,
-// U, and G on the matrix cores. Waves 1..3 only (pw = wave − 1, pt = thread − 64).
+// Diagnostics: when set (omldm_linear_seq_stamps), lane 0 of wave 0 and of wave 1 add
+// per-phase cycle counts (s_memtime) into g_seq_stamps[spoke][16]:
+//   0 scan, 1 scanner wait for producers, 2 post-scan (scatter/link/correct) (wave 0);
+//   4 produce (wave 1), 5 chunks, 6 wave-1 wait at the first barrier;
+//   8.. produce sub-phases (wave 1): 8 fence + dense + hash, 9 gather issue,
+//   10 grouping + links + U, 11 barrier, 12 MFMA + G, 13 barrier, 14 slow path + reset,
+//   15 gather consume.
+__device__ unsigned long long* g_seq_stamps;
+
+__device__ __forceinline__ void sub_stamp(unsigned long long* acc, unsigned long long& t, int k) {
+  if (acc) {
+    const unsigned long long now = clock64();
+    if (k >= 0) acc[k] += now - t;
+    t = now;
+  }
+}
+
+// Wave-local grouping of one field of the chunk being built (lane = row). Returns the
+// row's group representative (−1 when absent). tab holds (local slot << 6) | row; a lane
+// only trusts an entry it verified, so the table is never cleared.
+__device__ __forceinline__ int group_rows(volatile int* tab, volatile int* ovl, int& novl,
+                                          bool present, int loc) {
+  int rep = -1;
+  const int h1 = (int)(((uint32_t)loc * 0x9E3779B1u) >> 23);          // TB1 = 512
+  if (present) tab[h1] = (loc << 6) | (int)(threadIdx.x & 63);
+  const int e1 = present ? tab[h1] : 0;
+  if (present && (e1 >> 6) == loc) rep = e1 & 63;
+  novl = 0;
+  if (__ballot(present && rep < 0)) {
+    const int h2 = seq::TB1 + (int)(((uint32_t)loc * 0x85EBCA77u + 0x27D4EB2Fu) >> 24);  // TB2
+    const bool again = present && rep < 0;
+    if (again) tab[h2] = (loc << 6) | (int)(threadIdx.x & 63);
+    const int e2 = again ? tab[h2] : 0;
+    if (again && (e2 >> 6) == loc) rep = e2 & 63;
+    // third chance: the first unresolved lane of each remaining slot represents it; its
+    // slot goes to the wave's overflow list (what chunk lookups check last)
+    unsigned long long m = __ballot(present && rep < 0);
+    while (m) {
+      const int u = __builtin_ctzll(m);
+      const int lu = __builtin_amdgcn_readlane(loc, u);
+      if (present && rep < 0 && loc == lu) rep = u;
+      if ((int)(threadIdx.x & 63) == 0) ovl[novl] = (lu << 6) | u;
+      ++novl;
+      m = __ballot(present && rep < 0);
+    }
+  }
+  return rep;
+}
+
+// The representative row of `loc` among the chunk grouped last into tab/ovl (−1: the
+// slot does not occur there). Table entries may be stale (earlier fields or chunks), so
+// a hit is verified against that chunk's slots.
+__device__ __forceinline__ int lookup_rows(volatile int* tab, const volatile int* ovl, int novl,
+                                           const int* slots_f, int base_f, bool present, int loc) {
+  if (!present) return -1;
+  const int h1 = (int)(((uint32_t)loc * 0x9E3779B1u) >> 23);
+  const int e1 = tab[h1];
+  if ((e1 >> 6) == loc && (slots_f[e1 & 63] & 0x7fffffff) == base_f + loc) return e1 & 63;
+  const int h2 = seq::TB1 + (int)(((uint32_t)loc * 0x85EBCA77u + 0x27D4EB2Fu) >> 24);
+  const int e2 = tab[h2];
+  if ((e2 >> 6) == loc && (slots_f[e2 & 63] & 0x7fffffff) == base_f + loc) return e2 & 63;
+  for (int i = 0; i < novl; ++i)
+    if ((ovl[i] >> 6) == loc) return ovl[i] & 63;
+  return -1;
+}
+
+// Builds chunk n (buffer bn) while the scanner works on chunk o (buffer bo, has_o):
+// dense block, hashed slots, ‖x‖², the gather of the round-start margins from the
+// replica, the field groups of chunk n and the links of chunk o's entries into them, U,
+// and G on the matrix cores. Producer waves only (q = wave − 1, r = row).
 template <int KN>
-__device__ void produce(SeqSmem<KN>& sm, const ProdRegs<KN>& R, int b, int dn, int dc,
-                        const SeqParams& p, int& pbt) {
+__device__ void produce(SeqSmem<KN>& sm, const ProdRegs<KN>& R, ProdRegs<KN>& next,
+                        int next_row, bool load_next, const float* __restrict__ num,
+                        const uint32_t* __restrict__ tok, int last_row, bool valid, int bn,
+                        bool has_o, int dn, int dc, const SeqParams& p, int& pbt,
+                        const float* W, int (&code)[ProdRegs<KN>::NF], float& pacc,
+                        unsigned long long* sacc) {
+  constexpr int NF = ProdRegs<KN>::NF;
+  const int bo = bn ^ 1;
+  unsigned long long st_t = 0;
+  sub_stamp(sacc, st_t, -1);
   const int pt = (int)threadIdx.x - 64;
   const int r = pt & 63, q = __builtin_amdgcn_readfirstlane(pt >> 6);  // wave-uniform
   const int lane = threadIdx.x & 63;
-  float n2 = 0.f;
+  // ---- every earlier chunk's scatter has completed before this chunk's gather: each
+  // producer wave waits for its own atomics, then the producers meet (the scanner scans
+  // meanwhile); only then the next chunk's inputs are requested (a release fence waits
+  // for every outstanding load as well)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (!producer_barrier(&sm.pbar, pbt)) sm.stuck = 1;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (load_next) prod_load<KN>(next, num, dn, tok, dc, next_row, q, last_row);
+  // ---- dense block + the dense part of the round-start margin
+  float n2 = 0.f, pd = 0.f;
 #pragma unroll
   for (int k = 0; k < ProdRegs<KN>::NJ; ++k) {
-    const int j = q + 3 * k;
-    if (j < KN) {
-      sm.xn[b][r][j] = R.xv[k];
-      n2 = fmaf(R.xv[k], R.xv[k], n2);
+    const int j = q + seq::NP * k;
+    if (j < KN) {  // dense block: features, then the intercept column, then zero padding
+      const float x = !valid ? 0.f : (j < dn ? R.xv[k] : ((p.bias && j == dn) ? 1.f : 0.f));
+      sm.xn[bn][r][j] = x;
+      n2 = fmaf(x, x, n2);
+      pd = fmaf(x, sm.wn[j], pd);
     }
   }
-  // hash + group: insert the slot into its field's table, count members; the member that
-  // makes a group shared (second arrival) claims its U column
-  int ent[ProdRegs<KN>::NF];
-  int code[ProdRegs<KN>::NF];
+  // ---- hash; the previous link targets of this row are cleared for the new chunk
 #pragma unroll
-  for (int k = 0; k < ProdRegs<KN>::NF; ++k) {
-    const int f = q + 3 * k;
-    ent[k] = -1;
+  for (int k = 0; k < NF; ++k) {
+    const int f = q + seq::NP * k;
     code[k] = -1;
     if (f < dc) {
-      code[k] = hash_token_dev(R.tk[k], f, dn, p.span);
-      sm.slots[b][f][r] = code[k];
+      code[k] = hash_token_dev(valid ? R.tk[k] : kAbsentToken, f, dn, p.span);
+      sm.slots[bn][f][r] = code[k];
+      sm.cgrp[f][r] = 0.f;
     }
+    n2 += code[k] != -1 ? 1.f : 0.f;  // ‖x‖² over the feature list (CPU oracle semantics)
   }
+  sm.part_n[bn][q][r] = n2;
+  sub_stamp(sacc, st_t, 8);
+  // ---- gather (chunk o's update has not been scattered yet: corrected after the scan)
+  float wv[NF];
 #pragma unroll
-  for (int k = 0; k < ProdRegs<KN>::NF; ++k) {
-    const int f = q + 3 * k;
-    if (f < dc) {
-      if (code[k] != -1) {
-        n2 += 1.f;
-        const int key = code[k] & 0x7fffffff;
-        uint32_t h = ((uint32_t)key * 0x9E3779B1u) >> 25;  // TB = 128
-        for (int probe = 0; probe < seq::TB; ++probe) {
-          int cur = __hip_atomic_load(&sm.tkey[f][h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (cur == -1) {
-            const int prev = atomicCAS(&sm.tkey[f][h], -1, key);
-            cur = prev == -1 ? key : prev;
-          }
-          if (cur == key) {
-            ent[k] = (int)h;
-            break;
-          }
-          h = (h + 1) & (seq::TB - 1);
-        }
-        // ≤ 64 keys in 128 entries: the probe always terminates with a slot
-        if (atomicAdd(&sm.tcnt[f][ent[k]], 1) == 1) sm.tcol[f][ent[k]] = atomicAdd(&sm.ncols[b], 1);
-      }
-    }
-  }
-  sm.part_n[b][q][r] = n2;
-  if (!producer_barrier(&sm.pbar, pbt)) sm.stuck = 1;
-  // members of shared groups set their one-hot entry: the feature value ±1 (two tokens of
-  // a field that collide on a slot may carry opposite hash signs, so U·Uᵀ = Σ x_t·x_s);
-  // columns ≥ KU take the exact slow path
-  int col[ProdRegs<KN>::NF];
+  for (int k = 0; k < NF; ++k) wv[k] = W[code[k] != -1 ? (code[k] & 0x7fffffff) : 0];
+  sub_stamp(sacc, st_t, 9);
+  // ---- group each field of chunk n; link chunk o's entries of the field to them
+  volatile int* tab = sm.tab[q];
+  volatile int* ovl = sm.ovl[q];
+  volatile int* flg = sm.flag[q];
+  volatile int* gcl = sm.gcol[q];
+  int col[NF];
+  int used = 0;  // this wave's U columns (wave-uniform)
   bool slow = false;
 #pragma unroll
-  for (int k = 0; k < ProdRegs<KN>::NF; ++k) {
-    const int f = q + 3 * k;
+  for (int k = 0; k < NF; ++k) {
+    const int f = q + seq::NP * k;
     col[k] = -1;
-    if (f < dc && ent[k] >= 0 && sm.tcnt[f][ent[k]] >= 2) {
-      col[k] = sm.tcol[f][ent[k]];
-      if (col[k] < seq::KU) sm.U[r][col[k]] = code[k] < 0 ? 0xBF80 : 0x3F80;  // bf16 ∓1
-      else slow = true;
+    if (f >= dc) continue;  // wave-uniform
+    const int base_f = dn + f * (int)p.span;
+    const bool present = code[k] != -1;
+    const int loc = (code[k] & 0x7fffffff) - base_f;
+    int novl = 0;
+    const int rp = group_rows(tab, ovl, novl, present, loc);
+    sm.rep[bn][f][r] = (signed char)rp;
+    if (has_o) {
+      const int co = sm.slots[bo][f][r];
+      sm.xlink[f][r] = (signed char)lookup_rows(tab, ovl, novl, sm.slots[bn][f], base_f,
+                                                co != -1, (co & 0x7fffffff) - base_f);
+    }
+    // shared groups: flagged by a non-representative member; flagged representatives take
+    // this wave's next U columns (ballot + mbcnt), members store ±1 at U[row][column]
+    flg[r] = 0;
+    if (present && rp != r) flg[rp] = 1;
+    const bool lead = present && rp == r && flg[r] != 0;
+    const unsigned long long m = __ballot(lead);
+    if (lead)
+      gcl[r] = q * seq::CPW + used + (int)__builtin_amdgcn_mbcnt_hi(
+                   (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+    used += __builtin_popcountll(m);
+    if (present && (rp != r || lead)) {
+      col[k] = gcl[rp];
+      if (col[k] < (q + 1) * seq::CPW) sm.U[r][col[k]] = code[k] < 0 ? 0xBF80 : 0x3F80;
+      else slow = true;  // more than CPW shared groups in this wave: exact slow path
     }
   }
-  if (slow) sm.ovf[b] = 1;
+  if (lane == 0) sm.ucnt[bn][q] = min(used, seq::CPW);
+  if (__ballot(slow) && lane == 0) sm.ovf[bn] = 1;
+  sub_stamp(sacc, st_t, 10);
   if (!producer_barrier(&sm.pbar, pbt)) sm.stuck = 1;
-  // G tiles (I, J) ∈ {(0,0), (1,0), (1,1)}: the scan reads row s of G at columns t < s
-  // (G is symmetric; its upper-right tile stays 0)
-  {
+  sub_stamp(sacc, st_t, 11);
+  // ---- G tiles (I, J) ∈ {(0,0), (1,0), (1,1)}: the scan reads row s of G at columns t < s
+  // (G is symmetric; its upper-right tile stays 0). Producer waves 0-2, one tile each.
+  if (q < 3) {
     const int I0 = q == 0 ? 0 : 32, J0 = q == 2 ? 32 : 0;
     const int l31 = lane & 31, hi = lane >> 5;
     f32x16 acc = {};
 #pragma unroll
     for (int k0 = 0; k0 < KN; k0 += 2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sm.xn[b][I0 + l31][k0 + hi],
-                                                 sm.xn[b][J0 + l31][k0 + hi], acc, 0, 0, 0);
-    const int nc = min(__builtin_amdgcn_readfirstlane(sm.ncols[b]), seq::KU);
-    for (int k0 = 0; k0 < nc; k0 += 16) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sm.U[I0 + l31][k0 + 8 * hi]);
-      const bf16x8 bb = *reinterpret_cast<const bf16x8*>(&sm.U[J0 + l31][k0 + 8 * hi]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sm.xn[bn][I0 + l31][k0 + hi],
+                                                 sm.xn[bn][J0 + l31][k0 + hi], acc, 0, 0, 0);
+    for (int w = 0; w < seq::NP; ++w) {
+      const int nc = __builtin_amdgcn_readfirstlane(sm.ucnt[bn][w]);
+      for (int k0 = w * seq::CPW; k0 < w * seq::CPW + nc; k0 += 16) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sm.U[I0 + l31][k0 + 8 * hi]);
+        const bf16x8 bb = *reinterpret_cast<const bf16x8*>(&sm.U[J0 + l31][k0 + 8 * hi]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg)
-      sm.G[b][I0 + (reg & 3) + 8 * (reg >> 2) + 4 * hi][J0 + l31] = acc[reg];
+      sm.G[bn][I0 + (reg & 3) + 8 * (reg >> 2) + 4 * hi][J0 + l31] = acc[reg];
   }
+  sub_stamp(sacc, st_t, 12);
   if (!producer_barrier(&sm.pbar, pbt)) sm.stuck = 1;
-  if (__builtin_amdgcn_readfirstlane(sm.ovf[b])) {
-    // more shared groups than U columns: the overflowed ones add their counts directly
+  sub_stamp(sacc, st_t, 13);
+  if (__builtin_amdgcn_readfirstlane(sm.ovf[bn])) {
+    // groups past a wave's CPW columns: each such entry adds its products with every
+    // other row of the same slot in its field into its own row of G
 #pragma unroll
-    for (int k = 0; k < ProdRegs<KN>::NF; ++k) {
-      const int f = q + 3 * k;
-      if (col[k] >= seq::KU) {
+    for (int k = 0; k < NF; ++k) {
+      if (col[k] >= (q + 1) * seq::CPW) {
+        const int f = q + seq::NP * k;
         const int key = code[k] & 0x7fffffff;
         for (int t = 0; t < seq::CH; ++t) {
-          const int ct = sm.slots[b][f][t];
+          const int ct = sm.slots[bn][f][t];
           if (t != r && ct != -1 && (ct & 0x7fffffff) == key)
-            atomicAdd(&sm.G[b][r][t], (ct ^ code[k]) < 0 ? -1.f : 1.f);
+            atomicAdd(&sm.G[bn][r][t], (ct ^ code[k]) < 0 ? -1.f : 1.f);
         }
       }
     }
   }
-  // leave U, the tables and the other buffer's counters clean for the next chunk
+  // leave U and the other buffer's overflow flag clean for the next chunk
 #pragma unroll
-  for (int k = 0; k < ProdRegs<KN>::NF; ++k) {
-    const int f = q + 3 * k;
-    if (col[k] >= 0 && col[k] < seq::KU) sm.U[r][col[k]] = 0;
-    if (f < dc && ent[k] >= 0) {
-      sm.tkey[f][ent[k]] = -1;  // several members may clear the same entry: same values
-      sm.tcnt[f][ent[k]] = 0;
-      sm.tcol[f][ent[k]] = -1;
-    }
-  }
-  if (pt == 0) {
-    sm.ncols[b ^ 1] = 0;
-    sm.ovf[b ^ 1] = 0;
-  }
+  for (int k = 0; k < NF; ++k)
+    if (col[k] >= 0 && col[k] < (q + 1) * seq::CPW) sm.U[r][col[k]] = 0;
+  if (pt == 0) sm.ovf[bo] = 0;
+  sub_stamp(sacc, st_t, 14);
+  // ---- the gathered categorical weights (in flight since the gather)
+  float pc = 0.f;
+#pragma unroll
+  for (int k = 0; k < NF; ++k) pc += code[k] == -1 ? 0.f : (code[k] < 0 ? -wv[k] : wv[k]);
+  pacc = pd + pc;
+  sub_stamp(sacc, st_t, 15);
 }
 
 template <int RULE, int KN>
@@ -305,6 +409,7 @@ __global__ __launch_bounds__(seq::NT, 1) void linear_seq_kernel(
     const float* __restrict__ num, int dn, const uint32_t* __restrict__ tok, int dc,
     const void* __restrict__ yv, int B, int R, float* __restrict__ rep, int dim,
     float* __restrict__ ws, SeqParams p) {
+  constexpr int NF = ProdRegs<KN>::NF;
   __shared__ SeqSmem<KN> sm;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -320,80 +425,73 @@ __global__ __launch_bounds__(seq::NT, 1) void linear_seq_kernel(
   }
   const int nch = (t1 - t0 + seq::CH - 1) / seq::CH;
 
-  // ---- init: tables empty, U zero, dense weights from the replica, G's lower-left tile 0
-  for (int i = tid; i < seq::MAXF * seq::TB; i += seq::NT) {
-    (&sm.tkey[0][0])[i] = -1;
-    (&sm.tcnt[0][0])[i] = 0;
-    (&sm.tcol[0][0])[i] = -1;
-  }
+  // ---- init: tables, U zero, dense weights from the replica, G's upper-right tiles 0
+  for (int i = tid; i < seq::NP * (seq::TB1 + seq::TB2); i += seq::NT) (&sm.tab[0][0])[i] = -1;
   for (int i = tid; i < seq::CH * (seq::KU + seq::UPAD); i += seq::NT) (&sm.U[0][0])[i] = 0;
   for (int i = tid; i < 2 * 32 * 32; i += seq::NT) {
     const int b = i >> 10, t = (i >> 5) & 31, c = 32 + (i & 31);
     sm.G[b][t][c] = 0.f;
   }
   for (int i = tid; i < 2 * seq::CH * (KN + 1); i += seq::NT) (&sm.xn[0][0][0])[i] = 0.f;
-  if (tid < KN) sm.wn[tid] = tid < dn ? W[tid] : ((p.bias && tid == dn) ? W[dim - 1] : 0.f);
-  if (tid < 2) {
-    sm.ncols[tid] = 0;
-    sm.ovf[tid] = 0;
+  for (int i = tid; i < 2 * seq::MAXF * seq::CH; i += seq::NT) (&sm.slots[0][0][0])[i] = -1;
+  for (int i = tid; i < seq::MAXF * seq::CH; i += seq::NT) {
+    (&sm.cgrp[0][0])[i] = 0.f;
+    (&sm.xlink[0][0])[i] = -1;
   }
+  if (tid < KN) {
+    sm.wn[tid] = tid < dn ? W[tid] : ((p.bias && tid == dn) ? W[dim - 1] : 0.f);
+    sm.dwn[tid] = 0.f;
+  }
+  if (tid < 2) sm.ovf[tid] = 0;
   if (tid == 0) {
     sm.pbar = 0;
     sm.stuck = 0;
   }
   __syncthreads();
 
-  // gather of chunk k into buffer b: round-start margins from the replica + dense weights
-  auto gather = [&](int b) {
-    const int r = tid & 63, q4 = __builtin_amdgcn_readfirstlane(tid >> 6);
-    float acc = 0.f;
-    float wv[(seq::MAXF + 3) / 4];
-    int code[(seq::MAXF + 3) / 4];
-#pragma unroll
-    for (int k = 0; k < (seq::MAXF + 3) / 4; ++k) {
-      const int f = q4 + 4 * k;
-      code[k] = f < dc ? sm.slots[b][f][r] : -1;
-      wv[k] = W[code[k] != -1 ? (code[k] & 0x7fffffff) : 0];  // unconditional (see prod_load)
+  unsigned long long* stamps = g_seq_stamps;
+  unsigned long long st_acc[16] = {};
+  unsigned long long st_t = 0;
+  auto stamp = [&](int k) {
+    if (stamps) {
+      const unsigned long long now = clock64();
+      if (k >= 0) st_acc[k] += now - st_t;
+      st_t = now;
     }
-#pragma unroll
-    for (int k = 0; k < (seq::MAXF + 3) / 4; ++k)
-      acc += code[k] == -1 ? 0.f : (code[k] < 0 ? -wv[k] : wv[k]);
-#pragma unroll
-    for (int k = q4; k < KN; k += 4) acc = fmaf(sm.xn[b][r][k], sm.wn[k], acc);
-    sm.part_p[q4][r] = acc;
   };
 
   int pbt = 0;  // producer barrier target
   ProdRegs<KN> PR;
   const int pq = __builtin_amdgcn_readfirstlane((tid - 64) >> 6), pr = (tid - 64) & 63;
-  // scanner state
   float loss = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f;
   float ynext = 0.f;
   if (wave == 0) {
     ynext = load_y(yv, min(t0 + lane, t1 - 1), p.y8);
   } else {
-    const int row = t0 + pr;
-    prod_load<KN>(PR, num, dn, tok, dc, row, row < t1, pq, p.bias, t1 - 1);
+    prod_load<KN>(PR, num, dn, tok, dc, t0 + pr, pq, t1 - 1);
   }
 
-  // Software pipeline over chunks: iteration c scans chunk c (wave 0) while waves 1-3
-  // build chunk c + 1; then everyone scatters chunk c and gathers chunk c + 1's margins.
-  // c = −1 is the prologue (build + gather of chunk 0 only).
-  for (int c = -1; c < nch; ++c) {
-    const int b = c & 1;  // buffer of chunk c (c = −1 → 1, unused)
-    if (wave == 0) {
+  // Iteration c: the scanner scans chunk c while the producers build chunk c + 1; then
+  // chunk c is scattered and chunk c + 1's margins corrected. c = −1 is the prologue.
+  // The two roles run separate loops with the same barrier sequence (s_barrier counts
+  // waves), so each loop carries only its own outstanding loads in the compiler's wait
+  // analysis.
+  if (wave == 0) {
+    for (int c = -1; c < nch; ++c) {
+      const int b = c & 1;  // buffer of chunk c
+      stamp(-1);
       if (c >= 0) {
-        // ---------------- scan chunk c
         const int row = t0 + c * seq::CH + lane;
         const bool valid = row < t1;
         // invalid rows (past the spoke's shard) get y = 0 and 1/‖x‖² = 0: c = 0 exactly
         const float y = valid ? ynext : 0.f;
-        if (c + 1 < nch) {
-          const int r1 = row + seq::CH;
-          ynext = load_y(yv, min(r1, t1 - 1), p.y8);
+        if (c + 1 < nch) ynext = load_y(yv, min(row + seq::CH, t1 - 1), p.y8);
+        float m = 0.f, n2 = 0.f;
+#pragma unroll
+        for (int q = 0; q < seq::NP; ++q) {
+          m += sm.part_p[q][lane];
+          n2 += sm.part_n[b][q][lane];
         }
-        float m = (sm.part_p[0][lane] + sm.part_p[1][lane]) + (sm.part_p[2][lane] + sm.part_p[3][lane]);
-        const float n2 = sm.part_n[b][0][lane] + sm.part_n[b][1][lane] + sm.part_n[b][2][lane];
         const float inv = (valid && n2 > 0.f) ? __builtin_amdgcn_rcpf(n2 + p.kadd) : 0.f;
         // the recurrence: step t broadcasts lane t's c_t (v_readlane) and every lane s adds
         // c_t·G[s][t] (row s of the symmetric G, four steps per ds_read_b128). c_t and m_t
@@ -416,49 +514,88 @@ __global__ __launch_bounds__(seq::NT, 1) void linear_seq_kernel(
           }
         }
         sm.cval[lane] = __builtin_bit_cast(float, cvec);
+        stamp(0);
         if (valid) {
           seq_stats<RULE>(__builtin_bit_cast(float, mvec), y, p, loss, mist, sqe);
           nex += 1.f;
         }
       }
-    } else if (c + 1 < nch) {
-      // ---------------- build chunk c + 1 (the inputs of c + 2 load meanwhile)
-      const ProdRegs<KN> cur = PR;
-      const int r2 = t0 + (c + 2) * seq::CH + pr;
-      if (c + 2 < nch) prod_load<KN>(PR, num, dn, tok, dc, r2, r2 < t1, pq, p.bias, t1 - 1);
-      produce<KN>(sm, cur, b ^ 1, dn, dc, p, pbt);
+      __syncthreads();  // B1: chunk c scanned, chunk c + 1 built
+      stamp(1);
+      __syncthreads();  // B2: chunk c's links and dense update accumulated
+      __syncthreads();  // B3: chunk c + 1's margins corrected
+      stamp(2);
+      st_acc[5] += 1;
     }
-    __syncthreads();
-    if (c >= 0) {
-      // ---------------- scatter chunk c into the replica (L2 fp32 atomics) + dense weights
-      const int r = tid & 63, q4 = __builtin_amdgcn_readfirstlane(tid >> 6);
-      const float cv = sm.cval[r];
-      if (cv != 0.f) {
+  } else {
+    const int q = pq, r = pr;
+    int code[NF];
+    float pacc = 0.f;
+    for (int c = -1; c < nch; ++c) {
+      const int b = c & 1;
+      const bool more = c + 1 < nch;
+      stamp(-1);
+      if (more) {
+        const ProdRegs<KN> cur = PR;
+        produce<KN>(sm, cur, PR, t0 + (c + 2) * seq::CH + r, c + 2 < nch, num, tok, t1 - 1,
+                    t0 + (c + 1) * seq::CH + r < t1, b ^ 1, c >= 0, dn, dc, p, pbt, W, code,
+                    pacc, stamps ? st_acc : nullptr);
+        stamp(4);
+      }
+      __syncthreads();  // B1
+      stamp(6);
+      if (c >= 0) {
+        // ---- chunk c: scatter its update into the replica (not waited for: the next
+        // gather fences), link it into chunk c + 1's groups, accumulate the dense update
+        const float cv = sm.cval[r];
 #pragma unroll
-        for (int k = 0; k < (seq::MAXF + 3) / 4; ++k) {
-          const int f = q4 + 4 * k;
-          const int code = f < dc ? sm.slots[b][f][r] : -1;
-          if (code != -1) unsafeAtomicAdd(&W[code & 0x7fffffff], code < 0 ? -cv : cv);
+        for (int k = 0; k < NF; ++k) {
+          const int f = q + seq::NP * k;
+          if (f < dc) {
+            const int co = sm.slots[b][f][r];
+            if (co != -1 && cv != 0.f) {
+              const float u = co < 0 ? -cv : cv;
+              unsafeAtomicAdd(&W[co & 0x7fffffff], u);
+              const int xl = sm.xlink[f][r];
+              if (xl >= 0 && more) atomicAdd(&sm.cgrp[f][xl], u);
+            }
+          }
+        }
+        for (int j = q; j < KN; j += seq::NP) {  // Δw_dense of chunk c (lane = row)
+          const float d = wave_sum(cv * sm.xn[b][r][j]);
+          if (lane == 0) sm.dwn[j] = d;
         }
       }
-      constexpr int PARTS = seq::NT / KN;
-      constexpr int RPP = seq::CH / PARTS;
-      const int kcol = tid % KN, part = tid / KN;
-      float d = 0.f;
+      __syncthreads();  // B2
+      if (more) {
+        // ---- chunk c + 1's exact round-start margins: raw gather + what chunk c changed
+        float corr = 0.f;
+        if (c >= 0) {
 #pragma unroll
-      for (int i = 0; i < RPP; ++i) {
-        const int rr = part * RPP + i;
-        d = fmaf(sm.cval[rr], sm.xn[b][rr][kcol], d);
+          for (int k = 0; k < NF; ++k) {
+            const int f = q + seq::NP * k;
+            if (f < dc && code[k] != -1) {
+              const float g = sm.cgrp[f][sm.rep[b ^ 1][f][r]];
+              corr += code[k] < 0 ? -g : g;
+            }
+          }
+          for (int j = q; j < KN; j += seq::NP) corr = fmaf(sm.xn[b ^ 1][r][j], sm.dwn[j], corr);
+        }
+        sm.part_p[q][r] = pacc + corr;
       }
-      if (d != 0.f) atomicAdd(&sm.wn[kcol], d);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (c >= 0) {
+        for (int j = q; j < KN; j += seq::NP)
+          if (lane == 0) sm.wn[j] += sm.dwn[j];  // w_dense after chunk c
+      }
+      __syncthreads();  // B3
     }
-    if (c + 1 < nch) gather(b ^ 1);
-    __syncthreads();
   }
 
+  if (stamps && lane == 0 && wave <= 1) {
+    for (int k = 0; k < 16; ++k)
+      if ((wave == 0) == (k < 4 || k == 5)) atomicAdd(&stamps[(size_t)s * 16 + k], st_acc[k]);
+  }
+  __syncthreads();
   // ---- round end: dense weights back into the replica, spoke statistics
   if (tid < dn && tid < KN) W[tid] = sm.wn[tid];
   if (p.bias && tid == 0) W[dim - 1] = sm.wn[dn];
@@ -480,8 +617,6 @@ __global__ __launch_bounds__(seq::NT, 1) void linear_seq_kernel(
   }
 }
 
-// dacc[j] = inv_p · Σ_{s < S_act} (rep[s][j] − w[j]); dacc[dim] = dacc[dim+1] = S_act·inv_p;
-// block 0 also folds the spoke statistics into the fp64 running totals.
 __global__ __launch_bounds__(256) void linear_seq_reduce_kernel(
     const float* __restrict__ rep, const float* __restrict__ w, int S_act, int dim,
     float* __restrict__ dacc, float inv_p, const float* __restrict__ ws, double* __restrict__ cum) {
@@ -612,8 +747,10 @@ OMLDM_API int omldm_linear_seq_round(const float* w, const float* num, int dn, c
   if (rule < 0 || rule > 2) return -5;
   const int kn_need = dn + (bias ? 1 : 0);
   if (kn_need > 32) return -2;
+  // grouping tables pack (local slot << 6 | row) in an int: ≤ 2^25 slots per field
+  if (dc > 0 && (long long)(dim - dn - 1) / dc >= (1LL << 25)) return -2;
   const SeqParams p{rule, variant, variant == 1 ? C : INFINITY, variant == 2 ? 0.5f / C : 0.f,
-                    eps, lr, inv_p, bias, y8, (uint32_t)(dim - dn - 1)};
+                    eps, lr, inv_p, bias, y8, dc > 0 ? (uint32_t)((dim - dn - 1) / dc) : 1u};
   hipStream_t st = (hipStream_t)stream;
   int e = kn_need <= 16 ? dispatch_seq<16>(rule, num, dn, (const uint32_t*)tok, dc, y, B, R, S, rep, dim, ws, p, st)
                         : dispatch_seq<32>(rule, num, dn, (const uint32_t*)tok, dc, y, B, R, S, rep, dim, ws, p, st);
@@ -623,6 +760,11 @@ OMLDM_API int omldm_linear_seq_round(const float* w, const float* num, int dn, c
   hipLaunchKernelGGL(linear_seq_reduce_kernel, dim3(grid_for(dim)), dim3(256), 0, st, rep, w,
                      S_act, dim, dacc, inv_p, ws, cum);
   return (int)hipGetLastError();
+}
+
+// Diagnostics: per-phase cycle accumulation into buf [S][16] (nullptr: off).
+OMLDM_API int omldm_linear_seq_stamps(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_seq_stamps), &buf, sizeof(buf));
 }
 
 OMLDM_API int omldm_linear_seq_apply(float* w, float* rep, int S, float* dacc, int dim,
@@ -645,6 +787,6 @@ OMLDM_API int omldm_hash_raw(const void* tok, long long B, int dc, int dn, long 
   int blocks = (int)((n + 255) / 256);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(hash_raw_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     (const uint32_t*)tok, n, dc, dn, (uint32_t)(dim - dn - 1), out);
+                     (const uint32_t*)tok, n, dc, dn, (uint32_t)((dim - dn - 1) / dc), out);
   return (int)hipGetLastError();
 }

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, lon
     } else if (j < nf) {
       const int c = (int)fj;
       if (cspan < 0) {  // raw binary wire: the 32-bit category token, hashed here
-        const int code = hash_token_dev(fj, j - dn, dn, (uint32_t)(dim - dn - 1));
+        const int code = hash_token_dev(fj, j - dn, dn, (uint32_t)((dim - dn - 1) / dc));
         if (code != -1) {
           idx = code & 0x7fffffff;
           v = code < 0 ? -1.f : 1.f;

@@ -124,7 +124,9 @@ class Job:
 
             self._gpu_parser = GpuJsonParser(self.device)
         self._trained_global = 0
-        self._flags = torch.zeros(4, dtype=torch.float32, device=self._coll_device())
+        # per-tick control flags: [active records, terminate, training rows, pending
+        # requests, checkpoint due] — a host tensor reduced over the gloo control group
+        self._flags = torch.zeros(5, dtype=torch.float64)
         # multi-rank control plane: rank 0 polls requests at the end of a tick and the
         # tick's flag all-reduce says whether the next tick must broadcast them — ticks
         # without requests (nearly all) cost no object broadcast
@@ -394,9 +396,12 @@ class Job:
         if self.world > 1 and self.rank == 0:
             self._ctrl_pending += self._poll_requests()
             self._flags[3] = float(len(self._ctrl_pending))
+        # rank 0's clock decides checkpoints: every rank snapshots at the same tick
+        self._flags[4] = 1.0 if (self.rank == 0 and self.checkpointer is not None
+                                 and self.checkpointer.due()) else 0.0
         with tracing.range("flags"):
-            self.comm.all_reduce_(self._flags, tag="heartbeat")
-            active, term, n_train, n_req = (float(v) for v in self._flags.tolist())
+            self.comm.all_reduce_host_(self._flags, tag="heartbeat")
+            active, term, n_train, n_req, ckpt = (float(v) for v in self._flags.tolist())
         self._ctrl_due = n_req > 0
         active += n_req
         self._trained_global += int(n_train)
@@ -414,7 +419,7 @@ class Job:
             self.idle.activity(time.time())  # idle = time since the last active tick ended
         if term > 0:
             self._terminate()
-        if self.checkpointer is not None and self.checkpointer.due():
+        if self.checkpointer is not None and ckpt > 0:
             self.egress.flush()  # outputs of the checkpointed ticks are in their topic
             self.checkpointer.save(self)
         self.ticks += 1
@@ -457,6 +462,8 @@ class Job:
             p.protocol.finalize()
         self.ingest.close()
         self.egress.close()
+        if self.checkpointer is not None:
+            self.checkpointer.close()
         if self.watchdog is not None:
             self.watchdog.stop()
         return self

@@ -16,6 +16,7 @@ import torch
 
 from omldm_amd.api.batch import FeatureSpace, HashedBatch, PolyBatch
 from omldm_amd.api.schemas import SINGLE_LEARNER_MODELS, Request
+from omldm_amd.engine.statistics import merge_bucketed
 from omldm_amd.models import make_learner, make_preprocessor
 from omldm_amd.parallel.comm import Comm
 from omldm_amd.parallel.protocols import make_protocol
@@ -43,6 +44,15 @@ class Pipeline:
         if d + 1 >= space.dim:
             raise ValueError("dense block wider than the hashed feature space")
         self.learner = make_learner(name, hyper, space, device)
+        # warm start: a Create carrying the reference's portable model format — a
+        # QueryResponse's learner.parameters / preprocessor parameters, bucketed keys
+        # ``name[start-end]`` merged back (FlinkSpoke.scala:198-219 hands the request's
+        # learner POJO to node creation)
+        if request.learner.parameters:
+            self.learner.load_parameters(merge_bucketed(request.learner.parameters))
+        for pre, pojo in zip(self.preprocessors, request.preProcessors or []):
+            if pojo.parameters:
+                pre.load_parameters(merge_bucketed(pojo.parameters))
         # hashed-linear pipelines without preprocessors keep their weights in the shared
         # HBM model store so forecasts are scored for all of them in one launch
         self.store, self.store_row = None, None

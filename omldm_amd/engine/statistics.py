@@ -44,51 +44,104 @@ def reduce_query_metrics(comm, loss_sum: float, score_sum: float, n: int, fitted
 
 
 def split_params(params: dict | None, bucket: int = 10000) -> list[dict]:
-    """FlinkNetwork.split: every list longer than ``bucket`` is cut into buckets keyed
-    ``name[start-end]``; bucket i collects the i-th slice of every parameter."""
+    """FlinkNetwork.split (omldm/network/FlinkNetwork.scala:48-149): every value is cut
+    into buckets of ``bucket`` elements — lists by element, strings by character — keyed
+    ``name[start-end]``; bucket i collects the i-th slice of every parameter. A value
+    that fits one bucket keeps its name; a one-element value or slice is unwrapped to
+    the element (``params.head``); a scalar is a one-element value; an empty list or
+    null yields no bucket."""
     if not params:
         return []
     buckets: dict[int, dict] = {}
     for name, val in params.items():
-        arr = val if isinstance(val, (list, tuple)) else [val]
+        if val is None:
+            arr = []
+        elif isinstance(val, (list, tuple, str)):
+            arr = val
+        else:
+            arr = [val]
         n = len(arr)
         nb = n // bucket + (0 if n % bucket == 0 else 1)
-        if nb <= 1:
-            buckets.setdefault(0, {})[name] = arr[0] if n == 1 and not isinstance(val, list) \
-                else val
+        if nb == 1:
+            buckets.setdefault(0, {})[name] = arr[0] if n == 1 else (
+                arr if isinstance(arr, str) else list(arr))
             continue
         for i in range(nb):
             s = i * bucket
-            e = min(n, s + bucket) - 1
-            buckets.setdefault(i, {})[f"{name}[{s}-{e}]"] = list(arr[s:e + 1])
+            e = (s + n % bucket - 1) if (i == nb - 1 and n % bucket) else (i + 1) * bucket - 1
+            sl = arr[s:e + 1]
+            buckets.setdefault(i, {})[f"{name}[{s}-{e}]"] = sl[0] if len(sl) == 1 else (
+                sl if isinstance(sl, str) else list(sl))
     return [buckets[i] for i in sorted(buckets)]
+
+
+_BUCKET_KEY = None
+
+
+def merge_bucketed(params: dict | None) -> dict:
+    """Inverse of ``split_params`` over the union of a response's bucket maps: keys
+    ``name[start-end]`` are reassembled into ``name`` (lists concatenated in start order,
+    strings joined); other keys pass through. What a user does to re-create a pipeline
+    from a bucketed QueryResponse (Create with ``learner.parameters``)."""
+    import re
+
+    global _BUCKET_KEY
+    if _BUCKET_KEY is None:
+        _BUCKET_KEY = re.compile(r"^(.*)\[(\d+)-(\d+)\]$")
+    if not params:
+        return {}
+    parts: dict[str, list] = {}
+    out: dict = {}
+    for k, v in params.items():
+        m = _BUCKET_KEY.match(k)
+        if m is None:
+            out[k] = v
+            continue
+        parts.setdefault(m.group(1), []).append((int(m.group(2)), int(m.group(3)), v))
+    for name, segs in parts.items():
+        segs.sort()
+        if all(isinstance(v, str) for _, _, v in segs):
+            out[name] = "".join(v for _, _, v in segs)
+            continue
+        flat: list = []
+        for s, e, v in segs:
+            if len(flat) != s:
+                raise ValueError(f"bucketed parameter {name!r}: gap before [{s}-{e}]")
+            flat.extend(v if isinstance(v, list) else [v])
+        out[name] = flat
+    return out
 
 
 def build_query_responses(response_id: int, mlp_id: int, preprocessors: list, learner: dict,
                           protocol: str, metrics: dict, bucket: int = 10000) -> list[QueryResponse]:
-    """One QueryResponse, or bucketed ones when the parameters exceed one bucket; the
-    statistics fields ride on the last bucket (FlinkNetwork.scala:187-237)."""
+    """The reference's sendQueryResponse (FlinkNetwork.scala:151-240): with at most two
+    buckets of parameters / hyper-parameters / data structure the response goes out
+    whole (``maxBuckets < 2``); otherwise one response per bucket index, the statistics
+    fields (preprocessors, protocol, dataFitted, loss, cumulativeLoss, score) riding on
+    the last parameter bucket (the last bucket when there are no parameters — the
+    reference drops them in that case)."""
     pb = split_params(learner.get("parameters"), bucket)
     hb = split_params(learner.get("hyperParameters"), bucket)
     sb = split_params(learner.get("dataStructure"), bucket)
     nb = max(len(pb), len(hb), len(sb), 1)
-    if nb < 2:
+    if nb - 1 < 2:
         return [QueryResponse(response_id, 0, mlp_id, preprocessors, learner, protocol,
                               metrics["dataFitted"], metrics["loss"], metrics["cumulativeLoss"],
                               metrics["score"])]
+    stats_at = len(pb) - 1 if pb else nb - 1
     out = []
     for i in range(nb):
         part = {"name": learner.get("name"),
                 "parameters": pb[i] if i < len(pb) else None,
                 "hyperParameters": hb[i] if i < len(hb) else None,
                 "dataStructure": sb[i] if i < len(sb) else None}
-        last = i == nb - 1
-        out.append(QueryResponse(response_id, i, mlp_id, preprocessors if last else None, part,
-                                 protocol if last else None,
-                                 metrics["dataFitted"] if last else None,
-                                 metrics["loss"] if last else None,
-                                 metrics["cumulativeLoss"] if last else None,
-                                 metrics["score"] if last else None))
+        st = i == stats_at
+        out.append(QueryResponse(response_id, i, mlp_id, preprocessors if st else None, part,
+                                 protocol if st else None,
+                                 metrics["dataFitted"] if st else None,
+                                 metrics["loss"] if st else None,
+                                 metrics["cumulativeLoss"] if st else None,
+                                 metrics["score"] if st else None))
     return out
 
 

@@ -150,7 +150,24 @@ class Learner:
         restoring the attribute dict)."""
 
     def parameters_map(self) -> dict:
+        """The learner's COMPLETE parameters as JSON-able lists/scalars — the reference's
+        only portable model format (QueryResponse ``learner.parameters``, bucketed by
+        10,000 on the wire, FlinkNetwork.scala:48-240). ``load_parameters`` of a fresh
+        learner with the same hyper-parameters reproduces the model exactly."""
         return {}
+
+    def load_parameters(self, params: dict) -> None:
+        """Warm start from ``parameters_map()`` output (a Create request's
+        ``learner.parameters``, bucketed keys already merged)."""
+        raise ValueError(f"{self.NAME}: no importable parameters")
+
+    @staticmethod
+    def _vec(params: dict, key: str, n: int | None = None) -> torch.Tensor:
+        v = params[key]
+        t = torch.as_tensor(v if isinstance(v, (list, tuple)) else [v], dtype=torch.float64)
+        if n is not None and t.numel() != n:
+            raise ValueError(f"parameter {key!r}: {t.numel()} values, expected {n}")
+        return t
 
     def data_structure(self) -> dict:
         return {"learner": self.NAME, "task": self.TASK, "nParams": self.num_params()}

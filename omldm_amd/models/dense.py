@@ -37,8 +37,11 @@ class ORR(Learner):
     """Online ridge regression: A = λI + Σxxᵀ, b = Σyx, w = A⁻¹b (intercept included).
     State = the augmented Gram matrix of [x, 1, y] — additive sufficient statistics, so
     worker merges are sums (merge_mode "sum") and exact. The per-round update is one
-    MFMA pass (csrc/kernels/dense_learners.hip: gram_mfma_kernel); the solve is a
-    Cholesky factorisation of the (d+1)×(d+1) system, refreshed lazily."""
+    MFMA pass (csrc/kernels/dense_learners.hip: gram_mfma_kernel) into an fp32 round
+    buffer that starts at zero (bounded: one round's rows), folded into the fp64 master
+    Gram — the reference keeps Breeze fp64 matrices, and an fp32 running sum of an
+    unbounded stream stops absorbing rows. The solve is a Cholesky factorisation of the
+    (d+1)×(d+1) system, refreshed lazily."""
 
     NAME = "ORR"
     TASK = "regression"
@@ -49,14 +52,17 @@ class ORR(Learner):
         super().__init__(hyper, space, device)
         self.d = _in_dim(self.hyper, space)
         self.ld = ((self.d + 2 + 31) // 32) * 32
-        self.G = torch.zeros((self.ld, self.ld), dtype=torch.float32, device=self.device)
+        self.G = torch.zeros((self.ld, self.ld), dtype=torch.float64, device=self.device)
+        self._G32 = torch.zeros((self.ld, self.ld), dtype=torch.float32, device=self.device)
         self._w = None
-        self.lam = hp_float(self.hyper, "lambda", 1.0)
+        self._retune()
 
     def fit(self, batch, ctx):
         if batch.B:
-            D.gram_update(batch.num.float(), batch.y, self.G, cnt=self.cum[1:2],
+            self._G32.zero_()
+            D.gram_update(batch.num.float(), batch.y, self._G32, cnt=self.cum[1:2],
                           pairs=getattr(batch, "pairs", None))
+            self.G += self._G32
         self._w = None
 
     def state_vector(self):
@@ -96,9 +102,30 @@ class ORR(Learner):
         self._w = None
 
     def parameters_map(self):
+        d = self.d
         w = self.weights().cpu()
-        return {"weights": w[: self.d].tolist(), "intercept": float(w[self.d]),
-                "fitted": float(self.G[self.d, self.d])}
+        return {"weights": w[:d].tolist(), "intercept": float(w[d]),
+                "fitted": int(round(float(self.cum[1]))),
+                # the sufficient statistics [x, 1, y]ᵀ[x, 1, y], row-major (d+2)²: what
+                # a warm-started learner needs to keep learning exactly
+                "gram": self.G[: d + 2, : d + 2].cpu().flatten().tolist()}
+
+    def load_parameters(self, params):
+        d = self.d
+        G = torch.zeros((self.ld, self.ld), dtype=torch.float64)
+        if params.get("gram") is not None:
+            G[: d + 2, : d + 2] = self._vec(params, "gram", (d + 2) ** 2).view(d + 2, d + 2)
+        else:  # weights only: b = λ·w with A = λI reproduces w (needs λ > 0)
+            if not self.lam > 0:
+                raise ValueError("ORR: importing weights without 'gram' needs lambda > 0")
+            w = torch.cat([self._vec(params, "weights", d),
+                           torch.tensor([float(params.get("intercept", 0.0))], dtype=torch.float64)])
+            G[: d + 1, d + 1] = self.lam * w
+            G[d + 1, : d + 1] = self.lam * w
+        self.G.copy_(G.to(self.device))
+        if params.get("fitted") is not None:
+            self.cum[1] = float(params["fitted"])
+        self._w = None
 
     def hyper_parameters(self):
         return {**self.hyper, "lambda": self.lam}
@@ -172,7 +199,15 @@ class KMeans(Learner):
         return inert, inert, batch.B
 
     def parameters_map(self):
-        return {"centroids": self.C.cpu().tolist(), "counts": self.n.cpu().tolist()}
+        return {"centroids": self.C.cpu().flatten().tolist(), "counts": self.n.cpu().tolist(),
+                "k": self.k, "dim": self.d}
+
+    def load_parameters(self, params):
+        C = self._vec(params, "centroids", self.k * self.d).float().view(self.k, self.d)
+        n = self._vec(params, "counts", self.k).float()
+        self.C.copy_(C.to(self.device))
+        self.n.copy_(n.to(self.device))
+        self._seeded = self.k  # imported centroids count as seeded
 
 
 # ---------------------------------------------------------------------- MultiClassPA
@@ -251,7 +286,20 @@ class MultiClassPA(Learner):
         return loss, (s.argmax(1) == y).float().sum(), int(ok.sum())
 
     def parameters_map(self):
-        return {"nClasses": self.K, "nonZero": int((self.W != 0).sum())}
+        """K prototypes over the hashed feature space, row-major [K, dim] (intercept in the
+        last slot of each row)."""
+        return {"weights": self.W.detach().float().cpu().flatten().tolist(),
+                "nClasses": self.K, "dim": self.dim}
+
+    def load_parameters(self, params):
+        if params.get("weights") is not None:
+            W = self._vec(params, "weights", self.K * self.dim).float().view(self.K, self.dim)
+        else:
+            W = torch.zeros((self.K, self.dim), dtype=torch.float32)
+            idx = self._vec(params, "nonZeroIndices").long()
+            W.view(-1)[idx] = self._vec(params, "nonZeroWeights", idx.numel()).float()
+        self.W.copy_(W.to(self.device))
+        self.on_state_loaded()
 
 
 # ------------------------------------------------------------------------------ NN
@@ -381,7 +429,25 @@ class NN(Learner):
                 "activation": self.act_name}
 
     def parameters_map(self):
-        return {"layers": [list(s) for s in self.shapes], "nParams": int(self.flat.numel())}
+        """Per layer l: ``W{l}`` (out × in, row-major) and ``b{l}`` — DL4J's
+        MultiLayerNetwork parameter table, flattened."""
+        out = {"layers": [list(s) for s in self.shapes[::2]]}
+        flat = self.flat.detach().float().cpu()
+        o = 0
+        for i, s in enumerate(self.shapes):
+            n = math.prod(s)
+            out[("W" if len(s) == 2 else "b") + str(i // 2)] = flat[o:o + n].tolist()
+            o += n
+        return out
+
+    def load_parameters(self, params):
+        flat = torch.empty(self.flat.numel(), dtype=torch.float32)
+        o = 0
+        for i, s in enumerate(self.shapes):
+            n = math.prod(s)
+            flat[o:o + n] = self._vec(params, ("W" if len(s) == 2 else "b") + str(i // 2), n).float()
+            o += n
+        self.flat.copy_(flat.to(self.device))
 
 
 # ------------------------------------------------------------------------------ HT
@@ -555,8 +621,32 @@ class HT(Learner):
         err = (p != y).float().sum()
         return err, (p == y).float().sum(), int(ok.sum())
 
+    _HT_ARRAYS = ("feature", "threshold", "left", "right", "classCounts", "S0", "S1", "S2",
+                  "lo", "hi", "since")
+
     def parameters_map(self):
+        """The tree (split feature / threshold / children / leaf class counts) and the
+        leaves' sufficient statistics (Gaussian per-(feature, class) moments, ranges,
+        points since the last split check), node-major over the ``nodes`` in use."""
         n = int(self.nnodes.item())
-        return {"nodes": n, "feature": self.feat[:n].int().tolist(),
-                "threshold": self.thr[:n].tolist(), "left": self.left[:n].int().tolist(),
-                "right": self.right[:n].int().tolist(), "classCounts": self.cc[:n].tolist()}
+        arrs = self._tree()[:11]
+        out = {"nodes": n}
+        for name, t in zip(self._HT_ARRAYS, arrs):
+            v = t[:n].detach().float().cpu().flatten()
+            out[name] = [int(x) for x in v.tolist()] if name in ("feature", "left", "right") \
+                else v.tolist()
+        return out
+
+    def load_parameters(self, params):
+        n = int(params["nodes"])
+        if not 1 <= n <= self.N:
+            raise ValueError(f"HT: {n} nodes for a {self.N}-node tree")
+        self.state.zero_()
+        self.feat.fill_(-1)
+        self.lo.fill_(float("inf"))
+        self.hi.fill_(float("-inf"))
+        for name, t in zip(self._HT_ARRAYS, self._tree()[:11]):
+            per = t[0].numel() if t.dim() > 1 else 1
+            v = self._vec(params, name, n * per).float().view((n,) + tuple(t.shape[1:]))
+            t[:n].copy_(v.to(self.device))
+        self.nnodes.fill_(n)

@@ -218,14 +218,35 @@ class LinearLearner(Learner):
                 "learningRate": r.lr, "lambda": r.lam, "bias": r.bias}
 
     def parameters_map(self) -> dict:
-        w = self.w.detach().cpu()
-        nz = torch.nonzero(w[: self.dim - 1]).flatten()
-        return {"weights": w[: self.dim - 1].tolist() if self.dim <= 1 << 16 else None,
-                "nonZeroIndices": nz.tolist(), "nonZeroWeights": w[nz].tolist(),
+        """The reference's VectorBias (weights + intercept): all dim − 1 hashed
+        weights (numerical slots first), dense."""
+        w = self.w.detach().float().cpu()
+        return {"weights": w[: self.dim - 1].tolist(),
                 "intercept": float(w[self.dim - 1]) if self.rule.bias else 0.0}
+
+    def load_parameters(self, params: dict) -> None:
+        """Dense ``weights`` (≤ dim − 1 values) or sparse ``nonZeroIndices`` /
+        ``nonZeroWeights``, plus ``intercept``."""
+        w = torch.zeros(self.dim, dtype=torch.float32)
+        if "weights" in params and params["weights"] is not None:
+            v = self._vec(params, "weights")
+            if v.numel() > self.dim - 1:
+                raise ValueError(f"{self.NAME}: {v.numel()} weights for a {self.dim}-slot model")
+            w[: v.numel()] = v.float()
+        elif "nonZeroIndices" in params:
+            idx = self._vec(params, "nonZeroIndices").long()
+            val = self._vec(params, "nonZeroWeights", idx.numel()).float()
+            if idx.numel() and (idx.min() < 0 or idx.max() >= self.dim - 1):
+                raise ValueError(f"{self.NAME}: weight index out of range")
+            w[idx] = val
+        if self.rule.bias and params.get("intercept") is not None:
+            w[self.dim - 1] = float(params["intercept"])
+        self.w.copy_(w.to(self.device))
+        self.on_state_loaded()
 
     def data_structure(self) -> dict:
         return {**super().data_structure(), "dim": self.dim, "numerical": self.space.dn,
+                "nonZero": int((self.w != 0).sum()),
                 "categorical": self.space.dc, "modelDtype": "bf16" if self.w16 is not None else "fp32"}
 
 

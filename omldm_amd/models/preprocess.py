@@ -54,9 +54,23 @@ class Preprocessor:
         return {"name": self.NAME, "hyperParameters": self.hyper, "parameters": {
             k: (v.tolist() if torch.is_tensor(v) else v) for k, v in self.state_dict().items()}}
 
+    # dtype of each list-valued parameter when imported (to_obj → Create warm start)
+    PARAM_DTYPES: dict = {}
+
+    def load_parameters(self, params: dict) -> None:
+        """Warm start from ``to_obj()["parameters"]`` (a Create's preProcessors entry)."""
+        sd = {}
+        for k, v in params.items():
+            if isinstance(v, list):
+                sd[k] = torch.tensor(v, dtype=self.PARAM_DTYPES.get(k, torch.float32))
+            else:
+                sd[k] = v
+        self.load_state_dict({**self.state_dict(), **sd})
+
 
 class StandardScaler(Preprocessor):
     NAME = "StandardScaler"
+    PARAM_DTYPES = {"mean": torch.float64, "m2": torch.float64}
 
     def __init__(self, hyper=None, device="cpu"):
         super().__init__(hyper, device)

@@ -9,7 +9,9 @@ from omldm_amd.ops.native import check, ptr
 
 
 def _gpu(t: torch.Tensor) -> bool:
-    return t.is_cuda
+    """The fused HIP kernels take fp32 vectors; other dtypes (ORR's fp64 sufficient
+    statistics) use the same math in PyTorch (small vectors, off the hot path)."""
+    return t.is_cuda and t.dtype == torch.float32
 
 
 def drift_norms(x: torch.Tensor, E: torch.Tensor, scale: float,
@@ -21,8 +23,8 @@ def drift_norms(x: torch.Tensor, E: torch.Tensor, scale: float,
         check(native.hip().omldm_drift_norms(ptr(x), ptr(E), x.numel(), float(scale), ptr(out),
                                              native.stream_of(x)), "omldm_drift_norms")
     else:
-        out[0] = ((x - E) * scale).pow(2).sum()
-        out[1] = E.pow(2).sum()
+        out[0] = ((x - E) * scale).pow(2).sum().to(out.dtype)
+        out[1] = E.pow(2).sum().to(out.dtype)
     return out
 
 

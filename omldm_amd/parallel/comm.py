@@ -56,6 +56,12 @@ class Comm:
         self.backend = dist.get_backend(group) if self.enabled else "none"
         self.fault = None  # utils.fault.FaultPlan (tests): may drop this rank's messages
         self.placement: dict = {}  # NUMA binding of this rank (utils/topology.py)
+        # host control plane: tiny per-tick decisions (flags, counters) reduce over gloo on
+        # host tensors, so reading them back never waits for the GPU stream (an RCCL
+        # all-reduce of a device tensor + .tolist() would drain every queued kernel)
+        self.ctrl_group = group
+        if self.enabled and self.world > 1 and self.backend != "gloo":
+            self.ctrl_group = dist.new_group(backend="gloo")
 
     # ------------------------------------------------------------ collectives
     def all_reduce_(self, t: torch.Tensor, tag: str = "sync", op=None, async_op=False):
@@ -65,6 +71,15 @@ class Comm:
         if self.world == 1:
             return None
         return dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+
+    def all_reduce_host_(self, t: torch.Tensor, tag: str = "heartbeat", op=None):
+        """SUM (or ``op``) of a small HOST tensor over the control group (gloo): no device
+        synchronisation."""
+        assert not t.is_cuda
+        self.stats.add(tag, t.numel() * t.element_size(), True)
+        if self.world == 1:
+            return
+        dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.ctrl_group)
 
     def reduce_bcast_(self, t: torch.Tensor, root: int = 0, tag: str = "sync"):
         """Single-hub semantics (HubParallelism == 1): reduce to root, root broadcasts."""

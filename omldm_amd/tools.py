@@ -5,6 +5,9 @@ topics, then ``flink run``):
     python -m omldm_amd.tools produce --bootstrap host:9092 --topic requests --file reqs.jsonl
     python -m omldm_amd.tools tail    --bootstrap host:9092 --topic responses [-n 20]
     python -m omldm_amd.tools synth   --bootstrap host:9092 --topic trainingData --n 100000
+    python -m omldm_amd.tools import-models --bootstrap host:9092 --file ckpt-000003/models.json
+        (re-creates every pipeline of a checkpoint's model export, warm-started, through
+         the requests topic — any world size, any job)
 
 ``--bootstrap`` also accepts ``file:///dir`` (FileBroker) for single-node runs.
 """
@@ -74,6 +77,11 @@ def main(argv=None) -> int:
     s.add_argument("--n", type=int, default=10000)
     s.add_argument("--operation", default="training")
     s.add_argument("--hash-dim", type=int, default=1 << 20)
+    im = sub.add_parser("import-models")
+    im.add_argument("--bootstrap", required=True)
+    im.add_argument("--file", required=True)
+    im.add_argument("--topic", default="requests")
+    im.add_argument("--id-offset", type=int, default=0, help="added to every pipeline id")
     a = ap.parse_args(argv)
     br = broker_for(a.bootstrap)
     if a.cmd == "topics":
@@ -94,6 +102,17 @@ def main(argv=None) -> int:
     elif a.cmd == "tail":
         for rec in _tail(br, a.topic, a.n):
             sys.stdout.write(rec.decode(errors="replace") + "\n")
+    elif a.cmd == "import-models":
+        import json
+
+        from omldm_amd.utils.checkpoint import import_requests
+
+        reqs = import_requests(a.file)
+        for r in reqs:
+            r["id"] = int(r["id"]) + a.id_offset
+            br.produce(a.topic, json.dumps(r))
+        br.flush()
+        print(f"produced {len(reqs)} Create request(s) to {a.topic}")
     elif a.cmd == "synth":
         from omldm_amd.api.batch import FeatureSpace
         from omldm_amd.io.synthetic import synth_json_records

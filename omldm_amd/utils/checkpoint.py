@@ -6,10 +6,16 @@ FsStateBackend — spoke state (test set, pipelines, record/request buffers), hu
 the PipelineMap and Kafka offsets; restore merges list state but loses the spoke
 pipelines.
 
-Here every rank writes ``<stateBackend>/ckpt-<n>/rank-<r>.pt`` (tensors moved to host
-first, so the GPU stream is not held), and rank 0 writes ``manifest.json`` after a
-barrier (so a manifest only exists for complete checkpoints). Everything is restored,
-including the pipelines (Q1 fixed). A checkpoint taken with G ranks restores on G' ranks
+Here every rank snapshots its state at the same tick (rank 0's clock decides, carried in
+the tick's control flags), copies it to host and hands it to a writer thread: the tick
+goes on while ``<stateBackend>/ckpt-<n>/rank-<r>.pt`` is written, then a ``rank-<r>.done``
+marker. Rank 0's writer also exports every pipeline in the reference's portable model
+format (``models.json``: one Create request per pipeline whose ``learner.parameters`` are
+the QueryResponse learner map — what ``python -m omldm_amd.tools import-models`` replays
+into any job) and writes ``manifest.json`` — versioned (``format``/``version``) — only
+once every rank's marker exists, so a manifest only exists for complete checkpoints. No
+barrier or file I/O sits in the tick. Everything is restored, including the pipelines
+(Q1 fixed). A checkpoint taken with G ranks restores on G' ranks
 (``rescale_owners``): new rank r OWNS old ranks {o : o mod G' = r} and takes over exactly
 their per-rank data — record buffers concatenated, holdout rings merged in FIFO order
 (rows beyond the ring are trained on, as the reference's restore does,
@@ -24,9 +30,13 @@ import glob
 import json
 import os
 import shutil
+import threading
 import time
 
 import torch
+
+FORMAT = "omldm-amd-checkpoint"
+VERSION = 2  # 1: round-2 manifests (no format field); 2: + models.json export, done markers
 
 
 def _root(state_backend: str) -> str:
@@ -47,14 +57,19 @@ def rescale_owners(old_world: int, new_world: int, rank: int) -> list[int]:
 
 class Checkpointer:
     KEEP = 3
+    WAIT_S = 600.0  # rank 0's writer waits this long for the other ranks' files
 
     def __init__(self, cfg, rank: int, world: int):
         self.root = _root(cfg.stateBackend)
         self.interval = cfg.checkInterval / 1000.0
         self.rank, self.world = rank, world
+        self.export = bool(getattr(cfg, "checkpointExport", True))
         self.last = time.time()
         os.makedirs(self.root, exist_ok=True)
         self.n = self._latest_index() + 1
+        self._writer: threading.Thread | None = None
+        self.errors: list = []
+        self.completed = 0  # manifests this rank's writer published (rank 0)
 
     def _latest_index(self) -> int:
         best = -1
@@ -69,24 +84,60 @@ class Checkpointer:
         return time.time() - self.last >= self.interval
 
     def save(self, job) -> str:
+        """Snapshot now (host copies), write in the background. At most one write per
+        rank is in flight: a new snapshot first waits for the previous write."""
         d = os.path.join(self.root, f"ckpt-{self.n:06d}")
-        os.makedirs(d, exist_ok=True)
         sd = job.state_dict()
-        tmp = os.path.join(d, f".rank-{self.rank}.pt.tmp")
-        torch.save(sd, tmp)
-        os.replace(tmp, os.path.join(d, f"rank-{self.rank}.pt"))
-        job.comm.barrier()
-        if self.rank == 0:
-            with open(os.path.join(d, "manifest.json"), "w") as f:
-                json.dump({"index": self.n, "world": self.world, "time": time.time(),
-                           "ticks": job.ticks, "pipelines": sorted(job.pipes)}, f)
-            old = sorted(glob.glob(os.path.join(self.root, "ckpt-*")))[:-self.KEEP]
-            for o in old:
-                shutil.rmtree(o, ignore_errors=True)
-        job.comm.barrier()
+        models = export_models(job) if (self.rank == 0 and self.export) else None
+        meta = {"format": FORMAT, "version": VERSION, "index": self.n, "world": self.world,
+                "time": time.time(), "ticks": job.ticks, "pipelines": sorted(job.pipes),
+                "files": [f"rank-{r}.pt" for r in range(self.world)],
+                "models": "models.json" if models is not None else None}
+        self.wait()
+        self._writer = threading.Thread(target=self._write, args=(d, sd, models, meta),
+                                         name=f"omldm-ckpt-{self.n}", daemon=True)
+        self._writer.start()
         self.n += 1
         self.last = time.time()
         return d
+
+    def _write(self, d: str, sd: dict, models, meta: dict) -> None:
+        try:
+            os.makedirs(d, exist_ok=True)
+            tmp = os.path.join(d, f".rank-{self.rank}.pt.tmp")
+            torch.save(sd, tmp)
+            os.replace(tmp, os.path.join(d, f"rank-{self.rank}.pt"))
+            with open(os.path.join(d, f"rank-{self.rank}.done"), "w") as f:
+                f.write("1")
+            if self.rank != 0:
+                return
+            if models is not None:
+                _atomic_json(os.path.join(d, "models.json"), models)
+            t0 = time.time()
+            while not all(os.path.exists(os.path.join(d, f"rank-{r}.done"))
+                          for r in range(self.world)):
+                if time.time() - t0 > self.WAIT_S:
+                    raise TimeoutError(f"checkpoint {d}: ranks did not finish their files")
+                time.sleep(0.01)
+            _atomic_json(os.path.join(d, "manifest.json"), meta)
+            self.completed += 1
+            done = sorted(os.path.dirname(m) for m in
+                          glob.glob(os.path.join(self.root, "ckpt-*", "manifest.json")))
+            for o in done[:-self.KEEP]:
+                shutil.rmtree(o, ignore_errors=True)
+        except Exception as e:  # surfaced by wait() / close()
+            self.errors.append(e)
+
+    def wait(self) -> None:
+        if self._writer is not None:
+            self._writer.join()
+            self._writer = None
+        if self.errors:
+            e, self.errors = self.errors[0], []
+            raise RuntimeError(f"checkpoint write failed: {e}") from e
+
+    def close(self) -> None:
+        self.wait()
 
     def restore(self, job) -> bool:
         idx = self._latest_index()
@@ -95,6 +146,7 @@ class Checkpointer:
         d = os.path.join(self.root, f"ckpt-{idx:06d}")
         with open(os.path.join(d, "manifest.json")) as f:
             man = json.load(f)
+        check_manifest(man)
         old_world = int(man["world"])
         src = self.rank % old_world
 
@@ -122,3 +174,54 @@ class Checkpointer:
             job.load_state_dict(sd, same_world=False, consumer_offsets=offsets, owned=owned)
         self.n = idx + 1
         return True
+
+
+def check_manifest(man: dict) -> int:
+    """Version of a checkpoint manifest this build can restore (round-2 manifests carry
+    no format field: version 1); anything else is refused with a clear error."""
+    fmt = man.get("format", FORMAT)
+    ver = int(man.get("version", 1))
+    if fmt != FORMAT:
+        raise ValueError(f"not an {FORMAT} manifest: format={fmt!r}")
+    if ver > VERSION:
+        raise ValueError(f"checkpoint version {ver} is newer than this build ({VERSION})")
+    for k in ("index", "world"):
+        if k not in man:
+            raise ValueError(f"checkpoint manifest lacks {k!r}")
+    return ver
+
+
+def _atomic_json(path: str, obj) -> None:
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f)
+    os.replace(tmp, path)
+
+
+def export_models(job) -> dict:
+    """Every pipeline as the Create request that re-creates it from the reference's
+    portable model format: learner {name, hyperParameters, parameters} (the QueryResponse
+    learner map, FlinkNetwork.scala:196-230), preprocessors with their parameters, and the
+    training configuration. Replayed by ``tools import-models``."""
+    out = []
+    for pid in sorted(job.pipes):
+        p = job.pipes[pid]
+        req = p.request.to_obj()
+        lrn = p.learner
+        hyper = {k: v for k, v in lrn.hyper_parameters().items() if not k.startswith("_")}
+        req.update({"id": pid, "request": "Create",
+                    "learner": {"name": lrn.NAME, "hyperParameters": hyper,
+                                "parameters": lrn.parameters_map()},
+                    "preProcessors": [pp.to_obj() for pp in p.preprocessors]})
+        out.append({"request": req, "protocol": p.protocol_name,
+                    "dataFitted": lrn.running_totals()["fitted"]})
+    return {"format": "omldm-amd-models", "version": 1, "pipelines": out}
+
+
+def import_requests(path: str) -> list[dict]:
+    """The Create requests of a ``models.json`` export (see export_models)."""
+    with open(path) as f:
+        obj = json.load(f)
+    if obj.get("format") != "omldm-amd-models":
+        raise ValueError(f"{path}: not a model export")
+    return [p["request"] for p in obj["pipelines"]]

@@ -64,6 +64,7 @@ class JobConfig:
     device: str = "auto"                  # auto | cuda | cpu
     maxTicks: int = 0                     # 0: until terminated (tests use a bound)
     restore: bool = False                 # restore from the latest checkpoint in stateBackend
+    checkpointExport: bool = True         # checkpoints also export models.json (Create requests)
     watchdogTimeout: int = 0              # ms without a finished tick → abort + exit (0: off)
     parseThreads: int = 8
     gpuParse: bool = True                 # parse + hash JSON records on the GPU (cuda only)

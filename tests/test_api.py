@@ -58,6 +58,32 @@ def test_split_params_reference_buckets():
     assert b[2]["w[20000-24999]"][-1] == 24999
 
 
+def test_split_params_strings_and_singletons_like_the_reference():
+    """FlinkNetwork.split: strings are bucketed by character, one-element slices unwrap."""
+    b = split_params({"s": "x" * 20001, "one": [7]}, 10000)
+    assert len(b) == 3 and b[0]["s[0-9999]"] == "x" * 10000 and b[2]["s[20000-20000]"] == "x"
+    assert b[0]["one"] == 7
+    assert split_params({"e": [], "n": None}, 10) == []
+
+
+def test_two_buckets_go_out_whole():
+    """maxBuckets < 2 (≤ 2 buckets) ⇒ one unbucketed response (FlinkNetwork.scala:187)."""
+    m = {"dataFitted": 1, "loss": 0.0, "cumulativeLoss": 0.0, "score": 1.0}
+    qs = build_query_responses(1, 1, [], {"name": "PA", "parameters": {"w": [0.0] * 15000}},
+                               "Synchronous", m, 10000)
+    assert len(qs) == 1 and len(qs[0].learner["parameters"]["w"]) == 15000
+
+
+def test_merge_bucketed_inverts_split():
+    from omldm_amd.engine.statistics import merge_bucketed
+
+    params = {"weights": [float(i) for i in range(25003)], "intercept": 0.5, "s": "ab" * 6000}
+    merged = {}
+    for b in split_params(params, 10000):
+        merged.update(b)
+    assert merge_bucketed(merged) == params
+
+
 def test_query_responses_bucketed_last_carries_stats():
     m = {"dataFitted": 10, "loss": 0.5, "cumulativeLoss": 0.4, "score": 0.9}
     learner = {"name": "PA", "parameters": {"weights": [0.0] * 25000}}

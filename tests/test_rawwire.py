@@ -75,9 +75,11 @@ def _golden_round(w, batch, space, R, S, rule, C=1.0, eps=0.1, lr=0.1, bias=True
     return out
 
 
-def test_raw_hash_matches_json_hash():
-    """A 32-bit token hashes exactly like hash_cat of its 4 little-endian bytes."""
+def test_raw_hash_is_field_aware_murmur3():
+    """A 32-bit token hashes as murmur3_32 of its 4 little-endian bytes with the field's
+    seed, into the field's own slot range (dn + f·span, span = (dim − dn − 1) / dc)."""
     space = FeatureSpace(13, 0, 26, 1 << 20)
+    span = (space.dim - 13 - 1) // 26
     rng = np.random.default_rng(1)
     tok = torch.from_numpy(rng.integers(-2**31, 2**31 - 1, size=(7, 26), dtype=np.int64)
                            .astype(np.int32))
@@ -87,8 +89,14 @@ def test_raw_hash_matches_json_hash():
     for i in range(7):
         for j in range(26):
             t = int(tok[i, j]) & 0xFFFFFFFF
-            want = -1 if t == 0xFFFFFFFF else h.omldm_hash_cat(struct.pack("<I", t), 4, j, 13, 1 << 20)
-            assert int(got[i, j]) == want
+            if t == 0xFFFFFFFF:
+                assert int(got[i, j]) == -1
+                continue
+            m = h.omldm_murmur3_32(struct.pack("<I", t), 4, 0x9747B28C + j)
+            slot = 13 + j * span + (m & 0x7FFFFFFF) % span
+            want = slot | 0x80000000 if m & 0x80000000 else slot
+            assert int(got[i, j]) & 0xFFFFFFFF == want
+            assert 13 + j * span <= (int(got[i, j]) & 0x7FFFFFFF) < 13 + (j + 1) * span
 
 
 def test_synth_raw_is_a_pure_function_of_seed_and_position():
@@ -218,3 +226,61 @@ def test_gpu_learner_raw_rounds_track_cpu():
     assert res["cuda"][1]["fitted"] == res["cpu"][1]["fitted"] == 6 * 16 * 700
     assert res["cuda"][1]["overflow"] == 0  # no producer barrier timed out
     assert abs(res["cuda"][1]["mistakes"] - res["cpu"][1]["mistakes"]) <= 0.002 * 6 * 16 * 700
+
+
+def _blocked_gram_scan(w, batch, space, R, S, C=1.0, chunk=64, bias=True):
+    """NumPy model of linear_seq.hip's algorithm (PA-I): per spoke, chunks of 64 rows;
+    round-start margins p = X·w_chunk0, G = X·Xᵀ over the hashed sparse rows, the scalar
+    recurrence m_t = p_t + Σ_{s<t} c_s·G[t][s], then the rank-64 update."""
+    dim = space.dim
+    cat = hash_raw(batch.tok, space).numpy()
+    num = batch.num.double().numpy()
+    y = batch.y.double().numpy()
+    B = batch.B
+    out = w.double().numpy().copy()
+    acc, n_act = np.zeros(dim), 0
+    for s in range(S):
+        a, b = min(s * R, B), min(s * R + R, B)
+        if a >= b:
+            continue
+        n_act += 1
+        W = w.double().numpy().copy()
+        for c0 in range(a, b, chunk):
+            rows = range(c0, min(b, c0 + chunk))
+            X = np.zeros((len(rows), dim))
+            n2 = np.zeros(len(rows))
+            for i, t in enumerate(rows):
+                X[i, :space.dn] = num[t]
+                n2[i] = (num[t] ** 2).sum()
+                for j in range(space.dc):
+                    cc = int(cat[t, j])
+                    if cc != -1:
+                        X[i, cc & 0x7FFFFFFF] += -1.0 if cc < 0 else 1.0
+                        n2[i] += 1.0
+                if bias:
+                    X[i, dim - 1] = 1.0
+                    n2[i] += 1.0
+            p = X @ W
+            G = X @ X.T
+            cvec = np.zeros(len(rows))
+            for i, t in enumerate(rows):
+                m = p[i] + (cvec[:i] * G[i, :i]).sum()
+                loss = max(0.0, 1 - y[t] * m)
+                cvec[i] = min(C, loss / n2[i]) * y[t]
+            W += X.T @ cvec
+        acc += W - w.double().numpy()
+    return out + acc / n_act
+
+
+def test_blocked_gram_scan_algorithm_matches_oracle():
+    """The GPU kernel's math (blocked-exact scan with cross-field slot collisions in a
+    small hash space) equals the per-example oracle."""
+    space = FeatureSpace(5, 0, 8, 1 << 8)  # tiny: many collisions, also across fields
+    batch = synth_raw(space, 300, seed=9, missing=0.05)
+    w = torch.randn(space.dim, generator=torch.Generator().manual_seed(2)) * 0.01
+    wc, dacc = w.clone(), torch.zeros(space.dim + 2)
+    rule = L.LinearRule(rule=L.RULE_HINGE, variant=L.PA1, C=0.7)
+    L.linear_seq_round(wc, batch, 150, 2, dacc, rule, 0.5)
+    L.linear_apply(wc, None, dacc)
+    ref = _blocked_gram_scan(w, batch, space, 150, 2, C=0.7)
+    assert np.allclose(wc.double().numpy(), ref, atol=1e-5, rtol=1e-4)
