@@ -68,6 +68,7 @@ class Pipeline:
             proto = cfg.get("protocol")
         if name in SINGLE_LEARNER_MODELS and comm.world == 1 and proto != "CentralizedTraining":
             cfg.setdefault("virtualSpokes", 1)
+        cfg["_tag"] = self.id  # point-to-point message tag of this pipeline's PS channels
         self.protocol = make_protocol(proto, comm, self.learner, cfg, spokes=spokes,
                                       max_msg_params=max_msg_params)
         self.protocol_name = self.protocol.NAME
@@ -109,6 +110,9 @@ class Pipeline:
         return self.learner.evaluate(self._pre(batch, False))
 
     def close(self) -> None:
+        # drain point-to-point channels (every rank deletes at the same tick), so a
+        # pipeline re-created under the same id starts on clean channels
+        self.protocol.finalize()
         if self.store is not None:
             self.store.remove(self.store_row)
             self.store = None

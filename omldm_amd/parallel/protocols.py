@@ -13,9 +13,11 @@ which is what lets a PS be a collective instead of a server process:
 
 * Synchronous — BSP round: the round delta (fused into the learner's kernel accumulator
   when the learner supports it) is summed by one all-reduce (H>1) or reduce+bcast (H=1).
-* Asynchronous — non-blocking: the round's local progress δ is pushed with an async
-  all-reduce and the merged update is pulled one round later; a worker never waits.
-* SSP — as Asynchronous with up to ``staleness`` pushes in flight.
+* Asynchronous — point-to-point, no barrier: a worker pushes its local progress δ to
+  the hub shard owners (non-blocking isend) and installs the hub's unicast reply when it
+  arrives; a slow worker never stops a fast one (parallel/p2p.py).
+* SSP — the same channels; the hub withholds a worker's reply while its clock leads the
+  slowest worker's by more than ``staleness``.
 * EASGD — elastic averaging toward a centre variable every ``tau`` rounds.
 * GM — geometric monitoring: sync only when some local drift ‖w_i − E‖² leaves the safe
   zone (a 4-byte max-reduction per round decides).
@@ -31,7 +33,6 @@ increments — additive sufficient statistics (ORR, K-means) must be summed.
 from __future__ import annotations
 
 import math
-from collections import deque
 from dataclasses import dataclass
 
 import torch
@@ -40,6 +41,7 @@ from omldm_amd.api.batch import HashedBatch
 from omldm_amd.models.base import Learner, RoundContext
 from omldm_amd.ops import merge as M
 from omldm_amd.parallel.comm import Comm
+from omldm_amd.parallel.p2p import AsyncPS
 
 
 @dataclass
@@ -239,73 +241,73 @@ class Synchronous(Protocol):
             self._E = sd["E"].to(self.learner.device)
 
 
-class _Delayed(Protocol):
-    """Shared machinery of Asynchronous (depth 1) and SSP (depth = staleness).
+class _PointToPoint(Protocol):
+    """Shared machinery of Asynchronous and SSP: every worker's round ends with a
+    non-blocking push of its local progress to the hub shard owners and the install of
+    whatever reply has arrived (parallel/p2p.py: AsyncPS). No collective per round."""
 
-    Invariant: x = E + shipped + new, where E is the merged global model as known here,
-    ``shipped`` the local progress pushed but not yet merged, ``new`` the unpushed rest.
-    A pull replaces the worker's own raw contribution by the merged global increment.
-    """
-
-    depth = 1
+    staleness: int | None = None
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
-        self._E = None
-        self._shipped = None
-        self._inflight: deque = deque()  # (work, reduced_buf, sent)
+        self._ps = None
+        self.tag = _cfg_int(self.cfg, "_tag", 0)
 
-    def _pull_one(self):
-        work, buf, sent = self._inflight.popleft()
-        if work is not None:
-            work.wait()
-        M.async_pull(self.learner.state_vector(), self._E, self._shipped, sent, buf,
-                     self._scale())
-        self.learner.on_state_loaded()
+    def _make(self):
+        x = self.learner.state_vector()
+        hubs = self.hubs if self.hubs > 0 else 1
+        self._ps = AsyncPS(self.comm, x.numel(), x.dtype, hubs, self.tag, self.staleness,
+                           self._scale())
+        self._ps.init(x)
 
     def round(self, batch):
         L = self.learner
-        if self._E is None:
-            self._E = L.state_vector().detach().clone()
-            self._shipped = torch.zeros_like(self._E)
+        if self.comm.world > 1 and self._ps is None:
+            self._make()  # every rank starts from the same (initial / restored) model
         L.fit(batch, self._ctx())
-        sent, buf = torch.empty_like(self._E), torch.empty_like(self._E)
-        M.async_push(L.state_vector(), self._E, self._shipped, sent, buf)
-        work = self.comm.all_reduce_(buf, tag="push", async_op=True)
-        self._inflight.append((work, buf, sent))
-        self._account_model_sync(L.num_params(), buf.numel() * buf.element_size())
-        while len(self._inflight) > self.depth:
-            self._pull_one()
         self.stats.rounds += 1
+        if self._ps is None:
+            return  # one worker: its local model IS the global model
+        x = L.state_vector()
+        installs = self._ps.installs
+        if self._ps.step(x):
+            nbytes = x.numel() * x.element_size()
+            self.stats.syncs += 1
+            self.stats.models_shipped += 2  # one push, one reply (unicast)
+            self.stats.bytes_shipped += 2 * nbytes
+            self.stats.num_of_blocks += 2 * max(1, math.ceil(x.numel() / self.max_msg_params))
+        if self._ps.installs != installs:
+            L.on_state_loaded()
+
+    @property
+    def max_lead(self) -> int:
+        return self._ps.max_lead if self._ps is not None else 0
 
     def finalize(self):
-        while self._inflight:
-            self._pull_one()
+        if self._ps is not None and self.comm.world > 1:
+            self._ps.finalize(self.learner.state_vector())
+            self.learner.on_state_loaded()
 
     def state_dict(self):
         self.finalize()
-        sd = super().state_dict()
-        sd["E"] = None if self._E is None else self._E.cpu()
-        return sd
+        return super().state_dict()
 
     def load_state_dict(self, sd):
         super().load_state_dict(sd)
-        if sd.get("E") is not None:
-            self._E = sd["E"].to(self.learner.device)
-            self._shipped = torch.zeros_like(self._E)
+        self._ps = None  # re-seeded from the restored model at the next round
 
 
-class Asynchronous(_Delayed):
+class Asynchronous(_PointToPoint):
     NAME = "Asynchronous"
-    depth = 1
+    staleness = None
 
 
-class SSP(_Delayed):
+class SSP(_PointToPoint):
     NAME = "SSP"
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
-        self.depth = max(0, _cfg_int(self.cfg, "staleness", 2))
+        self.staleness = max(0, _cfg_int(self.cfg, "staleness", 2))
 
 
 class EASGD(Protocol):

@@ -114,6 +114,11 @@ class Watchdog:
                 sys.stderr.write(f"[watchdog] rank {self.rank}: no progress for "
                                  f"{self.timeout:.1f}s — aborting\n")
                 sys.stderr.flush()
+                try:  # where every thread is stuck: the first thing a hang report needs
+                    import faulthandler
+                    faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                except Exception:
+                    pass
                 if self.on_expire is not None:
                     self.on_expire()
                     return

@@ -1,0 +1,115 @@
+"""Genuinely asynchronous Asynchronous and SSP protocols (parallel/p2p.py) on gloo, three
+ranks, one of them a straggler (50 ms per round).
+
+Reference: AsynchronousWorker / SSPWorker get unicast hub replies with no barrier
+(FlinkNetwork.scala:262-271, MLNodeGenerator.scala:26-33,55-62); an SSP hub withholds the
+reply of a worker more than ``staleness`` clocks ahead of the slowest.
+"""
+import json
+import os
+import shutil
+import socket
+import subprocess
+import sys
+import tempfile
+import textwrap
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = textwrap.dedent(r"""
+    import json, os, sys, time
+    sys.path.insert(0, sys.argv[1])
+    import torch
+    import torch.distributed as dist
+    from omldm_amd.api.batch import FeatureSpace
+    from omldm_amd.io.synthetic import synth_raw
+    from omldm_amd.models.linear import SVM
+    from omldm_amd.ops import linear as L
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.parallel.protocols import make_protocol
+
+    proto_name, seconds, slow = sys.argv[2], float(sys.argv[3]), int(sys.argv[4])
+    dist.init_process_group("gloo")
+    comm = Comm()
+    rank, world = comm.rank, comm.world
+    space = FeatureSpace(13, 0, 26, 1 << 12)
+    lrn = SVM({"variant": "PA-I"}, space, "cpu")
+    cfg = {"virtualSpokes": 2, "staleness": 2, "_tag": 3}
+    proto = make_protocol(proto_name, comm, lrn, cfg)
+    pool = [synth_raw(space, 256, start=(k * world + rank) * 256, seed=25).hashed(space)
+            for k in range(16)]
+    dist.barrier()
+    t0 = time.time()
+    k = 0
+    fixed = proto_name == "Synchronous"  # collectives: every rank runs the same rounds
+    while (k < 20) if fixed else (time.time() - t0 < seconds):
+        proto.round(pool[k % len(pool)])
+        if rank == slow:
+            time.sleep(0.05)
+        k += 1
+    proto.finalize()
+    elapsed = time.time() - t0
+    test = synth_raw(space, 4000, start=10**9, seed=25).hashed(space)
+    acc = float(((L.linear_predict(lrn.w, test) >= 0).float() * 2 - 1 == test.y).float().mean())
+    out = {"rank": rank, "rounds": k, "elapsed": elapsed, "acc": acc, "w0": float(lrn.w[5]),
+           "max_lead": getattr(proto, "max_lead", None),
+           "collectives": comm.stats.collectives}
+    with open(os.path.join(sys.argv[5], f"rank{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+""")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(proto, seconds=2.5, slow=1, world=3):
+    outdir = tempfile.mkdtemp(prefix="omldm_async_")
+    script = os.path.join(outdir, "worker.py")
+    with open(script, "w") as f:
+        f.write(WORKER)
+    env = dict(os.environ, OMP_NUM_THREADS="1", OMLDM_CPU_THREADS="1")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+                          "--master-port", str(_port()), script, ROOT, proto, str(seconds),
+                          str(slow), outdir], capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    res = {}
+    for r in range(world):
+        with open(os.path.join(outdir, f"rank{r}.json")) as f:
+            res[r] = json.load(f)
+    shutil.rmtree(outdir, ignore_errors=True)
+    return res
+
+
+def test_asynchronous_straggler_does_not_stall_fast_workers():
+    r = _run("Asynchronous")
+    slow = r[1]["rounds"]
+    assert r[0]["rounds"] >= 3 * slow and r[2]["rounds"] >= 3 * slow, r
+    # after finalize every rank holds the hub's global model, and it learned
+    assert r[0]["w0"] == r[1]["w0"] == r[2]["w0"]
+    assert min(x["acc"] for x in r.values()) > 0.7, r
+
+
+def test_ssp_bounds_the_lead_over_the_straggler():
+    r = _run("SSP")
+    slow = r[1]["rounds"]
+    # the hub answers a worker only within 2 clocks of the slowest: the fast workers' rounds
+    # stay within the bound (+1 for the push in flight, +1 for the final round)
+    assert r[0]["rounds"] <= slow + 2 + 2 and r[2]["rounds"] <= slow + 2 + 2, r
+    assert r[0]["max_lead"] <= 2, r  # rank 0 is the hub: the leads it answered
+    assert r[0]["w0"] == r[1]["w0"] == r[2]["w0"]
+    assert min(x["acc"] for x in r.values()) > 0.6, r
+
+
+def test_synchronous_is_paced_by_the_straggler_for_contrast():
+    r = _run("Synchronous")
+    # 20 lock-step rounds: the fast ranks wait out the straggler's 20 x 50 ms
+    assert r[0]["elapsed"] >= 0.9 and r[2]["elapsed"] >= 0.9, r
+    assert r[0]["w0"] == r[1]["w0"] == r[2]["w0"]
