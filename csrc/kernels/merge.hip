@@ -113,6 +113,75 @@ __global__ __launch_bounds__(256) void async_pull_kernel(float* __restrict__ x,
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// GM / FGM monitoring decisions on the device (one lane): the per-round safe-zone test and
+// the replicated hub logic read the 2-float drift norms where drift_norms_kernel left them
+// and write the message to reduce / the sync decision — no host round-trip inside a round.
+// The host reads the decision one round later through a pinned copy (protocols.py).
+//
+// FGM state st[8] (fp64): 0 c_prev (this worker's counter), 1 csum (Σ increments, hub),
+// 2 theta (quantum; 0 ⇔ E == 0), 3 phi0 = −ε‖E‖², 4 phi (this worker's last φ),
+// 5 decision latch (1 = full sync due), 6 subrounds.
+constexpr double kFgmBig = 1e12;  // counter of a worker that drifted while E == 0
+
+__device__ inline double fgm_counter(double phi, double phi0, double theta) {
+  const double num = phi - phi0;
+  if (theta <= 0.0) return num > 0.0 ? kFgmBig : 0.0;
+  return fmin(kFgmBig, fmax(0.0, floor(num / theta)));
+}
+
+// GM: msg[0] = 1 when ‖X_i‖² > θ·max(‖E‖², 1) (max-reduced over workers)
+__global__ void gm_local_kernel(const float* __restrict__ nrm, float thr, double* __restrict__ msg) {
+  if (threadIdx.x == 0) msg[0] = nrm[0] > thr * fmaxf(nrm[1], 1.f) ? 1.0 : 0.0;
+}
+
+// FGM worker: φ = ‖X_i‖² − ε‖E‖²; counter increment since the last report; msg = (Δc, φ)
+__global__ void fgm_local_kernel(const float* __restrict__ nrm, double* __restrict__ st,
+                                 double eps, double* __restrict__ msg) {
+  if (threadIdx.x != 0) return;
+  const double phi = (double)nrm[0] - eps * (double)nrm[1];
+  const double c = fgm_counter(phi, st[3], st[2]);
+  msg[0] = c - st[0];
+  msg[1] = phi;
+  st[0] = c;
+  st[4] = phi;
+}
+
+// FGM hub (replicated on every rank from the reduced msg): Σ counters > G ends the
+// subround; ψ = Σφ ≥ ε_ψ·G·φ(0) ends the round (full sync due), otherwise θ = −ψ/(2G).
+__global__ void fgm_hub_kernel(double* __restrict__ st, const double* __restrict__ msg,
+                               double eps_psi, int G, double* __restrict__ flag) {
+  if (threadIdx.x != 0) return;
+  if (st[5] == 0.0) {
+    st[1] += msg[0];
+    if (st[1] > (double)G) {
+      st[6] += 1.0;
+      const double psi = msg[1];
+      if (psi >= eps_psi * (double)G * st[3]) {
+        st[5] = 1.0;
+      } else {
+        st[2] = -psi / (2.0 * G);
+        st[1] = 0.0;
+        st[0] = fgm_counter(st[4], st[3], st[2]);  // counters restart in the new subround
+      }
+    }
+  }
+  flag[0] = st[5];
+}
+
+// FGM round start (after a full sync, E = x): φ(0) = −ε‖E‖², θ = −ψ/(2G) = −φ(0)/2
+__global__ void fgm_begin_kernel(const float* __restrict__ nrm, double* __restrict__ st,
+                                 double eps) {
+  if (threadIdx.x != 0) return;
+  const double phi0 = -eps * (double)nrm[1];
+  st[0] = 0.0;
+  st[1] = 0.0;
+  st[2] = phi0 < 0.0 ? -phi0 / 2.0 : 0.0;
+  st[3] = phi0;
+  st[4] = 0.0;
+  st[5] = 0.0;
+}
+
 static inline int grid_for(long long n) {
   long long b = (n + 255) / 256;
   if (b > 4096) b = 4096;
@@ -163,6 +232,30 @@ OMLDM_API int omldm_async_push(const float* x, const float* E, float* shipped, f
   if (n <= 0) return 0;
   hipLaunchKernelGGL(async_push_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x,
                      E, shipped, sent, buf, n);
+  return (int)hipGetLastError();
+}
+
+OMLDM_API int omldm_gm_local(const float* nrm, float thr, double* msg, void* stream) {
+  hipLaunchKernelGGL(gm_local_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, nrm, thr, msg);
+  return (int)hipGetLastError();
+}
+
+OMLDM_API int omldm_fgm_local(const float* nrm, double* st, double eps, double* msg,
+                              void* stream) {
+  hipLaunchKernelGGL(fgm_local_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, nrm, st, eps,
+                     msg);
+  return (int)hipGetLastError();
+}
+
+OMLDM_API int omldm_fgm_hub(double* st, const double* msg, double eps_psi, int G, double* flag,
+                            void* stream) {
+  hipLaunchKernelGGL(fgm_hub_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, st, msg, eps_psi,
+                     G, flag);
+  return (int)hipGetLastError();
+}
+
+OMLDM_API int omldm_fgm_begin(const float* nrm, double* st, double eps, void* stream) {
+  hipLaunchKernelGGL(fgm_begin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, nrm, st, eps);
   return (int)hipGetLastError();
 }
 

@@ -25,6 +25,7 @@ _hip = None
 _host = None
 
 vp, i32, i64, u32, u64, f32 = C.c_void_p, C.c_int, C.c_longlong, C.c_uint32, C.c_uint64, C.c_float
+f64 = C.c_double
 
 
 class NativeMissing(RuntimeError):
@@ -82,6 +83,10 @@ HIP_SIGS = [
     ("omldm_elastic_post", i32, [vp, vp, vp, vp, f32, i64, vp]),
     ("omldm_async_push", i32, [vp, vp, vp, vp, vp, i64, vp]),
     ("omldm_async_pull", i32, [vp, vp, vp, vp, vp, f32, i64, vp]),
+    ("omldm_gm_local", i32, [vp, f32, vp, vp]),
+    ("omldm_fgm_local", i32, [vp, vp, f64, vp, vp]),
+    ("omldm_fgm_hub", i32, [vp, vp, f64, i32, vp, vp]),
+    ("omldm_fgm_begin", i32, [vp, vp, f64, vp]),
     ("omldm_holdout_route", i32, [vp, vp, vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, i64, i64,
                                   i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp]),
     ("omldm_json_parse", i32, [vp, vp, i32, i32, i32, i32, i64, i32, vp, vp, vp, vp, vp, vp]),

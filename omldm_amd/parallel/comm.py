@@ -92,9 +92,9 @@ class Comm:
     def hub_reduce_(self, t: torch.Tensor, hubs: int = 0, tag: str = "sync"):
         """Sum ``t`` over workers through ``hubs`` parameter-server shards.
         hubs == 1: one hub (rank 0) — reduce + broadcast;
-        1 < hubs < world: hub h (rank h) owns the h-th contiguous slice — one reduce to and
-        one broadcast from each hub (the reference's sharded PS, FlinkHub keyed
-        ``net_hubIdx``);
+        1 < hubs < world: hub h (rank h) owns the h-th contiguous slice — every worker pushes
+        each slice to its hub and pulls the summed slice back, point-to-point (the
+        reference's sharded PS, FlinkHub keyed ``net_hubIdx``; _sharded_ps_);
         hubs == 0 or ≥ world: every rank is a hub — all-reduce (reduce-scatter +
         all-gather inside RCCL)."""
         if self.world == 1:
@@ -102,17 +102,63 @@ class Comm:
         elif hubs == 1:
             self.reduce_bcast_(t, 0, tag)
         elif 1 < hubs < self.world:
-            flat = t.view(-1)
-            n = flat.numel()
-            step = -(-n // hubs)
-            self.stats.add(tag, 2 * n * t.element_size())
-            for h in range(hubs):
-                sl = flat[h * step:min(n, (h + 1) * step)]
-                if sl.numel():
-                    dist.reduce(sl, dst=h, op=dist.ReduceOp.SUM, group=self.group)
-                    dist.broadcast(sl, src=h, group=self.group)
+            self._sharded_ps_(t, hubs, tag)
         else:
             self.all_reduce_(t, tag)
+
+    def _sharded_ps_(self, t: torch.Tensor, hubs: int, tag: str) -> None:
+        """1 < H < G parameter-server shards over point-to-point channels: phase 1 every
+        rank sends slice h to hub h (all sends/receives of the phase are posted at once,
+        so on a node they run concurrently over the direct xGMI links — a hub receives
+        its G−1 slices on G−1 different links), the hub sums them in rank order; phase 2
+        each hub sends its summed slice back to every rank. Per rank ≈ 2·n elements cross
+        the wire, the same as a ring all-reduce, in two latency steps instead of the 2H
+        serialised reduce/broadcast collectives."""
+        flat = t.view(-1)
+        n = flat.numel()
+        step = -(-n // hubs)
+        sl = [flat[h * step:min(n, (h + 1) * step)] for h in range(hubs)]
+        me, G = self.rank, self.world
+        self.stats.add(tag, 2 * n * t.element_size())
+        bufs = {}
+        ops = []
+        for h in range(hubs):
+            if h != me and sl[h].numel():
+                ops.append(dist.P2POp(dist.isend, sl[h], h, group=self.group))
+        if me < hubs and sl[me].numel():
+            for r in range(G):
+                if r != me:
+                    bufs[r] = self._p2p_buf(r, sl[me])
+                    ops.append(dist.P2POp(dist.irecv, bufs[r], r, group=self.group))
+        self._run_p2p(ops)
+        if bufs:
+            acc = sl[me]
+            parts = [acc.clone() if r == me else bufs[r] for r in range(G)]
+            acc.copy_(torch.stack(parts).sum(0))
+        ops = []
+        if me < hubs and sl[me].numel():
+            for r in range(G):
+                if r != me:
+                    ops.append(dist.P2POp(dist.isend, sl[me], r, group=self.group))
+        for h in range(hubs):
+            if h != me and sl[h].numel():
+                ops.append(dist.P2POp(dist.irecv, sl[h], h, group=self.group))
+        self._run_p2p(ops)
+
+    def _p2p_buf(self, r: int, like: torch.Tensor) -> torch.Tensor:
+        cache = self.__dict__.setdefault("_p2p_bufs", {})
+        key = (r, like.numel(), like.dtype, like.device)
+        b = cache.get(key)
+        if b is None:
+            b = cache[key] = torch.empty_like(like)
+        return b
+
+    @staticmethod
+    def _run_p2p(ops) -> None:
+        if not ops:
+            return
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
 
     def all_reduce_coalesced_(self, ts: list[torch.Tensor], tag: str = "sync", hubs: int = 0,
                               bucket_bytes: int = 64 << 20):
@@ -185,35 +231,43 @@ class Comm:
         return out
 
     def gather_tensor(self, t: torch.Tensor, dst: int = 0) -> list[torch.Tensor] | None:
-        """Variable-length gather along dim 0 (pads to the max length)."""
+        """Variable-length gather along dim 0 to ``dst`` only: the row counts travel over
+        the host control group (no device sync), then every worker sends its rows to the
+        hub point-to-point (RCCL send/recv over the xGMI link to the hub on GPUs) — the
+        hub alone receives, nothing is padded or all-gathered (the reference's
+        ForwardingWorker → CentralizedMLServer, MLNodeGenerator.scala:27,56)."""
         if self.world == 1:
             return [t]
-        n = torch.tensor([t.shape[0]], device=t.device, dtype=torch.int64)
-        ns = [torch.zeros_like(n) for _ in range(self.world)]
-        dist.all_gather(ns, n, group=self.group)
-        ns = [int(x.item()) for x in ns]
-        mx = max(ns)
-        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        pad[: t.shape[0]] = t
-        wire = None
-        if t.dtype in _BYTE_WIRE:
+        n = torch.tensor([t.shape[0]], dtype=torch.int64)
+        ns_t = [torch.zeros_like(n) for _ in range(self.world)] if self.rank == dst else None
+        dist.gather(n, ns_t, dst=dst, group=self.ctrl_group)
+        wire_dtype = t.dtype
+        src = t.contiguous()
+        if wire_dtype in _BYTE_WIRE:
             # int16 (the compact categorical slots), bool, …: neither RCCL nor gloo has the
-            # type, so the rows travel as their bytes and are viewed back after the gather
-            wire, pad = pad, pad.contiguous().view(torch.uint8)
-        outs = [torch.zeros_like(pad) for _ in range(self.world)] if self.rank == dst else None
-        if self.backend == "nccl":
-            # RCCL has no gather; all_gather keeps it a single collective.
-            outs_all = [torch.zeros_like(pad) for _ in range(self.world)]
-            dist.all_gather(outs_all, pad, group=self.group)
-            outs = outs_all if self.rank == dst else None
-        else:
-            dist.gather(pad, outs, dst=dst, group=self.group)
-        self.stats.add("gather", pad.numel() * pad.element_size())
+            # type, so the rows travel as their bytes and are viewed back on arrival
+            src = src.view(torch.uint8)
+        row_shape = tuple(src.shape[1:])
         if self.rank != dst:
+            if t.shape[0]:
+                self.stats.add("gather", src.numel() * src.element_size())
+                dist.send(src, dst=dst, group=self.group)
             return None
-        if wire is not None:
-            outs = [o.view(wire.dtype) for o in outs]
-        return [o[:k] for o, k in zip(outs, ns)]
+        ns = [int(x[0]) for x in ns_t]
+        outs, works = [], []
+        for r, k in enumerate(ns):
+            if r == dst:
+                outs.append(src)
+                continue
+            buf = torch.empty((k,) + row_shape, dtype=src.dtype, device=src.device)
+            outs.append(buf)
+            if k:
+                works.append(dist.irecv(buf, src=r, group=self.group))
+        for w in works:
+            w.wait()
+        if wire_dtype in _BYTE_WIRE:
+            outs = [o.view(wire_dtype) for o in outs]
+        return outs
 
     def barrier(self):
         if self.world > 1:

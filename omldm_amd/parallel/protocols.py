@@ -20,9 +20,11 @@ which is what lets a PS be a collective instead of a server process:
   slowest worker's by more than ``staleness``.
 * EASGD — elastic averaging toward a centre variable every ``tau`` rounds.
 * GM — geometric monitoring: sync only when some local drift ‖w_i − E‖² leaves the safe
-  zone (a 4-byte max-reduction per round decides).
-* FGM — functional geometric monitoring with rounds/subrounds: an 8-byte sum-reduction of
-  (counter increment, φ) per local round; a full model sync only at round end.
+  zone (an 8-byte max-reduction per round decides, on the device).
+* FGM — functional geometric monitoring with rounds/subrounds: a 16-byte sum-reduction of
+  (counter increment, φ) per local round, worker and hub logic on the device; a full
+  model sync only at round end. GM/FGM read their decision one round late (no host sync
+  inside a round).
 * CentralizedTraining — one worker, no communication.
 * SingleLearner — workers forward their points to the hub rank (0), which alone trains
   (HT, K-means); the hub model is broadcast back for serving.
@@ -369,36 +371,93 @@ def _model_sync(p: Protocol) -> None:
     p._account_model_sync(L.num_params(), d.numel() * d.element_size())
 
 
-class GM(Protocol):
-    NAME = "GM"
+class _LaggedDecision:
+    """A device-computed sync decision read by the host one round later.
+
+    The monitor writes its (reduced) decision into a device scalar and ``post`` starts a
+    non-blocking copy into pinned host memory behind it. ``take`` — called after the next
+    round's training kernels are enqueued — waits only for that copy, so the GPU always
+    has the next round queued while the host decides: no drain of the stream inside a
+    round. Every rank reduces the same flag, so every rank takes the same decision at the
+    same round and issues the same collectives."""
+
+    def __init__(self, device):
+        self.dev = torch.zeros(1, dtype=torch.float64, device=device)
+        cuda = self.dev.is_cuda
+        self.host = torch.zeros(1, dtype=torch.float64, pin_memory=cuda)
+        self._event = None
+        self.pending: float | None = None  # a decision restored from a checkpoint
+
+    def post(self) -> None:
+        if self.dev.is_cuda:
+            self.host.copy_(self.dev, non_blocking=True)
+            self._event = torch.cuda.Event()
+            self._event.record()
+        else:
+            self.host.copy_(self.dev)
+            self._event = True
+
+    def take(self) -> float | None:
+        if self.pending is not None:
+            v, self.pending = self.pending, None
+            return v
+        if self._event is None:
+            return None
+        if self._event is not True:
+            self._event.synchronize()
+        self._event = None
+        return float(self.host[0])
+
+    def peek_for_checkpoint(self) -> float | None:
+        """The outstanding decision, kept outstanding (a checkpoint must not change the
+        trajectory)."""
+        v = self.take()
+        self.pending = v
+        return v
+
+
+class _Monitored(Protocol):
+    """GM / FGM machinery: the estimate E, the lagged decision and the reduction of the
+    per-round monitoring message (RCCL on the device; over gloo through host memory)."""
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
-        self.threshold = _cfg_float(self.cfg, "threshold", 0.05)
         self._E = None
-        self._flag = None
+        self._lag = None
+        self._nrm = None
+        self._msg = None
+
+    def _buffers(self, nmsg: int):
+        if self._lag is None:
+            dev = self.learner.device
+            self._lag = _LaggedDecision(dev)
+            self._nrm = torch.zeros(2, dtype=torch.float32, device=dev)
+            self._msg = torch.zeros(nmsg, dtype=torch.float64, device=dev)
+
+    def _reduce_msg(self, tag: str, op=None) -> None:
+        if self.G > 1:
+            m = self._msg
+            if self.comm.backend == "nccl" or not m.is_cuda:
+                self.comm.all_reduce_(m, tag=tag, op=op)
+            else:  # gloo rehearsal with device tensors: through host memory
+                h = m.cpu()
+                self.comm.all_reduce_(h, tag=tag, op=op)
+                m.copy_(h)
+        self._account_small(self.G, self._msg.numel() * self._msg.element_size())
 
     def _full_sync(self):
         _model_sync(self)
 
-    def round(self, batch):
-        L = self.learner
-        if self._E is None:
-            self._E = L.state_vector().detach().clone()
-        L.fit(batch, self._ctx())
-        x = L.state_vector()
-        scale = self.G if L.merge_mode == "sum" else 1.0
-        x2, e2 = M.drift_norms(x, self._E, scale).tolist()  # [‖X_i‖², ‖E‖²], one pass
-        # safe zone: ‖X_i‖² ≤ θ·‖E‖² (θ·1 while E == 0); the decision is host arithmetic
-        viol = 1.0 if x2 > self.threshold * max(e2, 1.0) else 0.0
-        if self.G > 1:
-            v = self._small([viol])
-            self.comm.all_reduce_(v, tag="gm-flag", op=torch.distributed.ReduceOp.MAX)
-            viol = float(v.item())
-        self._account_small(self.G, 4)
-        if viol > 0:
-            self._full_sync()
-        self.stats.rounds += 1
+    def finalize(self):
+        """End of stream / query / checkpoint: a sync that is due is carried out now."""
+        if self._lag is not None and self._E is not None:
+            v = self._lag.take()
+            if v:
+                self._full_sync()
+                self._after_sync()
+
+    def _after_sync(self) -> None:
+        pass
 
     # E is identical on every rank (it only changes in a full sync) while the local
     # models differ by their unsynced drifts: E must be checkpointed, or a restored rank
@@ -406,15 +465,51 @@ class GM(Protocol):
     def state_dict(self):
         sd = super().state_dict()
         sd["E"] = None if self._E is None else self._E.cpu()
+        sd["pending"] = None if self._lag is None else self._lag.peek_for_checkpoint()
         return sd
 
     def load_state_dict(self, sd):
         super().load_state_dict(sd)
         if sd.get("E") is not None:
             self._E = sd["E"].to(self.learner.device)
+        self._lag = None
+        if sd.get("pending") is not None:
+            self._buffers(self.NMSG)
+            self._lag.pending = float(sd["pending"])
 
 
-class FGM(Protocol):
+class GM(_Monitored):
+    """Geometric monitoring: a worker leaves the safe zone when ‖X_i‖² > θ·‖E‖²; one
+    8-byte max-reduction per round; the decision is taken on the device and read by the
+    host one round later (the sync happens after the round following the violation)."""
+
+    NAME = "GM"
+    NMSG = 1
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.threshold = _cfg_float(self.cfg, "threshold", 0.05)
+
+    def round(self, batch):
+        L = self.learner
+        if self._E is None:
+            self._E = L.state_vector().detach().clone()
+        self._buffers(self.NMSG)
+        L.fit(batch, self._ctx())
+        if self._lag.take():
+            self._full_sync()  # x = E: no drift left to monitor this round
+        else:
+            x = L.state_vector()
+            scale = self.G if L.merge_mode == "sum" else 1.0
+            M.drift_norms(x, self._E, scale, out=self._nrm)   # [‖X_i‖², ‖E‖²], one pass
+            M.gm_local(self._nrm, self.threshold, self._msg)   # safe-zone test, on device
+            self._reduce_msg("gm-flag", op=torch.distributed.ReduceOp.MAX)
+            self._lag.dev.copy_(self._msg[:1])
+            self._lag.post()
+        self.stats.rounds += 1
+
+
+class FGM(_Monitored):
     """Functional Geometric Monitoring (variance safe function).
 
     Safe function on a worker's drift X_i (state − E, scaled by G for additive state):
@@ -423,97 +518,73 @@ class FGM(Protocol):
     subround: worker counter c_i = ⌊(φ(X_i) − φ(0)) / θ⌋, the hub sums increments;
     when Σ c_i > G the hub collects ψ = Σ φ(X_i): if ψ ≥ ε_ψ·G·φ(0) the round ends with
     a full model sync, otherwise a new subround starts with θ = −ψ / (2G).
-    The hub logic runs replicated on every rank from one 2-float all-reduce per local
-    round ((Δc_i, φ_i)), so only round ends move models over xGMI.
+    The worker and the (replicated) hub logic run on the device (merge.hip fgm_*_kernel)
+    around one 16-byte all-reduce per local round ((Δc_i, φ_i)); only the full-sync
+    decision reaches the host, one round late (_LaggedDecision), so only round ends move
+    models over xGMI and no round drains the stream.
     """
 
     NAME = "FGM"
+    NMSG = 2
 
     def __init__(self, *a, **k):
         super().__init__(*a, **k)
         self.eps = _cfg_float(self.cfg, "epsilon", 0.05)
         self.eps_psi = _cfg_float(self.cfg, "epsilonPsi", 0.01)
-        self._E = None
-        self._c_prev = 0.0     # this worker's counter in the current subround
-        self._csum = 0.0       # Σ counter increments of all workers (hub, replicated)
-        self._theta = None
-        self._phi0 = None
-        self.subrounds = 0
+        self._st = None
         self.fgm_rounds = 0
 
     def _begin_round(self):
         L = self.learner
-        self._E = L.state_vector().detach().clone()
-        e2 = float(self._E.pow(2).sum().item())
-        self._phi0 = -self.eps * e2
-        psi = self.G * self._phi0
-        self._theta = -psi / (2 * self.G) if psi < 0 else None
-        self._c_prev = 0.0
+        x = L.state_vector()
+        if self._E is None:
+            self._E = x.detach().clone()
+        M.drift_norms(x, self._E, 1.0, out=self._nrm)  # [·, ‖E‖²]
+        M.fgm_begin(self._nrm, self._st, self.eps)
         self.fgm_rounds += 1
 
-    def _full_sync(self):
-        _model_sync(self)
+    def _after_sync(self):
+        self._begin_round()
+
+    @property
+    def subrounds(self) -> int:
+        return 0 if self._st is None else int(self._st[6].item())
 
     def round(self, batch):
         L = self.learner
-        if self._E is None:
+        self._buffers(self.NMSG)
+        if self._st is None:
+            self._st = torch.zeros(8, dtype=torch.float64, device=L.device)
             self._begin_round()
         L.fit(batch, self._ctx())
-        if self._theta is None:  # E == 0: nothing to monitor against → sync, new round
+        if self._lag.take():
             self._full_sync()
             self._begin_round()
-            self.stats.rounds += 1
-            return
-        x = L.state_vector()
-        scale = self.G if L.merge_mode == "sum" else 1.0
-        # [‖X_i‖², ‖E‖²] in one device pass, then host arithmetic on two scalars (one
-        # read-back instead of a string of tiny launches per round)
-        x2, e2 = M.drift_norms(x, self._E, scale).tolist()
-        phi = x2 - self.eps * e2
-        c = max(0.0, math.floor((phi - self._phi0) / self._theta))
-        inc = c - self._c_prev
-        self._c_prev = c
-        if self.G > 1:
-            msg = self._small([inc, phi])
-            self.comm.all_reduce_(msg, tag="fgm-counters")
-            tot_inc, psi = msg.tolist()
         else:
-            tot_inc, psi = inc, phi
-        self._account_small(self.G, 8)
-        self._csum += tot_inc
-        if self._csum > self.G:
-            self.subrounds += 1
-            if psi >= self.eps_psi * self.G * self._phi0:
-                self._full_sync()
-                self._begin_round()
-                self._csum = 0.0
-            else:
-                self._theta = -psi / (2 * self.G)
-                self._csum = 0.0
-                # counters restart relative to the new subround
-                self._c_prev = max(0.0, math.floor((phi - self._phi0) / self._theta))
+            x = L.state_vector()
+            scale = self.G if L.merge_mode == "sum" else 1.0
+            M.drift_norms(x, self._E, scale, out=self._nrm)
+            M.fgm_local(self._nrm, self._st, self.eps, self._msg)
+            self._reduce_msg("fgm-counters")
+            M.fgm_hub(self._st, self._msg, self.eps_psi, self.G, self._lag.dev)
+            self._lag.post()
         self.stats.rounds += 1
 
     def state_dict(self):
         """The round/subround state is the hub's (identical on every rank) plus this
         worker's counter; E is the estimate every local drift is measured against."""
         sd = super().state_dict()
-        sd["E"] = None if self._E is None else self._E.cpu()
-        sd["fgm"] = {"c_prev": float(self._c_prev), "csum": float(self._csum),
-                     "theta": self._theta, "phi0": self._phi0, "subrounds": self.subrounds,
+        sd["fgm"] = {"state": None if self._st is None else self._st.cpu(),
                      "fgm_rounds": self.fgm_rounds}
         return sd
 
     def load_state_dict(self, sd):
         super().load_state_dict(sd)
-        if sd.get("E") is not None:
-            self._E = sd["E"].to(self.learner.device)
         f = sd.get("fgm")
-        if f:
-            self._c_prev, self._csum = float(f["c_prev"]), float(f["csum"])
-            self._theta = None if f["theta"] is None else float(f["theta"])
-            self._phi0 = None if f["phi0"] is None else float(f["phi0"])
-            self.subrounds, self.fgm_rounds = int(f["subrounds"]), int(f["fgm_rounds"])
+        if f and f.get("state") is not None:
+            self._buffers(self.NMSG)
+            self._st = f["state"].to(self.learner.device)
+            self.fgm_rounds = int(f["fgm_rounds"])
 
 
 class SingleLearner(Protocol):

@@ -21,7 +21,7 @@ rule = L.LinearRule(rule=L.RULE_HINGE, variant=L.PA1, C=1.0)
 lib = native.hip().cdll
 lib.omldm_linear_seq_stamps.argtypes = [ctypes.c_void_p]
 out = {}
-for S, R in [(16, 8192), (64, 2048)]:
+for S, R in [(16, 8192), (64, 8192), (256, 2048), (256, 8192)]:
     B = S * R
     b = synth_raw(space, B, seed=25)
     b = type(b)(b.num.to(dev), b.tok.to(dev), b.y.to(torch.int8).to(dev))
