@@ -178,7 +178,8 @@ class Job:
                     try:
                         self.pipes[net] = Pipeline(req, self.space, self.comm, self.device,
                                                    self.spokes, self.cfg.parallelism,
-                                                   self.cfg.maxMsgParams, store=self.store)
+                                                   self.cfg.maxMsgParams, store=self.store,
+                                                   seed=self.cfg.seed)
                     except (ValueError, TypeError, KeyError) as e:
                         # an ill-typed configuration (every rank fails the same way): the
                         # request is dropped and counted, the job goes on
@@ -300,7 +301,7 @@ class Job:
         loss, score, n = pipe.evaluate(test) if test.B else (0.0, 0.0, 0)
         tot = pipe.learner.running_totals()
         m = ST.reduce_query_metrics(self.comm, float(loss), float(score), int(n), tot["fitted"],
-                                    tot["loss_sum"])
+                                    tot["loss_sum"], pipe.mean_buffer_size())
         if pipe.learner.TASK == "regression":
             m["score"] = float(np.sqrt(max(m["score"], 0.0)))  # mean squared error → RMSE
         if self.rank == 0 and write:
@@ -434,7 +435,8 @@ class Job:
             m = self._answer(Request(id=pid, request="Query", requestId=-1), write=False)
             stats.append(ST.pipeline_statistics(pipe, m))
         self.egress.flush()
-        js = ST.job_statistics(self.cfg.jobName, self.world, self.idle.duration_ms(), stats)
+        js = ST.job_statistics(self.cfg.jobName, self.spokes * self.world,
+                               self.idle.duration_ms(), stats)
         js.metrics = self._metrics(js.duration)
         self.final_stats = js
         if self.rank == 0:
@@ -448,7 +450,8 @@ class Job:
         pct = (lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))], 3)) if lat else \
             (lambda q: None)
         cs = self.comm.stats
-        return {"trainedExamples": self._trained_global,
+        return {"ranks": self.world, "spokesPerRank": self.spokes,
+                "trainedExamples": self._trained_global,
                 "examplesPerSec": round(self._trained_global / max(duration_ms, 1) * 1e3, 1),
                 "forecastBatchLatencyMs": {"p50": pct(0.5), "p99": pct(0.99)},
                 "collectives": cs.collectives, "collectiveBytes": cs.bytes,

@@ -24,7 +24,8 @@ from omldm_amd.parallel.protocols import make_protocol
 
 class Pipeline:
     def __init__(self, request: Request, space: FeatureSpace, comm: Comm, device,
-                 spokes: int, parallelism: int, max_msg_params: int = 10000, store=None):
+                 spokes: int, parallelism: int, max_msg_params: int = 10000, store=None,
+                 seed: int = 25):
         self.id = int(request.id)
         self.request = request
         self.space = space
@@ -39,6 +40,7 @@ class Pipeline:
             d = p.out_dim(d)
         hyper = dict(request.learner.hyperParameters or {})
         hyper["_inDim"] = d
+        hyper["_seed"] = int(seed)  # the job's seed (Random.setSeed, FlinkSpoke.scala:52)
         # A widened dense block (PolynomialFeatures) keeps slots [0, d) for the hashed
         # learners; its top overlaps the lowest hashed slots like any hash collision.
         if d + 1 >= space.dim:
@@ -82,6 +84,10 @@ class Pipeline:
         # running statistics (reference Statistics / learning curve, FlinkHub.scala:95-156)
         self.learning_curve: list[tuple[float, int]] = []
         self._lc_last = (0.0, 0)
+        # mean buffer size (reference BufferingWrapper.getMeanBufferSize): the training
+        # records a spoke holds when its round starts — rows of the round / local spokes
+        self.spokes = max(1, int(spokes))
+        self._buf_sum, self._buf_rounds = 0.0, 0
 
     # --------------------------------------------------------------- data path
     def _pre(self, batch: HashedBatch, train: bool) -> HashedBatch:
@@ -95,12 +101,21 @@ class Pipeline:
             batch = p(batch, train=train)
         return batch
 
+    def _note_buffer(self, rows: int) -> None:
+        self._buf_sum += rows / self.spokes
+        self._buf_rounds += 1
+
+    def mean_buffer_size(self) -> float:
+        return self._buf_sum / self._buf_rounds if self._buf_rounds else 0.0
+
     def train(self, batch: HashedBatch) -> None:
         """One protocol round on this rank's training rows (possibly empty)."""
+        self._note_buffer(batch.B)
         self.protocol.round(self._pre(batch, True))
 
     def train_local(self, batch: HashedBatch) -> torch.Tensor:
         """Phase 1 of a split Synchronous round: train, return the buffer to reduce."""
+        self._note_buffer(batch.B)
         return self.protocol.local(self._pre(batch, True))
 
     def predict(self, batch: HashedBatch) -> torch.Tensor:
@@ -143,7 +158,8 @@ class Pipeline:
         return {"request": self.request.to_obj(), "learner": self.learner.state_dict(),
                 "preprocessors": [p.state_dict() for p in self.preprocessors],
                 "protocol": self.protocol.state_dict(),
-                "learning_curve": list(self.learning_curve)}
+                "learning_curve": list(self.learning_curve),
+                "buffer": [self._buf_sum, self._buf_rounds]}
 
     def load_state_dict(self, sd: dict) -> None:
         self.learner.load_state_dict(sd["learner"])
@@ -151,3 +167,5 @@ class Pipeline:
             p.load_state_dict(s)
         self.protocol.load_state_dict(sd.get("protocol", {}))
         self.learning_curve = [tuple(x) for x in sd.get("learning_curve", [])]
+        if sd.get("buffer"):
+            self._buf_sum, self._buf_rounds = float(sd["buffer"][0]), int(sd["buffer"][1])

@@ -26,12 +26,16 @@ from omldm_amd.api.schemas import JobStatistics, QueryResponse, Statistics
 
 
 def reduce_query_metrics(comm, loss_sum: float, score_sum: float, n: int, fitted: int,
-                         cum_loss: float) -> dict:
+                         cum_loss: float, mean_buffer: float = 0.0) -> dict:
     """ResponseConstructor merge over ranks: Σ fitted; loss/cumLoss/score averaged over
-    workers of per-worker means (reference semantics)."""
+    workers of per-worker means (reference semantics). ``meanBufferSize``: every spoke
+    reports its mean buffer size / P and the statistics operator sums them
+    (FlinkSpoke.scala:138, StatisticsOperator.scala:101) — the mean over spokes; a rank's
+    spokes share one value, so it is the mean over ranks."""
     dev = "cpu"
     per = torch.tensor([loss_sum / max(n, 1), score_sum / max(n, 1), float(fitted),
-                        cum_loss / max(fitted, 1), float(n), 1.0 if n > 0 else 0.0],
+                        cum_loss / max(fitted, 1), float(n), 1.0 if n > 0 else 0.0,
+                        float(mean_buffer)],
                        dtype=torch.float64, device=dev)
     if comm.world > 1 and comm.backend == "nccl":
         per = per.to(torch.device("cuda", torch.cuda.current_device()))
@@ -40,7 +44,8 @@ def reduce_query_metrics(comm, loss_sum: float, score_sum: float, n: int, fitted
     workers = max(1.0, float(per[5]))
     return {"loss": float(per[0]) / workers, "score": float(per[1]) / workers,
             "dataFitted": int(per[2]), "cumulativeLoss": float(per[3]) / workers,
-            "testPoints": int(per[4]), "workers": int(workers)}
+            "testPoints": int(per[4]), "workers": int(workers),
+            "meanBufferSize": float(per[6]) / max(1, comm.world)}
 
 
 def split_params(params: dict | None, bucket: int = 10000) -> list[dict]:
@@ -171,20 +176,36 @@ class IdleDetector:
         return int(((self.end or self.start) - self.start) * 1000)
 
 
+def merge_hub_statistics(hub_stats: list[dict], fitted: int) -> dict:
+    """StatisticsAggregateFunction.getResult (StateAccumulators.scala:94-108): the records
+    of a pipeline's H hubs are summed (updateStats), then blocks, models and fitted are
+    divided by H — bytes stay summed."""
+    H = max(1, len(hub_stats))
+    tot = {k: sum(int(h[k]) for h in hub_stats) for k in
+           ("modelsShipped", "bytesShipped", "numOfBlocks")}
+    return {"modelsShipped": tot["modelsShipped"] // H, "bytesShipped": tot["bytesShipped"],
+            # every hub counts the pipeline's global fitted examples: H·fitted / H
+            "numOfBlocks": tot["numOfBlocks"] // H, "fitted": fitted, "hubs": H}
+
+
 def pipeline_statistics(pipe, metrics: dict | None = None) -> Statistics:
     ps = pipe.protocol.stats
     lc = pipe.learning_curve
+    fitted = int(metrics["dataFitted"]) if metrics else pipe.learner.running_totals()["fitted"]
+    merged = merge_hub_statistics(pipe.protocol.hub_statistics(), fitted)
     st = Statistics(pipeline=pipe.id, protocol=pipe.protocol_name,
-                    modelsShipped=ps.models_shipped, bytesShipped=ps.bytes_shipped,
-                    numOfBlocks=ps.num_of_blocks,
-                    fitted=int(metrics["dataFitted"]) if metrics else
-                    pipe.learner.running_totals()["fitted"],
+                    modelsShipped=merged["modelsShipped"], bytesShipped=merged["bytesShipped"],
+                    numOfBlocks=merged["numOfBlocks"], fitted=merged["fitted"],
                     learningCurve=[x[0] for x in lc] or None, lcx=[x[1] for x in lc] or None,
+                    meanBufferSize=float(metrics.get("meanBufferSize", 0.0)) if metrics else
+                    pipe.mean_buffer_size(),
                     score=metrics["score"] if metrics else None,
-                    extra={"syncs": ps.syncs, "rounds": ps.rounds,
+                    extra={"syncs": ps.syncs, "rounds": ps.rounds, "hubs": merged["hubs"],
                            "smallMessages": ps.small_messages})
     return st
 
 
 def job_statistics(job_name: str, parallelism: int, duration_ms: int, stats: list) -> JobStatistics:
+    """``parallelism`` is the job's spoke parallelism (StatisticsOperator.scala:109-113:
+    the operator's parallelism = the spoke count P), i.e. spokes per rank × ranks."""
     return JobStatistics(job_name, parallelism, duration_ms, sorted(stats, key=lambda s: s.pipeline))

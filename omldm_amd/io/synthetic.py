@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import json
 import os
+import zlib
 
 import numpy as np
 import torch
@@ -53,7 +54,9 @@ def synth_raw(space: FeatureSpace, B: int, start: int = 0, seed: int = 25, task:
 
 def synth_json_records(n: int, space: FeatureSpace, start: int = 0, seed: int = 25,
                        operation: str = "training", task: int = 0) -> list[str]:
-    """DataInstance JSON lines (numerical/discrete/categorical features + target)."""
+    """DataInstance JSON lines (numerical/discrete/categorical features + target); record i
+    is a pure function of (seed, start, i) in every process (a stable CRC of each category
+    string, not Python's per-process salted ``hash``)."""
     rng = np.random.default_rng(seed * 1_000_003 + start)
     wn = np.random.default_rng(seed).normal(size=space.n_numerical + space.n_discrete)
     out = []
@@ -63,7 +66,7 @@ def synth_json_records(n: int, space: FeatureSpace, start: int = 0, seed: int = 
         cats = [f"c{j}_{int(rng.integers(0, 10 ** (1 + j % 4)) ** 1)}"
                 for j in range(space.n_categorical)]
         s = float(np.dot(wn, np.concatenate([xn, xd]))) + sum(
-            (hash(c) % 7 - 3) * 0.1 for c in cats)
+            (zlib.crc32(c.encode()) % 7 - 3) * 0.1 for c in cats)
         rec = {"numericalFeatures": xn.tolist(), "discreteFeatures": xd.tolist(),
                "categoricalFeatures": cats, "operation": operation}
         if operation == "training":

@@ -85,7 +85,8 @@ class Learner:
 
     # ---------------------------------------------------------------- API maps
     def hyper_parameters(self) -> dict:
-        return dict(self.hyper)
+        """The user-visible hyper-parameters (engine-internal ``_``-keys left out)."""
+        return {k: v for k, v in self.hyper.items() if not str(k).startswith("_")}
 
     # hyper-parameters that fix the model's shape: an Update may not change them on a
     # live pipeline (it is dropped and counted, like any invalid request)

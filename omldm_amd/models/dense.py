@@ -128,7 +128,7 @@ class ORR(Learner):
         self._w = None
 
     def hyper_parameters(self):
-        return {**self.hyper, "lambda": self.lam}
+        return {**super().hyper_parameters(), "lambda": self.lam}
 
 
 # ------------------------------------------------------------------------- K-means
@@ -356,7 +356,7 @@ class NN(Learner):
         # instead of K/2; default fp32 keeps DL4J's fp32 arithmetic
         if str(h.get("matmulDtype", "fp32")).lower() in ("bf16", "bfloat16"):
             self.act |= D.MLP_BF16
-        self.seed = hp_int(h, "seed", 25)
+        self.seed = hp_int(h, "seed", hp_int(h, "_seed", 25))
         self.widths = [self.d] + [int(v) for v in hidden] + [max(1, self.K)]
         if len(self.widths) - 1 > D.MLP_MAX_LAYERS:
             raise ValueError(f"NN supports at most {D.MLP_MAX_LAYERS} layers")
@@ -425,7 +425,7 @@ class NN(Learner):
         return loss, score, int(ok.sum())
 
     def hyper_parameters(self):
-        return {**self.hyper, "learningRate": self.lr, "miniBatchSize": self.MB,
+        return {**super().hyper_parameters(), "learningRate": self.lr, "miniBatchSize": self.MB,
                 "activation": self.act_name}
 
     def parameters_map(self):

@@ -214,7 +214,7 @@ class LinearLearner(Learner):
         r = self.rule
         names = {L.PA: "PA", L.PA1: "PA-I", L.PA2: "PA-II"}
         variant = "Pegasos" if r.rule == L.RULE_PEGASOS else names[r.variant]
-        return {**self.hyper, "C": r.C, "variant": variant, "epsilon": r.eps,
+        return {**super().hyper_parameters(), "C": r.C, "variant": variant, "epsilon": r.eps,
                 "learningRate": r.lr, "lambda": r.lam, "bias": r.bias}
 
     def parameters_map(self) -> dict:

@@ -35,8 +35,13 @@ class CommStats:
     bytes: int = 0
     small_collectives: int = 0
     per_tag: dict = field(default_factory=dict)
+    # when a list: every call is appended as (kind, tag, bytes) — the exact per-round
+    # communication schedule (tests pin it per protocol)
+    trace: list | None = None
 
-    def add(self, tag: str, nbytes: int, small: bool = False):
+    def add(self, tag: str, nbytes: int, small: bool = False, kind: str = "all_reduce"):
+        if self.trace is not None:
+            self.trace.append((kind, tag, int(nbytes)))
         self.collectives += 1
         self.bytes += nbytes
         if small:
@@ -76,14 +81,14 @@ class Comm:
         """SUM (or ``op``) of a small HOST tensor over the control group (gloo): no device
         synchronisation."""
         assert not t.is_cuda
-        self.stats.add(tag, t.numel() * t.element_size(), True)
+        self.stats.add(tag, t.numel() * t.element_size(), True, kind="host_all_reduce")
         if self.world == 1:
             return
         dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.ctrl_group)
 
     def reduce_bcast_(self, t: torch.Tensor, root: int = 0, tag: str = "sync"):
         """Single-hub semantics (HubParallelism == 1): reduce to root, root broadcasts."""
-        self.stats.add(tag, 2 * t.numel() * t.element_size())
+        self.stats.add(tag, 2 * t.numel() * t.element_size(), kind="reduce+bcast")
         if self.world == 1:
             return
         dist.reduce(t, dst=root, op=dist.ReduceOp.SUM, group=self.group)
@@ -119,7 +124,7 @@ class Comm:
         step = -(-n // hubs)
         sl = [flat[h * step:min(n, (h + 1) * step)] for h in range(hubs)]
         me, G = self.rank, self.world
-        self.stats.add(tag, 2 * n * t.element_size())
+        self.stats.add(tag, 2 * n * t.element_size(), kind="p2p_shards")
         bufs = {}
         ops = []
         for h in range(hubs):
@@ -212,8 +217,9 @@ class Comm:
                     t.copy_(flat[o:o + n])
                     o += n
 
-    def broadcast_(self, t: torch.Tensor, src: int = 0):
+    def broadcast_(self, t: torch.Tensor, src: int = 0, tag: str = "bcast"):
         if self.world > 1:
+            self.stats.add(tag, t.numel() * t.element_size(), kind="broadcast")
             dist.broadcast(t, src=src, group=self.group)
 
     def broadcast_object(self, obj, src: int = 0):
@@ -250,7 +256,7 @@ class Comm:
         row_shape = tuple(src.shape[1:])
         if self.rank != dst:
             if t.shape[0]:
-                self.stats.add("gather", src.numel() * src.element_size())
+                self.stats.add("gather", src.numel() * src.element_size(), kind="p2p_send")
                 dist.send(src, dst=dst, group=self.group)
             return None
         ns = [int(x[0]) for x in ns_t]

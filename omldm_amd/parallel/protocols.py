@@ -55,6 +55,9 @@ class ProtocolStatistics:
     syncs: int = 0
     rounds: int = 0
     small_messages: int = 0
+    # per hub shard [models, bytes, blocks] — what each of the H hubs of the reference
+    # counts for its own shard (FlinkHub.scala:118-127), merged by the reference rule
+    hubs: list | None = None
 
     def as_dict(self) -> dict:
         return {"protocol": self.protocol, "modelsShipped": self.models_shipped,
@@ -94,13 +97,36 @@ class Protocol:
     def _ctx(self, fused: bool = False) -> RoundContext:
         return RoundContext(spokes=self.spokes, inv_p=1.0, fused_delta=fused)
 
+    def n_hubs(self) -> int:
+        """Parameter-server shards of this pipeline: HubParallelism, every rank when 0."""
+        return max(1, min(self.G, self.hubs if self.hubs > 0 else self.G))
+
     def _account_model_sync(self, nparams: int, nbytes: int) -> None:
-        """Every worker pushes one model to the hub and pulls one back."""
-        g = self.G
+        """Every worker pushes one model to the hub(s) and pulls one back: hub h of H sees
+        2G messages of its shard, in ⌈shard/maxMsgParams⌉ blocks each."""
+        g, H = self.G, self.n_hubs()
         self.stats.syncs += 1
         self.stats.models_shipped += 2 * g
         self.stats.bytes_shipped += 2 * g * nbytes
         self.stats.num_of_blocks += 2 * g * max(1, math.ceil(nparams / self.max_msg_params))
+        if self.stats.hubs is None or len(self.stats.hubs) != H:
+            self.stats.hubs = [[0, 0, 0] for _ in range(H)]
+        step = -(-max(1, nparams) // H)
+        for h in range(H):
+            shard = max(0, min(nparams, (h + 1) * step) - h * step)
+            hs = self.stats.hubs[h]
+            hs[0] += 2 * g
+            hs[1] += 2 * g * (nbytes * shard // max(1, nparams))
+            hs[2] += 2 * g * max(1, math.ceil(shard / self.max_msg_params))
+
+    def hub_statistics(self) -> list[dict]:
+        """One statistics record per hub shard (models, bytes, blocks)."""
+        if not self.stats.hubs:
+            return [{"modelsShipped": self.stats.models_shipped,
+                     "bytesShipped": self.stats.bytes_shipped,
+                     "numOfBlocks": self.stats.num_of_blocks}]
+        return [{"modelsShipped": m, "bytesShipped": b, "numOfBlocks": k}
+                for m, b, k in self.stats.hubs]
 
     def _small(self, vals: list) -> torch.Tensor:
         """A few fp32 scalars for a small collective, on the device the backend reduces

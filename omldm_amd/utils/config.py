@@ -3,8 +3,13 @@ MI355X-native engine's own flags.
 
 Reference flags: omldm/Job.scala:110-168 (ParameterTool.fromArgs), defaults in
 omldm/utils/DefaultJobParameters.scala:4-11, omldm/utils/Checkpointing.scala:11-23,
-omldm/job/FlinkLearning.scala:43-48. ``psMessages*`` flags are
-accepted and ignored: the parameter-server feedback loop is RCCL, not a Kafka topic.
+omldm/job/FlinkLearning.scala:43-48. Accepted and ignored, with
+the reason: ``psMessages*`` (the parameter-server feedback loop is RCCL / point-to-point,
+not a Kafka topic) and ``local`` (the reference picks a local mini-cluster or a remote
+Flink environment; here every launch is one process per GPU through omldm_amd.launch).
+The reference's hub cache (StateAccumulators.scala:38) and 100-record heartbeat
+(FlinkSpoke.scala:85) have no knob: hubs are collectives with no message cache, and
+every tick's control all-reduce is the heartbeat.
 """
 from __future__ import annotations
 
@@ -48,11 +53,9 @@ class JobConfig:
     # ---- reference constants made configurable
     recordBufferSize: int = 100000        # SpokeLogic.scala:32
     requestBufferSize: int = 10000        # SpokeLogic.scala:35
-    hubCacheSize: int = 20000             # StateAccumulators.scala:38
     queryBucketSize: int = 10000          # FlinkNetwork.scala:50
     bucketBytes: int = 64 << 20           # cap of one coalesced collective bucket
-    heartbeatEvery: int = 100             # FlinkSpoke.scala:85
-    seed: int = 25                        # FlinkSpoke.scala:52
+    seed: int = 25                        # FlinkSpoke.scala:52: default seed of seeded learners
     # ---- MI355X-native engine
     numFeatures: int = 13                 # numerical features per point (dense slots)
     discreteFeatures: int = 0             # discrete features per point (dense slots)

@@ -92,7 +92,9 @@ def test_kill_rank_restart_on_fewer_ranks(tmp_path):
     assert any("on 1 rank(s)" in m for m in logs), logs
     perf = Consumer(br, "performance", all_partitions=True).poll(10)
     js = json.loads(perf[-1])
-    assert js["jobName"] == "fault-test" and js["parallelism"] == 1
+    # JobStatistics.parallelism is the spoke parallelism (16 spokes on the one rank left)
+    assert js["jobName"] == "fault-test" and js["parallelism"] == 16
+    assert js["metrics"]["ranks"] == 1
     st = js["statistics"][0]
     # every partition fully consumed; the restored rank trained on the rest of the stream
     man = sorted((tmp_path / "ckpt").glob("ckpt-*/manifest.json"))[-1]
