@@ -35,6 +35,7 @@
 // refreshes every replica.
 #include "common.h"
 #include "hash_dev.h"
+#include "seq_common.h"
 
 namespace omldm {
 
@@ -52,17 +53,6 @@ constexpr int TB1 = 512;   // per-wave grouping table, first hash
 constexpr int TB2 = 256;   // second hash (keys that lost the first)
 constexpr int WS = 8;      // per-spoke stat row: loss, n, mistakes, sq_err, 1, stuck, 0, 0
 }  // namespace seq
-
-enum SeqRule : int { kSeqHinge = 0, kSeqEps = 1, kSeqLogistic = 2 };
-
-struct SeqParams {
-  int rule, variant;
-  float cclip;  // τ clip: C for PA-I, +inf otherwise
-  float kadd;   // τ denominator offset: 1/(2C) for PA-II
-  float eps, lr, inv_p;
-  int bias, y8;
-  uint32_t span;  // slots per categorical field: (dim − dn − 1) / dc (field-aware hashing)
-};
 
 // v_writelane_b32 (no clang builtin in this toolchain: the LLVM intrinsic by name)
 extern "C" __device__ int omldm_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
@@ -109,45 +99,6 @@ __device__ __forceinline__ bool producer_barrier(int* ctr, int& target) {
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   return true;
-}
-
-// c(m) of one example for the lane's own row (the value is used only at its step).
-template <int RULE>
-__device__ __forceinline__ float seq_candidate(float m, float y, float inv, const SeqParams& p) {
-  if constexpr (RULE == kSeqHinge) {
-    const float l = fmaxf(0.f, fmaf(-y, m, 1.f));
-    return fminf(p.cclip, l * inv) * y;
-  } else if constexpr (RULE == kSeqEps) {
-    const float err = y - m;
-    const float l = fmaxf(0.f, fabsf(err) - p.eps);
-    const float tau = fminf(p.cclip, l * inv);
-    return err >= 0.f ? tau : -tau;
-  } else {
-    const float z = y * m;
-    return p.lr * y * __builtin_amdgcn_rcpf(1.f + __expf(z));
-  }
-}
-
-template <int RULE>
-__device__ __forceinline__ void seq_stats(float m, float y, const SeqParams& p, float& loss,
-                                          float& mist, float& sqe) {
-  if constexpr (RULE == kSeqHinge) {
-    const float ym = y * m;
-    loss += fmaxf(0.f, 1.f - ym);
-    mist += ym <= 0.f ? 1.f : 0.f;
-  } else if constexpr (RULE == kSeqEps) {
-    const float err = y - m;
-    loss += fmaxf(0.f, fabsf(err) - p.eps);
-    sqe = fmaf(err, err, sqe);
-  } else {
-    const float z = y * m;
-    loss += fmaxf(-z, 0.f) + __logf(1.f + __expf(-fabsf(z)));
-    mist += z <= 0.f ? 1.f : 0.f;
-  }
-}
-
-__device__ __forceinline__ float load_y(const void* yv, int t, int y8) {
-  return y8 ? (float)static_cast<const int8_t*>(yv)[t] : static_cast<const float*>(yv)[t];
 }
 
 // Producer state carried between chunks: the raw inputs of the next chunk, in registers.
@@ -759,6 +710,16 @@ OMLDM_API int omldm_linear_seq_round(const float* w, const float* num, int dn, c
   const int S_act = sact < S ? (int)sact : S;
   hipLaunchKernelGGL(linear_seq_reduce_kernel, dim3(grid_for(dim)), dim3(256), 0, st, rep, w,
                      S_act, dim, dacc, inv_p, ws, cum);
+  return (int)hipGetLastError();
+}
+
+// Round end shared with linear_scan.hip: replicas of the S_act active spokes averaged into
+// the round accumulator, spoke statistics into the running totals.
+OMLDM_API int omldm_linear_seq_reduce(const float* rep, const float* w, int S_act, int dim,
+                                      float* dacc, float inv_p, const float* ws, double* cum,
+                                      void* stream) {
+  hipLaunchKernelGGL(linear_seq_reduce_kernel, dim3(grid_for(dim)), dim3(256), 0,
+                     (hipStream_t)stream, rep, w, S_act, dim, dacc, inv_p, ws, cum);
   return (int)hipGetLastError();
 }
 

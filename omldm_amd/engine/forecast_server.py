@@ -1,0 +1,196 @@
+"""Per-record forecasting: every forecasting record is answered as it arrives.
+
+Reference: a forecasting point reaching a spoke is predicted at once by every pipeline
+(``FlinkSpoke.processElement1`` → ``node.receiveTuple`` → ``predict``,
+omldm/operators/spoke/FlinkSpoke.scala:101-105) and the Prediction is emitted right away
+(omldm/network/FlinkNetwork.scala:243-257) — no batching, so the record-in →
+Prediction-out latency is one predict.
+
+Here the engine's tick batches training rows (throughput); forecasting records take a
+separate low-latency lane: a host thread consumes the forecasting topic, parses each
+record natively (csrc/host/ingest.cpp, the same hashing as the GPU parser), hands it to
+the PERSISTENT serving wavefront (csrc/kernels/serving.hip: one resident wave polling a
+coherent pinned mailbox; no kernel launch, no stream synchronisation per request) that
+scores it against every hashed-linear pipeline of the HBM model store in one pass, and
+produces one Prediction per pipeline. The wave reads the live weights the training
+rounds update (at most one round stale, like a reference spoke between two syncs).
+
+Pipelines the wave cannot score (a preprocessor in front, dense learners) keep the
+batched path: while any exists, records are handed to the tick (``take_fallback``).
+"""
+from __future__ import annotations
+
+import collections
+import threading
+import time
+
+import numpy as np
+import torch
+
+from omldm_amd.io.egress import RawRecords, format_predictions
+from omldm_amd.ops import native
+
+OP_FORECASTING = 1
+
+
+class ForecastServer:
+    IDLE_SLEEP_S = 20e-6
+
+    def __init__(self, job, lifetime_us: int = 3_600_000_000):
+        self.job = job
+        self.space = job.space
+        self.consumer = job.fcst_in
+        self.topic = job.cfg.predictionsTopic
+        self.broker = job.brokers["predictions"]
+        self.lifetime_us = int(lifetime_us)
+        self.lock = threading.Lock()
+        self._server = None
+        self._served: list = []       # (pipeline id, store row, classification?) in W order
+        self._row0 = 0
+        self.fallback: collections.deque = collections.deque()
+        self.latency_us: collections.deque = collections.deque(maxlen=1 << 16)
+        self.served = 0
+        self.invalid = 0
+        dn, dc = self.space.dn, self.space.dc
+        # one record's parse buffers (omldm_serve_request copies them into the mailbox)
+        self._num = torch.zeros((1, dn), dtype=torch.float32)
+        self._cat = torch.full((1, dc), -1, dtype=self.space.cat_dtype)
+        self._y = torch.zeros(1, dtype=torch.float32)
+        self._op = np.zeros(1, dtype=np.int8)
+        self._offs = np.zeros(2, dtype=np.int64)
+        self._busy = False             # a polled batch is being answered
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="omldm-forecast", daemon=True)
+
+    # ----------------------------------------------------------------- control
+    def start(self) -> None:
+        self._thread.start()
+
+    def close(self) -> None:
+        self._stop.set()
+        self._thread.join(5.0)
+        with self.lock:
+            self._stop_wave()
+
+    def _stop_wave(self) -> None:
+        if self._server is not None:
+            self._server.close()
+            self._server = None
+
+    def suspend(self) -> None:
+        """Before the model store may move (a Create can grow its arena): the wave stops
+        reading it until ``reconfigure``."""
+        with self.lock:
+            self._stop_wave()
+            self._served = []
+
+    def reconfigure(self) -> None:
+        """After a Create / Delete / restore (main thread): serve the model-store
+        pipelines with the wave when every pipeline lives in the store, else hand all
+        records to the batched path."""
+        with self.lock:
+            self._build_wave()
+
+    def _build_wave(self) -> None:
+        from omldm_amd.ops.serving import PredictServer
+
+        self._stop_wave()
+        self._served = []
+        pipes = [self.job.pipes[pid] for pid in sorted(self.job.pipes)]
+        if not pipes or any(p.store is None for p in pipes):
+            return
+        biases = {bool(p.learner.rule.bias) for p in pipes}
+        if len(biases) != 1:
+            return
+        rows = [p.store_row for p in pipes]
+        lo, hi = min(rows), max(rows) + 1
+        W = self.job.store.W[lo:hi]
+        torch.cuda.synchronize(W.device)
+        srv = PredictServer(W, self.space.dn, self.space.dc, biases.pop(),
+                            cat_span=self.space.cat_span)
+        srv.start(lifetime_us=self.lifetime_us)
+        self._server = srv
+        self._row0 = lo
+        self._served = [(p.id, p.store_row, p.learner.TASK == "classification") for p in pipes]
+
+    def take_fallback(self) -> list:
+        out = []
+        while self.fallback:
+            out.append(self.fallback.popleft())
+        return out
+
+    def latency_percentiles(self) -> dict:
+        lat = sorted(self.latency_us)
+        if not lat:
+            return {"p50": None, "p99": None, "n": 0}
+        return {"p50": round(lat[len(lat) // 2], 2),
+                "p99": round(lat[min(len(lat) - 1, int(0.99 * len(lat)))], 2), "n": len(lat)}
+
+    # --------------------------------------------------------------- data path
+    def _parse(self, rec: bytes) -> bool:
+        sp = self.space
+        self._offs[1] = len(rec)
+        self._cat.fill_(-1)
+        self._num.zero_()
+        native.host().omldm_parse_instances(
+            rec, self._offs.ctypes.data, 1, sp.n_numerical, sp.n_discrete, sp.dc, sp.dim,
+            sp.cat_span, self._num.data_ptr(), self._cat.data_ptr(), self._y.data_ptr(),
+            self._op.ctypes.data, 1)
+        return int(self._op[0]) == OP_FORECASTING
+
+    def serve_one(self, rec: bytes, t_in: float | None = None) -> bool:
+        """Answers one forecasting record with the wave. False: not served here (no
+        wave, or a pipeline it cannot score) — the caller keeps it for the tick."""
+        t_in = time.perf_counter() if t_in is None else t_in
+        with self.lock:
+            srv = self._server
+            if srv is None:
+                return False
+            if not self._parse(rec):
+                self.invalid += 1
+                return True
+            try:
+                out = srv.request_raw(self._num.data_ptr(), self._cat.data_ptr())
+            except TimeoutError:  # the wave's lifetime ended: a fresh one, same models
+                self._build_wave()
+                out = self._server.request_raw(self._num.data_ptr(), self._cat.data_ptr())
+            raw = RawRecords(np.frombuffer(rec, dtype=np.uint8),
+                             np.zeros(1, dtype=np.int64), np.array([len(rec)], dtype=np.int64))
+            for pid, row, cls in self._served:
+                s = float(out[row - self._row0])
+                p = (1.0 if s >= 0 else -1.0) if cls else s
+                block, offs = format_predictions(raw, pid, [p])
+                self.broker.produce(self.topic, block[:int(offs[1]) - 1])
+            self.served += 1
+        self.latency_us.append((time.perf_counter() - t_in) * 1e6)
+        return True
+
+    def catch_up(self, timeout_s: float = 5.0) -> bool:
+        """Waits until every forecasting record in the topic when called is answered (or
+        handed to the tick). The engine calls it at the end of a tick, so a tick's outputs
+        are complete when it returns; records keep being answered one by one as they
+        arrive in between."""
+        if not self._thread.is_alive():
+            return True
+        target = {p: self.consumer.broker.end_offset(self.consumer.topic, p)
+                  for p in self.consumer.parts}
+        t0 = time.time()
+        while time.time() - t0 < timeout_s:
+            if not self._busy and all(self.consumer.offsets[p] >= o for p, o in target.items()):
+                return True
+            time.sleep(self.IDLE_SLEEP_S)
+        return False
+
+    def _run(self) -> None:
+        while not self._stop.is_set():
+            self._busy = True
+            recs = self.consumer.poll(64)
+            if not recs:
+                self._busy = False
+                time.sleep(self.IDLE_SLEEP_S)
+                continue
+            t_in = time.perf_counter()
+            for i, rec in enumerate(recs):
+                if not self.serve_one(rec, t_in if i == 0 else None):
+                    self.fallback.append(rec)
+            self._busy = False

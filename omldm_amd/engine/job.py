@@ -92,7 +92,16 @@ class Job:
             from omldm_amd.ops.ingest import XcdLanes
 
             self.lanes = XcdLanes.get(self.device, cfg.ingestCUs)
-        self.ingest = TickIngest([self.train_in, self.fcst_in], cfg.batchSize,
+        # forecasting records: a per-record low-latency lane on the resident serving wave
+        # (engine/forecast_server.py) on GPU ranks; otherwise batched with the training rows
+        fs = str(cfg.forecastServer).lower()
+        self.fserver = None
+        if fs in ("true", "1") or (fs == "auto" and self.device.type == "cuda"):
+            from omldm_amd.engine.forecast_server import ForecastServer
+
+            self.fserver = ForecastServer(self)
+        self.ingest = TickIngest([self.train_in] if self.fserver else
+                                 [self.train_in, self.fcst_in], cfg.batchSize,
                                  pinned=self.device.type == "cuda",
                                  prefetch=str(cfg.prefetch).lower() in ("true", "1") or (
                                      str(cfg.prefetch).lower() == "auto" and
@@ -146,6 +155,9 @@ class Job:
             self.checkpointer = Checkpointer(cfg, self.rank, self.world)
             if cfg.restore:
                 self.checkpointer.restore(self)
+        if self.fserver is not None:
+            self.fserver.reconfigure()
+            self.fserver.start()
 
     def _coll_device(self):
         return self.device if self.comm.backend == "nccl" else torch.device("cpu")
@@ -169,6 +181,10 @@ class Job:
         else:
             msgs = []
         queries = []
+        moves = self.fserver is not None and any(
+            Request.from_json(robj).request in ("Create", "Delete") for _, _, robj in msgs)
+        if moves:
+            self.fserver.suspend()  # a Create may grow (move) the model store arena
         for net, dest, robj in msgs:
             req = Request.from_json(robj)
             if dest not in (ALL, self.rank) and req.request != "Query":
@@ -195,6 +211,8 @@ class Job:
                     old.close()
             elif req.request == "Query" and net in self.pipes:
                 queries.append(req)
+        if moves:
+            self.fserver.reconfigure()
         return len(msgs), queries
 
     def _bad_request(self, req, err) -> None:
@@ -233,7 +251,8 @@ class Job:
         """Offsets after the last block this job processed (the prefetcher may have read
         further; those records are re-read after a restore)."""
         if self._committed is not None:
-            return {"train": dict(self._committed[0]), "forecast": dict(self._committed[1])}
+            fc = self._committed[1] if len(self._committed) > 1 else self.fcst_in.offsets
+            return {"train": dict(self._committed[0]), "forecast": dict(fc)}
         return {"train": dict(self.train_in.offsets), "forecast": dict(self.fcst_in.offsets)}
 
     def _forecast(self, batch: HashedBatch, raw: RawRecords | None):
@@ -267,6 +286,21 @@ class Job:
                     for p in preds.tolist():
                         prod.produce(self.cfg.predictionsTopic, Prediction(pid, None, p).to_json())
                 self.counters["predictions"] += len(preds)
+
+    def _forecast_fallback(self) -> None:
+        """Forecasting records the serving wave handed back (a pipeline it cannot score):
+        predicted in one batch by every pipeline, like the batched path."""
+        recs = self.fserver.take_fallback()
+        if not recs or not self.pipes:
+            self.fserver.fallback.extendleft(reversed(recs))  # no pipeline yet: keep them
+            return
+        buf, offs = join_block(recs)
+        batch, op, _ = parse_block(buf, offs, self.space, self.cfg.parseThreads)
+        fidx = np.nonzero(op == OP_FORECASTING)[0]
+        self.counters["invalid"] += int(len(recs) - len(fidx))
+        if len(fidx):
+            raw = RawRecords.from_view(batch.raw, fidx)
+            self._forecast(batch.without_raw().select(torch.from_numpy(fidx)).to(self.device), raw)
 
     def _train(self, batch: HashedBatch, direct: HashedBatch | None = None):
         """One round of every pipeline. Synchronous pipelines train first and their
@@ -334,6 +368,8 @@ class Job:
             self.watchdog.beat()
         with tracing.range("control"):
             n_ctrl, queries = self._control()
+        if self.fserver is not None:
+            self._forecast_fallback()
         with tracing.range("poll"):
             block = self._poll()
         if isinstance(block, TickBlock):
@@ -420,6 +456,8 @@ class Job:
             self.idle.activity(time.time())  # idle = time since the last active tick ended
         if term > 0:
             self._terminate()
+        if self.fserver is not None and not self.fserver.catch_up():
+            print(f"[omldm] rank {self.rank}: forecast lane behind after 5 s", flush=True)
         if self.checkpointer is not None and ckpt > 0:
             self.egress.flush()  # outputs of the checkpointed ticks are in their topic
             self.checkpointer.save(self)
@@ -450,7 +488,9 @@ class Job:
         pct = (lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))], 3)) if lat else \
             (lambda q: None)
         cs = self.comm.stats
+        fsl = self.fserver.latency_percentiles() if self.fserver is not None else None
         return {"ranks": self.world, "spokesPerRank": self.spokes,
+                "forecastRecordLatencyUs": fsl,
                 "trainedExamples": self._trained_global,
                 "examplesPerSec": round(self._trained_global / max(duration_ms, 1) * 1e3, 1),
                 "forecastBatchLatencyMs": {"p50": pct(0.5), "p99": pct(0.99)},
@@ -463,6 +503,8 @@ class Job:
             self.tick()
         for p in self.pipes.values():
             p.protocol.finalize()
+        if self.fserver is not None:
+            self.fserver.close()
         self.ingest.close()
         self.egress.close()
         if self.checkpointer is not None:

@@ -208,6 +208,11 @@ def linear_predict(w: torch.Tensor, batch: HashedBatch, wscale: torch.Tensor | N
 SEQ_RULES = (RULE_HINGE, RULE_EPS, RULE_LOGISTIC)
 
 
+# GPU kernel of the exact sequential round: "scan" (linear_scan.hip, default) or "seq"
+# (linear_seq.hip: every spoke builds its own chunk Grams) — an A/B knob
+SEQ_KERNEL = os.environ.get("OMLDM_SEQ_KERNEL", "scan")
+
+
 def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
                      rule: LinearRule, inv_p: float, cum: torch.Tensor | None = None,
                      stats: torch.Tensor | None = None, replicas: torch.Tensor | None = None
@@ -236,12 +241,26 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
         ws = _workspace(w.device, S * WS_STAT, key="seq_ws")
         if replicas is None:
             replicas = _workspace(w.device, S * dim, key="seq_replicas")
-        rc = native.hip().omldm_linear_seq_round(
-            ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
-            int(y.dtype == torch.int8), batch.B, R, S, ptr(replicas), ptr(dacc), dim, ptr(ws),
-            ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, inv_p, int(rule.bias),
-            native.stream_of(w))
-        check(rc, "omldm_linear_seq_round")
+        if SEQ_KERNEL == "scan" and 0 < tok.shape[1] and tok.shape[1] + num.shape[1] <= 50:
+            # v2 (csrc/kernels/linear_scan.hip): hash + chunk Grams over the whole GPU, one
+            # scan workgroup per spoke
+            h = native.hip()
+            slots = _workspace(w.device, batch.B * tok.shape[1], key="scan_slots")
+            prep = _workspace(w.device, int(h.omldm_linear_scan_prep_floats(R, S)),
+                              key="scan_prep")
+            rc = h.omldm_linear_scan_round(
+                ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
+                int(y.dtype == torch.int8), batch.B, R, S, ptr(replicas), ptr(dacc), dim,
+                ptr(ws), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, inv_p,
+                int(rule.bias), ptr(slots), ptr(prep), native.stream_of(w))
+            check(rc, "omldm_linear_scan_round")
+        else:
+            rc = native.hip().omldm_linear_seq_round(
+                ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
+                int(y.dtype == torch.int8), batch.B, R, S, ptr(replicas), ptr(dacc), dim,
+                ptr(ws), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, inv_p,
+                int(rule.bias), native.stream_of(w))
+            check(rc, "omldm_linear_seq_round")
         if stats is not None:
             stats.copy_(ws[: S * WS_STAT].view(S, WS_STAT)[:, :STAT_W])
     else:

@@ -74,6 +74,7 @@ class JobConfig:
     prefetch: str = "auto"                # read tick k+1 while tick k trains (auto: on GPU)
     ingestCUs: int = 0                    # GPU: CUs (one XCD block) for ingest copies; 0 off (e2e A/B: no gain, host-bound)
     ingestCopy: str = "pull"              # GPU staging copy: pull (kernel) | sdma (hipMemcpyAsync)
+    forecastServer: str = "auto"          # per-record forecasts on the resident serving wave (auto: GPU)
     extra: dict = field(default_factory=dict)
 
     @staticmethod

@@ -154,6 +154,12 @@ def test_gpu_hash_raw_matches_cpu():
     assert torch.equal(hash_raw(b.tok.to(_cuda()), space).cpu(), hash_raw(b.tok, space))
 
 
+@pytest.fixture
+def kernel(request, monkeypatch):
+    monkeypatch.setattr(L, "SEQ_KERNEL", request.param)
+    return request.param
+
+
 def _seq_case(space, B, S, R, rule, variant=L.PA1, task=0, missing=0.0, y8=False, bias=True,
               seed=11, scale=0.01):
     batch = synth_raw(space, B, seed=seed, task=task, missing=missing)
@@ -176,10 +182,11 @@ def _seq_case(space, B, S, R, rule, variant=L.PA1, task=0, missing=0.0, y8=False
 
 
 @gpu
+@pytest.mark.parametrize("kernel", ["scan", "seq"], indirect=True)
 @pytest.mark.parametrize("rule,variant,task", [(L.RULE_HINGE, L.PA1, 0), (L.RULE_HINGE, L.PA, 0),
                                                (L.RULE_HINGE, L.PA2, 0), (L.RULE_EPS, L.PA1, 1),
                                                (L.RULE_LOGISTIC, L.PA1, 0)])
-def test_gpu_seq_round_matches_cpu(rule, variant, task):
+def test_gpu_seq_round_matches_cpu(kernel, rule, variant, task):
     space = FeatureSpace(13, 0, 26, 1 << 16)
     # 5 spokes × 300 rows (chunks of 64: 4 full + a 44-row tail) + a 100-row last spoke
     wc, wg, rep, cum, batch = _seq_case(space, 1300, 5, 300, rule, variant, task, missing=0.05)
@@ -189,7 +196,8 @@ def test_gpu_seq_round_matches_cpu(rule, variant, task):
 
 
 @gpu
-def test_gpu_seq_round_int8_labels_no_bias_wide_dense():
+@pytest.mark.parametrize("kernel", ["scan", "seq"], indirect=True)
+def test_gpu_seq_round_int8_labels_no_bias_wide_dense(kernel):
     # dn + bias > 16: the 32-column dense MFMA path; int8 labels; no intercept
     space = FeatureSpace(20, 0, 8, 1 << 12)
     wc, wg, _, cum, _ = _seq_case(space, 700, 3, 256, L.RULE_HINGE, y8=True, bias=False)
@@ -197,7 +205,8 @@ def test_gpu_seq_round_int8_labels_no_bias_wide_dense():
 
 
 @gpu
-def test_gpu_seq_round_many_shared_groups_slow_path():
+@pytest.mark.parametrize("kernel", ["scan", "seq"], indirect=True)
+def test_gpu_seq_round_many_shared_groups_slow_path(kernel):
     """A tiny hash space makes nearly every (field, value) shared inside a chunk and many
     values collide with opposite signs: more shared groups than U columns exercises
     the exact overflow path; collisions exercise the ±1 one-hot."""
@@ -207,7 +216,8 @@ def test_gpu_seq_round_many_shared_groups_slow_path():
 
 
 @gpu
-def test_gpu_learner_raw_rounds_track_cpu():
+@pytest.mark.parametrize("kernel", ["scan", "seq"], indirect=True)
+def test_gpu_learner_raw_rounds_track_cpu(kernel):
     """Several Synchronous rounds through SVM.fit(RawBatch): GPU and CPU models agree."""
     from omldm_amd.models.linear import SVM
     from omldm_amd.parallel.comm import Comm
