@@ -79,6 +79,65 @@ def shard_start(k: int, rank: int, world: int, B: int) -> int:
     return (k * world + rank) * B
 
 
+def engine_forecast_latency(n: int) -> dict:
+    """Record produced into the forecasting topic → its Prediction in the predictions
+    topic, through the engine (Job + per-record forecast lane on the resident serving
+    wave, engine/forecast_server.py) with a trained linear SVM pipeline."""
+    import uuid
+
+    from omldm_amd.engine.job import Job
+    from omldm_amd.io.synthetic import synth_json_records
+    from omldm_amd.io.transport import MemoryBroker
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.utils.config import JobConfig
+
+    class Timed(MemoryBroker):
+        def __init__(self):
+            super().__init__()
+            self.t_out: list = []
+
+        def produce(self, topic, value, partition=None, key=None):
+            super().produce(topic, value, partition, key)
+            if topic == "predictions":
+                self.t_out.append(time.perf_counter())
+
+    name = "bench-" + uuid.uuid4().hex
+    br = Timed()
+    MemoryBroker._registry[name] = br
+    args = []
+    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+              "predictionsAddr", "performanceAddr"):
+        args += [f"--{k}", f"memory://{name}"]
+    args += ["--batchSize", "8192", "--parallelism", "16", "--test", "false"]
+    cfg = JobConfig.from_args(args)
+    sp = FeatureSpace(cfg.numFeatures, 0, cfg.catFeatures, cfg.hashDim)
+    job = Job(cfg, Comm(), torch.device("cuda", torch.cuda.current_device()))
+    br.produce("requests", json.dumps({"id": 1, "request": "Create",
+                                       "learner": {"name": "SVM"},
+                                       "trainingConfiguration": {"protocol": "Synchronous"}}))
+    for r in synth_json_records(16384, sp):
+        br.produce("trainingData", r)
+    for _ in range(3):
+        job.tick()
+    recs = synth_json_records(n + 20, sp, start=10**9, operation="forecasting")
+    t_in = []
+    for r in recs:
+        k = len(br.t_out)
+        t_in.append(time.perf_counter())
+        br.produce("forecastingData", r)
+        t = time.perf_counter()
+        while len(br.t_out) == k and time.perf_counter() - t < 1.0:
+            time.sleep(0)
+        time.sleep(100e-6)  # records arrive one at a time
+    job.fserver.close()
+    lat = sorted((o - i) * 1e6 for i, o in zip(t_in[20:], br.t_out[20:]))
+    return {"p50": round(lat[len(lat) // 2], 2),
+            "p99": round(lat[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
+            "what": f"{len(lat)} JSON forecasting records, each produced into the topic → its "
+                    "Prediction produced (engine forecast lane: host poll + native parse + "
+                    "resident serving wave + native Prediction formatting), trained SVM"}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,11 +157,15 @@ def main(argv=None) -> int:
     ap.add_argument("--cu-layout", type=int, default=1)
     ap.add_argument("--pull-blocks", type=int, default=16)
     ap.add_argument("--lane", default="split", choices=["split", "plain"])
+    ap.add_argument("--prep-ahead", type=int, default=1,
+                    help="v2 round: hash + chunk Grams of batch k+1 on their own stream")
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
     ap.add_argument("--latency-samples", type=int, default=2000)
     ap.add_argument("--ref", default="auto", choices=["auto", "on", "off"],
                     help="CPU reference-semantics accuracy on the same stream (rank 0)")
     ap.add_argument("--ref-max-examples", type=float, default=6e7)
+    ap.add_argument("--engine-latency", type=int, default=300,
+                    help="forecasting records timed through the engine (rank 0; 0 = skip)")
     a = ap.parse_args(argv)
 
     comm, device = init_distributed()
@@ -149,6 +212,17 @@ def main(argv=None) -> int:
             raw_streams += [raw, rawc]
             lane = {"copy": torch.cuda.ExternalStream(raw, device=device),
                     "compute": torch.cuda.ExternalStream(rawc, device=device)}
+    # passes 1-2 of the next round (hash + chunk Grams, model-independent) run on their own
+    # stream as soon as its batch has landed, overlapping the current round's scan
+    prep_stream = None
+    if on_gpu and a.prep_ahead and L.scan_eligible(dev[0].batch):
+        if a.lane == "split" and a.ingest_cus > 0:
+            rawp = native.hip().omldm_stream_create_cumask_ex(a.ingest_cus, 1, a.cu_layout)
+            assert rawp, "hipExtStreamCreateWithCUMask failed"
+            raw_streams.append(rawp)
+            prep_stream = torch.cuda.ExternalStream(rawp, device=device)
+        else:
+            prep_stream = torch.cuda.Stream(device)
     copied = [torch.cuda.Event() for _ in range(nslots)] if on_gpu else None
     consumed = [torch.cuda.Event() for _ in range(nslots)] if on_gpu else None
 
@@ -160,6 +234,15 @@ def main(argv=None) -> int:
         else:
             dst.copy_(src, non_blocking=True)
 
+    def prepare(slot: int, after=None):
+        if prep_stream is None:
+            return
+        if after is not None:
+            prep_stream.wait_event(after)
+        b = dev[slot].batch
+        b.prep = L.linear_scan_prepare(b, R, S, space.dim, bool(learner.rule.bias), slot=slot,
+                                       stream=prep_stream)
+
     def prefetch(k: int):
         if a.ingest == "device":
             return
@@ -170,11 +253,16 @@ def main(argv=None) -> int:
                 cs.wait_event(consumed[slot])
                 h2d(dev[slot].flat, src.flat)
                 copied[slot].record(cs)
+            prepare(slot, copied[slot])
         else:
             dev[slot].flat.copy_(src.flat)
 
     def _step(k: int):
         if a.ingest == "device":
+            if prep_stream is not None:  # the next batch's passes 1-2 overlap this scan
+                nb = (k + 1) % a.pool
+                prep_stream.wait_stream(torch.cuda.current_stream(device))
+                prepare(nb)
             proto.round(dev[k % a.pool].batch)
             return
         slot = k % nslots
@@ -273,6 +361,9 @@ def main(argv=None) -> int:
     p50 = statistics.median(lat_us) if lat_us else None
     p99 = sorted(lat_us)[int(0.99 * (len(lat_us) - 1))] if lat_us else None
 
+    eng = engine_forecast_latency(a.engine_latency) if (rank == 0 and on_gpu and
+                                                         a.engine_latency > 0) else None
+
     total_examples = a.steps * B * world
     value = total_examples / elapsed
     if rank == 0:
@@ -299,6 +390,9 @@ def main(argv=None) -> int:
                        "semantics": "exact sequential per spoke, replicas averaged per round"},
             "p50_predict_latency_us": None if p50 is None else round(p50, 2),
             "p99_predict_latency_us": None if p99 is None else round(p99, 2),
+            "engine_forecast_p50_us": None if eng is None else eng["p50"],
+            "engine_forecast_p99_us": None if eng is None else eng["p99"],
+            "engine_forecast_semantics": None if eng is None else eng["what"],
             "per_gpu_examples_per_s": round(value / world, 1),
             "holdout_accuracy": None if acc is None else round(acc, 4),
             "ref_holdout_accuracy": None if ref_acc is None else round(ref_acc, 4),

@@ -529,40 +529,72 @@ OMLDM_API long long omldm_linear_scan_prep_floats(int R, int S) {
   return (long long)S * nchs * scan::PREP;
 }
 
+static int scan_check(int dc, int dn, int dim, int bias, int rule, int R) {
+  if (R <= 0 || dc > scan::MAXF || dc <= 0 || dn < 0 || dim <= dn + 1) return -2;
+  if (rule < 0 || rule > 2) return -5;
+  if (dn + (bias ? 1 : 0) > scan::KNMAX) return -2;
+  if ((long long)(dim - dn - 1) / dc < 1) return -2;
+  if (dc + dn > 50) return -3;  // the LDS ring of raw chunk inputs: use linear_seq instead
+  return 0;
+}
+
+// Passes 1-2 (hash, chunk Grams) of a round into (slots_ws, prep_ws) — independent of the
+// model, so they may run ahead on another stream while the previous round scans.
+OMLDM_API int omldm_linear_scan_prepare(const float* num, int dn, const void* tok, int dc, int B,
+                                        int R, int S, int dim, int bias, int* slots_ws,
+                                        float* prep_ws, void* stream) {
+  if (S <= 0 || B <= 0) return 0;
+  int e = scan_check(dc, dn, dim, bias, 0, R);
+  if (e) return e;
+  hipStream_t st = (hipStream_t)stream;
+  e = omldm_hash_raw(tok, B, dc, dn, dim, slots_ws, stream);
+  if (e) return e;
+  const int nchs = (R + scan::CH - 1) / scan::CH;
+  const long long sact = ((long long)B + R - 1) / R;
+  const int S_act = sact < S ? (int)sact : S;
+  if (dn + (bias ? 1 : 0) <= 16)
+    hipLaunchKernelGGL(scan_prep_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, slots_ws, dc,
+                       num, dn, B, R, bias, prep_ws, nchs);
+  else
+    hipLaunchKernelGGL(scan_prep_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, slots_ws, dc,
+                       num, dn, B, R, bias, prep_ws, nchs);
+  return (int)hipGetLastError();
+}
+
+// Pass 3 (the scan) + the round end, on a prepared round.
+OMLDM_API int omldm_linear_scan_run(const float* w, const float* num, int dn, int dc, const void* y,
+                                    int y8, int B, int R, int S, float* rep, float* dacc, int dim,
+                                    float* ws, double* cum, int rule, int variant, float C,
+                                    float eps, float lr, float inv_p, int bias,
+                                    const int* slots_ws, const float* prep_ws, void* stream) {
+  if (S <= 0 || B <= 0) return 0;
+  int e = scan_check(dc, dn, dim, bias, rule, R);
+  if (e) return e;
+  hipStream_t st = (hipStream_t)stream;
+  const SeqParams p{rule, variant, variant == 1 ? C : INFINITY, variant == 2 ? 0.5f / C : 0.f,
+                    eps, lr, inv_p, bias, y8, (uint32_t)((dim - dn - 1) / dc)};
+  const int nchs = (R + scan::CH - 1) / scan::CH;
+  const long long sact = ((long long)B + R - 1) / R;
+  const int S_act = sact < S ? (int)sact : S;
+  e = dn + (bias ? 1 : 0) <= 16
+          ? dispatch_scan<16>(rule, slots_ws, dc, num, dn, y, B, R, S, prep_ws, nchs, rep, dim, ws, p, st)
+          : dispatch_scan<32>(rule, slots_ws, dc, num, dn, y, B, R, S, prep_ws, nchs, rep, dim, ws, p, st);
+  if (e) return e;
+  return omldm_linear_seq_reduce(rep, w, S_act, dim, dacc, inv_p, ws, cum, stream);
+}
+
 // One Synchronous round of S exact sequential spokes on the raw wire (see the file
-// comment). Same contract as omldm_linear_seq_round, plus workspaces: slots_ws [B·dc]
-// int32, prep_ws [omldm_linear_scan_prep_floats(R, S)] fp32.
+// comment): prepare + run on one stream. Same contract as omldm_linear_seq_round, plus
+// workspaces: slots_ws [B·dc] int32, prep_ws [omldm_linear_scan_prep_floats(R, S)] fp32.
 OMLDM_API int omldm_linear_scan_round(const float* w, const float* num, int dn, const void* tok,
                                       int dc, const void* y, int y8, int B, int R, int S,
                                       float* rep, float* dacc, int dim, float* ws, double* cum,
                                       int rule, int variant, float C, float eps, float lr,
                                       float inv_p, int bias, int* slots_ws, float* prep_ws,
                                       void* stream) {
-  if (S <= 0 || B <= 0) return 0;
-  if (R <= 0 || dc > scan::MAXF || dc <= 0 || dn < 0 || dim <= dn + 1) return -2;
-  if (rule < 0 || rule > 2) return -5;
-  const int kn_need = dn + (bias ? 1 : 0);
-  if (kn_need > scan::KNMAX) return -2;
-  if ((long long)(dim - dn - 1) / dc < 1) return -2;
-  if (dc + dn > 50) return -3;  // the LDS ring of raw chunk inputs: use linear_seq instead
-  hipStream_t st = (hipStream_t)stream;
-  const SeqParams p{rule, variant, variant == 1 ? C : INFINITY, variant == 2 ? 0.5f / C : 0.f,
-                    eps, lr, inv_p, bias, y8, (uint32_t)((dim - dn - 1) / dc)};
-  int e = omldm_hash_raw(tok, B, dc, dn, dim, slots_ws, stream);
+  int e = omldm_linear_scan_prepare(num, dn, tok, dc, B, R, S, dim, bias, slots_ws, prep_ws,
+                                    stream);
   if (e) return e;
-  const int nchs = (R + scan::CH - 1) / scan::CH;
-  const long long sact = ((long long)B + R - 1) / R;
-  const int S_act = sact < S ? (int)sact : S;
-  if (kn_need <= 16)
-    hipLaunchKernelGGL(scan_prep_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, slots_ws, dc,
-                       num, dn, B, R, bias, prep_ws, nchs);
-  else
-    hipLaunchKernelGGL(scan_prep_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, slots_ws, dc,
-                       num, dn, B, R, bias, prep_ws, nchs);
-  e = (int)hipGetLastError();
-  if (e) return e;
-  e = kn_need <= 16 ? dispatch_scan<16>(rule, slots_ws, dc, num, dn, y, B, R, S, prep_ws, nchs, rep, dim, ws, p, st)
-                    : dispatch_scan<32>(rule, slots_ws, dc, num, dn, y, B, R, S, prep_ws, nchs, rep, dim, ws, p, st);
-  if (e) return e;
-  return omldm_linear_seq_reduce(rep, w, S_act, dim, dacc, inv_p, ws, cum, stream);
+  return omldm_linear_scan_run(w, num, dn, dc, y, y8, B, R, S, rep, dacc, dim, ws, cum, rule,
+                               variant, C, eps, lr, inv_p, bias, slots_ws, prep_ws, stream);
 }

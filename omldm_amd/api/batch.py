@@ -228,6 +228,8 @@ class RawBatch:
     num: torch.Tensor
     tok: torch.Tensor
     y: torch.Tensor
+    # passes 1-2 of the v2 round made ahead of the round (ops.linear.ScanPrep), or None
+    prep: object = None
 
     @property
     def B(self) -> int:

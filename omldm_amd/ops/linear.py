@@ -213,6 +213,42 @@ SEQ_RULES = (RULE_HINGE, RULE_EPS, RULE_LOGISTIC)
 SEQ_KERNEL = os.environ.get("OMLDM_SEQ_KERNEL", "scan")
 
 
+@dataclass
+class ScanPrep:
+    """Passes 1-2 of a v2 round (hashed slots + chunk Grams G/X1/X2) — model-independent,
+    so they can be made on another stream while the previous round scans."""
+
+    slots: torch.Tensor
+    prep: torch.Tensor
+    key: tuple          # (B, R, S, dim, bias) it was made for
+    event: object = None
+
+
+def scan_eligible(batch: RawBatch) -> bool:
+    return (SEQ_KERNEL == "scan" and batch.y.is_cuda and 0 < batch.dc
+            and batch.dc + batch.dn <= 50)
+
+
+def linear_scan_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool, slot: int = 0,
+                        stream=None) -> ScanPrep:
+    """Hash the batch's tokens and build its chunk Grams into workspace ``slot`` on
+    ``stream`` (default: the current stream); an event marks completion when a stream is
+    given."""
+    h = native.hip()
+    dev = batch.y.device
+    slots = _workspace(dev, batch.B * batch.dc, key=f"scan_slots{slot}")
+    prep = _workspace(dev, int(h.omldm_linear_scan_prep_floats(R, S)), key=f"scan_prep{slot}")
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    check(h.omldm_linear_scan_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), batch.dc,
+                                      batch.B, R, S, dim, int(bias), ptr(slots), ptr(prep),
+                                      st.cuda_stream), "omldm_linear_scan_prepare")
+    ev = None
+    if stream is not None:
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    return ScanPrep(slots, prep, (batch.B, R, S, dim, bool(bias)), ev)
+
+
 def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
                      rule: LinearRule, inv_p: float, cum: torch.Tensor | None = None,
                      stats: torch.Tensor | None = None, replicas: torch.Tensor | None = None
@@ -241,19 +277,21 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
         ws = _workspace(w.device, S * WS_STAT, key="seq_ws")
         if replicas is None:
             replicas = _workspace(w.device, S * dim, key="seq_replicas")
-        if SEQ_KERNEL == "scan" and 0 < tok.shape[1] and tok.shape[1] + num.shape[1] <= 50:
-            # v2 (csrc/kernels/linear_scan.hip): hash + chunk Grams over the whole GPU, one
-            # scan workgroup per spoke
-            h = native.hip()
-            slots = _workspace(w.device, batch.B * tok.shape[1], key="scan_slots")
-            prep = _workspace(w.device, int(h.omldm_linear_scan_prep_floats(R, S)),
-                              key="scan_prep")
-            rc = h.omldm_linear_scan_round(
-                ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
+        if scan_eligible(batch):
+            # v2 (csrc/kernels/linear_scan.hip): hash + chunk Grams over the whole GPU
+            # (possibly made ahead on another stream: batch.prep), one scan workgroup per
+            # spoke
+            sp = batch.prep
+            if not (isinstance(sp, ScanPrep) and sp.key == (batch.B, R, S, dim, bool(rule.bias))):
+                sp = linear_scan_prepare(batch, R, S, dim, bool(rule.bias))
+            elif sp.event is not None:
+                torch.cuda.current_stream(w.device).wait_event(sp.event)
+            rc = native.hip().omldm_linear_scan_run(
+                ptr(w), ptr(num), num.shape[1], tok.shape[1], ptr(y),
                 int(y.dtype == torch.int8), batch.B, R, S, ptr(replicas), ptr(dacc), dim,
                 ptr(ws), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, inv_p,
-                int(rule.bias), ptr(slots), ptr(prep), native.stream_of(w))
-            check(rc, "omldm_linear_scan_round")
+                int(rule.bias), ptr(sp.slots), ptr(sp.prep), native.stream_of(w))
+            check(rc, "omldm_linear_scan_run")
         else:
             rc = native.hip().omldm_linear_seq_round(
                 ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),

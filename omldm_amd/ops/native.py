@@ -60,6 +60,9 @@ HIP_SIGS = [
     ("omldm_linear_scan_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32,
                                       vp, vp, i32, i32, f32, f32, f32, f32, i32, vp, vp, vp]),
     ("omldm_linear_scan_prep_floats", i64, [i32, i32]),
+    ("omldm_linear_scan_prepare", i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
+    ("omldm_linear_scan_run", i32, [vp, vp, i32, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp,
+                                    vp, i32, i32, f32, f32, f32, f32, i32, vp, vp, vp]),
     ("omldm_linear_seq_reduce", i32, [vp, vp, i32, i32, vp, f32, vp, vp, vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
     ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
