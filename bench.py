@@ -138,6 +138,62 @@ def engine_forecast_latency(n: int) -> dict:
                     "resident serving wave + native Prediction formatting), trained SVM"}
 
 
+def engine_e2e_rate(records: int, batch: int = 65536) -> dict:
+    """Records/s of the training stream through the whole engine (rank 0, one GPU): JSON
+    DataInstance records in a file topic → pinned staging → GPU parse + feature hashing →
+    holdout routing → Synchronous round of a linear SVM (fp32, the job's default spokes)
+    → statistics. Record generation is not timed; the topic replays 20,000 distinct
+    records (bench/engine_e2e.py is the standalone, multi-GPU form)."""
+    import tempfile
+
+    from omldm_amd.engine.job import Job
+    from omldm_amd.io.synthetic import synth_json_records
+    from omldm_amd.io.transport import FileBroker
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.utils.config import JobConfig
+
+    sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
+    parts = 8
+    with tempfile.TemporaryDirectory() as root:
+        br = FileBroker(root)
+        br.create_topic("trainingData", parts)
+        br.create_topic("forecastingData", parts)
+        uniq = synth_json_records(20000, sp, start=0, seed=3)
+        for p in range(parts):
+            recs = [uniq[i % len(uniq)] for i in range(p, records, parts)]
+            br.produce_block("trainingData", p, ("\n".join(recs) + "\n").encode())
+        br.produce("requests", json.dumps({"id": 1, "request": "Create",
+                                           "learner": {"name": "SVM"},
+                                           "trainingConfiguration": {"protocol": "Synchronous"}}))
+        args = []
+        for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+                  "predictionsAddr", "performanceAddr"):
+            args += [f"--{k}", f"file://{root}"]
+        cfg = JobConfig.from_args(args + ["--hashDim", str(sp.dim), "--fieldAware", "true",
+                                          "--batchSize", str(batch), "--timeout", "1000",
+                                          "--test", "false", "--jobName", "bench-e2e"])
+        dev = torch.device("cuda", torch.cuda.current_device())
+        job = Job(cfg, Comm(), dev)
+        while not job.pipes:
+            job.tick()
+        for _ in range(2):  # staging slots grow to the record size
+            job.tick()
+        torch.cuda.synchronize(dev)
+        r0 = job.counters["records"]
+        t0 = time.perf_counter()
+        while job.counters["records"] + job.counters["invalid"] < records:
+            job.tick()
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        n = job.counters["records"] - r0
+        if job.fserver is not None:
+            job.fserver.close()
+        job.ingest.close()
+        job.egress.close()
+    return {"records_per_s": round(n / max(wall, 1e-9), 1), "records": n,
+            "spokes": job.spokes, "batch": batch}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,6 +220,8 @@ def main(argv=None) -> int:
     ap.add_argument("--ref", default="auto", choices=["auto", "on", "off"],
                     help="CPU reference-semantics accuracy on the same stream (rank 0)")
     ap.add_argument("--ref-max-examples", type=float, default=6e7)
+    ap.add_argument("--engine-e2e", type=int, default=524288,
+                    help="JSON records timed through the whole engine (rank 0; 0 = skip)")
     ap.add_argument("--engine-latency", type=int, default=300,
                     help="forecasting records timed through the engine (rank 0; 0 = skip)")
     a = ap.parse_args(argv)
@@ -363,6 +421,7 @@ def main(argv=None) -> int:
 
     eng = engine_forecast_latency(a.engine_latency) if (rank == 0 and on_gpu and
                                                          a.engine_latency > 0) else None
+    e2e = engine_e2e_rate(a.engine_e2e) if (rank == 0 and on_gpu and a.engine_e2e > 0) else None
 
     total_examples = a.steps * B * world
     value = total_examples / elapsed
@@ -393,6 +452,11 @@ def main(argv=None) -> int:
             "engine_forecast_p50_us": None if eng is None else eng["p50"],
             "engine_forecast_p99_us": None if eng is None else eng["p99"],
             "engine_forecast_semantics": None if eng is None else eng["what"],
+            "engine_e2e_records_per_s": None if e2e is None else e2e["records_per_s"],
+            "engine_e2e_semantics": None if e2e is None else
+            f"JSON DataInstance file topic -> GPU parse + hashing -> holdout -> Synchronous "
+            f"linear SVM fp32, {e2e['spokes']} spokes, {e2e['records']} records timed "
+            "(one GPU, rank 0)",
             "per_gpu_examples_per_s": round(value / world, 1),
             "holdout_accuracy": None if acc is None else round(acc, 4),
             "ref_holdout_accuracy": None if ref_acc is None else round(ref_acc, 4),

@@ -93,7 +93,8 @@ __global__ __launch_bounds__(256) void scan_prep_kernel(const int* __restrict__ 
 #pragma unroll 1
   for (int d = 0; d < 3; ++d) {
     float acc[4][4] = {};
-    if (c - d >= 0) {
+    // G keeps its strictly lower triangle only: blocks right of the diagonal stay 0
+    if (c - d >= 0 && !(d == 0 && bj > bi)) {
       int cnt[4][4] = {};
       for (int f = 0; f < dc; ++f) {
         const int4 a4 = *reinterpret_cast<const int4*>(&sl[0][f][4 * bi]);

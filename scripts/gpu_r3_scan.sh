@@ -13,5 +13,5 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 tail -8 gpurun_out/r3_new_tests.log
 timeout -k 10 240 python bench.py --steps 20 --warmup 5 --latency-samples 500 > gpurun_out/r3_bench.json 2> gpurun_out/r3_bench.err || { tail -30 gpurun_out/r3_bench.err; exit 6; }
 cat gpurun_out/r3_bench.json
-timeout -k 10 240 python bench.py --steps 20 --warmup 5 --latency-samples 10 --engine-latency 0 --ingest device --ref off > gpurun_out/r3_bench_dev.json 2> gpurun_out/r3_bench_dev.err || { tail -30 gpurun_out/r3_bench_dev.err; exit 7; }
+timeout -k 10 240 python bench.py --steps 20 --warmup 5 --latency-samples 10 --engine-latency 0 --engine-e2e 0 --ingest device --ref off > gpurun_out/r3_bench_dev.json 2> gpurun_out/r3_bench_dev.err || { tail -30 gpurun_out/r3_bench_dev.err; exit 7; }
 cat gpurun_out/r3_bench_dev.json
