@@ -266,7 +266,7 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
       if (k >= 0 && k < nch) {
         const int b = k & 1;
         const int row = t0 + k * scan::CH + lane;
-        const bool valid = row < t1;
+        const bool valid = row < t1 && ynx == ynx;  // a NaN target: not fitted
         const float y = valid ? ynx : 0.f;
         const float n2 = valid ? n2nx : 0.f;
         if (k + 1 < nch) {
@@ -559,6 +559,26 @@ OMLDM_API int omldm_linear_scan_prepare(const float* num, int dn, const void* to
   else
     hipLaunchKernelGGL(scan_prep_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, slots_ws, dc,
                        num, dn, B, R, bias, prep_ws, nchs);
+  return (int)hipGetLastError();
+}
+
+// Pass 2 alone, on slots that are already hashed (the engine's field-aware batches:
+// HashedBatch.to_wide() int32 signed slots, dn + f·span + local).
+OMLDM_API int omldm_linear_scan_prepare_slots(const float* num, int dn, const int* slots, int dc,
+                                              int B, int R, int S, int dim, int bias,
+                                              float* prep_ws, void* stream) {
+  if (S <= 0 || B <= 0) return 0;
+  int e = scan_check(dc, dn, dim, bias, 0, R);
+  if (e) return e;
+  const int nchs = (R + scan::CH - 1) / scan::CH;
+  const long long sact = ((long long)B + R - 1) / R;
+  const int S_act = sact < S ? (int)sact : S;
+  if (dn + (bias ? 1 : 0) <= 16)
+    hipLaunchKernelGGL(scan_prep_kernel<16>, dim3(nchs, S_act), dim3(256), 0, (hipStream_t)stream,
+                       slots, dc, num, dn, B, R, bias, prep_ws, nchs);
+  else
+    hipLaunchKernelGGL(scan_prep_kernel<32>, dim3(nchs, S_act), dim3(256), 0, (hipStream_t)stream,
+                       slots, dc, num, dn, B, R, bias, prep_ws, nchs);
   return (int)hipGetLastError();
 }
 

@@ -104,11 +104,31 @@ class LinearLearner(Learner):
         logistic SGD without L2); other rules hash the batch and take the spoke-table path."""
         return self.rule.rule in L.SEQ_RULES and self.rule.lam == 0.0 and self.w16 is None
 
-    def _fit_raw(self, batch: RawBatch, ctx: RoundContext) -> None:
-        B = batch.B
+    @staticmethod
+    def _seq_geometry(B: int, ctx: RoundContext) -> tuple[int, int]:
         S = max(1, int(ctx.spokes))
         R = max(1, -(-B // S)) if B else 1
         S = max(1, -(-B // R)) if B else S
+        return R, S
+
+    def _slots_scan_eligible(self, batch) -> bool:
+        """The engine's field-aware hashed batches train through the v2 scan round too
+        (slots already hashed: pass 1 skipped)."""
+        return (type(batch) is HashedBatch and batch.cat_span > 0 and self.w.is_cuda
+                and self.seq_capable() and L.SEQ_KERNEL == "scan" and batch.B > 0
+                and 0 < batch.dc and batch.dc + batch.dn <= 50)
+
+    def _fit_slots(self, batch: HashedBatch, ctx: RoundContext) -> None:
+        wide = batch.to_wide()
+        rb = RawBatch(batch.num.float().contiguous(), wide.cat.contiguous(),
+                      batch.y.float().contiguous())
+        R, S = self._seq_geometry(rb.B, ctx)
+        rb.prep = L.linear_scan_prepare_slots(rb, R, S, self.dim, bool(self.rule.bias))
+        self._fit_raw(rb, ctx)
+
+    def _fit_raw(self, batch: RawBatch, ctx: RoundContext) -> None:
+        B = batch.B
+        R, S = self._seq_geometry(B, ctx)
         on_gpu = self.w.is_cuda
         if on_gpu:
             if self.replicas is None or self.replicas.shape[0] < S:
@@ -135,6 +155,8 @@ class LinearLearner(Learner):
             if self.seq_capable():
                 return self._fit_raw(batch, ctx)
             batch = batch.hashed(self.space)
+        if self._slots_scan_eligible(batch):
+            return self._fit_slots(batch, ctx)
         B = batch.B
         S = max(1, int(ctx.spokes))
         R = max(1, -(-B // S)) if B else 1

@@ -249,6 +249,19 @@ def linear_scan_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool, s
     return ScanPrep(slots, prep, (batch.B, R, S, dim, bool(bias)), ev)
 
 
+def linear_scan_prepare_slots(batch: RawBatch, R: int, S: int, dim: int, bias: bool) -> ScanPrep:
+    """Pass 2 for a batch whose ``tok`` already holds field-aware signed slots (int32,
+    dn + field·span + local | sign << 31, −1 absent): the engine's hashed batches."""
+    h = native.hip()
+    prep = _workspace(batch.y.device, int(h.omldm_linear_scan_prep_floats(R, S)),
+                      key="scan_prep_slots")
+    check(h.omldm_linear_scan_prepare_slots(ptr(batch.num), batch.dn, ptr(batch.tok), batch.dc,
+                                            batch.B, R, S, dim, int(bias), ptr(prep),
+                                            native.stream_of(batch.y)),
+          "omldm_linear_scan_prepare_slots")
+    return ScanPrep(batch.tok, prep, (batch.B, R, S, dim, bool(bias)), None)
+
+
 def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
                      rule: LinearRule, inv_p: float, cum: torch.Tensor | None = None,
                      stats: torch.Tensor | None = None, replicas: torch.Tensor | None = None

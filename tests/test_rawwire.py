@@ -294,3 +294,29 @@ def test_blocked_gram_scan_algorithm_matches_oracle():
     L.linear_apply(wc, None, dacc)
     ref = _blocked_gram_scan(w, batch, space, 150, 2, C=0.7)
     assert np.allclose(wc.double().numpy(), ref, atol=1e-5, rtol=1e-4)
+
+
+@gpu
+def test_gpu_engine_field_aware_batches_take_the_scan_round():
+    """The engine's field-aware hashed batches (slots already hashed) train through the
+    v2 scan round on the GPU and agree with the CPU's exact sequential virtual spokes."""
+    from omldm_amd.api.batch import HashedBatch
+    from omldm_amd.io.synthetic import synth_batch
+    from omldm_amd.models.linear import SVM
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.parallel.protocols import Synchronous
+
+    space = FeatureSpace(13, 0, 26, 1 << 18, field_aware=True)
+    res = {}
+    for dev in ("cpu", "cuda"):
+        lrn = SVM({"variant": "PA-I", "C": 1.0}, space, dev)
+        assert dev == "cpu" or lrn._slots_scan_eligible(synth_batch(space, 64).to(dev))
+        proto = Synchronous(Comm(), lrn, {"virtualSpokes": 16})
+        for k in range(4):
+            b = synth_batch(space, 16 * 500, start=k * 16 * 500, seed=25)
+            assert type(b) is HashedBatch and b.cat_span > 0
+            proto.round(b.to(dev) if dev == "cuda" else b)
+        res[dev] = (lrn.w.cpu(), lrn.running_totals())
+    assert torch.allclose(res["cuda"][0], res["cpu"][0], atol=1e-3, rtol=1e-2), \
+        (res["cuda"][0] - res["cpu"][0]).abs().max()
+    assert res["cuda"][1]["fitted"] == res["cpu"][1]["fitted"] == 4 * 16 * 500
