@@ -16,12 +16,12 @@ Reference surface:
   the hub-message fan-out of FlinkLearning (omldm/job/FlinkLearning.scala:65-75).
 
 MI355X mapping. The training hot path never materialises these messages — the
-protocols in ``omldm_amd.parallel.protocols`` are collectives over RCCL. The message
-layer exists for (a) the control plane and statistics (byte accounting identical for
-every protocol), (b) ``CollectiveNetwork``: a point-to-point Network over
-torch.distributed (RCCL send/recv on GPUs, gloo on CPU) for user-defined node programs,
-and (c) ``LocalNetwork``: a deterministic in-process network with a seeded scheduler
-that permutes deliveries — the fake transport the protocol golden tests run on.
+protocols in ``omldm_amd.parallel.protocols`` are collectives over RCCL, and the
+point-to-point parameter-server channels of Asynchronous / SSP live in
+``omldm_amd.parallel.p2p``. The message layer exists for (a) the control plane and
+statistics (byte accounting identical for every protocol) and (b) ``LocalNetwork``: a
+deterministic in-process network with a seeded scheduler that permutes deliveries — the
+fake transport the protocol golden tests run on.
 """
 from __future__ import annotations
 
@@ -251,43 +251,6 @@ class LocalNetwork(Network):
         while n < max_steps and self.step():
             n += 1
         return n
-
-
-class CollectiveNetwork(Network):
-    """Point-to-point Network over torch.distributed: spoke i ↔ rank i, hub h ↔ rank
-    h % world. Payloads are tensors (RCCL send/recv over xGMI on GPUs, gloo on CPU);
-    ``broadcast`` to every spoke is one ``dist.broadcast``. Message headers are not
-    transmitted (the receiver's program knows what it expects, as in an SPMD round) but
-    are accounted with the same sizes as the reference's messages."""
-
-    def __init__(self, descriptor: NetworkDescriptor, group=None):
-        super().__init__(descriptor)
-        import torch.distributed as dist
-
-        self.dist = dist
-        self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-
-    def rank_of(self, nid: NodeId) -> int:
-        return nid.node_id % self.world
-
-    def send(self, source, destination, rpc, data):
-        msg = SpokeMessage(self.descriptor.network_id, rpc, source, destination, data)
-        self._account(msg)
-        if self.rank_of(destination) != self.rank:
-            self.dist.send(data, dst=self.rank_of(destination), group=self.group)
-
-    def recv(self, source: NodeId, out) -> None:
-        if self.rank_of(source) != self.rank:
-            self.dist.recv(out, src=self.rank_of(source), group=self.group)
-
-    def broadcast(self, source, destinations, data):
-        msg = HubMessage(self.descriptor.network_id, list(destinations.values()), source,
-                         list(destinations), data)
-        self._account(msg)
-        if self.world > 1:
-            self.dist.broadcast(data, src=self.rank_of(source), group=self.group)
 
 
 def hub_message_round_robin(counter: list, n_partitions: int) -> int:
