@@ -382,7 +382,7 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
     auto stage_src = [&](int u) {
       const int i = min(hl + 64 * scan::NH * u, 3 * scan::MAT / 4 - 1);
       const int mtx = i >> 10, e = i & 1023;
-      const int kc = min(cn + mtx, nch - 1);
+      const int kc = max(0, min(cn + mtx, nch - 1));  // cn = −1 in the first iteration
       return reinterpret_cast<const float4*>(chunk_prep(kc) + mtx * scan::MAT) + e;
     };
     const float4 v0 = *stage_src(0), v1 = *stage_src(1), v2 = *stage_src(2), v3 = *stage_src(3),
