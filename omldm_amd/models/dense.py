@@ -75,13 +75,16 @@ class ORR(Learner):
         if self._w is None:
             d = self.d
             A = self.G[: d + 1, : d + 1].double()
-            A = A + self.lam * torch.eye(d + 1, dtype=A.dtype, device=A.device)
-            b = self.G[: d + 1, d + 1].double()
-            Lc, info = torch.linalg.cholesky_ex(A)
-            if int(info.item()) == 0:
-                self._w = torch.cholesky_solve(b.unsqueeze(1), Lc).squeeze(1).float()
+            eye = torch.eye(d + 1, dtype=A.dtype, device=A.device)
+            if self.lam > 0:
+                A = A + self.lam * eye
             else:
-                self._w = torch.linalg.lstsq(A, b.unsqueeze(1)).solution.squeeze(1).float()
+                # λ = 0: a relative jitter keeps A positive definite, so the Cholesky solve
+                # never has to be checked on the host (no device → host sync per predict)
+                A = A + (1e-12 * (torch.diagonal(A).sum() / (d + 1)) + 1e-30) * eye
+            b = self.G[: d + 1, d + 1].double()
+            Lc, _ = torch.linalg.cholesky_ex(A)
+            self._w = torch.cholesky_solve(b.unsqueeze(1), Lc).squeeze(1).float()
         return self._w
 
     def predict(self, batch):
