@@ -20,9 +20,11 @@ batched path: while any exists, records are handed to the tick (``take_fallback`
 """
 from __future__ import annotations
 
+import atexit
 import collections
 import threading
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -32,12 +34,24 @@ from omldm_amd.ops import native
 
 OP_FORECASTING = 1
 
+_LIVE: "weakref.WeakSet[ForecastServer]" = weakref.WeakSet()
+
+
+@atexit.register
+def _stop_all() -> None:
+    """No resident wave outlives its process (a Job that was never run to the end)."""
+    for fs in list(_LIVE):
+        try:
+            fs.close()
+        except Exception:  # noqa: BLE001 — best effort at interpreter exit
+            pass
+
 
 class ForecastServer:
     IDLE_SLEEP_S = 20e-6
     SPIN_S = 2e-3  # after a record, poll without sleeping this long (sleep(0) yields the GIL)
 
-    def __init__(self, job, lifetime_us: int = 3_600_000_000):
+    def __init__(self, job, lifetime_us: int = 30_000_000):
         self.job = job
         self.space = job.space
         self.consumer = job.fcst_in
@@ -56,12 +70,15 @@ class ForecastServer:
         # one record's parse buffers (omldm_serve_request copies them into the mailbox)
         self._num = torch.zeros((1, dn), dtype=torch.float32)
         self._cat = torch.full((1, dc), -1, dtype=self.space.cat_dtype)
+        # the mailbox carries int32 per field: the wide slot, or the compact uint16 value
+        self._cat32 = np.full(max(dc, 1), -1, dtype=np.int32)
         self._y = torch.zeros(1, dtype=torch.float32)
         self._op = np.zeros(1, dtype=np.int8)
         self._offs = np.zeros(2, dtype=np.int64)
         self._busy = False             # a polled batch is being answered
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, name="omldm-forecast", daemon=True)
+        _LIVE.add(self)
 
     # ----------------------------------------------------------------- control
     def start(self) -> None:
@@ -69,7 +86,8 @@ class ForecastServer:
 
     def close(self) -> None:
         self._stop.set()
-        self._thread.join(5.0)
+        if self._thread.is_alive():
+            self._thread.join(5.0)
         with self.lock:
             self._stop_wave()
 
@@ -92,7 +110,7 @@ class ForecastServer:
         with self.lock:
             self._build_wave()
 
-    def _build_wave(self) -> None:
+    def _build_wave(self, sync: bool = True) -> None:
         from omldm_amd.ops.serving import PredictServer
 
         self._stop_wave()
@@ -106,7 +124,8 @@ class ForecastServer:
         rows = [p.store_row for p in pipes]
         lo, hi = min(rows), max(rows) + 1
         W = self.job.store.W[lo:hi]
-        torch.cuda.synchronize(W.device)
+        if sync:  # a Create's weights copied into the store have landed
+            torch.cuda.synchronize(W.device)
         srv = PredictServer(W, self.space.dn, self.space.dc, biases.pop(),
                             cat_span=self.space.cat_span)
         srv.start(lifetime_us=self.lifetime_us)
@@ -137,6 +156,10 @@ class ForecastServer:
             rec, self._offs.ctypes.data, 1, sp.n_numerical, sp.n_discrete, sp.dc, sp.dim,
             sp.cat_span, self._num.data_ptr(), self._cat.data_ptr(), self._y.data_ptr(),
             self._op.ctypes.data, 1)
+        if sp.cat_span > 0:
+            self._cat32[: sp.dc] = self._cat.numpy()[0].view(np.uint16)
+        else:
+            self._cat32[: sp.dc] = self._cat.numpy()[0]
         return int(self._op[0]) == OP_FORECASTING
 
     def serve_one(self, rec: bytes, t_in: float | None = None) -> bool:
@@ -150,11 +173,15 @@ class ForecastServer:
             if not self._parse(rec):
                 self.invalid += 1
                 return True
+            cat = self._cat32.ctypes.data
+            if not srv.lib.omldm_serve_alive(srv.mb):  # lifetime over: a fresh wave
+                self._build_wave(sync=False)
+                srv = self._server
             try:
-                out = srv.request_raw(self._num.data_ptr(), self._cat.data_ptr())
+                out = srv.request_raw(self._num.data_ptr(), cat)
             except TimeoutError:  # the wave's lifetime ended: a fresh one, same models
-                self._build_wave()
-                out = self._server.request_raw(self._num.data_ptr(), self._cat.data_ptr())
+                self._build_wave(sync=False)
+                out = self._server.request_raw(self._num.data_ptr(), cat)
             raw = RawRecords(np.frombuffer(rec, dtype=np.uint8),
                              np.zeros(1, dtype=np.int64), np.array([len(rec)], dtype=np.int64))
             for pid, row, cls in self._served:
