@@ -342,23 +342,32 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
     wn[i] = (j < KN) ? (j < dn ? W[j] : ((p.bias && j == dn) ? W[dim - 1] : 0.f)) : 0.f;
   }
   const int slot_dw = dc * scan::CH;
-  // raw inputs of chunk kc: dword d of the chunk image (slots then num), clamped source
-  auto raw_src = [&](int kc, int d) -> const int* {
-    const int kk = min(kc, nch - 1);
-    const int base_row = t0 + kk * scan::CH;
+  // this lane's dwords of a chunk's raw image (slots then num): d = hl + 64·NH·u, the
+  // same in every chunk, so the (row, column) split is done once (integer division is
+  // ~40 VALU instructions)
+  int rrow[kRawLd], rcol[kRawLd];
+#pragma unroll
+  for (int u = 0; u < kRawLd; ++u) {
+    const int d = min(hl + 64 * scan::NH * u, rdw - 1);
     if (d < slot_dw) {
-      const int row = min(base_row + d / dc, t1 - 1);
-      return slots + (size_t)row * dc + (d - (d / dc) * dc);
+      rrow[u] = d / dc;
+      rcol[u] = d - rrow[u] * dc;
+    } else {
+      const int e = d - slot_dw, dd = max(dn, 1);
+      rrow[u] = e / dd;
+      rcol[u] = -1 - (e - rrow[u] * dd);  // < 0: a numerical column
     }
-    const int e = d - slot_dw;
-    const int row = min(base_row + e / max(dn, 1), t1 - 1);
-    return reinterpret_cast<const int*>(num) + (size_t)row * dn + (e - (e / max(dn, 1)) * dn);
+  }
+  // raw inputs of chunk kc: the lane's dword u, clamped source
+  auto raw_src = [&](int kc, int u) -> const int* {
+    const int row = min(t0 + min(kc, nch - 1) * scan::CH + rrow[u], t1 - 1);
+    return rcol[u] >= 0 ? slots + (size_t)row * dc + rcol[u]
+                        : reinterpret_cast<const int*>(num) + (size_t)row * dn + (-1 - rcol[u]);
   };
   // its row validity (rows past the shard: absent slots, zero features)
-  auto raw_fix = [&](int kc, int d, int v) -> int {
-    const int base_row = t0 + kc * scan::CH;
-    if (d < slot_dw) return base_row + d / dc < t1 ? v : -1;
-    return base_row + (d - slot_dw) / max(dn, 1) < t1 ? v : 0;
+  auto raw_fix = [&](int kc, int u, int v) -> int {
+    if (t0 + kc * scan::CH + rrow[u] < t1) return v;
+    return rcol[u] >= 0 ? -1 : 0;
   };
   int rv[kRawLd];
 
@@ -390,7 +399,7 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
     // ---- raw inputs of chunk cn + 1 (coalesced dwords; LDS ring at the end)
     const int kr = cn + 1;
 #pragma unroll
-    for (int u = 0; u < kRawLd; ++u) rv[u] = *raw_src(kr, min(hl + 64 * scan::NH * u, rdw - 1));
+    for (int u = 0; u < kRawLd; ++u) rv[u] = *raw_src(kr, u);
     if (wave == 1) stamp(3);
     if (cn >= 0 && cn < nch) {
       // ---- dense part of chunk cn's margins (w_dense after chunks ≤ k − 2)
@@ -459,7 +468,7 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
 #pragma unroll
       for (int u = 0; u < kRawLd; ++u) {
         const int d = hl + 64 * scan::NH * u;
-        if (d < rdw) dst[d] = raw_fix(kr, d, rv[u]);
+        if (d < rdw) dst[d] = raw_fix(kr, u, rv[u]);
       }
     }
     if (wave == 1) {

@@ -29,11 +29,13 @@ def test_rounds_do_not_wait_for_the_device(proto):
     batches = [synth_batch(SP, 1024, start=i * 1024).to(dev) for i in range(6)]
     P.round(batches[0])  # buffers, first decision posted
     torch.cuda.synchronize()
-    # calibrate the spin: ~200 ms of device time
-    t = time.perf_counter()
-    torch.cuda._sleep(10_000_000)
-    torch.cuda.synchronize()
-    per = (time.perf_counter() - t) / 10_000_000
+    # calibrate the spin: ~200 ms of device time (the second measurement: the first
+    # includes the spin kernel's first launch)
+    for _ in range(2):
+        t = time.perf_counter()
+        torch.cuda._sleep(20_000_000)
+        torch.cuda.synchronize()
+        per = (time.perf_counter() - t) / 20_000_000
     cycles = int(0.2 / max(per, 1e-12))
     torch.cuda._sleep(cycles)
     # GM/FGM: the host may run one round ahead of the device (the decision of round k is
@@ -47,6 +49,6 @@ def test_rounds_do_not_wait_for_the_device(proto):
         P.round(b)
     torch.cuda.synchronize()
     total_s = time.perf_counter() - t
-    assert total_s > 0.15, total_s  # the spin really ran
-    assert host_s < 0.05, (proto, host_s, total_s)
+    assert total_s > 0.08, total_s  # the spin really ran
+    assert host_s < 0.25 * total_s, (proto, host_s, total_s)
     assert L.running_totals()["fitted"] == 6 * 1024
