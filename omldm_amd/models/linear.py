@@ -116,7 +116,7 @@ class LinearLearner(Learner):
         (slots already hashed: pass 1 skipped)."""
         return (type(batch) is HashedBatch and batch.cat_span > 0 and self.w.is_cuda
                 and self.seq_capable() and L.SEQ_KERNEL == "scan" and batch.B > 0
-                and 0 < batch.dc and batch.dc + batch.dn <= 50)
+                and 0 < batch.dc and L.scan_fits(batch.dn, batch.dc))
 
     def _fit_slots(self, batch: HashedBatch, ctx: RoundContext) -> None:
         wide = batch.to_wide()

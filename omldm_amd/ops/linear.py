@@ -224,9 +224,20 @@ class ScanPrep:
     event: object = None
 
 
+_SCAN_FITS: dict = {}
+
+
+def scan_fits(dn: int, dc: int) -> bool:
+    """The v2 round's LDS holds this (dn, dc) shape (else linear_seq.hip runs)."""
+    key = (int(dn), int(dc))
+    if key not in _SCAN_FITS:
+        _SCAN_FITS[key] = bool(native.hip().omldm_linear_scan_fits(*key))
+    return _SCAN_FITS[key]
+
+
 def scan_eligible(batch: RawBatch) -> bool:
     return (SEQ_KERNEL == "scan" and batch.y.is_cuda and 0 < batch.dc
-            and batch.dc + batch.dn <= 50)
+            and scan_fits(batch.dn, batch.dc))
 
 
 def linear_scan_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool, slot: int = 0,

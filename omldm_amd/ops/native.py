@@ -60,6 +60,7 @@ HIP_SIGS = [
     ("omldm_linear_scan_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32,
                                       vp, vp, i32, i32, f32, f32, f32, f32, i32, vp, vp, vp]),
     ("omldm_linear_scan_prep_floats", i64, [i32, i32]),
+    ("omldm_linear_scan_fits", i32, [i32, i32]),
     ("omldm_linear_scan_prepare", i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     ("omldm_linear_scan_prepare_slots", i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp]),
     ("omldm_linear_scan_run", i32, [vp, vp, i32, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp,
