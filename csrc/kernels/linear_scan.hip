@@ -45,8 +45,7 @@ constexpr int KNMAX = 32;
 constexpr int NJ = (KNMAX + NH - 1) / NH;  // dense columns per helper lane
 constexpr int GXB = (CH + NH - 1) / NH;    // X2 columns per helper wave
 constexpr int MAT = CH * CH;
-constexpr int REPF = MAXF * CH / 4;        // uint8 group representative per (field, row)
-constexpr int PREP = 3 * MAT + CH + REPF;  // G | X1 | X2 | ‖x‖² | rep per chunk (floats)
+constexpr int PREP = 3 * MAT + CH;         // G | X1 | X2 | ‖x‖² per chunk (floats)
 constexpr int NV4 = (2 * MAT / 4 + 64 * NH - 1) / (64 * NH);  // float4 of G+X1 per helper lane
 constexpr int WS = 8;
 constexpr int ABSENT_A = 0x7ffffffe;       // never equal to a slot (slots < 2^31 − 2)
@@ -90,25 +89,6 @@ __global__ __launch_bounds__(256) void scan_prep_kernel(const int* __restrict__ 
     for (int j = 0; j < KN; ++j) n2 = fmaf(xn[0][tid][j], xn[0][tid][j], n2);
     for (int f = 0; f < dc; ++f) n2 += sl[0][f][tid] != -1 ? 1.f : 0.f;
     out[3 * scan::MAT + tid] = n2;
-  }
-  {  // group representative of each (field, row): the first row of the chunk with the
-     // same slot (the scan pre-sums a chunk's updates per slot: one L2 atomic per group)
-    uint8_t* rep = reinterpret_cast<uint8_t*>(out + 3 * scan::MAT + scan::CH);
-    for (int idx = tid; idx < dc * scan::CH; idx += 256) {
-      const int f = idx >> 6, r = idx & 63;
-      const int v = sl[0][f][r];
-      int rp = r;
-      if (v != -1) {
-        for (int r2 = 0; r2 < r; ++r2) {
-          const int o = sl[0][f][r2];
-          if (o != -1 && ((o ^ v) & 0x7fffffff) == 0) {
-            rp = r2;
-            break;
-          }
-        }
-      }
-      rep[idx] = (uint8_t)rp;
-    }
   }
   const int bi = tid >> 4, bj = tid & 15;
 #pragma unroll 1
@@ -252,8 +232,7 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
   const int nch = (t1 - t0 + scan::CH - 1) / scan::CH;
   const float* P0 = prep + (size_t)s * nchs * scan::PREP;
   auto chunk_prep = [&](int k) { return P0 + (size_t)k * scan::PREP; };
-  // dwords of one ring slot: slots [64][dc] | num [64][dn] | group reps uint8 [dc][64]
-  const int rdw = (dc + dn) * scan::CH + dc * scan::CH / 4;
+  const int rdw = (dc + dn) * scan::CH;  // dwords of one ring slot
   auto ring_sl = [&](int k) { return ring + (k & 3) * rdw; };
   auto ring_x = [&](int k) { return reinterpret_cast<const float*>(ring + (k & 3) * rdw + dc * scan::CH); };
 
@@ -367,39 +346,30 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
   // this lane's dwords of a chunk's raw image (slots then num): d = hl + 64·NH·u, the
   // same in every chunk, so the (row, column) split is done once (integer division is
   // ~40 VALU instructions)
-  const int rep_dw0 = (dc + dn) * scan::CH;
-  int rrow[kRawLd], rcol[kRawLd];  // rcol ≥ 0: slot column; < 0: num column; rrow < 0: rep
+  int rrow[kRawLd], rcol[kRawLd];
 #pragma unroll
   for (int u = 0; u < kRawLd; ++u) {
     const int d = min(hl + 64 * scan::NH * u, rdw - 1);
     if (d < slot_dw) {
       rrow[u] = d / dc;
       rcol[u] = d - rrow[u] * dc;
-    } else if (d < rep_dw0) {
+    } else {
       const int e = d - slot_dw, dd = max(dn, 1);
       rrow[u] = e / dd;
       rcol[u] = -1 - (e - rrow[u] * dd);  // < 0: a numerical column
-    } else {
-      rrow[u] = -1;
-      rcol[u] = d - rep_dw0;  // dword of the chunk's rep bytes (prep output)
     }
   }
   // raw inputs of chunk kc: the lane's dword u, clamped source
   auto raw_src = [&](int kc, int u) -> const int* {
-    const int kk = min(kc, nch - 1);
-    if (rrow[u] < 0)
-      return reinterpret_cast<const int*>(chunk_prep(kk) + 3 * scan::MAT + scan::CH) + rcol[u];
-    const int row = min(t0 + kk * scan::CH + rrow[u], t1 - 1);
+    const int row = min(t0 + min(kc, nch - 1) * scan::CH + rrow[u], t1 - 1);
     return rcol[u] >= 0 ? slots + (size_t)row * dc + rcol[u]
                         : reinterpret_cast<const int*>(num) + (size_t)row * dn + (-1 - rcol[u]);
   };
   // its row validity (rows past the shard: absent slots, zero features)
   auto raw_fix = [&](int kc, int u, int v) -> int {
-    if (rrow[u] < 0 || t0 + kc * scan::CH + rrow[u] < t1) return v;
+    if (t0 + kc * scan::CH + rrow[u] < t1) return v;
     return rcol[u] >= 0 ? -1 : 0;
   };
-  const int nfe = (dc + scan::NH - 1) / scan::NH;  // fields per helper wave
-  float* gsum = reinterpret_cast<float*>(ring + 4 * rdw) + q * nfe * scan::CH;
   int rv[kRawLd];
 
   auto iteration = [&](int k) __attribute__((always_inline)) {
@@ -475,28 +445,12 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
       const int* ssl = ring_sl(ks);
       const float* sx = ring_x(ks);
       const float cv = sm.cb[ks & 1][r];
-      const uint8_t* rep8 = reinterpret_cast<const uint8_t*>(ssl + rep_dw0);
-      // the chunk's updates pre-summed per slot in LDS (wave-private: this wave's fields),
-      // then one L2 atomic per distinct slot from its group's representative row
-#pragma unroll
-      for (int i = 0; i < scan::NF; ++i)
-        if (i < nfe) gsum[i * scan::CH + r] = 0.f;
 #pragma unroll
       for (int i = 0; i < scan::NF; ++i) {
         const int f = q + scan::NH * i;
         if (f < dc) {
           const int cd = ssl[r * dc + f];
-          if (cd != -1 && cv != 0.f)
-            atomicAdd(&gsum[i * scan::CH + rep8[f * scan::CH + r]], cd < 0 ? -cv : cv);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < scan::NF; ++i) {
-        const int f = q + scan::NH * i;
-        if (f < dc) {
-          const int cd = ssl[r * dc + f];
-          const float v = gsum[i * scan::CH + r];
-          if (cd != -1 && rep8[f * scan::CH + r] == r && v != 0.f) add_rep(&W[cd & 0x7fffffff], v);
+          if (cd != -1 && cv != 0.f) add_rep(&W[cd & 0x7fffffff], cd < 0 ? -cv : cv);
         }
       }
 #pragma unroll
@@ -539,11 +493,9 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
   }
 }
 
-// dynamic LDS of the scan: the 4-chunk ring of raw inputs + the per-wave group sums
+// dynamic LDS of the scan: the 4-chunk ring of raw inputs (slots [64][dc] | num [64][dn])
 static size_t scan_dyn_lds(int dc, int dn) {
-  const size_t rdw = (size_t)(dc + dn) * scan::CH + (size_t)dc * scan::CH / 4;
-  const size_t nfe = (dc + scan::NH - 1) / scan::NH;
-  return (4 * rdw + scan::NH * nfe * scan::CH) * sizeof(int);
+  return (size_t)4 * (dc + dn) * scan::CH * sizeof(int);
 }
 
 template <int RULE, int KN>
@@ -589,7 +541,8 @@ OMLDM_API int omldm_linear_scan_stamps(void* buf) {
 
 // 1 when the v2 round supports this (dn, dc) shape (its LDS fits), else 0.
 OMLDM_API int omldm_linear_scan_fits(int dn, int dc) {
-  return dc > 0 && dc <= scan::MAXF && scan_dyn_lds(dc, dn) + sizeof(ScanSmem) <= 160 * 1024;
+  return dc > 0 && dc <= scan::MAXF && dc + dn <= 50 &&
+         scan_dyn_lds(dc, dn) + sizeof(ScanSmem) <= 160 * 1024;
 }
 
 // Floats of prep workspace one round needs (S spokes of R rows).
@@ -604,7 +557,7 @@ static int scan_check(int dc, int dn, int dim, int bias, int rule, int R) {
   if (dn + (bias ? 1 : 0) > scan::KNMAX) return -2;
   if ((long long)(dim - dn - 1) / dc < 1) return -2;
   // the LDS ring of raw chunk inputs must fit beside the static LDS: else use linear_seq
-  if (scan_dyn_lds(dc, dn) + sizeof(ScanSmem) > 160 * 1024) return -3;
+  if (dc + dn > 50 || scan_dyn_lds(dc, dn) + sizeof(ScanSmem) > 160 * 1024) return -3;
   return 0;
 }
 
