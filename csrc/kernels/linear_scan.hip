@@ -401,26 +401,6 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
     const int kr = cn + 1;
 #pragma unroll
     for (int u = 0; u < kRawLd; ++u) rv[u] = *raw_src(kr, u);
-    // ---- scatter chunk k − 1's categorical update (c known since the last barrier):
-    // issued right behind this wave's gathers, so the L2 atomics stream while the gathers
-    // are in flight. A wave's gathers reach L2 ahead of its later atomics, so chunk cn's
-    // margins still see the replica of chunks ≤ k − 2 (what the X2 / X1 folds assume);
-    // the s_waitcnt at the top of the next iteration lands them before its gathers.
-    {
-      const int ks = k - 1;
-      if (ks >= 0 && ks < nch) {
-        const int* ssl = ring_sl(ks);
-        const float cv = sm.cb[ks & 1][r];
-#pragma unroll
-        for (int i = 0; i < scan::NF; ++i) {
-          const int f = q + scan::NH * i;
-          if (f < dc) {
-            const int cd = ssl[r * dc + f];
-            if (cd != -1 && cv != 0.f) add_rep(&W[cd & 0x7fffffff], cd < 0 ? -cv : cv);
-          }
-        }
-      }
-    }
     if (wave == 1) stamp(3);
     if (cn >= 0 && cn < nch) {
       // ---- dense part of chunk cn's margins (w_dense after chunks ≤ k − 2)
@@ -459,11 +439,20 @@ __global__ __launch_bounds__(scan::NT, 1) void scan_round_kernel(
     stage_put(5, v5);
     stage_put(6, v6);
     if (wave == 1) stamp(5);
-    // ---- chunk k − 1's dense update (after this iteration's dense snapshot)
+    // ---- scatter chunk k − 1 (c known since the last barrier) and its dense update
     const int ks = k - 1;
     if (ks >= 0 && ks < nch) {
+      const int* ssl = ring_sl(ks);
       const float* sx = ring_x(ks);
       const float cv = sm.cb[ks & 1][r];
+#pragma unroll
+      for (int i = 0; i < scan::NF; ++i) {
+        const int f = q + scan::NH * i;
+        if (f < dc) {
+          const int cd = ssl[r * dc + f];
+          if (cd != -1 && cv != 0.f) add_rep(&W[cd & 0x7fffffff], cd < 0 ? -cv : cv);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < scan::NJ; ++i) {
         const int j = q + scan::NH * i;
