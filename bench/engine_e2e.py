@@ -42,6 +42,10 @@ def main(argv=None) -> int:
                     help="engine ingestCopy (staging copy: pull kernel or SDMA)")
     ap.add_argument("--forecast-frac", type=float, default=0.0,
                     help="share of the records sent to forecastingData (→ predictions)")
+    ap.add_argument("--spokes", type=int, default=0,
+                    help="spokesPerDevice (0: the job default, parallelism / world = 16)")
+    ap.add_argument("--model-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--forecast-server", default="auto", help="engine forecastServer flag")
     ap.add_argument("--unique", type=int, default=100_000,
                     help="distinct JSON records generated; the topic replays them")
     a = ap.parse_args(argv)
@@ -69,7 +73,7 @@ def main(argv=None) -> int:
         for i in range(a.pipelines):
             br.produce("requests", json.dumps({
                 "id": i + 1, "request": "Create",
-                "learner": {"name": "SVM", "hyperParameters": {"modelDtype": "bf16",
+                "learner": {"name": "SVM", "hyperParameters": {"modelDtype": a.model_dtype,
                                                                "tableLog2": 11}},
                 "trainingConfiguration": {"protocol": "Synchronous"}}))
         addr = f"file://{root}"
@@ -79,7 +83,8 @@ def main(argv=None) -> int:
             args += [f"--{k}", addr]
         cfg = JobConfig.from_args(args + ["--hashDim", str(sp.dim), "--fieldAware", "true",
                                           "--batchSize", str(a.batch), "--timeout", "1000",
-                                          "--spokesPerDevice", "4096",
+                                          "--spokesPerDevice", str(a.spokes),
+                                          "--forecastServer", a.forecast_server,
                                           "--parseThreads", str(a.threads), "--jobName", "e2e"]
                                   + (["--ingestCUs", str(a.ingest_cus)]
                                      if a.ingest_cus is not None else [])
@@ -109,6 +114,7 @@ def main(argv=None) -> int:
                 "value": round((job.counters["records"] - r0) * comm.world / max(wall, 1e-9), 1),
                 "unit": "records/s", "n_gpus": comm.world, "records": job.counters["records"],
                 "pipelines": a.pipelines, "batch": a.batch, "wall_s": round(wall, 3),
+                "spokes": job.spokes, "model_dtype": a.model_dtype,
                 "forecast_frac": a.forecast_frac, "predictions": job.counters["predictions"],
                 "generate_s": round(gen_s, 1), "stages_ms": stages,
                 "ticks_timed": stages.get("poll", {}).get("calls"),

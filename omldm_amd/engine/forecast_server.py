@@ -49,7 +49,11 @@ def _stop_all() -> None:
 
 class ForecastServer:
     IDLE_SLEEP_S = 20e-6
-    SPIN_S = 2e-3  # after a record, poll without sleeping this long (sleep(0) yields the GIL)
+    # idle polling backs off in tiers so a quiet forecasting topic costs the training tick
+    # nothing: busy-poll (sleep(0) yields the GIL) for 2 ms after a record, then 50 µs
+    # sleeps, then 1 ms sleeps once the topic has been quiet for 50 ms
+    SPIN_S = 2e-3
+    WARM_S = 50e-3
 
     def __init__(self, job, lifetime_us: int = 30_000_000):
         self.job = job
@@ -216,9 +220,9 @@ class ForecastServer:
             recs = self.consumer.poll(64)
             if not recs:
                 self._busy = False
-                # busy-poll right after traffic (a sleep costs ~60 µs of latency), back off
-                # to short sleeps when the topic has been quiet
-                time.sleep(0 if time.perf_counter() - last < self.SPIN_S else self.IDLE_SLEEP_S)
+                quiet = time.perf_counter() - last
+                time.sleep(0 if quiet < self.SPIN_S else
+                           (50e-6 if quiet < self.WARM_S else 1e-3))
                 continue
             last = time.perf_counter()
             t_in = time.perf_counter()
