@@ -79,7 +79,7 @@ class ForecastServer:
         self._y = torch.zeros(1, dtype=torch.float32)
         self._op = np.zeros(1, dtype=np.int8)
         self._offs = np.zeros(2, dtype=np.int64)
-        self._busy = False             # a polled batch is being answered
+        self._done: dict = {}          # consumer offsets up to which every record is answered
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, name="omldm-forecast", daemon=True)
         _LIVE.add(self)
@@ -208,18 +208,23 @@ class ForecastServer:
                   for p in self.consumer.parts}
         t0 = time.time()
         while time.time() - t0 < timeout_s:
-            if not self._busy and all(self.consumer.offsets[p] >= o for p, o in target.items()):
+            done = self._done
+            if all(done.get(p, 0) >= o for p, o in target.items()):
                 return True
             time.sleep(self.IDLE_SLEEP_S)
         return False
 
+    def _pending(self) -> bool:
+        br, topic, offs = self.consumer.broker, self.consumer.topic, self.consumer.offsets
+        return any(br.end_offset(topic, p) > o for p, o in offs.items())
+
     def _run(self) -> None:
         last = 0.0
         while not self._stop.is_set():
-            self._busy = True
-            recs = self.consumer.poll(64)
+            # a cheap look at the end offsets first: a quiet topic is not polled
+            recs = self.consumer.poll(64) if self._pending() else []
             if not recs:
-                self._busy = False
+                self._done = dict(self.consumer.offsets)  # everything before is answered
                 quiet = time.perf_counter() - last
                 time.sleep(0 if quiet < self.SPIN_S else
                            (50e-6 if quiet < self.WARM_S else 1e-3))
@@ -229,4 +234,4 @@ class ForecastServer:
             for i, rec in enumerate(recs):
                 if not self.serve_one(rec, t_in if i == 0 else None):
                     self.fallback.append(rec)
-            self._busy = False
+            self._done = dict(self.consumer.offsets)
