@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import atexit
 import collections
+import os
 import threading
 import time
 import weakref
@@ -55,7 +56,7 @@ class ForecastServer:
     SPIN_S = 2e-3
     WARM_S = 50e-3
 
-    def __init__(self, job, lifetime_us: int = 30_000_000):
+    def __init__(self, job, lifetime_us: int = 2_000_000):
         self.job = job
         self.space = job.space
         self.consumer = job.fcst_in
@@ -64,6 +65,7 @@ class ForecastServer:
         self.lifetime_us = int(lifetime_us)
         self.lock = threading.Lock()
         self._server = None
+        self._spec = None             # (first store row, end row, bias) the wave serves
         self._served: list = []       # (pipeline id, store row, classification?) in W order
         self._row0 = 0
         self.fallback: collections.deque = collections.deque()
@@ -105,37 +107,55 @@ class ForecastServer:
         reading it until ``reconfigure``."""
         with self.lock:
             self._stop_wave()
+            self._spec = None
             self._served = []
 
     def reconfigure(self) -> None:
         """After a Create / Delete / restore (main thread): serve the model-store
         pipelines with the wave when every pipeline lives in the store, else hand all
-        records to the batched path."""
+        records to the batched path. The wave itself starts with the first record: a
+        resident wave holds one of the process's hardware queues (4 on this pool), which
+        costs the training tick's copy / parse / compute overlap while no forecast
+        arrives (engine end-to-end 33 → 15 M records/s with an idle resident wave)."""
         with self.lock:
-            self._build_wave()
+            self._stop_wave()
+            self._spec = None
+            self._served = []
+            if os.environ.get("OMLDM_FS_NOWAVE"):  # diagnostics: the lane without the wave
+                return
+            pipes = [self.job.pipes[pid] for pid in sorted(self.job.pipes)]
+            if not pipes or any(p.store is None for p in pipes):
+                return
+            biases = {bool(p.learner.rule.bias) for p in pipes}
+            if len(biases) != 1:
+                return
+            rows = [p.store_row for p in pipes]
+            lo, hi = min(rows), max(rows) + 1
+            self._spec = (lo, hi, biases.pop())
+            self._row0 = lo
+            self._served = [(p.id, p.store_row, p.learner.TASK == "classification")
+                            for p in pipes]
 
-    def _build_wave(self, sync: bool = True) -> None:
+    @property
+    def serving(self) -> bool:
+        """Records are answered by the wave (else they go to the batched path)."""
+        return self._spec is not None
+
+    def _ensure_wave(self):
+        """Under the lock: a live wave over the configured store rows (started on the
+        first record, restarted after its lifetime)."""
         from omldm_amd.ops.serving import PredictServer
 
+        srv = self._server
+        if srv is not None and srv.lib.omldm_serve_alive(srv.mb):
+            return srv
         self._stop_wave()
-        self._served = []
-        pipes = [self.job.pipes[pid] for pid in sorted(self.job.pipes)]
-        if not pipes or any(p.store is None for p in pipes):
-            return
-        biases = {bool(p.learner.rule.bias) for p in pipes}
-        if len(biases) != 1:
-            return
-        rows = [p.store_row for p in pipes]
-        lo, hi = min(rows), max(rows) + 1
+        lo, hi, bias = self._spec
         W = self.job.store.W[lo:hi]
-        if sync:  # a Create's weights copied into the store have landed
-            torch.cuda.synchronize(W.device)
-        srv = PredictServer(W, self.space.dn, self.space.dc, biases.pop(),
-                            cat_span=self.space.cat_span)
+        srv = PredictServer(W, self.space.dn, self.space.dc, bias, cat_span=self.space.cat_span)
         srv.start(lifetime_us=self.lifetime_us)
         self._server = srv
-        self._row0 = lo
-        self._served = [(p.id, p.store_row, p.learner.TASK == "classification") for p in pipes]
+        return srv
 
     def take_fallback(self) -> list:
         out = []
@@ -171,21 +191,18 @@ class ForecastServer:
         wave, or a pipeline it cannot score) — the caller keeps it for the tick."""
         t_in = time.perf_counter() if t_in is None else t_in
         with self.lock:
-            srv = self._server
-            if srv is None:
+            if self._spec is None:
                 return False
             if not self._parse(rec):
                 self.invalid += 1
                 return True
             cat = self._cat32.ctypes.data
-            if not srv.lib.omldm_serve_alive(srv.mb):  # lifetime over: a fresh wave
-                self._build_wave(sync=False)
-                srv = self._server
+            srv = self._ensure_wave()
             try:
                 out = srv.request_raw(self._num.data_ptr(), cat)
-            except TimeoutError:  # the wave's lifetime ended: a fresh one, same models
-                self._build_wave(sync=False)
-                out = self._server.request_raw(self._num.data_ptr(), cat)
+            except TimeoutError:  # the wave's lifetime ended under the request
+                self._stop_wave()
+                out = self._ensure_wave().request_raw(self._num.data_ptr(), cat)
             raw = RawRecords(np.frombuffer(rec, dtype=np.uint8),
                              np.zeros(1, dtype=np.int64), np.array([len(rec)], dtype=np.int64))
             for pid, row, cls in self._served:
@@ -220,17 +237,22 @@ class ForecastServer:
 
     def _run(self) -> None:
         last = 0.0
+        idle_marked = False
         while not self._stop.is_set():
-            # a cheap look at the end offsets first: a quiet topic is not polled
-            recs = self.consumer.poll(64) if self._pending() else []
+            quiet = time.perf_counter() - last
+            # right after traffic the topic is polled directly; a quiet topic is looked at
+            # through its end offsets first (cheap) and not polled
+            recs = self.consumer.poll(64) if (quiet < self.SPIN_S or self._pending()) else []
             if not recs:
-                self._done = dict(self.consumer.offsets)  # everything before is answered
-                quiet = time.perf_counter() - last
+                if not idle_marked:  # everything polled so far is answered
+                    self._done = dict(self.consumer.offsets)
+                    idle_marked = True
                 time.sleep(0 if quiet < self.SPIN_S else
                            (50e-6 if quiet < self.WARM_S else 1e-3))
                 continue
+            idle_marked = False
             last = time.perf_counter()
-            t_in = time.perf_counter()
+            t_in = last
             for i, rec in enumerate(recs):
                 if not self.serve_one(rec, t_in if i == 0 else None):
                     self.fallback.append(rec)

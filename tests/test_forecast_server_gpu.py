@@ -56,7 +56,7 @@ def test_wave_answers_every_record_like_the_batched_predict():
         br.produce("trainingData", r)
     for _ in range(4):
         job.tick()
-    assert job.fserver._server is not None  # both pipelines live in the model store
+    assert job.fserver.serving  # both pipelines live in the model store
     fc = synth_json_records(40, SP, start=70000, operation="forecasting")
     for r in fc:
         br.produce("forecastingData", r)
@@ -86,7 +86,7 @@ def test_dense_pipeline_sends_records_to_the_batched_path():
         br.produce("trainingData", r)
     for _ in range(3):
         job.tick()
-    assert job.fserver._server is None  # the NN is not in the model store
+    assert not job.fserver.serving  # the NN is not in the model store
     for r in synth_json_records(10, SP, start=50000, operation="forecasting"):
         br.produce("forecastingData", r)
     for _ in range(2):
@@ -96,5 +96,5 @@ def test_dense_pipeline_sends_records_to_the_batched_path():
     # deleting the dense pipeline brings the wave back
     br.produce("requests", json.dumps({"id": 2, "request": "Delete"}))
     job.tick()
-    assert job.fserver._server is not None
+    assert job.fserver.serving
     job.fserver.close()
