@@ -13,12 +13,18 @@ One step == one Synchronous round on every GPU, all inside the timed region:
   pinned host micro-batch on the raw binary wire (fp32 numerical features, 32-bit
   category TOKENS, int8 labels) ──pull-copy kernel on a CU-masked ingest lane (copy of
   batch k+1 overlaps the round on batch k)──► HBM
-  → linear_seq kernel (csrc/kernels/linear_seq.hip): per spoke one workgroup; producer
-    waves murmur3-hash the tokens and build each 64-row chunk's Gram matrix on the matrix
-    cores (fp32 MFMA for the dense block, bf16 MFMA for the categorical one-hot); the
-    scanner wave runs the exact PA-I recurrence; updates go to the spoke's replica
+  → passes 1-2 of the v2 round (csrc/kernels/linear_scan.hip) on their own CU-masked
+    stream as soon as the batch lands: murmur3 hashing of the tokens, then every 64-row
+    chunk's Gram G and cross Grams X1 / X2 over the whole GPU — overlapping the previous
+    round's scan (--prep-ahead)
+  → the scan: one workgroup per spoke; the scanner wave runs the exact PA-I recurrence
+    and folds each chunk's updates into the next two chunks' margins, seven helper waves
+    gather / scatter the spoke's replica (fields split between them, no fences)
   → replica average into the round accumulator → RCCL all-reduce over xGMI (N > 1)
   → apply: w = average, every replica ← w.
+Also reported (rank 0): the engine's per-record forecast latency (a JSON record produced
+into the forecasting topic → its Prediction, `engine_forecast_*`) and the engine's
+end-to-end JSON training rate (`engine_e2e_*`).
 Quality is reported next to the speed: holdout accuracy of the trained model and of the
 CPU reference-semantics learner (csrc/host/rawwire.cpp, P = 16·N sequential spokes) on
 exactly the same stream and example count.
