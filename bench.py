@@ -117,7 +117,7 @@ def engine_forecast_latency(n: int) -> dict:
     args += ["--batchSize", "8192", "--parallelism", "16", "--test", "false"]
     cfg = JobConfig.from_args(args)
     sp = FeatureSpace(cfg.numFeatures, 0, cfg.catFeatures, cfg.hashDim)
-    job = Job(cfg, Comm(), torch.device("cuda", torch.cuda.current_device()))
+    job = Job(cfg, Comm.local(), torch.device("cuda", torch.cuda.current_device()))
     br.produce("requests", json.dumps({"id": 1, "request": "Create",
                                        "learner": {"name": "SVM"},
                                        "trainingConfiguration": {"protocol": "Synchronous"}}))
@@ -179,7 +179,7 @@ def engine_e2e_rate(records: int, batch: int = 65536) -> dict:
                                           "--batchSize", str(batch), "--timeout", "1000",
                                           "--test", "false", "--jobName", "bench-e2e"])
         dev = torch.device("cuda", torch.cuda.current_device())
-        job = Job(cfg, Comm(), dev)
+        job = Job(cfg, Comm.local(), dev)
         while not job.pipes:
             job.tick()
         for _ in range(2):  # staging slots grow to the record size

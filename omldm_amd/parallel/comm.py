@@ -52,6 +52,16 @@ class CommStats:
 class Comm:
     """World communicator (one rank per GPU)."""
 
+    @classmethod
+    def local(cls) -> "Comm":
+        """A one-rank communicator even inside a multi-rank job (a rank-local engine,
+        e.g. a benchmark's side measurement): no collective ever leaves the process."""
+        c = cls.__new__(cls)
+        c.group, c.enabled, c.rank, c.world = None, False, 0, 1
+        c.stats, c.backend, c.fault, c.placement = CommStats(), "none", None, {}
+        c.ctrl_group = None
+        return c
+
     def __init__(self, group=None):
         self.group = group
         self.enabled = dist.is_available() and dist.is_initialized()
