@@ -306,7 +306,8 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
             # (possibly made ahead on another stream: batch.prep), one scan workgroup per
             # spoke
             sp = batch.prep
-            if not (isinstance(sp, ScanPrep) and sp.key == (batch.B, R, S, dim, bool(rule.bias))):
+            key = (batch.B, R, S, dim, bool(rule.bias))
+            if not (isinstance(sp, ScanPrep) and sp.key == key):
                 sp = linear_scan_prepare(batch, R, S, dim, bool(rule.bias))
             elif sp.event is not None:
                 torch.cuda.current_stream(w.device).wait_event(sp.event)

@@ -111,7 +111,8 @@ def _two_rank_job(tmp_path, field_aware, device, env=None):
         os.environ.update(env_before)
     assert rc == 0, logs
     js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
-    assert js["jobName"] == "two-rank" and js["metrics"]["ranks"] == 2 and js["parallelism"] == 2 * js["metrics"]["spokesPerRank"]
+    assert js["jobName"] == "two-rank" and js["metrics"]["ranks"] == 2
+    assert js["parallelism"] == 2 * js["metrics"]["spokesPerRank"]
     stats = {s["pipeline"]: s for s in js["statistics"]}
     assert sorted(stats) == [p[0] for p in PIPES] + [9]
     assert stats[9]["protocol"] == "Asynchronous" and stats[9]["fitted"] > 0
@@ -187,7 +188,8 @@ def _kill_restore(tmp_path, pipes, device, env=None):
     assert rc == 0, logs
     assert any("on 1 rank(s)" in m for m in logs), logs
     js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
-    assert js["jobName"] == "restore-all" and js["metrics"]["ranks"] == 1 and js["parallelism"] == 1 * js["metrics"]["spokesPerRank"]
+    assert js["jobName"] == "restore-all" and js["metrics"]["ranks"] == 1
+    assert js["parallelism"] == 1 * js["metrics"]["spokesPerRank"]
     stats = {s["pipeline"]: s for s in js["statistics"]}
     assert sorted(stats) == [p[0] for p in pipes]
     for pid, learner, proto, _, _ in pipes:
@@ -241,7 +243,8 @@ def test_two_rank_job_over_kafka_with_compressed_topics(tmp_path):
         rd = KafkaBroker(fk.addr)
         perf, _ = rd.consume("performance", 0, 0, 10)
         js = json.loads(perf[-1])
-        assert js["jobName"] == "kafka-two-rank" and js["metrics"]["ranks"] == 2 and js["parallelism"] == 2 * js["metrics"]["spokesPerRank"]
+        assert js["jobName"] == "kafka-two-rank" and js["metrics"]["ranks"] == 2
+        assert js["parallelism"] == 2 * js["metrics"]["spokesPerRank"]
         assert sorted(s["pipeline"] for s in js["statistics"]) == [1, 2, 3, 4]
         assert all(s["fitted"] > 0 for s in js["statistics"])
         preds = []
@@ -308,7 +311,8 @@ def _four_rank(tmp_path, device, env=None):
         os.environ.update(env_before)
     assert rc == 0, logs
     js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
-    assert js["metrics"]["ranks"] == 4 and js["parallelism"] == 4 * js["metrics"]["spokesPerRank"]
+    assert js["metrics"]["ranks"] == 4
+    assert js["parallelism"] == 4 * js["metrics"]["spokesPerRank"]
     stats = {s["pipeline"]: s for s in js["statistics"]}
     assert sorted(stats) == sorted(layouts)
     assert all(s["fitted"] > 0 and s["protocol"] == "Synchronous" for s in stats.values())
@@ -356,7 +360,8 @@ def test_restore_grows_from_one_rank_to_two(tmp_path):
         os.environ.update(env_before)
     assert rc == 0, logs
     js = json.loads(Consumer(br, "performance", all_partitions=True).poll(10)[-1])
-    assert js["jobName"] == "grow" and js["metrics"]["ranks"] == 2 and js["parallelism"] == 2 * js["metrics"]["spokesPerRank"]
+    assert js["jobName"] == "grow" and js["metrics"]["ranks"] == 2
+    assert js["parallelism"] == 2 * js["metrics"]["spokesPerRank"]
     # the restored consumer offsets: the second run trained only on what the first did
     # not consume (a fresh start would re-train on all ≈ 0.8 × 4000 rows)
     assert js["metrics"]["trainedExamples"] < 2900, js["metrics"]["trainedExamples"]
