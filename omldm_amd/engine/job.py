@@ -74,6 +74,13 @@ class Job:
         self.space = FeatureSpace(cfg.numFeatures, cfg.discreteFeatures, cfg.catFeatures,
                                   cfg.hashDim, field_aware=cfg.fieldAware)
         self.spokes = cfg.spokesPerDevice or max(1, cfg.parallelism // self.world)
+        # spoke-parallelism gate (FlinkSpoke.scala:69-71,145-156,345-348): the job records
+        # the largest spoke parallelism it has run at (kept in checkpoints); while it runs
+        # below it — restored onto fewer spokes — Create requests wait in request_buffer,
+        # and a restore at that parallelism or more creates them first thing
+        self.parallelism = self.spokes * self.world
+        self.spoke_parallelism = self.parallelism
+        self.request_buffer: list = []
         b = {k: broker_for(getattr(cfg, k + "Addr")) for k in
              ("trainingData", "forecastingData", "requests", "responses", "predictions",
               "performance")}
@@ -180,6 +187,10 @@ class Job:
             self._ctrl_pending = []
         else:
             msgs = []
+        gated = self.cfg.parallelismGate and self.parallelism < self.spoke_parallelism
+        if self.request_buffer and not gated:
+            msgs = self.request_buffer + list(msgs)
+            self.request_buffer = []
         queries = []
         moves = self.fserver is not None and any(
             Request.from_json(robj).request in ("Create", "Delete") for _, _, robj in msgs)
@@ -190,7 +201,12 @@ class Job:
             if dest not in (ALL, self.rank) and req.request != "Query":
                 continue
             if req.request == "Create":
-                if net not in self.pipes:
+                if gated:
+                    if len(self.request_buffer) < self.cfg.requestBufferSize:
+                        self.request_buffer.append((net, dest, robj))
+                    else:
+                        self._bad_request(req, "request buffer full")
+                elif net not in self.pipes:
                     try:
                         self.pipes[net] = Pipeline(req, self.space, self.comm, self.device,
                                                    self.spokes, self.cfg.parallelism,
@@ -520,7 +536,9 @@ class Job:
               "consumers": {k: {"offsets": v} for k, v in self.consumer_offsets().items()},
               "record_buffer": [r for b in self.record_buffer for r in RawView(*b)],
               "ticks": self.ticks,
-              "counters": dict(self.counters), "world": self.world}
+              "counters": dict(self.counters), "world": self.world,
+              "spoke_parallelism": self.spoke_parallelism,
+              "request_buffer": [list(m) for m in self.request_buffer]}
         if self.rank == 0:
             sd["pipeline_map"] = self.pmap.state_dict()
             sd["requests"] = self.req_in.state_dict()
@@ -567,6 +585,10 @@ class Job:
         self.record_buffer = [join_block(recs)] if recs else []
         self._buffered = len(recs)
         self.ticks = int(sd.get("ticks", 0))
+        # the gate's state is the same on every rank (every rank applies every Create);
+        # a restore onto more spokes raises the recorded parallelism (checkParallelism)
+        self.spoke_parallelism = max(self.parallelism, int(sd.get("spoke_parallelism", 0)))
+        self.request_buffer = [tuple(m) for m in sd.get("request_buffer", [])]
         if self.rank == 0 and "pipeline_map" in sd:
             self.pmap.load_state_dict(sd["pipeline_map"])
             self.req_in.load_state_dict(sd.get("requests", {}))

@@ -64,6 +64,9 @@ class JobConfig:
     fieldAware: bool = False              # compact uint16 field-aware categorical slots
     batchSize: int = 65536                # records per engine tick and rank
     spokesPerDevice: int = 0              # virtual spokes per rank (0: parallelism / world)
+    # Creates wait while the job runs below the spoke parallelism it has reached before
+    # (a restore onto fewer spokes); FlinkSpoke.scala:69-71,145-156,345-348
+    parallelismGate: bool = True
     device: str = "auto"                  # auto | cuda | cpu
     maxTicks: int = 0                     # 0: until terminated (tests use a bound)
     restore: bool = False                 # restore from the latest checkpoint in stateBackend

@@ -193,3 +193,36 @@ def test_shrink_restore_merges_buffers_holdout_and_counters(tmp_path):
     assert job2.counters["records"] == sum(sd["counters"]["records"] for sd in sds)
     job2.tick()  # the spilled holdout rows are trained on (not held out again)
     assert job2.pipes[1].learner.running_totals()["fitted"] >= int(sum(fit)) + spill
+
+
+def test_parallelism_gate_buffers_creates_until_the_job_grows_back(tmp_path):
+    """FlinkSpoke.scala:69-71,145-156,345-348: a job restored onto fewer spokes than it
+    ran at keeps new Create requests waiting (checkpointed); restored at that parallelism
+    or more it creates them first thing, and the recorded parallelism grows with it."""
+    name = uuid.uuid4().hex
+    ck = ["--checkpointing", "true", "--checkInterval", "0", "--stateBackend",
+          f"file://{tmp_path}"]
+    job, br, _ = make_job(ck + ["--spokesPerDevice", "8"], name=name)
+    create(br, 1, "PA")
+    job.tick()
+    assert job.spoke_parallelism == 8 and set(job.pipes) == {1}
+    job.checkpointer.save(job)
+    # restored on 4 spokes: pipeline 1 comes back, the new Create waits
+    job2, _, _ = make_job(ck + ["--restore", "true", "--spokesPerDevice", "4"], name=name)
+    assert job2.parallelism == 4 and job2.spoke_parallelism == 8
+    create(br, 2, "SVM")
+    job2.tick()
+    job2.tick()
+    assert set(job2.pipes) == {1} and [m[0] for m in job2.request_buffer] == [2]
+    job2.checkpointer.save(job2)
+    # restored on 16 spokes: the buffered Create is applied, the job records 16
+    job3, _, _ = make_job(ck + ["--restore", "true", "--spokesPerDevice", "16"], name=name)
+    assert job3.spoke_parallelism == 16 and len(job3.request_buffer) == 1
+    job3.tick()
+    assert set(job3.pipes) == {1, 2} and job3.request_buffer == []
+    # the gate can be switched off
+    job4, _, _ = make_job(ck + ["--restore", "true", "--spokesPerDevice", "2",
+                                "--parallelismGate", "false"], name=name)
+    create(br, 3, "PA")
+    job4.tick()
+    assert 3 in job4.pipes
