@@ -107,6 +107,8 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(device)
         wall = time.time() - t0
         stages = tracing.report()
+        fs = job.fserver
+        lane = {"served": fs.served, **fs.latency_percentiles()} if fs is not None else None
         job.run()  # idle timeout → final statistics
         if comm.rank == 0:
             print(json.dumps({
@@ -116,6 +118,7 @@ def main(argv=None) -> int:
                 "pipelines": a.pipelines, "batch": a.batch, "wall_s": round(wall, 3),
                 "spokes": job.spokes, "model_dtype": a.model_dtype,
                 "forecast_frac": a.forecast_frac, "predictions": job.counters["predictions"],
+                "forecast_lane": lane,
                 "generate_s": round(gen_s, 1), "stages_ms": stages,
                 "ticks_timed": stages.get("poll", {}).get("calls"),
                 "device": str(device)}), flush=True)
