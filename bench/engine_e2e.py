@@ -100,13 +100,20 @@ def main(argv=None) -> int:
         r0 = job.counters["records"]
         tracing.reset()
         t0 = time.time()
-        while job.counters["records"] + job.counters["invalid"] < a.records // comm.world:
+        # forecasting records on the per-record lane are not counted by the tick
+        want = (a.records - (n_fc if job.fserver is not None else 0)) // comm.world
+        stall = 0
+        while job.counters["records"] + job.counters["invalid"] < want and stall < 200:
+            seen = job.counters["records"] + job.counters["invalid"]
             job.tick()
+            stall = 0 if job.counters["records"] + job.counters["invalid"] > seen else stall + 1
         job.egress.flush()  # predictions are in their topic
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         wall = time.time() - t0
         stages = tracing.report()
+        if job.fserver is not None:  # the forecast lane finishes (not in the training wall)
+            job.fserver.catch_up(30.0)
         fs = job.fserver
         lane = {"served": fs.served, **fs.latency_percentiles()} if fs is not None else None
         job.run()  # idle timeout → final statistics
