@@ -217,12 +217,9 @@ class TickIngest:
             ev.record(cs)
             blk.staged = ev
             blk.event = ev  # the host slot may be rewritten once this copy is done
-            if blk.parsed is not None:
-                from omldm_amd.utils import tracing
-
-                with tracing.range("ingest_stage_wait"):
-                    ev.synchronize()  # (ingest thread) the tick gets host-side counts
-                blk.counts = blk.out[5].numpy().copy()
+            # the host-side counts are read by the tick (ops.ingest.parse_block) once the
+            # event is done: this thread goes on to the next block's copy at once
+            blk.counts = None
 
     def _parse(self, blk: TickBlock, cs) -> None:
         """JSON parse of the staged block into slot-persistent device outputs, plus the

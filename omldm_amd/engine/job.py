@@ -462,8 +462,9 @@ class Job:
             self._train(tb, spill)
         for q in queries:
             self._answer(q)
-        for pipe in self.pipes.values():
-            pipe.record_learning_curve()
+        with tracing.range("learning_curve"):
+            for pipe in self.pipes.values():
+                pipe.record_learning_curve()
         if isinstance(block, TickBlock) and block.n and self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
@@ -472,7 +473,9 @@ class Job:
             self.idle.activity(time.time())  # idle = time since the last active tick ended
         if term > 0:
             self._terminate()
-        if self.fserver is not None and not self.fserver.catch_up():
+        with tracing.range("catch_up"):
+            behind = self.fserver is not None and not self.fserver.catch_up()
+        if behind:
             print(f"[omldm] rank {self.rank}: forecast lane behind after 5 s", flush=True)
         if self.checkpointer is not None and ckpt > 0:
             self.egress.flush()  # outputs of the checkpointed ticks are in their topic

@@ -84,6 +84,8 @@ class Pipeline:
         # running statistics (reference Statistics / learning curve, FlinkHub.scala:95-156)
         self.learning_curve: list[tuple[float, int]] = []
         self._lc_last = (0.0, 0)
+        self._lc_host = None     # pinned copy of the running totals (GPU)
+        self._lc_pending = None  # its event: the point is taken at the next tick
         # mean buffer size (reference BufferingWrapper.getMeanBufferSize): the training
         # records a spoke holds when its round starts — rows of the round / local spokes
         self.spokes = max(1, int(spokes))
@@ -139,8 +141,31 @@ class Pipeline:
         return s
 
     def record_learning_curve(self) -> None:
-        tot = self.learner.running_totals()
-        loss, n = tot["loss_sum"], tot["fitted"]
+        """One learning-curve point per tick: (mean loss of the rows fitted since the last
+        point, rows fitted so far). On a GPU the running totals are copied to pinned
+        memory behind the tick's round and read at the next tick, so the tick never waits
+        for its own round (reading them at once was a host sync per tick)."""
+        cum = self.learner.cum
+        if cum.device.type != "cuda":
+            self._lc_point(cum.tolist())
+            return
+        self.flush_learning_curve()
+        if self._lc_host is None or self._lc_host.shape != cum.shape:
+            self._lc_host = torch.empty(cum.shape, dtype=cum.dtype, pin_memory=True)
+        self._lc_host.copy_(cum, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._lc_pending = ev
+
+    def flush_learning_curve(self) -> None:
+        """Takes the point of the last tick in (before the curve is read or saved)."""
+        ev, self._lc_pending = self._lc_pending, None
+        if ev is not None:
+            ev.synchronize()
+            self._lc_point(self._lc_host.tolist())
+
+    def _lc_point(self, c: list) -> None:
+        loss, n = c[0], int(c[1])
         dl, dn = loss - self._lc_last[0], n - self._lc_last[1]
         if dn > 0:
             self.learning_curve.append((dl / dn, n))
@@ -155,6 +180,7 @@ class Pipeline:
     # --------------------------------------------------------------- checkpoint
     def state_dict(self) -> dict:
         self.protocol.finalize()
+        self.flush_learning_curve()
         return {"request": self.request.to_obj(), "learner": self.learner.state_dict(),
                 "preprocessors": [p.state_dict() for p in self.preprocessors],
                 "protocol": self.protocol.state_dict(),

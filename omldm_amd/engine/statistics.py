@@ -190,6 +190,7 @@ def merge_hub_statistics(hub_stats: list[dict], fitted: int) -> dict:
 
 def pipeline_statistics(pipe, metrics: dict | None = None) -> Statistics:
     ps = pipe.protocol.stats
+    pipe.flush_learning_curve()
     lc = pipe.learning_curve
     fitted = int(metrics["dataFitted"]) if metrics else pipe.learner.running_totals()["fitted"]
     merged = merge_hub_statistics(pipe.protocol.hub_statistics(), fitted)

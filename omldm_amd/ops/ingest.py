@@ -164,6 +164,12 @@ class GpuJsonParser:
         cur = torch.cuda.current_stream(dev)
         if blk.parsed is not None:
             cur.wait_event(blk.staged)
+            if blk.counts is None:  # staged a tick ahead: normally done by now
+                from omldm_amd.utils import tracing
+
+                with tracing.range("ingest_counts_wait"):
+                    blk.staged.synchronize()
+                blk.counts = blk.out[5].numpy().copy()
             num, cat, y, op = (t[:n] for t in blk.parsed)
             return HashedBatch(num, cat, y, blk.raw(), space.cat_span), op, blk.counts.copy()
         num = torch.empty((n, space.dn), dtype=torch.float32, device=dev)
