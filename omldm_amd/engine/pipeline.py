@@ -193,5 +193,8 @@ class Pipeline:
             p.load_state_dict(s)
         self.protocol.load_state_dict(sd.get("protocol", {}))
         self.learning_curve = [tuple(x) for x in sd.get("learning_curve", [])]
+        # the next learning-curve point covers the ticks after the restore, not all history
+        tot = self.learner.running_totals()
+        self._lc_last = (float(tot["loss_sum"]), int(tot["fitted"]))
         if sd.get("buffer"):
             self._buf_sum, self._buf_rounds = float(sd["buffer"][0]), int(sd["buffer"][1])

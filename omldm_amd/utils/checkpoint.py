@@ -87,12 +87,18 @@ class Checkpointer:
         """Snapshot now (host copies), write in the background. At most one write per
         rank is in flight: a new snapshot first waits for the previous write."""
         d = os.path.join(self.root, f"ckpt-{self.n:06d}")
-        sd = job.state_dict()
+        # host copies taken HERE, on the tick's thread: live tensors (scaler statistics,
+        # the holdout ring, models) keep changing in place after this returns
+        sd = host_copy(job.state_dict())
         models = export_models(job) if (self.rank == 0 and self.export) else None
         meta = {"format": FORMAT, "version": VERSION, "index": self.n, "world": self.world,
                 "time": time.time(), "ticks": job.ticks, "pipelines": sorted(job.pipes),
                 "files": [f"rank-{r}.pt" for r in range(self.world)],
                 "models": "models.json" if models is not None else None}
+        # every rank saves at the same tick (rank 0's clock, carried in the tick flags):
+        # the marker names the attempt, so files a crashed earlier attempt left in this
+        # directory never complete the manifest
+        meta["attempt"] = f"{self.n}:{job.ticks}"
         self.wait()
         self._writer = threading.Thread(target=self._write, args=(d, sd, models, meta),
                                          name=f"omldm-ckpt-{self.n}", daemon=True)
@@ -104,17 +110,19 @@ class Checkpointer:
     def _write(self, d: str, sd: dict, models, meta: dict) -> None:
         try:
             os.makedirs(d, exist_ok=True)
+            done = os.path.join(d, f"rank-{self.rank}.done")
+            if os.path.exists(done):  # left by a crashed attempt at this index
+                os.remove(done)
             tmp = os.path.join(d, f".rank-{self.rank}.pt.tmp")
             torch.save(sd, tmp)
             os.replace(tmp, os.path.join(d, f"rank-{self.rank}.pt"))
-            with open(os.path.join(d, f"rank-{self.rank}.done"), "w") as f:
-                f.write("1")
+            _atomic_text(done, meta["attempt"])
             if self.rank != 0:
                 return
             if models is not None:
                 _atomic_json(os.path.join(d, "models.json"), models)
             t0 = time.time()
-            while not all(os.path.exists(os.path.join(d, f"rank-{r}.done"))
+            while not all(_read_text(os.path.join(d, f"rank-{r}.done")) == meta["attempt"]
                           for r in range(self.world)):
                 if time.time() - t0 > self.WAIT_S:
                     raise TimeoutError(f"checkpoint {d}: ranks did not finish their files")
@@ -189,6 +197,34 @@ def check_manifest(man: dict) -> int:
         if k not in man:
             raise ValueError(f"checkpoint manifest lacks {k!r}")
     return ver
+
+
+def host_copy(obj):
+    """Deep copy of a state tree with every tensor in fresh host memory."""
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().to("cpu", copy=True)
+    if isinstance(obj, dict):
+        return {k: host_copy(v) for k, v in obj.items()}
+    if isinstance(obj, list):
+        return [host_copy(v) for v in obj]
+    if isinstance(obj, tuple):
+        return tuple(host_copy(v) for v in obj)
+    return obj
+
+
+def _atomic_text(path: str, text: str) -> None:
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write(text)
+    os.replace(tmp, path)
+
+
+def _read_text(path: str) -> str | None:
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
 
 
 def _atomic_json(path: str, obj) -> None:
