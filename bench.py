@@ -279,7 +279,8 @@ def main(argv=None) -> int:
     # passes 1-2 of the next round (hash + chunk Grams, model-independent) run on their own
     # stream as soon as its batch has landed, overlapping the current round's scan
     prep_stream = None
-    if on_gpu and a.prep_ahead and L.scan_eligible(dev[0].batch):
+    v3 = on_gpu and L.scan3_eligible(dev[0].batch, R, learner.rule.bias)
+    if on_gpu and a.prep_ahead and (v3 or L.scan_eligible(dev[0].batch)):
         if a.lane == "split" and a.ingest_cus > 0:
             rawp = native.hip().omldm_stream_create_cumask_ex(a.ingest_cus, 1, a.cu_layout)
             assert rawp, "hipExtStreamCreateWithCUMask failed"
@@ -304,8 +305,12 @@ def main(argv=None) -> int:
         if after is not None:
             prep_stream.wait_event(after)
         b = dev[slot].batch
-        b.prep = L.linear_scan_prepare(b, R, S, space.dim, bool(learner.rule.bias), slot=slot,
-                                       stream=prep_stream)
+        if v3:  # passes 1-3 of the table scan (csrc/kernels/linear_scan3.hip)
+            b.prep = L.linear_scan3_prepare(b, R, S, space.dim, bool(learner.rule.bias),
+                                            learner.rule, slot=slot, stream=prep_stream)
+        else:
+            b.prep = L.linear_scan_prepare(b, R, S, space.dim, bool(learner.rule.bias),
+                                           slot=slot, stream=prep_stream)
 
     def prefetch(k: int):
         if a.ingest == "device":
@@ -474,6 +479,8 @@ def main(argv=None) -> int:
             "backend": comm.backend, "rccl_ranks": world if comm.backend == "nccl" else 0,
             "collective_us_per_step": None if coll_ms is None
                                       else round(float(el[1].item()) * 1e3 / a.steps, 2),
+            "round_kernel": ("linear_scan3 (v3 table scan)" if v3 else L.SEQ_KERNEL) if on_gpu
+                            else "cpu",
             "numa": comm.placement, "ingest_lane": a.lane if on_gpu else None,
             "device": torch.cuda.get_device_name(device) if on_gpu else "cpu",
         }

@@ -1,0 +1,1015 @@
+// Exact sequential online linear learners, v3 ("table scan"): every spoke keeps the
+// weights it re-reads during a round in an LDS slot table, so the per-spoke workgroup
+// issues no global atomics and a third of v2's global gathers; the round end sums the
+// spokes' updates from sorted occurrence lists over the whole GPU instead of averaging
+// dense replicas.
+//
+// Semantics as linear_scan.hip / linear_seq.hip (the reference's spoke,
+// omldm/operators/spoke/FlinkSpoke.scala:92-107, with the Synchronous PS averaging the
+// replicas): P spokes, spoke s fits rows [s·R, (s+1)·R) strictly one example at a time on
+// its own replica of w, the round's model is the replica average. For additive learners
+// the margin of row t of chunk k (64 rows) is
+//     m_t = x_t·w + Σ_{s<t in the round} c_s·(x_s·x_t)
+// and is split by distance:
+//   * s in chunk k:        the scanner's recurrence over G_k (strictly lower Gram);
+//   * s in chunk k − 1:    folded by the scanner while it scans chunk k − 1, through
+//                          X1_k = X_k X_{k−1}ᵀ;
+//   * s in chunks ≤ k − 2: the base margin the helper waves assemble before the chunk:
+//                          dense columns from their running dense weights, categorical
+//                          fields from the spoke's SLOT TABLE (LDS) for every slot that
+//                          recurs two or more chunks apart, else from w itself.
+// A slot that occurs only inside a window of two consecutive chunks never needs a table
+// entry: G and X1 carry all its in-round updates. On the bench stream that leaves ~17.7 K
+// table slots per 8192-row spoke (fits LDS), 580 global gathers per chunk (v2: 1664) and
+// no global atomics (v2: 1664 per chunk).
+//
+// The scanner keeps each row's affine candidate u = a·m + b instead of m (a = −1/(‖x‖² +
+// kadd), b = y/(‖x‖² + kadd) for the hinge rule): with the Grams pre-scaled by the row's a
+// (prep), one step of the recurrence is med3 → v_readlane → fma.
+//
+// Passes of a round (all but 3 model-independent; 1, 2, 4 can run ahead on another stream):
+//   1. s3_slots_kernel   tokens → field-aware signed slots, FIELD-MAJOR [dc][B] (or a
+//                        transpose of already hashed row-major slots)
+//   2. s3_dedupe_kernel  one workgroup per (spoke, field): the field's occurrences sorted
+//                        by (slot, row) in LDS (bitonic), per-slot first/last chunk, table
+//                        ids, per-occurrence flags and the rank among equal slots of its
+//                        chunk → meta [dc][B]; the sorted list + per-tile offsets for 5.
+//   3. s3_gram_kernel    one workgroup per (spoke, chunk): a_t, G_k and X1_k (categorical
+//                        match counts on the VALU, the dense block on the matrix cores),
+//                        scaled by a_t; the chunk's dense columns transposed for the helpers
+//   4. s3_scan_kernel    one workgroup per spoke: scanner wave + 7 helper waves
+//   5. s3_combine_kernel one workgroup per (field, 512-slot tile): Σ over spokes of the
+//                        occurrences' c·sign, from the sorted lists (segmented sums, fixed
+//                        order, no atomics) → the round accumulator, dense; plus the dense
+//                        columns, the intercept and the statistics.
+#include "common.h"
+#include "hash_dev.h"
+#include "seq_common.h"
+
+namespace omldm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace s3 {
+constexpr int CH = 64;                     // rows per chunk = scanner lanes
+constexpr int NH = 7;                      // helper waves
+constexpr int NT = 64 * (NH + 1);
+constexpr int GS = CH + 4;                 // LDS row stride of G / X1
+constexpr int MAXF = 32;                   // categorical fields per row
+constexpr int NF = (MAXF + NH - 1) / NH;   // fields per helper wave (5)
+constexpr int KNMAX = 32;                  // dense columns (numerical + intercept)
+constexpr int NJ = (KNMAX + NH - 1) / NH;  // dense columns per helper wave (5)
+constexpr int MAT = CH * CH;
+constexpr int RMAX = 8192;                 // rows per spoke (the dedupe sort lives in LDS)
+constexpr int DT = 1024;                   // dedupe threads
+constexpr int TILE = 512;                  // slots per combine tile
+constexpr int WS = 8;                      // per-spoke stat row
+constexpr int DS = KNMAX;                  // per-spoke dense delta row
+// meta word of one occurrence: flags | sign | rank among equal slots of its chunk | table id
+constexpr uint32_t F_TG = 1u;              // margin reads the table (else w)
+constexpr uint32_t F_INIT = 2u;            // first occurrence: writes w[slot] into the table
+constexpr uint32_t F_SCAT = 4u;            // the slot recurs ≥ 2 chunks later: add c·sign
+constexpr uint32_t F_SIGN = 8u;
+constexpr int RANK_SHIFT = 4;
+constexpr uint32_t RANK_MASK = 63u;
+constexpr int LID_SHIFT = 10;
+}  // namespace s3
+
+// floats of one chunk's prep block: aG | aX1 | a | dense columns transposed [KN][64]
+template <int KN>
+__host__ __device__ constexpr int s3_prep_floats() {
+  return 2 * s3::MAT + s3::CH + KN * s3::CH;
+}
+
+__device__ __forceinline__ void spoke_rows(int s, int R, int B, int& t0, int& t1) {
+  const long long a = (long long)s * R;
+  t0 = a > B ? B : (int)a;
+  t1 = (a + R) > B ? B : (int)(a + R);
+}
+
+// ------------------------------------------------------------------ pass 1: slots
+// 256 rows per block through an LDS tile: coalesced row-major reads, coalesced
+// field-major writes. hashed = 0: tokens (murmur3 per field); 1: already slots.
+__global__ __launch_bounds__(256) void s3_slots_kernel(const uint32_t* __restrict__ src, int B,
+                                                       int dc, int dn, uint32_t span, int hashed,
+                                                       int* __restrict__ slotsT) {
+  __shared__ int tile[256][s3::MAXF + 1];
+  const int r0 = blockIdx.x * 256, tid = threadIdx.x;
+  const int nr = min(256, B - r0);
+  for (int i = tid; i < nr * dc; i += 256) {
+    const int r = i / dc, f = i - r * dc;
+    const uint32_t v = src[(size_t)r0 * dc + i];
+    tile[r][f] = hashed ? (int)v : hash_token_dev(v, f, dn, span);
+  }
+  __syncthreads();
+  if (tid < nr)
+    for (int f = 0; f < dc; ++f) slotsT[(size_t)f * B + r0 + tid] = tile[tid][f];
+}
+
+// ------------------------------------------------------------------ pass 2: dedupe
+// Block-wide inclusive scans over DT threads (16 waves); every thread passes its
+// aggregate, gets the inclusive scan of the aggregates back.
+template <typename T, typename Op>
+__device__ __forceinline__ T block_scan_incl(T v, Op op, T ident, T* wtot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T t = __shfl_up(v, d);
+    if (lane >= d) v = op(v, t);
+  }
+  if (lane == 63) wtot[wave] = v;
+  __syncthreads();
+  if (wave == 0) {
+    T x = lane < s3::DT / 64 ? wtot[lane] : ident;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      const T t = __shfl_up(x, d);
+      if (lane >= d) x = op(x, t);
+    }
+    if (lane < s3::DT / 64) wtot[lane] = x;
+  }
+  __syncthreads();
+  if (wave > 0) v = op(v, wtot[wave - 1]);
+  __syncthreads();  // wtot reusable
+  return v;
+}
+
+struct MaxOp {
+  __device__ int operator()(int a, int b) const { return a > b ? a : b; }
+};
+struct AddOp {
+  __device__ int operator()(int a, int b) const { return a + b; }
+};
+
+__device__ __forceinline__ uint32_t key_slot(unsigned long long k) { return (uint32_t)(k >> 32); }
+__device__ __forceinline__ int key_row(unsigned long long k) { return (int)((uint32_t)k >> 1); }
+
+// Grid (dc, S_act), DT threads, dynamic LDS: npow keys (8 B) + npow ints.
+// Outputs: meta [dc][B] (uint32, see s3:: bits; 0 for absent), the field's sorted keys
+// lists [S][dc][Rcap], counts [S][dc], tile offsets [S][dc][ntiles + 1] (span > 0), and
+// table ids from the spoke's counter lidcount[s] (zeroed before the launch).
+__global__ __launch_bounds__(s3::DT) void s3_dedupe_kernel(
+    const int* __restrict__ slotsT, int B, int R, int dc, int dn, uint32_t span, int ntiles,
+    int Rcap, uint32_t* __restrict__ meta, unsigned long long* __restrict__ lists,
+    int* __restrict__ counts, int* __restrict__ tileoff, int* __restrict__ lidcount) {
+  extern __shared__ unsigned long long keys[];
+  __shared__ int wtot[16];
+  __shared__ int wtot2[16];
+  __shared__ int s_npres, s_base;
+  const int f = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  const int n = t1 - t0;
+  if (n <= 0) return;
+  int npow = s3::DT;
+  while (npow < n) npow <<= 1;
+  int* aux = reinterpret_cast<int*>(keys + npow);
+  const int* col = slotsT + (size_t)f * B + t0;
+  for (int i = tid; i < npow; i += s3::DT) {
+    unsigned long long k = ~0ull;
+    if (i < n) {
+      const int v = col[i];
+      if (v != -1)
+        k = ((unsigned long long)(uint32_t)(v & 0x7fffffff) << 32) | ((unsigned long long)i << 1) |
+            (v < 0 ? 1ull : 0ull);
+    }
+    keys[i] = k;
+  }
+  if (tid == 0) s_npres = 0;
+  __syncthreads();
+  // bitonic sort, ascending
+  for (int k = 2; k <= npow; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < npow; i += s3::DT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = keys[i], b = keys[ixj];
+          const bool up = (i & k) == 0;
+          if ((a > b) == up) {
+            keys[i] = b;
+            keys[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < npow; i += s3::DT)
+    if (keys[i] != ~0ull && (i + 1 == npow || keys[i + 1] == ~0ull)) s_npres = i + 1;
+  __syncthreads();
+  const int np = s_npres;
+  const int EPT = npow / s3::DT;  // consecutive elements per thread
+  const int e0 = tid * EPT;
+  // ---- scan 1: segment start (same slot) and group start (same slot and chunk)
+  int segs = 0, grps = 0;
+  int seg_in[8], grp_in[8];
+  for (int q = 0; q < EPT; ++q) {
+    const int i = e0 + q;
+    int hs = 0, hg = 0;
+    if (i < np) {
+      const unsigned long long ki = keys[i];
+      if (i == 0) {
+        hs = hg = 1;
+      } else {
+        const unsigned long long kp = keys[i - 1];
+        hs = key_slot(ki) != key_slot(kp);
+        hg = hs || ((key_row(ki) >> 6) != (key_row(kp) >> 6));
+      }
+    }
+    segs = hs ? i : segs;
+    grps = hg ? i : grps;
+    seg_in[q] = segs;
+    grp_in[q] = grps;
+  }
+  // thread aggregates: the last head position seen (0 if none: a head at 0 exists)
+  const int sagg = block_scan_incl(segs, MaxOp(), 0, wtot);
+  const int gagg = block_scan_incl(grps, MaxOp(), 0, wtot2);
+  // exclusive prefix of this thread: the inclusive aggregate of thread tid − 1
+  __shared__ int incl_s[s3::DT], incl_g[s3::DT];
+  incl_s[tid] = sagg;
+  incl_g[tid] = gagg;
+  __syncthreads();
+  const int xs = tid ? incl_s[tid - 1] : 0, xg = tid ? incl_g[tid - 1] : 0;
+  for (int q = 0; q < EPT; ++q) {
+    seg_in[q] = seg_in[q] > xs ? seg_in[q] : xs;
+    grp_in[q] = grp_in[q] > xg ? grp_in[q] : xg;
+  }
+  __syncthreads();
+  // ---- per segment: last row (written by the segment's tail into aux[segment start])
+  for (int q = 0; q < EPT; ++q) {
+    const int i = e0 + q;
+    if (i < np && (i + 1 == np || key_slot(keys[i + 1]) != key_slot(keys[i])))
+      aux[seg_in[q]] = key_row(keys[i]);
+  }
+  __syncthreads();
+  // ---- scan 2: table ids of the table segments (heads where last − first chunk ≥ 2)
+  int tcnt = 0;
+  int tab_in[8];
+  for (int q = 0; q < EPT; ++q) {
+    const int i = e0 + q;
+    int t = 0;
+    if (i < np && seg_in[q] == i) {
+      const int first = key_row(keys[i]), last = aux[i];
+      t = ((last >> 6) - (first >> 6)) >= 2;
+    }
+    tab_in[q] = t;
+    tcnt += t;
+  }
+  const int tincl = block_scan_incl(tcnt, AddOp(), 0, wtot);
+  incl_s[tid] = tincl;
+  __syncthreads();
+  const int texcl = tid ? incl_s[tid - 1] : 0;
+  if (tid == s3::DT - 1) s_base = atomicAdd(&lidcount[s], tincl);
+  __syncthreads();
+  const int base = s_base;
+  // lid of each table head → aux2 (reuse incl_g as it is no longer needed? no: npow-sized)
+  // heads keep their local table id in the upper part of keys' LDS: store it in aux as
+  // (last_row << 16) would not fit; use a second npow array carved from incl arrays when
+  // npow ≤ DT, else pack: aux[i] = last_row | (local_lid + 1) << 14 (last_row < 2^13)
+  {
+    int run = texcl;
+    for (int q = 0; q < EPT; ++q) {
+      const int i = e0 + q;
+      if (tab_in[q]) {
+        aux[i] = (aux[i] & 0x3fff) | ((run + 1) << 14);
+        ++run;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- per occurrence: flags, rank, table id → meta (row order)
+  for (int q = 0; q < EPT; ++q) {
+    const int i = e0 + q;
+    if (i >= np) continue;
+    const unsigned long long ki = keys[i];
+    const int row = key_row(ki);
+    const int hs = seg_in[q];
+    const int a = aux[hs];
+    const int first = key_row(keys[hs]), last = a & 0x3fff;
+    const int ch = row >> 6;
+    const int lloc = (a >> 14) - 1;  // −1: not a table slot
+    uint32_t m = (ki & 1ull) ? s3::F_SIGN : 0u;
+    if (lloc >= 0) {
+      if (ch > (first >> 6)) m |= s3::F_TG;
+      if (i == hs) m |= s3::F_INIT;
+      if ((last >> 6) >= ch + 2) m |= s3::F_SCAT;
+      m |= (uint32_t)(base + lloc) << s3::LID_SHIFT;
+    }
+    m |= (uint32_t)((i - grp_in[q]) & s3::RANK_MASK) << s3::RANK_SHIFT;
+    meta[(size_t)f * B + t0 + row] = m;
+  }
+  // absent occurrences: meta 0 (written for every row not present)
+  for (int i = tid; i < n; i += s3::DT)
+    if (col[i] == -1) meta[(size_t)f * B + t0 + i] = 0u;
+  // ---- the sorted list, its count and the per-tile offsets (combine input)
+  unsigned long long* L = lists + ((size_t)s * dc + f) * Rcap;
+  for (int i = tid; i < np; i += s3::DT) L[i] = keys[i];
+  if (tid == 0) counts[s * dc + f] = np;
+  if (span > 0 && tileoff != nullptr) {
+    int* T = tileoff + ((size_t)s * dc + f) * (ntiles + 1);
+    const uint32_t lo = (uint32_t)dn + (uint32_t)f * span;
+    auto tile_of = [&](int i) -> int {
+      return (int)((key_slot(keys[i]) - lo) / (uint32_t)s3::TILE);
+    };
+    for (int i = tid; i <= np; i += s3::DT) {
+      const int prev = i == 0 ? -1 : tile_of(i - 1);
+      const int cur = i == np ? ntiles : tile_of(i);
+      for (int j = prev + 1; j <= cur && j <= ntiles; ++j) T[j] = i;
+    }
+    if (np == 0)
+      for (int j = tid; j <= ntiles; j += s3::DT) T[j] = 0;
+  }
+}
+
+// ------------------------------------------------------------------ pass 3: Grams
+// grid (chunks, S_act), 256 threads. Row scale a_t: −1/(‖x‖² + kadd) for the affine rules
+// (hinge, ε-insensitive), 1 for logistic; 0 for rows past the shard. Out, per chunk:
+// aG (strictly lower) | aX1 | a | dense [KN][64] (numerical columns, then the intercept).
+template <int KN>
+__global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ slotsT, int dc,
+                                                      const float* __restrict__ num, int dn,
+                                                      int B, int R, int bias, int affine,
+                                                      float kadd, float* __restrict__ prep,
+                                                      int nchs) {
+  const int c = blockIdx.x, s = blockIdx.y;
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  if (t0 + c * s3::CH >= t1) return;
+  constexpr int PF = s3_prep_floats<KN>();
+  float* out = prep + ((size_t)s * nchs + c) * PF;
+  __shared__ alignas(16) int sl[2][s3::MAXF][s3::CH + 4];
+  __shared__ float xn[2][s3::CH][KN + 1];
+  __shared__ float sa[s3::CH];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 2 * dc * s3::CH; i += 256) {
+    const int d = i / (dc * s3::CH), rem = i - d * dc * s3::CH;
+    const int f = rem / s3::CH, r = rem - f * s3::CH;  // field-major: coalesced per field
+    const int cc = c - d, row = t0 + cc * s3::CH + r;
+    sl[d][f][r] = (cc >= 0 && row < t1) ? slotsT[(size_t)f * B + row] : -1;
+  }
+  for (int i = tid; i < 2 * s3::CH * KN; i += 256) {
+    const int d = i / (s3::CH * KN), rem = i - d * s3::CH * KN;
+    const int r = rem / KN, j = rem - r * KN;
+    const int cc = c - d, row = t0 + cc * s3::CH + r;
+    float x = 0.f;
+    if (cc >= 0 && row < t1) x = j < dn ? num[(size_t)row * dn + j] : ((bias && j == dn) ? 1.f : 0.f);
+    xn[d][r][j] = x;
+  }
+  __syncthreads();
+  if (tid < s3::CH) {
+    float n2 = 0.f;
+    for (int j = 0; j < KN; ++j) n2 = fmaf(xn[0][tid][j], xn[0][tid][j], n2);
+    for (int f = 0; f < dc; ++f) n2 += sl[0][f][tid] != -1 ? 1.f : 0.f;
+    const bool live = t0 + c * s3::CH + tid < t1;
+    float a = 0.f;
+    if (live) a = affine ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : 1.f;
+    sa[tid] = a;
+    out[2 * s3::MAT + tid] = a;
+  }
+  // dense columns transposed for the helper waves (coalesced per column)
+  for (int i = tid; i < KN * s3::CH; i += 256) {
+    const int j = i / s3::CH, r = i - j * s3::CH;
+    out[2 * s3::MAT + s3::CH + i] = xn[0][r][j];
+  }
+  __syncthreads();
+  const int bi = tid >> 4, bj = tid & 15;
+#pragma unroll 1
+  for (int d = 0; d < 2; ++d) {
+    float acc[4][4] = {};
+    if (c - d >= 0 && !(d == 0 && bj > bi)) {
+      int cnt[4][4] = {};
+      for (int f = 0; f < dc; ++f) {
+        const int4 a4 = *reinterpret_cast<const int4*>(&sl[0][f][4 * bi]);
+        const int4 b4 = *reinterpret_cast<const int4*>(&sl[d][f][4 * bj]);
+        const int av[4] = {a4.x, a4.y, a4.z, a4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int a = av[i] == -1 ? 0x7ffffffe : av[i];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int x = a ^ bv[j];
+            cnt[i][j] += (x & 0x7fffffff) ? 0 : (x < 0 ? -1 : 1);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (float)cnt[i][j];
+      for (int q = 0; q < KN; ++q) {
+        float xa[4], xb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          xa[i] = xn[0][4 * bi + i][q];
+          xb[i] = xn[d][4 * bj + i][q];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(xa[i], xb[j], acc[i][j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = 4 * bi + i;
+      const float a = sa[t];
+      float4 v = make_float4(a * acc[i][0], a * acc[i][1], a * acc[i][2], a * acc[i][3]);
+      if (d == 0) {  // strictly lower: column ≥ row → 0
+        if (4 * bj + 0 >= t) v.x = 0.f;
+        if (4 * bj + 1 >= t) v.y = 0.f;
+        if (4 * bj + 2 >= t) v.z = 0.f;
+        if (4 * bj + 3 >= t) v.w = 0.f;
+      }
+      *reinterpret_cast<float4*>(&out[d * s3::MAT + t * s3::CH + 4 * bj]) = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ pass 4: scan
+struct S3Smem {
+  alignas(16) float G[2][s3::CH][s3::GS];   // aG_k by chunk parity
+  alignas(16) float X1[2][s3::CH][s3::GS];  // aX1_{k+1} (read by the scanner in chunk k)
+  float part[2][s3::NH][s3::CH];            // base-margin partials per helper wave
+  float cb[2][s3::CH];                      // c of the chunk, by parity
+};
+// + dynamic LDS: the slot table, `cap` floats
+
+template <int RULE>
+struct S3Cand {
+  float lo, hi, d;
+  __device__ __forceinline__ float operator()(float u, const SeqParams& p, float y) const {
+    if constexpr (RULE == kSeqHinge) {
+      return __builtin_amdgcn_fmed3f(u, lo, hi);
+    } else if constexpr (RULE == kSeqEps) {
+      return __builtin_amdgcn_fmed3f(u, 0.f, hi) + __builtin_amdgcn_fmed3f(u + d, lo, 0.f);
+    } else {
+      return p.lr * y * __builtin_amdgcn_rcpf(1.f + __expf(y * u));
+    }
+  }
+};
+
+__device__ unsigned long long* g_s3_stamps;
+
+template <int RULE, int KN>
+__global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void s3_scan_kernel(
+    const int* __restrict__ slotsT, const uint32_t* __restrict__ meta, int dc, int dn,
+    const void* __restrict__ yv, int B, int R, const float* __restrict__ prep, int nchs,
+    const float* __restrict__ w, int dim, float* __restrict__ aglob, int cap, long long gstride,
+    float* __restrict__ cout, float* __restrict__ ws, float* __restrict__ wsd, SeqParams p) {
+  __shared__ S3Smem sm;
+  extern __shared__ float tab[];  // [cap]
+  constexpr int PF = s3_prep_floats<KN>();
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int s = blockIdx.x;
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  if (t0 >= t1) {
+    if (tid < s3::WS) ws[(size_t)s * s3::WS + tid] = 0.f;
+    if (tid < s3::DS) wsd[(size_t)s * s3::DS + tid] = 0.f;
+    return;
+  }
+  const int nch = (t1 - t0 + s3::CH - 1) / s3::CH;
+  const float* P0 = prep + (size_t)s * nchs * PF;
+  auto chunk_prep = [&](int k) { return P0 + (size_t)k * PF; };
+  float* ag = aglob + (size_t)s * gstride;
+
+  unsigned long long* stamps = g_s3_stamps;
+  unsigned long long st_acc[8] = {};
+  unsigned long long st_t = stamps ? clock64() : 0;
+  auto stamp = [&](int k) {
+    if (stamps) {
+      const unsigned long long now = clock64();
+      st_acc[k] += now - st_t;
+      st_t = now;
+    }
+  };
+
+  if (wave == 0) {
+    // ---------------------------------------------------------------- scanner
+    __builtin_amdgcn_s_setprio(3);
+    float loss = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f;
+    float f1 = 0.f;  // a·(X1_k · c_{k−1}) for this lane's row of chunk k
+    float ynx = load_y(yv, min(t0 + lane, t1 - 1), p.y8);
+    float anx = chunk_prep(0)[2 * s3::MAT + lane];
+    for (int k = -1; k <= nch; ++k) {
+      if (k >= 0 && k < nch) {
+        const int b = k & 1;
+        const int row = t0 + k * s3::CH + lane;
+        const bool valid = row < t1 && ynx == ynx;
+        const float y = valid ? ynx : 0.f;
+        const float a = valid ? anx : 0.f;
+        if (k + 1 < nch) {
+          ynx = load_y(yv, min(row + s3::CH, t1 - 1), p.y8);
+          anx = chunk_prep(k + 1)[2 * s3::MAT + lane];
+        }
+        float m0 = 0.f;
+#pragma unroll
+        for (int q = 0; q < s3::NH; ++q) m0 += sm.part[b][q][lane];
+        S3Cand<RULE> cf;
+        float u, bc = 0.f;
+        const float inv = -a;
+        if constexpr (RULE == kSeqHinge) {
+          bc = y * inv;
+          cf.lo = y < 0.f ? -p.cclip : 0.f;
+          cf.hi = y < 0.f ? 0.f : (y > 0.f ? p.cclip : 0.f);
+          u = fmaf(a, m0, bc) + f1;
+        } else if constexpr (RULE == kSeqEps) {
+          bc = (y - p.eps) * inv;
+          cf.d = 2.f * p.eps * inv;
+          cf.lo = valid ? -p.cclip : 0.f;
+          cf.hi = valid ? p.cclip : 0.f;
+          u = fmaf(a, m0, bc) + f1;
+        } else {
+          u = m0 + f1;
+        }
+        const float* grow = &sm.G[b][lane][0];
+        const float* xrow = &sm.X1[b ^ 1][lane][0];
+        float n1 = 0.f;
+#pragma unroll
+        for (int t4 = 0; t4 < s3::CH; t4 += 4) {
+          const float4 g4 = *reinterpret_cast<const float4*>(grow + t4);
+          const float4 x4 = *reinterpret_cast<const float4*>(xrow + t4);
+          const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, xx[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float ct = readlane_f(cf(u, p, y), t4 + q);
+            u = fmaf(ct, gg[q], u);     // aG strictly lower: lane t frozen after step t
+            n1 = fmaf(ct, xx[q], n1);   // → chunk k+1 (off the dependency chain)
+            // pin the fold beside its step: left to itself the compiler parks the 64 c's
+            // in SGPRs and runs the fold as a serial tail after the chunk
+            asm volatile("" : "+v"(u), "+v"(n1));
+          }
+        }
+        const float c = cf(u, p, y);
+        sm.cb[b][lane] = c;
+        if (row < t1) cout[row] = c;
+        if (valid) {
+          float m;
+          if constexpr (RULE == kSeqLogistic) m = u;
+          else m = inv > 0.f ? (bc - u) * __builtin_amdgcn_rcpf(inv) : 0.f;
+          seq_stats<RULE>(m, y, p, loss, mist, sqe);
+          nex += 1.f;
+        }
+        f1 = n1;
+      }
+      stamp(0);
+      __syncthreads();
+      stamp(1);
+    }
+    if (stamps && lane == 0)
+      for (int q = 0; q < 2; ++q) atomicAdd(&stamps[(size_t)s * 16 + q], st_acc[q]);
+    loss = wave_sum(loss);
+    nex = wave_sum(nex);
+    mist = wave_sum(mist);
+    sqe = wave_sum(sqe);
+    if (lane == 0) {
+      float* wr = ws + (size_t)s * s3::WS;
+      wr[0] = loss;
+      wr[1] = nex;
+      wr[2] = mist;
+      wr[3] = sqe;
+      wr[4] = 1.f;
+      wr[5] = 0.f;
+      wr[6] = 0.f;
+      wr[7] = 0.f;
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------- helpers
+  // wave q owns categorical fields f ≡ q and dense columns j ≡ q (mod NH); lane r = row
+  const int q = wave - 1, r = lane;
+  const int hl = tid - 64;
+  float wn[s3::NJ], w0[s3::NJ];  // running dense weights of this wave's columns, round start
+#pragma unroll
+  for (int i = 0; i < s3::NJ; ++i) {
+    const int j = q + s3::NH * i;
+    w0[i] = (j < KN) ? (j < dn ? w[j] : ((p.bias && j == dn) ? w[dim - 1] : 0.f)) : 0.f;
+    wn[i] = w0[i];
+  }
+  // occurrence words of this wave's fields, rotated one chunk per iteration:
+  // c0/c1 chunk k+1 (margins), p1 chunk k, p2 chunk k−1 (scatter)
+  int c0[s3::NF];
+  uint32_t c1[s3::NF], p1[s3::NF], p2[s3::NF];
+#pragma unroll
+  for (int i = 0; i < s3::NF; ++i) p1[i] = p2[i] = 0u;
+#pragma unroll
+  for (int i = 0; i < s3::NF; ++i) {  // chunk k + 1 of iteration k = −1
+    const int f = q + s3::NH * i;
+    const bool ok = f < dc && t0 + r < t1;
+    c0[i] = ok ? slotsT[(size_t)f * B + t0 + r] : -1;
+    c1[i] = ok ? meta[(size_t)f * B + t0 + r] : 0u;
+  }
+
+  for (int k = -1; k <= nch; ++k) {
+    const int cn = k + 1, ks = k - 1;
+    if (wave == 1) stamp(7);
+    // previous iteration's global stores (table overflow) and this iteration's words
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wave == 1) stamp(2);
+    // ---- issue: w gathers of chunk cn (slots first seen in its window), Gram staging
+    float g[s3::NF];
+#pragma unroll
+    for (int i = 0; i < s3::NF; ++i) {
+      const bool glob = c0[i] != -1 && !(c1[i] & s3::F_TG);
+      g[i] = glob ? w[c0[i] & 0x7fffffff] : 0.f;
+    }
+    constexpr int NV4 = (2 * s3::MAT / 4 + 64 * s3::NH - 1) / (64 * s3::NH);  // 5
+    f32x4 v[NV4];
+#pragma unroll
+    for (int u = 0; u < NV4; ++u) {
+      const int i = min(hl + 64 * s3::NH * u, 2 * s3::MAT / 4 - 1);
+      const int mtx = i >> 10, e = i & 1023;  // 0: aG_{cn}, 1: aX1_{cn+1}
+      const int kc = max(0, min(cn + mtx, nch - 1));
+      v[u] = reinterpret_cast<const f32x4*>(chunk_prep(kc) + mtx * s3::MAT)[e];
+    }
+    // dense columns of chunk ks (update) and chunk cn (margins)
+    float xs[s3::NJ], xc[s3::NJ];
+#pragma unroll
+    for (int i = 0; i < s3::NJ; ++i) {
+      const int j = q + s3::NH * i;
+      xs[i] = (j < KN && ks >= 0) ? chunk_prep(ks)[2 * s3::MAT + s3::CH + j * s3::CH + r] : 0.f;
+      xc[i] = (j < KN && cn < nch) ? chunk_prep(cn)[2 * s3::MAT + s3::CH + j * s3::CH + r] : 0.f;
+    }
+    if (wave == 1) stamp(3);
+    // ---- scatter chunk ks into the table (rank order: no two lanes on one entry per
+    // instruction, adds in row order) and its dense update
+    if (ks >= 0) {
+      const float cv = sm.cb[ks & 1][r];
+#pragma unroll
+      for (int i = 0; i < s3::NF; ++i) {
+        const uint32_t m = p2[i];
+        const bool sc = (m & s3::F_SCAT) != 0u;
+        if (__builtin_amdgcn_ballot_w64(sc) == 0ull) continue;
+        const int rank = sc ? (int)((m >> s3::RANK_SHIFT) & s3::RANK_MASK) : -1;
+        const int lid = (int)(m >> s3::LID_SHIFT);
+        const float val = (m & s3::F_SIGN) ? -cv : cv;
+        int mr = rank;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) mr = max(mr, __shfl_xor(mr, d));
+        for (int rk = 0; rk <= mr; ++rk) {
+          if (rank == rk && val != 0.f) {
+            if (lid < cap) tab[lid] += val;
+            else atomicAdd(&ag[lid - cap], val);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < s3::NJ; ++i) {
+        const int j = q + s3::NH * i;
+        if (j < KN) wn[i] += wave_sum(cv * xs[i]);
+      }
+    }
+    if (wave == 1) stamp(6);
+    // ---- base margins of chunk cn: table entries (chunks ≤ k − 1 applied), w, dense
+    if (cn < nch) {
+      float base = 0.f;
+#pragma unroll
+      for (int i = 0; i < s3::NJ; ++i) base = fmaf(xc[i], wn[i], base);
+#pragma unroll
+      for (int i = 0; i < s3::NF; ++i) {
+        if (c0[i] == -1) continue;
+        const uint32_t m = c1[i];
+        const int lid = (int)(m >> s3::LID_SHIFT);
+        float val = g[i];
+        if (m & s3::F_TG) {
+          val = lid < cap ? tab[lid] : __hip_atomic_load(&ag[lid - cap], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (m & s3::F_INIT) {
+          if (lid < cap) tab[lid] = val;
+          else __hip_atomic_store(&ag[lid - cap], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        base += (m & s3::F_SIGN) ? -val : val;
+      }
+      sm.part[cn & 1][q][r] = base;
+    }
+    if (wave == 1) stamp(4);
+    // ---- aG_{cn} → G[cn & 1], aX1_{cn+1} → X1[(cn+1) & 1]
+#pragma unroll
+    for (int u = 0; u < NV4; ++u) {
+      const int i = hl + 64 * s3::NH * u;
+      const int mtx = i >> 10, e = i & 1023;
+      if (i < 2 * s3::MAT / 4 && cn + mtx < nch) {
+        const int row = e >> 4, col = (e & 15) * 4;
+        float* dst = mtx == 0 ? &sm.G[cn & 1][row][col] : &sm.X1[(cn + 1) & 1][row][col];
+        *reinterpret_cast<f32x4*>(dst) = v[u];
+      }
+    }
+    // ---- rotate the occurrence words, prefetch chunk cn + 1's
+#pragma unroll
+    for (int i = 0; i < s3::NF; ++i) {
+      p2[i] = p1[i];
+      p1[i] = c1[i];
+      const int f = q + s3::NH * i;
+      const int row = t0 + (cn + 1) * s3::CH + r;
+      const bool ok = cn + 1 < nch && f < dc && row < t1;
+      c0[i] = ok ? slotsT[(size_t)f * B + row] : -1;
+      c1[i] = ok ? meta[(size_t)f * B + row] : 0u;
+    }
+    if (wave == 1) stamp(5);
+    __syncthreads();
+  }
+  if (stamps && lane == 0 && wave == 1)
+    for (int k = 2; k < 8; ++k) atomicAdd(&stamps[(size_t)s * 16 + k], st_acc[k]);
+  // round end: this wave's dense deltas
+#pragma unroll
+  for (int i = 0; i < s3::NJ; ++i) {
+    const int j = q + s3::NH * i;
+    if (lane == 0 && j < KN) wsd[(size_t)s * s3::DS + j] = wn[i] - w0[i];
+  }
+  if (q == 0 && lane >= KN && lane < s3::DS) wsd[(size_t)s * s3::DS + lane] = 0.f;
+}
+
+// ------------------------------------------------------------------ pass 5: combine
+// grid: block 0 the numerical columns, blocks 1 … dc·ntiles the tiles, the last block the
+// tail / intercept / scalars / statistics; 512 threads.
+// Tile (f, j) = slots [dn + f·span + j·TILE, …). Wave w sums spokes w, w + 8, … into its
+// own LDS row (segmented sums over the sorted occurrences, carried across batches, plain
+// read-add-write: a wave owns its row), the rows are added in wave order: the result does
+// not depend on timing.
+__global__ __launch_bounds__(512) void s3_combine_kernel(
+    const unsigned long long* __restrict__ lists, const int* __restrict__ tileoff,
+    const float* __restrict__ cout, const float* __restrict__ ws, const float* __restrict__ wsd,
+    int S_act, int R, int dc, int dn, uint32_t span, int ntiles, int Rcap, int dim, int bias,
+    int KN, float inv_p, int tile_lo, int tile_hi, float* __restrict__ dacc,
+    double* __restrict__ cum) {
+  __shared__ float acc[8][s3::TILE];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int blk = tile_lo + blockIdx.x;
+  if (blk >= tile_hi) return;
+  if (blk == 0) {  // numerical columns
+    for (int i = tid; i < dn; i += 512) {
+      float v = 0.f;
+      for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + i];
+      dacc[i] = v * inv_p;
+    }
+    return;
+  }
+  if (blk == dc * ntiles + 1) {
+    // the unused tail after the last field, the intercept, the accumulator's scalars, stats
+    for (int i = dn + dc * (int)span + tid; i < dim; i += 512) {
+      float v = 0.f;
+      if (i == dim - 1 && bias)
+        for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + dn];
+      dacc[i] = v * inv_p;
+    }
+    if (tid == 0) {
+      dacc[dim] = (float)S_act * inv_p;
+      dacc[dim + 1] = (float)S_act * inv_p;
+    }
+    if (cum && tid < 6 && tid != 4) {
+      double t = 0.0;
+      for (int s = 0; s < S_act; ++s) t += (double)ws[(size_t)s * s3::WS + tid];
+      cum[tid] += t;
+    }
+    return;
+  }
+  const int f = (blk - 1) / ntiles, j = (blk - 1) - f * ntiles;
+  const uint32_t flo = (uint32_t)dn + (uint32_t)f * span;
+  const uint32_t lo = flo + (uint32_t)j * s3::TILE;
+  const uint32_t hi = min(lo + (uint32_t)s3::TILE, flo + span);
+  for (int i = tid; i < 8 * s3::TILE; i += 512) (&acc[0][0])[i] = 0.f;
+  __syncthreads();
+  float* my = acc[wave];
+  for (int s = wave; s < S_act; s += 8) {
+    const int* T = tileoff + ((size_t)s * dc + f) * (ntiles + 1);
+    const int i0 = T[j], i1 = T[j + 1];
+    const unsigned long long* L = lists + ((size_t)s * dc + f) * Rcap;
+    const float* cs = cout + (size_t)s * R;
+    float carry = 0.f;
+    int cslot = -1;
+    for (int b0 = i0; b0 < i1; b0 += 64) {
+      const int i = b0 + lane;
+      const bool ok = i < i1;
+      const unsigned long long kk = ok ? L[i] : ~0ull;
+      const int slot = ok ? (int)key_slot(kk) : -2 - lane;  // distinct sentinels past the end
+      float v = ok ? cs[key_row(kk)] : 0.f;
+      if (kk & 1ull) v = -v;
+      // the previous batch's open segment continues into this one, or is flushed
+      if (lane == 0 && cslot >= 0) {
+        if (slot == cslot) v += carry;
+        else my[cslot - (int)lo] += carry;
+      }
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const float t = __shfl_up(v, d);
+        const int ts = __shfl_up(slot, d);
+        if (lane >= d && ts == slot) v += t;
+      }
+      const int nslot = __shfl_down(slot, 1);
+      const bool more = b0 + 64 < i1;
+      const bool tail = ok && (lane == 63 ? !more : nslot != slot);
+      if (tail) my[slot - (int)lo] += v;
+      // lane 63's segment stays open when the range goes on
+      cslot = more ? __shfl(slot, 63) : -1;
+      carry = more ? __shfl(v, 63) : 0.f;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = lo + tid; i < hi; i += 512) {
+    const int e = (int)(i - lo);
+    float t = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < 8; ++w2) t += acc[w2][e];
+    dacc[i] = t * inv_p;
+  }
+}
+
+template <int RULE, int KN>
+static int s3_launch_scan(const int* slotsT, const uint32_t* meta, int dc, int dn, const void* y,
+                          int B, int R, int S_act, const float* prep, int nchs, const float* w,
+                          int dim, float* aglob, int cap, long long gstride, float* cout, float* ws,
+                          float* wsd, const SeqParams& p, hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&s3_scan_kernel<RULE, KN>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024 - (int)sizeof(S3Smem));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((s3_scan_kernel<RULE, KN>), dim3(S_act), dim3(s3::NT),
+                     (size_t)cap * sizeof(float), st, slotsT, meta, dc, dn, y, B, R, prep, nchs, w,
+                     dim, aglob, cap, gstride, cout, ws, wsd, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace omldm
+
+using namespace omldm;
+
+// ------------------------------------------------------------------ host API
+namespace {
+int s3_sact(int B, int R, int S) {
+  const long long sact = ((long long)B + R - 1) / R;
+  return sact < S ? (int)sact : S;
+}
+int s3_kn(int dn, int bias) { return dn + (bias ? 1 : 0) <= 16 ? 16 : 32; }
+int s3_ntiles(uint32_t span) { return (int)((span + s3::TILE - 1) / s3::TILE); }
+int s3_rcap(int R) { return (R + 63) & ~63; }
+}  // namespace
+
+static int g_s3_cap_override = -1;  // tests: a small LDS table forces the global spill path
+
+// Max table entries the scan keeps in LDS.
+OMLDM_API int omldm_scan3_lds_cap() {
+  const int hw = (int)((160 * 1024 - sizeof(S3Smem)) / sizeof(float)) - 64;
+  return g_s3_cap_override >= 0 && g_s3_cap_override < hw ? g_s3_cap_override : hw;
+}
+
+OMLDM_API void omldm_scan3_set_cap(int cap) { g_s3_cap_override = cap; }
+
+// 1 when the v3 round handles this shape (field-aware slots, R ≤ RMAX).
+OMLDM_API int omldm_scan3_fits(int dn, int dc, int R, int bias) {
+  return dc > 0 && dc <= s3::MAXF && dn >= 0 && dn + (bias ? 1 : 0) <= s3::KNMAX && R > 0 &&
+         R <= s3::RMAX;
+}
+
+// Workspace sizes (in 4-byte words unless stated) for one round of S spokes × R rows,
+// B rows in all, dc fields, span slots per field.
+//   0 slotsT  [dc·B] int      1 meta   [dc·B] uint32     2 lists [S·dc·Rcap] uint64 (×2 words)
+//   3 counts  [S·dc]          4 tileoff [S·dc·(ntiles+1)] 5 lidcount [S]
+//   6 prep    [S·nchs·PF]     7 cout  [B]                 8 ws [S·WS]   9 wsd [S·DS]
+//  10 aglob   [S·gstride]
+OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn, int dc,
+                                         long long span, int bias) {
+  const long long nchs = (R + s3::CH - 1) / s3::CH;
+  const int kn = s3_kn(dn, bias);
+  const long long pf = kn == 16 ? s3_prep_floats<16>() : s3_prep_floats<32>();
+  const long long rcap = s3_rcap(R);
+  switch (which) {
+    case 0: case 1: return (long long)dc * B;
+    case 2: return 2LL * S * dc * rcap;
+    case 3: return (long long)S * dc;
+    case 4: return (long long)S * dc * (s3_ntiles((uint32_t)span) + 1);
+    case 5: return S;
+    case 6: return (long long)S * nchs * pf;
+    case 7: return B;
+    case 8: return (long long)S * s3::WS;
+    case 9: return (long long)S * s3::DS;
+    case 10: return (long long)S * ((long long)R * dc / 2 + 64);
+  }
+  return 0;
+}
+
+struct S3Ws {
+  int* slotsT;
+  uint32_t* meta;
+  unsigned long long* lists;
+  int* counts;
+  int* tileoff;
+  int* lidcount;
+  float* prep;
+  float* cout;
+  float* ws;
+  float* wsd;
+  float* aglob;
+};
+
+// Passes 1-3 (model-independent): slots, dedupe, Grams. `src` is the tokens (hashed = 0)
+// or row-major field-aware slots (hashed = 1). `ptrs` = the 11 workspaces above.
+OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int hashed, int dc,
+                                  int B, int R, int S, int dim, int bias, int rule, int variant,
+                                  float C, void* const* ptrs, void* stream) {
+  if (S <= 0 || B <= 0) return 0;
+  if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
+  if ((long long)(dim - dn - 1) / dc < 1) return -2;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t span = (uint32_t)((dim - dn - 1) / dc);
+  const S3Ws W{(int*)ptrs[0], (uint32_t*)ptrs[1], (unsigned long long*)ptrs[2], (int*)ptrs[3],
+               (int*)ptrs[4], (int*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7], (float*)ptrs[8],
+               (float*)ptrs[9], (float*)ptrs[10]};
+  const int S_act = s3_sact(B, R, S);
+  hipLaunchKernelGGL(s3_slots_kernel, dim3((B + 255) / 256), dim3(256), 0, st,
+                     (const uint32_t*)src, B, dc, dn, span, hashed, W.slotsT);
+  hipMemsetAsync(W.lidcount, 0, sizeof(int) * S, st);
+  int npow = s3::DT;
+  while (npow < R) npow <<= 1;
+  const size_t dl = (size_t)npow * (8 + 4);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&s3_dedupe_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(s3_dedupe_kernel, dim3(dc, S_act), dim3(s3::DT), dl, st, W.slotsT, B, R,
+                     dc, dn, span, s3_ntiles(span), s3_rcap(R), W.meta, W.lists, W.counts,
+                     W.tileoff, W.lidcount);
+  const int nchs = (R + s3::CH - 1) / s3::CH;
+  const int affine = rule != kSeqLogistic;
+  const float kadd = (rule != kSeqLogistic && variant == 2) ? 0.5f / C : 0.f;
+  if (s3_kn(dn, bias) == 16)
+    hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
+                       num, dn, B, R, bias, affine, kadd, W.prep, nchs);
+  else
+    hipLaunchKernelGGL(s3_gram_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
+                       num, dn, B, R, bias, affine, kadd, W.prep, nchs);
+  return (int)hipGetLastError();
+}
+
+// Pass 4 (the scan) + pass 5 (the combine into dacc) on a prepared round. The combine runs
+// as `parts` launches over disjoint tile ranges: part k completes dacc over a key range
+// (omldm_scan3_part_bounds) so its collective can start while the next part sums.
+OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int y8, int B, int R,
+                              int S, float* dacc, int dim, double* cum, int rule, int variant,
+                              float C, float eps, float lr, float inv_p, int bias,
+                              void* const* ptrs, int part, int parts, void* stream) {
+  if (S <= 0 || B <= 0) return 0;
+  if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t span = (uint32_t)((dim - dn - 1) / dc);
+  const S3Ws W{(int*)ptrs[0], (uint32_t*)ptrs[1], (unsigned long long*)ptrs[2], (int*)ptrs[3],
+               (int*)ptrs[4], (int*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7], (float*)ptrs[8],
+               (float*)ptrs[9], (float*)ptrs[10]};
+  const int S_act = s3_sact(B, R, S);
+  const int nchs = (R + s3::CH - 1) / s3::CH;
+  const int kn = s3_kn(dn, bias);
+  if (part == 0) {
+    const SeqParams p{rule, variant, variant == 1 ? C : INFINITY, variant == 2 ? 0.5f / C : 0.f,
+                      eps, lr, inv_p, bias, y8, span};
+    const int cap = omldm_scan3_lds_cap();
+    const long long gstride = (long long)R * dc / 2 + 64;
+    int e;
+    if (kn == 16) {
+      e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
+        : rule == kSeqEps ? s3_launch_scan<kSeqEps, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
+        : s3_launch_scan<kSeqLogistic, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st);
+    } else {
+      e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
+        : rule == kSeqEps ? s3_launch_scan<kSeqEps, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
+        : s3_launch_scan<kSeqLogistic, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st);
+    }
+    if (e) return e;
+  }
+  const int ntiles = s3_ntiles(span);
+  const int nblk = dc * ntiles + 2;
+  const int lo = (int)((long long)nblk * part / parts), hi = (int)((long long)nblk * (part + 1) / parts);
+  if (hi > lo)
+    hipLaunchKernelGGL(s3_combine_kernel, dim3(hi - lo), dim3(512), 0, st, W.lists, W.tileoff,
+                       W.cout, W.ws, W.wsd, S_act, R, dc, dn, span, ntiles, s3_rcap(R), dim, bias,
+                       kn, inv_p, lo, hi, dacc, cum);
+  return (int)hipGetLastError();
+}
+
+// [lo, hi) of dacc that combine part `part` of `parts` completes (the last part also the
+// numerical columns, the tail, the intercept and dacc[dim], dacc[dim + 1]).
+OMLDM_API int omldm_scan3_part_bounds(int dim, int dn, int dc, int part, int parts,
+                                      long long* lohi) {
+  const uint32_t span = (uint32_t)((dim - dn - 1) / dc);
+  const int ntiles = s3_ntiles(span);
+  const int nblk = dc * ntiles + 2;
+  const int lo = (int)((long long)nblk * part / parts), hi = (int)((long long)nblk * (part + 1) / parts);
+  auto start = [&](int blk) -> long long {  // first dacc index block blk writes
+    if (blk <= 0) return 0;
+    if (blk > dc * ntiles) return (long long)dn + (long long)dc * span;
+    const int f = (blk - 1) / ntiles, j = (blk - 1) - f * ntiles;
+    return (long long)dn + (long long)f * span + (long long)j * s3::TILE;
+  };
+  lohi[0] = start(lo);
+  lohi[1] = hi >= nblk ? (long long)dim + 2 : start(hi);
+  return 0;
+}
+
+OMLDM_API int omldm_scan3_stamps(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s3_stamps), &buf, sizeof(buf));
+}

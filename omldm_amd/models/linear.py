@@ -123,30 +123,36 @@ class LinearLearner(Learner):
         rb = RawBatch(batch.num.float().contiguous(), wide.cat.contiguous(),
                       batch.y.float().contiguous())
         R, S = self._seq_geometry(rb.B, ctx)
+        if L.scan3_eligible(rb, R, self.rule.bias):
+            return self._fit_raw(rb, ctx, hashed=True)
         rb.prep = L.linear_scan_prepare_slots(rb, R, S, self.dim, bool(self.rule.bias))
         self._fit_raw(rb, ctx)
 
-    def _fit_raw(self, batch: RawBatch, ctx: RoundContext) -> None:
+    def _fit_raw(self, batch: RawBatch, ctx: RoundContext, hashed: bool = False) -> None:
         B = batch.B
         R, S = self._seq_geometry(B, ctx)
         on_gpu = self.w.is_cuda
-        if on_gpu:
+        # v3 (the table scan) keeps no dense replicas: its round end sums the spokes'
+        # updates from the sorted occurrence lists; v1 / v2 average [S, dim] replicas
+        use_rep = on_gpu and not (B and L.scan3_eligible(batch, R, self.rule.bias))
+        if use_rep:
             if self.replicas is None or self.replicas.shape[0] < S:
                 self.replicas = torch.empty((S, self.dim), dtype=torch.float32, device=self.device)
                 self._rep_valid = False
             if not self._rep_valid:
                 L.linear_seq_broadcast(self.w, self.replicas)
                 self._rep_valid = True
+        parts = max(1, int(ctx.reduce_parts)) if ctx.on_reduce_part is not None else 1
         if B:
             L.linear_seq_round(self.w, batch, R, S, self.dacc, self.rule, ctx.inv_p,
-                               cum=self.cum, replicas=self.replicas if on_gpu else None)
+                               cum=self.cum, replicas=self.replicas if use_rep else None,
+                               parts=parts, on_part=ctx.on_reduce_part, hashed=hashed)
         else:
             self.dacc[self.dim:].zero_()
-        self._seq_pending = on_gpu
-        if ctx.on_reduce_part is not None:
-            parts = max(1, int(ctx.reduce_parts))
-            for k in range(parts):
-                ctx.on_reduce_part(k, *L.part_bounds(self.dim, k, parts, self.dacc.is_cuda))
+            if ctx.on_reduce_part is not None:  # still join every collective of the round
+                for k in range(parts):
+                    ctx.on_reduce_part(k, *L.part_bounds(self.dim, k, parts, self.dacc.is_cuda))
+        self._seq_pending = use_rep
         if not ctx.fused_delta:
             self.apply_delta()
 

@@ -208,9 +208,11 @@ def linear_predict(w: torch.Tensor, batch: HashedBatch, wscale: torch.Tensor | N
 SEQ_RULES = (RULE_HINGE, RULE_EPS, RULE_LOGISTIC)
 
 
-# GPU kernel of the exact sequential round: "scan" (linear_scan.hip, default) or "seq"
-# (linear_seq.hip: every spoke builds its own chunk Grams) — an A/B knob
-SEQ_KERNEL = os.environ.get("OMLDM_SEQ_KERNEL", "scan")
+# GPU kernel of the exact sequential round: "scan3" (linear_scan3.hip, default: LDS slot
+# table per spoke, whole-GPU combine), "scan" (linear_scan.hip, v2: dense replicas) or
+# "seq" (linear_seq.hip: every spoke builds its own chunk Grams) — an A/B knob; v3 falls
+# back to v2 / v1 for shapes it does not take (> 8192 rows per spoke, > 32 fields)
+SEQ_KERNEL = os.environ.get("OMLDM_SEQ_KERNEL", "scan3")
 
 
 @dataclass
@@ -273,10 +275,107 @@ def linear_scan_prepare_slots(batch: RawBatch, R: int, S: int, dim: int, bias: b
     return ScanPrep(batch.tok, prep, (batch.B, R, S, dim, bool(bias)), None)
 
 
+# ------------------------------------------------------------------ v3: the table scan
+S3_BUFS = ("slotsT", "meta", "lists", "counts", "tileoff", "lidcount", "prep", "cout", "ws",
+           "wsd", "aglob")
+_S3_SHARED = (7, 8, 9, 10)  # run-time buffers (scan → combine, same stream): one set per device
+
+
+@dataclass
+class Scan3Prep:
+    """Passes 1-3 of a v3 round (field-major slots, per-(spoke, field) dedupe with the
+    sorted occurrence lists, scaled chunk Grams) — model-independent, made ahead on
+    another stream while the previous round scans. ``ptrs`` = the 11 workspaces."""
+
+    bufs: list
+    ptrs: object
+    key: tuple          # (B, R, S, dim, bias, rule, variant, C, dn, dc) it was made for
+    event: object = None
+
+
+def scan3_fits(dn: int, dc: int, R: int, bias: bool) -> bool:
+    return bool(native.hip().omldm_scan3_fits(int(dn), int(dc), int(R), int(bias)))
+
+
+def scan3_eligible(batch: RawBatch, R: int, bias: bool) -> bool:
+    return (SEQ_KERNEL == "scan3" and batch.y.is_cuda and 0 < batch.dc
+            and scan3_fits(batch.dn, batch.dc, R, bias))
+
+
+def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
+    return (batch.B, R, S, dim, bool(bias), rule.rule, rule.variant, float(rule.C), batch.dn,
+            batch.dc)
+
+
+def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
+                         rule: "LinearRule", slot: int = 0, stream=None,
+                         hashed: bool = False) -> Scan3Prep:
+    """Passes 1-3 of a v3 round into workspace set ``slot`` on ``stream`` (default: the
+    current stream; an event marks completion when a stream is given). ``batch.tok``:
+    32-bit category tokens, or (``hashed``) int32 field-aware signed slots, row-major."""
+    h = native.hip()
+    dev = batch.y.device
+    span = (dim - batch.dn - 1) // batch.dc
+    bufs = []
+    for i, name in enumerate(S3_BUFS):
+        n = int(h.omldm_scan3_ws_words(i, batch.B, R, S, batch.dn, batch.dc, span, int(bias)))
+        key = f"s3_{name}" if i in _S3_SHARED else f"s3_{name}{slot}"
+        bufs.append(_workspace(dev, n, key=key))
+    import ctypes
+
+    ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    check(h.omldm_scan3_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), int(hashed), batch.dc,
+                                batch.B, R, S, dim, int(bias), rule.rule, rule.variant,
+                                float(rule.C), ptrs, st.cuda_stream), "omldm_scan3_prepare")
+    ev = None
+    if stream is not None:
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    return Scan3Prep(bufs, ptrs, _s3_key(batch, R, S, dim, bias, rule), ev)
+
+
+def scan3_part_bounds(dim: int, dn: int, dc: int, part: int, parts: int) -> tuple[int, int]:
+    import ctypes
+
+    lh = (ctypes.c_longlong * 2)()
+    check(native.hip().omldm_scan3_part_bounds(dim, dn, dc, part, parts, lh),
+          "omldm_scan3_part_bounds")
+    return int(lh[0]), int(lh[1])
+
+
+def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
+                       rule: "LinearRule", inv_p: float, cum: torch.Tensor | None = None,
+                       parts: int = 1, on_part=None, hashed: bool = False) -> None:
+    """One Synchronous round through the v3 table scan (csrc/kernels/linear_scan3.hip):
+    dacc[:dim] = inv_p·Σ_spokes Δ_s (written whole), dacc[dim] = dacc[dim+1] =
+    S_act·inv_p, so ``linear_apply`` averages the spokes' replicas into w. The combine
+    runs in ``parts`` launches over key ranges; ``on_part(k, lo, hi)`` is called after
+    part k with the slice of dacc it completed (its collective may start then)."""
+    dim = int(dacc.shape[0]) - 2
+    num, y = batch.num, batch.y
+    sp = batch.prep
+    key = _s3_key(batch, R, S, dim, rule.bias, rule)
+    if not (isinstance(sp, Scan3Prep) and sp.key == key):
+        sp = linear_scan3_prepare(batch, R, S, dim, bool(rule.bias), rule, hashed=hashed)
+    elif sp.event is not None:
+        torch.cuda.current_stream(w.device).wait_event(sp.event)
+    h = native.hip()
+    parts = max(1, int(parts))
+    for k in range(parts):
+        rc = h.omldm_scan3_run(ptr(w), num.shape[1], batch.dc, ptr(y), int(y.dtype == torch.int8),
+                               batch.B, R, S, ptr(dacc), dim, ptr(cum), rule.rule, rule.variant,
+                               rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), sp.ptrs, k, parts,
+                               native.stream_of(w))
+        check(rc, "omldm_scan3_run")
+        if on_part is not None:
+            on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts))
+
+
 def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
                      rule: LinearRule, inv_p: float, cum: torch.Tensor | None = None,
-                     stats: torch.Tensor | None = None, replicas: torch.Tensor | None = None
-                     ) -> None:
+                     stats: torch.Tensor | None = None, replicas: torch.Tensor | None = None,
+                     parts: int = 1, on_part=None, hashed: bool = False) -> bool:
     """One Synchronous round on the raw binary wire: S spokes, spoke s an exact
     sequential learner (the reference's per-example fit, FlinkSpoke.scala:92-107) over
     rows [s·R, (s+1)·R) on its own replica of w; tokens are hashed inside the round.
@@ -295,7 +394,19 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
     assert num.is_contiguous() and tok.is_contiguous() and y.is_contiguous()
     assert cum is None or cum.dtype == torch.float64
     if S <= 0 or batch.B == 0:
-        return
+        return False
+    if w.is_cuda and scan3_eligible(batch, R, rule.bias) and stats is None:
+        assert all(t.is_cuda for t in (num, tok, y)) and dacc.is_cuda
+        linear_scan3_round(w, batch, R, S, dacc, rule, inv_p, cum, parts, on_part, hashed)
+        return True
+    if on_part is not None:  # the other paths complete dacc in one go
+        def _report():
+            for k in range(max(1, int(parts))):
+                on_part(k, *part_bounds(int(dacc.shape[0]) - 2, k, max(1, int(parts)),
+                                        cuda=dacc.is_cuda))
+    else:
+        def _report():
+            pass
     if w.is_cuda:
         assert all(t.is_cuda for t in (num, tok, y)) and dacc.is_cuda
         ws = _workspace(w.device, S * WS_STAT, key="seq_ws")
@@ -326,6 +437,7 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
             check(rc, "omldm_linear_seq_round")
         if stats is not None:
             stats.copy_(ws[: S * WS_STAT].view(S, WS_STAT)[:, :STAT_W])
+        _report()
     else:
         st = stats if stats is not None else torch.zeros((S, STAT_W), dtype=torch.float32)
         native.host().omldm_cpu_linear_seq_round(
@@ -335,6 +447,8 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
         if cum is not None:
             cum[:STAT_W] += st.sum(0).double()
             cum[4] -= st[:, 4].sum().double()
+        _report()
+    return False
 
 
 def linear_seq_apply(w: torch.Tensor, replicas: torch.Tensor, dacc: torch.Tensor) -> None:

@@ -66,6 +66,16 @@ HIP_SIGS = [
     ("omldm_linear_scan_run", i32, [vp, vp, i32, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp,
                                     vp, i32, i32, f32, f32, f32, f32, i32, vp, vp, vp]),
     ("omldm_linear_seq_reduce", i32, [vp, vp, i32, i32, vp, f32, vp, vp, vp]),
+    ("omldm_scan3_lds_cap", i32, []),
+    ("omldm_scan3_set_cap", None, [i32]),
+    ("omldm_scan3_fits", i32, [i32, i32, i32, i32]),
+    ("omldm_scan3_ws_words", i64, [i32, i32, i32, i32, i32, i32, i64, i32]),
+    ("omldm_scan3_prepare", i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, f32,
+                                  vp, vp]),
+    ("omldm_scan3_run", i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, f32,
+                              f32, f32, f32, i32, vp, i32, i32, vp]),
+    ("omldm_scan3_part_bounds", i32, [i32, i32, i32, i32, i32, vp]),
+    ("omldm_scan3_stamps", i32, [vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
     ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),

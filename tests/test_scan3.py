@@ -1,0 +1,282 @@
+"""The v3 exact sequential round (csrc/kernels/linear_scan3.hip: per-spoke LDS slot table,
+whole-GPU combine) against the CPU oracle (csrc/host/rawwire.cpp) — and, on the CPU, a
+NumPy model of its schedule (which occurrences read the table, which write it, when) against
+the exact per-example spoke.
+
+Reference semantics pinned: each spoke fits its shard strictly one example at a time on its
+own replica (omldm/operators/spoke/FlinkSpoke.scala:92-107), the Synchronous PS averages the
+replicas.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+from omldm_amd.api.batch import FeatureSpace, RawBatch
+from omldm_amd.io.synthetic import synth_raw
+from omldm_amd.ops import linear as L
+from omldm_amd.ops import native
+from omldm_amd.ops.ingest import hash_raw
+from tests.test_rawwire import _blocked_gram_scan
+
+gpu = pytest.mark.gpu
+CH = 64
+
+
+def _cuda():
+    return torch.device("cuda", 0)
+
+
+def _occurrence_flags(cat: np.ndarray, a: int, b: int):
+    """The dedupe pass of one spoke (rows [a, b)), per field: for every present occurrence
+    (row, field) → (table id or −1, TG, INIT, SCAT, rank within its chunk's equal slots).
+    TG: the margin reads the table (the slot was first seen in an earlier chunk);
+    INIT: first occurrence of a table slot; SCAT: the slot recurs ≥ 2 chunks later."""
+    out = {}
+    lid = 0
+    for f in range(cat.shape[1]):
+        first, last = {}, {}
+        for t in range(a, b):
+            c = int(cat[t, f])
+            if c == -1:
+                continue
+            s = c & 0x7FFFFFFF
+            first.setdefault(s, t - a)
+            last[s] = t - a
+        ids = {}
+        for s in sorted(first):
+            if (last[s] >> 6) - (first[s] >> 6) >= 2:
+                ids[s] = lid
+                lid += 1
+        seen = {}
+        for t in range(a, b):
+            c = int(cat[t, f])
+            if c == -1:
+                continue
+            s, r = c & 0x7FFFFFFF, t - a
+            tab = s in ids
+            key = (s, r >> 6)
+            rank = seen.get(key, 0)
+            seen[key] = rank + 1
+            out[(t, f)] = (ids.get(s, -1), tab and (r >> 6) > (first[s] >> 6),
+                           tab and r == first[s], tab and (last[s] >> 6) >= (r >> 6) + 2, rank)
+    return out, lid
+
+
+def _scan3_model(w, batch, space, R, S, C=1.0, bias=True):
+    """NumPy model of linear_scan3.hip (PA-I): chunk j's base margin is assembled in the
+    helpers' iteration j − 1 — after chunk j − 2 was scattered into the table — from the
+    table (TG occurrences), w (the rest) and the dense weights after chunks ≤ j − 2; the
+    scanner adds X1_j·c_{j−1} and runs the in-chunk G_j recurrence."""
+    dim = space.dim
+    cat = hash_raw(batch.tok, space).numpy()
+    num = batch.num.double().numpy()
+    y = batch.y.double().numpy()
+    B = batch.B
+    w0 = w.double().numpy()
+    dcols = list(range(space.dn)) + ([dim - 1] if bias else [])
+    acc, n_act = np.zeros(dim), 0
+    for s in range(S):
+        a, b = min(s * R, B), min(s * R + R, B)
+        if a >= b:
+            continue
+        n_act += 1
+        flags, _ = _occurrence_flags(cat, a, b)
+        table = {}
+        wn = w0[dcols].copy()
+        chunks = []
+        for c0 in range(a, b, CH):
+            rows = list(range(c0, min(b, c0 + CH)))
+            X = np.zeros((len(rows), dim))
+            for i, t in enumerate(rows):
+                X[i, :space.dn] = num[t]
+                for f in range(space.dc):
+                    cc = int(cat[t, f])
+                    if cc != -1:
+                        X[i, cc & 0x7FFFFFFF] += -1.0 if cc < 0 else 1.0
+                if bias:
+                    X[i, dim - 1] = 1.0
+            chunks.append((rows, X))
+        cs = []
+        bases = {}
+
+        def build(j):  # helpers' margins of chunk j (iteration j − 1)
+            rows, X = chunks[j]
+            base = X[:, dcols] @ wn
+            for i, t in enumerate(rows):
+                for f in range(space.dc):
+                    cc = int(cat[t, f])
+                    if cc == -1:
+                        continue
+                    lid, tg, init, _, _ = flags[(t, f)]
+                    sl = cc & 0x7FFFFFFF
+                    v = table[lid] if tg else w0[sl]
+                    if init:
+                        table[lid] = w0[sl]
+                    base[i] += -v if cc < 0 else v
+            bases[j] = base
+
+        def scatter(j):  # helpers' scatter of chunk j (iteration j + 1)
+            nonlocal wn
+            rows, X = chunks[j]
+            for i, t in enumerate(rows):
+                for f in range(space.dc):
+                    cc = int(cat[t, f])
+                    if cc == -1:
+                        continue
+                    lid, _, _, sc, _ = flags[(t, f)]
+                    if sc:
+                        table[lid] += -cs[j][i] if cc < 0 else cs[j][i]
+            wn = wn + X[:, dcols].T @ cs[j]
+
+        nch = len(chunks)
+        build(0)
+        for k in range(nch):
+            # iteration k: helpers scatter k − 1, build k + 1; the scanner scans k
+            if k >= 1:
+                scatter(k - 1)
+            if k + 1 < nch:
+                build(k + 1)
+            rows, X = chunks[k]
+            m0 = bases[k].copy()
+            if k >= 1:
+                m0 += (X @ chunks[k - 1][1].T) @ cs[k - 1]
+            G = X @ X.T
+            n2 = (X * X).sum(1)
+            cvec = np.zeros(len(rows))
+            for i, t in enumerate(rows):
+                m = m0[i] + (cvec[:i] * G[i, :i]).sum()
+                cvec[i] = min(C, max(0.0, 1 - y[t] * m) / n2[i]) * y[t]
+            cs.append(cvec)
+        for j, (rows, X) in enumerate(chunks):
+            acc += X.T @ cs[j]
+    return w0 + acc / n_act
+
+
+def test_table_schedule_of_the_v3_scan_is_exact():
+    """Which occurrences read / initialise / update the slot table, and when, gives the
+    exact sequential spoke (tiny hash space: many table slots, repeats in a chunk)."""
+    space = FeatureSpace(4, 0, 6, 1 << 9)
+    batch = synth_raw(space, 900, seed=3, missing=0.05)
+    w = torch.randn(space.dim, generator=torch.Generator().manual_seed(5)) * 0.01
+    for R, S in ((450, 2), (300, 3), (64, 15), (200, 5)):
+        ref = _blocked_gram_scan(w, batch, space, R, S, C=0.7)
+        v3 = _scan3_model(w, batch, space, R, S, C=0.7)
+        assert np.allclose(v3, ref, atol=1e-10, rtol=1e-9), np.abs(v3 - ref).max()
+
+
+def test_occurrence_flags_cover_every_recurrence():
+    """Every later occurrence of a slot sees every earlier one's update: through G (same
+    chunk), X1 (previous chunk) or the table (SCAT earlier → TG later)."""
+    space = FeatureSpace(2, 0, 8, 1 << 10)
+    cat = hash_raw(synth_raw(space, 700, seed=7).tok, space).numpy()
+    flags, n = _occurrence_flags(cat, 0, 700)
+    assert n > 0
+    for (t, f), (lid, tg, init, sc, rank) in flags.items():
+        later = [(u, g) for (u, g) in flags if g == f and u > t
+                 and (cat[u, f] & 0x7FFFFFFF) == (cat[t, f] & 0x7FFFFFFF)]
+        for u, _ in later:
+            if (u >> 6) >= (t >> 6) + 2:
+                assert sc and flags[(u, f)][1], (t, u)
+
+
+# ------------------------------------------------------------------ GPU
+def _round(kernel, monkeypatch, space, B, S, R, rule, variant=L.PA1, task=0, missing=0.0,
+           y8=False, bias=True, seed=11, scale=0.01, parts=1):
+    monkeypatch.setattr(L, "SEQ_KERNEL", kernel)
+    batch = synth_raw(space, B, seed=seed, task=task, missing=missing)
+    if y8:
+        batch = RawBatch(batch.num, batch.tok, batch.y.to(torch.int8))
+    w = torch.randn(space.dim, generator=torch.Generator().manual_seed(seed)) * scale
+    lr = L.LinearRule(rule=rule, variant=variant, C=0.7, eps=0.1, lr=0.2, bias=bias)
+    wc, dc = w.clone(), torch.zeros(space.dim + 2)
+    L.linear_seq_round(wc, batch, R, S, dc, lr, 1.0 / S)
+    L.linear_apply(wc, None, dc)
+    dev = _cuda()
+    wg, dg = w.to(dev), torch.zeros(space.dim + 2, device=dev)
+    cum = torch.zeros(8, dtype=torch.float64, device=dev)
+    got = []
+    used = L.linear_seq_round(wg, batch.to(dev), R, S, dg, lr, 1.0 / S, cum=cum, parts=parts,
+                              on_part=lambda k, lo, hi: got.append((k, lo, hi)))
+    L.linear_apply(wg, None, dg)
+    torch.cuda.synchronize()
+    return wc, wg.cpu(), cum.cpu(), used, got
+
+
+@gpu
+@pytest.mark.parametrize("rule,variant,task", [(L.RULE_HINGE, L.PA1, 0), (L.RULE_HINGE, L.PA, 0),
+                                               (L.RULE_HINGE, L.PA2, 0), (L.RULE_EPS, L.PA1, 1),
+                                               (L.RULE_LOGISTIC, L.PA1, 0)])
+def test_gpu_scan3_round_matches_cpu(monkeypatch, rule, variant, task):
+    space = FeatureSpace(13, 0, 26, 1 << 16)
+    # 5 spokes × 300 rows (chunks of 64: 4 full + a 44-row tail) + a 100-row last spoke
+    wc, wg, cum, used, _ = _round("scan3", monkeypatch, space, 1300, 5, 300, rule, variant,
+                                  task, missing=0.05)
+    assert used
+    assert torch.allclose(wg, wc, atol=2e-4, rtol=1e-3), (wg - wc).abs().max()
+    assert int(cum[1]) == 1300
+
+
+@gpu
+def test_gpu_scan3_int8_labels_no_bias_wide_dense(monkeypatch):
+    space = FeatureSpace(20, 0, 8, 1 << 12)  # dn + bias > 16: the 32-column dense block
+    wc, wg, _, used, _ = _round("scan3", monkeypatch, space, 700, 3, 256, L.RULE_HINGE, y8=True,
+                                bias=False)
+    assert used and torch.allclose(wg, wc, atol=2e-4, rtol=1e-3), (wg - wc).abs().max()
+
+
+@gpu
+def test_gpu_scan3_tiny_hash_space_and_table_spill(monkeypatch):
+    """Almost every slot recurs inside a chunk and across chunks (ranks up to 63, most
+    occurrences table slots); then the same with a 16-entry LDS table, so nearly every
+    table slot takes the global spill path."""
+    space = FeatureSpace(3, 0, 32, 1 << 9)
+    h = native.hip()
+    for cap in (-1, 16):
+        h.omldm_scan3_set_cap(cap)
+        try:
+            wc, wg, _, used, _ = _round("scan3", monkeypatch, space, 1280, 2, 640, L.RULE_HINGE,
+                                        seed=4)
+        finally:
+            h.omldm_scan3_set_cap(-1)
+        assert used and torch.allclose(wg, wc, atol=5e-4, rtol=2e-3), (cap, (wg - wc).abs().max())
+
+
+@gpu
+def test_gpu_scan3_parts_report_key_ranges(monkeypatch):
+    """The combine in 4 launches: same model as in one, and the reported slices tile
+    [0, dim + 2) in order (each part's collective can start as it completes)."""
+    space = FeatureSpace(13, 0, 26, 1 << 16)
+    w1, g1, _, _, got1 = _round("scan3", monkeypatch, space, 2048, 4, 512, L.RULE_HINGE)
+    w4, g4, _, _, got4 = _round("scan3", monkeypatch, space, 2048, 4, 512, L.RULE_HINGE, parts=4)
+    assert torch.equal(g1, g4)
+    assert [k for k, _, _ in got4] == [0, 1, 2, 3]
+    assert got4[0][1] == 0 and got4[-1][2] == space.dim + 2
+    assert all(got4[i][2] == got4[i + 1][1] for i in range(3))
+    assert got1 == [(0, 0, space.dim + 2)]
+
+
+@gpu
+def test_gpu_scan3_bench_geometry_matches_cpu_oracle(monkeypatch):
+    """The headline's geometry: 16 spokes × 8192 rows, 2^20 hashed slots, 13 numerical +
+    26 categorical fields, PA-I; three rounds against the CPU oracle."""
+    from omldm_amd.models.linear import SVM
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.parallel.protocols import Synchronous
+
+    monkeypatch.setattr(L, "SEQ_KERNEL", "scan3")
+    space = FeatureSpace(13, 0, 26, 1 << 20)
+    B = 16 * 8192
+    res = {}
+    for dev in ("cpu", "cuda"):
+        lrn = SVM({"variant": "PA-I", "C": 1.0}, space, dev)
+        proto = Synchronous(Comm(), lrn, {"virtualSpokes": 16})
+        for k in range(3):
+            b = synth_raw(space, B, start=k * B, seed=25)
+            proto.round(b.to(dev) if dev == "cuda" else b)
+        res[dev] = (lrn.w.cpu(), lrn.running_totals())
+    d = (res["cuda"][0] - res["cpu"][0]).abs()
+    assert d.max() < 2e-3 and float(d.mean()) < 1e-6, (d.max(), d.mean())
+    assert res["cuda"][1]["fitted"] == res["cpu"][1]["fitted"] == 3 * B
+    assert abs(res["cuda"][1]["mistakes"] - res["cpu"][1]["mistakes"]) <= 1e-3 * 3 * B
