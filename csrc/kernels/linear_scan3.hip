@@ -89,8 +89,10 @@ __device__ __forceinline__ void spoke_rows(int s, int R, int B, int& t0, int& t1
 
 // ------------------------------------------------------------------ pass 1: slots
 // 256 rows per block through an LDS tile: coalesced row-major reads, coalesced
-// field-major writes. hashed = 0: tokens (murmur3 per field); 1: already slots.
-__global__ __launch_bounds__(256) void s3_slots_kernel(const uint32_t* __restrict__ src, int B,
+// field-major writes. hashed = 0: 32-bit tokens (murmur3 per field); 1: int32 signed
+// slots; 2: the engine's compact uint16 {sign, local} (0xFFFF absent), slot = dn +
+// f·span + local — the wire format trains without a widening pass.
+__global__ __launch_bounds__(256) void s3_slots_kernel(const void* __restrict__ src, int B,
                                                        int dc, int dn, uint32_t span, int hashed,
                                                        int* __restrict__ slotsT) {
   __shared__ int tile[256][s3::MAXF + 1];
@@ -98,8 +100,17 @@ __global__ __launch_bounds__(256) void s3_slots_kernel(const uint32_t* __restric
   const int nr = min(256, B - r0);
   for (int i = tid; i < nr * dc; i += 256) {
     const int r = i / dc, f = i - r * dc;
-    const uint32_t v = src[(size_t)r0 * dc + i];
-    tile[r][f] = hashed ? (int)v : hash_token_dev(v, f, dn, span);
+    int slot;
+    if (hashed == 2) {
+      const uint32_t v = reinterpret_cast<const uint16_t*>(src)[(size_t)r0 * dc + i];
+      slot = v == 0xFFFFu ? -1
+                          : (int)(((uint32_t)dn + (uint32_t)f * span + (v & 0x7FFFu)) |
+                                  ((v & 0x8000u) << 16));
+    } else {
+      const uint32_t v = reinterpret_cast<const uint32_t*>(src)[(size_t)r0 * dc + i];
+      slot = hashed ? (int)v : hash_token_dev(v, f, dn, span);
+    }
+    tile[r][f] = slot;
   }
   __syncthreads();
   if (tid < nr)
@@ -908,20 +919,23 @@ struct S3Ws {
 
 // Passes 1-3 (model-independent): slots, dedupe, Grams. `src` is the tokens (hashed = 0)
 // or row-major field-aware slots (hashed = 1). `ptrs` = the 11 workspaces above.
+// span: slots per field (0: (dim − dn − 1) / dc, the raw-token hashing's; the compact
+// wire's cat_span otherwise — fields occupy [dn + f·span, dn + (f + 1)·span)).
 OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int hashed, int dc,
                                   int B, int R, int S, int dim, int bias, int rule, int variant,
-                                  float C, void* const* ptrs, void* stream) {
+                                  float C, long long span_in, void* const* ptrs, void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
   if ((long long)(dim - dn - 1) / dc < 1) return -2;
+  if (span_in < 0 || (long long)dn + (long long)dc * span_in > (long long)dim - 1) return -2;
   hipStream_t st = (hipStream_t)stream;
-  const uint32_t span = (uint32_t)((dim - dn - 1) / dc);
+  const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
   const S3Ws W{(int*)ptrs[0], (uint32_t*)ptrs[1], (unsigned long long*)ptrs[2], (int*)ptrs[3],
                (int*)ptrs[4], (int*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7], (float*)ptrs[8],
                (float*)ptrs[9], (float*)ptrs[10]};
   const int S_act = s3_sact(B, R, S);
-  hipLaunchKernelGGL(s3_slots_kernel, dim3((B + 255) / 256), dim3(256), 0, st,
-                     (const uint32_t*)src, B, dc, dn, span, hashed, W.slotsT);
+  hipLaunchKernelGGL(s3_slots_kernel, dim3((B + 255) / 256), dim3(256), 0, st, src, B, dc, dn,
+                     span, hashed, W.slotsT);
   hipMemsetAsync(W.lidcount, 0, sizeof(int) * S, st);
   int npow = s3::DT;
   while (npow < R) npow <<= 1;
@@ -953,11 +967,13 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
 OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int y8, int B, int R,
                               int S, float* dacc, int dim, double* cum, int rule, int variant,
                               float C, float eps, float lr, float inv_p, int bias,
-                              void* const* ptrs, int part, int parts, void* stream) {
+                              long long span_in, void* const* ptrs, int part, int parts,
+                              void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
+  if (span_in < 0 || (long long)dn + (long long)dc * span_in > (long long)dim - 1) return -2;
   hipStream_t st = (hipStream_t)stream;
-  const uint32_t span = (uint32_t)((dim - dn - 1) / dc);
+  const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
   const S3Ws W{(int*)ptrs[0], (uint32_t*)ptrs[1], (unsigned long long*)ptrs[2], (int*)ptrs[3],
                (int*)ptrs[4], (int*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7], (float*)ptrs[8],
                (float*)ptrs[9], (float*)ptrs[10]};
@@ -993,9 +1009,9 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
 
 // [lo, hi) of dacc that combine part `part` of `parts` completes (the last part also the
 // numerical columns, the tail, the intercept and dacc[dim], dacc[dim + 1]).
-OMLDM_API int omldm_scan3_part_bounds(int dim, int dn, int dc, int part, int parts,
-                                      long long* lohi) {
-  const uint32_t span = (uint32_t)((dim - dn - 1) / dc);
+OMLDM_API int omldm_scan3_part_bounds(int dim, int dn, int dc, long long span_in, int part,
+                                      int parts, long long* lohi) {
+  const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
   const int ntiles = s3_ntiles(span);
   const int nblk = dc * ntiles + 2;
   const int lo = (int)((long long)nblk * part / parts), hi = (int)((long long)nblk * (part + 1) / parts);

@@ -81,6 +81,9 @@ class HashedBatch:
     y: torch.Tensor
     raw: list | None = field(default=None, compare=False)  # optional raw records (forecasting)
     cat_span: int = 0  # > 0: compact uint16 field-aware categorical format (int16 storage)
+    # rows per virtual spoke of a spoke-major batch (engine/holdout.py routes a tick into
+    # one), or None; a plain attribute, not carried by slicing / selection
+    shards = None
 
     @property
     def B(self) -> int:
@@ -174,6 +177,29 @@ class HashedBatch:
         c32 = ((c + 2**31) % 2**32 - 2**31).to(torch.int32)
         return HashedBatch(self.num, c32.contiguous(), self.y, self.raw, 0)
 
+    def spoke_padded(self, spokes: int) -> "HashedBatch":
+        """A spoke-major batch (``shards`` = rows per spoke) laid out as spokes × R rows,
+        R = max(shards): spoke s's rows at [s·R, s·R + shards[s]), the rest unlabeled
+        (y NaN, no features — the linear rounds skip them). Sharding it in R-row blocks
+        then trains every row on the spoke that routed it. Unchanged when the shards are
+        equal (or absent / of another spoke count)."""
+        sh = self.shards
+        if sh is None or len(sh) != spokes or len(set(sh)) <= 1 or not self.B:
+            return self
+        R = max(sh)
+        idx = np.full(spokes * R, self.B, dtype=np.int64)  # row B: the blank row
+        o = 0
+        for s, n in enumerate(sh):
+            idx[s * R:s * R + n] = np.arange(o, o + n)
+            o += n
+        ix = index_tensor(idx, self.y.device)
+        num = torch.cat([self.num, self.num.new_zeros((1, self.dn))])
+        cat = torch.cat([self.cat, self.cat.new_full((1, self.dc), -1)])
+        y = torch.cat([self.y, self.y.new_full((1,), float("nan"))])
+        out = HashedBatch(num[ix], cat[ix], y[ix], None, self.cat_span)
+        out.shards = (R,) * spokes
+        return out
+
     def dense(self, dim: int | None = None) -> torch.Tensor:
         """Materialise [B, dim] dense features (tests / small dense learners only)."""
         dim = dim or (self.dn + 1)
@@ -230,6 +256,9 @@ class RawBatch:
     y: torch.Tensor
     # passes 1-2 of the v2 round made ahead of the round (ops.linear.ScanPrep), or None
     prep: object = None
+    # > 0: ``tok`` holds the engine's compact int16 field-aware slots (HashedBatch.cat with
+    # this cat_span) instead of tokens — the v3 round reads them as they are
+    span: int = 0
 
     @property
     def B(self) -> int:

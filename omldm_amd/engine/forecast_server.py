@@ -82,6 +82,9 @@ class ForecastServer:
         self._op = np.zeros(1, dtype=np.int8)
         self._offs = np.zeros(2, dtype=np.int64)
         self._done: dict = {}          # consumer offsets up to which every record is answered
+        # held by the lane for one poll → answer / hand back → ``_done`` cycle, so a
+        # checkpoint sees ``_done`` and ``fallback`` of the same instant (``snapshot``)
+        self._cycle = threading.Lock()
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, name="omldm-forecast", daemon=True)
         _LIVE.add(self)
@@ -156,6 +159,15 @@ class ForecastServer:
         srv.start(lifetime_us=self.lifetime_us)
         self._server = srv
         return srv
+
+    def snapshot(self) -> tuple[dict, list]:
+        """Checkpoint view of the lane, taken between two of its cycles: the consumer
+        offsets up to which every forecasting record is answered or handed back, and the
+        handed-back records still waiting for the tick (saved with the job's state like
+        the record buffer, so a restore neither skips nor repeats a forecast)."""
+        with self._cycle:
+            done = dict(self._done) if self._thread.is_alive() else dict(self.consumer.offsets)
+            return done, list(self.fallback)
 
     def take_fallback(self) -> list:
         out = []
@@ -240,20 +252,20 @@ class ForecastServer:
         idle_marked = False
         while not self._stop.is_set():
             quiet = time.perf_counter() - last
-            # right after traffic the topic is polled directly; a quiet topic is looked at
-            # through its end offsets first (cheap) and not polled
-            recs = self.consumer.poll(64) if (quiet < self.SPIN_S or self._pending()) else []
-            if not recs:
+            with self._cycle:
+                # right after traffic the topic is polled directly; a quiet topic is looked
+                # at through its end offsets first (cheap) and not polled
+                recs = self.consumer.poll(64) if (quiet < self.SPIN_S or self._pending()) else []
+                if recs:
+                    idle_marked = False
+                    last = time.perf_counter()
+                    t_in = last
+                    for i, rec in enumerate(recs):
+                        if not self.serve_one(rec, t_in if i == 0 else None):
+                            self.fallback.append(rec)
+                    self._done = dict(self.consumer.offsets)
+                    continue
                 if not idle_marked:  # everything polled so far is answered
                     self._done = dict(self.consumer.offsets)
                     idle_marked = True
-                time.sleep(0 if quiet < self.SPIN_S else
-                           (50e-6 if quiet < self.WARM_S else 1e-3))
-                continue
-            idle_marked = False
-            last = time.perf_counter()
-            t_in = last
-            for i, rec in enumerate(recs):
-                if not self.serve_one(rec, t_in if i == 0 else None):
-                    self.fallback.append(rec)
-            self._done = dict(self.consumer.offsets)
+            time.sleep(0 if quiet < self.SPIN_S else (50e-6 if quiet < self.WARM_S else 1e-3))

@@ -1,13 +1,23 @@
-"""Holdout test set of a spoke (per rank), kept on the device.
+"""Holdout test sets of the virtual spokes of one rank, kept on the device.
 
-Reference (omldm/operators/spoke/FlinkSpoke.scala:95-104): a counter runs 0..9 over the
-training points; points 8 and 9 of every 10 are appended to a FIFO test set of
-``testSetSize``; when the FIFO is full the evicted (oldest) point is trained on instead.
-The test set scores queries (:160-163) and the final statistics (:136-138).
+Reference (omldm/operators/spoke/FlinkSpoke.scala:38-41,95-104): EVERY spoke runs its own
+counter 0..9 over the training points it receives; its points 8 and 9 of every 10 are
+appended to its own FIFO test set of ``testSetSize``; when that FIFO is full the evicted
+(oldest) point is trained on instead. A query scores each spoke's test set (:160-163, the
+−1 query :136-138) and ResponseConstructor averages the P spoke answers
+(omldm/utils/ResponseConstructor.scala:32-52).
 
-Micro-batch form: the positions of one batch are classified by the running counter;
-holdout rows enter the ring in order; rows they evict (and, once the ring is full, the
-earliest rows of the same batch) join the training rows of this round.
+Micro-batch form. A rank runs S virtual spokes; the tick's B training rows are dealt to
+them in contiguous shards (spoke s: rows [s·⌈B/S⌉, (s+1)·⌈B/S⌉)), the order the round
+itself shards a batch in. Each spoke classifies its shard's positions with its own
+counter; held rows enter its ring in order; rows they evict (and, once the ring is full,
+the earliest held rows of the same shard) join that spoke's training rows. The training
+batch is spoke-major — spoke s's rows are contiguous — and records each spoke's row
+count (``HashedBatch.shards``), so the round trains spoke s's rows on spoke s.
+
+Which rows are held depends only on the counters, so the host computes one small
+descriptor per spoke and two kernels move the rows (csrc/kernels/holdout.hip,
+``omldm_holdout_route_spokes``): no index arrays, no host synchronisation.
 """
 from __future__ import annotations
 
@@ -16,107 +26,148 @@ import torch
 
 from omldm_amd.api.batch import FeatureSpace, HashedBatch, index_tensor
 
+DESC_W = 12  # int64 words per spoke descriptor (csrc/kernels/holdout.hip: SpokeDesc)
+
+
+def held_before(x: int) -> int:
+    """Held positions among counter values [0, x): 8 and 9 of every ten."""
+    return (x // 10) * 2 + max(0, x % 10 - 8)
+
+
+def nonheld_row(r: np.ndarray, c: int) -> np.ndarray:
+    q = min(c, 8) + r
+    return (q // 8) * 10 + (q % 8) - c
+
+
+def held_row(r: np.ndarray, c: int) -> np.ndarray:
+    q = max(c - 8, 0) + r
+    return (q // 2) * 10 + 8 + (q % 2) - c
+
 
 class HoldoutSet:
-    def __init__(self, space: FeatureSpace, size: int, device, num_dtype=torch.float32):
+    def __init__(self, space: FeatureSpace, size: int, device, num_dtype=torch.float32,
+                 spokes: int = 1):
         self.size = int(size)
+        self.spokes = max(1, int(spokes))
         self.device = torch.device(device)
-        self.ring = HashedBatch.empty(space, self.size, device=self.device, num_dtype=num_dtype)
-        self.count = 0   # reference counter (mod 10)
-        self.head = 0    # next write position
-        self.filled = 0
+        self.space = space
+        S = self.spokes
+        # spoke s's ring: rows [s·size, (s+1)·size)
+        self.ring = HashedBatch.empty(space, S * self.size, device=self.device,
+                                      num_dtype=num_dtype)
+        self.count = np.zeros(S, dtype=np.int64)   # reference counter (mod 10), per spoke
+        self.head = np.zeros(S, dtype=np.int64)    # next write position, per spoke
+        self.filled = np.zeros(S, dtype=np.int64)
+        self._desc_host = None
 
-    @staticmethod
-    def _held_before(x: int) -> int:
-        """Held positions among counter values [0, x): 8 and 9 of every ten."""
-        return (x // 10) * 2 + max(0, x % 10 - 8)
+    _held_before = staticmethod(held_before)
 
-    def _route_device(self, batch: HashedBatch) -> HashedBatch:
-        """GPU form of ``route``: the same rows in the same order, moved by two kernels
-        (csrc/kernels/holdout.hip) from scalar segment descriptors — no index arrays,
-        no host synchronisation."""
+    # ------------------------------------------------------------------ routing
+    def shard_bounds(self, B: int) -> list[tuple[int, int]]:
+        """Spoke s's rows of a B-row tick: [s·⌈B/S⌉, (s+1)·⌈B/S⌉) ∩ [0, B)."""
+        S = self.spokes
+        R = -(-B // S) if B else 0
+        return [(min(s * R, B), min(s * R + R, B)) for s in range(S)]
+
+    def _plan(self, B: int) -> np.ndarray:
+        """One descriptor per spoke (b0, n0, n1, r1, n2, s2, ns, hs, rw, o0, c, 0) and the
+        advanced counters / heads / fills. n0 non-held rows, n1 evicted ring rows from
+        r1, n2 held rows from hold-ordinal s2 that never fit; ns held rows from ordinal
+        hs written to the ring from rw."""
+        S, size = self.spokes, self.size
+        desc = np.zeros((S, DESC_W), dtype=np.int64)
+        o = 0
+        for s, (a, b) in enumerate(self.shard_bounds(B)):
+            Bs, c = b - a, int(self.count[s])
+            head, filled = int(self.head[s]), int(self.filled[s])
+            n_hold = held_before(c + Bs) - held_before(c)
+            n0 = Bs - n_hold
+            r1 = (head - filled) % size
+            if n_hold >= size:
+                n1, n2, s2 = filled, n_hold - size, 0
+                ns, hs, rw = size, n_hold - size, 0
+                head, filled = 0, size
+            else:
+                n1, n2, s2 = max(0, filled + n_hold - size), 0, 0
+                ns, hs, rw = n_hold, 0, head
+                head, filled = (head + n_hold) % size, min(size, filled + n_hold)
+            desc[s] = (a, n0, n1, r1, n2, s2, ns, hs, rw, o, c, 0)
+            o += n0 + n1 + n2
+            self.count[s] = (c + Bs) % 10
+            self.head[s], self.filled[s] = head, filled
+        return desc
+
+    def _route_device(self, batch: HashedBatch, desc: np.ndarray) -> HashedBatch:
         from omldm_amd.ops import native
 
-        B, c, size = batch.B, self.count, self.size
-        n_hold = self._held_before(c + B) - self._held_before(c)
-        n_train = B - n_hold
-        self.count = (c + B) % 10
-        if n_hold >= size:
-            n1, r1 = self.filled, (self.head - self.filled) % size
-            n2, s2 = n_hold - size, 0
-            ns, hs, rw = size, n_hold - size, 0
-            self.head, self.filled = 0, size
-        else:
-            n1 = max(0, self.filled + n_hold - size)
-            r1 = (self.head - self.filled) % size
-            n2, s2 = 0, 0
-            ns, hs, rw = n_hold, 0, self.head
-            self.head = (self.head + n_hold) % size
-            self.filled = min(size, self.filled + n_hold)
-        n_out = n_train + n1 + n2
+        S = self.spokes
+        n = desc[:, 1] + desc[:, 2] + desc[:, 4]
+        n_out = int(n.sum())
         out = HashedBatch(torch.empty((n_out, batch.dn), dtype=batch.num.dtype, device=self.device),
                           torch.empty((n_out, batch.dc), dtype=batch.cat.dtype, device=self.device),
                           torch.empty(n_out, dtype=torch.float32, device=self.device),
                           cat_span=batch.cat_span)
+        # descriptors: pinned host → device on the compute stream (no sync); the pinned
+        # block stays referenced until the next route (the copy has run by then)
+        host = torch.from_numpy(np.ascontiguousarray(desc)).pin_memory()
+        dev = host.to(self.device, non_blocking=True)
+        self._desc_host = host
         p = native.ptr
-        rc = native.hip().omldm_holdout_route(
-            p(batch.num), p(batch.cat), p(batch.y), B, p(self.ring.num), p(self.ring.cat),
-            p(self.ring.y), size, p(out.num), p(out.cat), p(out.y), c, n_train, n1, r1, n2, s2,
-            ns, hs, rw, batch.dn, batch.dc, batch.num.element_size(), batch.cat.element_size(),
-            torch.cuda.current_stream(self.device).cuda_stream)
-        native.check(rc, "omldm_holdout_route")
+        rc = native.hip().omldm_holdout_route_spokes(
+            p(batch.num), p(batch.cat), p(batch.y), batch.B, p(self.ring.num), p(self.ring.cat),
+            p(self.ring.y), self.size, S, p(out.num), p(out.cat), p(out.y), n_out,
+            host.numpy().ctypes.data, p(dev), batch.dn, batch.dc, batch.num.element_size(),
+            batch.cat.element_size(), torch.cuda.current_stream(self.device).cuda_stream)
+        native.check(rc, "omldm_holdout_route_spokes")
+        self._desc_dev = dev
+        return out
+
+    def _route_host(self, batch: HashedBatch, desc: np.ndarray) -> HashedBatch:
+        """The same rows in the same order by explicit index arrays (CPU jobs, dtype
+        mismatches); the ring is written after the evicted rows are read."""
+        size = self.size
+        widx, wsrc = [], []
+        order = []  # ("b", idx) / ("r", idx) segments in output order
+        for s in range(self.spokes):
+            b0, n0, n1, r1, n2, s2, ns, hs, rw, _, c, _ = (int(v) for v in desc[s])
+            order.append(("b", b0 + nonheld_row(np.arange(n0), c)))
+            order.append(("r", s * size + (r1 + np.arange(n1)) % size))
+            order.append(("b", b0 + held_row(s2 + np.arange(n2), c)))
+            widx.append(s * size + (rw + np.arange(ns)) % size)
+            wsrc.append(b0 + held_row(hs + np.arange(ns), c))
+        parts = []
+        for kind, idx in order:
+            if idx.size == 0:
+                continue
+            if kind == "b":
+                parts.append(batch.select(idx).without_raw())
+            else:
+                r = self.ring.select(idx).to(batch.y.device)
+                parts.append(HashedBatch(r.num.to(batch.num.dtype), r.cat, r.y, None,
+                                         batch.cat_span))
+        out = HashedBatch.cat_batches(parts) if parts else batch.slice(0, 0).without_raw()
+        w = np.concatenate(widx) if widx else np.zeros(0, dtype=np.int64)
+        if w.size:
+            self._scatter(w, batch.select(np.concatenate(wsrc)))
         return out
 
     def route(self, batch: HashedBatch) -> HashedBatch:
-        """Returns the rows to train on this round (holdout-evicted rows included).
-        Which rows are held out depends only on the running counter, so every index
-        is computed on the host (numpy) and reaches the device as one non-blocking
-        copy — no stream synchronisation on the tick's critical path."""
+        """The rows to train on this round (holdout-evicted rows included), spoke-major,
+        with ``shards`` = the per-spoke row counts."""
         B = batch.B
         if B == 0 or self.size == 0:
+            if B:
+                batch.shards = tuple(b - a for a, b in self.shard_bounds(B))
             return batch
+        desc = self._plan(B)
         if (self.device.type == "cuda" and batch.y.device == self.device
                 and batch.num.dtype == self.ring.num.dtype and batch.cat.dtype == self.ring.cat.dtype
                 and all(t.is_contiguous() for t in (batch.num, batch.cat, batch.y))):
-            return self._route_device(batch)
-        pos = (np.arange(B, dtype=np.int64) + self.count) % 10
-        self.count = (self.count + B) % 10
-        hold = pos >= 8
-        idx_hold = np.flatnonzero(hold)
-        n_hold = int(idx_hold.size)
-        if n_hold == 0:
-            return batch
-        idx_train = np.flatnonzero(~hold)
-        out = [batch.select(idx_train)]
-        if n_hold >= self.size:
-            # earlier holdout rows of this batch are evicted by later ones: train on them
-            if self.filled:
-                out.append(self._ring_in_order())
-            spill = idx_hold[: n_hold - self.size]
-            if spill.size:
-                out.append(batch.select(spill))
-            keep = batch.select(idx_hold[n_hold - self.size:])
-            self._write(0, keep)
-            self.head = 0
-            self.filled = self.size
+            out = self._route_device(batch, desc)
         else:
-            new = batch.select(idx_hold)
-            n_evict = max(0, self.filled + n_hold - self.size)
-            if n_evict:
-                oldest = (self.head - self.filled) % self.size
-                ev = (np.arange(n_evict) + oldest) % self.size
-                out.append(self.ring.select(ev).to(batch.y.device))
-            pos_w = (np.arange(n_hold) + self.head) % self.size
-            self._scatter(pos_w, new)
-            self.head = (self.head + n_hold) % self.size
-            self.filled = min(self.size, self.filled + n_hold)
-        return HashedBatch.cat_batches(out)
-
-    def _write(self, at: int, rows: HashedBatch):
-        n = rows.B
-        self.ring.num[at:at + n] = rows.num.to(self.device, self.ring.num.dtype)
-        self.ring.cat[at:at + n] = rows.cat.to(self.device)
-        self.ring.y[at:at + n] = rows.y.to(self.device)
+            out = self._route_host(batch, desc)
+        out.shards = tuple(int(v) for v in desc[:, 1] + desc[:, 2] + desc[:, 4])
+        return out
 
     def _scatter(self, pos, rows: HashedBatch):
         p = index_tensor(pos, self.device)
@@ -124,54 +175,94 @@ class HoldoutSet:
         self.ring.cat[p] = rows.cat.to(self.device)
         self.ring.y[p] = rows.y.to(self.device)
 
-    def _ring_in_order(self) -> HashedBatch:
-        oldest = (self.head - self.filled) % self.size
-        idx = (np.arange(self.filled) + oldest) % self.size
-        return self.ring.select(idx)
+    # ------------------------------------------------------------------ test sets
+    def _spoke_order(self, s: int) -> np.ndarray:
+        f = int(self.filled[s])
+        return s * self.size + (np.arange(f) + int(self.head[s]) - f) % max(1, self.size)
+
+    def test_sets(self) -> list[HashedBatch]:
+        """Each spoke's test set, oldest row first."""
+        return [self.ring.select(self._spoke_order(s)) for s in range(self.spokes)]
 
     def test_set(self) -> HashedBatch:
-        return self._ring_in_order()
+        """Every spoke's test rows, spoke-major (``shards``: rows per spoke)."""
+        idx = [self._spoke_order(s) for s in range(self.spokes)]
+        out = self.ring.select(np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64))
+        out.shards = tuple(int(i.size) for i in idx)
+        return out
 
+    @property
+    def n_test(self) -> int:
+        return int(self.filled.sum())
+
+    # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:
         return {"num": self.ring.num.cpu(), "cat": self.ring.cat.cpu(), "y": self.ring.y.cpu(),
-                "count": self.count, "head": self.head, "filled": self.filled}
+                "count": self.count.tolist(), "head": self.head.tolist(),
+                "filled": self.filled.tolist(), "spokes": self.spokes, "size": self.size}
 
     @staticmethod
-    def _rows_in_order(sd: dict) -> tuple[torch.Tensor, ...]:
-        size, filled = sd["num"].shape[0], int(sd["filled"])
-        idx = (torch.arange(filled) + (int(sd["head"]) - filled)) % max(1, size)
-        return sd["num"][idx], sd["cat"][idx], sd["y"][idx]
+    def _spoke_rows(sd: dict) -> list[tuple[torch.Tensor, ...]]:
+        """Each saved spoke's rows, oldest first (a pre-spoke checkpoint is one spoke)."""
+        cnt = sd["count"]
+        S = int(sd.get("spokes", 1 if np.isscalar(cnt) else len(cnt)))
+        size = int(sd.get("size", sd["num"].shape[0] // max(1, S)))
+        heads = np.atleast_1d(np.asarray(sd["head"], dtype=np.int64))
+        fills = np.atleast_1d(np.asarray(sd["filled"], dtype=np.int64))
+        out = []
+        for s in range(S):
+            f = int(fills[s])
+            idx = torch.from_numpy(s * size + (np.arange(f) + int(heads[s]) - f) % max(1, size))
+            out.append((sd["num"][idx], sd["cat"][idx], sd["y"][idx]))
+        return out
 
     def load_merged(self, sds: list[dict]) -> HashedBatch | None:
-        """Re-scaled restore: the rings of several old ranks merged into this one, oldest
-        rows first (old-rank order). Rows beyond ``size`` are returned to be trained on
-        (reference restore: the merged test set is popped down to its maximum size and
-        the popped points are fed to every pipeline, FlinkSpoke.scala:307-317)."""
-        self.count, self.head, self.filled = 0, 0, 0
+        """Re-scaled restore: the spoke rings of the old ranks this rank takes over, dealt
+        to this rank's spokes (old spoke i → new spoke i mod S, oldest rows first). Rows
+        beyond a ring's ``size`` are returned to be trained on (reference restore: the
+        merged test set is popped down to its maximum size and the popped points are fed
+        to every pipeline, FlinkSpoke.scala:307-317)."""
+        S = self.spokes
+        self.count[:], self.head[:], self.filled[:] = 0, 0, 0
         if not sds:
             return None
-        parts = [self._rows_in_order(sd) for sd in sds]
-        num = torch.cat([p[0] for p in parts])
-        cat = torch.cat([p[1] for p in parts])
-        y = torch.cat([p[2] for p in parts])
-        n = num.shape[0]
-        keep = min(n, self.size)
-        spill = n - keep
-        if keep:
-            self.ring.num[:keep] = num[spill:].to(self.device, self.ring.num.dtype)
-            self.ring.cat[:keep] = cat[spill:].to(self.device)
-            self.ring.y[:keep] = y[spill:].to(self.device)
-        self.filled, self.head = keep, keep % max(1, self.size)
-        self.count = int(sds[0]["count"])
-        if spill == 0:
-            return None
-        return HashedBatch(num[:spill].to(self.ring.num.dtype), cat[:spill], y[:spill],
-                           cat_span=self.ring.cat_span)
+        old = [r for sd in sds for r in self._spoke_rows(sd)]
+        counts = [c for sd in sds for c in np.atleast_1d(np.asarray(sd["count"]))]
+        spill = []
+        for s in range(S):
+            mine = old[s::S]
+            if not mine:
+                continue
+            num = torch.cat([m[0] for m in mine])
+            cat = torch.cat([m[1] for m in mine])
+            y = torch.cat([m[2] for m in mine])
+            n = num.shape[0]
+            keep = min(n, self.size)
+            sp = n - keep
+            if keep:
+                a = s * self.size
+                self.ring.num[a:a + keep] = num[sp:].to(self.device, self.ring.num.dtype)
+                self.ring.cat[a:a + keep] = cat[sp:].to(self.device)
+                self.ring.y[a:a + keep] = y[sp:].to(self.device)
+            self.filled[s], self.head[s] = keep, keep % max(1, self.size)
+            self.count[s] = int(counts[s % len(counts)]) if counts else 0
+            if sp:
+                spill.append(HashedBatch(num[:sp].to(self.ring.num.dtype), cat[:sp], y[:sp],
+                                         cat_span=self.ring.cat_span))
+        return HashedBatch.cat_batches(spill) if spill else None
 
-    def load_state_dict(self, sd: dict) -> None:
-        n = min(self.size, sd["num"].shape[0])
+    def load_state_dict(self, sd: dict) -> HashedBatch | None:
+        """Same-rank restore. A checkpoint of a different spoke count (or the pre-spoke
+        single ring) is dealt like a re-scaled restore; its overflow is returned."""
+        cnt = sd["count"]
+        S_old = int(sd.get("spokes", 1 if np.isscalar(cnt) else len(cnt)))
+        if S_old != self.spokes or int(sd.get("size", self.size)) != self.size:
+            return self.load_merged([sd])
+        n = min(self.ring.num.shape[0], sd["num"].shape[0])
         self.ring.num[:n] = sd["num"][:n].to(self.device)
         self.ring.cat[:n] = sd["cat"][:n].to(self.device)
         self.ring.y[:n] = sd["y"][:n].to(self.device)
-        self.count, self.head = int(sd["count"]), int(sd["head"]) % max(1, self.size)
-        self.filled = min(self.size, int(sd["filled"]))
+        self.count[:] = np.asarray(sd["count"], dtype=np.int64)
+        self.head[:] = np.asarray(sd["head"], dtype=np.int64) % max(1, self.size)
+        self.filled[:] = np.minimum(self.size, np.asarray(sd["filled"], dtype=np.int64))
+        return None

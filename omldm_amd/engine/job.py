@@ -123,7 +123,8 @@ class Job:
         # predictions leave through a producer thread (formatted natively, io/egress.py)
         self.egress = EgressWriter(b["predictions"], enabled=self.device.type == "cuda")
         self.pipes: dict[int, Pipeline] = {}
-        self.holdout = HoldoutSet(self.space, cfg.testSetSize, self.device)
+        # one counter + FIFO test set per virtual spoke (FlinkSpoke.scala:38-41,95-104)
+        self.holdout = HoldoutSet(self.space, cfg.testSetSize, self.device, spokes=self.spokes)
         self.store = ModelStore(self.space.dim, self.device)
         self.record_buffer: list = []          # blocks (buf, offsets) waiting for a Create
         self._buffered = 0
@@ -263,13 +264,20 @@ class Job:
             return block
         return blk
 
-    def consumer_offsets(self) -> dict:
+    def consumer_offsets(self, fc_lane: dict | None = None) -> dict:
         """Offsets after the last block this job processed (the prefetcher may have read
-        further; those records are re-read after a restore)."""
-        if self._committed is not None:
-            fc = self._committed[1] if len(self._committed) > 1 else self.fcst_in.offsets
-            return {"train": dict(self._committed[0]), "forecast": dict(fc)}
-        return {"train": dict(self.train_in.offsets), "forecast": dict(self.fcst_in.offsets)}
+        further; those records are re-read after a restore). With the per-record lane the
+        forecasting offsets are ``fc_lane`` (ForecastServer.snapshot: answered or handed
+        back), never the live consumer position (records polled but not yet answered)."""
+        train = dict(self._committed[0]) if self._committed is not None else \
+            dict(self.train_in.offsets)
+        if fc_lane is not None:
+            fc = fc_lane
+        elif self._committed is not None and len(self._committed) > 1:
+            fc = self._committed[1]
+        else:
+            fc = self.fcst_in.offsets
+        return {"train": train, "forecast": dict(fc)}
 
     def _forecast(self, batch: HashedBatch, raw: RawRecords | None):
         """Predictions of every pipeline for the forecasting rows; ``raw`` holds their
@@ -307,8 +315,14 @@ class Job:
         """Forecasting records the serving wave handed back (a pipeline it cannot score):
         predicted in one batch by every pipeline, like the batched path."""
         recs = self.fserver.take_fallback()
-        if not recs or not self.pipes:
-            self.fserver.fallback.extendleft(reversed(recs))  # no pipeline yet: keep them
+        if not recs:
+            return
+        if not self.pipes:  # no pipeline yet: keep them, bounded like the record buffer
+            room = self.cfg.recordBufferSize
+            if len(recs) > room:
+                self.counters["dropped_buffer"] += len(recs) - room
+                recs = recs[len(recs) - room:]
+            self.fserver.fallback.extendleft(reversed(recs))
             return
         buf, offs = join_block(recs)
         batch, op, _ = parse_block(buf, offs, self.space, self.cfg.parseThreads)
@@ -325,7 +339,7 @@ class Job:
         protocols run their own rounds."""
         with tracing.range("route"):
             routed = self.holdout.route(batch)
-        if direct is not None and direct.B:  # rows that bypass the holdout
+        if direct is not None and direct.B:  # rows that bypass the holdout (no spoke layout)
             routed = HashedBatch.cat_batches([direct, routed]) if routed.B else direct
         groups: dict[int, list] = {}
         for pid in sorted(self.pipes):
@@ -347,13 +361,20 @@ class Job:
     def _answer(self, req: Request, response_id=None, write=True) -> dict:
         pipe = self.pipes[req.id]
         pipe.protocol.finalize()
-        test = self.holdout.test_set()
-        loss, score, n = pipe.evaluate(test) if test.B else (0.0, 0.0, 0)
+        # every spoke scores its own test set (FlinkSpoke.scala:136-138,160-163)
+        answers = []
+        reg = pipe.learner.TASK == "regression"
+        for test in self.holdout.test_sets():
+            if not test.B:
+                continue
+            loss, score, n = pipe.evaluate(test)
+            n = int(n)
+            if n:
+                sc = float(score) / n
+                answers.append((float(loss) / n, float(np.sqrt(max(sc, 0.0))) if reg else sc, n))
         tot = pipe.learner.running_totals()
-        m = ST.reduce_query_metrics(self.comm, float(loss), float(score), int(n), tot["fitted"],
-                                    tot["loss_sum"], pipe.mean_buffer_size())
-        if pipe.learner.TASK == "regression":
-            m["score"] = float(np.sqrt(max(m["score"], 0.0)))  # mean squared error → RMSE
+        m = ST.reduce_query_metrics(self.comm, answers, tot["fitted"], tot["loss_sum"],
+                                    pipe.mean_buffer_size(), self.spokes)
         if self.rank == 0 and write:
             learner = {"name": pipe.learner.NAME,
                        "hyperParameters": pipe.learner.hyper_parameters(),
@@ -534,10 +555,16 @@ class Job:
 
     # --------------------------------------------------------------- checkpoint
     def state_dict(self) -> dict:
+        fc_lane, fc_pending = (None, [])
+        if self.fserver is not None:
+            fc_lane, fc_pending = self.fserver.snapshot()
         sd = {"pipelines": {pid: p.state_dict() for pid, p in self.pipes.items()},
               "holdout": self.holdout.state_dict(),
-              "consumers": {k: {"offsets": v} for k, v in self.consumer_offsets().items()},
+              "consumers": {k: {"offsets": v}
+                            for k, v in self.consumer_offsets(fc_lane).items()},
               "record_buffer": [r for b in self.record_buffer for r in RawView(*b)],
+              # forecasting records the lane handed back, not yet predicted by a tick
+              "forecast_pending": [bytes(r) for r in fc_pending],
               "ticks": self.ticks,
               "counters": dict(self.counters), "world": self.world,
               "spoke_parallelism": self.spoke_parallelism,
@@ -560,7 +587,9 @@ class Job:
             pipe.load_state_dict(psd)
             self.pipes[int(pid)] = pipe
         if same_world:  # partition ownership only matches at the same world size
-            self.holdout.load_state_dict(sd["holdout"])
+            spill = self.holdout.load_state_dict(sd["holdout"])  # spoke count may differ
+            if spill is not None and spill.B:
+                self._restored_train = spill
             self.train_in.load_state_dict(sd["consumers"]["train"])
             self.fcst_in.load_state_dict(sd["consumers"]["forecast"])
             recs = list(sd.get("record_buffer", []))
@@ -585,6 +614,12 @@ class Job:
             for o in owned:
                 for k, v in o.get("counters", {}).items():
                     self.counters[k] = self.counters.get(k, 0) + v
+        pending = list(sd.get("forecast_pending", [])) if same_world else \
+            [r for o in (owned or []) for r in o.get("forecast_pending", [])]
+        if pending and self.fserver is not None:
+            self.fserver.fallback.extend(pending)
+        elif pending:  # no lane here: the batched path predicts them with the next tick
+            recs = recs + pending
         self.record_buffer = [join_block(recs)] if recs else []
         self._buffered = len(recs)
         self.ticks = int(sd.get("ticks", 0))

@@ -25,27 +25,33 @@ import torch
 from omldm_amd.api.schemas import JobStatistics, QueryResponse, Statistics
 
 
-def reduce_query_metrics(comm, loss_sum: float, score_sum: float, n: int, fitted: int,
-                         cum_loss: float, mean_buffer: float = 0.0) -> dict:
-    """ResponseConstructor merge over ranks: Σ fitted; loss/cumLoss/score averaged over
-    workers of per-worker means (reference semantics). ``meanBufferSize``: every spoke
-    reports its mean buffer size / P and the statistics operator sums them
-    (FlinkSpoke.scala:138, StatisticsOperator.scala:101) — the mean over spokes; a rank's
-    spokes share one value, so it is the mean over ranks."""
+def reduce_query_metrics(comm, answers: list, fitted: int, cum_loss: float,
+                         mean_buffer: float = 0.0, spokes: int = 1) -> dict:
+    """ResponseConstructor merge (omldm/utils/ResponseConstructor.scala:32-52) over every
+    virtual spoke of every rank: each spoke answers from its own test set
+    (FlinkSpoke.scala:160-163) with its mean loss and its score; dataFitted is summed,
+    loss / score averaged over the answering spokes (all P once every test set holds a
+    point), cumulativeLoss over all P spokes. ``answers``: this rank's (mean loss, score,
+    test points) per spoke with test points; ``spokes``: this rank's spoke count, whose
+    running totals (``fitted``, ``cum_loss``) the rank keeps jointly. ``meanBufferSize``:
+    every spoke reports its mean buffer size / P and the statistics operator sums them
+    (FlinkSpoke.scala:138, StatisticsOperator.scala:101) — the mean over spokes."""
     dev = "cpu"
-    per = torch.tensor([loss_sum / max(n, 1), score_sum / max(n, 1), float(fitted),
-                        cum_loss / max(fitted, 1), float(n), 1.0 if n > 0 else 0.0,
-                        float(mean_buffer)],
+    S = max(1, int(spokes))
+    per = torch.tensor([sum(a[0] for a in answers), sum(a[1] for a in answers), float(fitted),
+                        S * cum_loss / max(fitted, 1), float(sum(a[2] for a in answers)),
+                        float(len(answers)), S * float(mean_buffer), float(S)],
                        dtype=torch.float64, device=dev)
     if comm.world > 1 and comm.backend == "nccl":
         per = per.to(torch.device("cuda", torch.cuda.current_device()))
     comm.all_reduce_(per, tag="query")
     per = per.cpu()
     workers = max(1.0, float(per[5]))
+    P = max(1.0, float(per[7]))
     return {"loss": float(per[0]) / workers, "score": float(per[1]) / workers,
-            "dataFitted": int(per[2]), "cumulativeLoss": float(per[3]) / workers,
-            "testPoints": int(per[4]), "workers": int(workers),
-            "meanBufferSize": float(per[6]) / max(1, comm.world)}
+            "dataFitted": int(per[2]), "cumulativeLoss": float(per[3]) / P,
+            "testPoints": int(per[4]), "workers": int(per[5]), "spokes": int(P),
+            "meanBufferSize": float(per[6]) / P}
 
 
 def split_params(params: dict | None, bucket: int = 10000) -> list[dict]:

@@ -111,20 +111,25 @@ class LinearLearner(Learner):
         S = max(1, -(-B // R)) if B else S
         return R, S
 
-    def _slots_scan_eligible(self, batch) -> bool:
-        """The engine's field-aware hashed batches train through the v2 scan round too
-        (slots already hashed: pass 1 skipped)."""
-        return (type(batch) is HashedBatch and batch.cat_span > 0 and self.w.is_cuda
-                and self.seq_capable() and L.SEQ_KERNEL == "scan" and batch.B > 0
-                and 0 < batch.dc and L.scan_fits(batch.dn, batch.dc))
+    def _slots_scan_eligible(self, batch, ctx: RoundContext | None = None) -> bool:
+        """The engine's field-aware hashed batches train through the exact scan rounds too:
+        v3 reads the compact int16 slots as they are, v2 after widening them."""
+        if not (type(batch) is HashedBatch and batch.cat_span > 0 and self.w.is_cuda
+                and self.seq_capable() and batch.B > 0 and 0 < batch.dc):
+            return False
+        if L.SEQ_KERNEL == "scan3":
+            R, _ = self._seq_geometry(batch.B, ctx) if ctx is not None else (batch.B, 1)
+            if L.scan3_fits(batch.dn, batch.dc, R, self.rule.bias):
+                return True
+        return L.SEQ_KERNEL in ("scan", "scan3") and L.scan_fits(batch.dn, batch.dc)
 
     def _fit_slots(self, batch: HashedBatch, ctx: RoundContext) -> None:
-        wide = batch.to_wide()
-        rb = RawBatch(batch.num.float().contiguous(), wide.cat.contiguous(),
-                      batch.y.float().contiguous())
-        R, S = self._seq_geometry(rb.B, ctx)
-        if L.scan3_eligible(rb, R, self.rule.bias):
+        num, y = batch.num.float().contiguous(), batch.y.float().contiguous()
+        R, S = self._seq_geometry(batch.B, ctx)
+        rb = RawBatch(num, batch.cat.contiguous(), y, span=batch.cat_span)
+        if L.scan3_eligible(rb, R, self.rule.bias):  # compact slots straight into pass 1
             return self._fit_raw(rb, ctx, hashed=True)
+        rb = RawBatch(num, batch.to_wide().cat.contiguous(), y)
         rb.prep = L.linear_scan_prepare_slots(rb, R, S, self.dim, bool(self.rule.bias))
         self._fit_raw(rb, ctx)
 
@@ -161,7 +166,9 @@ class LinearLearner(Learner):
             if self.seq_capable():
                 return self._fit_raw(batch, ctx)
             batch = batch.hashed(self.space)
-        if self._slots_scan_eligible(batch):
+        # a holdout-routed tick: spoke s trains exactly the rows spoke s routed
+        batch = batch.spoke_padded(max(1, int(ctx.spokes)))
+        if self._slots_scan_eligible(batch, ctx):
             return self._fit_slots(batch, ctx)
         B = batch.B
         S = max(1, int(ctx.spokes))

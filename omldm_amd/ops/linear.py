@@ -302,9 +302,23 @@ def scan3_eligible(batch: RawBatch, R: int, bias: bool) -> bool:
             and scan3_fits(batch.dn, batch.dc, R, bias))
 
 
+def _s3_span(batch: RawBatch, dim: int) -> int:
+    """Slots per field: the compact wire's cat_span, else the token hashing's."""
+    return int(batch.span) if batch.span > 0 else (dim - batch.dn - 1) // batch.dc
+
+
+def _s3_mode(batch: RawBatch, hashed: bool) -> int:
+    """s3_slots_kernel input: 0 tokens, 1 int32 signed slots, 2 compact int16 slots."""
+    if batch.span > 0:
+        assert batch.tok.dtype == torch.int16, batch.tok.dtype
+        return 2
+    assert batch.tok.dtype == torch.int32, batch.tok.dtype
+    return 1 if hashed else 0
+
+
 def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
     return (batch.B, R, S, dim, bool(bias), rule.rule, rule.variant, float(rule.C), batch.dn,
-            batch.dc)
+            batch.dc, int(batch.span))
 
 
 def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
@@ -312,10 +326,12 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
                          hashed: bool = False) -> Scan3Prep:
     """Passes 1-3 of a v3 round into workspace set ``slot`` on ``stream`` (default: the
     current stream; an event marks completion when a stream is given). ``batch.tok``:
-    32-bit category tokens, or (``hashed``) int32 field-aware signed slots, row-major."""
+    32-bit category tokens, (``hashed``) int32 field-aware signed slots, or (``batch.span``
+    > 0) the compact int16 field-aware slots of the engine's wire, row-major."""
     h = native.hip()
     dev = batch.y.device
-    span = (dim - batch.dn - 1) // batch.dc
+    span = _s3_span(batch, dim)
+    mode = _s3_mode(batch, hashed)
     bufs = []
     for i, name in enumerate(S3_BUFS):
         n = int(h.omldm_scan3_ws_words(i, batch.B, R, S, batch.dn, batch.dc, span, int(bias)))
@@ -325,9 +341,9 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
 
     ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
     st = stream if stream is not None else torch.cuda.current_stream(dev)
-    check(h.omldm_scan3_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), int(hashed), batch.dc,
+    check(h.omldm_scan3_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), mode, batch.dc,
                                 batch.B, R, S, dim, int(bias), rule.rule, rule.variant,
-                                float(rule.C), ptrs, st.cuda_stream), "omldm_scan3_prepare")
+                                float(rule.C), span, ptrs, st.cuda_stream), "omldm_scan3_prepare")
     ev = None
     if stream is not None:
         ev = torch.cuda.Event()
@@ -335,11 +351,12 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
     return Scan3Prep(bufs, ptrs, _s3_key(batch, R, S, dim, bias, rule), ev)
 
 
-def scan3_part_bounds(dim: int, dn: int, dc: int, part: int, parts: int) -> tuple[int, int]:
+def scan3_part_bounds(dim: int, dn: int, dc: int, part: int, parts: int,
+                      span: int = 0) -> tuple[int, int]:
     import ctypes
 
     lh = (ctypes.c_longlong * 2)()
-    check(native.hip().omldm_scan3_part_bounds(dim, dn, dc, part, parts, lh),
+    check(native.hip().omldm_scan3_part_bounds(dim, dn, dc, span, part, parts, lh),
           "omldm_scan3_part_bounds")
     return int(lh[0]), int(lh[1])
 
@@ -362,14 +379,15 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
         torch.cuda.current_stream(w.device).wait_event(sp.event)
     h = native.hip()
     parts = max(1, int(parts))
+    span = _s3_span(batch, dim)
     for k in range(parts):
         rc = h.omldm_scan3_run(ptr(w), num.shape[1], batch.dc, ptr(y), int(y.dtype == torch.int8),
                                batch.B, R, S, ptr(dacc), dim, ptr(cum), rule.rule, rule.variant,
-                               rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), sp.ptrs, k, parts,
-                               native.stream_of(w))
+                               rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), span, sp.ptrs, k,
+                               parts, native.stream_of(w))
         check(rc, "omldm_scan3_run")
         if on_part is not None:
-            on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts))
+            on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts, span))
 
 
 def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
@@ -389,12 +407,15 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
     assert w.shape[0] == dim and w.dtype == torch.float32 and dacc.dtype == torch.float32
     assert rule.rule in SEQ_RULES and rule.lam == 0.0, "seq round: PA family / logistic, no L2"
     num, tok, y = batch.num, batch.tok, batch.y
-    assert num.dtype == torch.float32 and tok.dtype == torch.int32
+    assert num.dtype == torch.float32
+    assert tok.dtype == (torch.int16 if batch.span > 0 else torch.int32), tok.dtype
     assert y.dtype == torch.float32 or (y.dtype == torch.int8 and rule.rule != RULE_EPS)
     assert num.is_contiguous() and tok.is_contiguous() and y.is_contiguous()
     assert cum is None or cum.dtype == torch.float64
     if S <= 0 or batch.B == 0:
         return False
+    if batch.span > 0:  # compact slots: the v3 round is the only consumer
+        assert w.is_cuda and scan3_eligible(batch, R, rule.bias) and stats is None
     if w.is_cuda and scan3_eligible(batch, R, rule.bias) and stats is None:
         assert all(t.is_cuda for t in (num, tok, y)) and dacc.is_cuda
         linear_scan3_round(w, batch, R, S, dacc, rule, inv_p, cum, parts, on_part, hashed)

@@ -71,10 +71,10 @@ HIP_SIGS = [
     ("omldm_scan3_fits", i32, [i32, i32, i32, i32]),
     ("omldm_scan3_ws_words", i64, [i32, i32, i32, i32, i32, i32, i64, i32]),
     ("omldm_scan3_prepare", i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, f32,
-                                  vp, vp]),
+                                  i64, vp, vp]),
     ("omldm_scan3_run", i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, f32,
-                              f32, f32, f32, i32, vp, i32, i32, vp]),
-    ("omldm_scan3_part_bounds", i32, [i32, i32, i32, i32, i32, vp]),
+                              f32, f32, f32, i32, i64, vp, i32, i32, vp]),
+    ("omldm_scan3_part_bounds", i32, [i32, i32, i32, i64, i32, i32, vp]),
     ("omldm_scan3_stamps", i32, [vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
     ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
@@ -108,6 +108,8 @@ HIP_SIGS = [
     ("omldm_fgm_begin", i32, [vp, vp, f64, vp]),
     ("omldm_holdout_route", i32, [vp, vp, vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, i64, i64,
                                   i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp]),
+    ("omldm_holdout_route_spokes", i32, [vp, vp, vp, i64, vp, vp, vp, i32, i32, vp, vp, vp, i64,
+                                         vp, vp, i32, i32, i32, i32, vp]),
     ("omldm_json_parse", i32, [vp, vp, i32, i32, i32, i32, i64, i32, vp, vp, vp, vp, vp, vp]),
     ("omldm_copy_engine_create", vp, [i32]),
     ("omldm_copy_engine_destroy", None, [vp]),

@@ -61,7 +61,7 @@ class JobConfig:
     discreteFeatures: int = 0             # discrete features per point (dense slots)
     catFeatures: int = 26                 # categorical features per point (hashed)
     hashDim: int = 1 << 20                # hashed feature space (incl. dense slots, intercept)
-    fieldAware: bool = False              # compact uint16 field-aware categorical slots
+    fieldAware: bool = True               # compact uint16 field-aware slots (read by the v3 scan)
     batchSize: int = 65536                # records per engine tick and rank
     spokesPerDevice: int = 0              # virtual spokes per rank (0: parallelism / world)
     # Creates wait while the job runs below the spoke parallelism it has reached before

@@ -137,7 +137,9 @@ def test_checkpoint_restore_roundtrip(tmp_path):
     assert set(job2.pipes) == {1, 2}
     assert torch.equal(job2.pipes[1].learner.state_vector(), w)
     assert job2.pipes[1].learner.running_totals()["fitted"] == fitted
-    assert job2.holdout.filled == job.holdout.filled
+    assert (job2.holdout.filled == job.holdout.filled).all()
+    for a, b in zip(job2.holdout.test_sets(), job.holdout.test_sets()):
+        assert torch.equal(a.y, b.y)
     assert job2.train_in.offsets == job.consumer_offsets()["train"]
 
 
@@ -160,7 +162,7 @@ def test_shrink_restore_merges_buffers_holdout_and_counters(tmp_path):
     name = uuid.uuid4().hex
     sds = []
     for r in range(2):
-        job, br, _ = make_job(["--testSetSize", "64"], name=f"{name}-{r}")
+        job, br, _ = make_job(["--testSetSize", "16"], name=f"{name}-{r}")
         for rec in synth_json_records(300, SP, seed=r):
             br.produce("trainingData", rec)
         job.tick()                               # no pipeline yet → records buffered
@@ -182,14 +184,16 @@ def test_shrink_restore_merges_buffers_holdout_and_counters(tmp_path):
     (d / "manifest.json").write_text(json.dumps({"index": 0, "world": 2, "time": 0,
                                                  "ticks": 2, "pipelines": [1]}))
     job2, _, _ = make_job(["--restore", "true", "--stateBackend", f"file://{tmp_path}",
-                           "--testSetSize", "64"], name=f"{name}-new")
+                           "--testSetSize", "16"], name=f"{name}-new")
     assert job2._buffered == 40 + 41
     fit = [sd["pipelines"][1]["learner"]["cum"][1].item() for sd in sds]
     assert job2.pipes[1].learner.running_totals()["fitted"] == int(sum(fit))
-    held = sum(sd["holdout"]["filled"] for sd in sds)
+    held = sum(sum(sd["holdout"]["filled"]) for sd in sds)
     spill = job2._restored_train.B if getattr(job2, "_restored_train", None) is not None else 0
-    assert job2.holdout.filled + spill == held
-    assert job2.holdout.filled == job2.holdout.size == 64 and spill == held - 64 > 0
+    # 2 ranks × 4 spokes → 4 spokes: each new spoke merges two old rings, keeps 16 points
+    assert job2.holdout.n_test + spill == held
+    assert (job2.holdout.filled == job2.holdout.size).all() and job2.holdout.size == 16
+    assert spill == held - 4 * 16 > 0
     assert job2.counters["records"] == sum(sd["counters"]["records"] for sd in sds)
     job2.tick()  # the spilled holdout rows are trained on (not held out again)
     assert job2.pipes[1].learner.running_totals()["fitted"] >= int(sum(fit)) + spill

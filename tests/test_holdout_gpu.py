@@ -17,11 +17,13 @@ def _batch(sp, B, base, dev):
 
 
 @pytest.mark.parametrize("field_aware", [False, True])
-@pytest.mark.parametrize("size", [1, 7, 256])
-def test_device_route_matches_host(cuda, field_aware, size):
+@pytest.mark.parametrize("size,spokes", [(1, 1), (7, 1), (256, 1), (7, 5), (256, 16)])
+def test_device_route_matches_host(cuda, field_aware, size, spokes):
+    """The per-spoke device routing (omldm_holdout_route_spokes) moves the same rows
+    into the same places as the host index path, ring by ring."""
     sp = FeatureSpace(3, 1, 5, 1 << 16, field_aware=field_aware)
-    dev = HoldoutSet(sp, size, cuda)
-    ref = HoldoutSet(sp, size, "cpu")
+    dev = HoldoutSet(sp, size, cuda, spokes=spokes)
+    ref = HoldoutSet(sp, size, "cpu", spokes=spokes)
     rng = np.random.default_rng(size)
     base = 0
     for step in range(40):
@@ -34,7 +36,9 @@ def test_device_route_matches_host(cuda, field_aware, size):
         assert torch.equal(out_d.y.cpu(), out_h.y), step
         assert torch.equal(out_d.num.cpu(), out_h.num)
         assert torch.equal(out_d.cat.cpu(), out_h.cat)
-        assert (dev.count, dev.head, dev.filled) == (ref.count, ref.head, ref.filled)
+        assert out_d.shards == out_h.shards
+        for a, b in ((dev.count, ref.count), (dev.head, ref.head), (dev.filled, ref.filled)):
+            assert np.array_equal(a, b)
         t_d, t_h = dev.test_set(), ref.test_set()
         assert torch.equal(t_d.y.cpu(), t_h.y)
         assert torch.equal(t_d.cat.cpu(), t_h.cat)
