@@ -8,15 +8,21 @@ Prediction-out latency is one predict.
 
 Here the engine's tick batches training rows (throughput); forecasting records take a
 separate low-latency lane: a host thread consumes the forecasting topic, parses each
-record natively (csrc/host/ingest.cpp, the same hashing as the GPU parser), hands it to
-the PERSISTENT serving wavefront (csrc/kernels/serving.hip: one resident wave polling a
-coherent pinned mailbox; no kernel launch, no stream synchronisation per request) that
-scores it against every hashed-linear pipeline of the HBM model store in one pass, and
-produces one Prediction per pipeline. The wave reads the live weights the training
-rounds update (at most one round stale, like a reference spoke between two syncs).
+record natively (csrc/host/ingest.cpp, the same hashing as the GPU parser) and answers
+it for EVERY pipeline before taking the next one:
 
-Pipelines the wave cannot score (a preprocessor in front, dense learners) keep the
-batched path: while any exists, records are handed to the tick (``take_fallback``).
+* hashed-linear pipelines of the HBM model store (no preprocessor) are scored together
+  by the PERSISTENT serving wavefront (csrc/kernels/serving.hip: one resident wave
+  polling a coherent pinned mailbox; no kernel launch, no stream synchronisation per
+  request);
+* every other pipeline — preprocessors in front (StandardScaler, MinMaxScaler,
+  PolynomialFeatures), ORR, MultiClassPA, K-means, NN, Hoeffding tree — runs its own
+  predict kernels on a one-row batch on the lane's HIP stream (one stream sync per
+  record).
+
+Both read the live models the training rounds update (at most one round stale, like a
+reference spoke between two syncs). Records wait for the tick (``take_fallback``) only
+while no pipeline exists yet.
 """
 from __future__ import annotations
 
@@ -67,7 +73,11 @@ class ForecastServer:
         self._server = None
         self._spec = None             # (first store row, end row, bias) the wave serves
         self._served: list = []       # (pipeline id, store row, classification?) in W order
+        self._direct: list = []       # (pipeline id, Pipeline): one-row predicts on the lane
+        self._order: list = []        # every served pipeline id, in id order
         self._row0 = 0
+        self._stream = None           # the lane's HIP stream (direct predicts)
+        self.family_latency: dict = {}  # learner name → deque of µs (record in → outputs out)
         self.fallback: collections.deque = collections.deque()
         self.latency_us: collections.deque = collections.deque(maxlen=1 << 16)
         self.served = 0
@@ -106,43 +116,51 @@ class ForecastServer:
             self._server = None
 
     def suspend(self) -> None:
-        """Before the model store may move (a Create can grow its arena): the wave stops
-        reading it until ``reconfigure``."""
+        """Before the model store may move (a Create can grow its arena) or pipelines
+        change: the lane stops serving until ``reconfigure``."""
         with self.lock:
             self._stop_wave()
             self._spec = None
             self._served = []
+            self._direct = []
+            self._order = []
 
     def reconfigure(self) -> None:
-        """After a Create / Delete / restore (main thread): serve the model-store
-        pipelines with the wave when every pipeline lives in the store, else hand all
-        records to the batched path. The wave itself starts with the first record: a
-        resident wave holds one of the process's hardware queues (4 on this pool), which
-        costs the training tick's copy / parse / compute overlap while no forecast
-        arrives (engine end-to-end 33 → 15 M records/s with an idle resident wave)."""
+        """After a Create / Delete / restore (main thread): the model-store pipelines of
+        the most common bias go to the wave, every other pipeline to one-row predicts on
+        the lane's stream. The wave itself starts with the first record: a resident wave
+        holds one of the process's hardware queues (4 on this pool), which costs the
+        training tick's copy / parse / compute overlap while no forecast arrives (engine
+        end-to-end 33 → 15 M records/s with an idle resident wave)."""
         with self.lock:
             self._stop_wave()
             self._spec = None
-            self._served = []
-            if os.environ.get("OMLDM_FS_NOWAVE"):  # diagnostics: the lane without the wave
-                return
+            self._served, self._direct, self._order = [], [], []
             pipes = [self.job.pipes[pid] for pid in sorted(self.job.pipes)]
-            if not pipes or any(p.store is None for p in pipes):
-                return
-            biases = {bool(p.learner.rule.bias) for p in pipes}
-            if len(biases) != 1:
-                return
-            rows = [p.store_row for p in pipes]
-            lo, hi = min(rows), max(rows) + 1
-            self._spec = (lo, hi, biases.pop())
-            self._row0 = lo
-            self._served = [(p.id, p.store_row, p.learner.TASK == "classification")
-                            for p in pipes]
+            self._order = [p.id for p in pipes]
+            store = [p for p in pipes if p.store is not None]
+            if os.environ.get("OMLDM_FS_NOWAVE") or self.job.device.type != "cuda":
+                store = []  # diagnostics / CPU jobs: the lane without the wave
+            if store:
+                by_bias: dict = {}
+                for p in store:
+                    by_bias.setdefault(bool(p.learner.rule.bias), []).append(p)
+                bias, store = max(by_bias.items(), key=lambda kv: len(kv[1]))
+                rows = [p.store_row for p in store]
+                lo, hi = min(rows), max(rows) + 1
+                self._spec = (lo, hi, bias)
+                self._row0 = lo
+                self._served = [(p.id, p.store_row, p.learner.TASK == "classification")
+                                for p in store]
+            waved = {pid for pid, _, _ in self._served}
+            self._direct = [(p.id, p) for p in pipes if p.id not in waved]
+            if self._direct and self._stream is None and self.job.device.type == "cuda":
+                self._stream = torch.cuda.Stream(self.job.device)
 
     @property
     def serving(self) -> bool:
-        """Records are answered by the wave (else they go to the batched path)."""
-        return self._spec is not None
+        """Records are answered on the lane (else they wait in the fallback queue)."""
+        return bool(self._order)
 
     def _ensure_wave(self):
         """Under the lock: a live wave over the configured store rows (started on the
@@ -198,33 +216,80 @@ class ForecastServer:
             self._cat32[: sp.dc] = self._cat.numpy()[0]
         return int(self._op[0]) == OP_FORECASTING
 
+    def _predict_direct(self, pipe) -> float:
+        """One-row predict of a pipeline the wave does not score, on the lane's stream."""
+        from omldm_amd.api.batch import HashedBatch
+
+        dev = self.job.device
+        b = HashedBatch(self._num, self._cat, self._y, None, self.space.cat_span)
+        if self._stream is None:
+            return float(pipe.predict(b.to(dev))[0])
+        with torch.cuda.stream(self._stream):
+            out = pipe.predict(b.to(dev, non_blocking=False))
+            return float(out.float()[0].item())
+
     def serve_one(self, rec: bytes, t_in: float | None = None) -> bool:
-        """Answers one forecasting record with the wave. False: not served here (no
-        wave, or a pipeline it cannot score) — the caller keeps it for the tick."""
+        """Answers one forecasting record for every pipeline (wave + one-row predicts).
+        False: no pipeline yet — the caller keeps it for the tick."""
         t_in = time.perf_counter() if t_in is None else t_in
         with self.lock:
-            if self._spec is None:
+            if not self._order:
                 return False
             if not self._parse(rec):
                 self.invalid += 1
                 return True
-            cat = self._cat32.ctypes.data
-            srv = self._ensure_wave()
-            try:
-                out = srv.request_raw(self._num.data_ptr(), cat)
-            except TimeoutError:  # the wave's lifetime ended under the request
-                self._stop_wave()
-                out = self._ensure_wave().request_raw(self._num.data_ptr(), cat)
+            preds: dict = {}
+            t_w = None
+            if self._spec is not None:
+                cat = self._cat32.ctypes.data
+                srv = self._ensure_wave()
+                try:
+                    out = srv.request_raw(self._num.data_ptr(), cat)
+                except TimeoutError:  # the wave's lifetime ended under the request
+                    self._stop_wave()
+                    out = self._ensure_wave().request_raw(self._num.data_ptr(), cat)
+                for pid, row, cls in self._served:
+                    s = float(out[row - self._row0])
+                    preds[pid] = (1.0 if s >= 0 else -1.0) if cls else s
+                t_w = time.perf_counter()
+            fam_t: list = []
+            for pid, pipe in self._direct:
+                t0 = time.perf_counter()
+                preds[pid] = self._predict_direct(pipe)
+                fam_t.append((pipe.learner.NAME, time.perf_counter() - t0))
             raw = RawRecords(np.frombuffer(rec, dtype=np.uint8),
                              np.zeros(1, dtype=np.int64), np.array([len(rec)], dtype=np.int64))
-            for pid, row, cls in self._served:
-                s = float(out[row - self._row0])
-                p = (1.0 if s >= 0 else -1.0) if cls else s
-                block, offs = format_predictions(raw, pid, [p])
+            for pid in self._order:
+                block, offs = format_predictions(raw, pid, [preds[pid]])
                 self.broker.produce(self.topic, block[:int(offs[1]) - 1])
             self.served += 1
-        self.latency_us.append((time.perf_counter() - t_in) * 1e6)
+        t_out = time.perf_counter()
+        self.latency_us.append((t_out - t_in) * 1e6)
+        # per learner family: the record's parse + wave (store learners) or parse + its
+        # own one-row predict (the others), as if it were the only pipeline
+        base = (t_w - t_in) if t_w is not None else 0.0
+        if t_w is not None:
+            for pid, _, _ in self._served:
+                self._fam("linear-store", base)
+        for name, dt in fam_t:
+            self._fam(name, (base if t_w is None else 0.0) + dt)
         return True
+
+    def _fam(self, name: str, seconds: float) -> None:
+        q = self.family_latency.get(name)
+        if q is None:
+            q = self.family_latency[name] = collections.deque(maxlen=1 << 14)
+        q.append(seconds * 1e6)
+
+    def family_percentiles(self) -> dict:
+        out = {}
+        for name, q in list(self.family_latency.items()):
+            lat = sorted(q)
+            if lat:
+                out[name] = {"p50": round(lat[len(lat) // 2], 2),
+                             "p99": round(lat[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
+                             "n": len(lat)}
+        return out
 
     def catch_up(self, timeout_s: float = 5.0) -> bool:
         """Waits until every forecasting record in the topic when called is answered (or
@@ -248,6 +313,8 @@ class ForecastServer:
         return any(br.end_offset(topic, p) > o for p, o in offs.items())
 
     def _run(self) -> None:
+        if self.job.device.type == "cuda":
+            torch.cuda.set_device(self.job.device)
         last = 0.0
         idle_marked = False
         while not self._stop.is_set():

@@ -312,7 +312,7 @@ class Job:
                 self.counters["predictions"] += len(preds)
 
     def _forecast_fallback(self) -> None:
-        """Forecasting records the serving wave handed back (a pipeline it cannot score):
+        """Forecasting records the lane handed back (no pipeline existed when they came):
         predicted in one batch by every pipeline, like the batched path."""
         recs = self.fserver.take_fallback()
         if not recs:
@@ -531,6 +531,8 @@ class Job:
         fsl = self.fserver.latency_percentiles() if self.fserver is not None else None
         return {"ranks": self.world, "spokesPerRank": self.spokes,
                 "forecastRecordLatencyUs": fsl,
+                "forecastRecordLatencyUsPerLearner":
+                    self.fserver.family_percentiles() if self.fserver is not None else None,
                 "trainedExamples": self._trained_global,
                 "examplesPerSec": round(self._trained_global / max(duration_ms, 1) * 1e3, 1),
                 "forecastBatchLatencyMs": {"p50": pct(0.5), "p99": pct(0.99)},

@@ -108,6 +108,16 @@ HIP_SIGS = [
     ("omldm_fgm_begin", i32, [vp, vp, f64, vp]),
     ("omldm_holdout_route", i32, [vp, vp, vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, i64, i64,
                                   i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp]),
+    ("omldm_ipc_alloc", vp, [i64]),
+    ("omldm_ipc_free", i32, [vp]),
+    ("omldm_ipc_handle", i32, [vp, vp]),
+    ("omldm_ipc_handle_size", i32, []),
+    ("omldm_ipc_open", vp, [vp]),
+    ("omldm_ipc_close", i32, [vp]),
+    ("omldm_copy_d2d", i32, [vp, vp, i64, vp]),
+    ("omldm_p2p_delta", i32, [vp, vp, vp, vp, i64, vp]),
+    ("omldm_p2p_axpy", i32, [vp, vp, f32, i64, vp]),
+    ("omldm_p2p_install", i32, [vp, vp, vp, vp, i64, vp]),
     ("omldm_holdout_route_spokes", i32, [vp, vp, vp, i64, vp, vp, vp, i32, i32, vp, vp, vp, i64,
                                          vp, vp, i32, i32, i32, i32, vp]),
     ("omldm_json_parse", i32, [vp, vp, i32, i32, i32, i32, i64, i32, vp, vp, vp, vp, vp, vp]),

@@ -322,6 +322,8 @@ class _PointToPoint(Protocol):
 
     def load_state_dict(self, sd):
         super().load_state_dict(sd)
+        if self._ps is not None:
+            self._ps.close()
         self._ps = None  # re-seeded from the restored model at the next round
 
 

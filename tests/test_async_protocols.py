@@ -14,6 +14,8 @@ import sys
 import tempfile
 import textwrap
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 WORKER = textwrap.dedent(r"""
@@ -29,14 +31,15 @@ WORKER = textwrap.dedent(r"""
     from omldm_amd.parallel.protocols import make_protocol
 
     proto_name, seconds, slow = sys.argv[2], float(sys.argv[3]), int(sys.argv[4])
+    dev = sys.argv[6]  # "cpu", or "cuda": every rank on cuda:0, the device data plane
     dist.init_process_group("gloo")
     comm = Comm()
     rank, world = comm.rank, comm.world
     space = FeatureSpace(13, 0, 26, 1 << 12)
-    lrn = SVM({"variant": "PA-I"}, space, "cpu")
+    lrn = SVM({"variant": "PA-I"}, space, dev)
     cfg = {"virtualSpokes": 2, "staleness": 2, "_tag": 3}
     proto = make_protocol(proto_name, comm, lrn, cfg)
-    pool = [synth_raw(space, 256, start=(k * world + rank) * 256, seed=25).hashed(space)
+    pool = [synth_raw(space, 256, start=(k * world + rank) * 256, seed=25).hashed(space).to(dev)
             for k in range(16)]
     dist.barrier()
     t0 = time.time()
@@ -49,10 +52,12 @@ WORKER = textwrap.dedent(r"""
         k += 1
     proto.finalize()
     elapsed = time.time() - t0
-    test = synth_raw(space, 4000, start=10**9, seed=25).hashed(space)
+    test = synth_raw(space, 4000, start=10**9, seed=25).hashed(space).to(dev)
     acc = float(((L.linear_predict(lrn.w, test) >= 0).float() * 2 - 1 == test.y).float().mean())
+    ps = getattr(proto, "_ps", None)
     out = {"rank": rank, "rounds": k, "elapsed": elapsed, "acc": acc, "w0": float(lrn.w[5]),
            "max_lead": getattr(proto, "max_lead", None),
+           "plane": ps.plane if ps is not None else None,
            "collectives": comm.stats.collectives}
     with open(os.path.join(sys.argv[5], f"rank{rank}.json"), "w") as f:
         json.dump(out, f)
@@ -69,7 +74,7 @@ def _port():
     return p
 
 
-def _run(proto, seconds=2.5, slow=1, world=3):
+def _run(proto, seconds=2.5, slow=1, world=3, dev="cpu"):
     outdir = tempfile.mkdtemp(prefix="omldm_async_")
     script = os.path.join(outdir, "worker.py")
     with open(script, "w") as f:
@@ -78,7 +83,8 @@ def _run(proto, seconds=2.5, slow=1, world=3):
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
                           "--master-port", str(_port()), script, ROOT, proto, str(seconds),
-                          str(slow), outdir], capture_output=True, text=True, timeout=120, env=env)
+                          str(slow), outdir, dev], capture_output=True, text=True, timeout=120,
+                         env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     res = {}
     for r in range(world):
@@ -113,3 +119,19 @@ def test_synchronous_is_paced_by_the_straggler_for_contrast():
     # 20 lock-step rounds: the fast ranks wait out the straggler's 20 x 50 ms
     assert r[0]["elapsed"] >= 0.9 and r[2]["elapsed"] >= 0.9, r
     assert r[0]["w0"] == r[1]["w0"] == r[2]["w0"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("proto", ["Asynchronous", "SSP"])
+def test_device_plane_on_gpu(proto):
+    """Three ranks on cuda:0: pushes and replies move through the IPC mailboxes (no
+    model-sized host copy per round); same protocol guarantees as on the host plane."""
+    r = _run(proto, seconds=2.0, dev="cuda")
+    assert all(x["plane"] == "device" for x in r.values()), r
+    assert r[0]["w0"] == r[1]["w0"] == r[2]["w0"]
+    slow = r[1]["rounds"]
+    if proto == "SSP":
+        assert r[0]["rounds"] <= slow + 4 and r[0]["max_lead"] <= 2, r
+    else:
+        assert r[0]["rounds"] >= 3 * slow and r[2]["rounds"] >= 3 * slow, r
+    assert min(x["acc"] for x in r.values()) > 0.6, r

@@ -3,7 +3,8 @@
 
 * every forecasting record gets one Prediction per pipeline, equal to the batched predict
   of the same model;
-* pipelines the wave cannot score (a dense learner) send records to the batched path;
+* pipelines the wave cannot score (preprocessors, dense learners) are answered per record
+  by one-row predicts on the lane's stream;
 * the record-in → Prediction-out latency is measured per record.
 """
 import json
@@ -78,23 +79,47 @@ def test_wave_answers_every_record_like_the_batched_predict():
     assert perf["metrics"]["forecastRecordLatencyUs"]["n"] == 40
 
 
-def test_dense_pipeline_sends_records_to_the_batched_path():
+def test_every_pipeline_kind_is_answered_per_record():
+    """SVM (wave), SVM behind a StandardScaler, NN, ORR, MultiClassPA, K-means and a
+    Hoeffding tree in one job: every forecasting record is answered on the lane for all
+    seven pipelines (one-row predicts on the lane's stream for the six the wave does not
+    score), equal to the batched predict of the same models; latency per family."""
     job, br = _job()
-    _create(br, 1, "SVM")
-    _create(br, 2, "NN", {"hiddenLayers": [8]})
-    for r in synth_json_records(4000, SP):
+    specs = [(1, "SVM", None, None), (2, "SVM", None, ["StandardScaler"]),
+             (3, "NN", {"hiddenLayers": [8]}, None), (4, "ORR", None, ["MinMaxScaler"]),
+             (5, "MultiClassPA", {"nClasses": 2}, None), (6, "K-means", {"k": 3}, None),
+             (7, "HT", {"nClasses": 2}, ["PolynomialFeatures"])]
+    for pid, name, hyper, pre in specs:
+        br.produce("requests", json.dumps({
+            "id": pid, "request": "Create",
+            "learner": {"name": name, "hyperParameters": hyper or {}},
+            "preProcessors": [{"name": p} for p in (pre or [])],
+            "trainingConfiguration": {"protocol": "Synchronous"}}))
+    for r in synth_json_records(6000, SP):
         br.produce("trainingData", r)
-    for _ in range(3):
+    for _ in range(4):
         job.tick()
-    assert not job.fserver.serving  # the NN is not in the model store
-    for r in synth_json_records(10, SP, start=50000, operation="forecasting"):
+    fs = job.fserver
+    assert fs.serving and [pid for pid, _, _ in fs._served] == [1]
+    assert [pid for pid, _ in fs._direct] == [2, 3, 4, 5, 6, 7]
+    fc = synth_json_records(12, SP, start=70000, operation="forecasting")
+    for r in fc:
         br.produce("forecastingData", r)
-    for _ in range(2):
-        job.tick()
-    preds = [json.loads(x) for x in br.records("predictions")]
-    assert sorted(p["mlpId"] for p in preds) == [1] * 10 + [2] * 10
-    # deleting the dense pipeline brings the wave back
-    br.produce("requests", json.dumps({"id": 2, "request": "Delete"}))
     job.tick()
-    assert job.fserver.serving
+    assert not fs.fallback and fs.served == 12
+    preds = [json.loads(x) for x in br.records("predictions")]
+    assert sorted(p["mlpId"] for p in preds) == sorted(list(range(1, 8)) * 12)
+    batch, _, _ = parse_records(fc, SP)
+    batch = batch.without_raw().to("cuda")
+    for pid, name, _, _ in specs:
+        want = job.pipes[pid].predict(batch).float().cpu()
+        got = torch.tensor([p["prediction"] for p in preds if p["mlpId"] == pid])
+        assert torch.allclose(got, want, rtol=1e-4, atol=1e-4), (name, got, want)
+    fam = fs.family_percentiles()
+    assert set(fam) >= {"linear-store", "SVM", "NN", "ORR", "MultiClassPA", "K-means", "HT"}, fam
+    assert all(v["n"] >= 12 and v["p50"] < 20000 for v in fam.values()), fam
+    # deleting pipelines reconfigures the lane; the rest keep being answered
+    br.produce("requests", json.dumps({"id": 3, "request": "Delete"}))
+    job.tick()
+    assert [pid for pid, _ in fs._direct] == [2, 4, 5, 6, 7]
     job.fserver.close()
