@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import collections
 import json
+import os
 import time
 
 import numpy as np
@@ -166,6 +167,28 @@ class Job:
         if self.fserver is not None:
             self.fserver.reconfigure()
             self.fserver.start()
+        # diagnostics / multi-rank tests: a per-tick digest of every pipeline's model
+        # (replica agreement across ranks) and the final models, under this directory
+        self._trace_dir = os.environ.get("OMLDM_TRACE_MODELS") or None
+
+    def _trace_models(self, final: bool = False) -> None:
+        os.makedirs(self._trace_dir, exist_ok=True)
+        if final:
+            for pid, pipe in self.pipes.items():
+                torch.save(pipe.learner.state_vector().detach().cpu(),
+                           os.path.join(self._trace_dir, f"rank{self.rank}_final_{pid}.pt"))
+            return
+        import zlib
+
+        recs = []
+        for pid in sorted(self.pipes):
+            v = self.pipes[pid].learner.state_vector().detach().float().cpu().contiguous()
+            recs.append({"tick": self.ticks, "pid": pid,
+                         "protocol": self.pipes[pid].protocol_name,
+                         "crc": zlib.crc32(v.numpy().tobytes()), "sum": float(v.double().sum())})
+        with open(os.path.join(self._trace_dir, f"rank{self.rank}.jsonl"), "a") as f:
+            for r in recs:
+                f.write(json.dumps(r) + "\n")
 
     def _coll_device(self):
         return self.device if self.comm.backend == "nccl" else torch.device("cpu")
@@ -481,6 +504,8 @@ class Job:
         self._trained_global += int(n_train)
         if self.pipes and n_train > 0:
             self._train(tb, spill)
+            if self._trace_dir:
+                self._trace_models()
         for q in queries:
             self._answer(q)
         with tracing.range("learning_curve"):
@@ -545,6 +570,8 @@ class Job:
             self.tick()
         for p in self.pipes.values():
             p.protocol.finalize()
+        if self._trace_dir:
+            self._trace_models(final=True)
         if self.fserver is not None:
             self.fserver.close()
         self.ingest.close()

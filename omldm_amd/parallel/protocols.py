@@ -617,10 +617,37 @@ class FGM(_Monitored):
 
 class SingleLearner(Protocol):
     """Workers forward training points to the hub rank, which alone trains (HT, K-means);
-    reference: ForwardingWorker + CentralizedMLServer (MLNodeGenerator.scala:27,56)."""
+    reference: ForwardingWorker + CentralizedMLServer (MLNodeGenerator.scala:27,56).
+
+    The other ranks keep a replica only to serve forecasts and queries: the hub model is
+    broadcast every ``broadcastEvery`` rounds (default 8) and whenever the replicas are
+    read collectively — before a query, a checkpoint or the end of the stream
+    (``finalize``) — instead of G× the model bytes every round. Forecasts on a non-hub
+    rank may therefore lag the hub by up to ``broadcastEvery`` − 1 rounds."""
 
     NAME = "SingleLearner"
     HUB = 0
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.every = max(1, _cfg_int(self.cfg, "broadcastEvery", 8))
+        self._stale = 0  # rounds since the replicas last received the hub model
+
+    def _broadcast(self) -> None:
+        L = self.learner
+        v = L.state_vector()
+        self.comm.broadcast_(v, src=self.HUB)
+        L.on_state_loaded()
+        self._account_model_sync(L.num_params(), v.numel() * v.element_size())
+        self._stale = 0
+
+    def finalize(self) -> None:
+        if self.G > 1 and self._stale:
+            self._broadcast()
+
+    def state_dict(self):
+        self.finalize()
+        return super().state_dict()
 
     def round(self, batch):
         L = self.learner
@@ -633,13 +660,11 @@ class SingleLearner(Protocol):
                                  torch.cat(parts["y"]), None)
             L.fit(merged, RoundContext(spokes=1))
         self._account_small(self.G, batch.B)  # forwarded points
-        # hub → spokes: serve forecasts from an up-to-date replica
-        v = L.state_vector()
-        if self.G > 1:
-            self.comm.broadcast_(v, src=self.HUB)
-            L.on_state_loaded()
-            self._account_model_sync(L.num_params(), v.numel() * v.element_size())
         self.stats.rounds += 1
+        if self.G > 1:  # hub → replicas, every `every` rounds (finalize: on demand)
+            self._stale += 1
+            if self._stale >= self.every:
+                self._broadcast()
 
 
 PROTOCOLS = {c.NAME: c for c in (CentralizedTraining, Synchronous, Asynchronous, SSP, EASGD, GM,

@@ -109,14 +109,17 @@ def test_monitoring_one_small_reduction_or_one_sync_per_round(world, proto, tag,
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_single_learner_points_to_hub_only(world):
-    res = run(world, "K-means", "SingleLearner", rounds=3)
+    """Points go to the hub only; the hub model reaches the replicas every
+    ``broadcastEvery`` rounds (here 2), not every round."""
+    res = run(world, "K-means", "SingleLearner", {"broadcastEvery": 2}, rounds=3)
     nb = res[0]["model_bytes"]
-    assert res[0]["rounds"] == [[("broadcast", "bcast", nb)]] * 3  # the hub receives only
+    bc = ("broadcast", "bcast", nb)
+    assert res[0]["rounds"] == [[], [bc], []]  # the hub receives only
     for r in res[1:]:
-        for calls in r["rounds"]:
+        for k, calls in enumerate(r["rounds"]):
             sends = [c for c in calls if c[0] == "p2p_send"]
             assert [c[1] for c in sends] == ["gather"] * 3  # num, cat, y → hub
-            assert calls[-1] == ("broadcast", "bcast", nb)
+            assert (calls[-1] == bc) == (k == 1), (k, calls)
             assert not [c for c in calls if c[0] in ("all_reduce", "reduce+bcast")]
 
 
