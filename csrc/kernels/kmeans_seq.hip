@@ -1,0 +1,140 @@
+// Exact sequential (MacQueen) online k-means: the reference learner's per-point update
+// (nearest centroid, c ← c + (x − c)/n_c; the spoke fits one point
+// at a time, omldm/operators/spoke/FlinkSpoke.scala:92-107; K-means runs as SingleLearner,
+// :203-209), at GPU speed for k ≤ 64.
+//
+// One wavefront owns the whole model in REGISTERS: lane j holds centroid j (its d ≤ DM
+// coordinates) and its count n_j. Points stream in 64-row chunks, lane t holding point t
+// of the chunk; step s broadcasts point s with v_readlane (scalar registers), every lane
+// computes its centroid's squared distance, a DPP/readlane argmin picks j*, and lane j*
+// moves its centroid — no LDS, no barrier, no memory access on the per-point chain.
+// Seeding: while fewer than k centroids exist (n_j = 0), a point becomes the next
+// centroid (n = 1). Rows with a NaN target are not training points and are skipped.
+#include "common.h"
+
+namespace omldm {
+namespace {
+
+// (value, lane) minimum over the wave, ties to the lowest lane; wave-uniform result.
+__device__ __forceinline__ int wave_argmin(float v) {
+  const int lane = threadIdx.x & 63;
+  int idx = lane;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const float ov = __shfl_xor(v, d);
+    const int oi = __shfl_xor(idx, d);
+    if (ov < v || (ov == v && oi < idx)) {
+      v = ov;
+      idx = oi;
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(idx);
+}
+
+template <int DM>
+__global__ __launch_bounds__(64) void kmeans_seq_kernel(const float* __restrict__ x, int ldx,
+                                                        const float* __restrict__ y, int B,
+                                                        int d, int k, float* __restrict__ cent,
+                                                        float* __restrict__ cnt,
+                                                        double* __restrict__ cum) {
+  const int lane = threadIdx.x;
+  const bool mine = lane < k;
+  float c[DM];
+#pragma unroll
+  for (int i = 0; i < DM; ++i) c[i] = (mine && i < d) ? cent[(size_t)lane * d + i] : 0.f;
+  float n = mine ? cnt[lane] : 0.f;
+  // seeded centroids: a prefix (seeding fills them in order)
+  int seeded = __popcll(__builtin_amdgcn_ballot_w64(mine && n > 0.f));
+  double inertia = 0.0, fitted = 0.0;
+  float xr[DM];
+  float yr;
+  auto load = [&](int r0) {
+    const int r = r0 + lane;
+    const bool ok = r < B;
+#pragma unroll
+    for (int i = 0; i < DM; ++i) xr[i] = (ok && i < d) ? x[(size_t)r * ldx + i] : 0.f;
+    yr = ok ? (y ? y[r] : 0.f) : __builtin_nanf("");
+  };
+  load(0);
+  for (int r0 = 0; r0 < B; r0 += 64) {
+    float xc[DM];
+#pragma unroll
+    for (int i = 0; i < DM; ++i) xc[i] = xr[i];
+    const float yc = yr;
+    if (r0 + 64 < B) load(r0 + 64);  // the next chunk's loads fly under this chunk's steps
+    // training points of this chunk (non-NaN target, inside the batch)
+    unsigned long long live = __builtin_amdgcn_ballot_w64(yc == yc);
+    while (live) {
+      const int s = __builtin_ctzll(live);
+      live &= live - 1;
+      float xs[DM];
+#pragma unroll
+      for (int i = 0; i < DM; ++i)
+        xs[i] = i < d ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                                      __builtin_bit_cast(int, xc[i]), s))
+                      : 0.f;
+      fitted += 1.0;
+      if (seeded < k) {  // wave-uniform
+        if (lane == seeded) {
+#pragma unroll
+          for (int i = 0; i < DM; ++i) c[i] = xs[i];
+          n = 1.f;
+        }
+        ++seeded;
+        continue;
+      }
+      float dist = 0.f;
+#pragma unroll
+      for (int i = 0; i < DM; ++i) {
+        const float t = xs[i] - c[i];
+        dist = fmaf(t, t, dist);
+      }
+      const int j = wave_argmin(mine ? dist : __builtin_inff());
+      inertia += (double)__builtin_bit_cast(
+          float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, dist), j));
+      if (lane == j) {
+        n += 1.f;
+        const float a = 1.f / n;
+#pragma unroll
+        for (int i = 0; i < DM; ++i) c[i] = fmaf(a, xs[i] - c[i], c[i]);
+      }
+    }
+  }
+  if (mine) {
+#pragma unroll
+    for (int i = 0; i < DM; ++i)
+      if (i < d) cent[(size_t)lane * d + i] = c[i];
+    cnt[lane] = n;
+  }
+  if (lane == 0 && cum) {
+    cum[0] += inertia;
+    cum[1] += fitted;
+  }
+}
+
+}  // namespace
+}  // namespace omldm
+
+using namespace omldm;
+
+OMLDM_API int omldm_kmeans_seq_fits(int d, int k) { return d >= 1 && d <= 64 && k >= 1 && k <= 64; }
+
+// x [B, ldx] fp32 (first d columns used), y [B] (NaN: not a training point; nullptr: all
+// train), cent [k, d], cnt [k], cum (cum[0] += Σ squared distance to the chosen
+// centroid, cum[1] += points fitted) — all device pointers; one wave, one launch.
+OMLDM_API int omldm_kmeans_seq(const float* x, int ldx, const float* y, int B, int d, int k,
+                               float* cent, float* cnt, double* cum, void* stream) {
+  if (!omldm_kmeans_seq_fits(d, k) || ldx < d) return -1;
+  if (B <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (d <= 16)
+    hipLaunchKernelGGL(kmeans_seq_kernel<16>, dim3(1), dim3(64), 0, st, x, ldx, y, B, d, k, cent,
+                       cnt, cum);
+  else if (d <= 32)
+    hipLaunchKernelGGL(kmeans_seq_kernel<32>, dim3(1), dim3(64), 0, st, x, ldx, y, B, d, k, cent,
+                       cnt, cum);
+  else
+    hipLaunchKernelGGL(kmeans_seq_kernel<64>, dim3(1), dim3(64), 0, st, x, ldx, y, B, d, k, cent,
+                       cnt, cum);
+  return (int)hipGetLastError();
+}

@@ -136,10 +136,16 @@ class ORR(Learner):
 
 # ------------------------------------------------------------------------- K-means
 class KMeans(Learner):
-    """Online (sequential) k-means; a micro-batch moves each centroid by
-    c ← (n·c + Σx)/(n + m) — the sequential update c ← c + (x − c)/n with assignments
-    taken against the batch-start centroids. Runs in SingleLearner mode (the reference
-    forces it for K-means: omldm/operators/spoke/FlinkSpoke.scala:203-209)."""
+    """Online k-means. Runs in SingleLearner mode (the reference forces it for K-means:
+    omldm/operators/spoke/FlinkSpoke.scala:203-209).
+
+    ``mode: "sequential"`` (default for k ≤ 64, d ≤ 64): the reference learner's exact
+    per-point update — each training point, in stream order, moves its nearest centroid by
+    c ← c + (x − c)/n_c; the first k points seed the centroids (csrc/kernels/kmeans_seq.hip:
+    one wavefront holds the model in registers). ``mode: "minibatch"``: assignments of a
+    whole micro-batch against the batch-start centroids on the matrix cores, then
+    c ← (n·c + Σx)/(n + m) (the same update summed over the batch; tests pin its quality
+    gap against the sequential form)."""
 
     NAME = "K-means"
     TASK = "clustering"
@@ -160,9 +166,17 @@ class KMeans(Learner):
         self._cnt = torch.zeros_like(self.n)
         self._inert = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._seeded = 0
+        self._retune()
+
+    def _retune(self) -> None:
+        mode = str(self.hyper.get("mode", "sequential")).lower()
+        self.sequential = mode != "minibatch" and D.kmeans_seq_fits(self.d, self.k)
 
     def fit(self, batch, ctx):
         if batch.B == 0:
+            return
+        if self.sequential:
+            D.kmeans_seq(batch.num, batch.y, self.C, self.n, self.cum)
             return
         x = batch.num.float()
         if self._seeded < self.k:  # seed centroids with the first k training points
@@ -211,6 +225,8 @@ class KMeans(Learner):
         self.C.copy_(C.to(self.device))
         self.n.copy_(n.to(self.device))
         self._seeded = self.k  # imported centroids count as seeded
+        if self.sequential:  # the sequential kernel reads seeding from n > 0
+            self.n.clamp_(min=1.0)
 
 
 # ---------------------------------------------------------------------- MultiClassPA
@@ -476,6 +492,11 @@ class HT(Learner):
         self.grace = hp_int(self.hyper, "gracePeriod", 200)
         self.delta = hp_float(self.hyper, "delta", 1e-7)
         self.tau = hp_float(self.hyper, "tau", 0.05)
+        # due leaves are checked every `checkEvery` rows of a tick, not once per tick: the
+        # reference checks a leaf the moment it reaches the grace period, so a tree grows
+        # by many levels within one 65,536-row tick (tests/test_ht_sequential.py pins the
+        # gap to the per-point VFDT: none at 1,024, 0.93 → 0.56 accuracy at whole ticks)
+        self.check_every = max(1, hp_int(self.hyper, "checkEvery", 1024))
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -488,6 +509,7 @@ class HT(Learner):
         self.delta = hp_float(h, "delta", 1e-7)
         self.tau = hp_float(h, "tau", 0.05)
         self.nb = hp_int(h, "nBins", 16)
+        self._retune()
         dev = self.device
         N, d, C = self.N, self.d, self.Cn
         # flat state: feature, threshold, left, right, class counts, S0, S1, S2, lo, hi, since
@@ -523,6 +545,14 @@ class HT(Learner):
                 self.lo, self.hi, self.since, self.nnodes]
 
     def fit(self, batch, ctx):
+        B, step = batch.B, self.check_every
+        if B > step:
+            for a in range(0, B, step):
+                self._fit_part(batch.slice(a, min(B, a + step)))
+            return
+        self._fit_part(batch)
+
+    def _fit_part(self, batch):
         if self.device.type == "cuda":
             # device path (csrc/kernels/hoeffding.hip): no host synchronisation per round
             if batch.B:

@@ -159,6 +159,30 @@ def multiclass_round(W: torch.Tensor, batch: HashedBatch, R: int, S: int, nclass
             ptr(dacc), ptr(stats))
 
 
+def kmeans_seq(x: torch.Tensor, y: torch.Tensor | None, cent: torch.Tensor, n: torch.Tensor,
+               cum: torch.Tensor | None) -> None:
+    """Exact sequential (MacQueen) k-means over the rows of x, in order (GPU:
+    csrc/kernels/kmeans_seq.hip, one wave holding the model in registers; CPU:
+    csrc/host/dense_cpu.cpp). Rows with a NaN ``y`` are skipped."""
+    k, d = cent.shape
+    x = x.float().contiguous()
+    assert x.shape[1] >= d and cent.is_contiguous() and n.is_contiguous()
+    assert cum is None or cum.dtype == torch.float64
+    yv = None if y is None else y.float().contiguous()
+    if x.is_cuda:
+        check(native.hip().omldm_kmeans_seq(ptr(x), x.shape[1], ptr(yv), x.shape[0], d, k,
+                                            ptr(cent), ptr(n), ptr(cum), native.stream_of(x)),
+              "omldm_kmeans_seq")
+    else:
+        check(native.host().omldm_cpu_kmeans_seq(ptr(x), x.shape[1], ptr(yv), x.shape[0], d, k,
+                                                 ptr(cent), ptr(n), ptr(cum)),
+              "omldm_cpu_kmeans_seq")
+
+
+def kmeans_seq_fits(d: int, k: int) -> bool:
+    return 1 <= d <= 64 and 1 <= k <= 64
+
+
 def kmeans_apply(cent: torch.Tensor, n: torch.Tensor, sums: torch.Tensor, counts: torch.Tensor,
                  inertia: torch.Tensor, cum: torch.Tensor | None) -> None:
     """GPU: one launch — c ← (n·c + Σx)/(n + cnt) where n + cnt > 0, n += cnt, Σx = cnt = 0,

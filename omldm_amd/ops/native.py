@@ -108,6 +108,8 @@ HIP_SIGS = [
     ("omldm_fgm_begin", i32, [vp, vp, f64, vp]),
     ("omldm_holdout_route", i32, [vp, vp, vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, i64, i64,
                                   i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp]),
+    ("omldm_kmeans_seq_fits", i32, [i32, i32]),
+    ("omldm_kmeans_seq", i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     ("omldm_ipc_alloc", vp, [i64]),
     ("omldm_ipc_free", i32, [vp]),
     ("omldm_ipc_handle", i32, [vp, vp]),
@@ -138,6 +140,7 @@ HIP_SIGS = [
 ]
 
 HOST_SIGS = [
+    ("omldm_cpu_kmeans_seq", i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp]),
     ("omldm_murmur3_32", u32, [C.c_char_p, i64, u32]),
     ("omldm_crc32c", u32, [C.c_char_p, i64, u32]),
     ("omldm_hash_cat", C.c_int32, [C.c_char_p, i64, i32, i32, i64]),

@@ -1,8 +1,9 @@
 #!/bin/bash
 # Round 4: v3 table-scan tests, v2 vs v3 headline A/B, kernel trace of v3.
 mkdir -p gpurun_out/r4
-timeout -k 10 500 python -u -m pytest tests/test_scan3.py tests/test_holdout_gpu.py tests/test_rawwire.py tests/test_async_protocols.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r4/scan3_tests.txt 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_scan3.py tests/test_holdout_gpu.py tests/test_kmeans_seq.py tests/test_forecast_server_gpu.py tests/test_rawwire.py tests/test_async_protocols.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r4/scan3_tests.txt 2>&1
 rc=$?; tail -15 gpurun_out/r4/scan3_tests.txt; [ $rc -eq 0 ] || exit 4
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4/smoke.txt 2>&1 || exit 9
 OMLDM_SEQ_KERNEL=scan timeout -k 10 240 python bench.py --engine-e2e 0 --engine-latency 0 > gpurun_out/r4/bench_v2.json 2> gpurun_out/r4/bench_v2.err || exit 5
 timeout -k 10 240 python bench.py --engine-e2e 0 --engine-latency 0 > gpurun_out/r4/bench_v3.json 2> gpurun_out/r4/bench_v3.err || exit 6
 python - <<'PY'
