@@ -534,23 +534,27 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
         } else {
           u = m0 + f1;
         }
+        // the lane's rows of aG_k and aX1_{k+1} in VGPRs before the chain starts: an LDS
+        // read inside the chain cost ~20 of its ~48 cycles per step (scan_chain_probe)
         const float* grow = &sm.G[b][lane][0];
         const float* xrow = &sm.X1[b ^ 1][lane][0];
-        float n1 = 0.f;
+        float gg[s3::CH], xx[s3::CH];
 #pragma unroll
         for (int t4 = 0; t4 < s3::CH; t4 += 4) {
           const float4 g4 = *reinterpret_cast<const float4*>(grow + t4);
           const float4 x4 = *reinterpret_cast<const float4*>(xrow + t4);
-          const float gg[4] = {g4.x, g4.y, g4.z, g4.w}, xx[4] = {x4.x, x4.y, x4.z, x4.w};
+          gg[t4] = g4.x, gg[t4 + 1] = g4.y, gg[t4 + 2] = g4.z, gg[t4 + 3] = g4.w;
+          xx[t4] = x4.x, xx[t4 + 1] = x4.y, xx[t4 + 2] = x4.z, xx[t4 + 3] = x4.w;
+        }
+        float n1 = 0.f;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float ct = readlane_f(cf(u, p, y), t4 + q);
-            u = fmaf(ct, gg[q], u);     // aG strictly lower: lane t frozen after step t
-            n1 = fmaf(ct, xx[q], n1);   // → chunk k+1 (off the dependency chain)
-            // pin the fold beside its step: left to itself the compiler parks the 64 c's
-            // in SGPRs and runs the fold as a serial tail after the chunk
-            asm volatile("" : "+v"(u), "+v"(n1));
-          }
+        for (int t = 0; t < s3::CH; ++t) {
+          const float ct = readlane_f(cf(u, p, y), t);
+          u = fmaf(ct, gg[t], u);     // aG strictly lower: lane t frozen after step t
+          n1 = fmaf(ct, xx[t], n1);   // → chunk k+1 (off the dependency chain)
+          // pin the fold beside its step: left to itself the compiler parks the 64 c's
+          // in SGPRs and runs the fold as a serial tail after the chunk
+          asm volatile("" : "+v"(u), "+v"(n1));
         }
         const float c = cf(u, p, y);
         sm.cb[b][lane] = c;
@@ -599,77 +603,96 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
     w0[i] = (j < KN) ? (j < dn ? w[j] : ((p.bias && j == dn) ? w[dim - 1] : 0.f)) : 0.f;
     wn[i] = w0[i];
   }
-  // occurrence words of this wave's fields, rotated one chunk per iteration:
-  // c0/c1 chunk k+1 (margins), p1 chunk k, p2 chunk k−1 (scatter)
-  int c0[s3::NF];
-  uint32_t c1[s3::NF], p1[s3::NF], p2[s3::NF];
-#pragma unroll
-  for (int i = 0; i < s3::NF; ++i) p1[i] = p2[i] = 0u;
-#pragma unroll
-  for (int i = 0; i < s3::NF; ++i) {  // chunk k + 1 of iteration k = −1
-    const int f = q + s3::NH * i;
-    const bool ok = f < dc && t0 + r < t1;
-    c0[i] = ok ? slotsT[(size_t)f * B + t0 + r] : -1;
-    c1[i] = ok ? meta[(size_t)f * B + t0 + r] : 0u;
-  }
-
-  for (int k = -1; k <= nch; ++k) {
-    const int cn = k + 1, ks = k - 1;
-    if (wave == 1) stamp(7);
-    // previous iteration's global stores (table overflow) and this iteration's words
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (wave == 1) stamp(2);
-    // ---- issue: w gathers of chunk cn (slots first seen in its window), Gram staging
+  // Software pipeline, one chunk ahead. Iteration k margins chunk cn = k + 1 and scatters
+  // chunk k − 1 from the CUR set of registers while it fills the NXT set for chunk cn + 1:
+  // its words (slot, meta), the Gram staging, the dense columns, and — once the words are
+  // in, after this iteration's scatter and margins — the w gathers. Everything loaded is
+  // model-independent (w is the round-start model), so no load waits on the chain. The
+  // loop is unrolled by two with the sets swapping roles (a register rotation would make
+  // every NXT load complete before the barrier), and every load is issued unconditionally
+  // (clamped address, result selected after): loads under exec-masked branches leave the
+  // compiler unable to count the loads in flight, and it would wait for all of them.
+  constexpr int NV4 = (2 * s3::MAT / 4 + 64 * s3::NH - 1) / (64 * s3::NH);  // 5
+  struct Set {
+    int cs[s3::NF];
+    uint32_t cm[s3::NF];
     float g[s3::NF];
+    f32x4 v[NV4];
+    float xs[s3::NJ], xc[s3::NJ];  // dense columns of the chunk scattered / margined
+  };
+  uint32_t p1[s3::NF], p2[s3::NF];  // meta of chunk k (scattered next) and k − 1
+  auto load_words = [&](int ch, Set& S) {
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
-      const bool glob = c0[i] != -1 && !(c1[i] & s3::F_TG);
-      g[i] = glob ? w[c0[i] & 0x7fffffff] : 0.f;
+      const int f = q + s3::NH * i;
+      const int row = t0 + ch * s3::CH + r;
+      const bool ok = ch >= 0 && ch < nch && f < dc && row < t1;
+      const size_t at = ok ? (size_t)f * B + row : 0;
+      const int sv = slotsT[at];
+      const uint32_t mv = meta[at];
+      S.cs[i] = ok ? sv : -1;
+      S.cm[i] = ok ? mv : 0u;
     }
-    constexpr int NV4 = (2 * s3::MAT / 4 + 64 * s3::NH - 1) / (64 * s3::NH);  // 5
-    f32x4 v[NV4];
+  };
+  auto issue_gathers = [&](Set& S) {
+#pragma unroll
+    for (int i = 0; i < s3::NF; ++i) {
+      const bool glob = S.cs[i] != -1 && !(S.cm[i] & s3::F_TG);
+      S.g[i] = w[glob ? (S.cs[i] & 0x7fffffff) : 0];  // unused unless glob
+    }
+  };
+  // aG_{ch} and aX1_{ch+1} (clamped reads past the round: never stored)
+  auto issue_staging = [&](int ch, Set& S) {
 #pragma unroll
     for (int u = 0; u < NV4; ++u) {
       const int i = min(hl + 64 * s3::NH * u, 2 * s3::MAT / 4 - 1);
-      const int mtx = i >> 10, e = i & 1023;  // 0: aG_{cn}, 1: aX1_{cn+1}
-      const int kc = max(0, min(cn + mtx, nch - 1));
-      v[u] = reinterpret_cast<const f32x4*>(chunk_prep(kc) + mtx * s3::MAT)[e];
+      const int mtx = i >> 10, e = i & 1023;
+      const int kc = max(0, min(ch + mtx, nch - 1));
+      S.v[u] = reinterpret_cast<const f32x4*>(chunk_prep(kc) + mtx * s3::MAT)[e];
     }
-    // dense columns of chunk ks (update) and chunk cn (margins)
-    float xs[s3::NJ], xc[s3::NJ];
+  };
+  // dense columns of chunk ch (clamped chunk; 0 outside the round / past KN)
+  auto load_dense = [&](int ch, float* xd) {
 #pragma unroll
     for (int i = 0; i < s3::NJ; ++i) {
       const int j = q + s3::NH * i;
-      xs[i] = (j < KN && ks >= 0) ? chunk_prep(ks)[2 * s3::MAT + s3::CH + j * s3::CH + r] : 0.f;
-      xc[i] = (j < KN && cn < nch) ? chunk_prep(cn)[2 * s3::MAT + s3::CH + j * s3::CH + r] : 0.f;
+      const bool ok = j < KN && ch >= 0 && ch < nch;
+      const int jc = j < KN ? j : 0, cc = max(0, min(ch, nch - 1));
+      const float v = chunk_prep(cc)[2 * s3::MAT + s3::CH + jc * s3::CH + r];
+      xd[i] = ok ? v : 0.f;
     }
+  };
+  auto body = [&](int k, Set& CUR, Set& NXT) {
+    const int cn = k + 1, ks = k - 1;
+    if (wave == 1) stamp(7);
+    // ---- issue the NXT set (chunk cn + 1) but its gathers
+    load_words(cn + 1, NXT);
+    issue_staging(cn + 1, NXT);
+    load_dense(ks + 1, NXT.xs);
+    load_dense(cn + 1, NXT.xc);
     if (wave == 1) stamp(3);
-    // ---- scatter chunk ks into the table (rank order: no two lanes on one entry per
-    // instruction, adds in row order) and its dense update
+    // ---- scatter chunk ks into the table and its dense update: one LDS atomic add per
+    // occurrence (ds_add_f32; lanes on one entry are combined by the LDS unit inside the
+    // instruction — a software loop over the ranks of equal slots cost 13 K cycles per
+    // chunk, more than everything else of the chunk together)
     if (ks >= 0) {
       const float cv = sm.cb[ks & 1][r];
 #pragma unroll
       for (int i = 0; i < s3::NF; ++i) {
         const uint32_t m = p2[i];
-        const bool sc = (m & s3::F_SCAT) != 0u;
+        const bool sc = (m & s3::F_SCAT) != 0u && cv != 0.f;
         if (__builtin_amdgcn_ballot_w64(sc) == 0ull) continue;
-        const int rank = sc ? (int)((m >> s3::RANK_SHIFT) & s3::RANK_MASK) : -1;
         const int lid = (int)(m >> s3::LID_SHIFT);
         const float val = (m & s3::F_SIGN) ? -cv : cv;
-        int mr = rank;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) mr = max(mr, __shfl_xor(mr, d));
-        for (int rk = 0; rk <= mr; ++rk) {
-          if (rank == rk && val != 0.f) {
-            if (lid < cap) tab[lid] += val;
-            else atomicAdd(&ag[lid - cap], val);
-          }
+        if (sc) {
+          if (lid < cap) atomicAdd(&tab[lid], val);
+          else atomicAdd(&ag[lid - cap], val);
         }
       }
 #pragma unroll
       for (int i = 0; i < s3::NJ; ++i) {
         const int j = q + s3::NH * i;
-        if (j < KN) wn[i] += wave_sum(cv * xs[i]);
+        if (j < KN) wn[i] += wave_sum(cv * CUR.xs[i]);
       }
     }
     if (wave == 1) stamp(6);
@@ -677,21 +700,30 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
     if (cn < nch) {
       float base = 0.f;
 #pragma unroll
-      for (int i = 0; i < s3::NJ; ++i) base = fmaf(xc[i], wn[i], base);
+      for (int i = 0; i < s3::NJ; ++i) base = fmaf(CUR.xc[i], wn[i], base);
 #pragma unroll
       for (int i = 0; i < s3::NF; ++i) {
-        if (c0[i] == -1) continue;
-        const uint32_t m = c1[i];
+        const uint32_t m = CUR.cm[i];
+        const bool here = CUR.cs[i] != -1;
         const int lid = (int)(m >> s3::LID_SHIFT);
-        float val = g[i];
-        if (m & s3::F_TG) {
-          val = lid < cap ? tab[lid] : __hip_atomic_load(&ag[lid - cap], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if (m & s3::F_INIT) {
-          if (lid < cap) tab[lid] = val;
-          else __hip_atomic_store(&ag[lid - cap], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const bool tg = here && (m & s3::F_TG), init = here && !tg && (m & s3::F_INIT);
+        float val = CUR.g[i];
+        // the table's global spill (lid ≥ cap) on its own wave-uniform path: a global
+        // read merged into the LDS path would make every later use wait for all loads
+        if (__builtin_amdgcn_ballot_w64((tg || init) && lid >= cap) == 0ull) {
+          if (tg) val = tab[lid];
+          if (init) tab[lid] = val;
+        } else {
+          if (tg) val = lid < cap ? tab[lid] : __hip_atomic_load(&ag[lid - cap], __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (init) {
+            if (lid < cap) tab[lid] = val;
+            else __hip_atomic_store(&ag[lid - cap], val, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        base += (m & s3::F_SIGN) ? -val : val;
+        if (here) base += (m & s3::F_SIGN) ? -val : val;
       }
       sm.part[cn & 1][q][r] = base;
     }
@@ -704,22 +736,31 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
       if (i < 2 * s3::MAT / 4 && cn + mtx < nch) {
         const int row = e >> 4, col = (e & 15) * 4;
         float* dst = mtx == 0 ? &sm.G[cn & 1][row][col] : &sm.X1[(cn + 1) & 1][row][col];
-        *reinterpret_cast<f32x4*>(dst) = v[u];
+        *reinterpret_cast<f32x4*>(dst) = CUR.v[u];
       }
     }
-    // ---- rotate the occurrence words, prefetch chunk cn + 1's
+    // ---- the NXT gathers (its words have had the scatter and the margins to arrive)
+    issue_gathers(NXT);
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
       p2[i] = p1[i];
-      p1[i] = c1[i];
-      const int f = q + s3::NH * i;
-      const int row = t0 + (cn + 1) * s3::CH + r;
-      const bool ok = cn + 1 < nch && f < dc && row < t1;
-      c0[i] = ok ? slotsT[(size_t)f * B + row] : -1;
-      c1[i] = ok ? meta[(size_t)f * B + row] : 0u;
+      p1[i] = CUR.cm[i];
     }
     if (wave == 1) stamp(5);
     __syncthreads();
+  };
+
+  Set A, Bs;
+#pragma unroll
+  for (int i = 0; i < s3::NF; ++i) p1[i] = p2[i] = 0u;
+  load_words(0, A);
+  issue_staging(0, A);
+  load_dense(-2, A.xs);
+  load_dense(0, A.xc);
+  issue_gathers(A);
+  for (int k = -1; k <= nch; k += 2) {
+    body(k, A, Bs);
+    if (k + 1 <= nch) body(k + 1, Bs, A);
   }
   if (stamps && lane == 0 && wave == 1)
     for (int k = 2; k < 8; ++k) atomicAdd(&stamps[(size_t)s * 16 + k], st_acc[k]);

@@ -88,6 +88,11 @@ class TickIngest:
         assert copy_method in ("pull", "sdma"), copy_method
         self.copy_method = copy_method
         self._copy_stream = (copy_stream or torch.cuda.Stream(self.device)) if self.stage else None
+        self.h2d_timer = self.parse_timer = None  # device time of the copies / GPU parses
+        if self.stage:
+            from omldm_amd.utils.devtimer import LaggedTimer
+
+            self.h2d_timer, self.parse_timer = LaggedTimer(), LaggedTimer()
         self._parse_stream = parse_stream  # None: the parse follows the copy on its stream
         self.batch = max(1, int(batch_size))
         self.pinned = bool(pinned)
@@ -196,6 +201,7 @@ class TickIngest:
             if blk.consumed is not None:
                 cs.wait_event(blk.consumed)  # the parser of this slot's last use is done
                 blk.consumed = None
+            self.h2d_timer.start(cs)
             if self.copy_method == "sdma":
                 with torch.cuda.stream(cs):
                     blk.d_raw[:nbytes].copy_(blk.data[:nbytes], non_blocking=True)
@@ -203,6 +209,7 @@ class TickIngest:
             else:
                 pull_copy(blk.d_raw, blk.data[:nbytes], self.copy_blocks, cs.cuda_stream)
                 pull_copy(blk.d_offs, blk.offs_t[:n + 1], self.copy_blocks, cs.cuda_stream)
+            self.h2d_timer.stop(cs, nbytes + 8 * (n + 1))
             blk.parsed = None
             if self.space is not None:
                 ps = cs
@@ -211,7 +218,9 @@ class TickIngest:
                     copied.record(cs)
                     ps = self._parse_stream
                     ps.wait_event(copied)
+                self.parse_timer.start(ps)
                 self._parse(blk, ps)
+                self.parse_timer.stop(ps, nbytes)
                 cs = ps
             ev = torch.cuda.Event()
             ev.record(cs)

@@ -71,6 +71,8 @@ class Job:
         self.cfg = cfg
         self.comm = comm
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.rank, self.world = comm.rank, comm.world
         self.space = FeatureSpace(cfg.numFeatures, cfg.discreteFeatures, cfg.catFeatures,
                                   cfg.hashDim, field_aware=cfg.fieldAware)
@@ -167,6 +169,14 @@ class Job:
         if self.fserver is not None:
             self.fserver.reconfigure()
             self.fserver.start()
+        # device time of the training rounds and of the coalesced collectives (lagged
+        # event pairs, no host sync: utils/devtimer.py)
+        self._train_timer = self._coll_timer = None
+        if self.device.type == "cuda":
+            from omldm_amd.utils.devtimer import LaggedTimer
+
+            self._train_timer, self._coll_timer = LaggedTimer(), LaggedTimer()
+        self._t_start = time.time()
         # diagnostics / multi-rank tests: a per-tick digest of every pipeline's model
         # (replica agreement across ranks) and the final models, under this directory
         self._trace_dir = os.environ.get("OMLDM_TRACE_MODELS") or None
@@ -375,8 +385,13 @@ class Job:
                     pipe.train(routed)
         for hubs, items in groups.items():
             with tracing.range("sync:coalesced"):
+                if self._coll_timer is not None:
+                    self._coll_timer.start()
                 self.comm.all_reduce_coalesced_([b for _, b in items], tag="sync", hubs=hubs,
                                                 bucket_bytes=self.cfg.bucketBytes)
+                if self._coll_timer is not None:
+                    self._coll_timer.stop(nbytes=sum(b.numel() * b.element_size()
+                                                     for _, b in items))
             for pipe, _ in items:
                 pipe.protocol.finish()
 
@@ -503,7 +518,11 @@ class Job:
         active += n_req
         self._trained_global += int(n_train)
         if self.pipes and n_train > 0:
+            if self._train_timer is not None:
+                self._train_timer.start()
             self._train(tb, spill)
+            if self._train_timer is not None:
+                self._train_timer.stop()
             if self._trace_dir:
                 self._trace_models()
         for q in queries:
@@ -554,6 +573,24 @@ class Job:
             (lambda q: None)
         cs = self.comm.stats
         fsl = self.fserver.latency_percentiles() if self.fserver is not None else None
+        dev = {}
+        if self._train_timer is not None:
+            wall_ms = max(1e-3, (time.time() - self._t_start) * 1e3)
+            for t in (self._train_timer, self._coll_timer, self.ingest.h2d_timer,
+                      self.ingest.parse_timer):
+                if t is not None:
+                    t.settle()
+            tr, co = self._train_timer, self._coll_timer
+            h2d, pa = self.ingest.h2d_timer, self.ingest.parse_timer
+            dev = {"trainDeviceMs": round(tr.ms, 3),
+                   "collectiveDeviceMs": round(co.ms, 3), "collectiveGBps": co.gbps(),
+                   "h2dMs": round(h2d.ms, 3) if h2d else None,
+                   "h2dGBps": h2d.gbps() if h2d else None,
+                   "parseMs": round(pa.ms, 3) if pa else None,
+                   "parseGBps": pa.gbps() if pa else None,
+                   # share of the job's wall time the training rounds kept the GPU busy
+                   # (MFMA / VALU utilisation per kernel: rocprofv3 PMC, profiles/)
+                   "trainBusyFraction": round(tr.ms / wall_ms, 4)}
         return {"ranks": self.world, "spokesPerRank": self.spokes,
                 "forecastRecordLatencyUs": fsl,
                 "forecastRecordLatencyUsPerLearner":
@@ -563,7 +600,8 @@ class Job:
                 "forecastBatchLatencyMs": {"p50": pct(0.5), "p99": pct(0.99)},
                 "collectives": cs.collectives, "collectiveBytes": cs.bytes,
                 "collectiveBytesPerTag": dict(cs.per_tag), "counters": dict(self.counters),
-                "stages": tracing.report(), "modelStoreMB": round(self.store.bytes() / 2**20, 2)}
+                "stages": tracing.report(), "modelStoreMB": round(self.store.bytes() / 2**20, 2),
+                "device": dev}
 
     def run(self) -> "Job":
         while not self.terminated and (self.cfg.maxTicks <= 0 or self.ticks < self.cfg.maxTicks):

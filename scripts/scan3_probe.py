@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""v3 table scan at the headline geometry (16 spokes × 8192 rows, 2^20 slots): device time
+of the prepare (passes 1-3) and of the run (scan + combine) per round, and the scan
+kernel's per-phase cycles per chunk (linear_scan3.hip stamps). Diagnostics only (GPU)."""
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from omldm_amd.api.batch import FeatureSpace  # noqa: E402
+from omldm_amd.io.synthetic import synth_raw  # noqa: E402
+from omldm_amd.ops import linear as L  # noqa: E402
+from omldm_amd.ops import native  # noqa: E402
+
+dev = torch.device("cuda", 0)
+space = FeatureSpace(13, 0, 26, 1 << 20)
+rule = L.LinearRule(rule=L.RULE_HINGE, variant=L.PA1, C=1.0)
+S, R = 16, 8192
+L.SEQ_KERNEL = "scan3"
+b = synth_raw(space, S * R, seed=25)
+b = type(b)(b.num.to(dev), b.tok.to(dev), b.y.to(torch.int8).to(dev))
+w = torch.zeros(space.dim, device=dev)
+dacc = torch.zeros(space.dim + 2, device=dev)
+cum = torch.zeros(8, dtype=torch.float64, device=dev)
+for _ in range(3):
+    L.linear_seq_round(w, b, R, S, dacc, rule, 1.0 / S, cum=cum)
+    L.linear_apply(w, None, dacc)
+torch.cuda.synchronize()
+n = 10
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+tp = tr = 0.0
+for _ in range(n):
+    ev[0].record()
+    b.prep = L.linear_scan3_prepare(b, R, S, space.dim, True, rule)
+    ev[1].record()
+    L.linear_seq_round(w, b, R, S, dacc, rule, 1.0 / S, cum=cum)
+    L.linear_apply(w, None, dacc)
+    ev[2].record()
+    torch.cuda.synchronize()
+    tp += ev[0].elapsed_time(ev[1])
+    tr += ev[1].elapsed_time(ev[2])
+    b.prep = None
+lib = native.hip().cdll
+lib.omldm_scan3_stamps.argtypes = [ctypes.c_void_p]
+st = torch.zeros((S, 16), dtype=torch.int64, device=dev)
+lib.omldm_scan3_stamps(st.data_ptr())
+L.linear_seq_round(w, b, R, S, dacc, rule, 1.0 / S, cum=cum)
+torch.cuda.synchronize()
+lib.omldm_scan3_stamps(None)
+m = st.double().mean(0)
+nch = (R + 63) // 64 + 2
+names = ["scan", "scan_bar", "h_top_wait", "h_issue", "h_margins", "h_lds_prefetch", "h_scatter",
+         "h_bar"]
+print(json.dumps({"prepare_ms": round(tp / n, 4), "run_ms": round(tr / n, 4),
+                  "Mex_s": round(S * R / ((tp + tr) / n) / 1e3, 1),
+                  "stamps_cycles_per_chunk": {names[k]: round(float(m[k]) / nch, 1)
+                                              for k in range(8)}}), flush=True)

@@ -63,7 +63,7 @@ def test_lane_answers_every_pipeline_kind_per_record():
     assert fs.served == 9 and not fs.fallback
     preds = [json.loads(x) for x in br.records("predictions")]
     assert len(preds) == 6 * 9
-    batch, _, _ = parse_records(fc, SP)
+    batch, _, _ = parse_records(fc, job.space)
     batch = batch.without_raw()
     for pid, name, _, _ in specs:
         want = job.pipes[pid].predict(batch).float()

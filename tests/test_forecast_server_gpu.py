@@ -64,7 +64,7 @@ def test_wave_answers_every_record_like_the_batched_predict():
     job.tick()
     preds = [json.loads(x) for x in br.records("predictions")]
     assert len(preds) == 80
-    batch, _, _ = parse_records(fc, SP)
+    batch, _, _ = parse_records(fc, job.space)
     batch = batch.without_raw().to("cuda")
     for pid in (1, 2):
         want = job.pipes[pid].predict(batch).float().cpu()
@@ -109,7 +109,7 @@ def test_every_pipeline_kind_is_answered_per_record():
     assert not fs.fallback and fs.served == 12
     preds = [json.loads(x) for x in br.records("predictions")]
     assert sorted(p["mlpId"] for p in preds) == sorted(list(range(1, 8)) * 12)
-    batch, _, _ = parse_records(fc, SP)
+    batch, _, _ = parse_records(fc, job.space)
     batch = batch.without_raw().to("cuda")
     for pid, name, _, _ in specs:
         want = job.pipes[pid].predict(batch).float().cpu()
