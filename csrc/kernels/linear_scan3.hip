@@ -1,8 +1,8 @@
 // Exact sequential online linear learners, v3 ("table scan"): every spoke keeps the
 // weights it re-reads during a round in an LDS slot table, so the per-spoke workgroup
-// issues no global atomics and a third of v2's global gathers; the round end sums the
-// spokes' updates from sorted occurrence lists over the whole GPU instead of averaging
-// dense replicas.
+// issues no global atomics and a third of v2's global gathers; the round end adds the
+// spokes' updates straight into the round accumulator over the whole GPU instead of
+// averaging dense replicas.
 //
 // Semantics as linear_scan.hip / linear_seq.hip (the reference's spoke,
 // omldm/operators/spoke/FlinkSpoke.scala:92-107, with the Synchronous PS averaging the
@@ -20,28 +20,24 @@
 //                          recurs two or more chunks apart, else from w itself.
 // A slot that occurs only inside a window of two consecutive chunks never needs a table
 // entry: G and X1 carry all its in-round updates. On the bench stream that leaves ~17.7 K
-// table slots per 8192-row spoke (fits LDS), 580 global gathers per chunk (v2: 1664) and
-// no global atomics (v2: 1664 per chunk).
+// table slots per 8192-row spoke (fits LDS), ~580 global gathers per chunk (v2: 1664) and
+// no global atomics in the scan (v2: 1664 per chunk).
 //
 // The scanner keeps each row's affine candidate u = a·m + b instead of m (a = −1/(‖x‖² +
 // kadd), b = y/(‖x‖² + kadd) for the hinge rule): with the Grams pre-scaled by the row's a
-// (prep), one step of the recurrence is med3 → v_readlane → fma.
+// (prep), one step of the recurrence is med3 → v_readlane → fma, on rows held in VGPRs.
 //
-// Passes of a round (all but 3 model-independent; 1, 2, 4 can run ahead on another stream):
-//   1. s3_slots_kernel   tokens → field-aware signed slots, FIELD-MAJOR [dc][B] (or a
-//                        transpose of already hashed row-major slots)
-//   2. s3_dedupe_kernel  one workgroup per (spoke, field): the field's occurrences sorted
-//                        by (slot, row) in LDS (bitonic), per-slot first/last chunk, table
-//                        ids, per-occurrence flags and the rank among equal slots of its
-//                        chunk → meta [dc][B]; the sorted list + per-tile offsets for 5.
+// Passes of a round (1-3 model-independent: they run ahead on another stream):
+//   1. s3_slots_kernel   tokens (or slots) → field-aware signed slots, FIELD-MAJOR [dc][B]
+//   2. s3_flags_kernel   one workgroup per (field, spoke): an LDS hash table of the
+//                        field's slots (first / last row), table ids, per-occurrence
+//                        flags → meta [dc][B]
 //   3. s3_gram_kernel    one workgroup per (spoke, chunk): a_t, G_k and X1_k (categorical
-//                        match counts on the VALU, the dense block on the matrix cores),
-//                        scaled by a_t; the chunk's dense columns transposed for the helpers
+//                        match counts and the dense block), scaled by a_t; the chunk's
+//                        dense columns transposed for the helpers
 //   4. s3_scan_kernel    one workgroup per spoke: scanner wave + 7 helper waves
-//   5. s3_combine_kernel one workgroup per (field, 512-slot tile): Σ over spokes of the
-//                        occurrences' c·sign, from the sorted lists (segmented sums, fixed
-//                        order, no atomics) → the round accumulator, dense; plus the dense
-//                        columns, the intercept and the statistics.
+//   5. s3_scatter_kernel the whole GPU: dacc[slot] += inv_p·c·sign per occurrence (fp32
+//                        atomics), s3_dense_kernel: dense columns, scalars, statistics
 #include "common.h"
 #include "hash_dev.h"
 #include "seq_common.h"
@@ -60,18 +56,14 @@ constexpr int NF = (MAXF + NH - 1) / NH;   // fields per helper wave (5)
 constexpr int KNMAX = 32;                  // dense columns (numerical + intercept)
 constexpr int NJ = (KNMAX + NH - 1) / NH;  // dense columns per helper wave (5)
 constexpr int MAT = CH * CH;
-constexpr int RMAX = 8192;                 // rows per spoke (the dedupe sort lives in LDS)
-constexpr int DT = 1024;                   // dedupe threads
-constexpr int TILE = 512;                  // slots per combine tile
+constexpr int RMAX = 8192;                 // rows per spoke (16-bit rows in the flags table)
 constexpr int WS = 8;                      // per-spoke stat row
 constexpr int DS = KNMAX;                  // per-spoke dense delta row
-// meta word of one occurrence: flags | sign | rank among equal slots of its chunk | table id
+// meta word of one occurrence: flags | sign | table id
 constexpr uint32_t F_TG = 1u;              // margin reads the table (else w)
 constexpr uint32_t F_INIT = 2u;            // first occurrence: writes w[slot] into the table
 constexpr uint32_t F_SCAT = 4u;            // the slot recurs ≥ 2 chunks later: add c·sign
 constexpr uint32_t F_SIGN = 8u;
-constexpr int RANK_SHIFT = 4;
-constexpr uint32_t RANK_MASK = 63u;
 constexpr int LID_SHIFT = 10;
 }  // namespace s3
 
@@ -117,218 +109,111 @@ __global__ __launch_bounds__(256) void s3_slots_kernel(const void* __restrict__ 
     for (int f = 0; f < dc; ++f) slotsT[(size_t)f * B + r0 + tid] = tile[tid][f];
 }
 
-// ------------------------------------------------------------------ pass 2: dedupe
-// Block-wide inclusive scans over DT threads (16 waves); every thread passes its
-// aggregate, gets the inclusive scan of the aggregates back.
-template <typename T, typename Op>
-__device__ __forceinline__ T block_scan_incl(T v, Op op, T ident, T* wtot) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const T t = __shfl_up(v, d);
-    if (lane >= d) v = op(v, t);
-  }
-  if (lane == 63) wtot[wave] = v;
-  __syncthreads();
-  if (wave == 0) {
-    T x = lane < s3::DT / 64 ? wtot[lane] : ident;
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-      const T t = __shfl_up(x, d);
-      if (lane >= d) x = op(x, t);
-    }
-    if (lane < s3::DT / 64) wtot[lane] = x;
-  }
-  __syncthreads();
-  if (wave > 0) v = op(v, wtot[wave - 1]);
-  __syncthreads();  // wtot reusable
-  return v;
-}
+// ------------------------------------------------------------------ pass 2: flags
+// One workgroup per (field, spoke): every present occurrence of the field in the spoke's
+// rows is inserted into an LDS hash table keyed by its slot, which keeps the slot's first
+// and last row (one packed word, min/max by compare-and-swap). A slot whose first and
+// last occurrence are two or more chunks apart gets a table id (LDS counter, then a block
+// base from the spoke's counter lidcount[s], zeroed before the launch); every occurrence
+// gets its meta word: F_TG (the margin reads the table: a table slot seen in an earlier
+// chunk), F_INIT (the table slot's first occurrence), F_SCAT (the slot recurs ≥ 2 chunks
+// later), the sign and the table id; 0 for absent occurrences. No sort: the table ids
+// only need to be unique within the spoke.
+namespace s3 {
+constexpr int FT = 1024;                   // flags threads
+constexpr int HCAP = 16384;                // hash entries (≤ 8192 distinct slots: load ≤ ½)
+constexpr int RPT = RMAX / FT;             // rows per thread (8)
+}  // namespace s3
 
-struct MaxOp {
-  __device__ int operator()(int a, int b) const { return a > b ? a : b; }
-};
-struct AddOp {
-  __device__ int operator()(int a, int b) const { return a + b; }
-};
-
-__device__ __forceinline__ uint32_t key_slot(unsigned long long k) { return (uint32_t)(k >> 32); }
-__device__ __forceinline__ int key_row(unsigned long long k) { return (int)((uint32_t)k >> 1); }
-
-// Grid (dc, S_act), DT threads, dynamic LDS: npow keys (8 B) + npow ints.
-// Outputs: meta [dc][B] (uint32, see s3:: bits; 0 for absent), the field's sorted keys
-// lists [S][dc][Rcap], counts [S][dc], tile offsets [S][dc][ntiles + 1] (span > 0), and
-// table ids from the spoke's counter lidcount[s] (zeroed before the launch).
-__global__ __launch_bounds__(s3::DT) void s3_dedupe_kernel(
-    const int* __restrict__ slotsT, int B, int R, int dc, int dn, uint32_t span, int ntiles,
-    int Rcap, uint32_t* __restrict__ meta, unsigned long long* __restrict__ lists,
-    int* __restrict__ counts, int* __restrict__ tileoff, int* __restrict__ lidcount) {
-  extern __shared__ unsigned long long keys[];
-  __shared__ int wtot[16];
-  __shared__ int wtot2[16];
-  __shared__ int s_npres, s_base;
+__global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict__ slotsT, int B,
+                                                          int R, uint32_t* __restrict__ meta,
+                                                          int* __restrict__ lidcount) {
+  __shared__ int hkey[s3::HCAP];        // slot, −1 empty; after the inserts: local table id
+  __shared__ uint32_t hrow[s3::HCAP];   // first row << 16 | last row
+  __shared__ int s_cnt, s_base;
   const int f = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
   int t0, t1;
   spoke_rows(s, R, B, t0, t1);
   const int n = t1 - t0;
   if (n <= 0) return;
-  int npow = s3::DT;
-  while (npow < n) npow <<= 1;
-  int* aux = reinterpret_cast<int*>(keys + npow);
+  for (int i = tid; i < s3::HCAP; i += s3::FT) {
+    hkey[i] = -1;
+    hrow[i] = 0xFFFF0000u;
+  }
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
   const int* col = slotsT + (size_t)f * B + t0;
-  for (int i = tid; i < npow; i += s3::DT) {
-    unsigned long long k = ~0ull;
-    if (i < n) {
-      const int v = col[i];
-      if (v != -1)
-        k = ((unsigned long long)(uint32_t)(v & 0x7fffffff) << 32) | ((unsigned long long)i << 1) |
-            (v < 0 ? 1ull : 0ull);
+  int v[s3::RPT], h[s3::RPT];
+#pragma unroll
+  for (int q = 0; q < s3::RPT; ++q) {
+    const int i = tid + q * s3::FT;
+    v[q] = i < n ? col[i] : -1;
+    h[q] = -1;
+  }
+#pragma unroll
+  for (int q = 0; q < s3::RPT; ++q) {
+    if (v[q] == -1) continue;
+    const int i = tid + q * s3::FT;
+    const int key = v[q] & 0x7fffffff;
+    uint32_t at = ((uint32_t)key * 0x9E3779B1u) >> (32 - 14);
+    for (int probe = 0; probe < s3::HCAP; ++probe) {  // bounded: load ≤ ½
+      const int prev = atomicCAS(&hkey[at], -1, key);
+      if (prev == -1 || prev == key) break;
+      at = (at + 1) & (s3::HCAP - 1);
     }
-    keys[i] = k;
-  }
-  if (tid == 0) s_npres = 0;
-  __syncthreads();
-  // bitonic sort, ascending
-  for (int k = 2; k <= npow; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < npow; i += s3::DT) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long a = keys[i], b = keys[ixj];
-          const bool up = (i & k) == 0;
-          if ((a > b) == up) {
-            keys[i] = b;
-            keys[ixj] = a;
-          }
-        }
-      }
-      __syncthreads();
+    h[q] = (int)at;
+    uint32_t old = hrow[at];
+    while (true) {
+      const uint32_t fr = min(old >> 16, (uint32_t)i), lr = max(old & 0xFFFFu, (uint32_t)i);
+      const uint32_t nw = (fr << 16) | lr;
+      if (nw == old) break;
+      const uint32_t got = atomicCAS(&hrow[at], old, nw);
+      if (got == old) break;
+      old = got;
     }
   }
-  for (int i = tid; i < npow; i += s3::DT)
-    if (keys[i] != ~0ull && (i + 1 == npow || keys[i + 1] == ~0ull)) s_npres = i + 1;
   __syncthreads();
-  const int np = s_npres;
-  const int EPT = npow / s3::DT;  // consecutive elements per thread
-  const int e0 = tid * EPT;
-  // ---- scan 1: segment start (same slot) and group start (same slot and chunk)
-  int segs = 0, grps = 0;
-  int seg_in[8], grp_in[8];
-  for (int q = 0; q < EPT; ++q) {
-    const int i = e0 + q;
-    int hs = 0, hg = 0;
-    if (i < np) {
-      const unsigned long long ki = keys[i];
-      if (i == 0) {
-        hs = hg = 1;
-      } else {
-        const unsigned long long kp = keys[i - 1];
-        hs = key_slot(ki) != key_slot(kp);
-        hg = hs || ((key_row(ki) >> 6) != (key_row(kp) >> 6));
-      }
+  // table ids: the first occurrence of every table slot takes one
+  int mine = 0;
+  int lloc[s3::RPT];
+#pragma unroll
+  for (int q = 0; q < s3::RPT; ++q) {
+    lloc[q] = -1;
+    if (h[q] < 0) continue;
+    const int i = tid + q * s3::FT;
+    const uint32_t pr = hrow[h[q]];
+    const int first = (int)(pr >> 16), last = (int)(pr & 0xFFFFu);
+    if (i == first && (last >> 6) - (first >> 6) >= 2) {
+      lloc[q] = atomicAdd(&s_cnt, 1);
+      ++mine;
     }
-    segs = hs ? i : segs;
-    grps = hg ? i : grps;
-    seg_in[q] = segs;
-    grp_in[q] = grps;
-  }
-  // thread aggregates: the last head position seen (0 if none: a head at 0 exists)
-  const int sagg = block_scan_incl(segs, MaxOp(), 0, wtot);
-  const int gagg = block_scan_incl(grps, MaxOp(), 0, wtot2);
-  // exclusive prefix of this thread: the inclusive aggregate of thread tid − 1
-  __shared__ int incl_s[s3::DT], incl_g[s3::DT];
-  incl_s[tid] = sagg;
-  incl_g[tid] = gagg;
-  __syncthreads();
-  const int xs = tid ? incl_s[tid - 1] : 0, xg = tid ? incl_g[tid - 1] : 0;
-  for (int q = 0; q < EPT; ++q) {
-    seg_in[q] = seg_in[q] > xs ? seg_in[q] : xs;
-    grp_in[q] = grp_in[q] > xg ? grp_in[q] : xg;
   }
   __syncthreads();
-  // ---- per segment: last row (written by the segment's tail into aux[segment start])
-  for (int q = 0; q < EPT; ++q) {
-    const int i = e0 + q;
-    if (i < np && (i + 1 == np || key_slot(keys[i + 1]) != key_slot(keys[i])))
-      aux[seg_in[q]] = key_row(keys[i]);
-  }
-  __syncthreads();
-  // ---- scan 2: table ids of the table segments (heads where last − first chunk ≥ 2)
-  int tcnt = 0;
-  int tab_in[8];
-  for (int q = 0; q < EPT; ++q) {
-    const int i = e0 + q;
-    int t = 0;
-    if (i < np && seg_in[q] == i) {
-      const int first = key_row(keys[i]), last = aux[i];
-      t = ((last >> 6) - (first >> 6)) >= 2;
-    }
-    tab_in[q] = t;
-    tcnt += t;
-  }
-  const int tincl = block_scan_incl(tcnt, AddOp(), 0, wtot);
-  incl_s[tid] = tincl;
-  __syncthreads();
-  const int texcl = tid ? incl_s[tid - 1] : 0;
-  if (tid == s3::DT - 1) s_base = atomicAdd(&lidcount[s], tincl);
+  if (tid == 0) s_base = atomicAdd(&lidcount[s], s_cnt);
+#pragma unroll
+  for (int q = 0; q < s3::RPT; ++q)
+    if (lloc[q] >= 0) hkey[h[q]] = lloc[q];  // the slot's key is no longer looked up
   __syncthreads();
   const int base = s_base;
-  // lid of each table head → aux2 (reuse incl_g as it is no longer needed? no: npow-sized)
-  // heads keep their local table id in the upper part of keys' LDS: store it in aux as
-  // (last_row << 16) would not fit; use a second npow array carved from incl arrays when
-  // npow ≤ DT, else pack: aux[i] = last_row | (local_lid + 1) << 14 (last_row < 2^13)
-  {
-    int run = texcl;
-    for (int q = 0; q < EPT; ++q) {
-      const int i = e0 + q;
-      if (tab_in[q]) {
-        aux[i] = (aux[i] & 0x3fff) | ((run + 1) << 14);
-        ++run;
+  uint32_t* out = meta + (size_t)f * B + t0;
+#pragma unroll
+  for (int q = 0; q < s3::RPT; ++q) {
+    const int i = tid + q * s3::FT;
+    if (i >= n) continue;
+    uint32_t m = 0u;
+    if (h[q] >= 0) {
+      const uint32_t pr = hrow[h[q]];
+      const int first = (int)(pr >> 16), last = (int)(pr & 0xFFFFu);
+      const int ch = i >> 6;
+      m = v[q] < 0 ? s3::F_SIGN : 0u;
+      if ((last >> 6) - (first >> 6) >= 2) {
+        if (ch > (first >> 6)) m |= s3::F_TG;
+        if (i == first) m |= s3::F_INIT;
+        if ((last >> 6) >= ch + 2) m |= s3::F_SCAT;
+        m |= (uint32_t)(base + hkey[h[q]]) << s3::LID_SHIFT;
       }
     }
-  }
-  __syncthreads();
-  // ---- per occurrence: flags, rank, table id → meta (row order)
-  for (int q = 0; q < EPT; ++q) {
-    const int i = e0 + q;
-    if (i >= np) continue;
-    const unsigned long long ki = keys[i];
-    const int row = key_row(ki);
-    const int hs = seg_in[q];
-    const int a = aux[hs];
-    const int first = key_row(keys[hs]), last = a & 0x3fff;
-    const int ch = row >> 6;
-    const int lloc = (a >> 14) - 1;  // −1: not a table slot
-    uint32_t m = (ki & 1ull) ? s3::F_SIGN : 0u;
-    if (lloc >= 0) {
-      if (ch > (first >> 6)) m |= s3::F_TG;
-      if (i == hs) m |= s3::F_INIT;
-      if ((last >> 6) >= ch + 2) m |= s3::F_SCAT;
-      m |= (uint32_t)(base + lloc) << s3::LID_SHIFT;
-    }
-    m |= (uint32_t)((i - grp_in[q]) & s3::RANK_MASK) << s3::RANK_SHIFT;
-    meta[(size_t)f * B + t0 + row] = m;
-  }
-  // absent occurrences: meta 0 (written for every row not present)
-  for (int i = tid; i < n; i += s3::DT)
-    if (col[i] == -1) meta[(size_t)f * B + t0 + i] = 0u;
-  // ---- the sorted list, its count and the per-tile offsets (combine input)
-  unsigned long long* L = lists + ((size_t)s * dc + f) * Rcap;
-  for (int i = tid; i < np; i += s3::DT) L[i] = keys[i];
-  if (tid == 0) counts[s * dc + f] = np;
-  if (span > 0 && tileoff != nullptr) {
-    int* T = tileoff + ((size_t)s * dc + f) * (ntiles + 1);
-    const uint32_t lo = (uint32_t)dn + (uint32_t)f * span;
-    auto tile_of = [&](int i) -> int {
-      return (int)((key_slot(keys[i]) - lo) / (uint32_t)s3::TILE);
-    };
-    for (int i = tid; i <= np; i += s3::DT) {
-      const int prev = i == 0 ? -1 : tile_of(i - 1);
-      const int cur = i == np ? ntiles : tile_of(i);
-      for (int j = prev + 1; j <= cur && j <= ntiles; ++j) T[j] = i;
-    }
-    if (np == 0)
-      for (int j = tid; j <= ntiles; j += s3::DT) T[j] = 0;
+    out[i] = m;
   }
 }
 
@@ -774,97 +659,86 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
 }
 
 // ------------------------------------------------------------------ pass 5: combine
-// grid: block 0 the numerical columns, blocks 1 … dc·ntiles the tiles, the last block the
-// tail / intercept / scalars / statistics; 512 threads.
-// Tile (f, j) = slots [dn + f·span + j·TILE, …). Wave w sums spokes w, w + 8, … into its
-// own LDS row (segmented sums over the sorted occurrences, carried across batches, plain
-// read-add-write: a wave owns its row), the rows are added in wave order: the result does
-// not depend on timing.
-__global__ __launch_bounds__(512) void s3_combine_kernel(
-    const unsigned long long* __restrict__ lists, const int* __restrict__ tileoff,
-    const float* __restrict__ cout, const float* __restrict__ ws, const float* __restrict__ wsd,
-    int S_act, int R, int dc, int dn, uint32_t span, int ntiles, int Rcap, int dim, int bias,
-    int KN, float inv_p, int tile_lo, int tile_hi, float* __restrict__ dacc,
-    double* __restrict__ cum) {
-  __shared__ float acc[8][s3::TILE];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int blk = tile_lo + blockIdx.x;
-  if (blk >= tile_hi) return;
-  if (blk == 0) {  // numerical columns
-    for (int i = tid; i < dn; i += 512) {
-      float v = 0.f;
-      for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + i];
-      dacc[i] = v * inv_p;
-    }
-    return;
-  }
-  if (blk == dc * ntiles + 1) {
-    // the unused tail after the last field, the intercept, the accumulator's scalars, stats
-    for (int i = dn + dc * (int)span + tid; i < dim; i += 512) {
-      float v = 0.f;
-      if (i == dim - 1 && bias)
-        for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + dn];
-      dacc[i] = v * inv_p;
-    }
-    if (tid == 0) {
-      dacc[dim] = (float)S_act * inv_p;
-      dacc[dim + 1] = (float)S_act * inv_p;
-    }
-    if (cum && tid < 6 && tid != 4) {
-      double t = 0.0;
-      for (int s = 0; s < S_act; ++s) t += (double)ws[(size_t)s * s3::WS + tid];
-      cum[tid] += t;
-    }
-    return;
-  }
-  const int f = (blk - 1) / ntiles, j = (blk - 1) - f * ntiles;
-  const uint32_t flo = (uint32_t)dn + (uint32_t)f * span;
-  const uint32_t lo = flo + (uint32_t)j * s3::TILE;
-  const uint32_t hi = min(lo + (uint32_t)s3::TILE, flo + span);
-  for (int i = tid; i < 8 * s3::TILE; i += 512) (&acc[0][0])[i] = 0.f;
-  __syncthreads();
-  float* my = acc[wave];
-  for (int s = wave; s < S_act; s += 8) {
-    const int* T = tileoff + ((size_t)s * dc + f) * (ntiles + 1);
-    const int i0 = T[j], i1 = T[j + 1];
-    const unsigned long long* L = lists + ((size_t)s * dc + f) * Rcap;
-    const float* cs = cout + (size_t)s * R;
-    float carry = 0.f;
-    int cslot = -1;
-    for (int b0 = i0; b0 < i1; b0 += 64) {
-      const int i = b0 + lane;
-      const bool ok = i < i1;
-      const unsigned long long kk = ok ? L[i] : ~0ull;
-      const int slot = ok ? (int)key_slot(kk) : -2 - lane;  // distinct sentinels past the end
-      float v = ok ? cs[key_row(kk)] : 0.f;
-      if (kk & 1ull) v = -v;
-      // the previous batch's open segment continues into this one, or is flushed
-      if (lane == 0 && cslot >= 0) {
-        if (slot == cslot) v += carry;
-        else my[cslot - (int)lo] += carry;
-      }
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const float t = __shfl_up(v, d);
-        const int ts = __shfl_up(slot, d);
-        if (lane >= d && ts == slot) v += t;
-      }
-      const int nslot = __shfl_down(slot, 1);
-      const bool more = b0 + 64 < i1;
-      const bool tail = ok && (lane == 63 ? !more : nslot != slot);
-      if (tail) my[slot - (int)lo] += v;
-      // lane 63's segment stays open when the range goes on
-      cslot = more ? __shfl(slot, 63) : -1;
-      carry = more ? __shfl(v, 63) : 0.f;
-    }
+// dacc[slot] = inv_p · Σ over the spokes' occurrences of c_row · sign. Grid (row blocks of
+// SB rows, fields): a block first sums its occurrences per slot in an LDS hash table (a
+// low-cardinality field puts thousands of occurrences on a handful of slots: one global
+// atomic each serialised in L2 — 0.96 ms per round), then adds each distinct slot's sum
+// to dacc with one fp32 atomic; occurrences that find no free entry within a few probes
+// (high-cardinality fields: little repetition) go to dacc directly. c = 0 rows (most rows
+// the PA rule leaves alone) are skipped. The spokes' sums meet in L2 in arrival order: the
+// round's model is the replica average up to fp32 rounding of those sums.
+namespace s3 {
+constexpr int SB = 4096;     // rows per scatter block
+constexpr int SH = 4096;     // LDS hash entries per block
+constexpr int SPROBE = 8;
+}  // namespace s3
+
+__global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__ slotsT,
+                                                         const float* __restrict__ cout, int B,
+                                                         int n_rows, float inv_p,
+                                                         float* __restrict__ dacc) {
+  __shared__ int hk[s3::SH];
+  __shared__ float hv[s3::SH];
+  const int f = blockIdx.y, tid = threadIdx.x;
+  const int r0 = blockIdx.x * s3::SB, r1 = min(n_rows, r0 + s3::SB);
+  for (int i = tid; i < s3::SH; i += 256) {
+    hk[i] = -1;
+    hv[i] = 0.f;
   }
   __syncthreads();
-  for (uint32_t i = lo + tid; i < hi; i += 512) {
-    const int e = (int)(i - lo);
-    float t = 0.f;
-#pragma unroll
-    for (int w2 = 0; w2 < 8; ++w2) t += acc[w2][e];
-    dacc[i] = t * inv_p;
+  const int* col = slotsT + (size_t)f * B;
+  for (int row = r0 + tid; row < r1; row += 256) {
+    const int v = col[row];
+    if (v == -1) continue;
+    const float c = cout[row];
+    if (c == 0.f) continue;
+    const int key = v & 0x7fffffff;
+    const float val = v < 0 ? -c * inv_p : c * inv_p;
+    uint32_t at = ((uint32_t)key * 0x9E3779B1u) >> (32 - 12);
+    bool done = false;
+    for (int probe = 0; probe < s3::SPROBE; ++probe) {
+      const int prev = atomicCAS(&hk[at], -1, key);
+      if (prev == -1 || prev == key) {
+        atomicAdd(&hv[at], val);
+        done = true;
+        break;
+      }
+      at = (at + 1) & (s3::SH - 1);
+    }
+    if (!done) atomicAdd(&dacc[key], val);
+  }
+  __syncthreads();
+  for (int i = tid; i < s3::SH; i += 256) {
+    const int key = hk[i];
+    if (key != -1) atomicAdd(&dacc[key], hv[i]);
+  }
+}
+
+// The dense columns (numerical, intercept) from the spokes' dense deltas, the
+// accumulator's scalars and the round's statistics (one block).
+__global__ __launch_bounds__(256) void s3_dense_kernel(const float* __restrict__ ws,
+                                                       const float* __restrict__ wsd, int S_act,
+                                                       int dn, int dim, int bias, float inv_p,
+                                                       float* __restrict__ dacc,
+                                                       double* __restrict__ cum) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < dn; i += 256) {
+    float v = 0.f;
+    for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + i];
+    dacc[i] = v * inv_p;
+  }
+  if (tid == 0) {
+    float v = 0.f;
+    if (bias)
+      for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + dn];
+    dacc[dim - 1] = v * inv_p;
+    dacc[dim] = (float)S_act * inv_p;
+    dacc[dim + 1] = (float)S_act * inv_p;
+  }
+  if (cum && tid < 6 && tid != 4) {
+    double t = 0.0;
+    for (int s = 0; s < S_act; ++s) t += (double)ws[(size_t)s * s3::WS + tid];
+    cum[tid] += t;
   }
 }
 
@@ -897,8 +771,7 @@ int s3_sact(int B, int R, int S) {
   return sact < S ? (int)sact : S;
 }
 int s3_kn(int dn, int bias) { return dn + (bias ? 1 : 0) <= 16 ? 16 : 32; }
-int s3_ntiles(uint32_t span) { return (int)((span + s3::TILE - 1) / s3::TILE); }
-int s3_rcap(int R) { return (R + 63) & ~63; }
+constexpr size_t kFlagsLds = (size_t)s3::HCAP * 8;
 }  // namespace
 
 static int g_s3_cap_override = -1;  // tests: a small LDS table forces the global spill path
@@ -917,39 +790,32 @@ OMLDM_API int omldm_scan3_fits(int dn, int dc, int R, int bias) {
          R <= s3::RMAX;
 }
 
-// Workspace sizes (in 4-byte words unless stated) for one round of S spokes × R rows,
-// B rows in all, dc fields, span slots per field.
-//   0 slotsT  [dc·B] int      1 meta   [dc·B] uint32     2 lists [S·dc·Rcap] uint64 (×2 words)
-//   3 counts  [S·dc]          4 tileoff [S·dc·(ntiles+1)] 5 lidcount [S]
-//   6 prep    [S·nchs·PF]     7 cout  [B]                 8 ws [S·WS]   9 wsd [S·DS]
-//  10 aglob   [S·gstride]
+// Workspace sizes (4-byte words) for one round of S spokes × R rows, B rows in all, dc
+// fields:  0 slotsT [dc·B]   1 meta [dc·B]   2 lidcount [S]   3 prep [S·nchs·PF]
+//          4 cout [B]        5 ws [S·WS]     6 wsd [S·DS]     7 aglob [S·gstride]
 OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn, int dc,
                                          long long span, int bias) {
+  (void)span;
   const long long nchs = (R + s3::CH - 1) / s3::CH;
   const int kn = s3_kn(dn, bias);
   const long long pf = kn == 16 ? s3_prep_floats<16>() : s3_prep_floats<32>();
-  const long long rcap = s3_rcap(R);
   switch (which) {
     case 0: case 1: return (long long)dc * B;
-    case 2: return 2LL * S * dc * rcap;
-    case 3: return (long long)S * dc;
-    case 4: return (long long)S * dc * (s3_ntiles((uint32_t)span) + 1);
-    case 5: return S;
-    case 6: return (long long)S * nchs * pf;
-    case 7: return B;
-    case 8: return (long long)S * s3::WS;
-    case 9: return (long long)S * s3::DS;
-    case 10: return (long long)S * ((long long)R * dc / 2 + 64);
+    case 2: return S;
+    case 3: return (long long)S * nchs * pf;
+    case 4: return B;
+    case 5: return (long long)S * s3::WS;
+    case 6: return (long long)S * s3::DS;
+    case 7: return (long long)S * ((long long)R * dc / 2 + 64);
   }
   return 0;
 }
 
+OMLDM_API int omldm_scan3_nbufs() { return 8; }
+
 struct S3Ws {
   int* slotsT;
   uint32_t* meta;
-  unsigned long long* lists;
-  int* counts;
-  int* tileoff;
   int* lidcount;
   float* prep;
   float* cout;
@@ -958,10 +824,15 @@ struct S3Ws {
   float* aglob;
 };
 
-// Passes 1-3 (model-independent): slots, dedupe, Grams. `src` is the tokens (hashed = 0)
-// or row-major field-aware slots (hashed = 1). `ptrs` = the 11 workspaces above.
-// span: slots per field (0: (dim − dn − 1) / dc, the raw-token hashing's; the compact
-// wire's cat_span otherwise — fields occupy [dn + f·span, dn + (f + 1)·span)).
+static S3Ws s3_ws(void* const* ptrs) {
+  return S3Ws{(int*)ptrs[0], (uint32_t*)ptrs[1], (int*)ptrs[2], (float*)ptrs[3],
+              (float*)ptrs[4], (float*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7]};
+}
+
+// Passes 1-3 (model-independent): slots, flags, Grams. `src` is the tokens (hashed = 0),
+// row-major int32 field-aware slots (1) or the compact int16 slots (2). span: slots per
+// field (0: (dim − dn − 1) / dc, the raw-token hashing's; the compact wire's cat_span
+// otherwise — fields occupy [dn + f·span, dn + (f + 1)·span)).
 OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int hashed, int dc,
                                   int B, int R, int S, int dim, int bias, int rule, int variant,
                                   float C, long long span_in, void* const* ptrs, void* stream) {
@@ -971,25 +842,13 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   if (span_in < 0 || (long long)dn + (long long)dc * span_in > (long long)dim - 1) return -2;
   hipStream_t st = (hipStream_t)stream;
   const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
-  const S3Ws W{(int*)ptrs[0], (uint32_t*)ptrs[1], (unsigned long long*)ptrs[2], (int*)ptrs[3],
-               (int*)ptrs[4], (int*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7], (float*)ptrs[8],
-               (float*)ptrs[9], (float*)ptrs[10]};
+  const S3Ws W = s3_ws(ptrs);
   const int S_act = s3_sact(B, R, S);
   hipLaunchKernelGGL(s3_slots_kernel, dim3((B + 255) / 256), dim3(256), 0, st, src, B, dc, dn,
                      span, hashed, W.slotsT);
   hipMemsetAsync(W.lidcount, 0, sizeof(int) * S, st);
-  int npow = s3::DT;
-  while (npow < R) npow <<= 1;
-  const size_t dl = (size_t)npow * (8 + 4);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&s3_dedupe_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
-    attr = true;
-  }
-  hipLaunchKernelGGL(s3_dedupe_kernel, dim3(dc, S_act), dim3(s3::DT), dl, st, W.slotsT, B, R,
-                     dc, dn, span, s3_ntiles(span), s3_rcap(R), W.meta, W.lists, W.counts,
-                     W.tileoff, W.lidcount);
+  hipLaunchKernelGGL(s3_flags_kernel, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
+                     W.meta, W.lidcount);
   const int nchs = (R + s3::CH - 1) / s3::CH;
   const int affine = rule != kSeqLogistic;
   const float kadd = (rule != kSeqLogistic && variant == 2) ? 0.5f / C : 0.f;
@@ -1002,9 +861,9 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   return (int)hipGetLastError();
 }
 
-// Pass 4 (the scan) + pass 5 (the combine into dacc) on a prepared round. The combine runs
-// as `parts` launches over disjoint tile ranges: part k completes dacc over a key range
-// (omldm_scan3_part_bounds) so its collective can start while the next part sums.
+// Pass 4 (the scan) + pass 5 (the combine into dacc, zeroed here) on a prepared round.
+// `parts` is kept for the pipelined-sync interface: part 0 completes all of dacc (the
+// combine is a few tens of µs of atomics), later parts launch nothing.
 OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int y8, int B, int R,
                               int S, float* dacc, int dim, double* cum, int rule, int variant,
                               float C, float eps, float lr, float inv_p, int bias,
@@ -1013,57 +872,45 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
   if (span_in < 0 || (long long)dn + (long long)dc * span_in > (long long)dim - 1) return -2;
+  if (part != 0) return 0;
+  (void)parts;
   hipStream_t st = (hipStream_t)stream;
   const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
-  const S3Ws W{(int*)ptrs[0], (uint32_t*)ptrs[1], (unsigned long long*)ptrs[2], (int*)ptrs[3],
-               (int*)ptrs[4], (int*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7], (float*)ptrs[8],
-               (float*)ptrs[9], (float*)ptrs[10]};
+  const S3Ws W = s3_ws(ptrs);
   const int S_act = s3_sact(B, R, S);
   const int nchs = (R + s3::CH - 1) / s3::CH;
   const int kn = s3_kn(dn, bias);
-  if (part == 0) {
-    const SeqParams p{rule, variant, variant == 1 ? C : INFINITY, variant == 2 ? 0.5f / C : 0.f,
-                      eps, lr, inv_p, bias, y8, span};
-    const int cap = omldm_scan3_lds_cap();
-    const long long gstride = (long long)R * dc / 2 + 64;
-    int e;
-    if (kn == 16) {
-      e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
-        : rule == kSeqEps ? s3_launch_scan<kSeqEps, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
-        : s3_launch_scan<kSeqLogistic, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st);
-    } else {
-      e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
-        : rule == kSeqEps ? s3_launch_scan<kSeqEps, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
-        : s3_launch_scan<kSeqLogistic, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st);
-    }
-    if (e) return e;
+  const SeqParams p{rule, variant, variant == 1 ? C : INFINITY, variant == 2 ? 0.5f / C : 0.f,
+                    eps, lr, inv_p, bias, y8, span};
+  const int cap = omldm_scan3_lds_cap();
+  const long long gstride = (long long)R * dc / 2 + 64;
+  int e;
+  if (kn == 16) {
+    e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
+      : rule == kSeqEps ? s3_launch_scan<kSeqEps, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
+      : s3_launch_scan<kSeqLogistic, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st);
+  } else {
+    e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
+      : rule == kSeqEps ? s3_launch_scan<kSeqEps, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
+      : s3_launch_scan<kSeqLogistic, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st);
   }
-  const int ntiles = s3_ntiles(span);
-  const int nblk = dc * ntiles + 2;
-  const int lo = (int)((long long)nblk * part / parts), hi = (int)((long long)nblk * (part + 1) / parts);
-  if (hi > lo)
-    hipLaunchKernelGGL(s3_combine_kernel, dim3(hi - lo), dim3(512), 0, st, W.lists, W.tileoff,
-                       W.cout, W.ws, W.wsd, S_act, R, dc, dn, span, ntiles, s3_rcap(R), dim, bias,
-                       kn, inv_p, lo, hi, dacc, cum);
+  if (e) return e;
+  (void)span;
+  hipMemsetAsync(dacc, 0, sizeof(float) * (size_t)dim, st);
+  const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
+  hipLaunchKernelGGL(s3_scatter_kernel, dim3((n_rows + s3::SB - 1) / s3::SB, dc), dim3(256), 0, st,
+                     W.slotsT, W.cout, B, n_rows, inv_p, dacc);
+  hipLaunchKernelGGL(s3_dense_kernel, dim3(1), dim3(256), 0, st, W.ws, W.wsd, S_act, dn, dim,
+                     bias, inv_p, dacc, cum);
   return (int)hipGetLastError();
 }
 
-// [lo, hi) of dacc that combine part `part` of `parts` completes (the last part also the
-// numerical columns, the tail, the intercept and dacc[dim], dacc[dim + 1]).
+// [lo, hi) of dacc that combine part `part` of `parts` completes: part 0 all of it.
 OMLDM_API int omldm_scan3_part_bounds(int dim, int dn, int dc, long long span_in, int part,
                                       int parts, long long* lohi) {
-  const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
-  const int ntiles = s3_ntiles(span);
-  const int nblk = dc * ntiles + 2;
-  const int lo = (int)((long long)nblk * part / parts), hi = (int)((long long)nblk * (part + 1) / parts);
-  auto start = [&](int blk) -> long long {  // first dacc index block blk writes
-    if (blk <= 0) return 0;
-    if (blk > dc * ntiles) return (long long)dn + (long long)dc * span;
-    const int f = (blk - 1) / ntiles, j = (blk - 1) - f * ntiles;
-    return (long long)dn + (long long)f * span + (long long)j * s3::TILE;
-  };
-  lohi[0] = start(lo);
-  lohi[1] = hi >= nblk ? (long long)dim + 2 : start(hi);
+  (void)dn, (void)dc, (void)span_in, (void)parts;
+  lohi[0] = part == 0 ? 0 : (long long)dim + 2;
+  lohi[1] = (long long)dim + 2;
   return 0;
 }
 

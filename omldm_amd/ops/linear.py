@@ -276,16 +276,15 @@ def linear_scan_prepare_slots(batch: RawBatch, R: int, S: int, dim: int, bias: b
 
 
 # ------------------------------------------------------------------ v3: the table scan
-S3_BUFS = ("slotsT", "meta", "lists", "counts", "tileoff", "lidcount", "prep", "cout", "ws",
-           "wsd", "aglob")
-_S3_SHARED = (7, 8, 9, 10)  # run-time buffers (scan → combine, same stream): one set per device
+S3_BUFS = ("slotsT", "meta", "lidcount", "prep", "cout", "ws", "wsd", "aglob")
+_S3_SHARED = (4, 5, 6, 7)  # run-time buffers (scan → combine, same stream): one set per device
 
 
 @dataclass
 class Scan3Prep:
-    """Passes 1-3 of a v3 round (field-major slots, per-(spoke, field) dedupe with the
-    sorted occurrence lists, scaled chunk Grams) — model-independent, made ahead on
-    another stream while the previous round scans. ``ptrs`` = the 11 workspaces."""
+    """Passes 1-3 of a v3 round (field-major slots, per-(spoke, field) occurrence flags and
+    table ids, scaled chunk Grams) — model-independent, made ahead on another stream while
+    the previous round scans. ``ptrs`` = the 8 workspaces."""
 
     bufs: list
     ptrs: object

@@ -250,7 +250,7 @@ def test_gpu_scan3_parts_report_key_ranges(monkeypatch):
     space = FeatureSpace(13, 0, 26, 1 << 16)
     w1, g1, _, _, got1 = _round("scan3", monkeypatch, space, 2048, 4, 512, L.RULE_HINGE)
     w4, g4, _, _, got4 = _round("scan3", monkeypatch, space, 2048, 4, 512, L.RULE_HINGE, parts=4)
-    assert torch.equal(g1, g4)
+    assert torch.allclose(g1, g4, rtol=1e-6, atol=1e-7)  # atomic sums: order may differ
     assert [k for k, _, _ in got4] == [0, 1, 2, 3]
     assert got4[0][1] == 0 and got4[-1][2] == space.dim + 2
     assert all(got4[i][2] == got4[i + 1][1] for i in range(3))
