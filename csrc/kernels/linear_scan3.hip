@@ -48,13 +48,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace s3 {
 constexpr int CH = 64;                     // rows per chunk = scanner lanes
-constexpr int NH = 7;                      // helper waves
+#ifndef OMLDM_S3_NH
+#define OMLDM_S3_NH 11
+#endif
+// helper waves: 11 + the scanner = 12 waves, 3 per SIMD (≤ 168 VGPRs each): with 7 the
+// helpers' ~6 K cycles per chunk matched the scanner's and set the chunk period
+constexpr int NH = OMLDM_S3_NH;
 constexpr int NT = 64 * (NH + 1);
+constexpr int WPE = (NH + 1 + 3) / 4;      // waves per SIMD
+// (idling the two helpers that share the scanner's SIMD left the chain as slow: 317 vs
+// 303 µs per round — the SIMD's other waves are not what slows the scanner)
+constexpr int NHA = NH;
 constexpr int GS = CH + 4;                 // LDS row stride of G / X1
 constexpr int MAXF = 32;                   // categorical fields per row
-constexpr int NF = (MAXF + NH - 1) / NH;   // fields per helper wave (5)
+constexpr int NF = (MAXF + NHA - 1) / NHA;  // fields per working helper wave
 constexpr int KNMAX = 32;                  // dense columns (numerical + intercept)
-constexpr int NJ = (KNMAX + NH - 1) / NH;  // dense columns per helper wave (5)
+constexpr int NJ = (KNMAX + NHA - 1) / NHA;  // dense columns per working helper wave
 constexpr int MAT = CH * CH;
 constexpr int RMAX = 8192;                 // rows per spoke (16-bit rows in the flags table)
 constexpr int WS = 8;                      // per-spoke stat row
@@ -67,9 +76,15 @@ constexpr uint32_t F_SIGN = 8u;
 constexpr int LID_SHIFT = 10;
 }  // namespace s3
 
-// floats of one chunk's prep block: aG | aX1 | a | dense columns transposed [KN][64]
+// floats of one chunk's prep block: aG | aX1 | a | dense columns transposed [KN][64] | y
+// (the target as fp32, NaN for a row without one or past the shard: the scanner reads it
+// a chunk ahead with no conversion — an int8 label's convert made it wait for the load)
 template <int KN>
 __host__ __device__ constexpr int s3_prep_floats() {
+  return 2 * s3::MAT + s3::CH + KN * s3::CH + s3::CH;
+}
+template <int KN>
+__host__ __device__ constexpr int s3_prep_y() {
   return 2 * s3::MAT + s3::CH + KN * s3::CH;
 }
 
@@ -224,6 +239,7 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
 template <int KN>
 __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ slotsT, int dc,
                                                       const float* __restrict__ num, int dn,
+                                                      const void* __restrict__ yv, int y8,
                                                       int B, int R, int bias, int affine,
                                                       float kadd, float* __restrict__ prep,
                                                       int nchs) {
@@ -261,6 +277,7 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
     if (live) a = affine ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : 1.f;
     sa[tid] = a;
     out[2 * s3::MAT + tid] = a;
+    out[s3_prep_y<KN>() + tid] = live ? load_y(yv, t0 + c * s3::CH + tid, y8) : __builtin_nanf("");
   }
   // dense columns transposed for the helper waves (coalesced per column)
   for (int i = tid; i < KN * s3::CH; i += 256) {
@@ -325,7 +342,7 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
 struct S3Smem {
   alignas(16) float G[2][s3::CH][s3::GS];   // aG_k by chunk parity
   alignas(16) float X1[2][s3::CH][s3::GS];  // aX1_{k+1} (read by the scanner in chunk k)
-  float part[2][s3::NH][s3::CH];            // base-margin partials per helper wave
+  float part[2][s3::NHA][s3::CH];           // base-margin partials per working helper
   float cb[2][s3::CH];                      // c of the chunk, by parity
 };
 // + dynamic LDS: the slot table, `cap` floats
@@ -347,7 +364,7 @@ struct S3Cand {
 __device__ unsigned long long* g_s3_stamps;
 
 template <int RULE, int KN>
-__global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void s3_scan_kernel(
+__global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s3_scan_kernel(
     const int* __restrict__ slotsT, const uint32_t* __restrict__ meta, int dc, int dn,
     const void* __restrict__ yv, int B, int R, const float* __restrict__ prep, int nchs,
     const float* __restrict__ w, int dim, float* __restrict__ aglob, int cap, long long gstride,
@@ -371,7 +388,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   float* ag = aglob + (size_t)s * gstride;
 
   unsigned long long* stamps = g_s3_stamps;
-  unsigned long long st_acc[8] = {};
+  unsigned long long st_acc[12] = {};
   unsigned long long st_t = stamps ? clock64() : 0;
   auto stamp = [&](int k) {
     if (stamps) {
@@ -386,7 +403,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
     __builtin_amdgcn_s_setprio(3);
     float loss = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f;
     float f1 = 0.f;  // a·(X1_k · c_{k−1}) for this lane's row of chunk k
-    float ynx = load_y(yv, min(t0 + lane, t1 - 1), p.y8);
+    float ynx = chunk_prep(0)[s3_prep_y<KN>() + lane];
     float anx = chunk_prep(0)[2 * s3::MAT + lane];
     for (int k = -1; k <= nch; ++k) {
       if (k >= 0 && k < nch) {
@@ -396,12 +413,12 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
         const float y = valid ? ynx : 0.f;
         const float a = valid ? anx : 0.f;
         if (k + 1 < nch) {
-          ynx = load_y(yv, min(row + s3::CH, t1 - 1), p.y8);
+          ynx = chunk_prep(k + 1)[s3_prep_y<KN>() + lane];
           anx = chunk_prep(k + 1)[2 * s3::MAT + lane];
         }
         float m0 = 0.f;
 #pragma unroll
-        for (int q = 0; q < s3::NH; ++q) m0 += sm.part[b][q][lane];
+        for (int q = 0; q < s3::NHA; ++q) m0 += sm.part[b][q][lane];
         S3Cand<RULE> cf;
         float u, bc = 0.f;
         const float inv = -a;
@@ -431,6 +448,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
           gg[t4] = g4.x, gg[t4 + 1] = g4.y, gg[t4 + 2] = g4.z, gg[t4 + 3] = g4.w;
           xx[t4] = x4.x, xx[t4 + 1] = x4.y, xx[t4 + 2] = x4.z, xx[t4 + 3] = x4.w;
         }
+        stamp(8);
         float n1 = 0.f;
 #pragma unroll
         for (int t = 0; t < s3::CH; ++t) {
@@ -441,6 +459,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
           // in SGPRs and runs the fold as a serial tail after the chunk
           asm volatile("" : "+v"(u), "+v"(n1));
         }
+        stamp(9);
         const float c = cf(u, p, y);
         sm.cb[b][lane] = c;
         if (row < t1) cout[row] = c;
@@ -458,7 +477,8 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
       stamp(1);
     }
     if (stamps && lane == 0)
-      for (int q = 0; q < 2; ++q) atomicAdd(&stamps[(size_t)s * 16 + q], st_acc[q]);
+      for (int q = 0; q < 12; ++q)
+        if (q < 2 || q >= 8) atomicAdd(&stamps[(size_t)s * 16 + q], st_acc[q]);
     loss = wave_sum(loss);
     nex = wave_sum(nex);
     mist = wave_sum(mist);
@@ -478,13 +498,13 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   }
 
   // ------------------------------------------------------------------- helpers
-  // wave q owns categorical fields f ≡ q and dense columns j ≡ q (mod NH); lane r = row
+  // helper q owns categorical fields f ≡ q and dense columns j ≡ q (mod NHA); lane r = row
   const int q = wave - 1, r = lane;
-  const int hl = tid - 64;
+  const int hl = q * 64 + lane;
   float wn[s3::NJ], w0[s3::NJ];  // running dense weights of this wave's columns, round start
 #pragma unroll
   for (int i = 0; i < s3::NJ; ++i) {
-    const int j = q + s3::NH * i;
+    const int j = q + s3::NHA * i;
     w0[i] = (j < KN) ? (j < dn ? w[j] : ((p.bias && j == dn) ? w[dim - 1] : 0.f)) : 0.f;
     wn[i] = w0[i];
   }
@@ -497,7 +517,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   // every NXT load complete before the barrier), and every load is issued unconditionally
   // (clamped address, result selected after): loads under exec-masked branches leave the
   // compiler unable to count the loads in flight, and it would wait for all of them.
-  constexpr int NV4 = (2 * s3::MAT / 4 + 64 * s3::NH - 1) / (64 * s3::NH);  // 5
+  constexpr int NV4 = (2 * s3::MAT / 4 + 64 * s3::NHA - 1) / (64 * s3::NHA);
   struct Set {
     int cs[s3::NF];
     uint32_t cm[s3::NF];
@@ -509,7 +529,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   auto load_words = [&](int ch, Set& S) {
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
-      const int f = q + s3::NH * i;
+      const int f = q + s3::NHA * i;
       const int row = t0 + ch * s3::CH + r;
       const bool ok = ch >= 0 && ch < nch && f < dc && row < t1;
       const size_t at = ok ? (size_t)f * B + row : 0;
@@ -530,7 +550,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   auto issue_staging = [&](int ch, Set& S) {
 #pragma unroll
     for (int u = 0; u < NV4; ++u) {
-      const int i = min(hl + 64 * s3::NH * u, 2 * s3::MAT / 4 - 1);
+      const int i = min(hl + 64 * s3::NHA * u, 2 * s3::MAT / 4 - 1);
       const int mtx = i >> 10, e = i & 1023;
       const int kc = max(0, min(ch + mtx, nch - 1));
       S.v[u] = reinterpret_cast<const f32x4*>(chunk_prep(kc) + mtx * s3::MAT)[e];
@@ -540,7 +560,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   auto load_dense = [&](int ch, float* xd) {
 #pragma unroll
     for (int i = 0; i < s3::NJ; ++i) {
-      const int j = q + s3::NH * i;
+      const int j = q + s3::NHA * i;
       const bool ok = j < KN && ch >= 0 && ch < nch;
       const int jc = j < KN ? j : 0, cc = max(0, min(ch, nch - 1));
       const float v = chunk_prep(cc)[2 * s3::MAT + s3::CH + jc * s3::CH + r];
@@ -576,7 +596,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
       }
 #pragma unroll
       for (int i = 0; i < s3::NJ; ++i) {
-        const int j = q + s3::NH * i;
+        const int j = q + s3::NHA * i;
         if (j < KN) wn[i] += wave_sum(cv * CUR.xs[i]);
       }
     }
@@ -616,7 +636,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
     // ---- aG_{cn} → G[cn & 1], aX1_{cn+1} → X1[(cn+1) & 1]
 #pragma unroll
     for (int u = 0; u < NV4; ++u) {
-      const int i = hl + 64 * s3::NH * u;
+      const int i = hl + 64 * s3::NHA * u;
       const int mtx = i >> 10, e = i & 1023;
       if (i < 2 * s3::MAT / 4 && cn + mtx < nch) {
         const int row = e >> 4, col = (e & 15) * 4;
@@ -652,7 +672,7 @@ __global__ __launch_bounds__(s3::NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2)
   // round end: this wave's dense deltas
 #pragma unroll
   for (int i = 0; i < s3::NJ; ++i) {
-    const int j = q + s3::NH * i;
+    const int j = q + s3::NHA * i;
     if (lane == 0 && j < KN) wsd[(size_t)s * s3::DS + j] = wn[i] - w0[i];
   }
   if (q == 0 && lane >= KN && lane < s3::DS) wsd[(size_t)s * s3::DS + lane] = 0.f;
@@ -834,8 +854,9 @@ static S3Ws s3_ws(void* const* ptrs) {
 // field (0: (dim − dn − 1) / dc, the raw-token hashing's; the compact wire's cat_span
 // otherwise — fields occupy [dn + f·span, dn + (f + 1)·span)).
 OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int hashed, int dc,
-                                  int B, int R, int S, int dim, int bias, int rule, int variant,
-                                  float C, long long span_in, void* const* ptrs, void* stream) {
+                                  const void* y, int y8, int B, int R, int S, int dim, int bias,
+                                  int rule, int variant, float C, long long span_in,
+                                  void* const* ptrs, void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
   if ((long long)(dim - dn - 1) / dc < 1) return -2;
@@ -854,10 +875,10 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   const float kadd = (rule != kSeqLogistic && variant == 2) ? 0.5f / C : 0.f;
   if (s3_kn(dn, bias) == 16)
     hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
-                       num, dn, B, R, bias, affine, kadd, W.prep, nchs);
+                       num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
   else
     hipLaunchKernelGGL(s3_gram_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
-                       num, dn, B, R, bias, affine, kadd, W.prep, nchs);
+                       num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
   return (int)hipGetLastError();
 }
 

@@ -317,7 +317,7 @@ def _s3_mode(batch: RawBatch, hashed: bool) -> int:
 
 def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
     return (batch.B, R, S, dim, bool(bias), rule.rule, rule.variant, float(rule.C), batch.dn,
-            batch.dc, int(batch.span))
+            batch.dc, int(batch.span), batch.y.data_ptr())
 
 
 def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
@@ -340,9 +340,12 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
 
     ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
     st = stream if stream is not None else torch.cuda.current_stream(dev)
-    check(h.omldm_scan3_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), mode, batch.dc,
-                                batch.B, R, S, dim, int(bias), rule.rule, rule.variant,
-                                float(rule.C), span, ptrs, st.cuda_stream), "omldm_scan3_prepare")
+    y = batch.y
+    assert y.dtype in (torch.float32, torch.int8) and y.is_contiguous()
+    check(h.omldm_scan3_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), mode, batch.dc, ptr(y),
+                                int(y.dtype == torch.int8), batch.B, R, S, dim, int(bias),
+                                rule.rule, rule.variant, float(rule.C), span, ptrs,
+                                st.cuda_stream), "omldm_scan3_prepare")
     ev = None
     if stream is not None:
         ev = torch.cuda.Event()
@@ -358,6 +361,10 @@ def scan3_part_bounds(dim: int, dn: int, dc: int, part: int, parts: int,
     check(native.hip().omldm_scan3_part_bounds(dim, dn, dc, span, part, parts, lh),
           "omldm_scan3_part_bounds")
     return int(lh[0]), int(lh[1])
+
+
+# rounds run through the v3 scan in this process (tests: the engine's default path)
+SCAN3_ROUNDS = 0
 
 
 def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
@@ -376,6 +383,8 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
         sp = linear_scan3_prepare(batch, R, S, dim, bool(rule.bias), rule, hashed=hashed)
     elif sp.event is not None:
         torch.cuda.current_stream(w.device).wait_event(sp.event)
+    global SCAN3_ROUNDS
+    SCAN3_ROUNDS += 1
     h = native.hip()
     parts = max(1, int(parts))
     span = _s3_span(batch, dim)

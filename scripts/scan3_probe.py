@@ -52,9 +52,9 @@ torch.cuda.synchronize()
 lib.omldm_scan3_stamps(None)
 m = st.double().mean(0)
 nch = (R + 63) // 64 + 2
-names = ["scan", "scan_bar", "h_top_wait", "h_issue", "h_margins", "h_lds_prefetch", "h_scatter",
-         "h_bar"]
+names = ["scan_tail", "scan_bar", "h_top_wait", "h_issue", "h_margins", "h_lds_prefetch",
+         "h_scatter", "h_bar", "scan_head", "scan_chain"]
 print(json.dumps({"prepare_ms": round(tp / n, 4), "run_ms": round(tr / n, 4),
                   "Mex_s": round(S * R / ((tp + tr) / n) / 1e3, 1),
                   "stamps_cycles_per_chunk": {names[k]: round(float(m[k]) / nch, 1)
-                                              for k in range(8)}}), flush=True)
+                                              for k in range(10)}}), flush=True)

@@ -211,6 +211,7 @@ def test_parallelism_gate_buffers_creates_until_the_job_grows_back(tmp_path):
     job.tick()
     assert job.spoke_parallelism == 8 and set(job.pipes) == {1}
     job.checkpointer.save(job)
+    job.checkpointer.wait()  # the background write is done before the next job restores
     # restored on 4 spokes: pipeline 1 comes back, the new Create waits
     job2, _, _ = make_job(ck + ["--restore", "true", "--spokesPerDevice", "4"], name=name)
     assert job2.parallelism == 4 and job2.spoke_parallelism == 8
@@ -219,6 +220,7 @@ def test_parallelism_gate_buffers_creates_until_the_job_grows_back(tmp_path):
     job2.tick()
     assert set(job2.pipes) == {1} and [m[0] for m in job2.request_buffer] == [2]
     job2.checkpointer.save(job2)
+    job2.checkpointer.wait()
     # restored on 16 spokes: the buffered Create is applied, the job records 16
     job3, _, _ = make_job(ck + ["--restore", "true", "--spokesPerDevice", "16"], name=name)
     assert job3.spoke_parallelism == 16 and len(job3.request_buffer) == 1

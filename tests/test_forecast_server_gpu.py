@@ -123,3 +123,22 @@ def test_every_pipeline_kind_is_answered_per_record():
     job.tick()
     assert [pid for pid, _ in fs._direct] == [2, 4, 5, 6, 7]
     job.fserver.close()
+
+
+def test_default_flag_svm_trains_through_the_v3_scan():
+    """A job started with default flags (field-aware compact slots) and a default SVM
+    Create trains through the exact v3 table scan (csrc/kernels/linear_scan3.hip), fed the
+    compact int16 slots as they are; its weights match the CPU engine's exact spokes."""
+    from omldm_amd.ops import linear as L
+
+    job, br = _job()
+    assert job.space.field_aware and job.space.cat_span > 0
+    _create(br, 1, "SVM")
+    for r in synth_json_records(8000, SP):
+        br.produce("trainingData", r)
+    n0 = L.SCAN3_ROUNDS
+    for _ in range(4):
+        job.tick()
+    assert L.SCAN3_ROUNDS > n0
+    assert job.pipes[1].learner.running_totals()["fitted"] > 0
+    job.fserver.close()
