@@ -31,7 +31,8 @@
 //   1. s3_slots_kernel   tokens (or slots) → field-aware signed slots, FIELD-MAJOR [dc][B]
 //   2. s3_flags_kernel   one workgroup per (field, spoke): an LDS hash table of the
 //                        field's slots (first / last row), table ids, per-occurrence
-//                        flags → meta [dc][B]
+//                        flags → occurrence records {slot, meta} [dc][B] (one 8-B load
+//                        per occurrence in the scan)
 //   3. s3_gram_kernel    one workgroup per (spoke, chunk): a_t, G_k and X1_k (categorical
 //                        match counts and the dense block), scaled by a_t; the chunk's
 //                        dense columns transposed for the helpers
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
     if (lloc[q] >= 0) hkey[h[q]] = lloc[q];  // the slot's key is no longer looked up
   __syncthreads();
   const int base = s_base;
-  uint32_t* out = meta + (size_t)f * B + t0;
+  uint2* out = reinterpret_cast<uint2*>(meta) + (size_t)f * B + t0;  // {slot, meta}
 #pragma unroll
   for (int q = 0; q < s3::RPT; ++q) {
     const int i = tid + q * s3::FT;
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
         m |= (uint32_t)(base + hkey[h[q]]) << s3::LID_SHIFT;
       }
     }
-    out[i] = m;
+    out[i] = make_uint2((uint32_t)v[q], m);
   }
 }
 
@@ -362,6 +363,7 @@ struct S3Cand {
 };
 
 __device__ unsigned long long* g_s3_stamps;
+__device__ int g_s3_debug;  // diagnostics: 1 = every gather reads w[0] (latency experiment)
 
 template <int RULE, int KN>
 __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s3_scan_kernel(
@@ -388,6 +390,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   float* ag = aglob + (size_t)s * gstride;
 
   unsigned long long* stamps = g_s3_stamps;
+  const bool dbg_gather = g_s3_debug == 1;
   unsigned long long st_acc[12] = {};
   unsigned long long st_t = stamps ? clock64() : 0;
   auto stamp = [&](int k) {
@@ -533,17 +536,16 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       const int row = t0 + ch * s3::CH + r;
       const bool ok = ch >= 0 && ch < nch && f < dc && row < t1;
       const size_t at = ok ? (size_t)f * B + row : 0;
-      const int sv = slotsT[at];
-      const uint32_t mv = meta[at];
-      S.cs[i] = ok ? sv : -1;
-      S.cm[i] = ok ? mv : 0u;
+      const uint2 o = reinterpret_cast<const uint2*>(meta)[at];
+      S.cs[i] = ok ? (int)o.x : -1;
+      S.cm[i] = ok ? o.y : 0u;
     }
   };
   auto issue_gathers = [&](Set& S) {
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
       const bool glob = S.cs[i] != -1 && !(S.cm[i] & s3::F_TG);
-      S.g[i] = w[glob ? (S.cs[i] & 0x7fffffff) : 0];  // unused unless glob
+      S.g[i] = w[(glob && !dbg_gather) ? (S.cs[i] & 0x7fffffff) : 0];  // unused unless glob
     }
   };
   // aG_{ch} and aX1_{ch+1} (clamped reads past the round: never stored)
@@ -557,9 +559,10 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     }
   };
   // dense columns of chunk ch (clamped chunk; 0 outside the round / past KN)
+  constexpr int NJK = (KN + s3::NHA - 1) / s3::NHA;  // dense columns of this wave (≤ NJ)
   auto load_dense = [&](int ch, float* xd) {
 #pragma unroll
-    for (int i = 0; i < s3::NJ; ++i) {
+    for (int i = 0; i < NJK; ++i) {
       const int j = q + s3::NHA * i;
       const bool ok = j < KN && ch >= 0 && ch < nch;
       const int jc = j < KN ? j : 0, cc = max(0, min(ch, nch - 1));
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         }
       }
 #pragma unroll
-      for (int i = 0; i < s3::NJ; ++i) {
+      for (int i = 0; i < NJK; ++i) {
         const int j = q + s3::NHA * i;
         if (j < KN) wn[i] += wave_sum(cv * CUR.xs[i]);
       }
@@ -605,7 +608,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     if (cn < nch) {
       float base = 0.f;
 #pragma unroll
-      for (int i = 0; i < s3::NJ; ++i) base = fmaf(CUR.xc[i], wn[i], base);
+      for (int i = 0; i < NJK; ++i) base = fmaf(CUR.xc[i], wn[i], base);
 #pragma unroll
       for (int i = 0; i < s3::NF; ++i) {
         const uint32_t m = CUR.cm[i];
@@ -811,7 +814,7 @@ OMLDM_API int omldm_scan3_fits(int dn, int dc, int R, int bias) {
 }
 
 // Workspace sizes (4-byte words) for one round of S spokes × R rows, B rows in all, dc
-// fields:  0 slotsT [dc·B]   1 meta [dc·B]   2 lidcount [S]   3 prep [S·nchs·PF]
+// fields:  0 slotsT [dc·B]   1 occ [2·dc·B]   2 lidcount [S]   3 prep [S·nchs·PF]
 //          4 cout [B]        5 ws [S·WS]     6 wsd [S·DS]     7 aglob [S·gstride]
 OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn, int dc,
                                          long long span, int bias) {
@@ -820,7 +823,8 @@ OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn,
   const int kn = s3_kn(dn, bias);
   const long long pf = kn == 16 ? s3_prep_floats<16>() : s3_prep_floats<32>();
   switch (which) {
-    case 0: case 1: return (long long)dc * B;
+    case 0: return (long long)dc * B;
+    case 1: return 2LL * dc * B;  // {slot, meta} per occurrence
     case 2: return S;
     case 3: return (long long)S * nchs * pf;
     case 4: return B;
@@ -933,6 +937,10 @@ OMLDM_API int omldm_scan3_part_bounds(int dim, int dn, int dc, long long span_in
   lohi[0] = part == 0 ? 0 : (long long)dim + 2;
   lohi[1] = (long long)dim + 2;
   return 0;
+}
+
+OMLDM_API int omldm_scan3_debug(int v) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s3_debug), &v, sizeof(v));
 }
 
 OMLDM_API int omldm_scan3_stamps(void* buf) {

@@ -58,3 +58,16 @@ print(json.dumps({"prepare_ms": round(tp / n, 4), "run_ms": round(tr / n, 4),
                   "Mex_s": round(S * R / ((tp + tr) / n) / 1e3, 1),
                   "stamps_cycles_per_chunk": {names[k]: round(float(m[k]) / nch, 1)
                                               for k in range(10)}}), flush=True)
+
+# latency experiment: every gather reads w[0] (wrong model, timing only)
+lib.omldm_scan3_debug.argtypes = [ctypes.c_int]
+lib.omldm_scan3_debug(1)
+st.zero_()
+lib.omldm_scan3_stamps(st.data_ptr())
+L.linear_seq_round(w, b, R, S, dacc, rule, 1.0 / S, cum=cum)
+torch.cuda.synchronize()
+lib.omldm_scan3_stamps(None)
+lib.omldm_scan3_debug(0)
+m = st.double().mean(0)
+print(json.dumps({"gathers_hit_w0": {names[k]: round(float(m[k]) / nch, 1)
+                                     for k in range(10)}}), flush=True)
