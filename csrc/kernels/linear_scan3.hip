@@ -98,11 +98,12 @@ __device__ __forceinline__ void spoke_rows(int s, int R, int B, int& t0, int& t1
 // ------------------------------------------------------------------ pass 1: slots
 // 256 rows per block through an LDS tile: coalesced row-major reads, coalesced
 // field-major writes. hashed = 0: 32-bit tokens (murmur3 per field); 1: int32 signed
-// slots; 2: the engine's compact uint16 {sign, local} (0xFFFF absent), slot = dn +
-// f·span + local — the wire format trains without a widening pass.
+// slots; 2: the engine's compact uint16 {sign, local} (0xFFFF absent), slot = cbase +
+// f·span + local (cbase: the feature space's dense slot count, which a preprocessor
+// that widens the numerical block leaves unchanged) — the wire trains without widening.
 __global__ __launch_bounds__(256) void s3_slots_kernel(const void* __restrict__ src, int B,
                                                        int dc, int dn, uint32_t span, int hashed,
-                                                       int* __restrict__ slotsT) {
+                                                       int cbase, int* __restrict__ slotsT) {
   __shared__ int tile[256][s3::MAXF + 1];
   const int r0 = blockIdx.x * 256, tid = threadIdx.x;
   const int nr = min(256, B - r0);
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(256) void s3_slots_kernel(const void* __restrict__ 
     if (hashed == 2) {
       const uint32_t v = reinterpret_cast<const uint16_t*>(src)[(size_t)r0 * dc + i];
       slot = v == 0xFFFFu ? -1
-                          : (int)(((uint32_t)dn + (uint32_t)f * span + (v & 0x7FFFu)) |
+                          : (int)(((uint32_t)cbase + (uint32_t)f * span + (v & 0x7FFFu)) |
                                   ((v & 0x8000u) << 16));
     } else {
       const uint32_t v = reinterpret_cast<const uint32_t*>(src)[(size_t)r0 * dc + i];
@@ -860,17 +861,18 @@ static S3Ws s3_ws(void* const* ptrs) {
 OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int hashed, int dc,
                                   const void* y, int y8, int B, int R, int S, int dim, int bias,
                                   int rule, int variant, float C, long long span_in,
-                                  void* const* ptrs, void* stream) {
+                                  int cbase, void* const* ptrs, void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
   if ((long long)(dim - dn - 1) / dc < 1) return -2;
-  if (span_in < 0 || (long long)dn + (long long)dc * span_in > (long long)dim - 1) return -2;
+  if (cbase < 0) cbase = dn;
+  if (span_in < 0 || (long long)cbase + (long long)dc * span_in > (long long)dim - 1) return -2;
   hipStream_t st = (hipStream_t)stream;
   const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
   const S3Ws W = s3_ws(ptrs);
   const int S_act = s3_sact(B, R, S);
   hipLaunchKernelGGL(s3_slots_kernel, dim3((B + 255) / 256), dim3(256), 0, st, src, B, dc, dn,
-                     span, hashed, W.slotsT);
+                     span, hashed, cbase, W.slotsT);
   hipMemsetAsync(W.lidcount, 0, sizeof(int) * S, st);
   hipLaunchKernelGGL(s3_flags_kernel, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
                      W.meta, W.lidcount);
@@ -896,7 +898,7 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
                               void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
-  if (span_in < 0 || (long long)dn + (long long)dc * span_in > (long long)dim - 1) return -2;
+  if (span_in < 0) return -2;  // the slots' range was checked by the prepare
   if (part != 0) return 0;
   (void)parts;
   hipStream_t st = (hipStream_t)stream;

@@ -257,8 +257,11 @@ class RawBatch:
     # passes 1-2 of the v2 round made ahead of the round (ops.linear.ScanPrep), or None
     prep: object = None
     # > 0: ``tok`` holds the engine's compact int16 field-aware slots (HashedBatch.cat with
-    # this cat_span) instead of tokens — the v3 round reads them as they are
+    # this cat_span) instead of tokens — the v3 round reads them as they are; their slots
+    # start at ``cbase`` (the feature space's dense slot count: a preprocessor that widens
+    # ``num`` does not move them)
     span: int = 0
+    cbase: int = 0
 
     @property
     def B(self) -> int:

@@ -126,8 +126,8 @@ class LinearLearner(Learner):
     def _fit_slots(self, batch: HashedBatch, ctx: RoundContext) -> None:
         num, y = batch.num.float().contiguous(), batch.y.float().contiguous()
         R, S = self._seq_geometry(batch.B, ctx)
-        rb = RawBatch(num, batch.cat.contiguous(), y, span=batch.cat_span)
-        if L.scan3_eligible(rb, R, self.rule.bias):  # compact slots straight into pass 1
+        rb = RawBatch(num, batch.cat.contiguous(), y, span=batch.cat_span, cbase=self.space.dn)
+        if L.scan3_eligible_compact(rb, R, self.rule.bias, self.dim):  # compact slots as they are
             return self._fit_raw(rb, ctx, hashed=True)
         rb = RawBatch(num, batch.to_wide().cat.contiguous(), y)
         rb.prep = L.linear_scan_prepare_slots(rb, R, S, self.dim, bool(self.rule.bias))

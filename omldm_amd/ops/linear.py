@@ -306,6 +306,12 @@ def _s3_span(batch: RawBatch, dim: int) -> int:
     return int(batch.span) if batch.span > 0 else (dim - batch.dn - 1) // batch.dc
 
 
+def scan3_eligible_compact(batch: RawBatch, R: int, bias: bool, dim: int) -> bool:
+    """v3 on compact slots: the field ranges [cbase + f·span, …) must fit the model."""
+    return (scan3_eligible(batch, R, bias)
+            and batch.cbase + batch.dc * batch.span <= dim - 1)
+
+
 def _s3_mode(batch: RawBatch, hashed: bool) -> int:
     """s3_slots_kernel input: 0 tokens, 1 int32 signed slots, 2 compact int16 slots."""
     if batch.span > 0:
@@ -344,7 +350,8 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
     assert y.dtype in (torch.float32, torch.int8) and y.is_contiguous()
     check(h.omldm_scan3_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), mode, batch.dc, ptr(y),
                                 int(y.dtype == torch.int8), batch.B, R, S, dim, int(bias),
-                                rule.rule, rule.variant, float(rule.C), span, ptrs,
+                                rule.rule, rule.variant, float(rule.C), span,
+                                int(batch.cbase) if batch.span > 0 else -1, ptrs,
                                 st.cuda_stream), "omldm_scan3_prepare")
     ev = None
     if stream is not None:
