@@ -159,11 +159,11 @@ def engine_e2e_rate(records: int, batch: int = 65536) -> dict:
     from omldm_amd.utils.config import JobConfig
 
     sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
-    parts = 8
+    parts = 8  # partitions are read concurrently (one GIL-free pread each; 8 MB regions)
     with tempfile.TemporaryDirectory() as root:
         br = FileBroker(root)
         br.create_topic("trainingData", parts)
-        br.create_topic("forecastingData", parts)
+        br.create_topic("forecastingData", 8)
         uniq = synth_json_records(20000, sp, start=0, seed=3)
         for p in range(parts):
             recs = [uniq[i % len(uniq)] for i in range(p, records, parts)]

@@ -59,12 +59,13 @@ def main(argv=None) -> int:
         n_fc = int(a.records * a.forecast_frac)
         fc = synth_json_records(min(a.unique, max(n_fc, 1)), sp, start=10**7, seed=3,
                                 operation="forecasting") if n_fc else []
-        br.create_topic("forecastingData", a.partitions)
+        br.create_topic("forecastingData", min(8, a.partitions))  # a small topic
         for topic, n, src in (("trainingData", a.records - n_fc, uniq),
                               ("forecastingData", n_fc, fc)):
-            per_part = [[] for _ in range(a.partitions)]
+            np_ = a.partitions if topic == "trainingData" else min(8, a.partitions)
+            per_part = [[] for _ in range(np_)]
             for i in range(n):
-                per_part[i % a.partitions].append(src[i % len(src)])
+                per_part[i % np_].append(src[i % len(src)])
             for p, recs in enumerate(per_part):
                 if recs:
                     br.produce_block(topic, p, ("\n".join(recs) + "\n").encode())

@@ -58,7 +58,10 @@ class HoldoutSet:
         self.count = np.zeros(S, dtype=np.int64)   # reference counter (mod 10), per spoke
         self.head = np.zeros(S, dtype=np.int64)    # next write position, per spoke
         self.filled = np.zeros(S, dtype=np.int64)
-        self._desc_host = None
+        # descriptor staging: a ring of pinned host slots (the H2D copy reads a slot when
+        # the stream runs it; the slot is reused RING ticks later, after its event)
+        self._ring = None
+        self._ring_i = 0
 
     _held_before = staticmethod(held_before)
 
@@ -69,32 +72,39 @@ class HoldoutSet:
         R = -(-B // S) if B else 0
         return [(min(s * R, B), min(s * R + R, B)) for s in range(S)]
 
-    def _plan(self, B: int) -> np.ndarray:
+    @staticmethod
+    def _held_before_v(x: np.ndarray) -> np.ndarray:
+        return (x // 10) * 2 + np.maximum(0, x % 10 - 8)
+
+    def _plan(self, B: int, out: np.ndarray | None = None) -> np.ndarray:
         """One descriptor per spoke (b0, n0, n1, r1, n2, s2, ns, hs, rw, o0, c, 0) and the
-        advanced counters / heads / fills. n0 non-held rows, n1 evicted ring rows from
-        r1, n2 held rows from hold-ordinal s2 that never fit; ns held rows from ordinal
-        hs written to the ring from rw."""
+        advanced counters / heads / fills — vectorised over the spokes (the tick's host
+        cost). n0 non-held rows, n1 evicted ring rows from r1, n2 held rows from
+        hold-ordinal s2 that never fit; ns held rows from ordinal hs written to the ring
+        from rw."""
         S, size = self.spokes, self.size
-        desc = np.zeros((S, DESC_W), dtype=np.int64)
-        o = 0
-        for s, (a, b) in enumerate(self.shard_bounds(B)):
-            Bs, c = b - a, int(self.count[s])
-            head, filled = int(self.head[s]), int(self.filled[s])
-            n_hold = held_before(c + Bs) - held_before(c)
-            n0 = Bs - n_hold
-            r1 = (head - filled) % size
-            if n_hold >= size:
-                n1, n2, s2 = filled, n_hold - size, 0
-                ns, hs, rw = size, n_hold - size, 0
-                head, filled = 0, size
-            else:
-                n1, n2, s2 = max(0, filled + n_hold - size), 0, 0
-                ns, hs, rw = n_hold, 0, head
-                head, filled = (head + n_hold) % size, min(size, filled + n_hold)
-            desc[s] = (a, n0, n1, r1, n2, s2, ns, hs, rw, o, c, 0)
-            o += n0 + n1 + n2
-            self.count[s] = (c + Bs) % 10
-            self.head[s], self.filled[s] = head, filled
+        R = -(-B // S) if B else 0
+        a = np.minimum(np.arange(S, dtype=np.int64) * R, B)
+        Bs = np.minimum(a + R, B) - a
+        c, head, filled = self.count, self.head, self.filled
+        n_hold = self._held_before_v(c + Bs) - self._held_before_v(c)
+        n0 = Bs - n_hold
+        r1 = (head - filled) % size
+        full = n_hold >= size
+        n1 = np.where(full, filled, np.maximum(0, filled + n_hold - size))
+        n2 = np.where(full, n_hold - size, 0)
+        ns = np.where(full, size, n_hold)
+        hs = np.where(full, n_hold - size, 0)
+        rw = np.where(full, 0, head)
+        n_out = n0 + n1 + n2
+        o = np.concatenate([[0], np.cumsum(n_out)[:-1]])
+        desc = out if out is not None else np.zeros((S, DESC_W), dtype=np.int64)
+        for j, v in enumerate((a, n0, n1, r1, n2, np.zeros_like(a), ns, hs, rw, o, c)):
+            desc[:, j] = v
+        desc[:, 11] = 0
+        self.count = (c + Bs) % 10
+        self.head = np.where(full, 0, (head + n_hold) % size)
+        self.filled = np.where(full, size, np.minimum(size, filled + n_hold))
         return desc
 
     def _route_device(self, batch: HashedBatch, desc: np.ndarray) -> HashedBatch:
@@ -107,20 +117,38 @@ class HoldoutSet:
                           torch.empty((n_out, batch.dc), dtype=batch.cat.dtype, device=self.device),
                           torch.empty(n_out, dtype=torch.float32, device=self.device),
                           cat_span=batch.cat_span)
-        # descriptors: pinned host → device on the compute stream (no sync); the pinned
-        # block stays referenced until the next route (the copy has run by then)
-        host = torch.from_numpy(np.ascontiguousarray(desc)).pin_memory()
-        dev = host.to(self.device, non_blocking=True)
-        self._desc_host = host
+        # descriptors: a pinned ring slot → its device twin on the compute stream (no
+        # host sync, no allocation per tick)
+        host, dev, ev = self._slot()
+        host.numpy()[:] = desc
+        st = torch.cuda.current_stream(self.device)
+        dev.copy_(host, non_blocking=True)
+        ev.record(st)
         p = native.ptr
         rc = native.hip().omldm_holdout_route_spokes(
             p(batch.num), p(batch.cat), p(batch.y), batch.B, p(self.ring.num), p(self.ring.cat),
             p(self.ring.y), self.size, S, p(out.num), p(out.cat), p(out.y), n_out,
             host.numpy().ctypes.data, p(dev), batch.dn, batch.dc, batch.num.element_size(),
-            batch.cat.element_size(), torch.cuda.current_stream(self.device).cuda_stream)
+            batch.cat.element_size(), st.cuda_stream)
         native.check(rc, "omldm_holdout_route_spokes")
-        self._desc_dev = dev
         return out
+
+    RING = 8
+
+    def _slot(self):
+        if self._ring is None:
+            self._ring = [(torch.zeros((self.spokes, DESC_W), dtype=torch.int64).pin_memory(),
+                           torch.zeros((self.spokes, DESC_W), dtype=torch.int64,
+                                       device=self.device), torch.cuda.Event())
+                          for _ in range(self.RING)]
+            self._ring_fresh = [True] * self.RING
+        i = self._ring_i
+        self._ring_i = (i + 1) % self.RING
+        host, dev, ev = self._ring[i]
+        if not self._ring_fresh[i]:
+            ev.synchronize()  # its copy ran RING routes ago: normally long done
+        self._ring_fresh[i] = False
+        return host, dev, ev
 
     def _route_host(self, batch: HashedBatch, desc: np.ndarray) -> HashedBatch:
         """The same rows in the same order by explicit index arrays (CPU jobs, dtype

@@ -23,6 +23,7 @@ prefetcher's read-ahead position.
 from __future__ import annotations
 
 import collections
+import os
 import concurrent.futures as cf
 from dataclasses import dataclass, field
 
@@ -47,6 +48,12 @@ class TickBlock:
     parsed: tuple | None = None   # (num, cat, y, op) device views, parsed by the thread
     counts: np.ndarray | None = None  # host (training, forecasting, invalid) of `parsed`
     out: tuple | None = None      # slot-persistent parse outputs + counts buffers
+    # gap-free device layout: (host start, device start, bytes) per filled region, the
+    # device bytes, and the record offsets in it (pinned) — only the records cross PCIe,
+    # not the regions' unused tails (a third of the slot at the 1.5x read caps)
+    segs: list | None = None
+    dev_nbytes: int = 0
+    doffs_t: torch.Tensor | None = None
 
     @property
     def offs(self) -> np.ndarray:
@@ -112,7 +119,10 @@ class TickIngest:
             if prefetch and self.stage else None
         self._pending: collections.deque = collections.deque()
         nreg = sum(len(c.parts) for c in consumers)
-        self._readers = cf.ThreadPoolExecutor(min(8, nreg), thread_name_prefix="omldm-read") \
+        # one reader per partition region (GIL-free preads), up to 16: 8 reached 51 GB/s of
+        # log reads into pinned memory on the MI355X host (scripts/read_bw_probe.py)
+        nthr = int(os.environ.get("OMLDM_READERS", "16"))
+        self._readers = cf.ThreadPoolExecutor(min(nthr, nreg), thread_name_prefix="omldm-read") \
             if nreg > 1 else None
 
     def _alloc(self, n: int, dtype) -> torch.Tensor:
@@ -125,14 +135,18 @@ class TickIngest:
             return self._fill_block(blk)
 
     def _fill_block(self, blk: TickBlock) -> TickBlock:
+        from omldm_amd.utils import tracing
+
         if blk.event is not None:
-            blk.event.synchronize()  # the GPU has finished copying this slot's last use
+            with tracing.range("ingest_slot_wait"):
+                blk.event.synchronize()  # the GPU has finished copying this slot's last use
             blk.event = None
         # one region of the slot per (consumer, partition), sized from the observed
         # bytes per record; regions are read concurrently when the broker allows it
         jobs, pos = [], 0
         for c in self.consumers:
             for p, share, cap in c.read_plan(self.batch):
+                cap = (cap + 15) & ~15  # 16-B aligned regions (the pull copy's vectors)
                 jobs.append((c, p, share, pos, cap))
                 pos += cap
         if pos > blk.data.numel():
@@ -143,18 +157,22 @@ class TickIngest:
             c, p, share, start, cap = j
             return c.read_region(p, share, dst[start:start + cap])
 
-        if self._readers is not None and len(jobs) > 1 and \
-                all(c.broker.parallel_reads for c in self.consumers):
-            results = list(self._readers.map(read, jobs))
-        else:
-            results = [read(j) for j in jobs]
+        with tracing.range("ingest_pread"):
+            if self._readers is not None and len(jobs) > 1 and \
+                    all(c.broker.parallel_reads for c in self.consumers):
+                results = list(self._readers.map(read, jobs))
+            else:
+                results = [read(j) for j in jobs]
         # Offsets: records of a region are contiguous; the first record of a region
         # starts at the region start, so the record before it also spans the unused tail
         # of its own region. Parsers stop at the record's closing brace; ``ends`` keeps
         # the true end of such records for the raw echo of forecasts.
         offs = blk.offs_t.numpy()
         offs[0] = 0
-        n, end, gaps = 0, 0, []
+        if self.stage and (blk.doffs_t is None or blk.doffs_t.numel() < blk.offs_t.numel()):
+            blk.doffs_t = self._alloc(blk.offs_t.numel(), torch.int64)
+        doffs = blk.doffs_t.numpy() if self.stage else None
+        n, end, gaps, segs, dpos = 0, 0, [], [], 0
         for (c, p, share, start, cap), (k, o) in zip(jobs, results):
             if not k:
                 continue
@@ -162,8 +180,14 @@ class TickIngest:
                 gaps.append((n - 1, end))
             offs[n] = start
             offs[n + 1:n + k + 1] = o[1:k + 1] + start
+            used = int(o[k])
+            if doffs is not None:  # the same records packed (16-B aligned) for the device
+                doffs[n:n + k + 1] = offs[n:n + k + 1] - (start - dpos)
+                segs.append((start, dpos, used))
+                dpos = (dpos + used + 15) & ~15
             n += k
-            end = start + int(o[k])
+            end = start + used
+        blk.segs, blk.dev_nbytes = (segs, dpos) if doffs is not None else (None, 0)
         blk.ends = None
         if gaps:
             ends = offs[1:n + 1].copy()
@@ -185,7 +209,8 @@ class TickIngest:
     def _to_device(self, blk: TickBlock) -> None:
         from omldm_amd.ops.ingest import pull_copy
 
-        n, nbytes = blk.n, blk.nbytes
+        n = blk.n
+        nbytes = blk.dev_nbytes if blk.segs is not None else blk.nbytes
         with torch.cuda.device(self.device):
             grow = (blk.d_raw is None or blk.d_raw.numel() < nbytes + 16 or
                     blk.d_offs is None or blk.d_offs.numel() < n + 1)
@@ -202,14 +227,19 @@ class TickIngest:
                 cs.wait_event(blk.consumed)  # the parser of this slot's last use is done
                 blk.consumed = None
             self.h2d_timer.start(cs)
+            segs = blk.segs if blk.segs is not None else [(0, 0, nbytes)]
+            offs_src = blk.doffs_t if blk.segs is not None else blk.offs_t
             if self.copy_method == "sdma":
                 with torch.cuda.stream(cs):
-                    blk.d_raw[:nbytes].copy_(blk.data[:nbytes], non_blocking=True)
-                    blk.d_offs[:n + 1].copy_(blk.offs_t[:n + 1], non_blocking=True)
+                    for h, d, ln in segs:
+                        blk.d_raw[d:d + ln].copy_(blk.data[h:h + ln], non_blocking=True)
+                    blk.d_offs[:n + 1].copy_(offs_src[:n + 1], non_blocking=True)
             else:
-                pull_copy(blk.d_raw, blk.data[:nbytes], self.copy_blocks, cs.cuda_stream)
-                pull_copy(blk.d_offs, blk.offs_t[:n + 1], self.copy_blocks, cs.cuda_stream)
-            self.h2d_timer.stop(cs, nbytes + 8 * (n + 1))
+                for h, d, ln in segs:
+                    pull_copy(blk.d_raw[d:d + ln], blk.data[h:h + ln], self.copy_blocks,
+                              cs.cuda_stream)
+                pull_copy(blk.d_offs, offs_src[:n + 1], self.copy_blocks, cs.cuda_stream)
+            self.h2d_timer.stop(cs, sum(ln for _, _, ln in segs) + 8 * (n + 1))
             blk.parsed = None
             if self.space is not None:
                 ps = cs

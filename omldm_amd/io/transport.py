@@ -264,8 +264,10 @@ class FileBroker(Broker):
         return [x for x in lines if x.strip()], offset + used
 
     def end_offset(self, topic, partition):
-        path = os.path.join(self._dir(topic), f"{partition}.jsonl")
-        return os.path.getsize(path) if os.path.exists(path) else 0
+        try:  # one syscall: the tick's forecast catch-up asks for every partition
+            return os.stat(os.path.join(self._dir(topic), f"{partition}.jsonl")).st_size
+        except FileNotFoundError:
+            return 0
 
     def consume_block(self, topic, partition, offset, max_records):
         """Reads a chunk of the log and indexes its lines with one vectorised newline

@@ -326,6 +326,34 @@ def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
             batch.dc, int(batch.span), batch.y.data_ptr())
 
 
+_S3_WS_CACHE: dict = {}
+
+
+def _s3_workspaces(dev, B, R, S, dn, dc, span, bias, slot):
+    """The 8 workspaces of a v3 round and their pointer array, cached per geometry (the
+    lookup + ctypes array were a per-tick host cost); refreshed if a workspace moved."""
+    import ctypes
+
+    h = native.hip()
+    key = (str(dev), B, R, S, dn, dc, span, bias, slot)
+    hit = _S3_WS_CACHE.get(key)
+    bufs = []
+    for i, name in enumerate(S3_BUFS):
+        n = int(h.omldm_scan3_ws_words(i, B, R, S, dn, dc, span, int(bias))) if hit is None \
+            else hit[2][i]
+        wkey = f"s3_{name}" if i in _S3_SHARED else f"s3_{name}{slot}"
+        bufs.append(_workspace(dev, n, key=wkey))
+    if hit is not None and all(a.data_ptr() == b.data_ptr() for a, b in zip(bufs, hit[0])):
+        return hit[0], hit[1]
+    ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
+    sizes = [int(h.omldm_scan3_ws_words(i, B, R, S, dn, dc, span, int(bias)))
+             for i in range(len(S3_BUFS))]
+    if len(_S3_WS_CACHE) > 64:
+        _S3_WS_CACHE.clear()
+    _S3_WS_CACHE[key] = (bufs, ptrs, sizes)
+    return bufs, ptrs
+
+
 def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
                          rule: "LinearRule", slot: int = 0, stream=None,
                          hashed: bool = False) -> Scan3Prep:
@@ -337,14 +365,7 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
     dev = batch.y.device
     span = _s3_span(batch, dim)
     mode = _s3_mode(batch, hashed)
-    bufs = []
-    for i, name in enumerate(S3_BUFS):
-        n = int(h.omldm_scan3_ws_words(i, batch.B, R, S, batch.dn, batch.dc, span, int(bias)))
-        key = f"s3_{name}" if i in _S3_SHARED else f"s3_{name}{slot}"
-        bufs.append(_workspace(dev, n, key=key))
-    import ctypes
-
-    ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
+    bufs, ptrs = _s3_workspaces(dev, batch.B, R, S, batch.dn, batch.dc, span, bool(bias), slot)
     st = stream if stream is not None else torch.cuda.current_stream(dev)
     y = batch.y
     assert y.dtype in (torch.float32, torch.int8) and y.is_contiguous()
