@@ -144,6 +144,21 @@ def engine_forecast_latency(n: int) -> dict:
                     "resident serving wave + native Prediction formatting), trained SVM"}
 
 
+def cpu_baseline() -> dict | None:
+    """The reference-class CPU baseline measured on the MI355X host (same stream shape,
+    P = 16): bench/baselines/cpu_reference_mi355x_host_p16.json (a copy of
+    profiles/round4/'s; profiles/ does not travel to the GPU box)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench", "baselines",
+                        "cpu_reference_mi355x_host_p16.json")
+    try:
+        with open(path) as f:
+            d = json.loads(f.read().strip().splitlines()[-1])
+        return {"value": float(d["value"]), "source": os.path.relpath(path, os.path.dirname(
+            os.path.abspath(__file__)))}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def engine_e2e_rate(records: int, batch: int = 65536) -> dict:
     """Records/s of the training stream through the whole engine (rank 0, one GPU): JSON
     DataInstance records in a file topic → pinned staging → GPU parse + feature hashing →
@@ -438,13 +453,21 @@ def main(argv=None) -> int:
     value = total_examples / elapsed
     if rank == 0:
         wire = pool[0].wire_bytes
+        base = cpu_baseline() if a.learner == "SVM" else None
         out = {
             "metric": METRIC if a.learner == "SVM" else
                       "training examples/sec (whole node), online logistic regression, "
                       "1M-dim hashed features (BASELINE config 2)",
             "value": round(value, 1), "unit": "examples/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / base["value"], 2) if base else None,
+            "baseline": {"value": base["value"], "source": base["source"],
+                         "what": "reference-class CPU baseline (BASELINE.md: the reference "
+                                 "publishes no number): the reference's semantics in C++, "
+                                 "P = 16 sequential PA-I spokes + averaging (the reference's "
+                                 "default parallelism), measured on the MI355X box's host "
+                                 "CPU (bench/cpu_reference.py)"} if base else None,
             "dtype": "fp32",
             "data": "synthetic (Criteo-shaped raw stream: fp32 numerical features, 32-bit "
                     "category tokens hashed on the GPU inside the timed round, int8 ±1 labels; "

@@ -84,6 +84,9 @@ class HashedBatch:
     # rows per virtual spoke of a spoke-major batch (engine/holdout.py routes a tick into
     # one), or None; a plain attribute, not carried by slicing / selection
     shards = None
+    # a v3 scan prep made for this batch (ops.linear.Scan3Prep), shared by the pipelines
+    # that train on it within a tick; a plain attribute like ``shards``
+    prep = None
 
     @property
     def B(self) -> int:

@@ -28,6 +28,7 @@ import collections
 import json
 import os
 import time
+from contextlib import nullcontext as _nullcontext
 
 import numpy as np
 import torch
@@ -375,14 +376,25 @@ class Job:
         if direct is not None and direct.B:  # rows that bypass the holdout (no spoke layout)
             routed = HashedBatch.cat_batches([direct, routed]) if routed.B else direct
         groups: dict[int, list] = {}
-        for pid in sorted(self.pipes):
+        # several pipelines: each trains on its own stream (a linear pipeline's exact scan
+        # occupies 16 CUs, so M of them run side by side), joined before the collectives
+        streams = self._pipe_streams() if len(self.pipes) > 1 else None
+        main = torch.cuda.current_stream(self.device) if streams else None
+        for i, pid in enumerate(sorted(self.pipes)):
             pipe = self.pipes[pid]
-            with tracing.range(f"round:{pid}"):
+            st = streams[i % len(streams)] if streams else None
+            if st is not None:
+                st.wait_stream(main)
+            with tracing.range(f"round:{pid}"), (torch.cuda.stream(st) if st is not None
+                                                 else _nullcontext()):
                 if self.world > 1 and isinstance(pipe.protocol, Synchronous):
                     groups.setdefault(pipe.protocol.hubs, []).append(
                         (pipe, pipe.train_local(routed)))
                 else:
                     pipe.train(routed)
+        if streams:
+            for st in streams:
+                main.wait_stream(st)
         for hubs, items in groups.items():
             with tracing.range("sync:coalesced"):
                 if self._coll_timer is not None:
@@ -394,6 +406,14 @@ class Job:
                                                      for _, b in items))
             for pipe, _ in items:
                 pipe.protocol.finish()
+
+    def _pipe_streams(self):
+        n = int(self.cfg.pipelineStreams)
+        if self.device.type != "cuda" or n <= 1:
+            return None
+        if getattr(self, "_streams", None) is None:
+            self._streams = [torch.cuda.Stream(self.device) for _ in range(n)]
+        return self._streams[:n]
 
     # ------------------------------------------------------------------- queries
     def _answer(self, req: Request, response_id=None, write=True) -> dict:

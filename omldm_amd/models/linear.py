@@ -127,8 +127,13 @@ class LinearLearner(Learner):
         num, y = batch.num.float().contiguous(), batch.y.float().contiguous()
         R, S = self._seq_geometry(batch.B, ctx)
         rb = RawBatch(num, batch.cat.contiguous(), y, span=batch.cat_span, cbase=self.space.dn)
+        # a v3 prep made ahead for this batch (shared by every pipeline of the tick that
+        # trains on it; ops.linear checks that it matches)
+        rb.prep = getattr(batch, "prep", None)
         if L.scan3_eligible_compact(rb, R, self.rule.bias, self.dim):  # compact slots as they are
-            return self._fit_raw(rb, ctx, hashed=True)
+            self._fit_raw(rb, ctx, hashed=True)
+            batch.prep = rb.prep
+            return
         rb = RawBatch(num, batch.to_wide().cat.contiguous(), y)
         rb.prep = L.linear_scan_prepare_slots(rb, R, S, self.dim, bool(self.rule.bias))
         self._fit_raw(rb, ctx)

@@ -322,8 +322,11 @@ def _s3_mode(batch: RawBatch, hashed: bool) -> int:
 
 
 def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
-    return (batch.B, R, S, dim, bool(bias), rule.rule, rule.variant, float(rule.C), batch.dn,
-            batch.dc, int(batch.span), batch.y.data_ptr())
+    """What a v3 prep depends on: the batch, the geometry, the rule's row scale (C only
+    through PA-II's 1/(2C)) — pipelines that differ in C share one prep."""
+    c = float(rule.C) if rule.variant == PA2 else None
+    return (batch.B, R, S, dim, bool(bias), rule.rule == RULE_LOGISTIC, rule.variant == PA2, c,
+            batch.dn, batch.dc, int(batch.span), batch.y.data_ptr(), batch.tok.data_ptr())
 
 
 _S3_WS_CACHE: dict = {}
@@ -354,6 +357,41 @@ def _s3_workspaces(dev, B, R, S, dn, dc, span, bias, slot):
     return bufs, ptrs
 
 
+_S3_RUN_CACHE: dict = {}
+_S3_SLOTS = {"next": 0}
+S3_SLOT_RING = 16
+
+
+def _s3_slot_for(key) -> str:
+    """Workspace set of an inline prep: a ring of 16, one per distinct prep key in turn.
+    Pipelines of one tick may scan on different streams, so two preps alive in the same
+    tick must not share buffers (ticks are joined, so the ring only has to outlast the
+    distinct keys of one tick)."""
+    i = _S3_SLOTS["next"]
+    _S3_SLOTS["next"] = (i + 1) % S3_SLOT_RING
+    return f"k{i}"
+
+
+def _s3_run_ptrs(sp: "Scan3Prep", dev, stream: int):
+    """The prep's 4 model-independent workspaces + this stream's 4 run-time ones."""
+    import ctypes
+
+    key = (id(sp), stream)
+    hit = _S3_RUN_CACHE.get(key)
+    if hit is not None and hit[0] is sp:
+        return hit[1]
+    run = []
+    for i in _S3_SHARED:
+        n = sp.bufs[i].numel()
+        run.append(_workspace(dev, n, key=f"s3_{S3_BUFS[i]}@{stream}"))
+    ptrs = (ctypes.c_void_p * len(S3_BUFS))(*([b.data_ptr() for b in sp.bufs[:4]] +
+                                              [b.data_ptr() for b in run]))
+    if len(_S3_RUN_CACHE) > 256:
+        _S3_RUN_CACHE.clear()
+    _S3_RUN_CACHE[key] = (sp, ptrs, run)
+    return ptrs
+
+
 def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
                          rule: "LinearRule", slot: int = 0, stream=None,
                          hashed: bool = False) -> Scan3Prep:
@@ -374,10 +412,8 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
                                 rule.rule, rule.variant, float(rule.C), span,
                                 int(batch.cbase) if batch.span > 0 else -1, ptrs,
                                 st.cuda_stream), "omldm_scan3_prepare")
-    ev = None
-    if stream is not None:
-        ev = torch.cuda.Event()
-        ev.record(stream)
+    ev = torch.cuda.Event()  # pipelines on other streams that reuse the prep wait on it
+    ev.record(st)
     return Scan3Prep(bufs, ptrs, _s3_key(batch, R, S, dim, bias, rule), ev)
 
 
@@ -408,7 +444,9 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
     sp = batch.prep
     key = _s3_key(batch, R, S, dim, rule.bias, rule)
     if not (isinstance(sp, Scan3Prep) and sp.key == key):
-        sp = linear_scan3_prepare(batch, R, S, dim, bool(rule.bias), rule, hashed=hashed)
+        sp = linear_scan3_prepare(batch, R, S, dim, bool(rule.bias), rule, hashed=hashed,
+                                  slot=_s3_slot_for(key))
+        batch.prep = sp  # the next pipeline of the tick reuses it (same key)
     elif sp.event is not None:
         torch.cuda.current_stream(w.device).wait_event(sp.event)
     global SCAN3_ROUNDS
@@ -416,10 +454,13 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
     h = native.hip()
     parts = max(1, int(parts))
     span = _s3_span(batch, dim)
+    # run-time buffers (c per row, spoke statistics, the table spill) per stream: pipelines
+    # on different streams may scan the same prep concurrently
+    ptrs = _s3_run_ptrs(sp, w.device, native.stream_of(w))
     for k in range(parts):
         rc = h.omldm_scan3_run(ptr(w), num.shape[1], batch.dc, ptr(y), int(y.dtype == torch.int8),
                                batch.B, R, S, ptr(dacc), dim, ptr(cum), rule.rule, rule.variant,
-                               rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), span, sp.ptrs, k,
+                               rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), span, ptrs, k,
                                parts, native.stream_of(w))
         check(rc, "omldm_scan3_run")
         if on_part is not None:

@@ -78,6 +78,7 @@ class JobConfig:
     ingestCUs: int = 0                    # GPU: CUs (one XCD block) for ingest copies; 0 off (e2e A/B: no gain, host-bound)
     ingestCopy: str = "pull"              # GPU staging copy: pull (kernel) | sdma (hipMemcpyAsync)
     forecastServer: str = "auto"          # per-record forecasts on the resident serving wave (auto: GPU)
+    pipelineStreams: int = 8              # GPU: pipelines of a tick train on up to this many streams
     extra: dict = field(default_factory=dict)
 
     @staticmethod
