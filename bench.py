@@ -159,7 +159,7 @@ def cpu_baseline() -> dict | None:
         return None
 
 
-def engine_e2e_rate(records: int, batch: int = 65536) -> dict:
+def engine_e2e_rate(records: int, batch: int = 65536, fmt: str = "json") -> dict:
     """Records/s of the training stream through the whole engine (rank 0, one GPU): JSON
     DataInstance records in a file topic → pinned staging → GPU parse + feature hashing →
     holdout routing → Synchronous round of a linear SVM (fp32, the job's default spokes)
@@ -180,9 +180,15 @@ def engine_e2e_rate(records: int, batch: int = 65536) -> dict:
         br.create_topic("trainingData", parts)
         br.create_topic("forecastingData", 8)
         uniq = synth_json_records(20000, sp, start=0, seed=3)
+        if fmt == "dib":  # the same records as binary DIB records (omldm_amd/io/dib.py)
+            from omldm_amd.io.dib import records_to_dib
+
+            uniq = records_to_dib(uniq, sp.n_numerical, sp.n_discrete, sp.dc)
+        else:
+            uniq = [r.encode() for r in uniq]
         for p in range(parts):
             recs = [uniq[i % len(uniq)] for i in range(p, records, parts)]
-            br.produce_block("trainingData", p, ("\n".join(recs) + "\n").encode())
+            br.produce_block("trainingData", p, b"\n".join(recs) + b"\n")
         br.produce("requests", json.dumps({"id": 1, "request": "Create",
                                            "learner": {"name": "SVM"},
                                            "trainingConfiguration": {"protocol": "Synchronous"}}))
@@ -212,7 +218,8 @@ def engine_e2e_rate(records: int, batch: int = 65536) -> dict:
         job.ingest.close()
         job.egress.close()
     return {"records_per_s": round(n / max(wall, 1e-9), 1), "records": n,
-            "spokes": job.spokes, "batch": batch}
+            "spokes": job.spokes, "batch": batch,
+            "record_bytes": round(sum(len(r) + 1 for r in uniq) / len(uniq), 1)}
 
 
 def main(argv=None) -> int:
@@ -234,6 +241,8 @@ def main(argv=None) -> int:
     ap.add_argument("--cu-layout", type=int, default=1)
     ap.add_argument("--pull-blocks", type=int, default=16)
     ap.add_argument("--lane", default="split", choices=["split", "plain"])
+    ap.add_argument("--scan-cus", type=int, default=16,
+                    help="CUs the prep stream leaves to the round's scan (split lane)")
     ap.add_argument("--prep-ahead", type=int, default=1,
                     help="v2 round: hash + chunk Grams of batch k+1 on their own stream")
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
@@ -297,10 +306,16 @@ def main(argv=None) -> int:
     v3 = on_gpu and L.scan3_eligible(dev[0].batch, R, learner.rule.bias)
     if on_gpu and a.prep_ahead and (v3 or L.scan_eligible(dev[0].batch)):
         if a.lane == "split" and a.ingest_cus > 0:
-            rawp = native.hip().omldm_stream_create_cumask_ex(a.ingest_cus, 1, a.cu_layout)
-            assert rawp, "hipExtStreamCreateWithCUMask failed"
+            # the prep kernels fill every CU they may use; a few CUs (spread over the
+            # XCDs) kept for the compute stream let the next scan start on time instead
+            # of waiting for prep workgroups to drain from a CU (each scan workgroup
+            # takes a whole CU's LDS)
+            from omldm_amd.ops.ingest import copy_cu_bits, cumask_stream, reserve_cu_bits
+            total = torch.cuda.get_device_properties(device).multi_processor_count
+            taken = copy_cu_bits(total, a.ingest_cus, a.cu_layout)
+            keep = reserve_cu_bits(total, a.scan_cus, taken)
+            prep_stream, rawp = cumask_stream(set(range(total)) - taken - keep, total, device)
             raw_streams.append(rawp)
-            prep_stream = torch.cuda.ExternalStream(rawp, device=device)
         else:
             prep_stream = torch.cuda.Stream(device)
     copied = [torch.cuda.Event() for _ in range(nslots)] if on_gpu else None
@@ -448,6 +463,7 @@ def main(argv=None) -> int:
     eng = engine_forecast_latency(a.engine_latency) if (rank == 0 and on_gpu and
                                                          a.engine_latency > 0) else None
     e2e = engine_e2e_rate(a.engine_e2e) if (rank == 0 and on_gpu and a.engine_e2e > 0) else None
+    e2e_dib = engine_e2e_rate(2 * a.engine_e2e, fmt="dib") if e2e is not None else None
 
     total_examples = a.steps * B * world
     value = total_examples / elapsed
@@ -490,7 +506,11 @@ def main(argv=None) -> int:
             "engine_e2e_semantics": None if e2e is None else
             f"JSON DataInstance file topic -> GPU parse + hashing -> holdout -> Synchronous "
             f"linear SVM fp32, {e2e['spokes']} spokes, {e2e['records']} records timed "
-            "(one GPU, rank 0)",
+            f"(one GPU, rank 0), {e2e['record_bytes']} B/record",
+            "engine_e2e_dib_records_per_s": None if e2e_dib is None else e2e_dib["records_per_s"],
+            "engine_e2e_dib_semantics": None if e2e_dib is None else
+            f"the same records as binary DIB records ({e2e_dib['record_bytes']} B/record, "
+            f"omldm_amd/io/dib.py) through the same engine path, {e2e_dib['records']} timed",
             "per_gpu_examples_per_s": round(value / world, 1),
             "holdout_accuracy": None if acc is None else round(acc, 4),
             "ref_holdout_accuracy": None if ref_acc is None else round(ref_acc, 4),

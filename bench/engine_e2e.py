@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""End-to-end engine throughput: JSON DataInstance records in a topic → parse + hash (C++)
+"""End-to-end engine throughput: DataInstance records (JSON, or --format dib: the binary
+DIB record, omldm_amd/io/dib.py) in a topic → parse + hash
 → HBM → holdout routing → protocol round → statistics, through the real Job loop
 (the path a reference user exercises; the headline bench replays pre-hashed batches).
 
@@ -48,6 +49,9 @@ def main(argv=None) -> int:
     ap.add_argument("--forecast-server", default="auto", help="engine forecastServer flag")
     ap.add_argument("--unique", type=int, default=100_000,
                     help="distinct JSON records generated; the topic replays them")
+    ap.add_argument("--format", default="json", choices=["json", "dib"],
+                    help="topic records: DataInstance JSON (≈ 507 B) or the binary DIB "
+                         "record of the same objects (≈ 162 B, omldm_amd/io/dib.py)")
     a = ap.parse_args(argv)
     comm, device = init_distributed()
     sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
@@ -59,6 +63,15 @@ def main(argv=None) -> int:
         n_fc = int(a.records * a.forecast_frac)
         fc = synth_json_records(min(a.unique, max(n_fc, 1)), sp, start=10**7, seed=3,
                                 operation="forecasting") if n_fc else []
+        if a.format == "dib":
+            from omldm_amd.io.dib import records_to_dib
+
+            uniq = records_to_dib(uniq, sp.n_numerical, sp.n_discrete, sp.dc)
+            fc = records_to_dib(fc, sp.n_numerical, sp.n_discrete, sp.dc) if fc else []
+        else:
+            uniq = [r.encode() for r in uniq]
+            fc = [r.encode() for r in fc]
+        rec_bytes = sum(len(r) + 1 for r in uniq) / max(1, len(uniq))
         br.create_topic("forecastingData", min(8, a.partitions))  # a small topic
         for topic, n, src in (("trainingData", a.records - n_fc, uniq),
                               ("forecastingData", n_fc, fc)):
@@ -68,7 +81,7 @@ def main(argv=None) -> int:
                 per_part[i % np_].append(src[i % len(src)])
             for p, recs in enumerate(per_part):
                 if recs:
-                    br.produce_block(topic, p, ("\n".join(recs) + "\n").encode())
+                    br.produce_block(topic, p, b"\n".join(recs) + b"\n")
         del per_part
         gen_s = time.time() - t
         for i in range(a.pipelines):
@@ -120,7 +133,9 @@ def main(argv=None) -> int:
         job.run()  # idle timeout → final statistics
         if comm.rank == 0:
             print(json.dumps({
-                "metric": "end-to-end engine records/s (JSON topics → training + predictions)",
+                "metric": "end-to-end engine records/s (%s topics → training + predictions)"
+                          % ("JSON" if a.format == "json" else "DIB binary"),
+                "format": a.format, "record_bytes": round(rec_bytes, 1),
                 "value": round((job.counters["records"] - r0) * comm.world / max(wall, 1e-9), 1),
                 "unit": "records/s", "n_gpus": comm.world, "records": job.counters["records"],
                 "pipelines": a.pipelines, "batch": a.batch, "wall_s": round(wall, 3),

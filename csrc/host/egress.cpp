@@ -12,6 +12,8 @@
 #include <cstdint>
 #include <cstring>
 
+#include "dib.h"
+
 #define OMLDM_HOST_API extern "C" __attribute__((visibility("default")))
 
 namespace {
@@ -36,6 +38,55 @@ int format_number(double v, char* p) {
   return n;
 }
 
+// A DIB record's echo as DataInstance JSON: its features (the categorical ones as the
+// 32-bit hashes the record carries, "#%08x"), target and operation. Returns bytes written.
+int render_dib(const uint8_t* a, const uint8_t* b, char* out) {
+  omldm_dib::Reader r{a + 1, b};
+  const uint8_t op = r.get(), flags = r.get(), nn = r.get(), nd = r.get(), nc = r.get();
+  const float y = (flags & 1) ? r.getf() : 0.f;
+  int pos = 0;
+  auto put = [&](const char* t) {
+    const size_t n = std::strlen(t);
+    std::memcpy(out + pos, t, n);
+    pos += int(n);
+  };
+  for (int arr = 0; arr < 2; ++arr) {
+    put(arr == 0 ? "{\"numericalFeatures\": [" : "], \"discreteFeatures\": [");
+    const int cnt = arr == 0 ? nn : nd;
+    for (int j = 0; j < cnt; ++j) {
+      if (j) put(", ");
+      pos += format_number(double(r.getf()), out + pos);
+    }
+  }
+  put("], \"categoricalFeatures\": [");
+  static const char hx[] = "0123456789abcdef";
+  for (int j = 0; j < nc; ++j) {
+    const uint32_t h = r.get32();
+    put(j ? ", \"#" : "\"#");
+    for (int k = 7; k >= 0; --k) out[pos++] = hx[(h >> (4 * k)) & 15];
+    out[pos++] = '"';
+  }
+  put("]");
+  if (flags & 1) {
+    put(", \"target\": ");
+    pos += format_number(double(y), out + pos);
+  }
+  put(op == 0 ? ", \"operation\": \"training\"}" : ", \"operation\": \"forecasting\"}");
+  return pos;
+}
+
+// JSON: surrounding whitespace; DIB: only the log's '\n' (payload bytes may be 0x20 …)
+inline void trim(const uint8_t* buf, int64_t& a, int64_t& b) {
+  while (a < b && is_ws(buf[a])) ++a;
+  if (a < b && buf[a] == omldm_dib::kMagic) {
+    if (buf[b - 1] == '\n') --b;
+    return;
+  }
+  while (b > a && is_ws(buf[b - 1])) --b;
+}
+
+inline int64_t dib_bound(int64_t bytes) { return bytes * 10 + 160; }
+
 }  // namespace
 
 // Renders record i as {"mlpId": id, "dataPoint": <buf[starts[i], ends[i]) trimmed>,
@@ -54,25 +105,25 @@ OMLDM_HOST_API int64_t omldm_format_predictions(const uint8_t* buf, const int64_
   int64_t need = 0;
   for (int64_t i = 0; i < n; ++i) {
     int64_t a = starts[i], b = ends[i];
-    while (a < b && is_ws(buf[a])) ++a;
-    while (b > a && is_ws(buf[b - 1])) --b;
-    need += (sizeof(k0) - 1) + idn + (sizeof(k1) - 1) + (b - a > 0 ? b - a : 4) +
-            (sizeof(k2) - 1) + 40 + 2;
+    trim(buf, a, b);
+    const int64_t body = b - a > 0 ? (buf[a] == omldm_dib::kMagic ? dib_bound(b - a) : b - a) : 4;
+    need += (sizeof(k0) - 1) + idn + (sizeof(k1) - 1) + body + (sizeof(k2) - 1) + 40 + 2;
   }
   if (need > cap) return -need;
   int64_t pos = 0;
   out_offs[0] = 0;
   for (int64_t i = 0; i < n; ++i) {
     int64_t a = starts[i], b = ends[i];
-    while (a < b && is_ws(buf[a])) ++a;
-    while (b > a && is_ws(buf[b - 1])) --b;
+    trim(buf, a, b);
     std::memcpy(out + pos, k0, sizeof(k0) - 1);
     pos += sizeof(k0) - 1;
     std::memcpy(out + pos, idbuf, idn);
     pos += idn;
     std::memcpy(out + pos, k1, sizeof(k1) - 1);
     pos += sizeof(k1) - 1;
-    if (b > a) {
+    if (b > a && buf[a] == omldm_dib::kMagic) {
+      pos += render_dib(buf + a, buf + b, reinterpret_cast<char*>(out + pos));
+    } else if (b > a) {
       std::memcpy(out + pos, buf + a, size_t(b - a));
       pos += b - a;
     } else {

@@ -21,6 +21,7 @@
 #include <thread>
 #include <vector>
 
+#include "dib.h"
 #include "hashing.h"
 
 #define OMLDM_HOST_API extern "C" __attribute__((visibility("default")))
@@ -206,13 +207,53 @@ inline bool key_is(const char* s, size_t n, const char* k) {
   return std::strlen(k) == n && std::memcmp(s, k, n) == 0;
 }
 
+// ---------------------------------------------------------------- DIB (binary records)
+// Format: csrc/host/dib.h.
+int parse_dib(const uint8_t* b, const uint8_t* e, int dnum, int ddisc, int dc, int64_t dim,
+              float* num, int32_t* cat, uint16_t* cat16, int cspan, float* y) {
+  omldm_dib::Reader r{b + 1, e};
+  const int dn = dnum + ddisc;
+  const uint8_t op = r.get(), flags = r.get(), nn = r.get(), nd = r.get(), nc = r.get();
+  if (flags & 1) *y = r.getf();
+  for (int j = 0; j < nn; ++j) {
+    const float v = r.getf();
+    if (j < dnum) num[j] = v;
+  }
+  for (int j = 0; j < nd; ++j) {
+    const float v = r.getf();
+    if (j < ddisc) num[dnum + j] = v;
+  }
+  for (int j = 0; j < nc; ++j) {
+    const uint32_t h = r.get32();
+    if (j >= dc) continue;
+    if (cat16) {
+      cat16[j] = uint16_t(((h >> 31) << 15) | ((h & 0x7fffffffu) % uint32_t(cspan)));
+    } else {
+      const int32_t slot = int32_t(dn + int64_t(h & 0x7fffffffu) % (dim - dn - 1));
+      cat[j] = (h & 0x80000000u) ? int32_t(uint32_t(slot) | 0x80000000u) : slot;
+    }
+  }
+  if (!r.ok || op > 1 || !(flags & 2)) return -1;
+  if (op == 0 && std::isnan(*y)) return -1;
+  return op;
+}
+
+// Raw capture of a JSON record for the DIB encoder: the category hashes before they are
+// reduced to slots, their count, and whether any feature array was present.
+struct RawCapture {
+  uint32_t* h;
+  int nc = 0;
+  bool any = false;
+};
+
 // Parses one record. Returns op code (0/1) or -1.
 int parse_one(const char* b, const char* e, int dnum, int ddisc, int dc, int64_t dim, float* num,
-              void* catv, int cspan, float* y) {
+              void* catv, int cspan, float* y, RawCapture* raw = nullptr) {
   int32_t* cat = static_cast<int32_t*>(catv);
   uint16_t* cat16 = static_cast<uint16_t*>(catv);
   if (cspan > 0) {
-    for (int j = 0; j < dc; ++j) cat16[j] = 0xFFFF;
+    if (cat16)
+      for (int j = 0; j < dc; ++j) cat16[j] = 0xFFFF;
     cat = nullptr;
   }
   const int dn = dnum + ddisc;
@@ -220,6 +261,9 @@ int parse_one(const char* b, const char* e, int dnum, int ddisc, int dc, int64_t
   if (cat)
     for (int j = 0; j < dc; ++j) cat[j] = -1;
   *y = std::nanf("");
+  if (b < e && uint8_t(*b) == omldm_dib::kMagic && !raw)
+    return parse_dib(reinterpret_cast<const uint8_t*>(b), reinterpret_cast<const uint8_t*>(e),
+                     dnum, ddisc, dc, dim, num, cat, cat ? nullptr : cat16, cspan, y);
   Cursor c{b, e};
   c.ws();
   if (size_t(c.e - c.p) >= 3 && std::memcmp(c.p, "EOS", 3) == 0) return -1;
@@ -264,8 +308,14 @@ int parse_one(const char* b, const char* e, int dnum, int ddisc, int dc, int64_t
             if (!c.str(s, n)) return -1;
             if (j < dc) {
               const uint8_t* us = reinterpret_cast<const uint8_t*>(s);
-              if (cat) cat[j] = hash_cat(us, n, j, dn, dim);
-              else cat16[j] = hash_cat16(us, n, j, cspan);
+              if (raw) {
+                raw->h[j] = murmur3_32(us, n, kSeedBase + uint32_t(j));
+                raw->nc = j + 1;
+              } else if (cat) {
+                cat[j] = hash_cat(us, n, j, dn, dim);
+              } else {
+                cat16[j] = hash_cat16(us, n, j, cspan);
+              }
             }
             ++j;
             if (c.eat(',')) continue;
@@ -295,9 +345,30 @@ int parse_one(const char* b, const char* e, int dnum, int ddisc, int dc, int64_t
     if (c.eat('}')) break;
     return -1;
   }
+  if (raw) raw->any = any_features;
   if (!c.ok || !any_features) return -1;
   if (op == 0 && std::isnan(*y)) return -1;  // a training point needs a target
   return op;
+}
+
+inline void dib_put(std::vector<uint8_t>& o, uint8_t c) {
+  if (c == 0x0A) {
+    o.push_back(0xDB);
+    o.push_back(0xDC);
+  } else if (c == 0xDB) {
+    o.push_back(0xDB);
+    o.push_back(0xDD);
+  } else {
+    o.push_back(c);
+  }
+}
+inline void dib_put32(std::vector<uint8_t>& o, uint32_t v) {
+  for (int k = 0; k < 4; ++k) dib_put(o, uint8_t(v >> (8 * k)));
+}
+inline void dib_putf(std::vector<uint8_t>& o, float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  dib_put32(o, u);
 }
 
 template <typename F>
@@ -351,6 +422,66 @@ OMLDM_HOST_API int64_t omldm_parse_instances(const char* buf, const int64_t* off
     valid += v;
   });
   return valid.load();
+}
+
+// JSON DataInstance records buf[off[i], off[i+1]) → DIB records (each ending in '\n')
+// written back to back into out (cap bytes); out_offs[i] = start of record i,
+// out_offs[n] = bytes written. A record the JSON parser rejects becomes an invalid DIB
+// record (op 0xFF), so both topics count the same invalid records. Returns the bytes
+// written, or -1 if cap is too small.
+OMLDM_HOST_API int64_t omldm_json_to_dib(const char* buf, const int64_t* off, int n, int dnum,
+                                         int ddisc, int dc, uint8_t* out, int64_t cap,
+                                         int64_t* out_offs, int nthreads) {
+  if (n <= 0) {
+    out_offs[0] = 0;
+    return 0;
+  }
+  const int nt = std::max(1, std::min(nthreads, (n + 255) / 256));
+  std::vector<std::vector<uint8_t>> part(nt);
+  std::vector<std::vector<int64_t>> lens(nt);
+  const int chunk = (n + nt - 1) / nt;
+  auto work = [&](int t) {
+    const int a = t * chunk, b = std::min(n, a + chunk);
+    std::vector<float> num(size_t(dnum + ddisc) + 1);
+    std::vector<uint32_t> h(size_t(dc) + 1);
+    auto& o = part[t];
+    o.reserve(size_t(b - a) * size_t(16 + 4 * (dnum + ddisc + dc)));
+    for (int i = a; i < b; ++i) {
+      const size_t start = o.size();
+      RawCapture rc{h.data()};
+      float y;
+      const int op = parse_one(buf + off[i], buf + off[i + 1], dnum, ddisc, dc, int64_t(1) << 30,
+                               num.data(), nullptr, 1, &y, &rc);
+      o.push_back(omldm_dib::kMagic);
+      const bool has_y = !std::isnan(y);
+      dib_put(o, op < 0 ? uint8_t(0xFF) : uint8_t(op));
+      dib_put(o, uint8_t((has_y ? 1 : 0) | (rc.any ? 2 : 0)));
+      dib_put(o, uint8_t(dnum));
+      dib_put(o, uint8_t(ddisc));
+      dib_put(o, uint8_t(rc.nc));
+      if (has_y) dib_putf(o, y);
+      for (int j = 0; j < dnum + ddisc; ++j) dib_putf(o, num[j]);
+      for (int j = 0; j < rc.nc; ++j) dib_put32(o, h[j]);
+      o.push_back('\n');
+      lens[t].push_back(int64_t(o.size() - start));
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  int64_t pos = 0;
+  int i = 0;
+  for (int t = 0; t < nt; ++t) {
+    if (pos + int64_t(part[t].size()) > cap) return -1;
+    std::memcpy(out + pos, part[t].data(), part[t].size());
+    for (int64_t L : lens[t]) {
+      out_offs[i++] = pos;
+      pos += L;
+    }
+  }
+  out_offs[n] = pos;
+  return pos;
 }
 
 // Deterministic synthetic stream (Criteo-like shape): dn Gaussian numerical features,

@@ -92,6 +92,29 @@ OMLDM_API void* omldm_stream_create_cumask_ex(int ncu, int invert, int layout) {
   return (void*)s;
 }
 
+// A stream restricted to the CUs whose bits are set in mask[0..words) (bit c = the c-th
+// CU in the runtime's CU-mask order).
+OMLDM_API void* omldm_stream_create_cumask_words(const uint32_t* mask, int words) {
+  hipStream_t s = nullptr;
+  if (words <= 0 || hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess)
+    return nullptr;
+  return (void*)s;
+}
+
+// Where a workgroup launched on `stream` runs: out[0] = XCC id, out[1] = HW_ID (CU, SH,
+// SE fields) — maps CU-mask bits to XCDs (scripts/cumask_probe.py).
+__global__ void cu_probe_kernel(int* out) {
+  if (threadIdx.x == 0) {
+    out[0] = (int)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID
+    out[1] = (int)__builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID
+  }
+}
+
+OMLDM_API int omldm_cu_probe(int* out, void* stream) {
+  hipLaunchKernelGGL(cu_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+  return (int)hipGetLastError();
+}
+
 OMLDM_API void* omldm_stream_create_cumask(int ncu) { return omldm_stream_create_cumask_ex(ncu, 0, 0); }
 
 OMLDM_API int omldm_stream_destroy(void* s) { return (int)hipStreamDestroy((hipStream_t)s); }

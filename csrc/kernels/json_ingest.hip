@@ -1,4 +1,5 @@
-// GPU DataInstance JSON parser + feature hashing ("device feature_hash").
+// GPU DataInstance JSON parser + feature hashing ("device feature_hash"),
+// and the decoder of the binary DIB records that may share a topic with JSON (dib.h).
 //
 // Reference: Jackson parses every record on a JVM thread (DataInstanceParser /
 // DataPointParser, omldm/utils/parsers/DataInstanceParser.scala:12-22,
@@ -199,6 +200,63 @@ __device__ uint32_t murmur3_dev(const unsigned char* d, int len, uint32_t seed) 
   return h1;
 }
 
+// A DIB record (binary DataInstance, csrc/host/dib.h): 0xB1, then the SLIP-stuffed
+// payload op | flags | nn | nd | nc | [f32 target] | f32 num[nn] | f32 disc[nd] |
+// u32 murmur3 hash[nc]. Same outputs and validity rules as the host's parse_dib.
+struct DibRd {
+  const unsigned char* p;
+  const unsigned char* e;
+  bool ok;
+  __device__ __forceinline__ uint32_t get() {
+    if (p >= e) return ok = false, 0u;
+    uint32_t c = *p++;
+    if (c == 0xDBu) {
+      if (p >= e) return ok = false, 0u;
+      const uint32_t d = *p++;
+      c = d == 0xDCu ? 0x0Au : (d == 0xDDu ? 0xDBu : (ok = false, 0u));
+    }
+    return c;
+  }
+  __device__ __forceinline__ uint32_t get32() {
+    uint32_t v = get();
+    v |= get() << 8;
+    v |= get() << 16;
+    v |= get() << 24;
+    return v;
+  }
+};
+
+__device__ __forceinline__ int parse_dib_record(const unsigned char* b, const unsigned char* e,
+                                                int dnum, int ddisc, int dc, long long dim,
+                                                int cspan, float* num, int* cat32,
+                                                unsigned short* cat16, float* y) {
+  const int dn = dnum + ddisc;
+  DibRd r{b + 1, e, true};
+  const uint32_t op = r.get(), flags = r.get(), nn = r.get(), nd = r.get(), nc = r.get();
+  if (flags & 1u) *y = __uint_as_float(r.get32());
+  for (uint32_t j = 0; j < nn; ++j) {
+    const float v = __uint_as_float(r.get32());
+    if ((int)j < dnum) num[j] = v;
+  }
+  for (uint32_t j = 0; j < nd; ++j) {
+    const float v = __uint_as_float(r.get32());
+    if ((int)j < ddisc) num[dnum + j] = v;
+  }
+  for (uint32_t j = 0; j < nc; ++j) {
+    const uint32_t h = r.get32();
+    if ((int)j >= dc) continue;
+    if (cspan > 0) {
+      cat16[j] = (unsigned short)(((h >> 31) << 15) | ((h & 0x7fffffffu) % (uint32_t)cspan));
+    } else {
+      const int slot = (int)(dn + (long long)(h & 0x7fffffffu) % (dim - dn - 1));
+      cat32[j] = (h & 0x80000000u) ? (int)((uint32_t)slot | 0x80000000u) : slot;
+    }
+  }
+  if (!r.ok || op > 1u || !(flags & 2u)) return -1;
+  if (op == 0u && __builtin_isnan(*y)) return -1;
+  return (int)op;
+}
+
 // One record → outputs; returns op (0 training, 1 forecasting) or -1.
 __device__ __forceinline__ int parse_record(const unsigned char* b, const unsigned char* e, int dnum, int ddisc,
                             int dc, long long dim, int cspan, float* num, int* cat32,
@@ -210,6 +268,8 @@ __device__ __forceinline__ int parse_record(const unsigned char* b, const unsign
     else cat32[j] = -1;
   }
   *y = __builtin_nanf("");
+  if (b < e && *b == 0xB1u)
+    return parse_dib_record(b, e, dnum, ddisc, dc, dim, cspan, num, cat32, cat16, y);
   JCur c{b, e, true};
   jws(c);
   if (c.e - c.p >= 3 && c.p[0] == 'E' && c.p[1] == 'O' && c.p[2] == 'S') return -1;

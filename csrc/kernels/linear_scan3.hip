@@ -38,7 +38,7 @@
 //                        dense columns transposed for the helpers
 //   4. s3_scan_kernel    one workgroup per spoke: scanner wave + 7 helper waves
 //   5. s3_scatter_kernel the whole GPU: dacc[slot] += inv_p·c·sign per occurrence (fp32
-//                        atomics), s3_dense_kernel: dense columns, scalars, statistics
+//                        atomics) + one block for the dense columns, scalars, statistics
 #include "common.h"
 #include "hash_dev.h"
 #include "seq_common.h"
@@ -340,6 +340,133 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
   }
 }
 
+// Pass 3 on the matrix cores (the default; s3_gram_kernel above is the VALU reference the
+// GPU test compares it with). grid (chunks, S_act), 256 threads = 4 waves. Every load of the
+// chunk pair (slots of chunks c and c − 1, their numerical rows) is issued before the first
+// LDS write — the VALU kernel's strided load loops waited on global memory once per
+// iteration. Each wave then owns two 32 × 32 tiles of the output in the MFMA C layout
+// (lane: column J0 + l31; register reg: row I0 + (reg & 3) + 8·(reg >> 2) + 4·(l >> 5)):
+// the categorical ±1 match counts of its 16 (row, column) pairs go into the accumulator
+// (exact small integers), then v_mfma_f32_32x32x2_f32 adds the dense Gram x_i·x_j over
+// the KN columns. Tiles: aX1 (d = 1) tile (w >> 1, w & 1); aG (d = 0) tiles (0,0), (1,0),
+// (1,1) on waves 0-2 (wave 3's upper-right aG tile is all zero).
+template <int KN>
+__global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict__ slotsT, int dc,
+                                                           const float* __restrict__ num, int dn,
+                                                           const void* __restrict__ yv, int y8,
+                                                           int B, int R, int bias, int affine,
+                                                           float kadd, float* __restrict__ prep,
+                                                           int nchs) {
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  const int c = blockIdx.x, s = blockIdx.y;
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  if (t0 + c * s3::CH >= t1) return;
+  constexpr int PF = s3_prep_floats<KN>();
+  float* out = prep + ((size_t)s * nchs + c) * PF;
+  __shared__ alignas(16) int sl[2][s3::MAXF][s3::CH + 4];
+  __shared__ float xn[2][s3::CH][KN + 1];
+  __shared__ float sa[s3::CH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // ---- all loads in flight at once (clamped addresses, results selected after)
+  constexpr int NSL = 2 * s3::MAXF * s3::CH / 256, NXN = 2 * s3::CH * KN / 256;
+  int sv[NSL];
+  float xv[NXN];
+#pragma unroll
+  for (int u = 0; u < NSL; ++u) {
+    const int i = tid + 256 * u;  // [d][f][r], r fastest: coalesced per field
+    const int d = i / (s3::MAXF * s3::CH), rem = i - d * s3::MAXF * s3::CH;
+    const int f = rem / s3::CH, r = rem - f * s3::CH;
+    const int cc = c - d, row = t0 + cc * s3::CH + r;
+    const bool ok = f < dc && cc >= 0 && row < t1;
+    const int v = slotsT[ok ? (size_t)f * B + row : 0];
+    sv[u] = ok ? v : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < NXN; ++u) {
+    const int i = tid + 256 * u;  // [d][r][j]
+    const int d = i / (s3::CH * KN), rem = i - d * s3::CH * KN;
+    const int r = rem / KN, j = rem - r * KN;
+    const int cc = c - d, row = t0 + cc * s3::CH + r;
+    const bool in = cc >= 0 && row < t1;
+    const float x = dn > 0 ? num[(in && j < dn) ? (size_t)row * dn + j : 0] : 0.f;
+    xv[u] = in ? (j < dn ? x : ((bias && j == dn) ? 1.f : 0.f)) : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < NSL; ++u) {
+    const int i = tid + 256 * u;
+    const int d = i / (s3::MAXF * s3::CH), rem = i - d * s3::MAXF * s3::CH;
+    sl[d][rem / s3::CH][rem % s3::CH] = sv[u];
+  }
+#pragma unroll
+  for (int u = 0; u < NXN; ++u) {
+    const int i = tid + 256 * u;
+    const int d = i / (s3::CH * KN), rem = i - d * s3::CH * KN;
+    xn[d][rem / KN][rem % KN] = xv[u];
+  }
+  __syncthreads();
+  if (tid < s3::CH) {
+    float n2 = 0.f;
+    for (int j = 0; j < KN; ++j) n2 = fmaf(xn[0][tid][j], xn[0][tid][j], n2);
+    for (int f = 0; f < dc; ++f) n2 += sl[0][f][tid] != -1 ? 1.f : 0.f;
+    const bool live = t0 + c * s3::CH + tid < t1;
+    float a = 0.f;
+    if (live) a = affine ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : 1.f;
+    sa[tid] = a;
+    out[2 * s3::MAT + tid] = a;
+    out[s3_prep_y<KN>() + tid] = live ? load_y(yv, t0 + c * s3::CH + tid, y8) : __builtin_nanf("");
+  }
+  for (int i = tid; i < KN * s3::CH; i += 256) {
+    const int j = i / s3::CH, r = i - j * s3::CH;
+    out[2 * s3::MAT + s3::CH + i] = xn[0][r][j];
+  }
+  __syncthreads();
+  const int l31 = lane & 31, hi = lane >> 5;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    // pass 0: the aX1 tile (d = 1) of this wave; pass 1: its aG tile (d = 0)
+    const int d = pass == 0 ? 1 : 0;
+    const int I0 = pass == 0 ? 32 * (wave >> 1) : (wave == 0 ? 0 : 32);
+    const int J0 = pass == 0 ? 32 * (wave & 1) : (wave == 2 ? 32 : 0);
+    const bool zero = (pass == 1 && wave == 3) || c - d < 0;
+    f32x16 acc;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+    if (!zero) {
+      int cnt[16];
+#pragma unroll
+      for (int g = 0; g < 16; ++g) cnt[g] = 0;
+      for (int f = 0; f < dc; ++f) {
+        const int b = sl[d][f][J0 + l31];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int4 a4 = *reinterpret_cast<const int4*>(&sl[0][f][I0 + 8 * g + 4 * hi]);
+          const int av[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int a = av[e] == -1 ? 0x7ffffffe : av[e];
+            const int x = a ^ b;
+            cnt[4 * g + e] += (x & 0x7fffffff) ? 0 : (x < 0 ? -1 : 1);
+          }
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[g] = (float)cnt[g];
+#pragma unroll
+      for (int k0 = 0; k0 < KN; k0 += 2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xn[0][I0 + l31][k0 + hi], xn[d][J0 + l31][k0 + hi],
+                                                   acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int t = I0 + (g & 3) + 8 * (g >> 2) + 4 * hi, col = J0 + l31;
+      float v = sa[t] * acc[g];
+      if (d == 0 && col >= t) v = 0.f;  // aG strictly lower
+      out[d * s3::MAT + t * s3::CH + col] = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ pass 4: scan
 struct S3Smem {
   alignas(16) float G[2][s3::CH][s3::GS];   // aG_k by chunk parity
@@ -373,7 +500,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     const float* __restrict__ w, int dim, float* __restrict__ aglob, int cap, long long gstride,
     float* __restrict__ cout, float* __restrict__ ws, float* __restrict__ wsd, SeqParams p) {
   __shared__ S3Smem sm;
-  extern __shared__ float tab[];  // [cap]
+  extern __shared__ float tab[];  // [cap] + 64 scratch words (one per lane)
   constexpr int PF = s3_prep_floats<KN>();
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -593,7 +720,10 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         if (__builtin_amdgcn_ballot_w64(sc) == 0ull) continue;
         const int lid = (int)(m >> s3::LID_SHIFT);
         const float val = (m & s3::F_SIGN) ? -cv : cv;
-        if (sc) {
+        if (__builtin_amdgcn_ballot_w64(sc && lid >= cap) == 0ull) {
+          // every lane adds (the others 0 into its own word past the table): no exec branch
+          atomicAdd(&tab[sc ? lid : cap + lane], sc ? val : 0.f);
+        } else if (sc) {
           if (lid < cap) atomicAdd(&tab[lid], val);
           else atomicAdd(&ag[lid - cap], val);
         }
@@ -620,8 +750,11 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         // the table's global spill (lid ≥ cap) on its own wave-uniform path: a global
         // read merged into the LDS path would make every later use wait for all loads
         if (__builtin_amdgcn_ballot_w64((tg || init) && lid >= cap) == 0ull) {
-          if (tg) val = tab[lid];
-          if (init) tab[lid] = val;
+          // one read and one write per lane, the lanes without a table entry on their own
+          // word past the table (tab[cap + lane]): no exec-masked branches in this path
+          const float tv = tab[tg ? lid : cap + lane];
+          val = tg ? tv : val;
+          tab[init ? lid : cap + lane] = val;
         } else {
           if (tg) val = lid < cap ? tab[lid] : __hip_atomic_load(&ag[lid - cap], __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -691,6 +824,33 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
 // (high-cardinality fields: little repetition) go to dacc directly. c = 0 rows (most rows
 // the PA rule leaves alone) are skipped. The spokes' sums meet in L2 in arrival order: the
 // round's model is the replica average up to fp32 rounding of those sums.
+// The dense columns (numerical, intercept) from the spokes' dense deltas, the
+// accumulator's scalars and the round's statistics (one block of 256 threads; run as the extra row of the scatter grid).
+__device__ void s3_dense_body(const float* __restrict__ ws,
+                              const float* __restrict__ wsd, int S_act, int dn, int dim,
+                              int bias, float inv_p, float* __restrict__ dacc,
+                              double* __restrict__ cum) {
+  const int tid = threadIdx.x;
+  for (int i = tid; i < dn; i += 256) {
+    float v = 0.f;
+    for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + i];
+    dacc[i] = v * inv_p;
+  }
+  if (tid == 0) {
+    float v = 0.f;
+    if (bias)
+      for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + dn];
+    dacc[dim - 1] = v * inv_p;
+    dacc[dim] = (float)S_act * inv_p;
+    dacc[dim + 1] = (float)S_act * inv_p;
+  }
+  if (cum && tid < 6 && tid != 4) {
+    double t = 0.0;
+    for (int s = 0; s < S_act; ++s) t += (double)ws[(size_t)s * s3::WS + tid];
+    cum[tid] += t;
+  }
+}
+
 namespace s3 {
 constexpr int SB = 4096;     // rows per scatter block
 constexpr int SH = 4096;     // LDS hash entries per block
@@ -700,7 +860,15 @@ constexpr int SPROBE = 8;
 __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__ slotsT,
                                                          const float* __restrict__ cout, int B,
                                                          int n_rows, float inv_p,
-                                                         float* __restrict__ dacc) {
+                                                         float* __restrict__ dacc, int dc,
+                                                         const float* __restrict__ ws,
+                                                         const float* __restrict__ wsd, int S_act,
+                                                         int dn, int dim, int bias,
+                                                         double* __restrict__ cum) {
+  if ((int)blockIdx.y == dc) {  // the dense columns / scalars / statistics: one extra block
+    if (blockIdx.x == 0) s3_dense_body(ws, wsd, S_act, dn, dim, bias, inv_p, dacc, cum);
+    return;
+  }
   __shared__ int hk[s3::SH];
   __shared__ float hv[s3::SH];
   const int f = blockIdx.y, tid = threadIdx.x;
@@ -738,34 +906,6 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
   }
 }
 
-// The dense columns (numerical, intercept) from the spokes' dense deltas, the
-// accumulator's scalars and the round's statistics (one block).
-__global__ __launch_bounds__(256) void s3_dense_kernel(const float* __restrict__ ws,
-                                                       const float* __restrict__ wsd, int S_act,
-                                                       int dn, int dim, int bias, float inv_p,
-                                                       float* __restrict__ dacc,
-                                                       double* __restrict__ cum) {
-  const int tid = threadIdx.x;
-  for (int i = tid; i < dn; i += 256) {
-    float v = 0.f;
-    for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + i];
-    dacc[i] = v * inv_p;
-  }
-  if (tid == 0) {
-    float v = 0.f;
-    if (bias)
-      for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + dn];
-    dacc[dim - 1] = v * inv_p;
-    dacc[dim] = (float)S_act * inv_p;
-    dacc[dim + 1] = (float)S_act * inv_p;
-  }
-  if (cum && tid < 6 && tid != 4) {
-    double t = 0.0;
-    for (int s = 0; s < S_act; ++s) t += (double)ws[(size_t)s * s3::WS + tid];
-    cum[tid] += t;
-  }
-}
-
 template <int RULE, int KN>
 static int s3_launch_scan(const int* slotsT, const uint32_t* meta, int dc, int dn, const void* y,
                           int B, int R, int S_act, const float* prep, int nchs, const float* w,
@@ -779,7 +919,7 @@ static int s3_launch_scan(const int* slotsT, const uint32_t* meta, int dc, int d
     attr_set = true;
   }
   hipLaunchKernelGGL((s3_scan_kernel<RULE, KN>), dim3(S_act), dim3(s3::NT),
-                     (size_t)cap * sizeof(float), st, slotsT, meta, dc, dn, y, B, R, prep, nchs, w,
+                     (size_t)(cap + 64) * sizeof(float), st, slotsT, meta, dc, dn, y, B, R, prep, nchs, w,
                      dim, aglob, cap, gstride, cout, ws, wsd, p);
   return (int)hipGetLastError();
 }
@@ -807,6 +947,10 @@ OMLDM_API int omldm_scan3_lds_cap() {
 }
 
 OMLDM_API void omldm_scan3_set_cap(int cap) { g_s3_cap_override = cap; }
+
+// 1: pass 3 on the VALU reference kernel (tests: A/B against the MFMA kernel)
+static int g_s3_gram_valu = 0;
+OMLDM_API void omldm_scan3_set_gram_valu(int v) { g_s3_gram_valu = v; }
 
 // 1 when the v3 round handles this shape (field-aware slots, R ≤ RMAX).
 OMLDM_API int omldm_scan3_fits(int dn, int dc, int R, int bias) {
@@ -879,23 +1023,32 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   const int nchs = (R + s3::CH - 1) / s3::CH;
   const int affine = rule != kSeqLogistic;
   const float kadd = (rule != kSeqLogistic && variant == 2) ? 0.5f / C : 0.f;
-  if (s3_kn(dn, bias) == 16)
-    hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
-                       num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
-  else
-    hipLaunchKernelGGL(s3_gram_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
-                       num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+  if (g_s3_gram_valu) {
+    if (s3_kn(dn, bias) == 16)
+      hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
+                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+    else
+      hipLaunchKernelGGL(s3_gram_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
+                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+  } else if (s3_kn(dn, bias) == 16) {
+    hipLaunchKernelGGL(s3_gram_mfma_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT,
+                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+  } else {
+    hipLaunchKernelGGL(s3_gram_mfma_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT,
+                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+  }
   return (int)hipGetLastError();
 }
 
-// Pass 4 (the scan) + pass 5 (the combine into dacc, zeroed here) on a prepared round.
+// Pass 4 (the scan) + pass 5 (the combine into dacc; zeroed here unless flags bit 0 says
+// the caller keeps it zero) on a prepared round.
 // `parts` is kept for the pipelined-sync interface: part 0 completes all of dacc (the
 // combine is a few tens of µs of atomics), later parts launch nothing.
 OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int y8, int B, int R,
                               int S, float* dacc, int dim, double* cum, int rule, int variant,
                               float C, float eps, float lr, float inv_p, int bias,
                               long long span_in, void* const* ptrs, int part, int parts,
-                              void* stream) {
+                              int flags, void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
   if (span_in < 0) return -2;  // the slots' range was checked by the prepare
@@ -923,12 +1076,14 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
   }
   if (e) return e;
   (void)span;
-  hipMemsetAsync(dacc, 0, sizeof(float) * (size_t)dim, st);
+  // flags bit 0: dacc[:dim] is already zero (linear_apply clears it after every round), so
+  // the combine adds straight into it (a memset beside the prep kernels took 15-20 us)
+  if (!(flags & 1)) hipMemsetAsync(dacc, 0, sizeof(float) * (size_t)dim, st);
   const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
-  hipLaunchKernelGGL(s3_scatter_kernel, dim3((n_rows + s3::SB - 1) / s3::SB, dc), dim3(256), 0, st,
-                     W.slotsT, W.cout, B, n_rows, inv_p, dacc);
-  hipLaunchKernelGGL(s3_dense_kernel, dim3(1), dim3(256), 0, st, W.ws, W.wsd, S_act, dn, dim,
-                     bias, inv_p, dacc, cum);
+  const int nblk = (n_rows + s3::SB - 1) / s3::SB;
+  hipLaunchKernelGGL(s3_scatter_kernel, dim3(nblk > 0 ? nblk : 1, dc + 1), dim3(256), 0, st,
+                     W.slotsT, W.cout, B, n_rows, inv_p, dacc, dc, W.ws, W.wsd, S_act, dn, dim,
+                     bias, cum);
   return (int)hipGetLastError();
 }
 

@@ -95,5 +95,7 @@ def parse_records(records: list, space: FeatureSpace, threads: int | None = None
             threads)
     raw = None
     if keep_raw:
-        raw = [e.decode() if isinstance(e, (bytes, bytearray)) else e for e in enc]
+        # DIB records (io/dib.py) stay bytes: their payload is not text
+        raw = [e.decode() if isinstance(e, (bytes, bytearray)) and not (e and e[0] == 0xB1)
+               else e for e in enc]
     return HashedBatch(num, cat, y, raw, space.cat_span), op, int(valid)

@@ -14,6 +14,50 @@ import torch
 from omldm_amd.ops import native
 
 
+def copy_cu_bits(total: int, ncu: int, layout: int) -> set[int]:
+    """CU-mask bits of the ingest lane (same choice as omldm_stream_create_cumask_ex)."""
+    if ncu <= 0 or ncu >= total:
+        return set(range(total))
+    if layout == 1:
+        return set(range(ncu))
+    step = total // ncu
+    return {total - 1 - i * step for i in range(ncu)}
+
+
+def reserve_cu_bits(total: int, n: int, taken: set[int], nxcd: int = 8) -> set[int]:
+    """n CU-mask bits outside ``taken``, spread evenly over the XCDs. The bit → XCD map
+    (round-robin c % nxcd, or blocked c // (total / nxcd)) is measured by
+    scripts/cumask_probe.py; a bit c = per·x + x + nxcd·j is on XCD x under both, so the
+    choice does not depend on which one the runtime uses."""
+    if n <= 0:
+        return set()
+    if total % nxcd:
+        nxcd = 1
+    per = total // nxcd
+    quota = -(-n // nxcd)
+    out: set[int] = set()
+    for x in range(nxcd):
+        got = 0
+        for j in range(per // nxcd):
+            c = per * x + x + nxcd * j
+            if c < total and c not in taken and got < quota and len(out) < n:
+                out.add(c)
+                got += 1
+    return out
+
+
+def cumask_stream(bits: set[int], total: int, device=None):
+    """A torch ExternalStream restricted to the CUs in ``bits`` (returns (stream, raw))."""
+    words = (total + 31) // 32
+    arr = (native.u32 * words)()
+    for c in bits:
+        arr[c >> 5] |= 1 << (c & 31)
+    raw = native.hip().omldm_stream_create_cumask_words(arr, words)
+    if not raw:
+        raise RuntimeError("hipExtStreamCreateWithCUMask failed")
+    return torch.cuda.ExternalStream(raw, device=device), raw
+
+
 class CopyEngine:
     def __init__(self, nstreams: int = 2):
         self.lib = native.hip()

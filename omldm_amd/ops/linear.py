@@ -433,10 +433,13 @@ SCAN3_ROUNDS = 0
 
 def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
                        rule: "LinearRule", inv_p: float, cum: torch.Tensor | None = None,
-                       parts: int = 1, on_part=None, hashed: bool = False) -> None:
+                       parts: int = 1, on_part=None, hashed: bool = False,
+                       dacc_zero: bool = True) -> None:
     """One Synchronous round through the v3 table scan (csrc/kernels/linear_scan3.hip):
-    dacc[:dim] = inv_p·Σ_spokes Δ_s (written whole), dacc[dim] = dacc[dim+1] =
-    S_act·inv_p, so ``linear_apply`` averages the spokes' replicas into w. The combine
+    dacc[:dim] += inv_p·Σ_spokes Δ_s, dacc[dim] = dacc[dim+1] = S_act·inv_p, so
+    ``linear_apply`` averages the spokes' replicas into w. Like every round kernel it
+    expects dacc[:dim] = 0 on entry (``linear_apply`` leaves it so); ``dacc_zero=False``
+    zeroes it first. The combine
     runs in ``parts`` launches over key ranges; ``on_part(k, lo, hi)`` is called after
     part k with the slice of dacc it completed (its collective may start then)."""
     dim = int(dacc.shape[0]) - 2
@@ -461,7 +464,7 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
         rc = h.omldm_scan3_run(ptr(w), num.shape[1], batch.dc, ptr(y), int(y.dtype == torch.int8),
                                batch.B, R, S, ptr(dacc), dim, ptr(cum), rule.rule, rule.variant,
                                rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), span, ptrs, k,
-                               parts, native.stream_of(w))
+                               parts, int(bool(dacc_zero)), native.stream_of(w))
         check(rc, "omldm_scan3_run")
         if on_part is not None:
             on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts, span))

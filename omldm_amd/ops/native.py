@@ -68,12 +68,13 @@ HIP_SIGS = [
     ("omldm_linear_seq_reduce", i32, [vp, vp, i32, i32, vp, f32, vp, vp, vp]),
     ("omldm_scan3_lds_cap", i32, []),
     ("omldm_scan3_set_cap", None, [i32]),
+    ("omldm_scan3_set_gram_valu", None, [i32]),
     ("omldm_scan3_fits", i32, [i32, i32, i32, i32]),
     ("omldm_scan3_ws_words", i64, [i32, i32, i32, i32, i32, i32, i64, i32]),
     ("omldm_scan3_prepare", i32, [vp, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32,
                                   i32, f32, i64, i32, vp, vp]),
     ("omldm_scan3_run", i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, f32,
-                              f32, f32, f32, i32, i64, vp, i32, i32, vp]),
+                              f32, f32, f32, i32, i64, vp, i32, i32, i32, vp]),
     ("omldm_scan3_part_bounds", i32, [i32, i32, i32, i64, i32, i32, vp]),
     ("omldm_scan3_stamps", i32, [vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
@@ -132,6 +133,8 @@ HIP_SIGS = [
     ("omldm_event_record", i32, [vp, vp]),
     ("omldm_stream_create_cumask", vp, [i32]),
     ("omldm_stream_create_cumask_ex", vp, [i32, i32, i32]),
+    ("omldm_stream_create_cumask_words", vp, [vp, i32]),
+    ("omldm_cu_probe", i32, [vp, vp]),
     ("omldm_host_device_ptr", vp, [vp]),
     ("omldm_stream_destroy", i32, [vp]),
     ("omldm_host_register", i32, [vp, i64]),
@@ -142,6 +145,7 @@ HIP_SIGS = [
 HOST_SIGS = [
     ("omldm_cpu_kmeans_seq", i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp]),
     ("omldm_murmur3_32", u32, [C.c_char_p, i64, u32]),
+    ("omldm_json_to_dib", i64, [vp, vp, i32, i32, i32, i32, vp, i64, vp, i32]),
     ("omldm_crc32c", u32, [C.c_char_p, i64, u32]),
     ("omldm_hash_cat", C.c_int32, [C.c_char_p, i64, i32, i32, i64]),
     ("omldm_hash_cat16", C.c_int32, [C.c_char_p, i64, i32, i32]),

@@ -84,3 +84,30 @@ def test_gpu_parser_exact_size_buffer_and_group_edges(cuda):
         assert np.array_equal(op.cpu().numpy(), hop)
         ok = torch.from_numpy(hop >= 0)
         assert torch.equal(num.cpu()[ok], hb.num[ok]) and torch.equal(cat.cpu()[ok], hb.cat[ok])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field_aware", [False, True])
+def test_gpu_parser_decodes_dib_like_the_json(cuda, field_aware):
+    """DIB records (omldm_amd/io/dib.py) interleaved with JSON in one block: the GPU
+    parser's rows equal the host parser's rows of the JSON originals."""
+    from omldm_amd.io import dib
+    from omldm_amd.ops.ingest import GpuJsonParser
+
+    sp = FeatureSpace(13, 2, 26, 1 << 20, field_aware=field_aware)
+    recs = [r.encode() for r in synth_json_records(2000, sp, seed=5)] + ADVERSARIAL * 2
+    d = dib.records_to_dib(recs, sp.n_numerical, sp.n_discrete, sp.dc)
+    mixed = [x for i, pair in enumerate(zip(recs, d)) for x in (pair if i % 3 else pair[::-1])]
+    buf, offs = join_block([r + b"\n" for r in mixed])
+    hb, hop, hval = parse_block(*join_block(recs), sp, 4)
+    gb, gop, gval = GpuJsonParser(cuda).parse(buf, offs, sp)
+    torch.cuda.synchronize()
+    g = gop.cpu().numpy()
+    assert np.array_equal(g[0::2], hop) and np.array_equal(g[1::2], hop)
+    assert gval.cpu().tolist()[:2] == [2 * int((hop == 0).sum()), 2 * int((hop == 1).sum())]
+    ok = torch.from_numpy(hop >= 0)
+    for k in (0, 1):
+        assert torch.equal(gb.num.cpu()[k::2][ok], hb.num[ok])
+        assert torch.equal(gb.cat.cpu()[k::2][ok], hb.cat[ok])
+        assert torch.equal(torch.nan_to_num(gb.y.cpu()[k::2][ok], nan=-7.0),
+                           torch.nan_to_num(hb.y[ok], nan=-7.0))

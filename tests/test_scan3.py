@@ -280,3 +280,34 @@ def test_gpu_scan3_bench_geometry_matches_cpu_oracle(monkeypatch):
     assert d.max() < 2e-3 and float(d.mean()) < 1e-6, (d.max(), d.mean())
     assert res["cuda"][1]["fitted"] == res["cpu"][1]["fitted"] == 3 * B
     assert abs(res["cuda"][1]["mistakes"] - res["cpu"][1]["mistakes"]) <= 1e-3 * 3 * B
+
+
+@gpu
+@pytest.mark.parametrize("dn,exact", [(0, True), (13, False)])
+def test_gpu_scan3_mfma_prep_matches_valu_prep(dn, exact):
+    """Pass 3 on the matrix cores (s3_gram_mfma_kernel: ±1 slot-match counts in the MFMA
+    accumulator, then v_mfma_f32_32x32x2_f32 over the dense columns) against the VALU
+    reference kernel, every float of every chunk's prep block. With only the intercept as
+    dense column every Gram entry is a small integer: bit-equal. With 13 numerical
+    columns the dot products are summed in a different order: equal to fp32 rounding."""
+    dev = _cuda()
+    space = FeatureSpace(dn, 0, 26, 1 << 16)
+    S, R = 4, 512
+    batch = synth_raw(space, S * R, seed=7, missing=0.05).to(dev)
+    lr = L.LinearRule(rule=L.RULE_HINGE, variant=L.PA1, C=1.0, bias=True)
+    h = native.hip()
+    preps = []
+    for valu, slot in ((0, 14), (1, 15)):
+        h.omldm_scan3_set_gram_valu(valu)
+        try:
+            sp = L.linear_scan3_prepare(batch, R, S, space.dim, True, lr, slot=slot)
+            torch.cuda.synchronize()
+            preps.append(sp.bufs[3].clone().cpu())
+        finally:
+            h.omldm_scan3_set_gram_valu(0)
+    a, b = preps
+    if exact:
+        assert torch.equal(a, b), (a - b).abs().max()
+    else:
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()
+        assert (a == b).float().mean() > 0.5  # the categorical entries are exact
