@@ -36,9 +36,15 @@
 //   3. s3_gram_kernel    one workgroup per (spoke, chunk): a_t, G_k and X1_k (categorical
 //                        match counts and the dense block), scaled by a_t; the chunk's
 //                        dense columns transposed for the helpers
-//   4. s3_scan_kernel    one workgroup per spoke: scanner wave + 7 helper waves
-//   5. s3_scatter_kernel the whole GPU: dacc[slot] += inv_p·c·sign per occurrence (fp32
-//                        atomics) + one block for the dense columns, scalars, statistics
+//   4. s3_scan_kernel    one workgroup per spoke: scanner wave + 11 helper waves; in the
+//                        same launch, combiner workgroups (one per spoke by default) fold
+//                        dacc[slot] += inv_p·c·sign per occurrence WHILE the spoke scans:
+//                        the scanner publishes each row's c as an {epoch, c} 8-B granule
+//                        (write-through), the combiner polls the granules chunk by chunk,
+//                        sums per slot in an LDS hash and adds each sum to dacc at the end
+//   5. s3_tail_kernel    one block: the dense columns, scalars and statistics
+//      (s3_scatter_kernel: the earlier whole-GPU combine after the scan, kept as the A/B
+//      reference — omldm_scan3_set_comb(0))
 #include "common.h"
 #include "hash_dev.h"
 #include "seq_common.h"
@@ -426,8 +432,9 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
   for (int pass = 0; pass < 2; ++pass) {
     // pass 0: the aX1 tile (d = 1) of this wave; pass 1: its aG tile (d = 0)
     const int d = pass == 0 ? 1 : 0;
-    const int I0 = pass == 0 ? 32 * (wave >> 1) : (wave == 0 ? 0 : 32);
-    const int J0 = pass == 0 ? 32 * (wave & 1) : (wave == 2 ? 32 : 0);
+    // aG tiles: wave 0 (0,0), 1 (32,0), 2 (32,32), 3 (0,32) — the all-zero upper right
+    const int I0 = pass == 0 ? 32 * (wave >> 1) : ((wave == 1 || wave == 2) ? 32 : 0);
+    const int J0 = pass == 0 ? 32 * (wave & 1) : (wave >= 2 ? 32 : 0);
     const bool zero = (pass == 1 && wave == 3) || c - d < 0;
     f32x16 acc;
 #pragma unroll
@@ -492,16 +499,118 @@ struct S3Cand {
 
 __device__ unsigned long long* g_s3_stamps;
 __device__ int g_s3_debug;  // diagnostics: 1 = every gather reads w[0] (latency experiment)
+__device__ int g_s3_comb_err;  // a combiner gave up waiting for its spoke (bounded spin)
+
+// The in-launch combine (Guideline 16, R2 "the data is the flag"): the scanner stores row
+// t's c as one 8-B granule {epoch << 32 | bits(c)} with a relaxed agent-scope atomic store
+// (global_store_dwordx2 sc1: write-through, no release fence), the combiner re-reads a
+// chunk's 64 granules with agent-scope atomic loads (sc1, past its L1) until every tag is
+// this round's epoch. The granule buffer is zeroed when allocated and every round on it
+// takes the next epoch (never 0), so no granule of an earlier round can match.
+typedef __attribute__((address_space(1))) unsigned long long s3_gu64;
+struct S3Comb {
+  unsigned long long* gran;  // [B] granules: the scanner's c per row
+  uint32_t epoch;
+  int S_act;                 // blocks [0, S_act) scan, the rest combine
+  float* dacc;
+  float inv_p;
+};
+namespace s3 {
+constexpr int CHASH = 8192;          // combiner LDS hash entries (keys in G, sums in X1)
+constexpr unsigned SPIN_MAX = 1u << 21;      // polls before a combiner gives up (~1 s)
+}  // namespace s3
+
+// One combiner workgroup: spoke i mod S_act, part i / S_act. Its waves take the spoke's
+// chunks round-robin (wave w of part j: chunks j·12 + w, then + 12·parts), every field of
+// the chunk: a wave has 12 chunk periods to fold its chunk, so the combine keeps pace with
+// the scanner and only the last chunk is left when the scan ends (one wave per field, every
+// chunk, fell behind: its slot loads and its poll were one round trip each per chunk). All
+// of a chunk's slot loads are issued before the poll. Rows with c = 0 add nothing.
+__device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int dc, int B, int R,
+                                           const S3Comb& cb, S3Smem& sm) {
+  const int i = (int)blockIdx.x - cb.S_act;
+  const int s = i % cb.S_act, part = i / cb.S_act;
+  const int nparts = ((int)gridDim.x - cb.S_act) / cb.S_act;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int* hk = reinterpret_cast<int*>(&sm.G[0][0][0]);
+  float* hv = &sm.X1[0][0][0];
+  for (int j = tid; j < s3::CHASH; j += s3::NT) {
+    hk[j] = -1;
+    hv[j] = 0.f;
+  }
+  __syncthreads();
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  const int nch = t0 < t1 ? (t1 - t0 + s3::CH - 1) / s3::CH : 0;
+  const int wstride = nparts * (s3::NH + 1);
+  const unsigned long long want = (unsigned long long)cb.epoch;
+  for (int k = part * (s3::NH + 1) + wave; k < nch; k += wstride) {
+    const int row = t0 + k * s3::CH + lane;
+    const bool in = row < t1;
+    int v[s3::MAXF];
+#pragma unroll
+    for (int f = 0; f < s3::MAXF; ++f) {
+      const bool ok = in && f < dc;
+      const int x = slotsT[ok ? (size_t)f * B + row : 0];
+      v[f] = ok ? x : -1;
+    }
+    unsigned long long g = 0;
+    bool ready = false;
+    for (unsigned spins = 0; spins < s3::SPIN_MAX; ++spins) {
+      g = in ? __hip_atomic_load((s3_gu64*)(cb.gran + row), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT)
+             : (want << 32);
+      if (__builtin_amdgcn_ballot_w64((g >> 32) != want) == 0ull) {
+        ready = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ready) {
+      if (lane == 0) atomicExch(&g_s3_comb_err, 1);
+      break;
+    }
+    const float c = __uint_as_float((uint32_t)g);
+    if (__builtin_amdgcn_ballot_w64(c != 0.f) == 0ull) continue;
+#pragma unroll
+    for (int f = 0; f < s3::MAXF; ++f) {
+      if (c == 0.f || v[f] == -1) continue;
+      const int key = v[f] & 0x7fffffff;
+      const float val = v[f] < 0 ? -c * cb.inv_p : c * cb.inv_p;
+      uint32_t at = ((uint32_t)key * 0x9E3779B1u) >> (32 - 13);
+      bool done = false;
+      for (int probe = 0; probe < 8; ++probe) {
+        const int prev = atomicCAS(&hk[at], -1, key);
+        if (prev == -1 || prev == key) {
+          atomicAdd(&hv[at], val);
+          done = true;
+          break;
+        }
+        at = (at + 1) & (s3::CHASH - 1);
+      }
+      if (!done) atomicAdd(&cb.dacc[key], val);
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < s3::CHASH; j += s3::NT) {
+    const int key = hk[j];
+    if (key != -1) atomicAdd(&cb.dacc[key], hv[j]);
+  }
+}
 
 template <int RULE, int KN>
 __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s3_scan_kernel(
     const int* __restrict__ slotsT, const uint32_t* __restrict__ meta, int dc, int dn,
     const void* __restrict__ yv, int B, int R, const float* __restrict__ prep, int nchs,
     const float* __restrict__ w, int dim, float* __restrict__ aglob, int cap, long long gstride,
-    float* __restrict__ cout, float* __restrict__ ws, float* __restrict__ wsd, SeqParams p) {
+    S3Comb cb, float* __restrict__ ws, float* __restrict__ wsd, SeqParams p) {
   __shared__ S3Smem sm;
   extern __shared__ float tab[];  // [cap] + 64 scratch words (one per lane)
   constexpr int PF = s3_prep_floats<KN>();
+  if ((int)blockIdx.x >= cb.S_act) {  // a combiner workgroup
+    s3_combine(slotsT, dc, B, R, cb, sm);
+    return;
+  }
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int s = blockIdx.x;
@@ -593,7 +702,10 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         stamp(9);
         const float c = cf(u, p, y);
         sm.cb[b][lane] = c;
-        if (row < t1) cout[row] = c;
+        if (row < t1)  // the row's granule (write-through): the combiner polls it
+          __hip_atomic_store((s3_gu64*)(cb.gran + row),
+                             ((unsigned long long)cb.epoch << 32) | __float_as_uint(c),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (valid) {
           float m;
           if constexpr (RULE == kSeqLogistic) m = u;
@@ -720,10 +832,9 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         if (__builtin_amdgcn_ballot_w64(sc) == 0ull) continue;
         const int lid = (int)(m >> s3::LID_SHIFT);
         const float val = (m & s3::F_SIGN) ? -cv : cv;
-        if (__builtin_amdgcn_ballot_w64(sc && lid >= cap) == 0ull) {
-          // every lane adds (the others 0 into its own word past the table): no exec branch
-          atomicAdd(&tab[sc ? lid : cap + lane], sc ? val : 0.f);
-        } else if (sc) {
+        // (a branch-free form — every lane adding, the others 0 into a word of their own past
+        // the table — measured slower: 961 → 1118 cycles per chunk)
+        if (sc) {
           if (lid < cap) atomicAdd(&tab[lid], val);
           else atomicAdd(&ag[lid - cap], val);
         }
@@ -750,11 +861,11 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         // the table's global spill (lid ≥ cap) on its own wave-uniform path: a global
         // read merged into the LDS path would make every later use wait for all loads
         if (__builtin_amdgcn_ballot_w64((tg || init) && lid >= cap) == 0ull) {
-          // one read and one write per lane, the lanes without a table entry on their own
-          // word past the table (tab[cap + lane]): no exec-masked branches in this path
-          const float tv = tab[tg ? lid : cap + lane];
-          val = tg ? tv : val;
-          tab[init ? lid : cap + lane] = val;
+          // exec-masked: the write needs the gathered w only on a slot's first occurrence (a
+          // branch-free read + write per lane made every field's LDS write wait for its
+          // gather: margins 1.6 K → 4.5 K cycles per chunk, scripts/scan3_probe.py)
+          if (tg) val = tab[lid];
+          if (init) tab[lid] = val;
         } else {
           if (tg) val = lid < cap ? tab[lid] : __hip_atomic_load(&ag[lid - cap], __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -857,8 +968,16 @@ constexpr int SH = 4096;     // LDS hash entries per block
 constexpr int SPROBE = 8;
 }  // namespace s3
 
+__global__ __launch_bounds__(256) void s3_tail_kernel(const float* __restrict__ ws,
+                                                      const float* __restrict__ wsd, int S_act,
+                                                      int dn, int dim, int bias, float inv_p,
+                                                      float* __restrict__ dacc,
+                                                      double* __restrict__ cum) {
+  s3_dense_body(ws, wsd, S_act, dn, dim, bias, inv_p, dacc, cum);
+}
+
 __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__ slotsT,
-                                                         const float* __restrict__ cout, int B,
+                                                         const unsigned long long* __restrict__ gran, int B,
                                                          int n_rows, float inv_p,
                                                          float* __restrict__ dacc, int dc,
                                                          const float* __restrict__ ws,
@@ -882,7 +1001,7 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
   for (int row = r0 + tid; row < r1; row += 256) {
     const int v = col[row];
     if (v == -1) continue;
-    const float c = cout[row];
+    const float c = __uint_as_float((uint32_t)gran[row]);  // a kernel boundary after the scan
     if (c == 0.f) continue;
     const int key = v & 0x7fffffff;
     const float val = v < 0 ? -c * inv_p : c * inv_p;
@@ -909,8 +1028,8 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
 template <int RULE, int KN>
 static int s3_launch_scan(const int* slotsT, const uint32_t* meta, int dc, int dn, const void* y,
                           int B, int R, int S_act, const float* prep, int nchs, const float* w,
-                          int dim, float* aglob, int cap, long long gstride, float* cout, float* ws,
-                          float* wsd, const SeqParams& p, hipStream_t st) {
+                          int dim, float* aglob, int cap, long long gstride, const S3Comb& cb,
+                          int ncomb, float* ws, float* wsd, const SeqParams& p, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&s3_scan_kernel<RULE, KN>),
@@ -918,9 +1037,10 @@ static int s3_launch_scan(const int* slotsT, const uint32_t* meta, int dc, int d
                         160 * 1024 - (int)sizeof(S3Smem));
     attr_set = true;
   }
-  hipLaunchKernelGGL((s3_scan_kernel<RULE, KN>), dim3(S_act), dim3(s3::NT),
+  // blocks [0, S_act) scan (dispatched first), then ncomb combiner blocks per spoke
+  hipLaunchKernelGGL((s3_scan_kernel<RULE, KN>), dim3(S_act * (1 + ncomb)), dim3(s3::NT),
                      (size_t)(cap + 64) * sizeof(float), st, slotsT, meta, dc, dn, y, B, R, prep, nchs, w,
-                     dim, aglob, cap, gstride, cout, ws, wsd, p);
+                     dim, aglob, cap, gstride, cb, ws, wsd, p);
   return (int)hipGetLastError();
 }
 
@@ -952,6 +1072,21 @@ OMLDM_API void omldm_scan3_set_cap(int cap) { g_s3_cap_override = cap; }
 static int g_s3_gram_valu = 0;
 OMLDM_API void omldm_scan3_set_gram_valu(int v) { g_s3_gram_valu = v; }
 
+// combiner workgroups per spoke in the scan's launch (0: the whole-GPU scatter kernel after
+// the scan — the A/B reference); at most (MAXF + 11) / 12 parts do work
+static int g_s3_comb = 1;
+OMLDM_API void omldm_scan3_set_comb(int v) { g_s3_comb = v < 0 ? 0 : (v > 3 ? 3 : v); }
+OMLDM_API int omldm_scan3_get_comb() { return g_s3_comb; }
+
+// 1 if a combiner gave up waiting for its spoke's granules since the last call (resets it;
+// synchronises the device)
+OMLDM_API int omldm_scan3_comb_err() {
+  int v = 0, z = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_s3_comb_err), sizeof(v)) != hipSuccess) return -1;
+  if (v) hipMemcpyToSymbol(HIP_SYMBOL(g_s3_comb_err), &z, sizeof(z));
+  return v;
+}
+
 // 1 when the v3 round handles this shape (field-aware slots, R ≤ RMAX).
 OMLDM_API int omldm_scan3_fits(int dn, int dc, int R, int bias) {
   return dc > 0 && dc <= s3::MAXF && dn >= 0 && dn + (bias ? 1 : 0) <= s3::KNMAX && R > 0 &&
@@ -960,7 +1095,8 @@ OMLDM_API int omldm_scan3_fits(int dn, int dc, int R, int bias) {
 
 // Workspace sizes (4-byte words) for one round of S spokes × R rows, B rows in all, dc
 // fields:  0 slotsT [dc·B]   1 occ [2·dc·B]   2 lidcount [S]   3 prep [S·nchs·PF]
-//          4 cout [B]        5 ws [S·WS]     6 wsd [S·DS]     7 aglob [S·gstride]
+//          4 granules [2·B]  5 ws [S·WS]     6 wsd [S·DS]     7 aglob [S·gstride]
+// (the granule buffer must be zeroed when allocated: see S3Comb)
 OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn, int dc,
                                          long long span, int bias) {
   (void)span;
@@ -972,7 +1108,7 @@ OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn,
     case 1: return 2LL * dc * B;  // {slot, meta} per occurrence
     case 2: return S;
     case 3: return (long long)S * nchs * pf;
-    case 4: return B;
+    case 4: return 2LL * B;
     case 5: return (long long)S * s3::WS;
     case 6: return (long long)S * s3::DS;
     case 7: return (long long)S * ((long long)R * dc / 2 + 64);
@@ -987,7 +1123,7 @@ struct S3Ws {
   uint32_t* meta;
   int* lidcount;
   float* prep;
-  float* cout;
+  unsigned long long* gran;
   float* ws;
   float* wsd;
   float* aglob;
@@ -995,7 +1131,7 @@ struct S3Ws {
 
 static S3Ws s3_ws(void* const* ptrs) {
   return S3Ws{(int*)ptrs[0], (uint32_t*)ptrs[1], (int*)ptrs[2], (float*)ptrs[3],
-              (float*)ptrs[4], (float*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7]};
+              (unsigned long long*)ptrs[4], (float*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7]};
 }
 
 // Passes 1-3 (model-independent): slots, flags, Grams. `src` is the tokens (hashed = 0),
@@ -1044,11 +1180,14 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
 // the caller keeps it zero) on a prepared round.
 // `parts` is kept for the pipelined-sync interface: part 0 completes all of dacc (the
 // combine is a few tens of µs of atomics), later parts launch nothing.
+// `epoch`: this round's granule tag on the granule buffer ptrs[4] (≥ 1, one more than the
+// last round that used the buffer; the buffer was zeroed when allocated).
 OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int y8, int B, int R,
                               int S, float* dacc, int dim, double* cum, int rule, int variant,
                               float C, float eps, float lr, float inv_p, int bias,
                               long long span_in, void* const* ptrs, int part, int parts,
-                              int flags, void* stream) {
+                              int flags, unsigned epoch, void* stream) {
+  if (epoch == 0u) return -2;
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
   if (span_in < 0) return -2;  // the slots' range was checked by the prepare
@@ -1064,25 +1203,32 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
                     eps, lr, inv_p, bias, y8, span};
   const int cap = omldm_scan3_lds_cap();
   const long long gstride = (long long)R * dc / 2 + 64;
-  int e;
-  if (kn == 16) {
-    e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
-      : rule == kSeqEps ? s3_launch_scan<kSeqEps, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
-      : s3_launch_scan<kSeqLogistic, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st);
-  } else {
-    e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
-      : rule == kSeqEps ? s3_launch_scan<kSeqEps, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st)
-      : s3_launch_scan<kSeqLogistic, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, W.cout, W.ws, W.wsd, p, st);
-  }
-  if (e) return e;
-  (void)span;
   // flags bit 0: dacc[:dim] is already zero (linear_apply clears it after every round), so
   // the combine adds straight into it (a memset beside the prep kernels took 15-20 us)
   if (!(flags & 1)) hipMemsetAsync(dacc, 0, sizeof(float) * (size_t)dim, st);
+  const int ncomb = g_s3_comb;
+  const S3Comb cb{W.gran, epoch, S_act, dacc, inv_p};
+  int e;
+  if (kn == 16) {
+    e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
+      : rule == kSeqEps ? s3_launch_scan<kSeqEps, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
+      : s3_launch_scan<kSeqLogistic, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st);
+  } else {
+    e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
+      : rule == kSeqEps ? s3_launch_scan<kSeqEps, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
+      : s3_launch_scan<kSeqLogistic, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st);
+  }
+  if (e) return e;
+  (void)span;
+  if (ncomb > 0) {  // the categorical slots were combined in the scan's launch
+    hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, W.ws, W.wsd, S_act, dn, dim,
+                       bias, inv_p, dacc, cum);
+    return (int)hipGetLastError();
+  }
   const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
   const int nblk = (n_rows + s3::SB - 1) / s3::SB;
   hipLaunchKernelGGL(s3_scatter_kernel, dim3(nblk > 0 ? nblk : 1, dc + 1), dim3(256), 0, st,
-                     W.slotsT, W.cout, B, n_rows, inv_p, dacc, dc, W.ws, W.wsd, S_act, dn, dim,
+                     W.slotsT, W.gran, B, n_rows, inv_p, dacc, dc, W.ws, W.wsd, S_act, dn, dim,
                      bias, cum);
   return (int)hipGetLastError();
 }

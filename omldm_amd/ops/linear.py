@@ -372,24 +372,56 @@ def _s3_slot_for(key) -> str:
     return f"k{i}"
 
 
+# The scanner's per-row c granules {epoch, c} (one buffer per stream): zeroed when
+# allocated, and every round on the buffer tags its granules with the next epoch, so the
+# combiner workgroups of a round never take an earlier round's granule for this one's.
+_S3_GRAN: dict = {}
+
+
+def _s3_granules(dev, n: int, stream: int) -> list:
+    key = (str(dev), stream)
+    g = _S3_GRAN.get(key)
+    if g is None or g[0].numel() < n:
+        t = torch.zeros(max(n, 1 << 17), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize(dev)  # zeroed before any stream's round reads it
+        g = [t, 0]
+        _S3_GRAN[key] = g
+    return g
+
+
+def _s3_next_epoch(g: list) -> int:
+    g[1] += 1
+    if g[1] >= 0xFFFFFFFF:  # wrapped: start over on a zeroed buffer
+        g[0].zero_()
+        torch.cuda.synchronize(g[0].device)
+        g[1] = 1
+    return g[1]
+
+
 def _s3_run_ptrs(sp: "Scan3Prep", dev, stream: int):
-    """The prep's 4 model-independent workspaces + this stream's 4 run-time ones."""
+    """The prep's 4 model-independent workspaces + this stream's 4 run-time ones, and the
+    stream's granule buffer entry [tensor, epoch]."""
     import ctypes
 
     key = (id(sp), stream)
     hit = _S3_RUN_CACHE.get(key)
-    if hit is not None and hit[0] is sp:
-        return hit[1]
+    if hit is not None and hit[0] is sp and hit[3][0] is _S3_GRAN.get((str(dev), stream), [None])[0]:
+        return hit[1], hit[3]
     run = []
+    gran = None
     for i in _S3_SHARED:
         n = sp.bufs[i].numel()
-        run.append(_workspace(dev, n, key=f"s3_{S3_BUFS[i]}@{stream}"))
+        if S3_BUFS[i] == "cout":
+            gran = _s3_granules(dev, n, stream)
+            run.append(gran[0])
+        else:
+            run.append(_workspace(dev, n, key=f"s3_{S3_BUFS[i]}@{stream}"))
     ptrs = (ctypes.c_void_p * len(S3_BUFS))(*([b.data_ptr() for b in sp.bufs[:4]] +
                                               [b.data_ptr() for b in run]))
     if len(_S3_RUN_CACHE) > 256:
         _S3_RUN_CACHE.clear()
-    _S3_RUN_CACHE[key] = (sp, ptrs, run)
-    return ptrs
+    _S3_RUN_CACHE[key] = (sp, ptrs, run, gran)
+    return ptrs, gran
 
 
 def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
@@ -455,16 +487,19 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
     global SCAN3_ROUNDS
     SCAN3_ROUNDS += 1
     h = native.hip()
+    if SCAN3_ROUNDS == 1 and "OMLDM_S3_COMB" in os.environ:  # A/B: 0 = combine after the scan
+        h.omldm_scan3_set_comb(int(os.environ["OMLDM_S3_COMB"]))
     parts = max(1, int(parts))
     span = _s3_span(batch, dim)
     # run-time buffers (c per row, spoke statistics, the table spill) per stream: pipelines
     # on different streams may scan the same prep concurrently
-    ptrs = _s3_run_ptrs(sp, w.device, native.stream_of(w))
+    ptrs, gran = _s3_run_ptrs(sp, w.device, native.stream_of(w))
+    epoch = _s3_next_epoch(gran)
     for k in range(parts):
         rc = h.omldm_scan3_run(ptr(w), num.shape[1], batch.dc, ptr(y), int(y.dtype == torch.int8),
                                batch.B, R, S, ptr(dacc), dim, ptr(cum), rule.rule, rule.variant,
                                rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), span, ptrs, k,
-                               parts, int(bool(dacc_zero)), native.stream_of(w))
+                               parts, int(bool(dacc_zero)), epoch, native.stream_of(w))
         check(rc, "omldm_scan3_run")
         if on_part is not None:
             on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts, span))

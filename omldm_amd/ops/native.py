@@ -74,7 +74,10 @@ HIP_SIGS = [
     ("omldm_scan3_prepare", i32, [vp, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32,
                                   i32, f32, i64, i32, vp, vp]),
     ("omldm_scan3_run", i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, f32,
-                              f32, f32, f32, i32, i64, vp, i32, i32, i32, vp]),
+                              f32, f32, f32, i32, i64, vp, i32, i32, i32, u32, vp]),
+    ("omldm_scan3_set_comb", None, [i32]),
+    ("omldm_scan3_get_comb", i32, []),
+    ("omldm_scan3_comb_err", i32, []),
     ("omldm_scan3_part_bounds", i32, [i32, i32, i32, i64, i32, i32, vp]),
     ("omldm_scan3_stamps", i32, [vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),

@@ -311,3 +311,38 @@ def test_gpu_scan3_mfma_prep_matches_valu_prep(dn, exact):
     else:
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()
         assert (a == b).float().mean() > 0.5  # the categorical entries are exact
+
+
+@gpu
+@pytest.mark.parametrize("S,R,dn", [(16, 8192, 13), (5, 700, 0), (3, 1300, 13)])
+def test_gpu_scan3_inlaunch_combine_matches_scatter(S, R, dn):
+    """The combine folded into the scan's launch (combiner workgroups polling the scanner's
+    {epoch, c} granules) against the whole-GPU scatter kernel after the scan: the same
+    weights up to the fp32 order of the atomic sums, over three rounds on one granule
+    buffer (epochs 1..3), and no combiner gave up waiting."""
+    from omldm_amd.models.linear import SVM
+    from omldm_amd.parallel.comm import Comm
+    from omldm_amd.parallel.protocols import Synchronous
+
+    dev = _cuda()
+    h = native.hip()
+    space = FeatureSpace(dn, 0, 26, 1 << 20)
+    B = S * R - 17  # a short last spoke
+    res = {}
+    try:
+        for comb in (0, 1, 2):
+            h.omldm_scan3_set_comb(comb)
+            lrn = SVM({"variant": "PA-I", "C": 1.0}, space, dev)
+            proto = Synchronous(Comm(), lrn, {"virtualSpokes": S})
+            for k in range(3):
+                proto.round(synth_raw(space, B, start=k * B, seed=31).to(dev))
+            torch.cuda.synchronize()
+            assert h.omldm_scan3_comb_err() == 0
+            res[comb] = (lrn.w.cpu(), lrn.running_totals())
+    finally:
+        h.omldm_scan3_set_comb(1)
+    for comb in (1, 2):
+        d = (res[comb][0] - res[0][0]).abs()
+        assert float(d.max()) < 1e-4, (comb, float(d.max()))
+        assert res[comb][1]["fitted"] == res[0][1]["fitted"] == 3 * B
+        assert abs(res[comb][1]["mistakes"] - res[0][1]["mistakes"]) <= 2
