@@ -240,6 +240,8 @@ def main(argv=None) -> int:
     ap.add_argument("--ingest-cus", type=int, default=16)
     ap.add_argument("--cu-layout", type=int, default=1)
     ap.add_argument("--pull-blocks", type=int, default=16)
+    ap.add_argument("--pull-wt", type=int, default=1,
+                    help="pull copy stores write-through (the batch leaves the copy XCD's L2)")
     ap.add_argument("--lane", default="split", choices=["split", "plain"])
     ap.add_argument("--scan-cus", type=int, default=16,
                     help="CUs the prep stream leaves to the round's scan (split lane)")
@@ -292,6 +294,7 @@ def main(argv=None) -> int:
     raw_streams = []
     lane = {"copy": None, "compute": None}
     if on_gpu:
+        native.hip().omldm_pull_copy_set_wt(int(a.pull_wt))
         lane = {"copy": torch.cuda.Stream(device), "compute": torch.cuda.current_stream(device)}
         if a.lane == "split" and a.ingest_cus > 0:
             raw = native.hip().omldm_stream_create_cumask_ex(a.ingest_cus, 0, a.cu_layout)

@@ -36,6 +36,31 @@ __global__ __launch_bounds__(256) void pull_copy_kernel(const u32x4* __restrict_
   for (; i < n16; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
 }
 
+// The same copy with write-through (sc1) buffer stores: the copied lines leave the copying
+// XCD's L2 instead of staying there (a plain 20-MB store pass evicts what the training
+// kernels on that XCD keep in its 4-MB L2; the batch is read next by every XCD anyway, from
+// HBM). nbytes < 2^31 (one buffer descriptor).
+__global__ __launch_bounds__(256) void pull_copy_wt_kernel(const u32x4* __restrict__ src,
+                                                           u32x4* __restrict__ dst, long long n16) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)(n16 * 16), 0x00020000);
+  const int tid = blockIdx.x * 256 + threadIdx.x;
+  const int stride = gridDim.x * 256;
+  const int n = (int)n16;
+  int i = tid;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const u32x4 a = __builtin_nontemporal_load(src + i);
+    const u32x4 b = __builtin_nontemporal_load(src + i + stride);
+    const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+    const u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
+    __builtin_amdgcn_raw_buffer_store_b128(a, rs, i * 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(b, rs, (i + stride) * 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(c, rs, (i + 2 * stride) * 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(d, rs, (i + 3 * stride) * 16, 0, 16);
+  }
+  for (; i < n; i += stride)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_nontemporal_load(src + i), rs, i * 16, 0, 16);
+}
+
 // U loads in flight per lane before the stores (few waves, deep queues: long-latency PCIe
 // reads from many waves clog the memory pipeline shared with the training kernels).
 template <int U>
@@ -163,6 +188,10 @@ OMLDM_API int omldm_host_register(void* p, long long nbytes) {
 }
 
 // Copies nbytes from a pinned (device-mapped) host buffer to device memory by kernel.
+// 1: the default pull copy stores write-through (pull_copy_wt_kernel)
+static int g_pull_wt = 1;
+OMLDM_API void omldm_pull_copy_set_wt(int v) { g_pull_wt = v; }
+
 OMLDM_API int omldm_pull_copy(const void* host_src, void* dst, long long nbytes, int blocks,
                               void* stream) {
   if (nbytes <= 0) return 0;
@@ -185,6 +214,9 @@ OMLDM_API int omldm_pull_copy(const void* host_src, void* dst, long long nbytes,
     else if (U == 16)
       hipLaunchKernelGGL(pull_copy_u_kernel<16>, dim3(nblk), dim3(256), 0, st,
                          (const u32x4*)src, (u32x4*)dst, n16);
+    else if (g_pull_wt && n16 * 16 < (1LL << 31))
+      hipLaunchKernelGGL(pull_copy_wt_kernel, dim3(nblk), dim3(256), 0, st, (const u32x4*)src,
+                         (u32x4*)dst, n16);
     else
       hipLaunchKernelGGL(pull_copy_kernel, dim3(nblk), dim3(256), 0, st, (const u32x4*)src,
                          (u32x4*)dst, n16);

@@ -49,6 +49,9 @@
 #include "hash_dev.h"
 #include "seq_common.h"
 
+#include <mutex>
+#include <unordered_map>
+
 namespace omldm {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -508,7 +511,12 @@ __device__ int g_s3_comb_err;  // a combiner gave up waiting for its spoke (boun
 // this round's epoch. The granule buffer is zeroed when allocated and every round on it
 // takes the next epoch (never 0), so no granule of an earlier round can match.
 typedef __attribute__((address_space(1))) unsigned long long s3_gu64;
+template <bool B>
+struct S3Tag {
+  static constexpr bool value = B;
+};
 struct S3Comb {
+  const int* lidcount;       // [S] table entries per spoke (the flags pass)
   unsigned long long* gran;  // [B] granules: the scanner's c per row
   uint32_t epoch;
   int S_act;                 // blocks [0, S_act) scan, the rest combine
@@ -810,7 +818,12 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       xd[i] = ok ? v : 0.f;
     }
   };
-  auto body = [&](int k, Set& CUR, Set& NXT) {
+  // SPILL: the spoke's table outgrows the LDS (ids ≥ cap live in aglob). The two forms are
+  // separate loops: a global table access anywhere in the loop made the compiler wait for
+  // every load in flight (vmcnt(0)) before each field's margin, i.e. for the NXT set issued
+  // at the top of the body — a memory round trip per chunk.
+  auto body = [&](auto spill_tag, int k, Set& CUR, Set& NXT) {
+    constexpr bool SPILL = decltype(spill_tag)::value;
     const int cn = k + 1, ks = k - 1;
     if (wave == 1) stamp(7);
     // ---- issue the NXT set (chunk cn + 1) but its gathers
@@ -835,8 +848,12 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         // (a branch-free form — every lane adding, the others 0 into a word of their own past
         // the table — measured slower: 961 → 1118 cycles per chunk)
         if (sc) {
-          if (lid < cap) atomicAdd(&tab[lid], val);
-          else atomicAdd(&ag[lid - cap], val);
+          if constexpr (SPILL) {
+            if (lid < cap) atomicAdd(&tab[lid], val);
+            else atomicAdd(&ag[lid - cap], val);
+          } else {
+            atomicAdd(&tab[lid], val);
+          }
         }
       }
 #pragma unroll
@@ -860,13 +877,13 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         float val = CUR.g[i];
         // the table's global spill (lid ≥ cap) on its own wave-uniform path: a global
         // read merged into the LDS path would make every later use wait for all loads
-        if (__builtin_amdgcn_ballot_w64((tg || init) && lid >= cap) == 0ull) {
+        if (!SPILL || __builtin_amdgcn_ballot_w64((tg || init) && lid >= cap) == 0ull) {
           // exec-masked: the write needs the gathered w only on a slot's first occurrence (a
           // branch-free read + write per lane made every field's LDS write wait for its
           // gather: margins 1.6 K → 4.5 K cycles per chunk, scripts/scan3_probe.py)
           if (tg) val = tab[lid];
           if (init) tab[lid] = val;
-        } else {
+        } else if constexpr (SPILL) {
           if (tg) val = lid < cap ? tab[lid] : __hip_atomic_load(&ag[lid - cap], __ATOMIC_RELAXED,
                                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
           if (init) {
@@ -911,9 +928,16 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   load_dense(-2, A.xs);
   load_dense(0, A.xc);
   issue_gathers(A);
-  for (int k = -1; k <= nch; k += 2) {
-    body(k, A, Bs);
-    if (k + 1 <= nch) body(k + 1, Bs, A);
+  if (cb.lidcount[s] <= cap) {  // the whole table in LDS (every spoke of the bench stream)
+    for (int k = -1; k <= nch; k += 2) {
+      body(S3Tag<false>{}, k, A, Bs);
+      if (k + 1 <= nch) body(S3Tag<false>{}, k + 1, Bs, A);
+    }
+  } else {
+    for (int k = -1; k <= nch; k += 2) {
+      body(S3Tag<true>{}, k, A, Bs);
+      if (k + 1 <= nch) body(S3Tag<true>{}, k + 1, Bs, A);
+    }
   }
   if (stamps && lane == 0 && wave == 1)
     for (int k = 2; k < 8; ++k) atomicAdd(&stamps[(size_t)s * 16 + k], st_acc[k]);
@@ -1134,6 +1158,35 @@ static S3Ws s3_ws(void* const* ptrs) {
               (unsigned long long*)ptrs[4], (float*)ptrs[5], (float*)ptrs[6], (float*)ptrs[7]};
 }
 
+// The Gram pass needs the slots but not the flags: it runs on a companion stream of the
+// caller's (same CU mask) beside the flags pass, and the caller's stream waits for both.
+static int g_s3_prep_split = 0;  // measured: 309.5 (on) vs 319.8 M ex/s (off)
+OMLDM_API void omldm_scan3_set_prep_split(int v) { g_s3_prep_split = v; }
+namespace {
+struct S3Side {
+  hipStream_t side;
+  hipEvent_t fork, join;
+};
+std::mutex g_s3_side_mu;
+std::unordered_map<hipStream_t, S3Side> g_s3_side;
+
+S3Side* s3_side(hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_s3_side_mu);
+  auto it = g_s3_side.find(st);
+  if (it != g_s3_side.end()) return &it->second;
+  S3Side sd{};
+  uint32_t mask[32] = {};
+  const bool masked = st != nullptr && hipExtStreamGetCUMask(st, 32, mask) == hipSuccess;
+  if (!(masked && hipExtStreamCreateWithCUMask(&sd.side, 32, mask) == hipSuccess) &&
+      hipStreamCreateWithFlags(&sd.side, hipStreamNonBlocking) != hipSuccess)
+    return nullptr;
+  if (hipEventCreateWithFlags(&sd.fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&sd.join, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  return &g_s3_side.emplace(st, sd).first->second;
+}
+}  // namespace
+
 // Passes 1-3 (model-independent): slots, flags, Grams. `src` is the tokens (hashed = 0),
 // row-major int32 field-aware slots (1) or the compact int16 slots (2). span: slots per
 // field (0: (dim − dn − 1) / dc, the raw-token hashing's; the compact wire's cat_span
@@ -1154,6 +1207,13 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   hipLaunchKernelGGL(s3_slots_kernel, dim3((B + 255) / 256), dim3(256), 0, st, src, B, dc, dn,
                      span, hashed, cbase, W.slotsT);
   hipMemsetAsync(W.lidcount, 0, sizeof(int) * S, st);
+  S3Side* sd = g_s3_prep_split ? s3_side(st) : nullptr;
+  hipStream_t gst = st;  // the Gram pass's stream
+  if (sd) {
+    hipEventRecord(sd->fork, st);
+    hipStreamWaitEvent(sd->side, sd->fork, 0);
+    gst = sd->side;
+  }
   hipLaunchKernelGGL(s3_flags_kernel, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
                      W.meta, W.lidcount);
   const int nchs = (R + s3::CH - 1) / s3::CH;
@@ -1161,17 +1221,21 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   const float kadd = (rule != kSeqLogistic && variant == 2) ? 0.5f / C : 0.f;
   if (g_s3_gram_valu) {
     if (s3_kn(dn, bias) == 16)
-      hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
+      hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT, dc,
                          num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
     else
-      hipLaunchKernelGGL(s3_gram_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT, dc,
+      hipLaunchKernelGGL(s3_gram_kernel<32>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT, dc,
                          num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
   } else if (s3_kn(dn, bias) == 16) {
-    hipLaunchKernelGGL(s3_gram_mfma_kernel<16>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT,
+    hipLaunchKernelGGL(s3_gram_mfma_kernel<16>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT,
                        dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
   } else {
-    hipLaunchKernelGGL(s3_gram_mfma_kernel<32>, dim3(nchs, S_act), dim3(256), 0, st, W.slotsT,
+    hipLaunchKernelGGL(s3_gram_mfma_kernel<32>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT,
                        dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+  }
+  if (sd) {
+    hipEventRecord(sd->join, gst);
+    hipStreamWaitEvent(st, sd->join, 0);
   }
   return (int)hipGetLastError();
 }
@@ -1207,7 +1271,7 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
   // the combine adds straight into it (a memset beside the prep kernels took 15-20 us)
   if (!(flags & 1)) hipMemsetAsync(dacc, 0, sizeof(float) * (size_t)dim, st);
   const int ncomb = g_s3_comb;
-  const S3Comb cb{W.gran, epoch, S_act, dacc, inv_p};
+  const S3Comb cb{W.lidcount, W.gran, epoch, S_act, dacc, inv_p};
   int e;
   if (kn == 16) {
     e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)

@@ -432,6 +432,10 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
     32-bit category tokens, (``hashed``) int32 field-aware signed slots, or (``batch.span``
     > 0) the compact int16 field-aware slots of the engine's wire, row-major."""
     h = native.hip()
+    if "OMLDM_S3_GRAM_VALU" in os.environ:  # A/B: pass 3 on the VALU reference kernel
+        h.omldm_scan3_set_gram_valu(int(os.environ["OMLDM_S3_GRAM_VALU"]))
+    if "OMLDM_S3_PREP_SPLIT" in os.environ:  # A/B: 0 = flags and Grams on one stream
+        h.omldm_scan3_set_prep_split(int(os.environ["OMLDM_S3_PREP_SPLIT"]))
     dev = batch.y.device
     span = _s3_span(batch, dim)
     mode = _s3_mode(batch, hashed)

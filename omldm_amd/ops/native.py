@@ -76,6 +76,7 @@ HIP_SIGS = [
     ("omldm_scan3_run", i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, f32,
                               f32, f32, f32, i32, i64, vp, i32, i32, i32, u32, vp]),
     ("omldm_scan3_set_comb", None, [i32]),
+    ("omldm_scan3_set_prep_split", None, [i32]),
     ("omldm_scan3_get_comb", i32, []),
     ("omldm_scan3_comb_err", i32, []),
     ("omldm_scan3_part_bounds", i32, [i32, i32, i32, i64, i32, i32, vp]),
@@ -84,6 +85,7 @@ HIP_SIGS = [
     ("omldm_scale", i32, [vp, vp, i32, i32, i32, vp, vp, C.c_double, vp, vp, vp]),
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
     ("omldm_pull_copy", i32, [vp, vp, i64, i32, vp]),
+    ("omldm_pull_copy_set_wt", None, [i32]),
     ("omldm_h2d_async", i32, [vp, vp, i64, vp]),
     ("omldm_gram_update", i32, [vp, vp, i32, i32, vp, i32, vp, vp, vp]),
     ("omldm_gram_update_poly2", i32, [vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp]),

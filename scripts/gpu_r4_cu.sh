@@ -3,7 +3,7 @@
 # and the headline bench with / without CUs kept for the scan (trace of the timed loop)
 mkdir -p gpurun_out/r4
 timeout -k 10 300 python -u -m pytest tests/test_scan3.py -x -q --timeout 200 --timeout-method thread 2>&1 | tail -2 || exit 3
-timeout -k 10 120 python scripts/cumask_probe.py || exit 4
+PYTHONPATH=. timeout -k 10 120 python scripts/cumask_probe.py || exit 4
 b() {  # name, args
   n=$1; shift
   timeout -k 10 240 python bench.py --engine-e2e 0 --engine-latency 0 "$@" > gpurun_out/r4/bcu_$n.json 2> gpurun_out/r4/bcu_$n.err || return 1
