@@ -18,3 +18,9 @@ b wt_k0b --scan-cus 0 || exit 9
 b pl_k0b --scan-cus 0 --pull-wt 0 || exit 10
 b wt_k0_i8 --scan-cus 0 --ingest-cus 8 || exit 11
 b wt_k0_s4 --scan-cus 0 --slots 4 || exit 12
+for f in dib json; do
+  timeout -k 10 240 python bench/engine_e2e.py --records 4000000 --batch 131072 --format $f > gpurun_out/r4/e2e_$f.json 2> gpurun_out/r4/e2e_$f.err || exit 13
+  python -c "
+import json; d=json.loads(open('gpurun_out/r4/e2e_$f.json').read().strip().splitlines()[-1])
+st=d.get('stages_ms',{}); print('$f', d['value'], d.get('record_bytes'), d.get('wall_s'), {k: round(v['host_ms']/max(1,v['calls']),2) for k,v in st.items() if v.get('host_ms',0)>1})"
+done
