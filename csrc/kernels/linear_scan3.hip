@@ -138,16 +138,17 @@ __global__ __launch_bounds__(256) void s3_slots_kernel(const void* __restrict__ 
 // ------------------------------------------------------------------ pass 2: flags
 // One workgroup per (field, spoke): every present occurrence of the field in the spoke's
 // rows is inserted into an LDS hash table keyed by its slot, which keeps the slot's first
-// and last row (one packed word, min/max by compare-and-swap). A slot whose first and
-// last occurrence are two or more chunks apart gets a table id (LDS counter, then a block
-// base from the spoke's counter lidcount[s], zeroed before the launch); every occurrence
-// gets its meta word: F_TG (the margin reads the table: a table slot seen in an earlier
-// chunk), F_INIT (the table slot's first occurrence), F_SCAT (the slot recurs ≥ 2 chunks
-// later), the sign and the table id; 0 for absent occurrences. No sort: the table ids
-// only need to be unique within the spoke.
+// and last row (LDS atomic min / max: a compare-and-swap loop on one packed word retried
+// under contention — thousands of rows of a low-cardinality field on one entry). A slot
+// whose first and last occurrence are two or more chunks apart gets a table id (one LDS
+// add per wave, then a block base from the spoke's counter lidcount[s], zeroed before the
+// launch); every occurrence gets its meta word: F_TG (the margin reads the table: a table
+// slot seen in an earlier chunk), F_INIT (the table slot's first occurrence), F_SCAT (the
+// slot recurs ≥ 2 chunks later), the sign and the table id; 0 for absent occurrences. No
+// sort: the table ids only need to be unique within the spoke.
 namespace s3 {
 constexpr int FT = 1024;                   // flags threads
-constexpr int HCAP = 16384;                // hash entries (≤ 8192 distinct slots: load ≤ ½)
+constexpr int HCAP = 12288;                // hash entries (≤ 8192 distinct slots: load ≤ 2/3)
 constexpr int RPT = RMAX / FT;             // rows per thread (8)
 }  // namespace s3
 
@@ -155,16 +156,18 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
                                                           int R, uint32_t* __restrict__ meta,
                                                           int* __restrict__ lidcount) {
   __shared__ int hkey[s3::HCAP];        // slot, −1 empty; after the inserts: local table id
-  __shared__ uint32_t hrow[s3::HCAP];   // first row << 16 | last row
+  __shared__ uint32_t hfirst[s3::HCAP];  // first row (atomic min)
+  __shared__ uint32_t hlast[s3::HCAP];   // last row (atomic max)
   __shared__ int s_cnt, s_base;
-  const int f = blockIdx.x, s = blockIdx.y, tid = threadIdx.x;
+  const int f = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
   int t0, t1;
   spoke_rows(s, R, B, t0, t1);
   const int n = t1 - t0;
   if (n <= 0) return;
   for (int i = tid; i < s3::HCAP; i += s3::FT) {
     hkey[i] = -1;
-    hrow[i] = 0xFFFF0000u;
+    hfirst[i] = 0xFFFFFFFFu;
+    hlast[i] = 0u;
   }
   if (tid == 0) s_cnt = 0;
   __syncthreads();
@@ -181,38 +184,37 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
     if (v[q] == -1) continue;
     const int i = tid + q * s3::FT;
     const int key = v[q] & 0x7fffffff;
-    uint32_t at = ((uint32_t)key * 0x9E3779B1u) >> (32 - 14);
-    for (int probe = 0; probe < s3::HCAP; ++probe) {  // bounded: load ≤ ½
+    uint32_t at = __umulhi((uint32_t)key * 0x9E3779B1u, (uint32_t)s3::HCAP);
+    for (int probe = 0; probe < s3::HCAP; ++probe) {  // bounded: load ≤ 2/3
       const int prev = atomicCAS(&hkey[at], -1, key);
       if (prev == -1 || prev == key) break;
-      at = (at + 1) & (s3::HCAP - 1);
+      at = at + 1 == (uint32_t)s3::HCAP ? 0u : at + 1;
     }
     h[q] = (int)at;
-    uint32_t old = hrow[at];
-    while (true) {
-      const uint32_t fr = min(old >> 16, (uint32_t)i), lr = max(old & 0xFFFFu, (uint32_t)i);
-      const uint32_t nw = (fr << 16) | lr;
-      if (nw == old) break;
-      const uint32_t got = atomicCAS(&hrow[at], old, nw);
-      if (got == old) break;
-      old = got;
-    }
+    atomicMin(&hfirst[at], (uint32_t)i);
+    atomicMax(&hlast[at], (uint32_t)i);
   }
   __syncthreads();
-  // table ids: the first occurrence of every table slot takes one
-  int mine = 0;
+  // table ids: the first occurrence of every table slot takes one (one LDS add per wave)
   int lloc[s3::RPT];
 #pragma unroll
   for (int q = 0; q < s3::RPT; ++q) {
-    lloc[q] = -1;
-    if (h[q] < 0) continue;
     const int i = tid + q * s3::FT;
-    const uint32_t pr = hrow[h[q]];
-    const int first = (int)(pr >> 16), last = (int)(pr & 0xFFFFu);
-    if (i == first && (last >> 6) - (first >> 6) >= 2) {
-      lloc[q] = atomicAdd(&s_cnt, 1);
-      ++mine;
+    bool take = false;
+    if (h[q] >= 0) {
+      const int first = (int)hfirst[h[q]], last = (int)hlast[h[q]];
+      take = i == first && (last >> 6) - (first >> 6) >= 2;
     }
+    const unsigned long long mask = __ballot(take);
+    int wbase = 0;
+    if (mask) {
+      const int leader = __ffsll((long long)mask) - 1;
+      if (lane == leader) wbase = atomicAdd(&s_cnt, __popcll(mask));
+      wbase = __shfl(wbase, leader);
+    }
+    const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    lloc[q] = take ? wbase + rank : -1;
   }
   __syncthreads();
   if (tid == 0) s_base = atomicAdd(&lidcount[s], s_cnt);
@@ -228,8 +230,7 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
     if (i >= n) continue;
     uint32_t m = 0u;
     if (h[q] >= 0) {
-      const uint32_t pr = hrow[h[q]];
-      const int first = (int)(pr >> 16), last = (int)(pr & 0xFFFFu);
+      const int first = (int)hfirst[h[q]], last = (int)hlast[h[q]];
       const int ch = i >> 6;
       m = v[q] < 0 ? s3::F_SIGN : 0u;
       if ((last >> 6) - (first >> 6) >= 2) {
@@ -1079,7 +1080,7 @@ int s3_sact(int B, int R, int S) {
   return sact < S ? (int)sact : S;
 }
 int s3_kn(int dn, int bias) { return dn + (bias ? 1 : 0) <= 16 ? 16 : 32; }
-constexpr size_t kFlagsLds = (size_t)s3::HCAP * 8;
+constexpr size_t kFlagsLds = (size_t)s3::HCAP * 12;
 }  // namespace
 
 static int g_s3_cap_override = -1;  // tests: a small LDS table forces the global spill path
