@@ -159,7 +159,7 @@ def cpu_baseline() -> dict | None:
         return None
 
 
-def engine_e2e_rate(records: int, batch: int = 65536, fmt: str = "json") -> dict:
+def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dict:
     """Records/s of the training stream through the whole engine (rank 0, one GPU): JSON
     DataInstance records in a file topic → pinned staging → GPU parse + feature hashing →
     holdout routing → Synchronous round of a linear SVM (fp32, the job's default spokes)
@@ -256,7 +256,7 @@ def main(argv=None) -> int:
     ap.add_argument("--ref", default="auto", choices=["auto", "on", "off"],
                     help="CPU reference-semantics accuracy on the same stream (rank 0)")
     ap.add_argument("--ref-max-examples", type=float, default=6e7)
-    ap.add_argument("--engine-e2e", type=int, default=524288,
+    ap.add_argument("--engine-e2e", type=int, default=1048576,
                     help="JSON records timed through the whole engine (rank 0; 0 = skip)")
     ap.add_argument("--engine-latency", type=int, default=300,
                     help="forecasting records timed through the engine (rank 0; 0 = skip)")

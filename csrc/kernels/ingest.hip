@@ -79,6 +79,40 @@ __global__ __launch_bounds__(256) void pull_copy_u_kernel(const u32x4* __restric
   for (; i < n16; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
 }
 
+// Several (host src → device dst, bytes) segments in one launch: blockIdx.y = segment
+// (the engine's staging slot is one region per partition, plus the record offsets — a
+// launch per segment cost the staging thread a HIP call each). src / dst 16-B aligned; a
+// segment's last partial vector is copied bytewise by block 0.
+struct PullSegs {
+  static constexpr int kMax = 64;
+  const unsigned char* src[kMax];
+  unsigned char* dst[kMax];
+  long long n[kMax];
+};
+
+__global__ __launch_bounds__(256) void pull_copy_segs_kernel(PullSegs d) {
+  const int sg = blockIdx.y;
+  const u32x4* src = reinterpret_cast<const u32x4*>(d.src[sg]);
+  u32x4* dst = reinterpret_cast<u32x4*>(d.dst[sg]);
+  const long long n = d.n[sg], n16 = n >> 4;
+  const long long stride = (long long)gridDim.x * 256;
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u32x4 a = __builtin_nontemporal_load(src + i);
+    const u32x4 b = __builtin_nontemporal_load(src + i + stride);
+    const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+    const u32x4 e = __builtin_nontemporal_load(src + i + 3 * stride);
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = e;
+  }
+  for (; i < n16; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
+  const int tail = (int)(n & 15);
+  if (blockIdx.x == 0 && (int)threadIdx.x < tail)
+    d.dst[sg][n16 * 16 + threadIdx.x] = d.src[sg][n16 * 16 + threadIdx.x];
+}
+
 __global__ void pull_tail_kernel(const unsigned char* __restrict__ src,
                                  unsigned char* __restrict__ dst, long long n) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -188,6 +222,35 @@ OMLDM_API int omldm_host_register(void* p, long long nbytes) {
 }
 
 // Copies nbytes from a pinned (device-mapped) host buffer to device memory by kernel.
+// nseg (host src, device dst, bytes) segments in one launch (seg = 3 int64 each), about
+// `blocks` workgroups in all. Host sources are mapped to their device addresses here.
+OMLDM_API int omldm_pull_copy_segs(const long long* seg, int nseg, int blocks, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (blocks <= 0) blocks = 128;
+  for (int base = 0; base < nseg; base += PullSegs::kMax) {
+    const int cnt = nseg - base < PullSegs::kMax ? nseg - base : PullSegs::kMax;
+    PullSegs d{};
+    long long big = 0;
+    for (int k = 0; k < cnt; ++k) {
+      const long long* q = seg + 3 * (base + k);
+      const void* src = reinterpret_cast<const void*>(q[0]);
+      void* alias = nullptr;
+      if (hipHostGetDevicePointer(&alias, const_cast<void*>(src), 0) == hipSuccess && alias)
+        src = alias;
+      if (((uintptr_t)src & 15) || (q[1] & 15)) return -1;
+      d.src[k] = static_cast<const unsigned char*>(src);
+      d.dst[k] = reinterpret_cast<unsigned char*>(q[1]);
+      d.n[k] = q[2];
+      big = q[2] > big ? q[2] : big;
+    }
+    if (!big) continue;
+    int per = blocks / cnt;
+    per = per < 1 ? 1 : per;
+    hipLaunchKernelGGL(pull_copy_segs_kernel, dim3(per, cnt), dim3(256), 0, st, d);
+  }
+  return (int)hipGetLastError();
+}
+
 // 1: the default pull copy stores write-through (pull_copy_wt_kernel)
 static int g_pull_wt = 1;
 OMLDM_API void omldm_pull_copy_set_wt(int v) { g_pull_wt = v; }

@@ -54,6 +54,7 @@ class TickBlock:
     segs: list | None = None
     dev_nbytes: int = 0
     doffs_t: torch.Tensor | None = None
+    ends_buf: np.ndarray | None = None  # native fill: the slot's record-end array
 
     @property
     def offs(self) -> np.ndarray:
@@ -124,6 +125,13 @@ class TickIngest:
         nthr = int(os.environ.get("OMLDM_READERS", "16"))
         self._readers = cf.ThreadPoolExecutor(min(nthr, nreg), thread_name_prefix="omldm-read") \
             if nreg > 1 else None
+        from omldm_amd.io.transport import FileBroker
+
+        self._fds: dict = {}  # (consumer, partition) → the partition log's descriptor
+        # file-log topics: one native call per block (OMLDM_NATIVE_FILL=0: the Python path)
+        self._native_fill = (os.environ.get("OMLDM_NATIVE_FILL", "1") != "0" and consumers
+                             and all(isinstance(c.broker, FileBroker) and hasattr(c, "read_plan")
+                                     for c in consumers))
 
     def _alloc(self, n: int, dtype) -> torch.Tensor:
         return torch.empty(max(1, n), dtype=dtype, pin_memory=self.pinned)
@@ -141,6 +149,8 @@ class TickIngest:
             with tracing.range("ingest_slot_wait"):
                 blk.event.synchronize()  # the GPU has finished copying this slot's last use
             blk.event = None
+        if self._native_fill:
+            return self._fill_native(blk)
         # one region of the slot per (consumer, partition), sized from the observed
         # bytes per record; regions are read concurrently when the broker allows it
         jobs, pos = [], 0
@@ -198,6 +208,63 @@ class TickIngest:
         blk.offsets = [dict(c.offsets) for c in self.consumers]
         return blk
 
+    def _fill_native(self, blk: TickBlock) -> TickBlock:
+        """File-log topics: the whole block in one GIL-free call — the region reads on
+        native threads and the block's record index assembled there
+        (csrc/host/logio.cpp: omldm_fill_regions); same layout as the Python path."""
+        from omldm_amd.ops import native
+        from omldm_amd.utils import tracing
+
+        rows, owners, pos = [], [], 0
+        fds = self._fds
+        for ci, c in enumerate(self.consumers):
+            for p, share, cap in c.read_plan(self.batch):
+                cap = (cap + 15) & ~15
+                fd = fds.get((ci, p), -1)
+                if fd < 0:  # a partition log opened once it exists
+                    path = os.path.join(c.broker.root, c.topic, f"{p}.jsonl")
+                    if os.path.exists(path):
+                        fd = fds[(ci, p)] = c.broker._fd(path)
+                rows.append((fd, c.offsets[p], pos, cap, share if fd >= 0 else 0,
+                             int(share * c._avg_len * 1.02) + 4096))
+                owners.append((c, p))
+                pos += cap
+        if pos > blk.data.numel():
+            blk.data = self._alloc(int(pos * 1.25), torch.uint8)
+        nj = len(rows)
+        jobs = np.asarray(rows, dtype=np.int64).reshape(-1)
+        if self.stage and (blk.doffs_t is None or blk.doffs_t.numel() < blk.offs_t.numel()):
+            blk.doffs_t = self._alloc(blk.offs_t.numel(), torch.int64)
+        if blk.ends_buf is None or blk.ends_buf.shape[0] < blk.offs_t.numel():
+            blk.ends_buf = np.empty(blk.offs_t.numel(), dtype=np.int64)
+        res, segs, meta = (np.zeros(2 * max(1, nj), dtype=np.int64),
+                           np.zeros(3 * max(1, nj), dtype=np.int64), np.zeros(5, dtype=np.int64))
+        doffs = blk.doffs_t.numpy() if self.stage else None
+        with tracing.range("ingest_pread"):
+            n = native.host().omldm_fill_regions(
+                nj, jobs.ctypes.data, blk.data.data_ptr(), blk.offs_t.data_ptr(),
+                blk.ends_buf.ctypes.data, 0 if doffs is None else doffs.ctypes.data,
+                res.ctypes.data, segs.ctypes.data, meta.ctypes.data,
+                min(int(os.environ.get("OMLDM_READERS", "16")), max(1, nj)))
+        if n < 0:
+            raise OSError(-int(n), "reading the topic logs")
+        for j, (c, p) in enumerate(owners):  # consumer positions + bytes-per-record estimate
+            k, used = int(res[2 * j]), int(res[2 * j + 1])
+            nxt = int(rows[j][1]) + used
+            c.offsets[p] = nxt
+            if k:
+                c._avg_len = 0.8 * c._avg_len + 0.2 * (used / k)
+            elif rows[j][0] >= 0 and c.broker.end_offset(c.topic, p) > nxt:
+                c._avg_len *= 2
+        n, end, dpos, nsegs, ngaps = (int(v) for v in meta)
+        blk.segs = [tuple(int(v) for v in segs[3 * i:3 * i + 3]) for i in range(nsegs)] \
+            if self.stage else None
+        blk.dev_nbytes = dpos if self.stage else 0
+        blk.ends = blk.ends_buf[:n] if ngaps else None
+        blk.n, blk.nbytes = n, end
+        blk.offsets = [dict(c.offsets) for c in self.consumers]
+        return blk
+
     def _finish(self, blk: TickBlock) -> TickBlock:
         if self.stage and blk.n:
             from omldm_amd.utils import tracing
@@ -207,7 +274,7 @@ class TickIngest:
         return blk
 
     def _to_device(self, blk: TickBlock) -> None:
-        from omldm_amd.ops.ingest import pull_copy
+        from omldm_amd.ops.ingest import pull_copy_segs
 
         n = blk.n
         nbytes = blk.dev_nbytes if blk.segs is not None else blk.nbytes
@@ -234,11 +301,11 @@ class TickIngest:
                     for h, d, ln in segs:
                         blk.d_raw[d:d + ln].copy_(blk.data[h:h + ln], non_blocking=True)
                     blk.d_offs[:n + 1].copy_(offs_src[:n + 1], non_blocking=True)
-            else:
-                for h, d, ln in segs:
-                    pull_copy(blk.d_raw[d:d + ln], blk.data[h:h + ln], self.copy_blocks,
-                              cs.cuda_stream)
-                pull_copy(blk.d_offs, offs_src[:n + 1], self.copy_blocks, cs.cuda_stream)
+            else:  # the regions and the offsets in one launch
+                hb, db = blk.data.data_ptr(), blk.d_raw.data_ptr()
+                pull_copy_segs([(hb + h, db + d, ln) for h, d, ln in segs] +
+                               [(offs_src.data_ptr(), blk.d_offs.data_ptr(), 8 * (n + 1))],
+                               self.copy_blocks, cs.cuda_stream)
             self.h2d_timer.stop(cs, sum(ln for _, _, ln in segs) + 8 * (n + 1))
             blk.parsed = None
             if self.space is not None:

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
 import torch
 
 from omldm_amd.ops import native
@@ -143,6 +144,17 @@ def pull_copy(dst: torch.Tensor, src: torch.Tensor, blocks: int = 16, stream=Non
     native.check(native.hip().omldm_pull_copy(src.data_ptr(), dst.data_ptr(),
                                               src.numel() * src.element_size(), blocks, s),
                  "omldm_pull_copy")
+
+
+def pull_copy_segs(segs: list, blocks: int = 128, stream=None) -> None:
+    """One launch for several (host src ptr, device dst ptr, bytes) copies
+    (csrc/kernels/ingest.hip: pull_copy_segs_kernel); pointers 16-B aligned."""
+    if not segs:
+        return
+    s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    arr = np.asarray(segs, dtype=np.int64).reshape(-1)
+    native.check(native.hip().omldm_pull_copy_segs(arr.ctypes.data, len(segs), blocks, s),
+                 "omldm_pull_copy_segs")
 
 
 def json_parse(dbuf, doffs, n: int, space, num, cat, y, op, counts, stream) -> None:

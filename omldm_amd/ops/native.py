@@ -86,6 +86,7 @@ HIP_SIGS = [
     ("omldm_poly", i32, [vp, i32, i32, vp, i32, i32, vp, vp]),
     ("omldm_pull_copy", i32, [vp, vp, i64, i32, vp]),
     ("omldm_pull_copy_set_wt", None, [i32]),
+    ("omldm_pull_copy_segs", i32, [vp, i32, i32, vp]),
     ("omldm_h2d_async", i32, [vp, vp, i64, vp]),
     ("omldm_gram_update", i32, [vp, vp, i32, i32, vp, i32, vp, vp, vp]),
     ("omldm_gram_update_poly2", i32, [vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp]),
@@ -164,6 +165,7 @@ HOST_SIGS = [
     ("omldm_index_lines", i64, [vp, i64, i64, vp]),
     ("omldm_format_predictions", i64, [vp, vp, vp, i64, i32, vp, vp, i64, vp]),
     ("omldm_read_log", i64, [i32, i64, vp, i64, i64, vp, vp, i64]),
+    ("omldm_fill_regions", i64, [i32, vp, vp, vp, vp, vp, vp, vp, vp, i32]),
     ("omldm_codec_available", i32, [i32]),
     ("omldm_codec_decompress", i32, [i32, C.c_char_p, i64, vp, vp]),
     ("omldm_codec_compress", i32, [i32, C.c_char_p, i64, i32, vp, vp]),

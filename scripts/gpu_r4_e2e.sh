@@ -1,13 +1,15 @@
 #!/bin/bash
+# engine end-to-end (DIB / JSON topics): partitions (concurrent region reads) and tick size
 mkdir -p gpurun_out/r4
-for b in 65536 131072; do
-  timeout -k 10 240 python bench/engine_e2e.py --records 1500000 --batch $b > gpurun_out/r4/e2e_$b.json 2> gpurun_out/r4/e2e_$b.err || exit 5
+e() {  # name, args
+  n=$1; shift
+  timeout -k 10 240 python bench/engine_e2e.py "$@" > gpurun_out/r4/e2e_$n.json 2> gpurun_out/r4/e2e_$n.err || return 1
   python -c "
-import json; d=json.loads(open('gpurun_out/r4/e2e_$b.json').read().strip().splitlines()[-1])
-print($b, d['value'], d['wall_s'], d['ticks_timed']); st=d['stages_ms']
-for k,v in sorted(st.items(), key=lambda kv: -kv[1].get('total_ms',0))[:12]: print('  ', k, v)
-"
-done
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4/prof_e2e -o e2e -- python bench/engine_e2e.py --records 1000000 --batch 131072 > gpurun_out/r4/prof_e2e.log 2>&1 || exit 8
-f=$(find gpurun_out/r4/prof_e2e -name "*kernel_stats.csv" | head -1); [ -n "$f" ] && cp "$f" gpurun_out/r4/e2e_kernel_stats.csv && cut -c1-150 gpurun_out/r4/e2e_kernel_stats.csv | head -20
+import json; d=json.loads(open('gpurun_out/r4/e2e_$n.json').read().strip().splitlines()[-1])
+st=d.get('stages_ms',{}); print('$n', d['value'], d.get('wall_s'), d.get('ticks_timed'), {k: round(v['host_ms']/max(1,v['calls']),2) for k,v in st.items() if v.get('host_ms',0)>1})"
+}
+e dib8 --records 8000000 --batch 131072 --format dib --partitions 8 || exit 3
+e dib16 --records 8000000 --batch 131072 --format dib --partitions 16 || exit 4
+e dib32 --records 8000000 --batch 131072 --format dib --partitions 32 || exit 5
+e dib16b262 --records 8000000 --batch 262144 --format dib --partitions 16 || exit 6
+e json16 --records 4000000 --batch 131072 --format json --partitions 16 || exit 7

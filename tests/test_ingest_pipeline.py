@@ -112,3 +112,49 @@ def test_holdout_closed_forms():
             assert [nonheld_row(r, c) for r in range(len(keep))] == keep.tolist()
             assert [held_row(r, c) for r in range(len(hold))] == hold.tolist()
             assert HoldoutSet._held_before(c + B) - HoldoutSet._held_before(c) == len(hold)
+
+
+def test_native_block_fill_matches_python_path(tmp_path, monkeypatch):
+    """File-log topics fill a block in one native call (csrc/host/logio.cpp:
+    omldm_fill_regions): the same records, slot offsets, true record ends, device-packed
+    offsets, segments and consumer positions as the per-region Python path, block after
+    block (region gaps included: regions are sized with slack)."""
+    br = FileBroker(str(tmp_path))
+    br.create_topic("t", 5)
+    br.create_topic("f", 2)
+    recs = _records(1500, seed=4)
+    for i, r in enumerate(recs):
+        br.produce("t" if i % 4 else "f", r, partition=i % 5)
+    runs = {}
+    # one Python reader thread: its regions then update the bytes-per-record estimate in
+    # job order, as the native fill does (the slot layout of the next block depends on it)
+    monkeypatch.setenv("OMLDM_READERS", "1")
+    for native_fill in ("1", "0"):
+        monkeypatch.setenv("OMLDM_NATIVE_FILL", native_fill)
+        cons = [Consumer(br, "t"), Consumer(br, "f")]
+        ing = TickIngest(cons, batch_size=96, pinned=False, prefetch=False)
+        assert ing._native_fill == (native_fill == "1")
+        ing.stage = True  # the device-packing fields too (filled on the host)
+        out = []
+        for _ in range(100):
+            blk = ing._fill_block(ing._next_slot())
+            if blk.n == 0:
+                break
+            ends = None if blk.ends is None else blk.ends.copy()
+            out.append((blk.n, blk.nbytes, blk.offs.copy(), ends,
+                        blk.doffs_t.numpy()[: blk.n + 1].copy(), list(blk.segs),
+                        blk.dev_nbytes, [r for r in blk.raw()], blk.offsets))
+        ing.close()
+        runs[native_fill] = out
+    a, b = runs["1"], runs["0"]
+    assert len(a) == len(b) > 5
+    seen = 0
+    for x, y in zip(a, b):
+        assert x[0] == y[0] and x[1] == y[1] and x[6] == y[6] and x[8] == y[8]
+        assert np.array_equal(x[2], y[2]) and np.array_equal(x[4], y[4]) and x[5] == y[5]
+        assert (x[3] is None) == (y[3] is None)
+        if x[3] is not None:
+            assert np.array_equal(x[3], y[3])
+        assert x[7] == y[7]
+        seen += x[0]
+    assert seen == len(recs)

@@ -111,3 +111,25 @@ def test_gpu_parser_decodes_dib_like_the_json(cuda, field_aware):
         assert torch.equal(gb.cat.cpu()[k::2][ok], hb.cat[ok])
         assert torch.equal(torch.nan_to_num(gb.y.cpu()[k::2][ok], nan=-7.0),
                            torch.nan_to_num(hb.y[ok], nan=-7.0))
+
+
+@pytest.mark.gpu
+def test_gpu_pull_copy_segments_one_launch():
+    """Several pinned-host → HBM segments in one launch (csrc/kernels/ingest.hip:
+    pull_copy_segs_kernel): odd lengths (bytewise tails), the engine's slot layout."""
+    from omldm_amd.ops.ingest import pull_copy_segs
+
+    dev = torch.device("cuda", 0)
+    host = torch.randint(0, 256, (1 << 20,), dtype=torch.uint8).pin_memory()
+    out = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+    segs = [(0, 0, 1000), (4096, 1008, 77777), (200000, 90000, 16), (300000, 100000, 5),
+            (400016, 200000, 333331)]
+    pull_copy_segs([(host.data_ptr() + h, out.data_ptr() + d, n) for h, d, n in segs], 64)
+    torch.cuda.synchronize()
+    o = out.cpu()
+    for h, d, n in segs:
+        assert torch.equal(o[d:d + n], host[h:h + n])
+    untouched = torch.ones(1 << 20, dtype=torch.bool)
+    for h, d, n in segs:
+        untouched[d:d + n] = False
+    assert int(o[untouched].abs().sum()) == 0
