@@ -186,8 +186,9 @@ def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dic
             uniq = records_to_dib(uniq, sp.n_numerical, sp.n_discrete, sp.dc)
         else:
             uniq = [r.encode() for r in uniq]
+        total = records + 4 * batch  # the untimed Create / warmup ticks read some first
         for p in range(parts):
-            recs = [uniq[i % len(uniq)] for i in range(p, records, parts)]
+            recs = [uniq[i % len(uniq)] for i in range(p, total, parts)]
             br.produce_block("trainingData", p, b"\n".join(recs) + b"\n")
         br.produce("requests", json.dumps({"id": 1, "request": "Create",
                                            "learner": {"name": "SVM"},
@@ -208,7 +209,7 @@ def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dic
         torch.cuda.synchronize(dev)
         r0 = job.counters["records"]
         t0 = time.perf_counter()
-        while job.counters["records"] + job.counters["invalid"] < records:
+        while job.counters["records"] + job.counters["invalid"] < r0 + records:
             job.tick()
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
