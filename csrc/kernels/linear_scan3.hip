@@ -504,6 +504,7 @@ struct S3Cand {
 __device__ unsigned long long* g_s3_stamps;
 __device__ int g_s3_debug;  // diagnostics: 1 = every gather reads w[0] (latency experiment)
 __device__ int g_s3_comb_err;  // a combiner gave up waiting for its spoke (bounded spin)
+__device__ int g_s3_dense_order = 0;  // helpers' dense column ownership (see s3_scan_kernel)
 
 // The in-launch combine (Guideline 16, R2 "the data is the flag"): the scanner stores row
 // t's c as one 8-B granule {epoch << 32 | bits(c)} with a relaxed agent-scope atomic store
@@ -752,11 +753,17 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   // ------------------------------------------------------------------- helpers
   // helper q owns categorical fields f ≡ q and dense columns j ≡ q (mod NHA); lane r = row
   const int q = wave - 1, r = lane;
+  const int swave = g_s3_debug >= 16 ? g_s3_debug - 16 : 1;  // the stamped helper wave
+  // dense column ownership: j ≡ q (mod NHA) (order 0), or in the reverse order of the
+  // fields (order 1: the helpers that own a third categorical field do not also own a
+  // second dense column)
+  const int qd = g_s3_dense_order ? s3::NHA - 1 - q : q;
+  const int kd = dn + (p.bias ? 1 : 0);  // real dense columns (KN pads them to 16 / 32)
   const int hl = q * 64 + lane;
   float wn[s3::NJ], w0[s3::NJ];  // running dense weights of this wave's columns, round start
 #pragma unroll
   for (int i = 0; i < s3::NJ; ++i) {
-    const int j = q + s3::NHA * i;
+    const int j = qd + s3::NHA * i;
     w0[i] = (j < KN) ? (j < dn ? w[j] : ((p.bias && j == dn) ? w[dim - 1] : 0.f)) : 0.f;
     wn[i] = w0[i];
   }
@@ -812,7 +819,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   auto load_dense = [&](int ch, float* xd) {
 #pragma unroll
     for (int i = 0; i < NJK; ++i) {
-      const int j = q + s3::NHA * i;
+      const int j = qd + s3::NHA * i;
       const bool ok = j < KN && ch >= 0 && ch < nch;
       const int jc = j < KN ? j : 0, cc = max(0, min(ch, nch - 1));
       const float v = chunk_prep(cc)[2 * s3::MAT + s3::CH + jc * s3::CH + r];
@@ -826,13 +833,13 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   auto body = [&](auto spill_tag, int k, Set& CUR, Set& NXT) {
     constexpr bool SPILL = decltype(spill_tag)::value;
     const int cn = k + 1, ks = k - 1;
-    if (wave == 1) stamp(7);
+    if (wave == swave) stamp(7);
     // ---- issue the NXT set (chunk cn + 1) but its gathers
     load_words(cn + 1, NXT);
     issue_staging(cn + 1, NXT);
     load_dense(ks + 1, NXT.xs);
     load_dense(cn + 1, NXT.xc);
-    if (wave == 1) stamp(3);
+    if (wave == swave) stamp(3);
     // ---- scatter chunk ks into the table and its dense update: one LDS atomic add per
     // occurrence (ds_add_f32; lanes on one entry are combined by the LDS unit inside the
     // instruction — a software loop over the ranks of equal slots cost 13 K cycles per
@@ -859,18 +866,41 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       }
 #pragma unroll
       for (int i = 0; i < NJK; ++i) {
-        const int j = q + s3::NHA * i;
-        if (j < KN) wn[i] += wave_sum(cv * CUR.xs[i]);
+        const int j = qd + s3::NHA * i;
+        if (j < kd) wn[i] += wave_sum(cv * CUR.xs[i]);  // (padding columns are all zero)
       }
     }
-    if (wave == 1) stamp(6);
+    if (wave == swave) stamp(6);
     // ---- base margins of chunk cn: table entries (chunks ≤ k − 1 applied), w, dense
     if (cn < nch) {
       float base = 0.f;
 #pragma unroll
       for (int i = 0; i < NJK; ++i) base = fmaf(CUR.xc[i], wn[i], base);
+      if constexpr (!SPILL) {
+        // every field's table reads first, then the first-occurrence writes: within a
+        // chunk a table entry is either read (the slot was seen in an earlier chunk) or
+        // written (its first occurrence), never both, and fields have disjoint slots — so
+        // the reads need not wait for the previous field's write
+        float tv[s3::NF];
 #pragma unroll
-      for (int i = 0; i < s3::NF; ++i) {
+        for (int i = 0; i < s3::NF; ++i) {
+          const uint32_t m = CUR.cm[i];
+          const bool tg = CUR.cs[i] != -1 && (m & s3::F_TG);
+          tv[i] = 0.f;
+          if (tg) tv[i] = tab[(int)(m >> s3::LID_SHIFT)];
+        }
+#pragma unroll
+        for (int i = 0; i < s3::NF; ++i) {
+          const uint32_t m = CUR.cm[i];
+          const bool here = CUR.cs[i] != -1;
+          const bool tg = here && (m & s3::F_TG), init = here && !tg && (m & s3::F_INIT);
+          const float val = tg ? tv[i] : CUR.g[i];
+          if (init) tab[(int)(m >> s3::LID_SHIFT)] = val;
+          if (here) base += (m & s3::F_SIGN) ? -val : val;
+        }
+      }
+#pragma unroll
+      for (int i = 0; SPILL && i < s3::NF; ++i) {
         const uint32_t m = CUR.cm[i];
         const bool here = CUR.cs[i] != -1;
         const int lid = (int)(m >> s3::LID_SHIFT);
@@ -898,7 +928,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       }
       sm.part[cn & 1][q][r] = base;
     }
-    if (wave == 1) stamp(4);
+    if (wave == swave) stamp(4);
     // ---- aG_{cn} → G[cn & 1], aX1_{cn+1} → X1[(cn+1) & 1]
 #pragma unroll
     for (int u = 0; u < NV4; ++u) {
@@ -917,7 +947,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       p2[i] = p1[i];
       p1[i] = CUR.cm[i];
     }
-    if (wave == 1) stamp(5);
+    if (wave == swave) stamp(5);
     __syncthreads();
   };
 
@@ -940,12 +970,12 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       if (k + 1 <= nch) body(S3Tag<true>{}, k + 1, Bs, A);
     }
   }
-  if (stamps && lane == 0 && wave == 1)
+  if (stamps && lane == 0 && wave == swave)
     for (int k = 2; k < 8; ++k) atomicAdd(&stamps[(size_t)s * 16 + k], st_acc[k]);
   // round end: this wave's dense deltas
 #pragma unroll
   for (int i = 0; i < s3::NJ; ++i) {
-    const int j = q + s3::NHA * i;
+    const int j = qd + s3::NHA * i;
     if (lane == 0 && j < KN) wsd[(size_t)s * s3::DS + j] = wn[i] - w0[i];
   }
   if (q == 0 && lane >= KN && lane < s3::DS) wsd[(size_t)s * s3::DS + lane] = 0.f;
@@ -1305,6 +1335,10 @@ OMLDM_API int omldm_scan3_part_bounds(int dim, int dn, int dc, long long span_in
   lohi[0] = part == 0 ? 0 : (long long)dim + 2;
   lohi[1] = (long long)dim + 2;
   return 0;
+}
+
+OMLDM_API int omldm_scan3_dense_order(int v) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s3_dense_order), &v, sizeof(v));
 }
 
 OMLDM_API int omldm_scan3_debug(int v) {

@@ -71,3 +71,32 @@ lib.omldm_scan3_debug(0)
 m = st.double().mean(0)
 print(json.dumps({"gathers_hit_w0": {names[k]: round(float(m[k]) / nch, 1)
                                      for k in range(10)}}), flush=True)
+
+# per helper wave (g_s3_debug = 16 + wave selects the stamped helper): which helper sets
+# the chunk period (waves 4 and 8 share the scanner's SIMD)
+per = {}
+for wv in range(1, 12):
+    lib.omldm_scan3_debug(16 + wv)
+    st.zero_()
+    lib.omldm_scan3_stamps(st.data_ptr())
+    L.linear_seq_round(w, b, R, S, dacc, rule, 1.0 / S, cum=cum)
+    torch.cuda.synchronize()
+    lib.omldm_scan3_stamps(None)
+    m = st.double().mean(0)
+    per[wv] = {names[k]: round(float(m[k]) / nch) for k in range(2, 8)}
+lib.omldm_scan3_debug(0)
+print(json.dumps({"helper_waves": per}), flush=True)
+if os.environ.get("PROBE_DENSE_ORDERS"):
+    lib.omldm_scan3_dense_order.argtypes = [ctypes.c_int]
+    for order in (0, 1):
+        lib.omldm_scan3_dense_order(order)
+        torch.cuda.synchronize()
+        ev[0].record()
+        for _ in range(n):
+            L.linear_seq_round(w, b, R, S, dacc, rule, 1.0 / S, cum=cum)
+            L.linear_apply(w, None, dacc)
+        ev[1].record()
+        torch.cuda.synchronize()
+        print(json.dumps({"dense_order": order, "run_ms": round(ev[0].elapsed_time(ev[1]) / n, 4)}),
+              flush=True)
+    lib.omldm_scan3_dense_order(0)
