@@ -484,6 +484,7 @@ struct S3Smem {
   alignas(16) float X1[2][s3::CH][s3::GS];  // aX1_{k+1} (read by the scanner in chunk k)
   float part[2][s3::NHA][s3::CH];           // base-margin partials per working helper
   float cb[2][s3::CH];                      // c of the chunk, by parity
+  int last;                                 // s3_scan_arrive: this block arrived last
 };
 // + dynamic LDS: the slot table, `cap` floats
 
@@ -524,6 +525,11 @@ struct S3Comb {
   int S_act;                 // blocks [0, S_act) scan, the rest combine
   float* dacc;
   float inv_p;
+  // the round's tail (dense columns, scalars, statistics) run by the last scan block to
+  // finish: an epoch-tagged arrival word {epoch, count} (never zeroed: a word of an older
+  // epoch restarts at 1), null → s3_tail_kernel / the scatter grid's extra row instead
+  unsigned long long* arrive;
+  double* cum;
 };
 namespace s3 {
 constexpr int CHASH = 8192;          // combiner LDS hash entries (keys in G, sums in X1)
@@ -608,6 +614,46 @@ __device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int d
   }
 }
 
+// Forward: the tail body (defined with the combine pass below).
+__device__ void s3_dense_body(const float* __restrict__ ws, const float* __restrict__ wsd,
+                              int S_act, int dn, int dim, int bias, float inv_p,
+                              float* __restrict__ dacc, double* __restrict__ cum);
+
+// End of a scan workgroup (every wave comes here): with cb.arrive set, the block's spoke
+// statistics / dense deltas are published (each wave drains its stores, the workgroup
+// meets, one lane releases at agent scope and counts the block in), and the block that
+// arrives last acquires and runs the round's tail (Guideline 16: release → counter,
+// last arriver → acquire → plain loads). Saves the tail kernel's launch after the scan.
+// (the flag lives in S3Smem: the kernel's static + dynamic LDS is exactly 160 KB)
+__device__ __forceinline__ void s3_scan_arrive(const S3Comb& cb, const float* __restrict__ ws,
+                                               const float* __restrict__ wsd, int dn, int dim,
+                                               const SeqParams& p, S3Smem& sm) {
+  if (cb.arrive == nullptr) return;
+  int& s_last = sm.last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s3_gu64* a = (s3_gu64*)cb.arrive;
+    unsigned long long old = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long nw;
+    do {
+      nw = (uint32_t)(old >> 32) == cb.epoch ? old + 1
+                                             : (((unsigned long long)cb.epoch << 32) | 1ull);
+    } while (!__hip_atomic_compare_exchange_weak(a, &old, nw, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    s_last = (int)(uint32_t)nw == cb.S_act;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (s_last)
+    s3_dense_body(ws, wsd, cb.S_act, dn, dim, p.bias, p.inv_p, cb.dacc, cb.cum);
+}
+
 template <int RULE, int KN>
 __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s3_scan_kernel(
     const int* __restrict__ slotsT, const uint32_t* __restrict__ meta, int dc, int dn,
@@ -629,6 +675,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   if (t0 >= t1) {
     if (tid < s3::WS) ws[(size_t)s * s3::WS + tid] = 0.f;
     if (tid < s3::DS) wsd[(size_t)s * s3::DS + tid] = 0.f;
+    s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
     return;
   }
   const int nch = (t1 - t0 + s3::CH - 1) / s3::CH;
@@ -747,6 +794,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       wr[6] = 0.f;
       wr[7] = 0.f;
     }
+    s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
     return;
   }
 
@@ -979,6 +1027,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     if (lane == 0 && j < KN) wsd[(size_t)s * s3::DS + j] = wn[i] - w0[i];
   }
   if (q == 0 && lane >= KN && lane < s3::DS) wsd[(size_t)s * s3::DS + lane] = 0.f;
+  s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
 }
 
 // ------------------------------------------------------------------ pass 5: combine
@@ -995,7 +1044,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
 __device__ void s3_dense_body(const float* __restrict__ ws,
                               const float* __restrict__ wsd, int S_act, int dn, int dim,
                               int bias, float inv_p, float* __restrict__ dacc,
-                              double* __restrict__ cum) {
+                              double* __restrict__ cum) {  // (blockDim ≥ 256; dn < 256)
   const int tid = threadIdx.x;
   for (int i = tid; i < dn; i += 256) {
     float v = 0.f;
@@ -1281,7 +1330,7 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
                               int S, float* dacc, int dim, double* cum, int rule, int variant,
                               float C, float eps, float lr, float inv_p, int bias,
                               long long span_in, void* const* ptrs, int part, int parts,
-                              int flags, unsigned epoch, void* stream) {
+                              int flags, unsigned epoch, void* arrive, void* stream) {
   if (epoch == 0u) return -2;
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
@@ -1302,7 +1351,9 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
   // the combine adds straight into it (a memset beside the prep kernels took 15-20 us)
   if (!(flags & 1)) hipMemsetAsync(dacc, 0, sizeof(float) * (size_t)dim, st);
   const int ncomb = g_s3_comb;
-  const S3Comb cb{W.lidcount, W.gran, epoch, S_act, dacc, inv_p};
+  // the tail in the scan's launch (last scan block) when the caller gave an arrival word
+  const S3Comb cb{W.lidcount, W.gran, epoch, S_act, dacc, inv_p,
+                  static_cast<unsigned long long*>(arrive), cum};
   int e;
   if (kn == 16) {
     e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
@@ -1316,13 +1367,15 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
   if (e) return e;
   (void)span;
   if (ncomb > 0) {  // the categorical slots were combined in the scan's launch
-    hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, W.ws, W.wsd, S_act, dn, dim,
-                       bias, inv_p, dacc, cum);
+    if (!arrive)
+      hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, W.ws, W.wsd, S_act, dn, dim,
+                         bias, inv_p, dacc, cum);
     return (int)hipGetLastError();
   }
   const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
   const int nblk = (n_rows + s3::SB - 1) / s3::SB;
-  hipLaunchKernelGGL(s3_scatter_kernel, dim3(nblk > 0 ? nblk : 1, dc + 1), dim3(256), 0, st,
+  hipLaunchKernelGGL(s3_scatter_kernel, dim3(nblk > 0 ? nblk : 1, dc + (arrive ? 0 : 1)),
+                     dim3(256), 0, st,
                      W.slotsT, W.gran, B, n_rows, inv_p, dacc, dc, W.ws, W.wsd, S_act, dn, dim,
                      bias, cum);
   return (int)hipGetLastError();

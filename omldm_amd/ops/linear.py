@@ -381,8 +381,8 @@ _S3_GRAN: dict = {}
 def _s3_granules(dev, n: int, stream: int) -> list:
     key = (str(dev), stream)
     g = _S3_GRAN.get(key)
-    if g is None or g[0].numel() < n:
-        t = torch.zeros(max(n, 1 << 17), dtype=torch.float32, device=dev)
+    if g is None or g[0].numel() < n + 2:  # + the round's arrival word (the last 8 bytes)
+        t = torch.zeros(max(n + 2, 1 << 17), dtype=torch.float32, device=dev)
         torch.cuda.synchronize(dev)  # zeroed before any stream's round reads it
         g = [t, 0]
         _S3_GRAN[key] = g
@@ -463,6 +463,8 @@ def scan3_part_bounds(dim: int, dn: int, dc: int, part: int, parts: int,
     return int(lh[0]), int(lh[1])
 
 
+_S3_TAIL_KERNEL = os.environ.get("OMLDM_S3_TAIL") == "kernel"
+
 # rounds run through the v3 scan in this process (tests: the engine's default path)
 SCAN3_ROUNDS = 0
 
@@ -499,11 +501,15 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
     # on different streams may scan the same prep concurrently
     ptrs, gran = _s3_run_ptrs(sp, w.device, native.stream_of(w))
     epoch = _s3_next_epoch(gran)
+    # the round's tail runs in the scan's launch (its last scan block) on an arrival word at
+    # the granule buffer's end (OMLDM_S3_TAIL=kernel: a separate kernel after the scan)
+    arrive = (None if _S3_TAIL_KERNEL else
+              gran[0].data_ptr() + (gran[0].numel() // 2 - 1) * 8)
     for k in range(parts):
         rc = h.omldm_scan3_run(ptr(w), num.shape[1], batch.dc, ptr(y), int(y.dtype == torch.int8),
                                batch.B, R, S, ptr(dacc), dim, ptr(cum), rule.rule, rule.variant,
                                rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), span, ptrs, k,
-                               parts, int(bool(dacc_zero)), epoch, native.stream_of(w))
+                               parts, int(bool(dacc_zero)), epoch, arrive, native.stream_of(w))
         check(rc, "omldm_scan3_run")
         if on_part is not None:
             on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts, span))

@@ -74,7 +74,7 @@ HIP_SIGS = [
     ("omldm_scan3_prepare", i32, [vp, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32,
                                   i32, f32, i64, i32, vp, vp]),
     ("omldm_scan3_run", i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, f32,
-                              f32, f32, f32, i32, i64, vp, i32, i32, i32, u32, vp]),
+                              f32, f32, f32, i32, i64, vp, i32, i32, i32, u32, vp, vp]),
     ("omldm_scan3_set_comb", None, [i32]),
     ("omldm_scan3_set_prep_split", None, [i32]),
     ("omldm_scan3_get_comb", i32, []),
