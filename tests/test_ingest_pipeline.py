@@ -158,3 +158,21 @@ def test_native_block_fill_matches_python_path(tmp_path, monkeypatch):
         assert x[7] == y[7]
         seen += x[0]
     assert seen == len(recs)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_index_lines_native_matches_python_on_random_blocks(seed):
+    """The SIMD record indexer (64 bytes per step, csrc/host/logio.cpp) against a Python
+    scan: random record lengths (1..300 bytes, so newlines fall anywhere in a 64-byte
+    step), a trailing partial record, record caps that stop mid-step."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(1, 300, size=2000)
+    parts = [bytes(rng.integers(0, 9, size=int(n)).astype(np.uint8) + 48) + b"\n" for n in lens]
+    blob = b"".join(parts) + b"partial"
+    buf = np.frombuffer(blob, dtype=np.uint8)
+    ends = [i + 1 for i, c in enumerate(blob) if c == 10]
+    for cap in (len(ends) + 5, len(ends), 1337, 1, 64):
+        offs = np.zeros(len(ends) + 2, dtype=np.int64)
+        n = native.host().omldm_index_lines(buf.ctypes.data, len(buf), cap, offs.ctypes.data)
+        want = ends[:cap]
+        assert n == len(want) and offs[0] == 0 and list(offs[1:n + 1]) == want
