@@ -245,6 +245,8 @@ def main(argv=None) -> int:
                     help="GPU clock settle before the warmup: dense matmuls for this long on "
                          "a scratch tensor (no model state; a fresh box's first process ran "
                          "~15%% slower without it)")
+    ap.add_argument("--ahead", type=int, default=2,
+                    help="batches copied (and prepped) ahead of the round (≤ slots − 1)")
     ap.add_argument("--host-ahead-wait", type=int, default=1,
                     help="the host waits for a staging slot's last round before its copy "
                          "(no device-side barrier in the copy stream)")
@@ -383,7 +385,8 @@ def main(argv=None) -> int:
             proto.round(dev[k % a.pool].batch)
             return
         slot = k % nslots
-        prefetch(k + 1)
+        if ahead == 1 and k + 1 < n_rounds:
+            prefetch(k + 1)
         if on_gpu and not (v3 and prep_stream is not None):
             # (with a prep made ahead the round waits on the prep's event, which follows the
             # copy: a second cross-stream wait cost the round's launch ≈ 7 µs per step)
@@ -391,6 +394,11 @@ def main(argv=None) -> int:
         proto.round(dev[slot].batch)
         if on_gpu:
             consumed[slot].record()
+        if ahead > 1 and k + ahead < n_rounds:
+            # the copy of batch k + ahead goes after this round is queued: the host may wait
+            # for round k + ahead − nslots (its slot) while the device already has round k
+            # (no copy of a batch past the last round: the final sync would wait for it)
+            prefetch(k + ahead)
 
     def step(k: int):
         if on_gpu:
@@ -419,7 +427,10 @@ def main(argv=None) -> int:
     if on_gpu:
         for e in consumed:
             e.record()
-    prefetch(0)
+    ahead = max(1, min(int(a.ahead), nslots - 1)) if a.ingest != "device" else 1
+    n_rounds = a.warmup + a.steps
+    for j in range(min(ahead, n_rounds)):
+        prefetch(j)
     for k in range(a.warmup):
         step(k)
     sync()
