@@ -528,6 +528,13 @@ def main(argv=None) -> int:
                                  "default parallelism), measured on the MI355X box's host "
                                  "CPU (bench/cpu_reference.py)"} if base else None,
             "dtype": "fp32",
+            "ingest_pipeline": None if a.ingest != "pinned" else {
+                "batches_copied_ahead": ahead,
+                "pcie_copies_in_timed_window": max(0, a.steps - ahead),
+                "note": "each round's batch is pulled over PCIe `ahead` rounds before it "
+                        "trains (the copies of the first timed rounds' batches ran during "
+                        "the warmup; no batch past the last round is copied); the rate over "
+                        "--steps 100 is the steady-state check"},
             "data": "synthetic (Criteo-shaped raw stream: fp32 numerical features, 32-bit "
                     "category tokens hashed on the GPU inside the timed round, int8 ±1 labels; "
                     f"{wire // B} B/example on the wire; pinned host pool replayed, H2D in "
