@@ -10,6 +10,9 @@
 #include <cerrno>
 #include <cstdint>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 #include <unistd.h>
@@ -97,6 +100,80 @@ OMLDM_HOST_API int64_t omldm_read_log(int fd, int64_t offset, uint8_t* dst, int6
   return n;
 }
 
+// A small persistent pool for omldm_fill_regions (a std::thread per region per block cost
+// ≈ 10-20 µs of thread creation each, every tick). run(n, f) calls f(0 .. n-1) on up to
+// `size` workers plus the caller and returns when all are done; one batch at a time.
+namespace {
+class ReadPool {
+ public:
+  void run(int n, int width, const std::function<void(int)>& f) {
+    std::lock_guard<std::mutex> batch(batch_mu_);  // one block at a time
+    grow(width - 1);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &f;
+      total_ = n;
+      next_ = 0;
+      done_ = 0;
+      active_ = width - 1 < (int)workers_.size() ? width - 1 : (int)workers_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return done_ == total_ && busy_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void drain() {
+    for (;;) {
+      int j;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (next_ >= total_) return;
+        j = next_++;
+      }
+      (*fn_)(j);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (++done_ == total_) done_cv_.notify_all();
+    }
+  }
+  void grow(int want) {
+    while ((int)workers_.size() < want && (int)workers_.size() < 64) {
+      const int id = (int)workers_.size();
+      workers_.emplace_back([this, id] { loop(id); });
+      workers_.back().detach();
+    }
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= active_ || fn_ == nullptr) continue;
+        ++busy_;
+      }
+      drain();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--busy_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::mutex batch_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int total_ = 0, next_ = 0, done_ = 0, active_ = 0, busy_ = 0;
+  uint64_t gen_ = 0;
+};
+ReadPool& read_pool() {
+  static ReadPool* p = new ReadPool();  // never destroyed: detached workers outlive exit
+  return *p;
+}
+}  // namespace
+
 // One tick's block in one call: the (partition region) reads of the block run on up to
 // `nthreads` threads, then the block's record index is assembled here (the Python form of
 // this — a thread-pool task per region, then numpy slicing per region — held the GIL for
@@ -127,13 +204,7 @@ OMLDM_HOST_API int64_t omldm_fill_regions(int nj, const int64_t* jobs, uint8_t* 
   if (nt <= 1) {
     for (int j = 0; j < nj; ++j) run(j);
   } else {
-    std::vector<std::thread> th;
-    th.reserve(nt);
-    for (int t = 0; t < nt; ++t)
-      th.emplace_back([&, t] {
-        for (int j = t; j < nj; j += nt) run(j);
-      });
-    for (auto& x : th) x.join();
+    read_pool().run(nj, nt, run);
   }
   for (int j = 0; j < nj; ++j)
     if (rn[j] < 0) return rn[j];
