@@ -9,6 +9,7 @@
 // engine reads tick k+1 while the GPU trains on tick k.
 #include <cerrno>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <condition_variable>
 #include <functional>
@@ -100,9 +101,9 @@ OMLDM_HOST_API int64_t omldm_read_log(int fd, int64_t offset, uint8_t* dst, int6
   return n;
 }
 
-// A small persistent pool for omldm_fill_regions (a std::thread per region per block cost
-// ≈ 10-20 µs of thread creation each, every tick). run(n, f) calls f(0 .. n-1) on up to
-// `size` workers plus the caller and returns when all are done; one batch at a time.
+// A small persistent pool for omldm_fill_regions (opt-in, OMLDM_READ_POOL=1: measured
+// slower than a thread per region per block). run(n, width, f) calls f(0 .. n-1) on up to
+// width − 1 workers plus the caller and returns when all are done; one batch at a time.
 namespace {
 class ReadPool {
  public:
@@ -201,10 +202,25 @@ OMLDM_HOST_API int64_t omldm_fill_regions(int nj, const int64_t* jobs, uint8_t* 
     rn[j] = omldm_read_log(int(J[0]), J[1], slot + J[2], J[3], J[4], ro[j].data(), &ru[j], J[5]);
   };
   const int nt = nthreads < 1 ? 1 : (nthreads > nj ? nj : nthreads);
+  // measured (scripts/gpu_r4_pool.sh, same box, alternated): a thread per reader per block
+  // 149-150 M DIB records/s end to end, the pool 111-112 M (its workers' condition-variable
+  // wake-ups and the shared job counter cost more than thread creation): the pool is opt-in
+  static const bool use_pool = [] {
+    const char* e = std::getenv("OMLDM_READ_POOL");
+    return e && e[0] == '1';
+  }();
   if (nt <= 1) {
     for (int j = 0; j < nj; ++j) run(j);
-  } else {
+  } else if (use_pool) {
     read_pool().run(nj, nt, run);
+  } else {  // a thread per reader per block
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t] {
+        for (int j = t; j < nj; j += nt) run(j);
+      });
+    for (auto& x : th) x.join();
   }
   for (int j = 0; j < nj; ++j)
     if (rn[j] < 0) return rn[j];
