@@ -443,6 +443,11 @@ def main(argv=None) -> int:
     sync()
     elapsed = time.perf_counter() - t0
     coll_ms = proto.collective_time_ms() if proto.time_collectives else None
+    # the v3 round's in-launch combiners never gave up on a spoke (a timeout would leave a
+    # spoke's update out of the round accumulator): checked after the timed window
+    comb_err = int(native.hip().omldm_scan3_comb_err()) if on_gpu else 0
+    if comb_err:
+        raise RuntimeError("v3 scan: a combiner workgroup timed out during the bench rounds")
     el = torch.tensor([elapsed, coll_ms or 0.0], dtype=torch.float64,
                       device=device if comm.backend == "nccl" else "cpu")
     if world > 1:
@@ -572,6 +577,7 @@ def main(argv=None) -> int:
             "backend": comm.backend, "rccl_ranks": world if comm.backend == "nccl" else 0,
             "collective_us_per_step": None if coll_ms is None
                                       else round(float(el[1].item()) * 1e3 / a.steps, 2),
+            "combiner_timeouts": comb_err,
             "round_kernel": ("linear_scan3 (v3 table scan)" if v3 else L.SEQ_KERNEL) if on_gpu
                             else "cpu",
             "numa": comm.placement, "ingest_lane": a.lane if on_gpu else None,
@@ -592,6 +598,9 @@ def main(argv=None) -> int:
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if os.environ.get("OMLDM_DUMP_MAPS"):  # diagnostics: attribute exit-time crash addresses
+        with open("/proc/self/maps") as f, open(os.environ["OMLDM_DUMP_MAPS"], "w") as g:
+            g.write(f.read())
     return 0
 
 

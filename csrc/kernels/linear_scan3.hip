@@ -1191,6 +1191,18 @@ OMLDM_API int omldm_scan3_comb_err() {
   return v;
 }
 
+// The combiner-timeout flag OR-ed into out[0] (device-visible memory, e.g. the device alias
+// of a pinned host word) and cleared, in stream order and without a host sync: the engine
+// reads the word a tick later (utils/health.py) and fails the job if it is set.
+__global__ void s3_err_drain_kernel(int* out) {
+  if (threadIdx.x == 0) out[0] |= atomicExch(&g_s3_comb_err, 0);
+}
+
+OMLDM_API int omldm_scan3_comb_err_drain(int* out, void* stream) {
+  hipLaunchKernelGGL(s3_err_drain_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
+  return (int)hipGetLastError();
+}
+
 // 1 when the v3 round handles this shape (field-aware slots, R ≤ RMAX).
 OMLDM_API int omldm_scan3_fits(int dn, int dc, int R, int bias) {
   return dc > 0 && dc <= s3::MAXF && dn >= 0 && dn + (bias ? 1 : 0) <= s3::KNMAX && R > 0 &&
@@ -1266,6 +1278,23 @@ S3Side* s3_side(hipStream_t st) {
   return &g_s3_side.emplace(st, sd).first->second;
 }
 }  // namespace
+
+// Explicit teardown of the HIP objects this library created on demand (the companion prep
+// streams and their fork / join events): called from the Python loader's atexit hook, while
+// the HIP runtime is still up — not left to static destructors at process exit.
+OMLDM_API int omldm_scan3_teardown() {
+  std::lock_guard<std::mutex> lk(g_s3_side_mu);
+  int n = 0;
+  for (auto& kv : g_s3_side) {
+    hipStreamSynchronize(kv.second.side);
+    hipEventDestroy(kv.second.fork);
+    hipEventDestroy(kv.second.join);
+    hipStreamDestroy(kv.second.side);
+    ++n;
+  }
+  g_s3_side.clear();
+  return n;
+}
 
 // Passes 1-3 (model-independent): slots, flags, Grams. `src` is the tokens (hashed = 0),
 // row-major int32 field-aware slots (1) or the compact int16 slots (2). span: slots per

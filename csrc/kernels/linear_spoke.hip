@@ -127,7 +127,8 @@ template <int FPL, int CH, int RULE, typename NumT, typename WT>
 __global__ __launch_bounds__(64) void linear_round_kernel(
     const WT* __restrict__ w, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
     int dc, const void* __restrict__ yv, int B, int R, int dim, float* __restrict__ ws,
-    int2* __restrict__ tables, float* __restrict__ dacc, LinParams p, TableGeom g, int ablate) {
+    int2* __restrict__ tables, float* __restrict__ dacc, LinParams p, TableGeom g, int ablate,
+    Spill sp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int cap = 1 << g.log2cap;
   const int tsz = cap + kOvf;
@@ -260,10 +261,8 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
             const int prev = atomicCAS(&keys[b + j], kEmptyKey, key);
             if (prev == kEmptyKey || prev == key) sl = b + j;
           }
-          if (sl == -2) {
-            sl = table_find_or_insert(keys, key, g);
-            if (sl < 0) ovf += 1.f;
-          }
+          if (sl == -2) sl = table_find_or_insert(keys, key, g);
+          if (sl < 0) sl = spill_slot(sp, s, key, ovf);  // LDS table full: HBM spill
           slot[e][f] = sl;
         }
       }
@@ -274,34 +273,53 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
         for (int f = 0; f < FPL; ++f) loss_sum += wv[e][f] + xv[e][f] + (float)slot[e][f];
       continue;
     }
-    // Exact sequential online updates.
+    // Exact sequential online updates. A chunk with spilled keys takes its own copy of
+    // the loop (global reads and atomics on the chain, ordered row to row by vmcnt(0)); the
+    // in-LDS copy keeps no global access between the rows.
+    bool spl = false;
 #pragma unroll
-    for (int e = 0; e < CH; ++e) {
-      const float y = yy[e];
-      if (__builtin_isnan(y)) continue;  // wave-uniform
-      float pm = 0.f, pn = 0.f;
+    for (int e = 0; e < CH; ++e)
 #pragma unroll
-      for (int f = 0; f < FPL; ++f) {
-        const float d = dcol[f] >= 0 ? dreg[f] : (slot[e][f] >= 0 ? vals[slot[e][f]] : 0.f);
-        pm = fmaf(xv[e][f], wv[e][f] + d, pm);
-        pn = fmaf(xv[e][f], xv[e][f], pn);
-      }
-      wave_sum2(pm, pn);
-      float c, sh, rsh, eta;
-      row_rate<RULE>(p, tc - t0 + e, sh, rsh, eta);
-      Step<RULE>::run(sigma * pm, y, pn, eta, p, loss_sum, mist, sqe, c);
-      nex += 1.f;
-      sigma *= sh;
-      rsig *= rsh;
-      if (c != 0.f) {  // wave-uniform
-        const float cv = c * rsig;
+      for (int f = 0; f < FPL; ++f) spl = spl || is_spill(slot[e][f]);
+    auto rows = [&](auto spill_tag) {
+      constexpr bool SPL = decltype(spill_tag)::value;
+#pragma unroll
+      for (int e = 0; e < CH; ++e) {
+        const float y = yy[e];
+        if (__builtin_isnan(y)) continue;  // wave-uniform
+        float pm = 0.f, pn = 0.f;
 #pragma unroll
         for (int f = 0; f < FPL; ++f) {
-          if (dcol[f] >= 0) dreg[f] = fmaf(cv, xv[e][f], dreg[f]);
-          else if (slot[e][f] >= 0) atomicAdd(&vals[slot[e][f]], cv * xv[e][f]);
+          const int sl = slot[e][f];
+          float d = dcol[f] >= 0 ? dreg[f] : (sl >= 0 ? vals[sl] : 0.f);
+          if constexpr (SPL)
+            if (is_spill(sl)) d = spill_load(spill_vals<1>(sp, s, spill_index(sl)));
+          pm = fmaf(xv[e][f], wv[e][f] + d, pm);
+          pn = fmaf(xv[e][f], xv[e][f], pn);
+        }
+        wave_sum2(pm, pn);
+        float c, sh, rsh, eta;
+        row_rate<RULE>(p, tc - t0 + e, sh, rsh, eta);
+        Step<RULE>::run(sigma * pm, y, pn, eta, p, loss_sum, mist, sqe, c);
+        nex += 1.f;
+        sigma *= sh;
+        rsig *= rsh;
+        if (c != 0.f) {  // wave-uniform
+          const float cv = c * rsig;
+#pragma unroll
+          for (int f = 0; f < FPL; ++f) {
+            const int sl = slot[e][f];
+            if (dcol[f] >= 0) dreg[f] = fmaf(cv, xv[e][f], dreg[f]);
+            else if (sl >= 0) atomicAdd(&vals[sl], cv * xv[e][f]);
+            else if (SPL && is_spill(sl))
+              atomicAdd(spill_vals<1>(sp, s, spill_index(sl)), cv * xv[e][f]);
+          }
+          if constexpr (SPL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
       }
-    }
+    };
+    if (__builtin_amdgcn_ballot_w64(spl)) rows(SpillTag<true>{});
+    else rows(SpillTag<false>{});
   }
   __syncthreads();
   // Round end: the bucketed table (σ·Δ/P per slot) goes out with plain coalesced stores
@@ -325,6 +343,7 @@ __global__ __launch_bounds__(64) void linear_round_kernel(
       if (k >= 0 && v != 0.f) atomicAdd(&dacc[k], v);
     }
   }
+  spill_flush<1>(sp, s, 1, dim, scale, dacc, lane);  // (restores the region even under ablate)
 #pragma unroll
   for (int f = 0; f < FPL; ++f)
     if (dcol[f] >= 0) wrow[kWsStat + dcol[f]] = dreg[f] * scale;
@@ -840,13 +859,13 @@ template <int FPL, int CH, int RULE, typename NumT, typename WT>
 static int launch_round(const void* w, const void* num, int dn, const void* cat, int dc,
                         const void* y, int B, int R, int S, float* dacc, int dim, float* ws,
                         int2* tables, double* cum, const LinParams& p, TableGeom g, int ablate,
-                        int parts, hipStream_t st) {
+                        int parts, const Spill& sp, hipStream_t st) {
   auto fn = linear_round_kernel<FPL, CH, RULE, NumT, WT>;
   const size_t lds = ((size_t(1) << g.log2cap) + kOvf) * 8;
   int e = check_dyn_lds((const void*)fn, lds);
   if (e) return e;
   hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)w, (const NumT*)num, dn, cat, dc,
-                     y, B, R, dim, ws, tables, dacc, p, g, ablate);
+                     y, B, R, dim, ws, tables, dacc, p, g, ablate, sp);
   e = (int)hipGetLastError();
   if (e) return e;
   return launch_reduce(tables, B, R, S, g, dim, dacc, ws, dn, cum, 0, parts, ablate, st);
@@ -883,7 +902,8 @@ static int dispatch_round_rd(const void* w, int w_bf16, const void* num, int num
                              const void* cat, int dc, const void* y, int B, int R, int S,
                              float* dacc, int dim, float* ws, int2* tables, double* cum,
                              const LinParams& p, TableGeom g, int ablate, int parts,
-                             hipStream_t st) {
+                             const Spill& sp, hipStream_t st) {
+  (void)sp;  // the register-dedup round never drops: a full bucket adds to dacc directly
 #define OMLDM_RD(RM, NT, WTT)                                                                  \
   return launch_round_rd<RM, RULE, NT, WTT>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, ws,  \
                                             tables, cum, p, g, ablate, parts, st)
@@ -904,10 +924,10 @@ template <int FPL, int CH, int RULE>
 static int dispatch_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                           const void* cat, int dc, const void* y, int B, int R, int S, float* dacc,
                           int dim, float* ws, int2* tables, double* cum, const LinParams& p,
-                          TableGeom g, int ablate, int parts, hipStream_t st) {
+                          TableGeom g, int ablate, int parts, const Spill& sp, hipStream_t st) {
 #define OMLDM_LR(NT, WTT)                                                                      \
   return launch_round<FPL, CH, RULE, NT, WTT>(w, num, dn, cat, dc, y, B, R, S, dacc, dim, ws, \
-                                              tables, cum, p, g, ablate, parts, st)
+                                              tables, cum, p, g, ablate, parts, sp, st)
   if (num_bf16) {
     if (w_bf16) OMLDM_LR(__hip_bfloat16, __hip_bfloat16);
     OMLDM_LR(__hip_bfloat16, float);
@@ -922,33 +942,33 @@ static int dispatch_rule(int rule, const void* w, int w_bf16, const void* num, i
                          int dn, const void* cat, int dc, const void* y, int B, int R, int S,
                          float* dacc, int dim, float* ws, int2* tables, double* cum,
                          const LinParams& p, TableGeom g, int ablate, int parts,
-                         hipStream_t st) {
+                         const Spill& sp, hipStream_t st) {
   if (FPL == 1 && use_rd_path(p.cspan, dn + dc + (p.bias ? 1 : 0), R, ablate)) {
     if (rule == kHinge)
       return dispatch_round_rd<kHinge>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
-                                       dim, ws, tables, cum, p, g, ablate, parts, st);
+                                       dim, ws, tables, cum, p, g, ablate, parts, sp, st);
     if (rule == kEpsInsensitive)
       return dispatch_round_rd<kEpsInsensitive>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
                                                 dacc, dim, ws, tables, cum, p, g, ablate, parts,
-                                                st);
+                                                sp, st);
     if (rule == kPegasos)
       return dispatch_round_rd<kPegasos>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
-                                         dim, ws, tables, cum, p, g, ablate, parts, st);
+                                         dim, ws, tables, cum, p, g, ablate, parts, sp, st);
     return dispatch_round_rd<kLogistic>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
-                                        dim, ws, tables, cum, p, g, ablate, parts, st);
+                                        dim, ws, tables, cum, p, g, ablate, parts, sp, st);
   }
   if (rule == kHinge)
     return dispatch_round<FPL, CH, kHinge>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc,
-                                           dim, ws, tables, cum, p, g, ablate, parts, st);
+                                           dim, ws, tables, cum, p, g, ablate, parts, sp, st);
   if (rule == kEpsInsensitive)
     return dispatch_round<FPL, CH, kEpsInsensitive>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R,
                                                     S, dacc, dim, ws, tables, cum, p, g, ablate,
-                                                    parts, st);
+                                                    parts, sp, st);
   if (rule == kPegasos)
     return dispatch_round<FPL, CH, kPegasos>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
-                                             dacc, dim, ws, tables, cum, p, g, ablate, parts, st);
+                                             dacc, dim, ws, tables, cum, p, g, ablate, parts, sp, st);
   return dispatch_round<FPL, CH, kLogistic>(w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S,
-                                            dacc, dim, ws, tables, cum, p, g, ablate, parts, st);
+                                            dacc, dim, ws, tables, cum, p, g, ablate, parts, sp, st);
 }
 
 template <int FPL, typename NumT, typename WT>
@@ -1027,14 +1047,22 @@ int bucket_geom(int dim, int log2cap, TableGeom* g) {
 }
 }  // namespace omldm
 
-// tables: device scratch of S * ((1 << log2cap) + 64) int2.
+// 4-byte words of the HBM spill of S spokes (spoke_table.h: Spill), VK floats per entry.
+OMLDM_API long long omldm_spill_words(int S, int log2gcap, int VK) {
+  return (long long)spill_words(S, log2gcap, VK);
+}
+
+// tables: device scratch of S * ((1 << log2cap) + 64) int2; spill: omldm_spill_words(S,
+// log2gcap, 1) words (keys −1, the rest 0 when allocated; every round leaves it so).
 OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int num_bf16, int dn,
                                  const void* cat, int dc, const void* y, int y_i8, int B,
                                  int R, int S, float* dacc, int dim, float* ws, void* tables,
                                  double* cum, int rule, int variant, float C, float eps, float lr,
                                  float lam, float inv_p, int bias, int cspan, int log2cap,
-                                 int chunk, int ablate, int parts, float tbase, void* stream) {
+                                 int chunk, int ablate, int parts, float tbase, void* spill,
+                                 int log2gcap, void* stream) {
   if (S <= 0) return 0;
+  if (spill == nullptr || log2gcap < 6 || log2gcap > 24) return -6;  // the HBM spill is required
   if (log2cap < 4 || log2cap > 14) return -1;  // ≤ 128 KiB of LDS per spoke
   if (rule == kPegasos && !(lam > 0.f && tbase >= 2.f)) return -5;
   if (parts < 1 || parts > 64) return -4;
@@ -1050,10 +1078,11 @@ OMLDM_API int omldm_linear_round(const void* w, int w_bf16, const void* num, int
   const int F = dn + dc + (bias ? 1 : 0);
   hipStream_t st = (hipStream_t)stream;
   int2* tb = (int2*)tables;
-  if (F <= 64 && chunk <= 8) return dispatch_rule<1, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, st);
-  if (F <= 64) return dispatch_rule<1, 16>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, st);
-  if (F <= 128) return dispatch_rule<2, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, st);
-  if (F <= 256) return dispatch_rule<4, 4>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, st);
+  const Spill sp = make_spill(spill, S, log2gcap, 1);
+  if (F <= 64 && chunk <= 8) return dispatch_rule<1, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, sp, st);
+  if (F <= 64) return dispatch_rule<1, 16>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, sp, st);
+  if (F <= 128) return dispatch_rule<2, 8>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, sp, st);
+  if (F <= 256) return dispatch_rule<4, 4>(rule, w, w_bf16, num, num_bf16, dn, cat, dc, y, B, R, S, dacc, dim, ws, tb, cum, p, g, ablate, parts, sp, st);
   return -2;
 }
 

@@ -29,9 +29,10 @@ constexpr int kMcStat = 8;  // ws row: loss, n, mistakes, active, -, overflow, -
 // Slot of hashed key `key` (find or insert): one 16-byte read of the four slots at the
 // key's 4-aligned hashed start in its bucket, CAS into the first empty one, inline
 // re-reads when another lane won it, then the slow path (same probe order, so a key is
-// never inserted twice). -1: table full (counted as overflow, the update is dropped).
+// never inserted twice); a key the LDS table cannot take goes to the spoke's HBM spill
+// (spoke_table.h), so no update is dropped.
 __device__ __forceinline__ int mc_slot(int* keys, int key, int b, int4 q, TableGeom g,
-                                       float& ovf) {
+                                       const Spill& sp, int s, float& ovf) {
   int sl = q.x == key ? b : q.y == key ? b + 1 : q.z == key ? b + 2 : q.w == key ? b + 3 : -2;
   if (sl == -2) {
     const int j = q.x == kEmptyKey ? 0 : q.y == kEmptyKey ? 1 : q.z == kEmptyKey ? 2
@@ -51,10 +52,8 @@ __device__ __forceinline__ int mc_slot(int* keys, int key, int b, int4 q, TableG
     const int prev = atomicCAS(&keys[b + j], kEmptyKey, key);
     if (prev == kEmptyKey || prev == key) sl = b + j;
   }
-  if (sl == -2) {
-    sl = table_find_or_insert(keys, key, g);
-    if (sl < 0) ovf += 1.f;
-  }
+  if (sl == -2) sl = table_find_or_insert(keys, key, g);
+  if (sl < 0) sl = spill_slot(sp, s, key, ovf);  // LDS table full: the HBM spill
   return sl;
 }
 
@@ -98,7 +97,7 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
     const WT* __restrict__ Wt, const NumT* __restrict__ num, int dn, const void* __restrict__ cat,
     int dc, int cspan, const void* __restrict__ yv, int y_i8, int B, int R, int dim, int nclass,
     int variant, float C, int bias, float* __restrict__ ws, int2* __restrict__ tables,
-    float* __restrict__ dacc, TableGeom g, int ablate, int compact) {
+    float* __restrict__ dacc, TableGeom g, int ablate, int compact, Spill sp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int cap = 1 << g.log2cap;
   const int tsz = cap + kOvf;
@@ -181,8 +180,14 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
     }
 #pragma unroll
     for (int e = 0; e < CH; ++e)
-      slot[e] = (dcol < 0 && idx[e] >= 0) ? mc_slot(keys, idx[e], b0[e], kq[e], g, ovf) : -1;
-    // exact sequential updates
+      slot[e] = (dcol < 0 && idx[e] >= 0) ? mc_slot(keys, idx[e], b0[e], kq[e], g, sp, s, ovf) : -1;
+    // exact sequential updates (a chunk with spilled keys: its own copy of the loop, global
+    // reads / atomics on the chain ordered row to row by vmcnt(0))
+    bool spl = false;
+#pragma unroll
+    for (int e = 0; e < CH; ++e) spl = spl || is_spill(slot[e]);
+    auto rows = [&](auto spill_tag) {
+    constexpr bool SPL = decltype(spill_tag)::value;
 #pragma unroll
     for (int e = 0; e < CH; ++e) {
       const float y = yy[e];
@@ -192,6 +197,10 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
       if (dcol >= 0) {
 #pragma unroll
         for (int k = 0; k < K; ++k) d[k] = dreg[k];
+      } else if (SPL && is_spill(slot[e])) {
+        const float* gv = spill_vals<K>(sp, s, spill_index(slot[e]));
+#pragma unroll
+        for (int k = 0; k < K; ++k) d[k] = spill_load(gv + k);
       } else if (slot[e] >= 0) {
         if constexpr (K % 4 == 0) {
 #pragma unroll
@@ -248,9 +257,17 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
         } else if (slot[e] >= 0) {
           if (yc >= 0 && yc < nclass) atomicAdd(&vals[(size_t)slot[e] * K + yc], gy);
           atomicAdd(&vals[(size_t)slot[e] * K + r], -gy);
+        } else if (SPL && is_spill(slot[e])) {
+          float* gv = spill_vals<K>(sp, s, spill_index(slot[e]));
+          if (yc >= 0 && yc < nclass) atomicAdd(gv + yc, gy);
+          atomicAdd(gv + r, -gy);
         }
+        if constexpr (SPL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
+    };
+    if (__builtin_amdgcn_ballot_w64(spl)) rows(SpillTag<true>{});
+    else rows(SpillTag<false>{});
   }
   __syncthreads();
   // Round end: class k of slot i of spoke s → region k, [i >> seg][s][i & seg mask]
@@ -297,6 +314,7 @@ __global__ __launch_bounds__(64) void multiclass_round_kernel(
         if (v != 0.f) atomicAdd(&dacc[(size_t)k * dim + key], v);
       }
   }
+  spill_flush<K>(sp, s, nclass, dim, 1.f, dacc, lane);
   if (dcol >= 0)
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -675,7 +693,8 @@ template <int K, typename NumT, typename WT>
 static void launch_mc(const void* Wt, const void* num, int dn, const void* cat, int dc, int cspan,
                       const void* y, int y_i8, int B, int R, int S, int dim, int nclass,
                       int variant, float C, int bias, float* ws, int2* tables, float* dacc,
-                      TableGeom g, size_t lds, int compact, hipStream_t st, int* err) {
+                      TableGeom g, size_t lds, int compact, const Spill& sp, hipStream_t st,
+                      int* err) {
   int ablate = 0;  // timing diagnostics only: bit0 no flush, bit1 no sequential part
   if (const char* e = getenv("OMLDM_MC_ABLATE")) ablate = atoi(e);
   // register-dedup path: field-aware wire, ≤ 16 rows per spoke, K ≤ 4, compact flush
@@ -703,7 +722,7 @@ static void launch_mc(const void* Wt, const void* num, int dn, const void* cat, 
   if (*err) return;
   hipLaunchKernelGGL(fn, dim3(S), dim3(64), lds, st, (const WT*)Wt, (const NumT*)num, dn, cat, dc,
                      cspan, y, y_i8, B, R, dim, nclass, variant, C, bias, ws, tables, dacc, g,
-                     ablate, compact);
+                     ablate, compact, sp);
 }
 
 }  // namespace omldm
@@ -717,8 +736,10 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
                                      int dn, const void* cat, int dc, int cspan, const void* y, int y_i8,
                                      int B, int R, int S, int dim, int nclass, int variant,
                                      float C, int bias, float* dacc, float* stats, int log2cap,
-                                     float* ws, void* tables, void* stream) {
+                                     float* ws, void* tables, void* spill, int log2gcap,
+                                     void* stream) {
   if (S <= 0 || B <= 0) return 0;
+  if (spill == nullptr || log2gcap < 6 || log2gcap > 24) return -6;  // the HBM spill is required
   if (dn + dc + (bias ? 1 : 0) > 64) return -2;
   if (nclass < 2 || nclass > 16) return -3;
   if (log2cap < 6 || log2cap > 13) return -1;
@@ -730,6 +751,7 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
     g.qused = (int)(((hi < dim ? hi : dim) + (1LL << gl) - 1) >> gl);
   }
   const int K = nclass <= 2 ? 2 : nclass <= 4 ? 4 : nclass <= 8 ? 8 : 16;
+  const Spill sp = make_spill(spill, S, log2gcap, K);  // K floats per entry
   const size_t lds = ((size_t(1) << log2cap) + kOvf) * (4 + 4 * (size_t)K);
   if (lds > 160 * 1024) return -1;
   hipStream_t st = (hipStream_t)stream;
@@ -743,16 +765,16 @@ OMLDM_API int omldm_multiclass_round(const void* Wt, int wt_bf16, const void* nu
   {                                                                                          \
     if (num_bf16 && wt_bf16)                                                                 \
       launch_mc<KK, __hip_bfloat16, __hip_bfloat16>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, \
-          S, dim, nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, st, &e);           \
+          S, dim, nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, sp, st, &e);           \
     else if (num_bf16)                                                                       \
       launch_mc<KK, __hip_bfloat16, float>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim,  \
-          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, st, &e);                   \
+          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, sp, st, &e);                   \
     else if (wt_bf16)                                                                        \
       launch_mc<KK, float, __hip_bfloat16>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim,  \
-          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, st, &e);                   \
+          nclass, variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, sp, st, &e);                   \
     else                                                                                     \
       launch_mc<KK, float, float>(Wt, num, dn, cat, dc, cspan, y, y_i8, B, R, S, dim, nclass,   \
-          variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, st, &e);                           \
+          variant, C, bias, ws, (int2*)tables, dacc, g, lds, compact, sp, st, &e);                           \
   }
   if (K == 2) OMLDM_MC(2) else if (K == 4) OMLDM_MC(4) else if (K == 8) OMLDM_MC(8) else OMLDM_MC(16)
 #undef OMLDM_MC

@@ -15,6 +15,12 @@
 // cspan < 0: the request carries raw 32-bit category tokens (the binary wire), hashed by
 // the wave itself (hash_dev.h) — the same hash as the training round.
 //
+// Model versions: the wave reads one of two weight banks, chosen per request by the
+// request line's last dword (lane 63, covered by the checksum). The engine publishes each
+// round's models into the bank no request is reading and switches requests to it once the
+// publishing copy has completed (engine/forecast_server.py), so a prediction never sees a
+// model that is half-way through an update.
+//
 // Safety: the wave exits on the stop word or after `lifetime_us` of wall time
 // (s_memrealtime, 100 MHz), whichever comes first; every spin is bounded by it.
 #include "common.h"
@@ -26,7 +32,8 @@
 
 namespace omldm {
 
-constexpr int kReqWords = 64;  // request line: [seq, csum, payload (dn + dc dwords)]
+constexpr int kReqWords = 64;  // request line: [seq, csum, payload (dn + dc dwords), …, bank]
+constexpr int kBankWord = kReqWords - 1;
 
 struct alignas(256) Mailbox {
   unsigned int req[kReqWords];  // host → device (one 256-B line)
@@ -68,7 +75,8 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
 }
 
 template <typename WT, bool GROUPED>
-__global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, long long wstride,
+__global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w0,
+                                                   const WT* __restrict__ w1, long long wstride,
                                                    int M, int dn, int dc, int dim, int bias,
                                                    int cspan, Mailbox* mb,
                                                    unsigned long long lifetime_ticks) {
@@ -104,10 +112,11 @@ __global__ __launch_bounds__(64) void serve_kernel(const WT* __restrict__ w, lon
       continue;
     }
     // checksum over the payload lanes (position-mixed), keyed by the sequence
-    const bool pl = lane >= 2 && lane < 2 + nf;
+    const bool pl = (lane >= 2 && lane < 2 + nf) || lane == kBankWord;
     const uint32_t x = wave_xor(pl ? line_mix(d, (uint32_t)lane) : 0u) ^ line_mix(seq, 0u);
     const uint32_t csum = (uint32_t)__shfl((int)d, 1, 64);
     if (__builtin_amdgcn_readfirstlane(x == csum ? 1 : 0) == 0) continue;  // torn: re-poll
+    const WT* __restrict__ w = __builtin_amdgcn_readlane((int)d, kBankWord) ? w1 : w0;
     // lane j ← payload dword j (feature j)
     const unsigned int fj = (unsigned int)__shfl((int)d, (lane + 2) & 63, 64);
     int idx = -1;
@@ -192,10 +201,12 @@ OMLDM_API void omldm_mailbox_free(void* p) {
   if (p) hipHostFree(p);
 }
 
-OMLDM_API int omldm_serve_start(const void* w, int w_bf16, long long wstride, int M, int dn,
-                                int dc, int dim, int bias, int cspan, void* mailbox,
-                                long long lifetime_us, void* stream) {
-  if (M < 1 || M > 60 || dn + dc > kReqWords - 2 || dn + dc + (bias ? 1 : 0) > 64) return -2;
+// w1: the second weight bank (nullptr: the requests' bank 1 reads w as well).
+OMLDM_API int omldm_serve_start(const void* w, const void* w1, int w_bf16, long long wstride,
+                                int M, int dn, int dc, int dim, int bias, int cspan,
+                                void* mailbox, long long lifetime_us, void* stream) {
+  if (M < 1 || M > 60 || dn + dc > kReqWords - 3 || dn + dc + (bias ? 1 : 0) > 64) return -2;
+  if (w1 == nullptr) w1 = w;
   Mailbox* hmb = (Mailbox*)mailbox;
   void* dmb = nullptr;
   if (hipHostGetDevicePointer(&dmb, mailbox, 0) != hipSuccess || !dmb) return -3;
@@ -208,7 +219,8 @@ OMLDM_API int omldm_serve_start(const void* w, int w_bf16, long long wstride, in
   if (const char* e = getenv("OMLDM_SERVE_GROUPED")) grouped = e[0] == '1';
   hipStream_t st = (hipStream_t)stream;
 #define OMLDM_SERVE(WT, G)                                                                   \
-  hipLaunchKernelGGL((serve_kernel<WT, G>), dim3(1), dim3(64), 0, st, (const WT*)w, wstride, M, \
+  hipLaunchKernelGGL((serve_kernel<WT, G>), dim3(1), dim3(64), 0, st, (const WT*)w,          \
+                     (const WT*)w1, wstride, M,                                               \
                      dn, dc, dim, bias, cspan, (Mailbox*)dmb, ticks)
   if (w_bf16) {
     if (grouped) OMLDM_SERVE(__hip_bfloat16, true);
@@ -224,7 +236,7 @@ OMLDM_API int omldm_serve_start(const void* w, int w_bf16, long long wstride, in
 // Host side of one request: payload → checksum → sequence (release), then a bounded spin
 // on the completion sequence; copies the M scores out. Returns 0, or -1 on timeout.
 OMLDM_API int omldm_serve_request(void* mailbox, const float* num, int dn, const int* cat, int dc,
-                                  int M, float* out, long long timeout_us) {
+                                  int M, float* out, long long timeout_us, int bank) {
   Mailbox* mb = (Mailbox*)mailbox;
   const unsigned int seq = __atomic_load_n(&mb->req[0], __ATOMIC_RELAXED) + 1u;
   uint32_t x = line_mix(seq, 0u);
@@ -239,6 +251,9 @@ OMLDM_API int omldm_serve_request(void* mailbox, const float* num, int dn, const
     __atomic_store_n(&mb->req[2 + dn + j], u, __ATOMIC_RELAXED);
     x ^= line_mix(u, (uint32_t)(2 + dn + j));
   }
+  const uint32_t bk = bank ? 1u : 0u;
+  __atomic_store_n(&mb->req[kBankWord], bk, __ATOMIC_RELAXED);
+  x ^= line_mix(bk, (uint32_t)kBankWord);
   __atomic_store_n(&mb->req[1], x, __ATOMIC_RELAXED);
   __atomic_store_n(&mb->req[0], seq, __ATOMIC_RELEASE);
   const auto t0 = std::chrono::steady_clock::now();

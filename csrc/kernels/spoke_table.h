@@ -171,7 +171,115 @@ static __device__ __noinline__ int table_find_or_insert(int* keys, int key, Tabl
       if (prev == kEmptyKey || prev == key) return i;
     }
   }
-  return -1;  // table full: the update is dropped and counted as overflow
+  return -1;  // table full: the caller takes the key to the global spill (below)
+}
+
+// ---------------------------------------------------------------- global spill
+// A spoke whose distinct keys outgrow its LDS table (bucket and overflow area full) keeps
+// the rest in HBM, so no update is ever dropped: per spoke an open-addressing table
+// keys[gcap] (kEmptyKey when free), vals[gcap][VK] and the list of the entries it took
+// this round (count[s] of them). Round end: every listed entry is flushed into the
+// accumulator and restored to empty, so the region is clean for the next round without
+// a memset. Only the spoke's own wave touches its region: device-scope atomics keep the
+// lanes of one row coherent, and a row's reads of a spilled delta (agent-scope loads,
+// past L1) follow a vmcnt(0) after the previous row's atomics.
+// Slot encoding on the sequential chain: ≥ 0 LDS slot, −1 no key, ≤ −3: spill entry
+// (−3 − index).
+struct Spill {
+  int* keys;    // [S][gcap], every entry kEmptyKey when allocated
+  float* vals;  // [S][gcap][VK], zero when allocated
+  int* list;    // [S][gcap]
+  int* count;   // [S], zero when allocated
+  int log2gcap;
+};
+constexpr int kSpillBase = -3;
+// One contiguous caller buffer: keys [S·gcap] | vals [S·gcap·VK] | list [S·gcap] | count [S]
+// (spill_words(S, log2gcap, VK) 4-byte words; keys = −1, vals = count = 0 when allocated).
+inline size_t spill_words(int S, int log2gcap, int VK) {
+  return (size_t)S * ((size_t)1 << log2gcap) * (2 + (size_t)VK) + (size_t)S;
+}
+inline Spill make_spill(void* base, int S, int log2gcap, int VK) {
+  const size_t n = (size_t)S << log2gcap;
+  int* keys = static_cast<int*>(base);
+  float* vals = reinterpret_cast<float*>(keys + n);
+  int* list = reinterpret_cast<int*>(vals + n * VK);
+  return Spill{keys, vals, list, list + n, log2gcap};
+}
+template <bool B>
+struct SpillTag {
+  static constexpr bool value = B;
+};
+
+__device__ __forceinline__ bool is_spill(int sl) { return sl <= kSpillBase; }
+__device__ __forceinline__ int spill_index(int sl) { return kSpillBase - sl; }
+
+// Entry of `key` in spoke s's spill (find or insert); -1 only when all gcap entries are
+// taken (the host sizes gcap ≥ 2 × the spoke's key occurrences, so never).
+static __device__ __noinline__ int spill_find_or_insert(const Spill& sp, int s, int key) {
+  const int gcap = 1 << sp.log2gcap;
+  int* keys = sp.keys + (size_t)s * gcap;
+  uint32_t i = hmix((uint32_t)key) >> (32 - sp.log2gcap);
+  for (int q = 0; q < gcap; ++q) {
+    const int k = __hip_atomic_load(&keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == key) return (int)i;
+    if (k == kEmptyKey) {
+      const int prev = atomicCAS(&keys[i], kEmptyKey, key);
+      if (prev == kEmptyKey) {
+        const int at = atomicAdd(&sp.count[s], 1);
+        sp.list[(size_t)s * gcap + at] = (int)i;
+        return (int)i;
+      }
+      if (prev == key) return (int)i;
+    }
+    i = (i + 1) & (uint32_t)(gcap - 1);
+  }
+  return -1;
+}
+
+// The slot of a key the LDS table could not take: a spill entry, or -1 (counted in `ovf`).
+__device__ __forceinline__ int spill_slot(const Spill& sp, int s, int key, float& ovf) {
+  const int gi = spill_find_or_insert(sp, s, key);
+  if (gi < 0) {
+    ovf += 1.f;
+    return -1;
+  }
+  return kSpillBase - gi;
+}
+
+template <int VK>
+__device__ __forceinline__ float* spill_vals(const Spill& sp, int s, int gi) {
+  return sp.vals + ((size_t)s * (1 << sp.log2gcap) + gi) * VK;
+}
+
+__device__ __forceinline__ float spill_load(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Round end of one spoke wave (all 64 lanes): every listed entry → dacc[k·dim + key] +=
+// scale·vals[k] for k < nv, then the entry is restored (key empty, values 0).
+template <int VK>
+__device__ __forceinline__ void spill_flush(const Spill& sp, int s, int nv, int dim, float scale,
+                                            float* __restrict__ dacc, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int gcap = 1 << sp.log2gcap;
+  const int n = __hip_atomic_load(&sp.count[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (n == 0) return;
+  int* keys = sp.keys + (size_t)s * gcap;
+  for (int j = lane; j < n; j += kWave) {
+    const int gi = __hip_atomic_load(&sp.list[(size_t)s * gcap + j], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    const int key = __hip_atomic_load(&keys[gi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float* v = spill_vals<VK>(sp, s, gi);
+#pragma unroll
+    for (int k = 0; k < VK; ++k) {
+      const float x = spill_load(v + k);
+      if (k < nv && x != 0.f) atomicAdd(&dacc[(size_t)k * dim + key], x * scale);
+      v[k] = 0.f;
+    }
+    keys[gi] = kEmptyKey;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) sp.count[s] = 0;
 }
 
 // Bucket reduce of flushed spoke tables into dacc (linear_spoke.hip): key groups

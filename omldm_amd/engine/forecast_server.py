@@ -20,9 +20,21 @@ it for EVERY pipeline before taking the next one:
   predict kernels on a one-row batch on the lane's HIP stream (one stream sync per
   record).
 
-Both read the live models the training rounds update (at most one round stale, like a
-reference spoke between two syncs). Records wait for the tick (``take_fallback``) only
-while no pipeline exists yet.
+Consistency (the reference serialises a spoke's predict and fit in one operator,
+FlinkSpoke.scala:97-105, so a prediction sees a model between two fits):
+
+* the wave reads one of two published weight banks, never the live store rows: after a
+  tick's training the engine copies the served rows into the bank no request reads
+  (``publish``, on the compute stream, stream-ordered after the round's apply) and the
+  lane switches its requests to that bank once the copy's event has completed — an
+  answer never mixes slots of two rounds, and is at most one round stale;
+* a one-row predict of a direct pipeline waits for the tick's training to finish
+  (``begin_training`` / ``end_training``: the lane's stream waits on the event recorded
+  after the last round), and the tick's next training starts only after the lane's
+  in-flight predict has returned (the lane holds ``lock`` for a whole record) — so it reads
+  the model between two rounds, never one half-way through an update.
+
+Records wait for the tick (``take_fallback``) only while no pipeline exists yet.
 """
 from __future__ import annotations
 
@@ -77,6 +89,15 @@ class ForecastServer:
         self._order: list = []        # every served pipeline id, in id order
         self._row0 = 0
         self._stream = None           # the lane's HIP stream (direct predicts)
+        # published model banks of the store rows the wave serves (see the module doc)
+        self._banks = None            # [bank0, bank1]: copies of store.W
+        self._bank = 0                # the bank requests read
+        self._pend = None             # (bank, event): a publish the lane adopts when done
+        self._pub_lock = threading.Lock()
+        # direct predicts: training in flight → wait for its end event
+        self._trained = threading.Event()
+        self._trained.set()
+        self._train_ev = None
         self.family_latency: dict = {}  # learner name → deque of µs (record in → outputs out)
         self.fallback: collections.deque = collections.deque()
         self.latency_us: collections.deque = collections.deque(maxlen=1 << 16)
@@ -152,6 +173,15 @@ class ForecastServer:
                 self._row0 = lo
                 self._served = [(p.id, p.store_row, p.learner.TASK == "classification")
                                 for p in store]
+                # both banks start as the current models (the store may have moved)
+                W = self.job.store.W
+                with self._pub_lock:
+                    if self._banks is None or self._banks[0].shape != W.shape:
+                        self._banks = [torch.empty_like(W), torch.empty_like(W)]
+                    for b in self._banks:
+                        b.copy_(W)
+                    torch.cuda.synchronize(self.job.device)
+                    self._bank, self._pend = 0, None
             waved = {pid for pid, _, _ in self._served}
             self._direct = [(p.id, p) for p in pipes if p.id not in waved]
             if self._direct and self._stream is None and self.job.device.type == "cuda":
@@ -172,8 +202,9 @@ class ForecastServer:
             return srv
         self._stop_wave()
         lo, hi, bias = self._spec
-        W = self.job.store.W[lo:hi]
-        srv = PredictServer(W, self.space.dn, self.space.dc, bias, cat_span=self.space.cat_span)
+        b0, b1 = self._banks
+        srv = PredictServer(b0[lo:hi], self.space.dn, self.space.dc, bias,
+                            cat_span=self.space.cat_span, w1=b1[lo:hi])
         srv.start(lifetime_us=self.lifetime_us)
         self._server = srv
         return srv
@@ -186,6 +217,48 @@ class ForecastServer:
         with self._cycle:
             done = dict(self._done) if self._thread.is_alive() else dict(self.consumer.offsets)
             return done, list(self.fallback)
+
+    # ------------------------------------------------------ model publication
+    def begin_training(self) -> None:
+        """Tick thread, before the round's kernels are enqueued: waits for the lane's
+        in-flight record (its direct predicts read the models the round updates), then
+        holds later direct predicts until ``end_training``."""
+        with self.lock:
+            self._trained.clear()
+
+    def end_training(self) -> None:
+        """Tick thread, after the round (and the queries that may finalize models): the
+        event after the last kernel gates the lane's next direct predicts, and the served
+        store rows are published into the bank no request reads."""
+        try:
+            if self.job.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record()
+                self._train_ev = ev
+                self.publish()
+        finally:
+            self._trained.set()
+
+    def publish(self) -> None:
+        """Copy the served store rows into the bank requests do not read (current stream,
+        after the round's apply) and hand it to the lane with the copy's event."""
+        with self._pub_lock:
+            spec, banks = self._spec, self._banks
+            if spec is None or banks is None:
+                return
+            lo, hi, _ = spec
+            target = self._pend[0] if self._pend is not None else 1 - self._bank
+            banks[target][lo:hi].copy_(self.job.store.W[lo:hi], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pend = (target, ev)
+
+    def _read_bank(self) -> int:
+        """The bank this request reads: the latest publish whose copy has completed."""
+        with self._pub_lock:
+            if self._pend is not None and self._pend[1].query():
+                self._bank, self._pend = self._pend[0], None
+            return self._bank
 
     def take_fallback(self) -> list:
         out = []
@@ -222,9 +295,13 @@ class ForecastServer:
 
         dev = self.job.device
         b = HashedBatch(self._num, self._cat, self._y, None, self.space.cat_span)
+        if not self._trained.wait(60.0):
+            raise RuntimeError("forecast lane: the tick's training did not end within 60 s")
         if self._stream is None:
             return float(pipe.predict(b.to(dev))[0])
         with torch.cuda.stream(self._stream):
+            if self._train_ev is not None:
+                self._stream.wait_event(self._train_ev)  # the model between two rounds
             out = pipe.predict(b.to(dev, non_blocking=False))
             return float(out.float()[0].item())
 
@@ -243,11 +320,12 @@ class ForecastServer:
             if self._spec is not None:
                 cat = self._cat32.ctypes.data
                 srv = self._ensure_wave()
+                bank = self._read_bank()
                 try:
-                    out = srv.request_raw(self._num.data_ptr(), cat)
+                    out = srv.request_raw(self._num.data_ptr(), cat, bank=bank)
                 except TimeoutError:  # the wave's lifetime ended under the request
                     self._stop_wave()
-                    out = self._ensure_wave().request_raw(self._num.data_ptr(), cat)
+                    out = self._ensure_wave().request_raw(self._num.data_ptr(), cat, bank=bank)
                 for pid, row, cls in self._served:
                     s = float(out[row - self._row0])
                     preds[pid] = (1.0 if s >= 0 else -1.0) if cls else s

@@ -164,7 +164,12 @@ class Job:
         if cfg.checkpointing or cfg.restore:
             from omldm_amd.utils.checkpoint import Checkpointer
 
-            self.checkpointer = Checkpointer(cfg, self.rank, self.world)
+            import uuid
+
+            nonce = uuid.uuid4().hex if self.rank == 0 else None
+            if self.world > 1:  # every rank tags its done markers with rank 0's run nonce
+                nonce = comm.broadcast_object(nonce, src=0)
+            self.checkpointer = Checkpointer(cfg, self.rank, self.world, nonce=nonce)
             if cfg.restore:
                 self.checkpointer.restore(self)
         if self.fserver is not None:
@@ -173,10 +178,14 @@ class Job:
         # device time of the training rounds and of the coalesced collectives (lagged
         # event pairs, no host sync: utils/devtimer.py)
         self._train_timer = self._coll_timer = None
+        self._health = None
         if self.device.type == "cuda":
             from omldm_amd.utils.devtimer import LaggedTimer
+            from omldm_amd.utils.health import DeviceHealth
 
             self._train_timer, self._coll_timer = LaggedTimer(), LaggedTimer()
+            # dropped updates / combiner timeouts fail the job, read one tick late
+            self._health = DeviceHealth(self.device)
         self._t_start = time.time()
         # diagnostics / multi-rank tests: a per-tick digest of every pipeline's model
         # (replica agreement across ranks) and the final models, under this directory
@@ -537,16 +546,25 @@ class Job:
         self._ctrl_due = n_req > 0
         active += n_req
         self._trained_global += int(n_train)
-        if self.pipes and n_train > 0:
-            if self._train_timer is not None:
-                self._train_timer.start()
-            self._train(tb, spill)
-            if self._train_timer is not None:
-                self._train_timer.stop()
-            if self._trace_dir:
-                self._trace_models()
-        for q in queries:
-            self._answer(q)
+        fs = self.fserver if (self.pipes and (n_train > 0 or queries)) else None
+        if fs is not None:  # the lane's predicts see models between two rounds
+            fs.begin_training()
+        try:
+            if self.pipes and n_train > 0:
+                if self._train_timer is not None:
+                    self._train_timer.start()
+                self._train(tb, spill)
+                if self._train_timer is not None:
+                    self._train_timer.stop()
+                if self._health is not None:
+                    self._health.arm(self.pipes)
+                if self._trace_dir:
+                    self._trace_models()
+            for q in queries:
+                self._answer(q)
+        finally:
+            if fs is not None:
+                fs.end_training()
         with tracing.range("learning_curve"):
             for pipe in self.pipes.values():
                 pipe.record_learning_curve()
@@ -628,6 +646,8 @@ class Job:
             self.tick()
         for p in self.pipes.values():
             p.protocol.finalize()
+        if self._health is not None:
+            self._health.check()  # the last trained tick's words
         if self._trace_dir:
             self._trace_models(final=True)
         if self.fserver is not None:

@@ -144,11 +144,16 @@ def multiclass_round(W: torch.Tensor, batch: HashedBatch, R: int, S: int, nclass
         if Wt is None:
             Wt = proto_shadow(W)
         assert Wt.shape == (dim, class_pad(nclass)) and Wt.is_contiguous()
+        from omldm_amd.ops.linear import spill_log2cap, spill_workspace
+
+        lg = spill_log2cap(R, dn + dc + 1)
+        spill = spill_workspace(W.device, S, lg, class_pad(nclass))
         check(native.hip().omldm_multiclass_round(
             ptr(Wt), int(Wt.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
             dn, ptr(cat), dc, batch.cat_span,
             ptr(y), int(y.dtype == torch.int8), batch.B, R, S, dim, nclass, variant, C, int(bias),
-            ptr(dacc), ptr(stats), log2cap, ptr(ws), ptr(tables), native.stream_of(W)),
+            ptr(dacc), ptr(stats), log2cap, ptr(ws), ptr(tables), ptr(spill), lg,
+            native.stream_of(W)),
             "omldm_multiclass_round")
     else:
         batch = batch.to_wide()

@@ -38,13 +38,47 @@ WS_STAT = 8  # per-spoke workspace stat columns (see linear_spoke.hip kWsStat)
 _WS: dict = {}
 
 
-def _workspace(device, n: int, key: str = "ws") -> torch.Tensor:
-    """Per-device scratch (per-spoke rows, spoke delta tables). Stream-ordered reuse is
-    safe: every round kernel fully rewrites what its reduce/finish kernels read."""
-    t = _WS.get((device, key))
+def _workspace(device, n: int, key: str = "ws", per_stream: bool = True) -> torch.Tensor:
+    """Scratch (per-spoke rows, spoke delta tables), one buffer per (device, key, current
+    stream): every round kernel fully rewrites what its reduce/finish kernels read, so reuse
+    is safe in stream order — and pipelines that train side by side on different streams
+    (engine/job.py: pipelineStreams) get buffers of their own. ``per_stream=False``: one
+    buffer per device whose caller orders the streams itself (the v3 prep ring, the v3
+    run-time buffers keyed by stream in ``key``)."""
+    dev = torch.device(device)
+    sid = torch.cuda.current_stream(dev).cuda_stream if (per_stream and dev.type == "cuda") else 0
+    k = (device, key, sid)
+    t = _WS.get(k)
     if t is None or t.numel() < n:
         t = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=device)
-        _WS[(device, key)] = t
+        _WS[k] = t
+    return t
+
+
+_SPILL: dict = {}
+
+
+def spill_log2cap(R: int, keys_per_row: int) -> int:
+    """HBM spill entries per spoke (log2): ≥ 2 × the spoke's key occurrences, so a spoke
+    whose every key missed its LDS table still finds room (load ≤ 1/2)."""
+    return max(6, min(24, (2 * max(1, R) * max(1, keys_per_row) - 1).bit_length()))
+
+
+def spill_workspace(device, S: int, log2gcap: int, vk: int) -> torch.Tensor:
+    """The spokes' HBM spill (csrc/kernels/spoke_table.h: Spill) for the current stream:
+    keys −1, values and counters 0 when allocated; every round restores what it used, so
+    the buffer stays clean across rounds without a memset."""
+    dev = torch.device(device)
+    sid = torch.cuda.current_stream(dev).cuda_stream
+    key = (str(dev), sid, int(S), int(log2gcap), int(vk))
+    t = _SPILL.get(key)
+    if t is None:
+        words = int(native.hip().omldm_spill_words(int(S), int(log2gcap), int(vk)))
+        t = torch.zeros(words, dtype=torch.int32, device=dev)
+        t[: int(S) << int(log2gcap)].fill_(-1)
+        if len(_SPILL) > 16:
+            _SPILL.clear()
+        _SPILL[key] = t
     return t
 
 
@@ -59,7 +93,8 @@ def auto_log2cap(dim: int, rows: int, keys_per_row: int) -> int:
     ``keys_per_row`` hashed keys each: load factor ≤ 1/2 for distinct keys, clamped so
     a wave's table stays ≤ 64 KiB (occupancy: 8 KiB tables allow 20 waves per CU,
     64 KiB only 2 — profiles/round1_ablation.md "Occupancy"). Keys beyond the table
-    spill to the overflow path, so the size only affects speed, never the result."""
+    go to the spoke's HBM spill (spoke_table.h), so the size only affects speed, never
+    the result: no update is dropped."""
     want = max(1, 2 * rows * max(1, keys_per_row) - 1).bit_length()
     return min(13, max(min_log2cap(dim), want))
 
@@ -109,6 +144,8 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         wsw = WS_STAT + num.shape[1] + 1
         ws = _workspace(w.device, S * wsw)
         tables = _workspace(w.device, S * ((1 << log2cap) + 64) * 2, key="tables")
+        lg = spill_log2cap(R, num.shape[1] + cat.shape[1] + 1)
+        spill = spill_workspace(w.device, S, lg, 1)
         dp = native.dptr
         rc = native.hip().omldm_linear_round(
             ptr(w), int(w.dtype == torch.bfloat16), dp(num), int(num.dtype == torch.bfloat16),
@@ -116,7 +153,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
             ptr(dacc), dim,
             ptr(ws), ptr(tables), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr,
             rule.lam, inv_p, int(rule.bias), batch.cat_span, log2cap, int(chunk), int(ablate),
-            int(parts), float(rule.tbase), native.stream_of(w))
+            int(parts), float(rule.tbase), ptr(spill), lg, native.stream_of(w))
         check(rc, "omldm_linear_round")
         if on_part is not None:
             on_part(0, *part_bounds(dim, 0, parts, cuda=True))
@@ -290,6 +327,7 @@ class Scan3Prep:
     ptrs: object
     key: tuple          # (B, R, S, dim, bias, rule, variant, C, dn, dc) it was made for
     event: object = None
+    slot: object = None  # workspace set (ring slot "k<i>" for inline preps)
 
 
 def scan3_fits(dn: int, dc: int, R: int, bias: bool) -> bool:
@@ -345,7 +383,7 @@ def _s3_workspaces(dev, B, R, S, dn, dc, span, bias, slot):
         n = int(h.omldm_scan3_ws_words(i, B, R, S, dn, dc, span, int(bias))) if hit is None \
             else hit[2][i]
         wkey = f"s3_{name}" if i in _S3_SHARED else f"s3_{name}{slot}"
-        bufs.append(_workspace(dev, n, key=wkey))
+        bufs.append(_workspace(dev, n, key=wkey, per_stream=False))
     if hit is not None and all(a.data_ptr() == b.data_ptr() for a, b in zip(bufs, hit[0])):
         return hit[0], hit[1]
     ptrs = (ctypes.c_void_p * len(bufs))(*[b.data_ptr() for b in bufs])
@@ -362,14 +400,31 @@ _S3_SLOTS = {"next": 0}
 S3_SLOT_RING = 16
 
 
-def _s3_slot_for(key) -> str:
+_S3_SLOT_LAST: dict = {}  # ring slot → event after the last scan that read its prep
+
+
+def _s3_slot_for(key, device=None) -> str:
     """Workspace set of an inline prep: a ring of 16, one per distinct prep key in turn.
-    Pipelines of one tick may scan on different streams, so two preps alive in the same
-    tick must not share buffers (ticks are joined, so the ring only has to outlast the
-    distinct keys of one tick)."""
+    Pipelines of one tick may scan on different streams, so two preps alive at once must
+    not share buffers; a slot that comes round again while a scan on another stream may
+    still read it is reused only after that scan (the current stream — the one the new
+    prep is made on — waits on the event the last scan of the slot recorded)."""
     i = _S3_SLOTS["next"]
     _S3_SLOTS["next"] = (i + 1) % S3_SLOT_RING
-    return f"k{i}"
+    slot = f"k{i}"
+    ev = _S3_SLOT_LAST.pop(slot, None)
+    if ev is not None:
+        torch.cuda.current_stream(device).wait_event(ev)
+    return slot
+
+
+def _s3_mark_read(sp: "Scan3Prep") -> None:
+    """Record that a scan on the current stream read ``sp``'s ring slot (if it has one)."""
+    slot = getattr(sp, "slot", None)
+    if slot is not None and str(slot).startswith("k"):
+        ev = torch.cuda.Event()
+        ev.record()
+        _S3_SLOT_LAST[str(slot)] = ev
 
 
 # The scanner's per-row c granules {epoch, c} (one buffer per stream): zeroed when
@@ -415,7 +470,7 @@ def _s3_run_ptrs(sp: "Scan3Prep", dev, stream: int):
             gran = _s3_granules(dev, n, stream)
             run.append(gran[0])
         else:
-            run.append(_workspace(dev, n, key=f"s3_{S3_BUFS[i]}@{stream}"))
+            run.append(_workspace(dev, n, key=f"s3_{S3_BUFS[i]}@{stream}", per_stream=False))
     ptrs = (ctypes.c_void_p * len(S3_BUFS))(*([b.data_ptr() for b in sp.bufs[:4]] +
                                               [b.data_ptr() for b in run]))
     if len(_S3_RUN_CACHE) > 256:
@@ -450,7 +505,7 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
                                 st.cuda_stream), "omldm_scan3_prepare")
     ev = torch.cuda.Event()  # pipelines on other streams that reuse the prep wait on it
     ev.record(st)
-    return Scan3Prep(bufs, ptrs, _s3_key(batch, R, S, dim, bias, rule), ev)
+    return Scan3Prep(bufs, ptrs, _s3_key(batch, R, S, dim, bias, rule), ev, slot)
 
 
 def scan3_part_bounds(dim: int, dn: int, dc: int, part: int, parts: int,
@@ -486,7 +541,7 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
     key = _s3_key(batch, R, S, dim, rule.bias, rule)
     if not (isinstance(sp, Scan3Prep) and sp.key == key):
         sp = linear_scan3_prepare(batch, R, S, dim, bool(rule.bias), rule, hashed=hashed,
-                                  slot=_s3_slot_for(key))
+                                  slot=_s3_slot_for(key, w.device))
         batch.prep = sp  # the next pipeline of the tick reuses it (same key)
     elif sp.event is not None:
         torch.cuda.current_stream(w.device).wait_event(sp.event)
@@ -513,6 +568,7 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
         check(rc, "omldm_scan3_run")
         if on_part is not None:
             on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts, span))
+    _s3_mark_read(sp)
 
 
 def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,

@@ -44,7 +44,8 @@ HIP_SIGS = [
     ("omldm_linear_round", i32, [vp, i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, i32, vp, i32,
                                  vp,
                                  vp, vp, i32, i32, f32, f32, f32, f32, f32, i32, i32, i32, i32,
-                                 i32, i32, f32, vp]),
+                                 i32, i32, f32, vp, i32, vp]),
+    ("omldm_spill_words", i64, [i32, i32, i32]),
     ("omldm_linear_reduce_part", i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32,
                                        i32, i32, i32, vp]),
     ("omldm_linear_part_bounds", i32, [i32, i32, i32, vp]),
@@ -79,6 +80,8 @@ HIP_SIGS = [
     ("omldm_scan3_set_prep_split", None, [i32]),
     ("omldm_scan3_get_comb", i32, []),
     ("omldm_scan3_comb_err", i32, []),
+    ("omldm_scan3_comb_err_drain", i32, [vp, vp]),
+    ("omldm_scan3_teardown", i32, []),
     ("omldm_scan3_part_bounds", i32, [i32, i32, i32, i64, i32, i32, vp]),
     ("omldm_scan3_stamps", i32, [vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),
@@ -93,7 +96,7 @@ HIP_SIGS = [
     ("omldm_kmeans_assign", i32, [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
     ("omldm_kmeans_apply", i32, [vp, vp, i32, i32, vp, vp, vp, vp, vp]),
     ("omldm_multiclass_round", i32, [vp, i32, vp, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32,
-                                     i32, i32, i32, f32, i32, vp, vp, i32, vp, vp, vp]),
+                                     i32, i32, i32, f32, i32, vp, vp, i32, vp, vp, vp, i32, vp]),
     ("omldm_multiclass_apply", i32, [vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, i32, vp, vp]),
     ("omldm_mlp_lds_bytes", i64, [i32, vp]),
     ("omldm_mlp_round", i32, [vp, vp, vp, i64, i32, i32, i32, vp, i32, i32, f32, vp, vp, vp, vp,
@@ -227,7 +230,21 @@ def hip() -> _Lib:
                         f"{HIP_LIB_PATH} missing: the HIP kernels are required on GPU; "
                         "run python -m omldm_amd._build")
                 _hip = _Lib(HIP_LIB_PATH, HIP_SIGS)
+                import atexit
+
+                atexit.register(_hip_teardown)
     return _hip
+
+
+def _hip_teardown() -> None:
+    """Destroy the streams / events the kernel library created on demand while the HIP
+    runtime is still up (Python's atexit runs before the shared libraries' finalizers)."""
+    lib = _hip
+    if lib is not None and getattr(lib, "omldm_scan3_teardown", None) is not None:
+        try:
+            lib.omldm_scan3_teardown()
+        except Exception:  # noqa: BLE001 - best effort at exit
+            pass
 
 
 def check(rc: int, what: str) -> None:

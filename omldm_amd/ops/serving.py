@@ -3,8 +3,9 @@
 One resident wavefront polls a coherent pinned host mailbox; a request is a host write
 + sequence bump, the answer comes back through the same mailbox — no kernel launch or
 stream synchronisation on the request path. The wave exits on ``stop()`` or after its
-lifetime; weights it reads may lag training updates by at most one lifetime (relaunch
-after model syncs for fresher serving).
+lifetime. It reads one of two weight banks (``w`` / ``w1``), chosen per request: a
+publisher writes new models into the bank no request reads and switches requests over
+once the copy is complete (engine/forecast_server.py), so an answer never mixes versions.
 """
 from __future__ import annotations
 
@@ -19,11 +20,11 @@ from omldm_amd.ops.native import check, ptr
 SIGS = [
     ("omldm_mailbox_alloc", C.c_void_p, []),
     ("omldm_mailbox_free", None, [C.c_void_p]),
-    ("omldm_serve_start", C.c_int, [C.c_void_p, C.c_int, C.c_longlong, C.c_int, C.c_int, C.c_int,
-                                    C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_longlong,
-                                    C.c_void_p]),
+    ("omldm_serve_start", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_longlong, C.c_int,
+                                    C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                    C.c_longlong, C.c_void_p]),
     ("omldm_serve_request", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
-                                      C.c_int, C.c_void_p, C.c_longlong]),
+                                      C.c_int, C.c_void_p, C.c_longlong, C.c_int]),
     ("omldm_serve_stop", None, [C.c_void_p]),
     ("omldm_serve_alive", C.c_int, [C.c_void_p]),
     ("omldm_serve_exit_reason", C.c_int, [C.c_void_p]),
@@ -41,10 +42,15 @@ def _lib():
 
 
 class PredictServer:
-    def __init__(self, w: torch.Tensor, dn: int, dc: int, bias: bool = True, cat_span: int = 0):
+    def __init__(self, w: torch.Tensor, dn: int, dc: int, bias: bool = True, cat_span: int = 0,
+                 w1: torch.Tensor | None = None):
         assert w.is_cuda
         self.lib = _lib()
         self.W = w if w.dim() == 2 else w.unsqueeze(0)
+        self.W1 = None if w1 is None else (w1 if w1.dim() == 2 else w1.unsqueeze(0))
+        assert self.W1 is None or (self.W1.shape == self.W.shape and
+                                   self.W1.stride() == self.W.stride() and
+                                   self.W1.dtype == self.W.dtype)
         self.M, self.dim = int(self.W.shape[0]), int(self.W.shape[1])
         self.dn, self.dc, self.bias, self.cspan = dn, dc, bias, cat_span
         self.mb = self.lib.omldm_mailbox_alloc()
@@ -60,7 +66,8 @@ class PredictServer:
         self.out = (C.c_float * self.M)()
 
     def start(self, lifetime_us: int = 10_000_000) -> None:
-        check(self.lib.omldm_serve_start(ptr(self.W), int(self.W.dtype == torch.bfloat16),
+        check(self.lib.omldm_serve_start(ptr(self.W), ptr(self.W1),
+                                         int(self.W.dtype == torch.bfloat16),
                                          self.W.stride(0), self.M, self.dn, self.dc, self.dim,
                                          int(self.bias), self.cspan, self.mb, int(lifetime_us),
                                          self.stream.cuda_stream), "omldm_serve_start")
@@ -72,21 +79,22 @@ class PredictServer:
                 raise RuntimeError("serving wave did not start")
             time.sleep(1e-4)
 
-    def request_raw(self, num_ptr: int, cat_ptr: int, timeout_us: int = 1_000_000) -> list[float]:
+    def request_raw(self, num_ptr: int, cat_ptr: int, timeout_us: int = 1_000_000,
+                    bank: int = 0) -> list[float]:
         rc = self.lib.omldm_serve_request(self.mb, num_ptr, self.dn, cat_ptr, self.dc, self.M,
-                                          self.out, timeout_us)
+                                          self.out, timeout_us, int(bank))
         if rc:
             raise TimeoutError("serving wave did not answer")
         return list(self.out)
 
-    def request(self, point: HashedBatch) -> list[float]:
+    def request(self, point: HashedBatch, bank: int = 0) -> list[float]:
         """Scores of one point (row 0 of a host batch) against the M models."""
         num = point.num[0].float().contiguous()
         cat = point.cat[0].to(torch.int64)
         if point.cat_span:
             cat = cat & 0xFFFF
         cat = cat.to(torch.int32).contiguous()
-        return self.request_raw(num.data_ptr(), cat.data_ptr())
+        return self.request_raw(num.data_ptr(), cat.data_ptr(), bank=bank)
 
     def stop(self) -> None:
         self.lib.omldm_serve_stop(self.mb)

@@ -32,6 +32,7 @@ import os
 import shutil
 import threading
 import time
+import uuid
 
 import torch
 
@@ -59,8 +60,11 @@ class Checkpointer:
     KEEP = 3
     WAIT_S = 600.0  # rank 0's writer waits this long for the other ranks' files
 
-    def __init__(self, cfg, rank: int, world: int):
+    def __init__(self, cfg, rank: int, world: int, nonce: str | None = None):
         self.root = _root(cfg.stateBackend)
+        # one value per job run (rank 0's, broadcast by the Job): a done marker an earlier
+        # process left at the same index and tick can never match this run's attempt tag
+        self.nonce = nonce or uuid.uuid4().hex
         self.interval = cfg.checkInterval / 1000.0
         self.rank, self.world = rank, world
         self.export = bool(getattr(cfg, "checkpointExport", True))
@@ -98,7 +102,7 @@ class Checkpointer:
         # every rank saves at the same tick (rank 0's clock, carried in the tick flags):
         # the marker names the attempt, so files a crashed earlier attempt left in this
         # directory never complete the manifest
-        meta["attempt"] = f"{self.n}:{job.ticks}"
+        meta["attempt"] = f"{self.nonce}:{self.n}:{job.ticks}"
         self.wait()
         self._writer = threading.Thread(target=self._write, args=(d, sd, models, meta),
                                          name=f"omldm-ckpt-{self.n}", daemon=True)

@@ -91,7 +91,7 @@ def test_stale_done_markers_do_not_complete_a_manifest(tmp_path):
         def state_dict(self):
             return {"w": torch.ones(3)}
 
-    ck = Checkpointer(Cfg(), 0, 2)
+    ck = Checkpointer(Cfg(), 0, 2, nonce="run2")
     ck.WAIT_S = 0.5
     d = tmp_path / "ckpt-000000"
     d.mkdir()
@@ -105,7 +105,19 @@ def test_stale_done_markers_do_not_complete_a_manifest(tmp_path):
         assert "did not finish" in str(e)
     assert not (d / "manifest.json").exists()
     # the live rank 1 of the same attempt completes it
-    ck1 = Checkpointer(Cfg(), 1, 2)
+    # an earlier RUN's marker for the same index and tick (a deterministic replay reaches
+    # index 0 at tick 7 again) does not match this run's attempt either
+    (d / "rank-1.done").write_text("run1:0:7")
+    ck.n = 0
+    ck.save(FakeJob())
+    try:
+        ck.wait()
+        raise AssertionError("rank 0 published a manifest from an earlier run's marker")
+    except RuntimeError as e:
+        assert "did not finish" in str(e)
+    assert not (d / "manifest.json").exists()
+    # the live rank 1 of the same attempt (same run nonce, broadcast by the Job) completes it
+    ck1 = Checkpointer(Cfg(), 1, 2, nonce="run2")
     ck1.n = 0
     ck.n = 0
     ck.WAIT_S = 30
@@ -114,4 +126,4 @@ def test_stale_done_markers_do_not_complete_a_manifest(tmp_path):
     ck1.wait()
     ck.wait()
     man = json.loads((d / "manifest.json").read_text())
-    assert man["attempt"] == "0:7" and man["world"] == 2
+    assert man["attempt"] == "run2:0:7" and man["world"] == 2

@@ -142,3 +142,55 @@ def test_default_flag_svm_trains_through_the_v3_scan():
     assert L.SCAN3_ROUNDS > n0
     assert job.pipes[1].learner.running_totals()["fitted"] > 0
     job.fserver.close()
+
+
+def test_wave_reads_the_requested_bank():
+    """The resident wave scores against the weight bank each request names (the request
+    line's last dword, checksummed): bank 0 / bank 1 answers are those of w0 / w1."""
+    from omldm_amd.io.synthetic import synth_batch
+    from omldm_amd.ops import linear as L
+    from omldm_amd.ops.serving import PredictServer
+
+    b = synth_batch(SP, 8, seed=3)
+    w0 = torch.randn(2, SP.dim) * 0.1
+    w1 = torch.randn(2, SP.dim) * 0.1
+    srv = PredictServer(w0.cuda(), SP.dn, SP.dc, True, cat_span=0, w1=w1.cuda())
+    srv.start(lifetime_us=5_000_000)
+    try:
+        for i in range(8):
+            pt = b.slice(i, i + 1)
+            for bank, w in ((0, w0), (1, w1), (0, w0)):
+                got = torch.tensor(srv.request(pt, bank=bank))
+                want = L.linear_predict(w, pt)[0]
+                assert torch.allclose(got, want, rtol=1e-5, atol=1e-5), (i, bank, got, want)
+    finally:
+        srv.close()
+
+
+def test_forecasts_read_a_published_model_version():
+    """Between ticks the lane's answers equal the batched predict of the model after the
+    last round (the publish copy adopted once complete); the banks alternate per round, and
+    the live store rows are never what the wave reads."""
+    job, br = _job()
+    _create(br, 1, "SVM")
+    fs = job.fserver
+    banks_seen = set()
+    for t in range(5):
+        for r in synth_json_records(2000, SP, start=t * 2000):
+            br.produce("trainingData", r)
+        job.tick()
+        torch.cuda.synchronize()
+        assert fs._banks is not None and fs._banks[0].data_ptr() != job.store.W.data_ptr()
+        fc = synth_json_records(3, SP, start=90000 + 10 * t, operation="forecasting")
+        n0 = len(br.records("predictions"))
+        for r in fc:
+            br.produce("forecastingData", r)
+        assert fs.catch_up(10.0)
+        banks_seen.add(fs._bank)
+        preds = [json.loads(x) for x in br.records("predictions")[n0:]]
+        batch, _, _ = parse_records(fc, job.space)
+        want = job.pipes[1].predict(batch.without_raw().to("cuda")).float().cpu()
+        got = torch.tensor([p["prediction"] for p in preds])
+        assert torch.equal(got, want), (t, got, want)
+    assert banks_seen == {0, 1}
+    fs.close()
