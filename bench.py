@@ -187,9 +187,15 @@ def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dic
         else:
             uniq = [r.encode() for r in uniq]
         total = records + 4 * batch  # the untimed Create / warmup ticks read some first
+        import math
+
+        period = len(uniq) // math.gcd(parts, len(uniq))  # partition p replays uniq[p::parts]
         for p in range(parts):
-            recs = [uniq[i % len(uniq)] for i in range(p, total, parts)]
-            br.produce_block("trainingData", p, b"\n".join(recs) + b"\n")
+            n_p = len(range(p, total, parts))
+            cyc = b"".join(uniq[(p + parts * j) % len(uniq)] + b"\n" for j in range(period))
+            tail = b"".join(uniq[(p + parts * j) % len(uniq)] + b"\n"
+                            for j in range(n_p - n_p % period, n_p))
+            br.produce_block("trainingData", p, cyc * (n_p // period) + tail)
         br.produce("requests", json.dumps({"id": 1, "request": "Create",
                                            "learner": {"name": "SVM"},
                                            "trainingConfiguration": {"protocol": "Synchronous"}}))
@@ -207,19 +213,27 @@ def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dic
         for _ in range(2):  # staging slots grow to the record size
             job.tick()
         torch.cuda.synchronize(dev)
-        r0 = job.counters["records"]
+        from omldm_amd.utils import tracing
+
+        tracing.reset()
+        r0, k0 = job.counters["records"], job.ticks
         t0 = time.perf_counter()
         while job.counters["records"] + job.counters["invalid"] < r0 + records:
             job.tick()
         torch.cuda.synchronize(dev)
         wall = time.perf_counter() - t0
         n = job.counters["records"] - r0
+        ticks = job.ticks - k0
+        # host time per tick of every stage (tick thread; ingest_* on the reader / staging
+        # threads, which run beside it)
+        stages = {k: round(v["host_ms"] / max(1, ticks), 4) for k, v in tracing.report().items()}
         if job.fserver is not None:
             job.fserver.close()
         job.ingest.close()
         job.egress.close()
     return {"records_per_s": round(n / max(wall, 1e-9), 1), "records": n,
-            "spokes": job.spokes, "batch": batch,
+            "spokes": job.spokes, "batch": batch, "ticks": ticks,
+            "ms_per_tick": round(wall * 1e3 / max(1, ticks), 4), "stage_ms_per_tick": stages,
             "record_bytes": round(sum(len(r) + 1 for r in uniq) / len(uniq), 1)}
 
 
@@ -262,8 +276,9 @@ def main(argv=None) -> int:
     ap.add_argument("--ref", default="auto", choices=["auto", "on", "off"],
                     help="CPU reference-semantics accuracy on the same stream (rank 0)")
     ap.add_argument("--ref-max-examples", type=float, default=6e7)
-    ap.add_argument("--engine-e2e", type=int, default=1048576,
-                    help="JSON records timed through the whole engine (rank 0; 0 = skip)")
+    ap.add_argument("--engine-e2e", type=int, default=8388608,
+                    help="JSON (and DIB) records timed through the whole engine (rank 0; 0 = "
+                         "skip): 64 ticks of 131072 records, the steady state")
     ap.add_argument("--engine-latency", type=int, default=300,
                     help="forecasting records timed through the engine (rank 0; 0 = skip)")
     a = ap.parse_args(argv)
@@ -510,7 +525,7 @@ def main(argv=None) -> int:
     eng = engine_forecast_latency(a.engine_latency) if (rank == 0 and on_gpu and
                                                          a.engine_latency > 0) else None
     e2e = engine_e2e_rate(a.engine_e2e) if (rank == 0 and on_gpu and a.engine_e2e > 0) else None
-    e2e_dib = engine_e2e_rate(2 * a.engine_e2e, fmt="dib") if e2e is not None else None
+    e2e_dib = engine_e2e_rate(a.engine_e2e, fmt="dib") if e2e is not None else None
 
     total_examples = a.steps * B * world
     value = total_examples / elapsed
@@ -563,6 +578,9 @@ def main(argv=None) -> int:
             f"linear SVM fp32, {e2e['spokes']} spokes, {e2e['records']} records timed "
             f"(one GPU, rank 0), {e2e['record_bytes']} B/record",
             "engine_e2e_dib_records_per_s": None if e2e_dib is None else e2e_dib["records_per_s"],
+            "engine_e2e_stage_ms_per_tick": None if e2e is None else {
+                "json": {"ms_per_tick": e2e["ms_per_tick"], **e2e["stage_ms_per_tick"]},
+                "dib": {"ms_per_tick": e2e_dib["ms_per_tick"], **e2e_dib["stage_ms_per_tick"]}},
             "engine_e2e_dib_semantics": None if e2e_dib is None else
             f"the same records as binary DIB records ({e2e_dib['record_bytes']} B/record, "
             f"omldm_amd/io/dib.py) through the same engine path, {e2e_dib['records']} timed",

@@ -330,8 +330,36 @@ class Scan3Prep:
     slot: object = None  # workspace set (ring slot "k<i>" for inline preps)
 
 
+# v3 table-scan kernel generation: 4 = the split spoke (a scanner and a table workgroup per
+# spoke, csrc/kernels/linear_scan3.hip: s4_scan_kernel), 3 = one workgroup per spoke with
+# in-launch combiners (the A/B reference). Fixed per process before the first prepare.
+S3_MODE = int(os.environ.get("OMLDM_S3_MODE", "4"))
+_S3_MODE_SET = {"done": False}
+
+
+def _s3_lib():
+    h = native.hip()
+    if not _S3_MODE_SET["done"]:
+        h.omldm_scan3_set_mode(S3_MODE)
+        _S3_MODE_SET["done"] = True
+    return h
+
+
+def set_scan3_mode(mode: int) -> int:
+    """Switch the v3/v4 round generation (tests, A/B); returns the previous one. The
+    device must be idle: preps made for the other layout are dropped with the caches."""
+    global S3_MODE
+    old = S3_MODE
+    S3_MODE = 3 if int(mode) == 3 else 4
+    native.hip().omldm_scan3_set_mode(S3_MODE)
+    _S3_MODE_SET["done"] = True
+    _S3_WS_CACHE.clear()
+    _S3_RUN_CACHE.clear()
+    return old
+
+
 def scan3_fits(dn: int, dc: int, R: int, bias: bool) -> bool:
-    return bool(native.hip().omldm_scan3_fits(int(dn), int(dc), int(R), int(bias)))
+    return bool(_s3_lib().omldm_scan3_fits(int(dn), int(dc), int(R), int(bias)))
 
 
 def scan3_eligible(batch: RawBatch, R: int, bias: bool) -> bool:
@@ -364,7 +392,7 @@ def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
     through PA-II's 1/(2C)) — pipelines that differ in C share one prep."""
     c = float(rule.C) if rule.variant == PA2 else None
     return (batch.B, R, S, dim, bool(bias), rule.rule == RULE_LOGISTIC, rule.variant == PA2, c,
-            batch.dn, batch.dc, int(batch.span), batch.y.data_ptr(), batch.tok.data_ptr())
+            batch.dn, batch.dc, int(batch.span), batch.y.data_ptr(), batch.tok.data_ptr(), S3_MODE)
 
 
 _S3_WS_CACHE: dict = {}
@@ -375,8 +403,8 @@ def _s3_workspaces(dev, B, R, S, dn, dc, span, bias, slot):
     lookup + ctypes array were a per-tick host cost); refreshed if a workspace moved."""
     import ctypes
 
-    h = native.hip()
-    key = (str(dev), B, R, S, dn, dc, span, bias, slot)
+    h = _s3_lib()
+    key = (str(dev), B, R, S, dn, dc, span, bias, slot, S3_MODE)
     hit = _S3_WS_CACHE.get(key)
     bufs = []
     for i, name in enumerate(S3_BUFS):
@@ -486,7 +514,7 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
     current stream; an event marks completion when a stream is given). ``batch.tok``:
     32-bit category tokens, (``hashed``) int32 field-aware signed slots, or (``batch.span``
     > 0) the compact int16 field-aware slots of the engine's wire, row-major."""
-    h = native.hip()
+    h = _s3_lib()
     if "OMLDM_S3_GRAM_VALU" in os.environ:  # A/B: pass 3 on the VALU reference kernel
         h.omldm_scan3_set_gram_valu(int(os.environ["OMLDM_S3_GRAM_VALU"]))
     if "OMLDM_S3_PREP_SPLIT" in os.environ:  # A/B: 0 = flags and Grams on one stream
@@ -547,7 +575,7 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
         torch.cuda.current_stream(w.device).wait_event(sp.event)
     global SCAN3_ROUNDS
     SCAN3_ROUNDS += 1
-    h = native.hip()
+    h = _s3_lib()
     if SCAN3_ROUNDS == 1 and "OMLDM_S3_COMB" in os.environ:  # A/B: 0 = combine after the scan
         h.omldm_scan3_set_comb(int(os.environ["OMLDM_S3_COMB"]))
     parts = max(1, int(parts))

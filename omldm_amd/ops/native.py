@@ -82,6 +82,8 @@ HIP_SIGS = [
     ("omldm_scan3_comb_err", i32, []),
     ("omldm_scan3_comb_err_drain", i32, [vp, vp]),
     ("omldm_scan3_teardown", i32, []),
+    ("omldm_scan3_set_mode", None, [i32]),
+    ("omldm_scan3_get_mode", i32, []),
     ("omldm_scan3_part_bounds", i32, [i32, i32, i32, i64, i32, i32, vp]),
     ("omldm_scan3_stamps", i32, [vp]),
     ("omldm_colstats_update", i32, [vp, i32, i32, C.c_double, vp, vp, vp, vp, i32, vp, i32, vp]),

@@ -57,7 +57,9 @@ def test_hip_linear_round_spills_exactly(cuda, R, name, dtype):
     assert float(s_g[:, 5].sum()) == 0.0 and float(cum[5]) == 0.0  # nothing dropped
     np.testing.assert_allclose(s_g[:, 1].numpy(), s_cpu[:, 1].numpy())
     np.testing.assert_allclose(s_g[:, 2].numpy(), s_cpu[:, 2].numpy(), atol=2)
-    np.testing.assert_allclose(d_gpu.cpu().numpy(), d_cpu.numpy(), rtol=2e-3, atol=2e-5)
+    # fp32 summation order differs (Pegasos' first steps are η = 1/(λT) ~ 5e3: scale atol)
+    atol = 2e-5 * max(1.0, float(d_cpu.abs().max()))
+    np.testing.assert_allclose(d_gpu.cpu().numpy(), d_cpu.numpy(), rtol=2e-3, atol=atol)
     # a second round on the same (restored) spill region gives the same answer
     d2 = torch.zeros(BIG.dim + 2, device=cuda)
     L.linear_round(w.to(cuda), b.to(cuda), R, S, d2, None, rule, 1.0 / S)
