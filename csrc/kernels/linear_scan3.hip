@@ -81,33 +81,21 @@ constexpr int DS = KNMAX;                  // per-spoke dense delta row
 // meta word of one occurrence: flags | sign | table id
 constexpr uint32_t F_TG = 1u;              // margin reads the table (else w)
 constexpr uint32_t F_INIT = 2u;            // first occurrence: writes w[slot] into the table
-constexpr uint32_t F_SCAT = 4u;            // v3: the slot recurs ≥ 2 chunks later: add c·sign
-                                           // v4: the slot has a table id (every c·sign → table)
-constexpr uint32_t F_LAST = 16u;           // v4: the table slot's last occurrence (flush Δ)
+constexpr uint32_t F_SCAT = 4u;            // the slot recurs ≥ 2 chunks later: add c·sign
 constexpr uint32_t F_SIGN = 8u;
 constexpr int LID_SHIFT = 10;
-constexpr uint32_t F_MASK = (1u << LID_SHIFT) - 1u;
 }  // namespace s3
 
-// floats of one chunk's prep block: aG | aX1 [| aX2] | a | dense columns transposed
-// [KN][64] | y (the target as fp32, NaN for a row without one or past the shard: the
-// scanner reads it a chunk ahead with no conversion — an int8 label's convert made it wait
-// for the load). NX cross Grams: 1 (v3: X1 = X_k X_{k−1}ᵀ) or 2 (v4: also X2 = X_k X_{k−2}ᵀ).
-template <int KN, int NX = 1>
+// floats of one chunk's prep block: aG | aX1 | a | dense columns transposed [KN][64] | y
+// (the target as fp32, NaN for a row without one or past the shard: the scanner reads it
+// a chunk ahead with no conversion — an int8 label's convert made it wait for the load)
+template <int KN>
 __host__ __device__ constexpr int s3_prep_floats() {
-  return (1 + NX) * s3::MAT + s3::CH + KN * s3::CH + s3::CH;
+  return 2 * s3::MAT + s3::CH + KN * s3::CH + s3::CH;
 }
-template <int KN, int NX = 1>
+template <int KN>
 __host__ __device__ constexpr int s3_prep_y() {
-  return (1 + NX) * s3::MAT + s3::CH + KN * s3::CH;
-}
-template <int NX = 1>
-__host__ __device__ constexpr int s3_prep_a() {
-  return (1 + NX) * s3::MAT;
-}
-template <int NX = 1>
-__host__ __device__ constexpr int s3_prep_dense() {
-  return (1 + NX) * s3::MAT + s3::CH;
+  return 2 * s3::MAT + s3::CH + KN * s3::CH;
 }
 
 __device__ __forceinline__ void spoke_rows(int s, int R, int B, int& t0, int& t1) {
@@ -164,10 +152,9 @@ constexpr int HCAP = 12288;                // hash entries (≤ 8192 distinct sl
 constexpr int RPT = RMAX / FT;             // rows per thread (8)
 }  // namespace s3
 
-// DIST = 2 (v3): a table slot recurs ≥ 2 chunks apart; F_SCAT marks occurrences whose slot
-// recurs ≥ 2 chunks later. DIST = 3 (v4): ≥ 3 chunks apart; every occurrence of a table slot
-// carries F_SCAT (its c·sign goes to the table) and the last one F_LAST.
-template <int DIST>
+// M32 (round mode 4): the meta words alone, [dc][B] uint32 (the scan's helpers need no slot:
+// the round-start weights come from the w0-margin workgroups, s3_rare); else {slot, meta}.
+template <bool M32>
 __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict__ slotsT, int B,
                                                           int R, uint32_t* __restrict__ meta,
                                                           int* __restrict__ lidcount) {
@@ -219,7 +206,7 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
     bool take = false;
     if (h[q] >= 0) {
       const int first = (int)hfirst[h[q]], last = (int)hlast[h[q]];
-      take = i == first && (last >> 6) - (first >> 6) >= DIST;
+      take = i == first && (last >> 6) - (first >> 6) >= 2;
     }
     const unsigned long long mask = __ballot(take);
     int wbase = 0;
@@ -249,19 +236,15 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
       const int first = (int)hfirst[h[q]], last = (int)hlast[h[q]];
       const int ch = i >> 6;
       m = v[q] < 0 ? s3::F_SIGN : 0u;
-      if ((last >> 6) - (first >> 6) >= DIST) {
+      if ((last >> 6) - (first >> 6) >= 2) {
         if (ch > (first >> 6)) m |= s3::F_TG;
         if (i == first) m |= s3::F_INIT;
-        if constexpr (DIST == 2) {
-          if ((last >> 6) >= ch + 2) m |= s3::F_SCAT;
-        } else {
-          m |= s3::F_SCAT;
-          if (i == last) m |= s3::F_LAST;
-        }
+        if ((last >> 6) >= ch + 2) m |= s3::F_SCAT;
         m |= (uint32_t)(base + hkey[h[q]]) << s3::LID_SHIFT;
       }
     }
-    out[i] = make_uint2((uint32_t)v[q], m);
+    if constexpr (M32) meta[(size_t)f * B + t0 + i] = m;
+    else out[i] = make_uint2((uint32_t)v[q], m);
   }
 }
 
@@ -381,7 +364,7 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
 // (exact small integers), then v_mfma_f32_32x32x2_f32 adds the dense Gram x_i·x_j over
 // the KN columns. Tiles: aX1 (d = 1) tile (w >> 1, w & 1); aG (d = 0) tiles (0,0), (1,0),
 // (1,1) on waves 0-2 (wave 3's upper-right aG tile is all zero).
-template <int KN, int NX = 1>
+template <int KN>
 __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict__ slotsT, int dc,
                                                            const float* __restrict__ num, int dn,
                                                            const void* __restrict__ yv, int y8,
@@ -393,14 +376,14 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
   int t0, t1;
   spoke_rows(s, R, B, t0, t1);
   if (t0 + c * s3::CH >= t1) return;
-  constexpr int PF = s3_prep_floats<KN, NX>();
+  constexpr int PF = s3_prep_floats<KN>();
   float* out = prep + ((size_t)s * nchs + c) * PF;
-  __shared__ alignas(16) int sl[1 + NX][s3::MAXF][s3::CH + 4];
-  __shared__ float xn[1 + NX][s3::CH][KN + 1];
+  __shared__ alignas(16) int sl[2][s3::MAXF][s3::CH + 4];
+  __shared__ float xn[2][s3::CH][KN + 1];
   __shared__ float sa[s3::CH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // ---- all loads in flight at once (clamped addresses, results selected after)
-  constexpr int NSL = (1 + NX) * s3::MAXF * s3::CH / 256, NXN = (1 + NX) * s3::CH * KN / 256;
+  constexpr int NSL = 2 * s3::MAXF * s3::CH / 256, NXN = 2 * s3::CH * KN / 256;
   int sv[NSL];
   float xv[NXN];
 #pragma unroll
@@ -444,25 +427,23 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
     float a = 0.f;
     if (live) a = affine ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : 1.f;
     sa[tid] = a;
-    out[s3_prep_a<NX>() + tid] = a;
-    out[s3_prep_y<KN, NX>() + tid] =
-        live ? load_y(yv, t0 + c * s3::CH + tid, y8) : __builtin_nanf("");
+    out[2 * s3::MAT + tid] = a;
+    out[s3_prep_y<KN>() + tid] = live ? load_y(yv, t0 + c * s3::CH + tid, y8) : __builtin_nanf("");
   }
   for (int i = tid; i < KN * s3::CH; i += 256) {
     const int j = i / s3::CH, r = i - j * s3::CH;
-    out[s3_prep_dense<NX>() + i] = xn[0][r][j];
+    out[2 * s3::MAT + s3::CH + i] = xn[0][r][j];
   }
   __syncthreads();
   const int l31 = lane & 31, hi = lane >> 5;
 #pragma unroll 1
-  for (int pass = 0; pass < 1 + NX; ++pass) {
-    // passes 0 .. NX − 1: the aX(d) tile (d = pass + 1) of this wave; pass NX: its aG tile
-    const bool gpass = pass == NX;
-    const int d = gpass ? 0 : pass + 1;
+  for (int pass = 0; pass < 2; ++pass) {
+    // pass 0: the aX1 tile (d = 1) of this wave; pass 1: its aG tile (d = 0)
+    const int d = pass == 0 ? 1 : 0;
     // aG tiles: wave 0 (0,0), 1 (32,0), 2 (32,32), 3 (0,32) — the all-zero upper right
-    const int I0 = !gpass ? 32 * (wave >> 1) : ((wave == 1 || wave == 2) ? 32 : 0);
-    const int J0 = !gpass ? 32 * (wave & 1) : (wave >= 2 ? 32 : 0);
-    const bool zero = (gpass && wave == 3) || c - d < 0;
+    const int I0 = pass == 0 ? 32 * (wave >> 1) : ((wave == 1 || wave == 2) ? 32 : 0);
+    const int J0 = pass == 0 ? 32 * (wave & 1) : (wave >= 2 ? 32 : 0);
+    const bool zero = (pass == 1 && wave == 3) || c - d < 0;
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
@@ -566,10 +547,11 @@ constexpr unsigned SPIN_MAX = 1u << 21;      // polls before a combiner gives up
 // chunk, fell behind: its slot loads and its poll were one round trip each per chunk). All
 // of a chunk's slot loads are issued before the poll. Rows with c = 0 add nothing.
 __device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int dc, int B, int R,
-                                           const S3Comb& cb, S3Smem& sm) {
-  const int i = (int)blockIdx.x - cb.S_act;
+                                           const S3Comb& cb, S3Smem& sm, int base, int bid,
+                                           int nblk) {
+  const int i = bid - base;
   const int s = i % cb.S_act, part = i / cb.S_act;
-  const int nparts = ((int)gridDim.x - cb.S_act) / cb.S_act;
+  const int nparts = (nblk - base) / cb.S_act;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int* hk = reinterpret_cast<int*>(&sm.G[0][0][0]);
   float* hv = &sm.X1[0][0][0];
@@ -637,6 +619,76 @@ __device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int d
   }
 }
 
+// The w0-margin workgroup of a spoke (round mode 4). Mode 4's slot table holds the spoke's
+// DELTAS (zeroed at a slot's first occurrence, c·sign added by the scatter), so every
+// occurrence's round-start weight w0[slot] is model-independent within the round: this
+// workgroup gathers them for every chunk of its spoke, sums them per row and publishes the sum
+// as a granule {epoch, Σ ±w0} — it depends on nothing in the round and runs ahead of the
+// scan. The scan workgroup's helpers then issue no global gathers at all and read 4-byte meta
+// words (flags, sign, table id) instead of {slot, meta}. Fields f ≡ wave (mod 12); a chunk's
+// slots are loaded and its gathers issued a chunk ahead of their sum.
+namespace s3 {
+constexpr int NWR = NH + 1;                   // waves of the w0 workgroup (the block's)
+constexpr int NFR = (MAXF + NWR - 1) / NWR;  // fields per wave
+}  // namespace s3
+
+__device__ __forceinline__ void s3_rare(const int* __restrict__ slotsT, int dc, int B, int R,
+                                        const float* __restrict__ w, const S3Comb& cb,
+                                        unsigned long long* __restrict__ rgran, S3Smem& sm, int s) {
+  const int tid = threadIdx.x, r = tid & 63;
+  const int q = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  if (t0 >= t1) return;
+  const int nch = (t1 - t0 + s3::CH - 1) / s3::CH;
+  float (*part)[s3::NWR][s3::CH] = reinterpret_cast<float (*)[s3::NWR][s3::CH]>(&sm.G[0][0][0]);
+  const unsigned long long tag = (unsigned long long)cb.epoch << 32;
+  struct Set {
+    int cs[s3::NFR];
+    float g[s3::NFR];
+  };
+  auto load_slots = [&](int ch, Set& S) {
+#pragma unroll
+    for (int i = 0; i < s3::NFR; ++i) {
+      const int f = q + s3::NWR * i;
+      const int row = t0 + ch * s3::CH + r;
+      const bool ok = ch < nch && f < dc && row < t1;
+      const int v = slotsT[ok ? (size_t)f * B + row : 0];
+      S.cs[i] = ok ? v : -1;
+    }
+  };
+  auto issue_gathers = [&](Set& S) {
+#pragma unroll
+    for (int i = 0; i < s3::NFR; ++i) S.g[i] = w[S.cs[i] != -1 ? (S.cs[i] & 0x7fffffff) : 0];
+  };
+  auto body = [&](int k, Set& CUR, Set& NXT) {
+    load_slots(k + 1, NXT);
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < s3::NFR; ++i)
+      if (CUR.cs[i] != -1) m += CUR.cs[i] < 0 ? -CUR.g[i] : CUR.g[i];
+    part[k & 1][q][r] = m;
+    issue_gathers(NXT);
+    __syncthreads();
+    if (q == 0) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < s3::NWR; ++j) v += part[k & 1][j][r];
+      const int row = t0 + k * s3::CH + r;
+      if (row < t1)
+        __hip_atomic_store((s3_gu64*)(rgran + row), tag | __float_as_uint(v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  Set A, Bs;
+  load_slots(0, A);
+  issue_gathers(A);
+  for (int k = 0; k < nch; k += 2) {
+    body(k, A, Bs);
+    if (k + 1 < nch) body(k + 1, Bs, A);
+  }
+}
+
 // Forward: the tail body (defined with the combine pass below).
 __device__ void s3_dense_body(const float* __restrict__ ws, const float* __restrict__ wsd,
                               int S_act, int dn, int dim, int bias, float inv_p,
@@ -650,8 +702,9 @@ __device__ void s3_dense_body(const float* __restrict__ ws, const float* __restr
 // (the flag lives in S3Smem: the kernel's static + dynamic LDS is exactly 160 KB)
 __device__ __forceinline__ void s3_scan_arrive(const S3Comb& cb, const float* __restrict__ ws,
                                                const float* __restrict__ wsd, int dn, int dim,
-                                               const SeqParams& p, int& s_last) {
+                                               const SeqParams& p, S3Smem& sm) {
   if (cb.arrive == nullptr) return;
+  int& s_last = sm.last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -676,28 +729,37 @@ __device__ __forceinline__ void s3_scan_arrive(const S3Comb& cb, const float* __
     s3_dense_body(ws, wsd, cb.S_act, dn, dim, p.bias, p.inv_p, cb.dacc, cb.cum);
 }
 
-template <int RULE, int KN>
-__global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s3_scan_kernel(
+// RARE (round mode 4): blocks [S_act, 2·S_act) are the spokes' rare-slot workgroups
+// (s3_rare above) and the combiners follow them; the scanner adds each row's rare margin
+// from its granule (rgran), the helpers gather only the table slots' first occurrences.
+// One pipeline's workgroup `bid` of the round (`nblk` per pipeline): [0, S_act) the scan
+// workgroups, [S_act, 2·S_act) the rare-slot ones (RARE), then the combiners.
+template <int RULE, int KN, bool RARE>
+__device__ __forceinline__ void s3_scan_body(
+    int bid, int nblk, S3Smem& sm, float* tab,
     const int* __restrict__ slotsT, const uint32_t* __restrict__ meta, int dc, int dn,
     const void* __restrict__ yv, int B, int R, const float* __restrict__ prep, int nchs,
     const float* __restrict__ w, int dim, float* __restrict__ aglob, int cap, long long gstride,
-    S3Comb cb, float* __restrict__ ws, float* __restrict__ wsd, SeqParams p) {
-  __shared__ S3Smem sm;
-  extern __shared__ float tab[];  // [cap] + 64 scratch words (one per lane)
+    const S3Comb& cb, float* __restrict__ ws, float* __restrict__ wsd, const SeqParams& p,
+    unsigned long long* __restrict__ rgran) {
   constexpr int PF = s3_prep_floats<KN>();
-  if ((int)blockIdx.x >= cb.S_act) {  // a combiner workgroup
-    s3_combine(slotsT, dc, B, R, cb, sm);
+  if (bid >= cb.S_act) {
+    if (RARE && bid < 2 * cb.S_act) {  // a rare-slot workgroup
+      s3_rare(slotsT, dc, B, R, w, cb, rgran, sm, bid - cb.S_act);
+      return;
+    }
+    s3_combine(slotsT, dc, B, R, cb, sm, (RARE ? 2 : 1) * cb.S_act, bid, nblk);  // a combiner
     return;
   }
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int s = blockIdx.x;
+  const int s = bid;
   int t0, t1;
   spoke_rows(s, R, B, t0, t1);
   if (t0 >= t1) {
     if (tid < s3::WS) ws[(size_t)s * s3::WS + tid] = 0.f;
     if (tid < s3::DS) wsd[(size_t)s * s3::DS + tid] = 0.f;
-    s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm.last);
+    s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
     return;
   }
   const int nch = (t1 - t0 + s3::CH - 1) / s3::CH;
@@ -816,7 +878,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       wr[6] = 0.f;
       wr[7] = 0.f;
     }
-    s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm.last);
+    s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
     return;
   }
 
@@ -853,9 +915,36 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     float g[s3::NF];
     f32x4 v[NV4];
     float xs[s3::NJ], xc[s3::NJ];  // dense columns of the chunk scattered / margined
+    unsigned long long rg;         // RARE, helper 0: the row's rare-slot margin granule
   };
   uint32_t p1[s3::NF], p2[s3::NF];  // meta of chunk k (scattered next) and k − 1
+  // RARE: helper 0 loads each chunk's rare-slot margins (s3_rare's granules) with its words
+  // — a chunk ahead, like every helper load, instead of the scanner waiting on L2 (measured:
+  // a granule loaded by the scanner one chunk ahead still stalled it ≈ 2.2 K cycles per
+  // chunk) — and folds them into its base-margin partial
+  const unsigned long long want = (unsigned long long)cb.epoch;
+  bool dead = false;
+  auto load_rare = [&](int ch) -> unsigned long long {
+    const int row = t0 + ch * s3::CH + r;
+    const bool ok = RARE && q == 0 && ch >= 0 && ch < nch && row < t1;
+    return ok ? __hip_atomic_load((s3_gu64*)(rgran + row), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT)
+              : (want << 32);
+  };
   auto load_words = [&](int ch, Set& S) {
+    if constexpr (RARE) {  // 4-byte meta words; cs = 0 marks a table-slot occurrence
+      S.rg = load_rare(ch);
+#pragma unroll
+      for (int i = 0; i < s3::NF; ++i) {
+        const int f = q + s3::NHA * i;
+        const int row = t0 + ch * s3::CH + r;
+        const bool ok = ch >= 0 && ch < nch && f < dc && row < t1;
+        const uint32_t mm = meta[ok ? (size_t)f * B + row : 0];
+        S.cm[i] = ok ? mm : 0u;
+        S.cs[i] = ok && (mm & (s3::F_TG | s3::F_INIT)) ? 0 : -1;
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
       const int f = q + s3::NHA * i;
@@ -868,9 +957,11 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     }
   };
   auto issue_gathers = [&](Set& S) {
+    if constexpr (RARE) return;  // no gathers in the scan workgroup (s3_rare)
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
-      const bool glob = S.cs[i] != -1 && !(S.cm[i] & s3::F_TG);
+      // RARE: no gathers here (s3_rare sums every occurrence's w0)
+      const bool glob = !RARE && S.cs[i] != -1 && !(S.cm[i] & s3::F_TG);
       S.g[i] = w[(glob && !dbg_gather) ? (S.cs[i] & 0x7fffffff) : 0];  // unused unless glob
     }
   };
@@ -946,6 +1037,21 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       float base = 0.f;
 #pragma unroll
       for (int i = 0; i < NJK; ++i) base = fmaf(CUR.xc[i], wn[i], base);
+      if constexpr (RARE) {
+        if (q == 0) {  // wave-uniform
+          for (unsigned spins = 0;
+               __builtin_amdgcn_ballot_w64((CUR.rg >> 32) != want) != 0ull;) {
+            if (dead || ++spins > s3::SPIN_MAX) {  // bounded: the flag fails the round
+              if (!dead && r == 0) atomicExch(&g_s3_comb_err, 2);
+              dead = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            CUR.rg = load_rare(cn);
+          }
+          base += (CUR.rg >> 32) == want ? __uint_as_float((uint32_t)CUR.rg) : 0.f;
+        }
+      }
       if constexpr (!SPILL) {
         // every field's table reads first, then the first-occurrence writes: within a
         // chunk a table entry is either read (the slot was seen in an earlier chunk) or
@@ -964,9 +1070,10 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
           const uint32_t m = CUR.cm[i];
           const bool here = CUR.cs[i] != -1;
           const bool tg = here && (m & s3::F_TG), init = here && !tg && (m & s3::F_INIT);
-          const float val = tg ? tv[i] : CUR.g[i];
+          // RARE: the table holds the spoke's deltas (zeroed at the first occurrence)
+          const float val = tg ? tv[i] : (RARE ? 0.f : CUR.g[i]);
           if (init) tab[(int)(m >> s3::LID_SHIFT)] = val;
-          if (here) base += (m & s3::F_SIGN) ? -val : val;
+          if (here && (!RARE || tg)) base += (m & s3::F_SIGN) ? -val : val;
         }
       }
 #pragma unroll
@@ -975,7 +1082,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         const bool here = CUR.cs[i] != -1;
         const int lid = (int)(m >> s3::LID_SHIFT);
         const bool tg = here && (m & s3::F_TG), init = here && !tg && (m & s3::F_INIT);
-        float val = CUR.g[i];
+        float val = RARE ? 0.f : CUR.g[i];
         // the table's global spill (lid ≥ cap) on its own wave-uniform path: a global
         // read merged into the LDS path would make every later use wait for all loads
         if (!SPILL || __builtin_amdgcn_ballot_w64((tg || init) && lid >= cap) == 0ull) {
@@ -994,7 +1101,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (here) base += (m & s3::F_SIGN) ? -val : val;
+        if (here && (!RARE || tg)) base += (m & s3::F_SIGN) ? -val : val;
       }
       sm.part[cn & 1][q][r] = base;
     }
@@ -1049,506 +1156,57 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     if (lane == 0 && j < KN) wsd[(size_t)s * s3::DS + j] = wn[i] - w0[i];
   }
   if (q == 0 && lane >= KN && lane < s3::DS) wsd[(size_t)s * s3::DS + lane] = 0.f;
-  s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm.last);
+  s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
 }
 
-// ------------------------------------------------------------------ v4: the split spoke
-// One spoke on two CUs, its two workgroups meeting through epoch-tagged granules in L2
-// (Guideline 16: the data is the flag), so the categorical work no longer competes with
-// the scanner's staging for one CU's VMEM / LDS pipes (v3: the helpers set the chunk
-// period, ≈ 4.7 K cycles against the scanner's 3.2 K):
-//  * WG-S (blocks [0, S_act)): wave 0 the scanner (v3's recurrence over G_k with X1_{k+1}
-//    folded in the chain); waves 1..8 stage aG_{k+1} and aX1_{k+2} into LDS; wave 9 folds
-//    c_{k−1} into chunk k+1's margins through aX2_{k+1} (a·X_{k+1}X_{k−1}ᵀ, from the prep);
-//    waves 10-11 keep the dense columns' running weights (through chunk k−2) and their
-//    base margins for chunk k+1.
-//  * WG-T (blocks [S_act, 2·S_act)): the categorical fields and the spoke's slot table
-//    (every slot recurring ≥ 3 chunks apart) in the LDS of its own CU. For chunk j it polls
-//    the scanner's c granules; every table occurrence adds c·sign to the table, every
-//    other occurrence adds inv_p·c·sign straight to the round accumulator, and a table
-//    slot's last occurrence flushes inv_p·(w − w0) — no combiner workgroups. Then it
-//    assembles chunk j+3's categorical base margins (table entries, w gathers) and
-//    publishes them as {epoch, m} granules that the scanner polls a chunk ahead.
-// Row t of chunk k: m_t = x_t·w0 + Σ_{s<t} c_s x_s·x_t split by distance — chunk k (G),
-// k−1 (X1, the chain), k−2 (X2, the fold wave), ≤ k−3 (base margins: WG-T's table and w,
-// the dense waves) — so WG-T has two chunk periods to turn chunk j's c into chunk j+3's
-// margins. Every spin is bounded (g_s3_comb_err 2: the scanner, 3: WG-T).
-namespace s4 {
-constexpr int NW = s3::NH + 1;                    // waves per workgroup, both roles (12)
-constexpr int NT = 64 * NW;
-constexpr int NSTG = 8;                           // WG-S staging waves 1..8
-constexpr int FOLD = 1 + NSTG;                    // WG-S X2 fold wave
-constexpr int DENSE0 = FOLD + 1;                  // WG-S dense waves DENSE0..NW−1
-constexpr int NDW = NW - DENSE0;
-constexpr int NJD = (s3::KNMAX + NDW - 1) / NDW;  // dense columns per dense wave
-constexpr int NFT = (s3::MAXF + NW - 1) / NW;     // WG-T fields per wave
-constexpr int NV4 = (2 * s3::MAT / 4) / (64 * NSTG);  // f32x4 staged per lane per chunk
-static_assert(NV4 * 64 * NSTG == 2 * s3::MAT / 4, "staging split");
-}  // namespace s4
-
-struct S4Smem {
-  union {
-    struct {  // WG-S
-      alignas(16) float G[2][s3::CH][s3::GS];    // aG_k by chunk parity
-      alignas(16) float X1[2][s3::CH][s3::GS];   // aX1_{k+1}
-      alignas(16) float cb[4][s3::CH];           // c by chunk mod 4
-      float f2[2][s3::CH];                       // X2 fold of chunk k, by parity
-      float md[2][s4::NDW][s3::CH];              // dense base margins of chunk k, by parity
-      int last;
-    } s;
-    struct {  // WG-T: margin partials, then the slot table to the end of the LDS
-      float part[2][s4::NW][s3::CH];
-    } t;
-  };
+// Several pipelines that share one prep (the same batch and row scaling: BASELINE config 5's
+// concurrent classifiers) in ONE launch, each with its own model, accumulator, granule
+// buffers and rule constants (one pipeline is the M = 1 case). Blocks are role-major — every
+// pipeline's rare-slot workgroups, then the scan workgroups, then the combiners — so the grid
+// needs no co-residency: a block only waits on roles dispatched before it (a scan on its
+// rare-slot workgroup, a combiner on its scan), which never wait on it. One launch also
+// sidesteps the four hardware queues per process that capped concurrent pipeline streams.
+constexpr int kS3MaxPipes = 16;
+struct S3Pipe {
+  const float* w;
+  float* aglob;
+  float* ws;
+  float* wsd;
+  unsigned long long* rgran;
+  S3Comb cb;
+  SeqParams p;
+};
+struct S3Pipes {
+  int M;
+  int ncomb;
+  S3Pipe pipe[kS3MaxPipes];
 };
 
-template <bool SPILL>
-__device__ __forceinline__ void s4_table(const uint32_t* __restrict__ meta, int dc, int B, int R,
-                                         const float* __restrict__ w, float* __restrict__ aglob,
-                                         long long gstride, const S3Comb& cb,
-                                         unsigned long long* __restrict__ mgran, float* T,
-                                         int capT, int s, int t0, int t1, float inv_p,
-                                         S4Smem& sm) {
-  using namespace s3;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int q = __builtin_amdgcn_readfirstlane(tid >> 6), r = lane;
-  const int nch = (t1 - t0 + CH - 1) / CH;
-  float* ag = aglob + (size_t)s * gstride;
-  float* dacc = cb.dacc;
-  const unsigned long long want = (unsigned long long)cb.epoch;
-  bool dead = false;  // a poll timed out: no more spinning (the flag fails the round)
-  struct Words {
-    int cs[s4::NFT];
-    uint32_t cm[s4::NFT];
-    float g[s4::NFT];
-  };
-  auto load_words = [&](int ch, Words& S) {
-#pragma unroll
-    for (int i = 0; i < s4::NFT; ++i) {
-      const int f = q + s4::NW * i;
-      const int row = t0 + ch * CH + r;
-      const bool ok = ch >= 0 && ch < nch && f < dc && row < t1;
-      const uint2 o = reinterpret_cast<const uint2*>(meta)[ok ? (size_t)f * B + row : 0];
-      S.cs[i] = ok ? (int)o.x : -1;
-      S.cm[i] = ok ? o.y : 0u;
-    }
-  };
-  auto issue_gathers = [&](Words& S) {  // w0 of the margin occurrences that do not read the table
-#pragma unroll
-    for (int i = 0; i < s4::NFT; ++i) {
-      const bool glob = S.cs[i] != -1 && !(S.cm[i] & F_TG);
-      S.g[i] = w[glob ? (S.cs[i] & 0x7fffffff) : 0];
-    }
-  };
-  auto tread = [&](int lid) -> float {
-    if constexpr (SPILL) {
-      if (lid >= capT)
-        return __hip_atomic_load(&ag[lid - capT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    return T[lid];
-  };
-  // scatter words of the last three margin chunks (chunk j's are r3 at iteration j)
-  int r1s[s4::NFT], r2s[s4::NFT], r3s[s4::NFT];
-  uint32_t r1m[s4::NFT], r2m[s4::NFT], r3m[s4::NFT];
-  float gl[s4::NFT];  // w0 of the F_LAST occurrences of the next scatter chunk
-#pragma unroll
-  for (int i = 0; i < s4::NFT; ++i) {
-    r1s[i] = r2s[i] = r3s[i] = -1;
-    r1m[i] = r2m[i] = r3m[i] = 0u;
-    gl[i] = 0.f;
-  }
-  Words A, Bw;
-  load_words(0, A);
-  issue_gathers(A);
-  auto body = [&](int j, Words& CUR, Words& NXT) {
-    const int m = j + 3;  // margin chunk
-    load_words(m + 1, NXT);
-    // ---- chunk j's c (the scanner's granules), then its scatter
-    float cv = 0.f;
-    if (j >= 0) {
-      const int row = t0 + j * CH + r;
-      const bool in = row < t1;
-      unsigned long long g = in ? __hip_atomic_load((s3_gu64*)(cb.gran + row), __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT)
-                                : (want << 32);
-      for (unsigned spins = 0; __builtin_amdgcn_ballot_w64(in && (g >> 32) != want) != 0ull;) {
-        if (dead || ++spins > SPIN_MAX) {
-          if (!dead && lane == 0) atomicExch(&g_s3_comb_err, 3);
-          dead = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        g = in ? __hip_atomic_load((s3_gu64*)(cb.gran + row), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT)
-               : (want << 32);
-      }
-      cv = in && (g >> 32) == want ? __uint_as_float((uint32_t)g) : 0.f;
-#pragma unroll
-      for (int i = 0; i < s4::NFT; ++i) {
-        const int sl = r3s[i];
-        const uint32_t mm = r3m[i];
-        const bool here = sl != -1 && cv != 0.f;
-        const float val = (mm & F_SIGN) ? -cv : cv;
-        if (here && (mm & F_SCAT)) {
-          const int lid = (int)(mm >> LID_SHIFT);
-          if constexpr (SPILL) {
-            if (lid < capT) atomicAdd(&T[lid], val);
-            else atomicAdd(&ag[lid - capT], val);
-          } else {
-            atomicAdd(&T[lid], val);
-          }
-        } else if (here) {
-          atomicAdd(&dacc[sl & 0x7fffffff], inv_p * val);
-        }
-      }
-      if constexpr (SPILL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // a table slot's last occurrence: its spoke total is final (every add of this chunk
-      // came from this wave's instructions above, LDS ops of a wave complete in order)
-#pragma unroll
-      for (int i = 0; i < s4::NFT; ++i) {
-        const uint32_t mm = r3m[i];
-        if (r3s[i] != -1 && (mm & F_LAST)) {
-          const float d = tread((int)(mm >> LID_SHIFT)) - gl[i];
-          if (d != 0.f) atomicAdd(&dacc[r3s[i] & 0x7fffffff], inv_p * d);
-        }
-      }
-    }
-    // ---- base margins of chunk m: table entries (chunks ≤ m − 3 applied) or w0
-    if (m < nch) {
-      float base = 0.f;
-      if constexpr (!SPILL) {
-        float tv[s4::NFT];
-#pragma unroll
-        for (int i = 0; i < s4::NFT; ++i) {
-          const uint32_t mm = CUR.cm[i];
-          tv[i] = 0.f;
-          if (CUR.cs[i] != -1 && (mm & F_TG)) tv[i] = T[(int)(mm >> LID_SHIFT)];
-        }
-#pragma unroll
-        for (int i = 0; i < s4::NFT; ++i) {
-          const uint32_t mm = CUR.cm[i];
-          const bool here = CUR.cs[i] != -1;
-          const bool tg = here && (mm & F_TG), init = here && !tg && (mm & F_INIT);
-          const float val = tg ? tv[i] : CUR.g[i];
-          if (init) T[(int)(mm >> LID_SHIFT)] = val;
-          if (here) base += (mm & F_SIGN) ? -val : val;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < s4::NFT; ++i) {
-          const uint32_t mm = CUR.cm[i];
-          const bool here = CUR.cs[i] != -1;
-          const int lid = (int)(mm >> LID_SHIFT);
-          const bool tg = here && (mm & F_TG), init = here && !tg && (mm & F_INIT);
-          float val = CUR.g[i];
-          if (tg) val = tread(lid);
-          if (init) {
-            if (lid < capT) T[lid] = val;
-            else __hip_atomic_store(&ag[lid - capT], val, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (here) base += (mm & F_SIGN) ? -val : val;
-        }
-      }
-      sm.t.part[m & 1][q][r] = base;
-    }
-    issue_gathers(NXT);
-    // rotate the scatter words; w0 of the next scatter chunk's last occurrences
-#pragma unroll
-    for (int i = 0; i < s4::NFT; ++i) {
-      r3s[i] = r2s[i];
-      r3m[i] = r2m[i];
-      r2s[i] = r1s[i];
-      r2m[i] = r1m[i];
-      r1s[i] = CUR.cs[i];
-      r1m[i] = CUR.cm[i];
-      const bool last = r3s[i] != -1 && (r3m[i] & F_LAST);
-      gl[i] = w[last ? (r3s[i] & 0x7fffffff) : 0];
-    }
-    __syncthreads();
-    // ---- wave 0 publishes chunk m's margins (sum of the waves' partials)
-    if (q == 0 && m < nch) {
-      const int row = t0 + m * CH + r;
-      float v = 0.f;
-#pragma unroll
-      for (int k = 0; k < s4::NW; ++k) v += sm.t.part[m & 1][k][r];
-      if (row < t1)
-        __hip_atomic_store((s3_gu64*)(mgran + row), (want << 32) | __float_as_uint(v),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-  for (int j = -3; j < nch; j += 2) {
-    body(j, A, Bw);
-    if (j + 1 < nch) body(j + 1, Bw, A);
-  }
-}
-
-template <int RULE, int KN>
-__global__ __launch_bounds__(s4::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s4_scan_kernel(
-    const uint32_t* __restrict__ meta, int dc, int dn, int B, int R,
-    const float* __restrict__ prep, int nchs, const float* __restrict__ w, int dim,
-    float* __restrict__ aglob, long long gstride, int dynf, int cap_limit, S3Comb cb,
-    unsigned long long* __restrict__ mgran, float* __restrict__ ws, float* __restrict__ wsd,
-    SeqParams p) {
-  using namespace s3;
-  __shared__ S4Smem sm;
-  extern __shared__ float tab_dyn[];  // [dynf]: WG-T's table continues into it
-  constexpr int PF = s3_prep_floats<KN, 2>();
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if ((int)blockIdx.x >= cb.S_act) {  // WG-T
-    const int s = (int)blockIdx.x - cb.S_act;
-    int t0, t1;
-    spoke_rows(s, R, B, t0, t1);
-    if (t0 >= t1) return;
-    float* T = reinterpret_cast<float*>(&sm) + 2 * s4::NW * CH;
-    const int capT = min((int)((tab_dyn + dynf) - T), cap_limit);
-    if (cb.lidcount[s] <= capT)
-      s4_table<false>(meta, dc, B, R, w, aglob, gstride, cb, mgran, T, capT, s, t0, t1, p.inv_p, sm);
-    else
-      s4_table<true>(meta, dc, B, R, w, aglob, gstride, cb, mgran, T, capT, s, t0, t1, p.inv_p, sm);
-    return;
-  }
-  const int s = blockIdx.x;
-  int t0, t1;
-  spoke_rows(s, R, B, t0, t1);
-  if (t0 >= t1) {
-    if (tid < WS) ws[(size_t)s * WS + tid] = 0.f;
-    if (tid < DS) wsd[(size_t)s * DS + tid] = 0.f;
-    s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm.s.last);
-    return;
-  }
-  const int nch = (t1 - t0 + CH - 1) / CH;
-  const float* P0 = prep + (size_t)s * nchs * PF;
-  auto chunk_prep = [&](int k) { return P0 + (size_t)k * PF; };
-  const unsigned long long want = (unsigned long long)cb.epoch;
-
-  if (wave == 0) {
-    // ---------------------------------------------------------------- scanner
-    __builtin_amdgcn_s_setprio(3);
-    float loss = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f;
-    float f1 = 0.f;
-    float ynx = chunk_prep(0)[s3_prep_y<KN, 2>() + lane];
-    float anx = chunk_prep(0)[s3_prep_a<2>() + lane];
-    bool dead = false;
-    auto poll_margin = [&](int k) -> unsigned long long {
-      const int row = t0 + k * CH + lane;
-      return row < t1 ? __hip_atomic_load((s3_gu64*)(mgran + row), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT)
-                      : (want << 32);
-    };
-    unsigned long long gm = poll_margin(0);
-    for (int k = -1; k < nch; ++k) {
-      if (k >= 0) {
-        const int b = k & 1;
-        const int row = t0 + k * CH + lane;
-        const bool valid = row < t1 && ynx == ynx;
-        const float y = valid ? ynx : 0.f;
-        const float a = valid ? anx : 0.f;
-        if (k + 1 < nch) {
-          ynx = chunk_prep(k + 1)[s3_prep_y<KN, 2>() + lane];
-          anx = chunk_prep(k + 1)[s3_prep_a<2>() + lane];
-        }
-        // the categorical base margin from WG-T (bounded spin on this round's tag)
-        for (unsigned spins = 0; __builtin_amdgcn_ballot_w64((gm >> 32) != want) != 0ull;) {
-          if (dead || ++spins > SPIN_MAX) {
-            if (!dead && lane == 0) atomicExch(&g_s3_comb_err, 2);
-            dead = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          gm = poll_margin(k);
-        }
-        const float mcat = (gm >> 32) == want ? __uint_as_float((uint32_t)gm) : 0.f;
-        float m0 = mcat;
-#pragma unroll
-        for (int d = 0; d < s4::NDW; ++d) m0 += sm.s.md[b][d][lane];
-        const float fx = f1 + sm.s.f2[b][lane];
-        S3Cand<RULE> cf;
-        float u, bc = 0.f;
-        const float inv = -a;
-        if constexpr (RULE == kSeqHinge) {
-          bc = y * inv;
-          cf.lo = y < 0.f ? -p.cclip : 0.f;
-          cf.hi = y < 0.f ? 0.f : (y > 0.f ? p.cclip : 0.f);
-          u = fmaf(a, m0, bc) + fx;
-        } else if constexpr (RULE == kSeqEps) {
-          bc = (y - p.eps) * inv;
-          cf.d = 2.f * p.eps * inv;
-          cf.lo = valid ? -p.cclip : 0.f;
-          cf.hi = valid ? p.cclip : 0.f;
-          u = fmaf(a, m0, bc) + fx;
-        } else {
-          u = m0 + fx;
-        }
-        const float* grow = &sm.s.G[b][lane][0];
-        const float* xrow = &sm.s.X1[b ^ 1][lane][0];
-        float gg[CH], xx[CH];
-#pragma unroll
-        for (int t4 = 0; t4 < CH; t4 += 4) {
-          const float4 g4 = *reinterpret_cast<const float4*>(grow + t4);
-          const float4 x4 = *reinterpret_cast<const float4*>(xrow + t4);
-          gg[t4] = g4.x, gg[t4 + 1] = g4.y, gg[t4 + 2] = g4.z, gg[t4 + 3] = g4.w;
-          xx[t4] = x4.x, xx[t4 + 1] = x4.y, xx[t4 + 2] = x4.z, xx[t4 + 3] = x4.w;
-        }
-        float n1 = 0.f;
-#pragma unroll
-        for (int t = 0; t < CH; ++t) {
-          const float ct = readlane_f(cf(u, p, y), t);
-          u = fmaf(ct, gg[t], u);
-          n1 = fmaf(ct, xx[t], n1);
-          asm volatile("" : "+v"(u), "+v"(n1));
-        }
-        const float c = cf(u, p, y);
-        sm.s.cb[k & 3][lane] = c;
-        if (row < t1)
-          __hip_atomic_store((s3_gu64*)(cb.gran + row),
-                             ((unsigned long long)cb.epoch << 32) | __float_as_uint(c),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (valid) {
-          float mv;
-          if constexpr (RULE == kSeqLogistic) mv = u;
-          else mv = inv > 0.f ? (bc - u) * __builtin_amdgcn_rcpf(inv) : 0.f;
-          seq_stats<RULE>(mv, y, p, loss, mist, sqe);
-          nex += 1.f;
-        }
-        f1 = n1;
-        if (k + 1 < nch) gm = poll_margin(k + 1);  // in flight across the barrier
-      }
-      __syncthreads();
-    }
-    loss = wave_sum(loss);
-    nex = wave_sum(nex);
-    mist = wave_sum(mist);
-    sqe = wave_sum(sqe);
-    if (lane == 0) {
-      float* wr = ws + (size_t)s * WS;
-      wr[0] = loss;
-      wr[1] = nex;
-      wr[2] = mist;
-      wr[3] = sqe;
-      wr[4] = 1.f;
-      wr[5] = 0.f;
-      wr[6] = 0.f;
-      wr[7] = 0.f;
-    }
-  } else if (wave <= s4::NSTG) {
-    // ------------------------------------------------ staging: aG_{k+1}, aX1_{k+2}
-    const int hl = (wave - 1) * 64 + lane;
-    f32x4 v[s4::NV4];
-    auto load = [&](int cn) {
-#pragma unroll
-      for (int u = 0; u < s4::NV4; ++u) {
-        const int i = hl + 64 * s4::NSTG * u;
-        const int mtx = i >> 10, e = i & 1023;
-        const int kc = max(0, min(cn + mtx, nch - 1));
-        v[u] = reinterpret_cast<const f32x4*>(chunk_prep(kc) + mtx * MAT)[e];
-      }
-    };
-    load(0);
-    for (int k = -1; k < nch; ++k) {
-      const int cn = k + 1;
-#pragma unroll
-      for (int u = 0; u < s4::NV4; ++u) {
-        const int i = hl + 64 * s4::NSTG * u;
-        const int mtx = i >> 10, e = i & 1023;
-        if (cn + mtx < nch) {
-          const int row = e >> 4, col = (e & 15) * 4;
-          float* dst = mtx == 0 ? &sm.s.G[cn & 1][row][col] : &sm.s.X1[(cn + 1) & 1][row][col];
-          *reinterpret_cast<f32x4*>(dst) = v[u];
-        }
-      }
-      if (cn + 1 < nch) load(cn + 1);
-      __syncthreads();
-    }
-  } else if (wave == s4::FOLD) {
-    // ------------------------------------------------ X2 fold: f2(k+1) = aX2_{k+1}·c_{k−1}
-    float xr[CH];
-    auto load_row = [&](int cn) {  // this lane's row of aX2_cn
-      const f32x4* src = reinterpret_cast<const f32x4*>(chunk_prep(max(0, min(cn, nch - 1))) +
-                                                        2 * MAT + lane * CH);
-#pragma unroll
-      for (int t4 = 0; t4 < CH / 4; ++t4) {
-        const f32x4 x = src[t4];
-        xr[4 * t4] = x[0], xr[4 * t4 + 1] = x[1], xr[4 * t4 + 2] = x[2], xr[4 * t4 + 3] = x[3];
-      }
-    };
-    load_row(2);
-    for (int k = -1; k < nch; ++k) {
-      const int cn = k + 1;
-      if (cn < nch) {
-        float f = 0.f;
-        if (cn >= 2) {
-          // c_t broadcast from lane t (one VGPR for the chunk's c, not 64)
-          const float cv = sm.s.cb[(cn - 2) & 3][lane];
-#pragma unroll
-          for (int t = 0; t < CH; ++t) f = fmaf(readlane_f(cv, t), xr[t], f);
-          if (cn + 1 < nch) load_row(cn + 1);
-        }
-        sm.s.f2[cn & 1][lane] = f;
-      }
-      __syncthreads();
-    }
+template <int RULE, int KN, bool RARE>
+__global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s3_scan_kernel(
+    const int* __restrict__ slotsT, const uint32_t* __restrict__ meta, int dc, int dn,
+    const void* __restrict__ yv, int B, int R, const float* __restrict__ prep, int nchs,
+    int dim, int cap, long long gstride, int S_act, S3Pipes pp) {
+  __shared__ S3Smem sm;
+  extern __shared__ float tab[];  // [cap] + 64 scratch words (one per lane)
+  const int b = (int)blockIdx.x, M = pp.M;
+  const int nr = RARE ? M * S_act : 0, ns = M * S_act;
+  int pi, bid;
+  if (b < nr) {  // rare-slot workgroups first
+    pi = b / S_act;
+    bid = S_act + b % S_act;
+  } else if (b < nr + ns) {
+    pi = (b - nr) / S_act;
+    bid = (b - nr) % S_act;
   } else {
-    // ------------------------------------------------ dense columns
-    const int dw = wave - s4::DENSE0;
-    const int kd = dn + (p.bias ? 1 : 0);
-    constexpr int NJK = (KN + s4::NDW - 1) / s4::NDW;
-    float wn[NJK], w0[NJK], xs[NJK], xc[NJK];
-#pragma unroll
-    for (int i = 0; i < NJK; ++i) {
-      const int j = dw + s4::NDW * i;
-      w0[i] = (j < KN) ? (j < dn ? w[j] : ((p.bias && j == dn) ? w[dim - 1] : 0.f)) : 0.f;
-      wn[i] = w0[i];
-    }
-    auto load_dense = [&](int ch, float* xd) {
-#pragma unroll
-      for (int i = 0; i < NJK; ++i) {
-        const int j = dw + s4::NDW * i;
-        const bool ok = j < KN && ch >= 0 && ch < nch;
-        const int jc = j < KN ? j : 0, cc = max(0, min(ch, nch - 1));
-        const float x = chunk_prep(cc)[s3_prep_dense<2>() + jc * CH + lane];
-        xd[i] = ok ? x : 0.f;
-      }
-    };
-    auto update = [&](int ku) {  // running dense weights += Σ_rows c·x over chunk ku
-      const float cv = sm.s.cb[ku & 3][lane];
-#pragma unroll
-      for (int i = 0; i < NJK; ++i) {
-        const int j = dw + s4::NDW * i;
-        if (j < kd) wn[i] += wave_sum(cv * xs[i]);
-      }
-    };
-    load_dense(-3, xs);
-    load_dense(0, xc);
-    for (int k = -1; k < nch; ++k) {
-      const int cn = k + 1, ku = cn - 3;
-      if (ku >= 0) update(ku);
-      if (cn < nch) {
-        float base = 0.f;
-#pragma unroll
-        for (int i = 0; i < NJK; ++i) base = fmaf(xc[i], wn[i], base);
-        sm.s.md[cn & 1][dw][lane] = base;
-      }
-      load_dense(ku + 1, xs);
-      load_dense(cn + 1, xc);
-      __syncthreads();
-    }
-    // the last two chunks' updates (the loop applied chunks ≤ nch − 3; their c is in LDS
-    // after the final barrier)
-    for (int ku = max(0, nch - 2); ku < nch; ++ku) {
-      load_dense(ku, xs);
-      update(ku);
-    }
-#pragma unroll
-    for (int i = 0; i < NJK; ++i) {
-      const int j = dw + s4::NDW * i;
-      if (lane == 0 && j < KN) wsd[(size_t)s * DS + j] = wn[i] - w0[i];
-    }
-    if (dw == 0 && lane >= KN && lane < DS) wsd[(size_t)s * DS + lane] = 0.f;
+    const int c = b - nr - ns, per = S_act * pp.ncomb;
+    pi = c / per;
+    bid = S_act * (RARE ? 2 : 1) + c % per;
   }
-  s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm.s.last);
+  const S3Pipe& P = pp.pipe[pi];
+  s3_scan_body<RULE, KN, RARE>(bid, S_act * ((RARE ? 2 : 1) + pp.ncomb), sm, tab, slotsT, meta,
+                               dc, dn, yv, B, R, prep, nchs, P.w, dim, P.aglob, cap, gstride,
+                               P.cb, P.ws, P.wsd, P.p, P.rgran);
 }
 
 // ------------------------------------------------------------------ pass 5: combine
@@ -1650,43 +1308,43 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
   }
 }
 
-template <int RULE, int KN>
-static int s3_launch_scan(const int* slotsT, const uint32_t* meta, int dc, int dn, const void* y,
-                          int B, int R, int S_act, const float* prep, int nchs, const float* w,
-                          int dim, float* aglob, int cap, long long gstride, const S3Comb& cb,
-                          int ncomb, float* ws, float* wsd, const SeqParams& p, hipStream_t st) {
+template <int RULE, int KN, bool RARE>
+static int s3_launch_scan_t(const int* slotsT, const uint32_t* meta, int dc, int dn, const void* y,
+                            int B, int R, int S_act, const float* prep, int nchs, int dim, int cap,
+                            long long gstride, const S3Pipes& pp, hipStream_t st) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&s3_scan_kernel<RULE, KN>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&s3_scan_kernel<RULE, KN, RARE>),
                         hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024 - (int)sizeof(S3Smem));
     attr_set = true;
   }
-  // blocks [0, S_act) scan (dispatched first), then ncomb combiner blocks per spoke
-  hipLaunchKernelGGL((s3_scan_kernel<RULE, KN>), dim3(S_act * (1 + ncomb)), dim3(s3::NT),
-                     (size_t)(cap + 64) * sizeof(float), st, slotsT, meta, dc, dn, y, B, R, prep, nchs, w,
-                     dim, aglob, cap, gstride, cb, ws, wsd, p);
+  // per pipeline: S_act rare-slot (RARE), S_act scan and ncomb·S_act combiner workgroups,
+  // role-major across the pipelines (s3_scan_kernel)
+  const int nblk = pp.M * S_act * ((RARE ? 2 : 1) + pp.ncomb);
+  hipLaunchKernelGGL((s3_scan_kernel<RULE, KN, RARE>), dim3(nblk), dim3(s3::NT),
+                     (size_t)(cap + 64) * sizeof(float), st, slotsT, meta, dc, dn, y, B, R, prep,
+                     nchs, dim, cap, gstride, S_act, pp);
   return (int)hipGetLastError();
 }
 
-template <int RULE, int KN>
-static int s4_launch_scan(const uint32_t* meta, int dc, int dn, int B, int R, int S_act,
-                          const float* prep, int nchs, const float* w, int dim, float* aglob,
-                          long long gstride, int cap_limit, const S3Comb& cb,
-                          unsigned long long* mgran, float* ws, float* wsd, const SeqParams& p,
+template <int KN>
+static int s3_launch_scan(int rule, bool rare, const int* slotsT, const uint32_t* meta, int dc,
+                          int dn, const void* y, int B, int R, int S_act, const float* prep,
+                          int nchs, int dim, int cap, long long gstride, const S3Pipes& pp,
                           hipStream_t st) {
-  const int dyn = 160 * 1024 - (int)sizeof(S4Smem);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&s4_scan_kernel<RULE, KN>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, dyn);
-    attr_set = true;
+#define OMLDM_S3L(RL, RA) \
+  return s3_launch_scan_t<RL, KN, RA>(slotsT, meta, dc, dn, y, B, R, S_act, prep, nchs, dim, cap, \
+                                      gstride, pp, st)
+  if (rare) {
+    if (rule == kSeqHinge) OMLDM_S3L(kSeqHinge, true);
+    if (rule == kSeqEps) OMLDM_S3L(kSeqEps, true);
+    OMLDM_S3L(kSeqLogistic, true);
   }
-  // blocks [0, S_act): the scanner workgroups (dispatched first), then the table ones
-  hipLaunchKernelGGL((s4_scan_kernel<RULE, KN>), dim3(2 * S_act), dim3(s4::NT), (size_t)dyn, st,
-                     meta, dc, dn, B, R, prep, nchs, w, dim, aglob, gstride, dyn / 4, cap_limit, cb,
-                     mgran, ws, wsd, p);
-  return (int)hipGetLastError();
+  if (rule == kSeqHinge) OMLDM_S3L(kSeqHinge, false);
+  if (rule == kSeqEps) OMLDM_S3L(kSeqEps, false);
+  OMLDM_S3L(kSeqLogistic, false);
+#undef OMLDM_S3L
 }
 
 }  // namespace omldm
@@ -1705,9 +1363,10 @@ constexpr size_t kFlagsLds = (size_t)s3::HCAP * 12;
 
 static int g_s3_cap_override = -1;  // tests: a small LDS table forces the global spill path
 
-// Round kernel: 3 (one workgroup per spoke + in-launch combiners) or 4 (the split spoke:
-// a scanner and a table workgroup per spoke, distance-3 flags, X2 Grams). Fixed before a
-// process's first prepare (the prep layout and workspace sizes depend on it).
+// Round mode: 4 (default) = a rare-slot workgroup per spoke computes the round-start
+// weights of the non-table occurrences ahead of the scan (s3_rare); 3 = the scan workgroup's
+// helpers gather them themselves (the A/B reference). The granule buffer is 2·B words
+// longer in mode 4 (set before a process's first prepare: it sizes the workspaces).
 static int g_s3_mode = 4;
 OMLDM_API void omldm_scan3_set_mode(int m) { g_s3_mode = m == 3 ? 3 : 4; }
 OMLDM_API int omldm_scan3_get_mode() { return g_s3_mode; }
@@ -1766,15 +1425,13 @@ OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn,
   (void)span;
   const long long nchs = (R + s3::CH - 1) / s3::CH;
   const int kn = s3_kn(dn, bias);
-  const bool v4 = g_s3_mode == 4;
-  const long long pf = kn == 16 ? (v4 ? s3_prep_floats<16, 2>() : s3_prep_floats<16>())
-                                : (v4 ? s3_prep_floats<32, 2>() : s3_prep_floats<32>());
+  const long long pf = kn == 16 ? s3_prep_floats<16>() : s3_prep_floats<32>();
   switch (which) {
     case 0: return (long long)dc * B;
     case 1: return 2LL * dc * B;  // {slot, meta} per occurrence
     case 2: return S;
     case 3: return (long long)S * nchs * pf;
-    case 4: return (v4 ? 4LL : 2LL) * B;  // c granules [B] (+ v4: margin granules [B])
+    case 4: return (g_s3_mode == 4 ? 4LL : 2LL) * B;  // c granules (+ mode 4: rare margins)
     case 5: return (long long)S * s3::WS;
     case 6: return (long long)S * s3::DS;
     case 7: return (long long)S * ((long long)R * dc / 2 + 64);
@@ -1873,24 +1530,16 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
     hipStreamWaitEvent(sd->side, sd->fork, 0);
     gst = sd->side;
   }
-  const bool v4 = g_s3_mode == 4;
-  if (v4)
-    hipLaunchKernelGGL(s3_flags_kernel<3>, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
-                       W.meta, W.lidcount);
+  if (g_s3_mode == 4)
+    hipLaunchKernelGGL(s3_flags_kernel<true>, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B,
+                       R, W.meta, W.lidcount);
   else
-    hipLaunchKernelGGL(s3_flags_kernel<2>, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
-                       W.meta, W.lidcount);
+    hipLaunchKernelGGL(s3_flags_kernel<false>, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B,
+                       R, W.meta, W.lidcount);
   const int nchs = (R + s3::CH - 1) / s3::CH;
   const int affine = rule != kSeqLogistic;
   const float kadd = (rule != kSeqLogistic && variant == 2) ? 0.5f / C : 0.f;
-  if (v4) {  // G, X1 and X2 on the matrix cores
-    if (s3_kn(dn, bias) == 16)
-      hipLaunchKernelGGL((s3_gram_mfma_kernel<16, 2>), dim3(nchs, S_act), dim3(256), 0, gst,
-                         W.slotsT, dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
-    else
-      hipLaunchKernelGGL((s3_gram_mfma_kernel<32, 2>), dim3(nchs, S_act), dim3(256), 0, gst,
-                         W.slotsT, dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
-  } else if (g_s3_gram_valu) {
+  if (g_s3_gram_valu) {
     if (s3_kn(dn, bias) == 16)
       hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT, dc,
                          num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
@@ -1911,85 +1560,98 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   return (int)hipGetLastError();
 }
 
-// Pass 4 (the scan) + pass 5 (the combine into dacc; zeroed here unless flags bit 0 says
-// the caller keeps it zero) on a prepared round.
-// `parts` is kept for the pipelined-sync interface: part 0 completes all of dacc (the
-// combine is a few tens of µs of atomics), later parts launch nothing.
-// `epoch`: this round's granule tag on the granule buffer ptrs[4] (≥ 1, one more than the
-// last round that used the buffer; the buffer was zeroed when allocated).
+// Pass 4 (the scan) + pass 5 (the combine) of M ≥ 1 pipelines on one prepared round, one
+// launch (s3_scan_kernel). Pipeline m: model w[m], accumulator dacc[m] (zeroed here unless
+// flags bit 0 says the caller keeps it zero), running totals cum[m] (or null), rule
+// constants C / eps / lr / inv_p [m], its 8 workspace pointers ptrs[8m .. 8m+8) (the first four
+// — slots, occurrences, table counts, prep — the shared prep's; granules, spoke rows, dense
+// deltas and table spill its own), its granule epoch (≥ 1, one more than the last round on
+// that granule buffer, zeroed when allocated) and arrival word (null: tail kernel after).
+static int s3_run_impl(int M, const float* const* w, float* const* dacc, double* const* cum,
+                       const float* C, const float* eps, const float* lr, const float* inv_p,
+                       void* const* ptrs, const unsigned* epoch, void* const* arrive, int dn,
+                       int dc, const void* y, int y8, int B, int R, int S, int dim, int rule,
+                       int variant, int bias, long long span_in, int flags, hipStream_t st) {
+  if (M < 1 || M > kS3MaxPipes) return -4;
+  if (S <= 0 || B <= 0) return 0;
+  if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
+  if (span_in < 0) return -2;  // the slots' range was checked by the prepare
+  const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
+  const S3Ws W0 = s3_ws(ptrs);
+  const int S_act = s3_sact(B, R, S);
+  const int nchs = (R + s3::CH - 1) / s3::CH;
+  const int kn = s3_kn(dn, bias);
+  const int cap = omldm_scan3_lds_cap();
+  const long long gstride = (long long)R * dc / 2 + 64;
+  const bool rare = g_s3_mode == 4;
+  const int ncomb = g_s3_comb;
+  S3Pipes pp{};
+  pp.M = M;
+  pp.ncomb = ncomb > 0 ? ncomb : 0;
+  for (int m = 0; m < M; ++m) {
+    if (epoch[m] == 0u) return -2;
+    const S3Ws Wm = s3_ws(ptrs + 8 * m);
+    const SeqParams p{rule, variant, variant == 1 ? C[m] : INFINITY,
+                      variant == 2 ? 0.5f / C[m] : 0.f, eps[m], lr[m], inv_p[m], bias, y8, span};
+    // flags bit 0: dacc[:dim] is already zero (linear_apply clears it after every round), so
+    // the combine adds straight into it (a memset beside the prep kernels took 15-20 us)
+    if (!(flags & 1)) hipMemsetAsync(dacc[m], 0, sizeof(float) * (size_t)dim, st);
+    // the tail in the scan's launch (last scan block) when the caller gave an arrival word;
+    // mode 4: the rare-slot workgroups' margin granules follow the c granules
+    pp.pipe[m] = S3Pipe{w[m], Wm.aglob, Wm.ws, Wm.wsd, rare ? Wm.gran + B : nullptr,
+                        S3Comb{W0.lidcount, Wm.gran, epoch[m], S_act, dacc[m], inv_p[m],
+                               static_cast<unsigned long long*>(arrive[m]), cum[m]},
+                        p};
+  }
+  const int e = kn == 16 ? s3_launch_scan<16>(rule, rare, W0.slotsT, W0.meta, dc, dn, y, B, R,
+                                              S_act, W0.prep, nchs, dim, cap, gstride, pp, st)
+                         : s3_launch_scan<32>(rule, rare, W0.slotsT, W0.meta, dc, dn, y, B, R,
+                                              S_act, W0.prep, nchs, dim, cap, gstride, pp, st);
+  if (e) return e;
+  for (int m = 0; m < M; ++m) {
+    const S3Ws Wm = s3_ws(ptrs + 8 * m);
+    if (ncomb > 0) {  // the categorical slots were combined in the scan's launch
+      if (!arrive[m])
+        hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, Wm.ws, Wm.wsd, S_act, dn,
+                           dim, bias, inv_p[m], dacc[m], cum[m]);
+      continue;
+    }
+    const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
+    const int nblk = (n_rows + s3::SB - 1) / s3::SB;
+    hipLaunchKernelGGL(s3_scatter_kernel, dim3(nblk > 0 ? nblk : 1, dc + (arrive[m] ? 0 : 1)),
+                       dim3(256), 0, st, W0.slotsT, Wm.gran, B, n_rows, inv_p[m], dacc[m], dc,
+                       Wm.ws, Wm.wsd, S_act, dn, dim, bias, cum[m]);
+  }
+  return (int)hipGetLastError();
+}
+
+// One pipeline (the M = 1 case). `parts` is kept for the pipelined-sync interface: part 0
+// completes all of dacc (the combine is a few tens of µs of atomics), later parts launch
+// nothing.
 OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int y8, int B, int R,
                               int S, float* dacc, int dim, double* cum, int rule, int variant,
                               float C, float eps, float lr, float inv_p, int bias,
                               long long span_in, void* const* ptrs, int part, int parts,
                               int flags, unsigned epoch, void* arrive, void* stream) {
-  if (epoch == 0u) return -2;
-  if (S <= 0 || B <= 0) return 0;
-  if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
-  if (span_in < 0) return -2;  // the slots' range was checked by the prepare
   if (part != 0) return 0;
   (void)parts;
-  hipStream_t st = (hipStream_t)stream;
-  const uint32_t span = span_in > 0 ? (uint32_t)span_in : (uint32_t)((dim - dn - 1) / dc);
-  const S3Ws W = s3_ws(ptrs);
-  const int S_act = s3_sact(B, R, S);
-  const int nchs = (R + s3::CH - 1) / s3::CH;
-  const int kn = s3_kn(dn, bias);
-  const SeqParams p{rule, variant, variant == 1 ? C : INFINITY, variant == 2 ? 0.5f / C : 0.f,
-                    eps, lr, inv_p, bias, y8, span};
-  const int cap = omldm_scan3_lds_cap();
-  const long long gstride = (long long)R * dc / 2 + 64;
-  // flags bit 0: dacc[:dim] is already zero (linear_apply clears it after every round), so
-  // the combine adds straight into it (a memset beside the prep kernels took 15-20 us)
-  if (!(flags & 1)) hipMemsetAsync(dacc, 0, sizeof(float) * (size_t)dim, st);
-  const int ncomb = g_s3_comb;
-  // the tail in the scan's launch (last scan block) when the caller gave an arrival word
-  const S3Comb cb{W.lidcount, W.gran, epoch, S_act, dacc, inv_p,
-                  static_cast<unsigned long long*>(arrive), cum};
-  int e;
-  if (g_s3_mode == 4) {  // the split spoke: no combiner workgroups, no scatter pass
-    unsigned long long* mgran = W.gran + B;  // the margin granules follow the c granules
-#define OMLDM_S4(RL, K) \
-  s4_launch_scan<RL, K>(W.meta, dc, dn, B, R, S_act, W.prep, nchs, w, dim, W.aglob, gstride,      \
-                        g_s3_cap_override >= 0 ? g_s3_cap_override : (1 << 30), cb, mgran, W.ws, \
-                        W.wsd, p, st)
-    if (kn == 16)
-      e = rule == kSeqHinge ? OMLDM_S4(kSeqHinge, 16) : rule == kSeqEps ? OMLDM_S4(kSeqEps, 16)
-                                                                       : OMLDM_S4(kSeqLogistic, 16);
-    else
-      e = rule == kSeqHinge ? OMLDM_S4(kSeqHinge, 32) : rule == kSeqEps ? OMLDM_S4(kSeqEps, 32)
-                                                                       : OMLDM_S4(kSeqLogistic, 32);
-#undef OMLDM_S4
-    if (e) return e;
-    if (!arrive)
-      hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, W.ws, W.wsd, S_act, dn, dim,
-                         bias, inv_p, dacc, cum);
-    return (int)hipGetLastError();
-  }
-  if (kn == 16) {
-    e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
-      : rule == kSeqEps ? s3_launch_scan<kSeqEps, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
-      : s3_launch_scan<kSeqLogistic, 16>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st);
-  } else {
-    e = rule == kSeqHinge ? s3_launch_scan<kSeqHinge, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
-      : rule == kSeqEps ? s3_launch_scan<kSeqEps, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st)
-      : s3_launch_scan<kSeqLogistic, 32>(W.slotsT, W.meta, dc, dn, y, B, R, S_act, W.prep, nchs, w, dim, W.aglob, cap, gstride, cb, ncomb, W.ws, W.wsd, p, st);
-  }
-  if (e) return e;
-  (void)span;
-  if (ncomb > 0) {  // the categorical slots were combined in the scan's launch
-    if (!arrive)
-      hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, W.ws, W.wsd, S_act, dn, dim,
-                         bias, inv_p, dacc, cum);
-    return (int)hipGetLastError();
-  }
-  const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
-  const int nblk = (n_rows + s3::SB - 1) / s3::SB;
-  hipLaunchKernelGGL(s3_scatter_kernel, dim3(nblk > 0 ? nblk : 1, dc + (arrive ? 0 : 1)),
-                     dim3(256), 0, st,
-                     W.slotsT, W.gran, B, n_rows, inv_p, dacc, dc, W.ws, W.wsd, S_act, dn, dim,
-                     bias, cum);
-  return (int)hipGetLastError();
+  return s3_run_impl(1, &w, &dacc, &cum, &C, &eps, &lr, &inv_p, ptrs, &epoch, &arrive, dn, dc, y,
+                     y8, B, R, S, dim, rule, variant, bias, span_in, flags, (hipStream_t)stream);
 }
+
+// M pipelines sharing one prep, one launch (per-pipeline arrays as in s3_run_impl).
+OMLDM_API int omldm_scan3_run_multi(int M, const float* const* w, float* const* dacc,
+                                    double* const* cum, const float* C, const float* eps,
+                                    const float* lr, const float* inv_p, void* const* ptrs,
+                                    const unsigned* epoch, void* const* arrive, int dn, int dc,
+                                    const void* y, int y8, int B, int R, int S, int dim,
+                                    int rule, int variant, int bias, long long span_in, int flags,
+                                    void* stream) {
+  return s3_run_impl(M, w, dacc, cum, C, eps, lr, inv_p, ptrs, epoch, arrive, dn, dc, y, y8, B, R,
+                     S, dim, rule, variant, bias, span_in, flags, (hipStream_t)stream);
+}
+
+OMLDM_API int omldm_scan3_max_pipes() { return kS3MaxPipes; }
 
 // [lo, hi) of dacc that combine part `part` of `parts` completes: part 0 all of it.
 OMLDM_API int omldm_scan3_part_bounds(int dim, int dn, int dc, long long span_in, int part,

@@ -385,11 +385,29 @@ class Job:
         if direct is not None and direct.B:  # rows that bypass the holdout (no spoke layout)
             routed = HashedBatch.cat_batches([direct, routed]) if routed.B else direct
         groups: dict[int, list] = {}
+        # hashed-linear Synchronous pipelines without preprocessors that share a prep train
+        # in ONE multi-pipeline launch (ops.linear.linear_scan3_round_multi; BASELINE config 5)
+        fused = self._fused_groups(routed)
+        done = set()
+        for grp in fused:
+            with tracing.range("round:multi"):
+                ctx = grp[0].protocol._ctx(fused=True)
+                for pipe in grp:
+                    pipe._note_buffer(routed.B)
+                type(grp[0].learner).fit_group([p.learner for p in grp], routed, ctx)
+                for pipe in grp:
+                    done.add(pipe.id)
+                    buf = pipe.protocol.local_done()
+                    if self.world > 1:
+                        groups.setdefault(pipe.protocol.hubs, []).append((pipe, buf))
+                    else:
+                        pipe.protocol.finish()
+        rest = [pid for pid in sorted(self.pipes) if pid not in done]
         # several pipelines: each trains on its own stream (a linear pipeline's exact scan
         # occupies 16 CUs, so M of them run side by side), joined before the collectives
-        streams = self._pipe_streams() if len(self.pipes) > 1 else None
+        streams = self._pipe_streams() if len(rest) > 1 else None
         main = torch.cuda.current_stream(self.device) if streams else None
-        for i, pid in enumerate(sorted(self.pipes)):
+        for i, pid in enumerate(rest):
             pipe = self.pipes[pid]
             st = streams[i % len(streams)] if streams else None
             if st is not None:
@@ -415,6 +433,25 @@ class Job:
                                                      for _, b in items))
             for pipe, _ in items:
                 pipe.protocol.finish()
+
+    def _fused_groups(self, routed) -> list:
+        """Pipelines whose rounds share one launch: ≥ 2 hashed-linear Synchronous pipelines
+        without preprocessors, on a GPU, with equal ``group_key`` (same prep and rule)."""
+        if self.device.type != "cuda" or len(self.pipes) < 2 or not routed.B or \
+                str(self.cfg.fusePipelines).lower() in ("false", "0"):
+            return []
+        from omldm_amd.models.linear import LinearLearner
+
+        by_key: dict = {}
+        for pid in sorted(self.pipes):
+            p = self.pipes[pid]
+            if p.preprocessors or not isinstance(p.protocol, Synchronous) or \
+                    not isinstance(p.learner, LinearLearner) or not p.protocol.fusable():
+                continue
+            k = p.learner.group_key(routed, p.protocol._ctx(fused=True))
+            if k is not None:
+                by_key.setdefault((k, p.protocol.hubs), []).append(p)
+        return [g for g in by_key.values() if len(g) >= 2]
 
     def _pipe_streams(self):
         n = int(self.cfg.pipelineStreams)

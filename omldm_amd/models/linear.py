@@ -166,6 +166,57 @@ class LinearLearner(Learner):
         if not ctx.fused_delta:
             self.apply_delta()
 
+    # ------------------------------------------------------ several pipelines
+    def group_key(self, batch, ctx: RoundContext):
+        """Learners whose rounds on ``batch`` can share ONE v3 launch (same prep, same rule
+        family and variant, no shrink, fp32): a key, or None when this one cannot."""
+        if not (self.w.is_cuda and self.seq_capable() and batch.B > 0):
+            return None
+        if isinstance(batch, RawBatch):
+            rb = batch
+            R, _ = self._seq_geometry(batch.B, ctx)
+            if not L.scan3_eligible(rb, R, self.rule.bias):
+                return None
+        else:
+            b = batch.spoke_padded(max(1, int(ctx.spokes)))
+            if not self._slots_scan_eligible(b, ctx):
+                return None
+            R, _ = self._seq_geometry(b.B, ctx)
+            if not (L.SEQ_KERNEL == "scan3" and L.scan3_fits(b.dn, b.dc, R, self.rule.bias)
+                    and self.space.dn + b.dc * b.cat_span <= self.dim - 1):
+                return None
+        r = self.rule
+        return (self.dim, r.rule, r.variant, r.bias, r.C if r.variant == L.PA2 else None)
+
+    @staticmethod
+    def fit_group(learners: list, batch, ctx: RoundContext) -> None:
+        """One round of every learner in ``learners`` (equal ``group_key``) on ``batch`` in
+        one launch (ops.linear.linear_scan3_round_multi) — each learner ends exactly as its
+        own ``fit`` would leave it."""
+        first = learners[0]
+        hashed = False
+        if isinstance(batch, RawBatch):
+            rb = batch
+        else:
+            b = batch.spoke_padded(max(1, int(ctx.spokes)))
+            rb = RawBatch(b.num.float().contiguous(), b.cat.contiguous(), b.y.float().contiguous(),
+                          span=b.cat_span, cbase=first.space.dn)
+            rb.prep = getattr(b, "prep", None)
+            hashed = True
+        R, S = first._seq_geometry(rb.B, ctx)
+        step = L.scan3_max_pipes()
+        for i in range(0, len(learners), step):
+            grp = learners[i:i + step]
+            L.linear_scan3_round_multi([lr.w for lr in grp], rb, R, S, [lr.dacc for lr in grp],
+                                       [lr.rule for lr in grp], ctx.inv_p,
+                                       [lr.cum for lr in grp], hashed=hashed)
+        if not isinstance(batch, RawBatch):
+            batch.prep = rb.prep
+        for lr in learners:
+            lr._seq_pending = False
+            if not ctx.fused_delta:
+                lr.apply_delta()
+
     def fit(self, batch: HashedBatch, ctx: RoundContext) -> None:
         if isinstance(batch, RawBatch):
             if self.seq_capable():

@@ -481,24 +481,26 @@ def _s3_next_epoch(g: list) -> int:
     return g[1]
 
 
-def _s3_run_ptrs(sp: "Scan3Prep", dev, stream: int):
-    """The prep's 4 model-independent workspaces + this stream's 4 run-time ones, and the
-    stream's granule buffer entry [tensor, epoch]."""
+def _s3_run_ptrs(sp: "Scan3Prep", dev, stream: int, lane: int = 0):
+    """The prep's 4 model-independent workspaces + this stream's 4 run-time ones (run-time
+    set ``lane`` of the stream: pipelines of one multi-pipeline launch each take their own),
+    and the set's granule buffer entry [tensor, epoch]."""
     import ctypes
 
-    key = (id(sp), stream)
+    sk = stream if lane == 0 else (stream, lane)
+    key = (id(sp), sk)
     hit = _S3_RUN_CACHE.get(key)
-    if hit is not None and hit[0] is sp and hit[3][0] is _S3_GRAN.get((str(dev), stream), [None])[0]:
+    if hit is not None and hit[0] is sp and hit[3][0] is _S3_GRAN.get((str(dev), sk), [None])[0]:
         return hit[1], hit[3]
     run = []
     gran = None
     for i in _S3_SHARED:
         n = sp.bufs[i].numel()
         if S3_BUFS[i] == "cout":
-            gran = _s3_granules(dev, n, stream)
+            gran = _s3_granules(dev, n, sk)
             run.append(gran[0])
         else:
-            run.append(_workspace(dev, n, key=f"s3_{S3_BUFS[i]}@{stream}", per_stream=False))
+            run.append(_workspace(dev, n, key=f"s3_{S3_BUFS[i]}@{sk}", per_stream=False))
     ptrs = (ctypes.c_void_p * len(S3_BUFS))(*([b.data_ptr() for b in sp.bufs[:4]] +
                                               [b.data_ptr() for b in run]))
     if len(_S3_RUN_CACHE) > 256:
@@ -596,6 +598,59 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
         check(rc, "omldm_scan3_run")
         if on_part is not None:
             on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts, span))
+    _s3_mark_read(sp)
+
+
+def scan3_max_pipes() -> int:
+    return int(_s3_lib().omldm_scan3_max_pipes())
+
+
+def linear_scan3_round_multi(ws: list, batch: RawBatch, R: int, S: int, daccs: list,
+                             rules: list, inv_p: float, cums: list | None = None,
+                             hashed: bool = False) -> None:
+    """M Synchronous rounds of M pipelines on ONE batch through ONE v3 launch (BASELINE
+    config 5: concurrent classifiers on the same stream; csrc/kernels/linear_scan3.hip
+    s3_scan_kernel with M pipelines): one shared prep, per pipeline its model, accumulator,
+    granule buffer and rule constants. Every rule must share the prep (same row scaling)
+    and the update family; each accumulator ends as ``linear_scan3_round``'s would."""
+    import ctypes
+
+    M = len(ws)
+    assert 1 <= M <= scan3_max_pipes() and len(daccs) == M and len(rules) == M
+    r0 = rules[0]
+    dim = int(daccs[0].shape[0]) - 2
+    key = _s3_key(batch, R, S, dim, r0.bias, r0)
+    assert all(_s3_key(batch, R, S, dim, r.bias, r) == key and r.rule == r0.rule and
+               r.variant == r0.variant for r in rules), "pipelines must share the prep and rule"
+    sp = batch.prep
+    if not (isinstance(sp, Scan3Prep) and sp.key == key):
+        sp = linear_scan3_prepare(batch, R, S, dim, bool(r0.bias), r0, hashed=hashed,
+                                  slot=_s3_slot_for(key, ws[0].device))
+        batch.prep = sp
+    elif sp.event is not None:
+        torch.cuda.current_stream(ws[0].device).wait_event(sp.event)
+    global SCAN3_ROUNDS
+    SCAN3_ROUNDS += 1
+    h = _s3_lib()
+    stream = native.stream_of(ws[0])
+    span = _s3_span(batch, dim)
+    ptrs, epochs, arrives = [], [], []
+    for m in range(M):
+        pm, gran = _s3_run_ptrs(sp, ws[m].device, stream, lane=m)
+        ptrs += list(pm)
+        epochs.append(_s3_next_epoch(gran))
+        arrives.append(None if _S3_TAIL_KERNEL else
+                       gran[0].data_ptr() + (gran[0].numel() // 2 - 1) * 8)
+    cums = cums if cums is not None else [None] * M
+    P = lambda ts: (ctypes.c_void_p * M)(*[ptr(t) for t in ts])  # noqa: E731
+    F = lambda vs: (ctypes.c_float * M)(*[float(v) for v in vs])  # noqa: E731
+    num, y = batch.num, batch.y
+    check(h.omldm_scan3_run_multi(
+        M, P(ws), P(daccs), P(cums), F([r.C for r in rules]), F([r.eps for r in rules]),
+        F([r.lr for r in rules]), F([inv_p] * M), (ctypes.c_void_p * (8 * M))(*ptrs),
+        (ctypes.c_uint * M)(*epochs), (ctypes.c_void_p * M)(*arrives), num.shape[1], batch.dc,
+        ptr(y), int(y.dtype == torch.int8), batch.B, R, S, dim, r0.rule, r0.variant,
+        int(r0.bias), span, 1, stream), "omldm_scan3_run_multi")
     _s3_mark_read(sp)
 
 

@@ -204,6 +204,17 @@ class Synchronous(Protocol):
             self._buf = torch.sub(L.state_vector(), self._E, out=self._d)
         return self._buf
 
+    def local_done(self) -> torch.Tensor:
+        """Phase 1 when the learner's round already ran (a fused multi-pipeline launch,
+        engine/job.py): the buffer to sum over ranks."""
+        assert self.learner.supports_fused_delta
+        self._buf = self.learner.delta_buffer()
+        return self._buf
+
+    def fusable(self) -> bool:
+        """This round may run inside a multi-pipeline launch (not the pipelined sync)."""
+        return self.learner.supports_fused_delta and not self._pipelined()
+
     def finish(self) -> None:
         L, buf = self.learner, self._buf
         if L.supports_fused_delta:

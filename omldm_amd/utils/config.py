@@ -79,6 +79,7 @@ class JobConfig:
     ingestCopy: str = "pull"              # GPU staging copy: pull (kernel) | sdma (hipMemcpyAsync)
     forecastServer: str = "auto"          # per-record forecasts on the resident serving wave (auto: GPU)
     pipelineStreams: int = 8              # GPU: pipelines of a tick train on up to this many streams
+    fusePipelines: str = "true"           # GPU: hashed-linear pipelines sharing a prep: one launch
     extra: dict = field(default_factory=dict)
 
     @staticmethod

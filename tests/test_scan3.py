@@ -154,152 +154,6 @@ def _scan3_model(w, batch, space, R, S, C=1.0, bias=True):
     return w0 + acc / n_act
 
 
-def _occurrence_flags4(cat: np.ndarray, a: int, b: int):
-    """v4's flags pass (DIST = 3): a slot whose first and last occurrences are ≥ 3 chunks
-    apart gets a table id; per occurrence (table id or −1, TG, INIT, LAST)."""
-    out = {}
-    lid = 0
-    for f in range(cat.shape[1]):
-        first, last = {}, {}
-        for t in range(a, b):
-            c = int(cat[t, f])
-            if c == -1:
-                continue
-            s = c & 0x7FFFFFFF
-            first.setdefault(s, t - a)
-            last[s] = t - a
-        ids = {}
-        for s in sorted(first):
-            if (last[s] >> 6) - (first[s] >> 6) >= 3:
-                ids[s] = lid
-                lid += 1
-        for t in range(a, b):
-            c = int(cat[t, f])
-            if c == -1:
-                continue
-            s, r = c & 0x7FFFFFFF, t - a
-            tab = s in ids
-            out[(t, f)] = (ids.get(s, -1), tab and (r >> 6) > (first[s] >> 6),
-                           tab and r == first[s], tab and r == last[s])
-    return out, lid
-
-
-def _scan4_model(w, batch, space, R, S, C=1.0, bias=True):
-    """NumPy model of the v4 split spoke (s4_scan_kernel, PA-I): the table workgroup
-    scatters chunk j (table occurrences into the slot table, the others straight into the
-    accumulator, a table slot's Δ = table − w0 at its last occurrence) and then builds chunk
-    j + 3's categorical base margins; the dense waves' margins of chunk k use the dense
-    weights through chunk k − 3; the scanner adds X1_k·c_{k−1} + X2_k·c_{k−2} and runs the
-    in-chunk G_k recurrence. The accumulator is assembled the way the kernel does it."""
-    dim = space.dim
-    cat = hash_raw(batch.tok, space).numpy()
-    num = batch.num.double().numpy()
-    y = batch.y.double().numpy()
-    B = batch.B
-    w0 = w.double().numpy()
-    dcols = list(range(space.dn)) + ([dim - 1] if bias else [])
-    acc, n_act = np.zeros(dim), 0
-    for s in range(S):
-        a, b = min(s * R, B), min(s * R + R, B)
-        if a >= b:
-            continue
-        n_act += 1
-        flags, _ = _occurrence_flags4(cat, a, b)
-        table = {}
-        wn = w0[dcols].copy()
-        chunks = []
-        for c0 in range(a, b, CH):
-            rows = list(range(c0, min(b, c0 + CH)))
-            X = np.zeros((len(rows), dim))
-            for i, t in enumerate(rows):
-                X[i, :space.dn] = num[t]
-                for f in range(space.dc):
-                    cc = int(cat[t, f])
-                    if cc != -1:
-                        X[i, cc & 0x7FFFFFFF] += -1.0 if cc < 0 else 1.0
-                if bias:
-                    X[i, dim - 1] = 1.0
-            chunks.append((rows, X))
-        nch = len(chunks)
-        cs, mcat, md = [], {}, {}
-
-        def build(m):  # WG-T: categorical base margins of chunk m
-            rows, _ = chunks[m]
-            base = np.zeros(len(rows))
-            for i, t in enumerate(rows):
-                for f in range(space.dc):
-                    cc = int(cat[t, f])
-                    if cc == -1:
-                        continue
-                    lid, tg, init, _ = flags[(t, f)]
-                    sl = cc & 0x7FFFFFFF
-                    v = table[lid] if tg else w0[sl]
-                    if init:
-                        table[lid] = w0[sl]
-                    base[i] += -v if cc < 0 else v
-            mcat[m] = base
-
-        def scatter(j):  # WG-T: chunk j's updates
-            rows, _ = chunks[j]
-            for i, t in enumerate(rows):
-                for f in range(space.dc):
-                    cc = int(cat[t, f])
-                    if cc == -1:
-                        continue
-                    lid, _, _, _ = flags[(t, f)]
-                    val = -cs[j][i] if cc < 0 else cs[j][i]
-                    if lid >= 0:
-                        table[lid] += val
-                    else:
-                        acc[cc & 0x7FFFFFFF] += val
-            for i, t in enumerate(rows):
-                for f in range(space.dc):
-                    cc = int(cat[t, f])
-                    if cc != -1 and flags[(t, f)][3]:
-                        sl = cc & 0x7FFFFFFF
-                        acc[sl] += table[flags[(t, f)][0]] - w0[sl]
-
-        for m in range(min(3, nch)):
-            build(m)
-        for k in range(nch):
-            rows, X = chunks[k]
-            if k >= 3:  # the dense waves: weights through chunk k − 3
-                wn = wn + chunks[k - 3][1][:, dcols].T @ cs[k - 3]
-            md[k] = X[:, dcols] @ wn
-            m0 = mcat[k] + md[k]
-            if k >= 1:
-                m0 += (X @ chunks[k - 1][1].T) @ cs[k - 1]
-            if k >= 2:
-                m0 += (X @ chunks[k - 2][1].T) @ cs[k - 2]
-            G = X @ X.T
-            n2 = (X * X).sum(1)
-            cvec = np.zeros(len(rows))
-            for i, t in enumerate(rows):
-                m = m0[i] + (cvec[:i] * G[i, :i]).sum()
-                cvec[i] = min(C, max(0.0, 1 - y[t] * m) / n2[i]) * y[t]
-            cs.append(cvec)
-            scatter(k)
-            if k + 3 < nch:
-                build(k + 3)
-        for j, (rows, X) in enumerate(chunks):  # the dense columns (the round's tail)
-            acc[dcols] += X[:, dcols].T @ cs[j]
-    return w0 + acc / n_act
-
-
-def test_table_schedule_of_the_v4_split_spoke_is_exact():
-    """v4's schedule (distance-3 table, X2 fold, WG-T's accumulator route with last-
-    occurrence flushes) gives the exact sequential spokes."""
-    space = FeatureSpace(4, 0, 6, 1 << 9)
-    batch = synth_raw(space, 900, seed=3, missing=0.05)
-    w = torch.randn(space.dim, generator=torch.Generator().manual_seed(5)) * 0.01
-    for R, S in ((450, 2), (300, 3), (64, 15), (200, 5), (900, 1)):
-        ref = _blocked_gram_scan(w, batch, space, R, S, C=0.7)
-        v4 = _scan4_model(w, batch, space, R, S, C=0.7)
-        assert np.allclose(v4, ref, atol=1e-10, rtol=1e-9), np.abs(v4 - ref).max()
-    flags, n = _occurrence_flags4(hash_raw(batch.tok, space).numpy(), 0, 900)
-    assert n > 0 and any(v[3] for v in flags.values())
-
-
 def test_table_schedule_of_the_v3_scan_is_exact():
     """Which occurrences read / initialise / update the slot table, and when, gives the
     exact sequential spoke (tiny hash space: many table slots, repeats in a chunk)."""
@@ -403,9 +257,10 @@ def mode3():
                                                (3, 1300, 13, L.RULE_EPS, 1),
                                                (4, 2000, 13, L.RULE_LOGISTIC, 0),
                                                (2, 200, 20, L.RULE_HINGE, 0)])
-def test_gpu_scan4_split_spoke_matches_v3_and_cpu(S, R, dn, rule, task):
-    """v4 (a scanner and a table workgroup per spoke) against v3 and the CPU oracle over
-    three rounds on one granule buffer; no poll timed out (g_s3_comb_err 2 / 3)."""
+def test_gpu_scan3_rare_workgroup_mode_matches_v3_and_cpu(S, R, dn, rule, task):
+    """Round mode 4 (a rare-slot workgroup per spoke gathers the non-table occurrences' w
+    ahead of the scan, s3_rare) against mode 3 (the helpers gather them) and the CPU oracle
+    over three rounds on one granule buffer; no poll timed out (g_s3_comb_err)."""
     from omldm_amd.parallel.comm import Comm
     from omldm_amd.models.linear import LogisticRegression, RegressorPA, SVM
     from omldm_amd.parallel.protocols import Synchronous
@@ -437,51 +292,6 @@ def test_gpu_scan4_split_spoke_matches_v3_and_cpu(S, R, dn, rule, task):
         assert float(d.max()) < 2e-3 and float(d.mean()) < 1e-6, (mode, float(d.max()))
         assert res[4][1]["fitted"] == res[mode][1]["fitted"] == 3 * B
         assert abs(res[4][1]["mistakes"] - res[mode][1]["mistakes"]) <= 1e-3 * 3 * B + 2
-
-
-@gpu
-def test_gpu_scan4_prep_x2_block(monkeypatch):
-    """v4's prep block per chunk: aG | aX1 | aX2 | a | dense | y — G and X1 are v3's
-    (the same MFMA tiles), X2 = a_t·(x_t·x_s) against the rows of chunk k − 2 (dn = 0: small
-    integers, exact)."""
-    dev = _cuda()
-    space = FeatureSpace(0, 0, 26, 1 << 12)  # tiny space: many matches across chunks
-    S, R = 2, 384
-    batch = synth_raw(space, S * R, seed=7, missing=0.05).to(dev)
-    lr = L.LinearRule(rule=L.RULE_HINGE, variant=L.PA1, C=1.0, bias=True)
-    preps = {}
-    for mode in (3, 4):
-        old = L.set_scan3_mode(mode)
-        try:
-            sp = L.linear_scan3_prepare(batch, R, S, space.dim, True, lr, slot=14)
-            torch.cuda.synchronize()
-            preps[mode] = sp.bufs[3].clone().cpu()
-        finally:
-            L.set_scan3_mode(old)
-    MAT, nch = 64 * 64, R // 64
-    pf3 = 2 * MAT + 64 + 16 * 64 + 64
-    pf4 = 3 * MAT + 64 + 16 * 64 + 64
-    p3 = preps[3][: S * nch * pf3].view(S, nch, pf3)
-    p4 = preps[4][: S * nch * pf4].view(S, nch, pf4)
-    assert torch.equal(p3[..., : 2 * MAT], p4[..., : 2 * MAT])
-    assert torch.equal(p3[..., 2 * MAT:], p4[..., 3 * MAT:])
-    # X2 from the slots: a_t · Σ_f [slot match] · sign product (+ the intercept)
-    cat = hash_raw(batch.tok.cpu(), space).numpy()
-    for s in range(S):
-        for k in range(2, nch):
-            a = p4[s, k, 3 * MAT: 3 * MAT + 64].numpy()
-            X2 = p4[s, k, 2 * MAT: 3 * MAT].view(64, 64).numpy()
-            r0, q0 = s * R + k * 64, s * R + (k - 2) * 64
-            want = np.zeros((64, 64))
-            for i in range(64):
-                for j in range(64):
-                    v = 1.0  # intercept
-                    for f in range(space.dc):
-                        ci, cj = int(cat[r0 + i, f]), int(cat[q0 + j, f])
-                        if ci != -1 and cj != -1 and (ci & 0x7FFFFFFF) == (cj & 0x7FFFFFFF):
-                            v += (-1.0 if ci < 0 else 1.0) * (-1.0 if cj < 0 else 1.0)
-                    want[i, j] = a[i] * v
-            assert np.array_equal(X2, want.astype(np.float32)), (s, k)
 
 
 @gpu
