@@ -33,6 +33,7 @@ from omldm_amd.io.synthetic import synth_batch  # noqa: E402
 from omldm_amd.models.linear import SVM  # noqa: E402
 from omldm_amd.parallel.comm import init_distributed  # noqa: E402
 from omldm_amd.parallel.protocols import Synchronous  # noqa: E402
+from omldm_amd.ops import linear as L_ops  # noqa: E402
 
 
 def main(argv=None) -> int:
@@ -47,6 +48,13 @@ def main(argv=None) -> int:
                          "the chip; averaged: the round-2 geometry (8192 spokes × 16 rows, "
                          "bf16 models)")
     ap.add_argument("--streams", type=int, default=16)
+    ap.add_argument("--fused", type=int, default=1,
+                    help="exact mode: every pipeline's round in ONE launch sharing the prep "
+                         "(ops.linear.linear_scan3_round_multi) instead of one launch per "
+                         "pipeline on --streams streams")
+    ap.add_argument("--ref", type=int, default=1,
+                    help="CPU reference learners (exact sequential spokes) for the first and "
+                         "last pipeline on the same rounds: holdout accuracy must match")
     ap.add_argument("--spokes", type=int, default=None)
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--table-log2", type=int, default=10)
@@ -82,11 +90,17 @@ def main(argv=None) -> int:
         store.add(L)
         protos.append(Synchronous(comm, L, {"virtualSpokes": S}))
     streams = [torch.cuda.Stream(device) for _ in range(max(1, min(a.streams, M)))] \
-        if (exact and on_gpu) else None
+        if (exact and on_gpu and not a.fused) else None
+    fused = exact and on_gpu and bool(a.fused)
 
     def step(k):
         batch = ring[k % a.ring]
-        if streams is None:
+        if fused:
+            from omldm_amd.models.linear import LinearLearner
+
+            LinearLearner.fit_group([p.learner for p in protos], batch, protos[0]._ctx(fused=True))
+            bufs = [p.local_done() for p in protos]
+        elif streams is None:
             bufs = [p.local(batch) for p in protos]
         else:
             # one prep for the step (every pipeline's rule shares it), then the pipelines'
@@ -165,6 +179,24 @@ def main(argv=None) -> int:
         test = synth_batch(space, 20000, start=10**9, seed=25).to(device)
         sc = store.scores(test, rows)
         acc = ((sc >= 0).float() * 2 - 1 == test.y.unsqueeze(1)).float().mean(0)
+        ref = {}
+        if a.ref and exact:
+            # the CPU oracle (csrc/host/linear_cpu.cpp: exact sequential spokes) of the first and
+            # last pipeline over the same rounds (rank 0's batches: world 1 is the exact match)
+            from omldm_amd.parallel.comm import Comm
+
+            tc = test.to("cpu")
+            for i in sorted({0, M - 1}):
+                hyper = {"variant": "PA-I", "C": 0.25 * (1 + i % 8)}
+                lc = SVM(hyper, space, "cpu")
+                pc = Synchronous(Comm(), lc, {"virtualSpokes": S})
+                for k in range(a.warmup + a.steps):
+                    pc.round(ring[k % a.ring].to("cpu"))
+                s_ref = L_ops.linear_predict(lc.w, tc)
+                ref[i] = {"gpu": round(float(acc[i]), 4),
+                          "cpu_oracle": round(float(((s_ref >= 0).float() * 2 - 1 == tc.y)
+                                                    .float().mean()), 4),
+                          "max_abs_dw": float((lc.w - protos[i].learner.w.cpu()).abs().max())}
     if rank == 0:
         ex = a.steps * B * world
         print(json.dumps({
@@ -186,6 +218,8 @@ def main(argv=None) -> int:
             "latency_mode": a.latency_mode,
             "model_store_MB": round(store.bytes() / 2**20, 1),
             "holdout_accuracy_min_max": [round(float(acc.min()), 4), round(float(acc.max()), 4)],
+            "oracle_check": ref if rank == 0 else None,
+            "launches_per_step": 1 if fused else M,
         }), flush=True)
     if world > 1:
         dist.barrier()

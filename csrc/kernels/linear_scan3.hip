@@ -152,9 +152,7 @@ constexpr int HCAP = 12288;                // hash entries (≤ 8192 distinct sl
 constexpr int RPT = RMAX / FT;             // rows per thread (8)
 }  // namespace s3
 
-// M32 (round mode 4): the meta words alone, [dc][B] uint32 (the scan's helpers need no slot:
-// the round-start weights come from the w0-margin workgroups, s3_rare); else {slot, meta}.
-template <bool M32>
+// Output: the meta words, [dc][B] uint32 (the slots stay in slotsT).
 __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict__ slotsT, int B,
                                                           int R, uint32_t* __restrict__ meta,
                                                           int* __restrict__ lidcount) {
@@ -226,7 +224,6 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
     if (lloc[q] >= 0) hkey[h[q]] = lloc[q];  // the slot's key is no longer looked up
   __syncthreads();
   const int base = s_base;
-  uint2* out = reinterpret_cast<uint2*>(meta) + (size_t)f * B + t0;  // {slot, meta}
 #pragma unroll
   for (int q = 0; q < s3::RPT; ++q) {
     const int i = tid + q * s3::FT;
@@ -243,8 +240,7 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
         m |= (uint32_t)(base + hkey[h[q]]) << s3::LID_SHIFT;
       }
     }
-    if constexpr (M32) meta[(size_t)f * B + t0 + i] = m;
-    else out[i] = make_uint2((uint32_t)v[q], m);
+    meta[(size_t)f * B + t0 + i] = m;
   }
 }
 
@@ -546,12 +542,9 @@ constexpr unsigned SPIN_MAX = 1u << 21;      // polls before a combiner gives up
 // the scanner and only the last chunk is left when the scan ends (one wave per field, every
 // chunk, fell behind: its slot loads and its poll were one round trip each per chunk). All
 // of a chunk's slot loads are issued before the poll. Rows with c = 0 add nothing.
-__device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int dc, int B, int R,
-                                           const S3Comb& cb, S3Smem& sm, int base, int bid,
-                                           int nblk) {
-  const int i = bid - base;
-  const int s = i % cb.S_act, part = i / cb.S_act;
-  const int nparts = (nblk - base) / cb.S_act;
+__device__ __forceinline__ void s3_combine_spoke(const int* __restrict__ slotsT, int dc, int B,
+                                                 int R, const S3Comb& cb, S3Smem& sm, int s,
+                                                 int part, int nparts) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int* hk = reinterpret_cast<int*>(&sm.G[0][0][0]);
   float* hv = &sm.X1[0][0][0];
@@ -689,6 +682,14 @@ __device__ __forceinline__ void s3_rare(const int* __restrict__ slotsT, int dc, 
   }
 }
 
+// A combiner workgroup: spoke i mod S_act, part i / S_act of the combiner blocks.
+__device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int dc, int B, int R,
+                                           const S3Comb& cb, S3Smem& sm, int base, int bid,
+                                           int nblk) {
+  const int i = bid - base;
+  s3_combine_spoke(slotsT, dc, B, R, cb, sm, i % cb.S_act, i / cb.S_act, (nblk - base) / cb.S_act);
+}
+
 // Forward: the tail body (defined with the combine pass below).
 __device__ void s3_dense_body(const float* __restrict__ ws, const float* __restrict__ wsd,
                               int S_act, int dn, int dim, int bias, float inv_p,
@@ -734,9 +735,25 @@ __device__ __forceinline__ void s3_scan_arrive(const S3Comb& cb, const float* __
 // from its granule (rgran), the helpers gather only the table slots' first occurrences.
 // One pipeline's workgroup `bid` of the round (`nblk` per pipeline): [0, S_act) the scan
 // workgroups, [S_act, 2·S_act) the rare-slot ones (RARE), then the combiners.
+// End of a scan workgroup with rows (every wave): with `tail` (a launch too large for
+// in-launch combiners) the workgroup folds its own spoke's c·sign into the accumulator now
+// that its scan is done (s3_combine_spoke over its LDS, free after the last chunk), then
+// the arrival / round tail.
+__device__ __forceinline__ void s3_spoke_end(bool tail, const int* __restrict__ slotsT, int dc,
+                                             int B, int R, const S3Comb& cb,
+                                             const float* __restrict__ ws,
+                                             const float* __restrict__ wsd, int dn, int dim,
+                                             const SeqParams& p, S3Smem& sm, int s) {
+  if (tail) {
+    __syncthreads();  // the scanner is done with G / X1
+    s3_combine_spoke(slotsT, dc, B, R, cb, sm, s, 0, 1);
+  }
+  s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
+}
+
 template <int RULE, int KN, bool RARE>
 __device__ __forceinline__ void s3_scan_body(
-    int bid, int nblk, S3Smem& sm, float* tab,
+    int bid, int nblk, bool tail, S3Smem& sm, float* tab,
     const int* __restrict__ slotsT, const uint32_t* __restrict__ meta, int dc, int dn,
     const void* __restrict__ yv, int B, int R, const float* __restrict__ prep, int nchs,
     const float* __restrict__ w, int dim, float* __restrict__ aglob, int cap, long long gstride,
@@ -878,7 +895,7 @@ __device__ __forceinline__ void s3_scan_body(
       wr[6] = 0.f;
       wr[7] = 0.f;
     }
-    s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
+    s3_spoke_end(tail, slotsT, dc, B, R, cb, ws, wsd, dn, dim, p, sm, s);
     return;
   }
 
@@ -945,15 +962,17 @@ __device__ __forceinline__ void s3_scan_body(
       }
       return;
     }
+    // the helpers gather the non-table occurrences' w0 themselves: slot and meta word
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
       const int f = q + s3::NHA * i;
       const int row = t0 + ch * s3::CH + r;
       const bool ok = ch >= 0 && ch < nch && f < dc && row < t1;
       const size_t at = ok ? (size_t)f * B + row : 0;
-      const uint2 o = reinterpret_cast<const uint2*>(meta)[at];
-      S.cs[i] = ok ? (int)o.x : -1;
-      S.cm[i] = ok ? o.y : 0u;
+      const int sl = slotsT[at];
+      const uint32_t mm = meta[at];
+      S.cs[i] = ok ? sl : -1;
+      S.cm[i] = ok ? mm : 0u;
     }
   };
   auto issue_gathers = [&](Set& S) {
@@ -1156,16 +1175,17 @@ __device__ __forceinline__ void s3_scan_body(
     if (lane == 0 && j < KN) wsd[(size_t)s * s3::DS + j] = wn[i] - w0[i];
   }
   if (q == 0 && lane >= KN && lane < s3::DS) wsd[(size_t)s * s3::DS + lane] = 0.f;
-  s3_scan_arrive(cb, ws, wsd, dn, dim, p, sm);
+  s3_spoke_end(tail, slotsT, dc, B, R, cb, ws, wsd, dn, dim, p, sm, s);
 }
 
 // Several pipelines that share one prep (the same batch and row scaling: BASELINE config 5's
 // concurrent classifiers) in ONE launch, each with its own model, accumulator, granule
-// buffers and rule constants (one pipeline is the M = 1 case). Blocks are role-major — every
-// pipeline's rare-slot workgroups, then the scan workgroups, then the combiners — so the grid
-// needs no co-residency: a block only waits on roles dispatched before it (a scan on its
-// rare-slot workgroup, a combiner on its scan), which never wait on it. One launch also
-// sidesteps the four hardware queues per process that capped concurrent pipeline streams.
+// buffers and rule constants (one pipeline is the M = 1 case). Blocks are pipeline-major and,
+// within a pipeline, role-major — its w0-margin workgroups (RARE), its scan workgroups, its
+// combiners — so the grid needs no co-residency: a block only waits on blocks dispatched
+// before it (a scan on its w0 workgroup, a combiner on its scan), which never wait on it, and
+// the later pipelines' blocks take the CUs the earlier ones free. One launch also sidesteps
+// the four hardware queues per process that capped concurrent pipeline streams.
 constexpr int kS3MaxPipes = 16;
 struct S3Pipe {
   const float* w;
@@ -1178,7 +1198,8 @@ struct S3Pipe {
 };
 struct S3Pipes {
   int M;
-  int ncomb;
+  int ncomb;  // combiner workgroups per spoke (0: none)
+  int tail;   // 1: each scan workgroup combines its own spoke after its scan
   S3Pipe pipe[kS3MaxPipes];
 };
 
@@ -1189,22 +1210,14 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     int dim, int cap, long long gstride, int S_act, S3Pipes pp) {
   __shared__ S3Smem sm;
   extern __shared__ float tab[];  // [cap] + 64 scratch words (one per lane)
-  const int b = (int)blockIdx.x, M = pp.M;
-  const int nr = RARE ? M * S_act : 0, ns = M * S_act;
-  int pi, bid;
-  if (b < nr) {  // rare-slot workgroups first
-    pi = b / S_act;
-    bid = S_act + b % S_act;
-  } else if (b < nr + ns) {
-    pi = (b - nr) / S_act;
-    bid = (b - nr) % S_act;
-  } else {
-    const int c = b - nr - ns, per = S_act * pp.ncomb;
-    pi = c / per;
-    bid = S_act * (RARE ? 2 : 1) + c % per;
-  }
+  const int nblk = S_act * ((RARE ? 2 : 1) + pp.ncomb);  // per pipeline
+  const int pi = (int)blockIdx.x / nblk, local = (int)blockIdx.x % nblk;
+  int bid;
+  if (RARE && local < S_act) bid = S_act + local;  // its w0-margin workgroups first
+  else if (RARE && local < 2 * S_act) bid = local - S_act;
+  else bid = local;  // (!RARE: scan blocks [0, S_act), combiners after)
   const S3Pipe& P = pp.pipe[pi];
-  s3_scan_body<RULE, KN, RARE>(bid, S_act * ((RARE ? 2 : 1) + pp.ncomb), sm, tab, slotsT, meta,
+  s3_scan_body<RULE, KN, RARE>(bid, nblk, pp.tail != 0, sm, tab, slotsT, meta,
                                dc, dn, yv, B, R, prep, nchs, P.w, dim, P.aglob, cap, gstride,
                                P.cb, P.ws, P.wsd, P.p, P.rgran);
 }
@@ -1428,10 +1441,10 @@ OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn,
   const long long pf = kn == 16 ? s3_prep_floats<16>() : s3_prep_floats<32>();
   switch (which) {
     case 0: return (long long)dc * B;
-    case 1: return 2LL * dc * B;  // {slot, meta} per occurrence
+    case 1: return (long long)dc * B;  // meta word per occurrence
     case 2: return S;
     case 3: return (long long)S * nchs * pf;
-    case 4: return (g_s3_mode == 4 ? 4LL : 2LL) * B;  // c granules (+ mode 4: rare margins)
+    case 4: return 4LL * B;  // c granules + the w0-margin granules (mode 4)
     case 5: return (long long)S * s3::WS;
     case 6: return (long long)S * s3::DS;
     case 7: return (long long)S * ((long long)R * dc / 2 + 64);
@@ -1530,12 +1543,8 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
     hipStreamWaitEvent(sd->side, sd->fork, 0);
     gst = sd->side;
   }
-  if (g_s3_mode == 4)
-    hipLaunchKernelGGL(s3_flags_kernel<true>, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B,
-                       R, W.meta, W.lidcount);
-  else
-    hipLaunchKernelGGL(s3_flags_kernel<false>, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B,
-                       R, W.meta, W.lidcount);
+  hipLaunchKernelGGL(s3_flags_kernel, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
+                     W.meta, W.lidcount);
   const int nchs = (R + s3::CH - 1) / s3::CH;
   const int affine = rule != kSeqLogistic;
   const float kadd = (rule != kSeqLogistic && variant == 2) ? 0.5f / C : 0.f;
@@ -1583,11 +1592,30 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   const int kn = s3_kn(dn, bias);
   const int cap = omldm_scan3_lds_cap();
   const long long gstride = (long long)R * dc / 2 + 64;
-  const bool rare = g_s3_mode == 4;
-  const int ncomb = g_s3_comb;
+  // latency form (mode 4, the whole grid fits the GPU at one workgroup per CU): w0-margin
+  // workgroups + in-launch combiners beside the scans; throughput form (more pipelines than
+  // fit): one self-contained workgroup per spoke — helpers gather, the spoke combined by its
+  // own workgroup after its scan. Mode 3: helpers gather, in-launch combiners.
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
+  int ncomb = g_s3_comb;
+  bool rare = g_s3_mode == 4 && ncomb > 0;
+  bool tail = false;
+  if (rare && (long long)M * S_act * (2 + ncomb) > ncu - 16) {
+    rare = false;
+    tail = true;
+    ncomb = 0;
+  }
   S3Pipes pp{};
   pp.M = M;
   pp.ncomb = ncomb > 0 ? ncomb : 0;
+  pp.tail = tail ? 1 : 0;
   for (int m = 0; m < M; ++m) {
     if (epoch[m] == 0u) return -2;
     const S3Ws Wm = s3_ws(ptrs + 8 * m);
@@ -1610,7 +1638,7 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   if (e) return e;
   for (int m = 0; m < M; ++m) {
     const S3Ws Wm = s3_ws(ptrs + 8 * m);
-    if (ncomb > 0) {  // the categorical slots were combined in the scan's launch
+    if (ncomb > 0 || tail) {  // the categorical slots were combined in the scan's launch
       if (!arrive[m])
         hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, Wm.ws, Wm.wsd, S_act, dn,
                            dim, bias, inv_p[m], dacc[m], cum[m]);
