@@ -205,7 +205,8 @@ def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dic
             args += [f"--{k}", f"file://{root}"]
         cfg = JobConfig.from_args(args + ["--hashDim", str(sp.dim), "--fieldAware", "true",
                                           "--batchSize", str(batch), "--timeout", "1000",
-                                          "--test", "false", "--jobName", "bench-e2e"])
+                                          "--test", "false", "--jobName", "bench-e2e"]
+                              + os.environ.get("OMLDM_E2E_ARGS", "").split())
         dev = torch.device("cuda", torch.cuda.current_device())
         job = Job(cfg, Comm.local(), dev)
         while not job.pipes:

@@ -87,6 +87,9 @@ class HashedBatch:
     # a v3 scan prep made for this batch (ops.linear.Scan3Prep), shared by the pipelines
     # that train on it within a tick; a plain attribute like ``shards``
     prep = None
+    # (spokes, padded batch): spoke_padded's result, made once per tick (engine/job.py may
+    # make it ahead on its prep stream)
+    _padded = None
 
     @property
     def B(self) -> int:
@@ -189,6 +192,8 @@ class HashedBatch:
         sh = self.shards
         if sh is None or len(sh) != spokes or len(set(sh)) <= 1 or not self.B:
             return self
+        if self._padded is not None and self._padded[0] == spokes:
+            return self._padded[1]
         R = max(sh)
         idx = np.full(spokes * R, self.B, dtype=np.int64)  # row B: the blank row
         o = 0
@@ -201,6 +206,7 @@ class HashedBatch:
         y = torch.cat([self.y, self.y.new_full((1,), float("nan"))])
         out = HashedBatch(num[ix], cat[ix], y[ix], None, self.cat_span)
         out.shards = (R,) * spokes
+        self._padded = (spokes, out)
         return out
 
     def dense(self, dim: int | None = None) -> torch.Tensor:

@@ -179,6 +179,9 @@ class Job:
         # event pairs, no host sync: utils/devtimer.py)
         self._train_timer = self._coll_timer = None
         self._health = None
+        self._ready_ev = None          # the staging slot's parse event (route ahead)
+        self._route_stream = None
+        self._holdout_read_ev = None   # compute-stream reads of the holdout rings (queries)
         if self.device.type == "cuda":
             from omldm_amd.utils.devtimer import LaggedTimer
             from omldm_amd.utils.health import DeviceHealth
@@ -375,13 +378,51 @@ class Job:
             raw = RawRecords.from_view(batch.raw, fidx)
             self._forecast(batch.without_raw().select(torch.from_numpy(fidx)).to(self.device), raw)
 
+    def _route_ahead(self, batch: HashedBatch):
+        """GPU ticks whose training rows are a parsed staging slot (``self._ready_ev``):
+        the holdout routing and the v3 prep of the linear pipelines run on the route stream,
+        which waits only for that slot's parse — not for the previous tick's round on the
+        compute stream — so they overlap it; the compute stream waits for them. None: the
+        caller routes on the compute stream."""
+        ev_in = self._ready_ev
+        if ev_in is None or self.device.type != "cuda" or not batch.B or \
+                str(self.cfg.routeAhead).lower() in ("false", "0"):
+            return None
+        from omldm_amd.models.linear import LinearLearner
+
+        if self._route_stream is None:
+            self._route_stream = torch.cuda.Stream(self.device)
+        ps, cur = self._route_stream, torch.cuda.current_stream(self.device)
+        ps.wait_event(ev_in)
+        if self._holdout_read_ev is not None:  # queries read the rings the route rewrites
+            ps.wait_event(self._holdout_read_ev)
+            self._holdout_read_ev = None
+        with torch.cuda.stream(ps):
+            routed = self.holdout.route(batch)
+            for pid in sorted(self.pipes):
+                p = self.pipes[pid]
+                if isinstance(p.learner, LinearLearner) and not p.preprocessors and \
+                        p.learner.prepare_ahead(routed, p.protocol._ctx(fused=True), ps):
+                    break  # one prep per tick (pipelines of another prep key make theirs)
+        padded = routed._padded[1] if routed._padded is not None else None
+        for b in (routed, padded):
+            if b is not None:
+                for t in (b.num, b.cat, b.y):
+                    t.record_stream(cur)  # allocated on the route stream, read on compute
+        ev = torch.cuda.Event()
+        ev.record(ps)
+        cur.wait_event(ev)
+        return routed
+
     def _train(self, batch: HashedBatch, direct: HashedBatch | None = None):
         """One round of every pipeline. Synchronous pipelines train first and their
         round buffers are summed over ranks in ONE coalesced collective per hub layout
         (one flat bucket instead of one launch per pipeline); the other
         protocols run their own rounds."""
         with tracing.range("route"):
-            routed = self.holdout.route(batch)
+            routed = self._route_ahead(batch) if direct is None else None
+            if routed is None:
+                routed = self.holdout.route(batch)
         if direct is not None and direct.B:  # rows that bypass the holdout (no spoke layout)
             routed = HashedBatch.cat_batches([direct, routed]) if routed.B else direct
         groups: dict[int, list] = {}
@@ -521,8 +562,11 @@ class Job:
         if n_local:
             with tracing.range("parse"):
                 if self._gpu_parser is not None:  # raw JSON → HBM → one thread per record
+                    self._ready_ev = None
                     if isinstance(block, TickBlock):
                         batch, op_d, cnt = self._gpu_parser.parse_block(block, self.space)
+                        if block.parsed is not None:
+                            self._ready_ev = block.staged
                     else:
                         batch, op_d, cnt = self._gpu_parser.parse(buf, offs, self.space)
                     cnt = cnt if isinstance(cnt, np.ndarray) else cnt.cpu().numpy()
@@ -543,6 +587,7 @@ class Job:
             if op is None:  # a pure, valid training block: train on it as it is
                 tb = batch.without_raw()
             else:
+                self._ready_ev = None  # the training rows are selected on the compute stream
                 opt = torch.from_numpy(op)
                 fidx = torch.nonzero(opt == OP_FORECASTING).flatten()
                 tidx = torch.nonzero(opt == OP_TRAINING).flatten()
@@ -599,6 +644,9 @@ class Job:
                     self._trace_models()
             for q in queries:
                 self._answer(q)
+            if queries and self.device.type == "cuda":
+                self._holdout_read_ev = torch.cuda.Event()
+                self._holdout_read_ev.record()
         finally:
             if fs is not None:
                 fs.end_training()

@@ -10,6 +10,8 @@ preprocessors into the learner (MLPipeline.pipePoint, hs_err_pid77107.log:111).
 """
 from __future__ import annotations
 
+import collections
+
 import os
 
 import torch
@@ -84,8 +86,11 @@ class Pipeline:
         # running statistics (reference Statistics / learning curve, FlinkHub.scala:95-156)
         self.learning_curve: list[tuple[float, int]] = []
         self._lc_last = (0.0, 0)
-        self._lc_host = None     # pinned copy of the running totals (GPU)
-        self._lc_pending = None  # its event: the point is taken at the next tick
+        # GPU: pinned copies of the running totals behind each tick's round, with their
+        # events; a point is taken once its copy has landed (never waiting on the GPU while
+        # fewer than LC_LAG ticks are in flight)
+        self._lc_free: list = []
+        self._lc_pending: collections.deque = collections.deque()
         # mean buffer size (reference BufferingWrapper.getMeanBufferSize): the training
         # records a spoke holds when its round starts — rows of the round / local spokes
         self.spokes = max(1, int(spokes))
@@ -140,29 +145,47 @@ class Pipeline:
             return torch.where(s >= 0, 1.0, -1.0)
         return s
 
+    # ticks whose curve copies may be in flight: 1 (take the previous tick's point) measured
+    # best end to end — letting the host run further ahead put the next tick's round beside
+    # its parse on the GPU (JSON e2e 60-64 → 53 M records/s, DIB no better), A/B:
+    # OMLDM_LC_LAG (gpurun_out/r5/e2e_OMLDM_LC_LAG_*.json)
+    LC_LAG = int(os.environ.get("OMLDM_LC_LAG", "1"))
+
     def record_learning_curve(self) -> None:
         """One learning-curve point per tick: (mean loss of the rows fitted since the last
         point, rows fitted so far). On a GPU the running totals are copied to pinned
-        memory behind the tick's round and read at the next tick, so the tick never waits
-        for its own round (reading them at once was a host sync per tick)."""
+        memory behind the tick's round and read once the copy has landed — a tick never
+        waits for its own or the previous tick's round (waiting for the previous one made
+        the host and the GPU take turns; see LC_LAG)."""
         cum = self.learner.cum
         if cum.device.type != "cuda":
             self._lc_point(cum.tolist())
             return
-        self.flush_learning_curve()
-        if self._lc_host is None or self._lc_host.shape != cum.shape:
-            self._lc_host = torch.empty(cum.shape, dtype=cum.dtype, pin_memory=True)
-        self._lc_host.copy_(cum, non_blocking=True)
+        self._lc_drain(block_over=self.LC_LAG - 1)
+        host = self._lc_free.pop() if self._lc_free else None
+        if host is None or host.shape != cum.shape:
+            host = torch.empty(cum.shape, dtype=cum.dtype, pin_memory=True)
+        host.copy_(cum, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._lc_pending = ev
+        self._lc_pending.append((ev, host))
+
+    def _lc_drain(self, block_over: int) -> None:
+        """Take in the points whose copies have landed, oldest first (their order is the
+        curve's); wait only while more than ``block_over`` are still in flight."""
+        q = self._lc_pending
+        while q:
+            ev, host = q[0]
+            if len(q) <= block_over and not ev.query():
+                break
+            ev.synchronize()
+            q.popleft()
+            self._lc_point(host.tolist())
+            self._lc_free.append(host)
 
     def flush_learning_curve(self) -> None:
-        """Takes the point of the last tick in (before the curve is read or saved)."""
-        ev, self._lc_pending = self._lc_pending, None
-        if ev is not None:
-            ev.synchronize()
-            self._lc_point(self._lc_host.tolist())
+        """Takes every pending point in (before the curve is read or saved)."""
+        self._lc_drain(block_over=0)
 
     def _lc_point(self, c: list) -> None:
         loss, n = c[0], int(c[1])

@@ -188,6 +188,24 @@ class LinearLearner(Learner):
         r = self.rule
         return (self.dim, r.rule, r.variant, r.bias, r.C if r.variant == L.PA2 else None)
 
+    def prepare_ahead(self, batch: HashedBatch, ctx: RoundContext, stream) -> bool:
+        """Make the v3 prep of this learner's round on ``batch`` now, on ``stream``, and
+        attach it to the spoke-padded batch its ``fit`` will use (engine/job.py: the next
+        tick's route + prep run beside the current round). False: no v3 round here."""
+        if self.group_key(batch, ctx) is None:
+            return False
+        b = batch.spoke_padded(max(1, int(ctx.spokes)))
+        R, S = self._seq_geometry(b.B, ctx)
+        rb = RawBatch(b.num.float().contiguous(), b.cat.contiguous(), b.y.float().contiguous(),
+                      span=b.cat_span, cbase=self.space.dn)
+        key = L._s3_key(rb, R, S, self.dim, self.rule.bias, self.rule)
+        if isinstance(b.prep, L.Scan3Prep) and b.prep.key == key:
+            return True
+        b.prep = L.linear_scan3_prepare(rb, R, S, self.dim, bool(self.rule.bias), self.rule,
+                                        slot=L._s3_slot_for(key, self.w.device), stream=stream,
+                                        hashed=True)
+        return True
+
     @staticmethod
     def fit_group(learners: list, batch, ctx: RoundContext) -> None:
         """One round of every learner in ``learners`` (equal ``group_key``) on ``batch`` in

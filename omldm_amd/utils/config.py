@@ -80,6 +80,7 @@ class JobConfig:
     forecastServer: str = "auto"          # per-record forecasts on the resident serving wave (auto: GPU)
     pipelineStreams: int = 8              # GPU: pipelines of a tick train on up to this many streams
     fusePipelines: str = "true"           # GPU: hashed-linear pipelines sharing a prep: one launch
+    routeAhead: str = "true"              # GPU: holdout route + v3 prep beside the previous round
     extra: dict = field(default_factory=dict)
 
     @staticmethod

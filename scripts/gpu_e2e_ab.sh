@@ -1,8 +1,9 @@
 #!/bin/bash
-# A/B: engine ingest copy on one XCD (ingestCUs=16) vs plain streams (0), 2 reps each.
-set -u
-R=${GRAFT_REPO_ROOT:-$PWD}; cd $R; mkdir -p gpurun_out
-for rep in 1 2; do for b in 65536 131072; do for cus in 0 16; do
-  v=$(timeout -k 10 200 python bench/engine_e2e.py --records 4000000 --batch $b --ingest-cus $cus 2>/dev/null | python -c "import json,sys; print(round(json.loads(sys.stdin.read().strip().splitlines()[-1])['value']/1e6,1))") || exit 1
-  echo "rep $rep batch $b ingestCUs $cus: $v M rec/s"
-done; done; done
+# Engine end-to-end A/B (records/s of JSON and DIB topics through the whole engine).
+# Each tag is a comma-separated list of VAR=value settings (empty tag: defaults).
+set -e
+mkdir -p gpurun_out/r5
+for tag in "$@"; do
+  name=$(echo "$tag" | tr '=,-' '___')
+  env $(echo "$tag" | tr ',' ' ') timeout -k 10 200 python bench.py --steps 3 --warmup 1 --latency-samples 0 --engine-latency 0 --ref off > gpurun_out/r5/e2e_${name}.json 2> gpurun_out/r5/e2e_${name}.err
+done

@@ -64,7 +64,9 @@ def test_hip_linear_round_spills_exactly(cuda, R, name, dtype):
     d2 = torch.zeros(BIG.dim + 2, device=cuda)
     L.linear_round(w.to(cuda), b.to(cuda), R, S, d2, None, rule, 1.0 / S)
     torch.cuda.synchronize()
-    np.testing.assert_allclose(d2.cpu().numpy(), d_gpu.cpu().numpy(), rtol=1e-5, atol=1e-7)
+    # (the spokes' atomic adds into dacc land in any order: cancellations leave ~ulp(max|d|))
+    np.testing.assert_allclose(d2.cpu().numpy(), d_gpu.cpu().numpy(), rtol=1e-5,
+                               atol=1e-6 * max(1.0, float(d_cpu.abs().max())))
 
 
 @pytest.mark.gpu
