@@ -13,15 +13,16 @@ One step == one Synchronous round on every GPU, all inside the timed region:
   pinned host micro-batch on the raw binary wire (fp32 numerical features, 32-bit
   category TOKENS, int8 labels) ──pull-copy kernel on a CU-masked ingest lane (copy of
   batch k+1 overlaps the round on batch k)──► HBM
-  → passes 1-2 of the v2 round (csrc/kernels/linear_scan.hip) on their own CU-masked
-    stream as soon as the batch lands: murmur3 hashing of the tokens, then every 64-row
-    chunk's Gram G and cross Grams X1 / X2 over the whole GPU — overlapping the previous
-    round's scan (--prep-ahead)
-  → the scan: one workgroup per spoke; the scanner wave runs the exact PA-I recurrence
-    and folds each chunk's updates into the next two chunks' margins, seven helper waves
-    gather / scatter the spoke's replica (fields split between them, no fences)
-  → replica average into the round accumulator → RCCL all-reduce over xGMI (N > 1)
-  → apply: w = average, every replica ← w.
+  → passes 1-3 of the v3 round (csrc/kernels/linear_scan3.hip) on their own CU-masked
+    stream as soon as the batch lands: murmur3 hashing of the tokens, the per-field
+    occurrence sort (LDS slot-table flags), then every 64-row chunk's Gram G and cross
+    Gram X1 over the whole GPU — overlapping the previous round's scan (--prep-ahead)
+  → the scan: per spoke, a w0-margin workgroup sums the round-start model over every
+    occurrence ahead of the scan; the scan workgroup's scanner wave runs the exact PA-I
+    recurrence on the Grams, its helper waves keep the spoke's updates in an LDS slot
+    table (no dense replicas)
+  → in-launch combiners sum the spokes' updates into the round accumulator → RCCL
+    all-reduce over xGMI (N > 1) → apply: w += average update.
 Also reported (rank 0): the engine's per-record forecast latency (a JSON record produced
 into the forecasting topic → its Prediction, `engine_forecast_*`) and the engine's
 end-to-end JSON training rate (`engine_e2e_*`).
@@ -271,7 +272,7 @@ def main(argv=None) -> int:
     ap.add_argument("--scan-cus", type=int, default=0,
                     help="CUs the prep stream leaves to the round's scan (split lane)")
     ap.add_argument("--prep-ahead", type=int, default=1,
-                    help="v2 round: hash + chunk Grams of batch k+1 on their own stream")
+                    help="v3 round: hash, occurrence sort and chunk Grams of batch k+1 on their own stream")
     ap.add_argument("--hubs", type=int, default=0, help="HubParallelism (1 = reduce+bcast)")
     ap.add_argument("--latency-samples", type=int, default=2000)
     ap.add_argument("--ref", default="auto", choices=["auto", "on", "off"],
@@ -333,7 +334,7 @@ def main(argv=None) -> int:
     # stream as soon as its batch has landed, overlapping the current round's scan
     prep_stream = None
     v3 = on_gpu and L.scan3_eligible(dev[0].batch, R, learner.rule.bias)
-    if on_gpu and a.prep_ahead and (v3 or L.scan_eligible(dev[0].batch)):
+    if on_gpu and a.prep_ahead and v3:
         if a.lane == "split" and a.ingest_cus > 0:
             # the prep kernels fill every CU they may use; a few CUs (spread over the
             # XCDs) kept for the compute stream let the next scan start on time instead
@@ -363,13 +364,9 @@ def main(argv=None) -> int:
             return
         if after is not None:
             prep_stream.wait_event(after)
-        b = dev[slot].batch
-        if v3:  # passes 1-3 of the table scan (csrc/kernels/linear_scan3.hip)
-            b.prep = L.linear_scan3_prepare(b, R, S, space.dim, bool(learner.rule.bias),
-                                            learner.rule, slot=slot, stream=prep_stream)
-        else:
-            b.prep = L.linear_scan_prepare(b, R, S, space.dim, bool(learner.rule.bias),
-                                           slot=slot, stream=prep_stream)
+        b = dev[slot].batch  # passes 1-3 of the table scan (csrc/kernels/linear_scan3.hip)
+        b.prep = L.linear_scan3_prepare(b, R, S, space.dim, bool(learner.rule.bias),
+                                        learner.rule, slot=slot, stream=prep_stream)
 
     def prefetch(k: int):
         if a.ingest == "device":
@@ -597,7 +594,7 @@ def main(argv=None) -> int:
             "collective_us_per_step": None if coll_ms is None
                                       else round(float(el[1].item()) * 1e3 / a.steps, 2),
             "combiner_timeouts": comb_err,
-            "round_kernel": ("linear_scan3 (v3 table scan)" if v3 else L.SEQ_KERNEL) if on_gpu
+            "round_kernel": ("linear_scan3 (v3 table scan)" if v3 else "linear_seq (v1)") if on_gpu
                             else "cpu",
             "numa": comm.placement, "ingest_lane": a.lane if on_gpu else None,
             "device": torch.cuda.get_device_name(device) if on_gpu else "cpu",

@@ -4,7 +4,7 @@
 // spokes' updates straight into the round accumulator over the whole GPU instead of
 // averaging dense replicas.
 //
-// Semantics as linear_scan.hip / linear_seq.hip (the reference's spoke,
+// Semantics as linear_seq.hip (the reference's spoke,
 // omldm/operators/spoke/FlinkSpoke.scala:92-107, with the Synchronous PS averaging the
 // replicas): P spokes, spoke s fits rows [s·R, (s+1)·R) strictly one example at a time on
 // its own replica of w, the round's model is the replica average. For additive learners

@@ -713,7 +713,7 @@ OMLDM_API int omldm_linear_seq_round(const float* w, const float* num, int dn, c
   return (int)hipGetLastError();
 }
 
-// Round end shared with linear_scan.hip: replicas of the S_act active spokes averaged into
+// Round end of the v1 round: replicas of the S_act active spokes averaged into
 // the round accumulator, spoke statistics into the running totals.
 OMLDM_API int omldm_linear_seq_reduce(const float* rep, const float* w, int S_act, int dim,
                                       float* dacc, float inv_p, const float* ws, double* cum,

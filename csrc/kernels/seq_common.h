@@ -1,5 +1,5 @@
 // Shared pieces of the exact sequential linear rounds (linear_seq.hip: one workgroup per
-// spoke builds and scans each chunk; linear_scan.hip: chunk Grams precomputed by the
+// spoke builds and scans each chunk; linear_scan3.hip: chunk Grams precomputed by the
 // whole GPU, one scan workgroup per spoke): the update rules and the round parameters.
 #pragma once
 #include "common.h"

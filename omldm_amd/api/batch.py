@@ -263,7 +263,7 @@ class RawBatch:
     num: torch.Tensor
     tok: torch.Tensor
     y: torch.Tensor
-    # passes 1-2 of the v2 round made ahead of the round (ops.linear.ScanPrep), or None
+    # passes 1-3 of the v3 round made ahead of the round (ops.linear.Scan3Prep), or None
     prep: object = None
     # > 0: ``tok`` holds the engine's compact int16 field-aware slots (HashedBatch.cat with
     # this cat_span) instead of tokens — the v3 round reads them as they are; their slots

@@ -15,8 +15,15 @@ published Passive-Aggressive family (Crammer et al. 2006) — SURVEY.md Appendix
 * ``RegressorPA`` ε-insensitive loss, same τ family, update sign(y − w·x)·τ·x.
 * ``LogisticRegression`` (extension, BASELINE.json config 2): SGD on the log loss.
 
-All four run through one hand-written kernel (csrc/kernels/linear_spoke.hip): a round
-of S virtual spokes, each an exact sequential learner on its R-row shard.
+A round is S virtual spokes, each an exact sequential learner on its R-row shard:
+* the PA family, RegressorPA and logistic SGD (no L2 shrink, fp32 model) run the v3 table
+  scan (csrc/kernels/linear_scan3.hip: chunk Grams on the matrix cores, one scan workgroup
+  per spoke with its updates in an LDS slot table), on the raw wire and on the engine's
+  field-aware hashed batches; raw batches of a shape v3 does not take use v1
+  (csrc/kernels/linear_seq.hip, logged);
+* everything else — SVM's L2 shrink, Pegasos, bf16 models, hashed batches v3 does not
+  take — runs the spoke-table round (csrc/kernels/linear_spoke.hip: per-spoke LDS delta
+  tables spilling to HBM, spoke_table.h).
 """
 from __future__ import annotations
 
@@ -112,31 +119,27 @@ class LinearLearner(Learner):
         return R, S
 
     def _slots_scan_eligible(self, batch, ctx: RoundContext | None = None) -> bool:
-        """The engine's field-aware hashed batches train through the exact scan rounds too:
-        v3 reads the compact int16 slots as they are, v2 after widening them."""
+        """The engine's field-aware hashed batches train through the v3 table scan, which
+        reads their compact int16 slots as they are; other hashed batches take the
+        spoke-table round."""
         if not (type(batch) is HashedBatch and batch.cat_span > 0 and self.w.is_cuda
-                and self.seq_capable() and batch.B > 0 and 0 < batch.dc):
+                and self.seq_capable() and batch.B > 0 and 0 < batch.dc
+                and L.SEQ_KERNEL == "scan3"
+                and self.space.dn + batch.dc * batch.cat_span <= self.dim - 1):
             return False
-        if L.SEQ_KERNEL == "scan3":
-            R, _ = self._seq_geometry(batch.B, ctx) if ctx is not None else (batch.B, 1)
-            if L.scan3_fits(batch.dn, batch.dc, R, self.rule.bias):
-                return True
-        return L.SEQ_KERNEL in ("scan", "scan3") and L.scan_fits(batch.dn, batch.dc)
+        R, _ = self._seq_geometry(batch.B, ctx) if ctx is not None else (batch.B, 1)
+        return bool(L.scan3_fits(batch.dn, batch.dc, R, self.rule.bias))
 
     def _fit_slots(self, batch: HashedBatch, ctx: RoundContext) -> None:
         num, y = batch.num.float().contiguous(), batch.y.float().contiguous()
-        R, S = self._seq_geometry(batch.B, ctx)
+        R, _ = self._seq_geometry(batch.B, ctx)
         rb = RawBatch(num, batch.cat.contiguous(), y, span=batch.cat_span, cbase=self.space.dn)
-        # a v3 prep made ahead for this batch (shared by every pipeline of the tick that
-        # trains on it; ops.linear checks that it matches)
+        # a v3 prep made ahead for this batch (engine/job.py route stream, or the first
+        # pipeline of the tick that trains on it; ops.linear checks that it matches)
         rb.prep = getattr(batch, "prep", None)
-        if L.scan3_eligible_compact(rb, R, self.rule.bias, self.dim):  # compact slots as they are
-            self._fit_raw(rb, ctx, hashed=True)
-            batch.prep = rb.prep
-            return
-        rb = RawBatch(num, batch.to_wide().cat.contiguous(), y)
-        rb.prep = L.linear_scan_prepare_slots(rb, R, S, self.dim, bool(self.rule.bias))
-        self._fit_raw(rb, ctx)
+        assert L.scan3_eligible_compact(rb, R, self.rule.bias, self.dim), "v3 shape check"
+        self._fit_raw(rb, ctx, hashed=True)
+        batch.prep = rb.prep
 
     def _fit_raw(self, batch: RawBatch, ctx: RoundContext, hashed: bool = False) -> None:
         B = batch.B
@@ -180,10 +183,6 @@ class LinearLearner(Learner):
         else:
             b = batch.spoke_padded(max(1, int(ctx.spokes)))
             if not self._slots_scan_eligible(b, ctx):
-                return None
-            R, _ = self._seq_geometry(b.B, ctx)
-            if not (L.SEQ_KERNEL == "scan3" and L.scan3_fits(b.dn, b.dc, R, self.rule.bias)
-                    and self.space.dn + b.dc * b.cat_span <= self.dim - 1):
                 return None
         r = self.rule
         return (self.dim, r.rule, r.variant, r.bias, r.C if r.variant == L.PA2 else None)

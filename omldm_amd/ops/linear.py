@@ -6,6 +6,7 @@ identical semantics (golden oracle + CPU engine path).
 """
 from __future__ import annotations
 
+import logging
 import os
 from dataclasses import dataclass
 
@@ -14,6 +15,8 @@ import torch
 from omldm_amd.api.batch import HashedBatch, RawBatch
 from omldm_amd.ops import native
 from omldm_amd.ops.native import check, ptr
+
+log = logging.getLogger(__name__)
 
 STAT_W = 6  # loss_sum, n, mistakes, sq_err, sigma, overflow
 
@@ -246,70 +249,19 @@ SEQ_RULES = (RULE_HINGE, RULE_EPS, RULE_LOGISTIC)
 
 
 # GPU kernel of the exact sequential round: "scan3" (linear_scan3.hip, default: LDS slot
-# table per spoke, whole-GPU combine), "scan" (linear_scan.hip, v2: dense replicas) or
-# "seq" (linear_seq.hip: every spoke builds its own chunk Grams) — an A/B knob; v3 falls
-# back to v2 / v1 for shapes it does not take (> 8192 rows per spoke, > 32 fields)
+# table per spoke, whole-GPU combine) or "seq" (linear_seq.hip: every spoke builds its own
+# chunk Grams on dense replicas) — an A/B knob; v3 falls back to v1 (logged once) for raw
+# batches of a shape it does not take (> 8192 rows per spoke, > 32 fields)
 SEQ_KERNEL = os.environ.get("OMLDM_SEQ_KERNEL", "scan3")
+_V1_LOGGED: set = set()
 
 
-@dataclass
-class ScanPrep:
-    """Passes 1-2 of a v2 round (hashed slots + chunk Grams G/X1/X2) — model-independent,
-    so they can be made on another stream while the previous round scans."""
-
-    slots: torch.Tensor
-    prep: torch.Tensor
-    key: tuple          # (B, R, S, dim, bias) it was made for
-    event: object = None
-
-
-_SCAN_FITS: dict = {}
-
-
-def scan_fits(dn: int, dc: int) -> bool:
-    """The v2 round's LDS holds this (dn, dc) shape (else linear_seq.hip runs)."""
-    key = (int(dn), int(dc))
-    if key not in _SCAN_FITS:
-        _SCAN_FITS[key] = bool(native.hip().omldm_linear_scan_fits(*key))
-    return _SCAN_FITS[key]
-
-
-def scan_eligible(batch: RawBatch) -> bool:
-    return (SEQ_KERNEL == "scan" and batch.y.is_cuda and 0 < batch.dc
-            and scan_fits(batch.dn, batch.dc))
-
-
-def linear_scan_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool, slot: int = 0,
-                        stream=None) -> ScanPrep:
-    """Hash the batch's tokens and build its chunk Grams into workspace ``slot`` on
-    ``stream`` (default: the current stream); an event marks completion when a stream is
-    given."""
-    h = native.hip()
-    dev = batch.y.device
-    slots = _workspace(dev, batch.B * batch.dc, key=f"scan_slots{slot}")
-    prep = _workspace(dev, int(h.omldm_linear_scan_prep_floats(R, S)), key=f"scan_prep{slot}")
-    st = stream if stream is not None else torch.cuda.current_stream(dev)
-    check(h.omldm_linear_scan_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), batch.dc,
-                                      batch.B, R, S, dim, int(bias), ptr(slots), ptr(prep),
-                                      st.cuda_stream), "omldm_linear_scan_prepare")
-    ev = None
-    if stream is not None:
-        ev = torch.cuda.Event()
-        ev.record(stream)
-    return ScanPrep(slots, prep, (batch.B, R, S, dim, bool(bias)), ev)
-
-
-def linear_scan_prepare_slots(batch: RawBatch, R: int, S: int, dim: int, bias: bool) -> ScanPrep:
-    """Pass 2 for a batch whose ``tok`` already holds field-aware signed slots (int32,
-    dn + field·span + local | sign << 31, −1 absent): the engine's hashed batches."""
-    h = native.hip()
-    prep = _workspace(batch.y.device, int(h.omldm_linear_scan_prep_floats(R, S)),
-                      key="scan_prep_slots")
-    check(h.omldm_linear_scan_prepare_slots(ptr(batch.num), batch.dn, ptr(batch.tok), batch.dc,
-                                            batch.B, R, S, dim, int(bias), ptr(prep),
-                                            native.stream_of(batch.y)),
-          "omldm_linear_scan_prepare_slots")
-    return ScanPrep(batch.tok, prep, (batch.B, R, S, dim, bool(bias)), None)
+def _log_v1_fallback(batch: RawBatch, R: int) -> None:
+    key = (batch.dn, batch.dc, R)
+    if SEQ_KERNEL == "scan3" and key not in _V1_LOGGED:
+        _V1_LOGGED.add(key)
+        log.warning("exact sequential round: shape dn=%d dc=%d R=%d is outside the v3 table "
+                    "scan (linear_scan3.hip); running the v1 kernel (linear_seq.hip)", *key)
 
 
 # ------------------------------------------------------------------ v3: the table scan
@@ -697,29 +649,13 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
         ws = _workspace(w.device, S * WS_STAT, key="seq_ws")
         if replicas is None:
             replicas = _workspace(w.device, S * dim, key="seq_replicas")
-        if scan_eligible(batch):
-            # v2 (csrc/kernels/linear_scan.hip): hash + chunk Grams over the whole GPU
-            # (possibly made ahead on another stream: batch.prep), one scan workgroup per
-            # spoke
-            sp = batch.prep
-            key = (batch.B, R, S, dim, bool(rule.bias))
-            if not (isinstance(sp, ScanPrep) and sp.key == key):
-                sp = linear_scan_prepare(batch, R, S, dim, bool(rule.bias))
-            elif sp.event is not None:
-                torch.cuda.current_stream(w.device).wait_event(sp.event)
-            rc = native.hip().omldm_linear_scan_run(
-                ptr(w), ptr(num), num.shape[1], tok.shape[1], ptr(y),
-                int(y.dtype == torch.int8), batch.B, R, S, ptr(replicas), ptr(dacc), dim,
-                ptr(ws), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, inv_p,
-                int(rule.bias), ptr(sp.slots), ptr(sp.prep), native.stream_of(w))
-            check(rc, "omldm_linear_scan_run")
-        else:
-            rc = native.hip().omldm_linear_seq_round(
-                ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
-                int(y.dtype == torch.int8), batch.B, R, S, ptr(replicas), ptr(dacc), dim,
-                ptr(ws), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, inv_p,
-                int(rule.bias), native.stream_of(w))
-            check(rc, "omldm_linear_seq_round")
+        _log_v1_fallback(batch, R)  # v1 (csrc/kernels/linear_seq.hip)
+        rc = native.hip().omldm_linear_seq_round(
+            ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
+            int(y.dtype == torch.int8), batch.B, R, S, ptr(replicas), ptr(dacc), dim,
+            ptr(ws), ptr(cum), rule.rule, rule.variant, rule.C, rule.eps, rule.lr, inv_p,
+            int(rule.bias), native.stream_of(w))
+        check(rc, "omldm_linear_seq_round")
         if stats is not None:
             stats.copy_(ws[: S * WS_STAT].view(S, WS_STAT)[:, :STAT_W])
         _report()

@@ -58,14 +58,6 @@ HIP_SIGS = [
     ("omldm_linear_seq_apply", i32, [vp, vp, i32, vp, i32, vp]),
     ("omldm_linear_seq_broadcast", i32, [vp, vp, i32, i32, vp]),
     ("omldm_hash_raw", i32, [vp, i64, i32, i32, i64, vp, vp]),
-    ("omldm_linear_scan_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32,
-                                      vp, vp, i32, i32, f32, f32, f32, f32, i32, vp, vp, vp]),
-    ("omldm_linear_scan_prep_floats", i64, [i32, i32]),
-    ("omldm_linear_scan_fits", i32, [i32, i32]),
-    ("omldm_linear_scan_prepare", i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
-    ("omldm_linear_scan_prepare_slots", i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp]),
-    ("omldm_linear_scan_run", i32, [vp, vp, i32, i32, vp, i32, i32, i32, i32, vp, vp, i32, vp,
-                                    vp, i32, i32, f32, f32, f32, f32, i32, vp, vp, vp]),
     ("omldm_linear_seq_reduce", i32, [vp, vp, i32, i32, vp, f32, vp, vp, vp]),
     ("omldm_scan3_lds_cap", i32, []),
     ("omldm_scan3_set_cap", None, [i32]),

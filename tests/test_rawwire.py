@@ -182,7 +182,7 @@ def _seq_case(space, B, S, R, rule, variant=L.PA1, task=0, missing=0.0, y8=False
 
 
 @gpu
-@pytest.mark.parametrize("kernel", ["scan", "seq"], indirect=True)
+@pytest.mark.parametrize("kernel", ["seq"], indirect=True)  # v3: test_scan3.py
 @pytest.mark.parametrize("rule,variant,task", [(L.RULE_HINGE, L.PA1, 0), (L.RULE_HINGE, L.PA, 0),
                                                (L.RULE_HINGE, L.PA2, 0), (L.RULE_EPS, L.PA1, 1),
                                                (L.RULE_LOGISTIC, L.PA1, 0)])
@@ -196,7 +196,7 @@ def test_gpu_seq_round_matches_cpu(kernel, rule, variant, task):
 
 
 @gpu
-@pytest.mark.parametrize("kernel", ["scan", "seq"], indirect=True)
+@pytest.mark.parametrize("kernel", ["seq"], indirect=True)  # v3: test_scan3.py
 def test_gpu_seq_round_int8_labels_no_bias_wide_dense(kernel):
     # dn + bias > 16: the 32-column dense MFMA path; int8 labels; no intercept
     space = FeatureSpace(20, 0, 8, 1 << 12)
@@ -205,7 +205,7 @@ def test_gpu_seq_round_int8_labels_no_bias_wide_dense(kernel):
 
 
 @gpu
-@pytest.mark.parametrize("kernel", ["scan", "seq"], indirect=True)
+@pytest.mark.parametrize("kernel", ["seq"], indirect=True)  # v3: test_scan3.py
 def test_gpu_seq_round_many_shared_groups_slow_path(kernel):
     """A tiny hash space makes nearly every (field, value) shared inside a chunk and many
     values collide with opposite signs: more shared groups than U columns exercises
@@ -216,7 +216,7 @@ def test_gpu_seq_round_many_shared_groups_slow_path(kernel):
 
 
 @gpu
-@pytest.mark.parametrize("kernel", ["scan", "seq"], indirect=True)
+@pytest.mark.parametrize("kernel", ["seq"], indirect=True)  # v3: test_scan3.py
 def test_gpu_learner_raw_rounds_track_cpu(kernel):
     """Several Synchronous rounds through SVM.fit(RawBatch): GPU and CPU models agree."""
     from omldm_amd.models.linear import SVM
@@ -299,7 +299,7 @@ def test_blocked_gram_scan_algorithm_matches_oracle():
 @gpu
 def test_gpu_engine_field_aware_batches_take_the_scan_round():
     """The engine's field-aware hashed batches (slots already hashed) train through the
-    v2 scan round on the GPU and agree with the CPU's exact sequential virtual spokes."""
+    v3 table scan on the GPU and agree with the CPU's exact sequential virtual spokes."""
     from omldm_amd.api.batch import HashedBatch
     from omldm_amd.io.synthetic import synth_batch
     from omldm_amd.models.linear import SVM
@@ -320,69 +320,3 @@ def test_gpu_engine_field_aware_batches_take_the_scan_round():
     assert torch.allclose(res["cuda"][0], res["cpu"][0], atol=1e-3, rtol=1e-2), \
         (res["cuda"][0] - res["cpu"][0]).abs().max()
     assert res["cuda"][1]["fitted"] == res["cpu"][1]["fitted"] == 4 * 16 * 500
-
-
-def _lagged_scan_v2(w, batch, space, R, S, C=1.0, chunk=64, bias=True):
-    """NumPy model of linear_scan.hip's schedule (PA-I): chunk j's round-start margins
-    are gathered from the replica as it stood after chunks ≤ j − 3 (the helpers' gather
-    runs two chunks ahead of the scan) and corrected by the cross Grams:
-    m = X_j·W_{≤ j−3} + X1_j·c_{j−1} + X2_j·c_{j−2} (+ the in-chunk G_j recurrence)."""
-    dim = space.dim
-    cat = hash_raw(batch.tok, space).numpy()
-    num = batch.num.double().numpy()
-    y = batch.y.double().numpy()
-    B = batch.B
-    w0 = w.double().numpy()
-    acc, n_act = np.zeros(dim), 0
-    for s in range(S):
-        a, b = min(s * R, B), min(s * R + R, B)
-        if a >= b:
-            continue
-        n_act += 1
-        Xs, n2s = [], []
-        for c0 in range(a, b, chunk):
-            rows = range(c0, min(b, c0 + chunk))
-            X = np.zeros((len(rows), dim))
-            n2 = np.zeros(len(rows))
-            for i, t in enumerate(rows):
-                X[i, :space.dn] = num[t]
-                n2[i] = (num[t] ** 2).sum()
-                for jf in range(space.dc):
-                    cc = int(cat[t, jf])
-                    if cc != -1:
-                        X[i, cc & 0x7FFFFFFF] += -1.0 if cc < 0 else 1.0
-                        n2[i] += 1.0
-                if bias:
-                    X[i, dim - 1] = 1.0
-                    n2[i] += 1.0
-            Xs.append((X, n2, list(rows)))
-        updates, cs = [], []
-        for j, (X, n2, rows) in enumerate(Xs):
-            W_lag = w0 + sum(updates[: max(0, j - 2)], np.zeros(dim))  # chunks ≤ j − 3
-            m0 = X @ W_lag
-            if j >= 1:
-                m0 = m0 + (X @ Xs[j - 1][0].T) @ cs[j - 1]
-            if j >= 2:
-                m0 = m0 + (X @ Xs[j - 2][0].T) @ cs[j - 2]
-            G = X @ X.T
-            cvec = np.zeros(len(rows))
-            for i, t in enumerate(rows):
-                m = m0[i] + (cvec[:i] * G[i, :i]).sum()
-                cvec[i] = min(C, max(0.0, 1 - y[t] * m) / n2[i]) * y[t]
-            cs.append(cvec)
-            updates.append(X.T @ cvec)
-        acc += sum(updates, np.zeros(dim))
-    return w0 + acc / n_act
-
-
-def test_lagged_gather_schedule_of_the_v2_scan_is_exact():
-    """linear_scan.hip gathers chunk j's margins while chunks j − 2 and j − 1 are still
-    unscattered and folds them back in through X2 / X1: the same model as the exact
-    sequential spoke (field-aware slots: no cross-field collisions)."""
-    space = FeatureSpace(4, 0, 6, 1 << 9)
-    batch = synth_raw(space, 700, seed=3, missing=0.05)
-    w = torch.randn(space.dim, generator=torch.Generator().manual_seed(5)) * 0.01
-    for R, S in ((350, 2), (300, 3), (64, 11)):
-        ref = _blocked_gram_scan(w, batch, space, R, S, C=0.7)
-        v2 = _lagged_scan_v2(w, batch, space, R, S, C=0.7)
-        assert np.allclose(v2, ref, atol=1e-10, rtol=1e-9), np.abs(v2 - ref).max()
