@@ -280,7 +280,10 @@ def main(argv=None) -> int:
     ap.add_argument("--ref-max-examples", type=float, default=6e7)
     ap.add_argument("--engine-e2e", type=int, default=8388608,
                     help="JSON (and DIB) records timed through the whole engine (rank 0; 0 = "
-                         "skip): 64 ticks of 131072 records, the steady state")
+                         "skip): 16 ticks of 524288 records, the steady state")
+    ap.add_argument("--e2e-batch", type=int, default=524288,
+                    help="records per engine tick in the e2e runs (16 spokes × 8192-row "
+                         "rounds: 4 Synchronous rounds per tick, --roundRows)")
     ap.add_argument("--engine-latency", type=int, default=300,
                     help="forecasting records timed through the engine (rank 0; 0 = skip)")
     a = ap.parse_args(argv)
@@ -522,8 +525,9 @@ def main(argv=None) -> int:
 
     eng = engine_forecast_latency(a.engine_latency) if (rank == 0 and on_gpu and
                                                          a.engine_latency > 0) else None
-    e2e = engine_e2e_rate(a.engine_e2e) if (rank == 0 and on_gpu and a.engine_e2e > 0) else None
-    e2e_dib = engine_e2e_rate(a.engine_e2e, fmt="dib") if e2e is not None else None
+    e2e = engine_e2e_rate(a.engine_e2e, a.e2e_batch) \
+        if (rank == 0 and on_gpu and a.engine_e2e > 0) else None
+    e2e_dib = engine_e2e_rate(a.engine_e2e, a.e2e_batch, fmt="dib") if e2e is not None else None
 
     total_examples = a.steps * B * world
     value = total_examples / elapsed
@@ -574,7 +578,8 @@ def main(argv=None) -> int:
             "engine_e2e_semantics": None if e2e is None else
             f"JSON DataInstance file topic -> GPU parse + hashing -> holdout -> Synchronous "
             f"linear SVM fp32, {e2e['spokes']} spokes, {e2e['records']} records timed "
-            f"(one GPU, rank 0), {e2e['record_bytes']} B/record",
+            f"(one GPU, rank 0), {e2e['record_bytes']} B/record, ticks of {e2e['batch']} "
+            f"records = rounds of <= 8192 rows per spoke",
             "engine_e2e_dib_records_per_s": None if e2e_dib is None else e2e_dib["records_per_s"],
             "engine_e2e_stage_ms_per_tick": None if e2e is None else {
                 "json": {"ms_per_tick": e2e["ms_per_tick"], **e2e["stage_ms_per_tick"]},

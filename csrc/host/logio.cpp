@@ -68,37 +68,52 @@ OMLDM_HOST_API int64_t omldm_index_lines(const uint8_t* buf, int64_t len, int64_
 // reads ask for the missing records at the mean length seen so far (+10 %), never beyond
 // cap — so a tick reads what it consumes instead of a fixed safety margin that the next
 // tick reads again. Returns the record count (≥ 0) or -errno; *used = bytes consumed.
-OMLDM_HOST_API int64_t omldm_read_log(int fd, int64_t offset, uint8_t* dst, int64_t cap,
-                                      int64_t max_records, int64_t* offs, int64_t* used,
-                                      int64_t hint) {
+namespace {
+struct LogRead {  // a region read in progress
   int64_t got = 0, n = 0, pos = 0, scanned = 0;
-  int64_t want = hint > 0 && hint < cap ? hint : cap;
   bool eof = false;
-  offs[0] = 0;
+};
+
+// Goes on reading a region from state `s` (the bytes [0, s.got) are in dst and indexed up
+// to s.scanned) with a next read up to `want`, as omldm_read_log describes.
+int64_t read_log_cont(int fd, int64_t offset, uint8_t* dst, int64_t cap, int64_t max_records,
+                      int64_t* offs, LogRead& s, int64_t want) {
   for (;;) {
-    while (got < want) {
-      ssize_t r = pread(fd, dst + got, size_t(want - got), off_t(offset + got));
+    while (s.got < want) {
+      ssize_t r = pread(fd, dst + s.got, size_t(want - s.got), off_t(offset + s.got));
       if (r < 0) {
         if (errno == EINTR) continue;
-        *used = 0;
-        offs[0] = 0;
         return -errno;
       }
       if (r == 0) {
-        eof = true;
+        s.eof = true;
         break;
       }
-      got += r;
+      s.got += r;
     }
-    index_newlines(dst, scanned, got, max_records, offs, n, pos);
-    scanned = n >= max_records ? pos : got;
-    if (n >= max_records || eof || want >= cap) break;
-    const int64_t per = n ? pos / n : 2 * want;  // no complete record yet: double the read
-    const int64_t more = (max_records - n) * per / 10 * 11 + 4096;
-    want = got + more < cap ? got + more : cap;
+    index_newlines(dst, s.scanned, s.got, max_records, offs, s.n, s.pos);
+    s.scanned = s.n >= max_records ? s.pos : s.got;
+    if (s.n >= max_records || s.eof || want >= cap) return 0;
+    const int64_t per = s.n ? s.pos / s.n : 2 * want;  // no complete record yet: double it
+    const int64_t more = (max_records - s.n) * per / 10 * 11 + 4096;
+    want = s.got + more < cap ? s.got + more : cap;
   }
-  *used = offs[n];
-  return n;
+}
+}  // namespace
+
+OMLDM_HOST_API int64_t omldm_read_log(int fd, int64_t offset, uint8_t* dst, int64_t cap,
+                                      int64_t max_records, int64_t* offs, int64_t* used,
+                                      int64_t hint) {
+  LogRead s;
+  offs[0] = 0;
+  const int64_t e = read_log_cont(fd, offset, dst, cap, max_records, offs, s,
+                                  hint > 0 && hint < cap ? hint : cap);
+  if (e < 0) {
+    *used = 0;
+    return e;
+  }
+  *used = offs[s.n];
+  return s.n;
 }
 
 // A small persistent pool for omldm_fill_regions (opt-in, OMLDM_READ_POOL=1: measured
@@ -201,26 +216,151 @@ OMLDM_HOST_API int64_t omldm_fill_regions(int nj, const int64_t* jobs, uint8_t* 
     if (J[4] <= 0 || J[3] <= 0) return;
     rn[j] = omldm_read_log(int(J[0]), J[1], slot + J[2], J[3], J[4], ro[j].data(), &ru[j], J[5]);
   };
-  const int nt = nthreads < 1 ? 1 : (nthreads > nj ? nj : nthreads);
-  // measured (scripts/gpu_r4_pool.sh, same box, alternated): a thread per reader per block
-  // 149-150 M DIB records/s end to end, the pool 111-112 M (its workers' condition-variable
-  // wake-ups and the shared job counter cost more than thread creation): the pool is opt-in
-  static const bool use_pool = [] {
-    const char* e = std::getenv("OMLDM_READ_POOL");
-    return e && e[0] == '1';
-  }();
-  if (nt <= 1) {
-    for (int j = 0; j < nj; ++j) run(j);
-  } else if (use_pool) {
-    read_pool().run(nj, nt, run);
-  } else {  // a thread per reader per block
+  const int nt = nthreads < 1 ? 1 : nthreads;
+  // more readers than regions: each region's first read (its hint) is cut into pieces
+  // read and newline-indexed on their own threads, then stitched in order (records may
+  // straddle pieces: only the '\n' positions matter); a region short of records goes on
+  // reading on its own. OMLDM_READ_SPLIT=0: one thread per region.
+  const char* split_e = std::getenv("OMLDM_READ_SPLIT");
+  const bool split_env = !(split_e && split_e[0] == '0');
+  constexpr int64_t kMinPiece = 256 << 10;
+  const int per = nt / (nj > 0 ? nj : 1);
+  if (split_env && per >= 2) {
+    struct Piece {
+      int j;
+      int64_t a, b, got = 0;
+      int err = 0;
+      std::vector<int64_t> nl;
+    };
+    std::vector<Piece> pcs;
+    std::vector<int> first(nj + 1, 0);
+    for (int j = 0; j < nj; ++j) {
+      first[j] = (int)pcs.size();
+      const int64_t* J = jobs + 6 * j;
+      if (J[4] <= 0 || J[3] <= 0) continue;
+      const int64_t h = J[5] > 0 && J[5] < J[3] ? J[5] : J[3];
+      int np = (int)(h / kMinPiece);
+      np = np < 1 ? 1 : (np > per ? per : np);
+      for (int p = 0; p < np; ++p)
+        pcs.push_back(Piece{j, h * p / np, h * (p + 1) / np});
+    }
+    first[nj] = (int)pcs.size();
+    auto piece = [&](int i) {
+      Piece& q = pcs[i];
+      const int64_t* J = jobs + 6 * q.j;
+      uint8_t* dst = slot + J[2];
+      while (q.a + q.got < q.b) {
+        ssize_t r = pread(int(J[0]), dst + q.a + q.got, size_t(q.b - q.a - q.got),
+                          off_t(J[1] + q.a + q.got));
+        if (r < 0) {
+          if (errno == EINTR) continue;
+          q.err = errno;
+          return;
+        }
+        if (r == 0) break;
+        q.got += r;
+      }
+      q.nl.reserve(size_t(q.got / 96 + 8));
+      const uint8_t* b = dst + q.a;
+      int64_t i0 = 0;
+      const __m128i nlv = _mm_set1_epi8('\n');
+      for (; i0 + 64 <= q.got; i0 += 64) {
+        const __m128i* v = reinterpret_cast<const __m128i*>(b + i0);
+        uint64_t m =
+            (uint64_t)(unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(v), nlv)) |
+            ((uint64_t)(unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(v + 1), nlv)) << 16) |
+            ((uint64_t)(unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(v + 2), nlv)) << 32) |
+            ((uint64_t)(unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128(v + 3), nlv)) << 48);
+        while (m) {
+          q.nl.push_back(q.a + i0 + __builtin_ctzll(m) + 1);
+          m &= m - 1;
+        }
+      }
+      for (; i0 < q.got; ++i0)
+        if (b[i0] == '\n') q.nl.push_back(q.a + i0 + 1);
+    };
+    const int np_all = (int)pcs.size();
+    const int nth = nt < np_all ? nt : np_all;
+    {
+      std::vector<std::thread> th;
+      th.reserve(nth);
+      for (int t = 0; t < nth; ++t)
+        th.emplace_back([&, t] {
+          for (int i = t; i < np_all; i += nth) piece(i);
+        });
+      for (auto& x : th) x.join();
+    }
+    // stitch each region, then let the regions short of records read on (in parallel)
+    std::vector<LogRead> st(nj);
+    std::vector<int64_t> cont_want(nj, 0);
+    for (int j = 0; j < nj; ++j) {
+      const int64_t* J = jobs + 6 * j;
+      ro[j].assign(size_t(J[4] > 0 ? J[4] : 0) + 1, 0);
+      if (J[4] <= 0 || J[3] <= 0) continue;
+      LogRead& s = st[j];
+      int64_t* o = ro[j].data();
+      for (int i = first[j]; i < first[j + 1]; ++i) {
+        const Piece& q = pcs[i];
+        if (q.err) {
+          rn[j] = -q.err;
+          break;
+        }
+        for (size_t t = 0; t < q.nl.size() && s.n < J[4]; ++t) {
+          s.pos = q.nl[t];
+          o[++s.n] = s.pos;
+        }
+        s.got += q.got;
+        if (q.got < q.b - q.a) {
+          s.eof = true;
+          break;
+        }
+      }
+      if (rn[j] < 0) continue;
+      s.scanned = s.n >= J[4] ? s.pos : s.got;
+      const int64_t h = J[5] > 0 && J[5] < J[3] ? J[5] : J[3];
+      if (s.n >= J[4] || s.eof || h >= J[3]) {
+        rn[j] = s.n;
+        ru[j] = o[s.n];
+        continue;
+      }
+      const int64_t perr = s.n ? s.pos / s.n : 2 * h;
+      const int64_t more = (J[4] - s.n) * perr / 10 * 11 + 4096;
+      cont_want[j] = s.got + more < J[3] ? s.got + more : J[3];
+    }
     std::vector<std::thread> th;
-    th.reserve(nt);
-    for (int t = 0; t < nt; ++t)
-      th.emplace_back([&, t] {
-        for (int j = t; j < nj; j += nt) run(j);
-      });
+    for (int j = 0; j < nj; ++j)
+      if (cont_want[j] > 0)
+        th.emplace_back([&, j] {
+          const int64_t* J = jobs + 6 * j;
+          const int64_t e = read_log_cont(int(J[0]), J[1], slot + J[2], J[3], J[4],
+                                          ro[j].data(), st[j], cont_want[j]);
+          rn[j] = e < 0 ? e : st[j].n;
+          ru[j] = e < 0 ? 0 : ro[j][st[j].n];
+        });
     for (auto& x : th) x.join();
+  } else {
+    const int ntr = nt > nj ? nj : nt;
+    // measured (scripts/gpu_r4_pool.sh, same box, alternated): a thread per reader per
+    // block 149-150 M DIB records/s end to end, the pool 111-112 M (its workers'
+    // condition-variable wake-ups and the shared job counter cost more than thread
+    // creation): the pool is opt-in
+    static const bool use_pool = [] {
+      const char* e = std::getenv("OMLDM_READ_POOL");
+      return e && e[0] == '1';
+    }();
+    if (ntr <= 1) {
+      for (int j = 0; j < nj; ++j) run(j);
+    } else if (use_pool) {
+      read_pool().run(nj, ntr, run);
+    } else {  // a thread per reader per block
+      std::vector<std::thread> th;
+      th.reserve(ntr);
+      for (int t = 0; t < ntr; ++t)
+        th.emplace_back([&, t] {
+          for (int j = t; j < nj; j += ntr) run(j);
+        });
+      for (auto& x : th) x.join();
+    }
   }
   for (int j = 0; j < nj; ++j)
     if (rn[j] < 0) return rn[j];

@@ -245,7 +245,7 @@ class TickIngest:
                 nj, jobs.ctypes.data, blk.data.data_ptr(), blk.offs_t.data_ptr(),
                 blk.ends_buf.ctypes.data, 0 if doffs is None else doffs.ctypes.data,
                 res.ctypes.data, segs.ctypes.data, meta.ctypes.data,
-                min(int(os.environ.get("OMLDM_READERS", "16")), max(1, nj)))
+                max(1, int(os.environ.get("OMLDM_READERS", "16"))))
         if n < 0:
             raise OSError(-int(n), "reading the topic logs")
         for j, (c, p) in enumerate(owners):  # consumer positions + bytes-per-record estimate

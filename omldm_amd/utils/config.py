@@ -80,7 +80,8 @@ class JobConfig:
     forecastServer: str = "auto"          # per-record forecasts on the resident serving wave (auto: GPU)
     pipelineStreams: int = 8              # GPU: pipelines of a tick train on up to this many streams
     fusePipelines: str = "true"           # GPU: hashed-linear pipelines sharing a prep: one launch
-    routeAhead: str = "true"              # GPU: holdout route + v3 prep beside the previous round
+    routeAhead: str = "false"             # GPU: holdout route + v3 prep beside the previous round
+    roundRows: int = 8192                 # rows per spoke per round: larger ticks run more rounds
     extra: dict = field(default_factory=dict)
 
     @staticmethod

@@ -160,6 +160,44 @@ def test_native_block_fill_matches_python_path(tmp_path, monkeypatch):
     assert seen == len(recs)
 
 
+@pytest.mark.parametrize("uniform", [True, False])
+def test_split_region_reads_match_one_reader_per_region(tmp_path, monkeypatch, uniform):
+    """More readers than regions: each region's first read is cut into ≥ 256 KiB pieces
+    read and indexed on their own threads (csrc/host/logio.cpp: omldm_fill_regions) — the
+    same blocks as one thread per region, including regions whose hint falls short of
+    the records (variable record lengths) and the partial tail at the log's end."""
+    br = FileBroker(str(tmp_path))
+    br.create_topic("t", 2)
+    rng = np.random.default_rng(3)
+    for p in range(2):
+        lens = np.full(30011, 150) if uniform else rng.integers(20, 400, size=30011)
+        br.produce_block("t", p, b"".join(b"x" * int(n - 1) + b"\n" for n in lens))
+    runs = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("OMLDM_READ_SPLIT", split)
+        monkeypatch.setenv("OMLDM_READERS", "16")
+        cons = [Consumer(br, "t")]
+        ing = TickIngest(cons, batch_size=16384, pinned=False, prefetch=False)
+        assert ing._native_fill
+        ing.stage = True
+        out = []
+        for _ in range(100):
+            blk = ing._fill_block(ing._next_slot())
+            if blk.n == 0:
+                break
+            out.append((blk.n, blk.nbytes, blk.offs.copy(), list(blk.segs), blk.dev_nbytes,
+                        blk.doffs_t.numpy()[: blk.n + 1].copy(), [r for r in blk.raw()],
+                        blk.offsets))  # (gap bytes between regions are unread: not compared)
+        ing.close()
+        runs[split] = out
+    a, b = runs["1"], runs["0"]
+    assert len(a) == len(b) >= 4
+    for x, y in zip(a, b):
+        assert x[0] == y[0] and x[1] == y[1] and x[3] == y[3] and x[4] == y[4] and x[7] == y[7]
+        assert np.array_equal(x[2], y[2]) and np.array_equal(x[5], y[5]) and x[6] == y[6]
+    assert sum(x[0] for x in a) == 2 * 30011
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_index_lines_native_matches_python_on_random_blocks(seed):
     """The SIMD record indexer (64 bytes per step, csrc/host/logio.cpp) against a Python
