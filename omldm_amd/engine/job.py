@@ -390,10 +390,9 @@ class Job:
                 (rr > 0 and batch.B > rr * self.spokes) or \
                 str(self.cfg.routeAhead).lower() in ("false", "0"):
             return None
-        from omldm_amd.models.linear import LinearLearner
-
         if self._route_stream is None:
-            self._route_stream = torch.cuda.Stream(self.device)
+            self._route_stream = self.lanes.prep if self.lanes is not None else \
+                torch.cuda.Stream(self.device)
         ps, cur = self._route_stream, torch.cuda.current_stream(self.device)
         ps.wait_event(ev_in)
         if self._holdout_read_ev is not None:  # queries read the rings the route rewrites
@@ -401,11 +400,9 @@ class Job:
             self._holdout_read_ev = None
         with torch.cuda.stream(ps):
             routed = self.holdout.route(batch)
-            for pid in sorted(self.pipes):
-                p = self.pipes[pid]
-                if isinstance(p.learner, LinearLearner) and not p.preprocessors and \
-                        p.learner.prepare_ahead(routed, p.protocol._ctx(fused=True), ps):
-                    break  # one prep per tick (pipelines of another prep key make theirs)
+            p = self._linear_prep_pipe()  # one prep per tick (other prep keys make theirs)
+            if p is not None:
+                p.learner.prepare_ahead(routed, p.protocol._ctx(fused=True), ps)
         padded = routed._padded[1] if routed._padded is not None else None
         for b in (routed, padded):
             if b is not None:
@@ -427,8 +424,47 @@ class Job:
                 routed = self.holdout.route(batch)
         if direct is not None and direct.B:  # rows that bypass the holdout (no spoke layout)
             routed = HashedBatch.cat_batches([direct, routed]) if routed.B else direct
-        for part in self._round_split(routed):
+        parts = self._round_split(routed)
+        if len(parts) > 1:
+            self._prep_parts_ahead(parts)
+        for part in parts:
             self._train_round(part)
+
+    def _linear_prep_pipe(self):
+        """The first hashed-linear pipeline without preprocessors (whose v3 prep every
+        linear pipeline of the tick shares), or None."""
+        from omldm_amd.models.linear import LinearLearner
+
+        for pid in sorted(self.pipes):
+            p = self.pipes[pid]
+            if isinstance(p.learner, LinearLearner) and not p.preprocessors:
+                return p
+        return None
+
+    def _prep_parts_ahead(self, parts: list) -> None:
+        """Rounds 1 .. k-1 of a multi-round tick: their v3 preps (hash, occurrence flags,
+        chunk Grams — model-independent) run on the route stream while round 0 scans, so
+        each later round only scans (one prep workspace set per round, ops.linear ring)."""
+        if self.device.type != "cuda" or str(self.cfg.prepAhead).lower() in ("false", "0"):
+            return
+        pipe = self._linear_prep_pipe()
+        if pipe is None:
+            return
+        if self._route_stream is None:
+            self._route_stream = self.lanes.prep if self.lanes is not None else \
+                torch.cuda.Stream(self.device)
+        ps, cur = self._route_stream, torch.cuda.current_stream(self.device)
+        ps.wait_stream(cur)  # the parts' rows are cut on the compute stream
+        ctx = pipe.protocol._ctx(fused=True)
+        with torch.cuda.stream(ps):
+            for part in parts[1:]:
+                if not pipe.learner.prepare_ahead(part, ctx, ps):
+                    return
+                padded = part._padded[1] if part._padded is not None else None
+                for b in (part, padded):
+                    if b is not None:
+                        for t in (b.num, b.cat, b.y):
+                            t.record_stream(ps)  # read on the route stream, freed on compute
 
     def _round_split(self, routed: HashedBatch) -> list:
         """A tick whose spokes routed more than ``roundRows`` rows each trains in several

@@ -120,6 +120,7 @@ class XcdLanes:
         with torch.cuda.device(self.device):
             raw = [lib.omldm_stream_create_cumask_ex(int(ingest_cus), 0, 1),
                    lib.omldm_stream_create_cumask_ex(int(ingest_cus), 1, 1),
+                   lib.omldm_stream_create_cumask_ex(int(ingest_cus), 1, 1),
                    lib.omldm_stream_create_cumask_ex(int(ingest_cus), 1, 1)]
         if not all(raw):
             raise RuntimeError("hipExtStreamCreateWithCUMask failed")
@@ -129,6 +130,8 @@ class XcdLanes:
         # copy (the JSON parse), so it neither queues behind training nor runs on the
         # ingest CUs
         self.aux = torch.cuda.ExternalStream(raw[2], device=self.device)
+        # the engine's route / prep-ahead stream (engine/job.py), also off the ingest CUs
+        self.prep = torch.cuda.ExternalStream(raw[3], device=self.device)
 
     @classmethod
     def get(cls, device, ingest_cus: int = 16) -> "XcdLanes":

@@ -75,13 +75,14 @@ class JobConfig:
     parseThreads: int = 8
     gpuParse: bool = True                 # parse + hash JSON records on the GPU (cuda only)
     prefetch: str = "auto"                # read tick k+1 while tick k trains (auto: on GPU)
-    ingestCUs: int = 0                    # GPU: CUs (one XCD block) for ingest copies; 0 off (e2e A/B: no gain, host-bound)
+    ingestCUs: int = 32                   # GPU: CUs (one XCD) for ingest copies; 0 off (profiles/round5/e2e_*.json)
     ingestCopy: str = "pull"              # GPU staging copy: pull (kernel) | sdma (hipMemcpyAsync)
     forecastServer: str = "auto"          # per-record forecasts on the resident serving wave (auto: GPU)
     pipelineStreams: int = 8              # GPU: pipelines of a tick train on up to this many streams
     fusePipelines: str = "true"           # GPU: hashed-linear pipelines sharing a prep: one launch
     routeAhead: str = "false"             # GPU: holdout route + v3 prep beside the previous round
     roundRows: int = 8192                 # rows per spoke per round: larger ticks run more rounds
+    prepAhead: str = "true"               # GPU: later rounds' v3 preps beside the tick's first scan
     extra: dict = field(default_factory=dict)
 
     @staticmethod
