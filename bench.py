@@ -137,6 +137,8 @@ def engine_forecast_latency(n: int) -> dict:
             time.sleep(0)
         time.sleep(100e-6)  # records arrive one at a time
     job.fserver.close()
+    job.ingest.close()
+    job.egress.close()
     lat = sorted((o - i) * 1e6 for i, o in zip(t_in[20:], br.t_out[20:]))
     return {"p50": round(lat[len(lat) // 2], 2),
             "p99": round(lat[min(len(lat) - 1, int(0.99 * len(lat)))], 2),

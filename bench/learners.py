@@ -46,12 +46,33 @@ CASES = [
     ("HT", 2, {"nClasses": 4}, 1),
 ]
 
+# --preset p16: every learner at the reference's parallelism (16 spokes per GPU,
+# DefaultJobParameters.scala:5), 131072-row rounds = 8192 rows per spoke, the engine's
+# field-aware wire (the hashed-linear learners take the v3 table scan there; SVM's L2
+# shrink, Pegasos and bf16 models the spoke-table round)
+P16_CASES = [
+    ("PA", 0, {}, 16, "compact"),
+    ("SVM", 0, {}, 16, "compact"),
+    ("SVM@l2", 0, {"lambda": 1e-4}, 16, "compact"),
+    ("SVM@pegasos", 0, {"variant": "Pegasos", "lambda": 1e-4}, 16, "compact"),
+    ("SVM@bf16", 0, {"modelDtype": "bf16"}, 16, "compact"),
+    ("RegressorPA", 1, {}, 16, "compact"),
+    ("LogisticRegression", 0, {}, 16, "compact"),
+    ("MultiClassPA", 2, {"nClasses": 4}, 16, "compact"),
+    ("ORR", 1, {}, 16),
+    ("K-means", 0, {"k": 16}, 16),
+    ("NN", 0, {"hiddenLayers": [64, 64]}, 16),
+    ("HT", 2, {"nClasses": 4}, 16),
+]
+
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=131072)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--only", default="")
+    ap.add_argument("--preset", default="", choices=["", "p16"],
+                    help="p16: every learner at 16 spokes (the reference's parallelism)")
     ap.add_argument("--cases", default="",
                     help='JSON list of [name, task, hyper, spokes] replacing the default cases '
                          '(geometry sweeps)')
@@ -60,7 +81,8 @@ def main(argv=None) -> int:
     spaces = {"wide": FeatureSpace(13, 0, 26, 1 << 20),
               "compact": FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)}
     res = {}
-    cases = [tuple(c) for c in json.loads(a.cases)] if a.cases else CASES
+    cases = [tuple(c) for c in json.loads(a.cases)] if a.cases else (
+        P16_CASES if a.preset == "p16" else CASES)
     for case in cases:
         name, task, hyper, spokes = case[:4]
         space = spaces[case[4] if len(case) > 4 else "wide"]
@@ -82,6 +104,9 @@ def main(argv=None) -> int:
             continue
         if dev.type == "cuda":
             torch.cuda.synchronize()
+        from omldm_amd.ops import linear as OL
+
+        v3_before = OL.SCAN3_ROUNDS
         t = time.perf_counter()
         for k in range(a.steps):
             L.fit(ring[k % 3], ctx)
@@ -89,7 +114,12 @@ def main(argv=None) -> int:
             torch.cuda.synchronize()
         el = time.perf_counter() - t
         res[name] = {"examples_per_s": round(a.steps * a.batch / el, 1),
-                     "ms_per_round": round(el / a.steps * 1e3, 3), "spokes": spokes}
+                     "ms_per_round": round(el / a.steps * 1e3, 3), "spokes": spokes,
+                     "rows_per_spoke": -(-a.batch // spokes),
+                     "v3_table_scan": OL.SCAN3_ROUNDS > v3_before}
+        tot = L.running_totals() if hasattr(L, "running_totals") else {}
+        if "overflow" in tot:
+            res[name]["overflow"] = tot["overflow"]
     print(json.dumps({"metric": "per-learner training examples/s (1 GPU, 1 pipeline)",
                       "batch": a.batch, "steps": a.steps, "device": str(dev),
                       "learners": res}), flush=True)

@@ -220,9 +220,11 @@ OMLDM_HOST_API int64_t omldm_fill_regions(int nj, const int64_t* jobs, uint8_t* 
   // more readers than regions: each region's first read (its hint) is cut into pieces
   // read and newline-indexed on their own threads, then stitched in order (records may
   // straddle pieces: only the '\n' positions matter); a region short of records goes on
-  // reading on its own. OMLDM_READ_SPLIT=0: one thread per region.
+  // reading on its own.
+  // opt-in (OMLDM_READ_SPLIT=1): measured slower end to end on the MI355X host (DIB
+  // pread 1.02 vs 0.52 ms per 131072-record block, profiles/round5/e2e/)
   const char* split_e = std::getenv("OMLDM_READ_SPLIT");
-  const bool split_env = !(split_e && split_e[0] == '0');
+  const bool split_env = split_e && split_e[0] == '1';
   constexpr int64_t kMinPiece = 256 << 10;
   const int per = nt / (nj > 0 ? nj : 1);
   if (split_env && per >= 2) {

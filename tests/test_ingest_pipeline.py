@@ -174,7 +174,7 @@ def test_split_region_reads_match_one_reader_per_region(tmp_path, monkeypatch, u
         br.produce_block("t", p, b"".join(b"x" * int(n - 1) + b"\n" for n in lens))
     runs = {}
     for split in ("1", "0"):
-        monkeypatch.setenv("OMLDM_READ_SPLIT", split)
+        monkeypatch.setenv("OMLDM_READ_SPLIT", split)  # 1: opt in
         monkeypatch.setenv("OMLDM_READERS", "16")
         cons = [Consumer(br, "t")]
         ing = TickIngest(cons, batch_size=16384, pinned=False, prefetch=False)
