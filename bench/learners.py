@@ -109,7 +109,9 @@ def main(argv=None) -> int:
         v3_before = OL.SCAN3_ROUNDS
         t = time.perf_counter()
         for k in range(a.steps):
-            L.fit(ring[k % 3], ctx)
+            b = ring[k % 3]
+            b.prep, b._padded = None, None  # every round makes its own v3 prep (a new batch)
+            L.fit(b, ctx)
         if dev.type == "cuda":
             torch.cuda.synchronize()
         el = time.perf_counter() - t

@@ -89,13 +89,32 @@ constexpr int LID_SHIFT = 10;
 // floats of one chunk's prep block: aG | aX1 | a | dense columns transposed [KN][64] | y
 // (the target as fp32, NaN for a row without one or past the shard: the scanner reads it
 // a chunk ahead with no conversion — an int8 label's convert made it wait for the load)
+// | σ_t | 1/σ_{t+1} (shrinking rules: the model scale before / after the row's step,
+// s3_sigma_kernel). After the last spoke's blocks: σ at the end of each spoke [S].
 template <int KN>
 __host__ __device__ constexpr int s3_prep_floats() {
-  return 2 * s3::MAT + s3::CH + KN * s3::CH + s3::CH;
+  return 2 * s3::MAT + s3::CH + KN * s3::CH + 3 * s3::CH;
 }
 template <int KN>
 __host__ __device__ constexpr int s3_prep_y() {
   return 2 * s3::MAT + s3::CH + KN * s3::CH;
+}
+template <int KN>
+__host__ __device__ constexpr int s3_prep_sg() {
+  return s3_prep_y<KN>() + s3::CH;
+}
+template <int KN>
+__host__ __device__ constexpr int s3_prep_hh() {
+  return s3_prep_y<KN>() + 2 * s3::CH;
+}
+// the shrink of the model over row t of a spoke (local index i; y NaN: no step, no shrink)
+__device__ __forceinline__ float s3_shrink(int shr, float r, float tbase, int i, float y) {
+  if (shr == 0 || y != y) return 1.f;
+  if (shr == 2) {
+    const float T = tbase + (float)i;
+    return (T - 1.f) / T;
+  }
+  return r;
 }
 
 __device__ __forceinline__ void spoke_rows(int s, int R, int B, int& t0, int& t1) {
@@ -254,7 +273,7 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
                                                       const void* __restrict__ yv, int y8,
                                                       int B, int R, int bias, int affine,
                                                       float kadd, float* __restrict__ prep,
-                                                      int nchs) {
+                                                      int nchs, int shr, float shr_r) {
   const int c = blockIdx.x, s = blockIdx.y;
   int t0, t1;
   spoke_rows(s, R, B, t0, t1);
@@ -285,11 +304,18 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
     for (int j = 0; j < KN; ++j) n2 = fmaf(xn[0][tid][j], xn[0][tid][j], n2);
     for (int f = 0; f < dc; ++f) n2 += sl[0][f][tid] != -1 ? 1.f : 0.f;
     const bool live = t0 + c * s3::CH + tid < t1;
-    float a = 0.f;
-    if (live) a = affine ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : 1.f;
-    sa[tid] = a;
+    const float yt = live ? load_y(yv, t0 + c * s3::CH + tid, y8) : __builtin_nanf("");
+    // a: −1/(‖x‖² + kadd) (affine 1: hinge, ε), 1 (0: logistic), y (2: Pegasos, u = y·v).
+    // Shrinking affine rules scale the Grams by a·σ_t/σ_{t+1} = a/r (the scanner's u is
+    // (a·m + b)/σ_{t+1}); the others keep u in v-space units
+    float a = 0.f, g = 1.f;
+    if (live) {
+      a = affine == 1 ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : (affine == 2 ? (yt == yt ? yt : 0.f) : 1.f);
+      if (affine == 1 && shr == 1 && yt == yt) g = 1.f / shr_r;
+    }
+    sa[tid] = a * g;
     out[2 * s3::MAT + tid] = a;
-    out[s3_prep_y<KN>() + tid] = live ? load_y(yv, t0 + c * s3::CH + tid, y8) : __builtin_nanf("");
+    out[s3_prep_y<KN>() + tid] = yt;
   }
   // dense columns transposed for the helper waves (coalesced per column)
   for (int i = tid; i < KN * s3::CH; i += 256) {
@@ -366,7 +392,7 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
                                                            const void* __restrict__ yv, int y8,
                                                            int B, int R, int bias, int affine,
                                                            float kadd, float* __restrict__ prep,
-                                                           int nchs) {
+                                                           int nchs, int shr, float shr_r) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   const int c = blockIdx.x, s = blockIdx.y;
   int t0, t1;
@@ -420,11 +446,18 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
     for (int j = 0; j < KN; ++j) n2 = fmaf(xn[0][tid][j], xn[0][tid][j], n2);
     for (int f = 0; f < dc; ++f) n2 += sl[0][f][tid] != -1 ? 1.f : 0.f;
     const bool live = t0 + c * s3::CH + tid < t1;
-    float a = 0.f;
-    if (live) a = affine ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : 1.f;
-    sa[tid] = a;
+    const float yt = live ? load_y(yv, t0 + c * s3::CH + tid, y8) : __builtin_nanf("");
+    // a: −1/(‖x‖² + kadd) (affine 1: hinge, ε), 1 (0: logistic), y (2: Pegasos, u = y·v).
+    // Shrinking affine rules scale the Grams by a·σ_t/σ_{t+1} = a/r (the scanner's u is
+    // (a·m + b)/σ_{t+1}); the others keep u in v-space units
+    float a = 0.f, g = 1.f;
+    if (live) {
+      a = affine == 1 ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : (affine == 2 ? (yt == yt ? yt : 0.f) : 1.f);
+      if (affine == 1 && shr == 1 && yt == yt) g = 1.f / shr_r;
+    }
+    sa[tid] = a * g;
     out[2 * s3::MAT + tid] = a;
-    out[s3_prep_y<KN>() + tid] = live ? load_y(yv, t0 + c * s3::CH + tid, y8) : __builtin_nanf("");
+    out[s3_prep_y<KN>() + tid] = yt;
   }
   for (int i = tid; i < KN * s3::CH; i += 256) {
     const int j = i / s3::CH, r = i - j * s3::CH;
@@ -478,6 +511,49 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
   }
 }
 
+// Pass 3b (shrinking rules only): per spoke, the model scale σ_t before and 1/σ_{t+1} after
+// each row's step (σ ×= the row's shrink; rows without a target leave it alone) into the
+// chunks' prep blocks, and σ at the spoke's end into sig[s]. One wave per spoke: each lane
+// multiplies its run of rows, an exclusive product across the lanes, then each lane walks its
+// run again from that prefix.
+template <int KN>
+__global__ __launch_bounds__(64) void s3_sigma_kernel(float* __restrict__ prep, int nchs, int B,
+                                                      int R, int shr, float shr_r, float tbase,
+                                                      float* __restrict__ sig) {
+  constexpr int PF = s3_prep_floats<KN>();
+  const int s = blockIdx.x, lane = threadIdx.x;
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  const int n = t1 - t0;
+  if (n <= 0) return;
+  float* P0 = prep + (size_t)s * nchs * PF;
+  auto at = [&](int i) -> float* { return P0 + (size_t)(i >> 6) * PF + (i & 63); };
+  const int L = (n + 63) / 64, i0 = lane * L, i1 = min(n, i0 + L);
+  float pr = 1.f;
+  for (int i = i0; i < i1; ++i) pr *= s3_shrink(shr, shr_r, tbase, i, at(i)[s3_prep_y<KN>()]);
+  float incl = pr;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const float o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl *= o;
+  }
+  float sg = __shfl_up(incl, 1, 64);
+  if (lane == 0) sg = 1.f;
+  for (int i = i0; i < i1; ++i) {
+    float* b = at(i);
+    b[s3_prep_sg<KN>()] = sg;
+    sg *= s3_shrink(shr, shr_r, tbase, i, b[s3_prep_y<KN>()]);
+    b[s3_prep_hh<KN>()] = 1.f / sg;
+  }
+  const int tail = (64 - (n & 63)) & 63;  // rows past the shard in the last chunk
+  if (lane < tail) {
+    float* b = at(n + lane);
+    b[s3_prep_sg<KN>()] = 1.f;
+    b[s3_prep_hh<KN>()] = 1.f;
+  }
+  if (lane == 63) sig[s] = incl;
+}
+
 // ------------------------------------------------------------------ pass 4: scan
 struct S3Smem {
   alignas(16) float G[2][s3::CH][s3::GS];   // aG_k by chunk parity
@@ -496,8 +572,10 @@ struct S3Cand {
       return __builtin_amdgcn_fmed3f(u, lo, hi);
     } else if constexpr (RULE == kSeqEps) {
       return __builtin_amdgcn_fmed3f(u, 0.f, hi) + __builtin_amdgcn_fmed3f(u + d, lo, 0.f);
-    } else {
-      return p.lr * y * __builtin_amdgcn_rcpf(1.f + __expf(y * u));
+    } else if constexpr (RULE == kSeqPegasos) {  // u = y·v: a step below the threshold 1/σ_t
+      return u < lo ? hi : 0.f;
+    } else {  // lo = y·σ_t, hi = lr·y/σ_{t+1}
+      return hi * __builtin_amdgcn_rcpf(1.f + __expf(lo * u));
     }
   }
 };
@@ -530,7 +608,14 @@ struct S3Comb {
   // epoch restarts at 1), null → s3_tail_kernel / the scatter grid's extra row instead
   unsigned long long* arrive;
   double* cum;
+  const float* sig;  // shrinking rules: σ at each spoke's end (its c's scale), else null
+  int wbf;           // the model w is bf16 (modelDtype bf16: margins on the bf16 weights)
 };
+
+// w[i] of a bf16 model (wbf) or an fp32 one
+__device__ __forceinline__ float s3_w16(const float* w, long long i) {
+  return __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(w)[i] << 16);
+}
 namespace s3 {
 constexpr int CHASH = 8192;          // combiner LDS hash entries (keys in G, sums in X1)
 constexpr unsigned SPIN_MAX = 1u << 21;      // polls before a combiner gives up (~1 s)
@@ -558,6 +643,7 @@ __device__ __forceinline__ void s3_combine_spoke(const int* __restrict__ slotsT,
   const int nch = t0 < t1 ? (t1 - t0 + s3::CH - 1) / s3::CH : 0;
   const int wstride = nparts * (s3::NH + 1);
   const unsigned long long want = (unsigned long long)cb.epoch;
+  const float sc = cb.inv_p * (cb.sig ? cb.sig[s] : 1.f);  // σ_end·Σ c·x: the spoke's Δ
   for (int k = part * (s3::NH + 1) + wave; k < nch; k += wstride) {
     const int row = t0 + k * s3::CH + lane;
     const bool in = row < t1;
@@ -590,7 +676,7 @@ __device__ __forceinline__ void s3_combine_spoke(const int* __restrict__ slotsT,
     for (int f = 0; f < s3::MAXF; ++f) {
       if (c == 0.f || v[f] == -1) continue;
       const int key = v[f] & 0x7fffffff;
-      const float val = v[f] < 0 ? -c * cb.inv_p : c * cb.inv_p;
+      const float val = v[f] < 0 ? -c * sc : c * sc;
       uint32_t at = ((uint32_t)key * 0x9E3779B1u) >> (32 - 13);
       bool done = false;
       for (int probe = 0; probe < 8; ++probe) {
@@ -651,8 +737,13 @@ __device__ __forceinline__ void s3_rare(const int* __restrict__ slotsT, int dc, 
     }
   };
   auto issue_gathers = [&](Set& S) {
+    if (cb.wbf) {
 #pragma unroll
-    for (int i = 0; i < s3::NFR; ++i) S.g[i] = w[S.cs[i] != -1 ? (S.cs[i] & 0x7fffffff) : 0];
+      for (int i = 0; i < s3::NFR; ++i) S.g[i] = s3_w16(w, S.cs[i] != -1 ? (S.cs[i] & 0x7fffffff) : 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < s3::NFR; ++i) S.g[i] = w[S.cs[i] != -1 ? (S.cs[i] & 0x7fffffff) : 0];
+    }
   };
   auto body = [&](int k, Set& CUR, Set& NXT) {
     load_slots(k + 1, NXT);
@@ -692,8 +783,8 @@ __device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int d
 
 // Forward: the tail body (defined with the combine pass below).
 __device__ void s3_dense_body(const float* __restrict__ ws, const float* __restrict__ wsd,
-                              int S_act, int dn, int dim, int bias, float inv_p,
-                              float* __restrict__ dacc, double* __restrict__ cum);
+                              const float* __restrict__ sig, int S_act, int dn, int dim, int bias,
+                              float inv_p, float* __restrict__ dacc, double* __restrict__ cum);
 
 // End of a scan workgroup (every wave comes here): with cb.arrive set, the block's spoke
 // statistics / dense deltas are published (each wave drains its stores, the workgroup
@@ -727,7 +818,7 @@ __device__ __forceinline__ void s3_scan_arrive(const S3Comb& cb, const float* __
   }
   __syncthreads();
   if (s_last)
-    s3_dense_body(ws, wsd, cb.S_act, dn, dim, p.bias, p.inv_p, cb.dacc, cb.cum);
+    s3_dense_body(ws, wsd, cb.sig, cb.S_act, dn, dim, p.bias, p.inv_p, cb.dacc, cb.cum);
 }
 
 // RARE (round mode 4): blocks [S_act, 2·S_act) are the spokes' rare-slot workgroups
@@ -803,6 +894,10 @@ __device__ __forceinline__ void s3_scan_body(
     float f1 = 0.f;  // a·(X1_k · c_{k−1}) for this lane's row of chunk k
     float ynx = chunk_prep(0)[s3_prep_y<KN>() + lane];
     float anx = chunk_prep(0)[2 * s3::MAT + lane];
+    // shrinking rules (p.shr): the row's σ_t and 1/σ_{t+1} (s3_sigma_kernel), a chunk ahead
+    const bool shr = p.shr != 0;
+    float snx = shr ? chunk_prep(0)[s3_prep_sg<KN>() + lane] : 1.f;
+    float hnx = shr ? chunk_prep(0)[s3_prep_hh<KN>() + lane] : 1.f;
     for (int k = -1; k <= nch; ++k) {
       if (k >= 0 && k < nch) {
         const int b = k & 1;
@@ -810,9 +905,14 @@ __device__ __forceinline__ void s3_scan_body(
         const bool valid = row < t1 && ynx == ynx;
         const float y = valid ? ynx : 0.f;
         const float a = valid ? anx : 0.f;
+        const float sg = valid ? snx : 1.f, hh = valid ? hnx : 1.f;
         if (k + 1 < nch) {
           ynx = chunk_prep(k + 1)[s3_prep_y<KN>() + lane];
           anx = chunk_prep(k + 1)[2 * s3::MAT + lane];
+          if (shr) {
+            snx = chunk_prep(k + 1)[s3_prep_sg<KN>() + lane];
+            hnx = chunk_prep(k + 1)[s3_prep_hh<KN>() + lane];
+          }
         }
         float m0 = 0.f;
 #pragma unroll
@@ -820,18 +920,29 @@ __device__ __forceinline__ void s3_scan_body(
         S3Cand<RULE> cf;
         float u, bc = 0.f;
         const float inv = -a;
+        // shrinking rules keep v (w = σ·v) and step c' = c/σ_{t+1}: the affine rules' u is
+        // (a·σ_t·v + b)/σ_{t+1} (Grams scaled by a/r in the prep), so b and the clamps take
+        // the factor hh = 1/σ_{t+1} and the round-start margin a·σ_t·hh (sg = hh = 1 without)
         if constexpr (RULE == kSeqHinge) {
-          bc = y * inv;
-          cf.lo = y < 0.f ? -p.cclip : 0.f;
-          cf.hi = y < 0.f ? 0.f : (y > 0.f ? p.cclip : 0.f);
-          u = fmaf(a, m0, bc) + f1;
+          bc = y * inv * hh;
+          cf.lo = y < 0.f ? -p.cclip * hh : 0.f;
+          cf.hi = y < 0.f ? 0.f : (y > 0.f ? p.cclip * hh : 0.f);
+          u = fmaf(a * (sg * hh), m0, bc) + f1;
         } else if constexpr (RULE == kSeqEps) {
-          bc = (y - p.eps) * inv;
-          cf.d = 2.f * p.eps * inv;
-          cf.lo = valid ? -p.cclip : 0.f;
-          cf.hi = valid ? p.cclip : 0.f;
-          u = fmaf(a, m0, bc) + f1;
+          bc = (y - p.eps) * inv * hh;
+          cf.d = 2.f * p.eps * inv * hh;
+          cf.lo = valid ? -p.cclip * hh : 0.f;
+          cf.hi = valid ? p.cclip * hh : 0.f;
+          u = fmaf(a * (sg * hh), m0, bc) + f1;
+        } else if constexpr (RULE == kSeqPegasos) {
+          // u = y·v (a = y): a step c' = y/(λ·T·σ_{t+1}) when y·σ_t·v < 1
+          const float T = p.tbase + (float)(row - t0);
+          cf.lo = valid ? 1.f / sg : 0.f;
+          cf.hi = valid ? y * hh / (p.lam * T) : 0.f;
+          u = fmaf(a, m0, 0.f) + f1;
         } else {
+          cf.lo = y * sg;
+          cf.hi = p.lr * y * hh;
           u = m0 + f1;
         }
         // the lane's rows of aG_k and aX1_{k+1} in VGPRs before the chain starts: an LDS
@@ -866,8 +977,9 @@ __device__ __forceinline__ void s3_scan_body(
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (valid) {
           float m;
-          if constexpr (RULE == kSeqLogistic) m = u;
-          else m = inv > 0.f ? (bc - u) * __builtin_amdgcn_rcpf(inv) : 0.f;
+          if constexpr (RULE == kSeqLogistic) m = sg * u;
+          else if constexpr (RULE == kSeqPegasos) m = sg * y * u;
+          else m = inv > 0.f ? (bc - u) * __builtin_amdgcn_rcpf(inv * hh) : 0.f;
           seq_stats<RULE>(m, y, p, loss, mist, sqe);
           nex += 1.f;
         }
@@ -913,7 +1025,9 @@ __device__ __forceinline__ void s3_scan_body(
 #pragma unroll
   for (int i = 0; i < s3::NJ; ++i) {
     const int j = qd + s3::NHA * i;
-    w0[i] = (j < KN) ? (j < dn ? w[j] : ((p.bias && j == dn) ? w[dim - 1] : 0.f)) : 0.f;
+    const int jw = j < dn ? j : dim - 1;
+    const float wj = cb.wbf ? s3_w16(w, jw) : w[jw];
+    w0[i] = (j < KN && (j < dn || (p.bias && j == dn))) ? wj : 0.f;
     wn[i] = w0[i];
   }
   // Software pipeline, one chunk ahead. Iteration k margins chunk cn = k + 1 and scatters
@@ -977,6 +1091,14 @@ __device__ __forceinline__ void s3_scan_body(
   };
   auto issue_gathers = [&](Set& S) {
     if constexpr (RARE) return;  // no gathers in the scan workgroup (s3_rare)
+    if (cb.wbf) {
+#pragma unroll
+      for (int i = 0; i < s3::NF; ++i) {
+        const bool glob = !RARE && S.cs[i] != -1 && !(S.cm[i] & s3::F_TG);
+        S.g[i] = s3_w16(w, (glob && !dbg_gather) ? (S.cs[i] & 0x7fffffff) : 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
       // RARE: no gathers here (s3_rare sums every occurrence's w0)
@@ -1234,21 +1356,25 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
 // The dense columns (numerical, intercept) from the spokes' dense deltas, the
 // accumulator's scalars and the round's statistics (one block of 256 threads; run as the extra row of the scatter grid).
 __device__ void s3_dense_body(const float* __restrict__ ws,
-                              const float* __restrict__ wsd, int S_act, int dn, int dim,
-                              int bias, float inv_p, float* __restrict__ dacc,
+                              const float* __restrict__ wsd, const float* __restrict__ sig,
+                              int S_act, int dn, int dim, int bias, float inv_p,
+                              float* __restrict__ dacc,
                               double* __restrict__ cum) {  // (blockDim ≥ 256; dn < 256)
+  // shrinking rules: spoke s ends at σ_s·(w0 + δ_s): dacc gets Σ σ_s·δ_s and the apply's
+  // coefficient of w0, dacc[dim] = Σ σ_s (linear_apply: w = (dacc[dim]·w + dacc)/dacc[dim+1])
   const int tid = threadIdx.x;
   for (int i = tid; i < dn; i += 256) {
     float v = 0.f;
-    for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + i];
+    for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + i] * (sig ? sig[s] : 1.f);
     dacc[i] = v * inv_p;
   }
   if (tid == 0) {
-    float v = 0.f;
+    float v = 0.f, a = 0.f;
     if (bias)
-      for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + dn];
+      for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + dn] * (sig ? sig[s] : 1.f);
+    for (int s = 0; s < S_act; ++s) a += sig ? sig[s] : 1.f;
     dacc[dim - 1] = v * inv_p;
-    dacc[dim] = (float)S_act * inv_p;
+    dacc[dim] = a * inv_p;
     dacc[dim + 1] = (float)S_act * inv_p;
   }
   if (cum && tid < 6 && tid != 4) {
@@ -1265,11 +1391,12 @@ constexpr int SPROBE = 8;
 }  // namespace s3
 
 __global__ __launch_bounds__(256) void s3_tail_kernel(const float* __restrict__ ws,
-                                                      const float* __restrict__ wsd, int S_act,
+                                                      const float* __restrict__ wsd,
+                                                      const float* __restrict__ sig, int S_act,
                                                       int dn, int dim, int bias, float inv_p,
                                                       float* __restrict__ dacc,
                                                       double* __restrict__ cum) {
-  s3_dense_body(ws, wsd, S_act, dn, dim, bias, inv_p, dacc, cum);
+  s3_dense_body(ws, wsd, sig, S_act, dn, dim, bias, inv_p, dacc, cum);
 }
 
 __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__ slotsT,
@@ -1279,9 +1406,10 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
                                                          const float* __restrict__ ws,
                                                          const float* __restrict__ wsd, int S_act,
                                                          int dn, int dim, int bias,
-                                                         double* __restrict__ cum) {
+                                                         double* __restrict__ cum, int R,
+                                                         const float* __restrict__ sig) {
   if ((int)blockIdx.y == dc) {  // the dense columns / scalars / statistics: one extra block
-    if (blockIdx.x == 0) s3_dense_body(ws, wsd, S_act, dn, dim, bias, inv_p, dacc, cum);
+    if (blockIdx.x == 0) s3_dense_body(ws, wsd, sig, S_act, dn, dim, bias, inv_p, dacc, cum);
     return;
   }
   __shared__ int hk[s3::SH];
@@ -1300,7 +1428,8 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
     const float c = __uint_as_float((uint32_t)gran[row]);  // a kernel boundary after the scan
     if (c == 0.f) continue;
     const int key = v & 0x7fffffff;
-    const float val = v < 0 ? -c * inv_p : c * inv_p;
+    const float sc = sig ? inv_p * sig[row / R] : inv_p;
+    const float val = v < 0 ? -c * sc : c * sc;
     uint32_t at = ((uint32_t)key * 0x9E3779B1u) >> (32 - 12);
     bool done = false;
     for (int probe = 0; probe < s3::SPROBE; ++probe) {
@@ -1352,10 +1481,12 @@ static int s3_launch_scan(int rule, bool rare, const int* slotsT, const uint32_t
   if (rare) {
     if (rule == kSeqHinge) OMLDM_S3L(kSeqHinge, true);
     if (rule == kSeqEps) OMLDM_S3L(kSeqEps, true);
+    if (rule == kSeqPegasos) OMLDM_S3L(kSeqPegasos, true);
     OMLDM_S3L(kSeqLogistic, true);
   }
   if (rule == kSeqHinge) OMLDM_S3L(kSeqHinge, false);
   if (rule == kSeqEps) OMLDM_S3L(kSeqEps, false);
+  if (rule == kSeqPegasos) OMLDM_S3L(kSeqPegasos, false);
   OMLDM_S3L(kSeqLogistic, false);
 #undef OMLDM_S3L
 }
@@ -1443,7 +1574,7 @@ OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn,
     case 0: return (long long)dc * B;
     case 1: return (long long)dc * B;  // meta word per occurrence
     case 2: return S;
-    case 3: return (long long)S * nchs * pf;
+    case 3: return (long long)S * nchs * pf + S + 64;  // + σ at each spoke's end
     case 4: return 4LL * B;  // c granules + the w0-margin granules (mode 4)
     case 5: return (long long)S * s3::WS;
     case 6: return (long long)S * s3::DS;
@@ -1523,7 +1654,8 @@ OMLDM_API int omldm_scan3_teardown() {
 OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int hashed, int dc,
                                   const void* y, int y8, int B, int R, int S, int dim, int bias,
                                   int rule, int variant, float C, long long span_in,
-                                  int cbase, void* const* ptrs, void* stream) {
+                                  int cbase, int shr, float shr_r, float tbase,
+                                  void* const* ptrs, void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
   if ((long long)(dim - dn - 1) / dc < 1) return -2;
@@ -1546,21 +1678,33 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   hipLaunchKernelGGL(s3_flags_kernel, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
                      W.meta, W.lidcount);
   const int nchs = (R + s3::CH - 1) / s3::CH;
-  const int affine = rule != kSeqLogistic;
-  const float kadd = (rule != kSeqLogistic && variant == 2) ? 0.5f / C : 0.f;
+  // a per row: −1/(‖x‖² + kadd) (hinge, ε), 1 (logistic), y (Pegasos)
+  const int affine = rule == kSeqLogistic ? 0 : (rule == kSeqPegasos ? 2 : 1);
+  const float kadd = (affine == 1 && variant == 2) ? 0.5f / C : 0.f;
+  if (rule == kSeqPegasos && shr != 2) return -2;
   if (g_s3_gram_valu) {
     if (s3_kn(dn, bias) == 16)
       hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT, dc,
-                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r);
     else
       hipLaunchKernelGGL(s3_gram_kernel<32>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT, dc,
-                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r);
   } else if (s3_kn(dn, bias) == 16) {
     hipLaunchKernelGGL(s3_gram_mfma_kernel<16>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT,
-                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r);
   } else {
     hipLaunchKernelGGL(s3_gram_mfma_kernel<32>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT,
-                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs);
+                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r);
+  }
+  if (shr) {  // σ per row from the targets the Gram pass wrote into the prep
+    float* sig = W.prep + (size_t)S * nchs * (s3_kn(dn, bias) == 16 ? s3_prep_floats<16>()
+                                                                    : s3_prep_floats<32>());
+    if (s3_kn(dn, bias) == 16)
+      hipLaunchKernelGGL(s3_sigma_kernel<16>, dim3(S_act), dim3(64), 0, gst, W.prep, nchs, B, R,
+                         shr, shr_r, tbase, sig);
+    else
+      hipLaunchKernelGGL(s3_sigma_kernel<32>, dim3(S_act), dim3(64), 0, gst, W.prep, nchs, B, R,
+                         shr, shr_r, tbase, sig);
   }
   if (sd) {
     hipEventRecord(sd->join, gst);
@@ -1580,7 +1724,8 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
                        const float* C, const float* eps, const float* lr, const float* inv_p,
                        void* const* ptrs, const unsigned* epoch, void* const* arrive, int dn,
                        int dc, const void* y, int y8, int B, int R, int S, int dim, int rule,
-                       int variant, int bias, long long span_in, int flags, hipStream_t st) {
+                       int variant, int bias, long long span_in, int flags, int shr,
+                       const float* lam, const float* tbase, hipStream_t st) {
   if (M < 1 || M > kS3MaxPipes) return -4;
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
@@ -1592,6 +1737,11 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   const int kn = s3_kn(dn, bias);
   const int cap = omldm_scan3_lds_cap();
   const long long gstride = (long long)R * dc / 2 + 64;
+  if (rule == kSeqPegasos && shr != 2) return -2;
+  // shrinking rules: σ at each spoke's end, after the prep blocks (s3_sigma_kernel)
+  const float* sig = shr ? W0.prep + (size_t)S * nchs * (kn == 16 ? s3_prep_floats<16>()
+                                                                  : s3_prep_floats<32>())
+                         : nullptr;
   // latency form (mode 4, the whole grid fits the GPU at one workgroup per CU): w0-margin
   // workgroups + in-launch combiners beside the scans; throughput form (more pipelines than
   // fit): one self-contained workgroup per spoke — helpers gather, the spoke combined by its
@@ -1620,7 +1770,9 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
     if (epoch[m] == 0u) return -2;
     const S3Ws Wm = s3_ws(ptrs + 8 * m);
     const SeqParams p{rule, variant, variant == 1 ? C[m] : INFINITY,
-                      variant == 2 ? 0.5f / C[m] : 0.f, eps[m], lr[m], inv_p[m], bias, y8, span};
+                      variant == 2 ? 0.5f / C[m] : 0.f, eps[m], lr[m], inv_p[m], bias, y8, span,
+                      shr, lam ? lam[m] : 0.f, tbase ? tbase[m] : 0.f};
+    // flags bit 1: w[m] points at a bf16 model (modelDtype bf16: margins on bf16 weights)
     // flags bit 0: dacc[:dim] is already zero (linear_apply clears it after every round), so
     // the combine adds straight into it (a memset beside the prep kernels took 15-20 us)
     if (!(flags & 1)) hipMemsetAsync(dacc[m], 0, sizeof(float) * (size_t)dim, st);
@@ -1628,7 +1780,8 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
     // mode 4: the rare-slot workgroups' margin granules follow the c granules
     pp.pipe[m] = S3Pipe{w[m], Wm.aglob, Wm.ws, Wm.wsd, rare ? Wm.gran + B : nullptr,
                         S3Comb{W0.lidcount, Wm.gran, epoch[m], S_act, dacc[m], inv_p[m],
-                               static_cast<unsigned long long*>(arrive[m]), cum[m]},
+                               static_cast<unsigned long long*>(arrive[m]), cum[m], sig,
+                               (flags & 2) ? 1 : 0},
                         p};
   }
   const int e = kn == 16 ? s3_launch_scan<16>(rule, rare, W0.slotsT, W0.meta, dc, dn, y, B, R,
@@ -1640,15 +1793,15 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
     const S3Ws Wm = s3_ws(ptrs + 8 * m);
     if (ncomb > 0 || tail) {  // the categorical slots were combined in the scan's launch
       if (!arrive[m])
-        hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, Wm.ws, Wm.wsd, S_act, dn,
-                           dim, bias, inv_p[m], dacc[m], cum[m]);
+        hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, Wm.ws, Wm.wsd, sig, S_act,
+                           dn, dim, bias, inv_p[m], dacc[m], cum[m]);
       continue;
     }
     const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
     const int nblk = (n_rows + s3::SB - 1) / s3::SB;
     hipLaunchKernelGGL(s3_scatter_kernel, dim3(nblk > 0 ? nblk : 1, dc + (arrive[m] ? 0 : 1)),
                        dim3(256), 0, st, W0.slotsT, Wm.gran, B, n_rows, inv_p[m], dacc[m], dc,
-                       Wm.ws, Wm.wsd, S_act, dn, dim, bias, cum[m]);
+                       Wm.ws, Wm.wsd, S_act, dn, dim, bias, cum[m], R, sig);
   }
   return (int)hipGetLastError();
 }
@@ -1660,11 +1813,13 @@ OMLDM_API int omldm_scan3_run(const float* w, int dn, int dc, const void* y, int
                               int S, float* dacc, int dim, double* cum, int rule, int variant,
                               float C, float eps, float lr, float inv_p, int bias,
                               long long span_in, void* const* ptrs, int part, int parts,
-                              int flags, unsigned epoch, void* arrive, void* stream) {
+                              int flags, unsigned epoch, void* arrive, int shr, float lam,
+                              float tbase, void* stream) {
   if (part != 0) return 0;
   (void)parts;
   return s3_run_impl(1, &w, &dacc, &cum, &C, &eps, &lr, &inv_p, ptrs, &epoch, &arrive, dn, dc, y,
-                     y8, B, R, S, dim, rule, variant, bias, span_in, flags, (hipStream_t)stream);
+                     y8, B, R, S, dim, rule, variant, bias, span_in, flags, shr, &lam, &tbase,
+                     (hipStream_t)stream);
 }
 
 // M pipelines sharing one prep, one launch (per-pipeline arrays as in s3_run_impl).
@@ -1674,9 +1829,10 @@ OMLDM_API int omldm_scan3_run_multi(int M, const float* const* w, float* const* 
                                     const unsigned* epoch, void* const* arrive, int dn, int dc,
                                     const void* y, int y8, int B, int R, int S, int dim,
                                     int rule, int variant, int bias, long long span_in, int flags,
-                                    void* stream) {
+                                    int shr, const float* lam, const float* tbase, void* stream) {
   return s3_run_impl(M, w, dacc, cum, C, eps, lr, inv_p, ptrs, epoch, arrive, dn, dc, y, y8, B, R,
-                     S, dim, rule, variant, bias, span_in, flags, (hipStream_t)stream);
+                     S, dim, rule, variant, bias, span_in, flags, shr, lam, tbase,
+                     (hipStream_t)stream);
 }
 
 OMLDM_API int omldm_scan3_max_pipes() { return kS3MaxPipes; }

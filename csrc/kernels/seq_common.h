@@ -6,7 +6,8 @@
 
 namespace omldm {
 
-enum SeqRule : int { kSeqHinge = 0, kSeqEps = 1, kSeqLogistic = 2 };
+// kSeqPegasos: the v3 table scan only (linear_scan3.hip)
+enum SeqRule : int { kSeqHinge = 0, kSeqEps = 1, kSeqLogistic = 2, kSeqPegasos = 3 };
 
 struct SeqParams {
   int rule, variant;
@@ -15,6 +16,10 @@ struct SeqParams {
   float eps, lr, inv_p;
   int bias, y8;
   uint32_t span;  // slots per categorical field: (dim − dn − 1) / dc (field-aware hashing)
+  // v3 only — the model shrinks every step (w = σ·v): 0 none, 1 σ ×= r per row (L2: r = 1 − λ,
+  // logistic 1 − lr·λ), 2 Pegasos σ ×= (T − 1)/T with T = tbase + the row's index in the spoke
+  int shr;
+  float lam, tbase;
 };
 
 // c(m) of one example for the lane's own row (the value is used only at its step).
@@ -37,7 +42,7 @@ __device__ __forceinline__ float seq_candidate(float m, float y, float inv, cons
 template <int RULE>
 __device__ __forceinline__ void seq_stats(float m, float y, const SeqParams& p, float& loss,
                                           float& mist, float& sqe) {
-  if constexpr (RULE == kSeqHinge) {
+  if constexpr (RULE == kSeqHinge || RULE == kSeqPegasos) {
     const float ym = y * m;
     loss += fmaxf(0.f, 1.f - ym);
     mist += ym <= 0.f ? 1.f : 0.f;

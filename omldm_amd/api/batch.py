@@ -127,9 +127,11 @@ class HashedBatch:
         return HashedBatch(num, cat, y, raw, self.cat_span)
 
     def to(self, device, non_blocking: bool = False) -> "HashedBatch":
-        return self._like(self.num.to(device, non_blocking=non_blocking),
-                          self.cat.to(device, non_blocking=non_blocking),
-                          self.y.to(device, non_blocking=non_blocking), self.raw)
+        out = self._like(self.num.to(device, non_blocking=non_blocking),
+                         self.cat.to(device, non_blocking=non_blocking),
+                         self.y.to(device, non_blocking=non_blocking), self.raw)
+        out.shards = self.shards  # the same rows: the spoke layout travels with them
+        return out
 
     def slice(self, a: int, b: int) -> "HashedBatch":
         return self._like(self.num[a:b], self.cat[a:b], self.y[a:b],

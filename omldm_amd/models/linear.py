@@ -106,10 +106,19 @@ class LinearLearner(Learner):
     def _wread(self) -> torch.Tensor:
         return self.w16 if self.w16 is not None else self.w
 
-    def seq_capable(self) -> bool:
-        """Raw-wire rounds run the exact sequential Gram-scan kernel (PA family, RegressorPA,
-        logistic SGD without L2); other rules hash the batch and take the spoke-table path."""
-        return self.rule.rule in L.SEQ_RULES and self.rule.lam == 0.0 and self.w16 is None
+    def seq_capable(self, batch=None, ctx: RoundContext | None = None) -> bool:
+        """Raw-wire rounds run the exact sequential Gram-scan kernels (PA family, RegressorPA,
+        logistic SGD; v3 or v1). The shrinking rules (L2 λ > 0, Pegasos) and bf16 models have
+        only the v3 form: on a GPU, where the v3 scan takes ``batch`` (None: the caller checks
+        the shape). Everything else hashes the batch and takes the spoke-table round."""
+        if not L.shrinks(self.rule) and self.w16 is None:
+            return self.rule.rule in L.SEQ_RULES
+        if not (self.w.is_cuda and L.SEQ_KERNEL == "scan3"):
+            return False
+        if batch is None:
+            return True
+        R, _ = self._seq_geometry(batch.B, ctx) if ctx is not None else (batch.B, 1)
+        return bool(batch.B) and L.scan3_eligible(batch, R, self.rule.bias)
 
     @staticmethod
     def _seq_geometry(B: int, ctx: RoundContext) -> tuple[int, int]:
@@ -157,9 +166,11 @@ class LinearLearner(Learner):
                 self._rep_valid = True
         parts = max(1, int(ctx.reduce_parts)) if ctx.on_reduce_part is not None else 1
         if B:
-            L.linear_seq_round(self.w, batch, R, S, self.dacc, self.rule, ctx.inv_p,
+            self.rule.tbase = float(self.t0 + 1 + self.steps)  # Pegasos' step clock
+            L.linear_seq_round(self._wread(), batch, R, S, self.dacc, self.rule, ctx.inv_p,
                                cum=self.cum, replicas=self.replicas if use_rep else None,
                                parts=parts, on_part=ctx.on_reduce_part, hashed=hashed)
+            self.steps += R
         else:
             self.dacc[self.dim:].zero_()
             if ctx.on_reduce_part is not None:  # still join every collective of the round
@@ -185,7 +196,9 @@ class LinearLearner(Learner):
             if not self._slots_scan_eligible(b, ctx):
                 return None
         r = self.rule
-        return (self.dim, r.rule, r.variant, r.bias, r.C if r.variant == L.PA2 else None)
+        r.tbase = float(self.t0 + 1 + self.steps)  # (Pegasos: the prep depends on the clock)
+        return (self.dim, r.rule, r.variant, r.bias, r.C if r.variant == L.PA2 else None,
+                L._s3_shrink(r), self.w16 is not None)
 
     def prepare_ahead(self, batch: HashedBatch, ctx: RoundContext, stream) -> bool:
         """Make the v3 prep of this learner's round on ``batch`` now, on ``stream``, and
@@ -221,22 +234,26 @@ class LinearLearner(Learner):
             rb.prep = getattr(b, "prep", None)
             hashed = True
         R, S = first._seq_geometry(rb.B, ctx)
+        for lr in learners:
+            lr.rule.tbase = float(lr.t0 + 1 + lr.steps)
         step = L.scan3_max_pipes()
         for i in range(0, len(learners), step):
             grp = learners[i:i + step]
-            L.linear_scan3_round_multi([lr.w for lr in grp], rb, R, S, [lr.dacc for lr in grp],
+            L.linear_scan3_round_multi([lr._wread() for lr in grp], rb, R, S,
+                                       [lr.dacc for lr in grp],
                                        [lr.rule for lr in grp], ctx.inv_p,
                                        [lr.cum for lr in grp], hashed=hashed)
         if not isinstance(batch, RawBatch):
             batch.prep = rb.prep
         for lr in learners:
             lr._seq_pending = False
+            lr.steps += R
             if not ctx.fused_delta:
                 lr.apply_delta()
 
     def fit(self, batch: HashedBatch, ctx: RoundContext) -> None:
         if isinstance(batch, RawBatch):
-            if self.seq_capable():
+            if self.seq_capable(batch, ctx):
                 return self._fit_raw(batch, ctx)
             batch = batch.hashed(self.space)
         # a holdout-routed tick: spoke s trains exactly the rows spoke s routed

@@ -245,7 +245,25 @@ def linear_predict(w: torch.Tensor, batch: HashedBatch, wscale: torch.Tensor | N
 
 
 # ------------------------------------------------------------------ raw-wire sequential round
-SEQ_RULES = (RULE_HINGE, RULE_EPS, RULE_LOGISTIC)
+SEQ_RULES = (RULE_HINGE, RULE_EPS, RULE_LOGISTIC)  # v1 (linear_seq.hip) and the CPU oracle
+# the v3 table scan also takes the rules whose model shrinks every step (w = σ·v: the L2
+# shrink of SVM / RegressorPA / logistic with λ > 0, Pegasos): s3_sigma_kernel
+V3_RULES = SEQ_RULES + (RULE_PEGASOS,)
+
+
+def shrinks(rule: "LinearRule") -> bool:
+    return rule.rule == RULE_PEGASOS or rule.lam > 0.0
+
+
+def _s3_shrink(rule: "LinearRule") -> tuple[int, float, float]:
+    """(shr, r, tbase) of the v3 round: 0 no shrink; 1 σ ×= r per row (r = 1 − λ, logistic
+    1 − lr·λ; linear_cpu.cpp's shrink); 2 Pegasos σ ×= (T − 1)/T, T = tbase + row index."""
+    if rule.rule == RULE_PEGASOS:
+        return 2, 1.0, float(rule.tbase)
+    if rule.lam > 0.0:
+        r = 1.0 - (rule.lr * rule.lam if rule.rule == RULE_LOGISTIC else rule.lam)
+        return 1, float(r), 0.0
+    return 0, 1.0, 0.0
 
 
 # GPU kernel of the exact sequential round: "scan3" (linear_scan3.hip, default: LDS slot
@@ -343,7 +361,9 @@ def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
     """What a v3 prep depends on: the batch, the geometry, the rule's row scale (C only
     through PA-II's 1/(2C)) — pipelines that differ in C share one prep."""
     c = float(rule.C) if rule.variant == PA2 else None
-    return (batch.B, R, S, dim, bool(bias), rule.rule == RULE_LOGISTIC, rule.variant == PA2, c,
+    # the row scaling depends on the rule family (a = −1/(‖x‖²+kadd), 1 or y) and the shrink
+    fam = 2 if rule.rule == RULE_PEGASOS else int(rule.rule == RULE_LOGISTIC)
+    return (batch.B, R, S, dim, bool(bias), fam, rule.variant == PA2, c, _s3_shrink(rule),
             batch.dn, batch.dc, int(batch.span), batch.y.data_ptr(), batch.tok.data_ptr(), S3_MODE)
 
 
@@ -483,8 +503,8 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
     check(h.omldm_scan3_prepare(ptr(batch.num), batch.dn, ptr(batch.tok), mode, batch.dc, ptr(y),
                                 int(y.dtype == torch.int8), batch.B, R, S, dim, int(bias),
                                 rule.rule, rule.variant, float(rule.C), span,
-                                int(batch.cbase) if batch.span > 0 else -1, ptrs,
-                                st.cuda_stream), "omldm_scan3_prepare")
+                                int(batch.cbase) if batch.span > 0 else -1, *_s3_shrink(rule),
+                                ptrs, st.cuda_stream), "omldm_scan3_prepare")
     ev = torch.cuda.Event()  # pipelines on other streams that reuse the prep wait on it
     ev.record(st)
     return Scan3Prep(bufs, ptrs, _s3_key(batch, R, S, dim, bias, rule), ev, slot)
@@ -510,6 +530,8 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
                        rule: "LinearRule", inv_p: float, cum: torch.Tensor | None = None,
                        parts: int = 1, on_part=None, hashed: bool = False,
                        dacc_zero: bool = True) -> None:
+    # ``w``: the fp32 model, or its bf16 copy (modelDtype bf16: margins on the bf16 weights;
+    # linear_apply updates the fp32 master and refreshes the copy)
     """One Synchronous round through the v3 table scan (csrc/kernels/linear_scan3.hip):
     dacc[:dim] += inv_p·Σ_spokes Δ_s, dacc[dim] = dacc[dim+1] = S_act·inv_p, so
     ``linear_apply`` averages the spokes' replicas into w. Like every round kernel it
@@ -543,10 +565,12 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
     arrive = (None if _S3_TAIL_KERNEL else
               gran[0].data_ptr() + (gran[0].numel() // 2 - 1) * 8)
     for k in range(parts):
+        flags = int(bool(dacc_zero)) | (2 if w.dtype == torch.bfloat16 else 0)
         rc = h.omldm_scan3_run(ptr(w), num.shape[1], batch.dc, ptr(y), int(y.dtype == torch.int8),
                                batch.B, R, S, ptr(dacc), dim, ptr(cum), rule.rule, rule.variant,
                                rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), span, ptrs, k,
-                               parts, int(bool(dacc_zero)), epoch, arrive, native.stream_of(w))
+                               parts, flags, epoch, arrive, _s3_shrink(rule)[0],
+                               float(rule.lam), float(rule.tbase), native.stream_of(w))
         check(rc, "omldm_scan3_run")
         if on_part is not None:
             on_part(k, *scan3_part_bounds(dim, batch.dn, batch.dc, k, parts, span))
@@ -569,6 +593,7 @@ def linear_scan3_round_multi(ws: list, batch: RawBatch, R: int, S: int, daccs: l
 
     M = len(ws)
     assert 1 <= M <= scan3_max_pipes() and len(daccs) == M and len(rules) == M
+    assert len({w.dtype for w in ws}) == 1, "one launch: every model fp32 or every model bf16"
     r0 = rules[0]
     dim = int(daccs[0].shape[0]) - 2
     key = _s3_key(batch, R, S, dim, r0.bias, r0)
@@ -602,7 +627,9 @@ def linear_scan3_round_multi(ws: list, batch: RawBatch, R: int, S: int, daccs: l
         F([r.lr for r in rules]), F([inv_p] * M), (ctypes.c_void_p * (8 * M))(*ptrs),
         (ctypes.c_uint * M)(*epochs), (ctypes.c_void_p * M)(*arrives), num.shape[1], batch.dc,
         ptr(y), int(y.dtype == torch.int8), batch.B, R, S, dim, r0.rule, r0.variant,
-        int(r0.bias), span, 1, stream), "omldm_scan3_run_multi")
+        int(r0.bias), span, 1 | (2 if ws[0].dtype == torch.bfloat16 else 0),
+        _s3_shrink(r0)[0], F([r.lam for r in rules]),
+        F([r.tbase for r in rules]), stream), "omldm_scan3_run_multi")
     _s3_mark_read(sp)
 
 
@@ -620,8 +647,9 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
     spoke; ``replicas`` is its [S, dim] fp32 scratch, allocated here if None).
     CPU: csrc/host/rawwire.cpp (the golden oracle)."""
     dim = int(dacc.shape[0]) - 2
-    assert w.shape[0] == dim and w.dtype == torch.float32 and dacc.dtype == torch.float32
-    assert rule.rule in SEQ_RULES and rule.lam == 0.0, "seq round: PA family / logistic, no L2"
+    assert w.shape[0] == dim and dacc.dtype == torch.float32
+    assert w.dtype == torch.float32 or (w.dtype == torch.bfloat16 and w.is_cuda)
+    assert rule.rule in V3_RULES, "seq round: PA family / logistic (+ Pegasos on v3)"
     num, tok, y = batch.num, batch.tok, batch.y
     assert num.dtype == torch.float32
     assert tok.dtype == (torch.int16 if batch.span > 0 else torch.int32), tok.dtype
@@ -636,6 +664,10 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
         assert all(t.is_cuda for t in (num, tok, y)) and dacc.is_cuda
         linear_scan3_round(w, batch, R, S, dacc, rule, inv_p, cum, parts, on_part, hashed)
         return True
+    # a shrinking rule (L2, Pegasos) or a bf16 model has no v1 / raw CPU form: the learner
+    # hashes the batch and takes the spoke-table round instead (models/linear.py: seq_capable)
+    assert not shrinks(rule) and w.dtype == torch.float32, \
+        "shrinking rules / bf16 models take the v3 scan or the spoke-table round"
     if on_part is not None:  # the other paths complete dacc in one go
         def _report():
             for k in range(max(1, int(parts))):

@@ -383,3 +383,51 @@ def test_gpu_scan3_inlaunch_combine_matches_scatter(mode3, S, R, dn):
         assert float(d.max()) < 1e-4, (comb, float(d.max()))
         assert res[comb][1]["fitted"] == res[0][1]["fitted"] == 3 * B
         assert abs(res[comb][1]["mistakes"] - res[0][1]["mistakes"]) <= 2
+
+
+@gpu
+@pytest.mark.parametrize("name,hyper,task", [
+    ("SVM", {"lambda": 1e-4}, 0),
+    ("SVM", {"variant": "Pegasos", "lambda": 1e-4}, 0),
+    ("SVM", {"variant": "PA-II", "lambda": 1e-3, "C": 0.5}, 0),
+    ("RegressorPA", {"lambda": 1e-3}, 1),
+    ("LogisticRegression", {"lambda": 1e-2, "learningRate": 0.2}, 0),
+    ("SVM", {"modelDtype": "bf16"}, 0),
+    ("SVM", {"modelDtype": "bf16", "lambda": 1e-4}, 0),
+])
+@pytest.mark.parametrize("S,R,uneven", [(16, 4096, False), (5, 300, True)])
+def test_gpu_scan3_shrinking_rules_match_cpu(name, hyper, task, S, R, uneven):
+    """Rules whose model shrinks every step (w = σ·v: L2 λ > 0, Pegasos' (T − 1)/T) and
+    bf16 models (margins on the bf16 weights) on the v3 table scan (s3_sigma_kernel + the
+    σ-scaled recurrence) against the CPU spoke-table oracle (linear_cpu.cpp), three rounds on
+    the engine's field-aware wire; uneven: spokes routed different row counts (blank rows,
+    no shrink)."""
+    from omldm_amd.io.synthetic import synth_batch
+    from omldm_amd.models import make_learner
+    from omldm_amd.models.base import RoundContext
+
+    dev = _cuda()
+    space = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
+    res = {}
+    for d in ("cpu", dev):
+        lrn = make_learner(name, dict(hyper), space, d)
+        before = L.SCAN3_ROUNDS
+        for k in range(3):
+            b = synth_batch(space, S * R - (37 if uneven else 0), start=k * S * R, task=task,
+                            seed=41)
+            if uneven:  # spoke s routed R − 7·(s % 3) rows
+                sh = [R - 7 * (s % 3) for s in range(S)]
+                sh[-1] += b.B - sum(sh)
+                b.shards = tuple(sh)
+            lrn.fit(b.to(d) if d != "cpu" else b, RoundContext(spokes=S, inv_p=1.0 / S))
+        if d != "cpu":
+            torch.cuda.synchronize()
+            assert L.SCAN3_ROUNDS - before == 3, "the v3 scan did not take the rounds"
+            assert native.hip().omldm_scan3_comb_err() == 0
+        res[str(d)] = (lrn.state_vector().detach().float().cpu(), lrn.running_totals())
+    wg, wc = res[str(dev)][0], res["cpu"][0]
+    scale = max(1.0, float(wc.abs().max()))
+    np.testing.assert_allclose(wg.numpy(), wc.numpy(), rtol=3e-3, atol=3e-5 * scale)
+    tg, tc = res[str(dev)][1], res["cpu"][1]
+    assert tg["fitted"] == tc["fitted"]
+    assert abs(tg["mistakes"] - tc["mistakes"]) <= 2e-3 * tc["fitted"] + 2
