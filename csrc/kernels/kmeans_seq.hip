@@ -15,20 +15,29 @@
 namespace omldm {
 namespace {
 
-// (value, lane) minimum over the wave, ties to the lowest lane; wave-uniform result.
-__device__ __forceinline__ int wave_argmin(float v) {
-  const int lane = threadIdx.x & 63;
-  int idx = lane;
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const float ov = __shfl_xor(v, d);
-    const int oi = __shfl_xor(idx, d);
-    if (ov < v || (ov == v && oi < idx)) {
-      v = ov;
-      idx = oi;
-    }
-  }
-  return __builtin_amdgcn_readfirstlane(idx);
+// The lowest lane holding the wave's minimum of v (wave-uniform). The minimum climbs to
+// lane 63 through DPP moves (row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15 /
+// 31 across the rows: one VALU op per step, no LDS round trip — the ds_bpermute butterfly
+// cost ~700 of the ~1000 cycles of a point's chain), then one compare + ballot finds its
+// lowest lane.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_min_step(float v) {
+  const int o = __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                            CTRL, ROWS, 0xf, false);
+  return fminf(v, __builtin_bit_cast(float, o));
+}
+
+__device__ __forceinline__ int wave_argmin(float v, float& vmin) {
+  float m = v;
+  m = dpp_min_step<0x111, 0xf>(m);  // row_shr:1
+  m = dpp_min_step<0x112, 0xf>(m);  // row_shr:2
+  m = dpp_min_step<0x114, 0xf>(m);  // row_shr:4
+  m = dpp_min_step<0x118, 0xf>(m);  // row_shr:8  → lane 15 of each row: the row's minimum
+  m = dpp_min_step<0x142, 0xa>(m);  // row_bcast:15 → lanes 31, 63: two rows' minimum
+  m = dpp_min_step<0x143, 0xc>(m);  // row_bcast:31 → lane 63: the wave's minimum
+  vmin = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, m), 63));
+  const unsigned long long at = __builtin_amdgcn_ballot_w64(v == vmin);
+  return at ? __builtin_ctzll(at) : 0;  // (no lane: every distance NaN)
 }
 
 template <int DM>
@@ -83,15 +92,17 @@ __global__ __launch_bounds__(64) void kmeans_seq_kernel(const float* __restrict_
         ++seeded;
         continue;
       }
-      float dist = 0.f;
+      // four independent partial sums: the distance is on the per-point chain
+      float dp[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < DM; ++i) {
         const float t = xs[i] - c[i];
-        dist = fmaf(t, t, dist);
+        dp[i & 3] = fmaf(t, t, dp[i & 3]);
       }
-      const int j = wave_argmin(mine ? dist : __builtin_inff());
-      inertia += (double)__builtin_bit_cast(
-          float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, dist), j));
+      const float dist = (dp[0] + dp[1]) + (dp[2] + dp[3]);
+      float dmin;
+      const int j = wave_argmin(mine ? dist : __builtin_inff(), dmin);
+      inertia += (double)dmin;
       if (lane == j) {
         n += 1.f;
         const float a = 1.f / n;
