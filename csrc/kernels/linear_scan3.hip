@@ -844,7 +844,7 @@ __device__ __forceinline__ void s3_spoke_end(bool tail, const int* __restrict__ 
 
 template <int RULE, int KN, bool RARE>
 __device__ __forceinline__ void s3_scan_body(
-    int bid, int nblk, bool tail, S3Smem& sm, float* tab,
+    int bid, int nblk, int tail, S3Smem& sm, float* tab,
     const int* __restrict__ slotsT, const uint32_t* __restrict__ meta, int dc, int dn,
     const void* __restrict__ yv, int B, int R, const float* __restrict__ prep, int nchs,
     const float* __restrict__ w, int dim, float* __restrict__ aglob, int cap, long long gstride,
@@ -854,6 +854,10 @@ __device__ __forceinline__ void s3_scan_body(
   if (bid >= cb.S_act) {
     if (RARE && bid < 2 * cb.S_act) {  // a rare-slot workgroup
       s3_rare(slotsT, dc, B, R, w, cb, rgran, sm, bid - cb.S_act);
+      if (tail == 2) {  // then the spoke's combiner: its w0 pass ends long before the scan
+        __syncthreads();
+        s3_combine_spoke(slotsT, dc, B, R, cb, sm, bid - cb.S_act, 0, 1);
+      }
       return;
     }
     s3_combine(slotsT, dc, B, R, cb, sm, (RARE ? 2 : 1) * cb.S_act, bid, nblk);  // a combiner
@@ -1007,7 +1011,7 @@ __device__ __forceinline__ void s3_scan_body(
       wr[6] = 0.f;
       wr[7] = 0.f;
     }
-    s3_spoke_end(tail, slotsT, dc, B, R, cb, ws, wsd, dn, dim, p, sm, s);
+    s3_spoke_end(tail == 1, slotsT, dc, B, R, cb, ws, wsd, dn, dim, p, sm, s);
     return;
   }
 
@@ -1297,7 +1301,7 @@ __device__ __forceinline__ void s3_scan_body(
     if (lane == 0 && j < KN) wsd[(size_t)s * s3::DS + j] = wn[i] - w0[i];
   }
   if (q == 0 && lane >= KN && lane < s3::DS) wsd[(size_t)s * s3::DS + lane] = 0.f;
-  s3_spoke_end(tail, slotsT, dc, B, R, cb, ws, wsd, dn, dim, p, sm, s);
+  s3_spoke_end(tail == 1, slotsT, dc, B, R, cb, ws, wsd, dn, dim, p, sm, s);
 }
 
 // Several pipelines that share one prep (the same batch and row scaling: BASELINE config 5's
@@ -1321,7 +1325,8 @@ struct S3Pipe {
 struct S3Pipes {
   int M;
   int ncomb;  // combiner workgroups per spoke (0: none)
-  int tail;   // 1: each scan workgroup combines its own spoke after its scan
+  int tail;   // 1: each scan workgroup combines its own spoke after its scan; 2: the
+              // spoke's w0-margin workgroup combines it once its w0 pass is done (RARE)
   S3Pipe pipe[kS3MaxPipes];
 };
 
@@ -1339,7 +1344,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   else if (RARE && local < 2 * S_act) bid = local - S_act;
   else bid = local;  // (!RARE: scan blocks [0, S_act), combiners after)
   const S3Pipe& P = pp.pipe[pi];
-  s3_scan_body<RULE, KN, RARE>(bid, nblk, pp.tail != 0, sm, tab, slotsT, meta,
+  s3_scan_body<RULE, KN, RARE>(bid, nblk, pp.tail, sm, tab, slotsT, meta,
                                dc, dn, yv, B, R, prep, nchs, P.w, dim, P.aglob, cap, gstride,
                                P.cb, P.ws, P.wsd, P.p, P.rgran);
 }
@@ -1531,6 +1536,13 @@ OMLDM_API void omldm_scan3_set_gram_valu(int v) { g_s3_gram_valu = v; }
 // the scan — the A/B reference); at most (MAXF + 11) / 12 parts do work
 static int g_s3_comb = 1;
 OMLDM_API void omldm_scan3_set_comb(int v) { g_s3_comb = v < 0 ? 0 : (v > 3 ? 3 : v); }
+// launch form of a mode-4 round: 0 / 1 the latency form (pipelines beyond the GPU's CUs run
+// in later waves of workgroups: the pipeline-major block order needs no co-residency), 2 the
+// throughput form (one self-contained workgroup per spoke, helpers gather),
+// 3 w0-margin workgroups with each scan workgroup combining its own spoke (no combiners),
+// 4 two workgroups per spoke: the w0-margin workgroup combines the spoke after its w0 pass
+static int g_s3_form = 0;
+OMLDM_API void omldm_scan3_set_form(int v) { g_s3_form = v < 0 || v > 4 ? 0 : v; }
 OMLDM_API int omldm_scan3_get_comb() { return g_s3_comb; }
 
 // 1 if a combiner gave up waiting for its spoke's granules since the last call (resets it;
@@ -1742,10 +1754,10 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   const float* sig = shr ? W0.prep + (size_t)S * nchs * (kn == 16 ? s3_prep_floats<16>()
                                                                   : s3_prep_floats<32>())
                          : nullptr;
-  // latency form (mode 4, the whole grid fits the GPU at one workgroup per CU): w0-margin
-  // workgroups + in-launch combiners beside the scans; throughput form (more pipelines than
-  // fit): one self-contained workgroup per spoke — helpers gather, the spoke combined by its
-  // own workgroup after its scan. Mode 3: helpers gather, in-launch combiners.
+  // latency form (mode 4): w0-margin workgroups + in-launch combiners beside the scans, the
+  // grid in waves of workgroups when it exceeds the GPU; throughput form (OMLDM_S3_FORM=2):
+  // one self-contained workgroup per spoke — helpers gather, the spoke combined by its own
+  // workgroup after its scan. Mode 3: helpers gather, in-launch combiners.
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
@@ -1757,15 +1769,25 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   int ncomb = g_s3_comb;
   bool rare = g_s3_mode == 4 && ncomb > 0;
   bool tail = false;
-  if (rare && (long long)M * S_act * (2 + ncomb) > ncu - 16) {
+  int tailm = 0;
+  // auto = the latency form at every pipeline count (profiles/round5/mp_form*.json: 16
+  // pipelines 1.19 ms in three waves of workgroups vs 1.32 ms in the throughput form)
+  (void)ncu;
+  if (rare && g_s3_form == 2) {
     rare = false;
     tail = true;
+    ncomb = 0;
+  } else if (rare && g_s3_form == 3) {
+    tail = true;
+    ncomb = 0;
+  } else if (rare && g_s3_form == 4) {
+    tailm = 2;
     ncomb = 0;
   }
   S3Pipes pp{};
   pp.M = M;
   pp.ncomb = ncomb > 0 ? ncomb : 0;
-  pp.tail = tail ? 1 : 0;
+  pp.tail = tail ? 1 : tailm;
   for (int m = 0; m < M; ++m) {
     if (epoch[m] == 0u) return -2;
     const S3Ws Wm = s3_ws(ptrs + 8 * m);
@@ -1791,7 +1813,7 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   if (e) return e;
   for (int m = 0; m < M; ++m) {
     const S3Ws Wm = s3_ws(ptrs + 8 * m);
-    if (ncomb > 0 || tail) {  // the categorical slots were combined in the scan's launch
+    if (ncomb > 0 || tail || tailm) {  // the categorical slots were combined in the scan's launch
       if (!arrive[m])
         hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, Wm.ws, Wm.wsd, sig, S_act,
                            dn, dim, bias, inv_p[m], dacc[m], cum[m]);

@@ -74,6 +74,7 @@ HIP_SIGS = [
                                     vp]),
     ("omldm_scan3_max_pipes", i32, []),
     ("omldm_scan3_set_comb", None, [i32]),
+    ("omldm_scan3_set_form", None, [i32]),
     ("omldm_scan3_set_prep_split", None, [i32]),
     ("omldm_scan3_get_comb", i32, []),
     ("omldm_scan3_comb_err", i32, []),
