@@ -97,7 +97,9 @@ def main(argv=None) -> int:
         L = make_learner(name.split("@")[0], hyper, space, dev)
         ctx = RoundContext(spokes=spokes)
         try:
-            for k in range(2):
+            # warm every v3 prep workspace set of the ring (ops.linear S3_SLOT_RING) too
+            for k in range(18):
+                ring[k % 3].prep, ring[k % 3]._padded = None, None
                 L.fit(ring[k % 3], ctx)
         except RuntimeError as e:  # a geometry the host guards refuse (sweeps)
             res[name] = {"error": str(e), "spokes": spokes}
