@@ -14,6 +14,7 @@ import sys
 import tempfile
 import textwrap
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -58,6 +59,11 @@ WORKER = textwrap.dedent(r"""
     out = {"rank": rank, "rounds": k, "elapsed": elapsed, "acc": acc, "w0": float(lrn.w[5]),
            "max_lead": getattr(proto, "max_lead", None),
            "plane": ps.plane if ps is not None else None,
+           "w": lrn.w.detach().cpu().tolist(),
+           "events": [e[0] for e in ps.events] if ps is not None else [],
+           "merges": ps.merges if ps is not None else [],
+           "reply_after": {str(k): v for k, v in ps.reply_after.items()} if ps is not None else {},
+           "scale": ps.scale if ps is not None else None,
            "collectives": comm.stats.collectives}
     with open(os.path.join(sys.argv[5], f"rank{rank}.json"), "w") as f:
         json.dump(out, f)
@@ -94,6 +100,68 @@ def _run(proto, seconds=2.5, slow=1, world=3, dev="cpu"):
     return res
 
 
+def _replay(res, world=3, dev="cpu"):
+    """Deterministic host replay of a logged Asynchronous / SSP run (parallel/p2p.py event
+    log): every worker's rounds, pushes and installs re-run on the CPU in the order the
+    hub merged the pushes; the n-th install of worker r takes the hub model as it stood
+    after reply_after[r][n] merges. Returns the hub's final global model."""
+    import torch
+
+    from omldm_amd.api.batch import FeatureSpace
+    from omldm_amd.io.synthetic import synth_raw
+    from omldm_amd.models.base import RoundContext
+    from omldm_amd.models.linear import SVM
+
+    space = FeatureSpace(13, 0, 26, 1 << 12)
+    ctx = RoundContext(spokes=2, inv_p=1.0)
+    hub = res[0]
+    scale = hub["scale"]
+    pools = {r: [synth_raw(space, 256, start=(k * world + r) * 256, seed=25).hashed(space).to(dev)
+                 for k in range(16)] for r in range(world)}
+    lrn = {r: SVM({"variant": "PA-I"}, space, dev) for r in range(world)}
+    x0 = lrn[0].w.clone()
+    glob = x0.clone()
+    snaps = [glob.clone()]
+    st = {r: {"cur": 0, "k": 0, "inst": 0, "base": x0.clone(), "x_push": None, "pushes": 0}
+          for r in range(world)}
+
+    def advance(r, until_push=True):
+        """Run worker r's events up to (and including) its next push; its δ."""
+        s, ev, L = st[r], res[r]["events"], lrn[r]
+        while s["cur"] < len(ev):
+            e = ev[s["cur"]]
+            s["cur"] += 1
+            if e == "step":  # the round trained just before this step
+                L.fit(pools[r][s["k"] % 16], ctx)
+                s["k"] += 1
+            elif e == "install":
+                m = hub["reply_after"][str(r)][s["inst"]]
+                s["inst"] += 1
+                assert m < len(snaps), (r, m, len(snaps))
+                snap = snaps[m]
+                L.w.copy_(snap + (L.w - s["x_push"]))
+                s["base"] = snap.clone()
+                L.on_state_loaded()
+            else:  # "push" / "final"
+                delta = L.w - s["base"]
+                s["x_push"] = L.w.clone()
+                s["pushes"] += 1
+                if until_push:
+                    return delta
+        assert not until_push, f"worker {r}: no push left to merge"
+        return None
+
+    for r, clock in hub["merges"]:
+        delta = advance(r)
+        assert st[r]["pushes"] == clock, (r, clock, st[r]["pushes"])
+        glob.add_(delta, alpha=scale)
+        snaps.append(glob.clone())
+    for r in range(world):  # the final replies' installs
+        advance(r, until_push=False)
+    assert all(st[r]["k"] == res[r]["rounds"] for r in range(world))
+    return glob.cpu()
+
+
 def test_asynchronous_straggler_does_not_stall_fast_workers():
     r = _run("Asynchronous")
     slow = r[1]["rounds"]
@@ -101,6 +169,11 @@ def test_asynchronous_straggler_does_not_stall_fast_workers():
     # after finalize every rank holds the hub's global model, and it learned
     assert r[0]["w0"] == r[1]["w0"] == r[2]["w0"]
     assert min(x["acc"] for x in r.values()) > 0.7, r
+    # ... and that model is exactly the deterministic replay of the logged event order
+    want = _replay(r)
+    for x in r.values():
+        np.testing.assert_allclose(np.asarray(x["w"], dtype=np.float32), want.numpy(),
+                                   rtol=0, atol=1e-6)
 
 
 def test_ssp_bounds_the_lead_over_the_straggler():
@@ -112,6 +185,10 @@ def test_ssp_bounds_the_lead_over_the_straggler():
     assert r[0]["max_lead"] <= 2, r  # rank 0 is the hub: the leads it answered
     assert r[0]["w0"] == r[1]["w0"] == r[2]["w0"]
     assert min(x["acc"] for x in r.values()) > 0.6, r
+    want = _replay(r)
+    for x in r.values():
+        np.testing.assert_allclose(np.asarray(x["w"], dtype=np.float32), want.numpy(),
+                                   rtol=0, atol=1e-6)
 
 
 def test_synchronous_is_paced_by_the_straggler_for_contrast():
@@ -135,3 +212,9 @@ def test_device_plane_on_gpu(proto):
     else:
         assert r[0]["rounds"] >= 3 * slow and r[2]["rounds"] >= 3 * slow, r
     assert min(x["acc"] for x in r.values()) > 0.6, r
+    # the device plane's merges / installs against the logged order replayed with the same
+    # GPU learners (the rounds' fp32 atomics may reorder: a tolerance, not bit equality)
+    want = _replay(r, dev="cuda")
+    got = np.asarray(r[0]["w"], dtype=np.float32)
+    np.testing.assert_allclose(got, want.numpy(), rtol=1e-3,
+                               atol=1e-4 * max(1.0, float(np.abs(got).max())))
