@@ -2,7 +2,7 @@
 8-GPU RCCL run is the driver's). It exercises the exact multi-GPU code path of bench.py —
 device-resident fused round accumulators summed by a collective, then applied — and
 checks the Synchronous invariant: two ranks × S spokes == one rank × 2S spokes on the
-concatenated batch."""
+concatenated batch, on the v3 table scan the bench runs at N > 1 (fp32 and bf16 models)."""
 import os
 import socket
 import tempfile
@@ -14,7 +14,10 @@ import torch.multiprocessing as mp
 from omldm_amd.api.batch import FeatureSpace
 
 SP = FeatureSpace(13, 0, 26, 1 << 16, field_aware=True)
-S, R, ROUNDS = 64, 16, 3
+ROUNDS = 3
+# (learner hyper-parameters, spokes per rank, rows per spoke)
+CASES = {"fp32": ({"variant": "PA-I"}, 16, 512),
+         "bf16": ({"variant": "PA-I", "modelDtype": "bf16"}, 64, 16)}
 
 
 def _port():
@@ -25,51 +28,59 @@ def _port():
     return p
 
 
-def _batch(rank, world, r):
+def _batch(rank, world, r, S, R):
     from omldm_amd.io.synthetic import synth_batch
 
     return synth_batch(SP, S * R, start=(r * world + rank) * S * R, seed=7)
 
 
-def _rank(rank, world, port, out, parts=1):
+def _rank(rank, world, port, out, parts, case):
     import torch.distributed as dist
 
     from omldm_amd.models.linear import SVM
+    from omldm_amd.ops import linear as OL
     from omldm_amd.parallel.comm import Comm
     from omldm_amd.parallel.protocols import Synchronous
 
+    hyper, S, R = CASES[case]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
-    L = SVM({"variant": "PA-I", "modelDtype": "bf16", "tableLog2": 10}, SP, dev)
+    L = SVM(dict(hyper), SP, dev)
     P = Synchronous(Comm(), L, {"virtualSpokes": S, "reduceParts": parts})
+    v3 = OL.SCAN3_ROUNDS
     for r in range(ROUNDS):
-        P.round(_batch(rank, world, r).to(dev))
+        P.round(_batch(rank, world, r, S, R).to(dev))
     torch.cuda.synchronize()
-    torch.save({"w": L.w.cpu()}, os.path.join(out, f"r{rank}.pt"))
+    torch.save({"w": L.w.cpu(), "v3": torch.tensor(OL.SCAN3_ROUNDS - v3)},
+               os.path.join(out, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("parts", [1, 3])
-def test_two_ranks_one_gpu_equal_one_rank_double_spokes(cuda, parts):
+@pytest.mark.parametrize("case,parts", [("fp32", 1), ("fp32", 3), ("bf16", 1)])
+def test_two_ranks_one_gpu_equal_one_rank_double_spokes(cuda, case, parts):
     from omldm_amd.api.batch import HashedBatch
     from omldm_amd.models.linear import SVM
     from omldm_amd.parallel.comm import Comm
     from omldm_amd.parallel.protocols import Synchronous
 
+    hyper, S, R = CASES[case]
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_rank, args=(2, _port(), d, parts), nprocs=2, start_method="spawn")
-        w0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)["w"]
-        w1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)["w"]
+        mp.start_processes(_rank, args=(2, _port(), d, parts, case), nprocs=2,
+                           start_method="spawn")
+        r0 = torch.load(os.path.join(d, "r0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "r1.pt"), weights_only=True)
+    assert int(r0["v3"]) == int(r1["v3"]) == ROUNDS, "the ranks' rounds left the v3 scan"
+    w0, w1 = r0["w"], r1["w"]
     torch.testing.assert_close(w0, w1)
     assert float(w0.abs().sum()) > 0
     # single rank, 2S spokes, rank-0 rows then rank-1 rows (spoke s ↔ rows [sR, sR+R))
-    L = SVM({"variant": "PA-I", "modelDtype": "bf16", "tableLog2": 10}, SP, cuda)
+    L = SVM(dict(hyper), SP, cuda)
     P = Synchronous(Comm(), L, {"virtualSpokes": 2 * S})
     for r in range(ROUNDS):
-        b = HashedBatch.cat_batches([_batch(0, 2, r), _batch(1, 2, r)])
+        b = HashedBatch.cat_batches([_batch(0, 2, r, S, R), _batch(1, 2, r, S, R)])
         P.round(b.to(cuda))
     torch.cuda.synchronize()
     torch.testing.assert_close(L.w.cpu(), w0, rtol=1e-3, atol=1e-4)
