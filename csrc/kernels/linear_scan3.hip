@@ -376,6 +376,10 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
   }
 }
 
+// Diagnostics: bit 0 skips the categorical match counts, bit 1 the dense MFMA, bit 2 the
+// output stores of s3_gram_mfma_kernel (scripts/gram_ablate.py; 0 in production)
+__device__ int g_s3_gram_ablate = 0;
+
 // Pass 3 on the matrix cores (the default; s3_gram_kernel above is the VALU reference the
 // GPU test compares it with). grid (chunks, S_act), 256 threads = 4 waves. Every load of the
 // chunk pair (slots of chunks c and c − 1, their numerical rows) is issued before the first
@@ -476,11 +480,12 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+    const int abl = g_s3_gram_ablate;
     if (!zero) {
       int cnt[16];
 #pragma unroll
       for (int g = 0; g < 16; ++g) cnt[g] = 0;
-      for (int f = 0; f < dc; ++f) {
+      for (int f = 0; f < ((abl & 1) ? 0 : dc); ++f) {
         const int b = sl[d][f][J0 + l31];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -496,11 +501,14 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
       }
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc[g] = (float)cnt[g];
+      if (!(abl & 2)) {
 #pragma unroll
-      for (int k0 = 0; k0 < KN; k0 += 2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xn[0][I0 + l31][k0 + hi], xn[d][J0 + l31][k0 + hi],
-                                                   acc, 0, 0, 0);
+        for (int k0 = 0; k0 < KN; k0 += 2)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xn[0][I0 + l31][k0 + hi],
+                                                     xn[d][J0 + l31][k0 + hi], acc, 0, 0, 0);
+      }
     }
+    if (abl & 4) continue;
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int t = I0 + (g & 3) + 8 * (g >> 2) + 4 * hi, col = J0 + l31;
@@ -610,7 +618,14 @@ struct S3Comb {
   double* cum;
   const float* sig;  // shrinking rules: σ at each spoke's end (its c's scale), else null
   int wbf;           // the model w is bf16 (modelDtype bf16: margins on the bf16 weights)
+  int cns;           // spokes per combiner workgroup (> 1: one part, chunks interleaved)
 };
+
+// workgroups of one pipeline: its w0-margin (RARE) and scan workgroups, then its combiners
+__host__ __device__ inline int s3_nper(int S_act, bool rare, int ncomb, int cns) {
+  const int nc = cns > 1 ? (S_act + cns - 1) / cns : ncomb * S_act;
+  return S_act * (rare ? 2 : 1) + (ncomb > 0 ? nc : 0);
+}
 
 // w[i] of a bf16 model (wbf) or an fp32 one
 __device__ __forceinline__ float s3_w16(const float* w, long long i) {
@@ -627,9 +642,12 @@ constexpr unsigned SPIN_MAX = 1u << 21;      // polls before a combiner gives up
 // the scanner and only the last chunk is left when the scan ends (one wave per field, every
 // chunk, fell behind: its slot loads and its poll were one round trip each per chunk). All
 // of a chunk's slot loads are issued before the poll. Rows with c = 0 add nothing.
+// ns > 1: one combiner for spokes s .. s + ns − 1, their chunks interleaved in time order
+// (chunk k of each spoke in turn: the spokes scan at the same pace) — fewer workgroups when
+// a launch holds more pipelines than the GPU has CUs.
 __device__ __forceinline__ void s3_combine_spoke(const int* __restrict__ slotsT, int dc, int B,
                                                  int R, const S3Comb& cb, S3Smem& sm, int s,
-                                                 int part, int nparts) {
+                                                 int part, int nparts, int ns = 1) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int* hk = reinterpret_cast<int*>(&sm.G[0][0][0]);
   float* hv = &sm.X1[0][0][0];
@@ -638,13 +656,16 @@ __device__ __forceinline__ void s3_combine_spoke(const int* __restrict__ slotsT,
     hv[j] = 0.f;
   }
   __syncthreads();
-  int t0, t1;
-  spoke_rows(s, R, B, t0, t1);
-  const int nch = t0 < t1 ? (t1 - t0 + s3::CH - 1) / s3::CH : 0;
+  const int nchs = (R + s3::CH - 1) / s3::CH;  // chunks of a full spoke
   const int wstride = nparts * (s3::NH + 1);
   const unsigned long long want = (unsigned long long)cb.epoch;
-  const float sc = cb.inv_p * (cb.sig ? cb.sig[s] : 1.f);  // σ_end·Σ c·x: the spoke's Δ
-  for (int k = part * (s3::NH + 1) + wave; k < nch; k += wstride) {
+  for (int kk = part * (s3::NH + 1) + wave; kk < nchs * ns; kk += wstride) {
+    const int si = s + kk % ns, k = kk / ns;
+    if (si >= cb.S_act) continue;
+    int t0, t1;
+    spoke_rows(si, R, B, t0, t1);
+    // σ_end·Σ c·x: the spoke's Δ
+    const float sc = cb.inv_p * (cb.sig ? cb.sig[si] : 1.f);
     const int row = t0 + k * s3::CH + lane;
     const bool in = row < t1;
     int v[s3::MAXF];
@@ -773,11 +794,16 @@ __device__ __forceinline__ void s3_rare(const int* __restrict__ slotsT, int dc, 
   }
 }
 
-// A combiner workgroup: spoke i mod S_act, part i / S_act of the combiner blocks.
+// A combiner workgroup: ns = 1: spoke i mod S_act, part i / S_act of the combiner blocks;
+// ns > 1 (one part): spokes ns·i .. ns·i + ns − 1.
 __device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int dc, int B, int R,
                                            const S3Comb& cb, S3Smem& sm, int base, int bid,
-                                           int nblk) {
+                                           int nblk, int ns) {
   const int i = bid - base;
+  if (ns > 1) {
+    s3_combine_spoke(slotsT, dc, B, R, cb, sm, ns * i, 0, 1, ns);
+    return;
+  }
   s3_combine_spoke(slotsT, dc, B, R, cb, sm, i % cb.S_act, i / cb.S_act, (nblk - base) / cb.S_act);
 }
 
@@ -860,7 +886,7 @@ __device__ __forceinline__ void s3_scan_body(
       }
       return;
     }
-    s3_combine(slotsT, dc, B, R, cb, sm, (RARE ? 2 : 1) * cb.S_act, bid, nblk);  // a combiner
+    s3_combine(slotsT, dc, B, R, cb, sm, (RARE ? 2 : 1) * cb.S_act, bid, nblk, cb.cns);
     return;
   }
   const int tid = threadIdx.x;
@@ -1337,7 +1363,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     int dim, int cap, long long gstride, int S_act, S3Pipes pp) {
   __shared__ S3Smem sm;
   extern __shared__ float tab[];  // [cap] + 64 scratch words (one per lane)
-  const int nblk = S_act * ((RARE ? 2 : 1) + pp.ncomb);  // per pipeline
+  const int nblk = s3_nper(S_act, RARE, pp.ncomb, pp.pipe[0].cb.cns);  // per pipeline
   const int pi = (int)blockIdx.x / nblk, local = (int)blockIdx.x % nblk;
   int bid;
   if (RARE && local < S_act) bid = S_act + local;  // its w0-margin workgroups first
@@ -1468,7 +1494,7 @@ static int s3_launch_scan_t(const int* slotsT, const uint32_t* meta, int dc, int
   }
   // per pipeline: S_act rare-slot (RARE), S_act scan and ncomb·S_act combiner workgroups,
   // role-major across the pipelines (s3_scan_kernel)
-  const int nblk = pp.M * S_act * ((RARE ? 2 : 1) + pp.ncomb);
+  const int nblk = pp.M * s3_nper(S_act, RARE, pp.ncomb, pp.pipe[0].cb.cns);
   hipLaunchKernelGGL((s3_scan_kernel<RULE, KN, RARE>), dim3(nblk), dim3(s3::NT),
                      (size_t)(cap + 64) * sizeof(float), st, slotsT, meta, dc, dn, y, B, R, prep,
                      nchs, dim, cap, gstride, S_act, pp);
@@ -1531,6 +1557,9 @@ OMLDM_API void omldm_scan3_set_cap(int cap) { g_s3_cap_override = cap; }
 // 1: pass 3 on the VALU reference kernel (tests: A/B against the MFMA kernel)
 static int g_s3_gram_valu = 0;
 OMLDM_API void omldm_scan3_set_gram_valu(int v) { g_s3_gram_valu = v; }
+OMLDM_API int omldm_scan3_set_gram_ablate(int v) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s3_gram_ablate), &v, sizeof(v));
+}
 
 // combiner workgroups per spoke in the scan's launch (0: the whole-GPU scatter kernel after
 // the scan — the A/B reference); at most (MAXF + 11) / 12 parts do work
@@ -1542,6 +1571,8 @@ OMLDM_API void omldm_scan3_set_comb(int v) { g_s3_comb = v < 0 ? 0 : (v > 3 ? 3 
 // 3 w0-margin workgroups with each scan workgroup combining its own spoke (no combiners),
 // 4 two workgroups per spoke: the w0-margin workgroup combines the spoke after its w0 pass
 static int g_s3_form = 0;
+static int g_s3_cns = 0;  // spokes per combiner workgroup: 0 auto
+OMLDM_API void omldm_scan3_set_cns(int v) { g_s3_cns = v < 0 || v > 16 ? 0 : v; }
 OMLDM_API void omldm_scan3_set_form(int v) { g_s3_form = v < 0 || v > 4 ? 0 : v; }
 OMLDM_API int omldm_scan3_get_comb() { return g_s3_comb; }
 
@@ -1772,7 +1803,6 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   int tailm = 0;
   // auto = the latency form at every pipeline count (profiles/round5/mp_form*.json: 16
   // pipelines 1.19 ms in three waves of workgroups vs 1.32 ms in the throughput form)
-  (void)ncu;
   if (rare && g_s3_form == 2) {
     rare = false;
     tail = true;
@@ -1784,6 +1814,10 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
     tailm = 2;
     ncomb = 0;
   }
+  // spokes per combiner workgroup (OMLDM_S3_CNS, A/B): 1 — a combiner of 2 or 4 spokes falls
+  // behind its scans (16 pipelines: 1.20 / 1.27 / 1.67 ms, profiles/round5/mp_cns*.json)
+  int cns = g_s3_cns > 0 ? g_s3_cns : 1;
+  if (!rare || ncomb != 1) cns = 1;
   S3Pipes pp{};
   pp.M = M;
   pp.ncomb = ncomb > 0 ? ncomb : 0;
@@ -1803,7 +1837,7 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
     pp.pipe[m] = S3Pipe{w[m], Wm.aglob, Wm.ws, Wm.wsd, rare ? Wm.gran + B : nullptr,
                         S3Comb{W0.lidcount, Wm.gran, epoch[m], S_act, dacc[m], inv_p[m],
                                static_cast<unsigned long long*>(arrive[m]), cum[m], sig,
-                               (flags & 2) ? 1 : 0},
+                               (flags & 2) ? 1 : 0, cns},
                         p};
   }
   const int e = kn == 16 ? s3_launch_scan<16>(rule, rare, W0.slotsT, W0.meta, dc, dn, y, B, R,

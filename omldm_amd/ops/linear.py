@@ -313,6 +313,7 @@ def _s3_lib():
         h.omldm_scan3_set_mode(S3_MODE)
         # A/B: the launch form (0 auto, 1 latency form always, 2 throughput form always)
         h.omldm_scan3_set_form(int(os.environ.get("OMLDM_S3_FORM", "0")))
+        h.omldm_scan3_set_cns(int(os.environ.get("OMLDM_S3_CNS", "0")))
         _S3_MODE_SET["done"] = True
     return h
 

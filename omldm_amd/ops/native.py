@@ -62,6 +62,7 @@ HIP_SIGS = [
     ("omldm_scan3_lds_cap", i32, []),
     ("omldm_scan3_set_cap", None, [i32]),
     ("omldm_scan3_set_gram_valu", None, [i32]),
+    ("omldm_scan3_set_gram_ablate", i32, [i32]),
     ("omldm_scan3_fits", i32, [i32, i32, i32, i32]),
     ("omldm_scan3_ws_words", i64, [i32, i32, i32, i32, i32, i32, i64, i32]),
     ("omldm_scan3_prepare", i32, [vp, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32,
@@ -75,6 +76,7 @@ HIP_SIGS = [
     ("omldm_scan3_max_pipes", i32, []),
     ("omldm_scan3_set_comb", None, [i32]),
     ("omldm_scan3_set_form", None, [i32]),
+    ("omldm_scan3_set_cns", None, [i32]),
     ("omldm_scan3_set_prep_split", None, [i32]),
     ("omldm_scan3_get_comb", i32, []),
     ("omldm_scan3_comb_err", i32, []),
