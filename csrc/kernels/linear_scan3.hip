@@ -308,12 +308,15 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
     // a: −1/(‖x‖² + kadd) (affine 1: hinge, ε), 1 (0: logistic), y (2: Pegasos, u = y·v).
     // Shrinking affine rules scale the Grams by a·σ_t/σ_{t+1} = a/r (the scanner's u is
     // (a·m + b)/σ_{t+1}); the others keep u in v-space units
+    // affine 3 (MultiClassPA, s3mc_scan_kernel): a = 1/(2‖x‖² + kadd), the Grams unscaled
     float a = 0.f, g = 1.f;
     if (live) {
-      a = affine == 1 ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : (affine == 2 ? (yt == yt ? yt : 0.f) : 1.f);
+      a = affine == 1 ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f)
+        : affine == 2 ? (yt == yt ? yt : 0.f)
+        : affine == 3 ? (n2 > 0.f ? 1.f / (2.f * n2 + kadd) : 0.f) : 1.f;
       if (affine == 1 && shr == 1 && yt == yt) g = 1.f / shr_r;
     }
-    sa[tid] = a * g;
+    sa[tid] = affine == 3 ? (live ? 1.f : 0.f) : a * g;
     out[2 * s3::MAT + tid] = a;
     out[s3_prep_y<KN>() + tid] = yt;
   }
@@ -454,12 +457,15 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
     // a: −1/(‖x‖² + kadd) (affine 1: hinge, ε), 1 (0: logistic), y (2: Pegasos, u = y·v).
     // Shrinking affine rules scale the Grams by a·σ_t/σ_{t+1} = a/r (the scanner's u is
     // (a·m + b)/σ_{t+1}); the others keep u in v-space units
+    // affine 3 (MultiClassPA, s3mc_scan_kernel): a = 1/(2‖x‖² + kadd), the Grams unscaled
     float a = 0.f, g = 1.f;
     if (live) {
-      a = affine == 1 ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f) : (affine == 2 ? (yt == yt ? yt : 0.f) : 1.f);
+      a = affine == 1 ? (n2 > 0.f ? -1.f / (n2 + kadd) : 0.f)
+        : affine == 2 ? (yt == yt ? yt : 0.f)
+        : affine == 3 ? (n2 > 0.f ? 1.f / (2.f * n2 + kadd) : 0.f) : 1.f;
       if (affine == 1 && shr == 1 && yt == yt) g = 1.f / shr_r;
     }
-    sa[tid] = a * g;
+    sa[tid] = affine == 3 ? (live ? 1.f : 0.f) : a * g;
     out[2 * s3::MAT + tid] = a;
     out[s3_prep_y<KN>() + tid] = yt;
   }
@@ -1481,6 +1487,468 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
   }
 }
 
+// ------------------------------------------------------------------ MultiClassPA on v3
+// The reference's MultiClassPA (K prototypes; row t moves prototype y_t by +τ·x_t and the
+// best wrong one r_t by −τ·x_t, τ = min(C, ℓ/(2‖x‖²)), ℓ = max(0, 1 − (s_y − s_r))) on the
+// same prep as the binary scan (slots, occurrence flags, unscaled chunk Grams, a_t =
+// 1/(2‖x‖² + kadd)). Per spoke one 12-wave workgroup: the scanner keeps the K scores of its
+// row as u[k] = (base margin) + Σ_{s<t} c_s^k·G_ts, the step broadcasts (τ_t, r_t) and
+// every lane adds ±τ_t·G[lane][t] to two of its K scores; the helpers assemble the K base
+// margins from the slot table (K floats per table slot: w0 at the first occurrence, the
+// spoke's updates added by the scatter) or the key-major prototypes, and stage the Grams.
+// Each row's (τ, r) goes to a record; s3mc_scatter_kernel adds the spokes' updates after.
+namespace s3 {
+constexpr int MCK = 4;  // classes on the v3 multiclass scan (K ≤ 4; more: the spoke tables)
+}
+
+template <int K>
+struct S3McSmem {
+  alignas(16) float G[2][s3::CH][s3::GS];
+  alignas(16) float X1[2][s3::CH][s3::GS];
+  float part[2][s3::NHA][K][s3::CH];  // base-margin partials per helper and class
+  float tau[2][s3::CH];               // τ of the chunk's rows, by parity
+  int rr[2][s3::CH];                  // r (the updated wrong class) of the chunk's rows
+};
+
+template <int K>
+__device__ __forceinline__ void s3mc_decide(const float (&u)[K], int yi, int nclass, float a,
+                                            float cmax, bool valid, float& tau, int& r,
+                                            float& margin) {
+  float sy = 0.f, best = -INFINITY;
+  r = -1;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k < nclass) {
+      if (k == yi) sy = u[k];
+      else if (u[k] > best) {
+        best = u[k];
+        r = k;
+      }
+    }
+  }
+  margin = sy - best;
+  const float loss = fmaxf(0.f, 1.f - margin);
+  tau = (valid && r >= 0 && a > 0.f) ? fminf(cmax, loss * a) : 0.f;
+}
+
+struct S3McArgs {
+  const float* Wt;  // key-major prototypes [dim][kp] (fp32)
+  int kp, nclass, variant;
+  float cmax;       // C (PA-I), +inf otherwise
+  float* ws;        // [S][WS] loss, rows, mistakes
+  float* wsd;       // [S][K][DS] dense-column updates per class
+  float* aglob;     // [S][gstride·K] the slot table past the LDS
+  float* tau;       // [B] τ per row
+  int* rr;          // [B] r per row
+};
+
+template <int K, int KN>
+__global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s3mc_scan_kernel(
+    const int* __restrict__ slotsT, const uint32_t* __restrict__ meta,
+    const int* __restrict__ lidcount, int dc, int dn, int bias, int B, int R,
+    const float* __restrict__ prep, int nchs, int dim, int cap, long long gstride, S3McArgs A) {
+  __shared__ S3McSmem<K> sm;
+  extern __shared__ float tab[];  // [cap]: table slot i's class k at i·K + k
+  constexpr int PF = s3_prep_floats<KN>();
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int s = blockIdx.x;
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  if (t0 >= t1) {
+    if (tid < s3::WS) A.ws[(size_t)s * s3::WS + tid] = 0.f;
+    for (int i = tid; i < K * s3::DS; i += s3::NT) A.wsd[(size_t)s * K * s3::DS + i] = 0.f;
+    return;
+  }
+  const int nch = (t1 - t0 + s3::CH - 1) / s3::CH;
+  const float* P0 = prep + (size_t)s * nchs * PF;
+  auto chunk_prep = [&](int k) { return P0 + (size_t)k * PF; };
+  float* ag = A.aglob + (size_t)s * gstride * K;
+
+  if (wave == 0) {
+    // ---------------------------------------------------------------- scanner
+    __builtin_amdgcn_s_setprio(3);
+    float loss = 0.f, nex = 0.f, mist = 0.f;
+    float f1[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) f1[k] = 0.f;
+    float ynx = chunk_prep(0)[s3_prep_y<KN>() + lane];
+    float anx = chunk_prep(0)[2 * s3::MAT + lane];
+    for (int k = -1; k <= nch; ++k) {
+      if (k >= 0 && k < nch) {
+        const int b = k & 1;
+        const int row = t0 + k * s3::CH + lane;
+        const bool valid = row < t1 && ynx == ynx;
+        const int yi = valid ? (int)ynx : -1;
+        const float a = valid ? anx : 0.f;
+        if (k + 1 < nch) {
+          ynx = chunk_prep(k + 1)[s3_prep_y<KN>() + lane];
+          anx = chunk_prep(k + 1)[2 * s3::MAT + lane];
+        }
+        float u[K], n1[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+          float m0 = 0.f;
+#pragma unroll
+          for (int q = 0; q < s3::NHA; ++q) m0 += sm.part[b][q][c][lane];
+          u[c] = m0 + f1[c];
+          n1[c] = 0.f;
+        }
+        // the lane's row of G_k in VGPRs; the chunk's steps are kept (τ_t, r_t, y_t) and
+        // folded into chunk k+1 through X1 after the chain (off it, from LDS)
+        const float* grow = &sm.G[b][lane][0];
+        float gg[s3::CH];
+#pragma unroll
+        for (int t4 = 0; t4 < s3::CH; t4 += 4) {
+          const float4 g4 = *reinterpret_cast<const float4*>(grow + t4);
+          gg[t4] = g4.x, gg[t4 + 1] = g4.y, gg[t4 + 2] = g4.z, gg[t4 + 3] = g4.w;
+        }
+#pragma unroll
+        for (int t = 0; t < s3::CH; ++t) {
+          float tl, mg;
+          int rl;
+          s3mc_decide<K>(u, yi, A.nclass, a, A.cmax, valid, tl, rl, mg);
+          const float ct = readlane_f(tl, t);
+          const int rt = __builtin_amdgcn_readlane(rl, t);
+          const int yt = __builtin_amdgcn_readlane(yi, t);
+#pragma unroll
+          for (int c = 0; c < K; ++c) {
+            const float cf = (c == yt ? ct : 0.f) - (c == rt ? ct : 0.f);
+            u[c] = fmaf(cf, gg[t], u[c]);   // G strictly lower: lane t frozen after step t
+          }
+        }
+        float tl, mg;
+        int rl;
+        s3mc_decide<K>(u, yi, A.nclass, a, A.cmax, valid, tl, rl, mg);
+        // chunk k+1's X1 fold: n1[c] = Σ_t c_t^c · X1_{k+1}[lane][t]
+        {
+          const float* xrow = &sm.X1[b ^ 1][lane][0];
+#pragma unroll 8
+          for (int t = 0; t < s3::CH; ++t) {
+            const float ct = readlane_f(tl, t);
+            const int rt = __builtin_amdgcn_readlane(rl, t);
+            const int yt = __builtin_amdgcn_readlane(yi, t);
+            const float x = xrow[t];
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+              const float cf = (c == yt ? ct : 0.f) - (c == rt ? ct : 0.f);
+              n1[c] = fmaf(cf, x, n1[c]);
+            }
+          }
+        }
+        sm.tau[b][lane] = tl;
+        sm.rr[b][lane] = rl;
+        if (row < t1) {
+          A.tau[row] = tl;
+          A.rr[row] = rl;
+        }
+        if (valid) {
+          loss += fmaxf(0.f, 1.f - mg);
+          nex += 1.f;
+          mist += mg <= 0.f ? 1.f : 0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < K; ++c) f1[c] = n1[c];
+      }
+      __syncthreads();
+    }
+    loss = wave_sum(loss);
+    nex = wave_sum(nex);
+    mist = wave_sum(mist);
+    if (lane == 0) {
+      float* wr = A.ws + (size_t)s * s3::WS;
+      wr[0] = loss, wr[1] = nex, wr[2] = mist;
+      for (int i = 3; i < s3::WS; ++i) wr[i] = 0.f;
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------- helpers
+  const int q = wave - 1, r = lane;
+  const int kd = dn + (bias ? 1 : 0);
+  const int hl = q * 64 + lane;
+  const int capid = cap / K;  // table slots in LDS; the rest in ag (global)
+  float wn[K][s3::NJ], w0[K][s3::NJ];
+#pragma unroll
+  for (int i = 0; i < s3::NJ; ++i) {
+    const int j = q + s3::NHA * i;
+    const int key = j < dn ? j : dim - 1;
+    const bool real = j < KN && (j < dn || (bias && j == dn));
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      w0[c][i] = real ? A.Wt[(size_t)key * A.kp + c] : 0.f;
+      wn[c][i] = w0[c][i];
+    }
+  }
+  constexpr int NV4 = (2 * s3::MAT / 4 + 64 * s3::NHA - 1) / (64 * s3::NHA);
+  constexpr int NJK = (KN + s3::NHA - 1) / s3::NHA;
+  struct Set {
+    int cs[s3::NF];
+    uint32_t cm[s3::NF];
+    float g[s3::NF][K];
+    f32x4 v[NV4];
+    float xs[s3::NJ], xc[s3::NJ];
+  };
+  uint32_t p1[s3::NF], p2[s3::NF];
+  auto load_words = [&](int ch, Set& S) {
+#pragma unroll
+    for (int i = 0; i < s3::NF; ++i) {
+      const int f = q + s3::NHA * i;
+      const int row = t0 + ch * s3::CH + r;
+      const bool ok = ch >= 0 && ch < nch && f < dc && row < t1;
+      const size_t at = ok ? (size_t)f * B + row : 0;
+      const int sl = slotsT[at];
+      const uint32_t mm = meta[at];
+      S.cs[i] = ok ? sl : -1;
+      S.cm[i] = ok ? mm : 0u;
+    }
+  };
+  auto issue_gathers = [&](Set& S) {
+#pragma unroll
+    for (int i = 0; i < s3::NF; ++i) {
+      const bool glob = S.cs[i] != -1 && !(S.cm[i] & s3::F_TG);
+      const float* src = A.Wt + (size_t)(glob ? (S.cs[i] & 0x7fffffff) : 0) * A.kp;
+      if constexpr (K == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        S.g[i][0] = v.x, S.g[i][1] = v.y, S.g[i][2] = v.z, S.g[i][3] = v.w;
+      } else {
+        const float2 v = *reinterpret_cast<const float2*>(src);
+        S.g[i][0] = v.x, S.g[i][1] = v.y;
+      }
+    }
+  };
+  auto issue_staging = [&](int ch, Set& S) {
+#pragma unroll
+    for (int u = 0; u < NV4; ++u) {
+      const int i = min(hl + 64 * s3::NHA * u, 2 * s3::MAT / 4 - 1);
+      const int mtx = i >> 10, e = i & 1023;
+      const int kc = max(0, min(ch + mtx, nch - 1));
+      S.v[u] = reinterpret_cast<const f32x4*>(chunk_prep(kc) + mtx * s3::MAT)[e];
+    }
+  };
+  auto load_dense = [&](int ch, float* xd) {
+#pragma unroll
+    for (int i = 0; i < NJK; ++i) {
+      const int j = q + s3::NHA * i;
+      const bool ok = j < KN && ch >= 0 && ch < nch;
+      const int jc = j < KN ? j : 0, cc = max(0, min(ch, nch - 1));
+      const float v = chunk_prep(cc)[2 * s3::MAT + s3::CH + jc * s3::CH + r];
+      xd[i] = ok ? v : 0.f;
+    }
+  };
+  // table slot `lid`, class c: LDS below capid slots, else the spoke's global spill area
+  auto tab_add = [&](auto spill_tag, int lid, int c, float v) {
+    constexpr bool SPILL = decltype(spill_tag)::value;
+    if (!SPILL || lid < capid) atomicAdd(&tab[lid * K + c], v);
+    else atomicAdd(&ag[(size_t)(lid - capid) * K + c], v);
+  };
+  auto body = [&](auto spill_tag, int k, Set& CUR, Set& NXT) {
+    constexpr bool SPILL = decltype(spill_tag)::value;
+    const int cn = k + 1, ks = k - 1;
+    load_words(cn + 1, NXT);
+    issue_staging(cn + 1, NXT);
+    load_dense(ks + 1, NXT.xs);
+    load_dense(cn + 1, NXT.xc);
+    // ---- scatter chunk ks: +τ·sign into class y, −τ·sign into class r
+    if (ks >= 0) {
+      const float tv = sm.tau[ks & 1][r];
+      const int rc = sm.rr[ks & 1][r];
+      const float yf = chunk_prep(ks)[s3_prep_y<KN>() + r];
+      const int yc = (yf == yf && yf >= 0.f && yf < (float)A.nclass) ? (int)yf : -1;
+#pragma unroll
+      for (int i = 0; i < s3::NF; ++i) {
+        const uint32_t m = p2[i];
+        const bool sc = (m & s3::F_SCAT) != 0u && tv != 0.f;
+        if (__builtin_amdgcn_ballot_w64(sc) == 0ull) continue;
+        const int lid = (int)(m >> s3::LID_SHIFT);
+        const float val = (m & s3::F_SIGN) ? -tv : tv;
+        if (sc) {
+          if (yc >= 0) tab_add(spill_tag, lid, yc, val);
+          if (rc >= 0) tab_add(spill_tag, lid, rc, -val);
+        }
+      }
+      if constexpr (SPILL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < NJK; ++i) {
+        const int j = q + s3::NHA * i;
+        if (j < kd) {
+#pragma unroll
+          for (int c = 0; c < K; ++c) {
+            const float cf = (c == yc ? tv : 0.f) - (c == rc ? tv : 0.f);
+            wn[c][i] += wave_sum(cf * CUR.xs[i]);
+          }
+        }
+      }
+    }
+    // ---- base margins of chunk cn
+    if (cn < nch) {
+      float base[K];
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        base[c] = 0.f;
+#pragma unroll
+        for (int i = 0; i < NJK; ++i) base[c] = fmaf(CUR.xc[i], wn[c][i], base[c]);
+      }
+#pragma unroll
+      for (int i = 0; i < s3::NF; ++i) {
+        const uint32_t m = CUR.cm[i];
+        const bool here = CUR.cs[i] != -1;
+        const bool tg = here && (m & s3::F_TG), init = here && !tg && (m & s3::F_INIT);
+        const int lid = (int)(m >> s3::LID_SHIFT);
+        float val[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) val[c] = CUR.g[i][c];
+        if (!SPILL || __builtin_amdgcn_ballot_w64((tg || init) && lid >= capid) == 0ull) {
+          if (tg) {
+#pragma unroll
+            for (int c = 0; c < K; ++c) val[c] = tab[lid * K + c];
+          }
+          if (init) {
+#pragma unroll
+            for (int c = 0; c < K; ++c) tab[lid * K + c] = val[c];
+          }
+        } else if constexpr (SPILL) {
+          float* gp = ag + (size_t)(lid >= capid ? lid - capid : 0) * K;
+          if (tg) {
+#pragma unroll
+            for (int c = 0; c < K; ++c)
+              val[c] = lid < capid ? tab[lid * K + c]
+                                   : __hip_atomic_load(gp + c, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          if (init) {
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+              if (lid < capid) tab[lid * K + c] = val[c];
+              else __hip_atomic_store(gp + c, val[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (here) {
+#pragma unroll
+          for (int c = 0; c < K; ++c) base[c] += (m & s3::F_SIGN) ? -val[c] : val[c];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < K; ++c) sm.part[cn & 1][q][c][r] = base[c];
+    }
+    // ---- aG_{cn} → G[cn & 1], aX1_{cn+1} → X1[(cn+1) & 1]
+#pragma unroll
+    for (int u = 0; u < NV4; ++u) {
+      const int i = hl + 64 * s3::NHA * u;
+      const int mtx = i >> 10, e = i & 1023;
+      if (i < 2 * s3::MAT / 4 && cn + mtx < nch) {
+        const int row = e >> 4, col = (e & 15) * 4;
+        float* dst = mtx == 0 ? &sm.G[cn & 1][row][col] : &sm.X1[(cn + 1) & 1][row][col];
+        *reinterpret_cast<f32x4*>(dst) = CUR.v[u];
+      }
+    }
+    issue_gathers(NXT);
+#pragma unroll
+    for (int i = 0; i < s3::NF; ++i) {
+      p2[i] = p1[i];
+      p1[i] = CUR.cm[i];
+    }
+    __syncthreads();
+  };
+  Set Sa, Sb;
+#pragma unroll
+  for (int i = 0; i < s3::NF; ++i) p1[i] = p2[i] = 0u;
+  load_words(0, Sa);
+  issue_staging(0, Sa);
+  load_dense(-2, Sa.xs);
+  load_dense(0, Sa.xc);
+  issue_gathers(Sa);
+  if (lidcount[s] <= capid) {
+    for (int k = -1; k <= nch; k += 2) {
+      body(S3Tag<false>{}, k, Sa, Sb);
+      if (k + 1 <= nch) body(S3Tag<false>{}, k + 1, Sb, Sa);
+    }
+  } else {
+    for (int k = -1; k <= nch; k += 2) {
+      body(S3Tag<true>{}, k, Sa, Sb);
+      if (k + 1 <= nch) body(S3Tag<true>{}, k + 1, Sb, Sa);
+    }
+  }
+  // round end: this wave's dense-column updates per class
+#pragma unroll
+  for (int i = 0; i < s3::NJ; ++i) {
+    const int j = q + s3::NHA * i;
+    if (lane == 0 && j < s3::DS)
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+        A.wsd[((size_t)s * K + c) * s3::DS + j] = j < KN ? wn[c][i] - w0[c][i] : 0.f;
+  }
+}
+
+// After the scan: dacc[k·dim + slot] += Σ over the spokes' occurrences of ±τ (class y: +,
+// class r: −), LDS-aggregated per block as s3_scatter_kernel; the extra row of blocks adds the
+// dense columns and the statistics (stats[0..3] += loss, rows, mistakes, active spokes).
+__global__ __launch_bounds__(256) void s3mc_scatter_kernel(
+    const int* __restrict__ slotsT, const float* __restrict__ tau, const int* __restrict__ rr,
+    const void* __restrict__ yv, int y8, int nclass, int B, int n_rows, float* __restrict__ dacc,
+    int dim, int dc, int dn, int bias, int K, int KN, const float* __restrict__ ws,
+    const float* __restrict__ wsd, int S_act, float* __restrict__ stats) {
+  if ((int)blockIdx.y == dc) {
+    if (blockIdx.x != 0) return;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < K * KN; i += 256) {
+      const int c = i / KN, j = i - c * KN;
+      if (j >= dn + (bias ? 1 : 0)) continue;
+      float v = 0.f;
+      for (int s = 0; s < S_act; ++s) v += wsd[((size_t)s * K + c) * s3::DS + j];
+      const int key = j < dn ? j : dim - 1;
+      dacc[(size_t)c * dim + key] += v;
+    }
+    if (tid < 3) {
+      float t = 0.f;
+      for (int s = 0; s < S_act; ++s) t += ws[(size_t)s * s3::WS + tid];
+      stats[tid] += t;
+    }
+    if (tid == 3) stats[3] += (float)S_act;
+    return;
+  }
+  __shared__ int hk[s3::SH];
+  __shared__ float hv[s3::SH];
+  const int f = blockIdx.y, tid = threadIdx.x;
+  const int r0 = blockIdx.x * s3::SB, r1 = min(n_rows, r0 + s3::SB);
+  for (int i = tid; i < s3::SH; i += 256) {
+    hk[i] = -1;
+    hv[i] = 0.f;
+  }
+  __syncthreads();
+  const int* col = slotsT + (size_t)f * B;
+  auto add = [&](int key, float val) {
+    uint32_t at = ((uint32_t)key * 0x9E3779B1u) >> (32 - 12);
+    for (int probe = 0; probe < s3::SPROBE; ++probe) {
+      const int prev = atomicCAS(&hk[at], -1, key);
+      if (prev == -1 || prev == key) {
+        atomicAdd(&hv[at], val);
+        return;
+      }
+      at = (at + 1) & (s3::SH - 1);
+    }
+    atomicAdd(&dacc[key], val);
+  };
+  for (int row = r0 + tid; row < r1; row += 256) {
+    const int v = col[row];
+    const float t = tau[row];
+    if (v == -1 || t == 0.f) continue;
+    const int slot = v & 0x7fffffff;
+    const float val = v < 0 ? -t : t;
+    const float yf = load_y(yv, row, y8);
+    const int yc = (yf == yf && yf >= 0.f && yf < (float)nclass) ? (int)yf : -1;
+    if (yc >= 0) add(yc * dim + slot, val);
+    if (rr[row] >= 0) add(rr[row] * dim + slot, -val);
+  }
+  __syncthreads();
+  for (int i = tid; i < s3::SH; i += 256) {
+    const int key = hk[i];
+    if (key != -1) atomicAdd(&dacc[key], hv[i]);
+  }
+}
+
 template <int RULE, int KN, bool RARE>
 static int s3_launch_scan_t(const int* slotsT, const uint32_t* meta, int dc, int dn, const void* y,
                             int B, int R, int S_act, const float* prep, int nchs, int dim, int cap,
@@ -1721,9 +2189,10 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   hipLaunchKernelGGL(s3_flags_kernel, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
                      W.meta, W.lidcount);
   const int nchs = (R + s3::CH - 1) / s3::CH;
-  // a per row: −1/(‖x‖² + kadd) (hinge, ε), 1 (logistic), y (Pegasos)
-  const int affine = rule == kSeqLogistic ? 0 : (rule == kSeqPegasos ? 2 : 1);
-  const float kadd = (affine == 1 && variant == 2) ? 0.5f / C : 0.f;
+  // a per row: −1/(‖x‖² + kadd) (hinge, ε), 1 (logistic), y (Pegasos), 1/(2‖x‖² + kadd)
+  // (MultiClassPA: rule 4)
+  const int affine = rule == kSeqLogistic ? 0 : rule == kSeqPegasos ? 2 : rule == 4 ? 3 : 1;
+  const float kadd = ((affine == 1 || affine == 3) && variant == 2) ? 0.5f / C : 0.f;
   if (rule == kSeqPegasos && shr != 2) return -2;
   if (g_s3_gram_valu) {
     if (s3_kn(dn, bias) == 16)
@@ -1912,4 +2381,67 @@ OMLDM_API int omldm_scan3_debug(int v) {
 
 OMLDM_API int omldm_scan3_stamps(void* buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s3_stamps), &buf, sizeof(buf));
+}
+
+// ------------------------------------------------------------------ MultiClassPA host API
+// The LDS slot table of the multiclass scan (floats) and its global spill (floats per spoke).
+OMLDM_API int omldm_scan3mc_lds_cap(int K) {
+  if (K == 2) return (int)((160 * 1024 - sizeof(S3McSmem<2>)) / sizeof(float)) / 2 * 2;
+  return (int)((160 * 1024 - sizeof(S3McSmem<4>)) / sizeof(float)) / 4 * 4;
+}
+OMLDM_API long long omldm_scan3mc_spill_floats(int R, int dc, int K) {
+  return ((long long)R * dc / 2 + 64) * K;
+}
+
+template <int K, int KN>
+static int s3mc_launch(const S3Ws& W, int dc, int dn, int bias, int B, int R, int S_act,
+                       int nchs, int dim, long long gstride, const S3McArgs& A, hipStream_t st) {
+  const int cap = omldm_scan3mc_lds_cap(K);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&s3mc_scan_kernel<K, KN>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024 - (int)sizeof(S3McSmem<K>));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((s3mc_scan_kernel<K, KN>), dim3(S_act), dim3(s3::NT),
+                     (size_t)cap * sizeof(float), st, W.slotsT, W.meta, W.lidcount, dc, dn, bias,
+                     B, R, W.prep, nchs, dim, cap, gstride, A);
+  return (int)hipGetLastError();
+}
+
+// One MultiClassPA round of S spokes on a prep made by omldm_scan3_prepare with rule 4:
+// dacc [K][dim] += Σ_s Δ_s, stats[0..3] += (loss, rows, mistakes, active spokes). Wt: the
+// key-major fp32 prototypes [dim][kp]; ptrs: the prep's 8 workspace pointers (slots, meta,
+// table counts, prep used); ws [S·8], wsd [S·K·32], aglob [S·omldm_scan3mc_spill_floats],
+// tau [B], rr [B] scratch. K ∈ {2, 4} (nclass ≤ K).
+OMLDM_API int omldm_scan3mc_run(const float* Wt, int kp, int K, int nclass, int dn, int dc,
+                                const void* y, int y8, int B, int R, int S, float* dacc, int dim,
+                                float* stats, int variant, float C, int bias, void* const* ptrs,
+                                float* ws, float* wsd, float* aglob, float* tau, int* rr,
+                                void* stream) {
+  if (S <= 0 || B <= 0) return 0;
+  if ((K != 2 && K != 4) || nclass < 2 || nclass > K || kp < K) return -2;
+  if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
+  hipStream_t st = (hipStream_t)stream;
+  const S3Ws W = s3_ws(ptrs);
+  const int S_act = s3_sact(B, R, S);
+  const int nchs = (R + s3::CH - 1) / s3::CH;
+  const long long gstride = (long long)R * dc / 2 + 64;
+  const S3McArgs A{Wt, kp, nclass, variant, variant == 1 ? C : INFINITY, ws, wsd, aglob, tau, rr};
+  const bool k16 = s3_kn(dn, bias) == 16;
+  int e;
+  if (K == 2)
+    e = k16 ? s3mc_launch<2, 16>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st)
+            : s3mc_launch<2, 32>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st);
+  else
+    e = k16 ? s3mc_launch<4, 16>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st)
+            : s3mc_launch<4, 32>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st);
+  if (e) return e;
+  const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
+  const int nblk = (n_rows + s3::SB - 1) / s3::SB;
+  hipLaunchKernelGGL(s3mc_scatter_kernel, dim3(nblk > 0 ? nblk : 1, dc + 1), dim3(256), 0, st,
+                     W.slotsT, tau, rr, y, y8, nclass, B, n_rows, dacc, dim, dc, dn, bias, K,
+                     s3_kn(dn, bias), ws, wsd, S_act, stats);
+  return (int)hipGetLastError();
 }

@@ -232,7 +232,9 @@ class KMeans(Learner):
 # ---------------------------------------------------------------------- MultiClassPA
 class MultiClassPA(Learner):
     """K-prototype Passive-Aggressive classifier on hashed features (labels 0..K-1);
-    virtual spokes per round (csrc/kernels/multiclass_spoke.hip)."""
+    virtual spokes per round: on a GPU with the field-aware wire and K ≤ 4 the v3 table scan
+    (csrc/kernels/linear_scan3.hip: s3mc_scan_kernel), else the spoke tables
+    (csrc/kernels/multiclass_spoke.hip)."""
 
     NAME = "MultiClassPA"
     TASK = "classification"
@@ -275,9 +277,14 @@ class MultiClassPA(Learner):
             return
         S = max(1, ctx.spokes)
         R = max(1, -(-batch.B // S))
-        D.multiclass_round(self.W, batch, R, S, self.K, self.variant, self.C, self.bias,
-                           self.dacc, self.st, log2cap=hp_int(self.hyper, "tableLog2", 0),
-                           Wt=self.Wt)
+        if D.multiclass_scan3_fits(batch, R, self.K, self.bias, self.Wt):
+            # exact sequential spokes on the v3 table scan (K ≤ 4, field-aware wire)
+            D.multiclass_scan3_round(self.Wt, batch, R, S, self.K, self.variant, self.C,
+                                     self.bias, self.dacc, self.st)
+        else:  # the spoke-table round (LDS delta tables spilling to HBM)
+            D.multiclass_round(self.W, batch, R, S, self.K, self.variant, self.C, self.bias,
+                               self.dacc, self.st, log2cap=hp_int(self.hyper, "tableLog2", 0),
+                               Wt=self.Wt)
         # every spoke with rows is active: ceil(B / R) of them, known on the host
         D.multiclass_apply(self.W, self.dacc, _host_scalar(self, -(-batch.B // R)), self.Wt,
                            st=self.st, cum=self.cum, fold=1)

@@ -345,6 +345,60 @@ def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int], act: int = 
     return mlp_forward_reference(w, x, widths, act)
 
 
+def multiclass_scan3_fits(batch, R: int, nclass: int, bias: bool, Wt) -> bool:
+    """The MultiClassPA round on the v3 table scan (csrc/kernels/linear_scan3.hip,
+    s3mc_scan_kernel) takes this batch: the engine's field-aware wire on a GPU, K ≤ 4 classes,
+    fp32 key-major prototypes, a shape the v3 prep takes."""
+    from omldm_amd.ops import linear as L
+
+    return (Wt is not None and Wt.is_cuda and Wt.dtype == torch.float32 and nclass <= 4
+            and getattr(batch, "cat_span", 0) > 0 and batch.B > 0 and 0 < batch.dc
+            and L.SEQ_KERNEL == "scan3" and batch.y.is_cuda
+            and batch.dn + batch.dc * batch.cat_span <= int(Wt.shape[0]) - 1
+            and L.scan3_fits(batch.dn, batch.dc, R, bias))
+
+
+def multiclass_scan3_round(Wt: torch.Tensor, batch, R: int, S: int, nclass: int, variant: int,
+                           C: float, bias: bool, dacc: torch.Tensor, stats: torch.Tensor) -> None:
+    """S exact sequential MultiClassPA spokes of R rows on the v3 table scan: the binary
+    scan's prep (slots, occurrence flags, chunk Grams; a_t = 1/(2‖x‖² + kadd)), one 12-wave
+    workgroup per spoke carrying the K scores of each row through the chunk recurrence, then
+    one scatter of the rows' ±τ into dacc [K, dim]. stats[0..3] += (loss, rows, mistakes,
+    active spokes), like ``multiclass_round``."""
+    from omldm_amd.api.batch import RawBatch
+    from omldm_amd.ops import linear as L
+    from omldm_amd.ops.linear import _workspace
+
+    dim, kp = int(Wt.shape[0]), int(Wt.shape[1])
+    K = 2 if nclass <= 2 else 4
+    num = batch.num.float().contiguous()
+    y = batch.y.float().contiguous() if batch.y.dtype != torch.int8 else batch.y.contiguous()
+    rb = RawBatch(num, batch.cat.contiguous(), y, span=batch.cat_span, cbase=batch.dn)
+    rule = L.LinearRule(rule=L.RULE_MULTI, variant=variant, C=C, bias=bias)
+    key = L._s3_key(rb, R, S, dim, bias, rule)
+    sp = getattr(batch, "prep", None)
+    if not (isinstance(sp, L.Scan3Prep) and sp.key == key):
+        sp = L.linear_scan3_prepare(rb, R, S, dim, bias, rule, hashed=True,
+                                    slot=L._s3_slot_for(key, Wt.device))
+        batch.prep = sp
+    elif sp.event is not None:
+        torch.cuda.current_stream(Wt.device).wait_event(sp.event)
+    L.SCAN3_ROUNDS += 1
+    h = native.hip()
+    dev = Wt.device
+    ws = _workspace(dev, S * 8, key="mc3_ws")
+    wsd = _workspace(dev, S * K * 32, key="mc3_wsd")
+    ag = _workspace(dev, S * int(h.omldm_scan3mc_spill_floats(R, batch.dc, K)), key="mc3_ag")
+    tau = _workspace(dev, batch.B, key="mc3_tau")
+    rr = _workspace(dev, batch.B, key="mc3_rr")  # int32 view of an fp32 scratch
+    check(h.omldm_scan3mc_run(ptr(Wt), kp, K, nclass, batch.dn, batch.dc, ptr(y),
+                              int(y.dtype == torch.int8), batch.B, R, S, ptr(dacc), dim, ptr(stats),
+                              int(variant), float(C), int(bias), sp.ptrs, ptr(ws), ptr(wsd),
+                              ptr(ag), ptr(tau), ptr(rr), native.stream_of(Wt)),
+          "omldm_scan3mc_run")
+    L._s3_mark_read(sp)
+
+
 def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor,
                      Wt: torch.Tensor | None = None, st: torch.Tensor | None = None,
                      cum: torch.Tensor | None = None, fold: int = 0,

@@ -21,6 +21,7 @@ log = logging.getLogger(__name__)
 STAT_W = 6  # loss_sum, n, mistakes, sq_err, sigma, overflow
 
 RULE_HINGE, RULE_EPS, RULE_LOGISTIC, RULE_PEGASOS = 0, 1, 2, 3
+RULE_MULTI = 4  # the MultiClassPA scan's prep (ops.dense.multiclass_scan3_round)
 PA, PA1, PA2 = 0, 1, 2
 
 
@@ -365,7 +366,7 @@ def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
     through PA-II's 1/(2C)) — pipelines that differ in C share one prep."""
     c = float(rule.C) if rule.variant == PA2 else None
     # the row scaling depends on the rule family (a = −1/(‖x‖²+kadd), 1 or y) and the shrink
-    fam = 2 if rule.rule == RULE_PEGASOS else int(rule.rule == RULE_LOGISTIC)
+    fam = {RULE_PEGASOS: 2, RULE_LOGISTIC: 1, RULE_MULTI: 3}.get(rule.rule, 0)
     return (batch.B, R, S, dim, bool(bias), fam, rule.variant == PA2, c, _s3_shrink(rule),
             batch.dn, batch.dc, int(batch.span), batch.y.data_ptr(), batch.tok.data_ptr(), S3_MODE)
 

@@ -74,6 +74,10 @@ HIP_SIGS = [
                                     i32, i32, i32, i32, i32, i32, i32, i32, i64, i32, i32, vp, vp,
                                     vp]),
     ("omldm_scan3_max_pipes", i32, []),
+    ("omldm_scan3mc_lds_cap", i32, [i32]),
+    ("omldm_scan3mc_spill_floats", i64, [i32, i32, i32]),
+    ("omldm_scan3mc_run", i32, [vp, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, vp, i32, vp,
+                                i32, f32, i32, vp, vp, vp, vp, vp, vp, vp]),
     ("omldm_scan3_set_comb", None, [i32]),
     ("omldm_scan3_set_form", None, [i32]),
     ("omldm_scan3_set_cns", None, [i32]),
