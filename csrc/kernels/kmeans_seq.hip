@@ -123,12 +123,121 @@ __global__ __launch_bounds__(64) void kmeans_seq_kernel(const float* __restrict_
   }
 }
 
+// Larger models (k ≤ 1024 centroids, d ≤ 256 coordinates): one workgroup of NW waves,
+// thread j owning centroid j, the centroids in LDS (row stride d + 1: the lanes' rows fall
+// in different banks), each 64-point chunk staged in LDS. Per point: every thread's distance
+// (the point's coordinates are LDS broadcasts), a DPP argmin per wave, the waves' minima
+// through LDS (ties to the lowest index), the owner's update, two barriers — the same
+// per-point order as the one-wave kernel, exact at any size that fits the LDS.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void kmeans_seq_wg_kernel(const float* __restrict__ x,
+                                                                int ldx,
+                                                                const float* __restrict__ y,
+                                                                int B, int d, int k,
+                                                                float* __restrict__ cent,
+                                                                float* __restrict__ cnt,
+                                                                double* __restrict__ cum) {
+  extern __shared__ float smem[];
+  const int ds = d + 1;
+  float* C = smem;                        // [k][ds]
+  float* xs = C + (size_t)k * ds;         // [64][d] the chunk's points
+  float* ysh = xs + 64 * d;               // [64]
+  float* rmin = ysh + 64;                 // [NW]
+  int* ridx = reinterpret_cast<int*>(rmin + NW);  // [NW]
+  int* sseed = ridx + NW;                 // [1]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool mine = tid < k;
+  for (int i = tid; i < k * d; i += NW * 64) C[(i / d) * ds + i % d] = cent[i];
+  float n = mine ? cnt[tid] : 0.f;
+  if (tid == 0) *sseed = 0;
+  __syncthreads();
+  if (mine && n > 0.f) atomicAdd(sseed, 1);  // seeded centroids form a prefix
+  __syncthreads();
+  int seeded = *sseed;
+  double inertia = 0.0, fitted = 0.0;
+  for (int r0 = 0; r0 < B; r0 += 64) {
+    __syncthreads();  // the previous chunk's points are consumed
+    for (int i = tid; i < 64 * d; i += NW * 64) {
+      const int r = r0 + i / d;
+      xs[i] = r < B ? x[(size_t)r * ldx + i % d] : 0.f;
+    }
+    if (tid < 64) ysh[tid] = r0 + tid < B ? (y ? y[r0 + tid] : 0.f) : __builtin_nanf("");
+    __syncthreads();
+    const int np = B - r0 < 64 ? B - r0 : 64;
+    for (int p = 0; p < np; ++p) {
+      if (ysh[p] != ysh[p]) continue;  // not a training point (block-uniform)
+      const float* xp = xs + p * d;
+      fitted += 1.0;
+      if (seeded < k) {  // block-uniform: the point becomes the next centroid
+        if (tid == seeded) {
+          for (int i = 0; i < d; ++i) C[tid * ds + i] = xp[i];
+          n = 1.f;
+        }
+        ++seeded;
+        __syncthreads();
+        continue;
+      }
+      float dist = __builtin_inff();
+      if (mine) {
+        float dp[4] = {0.f, 0.f, 0.f, 0.f};
+        const float* cr = C + tid * ds;
+        for (int i = 0; i < d; ++i) {
+          const float t = xp[i] - cr[i];
+          dp[i & 3] = fmaf(t, t, dp[i & 3]);
+        }
+        dist = (dp[0] + dp[1]) + (dp[2] + dp[3]);
+      }
+      float wmin;
+      const int wj = wave_argmin(dist, wmin);
+      if (lane == 0) {
+        rmin[wave] = wmin;
+        ridx[wave] = wave * 64 + wj;
+      }
+      __syncthreads();
+      float best = rmin[0];
+      int j = ridx[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w)
+        if (rmin[w] < best) {  // strictly: ties keep the lower wave (lower index)
+          best = rmin[w];
+          j = ridx[w];
+        }
+      if (tid == 0) inertia += (double)best;
+      if (tid == j) {
+        n += 1.f;
+        const float a = 1.f / n;
+        float* cr = C + tid * ds;
+        for (int i = 0; i < d; ++i) cr[i] = fmaf(a, xp[i] - cr[i], cr[i]);
+      }
+      __syncthreads();  // the update is visible to the next point's distances
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < k * d; i += NW * 64) cent[i] = C[(i / d) * ds + i % d];
+  if (mine) cnt[tid] = n;
+  if (tid == 0 && cum) {
+    cum[0] += inertia;
+    cum[1] += fitted;
+  }
+}
+
+size_t kmeans_wg_lds(int d, int k, int nw) {
+  return ((size_t)k * (d + 1) + 64 * d + 64 + 2 * nw + 1) * sizeof(float);
+}
+
 }  // namespace
 }  // namespace omldm
 
 using namespace omldm;
 
-OMLDM_API int omldm_kmeans_seq_fits(int d, int k) { return d >= 1 && d <= 64 && k >= 1 && k <= 64; }
+static bool kmeans_one_wave(int d, int k) { return d >= 1 && d <= 64 && k >= 1 && k <= 64; }
+
+OMLDM_API int omldm_kmeans_seq_fits(int d, int k) {
+  if (kmeans_one_wave(d, k)) return 1;
+  const int nw = (k + 63) / 64;
+  return d >= 1 && d <= 256 && k >= 1 && k <= 1024 &&
+         kmeans_wg_lds(d, k, nw <= 4 ? 4 : 16) <= 160 * 1024;
+}
 
 // x [B, ldx] fp32 (first d columns used), y [B] (NaN: not a training point; nullptr: all
 // train), cent [k, d], cnt [k], cum (cum[0] += Σ squared distance to the chosen
@@ -138,6 +247,22 @@ OMLDM_API int omldm_kmeans_seq(const float* x, int ldx, const float* y, int B, i
   if (!omldm_kmeans_seq_fits(d, k) || ldx < d) return -1;
   if (B <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (!kmeans_one_wave(d, k)) {  // the workgroup form
+    const int nw = (k + 63) / 64 <= 4 ? 4 : 16;
+    const size_t lds = kmeans_wg_lds(d, k, nw);
+    if (nw == 4) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_seq_wg_kernel<4>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipLaunchKernelGGL(kmeans_seq_wg_kernel<4>, dim3(1), dim3(256), lds, st, x, ldx, y, B, d,
+                         k, cent, cnt, cum);
+    } else {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_seq_wg_kernel<16>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipLaunchKernelGGL(kmeans_seq_wg_kernel<16>, dim3(1), dim3(1024), lds, st, x, ldx, y, B,
+                         d, k, cent, cnt, cum);
+    }
+    return (int)hipGetLastError();
+  }
   if (d <= 16)
     hipLaunchKernelGGL(kmeans_seq_kernel<16>, dim3(1), dim3(64), 0, st, x, ldx, y, B, d, k, cent,
                        cnt, cum);

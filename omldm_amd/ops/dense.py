@@ -185,7 +185,12 @@ def kmeans_seq(x: torch.Tensor, y: torch.Tensor | None, cent: torch.Tensor, n: t
 
 
 def kmeans_seq_fits(d: int, k: int) -> bool:
-    return 1 <= d <= 64 and 1 <= k <= 64
+    """The exact sequential kernel takes (d, k): one wavefront for k, d ≤ 64; a workgroup
+    with the centroids in LDS up to k ≤ 1024, d ≤ 256 (k·(d + 1) floats in 160 KiB)."""
+    if 1 <= d <= 64 and 1 <= k <= 64:
+        return True
+    nw = 4 if -(-k // 64) <= 4 else 16  # (kmeans_seq.hip: kmeans_wg_lds)
+    return 1 <= d <= 256 and 1 <= k <= 1024 and (k * (d + 1) + 64 * d + 64 + 2 * nw + 1) * 4 <= 160 << 10
 
 
 def kmeans_apply(cent: torch.Tensor, n: torch.Tensor, sums: torch.Tensor, counts: torch.Tensor,

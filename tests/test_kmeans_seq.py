@@ -83,8 +83,11 @@ def test_learner_default_is_sequential_and_minibatch_gap_is_pinned():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,k", [(3, 4), (13, 8), (20, 33), (64, 64)])
+@pytest.mark.parametrize("d,k", [(3, 4), (13, 8), (20, 33), (64, 64), (100, 20), (13, 200),
+                                 (128, 200)])
 def test_gpu_kernel_equals_cpu_oracle(d, k):
+    """The one-wave kernel (k, d ≤ 64) and the workgroup kernel (centroids in LDS, up to
+    k = 1024, d = 256) against the CPU MacQueen oracle."""
     x, y = _blobs(20000, d, k, seed=7 * d + k)
     out = {}
     for dev in ("cpu", "cuda"):
