@@ -592,9 +592,27 @@ __global__ __launch_bounds__(256) void ht_predict_kernel(
   out[row] = (float)best;
 }
 
+// The leaf of every row (exact per-point checks: models/dense.py HT._fit_exact).
+__global__ __launch_bounds__(256) void ht_route_kernel(
+    const float* __restrict__ x, int B, int d, int depth, const float* __restrict__ feat,
+    const float* __restrict__ thr, const float* __restrict__ left, const float* __restrict__ right,
+    int* __restrict__ out) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= B) return;
+  out[row] = ht_route(x + (size_t)row * d, feat, thr, left, right, depth);
+}
+
 }  // namespace omldm
 
 using namespace omldm;
+
+OMLDM_API int omldm_ht_route(const float* x, int B, int d, int depth, float* const* tree, int* out,
+                             void* stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(ht_route_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, x,
+                     B, d, depth, tree[0], tree[1], tree[2], tree[3], out);
+  return (int)hipGetLastError();
+}
 
 // tree: pointers in the order feat, thr, left, right, cc, S0, S1, S2, lo, hi, since, nnodes.
 // N: node capacity. ws: int scratch of omldm_ht_update_ws_ints(B, N, C) (0 → the wave-

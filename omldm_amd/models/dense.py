@@ -499,11 +499,11 @@ class HT(Learner):
         self.grace = hp_int(self.hyper, "gracePeriod", 200)
         self.delta = hp_float(self.hyper, "delta", 1e-7)
         self.tau = hp_float(self.hyper, "tau", 0.05)
-        # due leaves are checked every `checkEvery` rows of a tick, not once per tick: the
-        # reference checks a leaf the moment it reaches the grace period, so a tree grows
-        # by many levels within one 65,536-row tick (tests/test_ht_sequential.py pins the
-        # gap to the per-point VFDT: none at 1,024, 0.93 → 0.56 accuracy at whole ticks)
-        self.check_every = max(1, hp_int(self.hyper, "checkEvery", 1024))
+        # checkEvery 0 (default): a leaf is checked at the very point it reaches the grace
+        # period, as the reference's per-point VFDT (the tick is cut into segments ending at
+        # each due point: _fit_exact). checkEvery N > 0: due leaves are checked every N rows
+        # (faster; tests/test_ht_sequential.py pins its gap to the per-point form)
+        self.check_every = max(0, hp_int(self.hyper, "checkEvery", 0))
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -553,11 +553,83 @@ class HT(Learner):
 
     def fit(self, batch, ctx):
         B, step = batch.B, self.check_every
+        if step <= 0:
+            return self._fit_exact(batch)
         if B > step:
             for a in range(0, B, step):
                 self._fit_part(batch.slice(a, min(B, a + step)))
             return
         self._fit_part(batch)
+
+    def _fit_exact(self, batch):
+        """Per-point VFDT checks on the device: rows are routed once, and the tick is cut
+        into segments that end exactly at the next row where some leaf reaches its grace
+        period (rows of each leaf in stream order: the (grace − since)-th training row of
+        the leaf). Each segment's statistics are added in one launch, then the due leaf is
+        checked; rows after a split are routed again."""
+        import numpy as np
+
+        B = batch.B
+        if B == 0:
+            return
+        gpu = self.device.type == "cuda"
+        x = batch.num.float().contiguous()
+        ok = (~torch.isnan(batch.y)).cpu().numpy()
+        N, g = self.N, float(self.grace)
+
+        def route(xs):
+            if gpu:
+                return D.ht_route(xs, self.depth, self._tree()).cpu().numpy().astype(np.int64)
+            return self._route(xs).cpu().numpy().astype(np.int64)
+
+        def update(lo, hi, check):  # rows [lo, hi): statistics, then the due leaves' checks
+            if not gpu:  # (the CPU path checks inside _fit_part)
+                self._fit_part(batch.slice(lo, hi))
+                return
+            D.ht_update(x[lo:hi], batch.y[lo:hi], self.Cn, self.depth, self._tree(),
+                        self.cum[1:2], N=self.N)
+            if check:
+                D.ht_split(self.N, self.d, self.Cn, self.nb, g, self.delta, self.tau,
+                           self._tree())
+
+        a = 0
+        while a < B:
+            leaf = route(x[a:])
+            since = self.since.cpu().numpy().astype(np.float64)
+            isleaf = (self.feat.cpu().numpy() < 0)
+            nodes0 = int(self.nnodes.item())
+            rel = np.flatnonzero(ok[a:])                  # training rows, relative to a
+            lv = leaf[rel]
+            order = np.lexsort((rel, lv))                  # by leaf, then stream position
+            lv_s, pos_s = lv[order], rel[order]
+            cnt = np.bincount(lv_s, minlength=N)[:N]
+            start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+            keys = lv_s * (B + 1) + pos_s
+            done = np.zeros(N, dtype=np.int64)             # rows of each leaf consumed
+            e = 0                                          # rows [a, a + e) processed
+            split = False
+            while e < B - a:
+                need = np.maximum(1, np.ceil(g - since)).astype(np.int64)
+                idx = start + done + need - 1
+                due = (done + need <= cnt) & isleaf
+                if not due.any():
+                    break
+                first = int(pos_s[idx[due]].min())         # the earliest due row
+                end = first + 1
+                update(a + e, a + end, True)
+                newdone = np.searchsorted(keys, np.arange(N) * (B + 1) + end) - start
+                since += newdone - done
+                done = newdone
+                since[since >= g] = 0.0                    # the checked leaf (ht_split)
+                e = end
+                if int(self.nnodes.item()) != nodes0:      # a split: route the rest again
+                    split = True
+                    break
+            if not split:
+                if e < B - a:  # no leaf reaches its grace period in the rest of the tick
+                    update(a + e, B, False)
+                return
+            a += e
 
     def _fit_part(self, batch):
         if self.device.type == "cuda":

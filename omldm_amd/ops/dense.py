@@ -479,6 +479,17 @@ def ht_split(N: int, d: int, C: int, nb: int, grace: float, delta: float, tau: f
                                       native.stream_of(tree[0])), "omldm_ht_split")
 
 
+def ht_route(x: torch.Tensor, depth: int, tree: list[torch.Tensor]) -> torch.Tensor:
+    """The leaf node of every row (int32, device)."""
+    B, d = x.shape
+    out = torch.empty(B, dtype=torch.int32, device=x.device)
+    if B:
+        x = x.float().contiguous()
+        check(native.hip().omldm_ht_route(ptr(x), B, d, depth, _tree_ptrs(tree), ptr(out),
+                                          native.stream_of(x)), "omldm_ht_route")
+    return out
+
+
 def ht_predict(x: torch.Tensor, C: int, depth: int, tree: list[torch.Tensor]) -> torch.Tensor:
     B, d = x.shape
     out = torch.empty(B, dtype=torch.float32, device=x.device)

@@ -14,6 +14,7 @@ that needs several levels (checking only at tick ends: 0.93 → 0.56 accuracy).
 import math
 
 import numpy as np
+import pytest
 import torch
 
 from omldm_amd.api.batch import FeatureSpace, HashedBatch
@@ -145,3 +146,54 @@ def test_tick_level_tree_matches_the_per_point_tree_within_two_points():
         # the gap: splits made at tick ends instead of mid-tick
         assert acc >= acc_oracle - 0.02, (tick, acc, acc_oracle, res)
         assert nodes >= 3, res
+
+
+def _fit_ticks(ht, X, y, tick):
+    for a in range(0, X.shape[0], tick):
+        b = HashedBatch(torch.from_numpy(X[a:a + tick]).to(ht.device),
+                        torch.zeros((min(tick, X.shape[0] - a), 0), dtype=torch.int32,
+                                    device=ht.device),
+                        torch.from_numpy(y[a:a + tick]).to(ht.device))
+        ht.fit(b, RoundContext())
+
+
+def _acc(ht, Xt, yt):
+    b = HashedBatch(torch.from_numpy(Xt).to(ht.device),
+                    torch.zeros((len(Xt), 0), dtype=torch.int32, device=ht.device),
+                    torch.from_numpy(yt).to(ht.device))
+    return float((ht.predict(b).cpu().numpy() == yt).mean())
+
+
+def test_exact_mode_checks_at_the_grace_point_like_the_per_point_tree():
+    """checkEvery 0 (the default): the tick is cut at every point where a leaf reaches its
+    grace period, so the tree grows as the per-point VFDT does — the same number of nodes
+    and the same first split, at 65,536-row ticks."""
+    X, y = _stream(60000, seed=1)
+    Xt, yt = _stream(8000, seed=2)
+    ora = VFDT(6, 2)
+    for i in range(X.shape[0]):
+        ora.learn(X[i].astype(np.float64), y[i])
+    ht = HT({"nClasses": 2}, FeatureSpace(6, 0, 0, 1 << 8), "cpu")
+    assert ht.check_every == 0
+    _fit_ticks(ht, X, y, 65536)
+    assert abs(int(ht.nnodes.item()) - ora.nnodes) <= 2, (int(ht.nnodes.item()), ora.nnodes)
+    assert int(ht.feat[0]) == int(ora.feat[0])
+    acc_oracle = float((ora.predict(Xt.astype(np.float64)) == yt).mean())
+    assert _acc(ht, Xt, yt) >= acc_oracle - 0.005
+
+
+@pytest.mark.gpu
+def test_gpu_exact_mode_matches_the_cpu_exact_mode():
+    """The device path of the exact mode (ht_route + segments ending at each due point,
+    csrc/kernels/hoeffding.hip) grows the tree the CPU exact mode grows."""
+    X, y = _stream(60000, seed=3)
+    Xt, yt = _stream(8000, seed=4)
+    sp = FeatureSpace(6, 0, 0, 1 << 8)
+    res = {}
+    for dev in ("cpu", "cuda"):
+        ht = HT({"nClasses": 2}, sp, dev)
+        _fit_ticks(ht, X, y, 65536)
+        res[dev] = (int(ht.nnodes.item()), int(ht.feat[0]), _acc(ht, Xt, yt))
+    assert res["cuda"][1] == res["cpu"][1], res
+    assert abs(res["cuda"][0] - res["cpu"][0]) <= 2, res
+    assert abs(res["cuda"][2] - res["cpu"][2]) <= 0.005, res
