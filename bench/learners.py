@@ -62,7 +62,9 @@ P16_CASES = [
     ("ORR", 1, {}, 16),
     ("K-means", 0, {"k": 16}, 16),
     ("NN", 0, {"hiddenLayers": [64, 64]}, 16),
-    ("HT", 2, {"nClasses": 4}, 16),
+    ("HT", 2, {"nClasses": 4}, 16),                     # per-point split checks (default)
+    ("HT@check1024", 2, {"nClasses": 4, "checkEvery": 1024}, 16),
+    ("K-means@k256d32", 0, {"k": 256}, 16),            # the workgroup form (k > 64)
 ]
 
 
