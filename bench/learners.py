@@ -64,7 +64,7 @@ P16_CASES = [
     ("NN", 0, {"hiddenLayers": [64, 64]}, 16),
     ("HT", 2, {"nClasses": 4}, 16),                     # per-point split checks (default)
     ("HT@check1024", 2, {"nClasses": 4, "checkEvery": 1024}, 16),
-    ("K-means@k256d32", 0, {"k": 256}, 16),            # the workgroup form (k > 64)
+    ("K-means@k256", 0, {"k": 256}, 16),               # the workgroup form (k > 64)
 ]
 
 
