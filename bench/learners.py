@@ -110,6 +110,13 @@ def main(argv=None) -> int:
             torch.cuda.synchronize()
         from omldm_amd.ops import linear as OL
 
+        if dev.type == "cuda":  # out of the idle clocks the host-side setup left behind
+            xs = torch.randn(2048, 2048, device=dev)
+            t_end = time.perf_counter() + 0.3
+            while time.perf_counter() < t_end:
+                xs = torch.tanh(xs @ xs)
+                torch.cuda.synchronize()
+            del xs
         v3_before = OL.SCAN3_ROUNDS
         t = time.perf_counter()
         for k in range(a.steps):

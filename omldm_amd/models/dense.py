@@ -602,7 +602,8 @@ class HT(Learner):
             nodes0 = int(self.nnodes.item())
             rel = np.flatnonzero(ok[a:])                  # training rows, relative to a
             lv = leaf[rel]
-            order = np.lexsort((rel, lv))                  # by leaf, then stream position
+            # by leaf, then stream position (rel ascends: a stable radix sort on the leaf)
+            order = np.argsort(lv.astype(np.uint8 if N <= 256 else np.uint16), kind="stable")
             lv_s, pos_s = lv[order], rel[order]
             cnt = np.bincount(lv_s, minlength=N)[:N]
             start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
