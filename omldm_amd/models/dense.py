@@ -586,10 +586,10 @@ class HT(Learner):
             if not gpu:  # (the CPU path checks inside _fit_part)
                 self._fit_part(batch.slice(lo, hi))
                 return
-            # (short segments: the one-launch atomic form; the sorted reducer pays off on
-            # long ones)
+            # (the sorted reducer even for short segments: the atomic form serialises on the
+            # few leaves a segment's rows share — 5x slower per check, profiles/round5)
             D.ht_update(x[lo:hi], batch.y[lo:hi], self.Cn, self.depth, self._tree(),
-                        self.cum[1:2], N=self.N, sort=hi - lo > 4096)
+                        self.cum[1:2], N=self.N)
             if check:
                 D.ht_split(self.N, self.d, self.Cn, self.nb, g, self.delta, self.tau,
                            self._tree())
