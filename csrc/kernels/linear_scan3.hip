@@ -598,6 +598,7 @@ __device__ unsigned long long* g_s3_stamps;
 __device__ int g_s3_debug;  // diagnostics: 1 = every gather reads w[0] (latency experiment)
 __device__ int g_s3_comb_err;  // a combiner gave up waiting for its spoke (bounded spin)
 __device__ int g_s3_dense_order = 0;  // helpers' dense column ownership (see s3_scan_kernel)
+__device__ int g_s3_hprio = 0;         // helpers' issue priorities by age (A/B: see s3_scan_body)
 
 // The in-launch combine (Guideline 16, R2 "the data is the flag"): the scanner stores row
 // t's c as one 8-B granule {epoch << 32 | bits(c)} with a relaxed agent-scope atomic store
@@ -1051,6 +1052,15 @@ __device__ __forceinline__ void s3_scan_body(
   // helper q owns categorical fields f ≡ q and dense columns j ≡ q (mod NHA); lane r = row
   const int q = wave - 1, r = lane;
   const int swave = g_s3_debug >= 16 ? g_s3_debug - 16 : 1;  // the stamped helper wave
+  // A/B (off): issue priority by age on each SIMD. With equal priorities the oldest wave
+  // issues first and the youngest helpers (waves 8-11) set the chunk period; lifting them
+  // moves the starvation to the oldest (profiles/round5/probe_helpers_prio.txt: 0.263-0.266
+  // vs 0.270-0.274 ms) — the helpers share the SIMDs' issue slots, so only fewer helper
+  // instructions shorten the period
+  if (g_s3_hprio) {
+    if (q >= 7) __builtin_amdgcn_s_setprio(2);
+    else if (q >= 3) __builtin_amdgcn_s_setprio(1);
+  }
   // dense column ownership: j ≡ q (mod NHA) (order 0), or in the reverse order of the
   // fields (order 1: the helpers that own a third categorical field do not also own a
   // second dense column)
@@ -2369,6 +2379,10 @@ OMLDM_API int omldm_scan3_part_bounds(int dim, int dn, int dc, long long span_in
   lohi[0] = part == 0 ? 0 : (long long)dim + 2;
   lohi[1] = (long long)dim + 2;
   return 0;
+}
+
+OMLDM_API int omldm_scan3_hprio(int v) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s3_hprio), &v, sizeof(v));
 }
 
 OMLDM_API int omldm_scan3_dense_order(int v) {

@@ -86,6 +86,20 @@ for wv in range(1, 12):
     per[wv] = {names[k]: round(float(m[k]) / nch) for k in range(2, 8)}
 lib.omldm_scan3_debug(0)
 print(json.dumps({"helper_waves": per}), flush=True)
+if os.environ.get("PROBE_HPRIO"):
+    lib.omldm_scan3_hprio.argtypes = [ctypes.c_int]
+    for v in (0, 1, 0, 1):
+        lib.omldm_scan3_hprio(v)
+        torch.cuda.synchronize()
+        ev[0].record()
+        for _ in range(n):
+            L.linear_seq_round(w, b, R, S, dacc, rule, 1.0 / S, cum=cum)
+            L.linear_apply(w, None, dacc)
+        ev[1].record()
+        torch.cuda.synchronize()
+        print(json.dumps({"hprio": v, "run_ms": round(ev[0].elapsed_time(ev[1]) / n, 4)}),
+              flush=True)
+    lib.omldm_scan3_hprio(0)
 if os.environ.get("PROBE_DENSE_ORDERS"):
     lib.omldm_scan3_dense_order.argtypes = [ctypes.c_int]
     for order in (0, 1):
