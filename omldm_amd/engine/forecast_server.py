@@ -289,8 +289,11 @@ class ForecastServer:
             self._cat32[: sp.dc] = self._cat.numpy()[0]
         return int(self._op[0]) == OP_FORECASTING
 
-    def _predict_direct(self, pipe) -> float:
-        """One-row predict of a pipeline the wave does not score, on the lane's stream."""
+    def _predict_direct(self, pipes: list) -> list:
+        """One-row predicts of the pipelines the wave does not score, on the lane's stream:
+        the record moves to the device once, every pipeline's predict is enqueued, and one
+        copy brings all the answers back (one stream synchronisation per record, not one per
+        pipeline)."""
         from omldm_amd.api.batch import HashedBatch
 
         dev = self.job.device
@@ -298,12 +301,14 @@ class ForecastServer:
         if not self._trained.wait(60.0):
             raise RuntimeError("forecast lane: the tick's training did not end within 60 s")
         if self._stream is None:
-            return float(pipe.predict(b.to(dev))[0])
+            bd = b.to(dev)
+            return [float(pipe.predict(bd)[0]) for pipe in pipes]
         with torch.cuda.stream(self._stream):
             if self._train_ev is not None:
                 self._stream.wait_event(self._train_ev)  # the model between two rounds
-            out = pipe.predict(b.to(dev, non_blocking=False))
-            return float(out.float()[0].item())
+            bd = b.to(dev, non_blocking=False)
+            outs = [pipe.predict(bd).float().reshape(-1)[:1] for pipe in pipes]
+            return torch.cat(outs).cpu().tolist()
 
     def serve_one(self, rec: bytes, t_in: float | None = None) -> bool:
         """Answers one forecasting record for every pipeline (wave + one-row predicts).
@@ -331,10 +336,13 @@ class ForecastServer:
                     preds[pid] = (1.0 if s >= 0 else -1.0) if cls else s
                 t_w = time.perf_counter()
             fam_t: list = []
-            for pid, pipe in self._direct:
+            if self._direct:
                 t0 = time.perf_counter()
-                preds[pid] = self._predict_direct(pipe)
-                fam_t.append((pipe.learner.NAME, time.perf_counter() - t0))
+                vals = self._predict_direct([pipe for _, pipe in self._direct])
+                dt = (time.perf_counter() - t0) / len(self._direct)
+                for (pid, pipe), v in zip(self._direct, vals):
+                    preds[pid] = v
+                    fam_t.append((pipe.learner.NAME, dt))
             raw = RawRecords(np.frombuffer(rec, dtype=np.uint8),
                              np.zeros(1, dtype=np.int64), np.array([len(rec)], dtype=np.int64))
             for pid in self._order:
