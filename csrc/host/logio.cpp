@@ -283,7 +283,11 @@ OMLDM_HOST_API int64_t omldm_fill_regions(int nj, const int64_t* jobs, uint8_t* 
     };
     const int np_all = (int)pcs.size();
     const int nth = nt < np_all ? nt : np_all;
-    {
+    const char* pool_e = std::getenv("OMLDM_READ_POOL");
+    if (pool_e && pool_e[0] == '1') {  // persistent workers (no thread creation per block)
+      const std::function<void(int)> f = piece;
+      read_pool().run(np_all, nth, f);
+    } else {
       std::vector<std::thread> th;
       th.reserve(nth);
       for (int t = 0; t < nth; ++t)
