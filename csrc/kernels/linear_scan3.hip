@@ -83,6 +83,10 @@ constexpr uint32_t F_TG = 1u;              // margin reads the table (else w)
 constexpr uint32_t F_INIT = 2u;            // first occurrence: writes w[slot] into the table
 constexpr uint32_t F_SCAT = 4u;            // the slot recurs ≥ 2 chunks later: add c·sign
 constexpr uint32_t F_SIGN = 8u;
+// a non-table occurrence (its slot's occurrences span < 2 chunks) with the slot itself in
+// the id bits: the in-scan combine adds its c·sign straight to the accumulator
+constexpr uint32_t F_PRES = 16u;
+constexpr uint32_t F_TAB = F_TG | F_INIT | F_SCAT;  // any occurrence of a table slot
 constexpr int LID_SHIFT = 10;
 }  // namespace s3
 
@@ -171,10 +175,13 @@ constexpr int HCAP = 12288;                // hash entries (≤ 8192 distinct sl
 constexpr int RPT = RMAX / FT;             // rows per thread (8)
 }  // namespace s3
 
-// Output: the meta words, [dc][B] uint32 (the slots stay in slotsT).
+// Output: the meta words, [dc][B] uint32 (the slots stay in slotsT). enc: non-table
+// occurrences carry F_PRES and their slot (slots < 2^22); l2s (or null): each table id's slot,
+// [S][gs] (the in-scan combine's flush).
 __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict__ slotsT, int B,
                                                           int R, uint32_t* __restrict__ meta,
-                                                          int* __restrict__ lidcount) {
+                                                          int* __restrict__ lidcount, int enc,
+                                                          int* __restrict__ l2s, long long gs) {
   __shared__ int hkey[s3::HCAP];        // slot, −1 empty; after the inserts: local table id
   __shared__ uint32_t hfirst[s3::HCAP];  // first row (atomic min)
   __shared__ uint32_t hlast[s3::HCAP];   // last row (atomic max)
@@ -257,6 +264,9 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
         if (i == first) m |= s3::F_INIT;
         if ((last >> 6) >= ch + 2) m |= s3::F_SCAT;
         m |= (uint32_t)(base + hkey[h[q]]) << s3::LID_SHIFT;
+        if (l2s && lloc[q] >= 0) l2s[(size_t)s * gs + base + lloc[q]] = v[q] & 0x7fffffff;
+      } else if (enc) {
+        m |= s3::F_PRES | ((uint32_t)(v[q] & 0x7fffffff) << s3::LID_SHIFT);
       }
     }
     meta[(size_t)f * B + t0 + i] = m;
@@ -626,6 +636,13 @@ struct S3Comb {
   const float* sig;  // shrinking rules: σ at each spoke's end (its c's scale), else null
   int wbf;           // the model w is bf16 (modelDtype bf16: margins on the bf16 weights)
   int cns;           // spokes per combiner workgroup (> 1: one part, chunks interleaved)
+  // in-scan combine (no combiner workgroups): the helpers add every table occurrence's
+  // c·sign to the table and the scan workgroup flushes it through l2s ([S][gs]: each table
+  // id's slot) at its end; a non-table occurrence's (F_PRES) goes to dacc from the helpers
+  // (1: no c granules) or from the spoke's w0 workgroup after its pass (2: s3_fold_pres)
+  const int* l2s;
+  long long gs;
+  int inscan;
 };
 
 // workgroups of one pipeline: its w0-margin (RARE) and scan workgroups, then its combiners
@@ -801,6 +818,55 @@ __device__ __forceinline__ void s3_rare(const int* __restrict__ slotsT, int dc, 
   }
 }
 
+// In-scan combine with the w0-margin workgroups (S3Comb::inscan 2): once its w0 pass is
+// done, the spoke's w0 workgroup adds the non-table occurrences' c·sign (F_PRES: slots whose
+// occurrences span < 2 chunks, each a few adds) straight to the accumulator as the scanner's
+// granules arrive — chunks round-robin over its waves, every field of the chunk. (From the
+// helpers, one global atomic of 64 distinct lines per field and chunk took ~700 cycles of
+// the scan workgroup's memory pipeline per chunk.)
+__device__ __forceinline__ void s3_fold_pres(const uint32_t* __restrict__ meta, int dc, int B,
+                                             int R, const S3Comb& cb, int s) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int t0, t1;
+  spoke_rows(s, R, B, t0, t1);
+  const int nch = (t1 - t0 + s3::CH - 1) / s3::CH;
+  const float sc = cb.inv_p * (cb.sig ? cb.sig[s] : 1.f);
+  const unsigned long long want = (unsigned long long)cb.epoch;
+  for (int k = wave; k < nch; k += s3::NH + 1) {
+    const int row = t0 + k * s3::CH + lane;
+    const bool in = row < t1;
+    uint32_t m[s3::MAXF];
+#pragma unroll
+    for (int f = 0; f < s3::MAXF; ++f) {
+      const bool ok = in && f < dc;
+      const uint32_t x = meta[ok ? (size_t)f * B + row : 0];
+      m[f] = ok ? x : 0u;
+    }
+    unsigned long long g = 0;
+    bool ready = false;
+    for (unsigned spins = 0; spins < s3::SPIN_MAX; ++spins) {
+      g = in ? __hip_atomic_load((s3_gu64*)(cb.gran + row), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT)
+             : (want << 32);
+      if (__builtin_amdgcn_ballot_w64((g >> 32) != want) == 0ull) {
+        ready = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ready) {
+      if (lane == 0) atomicExch(&g_s3_comb_err, 1);
+      return;
+    }
+    const float c = __uint_as_float((uint32_t)g) * sc;
+    if (__builtin_amdgcn_ballot_w64(c != 0.f) == 0ull) continue;
+#pragma unroll
+    for (int f = 0; f < s3::MAXF; ++f)
+      if (c != 0.f && (m[f] & s3::F_PRES))
+        atomicAdd(&cb.dacc[m[f] >> s3::LID_SHIFT], (m[f] & s3::F_SIGN) ? -c : c);
+  }
+}
+
 // A combiner workgroup: ns = 1: spoke i mod S_act, part i / S_act of the combiner blocks;
 // ns > 1 (one part): spokes ns·i .. ns·i + ns − 1.
 __device__ __forceinline__ void s3_combine(const int* __restrict__ slotsT, int dc, int B, int R,
@@ -854,6 +920,57 @@ __device__ __forceinline__ void s3_scan_arrive(const S3Comb& cb, const float* __
     s3_dense_body(ws, wsd, cb.sig, cb.S_act, dn, dim, p.bias, p.inv_p, cb.dacc, cb.cum);
 }
 
+// In-scan combine, the scan workgroup's end: its table's deltas into the accumulator, one
+// atomic per table slot (mode 4's table holds deltas; mode 3's the running weights, so the
+// round-start weight is taken off), ids past the LDS from the global spill.
+template <bool RARE>
+__device__ __forceinline__ void s3_inscan_flush(const S3Comb& cb, const float* tab,
+                                                float* ag, int cap,
+                                                const float* __restrict__ w, int s) {
+  __syncthreads();  // the helpers' last scatter is in the table
+  const int n = cb.lidcount[s];
+  const float sc = cb.inv_p * (cb.sig ? cb.sig[s] : 1.f);
+  const int* l2 = cb.l2s + (size_t)s * cb.gs;
+  // FB entries per thread in flight: every slot load issued before the first atomic (one
+  // entry at a time, each atomic waited for its slot's load: ~1 µs per entry)
+  constexpr int FB = 8;
+  for (int i0 = threadIdx.x; i0 < n; i0 += FB * s3::NT) {
+    int slot[FB];
+    float d[FB];
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      const int i = i0 + u * s3::NT;
+      slot[u] = l2[i < n ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      const int i = i0 + u * s3::NT;
+      d[u] = i < min(n, cap) ? tab[i] : 0.f;
+    }
+    if (n > cap) {
+#pragma unroll
+      for (int u = 0; u < FB; ++u) {
+        const int i = i0 + u * s3::NT;
+        if (i >= cap && i < n)
+          d[u] = __hip_atomic_load(&ag[i - cap], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if constexpr (!RARE) {
+#pragma unroll
+      for (int u = 0; u < FB; ++u) {
+        const int i = i0 + u * s3::NT;
+        const int sl = i < n ? slot[u] : 0;
+        d[u] -= i < n ? (cb.wbf ? s3_w16(w, sl) : w[sl]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      const int i = i0 + u * s3::NT;
+      if (i < n && d[u] != 0.f) atomicAdd(&cb.dacc[slot[u]], sc * d[u]);
+    }
+  }
+}
+
 // RARE (round mode 4): blocks [S_act, 2·S_act) are the spokes' rare-slot workgroups
 // (s3_rare above) and the combiners follow them; the scanner adds each row's rare margin
 // from its granule (rgran), the helpers gather only the table slots' first occurrences.
@@ -887,6 +1004,7 @@ __device__ __forceinline__ void s3_scan_body(
   if (bid >= cb.S_act) {
     if (RARE && bid < 2 * cb.S_act) {  // a rare-slot workgroup
       s3_rare(slotsT, dc, B, R, w, cb, rgran, sm, bid - cb.S_act);
+      if (cb.inscan == 2) s3_fold_pres(meta, dc, B, R, cb, bid - cb.S_act);
       if (tail == 2) {  // then the spoke's combiner: its w0 pass ends long before the scan
         __syncthreads();
         s3_combine_spoke(slotsT, dc, B, R, cb, sm, bid - cb.S_act, 0, 1);
@@ -1008,7 +1126,7 @@ __device__ __forceinline__ void s3_scan_body(
         stamp(9);
         const float c = cf(u, p, y);
         sm.cb[b][lane] = c;
-        if (row < t1)  // the row's granule (write-through): the combiner polls it
+        if (row < t1 && cb.inscan != 1)  // the row's granule (write-through): a combiner polls it
           __hip_atomic_store((s3_gu64*)(cb.gran + row),
                              ((unsigned long long)cb.epoch << 32) | __float_as_uint(c),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1044,6 +1162,7 @@ __device__ __forceinline__ void s3_scan_body(
       wr[6] = 0.f;
       wr[7] = 0.f;
     }
+    if (cb.inscan) s3_inscan_flush<RARE>(cb, tab, ag, cap, w, s);
     s3_spoke_end(tail == 1, slotsT, dc, B, R, cb, ws, wsd, dn, dim, p, sm, s);
     return;
   }
@@ -1067,6 +1186,9 @@ __device__ __forceinline__ void s3_scan_body(
   const int qd = g_s3_dense_order ? s3::NHA - 1 - q : q;
   const int kd = dn + (p.bias ? 1 : 0);  // real dense columns (KN pads them to 16 / 32)
   const int hl = q * 64 + lane;
+  const bool inscan = cb.inscan != 0, inscan1 = cb.inscan == 1;  // 2: s3_fold_pres
+  const uint32_t tmask = inscan ? s3::F_TAB : s3::F_SCAT;
+  const float isc = inscan1 ? cb.inv_p * (cb.sig ? cb.sig[s] : 1.f) : 0.f;
   float wn[s3::NJ], w0[s3::NJ];  // running dense weights of this wave's columns, round start
 #pragma unroll
   for (int i = 0; i < s3::NJ; ++i) {
@@ -1197,10 +1319,14 @@ __device__ __forceinline__ void s3_scan_body(
 #pragma unroll
       for (int i = 0; i < s3::NF; ++i) {
         const uint32_t m = p2[i];
-        const bool sc = (m & s3::F_SCAT) != 0u && cv != 0.f;
-        if (__builtin_amdgcn_ballot_w64(sc) == 0ull) continue;
+        // in-scan combine: every table occurrence into the table (an entry nobody reads
+        // later takes the spoke's remaining deltas for the flush), the others to dacc
+        const bool sc = (m & tmask) != 0u && cv != 0.f;
+        const bool dr = inscan1 && (m & s3::F_PRES) != 0u && cv != 0.f;
+        if (__builtin_amdgcn_ballot_w64(sc || dr) == 0ull) continue;
         const int lid = (int)(m >> s3::LID_SHIFT);
         const float val = (m & s3::F_SIGN) ? -cv : cv;
+        if (dr) atomicAdd(&cb.dacc[lid], val * isc);  // lid = the slot (F_PRES)
         // (a branch-free form — every lane adding, the others 0 into a word of their own past
         // the table — measured slower: 961 → 1118 cycles per chunk)
         if (sc) {
@@ -1343,6 +1469,7 @@ __device__ __forceinline__ void s3_scan_body(
     if (lane == 0 && j < KN) wsd[(size_t)s * s3::DS + j] = wn[i] - w0[i];
   }
   if (q == 0 && lane >= KN && lane < s3::DS) wsd[(size_t)s * s3::DS + lane] = 0.f;
+  if (cb.inscan) s3_inscan_flush<RARE>(cb, tab, ag, cap, w, s);
   s3_spoke_end(tail == 1, slotsT, dc, B, R, cb, ws, wsd, dn, dim, p, sm, s);
 }
 
@@ -2021,6 +2148,11 @@ static int g_s3_cap_override = -1;  // tests: a small LDS table forces the globa
 // helpers gather them themselves (the A/B reference). The granule buffer is 2·B words
 // longer in mode 4 (set before a process's first prepare: it sizes the workspaces).
 static int g_s3_mode = 4;
+// the in-scan combine (S3Comb::inscan) in place of the combiner workgroups: 1 (auto) when
+// the combiners' grid exceeds one workgroup per CU (16 pipelines: 1.20 → 0.84 ms; one
+// pipeline: 0.311 vs 0.327-0.351 ms, profiles/round5/inscan/), 2 always, 0 never
+static int g_s3_inscan = 1;
+OMLDM_API void omldm_scan3_set_inscan(int v) { g_s3_inscan = v; }
 OMLDM_API void omldm_scan3_set_mode(int m) { g_s3_mode = m == 3 ? 3 : 4; }
 OMLDM_API int omldm_scan3_get_mode() { return g_s3_mode; }
 
@@ -2093,7 +2225,8 @@ OMLDM_API long long omldm_scan3_ws_words(int which, int B, int R, int S, int dn,
   const long long pf = kn == 16 ? s3_prep_floats<16>() : s3_prep_floats<32>();
   switch (which) {
     case 0: return (long long)dc * B;
-    case 1: return (long long)dc * B;  // meta word per occurrence
+    case 1:  // meta word per occurrence, then each table id's slot [S][R·dc/2 + 64]
+      return (long long)dc * B + (long long)S * ((long long)R * dc / 2 + 64);
     case 2: return S;
     case 3: return (long long)S * nchs * pf + S + 64;  // + σ at each spoke's end
     case 4: return 4LL * B;  // c granules + the w0-margin granules (mode 4)
@@ -2197,7 +2330,9 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
     gst = sd->side;
   }
   hipLaunchKernelGGL(s3_flags_kernel, dim3(dc, S_act), dim3(s3::FT), 0, st, W.slotsT, B, R,
-                     W.meta, W.lidcount);
+                     W.meta, W.lidcount, dim <= (1 << 22) ? 1 : 0,
+                     reinterpret_cast<int*>(W.meta + (size_t)dc * B),
+                     (long long)R * dc / 2 + 64);
   const int nchs = (R + s3::CH - 1) / s3::CH;
   // a per row: −1/(‖x‖² + kadd) (hinge, ε), 1 (logistic), y (Pegasos), 1/(2‖x‖² + kadd)
   // (MultiClassPA: rule 4)
@@ -2297,6 +2432,18 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   // behind its scans (16 pipelines: 1.20 / 1.27 / 1.67 ms, profiles/round5/mp_cns*.json)
   int cns = g_s3_cns > 0 ? g_s3_cns : 1;
   if (!rare || ncomb != 1) cns = 1;
+  // in-scan combine: no combiner workgroups. Auto (past one workgroup per CU): no w0-margin
+  // workgroups either — the helpers gather w0 and add the non-table occurrences (16
+  // pipelines: one wave of 256 workgroups instead of three); forced: the w0-margin
+  // workgroups while they fit, folding the non-table occurrences after their pass
+  const bool fits = (long long)M * s3_nper(S_act, rare, ncomb, cns) <= ncu;
+  const bool inscan = ncomb > 0 && g_s3_form < 2 && dim <= (1 << 22) &&
+                      (g_s3_inscan == 2 || (g_s3_inscan == 1 && !fits));
+  if (inscan) {
+    ncomb = 0;
+    cns = 1;
+    rare = g_s3_inscan == 2 && g_s3_mode == 4 && (long long)M * 2 * S_act <= ncu;
+  }
   S3Pipes pp{};
   pp.M = M;
   pp.ncomb = ncomb > 0 ? ncomb : 0;
@@ -2316,7 +2463,9 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
     pp.pipe[m] = S3Pipe{w[m], Wm.aglob, Wm.ws, Wm.wsd, rare ? Wm.gran + B : nullptr,
                         S3Comb{W0.lidcount, Wm.gran, epoch[m], S_act, dacc[m], inv_p[m],
                                static_cast<unsigned long long*>(arrive[m]), cum[m], sig,
-                               (flags & 2) ? 1 : 0, cns},
+                               (flags & 2) ? 1 : 0, cns,
+                               reinterpret_cast<const int*>(W0.meta + (size_t)dc * B),
+                               gstride, inscan ? (rare ? 2 : 1) : 0},
                         p};
   }
   const int e = kn == 16 ? s3_launch_scan<16>(rule, rare, W0.slotsT, W0.meta, dc, dn, y, B, R,
@@ -2326,7 +2475,7 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   if (e) return e;
   for (int m = 0; m < M; ++m) {
     const S3Ws Wm = s3_ws(ptrs + 8 * m);
-    if (ncomb > 0 || tail || tailm) {  // the categorical slots were combined in the scan's launch
+    if (ncomb > 0 || tail || tailm || inscan) {  // the categorical slots were combined in the scan's launch
       if (!arrive[m])
         hipLaunchKernelGGL(s3_tail_kernel, dim3(1), dim3(256), 0, st, Wm.ws, Wm.wsd, sig, S_act,
                            dn, dim, bias, inv_p[m], dacc[m], cum[m]);

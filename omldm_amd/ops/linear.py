@@ -315,6 +315,8 @@ def _s3_lib():
         # A/B: the launch form (0 auto, 1 latency form always, 2 throughput form always)
         h.omldm_scan3_set_form(int(os.environ.get("OMLDM_S3_FORM", "0")))
         h.omldm_scan3_set_cns(int(os.environ.get("OMLDM_S3_CNS", "0")))
+        # A/B: 0 = the combiner workgroups (the round-5 form) instead of the in-scan combine
+        h.omldm_scan3_set_inscan(int(os.environ.get("OMLDM_S3_INSCAN", "1")))
         _S3_MODE_SET["done"] = True
     return h
 

@@ -81,6 +81,7 @@ HIP_SIGS = [
     ("omldm_scan3_set_comb", None, [i32]),
     ("omldm_scan3_set_form", None, [i32]),
     ("omldm_scan3_set_cns", None, [i32]),
+    ("omldm_scan3_set_inscan", None, [i32]),
     ("omldm_scan3_set_prep_split", None, [i32]),
     ("omldm_scan3_get_comb", i32, []),
     ("omldm_scan3_comb_err", i32, []),

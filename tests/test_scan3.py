@@ -9,6 +9,8 @@ replicas.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -351,12 +353,15 @@ def test_gpu_scan3_mfma_prep_matches_valu_prep(mode3, dn, exact):
 
 
 @gpu
+@pytest.mark.parametrize("mode", [3, 4])
 @pytest.mark.parametrize("S,R,dn", [(16, 8192, 13), (5, 700, 0), (3, 1300, 13)])
-def test_gpu_scan3_inlaunch_combine_matches_scatter(mode3, S, R, dn):
+def test_gpu_scan3_inlaunch_combine_matches_scatter(mode, S, R, dn):
     """The combine folded into the scan's launch (combiner workgroups polling the scanner's
-    {epoch, c} granules) against the whole-GPU scatter kernel after the scan: the same
-    weights up to the fp32 order of the atomic sums, over three rounds on one granule
-    buffer (epochs 1..3), and no combiner gave up waiting."""
+    {epoch, c} granules; or the in-scan combine, forced: the table flushed at the scan
+    workgroup's end, the non-table occurrences added by the helpers (mode 3) or by the w0
+    workgroup after its pass (mode 4)) against the whole-GPU scatter kernel after the scan:
+    the same weights up to the fp32 order of the atomic sums, over three rounds on one
+    granule buffer (epochs 1..3), and no combiner gave up waiting."""
     from omldm_amd.models.linear import SVM
     from omldm_amd.parallel.comm import Comm
     from omldm_amd.parallel.protocols import Synchronous
@@ -366,23 +371,30 @@ def test_gpu_scan3_inlaunch_combine_matches_scatter(mode3, S, R, dn):
     space = FeatureSpace(dn, 0, 26, 1 << 20)
     B = S * R - 17  # a short last spoke
     res = {}
+    old = L.set_scan3_mode(mode)
     try:
-        for comb in (0, 1, 2):
+        # (combiner workgroups per spoke, in-scan combine): (0, -) the scatter kernel,
+        # (1 | 2, 0) combiner workgroups, (1, 2) the in-scan combine forced
+        for comb, inscan in ((0, 0), (1, 0), (2, 0), (1, 2)):
             h.omldm_scan3_set_comb(comb)
+            h.omldm_scan3_set_inscan(inscan)
             lrn = SVM({"variant": "PA-I", "C": 1.0}, space, dev)
             proto = Synchronous(Comm(), lrn, {"virtualSpokes": S})
             for k in range(3):
                 proto.round(synth_raw(space, B, start=k * B, seed=31).to(dev))
             torch.cuda.synchronize()
             assert h.omldm_scan3_comb_err() == 0
-            res[comb] = (lrn.w.cpu(), lrn.running_totals())
+            res[(comb, inscan)] = (lrn.w.cpu(), lrn.running_totals())
     finally:
         h.omldm_scan3_set_comb(1)
-    for comb in (1, 2):
-        d = (res[comb][0] - res[0][0]).abs()
-        assert float(d.max()) < 1e-4, (comb, float(d.max()))
-        assert res[comb][1]["fitted"] == res[0][1]["fitted"] == 3 * B
-        assert abs(res[comb][1]["mistakes"] - res[0][1]["mistakes"]) <= 2
+        h.omldm_scan3_set_inscan(int(os.environ.get("OMLDM_S3_INSCAN", "1")))
+        L.set_scan3_mode(old)
+    ref = res[(0, 0)]
+    for key in ((1, 0), (2, 0), (1, 2)):
+        d = (res[key][0] - ref[0]).abs()
+        assert float(d.max()) < 1e-4, (key, float(d.max()))
+        assert res[key][1]["fitted"] == ref[1]["fitted"] == 3 * B
+        assert abs(res[key][1]["mistakes"] - ref[1]["mistakes"]) <= 2
 
 
 @gpu
