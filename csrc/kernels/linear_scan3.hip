@@ -1496,8 +1496,42 @@ struct S3Pipes {
   int ncomb;  // combiner workgroups per spoke (0: none)
   int tail;   // 1: each scan workgroup combines its own spoke after its scan; 2: the
               // spoke's w0-margin workgroup combines it once its w0 pass is done (RARE)
+  // the prep made on another stream: every workgroup waits for its ready word to reach
+  // `wepoch` (omldm_scan3_signal at the prep's end) instead of the launch waiting on the
+  // prep's event (null: no wait)
+  const unsigned long long* wflag;
+  unsigned long long wepoch;
   S3Pipe pipe[kS3MaxPipes];
 };
+
+// A prep's ready word: the prep made ahead on its own stream ends with this one-lane kernel
+// (after the prep's kernels, stream order), and the round's launch waits for the word in
+// its workgroups (s3_wait_prep) instead of a cross-stream wait on an event: the barrier
+// packet released the scan ~11 µs after the previous round's apply and together with the
+// next prep's kernels (~7 µs and ahead of them without it; 0.311 → 0.292 ms per round,
+// profiles/round5/devgap/).
+__global__ void s3_signal_kernel(unsigned long long* flag, unsigned long long epoch) {
+  if (threadIdx.x == 0)
+    __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bounded: a prep that never signals fails the round loudly (g_s3_comb_err = 3).
+__device__ __forceinline__ void s3_wait_prep(const unsigned long long* flag,
+                                             unsigned long long epoch) {
+  if (flag == nullptr) return;
+  if (threadIdx.x == 0) {
+    for (unsigned spins = 0;
+         __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch;) {
+      if (++spins > s3::SPIN_MAX) {
+        atomicExch(&g_s3_comb_err, 3);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the prep's data past stale lines
+  }
+  __syncthreads();
+}
 
 template <int RULE, int KN, bool RARE>
 __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu(s3::WPE, s3::WPE))) void s3_scan_kernel(
@@ -1508,6 +1542,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   extern __shared__ float tab[];  // [cap] + 64 scratch words (one per lane)
   const int nblk = s3_nper(S_act, RARE, pp.ncomb, pp.pipe[0].cb.cns);  // per pipeline
   const int pi = (int)blockIdx.x / nblk, local = (int)blockIdx.x % nblk;
+  s3_wait_prep(pp.wflag, pp.wepoch);
   int bid;
   if (RARE && local < S_act) bid = S_act + local;  // its w0-margin workgroups first
   else if (RARE && local < 2 * S_act) bid = local - S_act;
@@ -2377,12 +2412,28 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
 // — slots, occurrences, table counts, prep — the shared prep's; granules, spoke rows, dense
 // deltas and table spill its own), its granule epoch (≥ 1, one more than the last round on
 // that granule buffer, zeroed when allocated) and arrival word (null: tail kernel after).
+// The next run on this thread waits in its launch for a prep's ready word (see S3Pipes)
+static thread_local const unsigned long long* t_s3_wflag = nullptr;
+static thread_local unsigned long long t_s3_wepoch = 0;
+OMLDM_API void omldm_scan3_wait_next(const void* flag, unsigned long long epoch) {
+  t_s3_wflag = static_cast<const unsigned long long*>(flag);
+  t_s3_wepoch = epoch;
+}
+OMLDM_API int omldm_scan3_signal(void* flag, unsigned long long epoch, void* stream) {
+  hipLaunchKernelGGL(s3_signal_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     static_cast<unsigned long long*>(flag), epoch);
+  return (int)hipGetLastError();
+}
+
 static int s3_run_impl(int M, const float* const* w, float* const* dacc, double* const* cum,
                        const float* C, const float* eps, const float* lr, const float* inv_p,
                        void* const* ptrs, const unsigned* epoch, void* const* arrive, int dn,
                        int dc, const void* y, int y8, int B, int R, int S, int dim, int rule,
                        int variant, int bias, long long span_in, int flags, int shr,
                        const float* lam, const float* tbase, hipStream_t st) {
+  const unsigned long long* wflag = t_s3_wflag;  // consumed whatever this call does
+  const unsigned long long wepoch = t_s3_wepoch;
+  t_s3_wflag = nullptr;
   if (M < 1 || M > kS3MaxPipes) return -4;
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
@@ -2446,6 +2497,8 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   }
   S3Pipes pp{};
   pp.M = M;
+  pp.wflag = wflag;
+  pp.wepoch = wepoch;
   pp.ncomb = ncomb > 0 ? ncomb : 0;
   pp.tail = tail ? 1 : tailm;
   for (int m = 0; m < M; ++m) {

@@ -299,6 +299,39 @@ class Scan3Prep:
     key: tuple          # (B, R, S, dim, bias, rule, variant, C, dn, dc) it was made for
     event: object = None
     slot: object = None  # workspace set (ring slot "k<i>" for inline preps)
+    ready: object = None  # (ready word address, epoch): set at the prep's end on its stream
+
+
+# The preps' ready words, one per (device, workspace slot), each counting its preps. A prep
+# made on a stream of its own ends with omldm_scan3_signal, and the round's launch waits for
+# the word in its workgroups (omldm_scan3_wait_next) instead of a cross-stream wait on the
+# prep's event: that barrier packet released the scan ~11 µs after the previous round's
+# apply (profiles/round5/devgap/: 0.311 → 0.292 ms per device-ingest round).
+# OMLDM_S3_READY=0: the event wait (A/B).
+_S3_READY_WAIT = os.environ.get("OMLDM_S3_READY", "1") != "0"
+_S3_READY: dict = {}
+
+
+def _s3_ready_word(dev, slot):
+    rec = _S3_READY.get(str(dev))
+    if rec is None:
+        rec = _S3_READY[str(dev)] = (torch.zeros(256, dtype=torch.int64, device=dev), {}, {})
+    words, index, epochs = rec
+    i = index.get(slot)
+    if i is None:
+        if len(index) >= words.numel():
+            return None
+        i = index[slot] = len(index)
+    epochs[slot] = epochs.get(slot, 0) + 1
+    return words.data_ptr() + 8 * i, epochs[slot]
+
+
+def _s3_wait_prep(sp, dev) -> None:
+    """Order the next v3 launch on the current stream after the prep ``sp``."""
+    if _S3_READY_WAIT and sp.ready is not None:
+        _s3_lib().omldm_scan3_wait_next(sp.ready[0], sp.ready[1])
+    elif sp.event is not None:
+        torch.cuda.current_stream(dev).wait_event(sp.event)
 
 
 # v3 table-scan kernel generation: 4 = the split spoke (a scanner and a table workgroup per
@@ -513,7 +546,12 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
                                 ptrs, st.cuda_stream), "omldm_scan3_prepare")
     ev = torch.cuda.Event()  # pipelines on other streams that reuse the prep wait on it
     ev.record(st)
-    return Scan3Prep(bufs, ptrs, _s3_key(batch, R, S, dim, bias, rule), ev, slot)
+    ready = None
+    if stream is not None and _S3_READY_WAIT:
+        ready = _s3_ready_word(dev, slot)
+        if ready is not None:
+            check(h.omldm_scan3_signal(ready[0], ready[1], st.cuda_stream), "omldm_scan3_signal")
+    return Scan3Prep(bufs, ptrs, _s3_key(batch, R, S, dim, bias, rule), ev, slot, ready)
 
 
 def scan3_part_bounds(dim: int, dn: int, dc: int, part: int, parts: int,
@@ -553,8 +591,8 @@ def linear_scan3_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: t
         sp = linear_scan3_prepare(batch, R, S, dim, bool(rule.bias), rule, hashed=hashed,
                                   slot=_s3_slot_for(key, w.device))
         batch.prep = sp  # the next pipeline of the tick reuses it (same key)
-    elif sp.event is not None:
-        torch.cuda.current_stream(w.device).wait_event(sp.event)
+    else:
+        _s3_wait_prep(sp, w.device)
     global SCAN3_ROUNDS
     SCAN3_ROUNDS += 1
     h = _s3_lib()
@@ -610,8 +648,8 @@ def linear_scan3_round_multi(ws: list, batch: RawBatch, R: int, S: int, daccs: l
         sp = linear_scan3_prepare(batch, R, S, dim, bool(r0.bias), r0, hashed=hashed,
                                   slot=_s3_slot_for(key, ws[0].device))
         batch.prep = sp
-    elif sp.event is not None:
-        torch.cuda.current_stream(ws[0].device).wait_event(sp.event)
+    else:
+        _s3_wait_prep(sp, ws[0].device)
     global SCAN3_ROUNDS
     SCAN3_ROUNDS += 1
     h = _s3_lib()

@@ -82,6 +82,8 @@ HIP_SIGS = [
     ("omldm_scan3_set_form", None, [i32]),
     ("omldm_scan3_set_cns", None, [i32]),
     ("omldm_scan3_set_inscan", None, [i32]),
+    ("omldm_scan3_wait_next", None, [vp, C.c_uint64]),
+    ("omldm_scan3_signal", i32, [vp, C.c_uint64, vp]),
     ("omldm_scan3_set_prep_split", None, [i32]),
     ("omldm_scan3_get_comb", i32, []),
     ("omldm_scan3_comb_err", i32, []),
