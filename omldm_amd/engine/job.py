@@ -816,6 +816,17 @@ class Job:
             self._health.check()  # the last trained tick's words
         if self._trace_dir:
             self._trace_models(final=True)
+        self.close()
+        return self
+
+    def close(self) -> None:
+        """Stop what the job runs beside its ticks — the forecast lane (thread and resident
+        wave), the ingest read-ahead, the egress writer, the checkpointer, the watchdog — and
+        wait for the device. Idempotent; ``run`` ends with it, and a caller that drives
+        ``tick`` itself (tests, embedding) calls it when done."""
+        if getattr(self, "_closed", False):
+            return
+        self._closed = True
         if self.fserver is not None:
             self.fserver.close()
         self.ingest.close()
@@ -824,7 +835,8 @@ class Job:
             self.checkpointer.close()
         if self.watchdog is not None:
             self.watchdog.stop()
-        return self
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     # --------------------------------------------------------------- checkpoint
     def state_dict(self) -> dict:

@@ -316,6 +316,7 @@ def _s3_ready_word(dev, slot):
     rec = _S3_READY.get(str(dev))
     if rec is None:
         rec = _S3_READY[str(dev)] = (torch.zeros(256, dtype=torch.int64, device=dev), {}, {})
+        torch.cuda.synchronize(dev)  # zero before a prep stream's first signal lands
     words, index, epochs = rec
     i = index.get(slot)
     if i is None:

@@ -51,6 +51,13 @@ def test_default_flags_engine_gpu(cuda, streams, learner):
     br = MemoryBroker.named(name)
     br.create_topic(cfg.trainingDataTopic, 2)
     job = Job(cfg, Comm(), cuda)
+    try:
+        _drive(job, br, cfg, streams, learner)
+    finally:
+        job.close()
+
+
+def _drive(job, br, cfg, streams, learner):
     br.produce("requests", json.dumps({
         "id": 7, "request": "Create",
         "learner": {"name": learner, "hyperParameters": HYPER.get(learner, {})},

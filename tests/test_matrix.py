@@ -116,6 +116,13 @@ def _run(learner, pre, field_aware, device, protocol="Synchronous", hyper=None, 
     br = MemoryBroker.named(name)
     br.create_topic(cfg.trainingDataTopic, 2)
     job = Job(cfg, Comm(), device)
+    try:
+        _drive(job, br, sp, learner, pre, protocol, hyper)
+    finally:
+        job.close()  # no lane thread, read-ahead or resident wave outlives the test
+
+
+def _drive(job, br, sp, learner, pre, protocol, hyper):
     br.produce("requests", json.dumps({
         "id": 7, "request": "Create",
         "learner": {"name": learner, "hyperParameters": hyper or HYPER.get(learner, {})},

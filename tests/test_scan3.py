@@ -344,7 +344,12 @@ def test_gpu_scan3_mfma_prep_matches_valu_prep(mode3, dn, exact):
             preps.append(sp.bufs[3].clone().cpu())
         finally:
             h.omldm_scan3_set_gram_valu(0)
-    a, b = preps
+    # the chunk blocks' Grams, row scales, dense columns and targets (σ_t / 1/σ_{t+1} and
+    # the per-spoke σ after the blocks are written for the shrinking rules only)
+    KN, CH = 16, 64
+    PF = 2 * CH * CH + CH + KN * CH + 3 * CH
+    nblk = S * (R // CH)
+    a, b = (p[:nblk * PF].view(nblk, PF)[:, :PF - 2 * CH] for p in preps)
     if exact:
         assert torch.equal(a, b), (a - b).abs().max()
     else:
