@@ -481,3 +481,30 @@ def test_gpu_multiclass_scan3_matches_cpu(K, variant, C, S, R):
     tg, tc = res[str(dev)][1], res["cpu"][1]
     assert tg["fitted"] == tc["fitted"] == 3 * (S * R - 11)
     assert abs(tg["mistakes"] - tc["mistakes"]) <= 2e-3 * tc["fitted"] + 2
+
+
+@gpu
+def test_gpu_scan3_prep_ready_word_never_set_fails_loudly():
+    """A round that waits for a prep's ready word which never reaches its epoch (a prep that
+    never ran) gives up after the bounded spin and raises the error word (3), which the
+    engine's health check turns into a failed tick — instead of hanging the GPU or scanning
+    silently (s3_wait_prep)."""
+    from omldm_amd.models.linear import SVM
+
+    dev = _cuda()
+    h = native.hip()
+    space = FeatureSpace(13, 0, 26, 1 << 16)
+    S, R = 2, 256
+    batch = synth_raw(space, S * R, seed=3).to(dev)
+    lrn = SVM({"variant": "PA-I", "C": 1.0}, space, dev)
+    rule = lrn.rule
+    sp = L.linear_scan3_prepare(batch, R, S, space.dim, bool(rule.bias), rule, slot=13)
+    torch.cuda.synchronize()
+    assert h.omldm_scan3_comb_err() in (0, 3)  # clear
+    never = torch.zeros(1, dtype=torch.int64, device=dev)
+    sp.ready, sp.event = (never.data_ptr(), 1), None
+    batch.prep = sp
+    dacc = torch.zeros(space.dim + 2, dtype=torch.float32, device=dev)
+    L.linear_scan3_round(lrn.w, batch, R, S, dacc, rule, 0.5)
+    torch.cuda.synchronize()
+    assert h.omldm_scan3_comb_err() == 3
