@@ -251,6 +251,9 @@ def main(argv=None) -> int:
     ap.add_argument("--rows", type=int, default=8192, help="examples per spoke per round")
     ap.add_argument("--dim-log2", type=int, default=20)
     ap.add_argument("--learner", default="SVM", choices=["SVM", "LogisticRegression"])
+    ap.add_argument("--model-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16: the learner's modelDtype (margins on bf16 weights, fp32 "
+                         "master and arithmetic; BASELINE config 2 names a bf16 model)")
     ap.add_argument("--pool", type=int, default=8, help="pinned host batches per rank")
     ap.add_argument("--ingest", default="pinned", choices=["pinned", "device"],
                     help="pinned: H2D copy of every batch inside the timed loop")
@@ -313,9 +316,10 @@ def main(argv=None) -> int:
             d.flat.copy_(p.flat)
 
     if a.learner == "SVM":
-        learner = SVM({"variant": "PA-I", "C": 1.0}, space, device)
+        learner = SVM({"variant": "PA-I", "C": 1.0, "modelDtype": a.model_dtype}, space, device)
     else:
-        learner = LogisticRegression({"learningRate": 0.1}, space, device)
+        learner = LogisticRegression({"learningRate": 0.1, "modelDtype": a.model_dtype}, space,
+                                     device)
     assert learner.seq_capable()
     proto = Synchronous(comm, learner, {"virtualSpokes": S,
                                         **({"HubParallelism": a.hubs} if a.hubs else {})})
@@ -551,7 +555,7 @@ def main(argv=None) -> int:
                                  "P = 16 sequential PA-I spokes + averaging (the reference's "
                                  "default parallelism), measured on the MI355X box's host "
                                  "CPU (bench/cpu_reference.py)"} if base else None,
-            "dtype": "fp32",
+            "dtype": a.model_dtype,
             "ingest_pipeline": None if a.ingest != "pinned" else {
                 "batches_copied_ahead": ahead,
                 "pcie_copies_in_timed_window": max(0, a.steps - ahead),
@@ -566,7 +570,9 @@ def main(argv=None) -> int:
                     "synthetic (HBM-resident replay, tokens hashed in the round)",
             "config": {"model": ("linear SVM PA-I" if a.learner == "SVM" else
                                  "logistic regression (SGD)") +
-                                f", 2^{a.dim_log2} hashed features (13 num + 26 cat + bias), fp32",
+                                f", 2^{a.dim_log2} hashed features (13 num + 26 cat + bias), " +
+                                ("fp32" if a.model_dtype == "fp32" else
+                                 "bf16 model (margins on the bf16 weights, fp32 master)"),
                        "global_batch": B * world, "seq_len": None,
                        "parallelism": f"dp{world}", "protocol": "Synchronous",
                        "spokes_per_gpu": S, "rows_per_spoke_per_round": R,
