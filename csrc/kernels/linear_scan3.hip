@@ -274,6 +274,21 @@ __global__ __launch_bounds__(s3::FT) void s3_flags_kernel(const int* __restrict_
 }
 
 // ------------------------------------------------------------------ pass 3: Grams
+// Column factors of the Grams (logistic without shrink, cscale = lr): column t of aG_k and
+// aX1_{k+1} is the effect of row t's step c_t = lr·y_t·ρ_t (ρ_t = 1/(1 + e^{y_t·u_t})), so
+// with the columns scaled by lr·y_t the scanner's chain steps on ρ_t alone: two dependent
+// multiplies fewer per row on the chain (scol[d][t]: row t of chunk c − d; 0 past the shard
+// or without a target). The scan takes it from cb's rule: s3_scan_body, RULE logistic, !shr.
+__device__ __forceinline__ void s3_gram_colscale(float (*scol)[s3::CH], float cscale,
+                                                 const void* __restrict__ yv, int y8, int t0,
+                                                 int t1, int c, int tid) {
+  if (cscale == 0.f || tid >= 2 * s3::CH) return;
+  const int d = tid / s3::CH, r = tid - d * s3::CH;
+  const int row = t0 + (c - d) * s3::CH + r;
+  const float y = (c - d >= 0 && row < t1) ? load_y(yv, row, y8) : 0.f;
+  scol[d][r] = y == y ? cscale * y : 0.f;
+}
+
 // grid (chunks, S_act), 256 threads. Row scale a_t: −1/(‖x‖² + kadd) for the affine rules
 // (hinge, ε-insensitive), 1 for logistic; 0 for rows past the shard. Out, per chunk:
 // aG (strictly lower) | aX1 | a | dense [KN][64] (numerical columns, then the intercept).
@@ -283,7 +298,8 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
                                                       const void* __restrict__ yv, int y8,
                                                       int B, int R, int bias, int affine,
                                                       float kadd, float* __restrict__ prep,
-                                                      int nchs, int shr, float shr_r) {
+                                                      int nchs, int shr, float shr_r,
+                                                      float cscale) {
   const int c = blockIdx.x, s = blockIdx.y;
   int t0, t1;
   spoke_rows(s, R, B, t0, t1);
@@ -293,7 +309,9 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
   __shared__ alignas(16) int sl[2][s3::MAXF][s3::CH + 4];
   __shared__ float xn[2][s3::CH][KN + 1];
   __shared__ float sa[s3::CH];
+  __shared__ float scol[2][s3::CH];  // column factors (s3_gram_colscale)
   const int tid = threadIdx.x;
+  s3_gram_colscale(scol, cscale, yv, y8, t0, t1, c, tid);
   for (int i = tid; i < 2 * dc * s3::CH; i += 256) {
     const int d = i / (dc * s3::CH), rem = i - d * dc * s3::CH;
     const int f = rem / s3::CH, r = rem - f * s3::CH;  // field-major: coalesced per field
@@ -378,6 +396,12 @@ __global__ __launch_bounds__(256) void s3_gram_kernel(const int* __restrict__ sl
       const int t = 4 * bi + i;
       const float a = sa[t];
       float4 v = make_float4(a * acc[i][0], a * acc[i][1], a * acc[i][2], a * acc[i][3]);
+      if (cscale != 0.f) {
+        v.x *= scol[d][4 * bj + 0];
+        v.y *= scol[d][4 * bj + 1];
+        v.z *= scol[d][4 * bj + 2];
+        v.w *= scol[d][4 * bj + 3];
+      }
       if (d == 0) {  // strictly lower: column ≥ row → 0
         if (4 * bj + 0 >= t) v.x = 0.f;
         if (4 * bj + 1 >= t) v.y = 0.f;
@@ -409,7 +433,8 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
                                                            const void* __restrict__ yv, int y8,
                                                            int B, int R, int bias, int affine,
                                                            float kadd, float* __restrict__ prep,
-                                                           int nchs, int shr, float shr_r) {
+                                                           int nchs, int shr, float shr_r,
+                                                           float cscale) {
   typedef float f32x16 __attribute__((ext_vector_type(16)));
   const int c = blockIdx.x, s = blockIdx.y;
   int t0, t1;
@@ -420,7 +445,9 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
   __shared__ alignas(16) int sl[2][s3::MAXF][s3::CH + 4];
   __shared__ float xn[2][s3::CH][KN + 1];
   __shared__ float sa[s3::CH];
+  __shared__ float scol[2][s3::CH];  // column factors (s3_gram_colscale)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  s3_gram_colscale(scol, cscale, yv, y8, t0, t1, c, tid);
   // ---- all loads in flight at once (clamped addresses, results selected after)
   constexpr int NSL = 2 * s3::MAXF * s3::CH / 256, NXN = 2 * s3::CH * KN / 256;
   int sv[NSL];
@@ -529,6 +556,7 @@ __global__ __launch_bounds__(256) void s3_gram_mfma_kernel(const int* __restrict
     for (int g = 0; g < 16; ++g) {
       const int t = I0 + (g & 3) + 8 * (g >> 2) + 4 * hi, col = J0 + l31;
       float v = sa[t] * acc[g];
+      if (cscale != 0.f) v *= scol[d][col];
       if (d == 0 && col >= t) v = 0.f;  // aG strictly lower
       out[d * s3::MAT + t * s3::CH + col] = v;
     }
@@ -1114,14 +1142,31 @@ __device__ __forceinline__ void s3_scan_body(
         }
         stamp(8);
         float n1 = 0.f;
+        // one step per row: lane t's step (its c, or for the logistic rule without shrink
+        // ρ_t = 1/(1 + e^{y_t·u_t}) with lr·y_t in the Grams' columns, s3_gram_colscale)
+        // broadcast, every later row's u and the next chunk's fold updated
+        auto chain = [&](auto step) {
 #pragma unroll
-        for (int t = 0; t < s3::CH; ++t) {
-          const float ct = readlane_f(cf(u, p, y), t);
-          u = fmaf(ct, gg[t], u);     // aG strictly lower: lane t frozen after step t
-          n1 = fmaf(ct, xx[t], n1);   // → chunk k+1 (off the dependency chain)
-          // pin the fold beside its step: left to itself the compiler parks the 64 c's
-          // in SGPRs and runs the fold as a serial tail after the chunk
-          asm volatile("" : "+v"(u), "+v"(n1));
+          for (int t = 0; t < s3::CH; ++t) {
+            const float ct = readlane_f(step(u), t);
+            u = fmaf(ct, gg[t], u);     // aG strictly lower: lane t frozen after step t
+            n1 = fmaf(ct, xx[t], n1);   // → chunk k+1 (off the dependency chain)
+            // pin the fold beside its step: left to itself the compiler parks the 64 c's
+            // in SGPRs and runs the fold as a serial tail after the chunk
+            asm volatile("" : "+v"(u), "+v"(n1));
+          }
+        };
+        if constexpr (RULE == kSeqLogistic) {
+          if (!shr) {
+            const float lo2 = y * 1.44269504088896341f;  // e^{y·u} = 2^{y·log2(e)·u}
+            chain([&](float v) {
+              return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(lo2 * v));
+            });
+          } else {
+            chain([&](float v) { return cf(v, p, y); });
+          }
+        } else {
+          chain([&](float v) { return cf(v, p, y); });
         }
         stamp(9);
         const float c = cf(u, p, y);
@@ -2343,7 +2388,7 @@ OMLDM_API int omldm_scan3_teardown() {
 OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int hashed, int dc,
                                   const void* y, int y8, int B, int R, int S, int dim, int bias,
                                   int rule, int variant, float C, long long span_in,
-                                  int cbase, int shr, float shr_r, float tbase,
+                                  int cbase, int shr, float shr_r, float tbase, float lr,
                                   void* const* ptrs, void* stream) {
   if (S <= 0 || B <= 0) return 0;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
@@ -2374,19 +2419,21 @@ OMLDM_API int omldm_scan3_prepare(const float* num, int dn, const void* src, int
   const int affine = rule == kSeqLogistic ? 0 : rule == kSeqPegasos ? 2 : rule == 4 ? 3 : 1;
   const float kadd = ((affine == 1 || affine == 3) && variant == 2) ? 0.5f / C : 0.f;
   if (rule == kSeqPegasos && shr != 2) return -2;
+  // logistic without shrink: the Grams' columns carry lr·y (s3_gram_colscale)
+  const float cscale = rule == kSeqLogistic && !shr ? lr : 0.f;
   if (g_s3_gram_valu) {
     if (s3_kn(dn, bias) == 16)
       hipLaunchKernelGGL(s3_gram_kernel<16>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT, dc,
-                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r);
+                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r, cscale);
     else
       hipLaunchKernelGGL(s3_gram_kernel<32>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT, dc,
-                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r);
+                         num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r, cscale);
   } else if (s3_kn(dn, bias) == 16) {
     hipLaunchKernelGGL(s3_gram_mfma_kernel<16>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT,
-                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r);
+                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r, cscale);
   } else {
     hipLaunchKernelGGL(s3_gram_mfma_kernel<32>, dim3(nchs, S_act), dim3(256), 0, gst, W.slotsT,
-                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r);
+                       dc, num, dn, y, y8, B, R, bias, affine, kadd, W.prep, nchs, shr, shr_r, cscale);
   }
   if (shr) {  // σ per row from the targets the Gram pass wrote into the prep
     float* sig = W.prep + (size_t)S * nchs * (s3_kn(dn, bias) == 16 ? s3_prep_floats<16>()

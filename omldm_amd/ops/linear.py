@@ -403,7 +403,9 @@ def _s3_key(batch, R, S, dim, bias, rule: "LinearRule") -> tuple:
     c = float(rule.C) if rule.variant == PA2 else None
     # the row scaling depends on the rule family (a = −1/(‖x‖²+kadd), 1 or y) and the shrink
     fam = {RULE_PEGASOS: 2, RULE_LOGISTIC: 1, RULE_MULTI: 3}.get(rule.rule, 0)
-    return (batch.B, R, S, dim, bool(bias), fam, rule.variant == PA2, c, _s3_shrink(rule),
+    # logistic without shrink: lr·y in the Grams' columns (linear_scan3.hip s3_gram_colscale)
+    lr = float(rule.lr) if fam == 1 and _s3_shrink(rule)[0] == 0 else None
+    return (batch.B, R, S, dim, bool(bias), fam, rule.variant == PA2, c, _s3_shrink(rule), lr,
             batch.dn, batch.dc, int(batch.span), batch.y.data_ptr(), batch.tok.data_ptr(), S3_MODE)
 
 
@@ -544,7 +546,7 @@ def linear_scan3_prepare(batch: RawBatch, R: int, S: int, dim: int, bias: bool,
                                 int(y.dtype == torch.int8), batch.B, R, S, dim, int(bias),
                                 rule.rule, rule.variant, float(rule.C), span,
                                 int(batch.cbase) if batch.span > 0 else -1, *_s3_shrink(rule),
-                                ptrs, st.cuda_stream), "omldm_scan3_prepare")
+                                float(rule.lr), ptrs, st.cuda_stream), "omldm_scan3_prepare")
     ev = torch.cuda.Event()  # pipelines on other streams that reuse the prep wait on it
     ev.record(st)
     ready = None

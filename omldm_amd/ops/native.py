@@ -66,7 +66,7 @@ HIP_SIGS = [
     ("omldm_scan3_fits", i32, [i32, i32, i32, i32]),
     ("omldm_scan3_ws_words", i64, [i32, i32, i32, i32, i32, i32, i64, i32]),
     ("omldm_scan3_prepare", i32, [vp, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32,
-                                  i32, f32, i64, i32, i32, f32, f32, vp, vp]),
+                                  i32, f32, i64, i32, i32, f32, f32, f32, vp, vp]),
     ("omldm_scan3_run", i32, [vp, i32, i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, f32,
                               f32, f32, f32, i32, i64, vp, i32, i32, i32, u32, vp, i32, f32, f32,
                               vp]),
