@@ -177,7 +177,8 @@ def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dic
     from omldm_amd.utils.config import JobConfig
 
     sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
-    parts = 8  # partitions are read concurrently (one GIL-free pread each; 8 MB regions)
+    # partitions are read concurrently (one GIL-free pread each; 8 MB regions)
+    parts = int(os.environ.get("OMLDM_E2E_PARTS", "8"))
     with tempfile.TemporaryDirectory() as root:
         br = FileBroker(root)
         br.create_topic("trainingData", parts)
@@ -231,10 +232,7 @@ def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dic
         # host time per tick of every stage (tick thread; ingest_* on the reader / staging
         # threads, which run beside it)
         stages = {k: round(v["host_ms"] / max(1, ticks), 4) for k, v in tracing.report().items()}
-        if job.fserver is not None:
-            job.fserver.close()
-        job.ingest.close()
-        job.egress.close()
+        job.close()
     return {"records_per_s": round(n / max(wall, 1e-9), 1), "records": n,
             "spokes": job.spokes, "batch": batch, "ticks": ticks,
             "ms_per_tick": round(wall * 1e3 / max(1, ticks), 4), "stage_ms_per_tick": stages,
