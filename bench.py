@@ -177,8 +177,10 @@ def engine_e2e_rate(records: int, batch: int = 131072, fmt: str = "json") -> dic
     from omldm_amd.utils.config import JobConfig
 
     sp = FeatureSpace(13, 0, 26, 1 << 20, field_aware=True)
-    # partitions are read concurrently (one GIL-free pread each; 8 MB regions)
-    parts = int(os.environ.get("OMLDM_E2E_PARTS", "8"))
+    # partitions are read concurrently (one GIL-free pread each; 8 MB regions): one per
+    # spoke of the reference's parallelism (16: JSON 93.7 / DIB 250 M records/s vs 91.6 /
+    # 241 M with 8, profiles/round5/e2e/parts_*.json)
+    parts = int(os.environ.get("OMLDM_E2E_PARTS", "16"))
     with tempfile.TemporaryDirectory() as root:
         br = FileBroker(root)
         br.create_topic("trainingData", parts)
