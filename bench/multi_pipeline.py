@@ -121,8 +121,7 @@ def main(argv=None) -> int:
             for st in streams:
                 main.wait_stream(st)
         comm.all_reduce_coalesced_(bufs, tag="sync")
-        for p in protos:
-            p.finish()
+        Synchronous.finish_group(protos)
 
     def sync():
         if on_gpu:

@@ -771,9 +771,9 @@ __global__ __launch_bounds__(256) void linear_predict_kernel(
 //   w = (a·w + D) / n,  a = D[dim] = Σσ/P, n = D[dim+1] = Σ1/P  (n == 0: no change);
 // D[0:dim] = 0 (D[dim:dim+2] are overwritten by the next round's finish kernel);
 // optional bf16 shadow of w for the gathers of the next round.
-__global__ __launch_bounds__(256) void linear_apply_kernel(float* __restrict__ w32,
-                                                           __hip_bfloat16* __restrict__ w16,
-                                                           float* __restrict__ dacc, int dim) {
+__device__ __forceinline__ void linear_apply_body(float* __restrict__ w32,
+                                                  __hip_bfloat16* __restrict__ w16,
+                                                  float* __restrict__ dacc, int dim) {
   const float n = dacc[dim + 1];
   const float a = n > 0.f ? dacc[dim] : 1.f;
   const float r = n > 0.f ? 1.f / n : 1.f;
@@ -803,6 +803,26 @@ __global__ __launch_bounds__(256) void linear_apply_kernel(float* __restrict__ w
     dacc[i] = 0.f;
     if (w16) w16[i] = __float2bfloat16(v);
   }
+}
+
+__global__ __launch_bounds__(256) void linear_apply_kernel(float* __restrict__ w32,
+                                                           __hip_bfloat16* __restrict__ w16,
+                                                           float* __restrict__ dacc, int dim) {
+  linear_apply_body(w32, w16, dacc, dim);
+}
+
+// M models of one dimension in one launch (grid.y = model): the pipelines of one fused
+// round (BASELINE config 5) — M launches of ~5 µs each, with the gaps between them, were
+// ~85 µs of a 16-pipeline step.
+constexpr int kApplyMaxM = 16;
+struct ApplyPtrs {
+  float* w32[kApplyMaxM];
+  __hip_bfloat16* w16[kApplyMaxM];
+  float* dacc[kApplyMaxM];
+};
+__global__ __launch_bounds__(256) void linear_apply_multi_kernel(ApplyPtrs P, int dim) {
+  const int m = blockIdx.y;
+  linear_apply_body(P.w32[m], P.w16[m], P.dacc[m], dim);
 }
 
 // Key range [lo, hi) of the accumulator that reduce part `part` of `parts` completes:
@@ -1124,6 +1144,23 @@ OMLDM_API int omldm_linear_predict(const void* w, int w_bf16, long long wstride,
   if (F <= 128) return dispatch_predict<2>(w, w_bf16, wstride, M, num, num_bf16, dn, cat, dc, B, dim, bias, cspan, wscale, out, st);
   if (F <= 256) return dispatch_predict<4>(w, w_bf16, wstride, M, num, num_bf16, dn, cat, dc, B, dim, bias, cspan, wscale, out, st);
   return -2;
+}
+
+OMLDM_API int omldm_linear_apply_multi(int M, float* const* w32, void* const* w16,
+                                       float* const* dacc, int dim, void* stream) {
+  if (M < 1 || M > kApplyMaxM) return -2;
+  ApplyPtrs P{};
+  for (int m = 0; m < M; ++m) {
+    P.w32[m] = w32[m];
+    P.w16[m] = static_cast<__hip_bfloat16*>(w16[m]);
+    P.dacc[m] = dacc[m];
+  }
+  int blocks = (dim / 4 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(linear_apply_multi_kernel, dim3(blocks, M), dim3(256), 0,
+                     (hipStream_t)stream, P, dim);
+  return (int)hipGetLastError();
 }
 
 OMLDM_API int omldm_linear_apply(float* w32, void* w16, float* dacc, int dim, void* stream) {

@@ -517,8 +517,8 @@ class Job:
                     buf = pipe.protocol.local_done()
                     if self.world > 1:
                         groups.setdefault(pipe.protocol.hubs, []).append((pipe, buf))
-                    else:
-                        pipe.protocol.finish()
+                if self.world == 1:  # the group's models averaged in one launch
+                    Synchronous.finish_group([p.protocol for p in grp])
         rest = [pid for pid in sorted(self.pipes) if pid not in done]
         # several pipelines: each trains on its own stream (a linear pipeline's exact scan
         # occupies 16 CUs, so M of them run side by side), joined before the collectives
@@ -548,8 +548,11 @@ class Job:
                 if self._coll_timer is not None:
                     self._coll_timer.stop(nbytes=sum(b.numel() * b.element_size()
                                                      for _, b in items))
+            syn = [pipe.protocol for pipe, _ in items if isinstance(pipe.protocol, Synchronous)]
+            Synchronous.finish_group(syn)
             for pipe, _ in items:
-                pipe.protocol.finish()
+                if not isinstance(pipe.protocol, Synchronous):
+                    pipe.protocol.finish()
 
     def _fused_groups(self, routed) -> list:
         """Pipelines whose rounds share one launch: ≥ 2 hashed-linear Synchronous pipelines

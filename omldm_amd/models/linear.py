@@ -248,8 +248,8 @@ class LinearLearner(Learner):
         for lr in learners:
             lr._seq_pending = False
             lr.steps += R
-            if not ctx.fused_delta:
-                lr.apply_delta()
+        if not ctx.fused_delta:  # the models averaged in one launch
+            LinearLearner.apply_delta_group(learners)
 
     def fit(self, batch: HashedBatch, ctx: RoundContext) -> None:
         if isinstance(batch, RawBatch):
@@ -280,6 +280,23 @@ class LinearLearner(Learner):
 
     def delta_buffer(self) -> torch.Tensor:
         return self.dacc
+
+    @staticmethod
+    def apply_delta_group(learners: list) -> None:
+        """``apply_delta`` of every learner; the plain averages (equal dimension) in one
+        launch."""
+        plain = [lr for lr in learners if not (lr._seq_pending and lr.replicas is not None)]
+        dims = {int(lr.w.shape[0]) for lr in plain}
+        if len(plain) > 1 and len(dims) == 1 and plain[0].w.is_cuda:
+            L.linear_apply_multi([lr.w for lr in plain], [lr.w16 for lr in plain],
+                                 [lr.dacc for lr in plain])
+            for lr in plain:
+                lr._rep_valid = False
+            rest = [lr for lr in learners if lr not in plain]
+        else:
+            rest = learners
+        for lr in rest:
+            lr.apply_delta()
 
     def apply_delta(self) -> None:
         if self._seq_pending and self.replicas is not None:

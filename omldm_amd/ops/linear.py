@@ -217,6 +217,24 @@ def linear_apply(w32: torch.Tensor, w16: torch.Tensor | None, dacc: torch.Tensor
         native.host().omldm_cpu_linear_apply(ptr(w32), ptr(w16), ptr(dacc), dim)
 
 
+def linear_apply_multi(w32s: list, w16s: list, daccs: list) -> None:
+    """``linear_apply`` of M equal-size models in one launch (GPU; M ≤ 16 per launch)."""
+    import ctypes
+
+    dim = int(w32s[0].shape[0])
+    if not w32s[0].is_cuda:
+        for w, w16, d in zip(w32s, w16s, daccs):
+            linear_apply(w, w16, d)
+        return
+    for i in range(0, len(w32s), 16):
+        ws, hs, ds = w32s[i:i + 16], w16s[i:i + 16], daccs[i:i + 16]
+        M = len(ws)
+        P = lambda ts: (ctypes.c_void_p * M)(*[ptr(t) for t in ts])  # noqa: E731
+        check(native.hip().omldm_linear_apply_multi(M, P(ws), P(hs), P(ds), dim,
+                                                    native.stream_of(ws[0])),
+              "omldm_linear_apply_multi")
+
+
 def linear_predict(w: torch.Tensor, batch: HashedBatch, wscale: torch.Tensor | None = None,
                    out: torch.Tensor | None = None, bias: bool = True) -> torch.Tensor:
     """Scores for every (point, model): w is [dim] or [M, dim]; returns [B] or [B, M]."""

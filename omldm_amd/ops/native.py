@@ -53,6 +53,7 @@ HIP_SIGS = [
     ("omldm_linear_predict", i32, [vp, i32, i64, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32,
                                    vp, vp, vp]),
     ("omldm_linear_apply", i32, [vp, vp, vp, i32, vp]),
+    ("omldm_linear_apply_multi", i32, [i32, vp, vp, vp, i32, vp]),
     ("omldm_linear_seq_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32,
                                      vp, vp, i32, i32, f32, f32, f32, f32, i32, vp]),
     ("omldm_linear_seq_apply", i32, [vp, vp, i32, vp, i32, vp]),

@@ -215,16 +215,34 @@ class Synchronous(Protocol):
         """This round may run inside a multi-pipeline launch (not the pipelined sync)."""
         return self.learner.supports_fused_delta and not self._pipelined()
 
-    def finish(self) -> None:
+    def finish(self, applied: bool = False) -> None:
+        """Phase 2: the summed buffer into the model (``applied``: ``finish_group`` already
+        averaged this learner's delta in its shared launch)."""
         L, buf = self.learner, self._buf
         if L.supports_fused_delta:
-            L.apply_delta()
+            if not applied:
+                L.apply_delta()
         else:
             M.fold_reload(self._E, buf, self._scale(), L.state_vector())  # E += s·Σd ; x = E
             L.on_state_loaded()
         self._account_model_sync(L.num_params(), buf.numel() * buf.element_size())
         self._buf = None
         self.stats.rounds += 1
+
+    @staticmethod
+    def finish_group(protos: list) -> None:
+        """``finish`` of several Synchronous pipelines; the hashed-linear models among them
+        are averaged in ONE launch (ops.linear.linear_apply_multi; BASELINE config 5: 16
+        apply launches and their gaps were ~85 µs of a 16-pipeline step)."""
+        from omldm_amd.models.linear import LinearLearner
+
+        lin = [p for p in protos if isinstance(p.learner, LinearLearner)
+               and p.learner.supports_fused_delta]
+        if len(lin) > 1:
+            LinearLearner.apply_delta_group([p.learner for p in lin])
+        done = {id(p) for p in lin} if len(lin) > 1 else set()
+        for p in protos:
+            p.finish(applied=id(p) in done)
 
     def _pipelined(self) -> bool:
         L = self.learner
