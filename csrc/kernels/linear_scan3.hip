@@ -2112,7 +2112,8 @@ __global__ __launch_bounds__(256) void s3mc_scatter_kernel(
     const int tid = threadIdx.x;
     for (int i = tid; i < K * KN; i += 256) {
       const int c = i / KN, j = i - c * KN;
-      if (j >= dn + (bias ? 1 : 0)) continue;
+      // dacc holds nclass rows: the padded classes (K > nclass) have none
+      if (j >= dn + (bias ? 1 : 0) || c >= nclass) continue;
       float v = 0.f;
       for (int s = 0; s < S_act; ++s) v += wsd[((size_t)s * K + c) * s3::DS + j];
       const int key = j < dn ? j : dim - 1;

@@ -508,3 +508,30 @@ def test_gpu_scan3_prep_ready_word_never_set_fails_loudly():
     L.linear_scan3_round(lrn.w, batch, R, S, dacc, rule, 0.5)
     torch.cuda.synchronize()
     assert h.omldm_scan3_comb_err() == 3
+
+
+@gpu
+def test_gpu_multiclass_scan3_padded_classes_stay_inside_the_accumulator():
+    """nClasses = 3 runs the K = 4 kernel (one padded class). The accumulator holds 3 rows;
+    the scatter's dense row must not touch a 4th: here dacc is a view with a guard region of
+    −0.0 after it (a stray `+= 0` would flip those to +0.0). The round-5 engine tests with 3
+    classes faulted intermittently on that write past the end of dacc."""
+    from omldm_amd.io.synthetic import synth_batch
+    from omldm_amd.ops import dense as D
+
+    dev = _cuda()
+    space = FeatureSpace(13, 0, 26, 1 << 16, field_aware=True)
+    nclass, S, R = 3, 4, 256
+    b = synth_batch(space, S * R, task=2, n_classes=nclass, seed=5).to(dev)
+    W = torch.zeros((nclass, space.dim), dtype=torch.float32, device=dev)
+    Wt = D.proto_shadow(W)
+    buf = torch.full(((nclass + 1) * space.dim,), -0.0, dtype=torch.float32, device=dev)
+    dacc = buf[: nclass * space.dim].view(nclass, space.dim)
+    dacc.zero_()
+    stats = torch.zeros(8, dtype=torch.float32, device=dev)
+    assert D.multiclass_scan3_fits(b, R, nclass, True, Wt)
+    D.multiclass_scan3_round(Wt, b, R, S, nclass, 1, 1.0, True, dacc, stats)
+    torch.cuda.synchronize()
+    guard = buf[nclass * space.dim:]
+    assert bool(torch.signbit(guard).all()), "the scatter wrote past the accumulator"
+    assert float(dacc.abs().sum()) > 0
