@@ -139,13 +139,14 @@ class KMeans(Learner):
     """Online k-means. Runs in SingleLearner mode (the reference forces it for K-means:
     omldm/operators/spoke/FlinkSpoke.scala:203-209).
 
-    ``mode: "sequential"`` (default for k ≤ 64, d ≤ 64): the reference learner's exact
-    per-point update — each training point, in stream order, moves its nearest centroid by
-    c ← c + (x − c)/n_c; the first k points seed the centroids (csrc/kernels/kmeans_seq.hip:
-    one wavefront holds the model in registers). ``mode: "minibatch"``: assignments of a
-    whole micro-batch against the batch-start centroids on the matrix cores, then
-    c ← (n·c + Σx)/(n + m) (the same update summed over the batch; tests pin its quality
-    gap against the sequential form)."""
+    ``mode: "sequential"`` (the default, at any k and d ≤ 8192): the reference learner's
+    exact per-point update — each training point, in stream order, moves its nearest
+    centroid by c ← c + (x − c)/n_c; the first k points seed the centroids
+    (csrc/kernels/kmeans_seq.hip: k ≤ 64 on one wavefront, G lanes per centroid; k ≤ 1024
+    on four waves exchanging their minima through LDS; past the LDS the centroids stay in
+    HBM). ``mode: "minibatch"``: assignments of a whole micro-batch against the batch-start
+    centroids on the matrix cores, then c ← (n·c + Σx)/(n + m) (the same update summed over
+    the batch; tests pin its quality gap against the sequential form)."""
 
     NAME = "K-means"
     TASK = "clustering"

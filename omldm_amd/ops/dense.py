@@ -184,13 +184,20 @@ def kmeans_seq(x: torch.Tensor, y: torch.Tensor | None, cent: torch.Tensor, n: t
               "omldm_cpu_kmeans_seq")
 
 
+def kmeans_seq_form(form: int = -1) -> int:
+    """GPU form of the exact sequential k-means: 1 = the fast one-wave kernel (every lane on
+    the per-point chain: G lanes per centroid or CPL centroids per lane, packed fp32, LDS
+    broadcast points; k ≤ 512, d ≤ 64), 0 = the earlier one-wave / workgroup kernels.
+    ``form`` < 0 only reads the current setting (default 1; env OMLDM_KMEANS_FAST=0)."""
+    return int(native.hip().omldm_kmeans_seq_form(int(form)))
+
+
 def kmeans_seq_fits(d: int, k: int) -> bool:
-    """The exact sequential kernel takes (d, k): one wavefront for k, d ≤ 64; a workgroup
-    with the centroids in LDS up to k ≤ 1024, d ≤ 256 (k·(d + 1) floats in 160 KiB)."""
-    if 1 <= d <= 64 and 1 <= k <= 64:
-        return True
-    nw = 4 if -(-k // 64) <= 4 else 16  # (kmeans_seq.hip: kmeans_wg_lds)
-    return 1 <= d <= 256 and 1 <= k <= 1024 and (k * (d + 1) + 64 * d + 64 + 2 * nw + 1) * 4 <= 160 << 10
+    """The exact sequential kernels take every (d, k) with d ≤ 8192
+    (csrc/kernels/kmeans_seq.hip): one wave for k ≤ 64 (G lanes per centroid), four waves
+    for k ≤ 1024 (d ≤ 64), the LDS workgroup form up to k·(d + 1) floats in 160 KiB, and
+    the HBM-resident form past that."""
+    return 1 <= d <= 8192 and k >= 1
 
 
 def kmeans_apply(cent: torch.Tensor, n: torch.Tensor, sums: torch.Tensor, counts: torch.Tensor,

@@ -130,6 +130,7 @@ HIP_SIGS = [
     ("omldm_holdout_route", i32, [vp, vp, vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, i64, i64,
                                   i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp]),
     ("omldm_kmeans_seq_fits", i32, [i32, i32]),
+    ("omldm_kmeans_seq_form", i32, [i32]),
     ("omldm_kmeans_seq", i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     ("omldm_ipc_alloc", vp, [i64]),
     ("omldm_ipc_free", i32, [vp]),

@@ -83,11 +83,24 @@ def test_learner_default_is_sequential_and_minibatch_gap_is_pinned():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,k", [(3, 4), (13, 8), (20, 33), (64, 64), (100, 20), (13, 200),
-                                 (128, 200)])
-def test_gpu_kernel_equals_cpu_oracle(d, k):
-    """The one-wave kernel (k, d ≤ 64) and the workgroup kernel (centroids in LDS, up to
-    k = 1024, d = 256) against the CPU MacQueen oracle."""
+@pytest.mark.parametrize("form", [1, 0])
+@pytest.mark.parametrize("d,k", [(3, 4), (13, 8), (13, 16), (20, 33), (64, 64), (100, 20),
+                                 (13, 200), (13, 256), (30, 100), (5, 500), (2, 3), (40, 2),
+                                 (128, 200), (13, 1500), (300, 40)])
+def test_gpu_kernel_equals_cpu_oracle(d, k, form):
+    """Both GPU forms against the CPU MacQueen oracle: form 1 = the fast one-wave kernel
+    (G lanes per centroid / CPL centroids per lane; k ≤ 512, d ≤ 64, else the workgroup
+    kernel), form 0 = the earlier one-wave kernel (k, d ≤ 64) and the workgroup kernel
+    (centroids in LDS, up to k = 1024, d = 256). Same assignments (equal counts)."""
+    prev = D.kmeans_seq_form()
+    D.kmeans_seq_form(form)
+    try:
+        _gpu_vs_oracle(d, k)
+    finally:
+        D.kmeans_seq_form(prev)
+
+
+def _gpu_vs_oracle(d, k):
     x, y = _blobs(20000, d, k, seed=7 * d + k)
     out = {}
     for dev in ("cpu", "cuda"):
