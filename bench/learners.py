@@ -64,6 +64,7 @@ P16_CASES = [
     ("NN", 0, {"hiddenLayers": [64, 64]}, 16),
     ("HT", 2, {"nClasses": 4}, 16),                     # per-point split checks (default)
     ("HT@check1024", 2, {"nClasses": 4, "checkEvery": 1024}, 16),
+    ("HT@hostloop", 2, {"nClasses": 4, "exactDevice": False}, 16),  # the host-driven A/B
     ("K-means@k256", 0, {"k": 256}, 16),               # the workgroup form (k > 64)
 ]
 

@@ -258,8 +258,9 @@ OMLDM_HOST_API void omldm_cpu_linear_apply(float* w32, uint16_t* w16, float* dac
   const float n = dacc[dim + 1];
   const float a = n > 0.f ? dacc[dim] : 1.f;
   const float r = n > 0.f ? 1.f / n : 1.f;
+  const bool keep = !(n < 0.f);  // n < 0: a round its kernel marked failed (discarded)
   for (int i = 0; i < dim; ++i) {
-    const float v = (a * w32[i] + dacc[i]) * r;
+    const float v = (a * w32[i] + (keep ? dacc[i] : 0.f)) * r;
     w32[i] = v;
     dacc[i] = 0.f;
     if (w16) {

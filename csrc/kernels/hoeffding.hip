@@ -602,6 +602,338 @@ __global__ __launch_bounds__(256) void ht_route_kernel(
   out[row] = ht_route(x + (size_t)row * d, feat, thr, left, right, depth);
 }
 
+// ---- exact per-point VFDT in one persistent launch (models/dense.py HT._fit_exact) -------
+// The reference learner checks a leaf at the very point it reaches gracePeriod points since
+// its last check (FlinkSpoke.scala:92-107: one point at a time). Between two such due points
+// every row's update is an order-free sum into its leaf, so one workgroup of 1024 threads
+// walks the tick in chunks of 1024 rows (one per thread):
+//  * the chunk's rows are staged in LDS and routed through the LDS copy of the tree;
+//  * each row's rank among the chunk's training rows of its leaf, in stream order (per-wave
+//    ballots, then a per-leaf prefix over the 16 waves);
+//  * the first due row = the lowest row whose rank since the segment start reaches its
+//    leaf's remaining grace (a ballot + one LDS atomic min);
+//  * the segment [start, due row] is added to the leaves' statistics (rows aggregated per
+//    (leaf, class) in the wave, one atomic per statistic), then the due leaf is checked by
+//    the whole workgroup (nBins candidate thresholds per feature, Hoeffding test) and, on a
+//    split, the chunk restarts after the due row under the new tree.
+// No host round trip and no synchronisation per segment (the host loop it replaces did
+// ~650 segments per 131072-row tick, each with .item() syncs). Statistics written by
+// atomics (L2) are read back with agent-scope loads (no stale L1 lines).
+constexpr int kHxNT = 1024;  // threads = rows per chunk
+
+struct HxTree {
+  float *feat, *thr, *left, *right, *cc, *S0, *S1, *S2, *lo, *hi, *since, *nnodes;
+};
+
+__device__ __forceinline__ float ld_l2(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void split_mass_l2(const HxTree& T, size_t base, int C, float t,
+                                              float* lm, float* rm) {
+  for (int c = 0; c < C; ++c) {
+    const float n = ld_l2(T.S0 + base + c);
+    const float nn = fmaxf(n, 1.f);
+    const float mu = ld_l2(T.S1 + base + c) / nn;
+    const float var = fmaxf(ld_l2(T.S2 + base + c) / nn - mu * mu, 1e-6f);
+    const float z = (t - mu) * rsqrtf(var);
+    const float cdf = 0.5f * (1.f + erff(z * 0.70710678f));
+    lm[c] = n * cdf;
+    rm[c] = n - lm[c];
+  }
+}
+
+size_t ht_exact_lds(int N, int d, int nb, bool stage) {
+  size_t b = (size_t)N * 16 + (size_t)N * 8 + (((size_t)16 * N + 15) & ~(size_t)15) +
+             (size_t)((d * nb + 3) & ~3) * 4;
+  if (stage) b += (size_t)kHxNT * d * 4;
+  return b;
+}
+
+__global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
+    const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int C, int depth,
+    int N, int nb, float grace, float delta, float tau, HxTree T, int stage_x,
+    double* __restrict__ nfit, unsigned long long* __restrict__ dbg) {
+  // dbg (diagnostics, may be null): [0] chunks staged, [1] segments, [2] split checks that
+  // split, [3] cycles in chunk setup, [4] cycles in due search, [5] cycles in statistics,
+  // [6] cycles in split checks
+  unsigned long long t_setup = 0, t_due = 0, t_stat = 0, t_split = 0, n_chunk = 0, n_seg = 0,
+                     n_split = 0;
+  extern __shared__ __attribute__((aligned(16))) unsigned char hx_smem[];
+  int4* tn = reinterpret_cast<int4*>(hx_smem);                 // [N] feat, thr, left, right
+  float* since_l = reinterpret_cast<float*>(tn + N);           // [N]
+  int* consumed = reinterpret_cast<int*>(since_l + N);         // [N] rows of the chunk added
+  unsigned char* cntw = reinterpret_cast<unsigned char*>(consumed + N);  // [16][N]
+  float* gains = reinterpret_cast<float*>(cntw + ((16 * N + 15) & ~15));  // [d·nb]
+  float* xs = gains + ((d * nb + 3) & ~3);                     // [kHxNT][d] when staged
+  __shared__ int s_first, s_leaf, s_flag, s_nn;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int n = tid; n < N; n += kHxNT) {
+    tn[n] = make_int4((int)T.feat[n], __float_as_int(T.thr[n]), (int)T.left[n], (int)T.right[n]);
+    since_l[n] = T.since[n];
+  }
+  if (tid == 0) s_nn = (int)T.nnodes[0];
+  __syncthreads();
+  float myfit = 0.f;
+  int c0 = 0;
+  while (c0 < B) {  // (uniform)
+    unsigned long long tc = __builtin_amdgcn_s_memtime();
+    ++n_chunk;
+    const int r = c0 + tid;
+    const bool inb = r < B;
+    const float yr = inb ? yv[r] : 0.f;
+    const bool valid = inb && !__builtin_isnan(yr);
+    int yi = valid ? (int)yr : 0;
+    yi = yi < 0 ? 0 : (yi >= C ? C - 1 : yi);
+    const int cend = min(c0 + kHxNT, B);  // exclusive
+    if (stage_x)
+      for (int e = tid; e < (cend - c0) * d; e += kHxNT) xs[e] = x[(size_t)c0 * d + e];
+    for (int e = tid; e < 16 * N; e += kHxNT) cntw[e] = 0;
+    for (int n = tid; n < N; n += kHxNT) consumed[n] = 0;
+    __syncthreads();
+    const float* xr = stage_x ? xs + (size_t)tid * d : x + (size_t)(inb ? r : 0) * d;
+    int leaf = 0;
+    if (inb) {
+      for (int it = 0; it <= depth; ++it) {
+        const int4 t = tn[leaf];
+        if (t.x < 0) break;
+        leaf = xr[t.x] <= __int_as_float(t.y) ? t.z : t.w;
+      }
+    }
+    // the row's rank among the chunk's training rows of its leaf (stream order)
+    int rank = 0;
+    {
+      unsigned long long pending = __ballot(valid);
+      const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+      while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const int L = __shfl(leaf, leader);
+        const unsigned long long m = __ballot(valid && leaf == L);
+        pending &= ~m;
+        if (valid && leaf == L) rank = __popcll(m & below);
+        if (lane == leader) cntw[w * N + L] = (unsigned char)__popcll(m);
+      }
+    }
+    __syncthreads();
+    if (valid)
+      for (int w2 = 0; w2 < w; ++w2) rank += cntw[w2 * N + leaf];
+    int base = c0;
+    bool restart = false;
+    t_setup += __builtin_amdgcn_s_memtime() - tc;
+    while (true) {
+      tc = __builtin_amdgcn_s_memtime();
+      ++n_seg;
+      bool due = false;
+      if (valid && r >= base) {
+        const float rem = ceilf(grace - since_l[leaf]);
+        const int need = rem < 1.f ? 1 : (int)rem;
+        due = rank - consumed[leaf] + 1 == need;
+      }
+      if (tid == 0) s_first = 0x7fffffff;
+      __syncthreads();
+      const unsigned long long dm = __ballot(due);
+      if (dm && lane == 0) atomicMin(&s_first, c0 + w * 64 + __ffsll((long long)dm) - 1);
+      __syncthreads();
+      const int first = s_first;
+      const int last = first == 0x7fffffff ? cend - 1 : first;  // inclusive
+      const bool seg = valid && r >= base && r <= last;
+      if (r == first) s_leaf = leaf;
+      t_due += __builtin_amdgcn_s_memtime() - tc;
+      tc = __builtin_amdgcn_s_memtime();
+      // the segment's rows into their leaves' statistics: the wave's first few (leaf, class)
+      // keys aggregated (one atomic per statistic: early on, every row of a wave shares a
+      // key and per-row atomics would serialise on it), the rest one atomic per row (a wave
+      // spread over many leaves: aggregating key by key cost ~3 K cycles per row)
+      {
+        const int key = seg ? leaf * C + yi : -1;
+        unsigned long long pending = __ballot(seg);
+        myfit += (float)(seg ? 1 : 0);
+        for (int it = 0; it < 3 && pending; ++it) {
+          const int leader = __ffsll((long long)pending) - 1;
+          const int k = __shfl(key, leader);
+          const bool mine = key == k;
+          const unsigned long long grp = __ballot(mine);
+          const int gn = __popcll(grp);
+          if (gn < 8 && it > 0) break;  // (a thin key: the per-row path is cheaper)
+          pending &= ~grp;
+          const float cnt = (float)gn;
+          const int nd = k / C, yc = k - nd * C;
+          if (lane == leader) {
+            atomicAdd(&T.cc[k], cnt);
+            atomicAdd(&since_l[nd], cnt);
+            atomicAdd(&consumed[nd], gn);
+          }
+          for (int f = 0; f < d; f += 2) {
+            const int fb = f + 1 < d ? f + 1 : f;
+            const float va = mine ? xr[f] : 0.f, vb = (mine && f + 1 < d) ? xr[fb] : 0.f;
+            float s1a = va, s1b = vb, s2a = va * va, s2b = vb * vb;
+            wave_sum2(s1a, s1b);
+            wave_sum2(s2a, s2b);
+            const float mna = wave_min(mine ? va : INFINITY), mxa = wave_max(mine ? va : -INFINITY);
+            const float mnb = wave_min(mine ? vb : INFINITY), mxb = wave_max(mine ? vb : -INFINITY);
+            if (lane == leader) {
+              const size_t o = ((size_t)nd * d + f) * C + yc;
+              atomicAdd(&T.S0[o], cnt);
+              atomicAdd(&T.S1[o], s1a);
+              atomicAdd(&T.S2[o], s2a);
+              atomic_min_f(&T.lo[nd * d + f], mna);
+              atomic_max_f(&T.hi[nd * d + f], mxa);
+              if (f + 1 < d) {
+                atomicAdd(&T.S0[o + C], cnt);
+                atomicAdd(&T.S1[o + C], s1b);
+                atomicAdd(&T.S2[o + C], s2b);
+                atomic_min_f(&T.lo[nd * d + f + 1], mnb);
+                atomic_max_f(&T.hi[nd * d + f + 1], mxb);
+              }
+            }
+          }
+        }
+        if ((pending >> lane) & 1ull) {  // the remaining rows: one atomic per statistic each
+          atomicAdd(&T.cc[key], 1.f);
+          atomicAdd(&since_l[leaf], 1.f);
+          atomicAdd(&consumed[leaf], 1);
+          for (int f = 0; f < d; ++f) {
+            const float v = xr[f];
+            const size_t o = ((size_t)leaf * d + f) * C + yi;
+            atomicAdd(&T.S0[o], 1.f);
+            atomicAdd(&T.S1[o], v);
+            atomicAdd(&T.S2[o], v * v);
+            atomic_min_f(&T.lo[leaf * d + f], v);
+            atomic_max_f(&T.hi[leaf * d + f], v);
+          }
+        }
+      }
+      if (first == 0x7fffffff) {
+        t_stat += __builtin_amdgcn_s_memtime() - tc;
+        break;
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the atomics landed in L2
+      __syncthreads();
+      t_stat += __builtin_amdgcn_s_memtime() - tc;
+      tc = __builtin_amdgcn_s_memtime();
+      // the due leaf's split check (ht_split_kernel's criterion, by the whole workgroup)
+      const int L = s_leaf;
+      float ccl[kHtMaxC];
+      float ntot = 0.f;
+      int nz = 0;
+      for (int c = 0; c < C; ++c) {
+        ccl[c] = ld_l2(T.cc + (size_t)L * C + c);
+        ntot += ccl[c];
+        nz += ccl[c] > 0.f;
+      }
+      bool split = false;
+      if (ntot < 2.f || nz < 2 || s_nn + 2 > N) {
+        __syncthreads();  // (every thread read since_l / s_nn above)
+        if (tid == 0) since_l[L] = 0.f;
+      } else {
+        const float h0 = entropy(ccl, C, ntot);
+        float lm[kHtMaxC], rm[kHtMaxC];
+        for (int p2 = tid; p2 < d * nb; p2 += kHxNT) {
+          const int f = p2 / nb, b = p2 - f * nb;
+          const float l = ld_l2(T.lo + (size_t)L * d + f), span = ld_l2(T.hi + (size_t)L * d + f) - l;
+          float g = -1.f;
+          if (span > 0.f) {
+            const float t = l + span * (float)(b + 1) / (float)(nb + 1);
+            split_mass_l2(T, ((size_t)L * d + f) * C, C, t, lm, rm);
+            float nl = 0.f, nr = 0.f;
+            for (int c = 0; c < C; ++c) {
+              nl += lm[c];
+              nr += rm[c];
+            }
+            g = h0 - (nl * entropy(lm, C, nl) + nr * entropy(rm, C, nr)) / fmaxf(nl + nr, 1e-12f);
+          }
+          gains[p2] = g;
+        }
+        __syncthreads();
+        if (w == 0) {
+          float g1 = -2.f, g2 = -2.f;
+          int f1 = 0x7fffffff, b1 = 0;
+          for (int f = lane; f < d; f += 64) {
+            float gm = -2.f;
+            int bm = 0;
+            for (int b = 0; b < nb; ++b) {
+              const float g = gains[f * nb + b];
+              bm = g > gm ? b : bm;
+              gm = g > gm ? g : gm;
+            }
+            if (gm > g1) {
+              g2 = g1;
+              g1 = gm;
+              f1 = f;
+              b1 = bm;
+            } else if (gm > g2) {
+              g2 = gm;
+            }
+          }
+#pragma unroll
+          for (int m = 1; m < 64; m <<= 1) {
+            const float og1 = __shfl_xor(g1, m), og2 = __shfl_xor(g2, m);
+            const int of1 = __shfl_xor(f1, m), ob1 = __shfl_xor(b1, m);
+            const bool take = og1 > g1 || (og1 == g1 && of1 < f1);
+            g2 = take ? fmaxf(g1, og2) : fmaxf(g2, og1);
+            g1 = take ? og1 : g1;
+            f1 = take ? of1 : f1;
+            b1 = take ? ob1 : b1;
+          }
+          if (lane == 0) {
+            if (d == 1) g2 = 0.f;
+            since_l[L] = 0.f;
+            const float R = __log2f((float)C);
+            const float eps = sqrtf(R * R * logf(1.f / delta) / (2.f * ntot));
+            int flag = 0;
+            if (g1 > 0.f && (g1 - g2 > eps || eps < tau)) {
+              const int old = s_nn;
+              const float l = ld_l2(T.lo + (size_t)L * d + f1);
+              const float span = ld_l2(T.hi + (size_t)L * d + f1) - l;
+              const float t = l + span * (float)(b1 + 1) / (float)(nb + 1);
+              split_mass_l2(T, ((size_t)L * d + f1) * C, C, t, lm, rm);
+              for (int c = 0; c < C; ++c) {
+                T.cc[(size_t)old * C + c] = lm[c];
+                T.cc[(size_t)(old + 1) * C + c] = rm[c];
+              }
+              T.thr[L] = t;
+              T.left[L] = (float)old;
+              T.right[L] = (float)(old + 1);
+              T.feat[L] = (float)f1;
+              T.nnodes[0] = (float)(old + 2);
+              tn[L] = make_int4(f1, __float_as_int(t), old, old + 1);
+              s_nn = old + 2;
+              flag = 1;
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            s_flag = flag;
+          }
+        }
+        __syncthreads();
+        split = s_flag != 0;
+      }
+      __syncthreads();
+      t_split += __builtin_amdgcn_s_memtime() - tc;
+      n_split += split;
+      base = first + 1;
+      if (split) {  // the rest of the chunk under the new tree
+        c0 = first + 1;
+        restart = true;
+        break;
+      }
+    }
+    if (!restart) c0 = cend;
+    __syncthreads();  // the chunk's LDS (rows, counts) is free
+  }
+  for (int n = tid; n < N; n += kHxNT) T.since[n] = since_l[n];
+  if (dbg && tid == 0) {
+    dbg[0] += n_chunk;
+    dbg[1] += n_seg;
+    dbg[2] += n_split;
+    dbg[3] += t_setup;
+    dbg[4] += t_due;
+    dbg[5] += t_stat;
+    dbg[6] += t_split;
+  }
+  const float f = wave_sum(myfit);
+  if (lane == 0 && nfit && f > 0.f) atomicAdd(nfit, (double)f);
+}
+
 }  // namespace omldm
 
 using namespace omldm;
@@ -689,5 +1021,25 @@ OMLDM_API int omldm_ht_predict(const float* x, int B, int d, int C, int depth,
   if (B <= 0) return 0;
   hipLaunchKernelGGL(ht_predict_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      x, B, d, C, depth, tree[0], tree[1], tree[2], tree[3], tree[4], out);
+  return (int)hipGetLastError();
+}
+
+// The exact per-point VFDT over a tick in one launch (x [B, d] contiguous fp32, y [B]:
+// NaN = not a training point). -2: the LDS layout does not fit (the host falls back).
+OMLDM_API int omldm_ht_exact(const float* x, const float* y, int B, int d, int C, int depth,
+                             int N, int nb, float grace, float delta, float tau,
+                             float* const* tree, double* nfit, unsigned long long* dbg,
+                             void* stream) {
+  if (B <= 0) return 0;
+  if (C < 1 || C > kHtMaxC || nb < 1 || d < 1) return -1;
+  const bool stage = ht_exact_lds(N, d, nb, true) <= 160 * 1024;
+  const size_t lds = ht_exact_lds(N, d, nb, stage);
+  if (lds > 160 * 1024 - 64) return -2;
+  const int e = check_dyn_lds((const void*)ht_exact_kernel, lds);
+  if (e) return e;
+  HxTree T{tree[0], tree[1], tree[2], tree[3], tree[4], tree[5],
+           tree[6], tree[7], tree[8], tree[9], tree[10], tree[11]};
+  hipLaunchKernelGGL(ht_exact_kernel, dim3(1), dim3(kHxNT), lds, (hipStream_t)stream, x, y, B, d,
+                     C, depth, N, nb, grace, delta, tau, T, (int)stage, nfit, dbg);
   return (int)hipGetLastError();
 }

@@ -1617,6 +1617,11 @@ __device__ void s3_dense_body(const float* __restrict__ ws,
   // shrinking rules: spoke s ends at σ_s·(w0 + δ_s): dacc gets Σ σ_s·δ_s and the apply's
   // coefficient of w0, dacc[dim] = Σ σ_s (linear_apply: w = (dacc[dim]·w + dacc)/dacc[dim+1])
   const int tid = threadIdx.x;
+  // a round whose launch recorded a failed bounded wait (a prep that never signalled, a
+  // combiner or helper that gave up) scanned stale or partial data: the apply discards it
+  // (dacc[dim+1] < 0: w unchanged, dacc cleared; a large negative survives a cross-rank
+  // sum, so every rank discards) and its statistics are not counted
+  const bool bad = __hip_atomic_load(&g_s3_comb_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   for (int i = tid; i < dn; i += 256) {
     float v = 0.f;
     for (int s = 0; s < S_act; ++s) v += wsd[(size_t)s * s3::DS + i] * (sig ? sig[s] : 1.f);
@@ -1629,9 +1634,9 @@ __device__ void s3_dense_body(const float* __restrict__ ws,
     for (int s = 0; s < S_act; ++s) a += sig ? sig[s] : 1.f;
     dacc[dim - 1] = v * inv_p;
     dacc[dim] = a * inv_p;
-    dacc[dim + 1] = (float)S_act * inv_p;
+    dacc[dim + 1] = bad ? -1e30f : (float)S_act * inv_p;
   }
-  if (cum && tid < 6 && tid != 4) {
+  if (cum && !bad && tid < 6 && tid != 4) {
     double t = 0.0;
     for (int s = 0; s < S_act; ++s) t += (double)ws[(size_t)s * s3::WS + tid];
     cum[tid] += t;
@@ -2280,7 +2285,10 @@ OMLDM_API int omldm_scan3_comb_err() {
 // of a pinned host word) and cleared, in stream order and without a host sync: the engine
 // reads the word a tick later (utils/health.py) and fails the job if it is set.
 __global__ void s3_err_drain_kernel(int* out) {
-  if (threadIdx.x == 0) out[0] |= atomicExch(&g_s3_comb_err, 0);
+  if (threadIdx.x == 0) {  // (the highest code: the waits are 1 combiner, 2 helper, 3 prep)
+    const int v = atomicExch(&g_s3_comb_err, 0);
+    out[0] = v > out[0] ? v : out[0];
+  }
 }
 
 OMLDM_API int omldm_scan3_comb_err_drain(int* out, void* stream) {
@@ -2545,6 +2553,15 @@ static int s3_run_impl(int M, const float* const* w, float* const* dacc, double*
   }
   S3Pipes pp{};
   pp.M = M;
+  // the in-launch wait for the prep's ready word only while the scan grid leaves most CUs
+  // to the prep's kernels (otherwise spinning LDS-heavy workgroups could hold the CUs the
+  // prep needs until the bounded wait gives up): past that, the stream waits on the word
+  if (wflag && (long long)M * s3_nper(S_act, rare, ncomb, cns) > ncu / 2) {
+    const hipError_t we = hipStreamWaitValue64(st, const_cast<unsigned long long*>(wflag),
+                                               wepoch, hipStreamWaitValueGte, ~0ull);
+    if (we != hipSuccess) return (int)we;
+    wflag = nullptr;
+  }
   pp.wflag = wflag;
   pp.wepoch = wepoch;
   pp.ncomb = ncomb > 0 ? ncomb : 0;

@@ -768,7 +768,8 @@ __global__ __launch_bounds__(256) void linear_predict_kernel(
 }
 
 // Model average over the round's active workers:
-//   w = (a·w + D) / n,  a = D[dim] = Σσ/P, n = D[dim+1] = Σ1/P  (n == 0: no change);
+//   w = (a·w + D) / n,  a = D[dim] = Σσ/P, n = D[dim+1] = Σ1/P  (n == 0: no change;
+//   n < 0: a round its kernel marked failed — w unchanged, D cleared);
 // D[0:dim] = 0 (D[dim:dim+2] are overwritten by the next round's finish kernel);
 // optional bf16 shadow of w for the gathers of the next round.
 __device__ __forceinline__ void linear_apply_body(float* __restrict__ w32,
@@ -777,6 +778,7 @@ __device__ __forceinline__ void linear_apply_body(float* __restrict__ w32,
   const float n = dacc[dim + 1];
   const float a = n > 0.f ? dacc[dim] : 1.f;
   const float r = n > 0.f ? 1.f / n : 1.f;
+  const bool keep = !(n < 0.f);  // (discard: D counts for nothing, NaN garbage included)
   const int n4 = dim >> 2;
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int stride = gridDim.x * blockDim.x;
@@ -784,7 +786,8 @@ __device__ __forceinline__ void linear_apply_body(float* __restrict__ w32,
   float4* d4 = reinterpret_cast<float4*>(dacc);
   for (int i = tid; i < n4; i += stride) {
     float4 wv = w4[i];
-    const float4 dv = d4[i];
+    float4 dv = d4[i];
+    if (!keep) dv = make_float4(0.f, 0.f, 0.f, 0.f);
     wv.x = fmaf(a, wv.x, dv.x) * r;
     wv.y = fmaf(a, wv.y, dv.y) * r;
     wv.z = fmaf(a, wv.z, dv.z) * r;
@@ -798,7 +801,7 @@ __device__ __forceinline__ void linear_apply_body(float* __restrict__ w32,
     }
   }
   for (int i = (n4 << 2) + tid; i < dim; i += stride) {
-    const float v = fmaf(a, w32[i], dacc[i]) * r;
+    const float v = fmaf(a, w32[i], keep ? dacc[i] : 0.f) * r;
     w32[i] = v;
     dacc[i] = 0.f;
     if (w16) w16[i] = __float2bfloat16(v);

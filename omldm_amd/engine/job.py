@@ -750,6 +750,11 @@ class Job:
         if behind:
             print(f"[omldm] rank {self.rank}: forecast lane behind after 5 s", flush=True)
         if self.checkpointer is not None and ckpt > 0:
+            if self._health is not None:
+                # this tick's device words first (blocking; the snapshot's host copy syncs
+                # anyway): a discarded round or a dropped update raises here, before a
+                # model it touched can be snapshotted and restored by a restart
+                self._health.check(block=True)
             self.egress.flush()  # outputs of the checkpointed ticks are in their topic
             self.checkpointer.save(self)
         self.ticks += 1

@@ -42,6 +42,12 @@ class Learner:
     supports_fused_delta = False
     supports_reduce_parts = False
 
+    def reduce_parts_apply(self, batch, ctx) -> bool:
+        """Whether this round's reduce really runs in key-range parts (the pipelined sync
+        starts each part's collective as soon as it is final); False when the round's kernel
+        completes the accumulator only at its end, so a parts split would be a no-op."""
+        return self.supports_reduce_parts
+
     def __init__(self, hyper: dict | None, space: FeatureSpace, device="cpu"):
         self.hyper = dict(hyper or {})
         self.space = space

@@ -505,6 +505,9 @@ class HT(Learner):
         # each due point: _fit_exact). checkEvery N > 0: due leaves are checked every N rows
         # (faster; tests/test_ht_sequential.py pins its gap to the per-point form)
         self.check_every = max(0, hp_int(self.hyper, "checkEvery", 0))
+        # exactDevice (default true): the exact mode's tick runs in one persistent launch;
+        # false keeps the host-driven segment loop (the A/B reference of the same semantics)
+        self.exact_device = str(self.hyper.get("exactDevice", False)).lower() not in ("0", "false")
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)
@@ -563,11 +566,12 @@ class HT(Learner):
         self._fit_part(batch)
 
     def _fit_exact(self, batch):
-        """Per-point VFDT checks on the device: rows are routed once, and the tick is cut
-        into segments that end exactly at the next row where some leaf reaches its grace
-        period (rows of each leaf in stream order: the (grace − since)-th training row of
-        the leaf). Each segment's statistics are added in one launch, then the due leaf is
-        checked; rows after a split are routed again."""
+        """Per-point VFDT checks: the tick is cut into segments that end exactly at the next
+        row where some leaf reaches its grace period (rows of each leaf in stream order: the
+        (grace − since)-th training row of the leaf); each segment's statistics are added,
+        then the due leaf is checked; rows after a split are routed again. GPU: the whole
+        loop is one persistent launch (D.ht_exact); the host-driven form below (one launch
+        per segment) is the CPU path and the A/B reference (exactDevice false)."""
         import numpy as np
 
         B = batch.B
@@ -575,6 +579,10 @@ class HT(Learner):
             return
         gpu = self.device.type == "cuda"
         x = batch.num.float().contiguous()
+        if gpu and self.exact_device and D.ht_exact(
+                x, batch.y, self.Cn, self.depth, self.N, self.nb, float(self.grace), self.delta,
+                self.tau, self._tree(), self.cum[1:2]):
+            return  # one persistent launch for the tick (csrc/kernels/hoeffding.hip)
         ok = (~torch.isnan(batch.y)).cpu().numpy()
         N, g = self.N, float(self.grace)
 

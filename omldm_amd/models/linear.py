@@ -120,6 +120,16 @@ class LinearLearner(Learner):
         R, _ = self._seq_geometry(batch.B, ctx) if ctx is not None else (batch.B, 1)
         return bool(batch.B) and L.scan3_eligible(batch, R, self.rule.bias)
 
+    def reduce_parts_apply(self, batch, ctx: RoundContext) -> bool:
+        """The spoke-table round reduces its tables in key-range parts; the v3 table scan
+        completes the accumulator only at its round end (no part is final earlier), so a
+        batch it takes runs one reduce and one collective."""
+        if not self.supports_reduce_parts:
+            return False
+        if isinstance(batch, RawBatch):
+            return not self.seq_capable(batch, ctx)
+        return self.group_key(batch, ctx) is None
+
     @staticmethod
     def _seq_geometry(B: int, ctx: RoundContext) -> tuple[int, int]:
         S = max(1, int(ctx.spokes))

@@ -146,7 +146,7 @@ def multiclass_round(W: torch.Tensor, batch: HashedBatch, R: int, S: int, nclass
         assert Wt.shape == (dim, class_pad(nclass)) and Wt.is_contiguous()
         from omldm_amd.ops.linear import spill_log2cap, spill_workspace
 
-        lg = spill_log2cap(R, dn + dc + 1)
+        lg = spill_log2cap(R, dn + dc + 1, S, class_pad(nclass))
         spill = spill_workspace(W.device, S, lg, class_pad(nclass))
         check(native.hip().omldm_multiclass_round(
             ptr(Wt), int(Wt.dtype == torch.bfloat16), ptr(num), int(num.dtype == torch.bfloat16),
@@ -484,6 +484,30 @@ def ht_split(N: int, d: int, C: int, nb: int, grace: float, delta: float, tau: f
              tree: list[torch.Tensor]) -> None:
     check(native.hip().omldm_ht_split(N, d, C, nb, grace, delta, tau, _tree_ptrs(tree),
                                       native.stream_of(tree[0])), "omldm_ht_split")
+
+
+def ht_exact(x: torch.Tensor, y: torch.Tensor, C: int, depth: int, N: int, nb: int,
+             grace: float, delta: float, tau: float, tree: list[torch.Tensor],
+             nfit: torch.Tensor | None, dbg: torch.Tensor | None = None) -> bool:
+    """The per-point VFDT over a whole tick in one persistent launch
+    (csrc/kernels/hoeffding.hip: ht_exact_kernel): each leaf is checked at the very row
+    where it reaches the grace period, no host round trip. False when the tree's LDS
+    layout does not fit (the caller keeps the host-driven segment loop). ``dbg``: an int64
+    [8] device tensor that accumulates chunks, segments, splits and the cycles of the
+    kernel's phases (diagnostics)."""
+    B, d = x.shape
+    if B == 0:
+        return True
+    x = x.float().contiguous()
+    y = y.float().contiguous()
+    assert nfit is None or nfit.dtype == torch.float64
+    rc = int(native.hip().omldm_ht_exact(ptr(x), ptr(y), B, d, C, depth, N, nb, float(grace),
+                                         float(delta), float(tau), _tree_ptrs(tree), ptr(nfit),
+                                         ptr(dbg), native.stream_of(x)))
+    if rc == -2:
+        return False
+    check(rc, "omldm_ht_exact")
+    return True
 
 
 def ht_route(x: torch.Tensor, depth: int, tree: list[torch.Tensor]) -> torch.Tensor:

@@ -62,10 +62,22 @@ def _workspace(device, n: int, key: str = "ws", per_stream: bool = True) -> torc
 _SPILL: dict = {}
 
 
-def spill_log2cap(R: int, keys_per_row: int) -> int:
+# HBM budget of one spill workspace (OMLDM_SPILL_BUDGET_MB, default 2 GiB of the 288 GB):
+# a MultiClassPA spill at R = 8192 with 16-float entries would otherwise take ~1.2 GB per
+# stream and up to 16 of them stay cached
+_SPILL_BUDGET = int(os.environ.get("OMLDM_SPILL_BUDGET_MB", "2048")) << 20
+
+
+def spill_log2cap(R: int, keys_per_row: int, S: int = 1, vk: int = 1) -> int:
     """HBM spill entries per spoke (log2): ≥ 2 × the spoke's key occurrences, so a spoke
-    whose every key missed its LDS table still finds room (load ≤ 1/2)."""
-    return max(6, min(24, (2 * max(1, R) * max(1, keys_per_row) - 1).bit_length()))
+    whose every key missed its LDS table still finds room (load ≤ 1/2), capped so the S
+    spokes' spill (entries of ``vk`` values) stays within the spill budget (keys past a
+    full spill are counted as overflow, which the engine's health check fails on)."""
+    lg = max(6, min(24, (2 * max(1, R) * max(1, keys_per_row) - 1).bit_length()))
+    words = native.hip().omldm_spill_words
+    while lg > 6 and int(words(int(S), lg, int(vk))) * 4 > _SPILL_BUDGET:
+        lg -= 1
+    return lg
 
 
 def spill_workspace(device, S: int, log2gcap: int, vk: int) -> torch.Tensor:
@@ -148,7 +160,7 @@ def linear_round(w: torch.Tensor, batch: HashedBatch, R: int, S: int, dacc: torc
         wsw = WS_STAT + num.shape[1] + 1
         ws = _workspace(w.device, S * wsw)
         tables = _workspace(w.device, S * ((1 << log2cap) + 64) * 2, key="tables")
-        lg = spill_log2cap(R, num.shape[1] + cat.shape[1] + 1)
+        lg = spill_log2cap(R, num.shape[1] + cat.shape[1] + 1, S, 1)
         spill = spill_workspace(w.device, S, lg, 1)
         dp = native.dptr
         rc = native.hip().omldm_linear_round(

@@ -117,6 +117,8 @@ HIP_SIGS = [
     ("omldm_ht_split", i32, [i32, i32, i32, i32, f32, f32, f32, vp, vp]),
     ("omldm_ht_predict", i32, [vp, i32, i32, i32, i32, vp, vp, vp]),
     ("omldm_ht_route", i32, [vp, i32, i32, i32, vp, vp, vp]),
+    ("omldm_ht_exact", i32, [vp, vp, i32, i32, i32, i32, i32, i32, f32, f32, f32, vp, vp, vp,
+                             vp]),
     ("omldm_drift_norms", i32, [vp, vp, i64, f32, vp, vp]),
     ("omldm_fold_reload", i32, [vp, vp, f32, vp, i64, vp]),
     ("omldm_elastic_pre", i32, [vp, vp, vp, vp, i64, vp]),

@@ -212,8 +212,9 @@ class Synchronous(Protocol):
         return self._buf
 
     def fusable(self) -> bool:
-        """This round may run inside a multi-pipeline launch (not the pipelined sync)."""
-        return self.learner.supports_fused_delta and not self._pipelined()
+        """This round may run inside a multi-pipeline launch (a v3 launch: its accumulator is
+        final only at the round end, so a reduceParts split never applies there)."""
+        return self.learner.supports_fused_delta
 
     def finish(self, applied: bool = False) -> None:
         """Phase 2: the summed buffer into the model (``applied``: ``finish_group`` already
@@ -244,13 +245,14 @@ class Synchronous(Protocol):
         for p in protos:
             p.finish(applied=id(p) in done)
 
-    def _pipelined(self) -> bool:
+    def _pipelined(self, batch) -> bool:
         L = self.learner
         return (self.reduce_parts > 1 and self.G > 1 and L.supports_fused_delta
-                and L.supports_reduce_parts and (self.hubs == 0 or self.hubs >= self.G))
+                and L.supports_reduce_parts and (self.hubs == 0 or self.hubs >= self.G)
+                and L.reduce_parts_apply(batch, self._ctx(fused=True)))
 
     def round(self, batch):
-        if self._pipelined():
+        if self._pipelined(batch):
             L, works = self.learner, []
             buf = L.delta_buffer()
 

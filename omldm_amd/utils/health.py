@@ -62,11 +62,16 @@ class DeviceHealth:
                 return  # still in flight: checked at the next arm / check
             ev.synchronize()
         self.event = None
-        if int(self.flag[0]):
+        code = int(self.flag[0])
+        if code:
             self.flag[0] = 0
+            what = {1: "an in-launch combiner timed out waiting for its spoke's granules",
+                    2: "a helper workgroup's bounded spin gave up",
+                    3: "the round's prep never set its ready word (the round waited for a "
+                       "prep that did not run)"}
             raise DeviceHealthError(
-                "v3 scan: an in-launch combiner timed out waiting for its spoke's granules "
-                "(linear_scan3.hip g_s3_comb_err); the round's update is incomplete")
+                f"v3 scan: {what.get(code, 'a bounded in-launch wait failed')} "
+                f"(linear_scan3.hip g_s3_comb_err = {code}); the round was discarded")
         bad = {pid: int(self.host[2 + i]) for i, pid in enumerate(self.pids)
                if float(self.host[2 + i]) != 0.0}
         if bad:

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Hoeffding tree: the persistent exact kernel vs the host-driven loop and the oracle, then
+# the P = 16 rates.
+set -u
+R=${GRAFT_REPO_ROOT:-$PWD}
+O=$R/gpurun_out/r6/ht
+mkdir -p $O
+cd $R
+timeout -k 10 400 python -u -m pytest tests/test_ht_sequential.py tests/test_kernels_dense.py -m gpu -x -q -k "ht or HT" --timeout 300 --timeout-method thread > $O/tests.txt 2>&1; rc=$?; tail -5 $O/tests.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench/learners.py --preset p16 --steps 5 --only HT > $O/learners.json 2> $O/learners.err || { tail -20 $O/learners.err; exit 3; }
+cat $O/learners.json

@@ -138,7 +138,7 @@ def test_config_reference_defaults_and_flags():
 
 
 def test_serde_helpers():
-    from omldm_amd.io.serde import (RecordMetadata, deserialize_data_instance,
+    from tests.serde_ref import (RecordMetadata, deserialize_data_instance,
                                     deserialize_request, serialize, string_to_doubles)
 
     md = RecordMetadata("trainingData", 3, None, 17, 1234)

@@ -197,3 +197,40 @@ def test_gpu_exact_mode_matches_the_cpu_exact_mode():
     assert res["cuda"][1] == res["cpu"][1], res
     assert abs(res["cuda"][0] - res["cpu"][0]) <= 2, res
     assert abs(res["cuda"][2] - res["cpu"][2]) <= 0.005, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,d", [(2, 6), (4, 6), (3, 13)])
+def test_gpu_persistent_exact_matches_the_host_driven_loop_and_the_oracle(C, d):
+    """The persistent one-launch exact mode (ht_exact_kernel) grows the tree the host-driven
+    segment loop grows (same split points, same nodes), and the per-point NumPy VFDT's."""
+    g = np.random.default_rng(7 + C)
+    X = g.uniform(-1, 1, size=(70000, d)).astype(np.float32)
+    y = ((X[:, 0] > 0.2).astype(int) + (X[:, 1] > -0.3).astype(int) * (C - 1)) % C
+    y = y.astype(np.float32)
+    flip = g.random(len(y)) < 0.05
+    y[flip] = g.integers(0, C, int(flip.sum()))
+    y[g.random(len(y)) < 0.02] = np.nan  # forecasting-like rows: not fitted
+    Xt = g.uniform(-1, 1, size=(6000, d)).astype(np.float32)
+    yt = (((Xt[:, 0] > 0.2).astype(int) + (Xt[:, 1] > -0.3).astype(int) * (C - 1)) % C)
+    sp = FeatureSpace(d, 0, 0, 1 << 8)
+    res = {}
+    for mode in (True, False):
+        ht = HT({"nClasses": C, "exactDevice": mode}, sp, "cuda")
+        _fit_ticks(ht, X, y, 65536)
+        torch.cuda.synchronize()
+        n = int(ht.nnodes.item())
+        res[mode] = (n, ht.feat[:n].cpu().numpy().copy(), ht.thr[:n].cpu().numpy().copy(),
+                     _acc(ht, Xt, yt.astype(np.float32)), int(ht.cum[1].item()))
+    dev, host = res[True], res[False]
+    assert dev[4] == host[4] == int((~np.isnan(y)).sum())
+    assert dev[0] == host[0], (dev[0], host[0])
+    assert np.array_equal(dev[1], host[1])
+    assert np.allclose(dev[2], host[2], rtol=1e-4, atol=1e-5)
+    assert abs(dev[3] - host[3]) <= 0.002
+    ora = VFDT(d, C)
+    for i in range(X.shape[0]):
+        if not np.isnan(y[i]):
+            ora.learn(X[i].astype(np.float64), y[i])
+    assert abs(dev[0] - ora.nnodes) <= 2, (dev[0], ora.nnodes)
+    assert int(dev[1][0]) == int(ora.feat[0])

@@ -505,8 +505,16 @@ def test_gpu_scan3_prep_ready_word_never_set_fails_loudly():
     sp.ready, sp.event = (never.data_ptr(), 1), None
     batch.prep = sp
     dacc = torch.zeros(space.dim + 2, dtype=torch.float32, device=dev)
+    w0 = lrn.w.clone()
     L.linear_scan3_round(lrn.w, batch, R, S, dacc, rule, 0.5)
     torch.cuda.synchronize()
+    # the round is discarded: the accumulator carries the failed mark, the apply leaves the
+    # model as it was and clears the accumulator (no stale-workspace update lands)
+    assert float(dacc[space.dim + 1]) < 0
+    L.linear_apply(lrn.w, None, dacc)
+    torch.cuda.synchronize()
+    assert torch.equal(lrn.w, w0)
+    assert float(dacc[: space.dim].abs().max()) == 0.0
     assert h.omldm_scan3_comb_err() == 3
 
 

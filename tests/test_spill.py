@@ -15,6 +15,7 @@ from omldm_amd.api.batch import FeatureSpace
 from omldm_amd.io.synthetic import synth_batch
 from omldm_amd.ops import dense as D
 from omldm_amd.ops import linear as L
+from omldm_amd.ops import native
 
 
 def test_spill_sizing():
@@ -129,3 +130,12 @@ def test_hip_engine_default_geometry_learner_matches_cpu(cuda, name, hyper, task
         models[str(dev)] = lr.state_vector().detach().float().cpu()
     np.testing.assert_allclose(models["cuda:0"].numpy(), models["cpu"].numpy(),
                                rtol=5e-3, atol=5e-5)
+
+
+def test_spill_is_capped_by_the_memory_budget():
+    """A MultiClassPA-sized spill (16 spokes, 8192 rows × 40 keys, 16-float entries) would
+    take ~1.2 GB per stream; the cap keeps one workspace within the budget."""
+    words = native.hip().omldm_spill_words
+    lg = L.spill_log2cap(8192, 40, 16, 16)
+    assert int(words(16, lg, 16)) * 4 <= L._SPILL_BUDGET
+    assert lg >= 6
