@@ -86,65 +86,139 @@ def shard_start(k: int, rank: int, world: int, B: int) -> int:
     return (k * world + rank) * B
 
 
-def engine_forecast_latency(n: int) -> dict:
+def engine_forecast_latency(n: int, train_records: int = 4_000_000) -> dict:
     """Record produced into the forecasting topic → its Prediction in the predictions
-    topic, through the engine (Job + per-record forecast lane on the resident serving
-    wave, engine/forecast_server.py) with a trained linear SVM pipeline."""
-    import uuid
+    topic, through the engine with a trained linear SVM pipeline: file topics, so the
+    forecast lane is the native thread (csrc/host/fcst_lane.cpp: pread → native parse →
+    resident serving wave → native Prediction formatting → append; no Python on the
+    record's path). t_in is taken before the record's append, t_out by the lane right after
+    its Prediction's append (both CLOCK_MONOTONIC); the bench thread waits in a native call
+    (GIL released), not in a Python spin. Measured twice: with the engine idle between
+    ticks, and while its tick thread trains on a pre-filled training topic (JSON records
+    through the engine's e2e path) — only records answered while training ran count there.
+    Per-stage µs (the lane's own clock) are reported with each."""
+    import tempfile
+    import threading
 
     from omldm_amd.engine.job import Job
     from omldm_amd.io.synthetic import synth_json_records
-    from omldm_amd.io.transport import MemoryBroker
+    from omldm_amd.io.transport import FileBroker
     from omldm_amd.parallel.comm import Comm
     from omldm_amd.utils.config import JobConfig
 
-    class Timed(MemoryBroker):
-        def __init__(self):
-            super().__init__()
-            self.t_out: list = []
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    with tempfile.TemporaryDirectory(dir=shm) as root:
+        br = FileBroker(root)
+        for t, n_p in (("trainingData", 16), ("forecastingData", 1), ("requests", 1),
+                       ("predictions", 1), ("responses", 1), ("performance", 1)):
+            br.create_topic(t, n_p)
+        args = []
+        for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
+                  "predictionsAddr", "performanceAddr"):
+            args += [f"--{k}", f"file://{root}"]
+        args += ["--batchSize", "524288", "--parallelism", "16", "--test", "false"]
+        cfg = JobConfig.from_args(args)
+        sp = FeatureSpace(cfg.numFeatures, 0, cfg.catFeatures, cfg.hashDim)
+        job = Job(cfg, Comm.local(), torch.device("cuda", torch.cuda.current_device()))
+        br.produce("requests", json.dumps({"id": 1, "request": "Create",
+                                           "learner": {"name": "SVM"},
+                                           "trainingConfiguration": {"protocol": "Synchronous"}}))
+        block = ("\n".join(r if isinstance(r, str) else r.decode()
+                            for r in synth_json_records(20000, sp)) + "\n").encode()
+        tfds = [os.open(os.path.join(root, "trainingData", f"{p}.jsonl"), os.O_WRONLY | os.O_APPEND)
+                for p in range(16)]
+        os.write(tfds[0], block)
+        for _ in range(3):
+            job.tick()
+        fs = job.fserver
+        lane = "native" if fs.native else "python"
+        recs = [r if isinstance(r, bytes) else r.encode()
+                for r in synth_json_records(2 * n + 40, sp, start=10**9, operation="forecasting")]
+        ffd = os.open(os.path.join(root, "forecastingData", "0.jsonl"), os.O_WRONLY | os.O_APPEND)
 
-        def produce(self, topic, value, partition=None, key=None):
-            super().produce(topic, value, partition, key)
-            if topic == "predictions":
-                self.t_out.append(time.perf_counter())
+        def send(batch, gap_s, while_=None):
+            lat = []
+            for i, r in enumerate(batch):
+                if while_ is not None and not while_():
+                    break
+                k = fs.native_stats()["served"] if fs.native else None
+                t_in = time.perf_counter()
+                os.write(ffd, r.replace(b"\n", b" ") + b"\n")
+                if fs.native:
+                    if not fs.native_wait(k + 1, 2.0):
+                        raise RuntimeError("native forecast lane: no answer within 2 s")
+                    t_out = fs.native_tout(k)
+                else:
+                    assert fs.catch_up(2.0)
+                    t_out = time.perf_counter()
+                lat.append((t_out - t_in) * 1e6)
+                t = time.perf_counter()
+                while time.perf_counter() - t < gap_s:  # records arrive one at a time
+                    time.sleep(0)
+            return lat
 
-    name = "bench-" + uuid.uuid4().hex
-    br = Timed()
-    MemoryBroker._registry[name] = br
-    args = []
-    for k in ("trainingDataAddr", "forecastingDataAddr", "requestsAddr", "responsesAddr",
-              "predictionsAddr", "performanceAddr"):
-        args += [f"--{k}", f"memory://{name}"]
-    args += ["--batchSize", "8192", "--parallelism", "16", "--test", "false"]
-    cfg = JobConfig.from_args(args)
-    sp = FeatureSpace(cfg.numFeatures, 0, cfg.catFeatures, cfg.hashDim)
-    job = Job(cfg, Comm.local(), torch.device("cuda", torch.cuda.current_device()))
-    br.produce("requests", json.dumps({"id": 1, "request": "Create",
-                                       "learner": {"name": "SVM"},
-                                       "trainingConfiguration": {"protocol": "Synchronous"}}))
-    for r in synth_json_records(16384, sp):
-        br.produce("trainingData", r)
-    for _ in range(3):
-        job.tick()
-    recs = synth_json_records(n + 20, sp, start=10**9, operation="forecasting")
-    t_in = []
-    for r in recs:
-        k = len(br.t_out)
-        t_in.append(time.perf_counter())
-        br.produce("forecastingData", r)
-        t = time.perf_counter()
-        while len(br.t_out) == k and time.perf_counter() - t < 1.0:
-            time.sleep(0)
-        time.sleep(100e-6)  # records arrive one at a time
-    job.fserver.close()
-    job.ingest.close()
-    job.egress.close()
-    lat = sorted((o - i) * 1e6 for i, o in zip(t_in[20:], br.t_out[20:]))
-    return {"p50": round(lat[len(lat) // 2], 2),
-            "p99": round(lat[min(len(lat) - 1, int(0.99 * len(lat)))], 2),
-            "what": f"{len(lat)} JSON forecasting records, each produced into the topic → its "
-                    "Prediction produced (engine forecast lane: host poll + native parse + "
-                    "resident serving wave + native Prediction formatting), trained SVM"}
+        def pct(lat):
+            lat = sorted(lat)
+            if not lat:
+                return None, None
+            return (round(lat[len(lat) // 2], 2),
+                    round(lat[min(len(lat) - 1, int(0.99 * len(lat)))], 2))
+
+        send(recs[:20], 100e-6)                      # wave start, warm caches
+        s0 = fs.native_stats() if fs.native else None
+        idle = send(recs[20:20 + n], 100e-6)
+        s1 = fs.native_stats() if fs.native else None
+
+        def stage_delta(a, b):
+            if a is None or b is None:
+                return None
+            d = max(1, b["served"] - a["served"])
+            return {k: round((b["stage_us"][k] * b["served"] - a["stage_us"][k] * a["served"])
+                             / d, 3) for k in b["stage_us"]}
+
+        # under training: the tick thread trains on a pre-filled JSON training topic
+        reps = max(1, train_records // 20000)
+        for i in range(reps):
+            os.write(tfds[i % 16], block)
+        end = {p: os.path.getsize(os.path.join(root, "trainingData", f"{p}.jsonl"))
+               for p in range(16)}
+        busy = threading.Event()
+        busy.set()
+        trained = {"records": 0, "s": 0.0}
+
+        def trainer():
+            t0 = time.perf_counter()
+            f0 = job.pipes[1].learner.running_totals()["fitted"]
+            while any(job.train_in.offsets.get(p, 0) < o for p, o in end.items()
+                      if p in job.train_in.offsets):
+                job.tick()
+            torch.cuda.current_stream().synchronize()  # (a device sync waits for the wave)
+            trained["s"] = time.perf_counter() - t0
+            trained["records"] = job.pipes[1].learner.running_totals()["fitted"] - f0
+            busy.clear()
+
+        th = threading.Thread(target=trainer)
+        th.start()
+        s2 = fs.native_stats() if fs.native else None
+        under = send(recs[20 + n:], 100e-6, while_=busy.is_set)
+        s3 = fs.native_stats() if fs.native else None
+        th.join()
+        job.close()
+        for fd in tfds + [ffd]:
+            os.close(fd)
+    p50, p99 = pct(idle)
+    u50, u99 = pct(under)
+    return {"p50": p50, "p99": p99, "lane": lane, "stage_us": stage_delta(s0, s1),
+            "train_p50": u50, "train_p99": u99, "train_n": len(under),
+            "train_stage_us": stage_delta(s2, s3),
+            "train_records_per_s": round(trained["records"] / trained["s"], 1)
+            if trained["s"] > 0 else None,
+            "what": f"{len(idle)} JSON forecasting records, each appended to the forecasting "
+                    f"file topic → its Prediction appended to the predictions topic ({lane} "
+                    "forecast lane: pread + native parse + resident serving wave + native "
+                    "Prediction formatting + append), trained SVM, engine idle between ticks; "
+                    f"train_*: {len(under)} records answered while the engine's tick thread "
+                    "trained on a pre-filled JSON training topic"}
 
 
 def cpu_baseline() -> dict | None:
@@ -581,6 +655,14 @@ def main(argv=None) -> int:
             "p99_predict_latency_us": None if p99 is None else round(p99, 2),
             "engine_forecast_p50_us": None if eng is None else eng["p50"],
             "engine_forecast_p99_us": None if eng is None else eng["p99"],
+            "engine_forecast_lane": None if eng is None else eng["lane"],
+            "engine_forecast_stage_us": None if eng is None else eng["stage_us"],
+            "engine_forecast_training_p50_us": None if eng is None else eng["train_p50"],
+            "engine_forecast_training_p99_us": None if eng is None else eng["train_p99"],
+            "engine_forecast_training_n": None if eng is None else eng["train_n"],
+            "engine_forecast_training_stage_us": None if eng is None else eng["train_stage_us"],
+            "engine_forecast_training_records_per_s":
+                None if eng is None else eng["train_records_per_s"],
             "engine_forecast_semantics": None if eng is None else eng["what"],
             "engine_e2e_records_per_s": None if e2e is None else e2e["records_per_s"],
             "engine_e2e_semantics": None if e2e is None else

@@ -605,21 +605,26 @@ __global__ __launch_bounds__(256) void ht_route_kernel(
 // ---- exact per-point VFDT in one persistent launch (models/dense.py HT._fit_exact) -------
 // The reference learner checks a leaf at the very point it reaches gracePeriod points since
 // its last check (FlinkSpoke.scala:92-107: one point at a time). Between two such due points
-// every row's update is an order-free sum into its leaf, so one workgroup of 1024 threads
-// walks the tick in chunks of 1024 rows (one per thread):
-//  * the chunk's rows are staged in LDS and routed through the LDS copy of the tree;
+// every row's update is an order-free sum into its leaf, so one workgroup of 256 threads
+// walks the tick in chunks of 256 rows (one per thread):
+//  * the chunk's rows are routed through the LDS copy of the tree;
 //  * each row's rank among the chunk's training rows of its leaf, in stream order (per-wave
-//    ballots, then a per-leaf prefix over the 16 waves);
+//    ballots, then a per-leaf prefix over the 4 waves);
 //  * the first due row = the lowest row whose rank since the segment start reaches its
 //    leaf's remaining grace (a ballot + one LDS atomic min);
-//  * the segment [start, due row] is added to the leaves' statistics (rows aggregated per
-//    (leaf, class) in the wave, one atomic per statistic), then the due leaf is checked by
-//    the whole workgroup (nBins candidate thresholds per feature, Hoeffding test) and, on a
-//    split, the chunk restarts after the due row under the new tree.
-// No host round trip and no synchronisation per segment (the host loop it replaces did
-// ~650 segments per 131072-row tick, each with .item() syncs). Statistics written by
-// atomics (L2) are read back with agent-scope loads (no stale L1 lines).
-constexpr int kHxNT = 1024;  // threads = rows per chunk
+//  * the segment [start, due row] is added to the leaves' statistics — held in LDS for the
+//    whole launch (class counts, per-(feature, class) moments, ranges), LDS atomics per
+//    row — then the due leaf is checked by the whole workgroup (nBins candidate thresholds
+//    per feature, Hoeffding test) and, on a split, the chunk restarts after the due row
+//    under the new tree.
+// No host round trip per segment (the host loop it replaces did ~650 segments per
+// 131072-row tick, each with .item() syncs) and no global atomics (a first form with L2
+// atomics spent ~45 K cycles per segment on them). S0 is the same for every feature (each
+// training row adds 1 to all of them), so the launch keeps it per (node, class) and writes
+// the per-feature copies back at its end. Σx / Σx² stay in global memory (L2 atomics) when
+// the tree is too large for the LDS (S12 = false).
+constexpr int kHxNT = 256;  // threads = rows per chunk
+constexpr int kHxNW = kHxNT / 64;
 
 struct HxTree {
   float *feat, *thr, *left, *right, *cc, *S0, *S1, *S2, *lo, *hi, *since, *nnodes;
@@ -629,50 +634,125 @@ __device__ __forceinline__ float ld_l2(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ void split_mass_l2(const HxTree& T, size_t base, int C, float t,
-                                              float* lm, float* rm) {
-  for (int c = 0; c < C; ++c) {
-    const float n = ld_l2(T.S0 + base + c);
-    const float nn = fmaxf(n, 1.f);
-    const float mu = ld_l2(T.S1 + base + c) / nn;
-    const float var = fmaxf(ld_l2(T.S2 + base + c) / nn - mu * mu, 1e-6f);
-    const float z = (t - mu) * rsqrtf(var);
-    const float cdf = 0.5f * (1.f + erff(z * 0.70710678f));
-    lm[c] = n * cdf;
-    rm[c] = n - lm[c];
-  }
+// LDS layout. Per node: tn (int4: feature, threshold, left, right), since, consumed, slot
+// (node → leaf slot, -1: not a leaf), cntw[NW] (u8 per-wave counts). Per leaf slot (a tree
+// of N nodes has ≤ (N + 1) / 2 leaves; a split hands its slot to the left child after
+// writing the parent's statistics back): node, cc[C], S0[C], lo[d], hi[d] and, with S12,
+// Σx[d·C], Σx²[d·C]. Then gains[d·nb] and the chunk's rows xs[NT][d].
+struct HxLayout {
+  size_t tn, since, consumed, slot, cntw, snode, cc, s0, lo, hi, s1, s2, gains, xs, bytes;
+  int NS;
+};
+
+__host__ __device__ inline HxLayout ht_exact_layout(int N, int d, int C, int nb, bool s12) {
+  HxLayout L{};
+  L.NS = (N + 1) / 2 + 1;
+  size_t o = 0;
+  auto put = [&](size_t n) {
+    const size_t at = o;
+    o += (n + 15) & ~(size_t)15;
+    return at;
+  };
+  const size_t ns = (size_t)L.NS;
+  L.tn = put((size_t)N * 16);
+  L.since = put((size_t)N * 4);
+  L.consumed = put((size_t)N * 4);
+  L.slot = put((size_t)N * 4);
+  L.cntw = put((size_t)kHxNW * N);
+  L.snode = put(ns * 4);
+  L.cc = put(ns * C * 4);
+  L.s0 = put(ns * C * 4);
+  L.lo = put(ns * d * 4);
+  L.hi = put(ns * d * 4);
+  L.s1 = s12 ? put(ns * d * C * 4) : 0;
+  L.s2 = s12 ? put(ns * d * C * 4) : 0;
+  L.gains = put((size_t)d * nb * 4);
+  L.xs = put((size_t)kHxNT * d * 4);
+  L.bytes = o;
+  return L;
 }
 
-size_t ht_exact_lds(int N, int d, int nb, bool stage) {
-  size_t b = (size_t)N * 16 + (size_t)N * 8 + (((size_t)16 * N + 15) & ~(size_t)15) +
-             (size_t)((d * nb + 3) & ~3) * 4;
-  if (stage) b += (size_t)kHxNT * d * 4;
-  return b;
+__device__ __forceinline__ void lds_min_f(float* a, float v) {  // (range: sign-split ints)
+  if (v >= 0.f)
+    atomicMin(reinterpret_cast<int*>(a), __float_as_int(v));
+  else
+    atomicMax(reinterpret_cast<unsigned int*>(a), __float_as_uint(v));
+}
+__device__ __forceinline__ void lds_max_f(float* a, float v) {
+  if (v >= 0.f)
+    atomicMax(reinterpret_cast<int*>(a), __float_as_int(v));
+  else
+    atomicMin(reinterpret_cast<unsigned int*>(a), __float_as_uint(v));
 }
 
+template <bool S12>
 __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
     const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int C, int depth,
-    int N, int nb, float grace, float delta, float tau, HxTree T, int stage_x,
-    double* __restrict__ nfit, unsigned long long* __restrict__ dbg) {
-  // dbg (diagnostics, may be null): [0] chunks staged, [1] segments, [2] split checks that
-  // split, [3] cycles in chunk setup, [4] cycles in due search, [5] cycles in statistics,
-  // [6] cycles in split checks
+    int N, int nb, float grace, float delta, float tau, HxTree T, double* __restrict__ nfit,
+    unsigned long long* __restrict__ dbg) {
+  // dbg (diagnostics, may be null): [0] chunks, [1] segments, [2] splits, [3..6] cycles in
+  // chunk setup / due search / statistics / split checks (wave 0's clock)
   unsigned long long t_setup = 0, t_due = 0, t_stat = 0, t_split = 0, n_chunk = 0, n_seg = 0,
                      n_split = 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char hx_smem[];
-  int4* tn = reinterpret_cast<int4*>(hx_smem);                 // [N] feat, thr, left, right
-  float* since_l = reinterpret_cast<float*>(tn + N);           // [N]
-  int* consumed = reinterpret_cast<int*>(since_l + N);         // [N] rows of the chunk added
-  unsigned char* cntw = reinterpret_cast<unsigned char*>(consumed + N);  // [16][N]
-  float* gains = reinterpret_cast<float*>(cntw + ((16 * N + 15) & ~15));  // [d·nb]
-  float* xs = gains + ((d * nb + 3) & ~3);                     // [kHxNT][d] when staged
-  __shared__ int s_first, s_leaf, s_flag, s_nn;
+  const HxLayout Ly = ht_exact_layout(N, d, C, nb, S12);
+  int4* tn = reinterpret_cast<int4*>(hx_smem + Ly.tn);
+  float* since_l = reinterpret_cast<float*>(hx_smem + Ly.since);
+  int* consumed = reinterpret_cast<int*>(hx_smem + Ly.consumed);
+  int* slot = reinterpret_cast<int*>(hx_smem + Ly.slot);
+  unsigned char* cntw = hx_smem + Ly.cntw;
+  int* snode = reinterpret_cast<int*>(hx_smem + Ly.snode);
+  float* ccl = reinterpret_cast<float*>(hx_smem + Ly.cc);
+  float* s0l = reinterpret_cast<float*>(hx_smem + Ly.s0);
+  float* lol = reinterpret_cast<float*>(hx_smem + Ly.lo);
+  float* hil = reinterpret_cast<float*>(hx_smem + Ly.hi);
+  float* s1 = reinterpret_cast<float*>(hx_smem + Ly.s1);
+  float* s2 = reinterpret_cast<float*>(hx_smem + Ly.s2);
+  float* gains = reinterpret_cast<float*>(hx_smem + Ly.gains);
+  float* xs = reinterpret_cast<float*>(hx_smem + Ly.xs);
+  const int NS = Ly.NS;
+  __shared__ int s_first, s_leaf, s_flag, s_nn, s_nslot;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // Σx / Σx² of slot k, feature f, class c: LDS (S12) or the node's global rows
+  auto s1p = [&](int k, int f, int c) -> float* {
+    return S12 ? s1 + ((size_t)k * d + f) * C + c : T.S1 + ((size_t)snode[k] * d + f) * C + c;
+  };
+  auto s2p = [&](int k, int f, int c) -> float* {
+    return S12 ? s2 + ((size_t)k * d + f) * C + c : T.S2 + ((size_t)snode[k] * d + f) * C + c;
+  };
+  // the leaves get slots (thread 0, node order)
+  if (tid == 0) {
+    s_nn = (int)T.nnodes[0];
+    int k = 0;
+    for (int n = 0; n < N; ++n) {
+      const bool leaf = n < s_nn && T.feat[n] < 0.f && k < NS;
+      slot[n] = leaf ? k : -1;
+      if (leaf) snode[k++] = n;
+    }
+    s_nslot = k;
+  }
   for (int n = tid; n < N; n += kHxNT) {
     tn[n] = make_int4((int)T.feat[n], __float_as_int(T.thr[n]), (int)T.left[n], (int)T.right[n]);
     since_l[n] = T.since[n];
   }
-  if (tid == 0) s_nn = (int)T.nnodes[0];
+  __syncthreads();
+  const int nslot0 = s_nslot;
+  for (int i = tid; i < nslot0 * C; i += kHxNT) {
+    const int k = i / C, c = i % C, n = snode[k];
+    ccl[i] = T.cc[(size_t)n * C + c];
+    s0l[i] = T.S0[(size_t)n * d * C + c];  // (feature 0: every feature's count)
+  }
+  for (int i = tid; i < nslot0 * d; i += kHxNT) {
+    const int k = i / d, f = i % d, n = snode[k];
+    lol[i] = T.lo[(size_t)n * d + f];
+    hil[i] = T.hi[(size_t)n * d + f];
+  }
+  if constexpr (S12)
+    for (int i = tid; i < nslot0 * d * C; i += kHxNT) {
+      const int k = i / (d * C), r = i % (d * C), n = snode[k];
+      s1[i] = T.S1[(size_t)n * d * C + r];
+      s2[i] = T.S2[(size_t)n * d * C + r];
+    }
   __syncthreads();
   float myfit = 0.f;
   int c0 = 0;
@@ -686,12 +766,30 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
     int yi = valid ? (int)yr : 0;
     yi = yi < 0 ? 0 : (yi >= C ? C - 1 : yi);
     const int cend = min(c0 + kHxNT, B);  // exclusive
-    if (stage_x)
-      for (int e = tid; e < (cend - c0) * d; e += kHxNT) xs[e] = x[(size_t)c0 * d + e];
-    for (int e = tid; e < 16 * N; e += kHxNT) cntw[e] = 0;
+    // the chunk's rows into LDS: one coalesced block, every load in flight before the
+    // stores (a load → store loop waited out one memory latency per element), then
+    // routing reads LDS
+    {
+      const int ne = (cend - c0) * d;
+      const float* src = x + (size_t)c0 * d;
+      for (int e0 = 0; e0 < ne; e0 += 16 * kHxNT) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int e = e0 + u * kHxNT + tid;
+          v[u] = src[e < ne ? e : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int e = e0 + u * kHxNT + tid;
+          if (e < ne) xs[e] = v[u];
+        }
+      }
+    }
+    for (int e = tid; e < kHxNW * N; e += kHxNT) cntw[e] = 0;
     for (int n = tid; n < N; n += kHxNT) consumed[n] = 0;
     __syncthreads();
-    const float* xr = stage_x ? xs + (size_t)tid * d : x + (size_t)(inb ? r : 0) * d;
+    const float* xr = xs + (size_t)tid * d;
     int leaf = 0;
     if (inb) {
       for (int it = 0; it <= depth; ++it) {
@@ -740,101 +838,76 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
       if (r == first) s_leaf = leaf;
       t_due += __builtin_amdgcn_s_memtime() - tc;
       tc = __builtin_amdgcn_s_memtime();
-      // the segment's rows into their leaves' statistics: the wave's first few (leaf, class)
-      // keys aggregated (one atomic per statistic: early on, every row of a wave shares a
-      // key and per-row atomics would serialise on it), the rest one atomic per row (a wave
-      // spread over many leaves: aggregating key by key cost ~3 K cycles per row)
-      {
-        const int key = seg ? leaf * C + yi : -1;
-        unsigned long long pending = __ballot(seg);
-        myfit += (float)(seg ? 1 : 0);
-        for (int it = 0; it < 3 && pending; ++it) {
-          const int leader = __ffsll((long long)pending) - 1;
-          const int k = __shfl(key, leader);
-          const bool mine = key == k;
-          const unsigned long long grp = __ballot(mine);
-          const int gn = __popcll(grp);
-          if (gn < 8 && it > 0) break;  // (a thin key: the per-row path is cheaper)
-          pending &= ~grp;
-          const float cnt = (float)gn;
-          const int nd = k / C, yc = k - nd * C;
-          if (lane == leader) {
-            atomicAdd(&T.cc[k], cnt);
-            atomicAdd(&since_l[nd], cnt);
-            atomicAdd(&consumed[nd], gn);
-          }
-          for (int f = 0; f < d; f += 2) {
-            const int fb = f + 1 < d ? f + 1 : f;
-            const float va = mine ? xr[f] : 0.f, vb = (mine && f + 1 < d) ? xr[fb] : 0.f;
-            float s1a = va, s1b = vb, s2a = va * va, s2b = vb * vb;
-            wave_sum2(s1a, s1b);
-            wave_sum2(s2a, s2b);
-            const float mna = wave_min(mine ? va : INFINITY), mxa = wave_max(mine ? va : -INFINITY);
-            const float mnb = wave_min(mine ? vb : INFINITY), mxb = wave_max(mine ? vb : -INFINITY);
-            if (lane == leader) {
-              const size_t o = ((size_t)nd * d + f) * C + yc;
-              atomicAdd(&T.S0[o], cnt);
-              atomicAdd(&T.S1[o], s1a);
-              atomicAdd(&T.S2[o], s2a);
-              atomic_min_f(&T.lo[nd * d + f], mna);
-              atomic_max_f(&T.hi[nd * d + f], mxa);
-              if (f + 1 < d) {
-                atomicAdd(&T.S0[o + C], cnt);
-                atomicAdd(&T.S1[o + C], s1b);
-                atomicAdd(&T.S2[o + C], s2b);
-                atomic_min_f(&T.lo[nd * d + f + 1], mnb);
-                atomic_max_f(&T.hi[nd * d + f + 1], mxb);
-              }
-            }
+      // the segment's rows into their leaves' statistics (LDS atomics, one row per thread)
+      if (seg) {
+        myfit += 1.f;
+        const int k = slot[leaf];
+        if (k >= 0) {
+          atomicAdd(&ccl[k * C + yi], 1.f);
+          atomicAdd(&s0l[k * C + yi], 1.f);
+          // the row's features first (one wait), then fire-and-forget LDS atomics: float
+          // add for the moments, float min / max for the range (no waits, no branches)
+          auto put = [&](int f, float v) {
+            atomicAdd(s1p(k, f, yi), v);
+            atomicAdd(s2p(k, f, yi), v * v);
+            __hip_atomic_fetch_min(&lol[k * d + f], v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_max(&hil[k * d + f], v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+          };
+          if (d <= 32) {
+            float v[32];
+#pragma unroll
+            for (int f = 0; f < 32; ++f) v[f] = f < d ? xr[f] : 0.f;
+#pragma unroll
+            for (int f = 0; f < 32; ++f)
+              if (f < d) put(f, v[f]);
+          } else {
+            for (int f = 0; f < d; ++f) put(f, xr[f]);
           }
         }
-        if ((pending >> lane) & 1ull) {  // the remaining rows: one atomic per statistic each
-          atomicAdd(&T.cc[key], 1.f);
-          atomicAdd(&since_l[leaf], 1.f);
-          atomicAdd(&consumed[leaf], 1);
-          for (int f = 0; f < d; ++f) {
-            const float v = xr[f];
-            const size_t o = ((size_t)leaf * d + f) * C + yi;
-            atomicAdd(&T.S0[o], 1.f);
-            atomicAdd(&T.S1[o], v);
-            atomicAdd(&T.S2[o], v * v);
-            atomic_min_f(&T.lo[leaf * d + f], v);
-            atomic_max_f(&T.hi[leaf * d + f], v);
-          }
-        }
+        atomicAdd(&since_l[leaf], 1.f);
+        atomicAdd(&consumed[leaf], 1);
       }
-      if (first == 0x7fffffff) {
-        t_stat += __builtin_amdgcn_s_memtime() - tc;
-        break;
-      }
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the atomics landed in L2
+      if constexpr (!S12) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (L2 atomics)
       __syncthreads();
       t_stat += __builtin_amdgcn_s_memtime() - tc;
+      if (first == 0x7fffffff) break;
       tc = __builtin_amdgcn_s_memtime();
       // the due leaf's split check (ht_split_kernel's criterion, by the whole workgroup)
-      const int L = s_leaf;
-      float ccl[kHtMaxC];
+      const int L = s_leaf, kL = slot[L];
+      bool split = false;
       float ntot = 0.f;
       int nz = 0;
-      for (int c = 0; c < C; ++c) {
-        ccl[c] = ld_l2(T.cc + (size_t)L * C + c);
-        ntot += ccl[c];
-        nz += ccl[c] > 0.f;
-      }
-      bool split = false;
-      if (ntot < 2.f || nz < 2 || s_nn + 2 > N) {
-        __syncthreads();  // (every thread read since_l / s_nn above)
-        if (tid == 0) since_l[L] = 0.f;
-      } else {
-        const float h0 = entropy(ccl, C, ntot);
+      if (kL >= 0)
+        for (int c = 0; c < C; ++c) {
+          ntot += ccl[kL * C + c];
+          nz += ccl[kL * C + c] > 0.f;
+        }
+      if (kL >= 0 && !(ntot < 2.f || nz < 2 || s_nn + 2 > N)) {
+        const float h0 = entropy(ccl + (size_t)kL * C, C, ntot);
         float lm[kHtMaxC], rm[kHtMaxC];
+        auto mass = [&](int f, float t) {  // class mass left / right of t (Gaussian CDFs)
+          for (int c = 0; c < C; ++c) {
+            const float n = s0l[kL * C + c];
+            const float nn = fmaxf(n, 1.f);
+            // (global Σ rows written by L2 atomics: agent-scope loads, no stale L1 lines)
+            const float m1 = S12 ? *s1p(kL, f, c) : ld_l2(s1p(kL, f, c));
+            const float m2 = S12 ? *s2p(kL, f, c) : ld_l2(s2p(kL, f, c));
+            const float mu = m1 / nn;
+            const float var = fmaxf(m2 / nn - mu * mu, 1e-6f);
+            const float z = (t - mu) * rsqrtf(var);
+            const float cdf = 0.5f * (1.f + erff(z * 0.70710678f));
+            lm[c] = n * cdf;
+            rm[c] = n - lm[c];
+          }
+        };
         for (int p2 = tid; p2 < d * nb; p2 += kHxNT) {
           const int f = p2 / nb, b = p2 - f * nb;
-          const float l = ld_l2(T.lo + (size_t)L * d + f), span = ld_l2(T.hi + (size_t)L * d + f) - l;
+          const float l = lol[kL * d + f], span = hil[kL * d + f] - l;
           float g = -1.f;
           if (span > 0.f) {
-            const float t = l + span * (float)(b + 1) / (float)(nb + 1);
-            split_mass_l2(T, ((size_t)L * d + f) * C, C, t, lm, rm);
+            mass(f, l + span * (float)(b + 1) / (float)(nb + 1));
             float nl = 0.f, nr = 0.f;
             for (int c = 0; c < C; ++c) {
               nl += lm[c];
@@ -875,22 +948,16 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
             f1 = take ? of1 : f1;
             b1 = take ? ob1 : b1;
           }
+          int flag = 0;
           if (lane == 0) {
             if (d == 1) g2 = 0.f;
-            since_l[L] = 0.f;
             const float R = __log2f((float)C);
             const float eps = sqrtf(R * R * logf(1.f / delta) / (2.f * ntot));
-            int flag = 0;
-            if (g1 > 0.f && (g1 - g2 > eps || eps < tau)) {
+            if (g1 > 0.f && (g1 - g2 > eps || eps < tau) && s_nslot < NS) {
               const int old = s_nn;
-              const float l = ld_l2(T.lo + (size_t)L * d + f1);
-              const float span = ld_l2(T.hi + (size_t)L * d + f1) - l;
+              const float l = lol[kL * d + f1], span = hil[kL * d + f1] - l;
               const float t = l + span * (float)(b1 + 1) / (float)(nb + 1);
-              split_mass_l2(T, ((size_t)L * d + f1) * C, C, t, lm, rm);
-              for (int c = 0; c < C; ++c) {
-                T.cc[(size_t)old * C + c] = lm[c];
-                T.cc[(size_t)(old + 1) * C + c] = rm[c];
-              }
+              mass(f1, t);
               T.thr[L] = t;
               T.left[L] = (float)old;
               T.right[L] = (float)(old + 1);
@@ -899,14 +966,64 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
               tn[L] = make_int4(f1, __float_as_int(t), old, old + 1);
               s_nn = old + 2;
               flag = 1;
-              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            s_flag = flag;
           }
+          flag = __shfl(flag, 0);
+          if (flag) {
+            // the parent's statistics back to its node rows (it is no leaf any more), then
+            // its slot to the left child and a fresh slot to the right one
+            const int n = L;
+            for (int i = lane; i < C; i += 64) {
+              T.cc[(size_t)n * C + i] = ccl[kL * C + i];
+              for (int f = 0; f < d; ++f) T.S0[((size_t)n * d + f) * C + i] = s0l[kL * C + i];
+            }
+            for (int i = lane; i < d; i += 64) {
+              T.lo[(size_t)n * d + i] = lol[kL * d + i];
+              T.hi[(size_t)n * d + i] = hil[kL * d + i];
+            }
+            if constexpr (S12)
+              for (int i = lane; i < d * C; i += 64) {
+                T.S1[(size_t)n * d * C + i] = s1[(size_t)kL * d * C + i];
+                T.S2[(size_t)n * d * C + i] = s2[(size_t)kL * d * C + i];
+              }
+            const int old = s_nn - 2, kR = s_nslot;
+            // (S12 false: the children's global Σ rows start at zero in the model state)
+            if (lane == 0) {
+              slot[L] = -1;
+              slot[old] = kL;
+              slot[old + 1] = kR;
+              snode[kL] = old;
+              snode[kR] = old + 1;
+              s_nslot = kR + 1;
+              for (int c = 0; c < C; ++c) {  // children start with the split class mass
+                ccl[kL * C + c] = lm[c];
+                ccl[kR * C + c] = rm[c];
+              }
+            }
+            for (int i = lane; i < C; i += 64) {
+              s0l[kL * C + i] = 0.f;
+              s0l[kR * C + i] = 0.f;
+            }
+            for (int i = lane; i < d; i += 64) {
+              lol[kL * d + i] = INFINITY;
+              hil[kL * d + i] = -INFINITY;
+              lol[kR * d + i] = INFINITY;
+              hil[kR * d + i] = -INFINITY;
+            }
+            if constexpr (S12)
+              for (int i = lane; i < d * C; i += 64) {
+                s1[(size_t)kL * d * C + i] = 0.f;
+                s2[(size_t)kL * d * C + i] = 0.f;
+                s1[(size_t)kR * d * C + i] = 0.f;
+                s2[(size_t)kR * d * C + i] = 0.f;
+              }
+          }
+          if (lane == 0) s_flag = flag;
         }
         __syncthreads();
         split = s_flag != 0;
       }
+      if (tid == 0) since_l[L] = 0.f;  // (checked: the grace count restarts)
       __syncthreads();
       t_split += __builtin_amdgcn_s_memtime() - tc;
       n_split += split;
@@ -918,9 +1035,27 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
       }
     }
     if (!restart) c0 = cend;
-    __syncthreads();  // the chunk's LDS (rows, counts) is free
   }
+  // the leaves' statistics back to their nodes' rows
+  const int nsl = s_nslot;
   for (int n = tid; n < N; n += kHxNT) T.since[n] = since_l[n];
+  for (int i = tid; i < nsl * C; i += kHxNT) {
+    const int k = i / C, c = i % C, n = snode[k];
+    T.cc[(size_t)n * C + c] = ccl[i];
+  }
+  for (int i = tid; i < nsl * d * C; i += kHxNT) {
+    const int k = i / (d * C), rr = i % (d * C), n = snode[k];
+    T.S0[(size_t)n * d * C + rr] = s0l[k * C + rr % C];
+    if constexpr (S12) {
+      T.S1[(size_t)n * d * C + rr] = s1[i];
+      T.S2[(size_t)n * d * C + rr] = s2[i];
+    }
+  }
+  for (int i = tid; i < nsl * d; i += kHxNT) {
+    const int k = i / d, f = i % d, n = snode[k];
+    T.lo[(size_t)n * d + f] = lol[i];
+    T.hi[(size_t)n * d + f] = hil[i];
+  }
   if (dbg && tid == 0) {
     dbg[0] += n_chunk;
     dbg[1] += n_seg;
@@ -1032,14 +1167,20 @@ OMLDM_API int omldm_ht_exact(const float* x, const float* y, int B, int d, int C
                              void* stream) {
   if (B <= 0) return 0;
   if (C < 1 || C > kHtMaxC || nb < 1 || d < 1) return -1;
-  const bool stage = ht_exact_lds(N, d, nb, true) <= 160 * 1024;
-  const size_t lds = ht_exact_lds(N, d, nb, stage);
-  if (lds > 160 * 1024 - 64) return -2;
-  const int e = check_dyn_lds((const void*)ht_exact_kernel, lds);
+  constexpr size_t kMax = 160 * 1024 - 256;
+  const bool s12 = ht_exact_layout(N, d, C, nb, true).bytes <= kMax;
+  const size_t lds = ht_exact_layout(N, d, C, nb, s12).bytes;
+  if (lds > kMax) return -2;
+  const void* fn = s12 ? (const void*)ht_exact_kernel<true> : (const void*)ht_exact_kernel<false>;
+  const int e = check_dyn_lds(fn, lds);
   if (e) return e;
   HxTree T{tree[0], tree[1], tree[2], tree[3], tree[4], tree[5],
            tree[6], tree[7], tree[8], tree[9], tree[10], tree[11]};
-  hipLaunchKernelGGL(ht_exact_kernel, dim3(1), dim3(kHxNT), lds, (hipStream_t)stream, x, y, B, d,
-                     C, depth, N, nb, grace, delta, tau, T, (int)stage, nfit, dbg);
+  if (s12)
+    hipLaunchKernelGGL(ht_exact_kernel<true>, dim3(1), dim3(kHxNT), lds, (hipStream_t)stream, x,
+                       y, B, d, C, depth, N, nb, grace, delta, tau, T, nfit, dbg);
+  else
+    hipLaunchKernelGGL(ht_exact_kernel<false>, dim3(1), dim3(kHxNT), lds, (hipStream_t)stream, x,
+                       y, B, d, C, depth, N, nb, grace, delta, tau, T, nfit, dbg);
   return (int)hipGetLastError();
 }

@@ -284,3 +284,24 @@ OMLDM_API int omldm_serve_exit_reason(void* mailbox) {
 OMLDM_API int omldm_serve_alive(void* mailbox) {
   return (int)__atomic_load_n(&((Mailbox*)mailbox)->alive, __ATOMIC_ACQUIRE);
 }
+
+// The published-bank word of the native forecast lane (csrc/host/fcst_lane.cpp): a pinned
+// coherent host word the GPU writes after a publish copy, in stream order
+// (hipStreamWriteValue32), so the lane switches banks only once the copy has completed.
+OMLDM_API void* omldm_bank_word_alloc() {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+    return nullptr;
+  memset(p, 0, 64);
+  return p;
+}
+
+OMLDM_API void omldm_bank_word_free(void* p) {
+  if (p) hipHostFree(p);
+}
+
+OMLDM_API int omldm_bank_word_set(void* word, unsigned int v, void* stream) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, word, 0) != hipSuccess || !d) return -3;
+  return (int)hipStreamWriteValue32((hipStream_t)stream, d, v, 0);
+}

@@ -35,6 +35,15 @@ FlinkSpoke.scala:97-105, so a prediction sees a model between two fits):
   the model between two rounds, never one half-way through an update.
 
 Records wait for the tick (``take_fallback``) only while no pipeline exists yet.
+
+Native lane (file topics, every pipeline on the wave — the engine's default linear
+pipelines): the whole lane runs in a C++ thread (csrc/host/fcst_lane.cpp: pread of the
+forecasting partitions → native parse → mailbox → native Prediction formatting → one
+append per record), so no Python — and no GIL shared with the tick thread — sits on the
+record's path. The Python thread then only supervises: it starts the resident wave when
+the lane asks for one. The bank a request reads is a pinned word the GPU sets after each
+publish copy (stream-ordered), the same at-most-one-round-stale guarantee. Kafka and
+in-process topics, and pipelines needing one-row predicts, keep the Python lane.
 """
 from __future__ import annotations
 
@@ -118,6 +127,13 @@ class ForecastServer:
         self._cycle = threading.Lock()
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, name="omldm-forecast", daemon=True)
+        self._native = None           # csrc/host/fcst_lane.cpp handle (file topics)
+        self._native_parts: list = []
+        self._native_fds: list = []
+        self._bank_word = None        # pinned word: the bank the native lane reads
+        self._nat_target = 0          # the bank of the native lane's last publish
+        self._native_lat = None       # its per-record latencies (µs, sorted), last read
+        self._last_native = None      # its last counters
         _LIVE.add(self)
 
     # ----------------------------------------------------------------- control
@@ -129,7 +145,13 @@ class ForecastServer:
         if self._thread.is_alive():
             self._thread.join(5.0)
         with self.lock:
+            self._stop_native()
             self._stop_wave()
+            if self._bank_word is not None:
+                from omldm_amd.ops.serving import _lib
+
+                _lib().omldm_bank_word_free(self._bank_word)
+                self._bank_word = None
 
     def _stop_wave(self) -> None:
         if self._server is not None:
@@ -140,6 +162,7 @@ class ForecastServer:
         """Before the model store may move (a Create can grow its arena) or pipelines
         change: the lane stops serving until ``reconfigure``."""
         with self.lock:
+            self._stop_native()
             self._stop_wave()
             self._spec = None
             self._served = []
@@ -154,6 +177,7 @@ class ForecastServer:
         training tick's copy / parse / compute overlap while no forecast arrives (engine
         end-to-end 33 → 15 M records/s with an idle resident wave)."""
         with self.lock:
+            self._stop_native()
             self._stop_wave()
             self._spec = None
             self._served, self._direct, self._order = [], [], []
@@ -186,6 +210,118 @@ class ForecastServer:
             self._direct = [(p.id, p) for p in pipes if p.id not in waved]
             if self._direct and self._stream is None and self.job.device.type == "cuda":
                 self._stream = torch.cuda.Stream(self.job.device)
+            if self._native_eligible():
+                self._start_native()
+
+    # ------------------------------------------------------------ native lane
+    def _native_eligible(self) -> bool:
+        from omldm_amd.io.transport import FileBroker
+
+        return (os.environ.get("OMLDM_FS_NATIVE", "1") != "0"
+                and self.job.device.type == "cuda" and self._spec is not None
+                and not self._direct and bool(self._served) and bool(self.consumer.parts)
+                and isinstance(self.consumer.broker, FileBroker)
+                and isinstance(self.broker, FileBroker))
+
+    @property
+    def native(self) -> bool:
+        """The lane runs in the native thread (csrc/host/fcst_lane.cpp)."""
+        return self._native is not None
+
+    def _start_native(self) -> None:
+        """Under the lock, after reconfigure: the native lane from the consumer's offsets."""
+        import ctypes
+
+        from omldm_amd.ops.serving import _lib
+
+        hl, sl = native.host(), _lib()
+        if self._bank_word is None:
+            self._bank_word = sl.omldm_bank_word_alloc()
+        ctypes.c_uint32.from_address(self._bank_word).value = 0  # both banks = W (above)
+        self._nat_target = 0
+        cb, topic = self.consumer.broker, self.consumer.topic
+        parts = list(self.consumer.parts)
+        fds = []
+        for p in parts:
+            path = os.path.join(cb.root, topic, f"{p}.jsonl")
+            if not os.path.exists(path):
+                open(path, "ab").close()
+            fds.append(os.open(path, os.O_RDONLY))
+        n_out = self.broker.partitions(self.topic)
+        outs = []
+        for p in range(n_out):
+            path = os.path.join(self.broker._dir(self.topic), f"{p}.jsonl")
+            outs.append(os.open(path, os.O_WRONLY | os.O_APPEND | os.O_CREAT, 0o644))
+        in_fds = np.array(fds, dtype=np.int32)
+        out_fds = np.array(outs, dtype=np.int32)
+        offs = np.array([self.consumer.offsets[p] for p in parts], dtype=np.int64)
+        lo = self._spec[0]
+        pids = np.array([pid for pid, _, _ in self._served], dtype=np.int32)
+        rows = np.array([row - lo for _, row, _ in self._served], dtype=np.int32)
+        cls = np.array([1 if c else 0 for _, _, c in self._served], dtype=np.int32)
+        sp = self.space
+        serve = ctypes.cast(sl.cdll.omldm_serve_request, ctypes.c_void_p).value
+        alive = ctypes.cast(sl.cdll.omldm_serve_alive, ctypes.c_void_p).value
+        h = hl.omldm_fcst_lane_start(
+            in_fds.ctypes.data, offs.ctypes.data, len(parts), out_fds.ctypes.data, len(outs),
+            sp.n_numerical, sp.n_discrete, sp.dc, sp.dim, sp.cat_span, serve, alive,
+            self._spec[1] - lo, pids.ctypes.data, rows.ctypes.data, cls.ctypes.data, len(pids),
+            self._bank_word)
+        if not h:
+            for fd in fds + outs:
+                os.close(fd)
+            return
+        self._native, self._native_parts, self._native_fds = h, parts, fds + outs
+        if self._server is not None:
+            hl.omldm_fcst_lane_set_mailbox(h, self._server.mb)
+
+    def _native_offsets(self) -> dict:
+        offs = np.zeros(max(1, len(self._native_parts)), dtype=np.int64)
+        native.host().omldm_fcst_lane_offsets(self._native, offs.ctypes.data)
+        return {p: int(offs[i]) for i, p in enumerate(self._native_parts)}
+
+    def _stop_native(self) -> None:
+        """Under the lock: the native lane stops; the consumer resumes at its offsets."""
+        h = self._native
+        if h is None:
+            return
+        self.native_stats()  # (the last counters, kept for the caller)
+        self.latency_percentiles()  # (and the lane's latencies)
+        offs = self._native_offsets()
+        native.host().omldm_fcst_lane_stop(h)
+        self._native = None
+        self.consumer.offsets.update(offs)
+        self._done = dict(self.consumer.offsets)
+        for fd in self._native_fds:
+            try:
+                os.close(fd)
+            except OSError:
+                pass
+        self._native_fds = []
+
+    def native_stats(self) -> dict | None:
+        """Answered records and the mean µs per stage of the native lane (poll, parse, wave,
+        format, produce, record) — None when it is not running."""
+        if self._native is None:
+            return self._last_native
+        st = np.zeros(9, dtype=np.int64)
+        native.host().omldm_fcst_lane_stats(self._native, st.ctypes.data)
+        n = max(1, int(st[0]))
+        names = ("poll", "parse", "wave", "format", "produce", "record")
+        out = {"served": int(st[0]), "invalid": int(st[1]), "write_errors": int(st[2]),
+               "stage_us": {k: round(float(st[3 + i]) / n / 1e3, 3) for i, k in enumerate(names)}}
+        self._last_native = out
+        return out
+
+    def native_wait(self, count: int, timeout_s: float = 1.0) -> bool:
+        """Blocks (GIL released) until the native lane has answered ``count`` records."""
+        h = self._native
+        return h is not None and native.host().omldm_fcst_lane_wait(
+            h, int(count), int(timeout_s * 1e6)) == 0
+
+    def native_tout(self, k: int) -> float:
+        """perf_counter-clock time at which the native lane answered record k."""
+        return native.host().omldm_fcst_lane_tout(self._native, int(k)) / 1e9
 
     @property
     def serving(self) -> bool:
@@ -215,6 +351,8 @@ class ForecastServer:
         handed-back records still waiting for the tick (saved with the job's state like
         the record buffer, so a restore neither skips nor repeats a forecast)."""
         with self._cycle:
+            if self._native is not None:
+                return self._native_offsets(), list(self.fallback)
             done = dict(self._done) if self._thread.is_alive() else dict(self.consumer.offsets)
             return done, list(self.fallback)
 
@@ -247,6 +385,24 @@ class ForecastServer:
             if spec is None or banks is None:
                 return
             lo, hi, _ = spec
+            if self._native is not None and self._bank_word is not None:
+                # the native lane reads the bank named by a pinned word the GPU sets after
+                # the copy (stream order): alternate banks, the word flips when it is done
+                import ctypes
+
+                from omldm_amd.ops.serving import _lib
+
+                # the last publish's word not written yet: the lane still reads the other
+                # bank, so this copy goes to the pending bank again (never the read one)
+                cur = ctypes.c_uint32.from_address(self._bank_word).value & 1
+                prev = self._nat_target
+                target = self._nat_target = prev if cur != prev else 1 - prev
+                banks[target][lo:hi].copy_(self.job.store.W[lo:hi], non_blocking=True)
+                check_rc = _lib().omldm_bank_word_set(
+                    self._bank_word, target, torch.cuda.current_stream().cuda_stream)
+                if check_rc != 0:
+                    raise RuntimeError(f"hipStreamWriteValue32 failed ({check_rc})")
+                return
             target = self._pend[0] if self._pend is not None else 1 - self._bank
             banks[target][lo:hi].copy_(self.job.store.W[lo:hi], non_blocking=True)
             ev = torch.cuda.Event()
@@ -267,7 +423,13 @@ class ForecastServer:
         return out
 
     def latency_percentiles(self) -> dict:
-        lat = sorted(self.latency_us)
+        if self._native is not None:  # the native lane's own per-record times
+            buf = np.zeros(1 << 16, dtype=np.int64)
+            n = int(native.host().omldm_fcst_lane_latencies(self._native, buf.ctypes.data,
+                                                              buf.size))
+            self._native_lat = sorted((buf[:n] / 1e3).tolist())
+        lat = self._native_lat if (self._native_lat and not self.latency_us) else \
+            sorted(self.latency_us)
         if not lat:
             return {"p50": None, "p99": None, "n": 0}
         return {"p50": round(lat[len(lat) // 2], 2),
@@ -388,7 +550,7 @@ class ForecastServer:
                   for p in self.consumer.parts}
         t0 = time.time()
         while time.time() - t0 < timeout_s:
-            done = self._done
+            done = self._native_offsets() if self._native is not None else self._done
             if all(done.get(p, 0) >= o for p, o in target.items()):
                 return True
             time.sleep(self.IDLE_SLEEP_S)
@@ -404,6 +566,16 @@ class ForecastServer:
         last = 0.0
         idle_marked = False
         while not self._stop.is_set():
+            if self._native is not None:  # supervise the native lane: start its wave
+                h = self._native
+                if native.host().omldm_fcst_lane_need_wave(h):
+                    with self.lock:
+                        if self._native is h:
+                            srv = self._ensure_wave()
+                            native.host().omldm_fcst_lane_set_mailbox(h, srv.mb)
+                    continue
+                time.sleep(200e-6)
+                continue
             quiet = time.perf_counter() - last
             with self._cycle:
                 # right after traffic the topic is polled directly; a quiet topic is looked

@@ -507,7 +507,7 @@ class HT(Learner):
         self.check_every = max(0, hp_int(self.hyper, "checkEvery", 0))
         # exactDevice (default true): the exact mode's tick runs in one persistent launch;
         # false keeps the host-driven segment loop (the A/B reference of the same semantics)
-        self.exact_device = str(self.hyper.get("exactDevice", False)).lower() not in ("0", "false")
+        self.exact_device = str(self.hyper.get("exactDevice", True)).lower() not in ("0", "false")
 
     def __init__(self, hyper, space, device="cpu"):
         super().__init__(hyper, space, device)

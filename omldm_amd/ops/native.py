@@ -182,6 +182,18 @@ HOST_SIGS = [
     ("omldm_index_lines", i64, [vp, i64, i64, vp]),
     ("omldm_format_predictions", i64, [vp, vp, vp, i64, i32, vp, vp, i64, vp]),
     ("omldm_read_log", i64, [i32, i64, vp, i64, i64, vp, vp, i64]),
+    ("omldm_fcst_lane_start", vp, [vp, vp, i32, vp, i32, i32, i32, i32, i64, i32, vp, vp, i32,
+                                   vp, vp, vp, i32, vp]),
+    ("omldm_fcst_lane_set_mailbox", None, [vp, vp]),
+    ("omldm_fcst_lane_need_wave", i32, [vp]),
+    ("omldm_fcst_lane_pause", i32, [vp, i32, i64]),
+    ("omldm_fcst_lane_offsets", None, [vp, vp]),
+    ("omldm_fcst_lane_stats", None, [vp, vp]),
+    ("omldm_fcst_lane_tout", i64, [vp, i64]),
+    ("omldm_fcst_lane_wait", i32, [vp, i64, i64]),
+    ("omldm_fcst_lane_now_ns", i64, []),
+    ("omldm_fcst_lane_latencies", i64, [vp, vp, i64]),
+    ("omldm_fcst_lane_stop", None, [vp]),
     ("omldm_fill_regions", i64, [i32, vp, vp, vp, vp, vp, vp, vp, vp, i32]),
     ("omldm_codec_available", i32, [i32]),
     ("omldm_codec_decompress", i32, [i32, C.c_char_p, i64, vp, vp]),

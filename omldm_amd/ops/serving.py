@@ -28,6 +28,9 @@ SIGS = [
     ("omldm_serve_stop", None, [C.c_void_p]),
     ("omldm_serve_alive", C.c_int, [C.c_void_p]),
     ("omldm_serve_exit_reason", C.c_int, [C.c_void_p]),
+    ("omldm_bank_word_alloc", C.c_void_p, []),
+    ("omldm_bank_word_free", None, [C.c_void_p]),
+    ("omldm_bank_word_set", C.c_int, [C.c_void_p, C.c_uint, C.c_void_p]),
 ]
 
 
