@@ -433,6 +433,14 @@ def main(argv=None) -> int:
             prep_stream = torch.cuda.Stream(device)
     copied = [torch.cuda.Event() for _ in range(nslots)] if on_gpu else None
     consumed = [torch.cuda.Event() for _ in range(nslots)] if on_gpu else None
+    # device time of each batch's copy and each round: timing-event pairs recorded in the
+    # loop, read after the final sync (no synchronisation inside the timed window), so the
+    # record says which lane bounded the step
+    ev_copy: dict = {}
+    ev_round: dict = {}
+
+    def _tev():
+        return torch.cuda.Event(enable_timing=True)
 
     def h2d(dst: torch.Tensor, src: torch.Tensor):
         if a.h2d == "pull":  # the GPU pulls the pinned batch over PCIe (csrc/kernels/ingest.hip)
@@ -466,11 +474,25 @@ def main(argv=None) -> int:
                     consumed[slot].synchronize()
                 else:
                     cs.wait_event(consumed[slot])
+                e0, e1 = _tev(), _tev()
+                e0.record(cs)
                 h2d(dev[slot].flat, src.flat)
+                e1.record(cs)
+                ev_copy[k] = (e0, e1)
                 copied[slot].record(cs)
             prepare(slot, copied[slot])
         else:
             dev[slot].flat.copy_(src.flat)
+
+    def _round(k: int, batch):
+        if not on_gpu:
+            proto.round(batch)
+            return
+        e0, e1 = _tev(), _tev()
+        e0.record()
+        proto.round(batch)
+        e1.record()
+        ev_round[k] = (e0, e1)
 
     def _step(k: int):
         if a.ingest == "device":
@@ -478,7 +500,7 @@ def main(argv=None) -> int:
                 nb = (k + 1) % a.pool
                 prep_stream.wait_stream(torch.cuda.current_stream(device))
                 prepare(nb)
-            proto.round(dev[k % a.pool].batch)
+            _round(k, dev[k % a.pool].batch)
             return
         slot = k % nslots
         if ahead == 1 and k + 1 < n_rounds:
@@ -487,7 +509,7 @@ def main(argv=None) -> int:
             # (with a prep made ahead the round waits on the prep's event, which follows the
             # copy: a second cross-stream wait cost the round's launch ≈ 7 µs per step)
             torch.cuda.current_stream().wait_event(copied[slot])
-        proto.round(dev[slot].batch)
+        _round(k, dev[slot].batch)
         if on_gpu:
             consumed[slot].record()
         if ahead > 1 and k + ahead < n_rounds:
@@ -539,6 +561,14 @@ def main(argv=None) -> int:
     sync()
     elapsed = time.perf_counter() - t0
     coll_ms = proto.collective_time_ms() if proto.time_collectives else None
+    timed = range(a.warmup, a.warmup + a.steps)
+
+    def _dev_ms(evs):
+        v = [evs[k][0].elapsed_time(evs[k][1]) for k in timed if k in evs]
+        return round(sum(v) / len(v), 4) if v else None
+
+    copy_dev_ms = _dev_ms(ev_copy) if on_gpu else None
+    round_dev_ms = _dev_ms(ev_round) if on_gpu else None
     # the v3 round's in-launch combiners never gave up on a spoke (a timeout would leave a
     # spoke's update out of the round accumulator): checked after the timed window
     comb_err = int(native.hip().omldm_scan3_comb_err()) if on_gpu else 0
@@ -561,7 +591,7 @@ def main(argv=None) -> int:
 
     acc = accuracy(learner.w) if rank == 0 else None
     fitted = learner.running_totals()["fitted"]
-    ref_acc = None
+    ref_acc = ref64_acc = ref64_maxdw = None
     P_ref = S * world
     do_ref = a.ref == "on" or (a.ref == "auto" and rounds * B * world <= a.ref_max_examples)
     if rank == 0 and do_ref:
@@ -575,10 +605,18 @@ def main(argv=None) -> int:
             gpool.append(RawBatch(torch.cat([p.num for p in parts]),
                                   torch.cat([p.tok for p in parts]),
                                   torch.cat([p.y for p in parts])))
+        w64, d64 = torch.zeros(space.dim, dtype=torch.float64), \
+            torch.zeros(space.dim + 2, dtype=torch.float64)
         for k in range(rounds):
             L.linear_seq_round(wref, gpool[k % a.pool], R, P_ref, dref, ref_rule, 1.0)
             L.linear_apply(wref, None, dref)
+            if a.learner == "SVM":  # the reference's Double learner on the same stream
+                L.linear_seq_round64(w64, gpool[k % a.pool], R, P_ref, d64, ref_rule, 1.0)
+                L.linear_apply64(w64, d64)
         ref_acc = accuracy(wref)
+        if a.learner == "SVM":
+            ref64_acc = accuracy(w64.float())
+            ref64_maxdw = float((w64 - learner.w.detach().double().cpu()).abs().max())
 
     # ---- p50 single-point predict latency: the persistent serving wave reading a pinned
     # mailbox (raw tokens, hashed by the wave), against the trained fp32 model
@@ -651,6 +689,15 @@ def main(argv=None) -> int:
                        "parallelism": f"dp{world}", "protocol": "Synchronous",
                        "spokes_per_gpu": S, "rows_per_spoke_per_round": R,
                        "semantics": "exact sequential per spoke, replicas averaged per round"},
+            "device_copy_ms_per_step": copy_dev_ms,
+            "device_round_ms_per_step": round_dev_ms,
+            "step_bound": None if copy_dev_ms is None or round_dev_ms is None else
+                          ("copy (H2D)" if copy_dev_ms > round_dev_ms else "round"),
+            "device_time_semantics": "mean device time of the timed steps' batch copies "
+                                     "(copy lane) and rounds (compute lane, prep + scan + "
+                                     "apply), from timing-event pairs read after the final "
+                                     "sync (the copies of the first `batches_copied_ahead` "
+                                     "timed rounds ran in the warmup)",
             "p50_predict_latency_us": None if p50 is None else round(p50, 2),
             "p99_predict_latency_us": None if p99 is None else round(p99, 2),
             "engine_forecast_p50_us": None if eng is None else eng["p50"],
@@ -682,6 +729,14 @@ def main(argv=None) -> int:
             "ref_holdout_accuracy": None if ref_acc is None else round(ref_acc, 4),
             "ref_semantics": f"CPU sequential PA-I, P={P_ref} spokes, same stream and "
                              f"{rounds * B * world} examples (csrc/host/rawwire.cpp)",
+            "ref64_holdout_accuracy": None if ref64_acc is None else round(ref64_acc, 4),
+            "ref64_accuracy_gap_pt": None if ref64_acc is None or acc is None
+                                     else round((ref64_acc - acc) * 100, 3),
+            "ref64_max_abs_dw": None if ref64_maxdw is None else float(f"{ref64_maxdw:.3e}"),
+            "ref64_semantics": "the same sequential PA-I learner in DOUBLE precision (the "
+                               "reference's Breeze Double model, StateAccumulators.scala:5,26)"
+                               ", same stream, spokes and rounds; holdout accuracy and the "
+                               "max |w64 - w| against the GPU's fp32 model",
             "accuracy_gap_pt": None if ref_acc is None or acc is None
                                else round((ref_acc - acc) * 100, 3),
             "fitted_examples_rank0": fitted,

@@ -49,6 +49,9 @@ def main(argv=None) -> int:
     ap.add_argument("--forecast-server", default="auto", help="engine forecastServer flag")
     ap.add_argument("--unique", type=int, default=100_000,
                     help="distinct JSON records generated; the topic replays them")
+    ap.add_argument("--learners", default="",
+                    help="comma list of pipelines' learners instead of --pipelines SVMs, "
+                         "each NAME or NAME:key=value/key=value (e.g. SVM,K-means:k=16)")
     ap.add_argument("--format", default="json", choices=["json", "dib"],
                     help="topic records: DataInstance JSON (≈ 507 B) or the binary DIB "
                          "record of the same objects (≈ 162 B, omldm_amd/io/dib.py)")
@@ -84,11 +87,20 @@ def main(argv=None) -> int:
                     br.produce_block(topic, p, b"\n".join(recs) + b"\n")
         del per_part
         gen_s = time.time() - t
-        for i in range(a.pipelines):
+        specs = []
+        for spec in [t for t in a.learners.split(",") if t]:
+            name, _, kv = spec.partition(":")
+            hyper = {}
+            for item in [t for t in kv.split("/") if t]:
+                k, _, v = item.partition("=")
+                hyper[k] = json.loads(v) if v[:1] in "-0123456789[{tf" else v
+            specs.append((name, hyper))
+        if not specs:
+            specs = [("SVM", {"modelDtype": a.model_dtype, "tableLog2": 11})] * a.pipelines
+        for i, (name, hyper) in enumerate(specs):
             br.produce("requests", json.dumps({
                 "id": i + 1, "request": "Create",
-                "learner": {"name": "SVM", "hyperParameters": {"modelDtype": a.model_dtype,
-                                                               "tableLog2": 11}},
+                "learner": {"name": name, "hyperParameters": hyper},
                 "trainingConfiguration": {"protocol": "Synchronous"}}))
         addr = f"file://{root}"
         args = []
@@ -138,7 +150,7 @@ def main(argv=None) -> int:
                 "format": a.format, "record_bytes": round(rec_bytes, 1),
                 "value": round((job.counters["records"] - r0) * comm.world / max(wall, 1e-9), 1),
                 "unit": "records/s", "n_gpus": comm.world, "records": job.counters["records"],
-                "pipelines": a.pipelines, "batch": a.batch, "wall_s": round(wall, 3),
+                "pipelines": len(specs), "learners": [n for n, _ in specs], "batch": a.batch, "wall_s": round(wall, 3),
                 "spokes": job.spokes, "model_dtype": a.model_dtype,
                 "forecast_frac": a.forecast_frac, "predictions": job.counters["predictions"],
                 "forecast_lane": lane,

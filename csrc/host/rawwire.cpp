@@ -69,36 +69,39 @@ struct Rule {
 };
 
 // (loss, mistake, sq_err, c) of one example with margin m, label y, ‖x‖² n2 — the same
-// closed forms as the GPU kernels (Crammer et al. 2006 PA family).
-inline float step(const Rule& r, float m, float y, float n2, float& loss, float& mist,
-                  float& sqe) {
+// closed forms as the GPU kernels (Crammer et al. 2006 PA family). T is
+// float (the GPU's precision) or double (the reference's Breeze Double vectors,
+// omldm/state/StateAccumulators.scala:5,26).
+template <typename T>
+inline T step(const Rule& r, T m, T y, T n2, T& loss, T& mist, T& sqe) {
+  const T C = (T)r.C, zero = (T)0, one = (T)1;
   if (r.rule == 0) {  // hinge: PA / PA-I / PA-II
-    const float ym = y * m;
-    const float l = std::fmax(0.f, 1.f - ym);
+    const T ym = y * m;
+    const T l = std::fmax(zero, one - ym);
     loss += l;
-    mist += ym <= 0.f ? 1.f : 0.f;
-    if (l <= 0.f || n2 <= 0.f) return 0.f;
-    const float tau = r.variant == 0 ? l / n2
-                    : r.variant == 1 ? std::fmin(r.C, l / n2)
-                                     : l / (n2 + 0.5f / r.C);
+    mist += ym <= zero ? one : zero;
+    if (l <= zero || n2 <= zero) return zero;
+    const T tau = r.variant == 0 ? l / n2
+                : r.variant == 1 ? std::fmin(C, l / n2)
+                                 : l / (n2 + (T)0.5 / C);
     return tau * y;
   }
   if (r.rule == 1) {  // ε-insensitive regression
-    const float err = y - m;
-    const float l = std::fmax(0.f, std::fabs(err) - r.eps);
+    const T err = y - m;
+    const T l = std::fmax(zero, std::fabs(err) - (T)r.eps);
     loss += l;
     sqe += err * err;
-    if (l <= 0.f || n2 <= 0.f) return 0.f;
-    const float tau = r.variant == 0 ? l / n2
-                    : r.variant == 1 ? std::fmin(r.C, l / n2)
-                                     : l / (n2 + 0.5f / r.C);
-    return err >= 0.f ? tau : -tau;
+    if (l <= zero || n2 <= zero) return zero;
+    const T tau = r.variant == 0 ? l / n2
+                : r.variant == 1 ? std::fmin(C, l / n2)
+                                 : l / (n2 + (T)0.5 / C);
+    return err >= zero ? tau : -tau;
   }
   // logistic SGD
-  const float z = y * m;
-  loss += z > 0.f ? std::log1p(std::exp(-z)) : (-z + std::log1p(std::exp(z)));
-  mist += z <= 0.f ? 1.f : 0.f;
-  return r.lr * y / (1.f + std::exp(z));
+  const T z = y * m;
+  loss += z > zero ? std::log1p(std::exp(-z)) : (-z + std::log1p(std::exp(z)));
+  mist += z <= zero ? one : zero;
+  return (T)r.lr * y / (one + std::exp(z));
 }
 
 }  // namespace
@@ -181,29 +184,30 @@ OMLDM_HOST_API void omldm_cpu_hash_raw(const uint32_t* tok, int64_t B, int dc, i
 // yields w + Σ Δ_s / P_active — model averaging). stats [S, 6]: loss, n, mistakes,
 // sq_err, 1, 0. The merge runs in spoke order: the result does not depend on nthreads.
 // y8 != 0: labels are int8.
-OMLDM_HOST_API int omldm_cpu_linear_seq_round(const float* w, const float* num, int dn,
+template <typename T>
+static int cpu_linear_seq_round(const T* w, const float* num, int dn,
                                               const uint32_t* tok, int dc, const void* yv,
-                                              int y8, int B, int R, int S, float* dacc, int dim,
+                                              int y8, int B, int R, int S, T* dacc, int dim,
                                               float* stats, int rule, int variant, float C,
                                               float eps, float lr, float inv_p, int bias,
                                               int nthreads) {
   const Rule r{rule, variant, C, eps, lr, 0.f};
   if (S <= 0 || R <= 0) return 0;
-  std::vector<std::vector<std::pair<int, float>>> out(S);
+  std::vector<std::vector<std::pair<int, T>>> out(S);
   const int nth = std::max(1, std::min(nthreads, S));
   parallel_for(S, nth, [&](int s0, int s1, int) {
-    std::vector<float> D(dim, 0.f);
+    std::vector<T> D(dim, (T)0);
     std::vector<int> touched;
     std::vector<int> idx(dn + dc + 1);
-    std::vector<float> xv(dn + dc + 1);
+    std::vector<T> xv(dn + dc + 1);
     for (int s = s0; s < s1; ++s) {
       const int64_t a = std::min<int64_t>(int64_t(s) * R, B);
       const int64_t b = std::min<int64_t>(a + R, B);
-      float loss = 0.f, nex = 0.f, mist = 0.f, sqe = 0.f;
+      T loss = 0, nex = 0, mist = 0, sqe = 0;
       touched.clear();
       for (int64_t t = a; t < b; ++t) {
-        const float yt = y8 ? float(static_cast<const int8_t*>(yv)[t])
-                            : static_cast<const float*>(yv)[t];
+        const T yt = y8 ? T(static_cast<const int8_t*>(yv)[t])
+                        : T(static_cast<const float*>(yv)[t]);
         if (std::isnan(yt)) continue;
         int F = 0;
         for (int j = 0; j < dn && j < dim; ++j) {
@@ -215,40 +219,40 @@ OMLDM_HOST_API int omldm_cpu_linear_seq_round(const float* w, const float* num, 
           if (tk == kAbsentToken) continue;
           const int32_t h = hash_token(tk, j, dn, dc, dim);
           idx[F] = h & 0x7fffffff;
-          xv[F++] = h < 0 ? -1.f : 1.f;
+          xv[F++] = h < 0 ? T(-1) : T(1);
         }
         if (bias) {
           idx[F] = dim - 1;
-          xv[F++] = 1.f;
+          xv[F++] = T(1);
         }
-        float m = 0.f, n2 = 0.f;
+        T m = 0, n2 = 0;
         for (int f = 0; f < F; ++f) {
           m += xv[f] * (w[idx[f]] + D[idx[f]]);
           n2 += xv[f] * xv[f];
         }
-        const float c = step(r, m, yt, n2, loss, mist, sqe);
-        nex += 1.f;
-        if (c != 0.f)
+        const T c = step<T>(r, m, yt, n2, loss, mist, sqe);
+        nex += T(1);
+        if (c != T(0))
           for (int f = 0; f < F; ++f) {
-            float& d = D[idx[f]];
-            if (d == 0.f) touched.push_back(idx[f]);
+            T& d = D[idx[f]];
+            if (d == T(0)) touched.push_back(idx[f]);
             d += c * xv[f];
           }
       }
       auto& o = out[s];
       o.clear();
       for (int j : touched) {
-        if (D[j] != 0.f) o.emplace_back(j, D[j]);
-        D[j] = 0.f;
+        if (D[j] != T(0)) o.emplace_back(j, D[j]);
+        D[j] = T(0);
       }
       // a key whose delta returned to exactly 0 and was touched again appears twice:
       // the first entry was taken and zeroed, the second finds 0 and is skipped
       float* st = stats ? stats + size_t(s) * 6 : nullptr;
       if (st) {
-        st[0] = loss;
-        st[1] = nex;
-        st[2] = mist;
-        st[3] = sqe;
+        st[0] = (float)loss;
+        st[1] = (float)nex;
+        st[2] = (float)mist;
+        st[3] = (float)sqe;
         st[4] = 1.f;
         st[5] = 0.f;
       }
@@ -256,9 +260,31 @@ OMLDM_HOST_API int omldm_cpu_linear_seq_round(const float* w, const float* num, 
   });
   for (int s = 0; s < S; ++s) {
     if (int64_t(s) * R >= B) continue;
-    for (auto& kv : out[s]) dacc[kv.first] += kv.second * inv_p;
-    dacc[dim] += inv_p;
-    dacc[dim + 1] += inv_p;
+    for (auto& kv : out[s]) dacc[kv.first] += kv.second * (T)inv_p;
+    dacc[dim] += (T)inv_p;
+    dacc[dim + 1] += (T)inv_p;
   }
   return 0;
+}
+
+OMLDM_HOST_API int omldm_cpu_linear_seq_round(const float* w, const float* num, int dn,
+                                              const uint32_t* tok, int dc, const void* yv,
+                                              int y8, int B, int R, int S, float* dacc, int dim,
+                                              float* stats, int rule, int variant, float C,
+                                              float eps, float lr, float inv_p, int bias,
+                                              int nthreads) {
+  return cpu_linear_seq_round<float>(w, num, dn, tok, dc, yv, y8, B, R, S, dacc, dim, stats,
+                                     rule, variant, C, eps, lr, inv_p, bias, nthreads);
+}
+
+// The same round in double precision (the reference's Breeze Double model): w, dacc fp64;
+// the bench's parity row (the fp32 kernels' accuracy against the Double learner's).
+OMLDM_HOST_API int omldm_cpu_linear_seq_round64(const double* w, const float* num, int dn,
+                                                const uint32_t* tok, int dc, const void* yv,
+                                                int y8, int B, int R, int S, double* dacc,
+                                                int dim, float* stats, int rule, int variant,
+                                                float C, float eps, float lr, float inv_p,
+                                                int bias, int nthreads) {
+  return cpu_linear_seq_round<double>(w, num, dn, tok, dc, yv, y8, B, R, S, dacc, dim, stats,
+                                      rule, variant, C, eps, lr, inv_p, bias, nthreads);
 }

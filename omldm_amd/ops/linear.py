@@ -781,6 +781,32 @@ def linear_seq_round(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: tor
     return False
 
 
+def linear_seq_round64(w: torch.Tensor, batch: RawBatch, R: int, S: int, dacc: torch.Tensor,
+                       rule: "LinearRule", inv_p: float) -> None:
+    """The reference semantics of one Synchronous round in DOUBLE precision (CPU; the
+    reference's Breeze Double model, omldm/state/StateAccumulators.scala:5,26): spoke s fits
+    rows [sR, sR + R) one at a time on its fp64 replica, dacc (fp64, [dim + 2]) collects the
+    averaged deltas; ``linear_apply64`` folds it into w. The fp32 kernels' parity row."""
+    assert w.dtype == torch.float64 and dacc.dtype == torch.float64 and not w.is_cuda
+    num, tok, y = batch.num.contiguous(), batch.tok.contiguous(), batch.y.contiguous()
+    dim = int(dacc.shape[0]) - 2
+    st = torch.zeros((S, STAT_W), dtype=torch.float32)
+    check(native.host().omldm_cpu_linear_seq_round64(
+        ptr(w), ptr(num), num.shape[1], ptr(tok), tok.shape[1], ptr(y),
+        int(y.dtype == torch.int8), batch.B, R, S, ptr(dacc), dim, ptr(st), rule.rule,
+        rule.variant, rule.C, rule.eps, rule.lr, inv_p, int(rule.bias), _cpu_threads()),
+        "omldm_cpu_linear_seq_round64")
+
+
+def linear_apply64(w: torch.Tensor, dacc: torch.Tensor) -> None:
+    """fp64 ``linear_apply``: w = (dacc[dim]·w + dacc[:dim]) / dacc[dim+1]; dacc = 0."""
+    dim = int(w.shape[0])
+    n = float(dacc[dim + 1])
+    if n > 0:
+        w.mul_(float(dacc[dim])).add_(dacc[:dim]).div_(n)
+    dacc.zero_()
+
+
 def linear_seq_apply(w: torch.Tensor, replicas: torch.Tensor, dacc: torch.Tensor) -> None:
     """GPU: w = model average of the (all-reduced) round accumulator, every replica ← w,
     dacc ← 0 (one pass over HBM)."""

@@ -209,6 +209,8 @@ HOST_SIGS = [
     ("omldm_cpu_hash_raw", None, [vp, i64, i32, i32, i64, vp, i32]),
     ("omldm_cpu_linear_seq_round", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, vp, i32,
                                          vp, i32, i32, f32, f32, f32, f32, i32, i32]),
+    ("omldm_cpu_linear_seq_round64", i32, [vp, vp, i32, vp, i32, vp, i32, i32, i32, i32, vp,
+                                           i32, vp, i32, i32, f32, f32, f32, f32, i32, i32]),
 ]
 
 
