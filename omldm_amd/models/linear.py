@@ -207,8 +207,11 @@ class LinearLearner(Learner):
                 return None
         r = self.rule
         r.tbase = float(self.t0 + 1 + self.steps)  # (Pegasos: the prep depends on the clock)
+        # (logistic: lr·y is folded into the prep's Gram columns, so only equal learning
+        # rates share a prep — ops.linear._s3_key)
         return (self.dim, r.rule, r.variant, r.bias, r.C if r.variant == L.PA2 else None,
-                L._s3_shrink(r), self.w16 is not None)
+                L._s3_shrink(r), self.w16 is not None,
+                float(r.lr) if r.rule == L.RULE_LOGISTIC else None)
 
     def prepare_ahead(self, batch: HashedBatch, ctx: RoundContext, stream) -> bool:
         """Make the v3 prep of this learner's round on ``batch`` now, on ``stream``, and

@@ -99,3 +99,21 @@ def test_engine_fuses_linear_pipelines_into_one_launch():
     for pid in models["true"]:
         d = (models["true"][pid] - models["false"][pid]).abs()
         assert float(d.max()) < 1e-4, (pid, float(d.max()))
+
+
+def test_logistic_pipelines_share_a_launch_only_at_equal_learning_rates():
+    """The logistic prep folds lr·y into its Gram columns: pipelines with different
+    learning rates need their own preps, so they never form one fused group (a mixed group
+    failed the one-launch assertion in the config-5 engine run)."""
+    from omldm_amd.api.batch import FeatureSpace
+    from omldm_amd.io.synthetic import synth_raw
+    from omldm_amd.models.base import RoundContext
+    from omldm_amd.models.linear import LogisticRegression
+
+    dev = torch.device("cuda", 0)
+    space = FeatureSpace(13, 0, 26, 1 << 16)
+    b = synth_raw(space, 16 * 256, seed=4).to(dev)
+    ctx = RoundContext(spokes=16, inv_p=1.0, fused_delta=True)
+    ks = [LogisticRegression({"learningRate": lr}, space, dev).group_key(b, ctx)
+          for lr in (0.05, 0.05, 0.2)]
+    assert ks[0] is not None and ks[0] == ks[1] and ks[0] != ks[2]
