@@ -634,6 +634,7 @@ struct S3Cand {
 
 __device__ unsigned long long* g_s3_stamps;
 __device__ int g_s3_debug;  // diagnostics: 1 = every gather reads w[0] (latency experiment)
+__device__ unsigned long long* g_s3mc_dbg;  // MultiClassPA scan phase cycles (null: off)
 __device__ int g_s3_comb_err;  // a combiner gave up waiting for its spoke (bounded spin)
 __device__ int g_s3_dense_order = 0;  // helpers' dense column ownership (see s3_scan_kernel)
 __device__ int g_s3_hprio = 0;         // helpers' issue priorities by age (A/B: see s3_scan_body)
@@ -1796,7 +1797,10 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     for (int k = 0; k < K; ++k) f1[k] = 0.f;
     float ynx = chunk_prep(0)[s3_prep_y<KN>() + lane];
     float anx = chunk_prep(0)[2 * s3::MAT + lane];
+    unsigned long long* const dbg = g_s3mc_dbg;
+    unsigned long long t_chain = 0, t_wait = 0;
     for (int k = -1; k <= nch; ++k) {
+      const unsigned long long ta = dbg ? __builtin_amdgcn_s_memtime() : 0;
       if (k >= 0 && k < nch) {
         const int b = k & 1;
         const int row = t0 + k * s3::CH + lane;
@@ -1872,7 +1876,14 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
         for (int c = 0; c < K; ++c) f1[c] = n1[c];
       }
-      __syncthreads();
+      if (dbg) {
+        const unsigned long long tb = __builtin_amdgcn_s_memtime();
+        __syncthreads();
+        t_chain += tb - ta;
+        t_wait += __builtin_amdgcn_s_memtime() - tb;
+      } else {
+        __syncthreads();
+      }
     }
     loss = wave_sum(loss);
     nex = wave_sum(nex);
@@ -1881,6 +1892,11 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       float* wr = A.ws + (size_t)s * s3::WS;
       wr[0] = loss, wr[1] = nex, wr[2] = mist;
       for (int i = 3; i < s3::WS; ++i) wr[i] = 0.f;
+      if (dbg) {  // [s·8]: chunks, scanner chain, scanner barrier wait, helper phases (sums)
+        atomicAdd(&dbg[s * 8 + 0], (unsigned long long)nch);
+        atomicAdd(&dbg[s * 8 + 1], t_chain);
+        atomicAdd(&dbg[s * 8 + 2], t_wait);
+      }
     }
     return;
   }
@@ -1964,9 +1980,12 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     if (!SPILL || lid < capid) atomicAdd(&tab[lid * K + c], v);
     else atomicAdd(&ag[(size_t)(lid - capid) * K + c], v);
   };
+  unsigned long long* const hdbg = g_s3mc_dbg;
+  unsigned long long h_sc = 0, h_mg = 0, h_st = 0, h_wt = 0;
   auto body = [&](auto spill_tag, int k, Set& CUR, Set& NXT) {
     constexpr bool SPILL = decltype(spill_tag)::value;
     const int cn = k + 1, ks = k - 1;
+    const unsigned long long ha = hdbg ? __builtin_amdgcn_s_memtime() : 0;
     load_words(cn + 1, NXT);
     issue_staging(cn + 1, NXT);
     load_dense(ks + 1, NXT.xs);
@@ -2002,6 +2021,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         }
       }
     }
+    const unsigned long long hb = hdbg ? __builtin_amdgcn_s_memtime() : 0;
     // ---- base margins of chunk cn
     if (cn < nch) {
       float base[K];
@@ -2055,6 +2075,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int c = 0; c < K; ++c) sm.part[cn & 1][q][c][r] = base[c];
     }
+    const unsigned long long hc = hdbg ? __builtin_amdgcn_s_memtime() : 0;
     // ---- aG_{cn} → G[cn & 1], aX1_{cn+1} → X1[(cn+1) & 1]
 #pragma unroll
     for (int u = 0; u < NV4; ++u) {
@@ -2072,7 +2093,16 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       p2[i] = p1[i];
       p1[i] = CUR.cm[i];
     }
-    __syncthreads();
+    if (hdbg) {
+      const unsigned long long hd = __builtin_amdgcn_s_memtime();
+      __syncthreads();
+      h_sc += hb - ha;
+      h_mg += hc - hb;
+      h_st += hd - hc;
+      h_wt += __builtin_amdgcn_s_memtime() - hd;
+    } else {
+      __syncthreads();
+    }
   };
   Set Sa, Sb;
 #pragma unroll
@@ -2101,6 +2131,13 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int c = 0; c < K; ++c)
         A.wsd[((size_t)s * K + c) * s3::DS + j] = j < KN ? wn[c][i] - w0[c][i] : 0.f;
+  }
+  if (hdbg && lane == 0) {  // helper phases summed over the helper waves
+    atomicAdd(&hdbg[s * 8 + 3], h_sc);
+    atomicAdd(&hdbg[s * 8 + 4], h_mg);
+    atomicAdd(&hdbg[s * 8 + 5], h_st);
+    atomicAdd(&hdbg[s * 8 + 6], h_wt);
+    if (q == 0) atomicAdd(&hdbg[s * 8 + 7], (unsigned long long)(lidcount[s] > capid));
   }
 }
 
@@ -2658,6 +2695,11 @@ OMLDM_API int omldm_scan3_dense_order(int v) {
 
 OMLDM_API int omldm_scan3_debug(int v) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s3_debug), &v, sizeof(v));
+}
+
+// MultiClassPA scan diagnostics: buf = u64 [S·8] (accumulated; null turns them off).
+OMLDM_API int omldm_scan3mc_debug(void* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_s3mc_dbg), &buf, sizeof(buf));
 }
 
 OMLDM_API int omldm_scan3_stamps(void* buf) {

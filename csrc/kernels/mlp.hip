@@ -40,6 +40,9 @@ struct MlpDesc {
   int lw[kMaxLayers], lb[kMaxLayers], ldw[kMaxLayers];
   int lh[kMaxLayers + 1], ldh[kMaxLayers + 1];
   int lg0, lg1, ldg, ly, total;
+  // round kernel v2 (mlp_round2_kernel): bias-gradient accumulators per layer, three
+  // rotating gradient buffers, a 4-float statistics scratch
+  int lbg[kMaxLayers], lgb[3], lsc;
 };
 
 // C[32×32] = A[32×K]·B[K×32] with A(i,k) = a[i·ars + k·acs], B(k,j) = b[k·brs + j·bcs].
@@ -483,6 +486,315 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ round kernel v2
+// The same mini-batch SGD, restructured for step latency (one 32-row step of a
+// [13, 64, 64, 1] spoke is a chain of ~10 small GEMMs on one CU; the v1 kernel spent
+// ~15 µs per step there, mostly in barriers, zero-padded work and serial loops):
+// * widths padded to 16, not 32 (13 → 16 inputs, 1 → 16 outputs: half the MFMAs of the
+//   first and last layers; row strides stay ≡ 4 floats mod 64 banks);
+// * the loss is the last layer's epilogue: a row's ≤ 16 logits sit in one 16-lane DPP
+//   row of the accumulator, so softmax max / sum / argmax are row_ror reductions and the
+//   output gradient goes straight to LDS (no loss phase, no barrier);
+// * bias gradients are column sums taken in the epilogue that produces each gradient
+//   (LDS float atomics), not a 32-row serial loop per layer;
+// * backward phase l computes dH_l (reads W_l) together with the update of W_{l+1} (whose
+//   dH was the previous phase) from three rotating gradient buffers, and the last phase
+//   updates W_1 and W_0 together: one barrier per layer instead of two;
+// * the valid-row count of a step comes from a ballot over the staged labels in every
+//   wave (no block-wide count);
+// * operand loads of the next 16-wide k step are issued before the current MFMAs.
+// Same arithmetic as v1 (fp32 MFMA, same mini-batch order); sums may associate
+// differently.
+template <bool AK, bool BK>
+__device__ __forceinline__ f32x4 gemm16p(const float* a, int ars, int acs, const float* b,
+                                         int brs, int bcs, int K, int bf16) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float* ap = a + r * ars + 4 * g * (AK ? 1 : acs);
+  const float* bp = b + 4 * g * (BK ? 1 : brs) + r * bcs;
+  float av[4], bv[4];
+  auto load = [&](int k, float (&x)[4], float (&y)[4]) {
+    if constexpr (AK) {
+      const float4 t = *reinterpret_cast<const float4*>(ap + k);
+      x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = ap[(k + u) * acs];
+    }
+    if constexpr (BK) {
+      const float4 t = *reinterpret_cast<const float4*>(bp + k);
+      y[0] = t.x; y[1] = t.y; y[2] = t.z; y[3] = t.w;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) y[u] = bp[(k + u) * brs];
+    }
+  };
+  load(0, av, bv);
+  for (int k = 0; k < K; k += 16) {
+    float an[4], bn[4];
+    if (k + 16 < K) load(k + 16, an, bn);
+    if (bf16) {
+      const bf16x4 af = {bf16_bits(av[0]), bf16_bits(av[1]), bf16_bits(av[2]), bf16_bits(av[3])};
+      const bf16x4 bfv = {bf16_bits(bv[0]), bf16_bits(bv[1]), bf16_bits(bv[2]), bf16_bits(bv[3])};
+      acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, bfv, acc, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+    if (k + 16 < K) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) av[u] = an[u], bv[u] = bn[u];
+    }
+  }
+  return acc;
+}
+
+// 16-lane DPP row reductions (every lane of the row gets the result)
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x124>(v));
+  return fmaxf(v, dpp_mov<0x128>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x124>(v);
+  return v + dpp_mov<0x128>(v);
+}
+__device__ __forceinline__ float row16_min(float v) {
+  v = fminf(v, dpp_mov<0xB1>(v));
+  v = fminf(v, dpp_mov<0x4E>(v));
+  v = fminf(v, dpp_mov<0x124>(v));
+  return fminf(v, dpp_mov<0x128>(v));
+}
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
+    const float* __restrict__ w, const float* __restrict__ x, const float* __restrict__ yv,
+    long long B, int R, float lr, float* __restrict__ dacc, float* __restrict__ stats,
+    float* __restrict__ nact, MlpDesc g, float* __restrict__ ws, int nparams) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr int NT = NW * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int ci = lane & 15, cg = lane >> 4;  // accumulator column / row group
+  const long long r0 = (long long)blockIdx.x * R;
+  const long long r1 = min(B, r0 + R);
+  if (r0 >= B) return;
+  load_model(w, sm, g);
+  const int L = g.L;
+  for (int l = 0; l < L; ++l)
+    for (int o = tid; o < g.np[l + 1]; o += NT) sm[g.lbg[l] + o] = 0.f;
+  if (tid < 4) sm[g.lsc + tid] = 0.f;
+  float loss = 0.f, corr = 0.f, nv = 0.f;
+  auto gb = [&](int j) { return sm + g.lgb[j % 3]; };
+  // staging: the next mini-batch's rows in registers while the current one trains
+  constexpr int kSlots = (kMB * 64 + NT - 1) / NT;
+  const int np0 = g.np[0], n0 = g.n[0], ld0 = g.ldh[0];
+  const bool pf = np0 <= 64;
+  int soff[kSlots], srow[kSlots], scol[kSlots];
+#pragma unroll
+  for (int j = 0; j < kSlots; ++j) {
+    const int i = tid + NT * j;
+    const bool in = pf && i < kMB * np0;
+    srow[j] = in ? i / np0 : -1;
+    scol[j] = in ? i - srow[j] * np0 : 0;
+    soff[j] = in ? srow[j] * ld0 + scol[j] : 0;
+  }
+  float xr[kSlots];
+  float yr = 0.f;
+  auto fetch = [&](long long m) {
+#pragma unroll
+    for (int j = 0; j < kSlots; ++j) {
+      const long long row = min(m + (srow[j] < 0 ? 0 : srow[j]), r1 - 1);
+      xr[j] = x[row * n0 + (scol[j] < n0 ? scol[j] : 0)];
+    }
+    yr = yv[min(m + (tid < kMB ? tid : 0), r1 - 1)];
+  };
+  if (pf) fetch(r0);
+  __syncthreads();
+  for (long long m0 = r0; m0 < r1; m0 += kMB) {
+    if (pf) {
+      float* H = sm + g.lh[0];
+#pragma unroll
+      for (int j = 0; j < kSlots; ++j)
+        if (srow[j] >= 0) H[soff[j]] = (m0 + srow[j] < r1 && scol[j] < n0) ? xr[j] : 0.f;
+      if (tid < kMB) sm[g.ly + tid] = m0 + tid < r1 ? yr : __builtin_nanf("");
+      if (m0 + kMB < r1) fetch(m0 + kMB);
+    } else {
+      stage_rows(x, m0, r1, sm, g);
+      if (tid < kMB) {
+        const long long row = m0 + tid;
+        sm[g.ly + tid] = row < r1 ? yv[row] : __builtin_nanf("");
+      }
+    }
+    __syncthreads();
+    // valid rows of the step: every wave counts them itself
+    const float yl = sm[g.ly + (lane & 31)];
+    const int cnt = __builtin_popcountll(__builtin_amdgcn_ballot_w64(lane < 32 && yl == yl));
+    if (cnt == 0) {
+      __syncthreads();
+      continue;
+    }
+    const float eta = lr / (float)cnt;
+    // ---- hidden layers: H_{l+1} = act(H_l · W_lᵀ + b_l)
+    for (int l = 0; l + 1 < L; ++l) {
+      const float* H = sm + g.lh[l];
+      float* Ho = sm + g.lh[l + 1];
+      const float* W = sm + g.lw[l];
+      const float* bs = sm + g.lb[l];
+      const int ntc = g.np[l + 1] / 16, nt = 2 * ntc, ldo = g.ldh[l + 1];
+      for (int t = wave; t < nt; t += NW) {
+        const int rt = t / ntc, ct = t - rt * ntc;
+        const f32x4 acc = gemm16p<true, true>(H + rt * 16 * g.ldh[l], g.ldh[l], 1,
+                                              W + ct * 16 * g.ldw[l], 1, g.ldw[l], g.np[l], g.bf16);
+        const int col = ct * 16 + ci;
+        const float bias = bs[col];
+        const bool pad = col >= g.n[l + 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = acc[q] + bias;
+          Ho[(rt * 16 + 4 * cg + q) * ldo + col] = pad ? 0.f : act_fwd(v, g.act);
+        }
+      }
+      __syncthreads();
+    }
+    // ---- output layer + loss (np_L = 16: one column tile, a row's logits in one DPP row)
+    {
+      const int l = L - 1;
+      float* GL = gb(L);
+      for (int rt = wave; rt < 2; rt += NW) {
+        const f32x4 acc = gemm16p<true, true>(sm + g.lh[l] + rt * 16 * g.ldh[l], g.ldh[l], 1,
+                                              sm + g.lw[l], 1, g.ldw[l], g.np[l], g.bf16);
+        const float bias = sm[g.lb[l] + ci];
+        float csum = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = rt * 16 + 4 * cg + q;
+          const float o = acc[q] + bias;
+          const float y = sm[g.ly + row];
+          const bool valid = y == y;
+          float gr = 0.f;
+          if (g.task == 2) {
+            const bool live = ci < g.K;
+            int yi = valid ? (int)y : 0;
+            yi = yi < 0 ? 0 : (yi >= g.K ? g.K - 1 : yi);
+            const float m = row16_max(live ? o : -INFINITY);
+            const float e = live ? __expf(o - m) : 0.f;
+            const float se = row16_sum(e);
+            const float am = row16_min(live && o == m ? (float)ci : 64.f);
+            gr = valid && live ? e / se - (ci == yi ? 1.f : 0.f) : 0.f;
+            if (valid && ci == yi) {
+              loss += -(o - m - __logf(se));
+              corr += (int)am == yi ? 1.f : 0.f;
+            }
+          } else if (ci == 0 && valid) {
+            if (g.task == 0) {
+              const float e = o - y;
+              gr = 2.f * e;
+              loss += e * e;
+            } else {
+              const float tt = y > 0.f ? 1.f : 0.f;
+              gr = 1.f / (1.f + __expf(-o)) - tt;
+              loss += fmaxf(o, 0.f) - o * tt + log1pf(__expf(-fabsf(o)));
+              corr += ((o >= 0.f) == (tt > 0.f)) ? 1.f : 0.f;
+            }
+          }
+          if (ci == 0 && valid) nv += 1.f;
+          GL[row * g.ldg + ci] = gr;
+          csum += gr;
+        }
+        atomicAdd(&sm[g.lbg[l] + ci], csum);
+      }
+      __syncthreads();
+    }
+    // ---- backward: phase l = dH_l (l ≥ 1) + update of W_{l+1} (l + 1 ≤ L − 1), and the
+    // last phase (l = 0) updates W_1 and W_0
+    for (int l = L - 1; l >= 0; --l) {
+      const int na = l >= 1 ? 2 * (g.np[l] / 16) : 0;
+      const int ub = l + 1 <= L - 1 ? l + 1 : -1;  // W_{l+1}
+      const int nb = ub >= 0 ? (g.np[ub + 1] / 16) * (g.np[ub] / 16) : 0;
+      const int nc = l == 0 ? (g.np[1] / 16) * (g.np[0] / 16) : 0;
+      for (int t = wave; t < na + nb + nc; t += NW) {
+        if (t < na) {  // dH_l = (G_{l+1} · W_l) ⊙ act'(H_l)
+          const float* Gc = gb(l + 1);
+          float* Gn = gb(l);
+          const float* W = sm + g.lw[l];
+          const float* H = sm + g.lh[l];
+          const int ntc = g.np[l] / 16, rt = t / ntc, ct = t - rt * ntc;
+          const f32x4 acc = gemm16p<true, false>(Gc + rt * 16 * g.ldg, g.ldg, 1, W + ct * 16,
+                                                 g.ldw[l], 1, g.np[l + 1], g.bf16);
+          const int col = ct * 16 + ci;
+          float csum = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int row = rt * 16 + 4 * cg + q;
+            const float v = acc[q] * act_grad(H[row * g.ldh[l] + col], g.act);
+            Gn[row * g.ldg + col] = v;
+            csum += v;
+          }
+          atomicAdd(&sm[g.lbg[l - 1] + col], csum);
+        } else {  // W_u −= η · G_{u+1}ᵀ · H_u
+          const int u = t < na + nb ? ub : 0;
+          const int tt = t < na + nb ? t - na : t - na - nb;
+          const float* Gc = gb(u + 1);
+          float* W = sm + g.lw[u];
+          const float* H = sm + g.lh[u];
+          const int ntc = g.np[u] / 16, to = tt / ntc, tc = tt - to * ntc;
+          const f32x4 acc = gemm16p<false, false>(Gc + to * 16, 1, g.ldg, H + tc * 16, g.ldh[u], 1,
+                                                  kMB, g.bf16);
+          const int c = tc * 16 + ci;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) W[(to * 16 + 4 * cg + q) * g.ldw[u] + c] -= eta * acc[q];
+        }
+      }
+      auto bias_step = [&](int u) {
+        for (int o = tid; o < g.np[u + 1]; o += NT) {
+          sm[g.lb[u] + o] -= eta * sm[g.lbg[u] + o];
+          sm[g.lbg[u] + o] = 0.f;
+        }
+      };
+      if (ub >= 0) bias_step(ub);
+      if (l == 0) bias_step(0);
+      __syncthreads();
+    }
+  }
+  // ---- round end: Δ = W_spoke − W_0 (as v1)
+  float* wrow = ws ? ws + (size_t)blockIdx.x * nparams : nullptr;
+  for (int l = 0; l < L; ++l) {
+    const int nin = g.n[l], nout = g.n[l + 1], ld = g.ldw[l];
+    const float* W = sm + g.lw[l];
+    for (int i = tid; i < nout * nin; i += NT) {
+      const int o = i / nin, c = i - o * nin;
+      const float d = W[o * ld + c] - w[g.woff[l] + i];
+      if (wrow) wrow[g.woff[l] + i] = d;
+      else if (d != 0.f) atomicAdd(&dacc[g.woff[l] + i], d);
+    }
+    for (int o = tid; o < nout; o += NT) {
+      const float d = sm[g.lb[l] + o] - w[g.boff[l] + o];
+      if (wrow) wrow[g.boff[l] + o] = d;
+      else if (d != 0.f) atomicAdd(&dacc[g.boff[l] + o], d);
+    }
+  }
+  loss = wave_sum(loss);
+  corr = wave_sum(corr);
+  nv = wave_sum(nv);
+  if (lane == 0 && nv > 0.f) {
+    atomicAdd(&sm[g.lsc + 0], loss);
+    atomicAdd(&sm[g.lsc + 1], nv);
+    atomicAdd(&sm[g.lsc + 2], corr);
+  }
+  __syncthreads();
+  if (tid == 0 && sm[g.lsc + 1] > 0.f) {
+    atomicAdd(&stats[0], sm[g.lsc + 0]);
+    atomicAdd(&stats[1], sm[g.lsc + 1]);
+    atomicAdd(&stats[2], sm[g.lsc + 2]);
+    atomicAdd(&stats[3], 1.f);
+    if (nact) atomicAdd(nact, 1.f);
+  }
+}
+
 // Inference: every block stages the model once and walks 32-row tiles (grid-stride).
 __global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restrict__ w,
                                                           const float* __restrict__ x,
@@ -504,7 +816,7 @@ __global__ __launch_bounds__(256) void mlp_forward_kernel(const float* __restric
   }
 }
 
-static int make_desc(int L, const int* widths, int task, int act, MlpDesc* g) {
+static int make_desc(int L, const int* widths, int task, int act, MlpDesc* g, int pad = 32) {
   if (L < 1 || L > kMaxLayers || (act & 0xff) > kIdentity || (act & ~0x1ff)) return -1;
   *g = MlpDesc{};
   g->L = L;
@@ -516,7 +828,7 @@ static int make_desc(int L, const int* widths, int task, int act, MlpDesc* g) {
   for (int l = 0; l <= L; ++l) {
     if (widths[l] < 1) return -1;
     g->n[l] = widths[l];
-    g->np[l] = (widths[l] + 31) & ~31;
+    g->np[l] = (widths[l] + pad - 1) / pad * pad;
   }
   for (int l = 0; l < L; ++l) {  // flat parameter layout: W_l [n_{l+1} × n_l], b_l
     g->woff[l] = off;
@@ -549,6 +861,18 @@ static int make_desc(int L, const int* widths, int task, int act, MlpDesc* g) {
   p += kMB * g->ldg;
   g->ly = p;
   p += kMB;
+  if (pad == 16) {  // v2 layout: three gradient buffers (lg0, lg1 + one more), bias grads
+    g->lgb[0] = g->lg0;
+    g->lgb[1] = g->lg1;
+    g->lgb[2] = p;
+    p += kMB * g->ldg;
+    for (int l = 0; l < L; ++l) {
+      g->lbg[l] = p;
+      p = al4(p + g->np[l + 1]);
+    }
+    g->lsc = p;
+    p += 4;
+  }
   g->total = p;
   return 0;
 }
@@ -578,6 +902,17 @@ __global__ __launch_bounds__(256) void mlp_colsum_kernel(const float* __restrict
 
 using namespace omldm;
 
+// Round kernel form: 0 v1 (mlp_round_kernel), 1 v2 with 4 waves, 2 v2 with 8 waves (v2 takes
+// output widths ≤ 16). `set` ≥ 0 sets it; the default comes from OMLDM_MLP_FORM (0).
+OMLDM_API int omldm_mlp_form(int set) {
+  static int form = [] {
+    const char* e = getenv("OMLDM_MLP_FORM");
+    return e ? atoi(e) : 0;
+  }();
+  if (set >= 0) form = set;
+  return form;
+}
+
 // LDS bytes the fused kernels need for this layer stack (host-side feasibility check).
 OMLDM_API long long omldm_mlp_lds_bytes(int L, const int* widths) {
   MlpDesc g;
@@ -597,14 +932,32 @@ OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, lo
   if (B <= 0 || S <= 0) return 0;
   if (R <= 0 || (long long)R * S < B) return -3;
   MlpDesc g;
-  if (make_desc(L, widths, task, act, &g)) return -1;
-  const size_t lds = (size_t)g.total * 4;
-  if (lds > 160 * 1024) return -2;
-  int e = check_dyn_lds((const void*)mlp_round_kernel, lds);
-  if (e) return e;
+  const int form = omldm_mlp_form(-1);
+  if (form > 0 && widths[L] <= 16 && make_desc(L, widths, task, act, &g, 16) == 0 &&
+      (size_t)g.total * 4 <= 160 * 1024) {
+    const size_t lds = (size_t)g.total * 4;
+    const int nparams = g.boff[g.L - 1] + g.n[g.L];
+    int e;
+    if (form == 2) {
+      if ((e = check_dyn_lds((const void*)mlp_round2_kernel<8>, lds))) return e;
+      hipLaunchKernelGGL(mlp_round2_kernel<8>, dim3(S), dim3(512), lds, (hipStream_t)stream, w, x,
+                         y, B, R, lr, dacc, stats, nact, g, ws, nparams);
+    } else {
+      if ((e = check_dyn_lds((const void*)mlp_round2_kernel<4>, lds))) return e;
+      hipLaunchKernelGGL(mlp_round2_kernel<4>, dim3(S), dim3(256), lds, (hipStream_t)stream, w, x,
+                         y, B, R, lr, dacc, stats, nact, g, ws, nparams);
+    }
+  } else {
+    if (make_desc(L, widths, task, act, &g)) return -1;
+    const size_t lds = (size_t)g.total * 4;
+    if (lds > 160 * 1024) return -2;
+    int e = check_dyn_lds((const void*)mlp_round_kernel, lds);
+    if (e) return e;
+    const int nparams = g.boff[g.L - 1] + g.n[g.L];
+    hipLaunchKernelGGL(mlp_round_kernel, dim3(S), dim3(256), lds, (hipStream_t)stream, w, x, y, B,
+                       R, lr, dacc, stats, nact, g, ws, nparams);
+  }
   const int nparams = g.boff[g.L - 1] + g.n[g.L];
-  hipLaunchKernelGGL(mlp_round_kernel, dim3(S), dim3(256), lds, (hipStream_t)stream, w, x, y, B,
-                     R, lr, dacc, stats, nact, g, ws, nparams);
   if (ws)
     hipLaunchKernelGGL(mlp_colsum_kernel, dim3((nparams + 255) / 256, (S + kMlpSlab - 1) / kMlpSlab),
                        dim3(256), 0, (hipStream_t)stream, ws, S, nparams, dacc);

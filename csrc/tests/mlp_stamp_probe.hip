@@ -25,6 +25,7 @@
 int main(int argc, char** argv) {
   const int S = argc > 1 ? atoi(argv[1]) : 512;
   const int bf16 = argc > 2 ? atoi(argv[2]) : 1;
+  if (argc > 3) omldm_mlp_form(atoi(argv[3]));  // 0 v1 (phase stamps), 1 / 2 v2 (4 / 8 waves)
   const long long B = 131072;
   const int R = (int)(B / S);
   const int widths[4] = {13, 64, 64, 1};

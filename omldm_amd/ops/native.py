@@ -132,6 +132,8 @@ HIP_SIGS = [
     ("omldm_holdout_route", i32, [vp, vp, vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, i64, i64,
                                   i64, i64, i64, i64, i64, i64, i32, i32, i32, i32, vp]),
     ("omldm_kmeans_seq_fits", i32, [i32, i32]),
+    ("omldm_scan3mc_debug", i32, [vp]),
+    ("omldm_mlp_form", i32, [i32]),
     ("omldm_kmeans_seq_form", i32, [i32]),
     ("omldm_kmeans_seq", i32, [vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     ("omldm_ipc_alloc", vp, [i64]),
@@ -144,6 +146,11 @@ HIP_SIGS = [
     ("omldm_p2p_delta", i32, [vp, vp, vp, vp, i64, vp]),
     ("omldm_p2p_axpy", i32, [vp, vp, f32, i64, vp]),
     ("omldm_p2p_install", i32, [vp, vp, vp, vp, i64, vp]),
+    ("omldm_sig_create", vp, [vp, vp, vp, vp, vp, vp, i64, i32, i32, i32, i32]),
+    ("omldm_sig_destroy", None, [vp]),
+    ("omldm_sig_state_words", i32, [i32]),
+    ("omldm_sig_hub", i32, [vp, vp, i64, f32, vp]),
+    ("omldm_sig_worker", i32, [vp, i32, vp, vp, vp, i64, i64, vp]),
     ("omldm_holdout_route_spokes", i32, [vp, vp, vp, i64, vp, vp, vp, i32, i32, vp, vp, vp, i64,
                                          vp, vp, i32, i32, i32, i32, vp]),
     ("omldm_json_parse", i32, [vp, vp, i32, i32, i32, i32, i64, i32, vp, vp, vp, vp, vp, vp]),

@@ -329,14 +329,20 @@ class _PointToPoint(Protocol):
             return  # one worker: its local model IS the global model
         x = L.state_vector()
         installs = self._ps.installs
-        if self._ps.step(x):
-            nbytes = x.numel() * x.element_size()
-            self.stats.syncs += 1
-            self.stats.models_shipped += 2  # one push, one reply (unicast)
-            self.stats.bytes_shipped += 2 * nbytes
-            self.stats.num_of_blocks += 2 * max(1, math.ceil(x.numel() / self.max_msg_params))
-        if self._ps.installs != installs:
+        pushed = self._ps.step(x)
+        if pushed:
+            self._count_pushes(1, x)
+        # the signal plane decides installs on the device (pushed is None): derived state
+        # is refreshed every round
+        if pushed is None or self._ps.installs != installs:
             L.on_state_loaded()
+
+    def _count_pushes(self, k: int, x) -> None:
+        nbytes = x.numel() * x.element_size()
+        self.stats.syncs += k
+        self.stats.models_shipped += 2 * k  # one push, one reply (unicast)
+        self.stats.bytes_shipped += 2 * k * nbytes
+        self.stats.num_of_blocks += 2 * k * max(1, math.ceil(x.numel() / self.max_msg_params))
 
     @property
     def max_lead(self) -> int:
@@ -344,7 +350,9 @@ class _PointToPoint(Protocol):
 
     def finalize(self):
         if self._ps is not None and self.comm.world > 1:
-            self._ps.finalize(self.learner.state_vector())
+            x = self.learner.state_vector()
+            self._ps.finalize(x)
+            self._count_pushes(self._ps.take_unreported_pushes(), x)
             self.learner.on_state_loaded()
 
     def state_dict(self):

@@ -46,11 +46,14 @@ WORKER = textwrap.dedent(r"""
     t0 = time.time()
     k = 0
     fixed = proto_name == "Synchronous"  # collectives: every rank runs the same rounds
+    import threading
+    threads = 0
     while (k < 20) if fixed else (time.time() - t0 < seconds):
         proto.round(pool[k % len(pool)])
         if rank == slow:
             time.sleep(0.05)
         k += 1
+        threads = max(threads, threading.active_count())
     proto.finalize()
     elapsed = time.time() - t0
     test = synth_raw(space, 4000, start=10**9, seed=25).hashed(space).to(dev)
@@ -64,7 +67,9 @@ WORKER = textwrap.dedent(r"""
            "merges": ps.merges if ps is not None else [],
            "reply_after": {str(k): v for k, v in ps.reply_after.items()} if ps is not None else {},
            "scale": ps.scale if ps is not None else None,
-           "collectives": comm.stats.collectives}
+           "collectives": comm.stats.collectives,
+           "push_msg_bytes": comm.stats.per_tag.get("async-push", 0),
+           "threads": threads, "syncs": proto.stats.syncs}
     with open(os.path.join(sys.argv[5], f"rank{rank}.json"), "w") as f:
         json.dump(out, f)
     dist.barrier()
@@ -80,12 +85,14 @@ def _port():
     return p
 
 
-def _run(proto, seconds=2.5, slow=1, world=3, dev="cpu"):
+def _run(proto, seconds=2.5, slow=1, world=3, dev="cpu", plane=None):
     outdir = tempfile.mkdtemp(prefix="omldm_async_")
     script = os.path.join(outdir, "worker.py")
     with open(script, "w") as f:
         f.write(WORKER)
     env = dict(os.environ, OMP_NUM_THREADS="1", OMLDM_CPU_THREADS="1")
+    if plane is not None:
+        env["OMLDM_P2P_PLANE"] = plane
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                           f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
                           "--master-port", str(_port()), script, ROOT, proto, str(seconds),
@@ -199,12 +206,20 @@ def test_synchronous_is_paced_by_the_straggler_for_contrast():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("plane", ["signal", "device"])
 @pytest.mark.parametrize("proto", ["Asynchronous", "SSP"])
-def test_device_plane_on_gpu(proto):
+def test_device_plane_on_gpu(proto, plane):
     """Three ranks on cuda:0: pushes and replies move through the IPC mailboxes (no
-    model-sized host copy per round); same protocol guarantees as on the host plane."""
-    r = _run(proto, seconds=2.0, dev="cuda")
-    assert all(x["plane"] == "device" for x in r.values()), r
+    model-sized host copy per round); same protocol guarantees as on the host plane.
+    ``signal`` (the default): the push / reply control words travel in HBM too — no gloo
+    header and no host thread per push; ``device``: headers on gloo."""
+    r = _run(proto, seconds=2.0, dev="cuda", plane=plane)
+    assert all(x["plane"] == plane for x in r.values()), r
+    if plane == "signal":
+        assert all(x["push_msg_bytes"] == 0 for x in r.values()), r
+        # no channel-service or request threads: the main thread (+ the runtime's own)
+        assert max(x["threads"] for x in r.values()) <= 3, [x["threads"] for x in r.values()]
+        assert all(x["syncs"] > 0 for x in r.values()), r
     assert r[0]["w0"] == r[1]["w0"] == r[2]["w0"]
     slow = r[1]["rounds"]
     if proto == "SSP":
