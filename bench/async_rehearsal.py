@@ -34,7 +34,7 @@ WORKER = textwrap.dedent(r"""
     import torch
     import torch.distributed as dist
     from omldm_amd.api.batch import FeatureSpace
-    from omldm_amd.io.synthetic import synth_raw
+    from omldm_amd.io.synthetic import synth_batch
     from omldm_amd.models.linear import SVM
     from omldm_amd.ops import linear as L
     from omldm_amd.parallel.comm import Comm
@@ -50,11 +50,12 @@ WORKER = textwrap.dedent(r"""
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
-    space = FeatureSpace(13, 0, 26, 1 << log2)
+    # the bench geometry: the engine's field-aware wire (the rounds take the v3 table scan)
+    space = FeatureSpace(13, 0, 26, 1 << log2, field_aware=True)
     lrn = SVM({"variant": "PA-I"}, space, dev)
     proto = make_protocol(proto_name, comm, lrn, {"virtualSpokes": spokes, "staleness": 2,
                                                   "_tag": 5})
-    pool = [synth_raw(space, batch, start=(k * world + rank) * batch, seed=31).hashed(space).to(dev)
+    pool = [synth_batch(space, batch, start=(k * world + rank) * batch, seed=31).to(dev)
             for k in range(8)]
     for k in range(3):  # warm-up (kernels, mailboxes)
         proto.round(pool[k])
@@ -75,7 +76,12 @@ WORKER = textwrap.dedent(r"""
 
     if ps is not None:
         ps.step = timed
-    syncs0 = proto.stats.syncs
+    def pushes_now():  # pushes sent so far (the signal plane counts them on the device)
+        if ps is not None and ps.plane == "signal":
+            return int(ps._sig.st[ps._sig.W_PUSHES].item())
+        return proto.stats.syncs
+
+    syncs0 = pushes_now()
     t0 = time.perf_counter()
     k = 0
     while time.perf_counter() - t0 < seconds:
@@ -88,6 +94,7 @@ WORKER = textwrap.dedent(r"""
     if dev.type == "cuda":
         torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    pushes = pushes_now() - syncs0
     # Python calls made by the exchange per round (every thread): 50 more rounds profiled
     import threading
     calls = [0]
@@ -109,10 +116,10 @@ WORKER = textwrap.dedent(r"""
     if dev.type == "cuda":
         torch.cuda.synchronize()
     proto.finalize()
-    test = synth_raw(space, 20000, start=10**9, seed=31).hashed(space).to(dev)
+    test = synth_batch(space, 20000, start=10**9, seed=31).to(dev)
     acc = float(((L.linear_predict(lrn.w, test) >= 0).float() * 2 - 1 == test.y).float().mean())
     out = {"rank": rank, "rounds": k, "elapsed_s": el, "rounds_per_s": k / el,
-           "pushes": proto.stats.syncs - syncs0, "exchange_host_us_per_round": 1e6 * t_ex / max(1, k),
+           "pushes": pushes, "exchange_host_us_per_round": 1e6 * t_ex / max(1, k),
            "plane": ps.plane if ps is not None else "collective", "acc": acc,
            "python_calls_per_exchange": calls[0] / n_prof if n_prof else None}
     with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:

@@ -69,6 +69,32 @@ P16_CASES = [
 ]
 
 
+def _quality(base, task, hyper, space, ring, spokes, dev, rounds):
+    """Holdout quality of the GPU learner against the same learner on the CPU (the
+    reference-semantics host path), both trained on the same ``rounds`` rounds of the
+    bench's stream at the bench's spokes: the learner's own evaluate() — loss per point
+    and score per point (accuracy for classifiers, the learner's score otherwise)."""
+    hold = synth_batch(space, 16384, start=10 ** 8, seed=26, task=task, n_classes=4)
+    if base == "NN":
+        hold = HashedBatch(hold.num, hold.cat, torch.where(hold.y > 0, 1.0, -1.0))
+    ctx = RoundContext(spokes=spokes)
+    out = {}
+    for where in (dev, torch.device("cpu")):
+        L = make_learner(base, hyper, space, where)
+        t = time.perf_counter()
+        for k in range(rounds):
+            b = ring[k % 3]
+            b.prep, b._padded = None, None
+            L.fit(b if where == dev else b.to("cpu"), ctx)
+        loss, score, n = L.evaluate(hold.to(where))
+        n = max(1, int(n))
+        out[where.type] = {"loss": round(float(loss) / n, 6), "score": round(float(score) / n, 6),
+                           "fit_s": round(time.perf_counter() - t, 3)}
+    out["score_gap"] = round(out[dev.type]["score"] - out["cpu"]["score"], 6)
+    out["rounds"] = rounds
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=131072)
@@ -76,6 +102,8 @@ def main(argv=None) -> int:
     ap.add_argument("--only", default="")
     ap.add_argument("--preset", default="", choices=["", "p16"],
                     help="p16: every learner at 16 spokes (the reference's parallelism)")
+    ap.add_argument("--quality-rounds", type=int, default=2,
+                    help="rounds of the GPU-vs-CPU holdout quality check per learner (0: off)")
     ap.add_argument("--cases", default="",
                     help='JSON list of [name, task, hyper, spokes] replacing the default cases '
                          '(geometry sweeps)')
@@ -134,6 +162,13 @@ def main(argv=None) -> int:
         tot = L.running_totals() if hasattr(L, "running_totals") else {}
         if "overflow" in tot:
             res[name]["overflow"] = tot["overflow"]
+        if a.quality_rounds > 0 and dev.type == "cuda":
+            try:
+                res[name]["quality"] = _quality(name.split("@")[0], task, hyper, space, ring,
+                                                spokes, dev, a.quality_rounds)
+            except (RuntimeError, NotImplementedError, ValueError) as e:
+                res[name]["quality"] = {"error": str(e)[:200]}
+            print(name, res[name], file=sys.stderr, flush=True)
     print(json.dumps({"metric": "per-learner training examples/s (1 GPU, 1 pipeline)",
                       "batch": a.batch, "steps": a.steps, "device": str(dev),
                       "learners": res}), flush=True)

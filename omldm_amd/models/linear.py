@@ -15,15 +15,17 @@ published Passive-Aggressive family (Crammer et al. 2006) — SURVEY.md Appendix
 * ``RegressorPA`` ε-insensitive loss, same τ family, update sign(y − w·x)·τ·x.
 * ``LogisticRegression`` (extension, BASELINE.json config 2): SGD on the log loss.
 
-A round is S virtual spokes, each an exact sequential learner on its R-row shard:
-* the PA family, RegressorPA and logistic SGD (no L2 shrink, fp32 model) run the v3 table
-  scan (csrc/kernels/linear_scan3.hip: chunk Grams on the matrix cores, one scan workgroup
-  per spoke with its updates in an LDS slot table), on the raw wire and on the engine's
-  field-aware hashed batches; raw batches of a shape v3 does not take use v1
-  (csrc/kernels/linear_seq.hip, logged);
-* everything else — SVM's L2 shrink, Pegasos, bf16 models, hashed batches v3 does not
-  take — runs the spoke-table round (csrc/kernels/linear_spoke.hip: per-spoke LDS delta
-  tables spilling to HBM, spoke_table.h).
+A round is S virtual spokes, each an exact sequential learner on its R-row shard. On a GPU
+every rule — the PA family, RegressorPA, logistic SGD, SVM's L2 shrink, Pegasos, bf16
+models — runs the v3 table scan (csrc/kernels/linear_scan3.hip: chunk Grams on the matrix
+cores, one scan workgroup per spoke with its updates in an LDS slot table; the shrinking
+rules carry the spoke's model scale σ through the chain) on the raw wire and on the
+engine's field-aware hashed batches (bench/learners.py --preset p16: 228–277 M ex/s at
+16 spokes, profiles/round6/learners_p16.json). What v3 does not take falls back, logged:
+raw batches of an unsupported shape without a shrink to v1 (csrc/kernels/linear_seq.hip);
+non-field-aware hashed batches, more than 32 categorical fields or R > 8192 rows per
+spoke to the spoke-table round (csrc/kernels/linear_spoke.hip: per-spoke LDS delta tables
+spilling to HBM, spoke_table.h, ≈1.2 M ex/s).
 """
 from __future__ import annotations
 
