@@ -1720,19 +1720,25 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
 // margins from the slot table (K floats per table slot: w0 at the first occurrence, the
 // spoke's updates added by the scatter) or the key-major prototypes, and stage the Grams.
 // Each row's (τ, r) goes to a record; s3mc_scatter_kernel adds the spokes' updates after.
+// K ∈ {2, 4, 8, 16} (nclass ≤ K; the classes past nclass cost uniform branches only): the
+// helpers add their base-margin partials into one K × 64 array with LDS float atomics
+// (the scanner reads K values per lane per chunk and clears them), so the LDS the scan
+// needs grows by K·512 bytes, not by K·NHA·512.
 namespace s3 {
-constexpr int MCK = 4;  // classes on the v3 multiclass scan (K ≤ 4; more: the spoke tables)
+constexpr int MCK = 16;  // classes on the v3 multiclass scan (more: the spoke tables)
 }
 
 template <int K>
 struct S3McSmem {
   alignas(16) float G[2][s3::CH][s3::GS];
   alignas(16) float X1[2][s3::CH][s3::GS];
-  float part[2][s3::NHA][K][s3::CH];  // base-margin partials per helper and class
-  float tau[2][s3::CH];               // τ of the chunk's rows, by parity
-  int rr[2][s3::CH];                  // r (the updated wrong class) of the chunk's rows
+  float part[2][K][s3::CH];  // base margins by class (the helpers' partials, LDS atomics)
+  float tau[2][s3::CH];      // τ of the chunk's rows, by parity
+  int rr[2][s3::CH];         // r (the updated wrong class) of the chunk's rows
 };
 
+// Branch-free (selects only): on the scanner's chain, a data-dependent branch per class
+// (exec-mask save / restore and a scalar branch) cost ~700 cycles per step at K = 4.
 template <int K>
 __device__ __forceinline__ void s3mc_decide(const float (&u)[K], int yi, int nclass, float a,
                                             float cmax, bool valid, float& tau, int& r,
@@ -1741,17 +1747,49 @@ __device__ __forceinline__ void s3mc_decide(const float (&u)[K], int yi, int ncl
   r = -1;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    if (k < nclass) {
-      if (k == yi) sy = u[k];
-      else if (u[k] > best) {
-        best = u[k];
-        r = k;
-      }
-    }
+    const float v = u[k];
+    const bool isy = k == yi;
+    sy = isy ? v : sy;
+    const bool gt = k < nclass && !isy && v > best;  // ties: the lowest index
+    best = gt ? v : best;
+    r = gt ? k : r;
   }
   margin = sy - best;
   const float loss = fmaxf(0.f, 1.f - margin);
   tau = (valid && r >= 0 && a > 0.f) ? fminf(cmax, loss * a) : 0.f;
+}
+
+// The scanner's form: w[c] = the row's score of class c with −inf at its own class (and
+// past nclass), sy = its own class's score — both kept up to date by the steps, so the
+// best wrong class is a max tree of depth log2 K (ties: the lowest index, as the scan in
+// class order) instead of a K-long compare chain on the step's critical path.
+template <int K>
+__device__ __forceinline__ void s3mc_decide_w(const float (&w)[K], float sy, float a, float cmax,
+                                              bool valid, float& tau, int& r, float& margin) {
+  float v[K];
+  int ix[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) v[c] = w[c], ix[c] = c;
+#pragma unroll
+  for (int st = 1; st < K; st <<= 1) {
+#pragma unroll
+    for (int i = 0; i + st < K; i += 2 * st) {
+      const bool gt = v[i + st] > v[i];
+      v[i] = gt ? v[i + st] : v[i];
+      ix[i] = gt ? ix[i + st] : ix[i];
+    }
+  }
+  r = v[0] == -INFINITY ? -1 : ix[0];
+  margin = sy - v[0];
+  const float loss = fmaxf(0.f, 1.f - margin);
+  tau = (valid && r >= 0 && a > 0.f) ? fminf(cmax, loss * a) : 0.f;
+}
+
+// The coefficient of class c in a step that moves class yt by +τ and class rt by −τ:
+// uniform operands, selected on the scalar unit (the sign through the bit pattern).
+__device__ __forceinline__ float s3mc_coef(int c, int yt, int rt, uint32_t ctb) {
+  const uint32_t v = c == yt ? ctb : (c == rt ? (ctb ^ 0x80000000u) : 0u);
+  return __uint_as_float(v);
 }
 
 struct S3McArgs {
@@ -1787,6 +1825,8 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   const float* P0 = prep + (size_t)s * nchs * PF;
   auto chunk_prep = [&](int k) { return P0 + (size_t)k * PF; };
   float* ag = A.aglob + (size_t)s * gstride * K;
+  for (int i = tid; i < 2 * K * s3::CH; i += s3::NT) (&sm.part[0][0][0])[i] = 0.f;
+  __syncthreads();
 
   if (wave == 0) {
     // ---------------------------------------------------------------- scanner
@@ -1811,14 +1851,19 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
           ynx = chunk_prep(k + 1)[s3_prep_y<KN>() + lane];
           anx = chunk_prep(k + 1)[2 * s3::MAT + lane];
         }
-        float u[K], n1[K];
+        // K ≤ 4: w[c] = the row's score of class c with −inf at its own class (and past
+        // nclass), sy = its own class's score, both kept up to date by the steps, and the
+        // best wrong class a max tree (s3mc_decide_w); K ≥ 8: the plain scores u = w and
+        // the branch-free class scan (s3mc_decide) — measured per K (profiles/round6/mc/)
+        constexpr bool TREE = K <= 4;
+        float w[K], n1[K], sy = 0.f;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
-          float m0 = 0.f;
-#pragma unroll
-          for (int q = 0; q < s3::NHA; ++q) m0 += sm.part[b][q][c][lane];
-          u[c] = m0 + f1[c];
+          const float v = sm.part[b][c][lane] + f1[c];
+          sm.part[b][c][lane] = 0.f;  // the helpers add chunk k + 2's partials here
           n1[c] = 0.f;
+          sy = c == yi ? v : sy;
+          w[c] = TREE && (c == yi || c >= A.nclass) ? -INFINITY : v;
         }
         // the lane's row of G_k in VGPRs; the chunk's steps are kept (τ_t, r_t, y_t) and
         // folded into chunk k+1 through X1 after the chain (off it, from LDS)
@@ -1829,37 +1874,33 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
           const float4 g4 = *reinterpret_cast<const float4*>(grow + t4);
           gg[t4] = g4.x, gg[t4 + 1] = g4.y, gg[t4 + 2] = g4.z, gg[t4 + 3] = g4.w;
         }
+        float tl, mg;
+        int rl;
 #pragma unroll
         for (int t = 0; t < s3::CH; ++t) {
-          float tl, mg;
-          int rl;
-          s3mc_decide<K>(u, yi, A.nclass, a, A.cmax, valid, tl, rl, mg);
-          const float ct = readlane_f(tl, t);
+          if constexpr (TREE) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
+          else s3mc_decide<K>(w, yi, A.nclass, a, A.cmax, valid, tl, rl, mg);
+          const uint32_t ctb = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(tl), t);
           const int rt = __builtin_amdgcn_readlane(rl, t);
           const int yt = __builtin_amdgcn_readlane(yi, t);
 #pragma unroll
-          for (int c = 0; c < K; ++c) {
-            const float cf = (c == yt ? ct : 0.f) - (c == rt ? ct : 0.f);
-            u[c] = fmaf(cf, gg[t], u[c]);   // G strictly lower: lane t frozen after step t
-          }
+          for (int c = 0; c < K; ++c)  // G strictly lower: lane t frozen after step t
+            w[c] = fmaf(s3mc_coef(c, yt, rt, ctb), gg[t], w[c]);  // −inf stays −inf
+          if constexpr (TREE) sy = fmaf(s3mc_coef(yi, yt, rt, ctb), gg[t], sy);
         }
-        float tl, mg;
-        int rl;
-        s3mc_decide<K>(u, yi, A.nclass, a, A.cmax, valid, tl, rl, mg);
+        if constexpr (TREE) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
+        else s3mc_decide<K>(w, yi, A.nclass, a, A.cmax, valid, tl, rl, mg);
         // chunk k+1's X1 fold: n1[c] = Σ_t c_t^c · X1_{k+1}[lane][t]
         {
           const float* xrow = &sm.X1[b ^ 1][lane][0];
 #pragma unroll 8
           for (int t = 0; t < s3::CH; ++t) {
-            const float ct = readlane_f(tl, t);
+            const uint32_t ctb = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(tl), t);
             const int rt = __builtin_amdgcn_readlane(rl, t);
             const int yt = __builtin_amdgcn_readlane(yi, t);
             const float x = xrow[t];
 #pragma unroll
-            for (int c = 0; c < K; ++c) {
-              const float cf = (c == yt ? ct : 0.f) - (c == rt ? ct : 0.f);
-              n1[c] = fmaf(cf, x, n1[c]);
-            }
+            for (int c = 0; c < K; ++c) n1[c] = fmaf(s3mc_coef(c, yt, rt, ctb), x, n1[c]);
           }
         }
         sm.tau[b][lane] = tl;
@@ -1906,18 +1947,18 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   const int kd = dn + (bias ? 1 : 0);
   const int hl = q * 64 + lane;
   const int capid = cap / K;  // table slots in LDS; the rest in ag (global)
-  float wn[K][s3::NJ], w0[K][s3::NJ];
-#pragma unroll
-  for (int i = 0; i < s3::NJ; ++i) {
+  constexpr int NJK0 = (KN + s3::NHA - 1) / s3::NHA;  // this wave's dense columns
+  float wn[K][NJK0];  // the round-start values are re-read at the round end
+  auto w0_at = [&](int i, int c) {
     const int j = q + s3::NHA * i;
     const int key = j < dn ? j : dim - 1;
     const bool real = j < KN && (j < dn || (bias && j == dn));
+    return real ? A.Wt[(size_t)key * A.kp + c] : 0.f;
+  };
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-      w0[c][i] = real ? A.Wt[(size_t)key * A.kp + c] : 0.f;
-      wn[c][i] = w0[c][i];
-    }
-  }
+  for (int i = 0; i < NJK0; ++i)
+#pragma unroll
+    for (int c = 0; c < K; ++c) wn[c][i] = w0_at(i, c);
   constexpr int NV4 = (2 * s3::MAT / 4 + 64 * s3::NHA - 1) / (64 * s3::NHA);
   constexpr int NJK = (KN + s3::NHA - 1) / s3::NHA;
   struct Set {
@@ -1946,9 +1987,12 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     for (int i = 0; i < s3::NF; ++i) {
       const bool glob = S.cs[i] != -1 && !(S.cm[i] & s3::F_TG);
       const float* src = A.Wt + (size_t)(glob ? (S.cs[i] & 0x7fffffff) : 0) * A.kp;
-      if constexpr (K == 4) {
-        const float4 v = *reinterpret_cast<const float4*>(src);
-        S.g[i][0] = v.x, S.g[i][1] = v.y, S.g[i][2] = v.z, S.g[i][3] = v.w;
+      if constexpr (K >= 4) {
+#pragma unroll
+        for (int c4 = 0; c4 < K; c4 += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + c4);
+          S.g[i][c4] = v.x, S.g[i][c4 + 1] = v.y, S.g[i][c4 + 2] = v.z, S.g[i][c4 + 3] = v.w;
+        }
       } else {
         const float2 v = *reinterpret_cast<const float2*>(src);
         S.g[i][0] = v.x, S.g[i][1] = v.y;
@@ -1982,12 +2026,33 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   };
   unsigned long long* const hdbg = g_s3mc_dbg;
   unsigned long long h_sc = 0, h_mg = 0, h_st = 0, h_wt = 0;
+  // K ≥ 8 (LEAN): the gathers and the Gram staging of a chunk are issued and consumed in
+  // the same body (their latency under the scatter work) instead of a body ahead: the
+  // K-wide gathers and the staged tiles are not live across the barrier (VGPR budget)
+  constexpr bool LEAN = K >= 8;
+  auto store_staging = [&](int cn, const Set& S) {
+#pragma unroll
+    for (int u = 0; u < NV4; ++u) {
+      const int i = hl + 64 * s3::NHA * u;
+      const int mtx = i >> 10, e = i & 1023;
+      if (i < 2 * s3::MAT / 4 && cn + mtx < nch) {
+        const int row = e >> 4, col = (e & 15) * 4;
+        float* dst = mtx == 0 ? &sm.G[cn & 1][row][col] : &sm.X1[(cn + 1) & 1][row][col];
+        *reinterpret_cast<f32x4*>(dst) = S.v[u];
+      }
+    }
+  };
   auto body = [&](auto spill_tag, int k, Set& CUR, Set& NXT) {
     constexpr bool SPILL = decltype(spill_tag)::value;
     const int cn = k + 1, ks = k - 1;
     const unsigned long long ha = hdbg ? __builtin_amdgcn_s_memtime() : 0;
     load_words(cn + 1, NXT);
-    issue_staging(cn + 1, NXT);
+    if constexpr (LEAN) {
+      issue_staging(cn, CUR);
+      if constexpr (K < 16) issue_gathers(CUR);  // K = 16: loaded in the margin loop
+    } else {
+      issue_staging(cn + 1, NXT);
+    }
     load_dense(ks + 1, NXT.xs);
     load_dense(cn + 1, NXT.xc);
     // ---- scatter chunk ks: +τ·sign into class y, −τ·sign into class r
@@ -2015,12 +2080,15 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         if (j < kd) {
 #pragma unroll
           for (int c = 0; c < K; ++c) {
-            const float cf = (c == yc ? tv : 0.f) - (c == rc ? tv : 0.f);
-            wn[c][i] += wave_sum(cf * CUR.xs[i]);
+            if (K <= 4 || c < A.nclass) {
+              const float cf = c == yc ? tv : (c == rc ? -tv : 0.f);
+              wn[c][i] += wave_sum(cf * CUR.xs[i]);
+            }
           }
         }
       }
     }
+    if constexpr (LEAN) store_staging(cn, CUR);  // the staged tiles die before the gathers' use
     const unsigned long long hb = hdbg ? __builtin_amdgcn_s_memtime() : 0;
     // ---- base margins of chunk cn
     if (cn < nch) {
@@ -2038,8 +2106,19 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         const bool tg = here && (m & s3::F_TG), init = here && !tg && (m & s3::F_INIT);
         const int lid = (int)(m >> s3::LID_SHIFT);
         float val[K];
+        if constexpr (K >= 16) {  // no prefetch at the widest template (VGPR budget): the
+          // helpers wait less than the scanner's chunk period there
+          const bool glob = here && !(m & s3::F_TG);
+          const float* src = A.Wt + (size_t)(glob ? (CUR.cs[i] & 0x7fffffff) : 0) * A.kp;
 #pragma unroll
-        for (int c = 0; c < K; ++c) val[c] = CUR.g[i][c];
+          for (int c4 = 0; c4 < K; c4 += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(src + c4);
+            val[c4] = v.x, val[c4 + 1] = v.y, val[c4 + 2] = v.z, val[c4 + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < K; ++c) val[c] = CUR.g[i][c];
+        }
         if (!SPILL || __builtin_amdgcn_ballot_w64((tg || init) && lid >= capid) == 0ull) {
           if (tg) {
 #pragma unroll
@@ -2073,21 +2152,13 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         }
       }
 #pragma unroll
-      for (int c = 0; c < K; ++c) sm.part[cn & 1][q][c][r] = base[c];
+      for (int c = 0; c < K; ++c)
+        if (K <= 4 || c < A.nclass) atomicAdd(&sm.part[cn & 1][c][r], base[c]);
     }
     const unsigned long long hc = hdbg ? __builtin_amdgcn_s_memtime() : 0;
-    // ---- aG_{cn} → G[cn & 1], aX1_{cn+1} → X1[(cn+1) & 1]
-#pragma unroll
-    for (int u = 0; u < NV4; ++u) {
-      const int i = hl + 64 * s3::NHA * u;
-      const int mtx = i >> 10, e = i & 1023;
-      if (i < 2 * s3::MAT / 4 && cn + mtx < nch) {
-        const int row = e >> 4, col = (e & 15) * 4;
-        float* dst = mtx == 0 ? &sm.G[cn & 1][row][col] : &sm.X1[(cn + 1) & 1][row][col];
-        *reinterpret_cast<f32x4*>(dst) = CUR.v[u];
-      }
-    }
-    issue_gathers(NXT);
+    // ---- aG_{cn} → G[cn & 1], aX1_{cn+1} → X1[(cn+1) & 1] (LEAN: before the margins)
+    if constexpr (!LEAN) store_staging(cn, CUR);
+    if constexpr (!LEAN) issue_gathers(NXT);
 #pragma unroll
     for (int i = 0; i < s3::NF; ++i) {
       p2[i] = p1[i];
@@ -2108,10 +2179,10 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
   for (int i = 0; i < s3::NF; ++i) p1[i] = p2[i] = 0u;
   load_words(0, Sa);
-  issue_staging(0, Sa);
+  if constexpr (!LEAN) issue_staging(0, Sa);
   load_dense(-2, Sa.xs);
   load_dense(0, Sa.xc);
-  issue_gathers(Sa);
+  if constexpr (!LEAN) issue_gathers(Sa);
   if (lidcount[s] <= capid) {
     for (int k = -1; k <= nch; k += 2) {
       body(S3Tag<false>{}, k, Sa, Sb);
@@ -2130,7 +2201,8 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
     if (lane == 0 && j < s3::DS)
 #pragma unroll
       for (int c = 0; c < K; ++c)
-        A.wsd[((size_t)s * K + c) * s3::DS + j] = j < KN ? wn[c][i] - w0[c][i] : 0.f;
+        A.wsd[((size_t)s * K + c) * s3::DS + j] =
+            (i < NJK0 && j < KN) ? wn[c][i < NJK0 ? i : 0] - w0_at(i, c) : 0.f;
   }
   if (hdbg && lane == 0) {  // helper phases summed over the helper waves
     atomicAdd(&hdbg[s * 8 + 3], h_sc);
@@ -2708,9 +2780,17 @@ OMLDM_API int omldm_scan3_stamps(void* buf) {
 
 // ------------------------------------------------------------------ MultiClassPA host API
 // The LDS slot table of the multiclass scan (floats) and its global spill (floats per spoke).
+template <int K>
+static int s3mc_cap() {
+  return (int)((160 * 1024 - sizeof(S3McSmem<K>)) / sizeof(float)) / K * K;
+}
 OMLDM_API int omldm_scan3mc_lds_cap(int K) {
-  if (K == 2) return (int)((160 * 1024 - sizeof(S3McSmem<2>)) / sizeof(float)) / 2 * 2;
-  return (int)((160 * 1024 - sizeof(S3McSmem<4>)) / sizeof(float)) / 4 * 4;
+  switch (K) {
+    case 2: return s3mc_cap<2>();
+    case 4: return s3mc_cap<4>();
+    case 8: return s3mc_cap<8>();
+    default: return s3mc_cap<16>();
+  }
 }
 OMLDM_API long long omldm_scan3mc_spill_floats(int R, int dc, int K) {
   return ((long long)R * dc / 2 + 64) * K;
@@ -2744,7 +2824,7 @@ OMLDM_API int omldm_scan3mc_run(const float* Wt, int kp, int K, int nclass, int 
                                 float* ws, float* wsd, float* aglob, float* tau, int* rr,
                                 void* stream) {
   if (S <= 0 || B <= 0) return 0;
-  if ((K != 2 && K != 4) || nclass < 2 || nclass > K || kp < K) return -2;
+  if ((K != 2 && K != 4 && K != 8 && K != 16) || nclass < 2 || nclass > K || kp < K) return -2;
   if (!omldm_scan3_fits(dn, dc, R, bias)) return -3;
   hipStream_t st = (hipStream_t)stream;
   const S3Ws W = s3_ws(ptrs);
@@ -2757,9 +2837,15 @@ OMLDM_API int omldm_scan3mc_run(const float* Wt, int kp, int K, int nclass, int 
   if (K == 2)
     e = k16 ? s3mc_launch<2, 16>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st)
             : s3mc_launch<2, 32>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st);
-  else
+  else if (K == 4)
     e = k16 ? s3mc_launch<4, 16>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st)
             : s3mc_launch<4, 32>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st);
+  else if (K == 8)
+    e = k16 ? s3mc_launch<8, 16>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st)
+            : s3mc_launch<8, 32>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st);
+  else
+    e = k16 ? s3mc_launch<16, 16>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st)
+            : s3mc_launch<16, 32>(W, dc, dn, bias, B, R, S_act, nchs, dim, gstride, A, st);
   if (e) return e;
   const int n_rows = (int)((long long)S_act * R < B ? (long long)S_act * R : B);
   const int nblk = (n_rows + s3::SB - 1) / s3::SB;

@@ -505,36 +505,35 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
 // * operand loads of the next 16-wide k step are issued before the current MFMAs.
 // Same arithmetic as v1 (fp32 MFMA, same mini-batch order); sums may associate
 // differently.
-template <bool AK, bool BK>
-__device__ __forceinline__ f32x4 gemm16p(const float* a, int ars, int acs, const float* b,
-                                         int brs, int bcs, int K, int bf16) {
+// One 16×16 tile, K a multiple of 16: operands read at the top of each 16-wide k step
+// (issued while the previous step's MFMAs are in the pipe), the accumulator chained through
+// the MFMAs in place — no register copies of it between steps (a copy waits for the
+// matrix pipe to drain). fp32 and bf16 are separate instantiations (no branch in the loop).
+template <bool AK, bool BK, bool BF16>
+__device__ __forceinline__ f32x4 gemm16t(const float* a, int ars, int acs, const float* b,
+                                         int brs, int bcs, int K) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   const float* ap = a + r * ars + 4 * g * (AK ? 1 : acs);
   const float* bp = b + 4 * g * (BK ? 1 : brs) + r * bcs;
-  float av[4], bv[4];
-  auto load = [&](int k, float (&x)[4], float (&y)[4]) {
+  for (int k = 0; k < K; k += 16) {
+    float av[4], bv[4];
     if constexpr (AK) {
       const float4 t = *reinterpret_cast<const float4*>(ap + k);
-      x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+      av[0] = t.x; av[1] = t.y; av[2] = t.z; av[3] = t.w;
     } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = ap[(k + u) * acs];
+      for (int u = 0; u < 4; ++u) av[u] = ap[(k + u) * acs];
     }
     if constexpr (BK) {
       const float4 t = *reinterpret_cast<const float4*>(bp + k);
-      y[0] = t.x; y[1] = t.y; y[2] = t.z; y[3] = t.w;
+      bv[0] = t.x; bv[1] = t.y; bv[2] = t.z; bv[3] = t.w;
     } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) y[u] = bp[(k + u) * brs];
+      for (int u = 0; u < 4; ++u) bv[u] = bp[(k + u) * brs];
     }
-  };
-  load(0, av, bv);
-  for (int k = 0; k < K; k += 16) {
-    float an[4], bn[4];
-    if (k + 16 < K) load(k + 16, an, bn);
-    if (bf16) {
+    if constexpr (BF16) {
       const bf16x4 af = {bf16_bits(av[0]), bf16_bits(av[1]), bf16_bits(av[2]), bf16_bits(av[3])};
       const bf16x4 bfv = {bf16_bits(bv[0]), bf16_bits(bv[1]), bf16_bits(bv[2]), bf16_bits(bv[3])};
       acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(af, bfv, acc, 0, 0, 0);
@@ -542,12 +541,14 @@ __device__ __forceinline__ f32x4 gemm16p(const float* a, int ars, int acs, const
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
     }
-    if (k + 16 < K) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) av[u] = an[u], bv[u] = bn[u];
-    }
   }
   return acc;
+}
+template <bool AK, bool BK>
+__device__ __forceinline__ f32x4 gemm16p(const float* a, int ars, int acs, const float* b,
+                                         int brs, int bcs, int K, int bf16) {
+  return bf16 ? gemm16t<AK, BK, true>(a, ars, acs, b, brs, bcs, K)
+              : gemm16t<AK, BK, false>(a, ars, acs, b, brs, bcs, K);
 }
 
 // 16-lane DPP row reductions (every lane of the row gets the result)
@@ -614,7 +615,11 @@ __global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
   };
   if (pf) fetch(r0);
   __syncthreads();
+#ifdef OMLDM_MLP_STAMPS
+  unsigned long long mlp_t_ = clock64();
+#endif
   for (long long m0 = r0; m0 < r1; m0 += kMB) {
+    MLP_STAMP(0);
     if (pf) {
       float* H = sm + g.lh[0];
 #pragma unroll
@@ -638,6 +643,7 @@ __global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
       continue;
     }
     const float eta = lr / (float)cnt;
+    MLP_STAMP(1);
     // ---- hidden layers: H_{l+1} = act(H_l · W_lᵀ + b_l)
     for (int l = 0; l + 1 < L; ++l) {
       const float* H = sm + g.lh[l];
@@ -660,6 +666,7 @@ __global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
       }
       __syncthreads();
     }
+    MLP_STAMP(2);
     // ---- output layer + loss (np_L = 16: one column tile, a row's logits in one DPP row)
     {
       const int l = L - 1;
@@ -697,7 +704,7 @@ __global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
             } else {
               const float tt = y > 0.f ? 1.f : 0.f;
               gr = 1.f / (1.f + __expf(-o)) - tt;
-              loss += fmaxf(o, 0.f) - o * tt + log1pf(__expf(-fabsf(o)));
+              loss += fmaxf(o, 0.f) - o * tt + __logf(1.f + __expf(-fabsf(o)));  // statistic
               corr += ((o >= 0.f) == (tt > 0.f)) ? 1.f : 0.f;
             }
           }
@@ -709,6 +716,7 @@ __global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
       }
       __syncthreads();
     }
+    MLP_STAMP(3);
     // ---- backward: phase l = dH_l (l ≥ 1) + update of W_{l+1} (l + 1 ≤ L − 1), and the
     // last phase (l = 0) updates W_1 and W_0
     for (int l = L - 1; l >= 0; --l) {
@@ -758,6 +766,7 @@ __global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
       if (ub >= 0) bias_step(ub);
       if (l == 0) bias_step(0);
       __syncthreads();
+      MLP_STAMP(4 + (l < 3 ? l : 3));  // 4: phase 0 (W_1, W_0), 5: phase 1, 6: phase 2
     }
   }
   // ---- round end: Δ = W_spoke − W_0 (as v1)
@@ -903,11 +912,11 @@ __global__ __launch_bounds__(256) void mlp_colsum_kernel(const float* __restrict
 using namespace omldm;
 
 // Round kernel form: 0 v1 (mlp_round_kernel), 1 v2 with 4 waves, 2 v2 with 8 waves (v2 takes
-// output widths ≤ 16). `set` ≥ 0 sets it; the default comes from OMLDM_MLP_FORM (0).
+// output widths ≤ 16). `set` ≥ 0 sets it; the default comes from OMLDM_MLP_FORM (2).
 OMLDM_API int omldm_mlp_form(int set) {
   static int form = [] {
     const char* e = getenv("OMLDM_MLP_FORM");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   if (set >= 0) form = set;
   return form;

@@ -73,8 +73,12 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> st((size_t)S * 8);
   CK(hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost));
   printf("S=%d R=%d bf16=%d: round (+colsum) best %.1f us\n", S, R, bf16, best * 1000.f);
-  const char* ph[] = {"", "stage+barrier", "forward", "loss", "backward rest", "bwd dH+sync",
-                      "bwd W update", "bwd bias+sync"};
+  const bool v2 = omldm_mlp_form(-1) > 0;
+  const char* ph1[] = {"", "stage+barrier", "forward", "loss", "backward rest", "bwd dH+sync",
+                       "bwd W update", "bwd bias+sync"};
+  const char* ph2[] = {"", "stage+barrier+cnt", "hidden forward", "output+loss", "bwd phase 0",
+                       "bwd phase 1", "bwd phase 2", "bwd phase 3+"};
+  const char* const* ph = v2 ? ph2 : ph1;
   const int mbs = (R + 31) / 32;
   for (int k = 1; k <= 7; ++k) {
     std::vector<double> v;

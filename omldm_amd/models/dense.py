@@ -233,7 +233,7 @@ class KMeans(Learner):
 # ---------------------------------------------------------------------- MultiClassPA
 class MultiClassPA(Learner):
     """K-prototype Passive-Aggressive classifier on hashed features (labels 0..K-1);
-    virtual spokes per round: on a GPU with the field-aware wire and K ≤ 4 the v3 table scan
+    virtual spokes per round: on a GPU with the field-aware wire and K ≤ 16 the v3 table scan
     (csrc/kernels/linear_scan3.hip: s3mc_scan_kernel), else the spoke tables
     (csrc/kernels/multiclass_spoke.hip)."""
 
@@ -279,7 +279,7 @@ class MultiClassPA(Learner):
         S = max(1, ctx.spokes)
         R = max(1, -(-batch.B // S))
         if D.multiclass_scan3_fits(batch, R, self.K, self.bias, self.Wt):
-            # exact sequential spokes on the v3 table scan (K ≤ 4, field-aware wire)
+            # exact sequential spokes on the v3 table scan (K ≤ 16, field-aware wire)
             D.multiclass_scan3_round(self.Wt, batch, R, S, self.K, self.variant, self.C,
                                      self.bias, self.dacc, self.st)
         else:  # the spoke-table round (LDS delta tables spilling to HBM)

@@ -5,6 +5,8 @@ csrc/kernels/multiclass_spoke.hip; CPU: identical math in PyTorch / the C++ mirr
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from omldm_amd.api.batch import HashedBatch
@@ -96,8 +98,11 @@ def kmeans_assign(x: torch.Tensor, y: torch.Tensor | None, cent: torch.Tensor,
 
 
 def class_pad(nclass: int) -> int:
-    """Row stride of the key-major prototype shadow (a power of two ≥ nclass)."""
-    return 2 if nclass <= 2 else 4 if nclass <= 4 else 8 if nclass <= 8 else 16
+    """Row stride of the key-major prototype shadow: a power of two ≥ nclass up to 16
+    (the K of the v3 multiclass scan), a multiple of 4 above."""
+    if nclass <= 16:
+        return 2 if nclass <= 2 else 4 if nclass <= 4 else 8 if nclass <= 8 else 16
+    return (nclass + 3) // 4 * 4
 
 
 def proto_shadow(W: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
@@ -357,13 +362,17 @@ def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int], act: int = 
     return mlp_forward_reference(w, x, widths, act)
 
 
+# classes the v3 multiclass scan takes (K templates 2 / 4 / 8 / 16; OMLDM_MC_SCAN_KMAX caps it)
+_MC_SCAN_KMAX = int(os.environ.get("OMLDM_MC_SCAN_KMAX", "8"))
+
+
 def multiclass_scan3_fits(batch, R: int, nclass: int, bias: bool, Wt) -> bool:
     """The MultiClassPA round on the v3 table scan (csrc/kernels/linear_scan3.hip,
-    s3mc_scan_kernel) takes this batch: the engine's field-aware wire on a GPU, K ≤ 4 classes,
+    s3mc_scan_kernel) takes this batch: the engine's field-aware wire on a GPU, K ≤ 16 classes,
     fp32 key-major prototypes, a shape the v3 prep takes."""
     from omldm_amd.ops import linear as L
 
-    return (Wt is not None and Wt.is_cuda and Wt.dtype == torch.float32 and nclass <= 4
+    return (Wt is not None and Wt.is_cuda and Wt.dtype == torch.float32 and nclass <= _MC_SCAN_KMAX
             and getattr(batch, "cat_span", 0) > 0 and batch.B > 0 and 0 < batch.dc
             and L.SEQ_KERNEL == "scan3" and batch.y.is_cuda
             and batch.dn + batch.dc * batch.cat_span <= int(Wt.shape[0]) - 1
@@ -382,7 +391,10 @@ def multiclass_scan3_round(Wt: torch.Tensor, batch, R: int, S: int, nclass: int,
     from omldm_amd.ops.linear import _workspace
 
     dim, kp = int(Wt.shape[0]), int(Wt.shape[1])
-    K = 2 if nclass <= 2 else 4
+    K = class_pad(nclass)  # the scan's class template: 2, 4, 8 or 16
+    kt = int(os.environ.get("OMLDM_MC_KT", "0") or 0)  # diagnostics: a wider template
+    if kt in (4, 8, 16) and kt > K and kt <= int(Wt.shape[1]):
+        K = kt
     num = batch.num.float().contiguous()
     y = batch.y.float().contiguous() if batch.y.dtype != torch.int8 else batch.y.contiguous()
     rb = RawBatch(num, batch.cat.contiguous(), y, span=batch.cat_span, cbase=batch.dn)
@@ -430,7 +442,8 @@ def multiclass_apply(W: torch.Tensor, dacc: torch.Tensor, nact: torch.Tensor,
         assert Wt is None or W.dim() == 2
         check(native.hip().omldm_multiclass_apply(
             ptr(W), ptr(dacc), dim, K, ptr(Wt), int(Wt is not None and Wt.dtype == torch.bfloat16),
-            class_pad(K), ptr(nact), ptr(st), ptr(cum), int(fold), ptr(nact_next),
+            int(Wt.shape[1]) if Wt is not None else class_pad(K), ptr(nact), ptr(st), ptr(cum),
+            int(fold), ptr(nact_next),
             native.stream_of(W)),
             "omldm_multiclass_apply")
     else:

@@ -452,12 +452,36 @@ def test_gpu_scan3_shrinking_rules_match_cpu(name, hyper, task, S, R, uneven):
 
 @gpu
 @pytest.mark.parametrize("K,variant,C", [(4, "PA-I", 1.0), (4, "PA", 1.0), (2, "PA-II", 0.5),
-                                         (3, "PA-I", 0.3)])
+                                         (3, "PA-I", 0.3), (6, "PA-II", 0.5), (8, "PA-I", 1.0),
+                                         (10, "PA-I", 1.0), (16, "PA", 1.0)])
 @pytest.mark.parametrize("S,R", [(16, 4096), (5, 300)])
 def test_gpu_multiclass_scan3_matches_cpu(K, variant, C, S, R):
     """MultiClassPA on the v3 table scan (s3mc_scan_kernel: K scores per row through the
-    chunk recurrence, then one scatter of ±τ into the K prototypes) against the CPU mirror
-    (dense_cpu.cpp), three rounds on the engine's field-aware wire."""
+    chunk recurrence, then one scatter of ±τ into the K prototypes; K templates 2 / 4 / 8 /
+    16 with the padded classes skipped) against the CPU mirror (dense_cpu.cpp), three rounds
+    on the engine's field-aware wire."""
+    _mc_scan3_vs_cpu(K, variant, C, S, R)
+
+
+@gpu
+@pytest.mark.parametrize("K", [4, 10])
+def test_gpu_multiclass_scan3_at_the_bench_geometry(K):
+    """The bench geometry: 16 spokes × 8192 rows, 2^20 hashed dimensions (verdict task:
+    K = 4 and K = 10 on the scan, equal to the CPU oracle)."""
+    _mc_scan3_vs_cpu(K, "PA-I", 1.0, 16, 8192, rounds=2)
+
+
+def _mc_scan3_vs_cpu(K, variant, C, S, R, rounds=3):
+    from omldm_amd.ops import dense as D
+
+    kmax, D._MC_SCAN_KMAX = D._MC_SCAN_KMAX, 16  # the wide template on, whatever the default
+    try:
+        _mc_scan3_vs_cpu_body(K, variant, C, S, R, rounds)
+    finally:
+        D._MC_SCAN_KMAX = kmax
+
+
+def _mc_scan3_vs_cpu_body(K, variant, C, S, R, rounds):
     from omldm_amd.io.synthetic import synth_batch
     from omldm_amd.models import make_learner
     from omldm_amd.models.base import RoundContext
@@ -468,18 +492,19 @@ def test_gpu_multiclass_scan3_matches_cpu(K, variant, C, S, R):
     for d in ("cpu", dev):
         lrn = make_learner("MultiClassPA", {"nClasses": K, "variant": variant, "C": C}, space, d)
         before = L.SCAN3_ROUNDS
-        for k in range(3):
+        for k in range(rounds):
             b = synth_batch(space, S * R - 11, start=k * S * R, task=2, n_classes=K, seed=43)
             lrn.fit(b.to(d) if d != "cpu" else b, RoundContext(spokes=S, inv_p=1.0 / S))
         if d != "cpu":
             torch.cuda.synchronize()
-            assert L.SCAN3_ROUNDS - before == 3, "the rounds left the v3 scan"
+            assert L.SCAN3_ROUNDS - before == rounds, "the rounds left the v3 scan"
         res[str(d)] = (lrn.W.detach().float().cpu(), lrn.running_totals())
     wg, wc = res[str(dev)][0], res["cpu"][0]
     scale = max(1.0, float(wc.abs().max()))
     np.testing.assert_allclose(wg.numpy(), wc.numpy(), rtol=3e-3, atol=3e-5 * scale)
     tg, tc = res[str(dev)][1], res["cpu"][1]
-    assert tg["fitted"] == tc["fitted"] == 3 * (S * R - 11)
+    assert tg["fitted"] == tc["fitted"] == rounds * (S * R - 11)
+    assert tg.get("overflow", 0) == 0
     assert abs(tg["mistakes"] - tc["mistakes"]) <= 2e-3 * tc["fitted"] + 2
 
 
