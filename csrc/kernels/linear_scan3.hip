@@ -1721,9 +1721,11 @@ __global__ __launch_bounds__(256) void s3_scatter_kernel(const int* __restrict__
 // spoke's updates added by the scatter) or the key-major prototypes, and stage the Grams.
 // Each row's (τ, r) goes to a record; s3mc_scatter_kernel adds the spokes' updates after.
 // K ∈ {2, 4, 8, 16} (nclass ≤ K; the classes past nclass cost uniform branches only): the
-// helpers add their base-margin partials into one K × 64 array with LDS float atomics
-// (the scanner reads K values per lane per chunk and clears them), so the LDS the scan
-// needs grows by K·512 bytes, not by K·NHA·512.
+// helpers add their base-margin partials into one K × 64 array with LDS 64-bit integer
+// atomics on 32.32 fixed point (the scanner reads K values per lane per chunk and clears
+// them), so the LDS the scan needs grows by K·1 KB, not by K·NHA·512 B — and the sum is
+// independent of the helpers' arrival order: with float atomics a near-tie between two
+// classes could resolve differently from run to run (the argmax is discontinuous).
 namespace s3 {
 constexpr int MCK = 16;  // classes on the v3 multiclass scan (more: the spoke tables)
 }
@@ -1732,7 +1734,7 @@ template <int K>
 struct S3McSmem {
   alignas(16) float G[2][s3::CH][s3::GS];
   alignas(16) float X1[2][s3::CH][s3::GS];
-  float part[2][K][s3::CH];  // base margins by class (the helpers' partials, LDS atomics)
+  long long part[2][K][s3::CH];  // base margins by class, 32.32 fixed point (LDS atomics)
   float tau[2][s3::CH];      // τ of the chunk's rows, by parity
   int rr[2][s3::CH];         // r (the updated wrong class) of the chunk's rows
 };
@@ -1825,7 +1827,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
   const float* P0 = prep + (size_t)s * nchs * PF;
   auto chunk_prep = [&](int k) { return P0 + (size_t)k * PF; };
   float* ag = A.aglob + (size_t)s * gstride * K;
-  for (int i = tid; i < 2 * K * s3::CH; i += s3::NT) (&sm.part[0][0][0])[i] = 0.f;
+  for (int i = tid; i < 2 * K * s3::CH; i += s3::NT) (&sm.part[0][0][0])[i] = 0;
   __syncthreads();
 
   if (wave == 0) {
@@ -1859,8 +1861,8 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         float w[K], n1[K], sy = 0.f;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
-          const float v = sm.part[b][c][lane] + f1[c];
-          sm.part[b][c][lane] = 0.f;  // the helpers add chunk k + 2's partials here
+          const float v = (float)(__ll2double_rn(sm.part[b][c][lane]) * 0x1p-32) + f1[c];
+          sm.part[b][c][lane] = 0;  // the helpers add chunk k + 2's partials here
           n1[c] = 0.f;
           sy = c == yi ? v : sy;
           w[c] = TREE && (c == yi || c >= A.nclass) ? -INFINITY : v;
@@ -2153,7 +2155,9 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
       }
 #pragma unroll
       for (int c = 0; c < K; ++c)
-        if (K <= 4 || c < A.nclass) atomicAdd(&sm.part[cn & 1][c][r], base[c]);
+        if (K <= 4 || c < A.nclass)
+          atomicAdd(reinterpret_cast<unsigned long long*>(&sm.part[cn & 1][c][r]),
+                    (unsigned long long)__double2ll_rn((double)base[c] * 0x1p32));
     }
     const unsigned long long hc = hdbg ? __builtin_amdgcn_s_memtime() : 0;
     // ---- aG_{cn} → G[cn & 1], aX1_{cn+1} → X1[(cn+1) & 1] (LEAN: before the margins)

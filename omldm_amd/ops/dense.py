@@ -363,7 +363,7 @@ def mlp_forward(w: torch.Tensor, x: torch.Tensor, widths: list[int], act: int = 
 
 
 # classes the v3 multiclass scan takes (K templates 2 / 4 / 8 / 16; OMLDM_MC_SCAN_KMAX caps it)
-_MC_SCAN_KMAX = int(os.environ.get("OMLDM_MC_SCAN_KMAX", "8"))
+_MC_SCAN_KMAX = int(os.environ.get("OMLDM_MC_SCAN_KMAX", "16"))
 
 
 def multiclass_scan3_fits(batch, R: int, nclass: int, bias: bool, Wt) -> bool:
