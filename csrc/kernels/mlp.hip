@@ -284,15 +284,25 @@ __device__ void stage_rows(const float* __restrict__ x, long long r0, long long 
 
 // Diagnostics only (csrc/tests/mlp_stamp_probe.hip builds with OMLDM_MLP_STAMPS): per
 // spoke, clock64 sums of the mini-batch phases (staging+barrier, forward, loss, backward).
+// The sums stay in registers until the round's end (a global read-modify-write per stamp
+// would put a memory round trip into every phase it measures).
 #ifdef OMLDM_MLP_STAMPS
 __device__ unsigned long long* g_mlp_stamps;
 #define MLP_STAMP(k)                                                                  \
   do {                                                                                \
     const unsigned long long now_ = clock64();                                        \
-    if (tid == 0 && (k) > 0) g_mlp_stamps[(size_t)blockIdx.x * 8 + (k)] += now_ - mlp_t_; \
+    if ((k) > 0) mlp_acc_[(k) & 7] += now_ - mlp_t_;                                    \
     mlp_t_ = now_;                                                                    \
   } while (0)
+#define MLP_STAMP_FLUSH()                                                             \
+  do {                                                                                \
+    if (tid == 0)                                                                     \
+      for (int k_ = 1; k_ < 8; ++k_) g_mlp_stamps[(size_t)blockIdx.x * 8 + k_] += mlp_acc_[k_]; \
+  } while (0)
 #else
+#define MLP_STAMP_FLUSH() \
+  do {                    \
+  } while (0)
 #define MLP_STAMP(k) \
   do {               \
   } while (0)
@@ -341,6 +351,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
   if (pf) fetch(r0);
 #ifdef OMLDM_MLP_STAMPS
   unsigned long long mlp_t_ = clock64();
+  unsigned long long mlp_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   for (long long m0 = r0; m0 < r1; m0 += kMB) {
     MLP_STAMP(0);
@@ -453,6 +464,7 @@ __global__ __launch_bounds__(256) void mlp_round_kernel(const float* __restrict_
     }
     MLP_STAMP(4);
   }
+  MLP_STAMP_FLUSH();
   // ---- round end: Δ = W_spoke − W_0. With a workspace: the spoke's own row, plain
   // coalesced stores (mlp_colsum_kernel sums the rows); without: atomics into the
   // accumulator (every spoke hits the same nparams addresses — the slow fallback).
@@ -617,6 +629,7 @@ __global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
   __syncthreads();
 #ifdef OMLDM_MLP_STAMPS
   unsigned long long mlp_t_ = clock64();
+  unsigned long long mlp_acc_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   for (long long m0 = r0; m0 < r1; m0 += kMB) {
     MLP_STAMP(0);
@@ -769,6 +782,7 @@ __global__ __launch_bounds__(NW * 64) void mlp_round2_kernel(
       MLP_STAMP(4 + (l < 3 ? l : 3));  // 4: phase 0 (W_1, W_0), 5: phase 1, 6: phase 2
     }
   }
+  MLP_STAMP_FLUSH();
   // ---- round end: Δ = W_spoke − W_0 (as v1)
   float* wrow = ws ? ws + (size_t)blockIdx.x * nparams : nullptr;
   for (int l = 0; l < L; ++l) {
@@ -911,12 +925,12 @@ __global__ __launch_bounds__(256) void mlp_colsum_kernel(const float* __restrict
 
 using namespace omldm;
 
-// Round kernel form: 0 v1 (mlp_round_kernel), 1 v2 with 4 waves, 2 v2 with 8 waves (v2 takes
-// output widths ≤ 16). `set` ≥ 0 sets it; the default comes from OMLDM_MLP_FORM (2).
+// Round kernel form: 0 v1 (mlp_round_kernel), 1 / 2 / 3 v2 with 4 / 8 / 16 waves (v2 takes
+// output widths ≤ 16). `set` ≥ 0 sets it; the default comes from OMLDM_MLP_FORM (3).
 OMLDM_API int omldm_mlp_form(int set) {
   static int form = [] {
     const char* e = getenv("OMLDM_MLP_FORM");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 3;
   }();
   if (set >= 0) form = set;
   return form;
@@ -947,7 +961,11 @@ OMLDM_API int omldm_mlp_round(const float* w, const float* x, const float* y, lo
     const size_t lds = (size_t)g.total * 4;
     const int nparams = g.boff[g.L - 1] + g.n[g.L];
     int e;
-    if (form == 2) {
+    if (form == 3) {
+      if ((e = check_dyn_lds((const void*)mlp_round2_kernel<16>, lds))) return e;
+      hipLaunchKernelGGL(mlp_round2_kernel<16>, dim3(S), dim3(1024), lds, (hipStream_t)stream, w,
+                         x, y, B, R, lr, dacc, stats, nact, g, ws, nparams);
+    } else if (form == 2) {
       if ((e = check_dyn_lds((const void*)mlp_round2_kernel<8>, lds))) return e;
       hipLaunchKernelGGL(mlp_round2_kernel<8>, dim3(S), dim3(512), lds, (hipStream_t)stream, w, x,
                          y, B, R, lr, dacc, stats, nact, g, ws, nparams);
