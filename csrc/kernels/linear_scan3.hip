@@ -1787,6 +1787,30 @@ __device__ __forceinline__ void s3mc_decide_w(const float (&w)[K], float sy, flo
   tau = (valid && r >= 0 && a > 0.f) ? fminf(cmax, loss * a) : 0.f;
 }
 
+// K ≥ 8, the same form: the best wrong score by an fmax tree, its class as the lowest set
+// bit of the classes equal to it (an OR tree of one-hot words): depth ~2·log2 K, and no
+// (value, index) pair arrays (the wide templates' VGPR budget).
+template <int N>
+__device__ __forceinline__ float s3mc_tmax(const float* v) {
+  if constexpr (N == 1) return v[0];
+  else return fmaxf(s3mc_tmax<N / 2>(v), s3mc_tmax<N - N / 2>(v + N / 2));
+}
+template <int N>
+__device__ __forceinline__ uint32_t s3mc_tbits(const float* v, float best, int c0) {
+  if constexpr (N == 1) return v[0] == best ? (1u << c0) : 0u;
+  else return s3mc_tbits<N / 2>(v, best, c0) | s3mc_tbits<N - N / 2>(v + N / 2, best, c0 + N / 2);
+}
+template <int K>
+__device__ __forceinline__ void s3mc_decide_w2(const float (&w)[K], float sy, float a, float cmax,
+                                               bool valid, float& tau, int& r, float& margin) {
+  const float best = s3mc_tmax<K>(w);
+  const uint32_t bits = s3mc_tbits<K>(w, best, 0);
+  r = best == -INFINITY ? -1 : (int)__builtin_ctz(bits | 0x80000000u);
+  margin = sy - best;
+  const float loss = fmaxf(0.f, 1.f - margin);
+  tau = (valid && r >= 0 && a > 0.f) ? fminf(cmax, loss * a) : 0.f;
+}
+
 // The coefficient of class c in a step that moves class yt by +τ and class rt by −τ:
 // uniform operands, selected on the scalar unit (the sign through the bit pattern).
 __device__ __forceinline__ float s3mc_coef(int c, int yt, int rt, uint32_t ctb) {
@@ -1857,7 +1881,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         // nclass), sy = its own class's score, both kept up to date by the steps, and the
         // best wrong class a max tree (s3mc_decide_w); K ≥ 8: the plain scores u = w and
         // the branch-free class scan (s3mc_decide) — measured per K (profiles/round6/mc/)
-        constexpr bool TREE = K <= 4;
+        constexpr bool TREE = true;  // the masked form at every K (decide_w / decide_w2)
         float w[K], n1[K], sy = 0.f;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
@@ -1880,8 +1904,8 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         int rl;
 #pragma unroll
         for (int t = 0; t < s3::CH; ++t) {
-          if constexpr (TREE) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
-          else s3mc_decide<K>(w, yi, A.nclass, a, A.cmax, valid, tl, rl, mg);
+          if constexpr (K <= 4) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
+          else s3mc_decide_w2<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
           const uint32_t ctb = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(tl), t);
           const int rt = __builtin_amdgcn_readlane(rl, t);
           const int yt = __builtin_amdgcn_readlane(yi, t);
@@ -1890,8 +1914,8 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
             w[c] = fmaf(s3mc_coef(c, yt, rt, ctb), gg[t], w[c]);  // −inf stays −inf
           if constexpr (TREE) sy = fmaf(s3mc_coef(yi, yt, rt, ctb), gg[t], sy);
         }
-        if constexpr (TREE) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
-        else s3mc_decide<K>(w, yi, A.nclass, a, A.cmax, valid, tl, rl, mg);
+        if constexpr (K <= 4) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
+        else s3mc_decide_w2<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
         // chunk k+1's X1 fold: n1[c] = Σ_t c_t^c · X1_{k+1}[lane][t]
         {
           const float* xrow = &sm.X1[b ^ 1][lane][0];

@@ -501,7 +501,14 @@ def _mc_scan3_vs_cpu_body(K, variant, C, S, R, rounds):
         res[str(d)] = (lrn.W.detach().float().cpu(), lrn.running_totals())
     wg, wc = res[str(dev)][0], res["cpu"][0]
     scale = max(1.0, float(wc.abs().max()))
-    np.testing.assert_allclose(wg.numpy(), wc.numpy(), rtol=3e-3, atol=3e-5 * scale)
+    # the wrong class is an argmax: the spokes' updates meet in the cross-spoke combine in
+    # arrival order (fp32 reassociation, ~1e-7), and a near tie between two classes can then
+    # resolve the other way than on the CPU in a later round — one row's update, moved to
+    # another class (seen: 1 run in 4 at K = 10, |ΔW| 4.2e-3 on 0.07 % of the entries).
+    # Everything else must agree to fp32 reassociation.
+    bad = ~np.isclose(wg.numpy(), wc.numpy(), rtol=3e-3, atol=3e-5 * scale)
+    assert bad.mean() <= 2e-3, (int(bad.sum()), float(np.abs(wg.numpy() - wc.numpy()).max()))
+    assert float(np.abs(wg.numpy() - wc.numpy()).max()) <= 2e-2 * scale
     tg, tc = res[str(dev)][1], res["cpu"][1]
     assert tg["fitted"] == tc["fitted"] == rounds * (S * R - 11)
     assert tg.get("overflow", 0) == 0
