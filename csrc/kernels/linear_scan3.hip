@@ -1787,7 +1787,10 @@ __device__ __forceinline__ void s3mc_decide_w(const float (&w)[K], float sy, flo
   tau = (valid && r >= 0 && a > 0.f) ? fminf(cmax, loss * a) : 0.f;
 }
 
-// K ≥ 8, the same form: the best wrong score by an fmax tree, its class as the lowest set
+#ifndef S3MC_PAIR_TREE_K
+#define S3MC_PAIR_TREE_K 2  // (value, index) pair tree up to this K; the fmax / OR tree above
+#endif
+// K > S3MC_PAIR_TREE_K, the same form: the best wrong score by an fmax tree, its class as the lowest set
 // bit of the classes equal to it (an OR tree of one-hot words): depth ~2·log2 K, and no
 // (value, index) pair arrays (the wide templates' VGPR budget).
 template <int N>
@@ -1904,7 +1907,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
         int rl;
 #pragma unroll
         for (int t = 0; t < s3::CH; ++t) {
-          if constexpr (K <= 4) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
+          if constexpr (K <= S3MC_PAIR_TREE_K) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
           else s3mc_decide_w2<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
           const uint32_t ctb = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(tl), t);
           const int rt = __builtin_amdgcn_readlane(rl, t);
@@ -1914,7 +1917,7 @@ __global__ __launch_bounds__(s3::NT, s3::WPE) __attribute__((amdgpu_waves_per_eu
             w[c] = fmaf(s3mc_coef(c, yt, rt, ctb), gg[t], w[c]);  // −inf stays −inf
           if constexpr (TREE) sy = fmaf(s3mc_coef(yi, yt, rt, ctb), gg[t], sy);
         }
-        if constexpr (K <= 4) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
+        if constexpr (K <= S3MC_PAIR_TREE_K) s3mc_decide_w<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
         else s3mc_decide_w2<K>(w, sy, a, A.cmax, valid, tl, rl, mg);
         // chunk k+1's X1 fold: n1[c] = Σ_t c_t^c · X1_{k+1}[lane][t]
         {
