@@ -73,6 +73,11 @@ def run(pipes, recs_block, n_blocks, a, device, comm, trace=False):
             job.tick()
         if device.type == "cuda":
             torch.cuda.synchronize(device)
+        prof = None
+        if trace and device.type == "cuda":  # in-process kernel trace (torch.profiler)
+            prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA,
+                                                      torch.profiler.ProfilerActivity.CPU])
+            prof.__enter__()
         t0 = time.perf_counter()
         ticks = 0
         want = n_blocks * a.block
@@ -82,6 +87,12 @@ def run(pipes, recs_block, n_blocks, a, device, comm, trace=False):
         if device.type == "cuda":
             torch.cuda.synchronize(device)
         wall = time.perf_counter() - t0
+        if prof is not None:
+            prof.__exit__(None, None, None)
+            table = prof.key_averages().table(sort_by="self_device_time_total", row_limit=40)
+            with open(trace, "w") as f:
+                f.write(f"# {len(pipes)} pipelines, {ticks} ticks, {wall * 1e3 / max(1, ticks):.3f} ms "
+                        f"per tick (profiled run)\n" + table + "\n")
         models = {pid: p.learner.state_vector().detach().float().cpu().clone()
                   for pid, p in job.pipes.items()}
         recs = job.counters["records"]
@@ -96,6 +107,7 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=131072, help="records per tick")
     ap.add_argument("--streams", type=int, default=2, help="engine pipelineStreams")
     ap.add_argument("--solo", type=int, default=1, help="one-pipeline reference runs")
+    ap.add_argument("--trace", default="", help="write a kernel summary of the 16-pipeline run")
     a = ap.parse_args(argv)
     comm, device = init_distributed()
     sp = FeatureSpace(13, 0, 26, 1 << 20)
@@ -103,6 +115,8 @@ def main(argv=None) -> int:
     n_blocks = max(1, a.records // a.block)
     pipes = [(i + 1, p) for i, p in enumerate(PIPES)]
     job, ms_tick, ticks, recs, models = run(pipes, block, n_blocks, a, device, comm)
+    if a.trace:
+        run(pipes, block, n_blocks, a, device, comm, trace=a.trace)
     out = {"metric": "BASELINE config 5 through the engine: 16 heterogeneous pipelines "
                      "(requests topic → Job ticks), ms per tick and pipeline-examples/s",
            "ms_per_tick": round(ms_tick, 3), "ticks": ticks, "records": recs,
