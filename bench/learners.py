@@ -59,6 +59,7 @@ P16_CASES = [
     ("RegressorPA", 1, {}, 16, "compact"),
     ("LogisticRegression", 0, {}, 16, "compact"),
     ("MultiClassPA", 2, {"nClasses": 4}, 16, "compact"),
+    ("MultiClassPA@k2", 2, {"nClasses": 2}, 16, "compact"),  # the binary-scan form
     ("ORR", 1, {}, 16),
     ("K-means", 0, {"k": 16}, 16),
     ("NN", 0, {"hiddenLayers": [64, 64]}, 16),
@@ -74,7 +75,8 @@ def _quality(base, task, hyper, space, ring, spokes, dev, rounds):
     reference-semantics host path), both trained on the same ``rounds`` rounds of the
     bench's stream at the bench's spokes: the learner's own evaluate() — loss per point
     and score per point (accuracy for classifiers, the learner's score otherwise)."""
-    hold = synth_batch(space, 16384, start=10 ** 8, seed=26, task=task, n_classes=4)
+    hold = synth_batch(space, 16384, start=10 ** 8, seed=26, task=task,
+                       n_classes=int(hyper.get("nClasses", 4)))
     if base == "NN":
         hold = HashedBatch(hold.num, hold.cat, torch.where(hold.y > 0, 1.0, -1.0))
     ctx = RoundContext(spokes=spokes)
@@ -121,7 +123,8 @@ def main(argv=None) -> int:
             continue
         ring = []
         for k in range(3):
-            b = synth_batch(space, a.batch, start=k * a.batch, seed=25, task=task, n_classes=4)
+            b = synth_batch(space, a.batch, start=k * a.batch, seed=25, task=task,
+                            n_classes=int(hyper.get("nClasses", 4)))
             if name.split("@")[0] in ("NN",):
                 b = HashedBatch(b.num, b.cat, torch.where(b.y > 0, 1.0, -1.0))
             ring.append(b.to(dev))

@@ -409,12 +409,13 @@ __global__ __launch_bounds__(64) void kmeans_fast_kernel(const float* __restrict
         ich += __builtin_bit_cast(float, mw);
         // the lowest lane holding the minimum (some lane always does: the mask is ≠ 0)
         const unsigned long long eq = __builtin_amdgcn_ballot_w64(key == mw);
-        if (grp == (int)__builtin_ctzll(eq | (1ull << 63)) / G) {
-          n += 1.f;
-          const float r = rcp_rn(n);
+        // the winner's lanes move the centroid; selects, not a divergent branch (no exec
+        // mask save / restore on the chain)
+        const bool win = grp == (int)__builtin_ctzll(eq | (1ull << 63)) / G;
+        n = win ? n + 1.f : n;
+        const float r = rcp_rn(n);
 #pragma unroll
-          for (int i = 0; i < ND; ++i) c[i] = fmaf(r, xc[i] - c[i], c[i]);
-        }
+        for (int i = 0; i < ND; ++i) c[i] = win ? fmaf(r, xc[i] - c[i], c[i]) : c[i];
       }
 #pragma unroll
       for (int i = 0; i < ND; ++i) xc[i] = xn[i];

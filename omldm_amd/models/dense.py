@@ -8,6 +8,8 @@ slots feed the linear family and MultiClassPA.
 """
 from __future__ import annotations
 
+import os
+
 import math
 
 import torch
@@ -273,11 +275,50 @@ class MultiClassPA(Learner):
         if self.Wt is not None:
             self.Wt[:, : self.K].copy_(self.W.t())
 
+    def _fit_two_classes(self, batch, ctx, R: int, S: int) -> bool:
+        """Two classes are one binary PA on v = w_0 − w_1: with y' = +1 for class 0 and −1
+        for class 1, the margin s_y − s_r is y'·v·x, the hinge loss is the same, the update
+        moves w_y by +τx and w_r by −τx, i.e. v by y'·2τ·x, and w_0 + w_1 never changes;
+        2τ is the binary step at C' = 2C (PA-I: min(2C, ℓ/‖x‖²); PA-II: ℓ/(‖x‖² + 1/(4C));
+        PA: ℓ/‖x‖²). So the round runs the binary v3 scan (its step chain is ~4× shorter
+        than the K-score scan's) and the prototypes are rebuilt from v and the invariant
+        sum. Same rows, same order, same running totals (hinge loss, margin ≤ 0 mistakes)."""
+        from omldm_amd.api.batch import RawBatch
+
+        if not (self.W.is_cuda and os.environ.get("OMLDM_MC_BINARY", "1") != "0"
+                and self.Wt is not None and self.Wt.dtype == torch.float32
+                and getattr(batch, "cat_span", 0) > 0 and batch.dc > 0 and batch.y.is_cuda
+                and L.SEQ_KERNEL == "scan3"
+                and batch.dn + batch.dc * batch.cat_span <= self.dim - 1
+                and L.scan3_fits(batch.dn, batch.dc, R, self.bias)):
+            return False
+        yf = batch.y.float()
+        yb = torch.where(yf == 0, 1.0, torch.where(yf == 1, -1.0, float("nan"))).contiguous()
+        rb = RawBatch(batch.num.float().contiguous(), batch.cat.contiguous(), yb,
+                      span=batch.cat_span, cbase=batch.dn)
+        if not L.scan3_eligible_compact(rb, R, self.bias, self.dim):
+            return False
+        rule = L.LinearRule(rule=L.RULE_HINGE, variant=self.variant, C=2.0 * self.C,
+                            bias=self.bias)
+        if getattr(self, "_dacc2", None) is None:
+            self._dacc2 = torch.zeros(self.dim + 2, dtype=torch.float32, device=self.device)
+        ssum = self.W[0] + self.W[1]
+        v = (self.W[0] - self.W[1]).contiguous()
+        L.linear_seq_round(v, rb, R, S, self._dacc2, rule, ctx.inv_p, cum=self.cum,
+                           hashed=True)
+        L.linear_apply(v, None, self._dacc2)
+        self.W[0].copy_((ssum + v) * 0.5)
+        self.W[1].copy_((ssum - v) * 0.5)
+        self.on_state_loaded()  # the key-major shadow
+        return True
+
     def fit(self, batch, ctx):
         if batch.B == 0:
             return
         S = max(1, ctx.spokes)
         R = max(1, -(-batch.B // S))
+        if self.K == 2 and self._fit_two_classes(batch, ctx, R, S):
+            return
         if D.multiclass_scan3_fits(batch, R, self.K, self.bias, self.Wt):
             # exact sequential spokes on the v3 table scan (K ≤ 16, field-aware wire)
             D.multiclass_scan3_round(self.Wt, batch, R, S, self.K, self.variant, self.C,

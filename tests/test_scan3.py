@@ -455,12 +455,36 @@ def test_gpu_scan3_shrinking_rules_match_cpu(name, hyper, task, S, R, uneven):
                                          (3, "PA-I", 0.3), (6, "PA-II", 0.5), (8, "PA-I", 1.0),
                                          (10, "PA-I", 1.0), (16, "PA", 1.0)])
 @pytest.mark.parametrize("S,R", [(16, 4096), (5, 300)])
-def test_gpu_multiclass_scan3_matches_cpu(K, variant, C, S, R):
+def test_gpu_multiclass_scan3_matches_cpu(K, variant, C, S, R, monkeypatch):
     """MultiClassPA on the v3 table scan (s3mc_scan_kernel: K scores per row through the
     chunk recurrence, then one scatter of ±τ into the K prototypes; K templates 2 / 4 / 8 /
     16 with the padded classes skipped) against the CPU mirror (dense_cpu.cpp), three rounds
-    on the engine's field-aware wire."""
+    on the engine's field-aware wire. (K = 2 here with the binary form off.)"""
+    monkeypatch.setenv("OMLDM_MC_BINARY", "0")
     _mc_scan3_vs_cpu(K, variant, C, S, R)
+
+
+@gpu
+@pytest.mark.parametrize("variant,C", [("PA-I", 1.0), ("PA", 1.0), ("PA-II", 0.5),
+                                       ("PA-I", 0.05)])
+@pytest.mark.parametrize("S,R", [(16, 4096), (5, 300), (16, 8192)])
+def test_gpu_multiclass_two_classes_on_the_binary_scan(variant, C, S, R, monkeypatch):
+    """K = 2 as one binary PA on v = w_0 − w_1 at C' = 2C (models/dense.py:
+    MultiClassPA._fit_two_classes) against the CPU mirror of the K-prototype rule."""
+    from omldm_amd.models.dense import MultiClassPA
+
+    taken = []
+    orig = MultiClassPA._fit_two_classes
+
+    def spy(self, *a):
+        taken.append(orig(self, *a))
+        return taken[-1]
+
+    monkeypatch.setattr(MultiClassPA, "_fit_two_classes", spy)
+    monkeypatch.delenv("OMLDM_MC_BINARY", raising=False)
+    rounds = 3 if R < 8192 else 2
+    _mc_scan3_vs_cpu(2, variant, C, S, R, rounds=rounds)
+    assert taken.count(True) == rounds, taken  # every GPU round took the binary form
 
 
 @gpu
