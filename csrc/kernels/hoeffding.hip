@@ -640,7 +640,7 @@ __device__ __forceinline__ float ld_l2(const float* p) {
 // writing the parent's statistics back): node, cc[C], S0[C], lo[d], hi[d] and, with S12,
 // Σx[d·C], Σx²[d·C]. Then gains[d·nb] and the chunk's rows xs[NT][d].
 struct HxLayout {
-  size_t tn, since, consumed, slot, cntw, snode, cc, s0, lo, hi, s1, s2, gains, xs, bytes;
+  size_t tn, since, consumed, slot, cntw, snode, cc, s0, lo, hi, s1, s2, gains, xs, lmask, bytes;
   int NS;
 };
 
@@ -668,6 +668,7 @@ __host__ __device__ inline HxLayout ht_exact_layout(int N, int d, int C, int nb,
   L.s2 = s12 ? put(ns * d * C * 4) : 0;
   L.gains = put((size_t)d * nb * 4);
   L.xs = put((size_t)kHxNT * d * 4);
+  L.lmask = put((size_t)kHxNW * ns * 8);
   L.bytes = o;
   return L;
 }
@@ -689,7 +690,7 @@ template <bool S12>
 __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
     const float* __restrict__ x, const float* __restrict__ yv, int B, int d, int C, int depth,
     int N, int nb, float grace, float delta, float tau, HxTree T, double* __restrict__ nfit,
-    unsigned long long* __restrict__ dbg) {
+    unsigned long long* __restrict__ dbg, int rank_masks) {
   // dbg (diagnostics, may be null): [0] chunks, [1] segments, [2] splits, [3..6] cycles in
   // chunk setup / due search / statistics / split checks (wave 0's clock)
   unsigned long long t_setup = 0, t_due = 0, t_stat = 0, t_split = 0, n_chunk = 0, n_seg = 0,
@@ -710,6 +711,8 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
   float* s2 = reinterpret_cast<float*>(hx_smem + Ly.s2);
   float* gains = reinterpret_cast<float*>(hx_smem + Ly.gains);
   float* xs = reinterpret_cast<float*>(hx_smem + Ly.xs);
+  // per wave and leaf slot: the lanes of the chunk's rows at that leaf (zero between uses)
+  unsigned long long* lmask = reinterpret_cast<unsigned long long*>(hx_smem + Ly.lmask);
   const int NS = Ly.NS;
   __shared__ int s_first, s_leaf, s_flag, s_nn, s_nslot;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -731,6 +734,7 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
     }
     s_nslot = k;
   }
+  for (int i = tid; i < kHxNW * NS; i += kHxNT) lmask[i] = 0ull;
   for (int n = tid; n < N; n += kHxNT) {
     tn[n] = make_int4((int)T.feat[n], __float_as_int(T.thr[n]), (int)T.left[n], (int)T.right[n]);
     since_l[n] = T.since[n];
@@ -800,9 +804,26 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
     }
     // the row's rank among the chunk's training rows of its leaf (stream order)
     int rank = 0;
-    {
+    const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const int ks = valid ? slot[leaf] : 0;
+    if (rank_masks && !__ballot(valid && ks < 0)) {
+      // every row's leaf has a slot: each row ORs its lane bit into its (wave, slot) mask,
+      // reads the mask back (one wave's LDS instructions complete in order, so the read sees
+      // every lane's OR) — rank = lanes below at the same leaf, count = all of them — and the
+      // leaf's first lane publishes the count and clears the mask for the next chunk. O(1)
+      // per row instead of one pass per distinct leaf of the wave.
+      unsigned long long* lm = lmask + (size_t)w * NS + ks;
+      if (valid) atomicOr(lm, 1ull << lane);
+      const unsigned long long m = valid ? *lm : 0ull;
+      if (valid) {
+        rank = __popcll(m & below);
+        if (rank == 0) {
+          cntw[w * N + leaf] = (unsigned char)__popcll(m);
+          *lm = 0ull;
+        }
+      }
+    } else {
       unsigned long long pending = __ballot(valid);
-      const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
       while (pending) {
         const int leader = __ffsll((long long)pending) - 1;
         const int L = __shfl(leaf, leader);
@@ -1172,15 +1193,20 @@ OMLDM_API int omldm_ht_exact(const float* x, const float* y, int B, int d, int C
   const size_t lds = ht_exact_layout(N, d, C, nb, s12).bytes;
   if (lds > kMax) return -2;
   const void* fn = s12 ? (const void*)ht_exact_kernel<true> : (const void*)ht_exact_kernel<false>;
+  static int rank_masks = -1;  // OMLDM_HT_RANK=0: the per-leaf ballot loop (the A/B)
+  if (rank_masks < 0) {
+    const char* ev = getenv("OMLDM_HT_RANK");
+    rank_masks = (ev && ev[0] == '0') ? 0 : 1;
+  }
   const int e = check_dyn_lds(fn, lds);
   if (e) return e;
   HxTree T{tree[0], tree[1], tree[2], tree[3], tree[4], tree[5],
            tree[6], tree[7], tree[8], tree[9], tree[10], tree[11]};
   if (s12)
     hipLaunchKernelGGL(ht_exact_kernel<true>, dim3(1), dim3(kHxNT), lds, (hipStream_t)stream, x,
-                       y, B, d, C, depth, N, nb, grace, delta, tau, T, nfit, dbg);
+                       y, B, d, C, depth, N, nb, grace, delta, tau, T, nfit, dbg, rank_masks);
   else
     hipLaunchKernelGGL(ht_exact_kernel<false>, dim3(1), dim3(kHxNT), lds, (hipStream_t)stream, x,
-                       y, B, d, C, depth, N, nb, grace, delta, tau, T, nfit, dbg);
+                       y, B, d, C, depth, N, nb, grace, delta, tau, T, nfit, dbg, rank_masks);
   return (int)hipGetLastError();
 }
