@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 import torch
 
-from omldm_amd.api.batch import FeatureSpace, RawBatch
+from omldm_amd.api.batch import FeatureSpace, HashedBatch, RawBatch
 from omldm_amd.io.synthetic import synth_raw
 from omldm_amd.ops import linear as L
 from omldm_amd.ops import native
@@ -462,6 +462,31 @@ def test_gpu_multiclass_scan3_matches_cpu(K, variant, C, S, R, monkeypatch):
     on the engine's field-aware wire. (K = 2 here with the binary form off.)"""
     monkeypatch.setenv("OMLDM_MC_BINARY", "0")
     _mc_scan3_vs_cpu(K, variant, C, S, R)
+
+
+@pytest.mark.parametrize("variant,C", [("PA-I", 1.0), ("PA-I", 0.005), ("PA", 1.0),
+                                       ("PA-II", 0.5), ("PA-II", 0.01)])
+def test_two_class_multiclass_pa_is_binary_pa_at_twice_c(variant, C):
+    """The identity the GPU's two-class form rests on (MultiClassPA._fit_two_classes), on the
+    CPU reference-semantics learners: K = 2 MultiClassPA at C and the binary PA learner at 2C
+    on labels 0 → +1, 1 → −1 give w_0 − w_1 = w after every round, and w_0 + w_1 stays 0."""
+    from omldm_amd.io.synthetic import synth_batch
+    from omldm_amd.models import make_learner
+    from omldm_amd.models.base import RoundContext
+
+    space = FeatureSpace(13, 0, 26, 1 << 16, field_aware=True)
+    S, R = 4, 300
+    mc = make_learner("MultiClassPA", {"nClasses": 2, "variant": variant, "C": C}, space, "cpu")
+    sv = make_learner("SVM", {"variant": variant, "C": 2 * C}, space, "cpu")
+    for k in range(3):
+        b = synth_batch(space, S * R - 7, start=k * S * R, task=2, n_classes=2, seed=43)
+        mc.fit(b, RoundContext(spokes=S, inv_p=1.0 / S))
+        yb = torch.where(b.y == 0, 1.0, torch.where(b.y == 1, -1.0, float("nan")))
+        sv.fit(HashedBatch(b.num, b.cat, yb, cat_span=b.cat_span),
+               RoundContext(spokes=S, inv_p=1.0 / S))
+        assert torch.allclose(mc.W[0] - mc.W[1], sv.w, rtol=1e-6, atol=1e-7)
+        assert float((mc.W[0] + mc.W[1]).abs().max()) <= 1e-7
+    assert mc.running_totals()["mistakes"] == sv.running_totals()["mistakes"]
 
 
 @gpu
