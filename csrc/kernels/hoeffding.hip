@@ -945,10 +945,21 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
           for (int f = lane; f < d; f += 64) {
             float gm = -2.f;
             int bm = 0;
-            for (int b = 0; b < nb; ++b) {
-              const float g = gains[f * nb + b];
-              bm = g > gm ? b : bm;
-              gm = g > gm ? g : gm;
+            if (nb <= 16) {  // every read in flight before the first compare
+              float gv[16];
+#pragma unroll
+              for (int b = 0; b < 16; ++b) gv[b] = b < nb ? gains[f * nb + b] : -2.f;
+#pragma unroll
+              for (int b = 0; b < 16; ++b) {
+                bm = gv[b] > gm ? b : bm;
+                gm = gv[b] > gm ? gv[b] : gm;
+              }
+            } else {
+              for (int b = 0; b < nb; ++b) {
+                const float g = gains[f * nb + b];
+                bm = g > gm ? b : bm;
+                gm = g > gm ? g : gm;
+              }
             }
             if (gm > g1) {
               g2 = g1;
@@ -959,8 +970,9 @@ __global__ __launch_bounds__(kHxNT) void ht_exact_kernel(
               g2 = gm;
             }
           }
-#pragma unroll
-          for (int m = 1; m < 64; m <<= 1) {
+          // lanes ≥ d hold no candidate: the butterfly spans the next power of two ≥ d
+          const int span = d >= 64 ? 64 : (d <= 1 ? 1 : 1 << (32 - __builtin_clz(d - 1)));
+          for (int m = 1; m < span; m <<= 1) {
             const float og1 = __shfl_xor(g1, m), og2 = __shfl_xor(g2, m);
             const int of1 = __shfl_xor(f1, m), ob1 = __shfl_xor(b1, m);
             const bool take = og1 > g1 || (og1 == g1 && of1 < f1);
