@@ -404,6 +404,8 @@ __global__ __launch_bounds__(64) void kmeans_fast_kernel(const float* __restrict
       // the distance unconditionally (a row that is not a training point wastes it), so the
       // next row's LDS read stays ahead of this row's chain
       const unsigned key = __builtin_bit_cast(unsigned, group_sum<G>(sqdist<ND>(xc, c))) | pad;
+      // 1/(n + 1) ahead of the argmin (it does not depend on it): off the point's chain
+      const float rn = rcp_rn(n + 1.f);
       if ((live >> s) & 1ull) {
         const unsigned mw = (unsigned)__builtin_amdgcn_readlane((int)wave_umin_groups<G>(key), 63);
         ich += __builtin_bit_cast(float, mw);
@@ -413,9 +415,8 @@ __global__ __launch_bounds__(64) void kmeans_fast_kernel(const float* __restrict
         // mask save / restore on the chain)
         const bool win = grp == (int)__builtin_ctzll(eq | (1ull << 63)) / G;
         n = win ? n + 1.f : n;
-        const float r = rcp_rn(n);
 #pragma unroll
-        for (int i = 0; i < ND; ++i) c[i] = win ? fmaf(r, xc[i] - c[i], c[i]) : c[i];
+        for (int i = 0; i < ND; ++i) c[i] = win ? fmaf(rn, xc[i] - c[i], c[i]) : c[i];
       }
 #pragma unroll
       for (int i = 0; i < ND; ++i) xc[i] = xn[i];
@@ -509,9 +510,12 @@ __global__ __launch_bounds__(256) void kmeans_mw_kernel(const float* __restrict_
     for (int s = 0; s < 64; ++s) {
       if (s + 1 < 64) lds_row<DPL, ND>(xb + (s + 1) * RS, xn);
       unsigned key[CPL];
+      float rn[CPL];  // 1/(n + 1) ahead of the argmin, off the point's chain
 #pragma unroll
-      for (int q = 0; q < CPL; ++q)
+      for (int q = 0; q < CPL; ++q) {
         key[q] = __builtin_bit_cast(unsigned, sqdist<ND>(xc, c[q])) | pad[q];
+        rn[q] = rcp_rn(n[q] + 1.f);
+      }
       if ((live >> s) & 1ull) {
         unsigned m = key[0];
 #pragma unroll
@@ -545,9 +549,8 @@ __global__ __launch_bounds__(256) void kmeans_mw_kernel(const float* __restrict_
           for (int q = 0; q < CPL; ++q)
             if ((int)(bj >> 8) == q) {
               n[q] += 1.f;
-              const float r = rcp_rn(n[q]);
 #pragma unroll
-              for (int i = 0; i < ND; ++i) c[q][i] = fmaf(r, xc[i] - c[q][i], c[q][i]);
+              for (int i = 0; i < ND; ++i) c[q][i] = fmaf(rn[q], xc[i] - c[q][i], c[q][i]);
             }
         }
       }
